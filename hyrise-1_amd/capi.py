@@ -1,0 +1,105 @@
+"""ctypes view of the C-ABI in include/hyrise_amd.h (libhyrise_amd.so).
+
+Used by bench.py and the multi-GPU shard driver to call the kernels on device buffers that are owned elsewhere
+(torch tensors), and by tests to check that the library exports every declared entry point. Structures mirror the
+header field for field.
+"""
+import ctypes
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libhyrise_amd.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "hyrise_amd.h")
+
+lib = ctypes.CDLL(LIB_PATH)
+
+HY_OK, HY_ERR_CAPACITY = 0, 6
+HY_TYPE_INT32, HY_TYPE_INT64, HY_TYPE_FLOAT, HY_TYPE_DOUBLE = 1, 2, 3, 4
+HY_COL_VALUE, HY_COL_DICT = 0, 1
+HY_OP_EQ, HY_OP_NE, HY_OP_LT, HY_OP_LE, HY_OP_GT, HY_OP_GE, HY_OP_ALL, HY_OP_NONE = range(8)
+HY_JOIN_INNER, HY_JOIN_LEFT, HY_JOIN_RIGHT, HY_JOIN_SEMI, HY_JOIN_ANTI = 0, 1, 2, 5, 6
+
+
+class RowID(ctypes.Structure):
+    _fields_ = [("chunk_id", ctypes.c_uint32), ("chunk_offset", ctypes.c_uint32)]
+
+
+class ColumnChunk(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("nulls", ctypes.c_void_p), ("dictionary", ctypes.c_void_p),
+                ("size", ctypes.c_uint32), ("dictionary_size", ctypes.c_uint32), ("kind", ctypes.c_int32),
+                ("vid_width", ctypes.c_int32)]
+
+
+class ScanChunk(ctypes.Structure):
+    _fields_ = [("column", ColumnChunk), ("op", ctypes.c_int32), ("search_vid", ctypes.c_uint32),
+                ("out_begin", ctypes.c_uint64)]
+
+
+class JoinChunk(ctypes.Structure):
+    _fields_ = [("column", ColumnChunk), ("pos_list", ctypes.c_void_p), ("size", ctypes.c_uint32),
+                ("chunk_id", ctypes.c_uint32)]
+
+
+class JoinSide(ctypes.Structure):
+    _fields_ = [("chunks", ctypes.POINTER(JoinChunk)), ("n_chunks", ctypes.c_uint32), ("value_type", ctypes.c_int32),
+                ("referenced", ctypes.POINTER(ColumnChunk)), ("n_referenced", ctypes.c_uint32),
+                ("fuse_dereference", ctypes.c_int32)]
+
+
+class JoinParams(ctypes.Structure):
+    _fields_ = [("mode", ctypes.c_int32), ("hashed_type", ctypes.c_int32), ("radix_bits", ctypes.c_uint32),
+                ("seed", ctypes.c_uint32)]
+
+
+class JoinResult(ctypes.Structure):
+    _fields_ = [("total_pairs", ctypes.c_uint64), ("capacity_required", ctypes.c_uint64)]
+
+
+_sigs = {
+    "hy_get_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "hy_set_device": (ctypes.c_int, [ctypes.c_int]),
+    "hy_last_error_message": (ctypes.c_char_p, []),
+    "hy_build_info": (ctypes.c_char_p, []),
+    "hy_stream_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
+    "hy_table_scan_workspace_size": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_size_t)]),
+    "hy_table_scan": (ctypes.c_int, [ctypes.POINTER(ScanChunk), ctypes.c_uint32, ctypes.c_int32, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                     ctypes.c_void_p]),
+    "hy_join_radix_bits": (ctypes.c_uint32, [ctypes.c_uint64, ctypes.c_uint32]),
+    "hy_murmur2": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                  ctypes.c_void_p]),
+    "hy_join_hash_workspace_size": (ctypes.c_int, [ctypes.POINTER(JoinSide), ctypes.POINTER(JoinSide),
+                                                   ctypes.POINTER(JoinParams), ctypes.POINTER(ctypes.c_size_t)]),
+    "hy_join_hash": (ctypes.c_int, [ctypes.POINTER(JoinSide), ctypes.POINTER(JoinSide), ctypes.POINTER(JoinParams),
+                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                    ctypes.c_void_p, ctypes.POINTER(JoinResult), ctypes.c_void_p, ctypes.c_size_t,
+                                    ctypes.c_void_p]),
+    "hy_expand_row_ids": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                         ctypes.c_void_p]),
+}
+for _name, (_res, _args) in _sigs.items():
+    _f = getattr(lib, _name)
+    _f.restype = _res
+    _f.argtypes = _args
+
+
+class HyError(RuntimeError):
+    pass
+
+
+def check(status, what=""):
+    if status != HY_OK:
+        raise HyError(f"{what} failed ({status}): {lib.hy_last_error_message().decode()}")
+
+
+def declared_symbols():
+    """Entry points declared in include/hyrise_amd.h."""
+    text = open(HEADER_PATH).read()
+    return sorted(set(re.findall(r"^\s*(?:hy_status|uint32_t|const char\*)\s+(hy_\w+)\s*\(", text, re.M)))
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    check(lib.hy_get_device_count(ctypes.byref(n)), "hy_get_device_count")
+    return n.value

@@ -1,0 +1,861 @@
+// C-ABI implementation (include/hyrise_amd.h): runtime wrappers, launch orchestration and workspace carving for
+// the gfx950 TableScan / JoinHash kernels. Nothing here throws across the boundary; every failure becomes an
+// hy_status plus a thread-local message.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "hyrise_amd.h"
+#include "../kernels/common.hpp"
+#include "../kernels/scan.hip"
+#include "../kernels/join.hip"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+hy_status fail(hy_status code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define HY_HIP(call)                                                                                       \
+  do {                                                                                                     \
+    hipError_t e_ = (call);                                                                                \
+    if (e_ != hipSuccess) return fail(HY_ERR_DEVICE, std::string(#call) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+inline hipStream_t S(hy_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// Bump allocator over the caller's workspace. Every carve is 256-byte aligned.
+struct Carver {
+  char* base;
+  size_t cap;
+  size_t used = 0;
+  bool ok = true;
+  template <typename T>
+  T* take(size_t count) {
+    used = (used + 255) & ~size_t(255);
+    T* p = reinterpret_cast<T*>(base ? base + used : nullptr);
+    used += count * sizeof(T);
+    if (base && used > cap) ok = false;
+    return p;
+  }
+};
+
+int grid_for(uint64_t n, int threads) {
+  const uint64_t g = (n + threads - 1) / threads;
+  return static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(g, 256 * 16)));
+}
+
+}  // namespace
+
+// ================================================================================================================
+// Runtime
+// ================================================================================================================
+extern "C" {
+
+hy_status hy_get_device_count(int* count) {
+  if (!count) return fail(HY_ERR_INVALID_ARGUMENT, "count is NULL");
+  int n = 0;
+  const hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) n = 0;
+  *count = n;
+  return HY_OK;
+}
+
+hy_status hy_set_device(int device) {
+  HY_HIP(hipSetDevice(device));
+  return HY_OK;
+}
+
+hy_status hy_malloc(void** ptr, size_t bytes) {
+  if (!ptr) return fail(HY_ERR_INVALID_ARGUMENT, "ptr is NULL");
+  // round up so that 16-byte vector loads past the last element stay inside the allocation
+  HY_HIP(hipMalloc(ptr, std::max<size_t>(256, (bytes + 255) & ~size_t(255))));
+  return HY_OK;
+}
+
+hy_status hy_free(void* ptr) {
+  if (ptr) HY_HIP(hipFree(ptr));
+  return HY_OK;
+}
+
+hy_status hy_memcpy_htod(void* dst, const void* src, size_t bytes, hy_stream_t stream) {
+  if (bytes) HY_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, S(stream)));
+  return HY_OK;
+}
+
+hy_status hy_memcpy_dtoh(void* dst, const void* src, size_t bytes, hy_stream_t stream) {
+  if (bytes) HY_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, S(stream)));
+  return HY_OK;
+}
+
+hy_status hy_memcpy_dtod(void* dst, const void* src, size_t bytes, hy_stream_t stream) {
+  if (bytes) HY_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, S(stream)));
+  return HY_OK;
+}
+
+hy_status hy_memset(void* dst, int value, size_t bytes, hy_stream_t stream) {
+  if (bytes) HY_HIP(hipMemsetAsync(dst, value, bytes, S(stream)));
+  return HY_OK;
+}
+
+hy_status hy_stream_create(hy_stream_t* stream) {
+  hipStream_t s;
+  HY_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  *stream = s;
+  return HY_OK;
+}
+
+hy_status hy_stream_destroy(hy_stream_t stream) {
+  HY_HIP(hipStreamDestroy(S(stream)));
+  return HY_OK;
+}
+
+hy_status hy_stream_synchronize(hy_stream_t stream) {
+  HY_HIP(hipStreamSynchronize(S(stream)));
+  return HY_OK;
+}
+
+const char* hy_last_error_message(void) { return g_last_error.c_str(); }
+
+const char* hy_build_info(void) { return "hyrise-amd gfx950 (CDNA4) HIP kernels: table_scan, reference_scan, join_hash"; }
+
+}  // extern "C"
+
+// ================================================================================================================
+// TableScan
+// ================================================================================================================
+namespace {
+
+enum ScanClass { SC_DICT8, SC_DICT16, SC_DICT32, SC_VALUE, SC_COUNT };
+
+int scan_class(const hy_scan_chunk& c) {
+  if (c.column.kind == HY_COL_VALUE) return SC_VALUE;
+  switch (c.column.vid_width) {
+    case 1:
+      return SC_DICT8;
+    case 2:
+      return SC_DICT16;
+    case 4:
+      return SC_DICT32;
+  }
+  return -1;
+}
+
+uint64_t scan_tiles(uint32_t size) { return (uint64_t(size) + hyk::SCAN_TILE - 1) / hyk::SCAN_TILE; }
+
+template <typename E, bool DICT>
+hy_status launch_scan(const hyk::ScanLaunchDesc& d, const void* constant, uint32_t* out, uint32_t* counts,
+                      hipStream_t s) {
+  hyk::ScanConst<E> c{};
+  if (!DICT && constant) std::memcpy(&c.value, constant, sizeof(E));
+  hipLaunchKernelGGL((hyk::scan_kernel<E, DICT>), dim3(static_cast<uint32_t>(d.n_tiles)), dim3(hyk::SCAN_THREADS), 0,
+                     s, d, c, out, counts);
+  HY_HIP(hipGetLastError());
+  return HY_OK;
+}
+
+// workspace layout for one class: chunks, tile prefix, chunk index, status
+size_t scan_class_bytes(uint32_t n_chunks, uint64_t n_tiles) {
+  Carver cv{nullptr, 0};
+  cv.take<hy_scan_chunk>(n_chunks);
+  cv.take<uint64_t>(n_chunks + 1);
+  cv.take<uint32_t>(n_chunks);
+  cv.take<uint64_t>(n_tiles + 1);
+  cv.take<uint32_t>(64);
+  return cv.used + 256;
+}
+
+}  // namespace
+
+extern "C" {
+
+hy_status hy_table_scan_workspace_size(const uint32_t* chunk_sizes, uint32_t n_chunks, size_t* bytes) {
+  if (!bytes || (n_chunks && !chunk_sizes)) return fail(HY_ERR_INVALID_ARGUMENT, "null argument");
+  uint64_t tiles = 0;
+  for (uint32_t i = 0; i < n_chunks; ++i) tiles += scan_tiles(chunk_sizes[i]);
+  // worst case: all chunks in one class, times the number of classes (carved sequentially)
+  *bytes = SC_COUNT * scan_class_bytes(n_chunks, tiles);
+  return HY_OK;
+}
+
+hy_status hy_table_scan(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_t value_type, const void* constant,
+                        uint32_t* out_offsets, uint32_t* counts, void* workspace, size_t workspace_bytes,
+                        hy_stream_t stream) {
+  if (n_chunks == 0) return HY_OK;
+  if (!chunks || !out_offsets || !counts) return fail(HY_ERR_INVALID_ARGUMENT, "null argument");
+  hipStream_t s = S(stream);
+  std::vector<std::vector<uint32_t>> by_class(SC_COUNT);
+  for (uint32_t i = 0; i < n_chunks; ++i) {
+    const int cls = scan_class(chunks[i]);
+    if (cls < 0) return fail(HY_ERR_INVALID_ARGUMENT, "bad vid width");
+    if (chunks[i].column.size && !aligned16(chunks[i].column.data))
+      return fail(HY_ERR_ALIGNMENT, "column data not 16-byte aligned");
+    if (chunks[i].column.nulls && !aligned16(chunks[i].column.nulls))
+      return fail(HY_ERR_ALIGNMENT, "null vector not 16-byte aligned");
+    by_class[cls].push_back(i);
+  }
+  if (!by_class[SC_VALUE].empty() &&
+      !(value_type == HY_TYPE_INT32 || value_type == HY_TYPE_INT64 || value_type == HY_TYPE_FLOAT ||
+        value_type == HY_TYPE_DOUBLE))
+    return fail(HY_ERR_UNSUPPORTED, "value scan type");
+  HY_HIP(hipMemsetAsync(counts, 0, sizeof(uint32_t) * n_chunks, s));
+
+  Carver cv{static_cast<char*>(workspace), workspace_bytes};
+  // host staging must outlive the async copies: keep everything until the stream is synchronized below
+  std::vector<std::vector<hy_scan_chunk>> h_chunks(SC_COUNT);
+  std::vector<std::vector<uint64_t>> h_tiles(SC_COUNT);
+  uint32_t* error = nullptr;
+  for (int cls = 0; cls < SC_COUNT; ++cls) {
+    const auto& idx = by_class[cls];
+    if (idx.empty()) continue;
+    const uint32_t nc = static_cast<uint32_t>(idx.size());
+    auto& hc = h_chunks[cls];
+    auto& ht = h_tiles[cls];
+    hc.resize(nc);
+    ht.resize(nc + 1);
+    uint64_t run = 0;
+    for (uint32_t k = 0; k < nc; ++k) {
+      hc[k] = chunks[idx[k]];
+      ht[k] = run;
+      run += hc[k].op == HY_OP_NONE ? 0 : scan_tiles(hc[k].column.size);
+    }
+    ht[nc] = run;
+    hyk::ScanLaunchDesc d{};
+    auto* dch = cv.take<hy_scan_chunk>(nc);
+    auto* dti = cv.take<uint64_t>(nc + 1);
+    auto* dix = cv.take<uint32_t>(nc);
+    auto* dst = cv.take<uint64_t>(run + 1);
+    auto* dmisc = cv.take<uint32_t>(64);
+    if (!cv.ok) return fail(HY_ERR_WORKSPACE, "scan workspace too small");
+    if (!error) {
+      error = dmisc + 1;
+      HY_HIP(hipMemsetAsync(error, 0, 4, s));
+    }
+    HY_HIP(hipMemcpyAsync(dch, hc.data(), sizeof(hy_scan_chunk) * nc, hipMemcpyHostToDevice, s));
+    HY_HIP(hipMemcpyAsync(dti, ht.data(), sizeof(uint64_t) * (nc + 1), hipMemcpyHostToDevice, s));
+    HY_HIP(hipMemcpyAsync(dix, idx.data(), sizeof(uint32_t) * nc, hipMemcpyHostToDevice, s));
+    HY_HIP(hipMemsetAsync(dst, 0, sizeof(uint64_t) * (run + 1), s));
+    HY_HIP(hipMemsetAsync(dmisc, 0, 4, s));
+    if (run == 0) continue;
+    d.chunks = dch;
+    d.chunk_tile_begin = dti;
+    d.chunk_index = dix;
+    d.n_chunks = nc;
+    d.n_tiles = run;
+    d.status = dst;
+    d.ticket = dmisc;
+    d.error = error;
+    hy_status st = HY_OK;
+    switch (cls) {
+      case SC_DICT8:
+        st = launch_scan<uint8_t, true>(d, nullptr, out_offsets, counts, s);
+        break;
+      case SC_DICT16:
+        st = launch_scan<uint16_t, true>(d, nullptr, out_offsets, counts, s);
+        break;
+      case SC_DICT32:
+        st = launch_scan<uint32_t, true>(d, nullptr, out_offsets, counts, s);
+        break;
+      case SC_VALUE:
+        switch (value_type) {
+          case HY_TYPE_INT32:
+            st = launch_scan<int32_t, false>(d, constant, out_offsets, counts, s);
+            break;
+          case HY_TYPE_INT64:
+            st = launch_scan<int64_t, false>(d, constant, out_offsets, counts, s);
+            break;
+          case HY_TYPE_FLOAT:
+            st = launch_scan<float, false>(d, constant, out_offsets, counts, s);
+            break;
+          case HY_TYPE_DOUBLE:
+            st = launch_scan<double, false>(d, constant, out_offsets, counts, s);
+            break;
+        }
+        break;
+    }
+    if (st != HY_OK) return st;
+  }
+  uint32_t herr = 0;
+  if (error) {
+    HY_HIP(hipMemcpyAsync(&herr, error, 4, hipMemcpyDeviceToHost, s));
+  }
+  HY_HIP(hipStreamSynchronize(s));
+  if (herr) return fail(HY_ERR_KERNEL, "scan look-back did not complete");
+  return HY_OK;
+}
+
+hy_status hy_reference_scan_workspace_size(uint64_t pos_list_size, size_t* bytes) {
+  if (!bytes) return fail(HY_ERR_INVALID_ARGUMENT, "null argument");
+  const uint64_t tiles = (pos_list_size + hyk::SCAN_TILE - 1) / hyk::SCAN_TILE;
+  Carver cv{nullptr, 0};
+  cv.take<uint64_t>(tiles + 1);
+  cv.take<uint32_t>(64);
+  cv.take<hy_scan_chunk>(1 << 20);  // referenced chunk descriptors (bounded below by the call)
+  *bytes = cv.used + 256;
+  return HY_OK;
+}
+
+hy_status hy_reference_scan(const hy_row_id* pos_list, uint64_t pos_list_size, const hy_scan_chunk* referenced_chunks,
+                            uint32_t n_referenced_chunks, int32_t value_type, const void* constant,
+                            uint32_t* out_positions, uint64_t* count, void* workspace, size_t workspace_bytes,
+                            hy_stream_t stream) {
+  if (!count) return fail(HY_ERR_INVALID_ARGUMENT, "null count");
+  hipStream_t s = S(stream);
+  HY_HIP(hipMemsetAsync(count, 0, 8, s));
+  if (pos_list_size == 0) return HY_OK;
+  if (n_referenced_chunks > (1u << 20)) return fail(HY_ERR_UNSUPPORTED, "too many referenced chunks");
+  const uint64_t tiles = (pos_list_size + hyk::SCAN_TILE - 1) / hyk::SCAN_TILE;
+  Carver cv{static_cast<char*>(workspace), workspace_bytes};
+  auto* dst = cv.take<uint64_t>(tiles + 1);
+  auto* dmisc = cv.take<uint32_t>(64);
+  auto* dch = cv.take<hy_scan_chunk>(std::max<uint32_t>(1, n_referenced_chunks));
+  if (!cv.ok) return fail(HY_ERR_WORKSPACE, "reference scan workspace too small");
+  HY_HIP(hipMemsetAsync(dst, 0, sizeof(uint64_t) * (tiles + 1), s));
+  HY_HIP(hipMemsetAsync(dmisc, 0, 256, s));
+  HY_HIP(hipMemcpyAsync(dch, referenced_chunks, sizeof(hy_scan_chunk) * n_referenced_chunks, hipMemcpyHostToDevice, s));
+  hyk::RefScanDesc d{pos_list, pos_list_size, dch, n_referenced_chunks, tiles, dst, dmisc, dmisc + 1};
+  auto go = [&](auto tag) -> hy_status {
+    using T = decltype(tag);
+    hyk::ScanConst<T> c{};
+    if (constant) std::memcpy(&c.value, constant, sizeof(T));
+    hipLaunchKernelGGL((hyk::ref_scan_kernel<T>), dim3(static_cast<uint32_t>(tiles)), dim3(hyk::SCAN_THREADS), 0, s, d,
+                       c, out_positions, count);
+    HY_HIP(hipGetLastError());
+    return HY_OK;
+  };
+  hy_status st;
+  switch (value_type) {
+    case HY_TYPE_INT32:
+      st = go(int32_t{});
+      break;
+    case HY_TYPE_INT64:
+      st = go(int64_t{});
+      break;
+    case HY_TYPE_FLOAT:
+      st = go(float{});
+      break;
+    case HY_TYPE_DOUBLE:
+      st = go(double{});
+      break;
+    default:
+      return fail(HY_ERR_UNSUPPORTED, "reference scan type");
+  }
+  if (st != HY_OK) return st;
+  uint32_t herr = 0;
+  HY_HIP(hipMemcpyAsync(&herr, dmisc + 1, 4, hipMemcpyDeviceToHost, s));
+  HY_HIP(hipStreamSynchronize(s));
+  if (herr) return fail(HY_ERR_KERNEL, "reference scan look-back did not complete");
+  return HY_OK;
+}
+
+hy_status hy_gather_row_ids(const hy_row_id* pos_list, const uint32_t* positions, uint64_t n, hy_row_id* out,
+                            hy_stream_t stream) {
+  if (n == 0) return HY_OK;
+  hipLaunchKernelGGL(hyk::gather_row_ids_kernel, dim3(grid_for(n, 256)), dim3(256), 0, S(stream), pos_list, positions,
+                     n, out);
+  HY_HIP(hipGetLastError());
+  return HY_OK;
+}
+
+hy_status hy_pos_list_chunk_first_seen(const hy_row_id* pos_list, uint64_t n, uint32_t n_chunks, uint64_t* first_seen,
+                                       hy_stream_t stream) {
+  if (n_chunks == 0) return HY_OK;
+  HY_HIP(hipMemsetAsync(first_seen, 0xFF, 8ull * n_chunks, S(stream)));
+  if (n == 0) return HY_OK;
+  hipLaunchKernelGGL(hyk::first_seen_kernel, dim3(grid_for(n, 256)), dim3(256), 0, S(stream), pos_list, n, n_chunks,
+                     reinterpret_cast<unsigned long long*>(first_seen));
+  HY_HIP(hipGetLastError());
+  return HY_OK;
+}
+
+hy_status hy_expand_row_ids(uint32_t chunk_id, const uint32_t* offsets, uint64_t n, hy_row_id* out,
+                            hy_stream_t stream) {
+  if (n == 0) return HY_OK;
+  hipLaunchKernelGGL(hyk::expand_row_ids_kernel, dim3(grid_for(n, 256)), dim3(256), 0, S(stream), chunk_id, offsets, n,
+                     out);
+  HY_HIP(hipGetLastError());
+  return HY_OK;
+}
+
+// ================================================================================================================
+// Hashing
+// ================================================================================================================
+hy_status hy_murmur2(const void* keys, uint64_t n, uint32_t key_bytes, uint32_t seed, uint32_t* out,
+                     hy_stream_t stream) {
+  if (n == 0) return HY_OK;
+  if (key_bytes == 4) {
+    hipLaunchKernelGGL(hyk::murmur_kernel_u32, dim3(grid_for(n, 256)), dim3(256), 0, S(stream),
+                       static_cast<const uint32_t*>(keys), n, seed, out);
+  } else if (key_bytes == 8) {
+    hipLaunchKernelGGL(hyk::murmur_kernel_u64, dim3(grid_for(n, 256)), dim3(256), 0, S(stream),
+                       static_cast<const uint64_t*>(keys), n, seed, out);
+  } else {
+    return fail(HY_ERR_UNSUPPORTED, "key_bytes must be 4 or 8");
+  }
+  HY_HIP(hipGetLastError());
+  return HY_OK;
+}
+
+// JoinHashImpl ctor (reference join_hash.cpp:640-668), evaluated in the same float arithmetic:
+//   size = B * (sizeof(T) + sizeof(void*)) + (B / 2) * (sizeof(PosList) + 2 * sizeof(RowID))
+//   cluster_count = max(1.0f, (2.0f * size) / 256000); radix_bits = ceil(log2(cluster_count))
+// sizeof(PosList) = 32 (std::vector with a polymorphic allocator), sizeof(RowID) = 8.
+uint32_t hy_join_radix_bits(uint64_t build_rows, uint32_t key_bytes) {
+  const uint64_t size = build_rows * (uint64_t(key_bytes) + 8) + (build_rows / 2) * (32 + 2 * 8);
+  const float adaption = 2.0f;
+  const float cluster_count = std::max(1.0f, (adaption * static_cast<float>(size)) / 256000);
+  return static_cast<uint32_t>(std::ceil(std::log2(cluster_count)));
+}
+
+}  // extern "C"
+
+// ================================================================================================================
+// JoinHash
+// ================================================================================================================
+namespace {
+
+struct SidePlan {
+  uint64_t n_rows = 0;
+  uint64_t n_tiles1 = 0;
+  std::vector<hyk::SrcChunk> chunks;
+  std::vector<uint64_t> tile_begin;
+  std::vector<uint64_t> row_begin;       // this table
+  std::vector<hyk::SrcChunk> referenced;
+  std::vector<uint64_t> ref_row_begin;   // referenced table
+  int32_t fuse = 0;
+  uint32_t map_uniform = 0;              // output RowID map (this table or referenced table when fused)
+};
+
+uint32_t uniform_of(const std::vector<uint64_t>& row_begin) {
+  const size_t n = row_begin.size() - 1;
+  if (n == 0) return 0;
+  if (n == 1) return static_cast<uint32_t>(std::max<uint64_t>(row_begin[1], 1));
+  const uint64_t u = row_begin[1] - row_begin[0];
+  if (u == 0) return 0;
+  for (size_t i = 1; i + 1 < n; ++i)
+    if (row_begin[i + 1] - row_begin[i] != u) return 0;
+  if (row_begin[n] - row_begin[n - 1] > u) return 0;
+  return static_cast<uint32_t>(u);
+}
+
+hyk::SrcChunk src_from(const hy_column_chunk& c, const hy_row_id* pos_list, uint32_t size, uint64_t row_begin) {
+  hyk::SrcChunk s{};
+  s.data = c.data;
+  s.nulls = c.nulls;
+  s.dictionary = c.dictionary;
+  s.pos_list = pos_list;
+  s.size = size;
+  s.dictionary_size = c.dictionary_size;
+  s.kind = c.kind;
+  s.vid_width = c.vid_width;
+  s.row_begin = row_begin;
+  return s;
+}
+
+hy_status plan_side(const hy_join_side* side, SidePlan& p) {
+  if (!side || (side->n_chunks && !side->chunks)) return fail(HY_ERR_INVALID_ARGUMENT, "join side");
+  p.chunks.resize(side->n_chunks);
+  p.tile_begin.resize(side->n_chunks + 1);
+  p.row_begin.resize(side->n_chunks + 1);
+  bool is_ref = false;
+  uint64_t rows = 0, tiles = 0;
+  for (uint32_t i = 0; i < side->n_chunks; ++i) {
+    const hy_join_chunk& c = side->chunks[i];
+    if (c.pos_list) is_ref = true;
+    p.chunks[i] = src_from(c.column, c.pos_list, c.size, rows);
+    p.row_begin[i] = rows;
+    p.tile_begin[i] = tiles;
+    rows += c.size;
+    tiles += (uint64_t(c.size) + hyk::PART_TILE - 1) / hyk::PART_TILE;
+  }
+  p.row_begin[side->n_chunks] = rows;
+  p.tile_begin[side->n_chunks] = tiles;
+  p.n_rows = rows;
+  p.n_tiles1 = tiles;
+  if (rows >= 0xFFFFFFFFull) return fail(HY_ERR_UNSUPPORTED, "join side exceeds 2^32-1 rows");
+  if (is_ref) {
+    p.referenced.resize(side->n_referenced);
+    p.ref_row_begin.resize(side->n_referenced + 1);
+    uint64_t rr = 0;
+    for (uint32_t i = 0; i < side->n_referenced; ++i) {
+      p.referenced[i] = src_from(side->referenced[i], nullptr, side->referenced[i].size, rr);
+      p.ref_row_begin[i] = rr;
+      rr += side->referenced[i].size;
+    }
+    p.ref_row_begin[side->n_referenced] = rr;
+    if (rr >= 0xFFFFFFFFull) return fail(HY_ERR_UNSUPPORTED, "referenced table exceeds 2^32-1 rows");
+  }
+  return HY_OK;
+}
+
+// Device pointers of one side inside the workspace.
+template <typename H>
+struct SideBufs {
+  hyk::SrcChunk* chunks;
+  uint64_t* tile_begin;
+  uint64_t* row_begin;
+  hyk::SrcChunk* referenced;
+  uint64_t* ref_row_begin;
+  uint32_t* hist1;
+  uint32_t* off1;
+  hyk::Rec<H>* rec1;
+  hyk::Rec<H>* rec2;
+  uint32_t* seg_begin;
+  uint64_t* seg_tile_begin;
+  uint32_t* hist2;
+  uint32_t* off2;
+  uint32_t* part_begin;
+  uint64_t max_tiles2;
+};
+
+struct Geometry {
+  uint32_t bits;
+  bool two_pass;
+  uint32_t hi_bits, lo_bits;
+  uint32_t n_digits1, n_digits2;
+};
+
+Geometry geometry(uint32_t bits) {
+  Geometry g{};
+  g.bits = bits;
+  g.two_pass = bits > 8;
+  g.lo_bits = g.two_pass ? 8 : bits;
+  g.hi_bits = g.two_pass ? bits - 8 : 0;
+  g.n_digits1 = g.two_pass ? (1u << g.hi_bits) : (1u << bits);
+  g.n_digits2 = g.two_pass ? 256u : 0u;
+  return g;
+}
+
+template <typename H>
+void carve_side(Carver& cv, const SidePlan& p, const Geometry& g, SideBufs<H>& b) {
+  b.chunks = cv.take<hyk::SrcChunk>(std::max<size_t>(1, p.chunks.size()));
+  b.tile_begin = cv.take<uint64_t>(p.tile_begin.size());
+  b.row_begin = cv.take<uint64_t>(p.row_begin.size());
+  b.referenced = cv.take<hyk::SrcChunk>(std::max<size_t>(1, p.referenced.size()));
+  b.ref_row_begin = cv.take<uint64_t>(std::max<size_t>(1, p.ref_row_begin.size()));
+  b.hist1 = cv.take<uint32_t>(std::max<uint64_t>(1, g.n_digits1 * p.n_tiles1));
+  b.off1 = cv.take<uint32_t>(std::max<uint64_t>(1, g.n_digits1 * p.n_tiles1));
+  b.rec1 = cv.take<hyk::Rec<H>>(std::max<uint64_t>(1, p.n_rows));
+  b.max_tiles2 = (p.n_rows + hyk::PART_TILE - 1) / hyk::PART_TILE + g.n_digits1;
+  if (g.two_pass) {
+    b.rec2 = cv.take<hyk::Rec<H>>(std::max<uint64_t>(1, p.n_rows));
+    b.seg_begin = cv.take<uint32_t>(g.n_digits1 + 1);
+    b.seg_tile_begin = cv.take<uint64_t>(g.n_digits1 + 1);
+    b.hist2 = cv.take<uint32_t>(b.max_tiles2 * 256);
+    b.off2 = cv.take<uint32_t>(b.max_tiles2 * 256);
+  } else {
+    b.rec2 = nullptr;
+    b.seg_begin = nullptr;
+    b.seg_tile_begin = nullptr;
+    b.hist2 = nullptr;
+    b.off2 = nullptr;
+  }
+  b.part_begin = cv.take<uint32_t>((1u << g.bits) + 1);
+}
+
+struct Common {
+  uint64_t* scan_status;
+  uint64_t scan_status_words;
+  uint32_t* misc;  // [0] ticket [1] error [2] overflow ...
+  uint64_t* totals;
+  uint64_t* join_status;
+};
+
+template <typename H>
+size_t join_bytes(const SidePlan& bp, const SidePlan& pp, const Geometry& g) {
+  Carver cv{nullptr, 0};
+  SideBufs<H> a, b;
+  carve_side<H>(cv, bp, g, a);
+  carve_side<H>(cv, pp, g, b);
+  const uint64_t max_scan =
+      std::max({uint64_t(g.n_digits1) * bp.n_tiles1, uint64_t(g.n_digits1) * pp.n_tiles1, a.max_tiles2 * 256,
+                b.max_tiles2 * 256, uint64_t(1)});
+  cv.take<uint64_t>(max_scan / hyk::SCAN_BLOCK + 2);
+  cv.take<uint32_t>(64);
+  cv.take<uint64_t>(8);
+  cv.take<uint64_t>((1u << g.bits) + 1);
+  return cv.used + 256;
+}
+
+hy_status run_scan(const uint32_t* in, uint32_t* out, uint64_t n, const Common& c, hipStream_t s,
+                   uint64_t* total_out = nullptr) {
+  if (n == 0) return HY_OK;
+  const uint64_t tiles = (n + hyk::SCAN_BLOCK - 1) / hyk::SCAN_BLOCK;
+  if (tiles + 1 > c.scan_status_words) return fail(HY_ERR_WORKSPACE, "scan status");
+  HY_HIP(hipMemsetAsync(c.scan_status, 0, sizeof(uint64_t) * (tiles + 1), s));
+  HY_HIP(hipMemsetAsync(c.misc, 0, 4, s));
+  hipLaunchKernelGGL(hyk::exclusive_scan_u32, dim3(static_cast<uint32_t>(tiles)), dim3(hyk::SCAN_T), 0, s, in, out, n,
+                     c.scan_status, c.misc, c.misc + 1, total_out);
+  HY_HIP(hipGetLastError());
+  return HY_OK;
+}
+
+template <typename T, typename H>
+hy_status partition_side(const SidePlan& p, const SideBufs<H>& b, const Geometry& g, uint32_t seed, bool keep_nulls,
+                         const Common& c, uint64_t* side_total, hipStream_t s, hyk::Rec<H>** final_recs) {
+  hyk::Side sd{};
+  sd.chunks = b.chunks;
+  sd.n_chunks = static_cast<uint32_t>(p.chunks.size());
+  sd.chunk_tile_begin = b.tile_begin;
+  sd.n_tiles = p.n_tiles1;
+  sd.referenced = b.referenced;
+  sd.n_referenced = static_cast<uint32_t>(p.referenced.size());
+  sd.referenced_row_begin = b.ref_row_begin;
+  sd.fuse_deref = p.fuse;
+  sd.keep_nulls = keep_nulls ? 1 : 0;
+  const uint32_t mask = g.bits >= 32 ? 0xFFFFFFFFu : ((1u << g.bits) - 1u);
+  const uint32_t n_parts = 1u << g.bits;
+
+  hyk::Digit d1{mask, g.two_pass ? 8u : 0u, g.n_digits1 - 1u, seed};
+  const int dbits1 = g.two_pass ? static_cast<int>(g.hi_bits) : static_cast<int>(g.bits);
+  const uint64_t h1n = uint64_t(g.n_digits1) * p.n_tiles1;
+  const uint64_t* total_dev = side_total;
+  HY_HIP(hipMemsetAsync(side_total, 0, 8, s));
+  if (p.n_tiles1 > 0) {
+    hipLaunchKernelGGL((hyk::part1_hist<T, H>), dim3(static_cast<uint32_t>(p.n_tiles1)), dim3(hyk::PART_THREADS), 0, s,
+                       sd, d1, g.n_digits1, b.hist1);
+    HY_HIP(hipGetLastError());
+    hy_status st = run_scan(b.hist1, b.off1, h1n, c, s, side_total);
+    if (st != HY_OK) return st;
+    hipLaunchKernelGGL((hyk::part1_scatter<T, H>), dim3(static_cast<uint32_t>(p.n_tiles1)), dim3(hyk::PART_THREADS), 0,
+                       s, sd, d1, dbits1, g.n_digits1, b.off1, b.rec1);
+    HY_HIP(hipGetLastError());
+  }
+
+  if (!g.two_pass) {
+    hipLaunchKernelGGL(hyk::bounds_single_pass, dim3((n_parts + 1 + 255) / 256), dim3(256), 0, s, b.off1, p.n_tiles1,
+                       n_parts, total_dev, b.part_begin);
+    HY_HIP(hipGetLastError());
+    *final_recs = b.rec1;
+    return HY_OK;
+  }
+  hipLaunchKernelGGL(hyk::seg_bounds, dim3((g.n_digits1 + 1 + 255) / 256), dim3(256), 0, s, b.off1, p.n_tiles1,
+                     g.n_digits1, total_dev, b.seg_begin);
+  HY_HIP(hipGetLastError());
+  hipLaunchKernelGGL(hyk::seg_tiles, dim3(1), dim3(64), 0, s, b.seg_begin, g.n_digits1, b.seg_tile_begin);
+  HY_HIP(hipGetLastError());
+  hyk::Segs sg{b.seg_begin, b.seg_tile_begin, g.n_digits1};
+  hyk::Digit d2{mask, 0u, 0xFFu, seed};
+  const uint64_t grid2 = b.max_tiles2;
+  hipLaunchKernelGGL((hyk::part2_hist<H>), dim3(static_cast<uint32_t>(grid2)), dim3(hyk::PART_THREADS), 0, s, sg, d2,
+                     256u, b.rec1, b.hist2);
+  HY_HIP(hipGetLastError());
+  hy_status st = run_scan(b.hist2, b.off2, grid2 * 256, c, s);
+  if (st != HY_OK) return st;
+  hipLaunchKernelGGL((hyk::part2_scatter<H>), dim3(static_cast<uint32_t>(grid2)), dim3(hyk::PART_THREADS), 0, s, sg,
+                     d2, 8, 256u, b.rec1, b.off2, b.rec2);
+  HY_HIP(hipGetLastError());
+  hipLaunchKernelGGL(hyk::bounds_two_pass, dim3((n_parts + 1 + 255) / 256), dim3(256), 0, s, b.off2, b.seg_begin,
+                     b.seg_tile_begin, g.n_digits1, 256u, total_dev, b.part_begin);
+  HY_HIP(hipGetLastError());
+  *final_recs = b.rec2;
+  return HY_OK;
+}
+
+hyk::RowMap make_map(const uint64_t* dev_row_begin, const std::vector<uint64_t>& host_row_begin) {
+  hyk::RowMap m{};
+  m.row_begin = dev_row_begin;
+  m.n_chunks = static_cast<uint32_t>(host_row_begin.size() - 1);
+  m.uniform = uniform_of(host_row_begin);
+  m.magic = 0;
+  if (m.uniform >= 2) {
+    // floor(2^64 / u) + 1
+    const unsigned __int128 two64 = static_cast<unsigned __int128>(1) << 64;
+    m.magic = static_cast<uint64_t>(two64 / m.uniform) + 1;
+  }
+  return m;
+}
+
+template <typename TB, typename TP, typename H>
+hy_status join_typed(const SidePlan& bp, const SidePlan& pp, const hy_join_params* prm, hy_row_id* out_build,
+                     hy_row_id* out_probe, uint64_t out_capacity, uint64_t* partition_begin,
+                     uint32_t* partition_counts, hy_join_result* result, void* workspace, size_t workspace_bytes,
+                     hipStream_t s) {
+  const Geometry g = geometry(prm->radix_bits);
+  if (workspace_bytes < join_bytes<H>(bp, pp, g)) return fail(HY_ERR_WORKSPACE, "join workspace too small");
+  Carver cv{static_cast<char*>(workspace), workspace_bytes};
+  SideBufs<H> bb, pb;
+  carve_side<H>(cv, bp, g, bb);
+  carve_side<H>(cv, pp, g, pb);
+  const uint64_t max_scan =
+      std::max({uint64_t(g.n_digits1) * bp.n_tiles1, uint64_t(g.n_digits1) * pp.n_tiles1, bb.max_tiles2 * 256,
+                pb.max_tiles2 * 256, uint64_t(1)});
+  Common c{};
+  c.scan_status_words = max_scan / hyk::SCAN_BLOCK + 2;
+  c.scan_status = cv.take<uint64_t>(c.scan_status_words);
+  c.misc = cv.take<uint32_t>(64);
+  c.totals = cv.take<uint64_t>(8);
+  c.join_status = cv.take<uint64_t>((1u << g.bits) + 1);
+  if (!cv.ok) return fail(HY_ERR_WORKSPACE, "join workspace too small");
+
+  auto upload = [&](auto* dst, const auto& v) -> hy_status {
+    if (!v.empty()) HY_HIP(hipMemcpyAsync(dst, v.data(), sizeof(v[0]) * v.size(), hipMemcpyHostToDevice, s));
+    return HY_OK;
+  };
+  for (auto* side : {&bp, &pp}) {
+    const SideBufs<H>& b = side == &bp ? bb : pb;
+    if (upload(b.chunks, side->chunks) || upload(b.tile_begin, side->tile_begin) || upload(b.row_begin, side->row_begin) ||
+        upload(b.referenced, side->referenced) || upload(b.ref_row_begin, side->ref_row_begin))
+      return HY_ERR_DEVICE;
+  }
+  const bool keep_nulls = prm->mode == HY_JOIN_LEFT || prm->mode == HY_JOIN_RIGHT;
+  hyk::Rec<H>* brec = nullptr;
+  hyk::Rec<H>* precs = nullptr;
+  hy_status st = partition_side<TB, H>(bp, bb, g, prm->seed, false, c, c.totals + 2, s, &brec);
+  if (st != HY_OK) return st;
+  st = partition_side<TP, H>(pp, pb, g, prm->seed, keep_nulls, c, c.totals + 3, s, &precs);
+  if (st != HY_OK) return st;
+
+  // largest build partition decides the LDS table size
+  const uint32_t n_parts = 1u << g.bits;
+  std::vector<uint32_t> hb(n_parts + 1);
+  HY_HIP(hipMemcpyAsync(hb.data(), bb.part_begin, sizeof(uint32_t) * (n_parts + 1), hipMemcpyDeviceToHost, s));
+  HY_HIP(hipStreamSynchronize(s));
+  uint32_t max_build = 0;
+  for (uint32_t i = 0; i < n_parts; ++i) max_build = std::max(max_build, hb[i + 1] - hb[i]);
+  uint32_t cap = 64;
+  while (cap < max_build + max_build / 2 + 1) cap <<= 1;
+  const size_t lds = sizeof(hyk::Slot<H>) * cap + 4 * size_t(max_build) + 2 * size_t(cap) * 2 +
+                     2 * size_t(max_build) * 2 + 64;
+  if (max_build > 65535 || lds > 150 * 1024)
+    return fail(HY_ERR_UNSUPPORTED, "build partition of " + std::to_string(max_build) +
+                                        " rows exceeds the LDS hash table (skewed join keys)");
+
+  hyk::JoinDesc jd{};
+  jd.build_begin = bb.part_begin;
+  jd.probe_begin = pb.part_begin;
+  jd.n_parts = n_parts;
+  jd.cap = cap;
+  jd.max_build = std::max<uint32_t>(max_build, 1);
+  jd.mode = prm->mode;
+  jd.build_map = bp.fuse ? make_map(bb.ref_row_begin, bp.ref_row_begin) : make_map(bb.row_begin, bp.row_begin);
+  jd.probe_map = pp.fuse ? make_map(pb.ref_row_begin, pp.ref_row_begin) : make_map(pb.row_begin, pp.row_begin);
+  jd.capacity = out_capacity;
+  jd.status = c.join_status;
+  jd.ticket = c.misc + 4;
+  jd.error = c.misc + 1;
+  jd.overflow = c.misc + 2;
+  jd.total = c.totals + 1;
+  HY_HIP(hipMemsetAsync(c.join_status, 0, sizeof(uint64_t) * n_parts, s));
+  HY_HIP(hipMemsetAsync(c.misc, 0, 64 * 4, s));
+  HY_HIP(hipMemsetAsync(c.totals, 0, 8 * 2, s));
+  hipLaunchKernelGGL((hyk::join_partition<H>), dim3(n_parts), dim3(hyk::JOIN_THREADS), lds, s, jd, brec, precs,
+                     out_build, out_probe, partition_begin, partition_counts);
+  HY_HIP(hipGetLastError());
+  uint32_t flags[4] = {0, 0, 0, 0};
+  uint64_t total = 0;
+  HY_HIP(hipMemcpyAsync(flags, c.misc, 16, hipMemcpyDeviceToHost, s));
+  HY_HIP(hipMemcpyAsync(&total, c.totals + 1, 8, hipMemcpyDeviceToHost, s));
+  HY_HIP(hipStreamSynchronize(s));
+  if (flags[1]) return fail(HY_ERR_KERNEL, "join look-back did not complete");
+  if (result) {
+    result->total_pairs = total;
+    result->capacity_required = total;
+  }
+  if (flags[2] || total > out_capacity)
+    return fail(HY_ERR_CAPACITY, "join output needs " + std::to_string(total) + " pairs");
+  return HY_OK;
+}
+
+int type_bytes(int32_t t) { return (t == HY_TYPE_INT32 || t == HY_TYPE_FLOAT) ? 4 : (t == HY_TYPE_INT64 || t == HY_TYPE_DOUBLE) ? 8 : 0; }
+
+template <typename F>
+hy_status dispatch_type(int32_t t, F&& f) {
+  switch (t) {
+    case HY_TYPE_INT32:
+      return f(int32_t{});
+    case HY_TYPE_INT64:
+      return f(int64_t{});
+    case HY_TYPE_FLOAT:
+      return f(float{});
+    case HY_TYPE_DOUBLE:
+      return f(double{});
+  }
+  return fail(HY_ERR_UNSUPPORTED, "join column type");
+}
+
+hy_status prepare(const hy_join_side* build, const hy_join_side* probe, const hy_join_params* params, SidePlan& bp,
+                  SidePlan& pp) {
+  if (!params) return fail(HY_ERR_INVALID_ARGUMENT, "params");
+  if (params->radix_bits > 16) return fail(HY_ERR_UNSUPPORTED, "radix_bits > 16");
+  if (!(params->mode == HY_JOIN_INNER || params->mode == HY_JOIN_LEFT || params->mode == HY_JOIN_RIGHT ||
+        params->mode == HY_JOIN_SEMI || params->mode == HY_JOIN_ANTI))
+    return fail(HY_ERR_UNSUPPORTED, "join mode");
+  hy_status st = plan_side(build, bp);
+  if (st != HY_OK) return st;
+  st = plan_side(probe, pp);
+  if (st != HY_OK) return st;
+  // fuse the dereference when the side is a reference table (one PosList per chunk shared by the join column)
+  bp.fuse = (!bp.referenced.empty() && build->fuse_dereference) ? 1 : 0;
+  pp.fuse = (!pp.referenced.empty() && probe->fuse_dereference) ? 1 : 0;
+  if (!type_bytes(build->value_type) || !type_bytes(probe->value_type) || !type_bytes(params->hashed_type))
+    return fail(HY_ERR_UNSUPPORTED, "join column type");
+  return HY_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+hy_status hy_join_hash_workspace_size(const hy_join_side* build, const hy_join_side* probe,
+                                      const hy_join_params* params, size_t* bytes) {
+  if (!bytes) return fail(HY_ERR_INVALID_ARGUMENT, "bytes");
+  SidePlan bp, pp;
+  hy_status st = prepare(build, probe, params, bp, pp);
+  if (st != HY_OK) return st;
+  const Geometry g = geometry(params->radix_bits);
+  *bytes = type_bytes(params->hashed_type) == 4 ? join_bytes<int32_t>(bp, pp, g) : join_bytes<int64_t>(bp, pp, g);
+  return HY_OK;
+}
+
+hy_status hy_join_hash(const hy_join_side* build, const hy_join_side* probe, const hy_join_params* params,
+                       hy_row_id* out_build, hy_row_id* out_probe, uint64_t out_capacity, uint64_t* partition_begin,
+                       uint32_t* partition_counts, hy_join_result* result, void* workspace, size_t workspace_bytes,
+                       hy_stream_t stream) {
+  SidePlan bp, pp;
+  hy_status st = prepare(build, probe, params, bp, pp);
+  if (st != HY_OK) return st;
+  if (!partition_begin || !partition_counts) return fail(HY_ERR_INVALID_ARGUMENT, "partition arrays");
+  hipStream_t s = S(stream);
+  return dispatch_type(params->hashed_type, [&](auto htag) -> hy_status {
+    using H = decltype(htag);
+    return dispatch_type(build->value_type, [&](auto btag) -> hy_status {
+      using TB = decltype(btag);
+      return dispatch_type(probe->value_type, [&](auto ptag) -> hy_status {
+        using TP = decltype(ptag);
+        // only hashed types reachable through JoinHashTraits are instantiated
+        constexpr bool ok_b = sizeof(H) >= sizeof(TB) || std::is_floating_point_v<H>;
+        constexpr bool ok_p = sizeof(H) >= sizeof(TP) || std::is_floating_point_v<H>;
+        constexpr bool ok_f = !(std::is_floating_point_v<TB> && !std::is_floating_point_v<H>) &&
+                              !(std::is_floating_point_v<TP> && !std::is_floating_point_v<H>);
+        if constexpr (ok_b && ok_p && ok_f) {
+          return join_typed<TB, TP, H>(bp, pp, params, out_build, out_probe, out_capacity, partition_begin,
+                                       partition_counts, result, workspace, workspace_bytes, s);
+        } else {
+          return fail(HY_ERR_UNSUPPORTED, "hashed type not reachable from column types");
+        }
+      });
+    });
+  });
+}
+
+hy_status hy_dereference_row_ids(const hy_row_id* rows, uint64_t n, const hy_row_id* const* chunk_pos_lists,
+                                 hy_row_id* out, hy_stream_t stream) {
+  if (n == 0) return HY_OK;
+  hipLaunchKernelGGL(hyk::dereference_kernel, dim3(grid_for(n, 256)), dim3(256), 0, S(stream), rows, n,
+                     chunk_pos_lists, out);
+  HY_HIP(hipGetLastError());
+  return HY_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,311 @@
+// Python bindings of the host operator layer (tests, bench, smoke). Mirrors the reference's C++ test vocabulary:
+// load_table, ChunkEncoder, TableWrapper, TableScan, JoinHash, Aggregate, ReferenceColumn, PosList.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "device.hpp"
+#include "operators.hpp"
+#include "storage.hpp"
+
+namespace py = pybind11;
+using namespace hyrise;
+
+namespace {
+
+AllTypeVariant to_variant(const py::handle& o) {
+  if (o.is_none()) return NullValue{};
+  if (py::isinstance<py::bool_>(o)) return static_cast<int32_t>(o.cast<bool>());
+  if (py::isinstance<py::int_>(o)) {
+    const auto v = o.cast<long long>();
+    if (v >= INT32_MIN && v <= INT32_MAX) return static_cast<int32_t>(v);
+    return static_cast<int64_t>(v);
+  }
+  if (py::isinstance<py::float_>(o)) return o.cast<double>();
+  if (py::isinstance<py::str>(o)) return o.cast<std::string>();
+  // typed wrappers from Python: (type_name, value)
+  if (py::isinstance<py::tuple>(o) && py::len(o) == 2) {
+    const auto t = o[py::int_(0)].cast<std::string>();
+    const py::handle v = o[py::int_(1)];
+    if (t == "int") return v.cast<int32_t>();
+    if (t == "long") return v.cast<int64_t>();
+    if (t == "float") return v.cast<float>();
+    if (t == "double") return v.cast<double>();
+    if (t == "string") return v.cast<std::string>();
+  }
+  throw std::invalid_argument("cannot convert Python object to AllTypeVariant");
+}
+
+py::object to_py(const AllTypeVariant& v) {
+  switch (v.index()) {
+    case 0:
+      return py::none();
+    case 1:
+      return py::int_(std::get<int32_t>(v));
+    case 2:
+      return py::int_(std::get<int64_t>(v));
+    case 3:
+      return py::float_(static_cast<double>(std::get<float>(v)));
+    case 4:
+      return py::float_(std::get<double>(v));
+    default:
+      return py::str(std::get<std::string>(v));
+  }
+}
+
+py::array_t<uint32_t> pos_list_array(const PosList& pl) {
+  py::array_t<uint32_t> a({static_cast<py::ssize_t>(pl.size()), static_cast<py::ssize_t>(2)});
+  if (!pl.empty()) std::memcpy(a.mutable_data(), pl.data(), pl.size() * sizeof(RowID));
+  return a;
+}
+
+std::shared_ptr<PosList> pos_list_from_array(py::array_t<uint32_t, py::array::c_style | py::array::forcecast> a) {
+  Assert(a.ndim() == 2 && a.shape(1) == 2, "PosList array must have shape (n, 2)");
+  auto pl = std::make_shared<PosList>(a.shape(0));
+  if (a.shape(0)) std::memcpy(pl->data(), a.data(), a.shape(0) * sizeof(RowID));
+  return pl;
+}
+
+// Builds a data table from numpy columns (one array per column), split into chunks of chunk_size rows.
+std::shared_ptr<Table> table_from_arrays(const std::vector<std::tuple<std::string, DataType, bool>>& defs_in,
+                                         const std::vector<py::array>& arrays, const std::vector<py::object>& nulls,
+                                         uint32_t chunk_size) {
+  TableColumnDefinitions defs;
+  for (const auto& [n, t, nl] : defs_in) defs.emplace_back(n, t, nl);
+  auto table = std::make_shared<Table>(defs, TableType::Data, chunk_size);
+  Assert(arrays.size() == defs.size(), "one array per column");
+  const size_t rows = arrays.empty() ? 0 : static_cast<size_t>(arrays[0].shape(0));
+  for (size_t begin = 0; begin < rows; begin += chunk_size) {
+    const size_t n = std::min<size_t>(chunk_size, rows - begin);
+    ChunkColumns cols;
+    for (size_t c = 0; c < defs.size(); ++c) {
+      Assert(static_cast<size_t>(arrays[c].shape(0)) == rows, "columns must have equal length");
+      std::optional<std::vector<uint8_t>> nv;
+      if (defs[c].nullable) {
+        nv.emplace(n, 0);
+        if (c < nulls.size() && !nulls[c].is_none()) {
+          auto na = nulls[c].cast<py::array_t<uint8_t, py::array::c_style | py::array::forcecast>>();
+          std::memcpy(nv->data(), na.data() + begin, n);
+        }
+      }
+      resolve_data_type(defs[c].data_type, [&](auto tag) {
+        using T = decltype(tag);
+        if constexpr (std::is_same_v<T, std::string>) {
+          std::vector<std::string> v;
+          for (size_t i = 0; i < n; ++i) v.push_back(py::str(arrays[c][py::int_(begin + i)]).cast<std::string>());
+          cols.push_back(std::make_shared<ValueColumn<std::string>>(std::move(v), std::move(nv)));
+        } else {
+          auto a = py::array_t<T, py::array::c_style | py::array::forcecast>(arrays[c]);
+          std::vector<T> v(a.data() + begin, a.data() + begin + n);
+          cols.push_back(std::make_shared<ValueColumn<T>>(std::move(v), std::move(nv)));
+        }
+      });
+    }
+    table->append_chunk(cols);
+  }
+  return table;
+}
+
+py::list table_rows(const Table& t) {
+  py::list rows;
+  for (const auto& chunk : t.chunks()) {
+    for (ChunkOffset o = 0; o < chunk->size(); ++o) {
+      py::tuple row(chunk->column_count());
+      for (ColumnID c = 0; c < chunk->column_count(); ++c) row[c] = to_py((*chunk->get_column(c))[o]);
+      rows.append(row);
+    }
+  }
+  return rows;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_hyrise_host, m) {
+  m.doc() = "Hyrise MI355X operator layer (host side)";
+
+  py::register_exception<std::logic_error>(m, "LogicError", PyExc_RuntimeError);
+
+  py::enum_<DataType>(m, "DataType")
+      .value("Null", DataType::Null)
+      .value("Int", DataType::Int)
+      .value("Long", DataType::Long)
+      .value("Float", DataType::Float)
+      .value("Double", DataType::Double)
+      .value("String", DataType::String);
+  py::enum_<PredicateCondition>(m, "PredicateCondition")
+      .value("Equals", PredicateCondition::Equals)
+      .value("NotEquals", PredicateCondition::NotEquals)
+      .value("LessThan", PredicateCondition::LessThan)
+      .value("LessThanEquals", PredicateCondition::LessThanEquals)
+      .value("GreaterThan", PredicateCondition::GreaterThan)
+      .value("GreaterThanEquals", PredicateCondition::GreaterThanEquals)
+      .value("Between", PredicateCondition::Between)
+      .value("In", PredicateCondition::In)
+      .value("Like", PredicateCondition::Like)
+      .value("NotLike", PredicateCondition::NotLike)
+      .value("IsNull", PredicateCondition::IsNull)
+      .value("IsNotNull", PredicateCondition::IsNotNull);
+  py::enum_<JoinMode>(m, "JoinMode")
+      .value("Inner", JoinMode::Inner)
+      .value("Left", JoinMode::Left)
+      .value("Right", JoinMode::Right)
+      .value("Outer", JoinMode::Outer)
+      .value("Cross", JoinMode::Cross)
+      .value("Semi", JoinMode::Semi)
+      .value("Anti", JoinMode::Anti);
+  py::enum_<TableType>(m, "TableType").value("References", TableType::References).value("Data", TableType::Data);
+  py::enum_<EncodingType>(m, "EncodingType")
+      .value("Unencoded", EncodingType::Unencoded)
+      .value("Dictionary", EncodingType::Dictionary)
+      .value("RunLength", EncodingType::RunLength)
+      .value("FixedStringDictionary", EncodingType::FixedStringDictionary)
+      .value("FrameOfReference", EncodingType::FrameOfReference);
+  py::enum_<AggregateFunction>(m, "AggregateFunction")
+      .value("Min", AggregateFunction::Min)
+      .value("Max", AggregateFunction::Max)
+      .value("Sum", AggregateFunction::Sum)
+      .value("Avg", AggregateFunction::Avg)
+      .value("Count", AggregateFunction::Count)
+      .value("CountDistinct", AggregateFunction::CountDistinct);
+
+  py::class_<BaseColumn, std::shared_ptr<BaseColumn>>(m, "BaseColumn")
+      .def("size", &BaseColumn::size)
+      .def("__len__", &BaseColumn::size)
+      .def("data_type", &BaseColumn::data_type)
+      .def("encoding_type", &BaseColumn::encoding_type)
+      .def("is_reference", &BaseColumn::is_reference)
+      .def("__getitem__", [](const BaseColumn& c, uint32_t o) {
+        if (o >= c.size()) throw py::index_error();
+        return to_py(c[o]);
+      })
+      .def("values", [](const BaseColumn& c) {
+        py::list l;
+        for (ChunkOffset o = 0; o < c.size(); ++o) l.append(to_py(c[o]));
+        return l;
+      })
+      .def("attribute_vector_width", [](const BaseColumn& c) -> int {
+        const auto* d = dynamic_cast<const BaseDictionaryColumn*>(&c);
+        Assert(d != nullptr, "not a dictionary column");
+        return d->attribute_vector().width();
+      })
+      .def("lower_bound", [](const BaseColumn& c, py::object v) {
+        const auto* d = dynamic_cast<const BaseDictionaryColumn*>(&c);
+        Assert(d != nullptr, "not a dictionary column");
+        return d->lower_bound(to_variant(v));
+      })
+      .def("upper_bound", [](const BaseColumn& c, py::object v) {
+        const auto* d = dynamic_cast<const BaseDictionaryColumn*>(&c);
+        Assert(d != nullptr, "not a dictionary column");
+        return d->upper_bound(to_variant(v));
+      })
+      .def("unique_values_count", [](const BaseColumn& c) {
+        const auto* d = dynamic_cast<const BaseDictionaryColumn*>(&c);
+        Assert(d != nullptr, "not a dictionary column");
+        return d->unique_values_count();
+      });
+
+  py::class_<ReferenceColumn, BaseColumn, std::shared_ptr<ReferenceColumn>>(m, "ReferenceColumn")
+      .def(py::init([](std::shared_ptr<Table> t, ColumnID c, py::array_t<uint32_t> pl) {
+             return std::make_shared<ReferenceColumn>(t, c, pos_list_from_array(pl));
+           }),
+           py::arg("referenced_table"), py::arg("referenced_column_id"), py::arg("pos_list"))
+      .def("pos_list", [](const ReferenceColumn& c) { return pos_list_array(*c.pos_list()); })
+      .def("pos_list_id", [](const ReferenceColumn& c) { return reinterpret_cast<uintptr_t>(c.pos_list().get()); })
+      .def("referenced_table", [](const ReferenceColumn& c) { return std::const_pointer_cast<Table>(c.referenced_table()); })
+      .def("referenced_column_id", &ReferenceColumn::referenced_column_id)
+      .def("referenced_table_id",
+           [](const ReferenceColumn& c) { return reinterpret_cast<uintptr_t>(c.referenced_table().get()); });
+
+  py::class_<Chunk, std::shared_ptr<Chunk>>(m, "Chunk")
+      .def("size", &Chunk::size)
+      .def("column_count", &Chunk::column_count)
+      .def("get_column", &Chunk::get_column);
+
+  py::class_<Table, std::shared_ptr<Table>>(m, "Table")
+      .def(py::init([](const std::vector<std::tuple<std::string, DataType, bool>>& defs, TableType type,
+                       uint32_t chunk_size) {
+             TableColumnDefinitions d;
+             for (const auto& [n, t, nl] : defs) d.emplace_back(n, t, nl);
+             return std::make_shared<Table>(d, type, chunk_size);
+           }),
+           py::arg("column_definitions"), py::arg("type") = TableType::Data, py::arg("chunk_size") = CHUNK_MAX_SIZE)
+      .def_static("from_arrays", &table_from_arrays, py::arg("column_definitions"), py::arg("arrays"),
+                  py::arg("nulls") = std::vector<py::object>{}, py::arg("chunk_size") = CHUNK_MAX_SIZE)
+      .def("id", [](const Table& t) { return reinterpret_cast<uintptr_t>(&t); })
+      .def("type", &Table::type)
+      .def("column_count", &Table::column_count)
+      .def("row_count", &Table::row_count)
+      .def("chunk_count", &Table::chunk_count)
+      .def("max_chunk_size", &Table::max_chunk_size)
+      .def("column_name", &Table::column_name)
+      .def("column_names", &Table::column_names)
+      .def("column_data_type", &Table::column_data_type)
+      .def("column_is_nullable", &Table::column_is_nullable)
+      .def("column_id_by_name", &Table::column_id_by_name)
+      .def("get_chunk", &Table::get_chunk)
+      .def("append", [](Table& t, const py::list& values) {
+        std::vector<AllTypeVariant> v;
+        for (auto o : values) v.push_back(to_variant(o));
+        t.append(v);
+      })
+      .def("append_chunk", [](Table& t, const std::vector<std::shared_ptr<BaseColumn>>& cols) { t.append_chunk(cols); })
+      .def("get_value", [](const Table& t, ColumnID c, uint64_t r) { return to_py(t.get_value(c, r)); })
+      .def("rows", [](const Table& t) { return table_rows(t); })
+      .def("column_definitions", [](const Table& t) {
+        py::list l;
+        for (const auto& d : t.column_definitions()) l.append(py::make_tuple(d.name, d.data_type, d.nullable));
+        return l;
+      });
+
+  m.def("load_table", &load_table, py::arg("file_name"), py::arg("chunk_size") = CHUNK_MAX_SIZE);
+  m.def("encode_chunks", &ChunkEncoder::encode_chunks);
+  m.def("encode_all_chunks", &ChunkEncoder::encode_all_chunks);
+  m.def("join_hashed_type", &join_hashed_type);
+  m.def("join_radix_bits", [](uint64_t rows, uint32_t key_bytes) { return hy_join_radix_bits(rows, key_bytes); });
+  m.def("device_count", []() {
+    int n = 0;
+    hy_get_device_count(&n);
+    return n;
+  });
+  m.def("build_info", []() { return std::string(hy_build_info()); });
+
+  py::class_<OperatorPerformanceData>(m, "OperatorPerformanceData")
+      .def_readonly("walltime_ns", &OperatorPerformanceData::walltime_ns)
+      .def_readonly("rows_in", &OperatorPerformanceData::rows_in);
+
+  py::class_<AbstractOperator, std::shared_ptr<AbstractOperator>>(m, "AbstractOperator")
+      .def("execute", &AbstractOperator::execute, py::call_guard<py::gil_scoped_release>())
+      .def("get_output", [](const AbstractOperator& o) { return std::const_pointer_cast<Table>(o.get_output()); })
+      .def("name", &AbstractOperator::name)
+      .def("description", &AbstractOperator::description)
+      .def("performance_data", &AbstractOperator::performance_data);
+
+  py::class_<TableWrapper, AbstractOperator, std::shared_ptr<TableWrapper>>(m, "TableWrapper")
+      .def(py::init<std::shared_ptr<const Table>>());
+
+  py::class_<TableScan, AbstractOperator, std::shared_ptr<TableScan>>(m, "TableScan")
+      .def(py::init([](std::shared_ptr<AbstractOperator> in, ColumnID col, PredicateCondition cond, py::object value) {
+             return std::make_shared<TableScan>(in, col, cond, to_variant(value));
+           }),
+           py::arg("input"), py::arg("column_id"), py::arg("predicate_condition"), py::arg("value"))
+      .def("set_excluded_chunk_ids", &TableScan::set_excluded_chunk_ids);
+
+  py::class_<JoinHash, AbstractOperator, std::shared_ptr<JoinHash>>(m, "JoinHash")
+      .def(py::init([](std::shared_ptr<AbstractOperator> l, std::shared_ptr<AbstractOperator> r, JoinMode mode,
+                       std::pair<ColumnID, ColumnID> cols, PredicateCondition cond, size_t radix_bits) {
+             return std::make_shared<JoinHash>(l, r, mode, cols, cond, radix_bits);
+           }),
+           py::arg("left"), py::arg("right"), py::arg("mode"), py::arg("column_ids"), py::arg("predicate_condition"),
+           py::arg("radix_bits") = 9)
+      .def("used_radix_bits", &JoinHash::used_radix_bits);
+
+  py::class_<AggregateColumnDefinition>(m, "AggregateColumnDefinition")
+      .def(py::init<std::optional<ColumnID>, AggregateFunction>(), py::arg("column"), py::arg("function"))
+      .def_readonly("column", &AggregateColumnDefinition::column)
+      .def_readonly("function", &AggregateColumnDefinition::function);
+
+  py::class_<Aggregate, AbstractOperator, std::shared_ptr<Aggregate>>(m, "Aggregate")
+      .def(py::init<std::shared_ptr<const AbstractOperator>, std::vector<AggregateColumnDefinition>,
+                    std::vector<ColumnID>>(),
+           py::arg("input"), py::arg("aggregates"), py::arg("groupby_column_ids"));
+}

@@ -1,0 +1,125 @@
+#include "device.hpp"
+
+#include <algorithm>
+#include <cstring>
+
+namespace hyrise {
+
+namespace {
+struct StreamHolder {
+  hy_stream_t stream = nullptr;
+  ~StreamHolder() {
+    if (stream) hy_stream_destroy(stream);
+  }
+};
+
+std::shared_ptr<DeviceBuffer> upload(const void* host, size_t bytes, hy_stream_t s) {
+  auto buf = std::make_shared<DeviceBuffer>(std::max<size_t>(bytes, 16));
+  if (bytes) hy_check(hy_memcpy_htod(buf->get(), host, bytes, s), "hy_memcpy_htod");
+  return buf;
+}
+}  // namespace
+
+void require_device() {
+  int n = 0;
+  hy_get_device_count(&n);
+  if (n <= 0) Fail("hyrise-amd: no HIP device available — the GPU operators have no CPU fallback");
+}
+
+hy_stream_t operator_stream() {
+  thread_local StreamHolder holder;
+  if (!holder.stream) {
+    require_device();
+    hy_check(hy_stream_create(&holder.stream), "hy_stream_create");
+  }
+  return holder.stream;
+}
+
+int32_t hy_type_of(DataType t) {
+  switch (t) {
+    case DataType::Int:
+      return HY_TYPE_INT32;
+    case DataType::Long:
+      return HY_TYPE_INT64;
+    case DataType::Float:
+      return HY_TYPE_FLOAT;
+    case DataType::Double:
+      return HY_TYPE_DOUBLE;
+    default:
+      return 0;
+  }
+}
+
+std::shared_ptr<DeviceColumn> device_column(const BaseColumn& column) {
+  return column.device_mirror_or_create([&]() {
+    hy_stream_t s = operator_stream();
+    auto d = std::make_shared<DeviceColumn>();
+    d->desc.size = static_cast<uint32_t>(column.size());
+    if (const auto* dict = dynamic_cast<const BaseDictionaryColumn*>(&column)) {
+      const auto& av = dict->attribute_vector();
+      d->data = upload(av.bytes().data(), av.bytes().size(), s);
+      d->desc.kind = HY_COL_DICT;
+      d->desc.vid_width = av.width();
+      d->desc.dictionary_size = static_cast<uint32_t>(dict->unique_values_count());
+      d->desc.data = d->data->get();
+      if (column.data_type() != DataType::String) {
+        resolve_data_type(column.data_type(), [&](auto tag) {
+          using T = decltype(tag);
+          if constexpr (!std::is_same_v<T, std::string>) {
+            const auto& dv = static_cast<const DictionaryColumn<T>&>(column).dictionary();
+            d->dictionary = upload(dv.data(), dv.size() * sizeof(T), s);
+            d->desc.dictionary = d->dictionary->get();
+          }
+        });
+      }
+    } else {
+      Assert(!column.is_reference(), "device_column of a ReferenceColumn");
+      Assert(column.data_type() != DataType::String,
+             "hyrise-amd: unencoded string columns are not resident on the device (dictionary-encode them)");
+      resolve_data_type(column.data_type(), [&](auto tag) {
+        using T = decltype(tag);
+        if constexpr (!std::is_same_v<T, std::string>) {
+          const auto& vc = static_cast<const ValueColumn<T>&>(column);
+          d->data = upload(vc.values().data(), vc.values().size() * sizeof(T), s);
+          d->desc.data = d->data->get();
+          if (vc.is_nullable()) {
+            d->nulls = upload(vc.null_values().data(), vc.null_values().size(), s);
+            d->desc.nulls = d->nulls->as<uint8_t>();
+          }
+        }
+      });
+      d->desc.kind = HY_COL_VALUE;
+    }
+    hy_check(hy_stream_synchronize(s), "hy_stream_synchronize");
+    return d;
+  });
+}
+
+std::shared_ptr<DevicePosList> device_pos_list(const PosList& pos_list) {
+  if (auto d = pos_list.device_mirror()) return d;
+  hy_stream_t s = operator_stream();
+  auto d = std::make_shared<DevicePosList>();
+  d->size = pos_list.size();
+  d->rows = upload(pos_list.data(), pos_list.size() * sizeof(RowID), s);
+  hy_check(hy_stream_synchronize(s), "hy_stream_synchronize");
+  pos_list.set_device_mirror(d);
+  return d;
+}
+
+std::shared_ptr<PosList> pos_list_from_device(std::shared_ptr<DeviceBuffer> rows, uint64_t offset, uint64_t n) {
+  auto pl = std::make_shared<PosList>(n);
+  if (n) {
+    hy_stream_t s = operator_stream();
+    hy_check(hy_memcpy_dtoh(pl->data(), rows->as<RowID>() + offset, n * sizeof(RowID), s), "hy_memcpy_dtoh");
+    hy_check(hy_stream_synchronize(s), "hy_stream_synchronize");
+  }
+  // device mirror: a view into the shared buffer (kept alive by the shared_ptr)
+  auto d = std::make_shared<DevicePosList>();
+  d->size = n;
+  d->rows = std::move(rows);
+  d->view_offset = offset;
+  pl->set_device_mirror(d);
+  return pl;
+}
+
+}  // namespace hyrise

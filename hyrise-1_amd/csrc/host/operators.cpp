@@ -1,0 +1,589 @@
+#include "operators.hpp"
+
+#include <algorithm>
+#include <numeric>
+#include <unordered_map>
+
+namespace hyrise {
+
+// reference abstract_operator.cpp:25-54
+void AbstractOperator::execute() {
+  Assert(!_input_left || _input_left->get_output(), "Left input has not been executed");
+  Assert(!_input_right || _input_right->get_output(), "Right input has not been executed");
+  Assert(!_output, "Operator has already been executed");
+  const auto t0 = std::chrono::steady_clock::now();
+  _output = _on_execute();
+  _on_cleanup();
+  _performance_data.walltime_ns = static_cast<uint64_t>(
+      std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count());
+}
+
+// ================================================================================================================
+// TableScan
+// ================================================================================================================
+namespace {
+
+int32_t value_op(PredicateCondition c) {
+  switch (c) {
+    case PredicateCondition::Equals:
+      return HY_OP_EQ;
+    case PredicateCondition::NotEquals:
+      return HY_OP_NE;
+    case PredicateCondition::LessThan:
+      return HY_OP_LT;
+    case PredicateCondition::LessThanEquals:
+      return HY_OP_LE;
+    case PredicateCondition::GreaterThan:
+      return HY_OP_GT;
+    case PredicateCondition::GreaterThanEquals:
+      return HY_OP_GE;
+    default:
+      Fail("Unsupported operator.");  // reference with_comparator, type_comparison.hpp:100-123
+  }
+}
+
+// Dictionary rewrite: reference single_column_table_scan_impl.cpp:87-205 and .hpp:52-76.
+void dictionary_predicate(const BaseDictionaryColumn& col, PredicateCondition cond, const AllTypeVariant& value,
+                          int32_t* op, uint32_t* search_vid) {
+  ValueID svid;
+  switch (cond) {
+    case PredicateCondition::Equals:
+    case PredicateCondition::NotEquals:
+    case PredicateCondition::LessThan:
+    case PredicateCondition::GreaterThanEquals:
+      svid = col.lower_bound(value);
+      break;
+    case PredicateCondition::LessThanEquals:
+    case PredicateCondition::GreaterThan:
+      svid = col.upper_bound(value);
+      break;
+    default:
+      Fail("Unsupported comparison type encountered");
+  }
+  // _right_value_matches_all
+  bool all = false, none = false;
+  switch (cond) {
+    case PredicateCondition::Equals:
+      all = svid != col.upper_bound(value) && col.unique_values_count() == 1u;
+      none = svid == col.upper_bound(value);
+      break;
+    case PredicateCondition::NotEquals:
+      all = svid == col.upper_bound(value);
+      none = svid == col.upper_bound(value) && col.unique_values_count() == 1u;
+      break;
+    case PredicateCondition::LessThan:
+    case PredicateCondition::LessThanEquals:
+      all = svid == INVALID_VALUE_ID;
+      none = svid == 0u;
+      break;
+    case PredicateCondition::GreaterThanEquals:
+    case PredicateCondition::GreaterThan:
+      all = svid == 0u;
+      none = svid == INVALID_VALUE_ID;
+      break;
+    default:
+      break;
+  }
+  *search_vid = svid;
+  if (all) {
+    *op = HY_OP_ALL;
+    return;
+  }
+  if (none) {
+    *op = HY_OP_NONE;
+    return;
+  }
+  switch (cond) {  // _with_operator_for_dict_column_scan
+    case PredicateCondition::Equals:
+      *op = HY_OP_EQ;
+      break;
+    case PredicateCondition::NotEquals:
+      *op = HY_OP_NE;
+      break;
+    case PredicateCondition::LessThan:
+    case PredicateCondition::LessThanEquals:
+      *op = HY_OP_LT;
+      break;
+    default:
+      *op = HY_OP_GE;
+      break;
+  }
+}
+
+// Builds the scan descriptor of one data column chunk. constant_out receives type_cast<T>(value) for value columns.
+hy_scan_chunk scan_descriptor(const BaseColumn& column, DataType type, PredicateCondition cond,
+                              const AllTypeVariant& value) {
+  hy_scan_chunk sc{};
+  if (const auto* dict = dynamic_cast<const BaseDictionaryColumn*>(&column)) {
+    dictionary_predicate(*dict, cond, value, &sc.op, &sc.search_vid);
+  } else {
+    Assert(type != DataType::String,
+           "hyrise-amd: TableScan on an unencoded string column is not supported by the device path");
+    sc.op = value_op(cond);
+  }
+  sc.column = device_column(column)->desc;
+  return sc;
+}
+
+struct ScanConstant {
+  alignas(8) unsigned char bytes[8] = {0};
+};
+
+ScanConstant typed_constant(DataType type, const AllTypeVariant& value) {
+  ScanConstant c;
+  switch (type) {
+    case DataType::Int: {
+      const int32_t v = type_cast<int32_t>(value);
+      std::memcpy(c.bytes, &v, 4);
+      break;
+    }
+    case DataType::Long: {
+      const int64_t v = type_cast<int64_t>(value);
+      std::memcpy(c.bytes, &v, 8);
+      break;
+    }
+    case DataType::Float: {
+      const float v = type_cast<float>(value);
+      std::memcpy(c.bytes, &v, 4);
+      break;
+    }
+    case DataType::Double: {
+      const double v = type_cast<double>(value);
+      std::memcpy(c.bytes, &v, 8);
+      break;
+    }
+    default:
+      break;
+  }
+  return c;
+}
+
+// Iteration order of the reference's std::unordered_map<ChunkID, ChunkOffsetsList> built by
+// split_pos_list_by_chunk_id (chunk_offset_mapping.cpp:5-21): replay the insertion of the distinct chunk ids in
+// order of first appearance into the same libstdc++ container type.
+std::vector<ChunkID> unordered_map_order(const std::vector<ChunkID>& first_appearance_order) {
+  std::unordered_map<ChunkID, int> m;
+  for (const auto c : first_appearance_order) m[c];
+  std::vector<ChunkID> out;
+  for (const auto& kv : m) out.push_back(kv.first);
+  return out;
+}
+
+}  // namespace
+
+const std::string TableScan::description() const {
+  return "TableScan (Col #" + std::to_string(_left_column_id) + " " + predicate_condition_to_string(_predicate_condition) +
+         ")";
+}
+
+std::shared_ptr<const Table> TableScan::_on_execute() {
+  const auto in_table = input_table_left();
+  switch (_predicate_condition) {
+    case PredicateCondition::Like:
+    case PredicateCondition::NotLike:
+    case PredicateCondition::IsNull:
+    case PredicateCondition::IsNotNull:
+    case PredicateCondition::In:
+      Fail("hyrise-amd: predicate " + predicate_condition_to_string(_predicate_condition) +
+           " is not supported by the device TableScan");
+    case PredicateCondition::Between:
+      Fail("Unsupported comparison type encountered");  // reference: BETWEEN is split before it reaches the scan
+    default:
+      break;
+  }
+  auto output = std::make_shared<Table>(in_table->column_definitions(), TableType::References);
+  // reference single_column_table_scan_impl.cpp:23-36: comparing with NULL matches nothing
+  if (variant_is_null(_right_value)) return output;
+  require_device();
+  hy_stream_t s = operator_stream();
+  const auto col_type = in_table->column_data_type(_left_column_id);
+  std::vector<bool> excluded(in_table->chunk_count(), false);
+  for (const auto c : _excluded_chunk_ids)
+    if (c < excluded.size()) excluded[c] = true;
+  _performance_data.rows_in = in_table->row_count();
+
+  if (in_table->type() == TableType::Data) {
+    std::vector<hy_scan_chunk> descs;
+    std::vector<ChunkID> chunk_ids;
+    std::vector<uint32_t> sizes;
+    uint64_t total = 0;
+    for (ChunkID c = 0; c < in_table->chunk_count(); ++c) {
+      if (excluded[c]) continue;
+      const auto column = in_table->get_chunk(c)->get_column(_left_column_id);
+      auto d = scan_descriptor(*column, col_type, _predicate_condition, _right_value);
+      d.out_begin = total;
+      total += column->size();
+      descs.push_back(d);
+      chunk_ids.push_back(c);
+      sizes.push_back(static_cast<uint32_t>(column->size()));
+    }
+    if (descs.empty()) return output;
+    const auto constant = typed_constant(col_type, _right_value);
+    size_t ws_bytes = 0;
+    hy_check(hy_table_scan_workspace_size(sizes.data(), static_cast<uint32_t>(sizes.size()), &ws_bytes),
+             "hy_table_scan_workspace_size");
+    DeviceBuffer ws(ws_bytes);
+    DeviceBuffer offsets(std::max<uint64_t>(total, 1) * 4);
+    DeviceBuffer counts(descs.size() * 4);
+    hy_check(hy_table_scan(descs.data(), static_cast<uint32_t>(descs.size()), hy_type_of(col_type), constant.bytes,
+                           offsets.as<uint32_t>(), counts.as<uint32_t>(), ws.get(), ws_bytes, s),
+             "hy_table_scan");
+    std::vector<uint32_t> h_counts(descs.size());
+    hy_check(hy_memcpy_dtoh(h_counts.data(), counts.get(), 4 * descs.size(), s), "hy_memcpy_dtoh");
+    hy_check(hy_stream_synchronize(s), "sync");
+    uint64_t matches = 0;
+    for (auto c : h_counts) matches += c;
+    // device RowIDs for all matches (so downstream GPU operators reuse them), then the host PosLists
+    auto rows = std::make_shared<DeviceBuffer>(std::max<uint64_t>(matches, 1) * sizeof(RowID));
+    uint64_t pos = 0;
+    std::vector<std::pair<uint64_t, uint32_t>> views;  // (offset, count) per chunk
+    for (size_t k = 0; k < descs.size(); ++k) {
+      if (h_counts[k])
+        hy_check(hy_expand_row_ids(chunk_ids[k], offsets.as<uint32_t>() + descs[k].out_begin, h_counts[k],
+                                   rows->as<hy_row_id>() + pos, s),
+                 "hy_expand_row_ids");
+      views.emplace_back(pos, h_counts[k]);
+      pos += h_counts[k];
+    }
+    hy_check(hy_stream_synchronize(s), "sync");
+    for (size_t k = 0; k < descs.size(); ++k) {
+      if (views[k].second == 0) continue;  // reference table_scan.cpp:99: no empty output chunks
+      auto pl = pos_list_from_device(rows, views[k].first, views[k].second);
+      ChunkColumns cols;
+      for (ColumnID col = 0; col < in_table->column_count(); ++col)
+        cols.push_back(std::make_shared<ReferenceColumn>(in_table, col, pl));
+      output->append_chunk(cols);
+    }
+    return output;
+  }
+
+  // ---- reference-table input (base_single_column_table_scan_impl.cpp:36-60, table_scan.cpp:104-145) ----
+  for (ChunkID c = 0; c < in_table->chunk_count(); ++c) {
+    if (excluded[c]) continue;
+    const auto chunk = in_table->get_chunk(c);
+    const auto ref = std::dynamic_pointer_cast<const ReferenceColumn>(chunk->get_column(_left_column_id));
+    Assert(ref != nullptr, "All columns should be of type ReferenceColumn.");
+    const auto& pos_list = *ref->pos_list();
+    if (pos_list.empty()) continue;
+    const auto& rtable = ref->referenced_table();
+    const ColumnID rcol = ref->referenced_column_id();
+    std::vector<hy_scan_chunk> rdesc(rtable->chunk_count());
+    for (ChunkID r = 0; r < rtable->chunk_count(); ++r)
+      rdesc[r] = scan_descriptor(*rtable->get_chunk(r)->get_column(rcol), col_type, _predicate_condition, _right_value);
+    const auto constant = typed_constant(col_type, _right_value);
+    const auto dpl = device_pos_list(pos_list);
+    const uint64_t m = pos_list.size();
+
+    // distinct referenced chunks in order of first appearance -> the reference's unordered_map iteration order
+    DeviceBuffer first(std::max<size_t>(rtable->chunk_count(), 1) * 8);
+    hy_check(hy_pos_list_chunk_first_seen(dpl->ptr(), m, rtable->chunk_count(), first.as<uint64_t>(), s),
+             "hy_pos_list_chunk_first_seen");
+    std::vector<uint64_t> h_first(rtable->chunk_count());
+    hy_check(hy_memcpy_dtoh(h_first.data(), first.get(), 8 * h_first.size(), s), "dtoh");
+    hy_check(hy_stream_synchronize(s), "sync");
+    std::vector<ChunkID> seen;
+    for (ChunkID r = 0; r < h_first.size(); ++r)
+      if (h_first[r] != ~0ull) seen.push_back(r);
+    std::sort(seen.begin(), seen.end(), [&](ChunkID a, ChunkID b) { return h_first[a] < h_first[b]; });
+    const auto groups = unordered_map_order(seen);
+
+    size_t ws_bytes = 0;
+    hy_check(hy_reference_scan_workspace_size(m, &ws_bytes), "hy_reference_scan_workspace_size");
+    DeviceBuffer ws(ws_bytes);
+    DeviceBuffer positions(std::max<uint64_t>(m, 1) * 4);
+    DeviceBuffer count(8);
+    uint64_t total = 0;
+    if (groups.size() <= 1) {
+      hy_check(hy_reference_scan(dpl->ptr(), m, rdesc.data(), static_cast<uint32_t>(rdesc.size()), hy_type_of(col_type),
+                                 constant.bytes, positions.as<uint32_t>(), count.as<uint64_t>(), ws.get(), ws_bytes, s),
+               "hy_reference_scan");
+      hy_check(hy_memcpy_dtoh(&total, count.get(), 8, s), "dtoh");
+      hy_check(hy_stream_synchronize(s), "sync");
+    } else {
+      // one pass per referenced chunk, in the unordered_map's iteration order (positions ascending inside each)
+      if (groups.size() > 64)
+        Fail("hyrise-amd: reference scan over a PosList spanning more than 64 chunks is not supported yet");
+      for (const auto g : groups) {
+        auto masked = rdesc;
+        for (ChunkID r = 0; r < masked.size(); ++r)
+          if (r != g) masked[r].op = HY_OP_NONE;
+        hy_check(hy_reference_scan(dpl->ptr(), m, masked.data(), static_cast<uint32_t>(masked.size()),
+                                   hy_type_of(col_type), constant.bytes, positions.as<uint32_t>() + total,
+                                   count.as<uint64_t>(), ws.get(), ws_bytes, s),
+                 "hy_reference_scan");
+        uint64_t n = 0;
+        hy_check(hy_memcpy_dtoh(&n, count.get(), 8, s), "dtoh");
+        hy_check(hy_stream_synchronize(s), "sync");
+        total += n;
+      }
+    }
+    if (total == 0) continue;
+    // filtered PosLists, shared per distinct input PosList (table_scan.cpp:115-145)
+    std::map<const PosList*, std::shared_ptr<PosList>> filtered;
+    ChunkColumns cols;
+    for (ColumnID col = 0; col < in_table->column_count(); ++col) {
+      const auto rc = std::dynamic_pointer_cast<const ReferenceColumn>(chunk->get_column(col));
+      Assert(rc != nullptr, "All columns should be of type ReferenceColumn.");
+      auto& f = filtered[rc->pos_list().get()];
+      if (!f) {
+        const auto src = device_pos_list(*rc->pos_list());
+        auto rows = std::make_shared<DeviceBuffer>(total * sizeof(RowID));
+        hy_check(hy_gather_row_ids(src->ptr(), positions.as<uint32_t>(), total, rows->as<hy_row_id>(), s),
+                 "hy_gather_row_ids");
+        hy_check(hy_stream_synchronize(s), "sync");
+        f = pos_list_from_device(rows, 0, total);
+      }
+      cols.push_back(std::make_shared<ReferenceColumn>(rc->referenced_table(), rc->referenced_column_id(), f));
+    }
+    output->append_chunk(cols);
+  }
+  return output;
+}
+
+// ================================================================================================================
+// JoinHash
+// ================================================================================================================
+DataType join_hashed_type(DataType l, DataType r) {
+  auto is_float = [](DataType t) { return t == DataType::Float || t == DataType::Double; };
+  if (l == DataType::String || r == DataType::String) return DataType::String;
+  if (is_float(l) && is_float(r)) return data_type_size(l) < data_type_size(r) ? r : l;
+  if (!is_float(l) && !is_float(r)) return data_type_size(l) < data_type_size(r) ? r : l;
+  return is_float(l) ? l : r;
+}
+
+namespace {
+
+using PosListsVec = std::vector<std::shared_ptr<const PosList>>;
+
+struct JoinSideInput {
+  std::vector<hy_join_chunk> chunks;
+  std::vector<hy_column_chunk> referenced;
+  int32_t fuse = 0;
+  // per-column PosList groups for reference tables (setup_pos_lists_by_column, join_hash.cpp:533-562)
+  std::vector<int> column_group;         // column -> group id
+  std::vector<PosListsVec> groups;       // group id -> per-chunk PosLists
+  int join_group = -1;
+};
+
+JoinSideInput describe_side(const std::shared_ptr<const Table>& table, ColumnID column_id) {
+  JoinSideInput in;
+  const bool is_ref = table->type() == TableType::References;
+  if (is_ref) {
+    std::map<PosListsVec, int> ids;
+    for (ColumnID col = 0; col < table->column_count(); ++col) {
+      PosListsVec v;
+      for (ChunkID c = 0; c < table->chunk_count(); ++c)
+        v.push_back(std::static_pointer_cast<const ReferenceColumn>(table->get_chunk(c)->get_column(col))->pos_list());
+      auto it = ids.find(v);
+      if (it == ids.end()) {
+        it = ids.emplace(v, static_cast<int>(in.groups.size())).first;
+        in.groups.push_back(v);
+      }
+      in.column_group.push_back(it->second);
+    }
+    in.join_group = in.column_group.at(column_id);
+  }
+  std::shared_ptr<const Table> referenced;
+  ColumnID rcol = 0;
+  for (ChunkID c = 0; c < table->chunk_count(); ++c) {
+    const auto column = table->get_chunk(c)->get_column(column_id);
+    hy_join_chunk jc{};
+    jc.chunk_id = c;
+    jc.size = static_cast<uint32_t>(column->size());
+    if (is_ref) {
+      const auto rc = std::static_pointer_cast<const ReferenceColumn>(column);
+      if (!referenced) {
+        referenced = rc->referenced_table();
+        rcol = rc->referenced_column_id();
+      }
+      Assert(rc->referenced_table() == referenced && rc->referenced_column_id() == rcol,
+             "hyrise-amd: a join column referencing several tables is not supported");
+      jc.pos_list = device_pos_list(*rc->pos_list())->ptr();
+    } else {
+      jc.column = device_column(*column)->desc;
+    }
+    in.chunks.push_back(jc);
+  }
+  if (referenced) {
+    for (ChunkID r = 0; r < referenced->chunk_count(); ++r)
+      in.referenced.push_back(device_column(*referenced->get_chunk(r)->get_column(rcol))->desc);
+    // fuse the dereference when every column shares the join column's PosLists and referenced table
+    bool fuse = true;
+    for (ColumnID col = 0; col < table->column_count() && fuse; ++col) {
+      if (in.column_group[col] != in.join_group) fuse = false;
+      for (ChunkID c = 0; c < table->chunk_count() && fuse; ++c)
+        if (std::static_pointer_cast<const ReferenceColumn>(table->get_chunk(c)->get_column(col))->referenced_table() !=
+            referenced)
+          fuse = false;
+    }
+    in.fuse = fuse ? 1 : 0;
+  }
+  return in;
+}
+
+int32_t join_mode(JoinMode m) {
+  switch (m) {
+    case JoinMode::Inner:
+    case JoinMode::Outer:  // the reference's probe emits only matches for Outer (join_hash.cpp:405-435)
+    case JoinMode::Cross:
+      return HY_JOIN_INNER;
+    case JoinMode::Left:
+      return HY_JOIN_LEFT;
+    case JoinMode::Right:
+      return HY_JOIN_RIGHT;
+    case JoinMode::Semi:
+      return HY_JOIN_SEMI;
+    case JoinMode::Anti:
+      return HY_JOIN_ANTI;
+  }
+  return HY_JOIN_INNER;
+}
+
+// write_output_columns (join_hash.cpp:564-613) for one side of one partition.
+void write_output_columns(ChunkColumns& out, const std::shared_ptr<const Table>& input_table, const JoinSideInput& side,
+                          const std::shared_ptr<DeviceBuffer>& rows, uint64_t offset, uint64_t n,
+                          std::map<std::pair<int, uint64_t>, std::shared_ptr<PosList>>& cache,
+                          std::vector<std::shared_ptr<DeviceBuffer>>& group_ptr_arrays,
+                          std::shared_ptr<Table>& dummy_table) {
+  hy_stream_t s = operator_stream();
+  if (input_table->type() == TableType::Data) {
+    auto pl = pos_list_from_device(rows, offset, n);
+    for (ColumnID col = 0; col < input_table->column_count(); ++col)
+      out.push_back(std::make_shared<ReferenceColumn>(input_table, col, pl));
+    return;
+  }
+  if (input_table->chunk_count() == 0) {
+    if (!dummy_table) dummy_table = Table::create_dummy_table(input_table->column_definitions());
+    auto pl = pos_list_from_device(rows, offset, n);
+    for (ColumnID col = 0; col < input_table->column_count(); ++col)
+      out.push_back(std::make_shared<ReferenceColumn>(dummy_table, col, pl));
+    return;
+  }
+  std::shared_ptr<PosList> fused;
+  for (ColumnID col = 0; col < input_table->column_count(); ++col) {
+    const int g = side.column_group[col];
+    std::shared_ptr<PosList> pl;
+    if (side.fuse) {
+      if (!fused) fused = pos_list_from_device(rows, offset, n);
+      pl = fused;
+    } else {
+      auto& cached = cache[{g, offset}];
+      if (!cached) {
+        if (!group_ptr_arrays[g]) {
+          std::vector<const hy_row_id*> ptrs;
+          for (const auto& p : side.groups[g]) ptrs.push_back(device_pos_list(*p)->ptr());
+          group_ptr_arrays[g] = std::make_shared<DeviceBuffer>(ptrs.size() * sizeof(void*));
+          hy_check(hy_memcpy_htod(group_ptr_arrays[g]->get(), ptrs.data(), ptrs.size() * sizeof(void*), s), "htod");
+          hy_check(hy_stream_synchronize(s), "sync");
+        }
+        auto deref = std::make_shared<DeviceBuffer>(std::max<uint64_t>(n, 1) * sizeof(RowID));
+        hy_check(hy_dereference_row_ids(rows->as<hy_row_id>() + offset, n,
+                                        group_ptr_arrays[g]->as<const hy_row_id* const>(), deref->as<hy_row_id>(), s),
+                 "hy_dereference_row_ids");
+        hy_check(hy_stream_synchronize(s), "sync");
+        cached = pos_list_from_device(deref, 0, n);
+      }
+      pl = cached;
+    }
+    const auto rc = std::static_pointer_cast<const ReferenceColumn>(input_table->get_chunk(0)->get_column(col));
+    out.push_back(std::make_shared<ReferenceColumn>(rc->referenced_table(), rc->referenced_column_id(), pl));
+  }
+}
+
+}  // namespace
+
+std::shared_ptr<const Table> JoinHash::_on_execute() {
+  const auto left_in = input_table_left();
+  const auto right_in = input_table_right();
+  // reference join_hash.cpp:55-76
+  bool inputs_swapped = (_mode == JoinMode::Left || _mode == JoinMode::Anti || _mode == JoinMode::Semi);
+  if (!inputs_swapped && left_in->row_count() > right_in->row_count()) inputs_swapped = true;
+  const auto build_table = inputs_swapped ? right_in : left_in;
+  const auto probe_table = inputs_swapped ? left_in : right_in;
+  const ColumnID build_col = inputs_swapped ? _column_ids.second : _column_ids.first;
+  const ColumnID probe_col = inputs_swapped ? _column_ids.first : _column_ids.second;
+  const DataType build_type = build_table->column_data_type(build_col);
+  const DataType probe_type = probe_table->column_data_type(probe_col);
+  const DataType hashed = join_hashed_type(build_type, probe_type);
+  if (hashed == DataType::String)
+    Fail("hyrise-amd: JoinHash on string columns is not supported by the device path");
+
+  const bool semi_anti = _mode == JoinMode::Semi || _mode == JoinMode::Anti;
+  TableColumnDefinitions defs;
+  if (inputs_swapped) {
+    defs = probe_table->column_definitions();
+    if (!semi_anti)
+      for (const auto& d : build_table->column_definitions()) defs.push_back(d);
+  } else {
+    defs = build_table->column_definitions();
+    for (const auto& d : probe_table->column_definitions()) defs.push_back(d);
+  }
+  auto output = std::make_shared<Table>(defs, TableType::References);
+  require_device();
+  hy_stream_t s = operator_stream();
+  _performance_data.rows_in = build_table->row_count() + probe_table->row_count();
+
+  JoinSideInput bside = describe_side(build_table, build_col);
+  JoinSideInput pside = describe_side(probe_table, probe_col);
+  hy_join_side b{bside.chunks.data(), static_cast<uint32_t>(bside.chunks.size()), hy_type_of(build_type),
+                 bside.referenced.data(), static_cast<uint32_t>(bside.referenced.size()), bside.fuse};
+  hy_join_side p{pside.chunks.data(), static_cast<uint32_t>(pside.chunks.size()), hy_type_of(probe_type),
+                 pside.referenced.data(), static_cast<uint32_t>(pside.referenced.size()), pside.fuse};
+  hy_join_params prm{};
+  prm.mode = join_mode(_mode);
+  prm.hashed_type = hy_type_of(hashed);
+  // the constructor's radix_bits is ignored and recomputed from the build side (join_hash.cpp:640-668)
+  prm.radix_bits = hy_join_radix_bits(build_table->row_count(), static_cast<uint32_t>(data_type_size(build_type)));
+  prm.seed = 17;
+  _used_radix_bits = prm.radix_bits;
+
+  size_t ws_bytes = 0;
+  hy_check(hy_join_hash_workspace_size(&b, &p, &prm, &ws_bytes), "hy_join_hash_workspace_size");
+  DeviceBuffer ws(ws_bytes);
+  const uint32_t n_parts = 1u << prm.radix_bits;
+  DeviceBuffer part_begin(8 * n_parts), part_count(4 * n_parts);
+  uint64_t capacity = std::max<uint64_t>(probe_table->row_count() + build_table->row_count(), 16);
+  std::shared_ptr<DeviceBuffer> out_b, out_p;
+  hy_join_result res{};
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    out_b = std::make_shared<DeviceBuffer>(capacity * sizeof(RowID));
+    out_p = std::make_shared<DeviceBuffer>(capacity * sizeof(RowID));
+    const hy_status st = hy_join_hash(&b, &p, &prm, out_b->as<hy_row_id>(), out_p->as<hy_row_id>(), capacity,
+                                      part_begin.as<uint64_t>(), part_count.as<uint32_t>(), &res, ws.get(), ws_bytes, s);
+    if (st == HY_ERR_CAPACITY && attempt == 0) {
+      capacity = std::max<uint64_t>(res.capacity_required, 16);
+      continue;
+    }
+    hy_check(st, "hy_join_hash");
+    break;
+  }
+  std::vector<uint64_t> h_begin(n_parts);
+  std::vector<uint32_t> h_count(n_parts);
+  hy_check(hy_memcpy_dtoh(h_begin.data(), part_begin.get(), 8 * n_parts, s), "dtoh");
+  hy_check(hy_memcpy_dtoh(h_count.data(), part_count.get(), 4 * n_parts, s), "dtoh");
+  hy_check(hy_stream_synchronize(s), "sync");
+
+  std::map<std::pair<int, uint64_t>, std::shared_ptr<PosList>> bcache, pcache;
+  std::vector<std::shared_ptr<DeviceBuffer>> bptrs(bside.groups.size()), pptrs(pside.groups.size());
+  std::shared_ptr<Table> bdummy, pdummy;
+  for (uint32_t part = 0; part < n_parts; ++part) {
+    const uint64_t n = h_count[part];
+    if (n == 0) continue;  // join_hash.cpp:835-837
+    ChunkColumns cols;
+    if (inputs_swapped) {
+      write_output_columns(cols, probe_table, pside, out_p, h_begin[part], n, pcache, pptrs, pdummy);
+      if (!semi_anti) write_output_columns(cols, build_table, bside, out_b, h_begin[part], n, bcache, bptrs, bdummy);
+    } else {
+      write_output_columns(cols, build_table, bside, out_b, h_begin[part], n, bcache, bptrs, bdummy);
+      write_output_columns(cols, probe_table, pside, out_p, h_begin[part], n, pcache, pptrs, pdummy);
+    }
+    output->append_chunk(cols);
+  }
+  return output;
+}
+
+std::shared_ptr<const Table> Aggregate::_on_execute() {
+  Fail("hyrise-amd: Aggregate device path not built yet");
+}
+
+}  // namespace hyrise

@@ -1,0 +1,160 @@
+// Operator layer: the reference's AbstractOperator surface with GPU-backed TableScan / JoinHash / Aggregate.
+//
+//   AbstractOperator::execute / get_output / _on_execute   reference src/lib/operators/abstract_operator.cpp:25-67
+//   TableWrapper                                           reference src/lib/operators/table_wrapper.cpp
+//   TableScan(in, ColumnID, PredicateCondition, value)     reference src/lib/operators/table_scan.hpp:22-23
+//   JoinHash(l, r, JoinMode, ColumnIDPair, PredicateCondition, radix_bits = 9)
+//                                                          reference src/lib/operators/join_hash.hpp:26-28
+//   Aggregate(in, aggregates, groupby_column_ids)          reference src/lib/operators/aggregate.hpp:87-88
+//
+// The compute of TableScan / JoinHash / Aggregate runs in the gfx950 kernels behind include/hyrise_amd.h; there is
+// no CPU fallback: without a device these operators throw.
+#pragma once
+
+#include <chrono>
+#include <map>
+#include <optional>
+#include <string>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+#include "device.hpp"
+#include "storage.hpp"
+
+namespace hyrise {
+
+enum class OperatorType { TableWrapper, TableScan, JoinHash, Aggregate, Mock };
+
+struct OperatorPerformanceData {
+  uint64_t walltime_ns = 0;  // reference operator_performance_data.hpp:15
+  uint64_t rows_in = 0;
+};
+
+class AbstractOperator : public std::enable_shared_from_this<AbstractOperator> {
+ public:
+  AbstractOperator(OperatorType type, std::shared_ptr<const AbstractOperator> left = nullptr,
+                   std::shared_ptr<const AbstractOperator> right = nullptr)
+      : _type(type), _input_left(std::move(left)), _input_right(std::move(right)) {}
+  virtual ~AbstractOperator() = default;
+
+  void execute();
+  std::shared_ptr<const Table> get_output() const { return _output; }
+  void clear_output() { _output.reset(); }
+
+  OperatorType type() const { return _type; }
+  virtual const std::string name() const = 0;
+  virtual const std::string description() const { return name(); }
+
+  std::shared_ptr<const AbstractOperator> input_left() const { return _input_left; }
+  std::shared_ptr<const AbstractOperator> input_right() const { return _input_right; }
+  std::shared_ptr<const Table> input_table_left() const { return _input_left->get_output(); }
+  std::shared_ptr<const Table> input_table_right() const { return _input_right->get_output(); }
+  const OperatorPerformanceData& performance_data() const { return _performance_data; }
+
+ protected:
+  virtual std::shared_ptr<const Table> _on_execute() = 0;
+  virtual void _on_cleanup() {}
+
+  const OperatorType _type;
+  std::shared_ptr<const AbstractOperator> _input_left, _input_right;
+  std::shared_ptr<const Table> _output;
+  OperatorPerformanceData _performance_data;
+};
+
+class TableWrapper final : public AbstractOperator {
+ public:
+  explicit TableWrapper(std::shared_ptr<const Table> table)
+      : AbstractOperator(OperatorType::TableWrapper), _table(std::move(table)) {}
+  const std::string name() const override { return "TableWrapper"; }
+
+ protected:
+  std::shared_ptr<const Table> _on_execute() override { return _table; }
+  std::shared_ptr<const Table> _table;
+};
+
+class TableScan final : public AbstractOperator {
+ public:
+  TableScan(std::shared_ptr<const AbstractOperator> in, ColumnID left_column_id, PredicateCondition predicate_condition,
+            AllTypeVariant right_value)
+      : AbstractOperator(OperatorType::TableScan, std::move(in)),
+        _left_column_id(left_column_id),
+        _predicate_condition(predicate_condition),
+        _right_value(std::move(right_value)) {}
+
+  const std::string name() const override { return "TableScan"; }
+  const std::string description() const override;
+  ColumnID left_column_id() const { return _left_column_id; }
+  PredicateCondition predicate_condition() const { return _predicate_condition; }
+  const AllTypeVariant& right_value() const { return _right_value; }
+  void set_excluded_chunk_ids(const std::vector<ChunkID>& ids) { _excluded_chunk_ids = ids; }
+
+ protected:
+  std::shared_ptr<const Table> _on_execute() override;
+
+ private:
+  ColumnID _left_column_id;
+  PredicateCondition _predicate_condition;
+  AllTypeVariant _right_value;
+  std::vector<ChunkID> _excluded_chunk_ids;
+};
+
+class JoinHash final : public AbstractOperator {
+ public:
+  JoinHash(std::shared_ptr<const AbstractOperator> left, std::shared_ptr<const AbstractOperator> right, JoinMode mode,
+           std::pair<ColumnID, ColumnID> column_ids, PredicateCondition predicate_condition, size_t radix_bits = 9)
+      : AbstractOperator(OperatorType::JoinHash, std::move(left), std::move(right)),
+        _mode(mode),
+        _column_ids(column_ids),
+        _predicate_condition(predicate_condition),
+        _radix_bits(radix_bits) {
+    Assert(predicate_condition == PredicateCondition::Equals, "Operator not supported by Hash Join.");
+  }
+  const std::string name() const override { return "JoinHash"; }
+  JoinMode mode() const { return _mode; }
+  // radix bits actually used by the last execution (the constructor argument is ignored, as in the reference)
+  uint32_t used_radix_bits() const { return _used_radix_bits; }
+
+ protected:
+  std::shared_ptr<const Table> _on_execute() override;
+
+ private:
+  JoinMode _mode;
+  std::pair<ColumnID, ColumnID> _column_ids;
+  PredicateCondition _predicate_condition;
+  size_t _radix_bits;
+  uint32_t _used_radix_bits = 0;
+};
+
+struct AggregateColumnDefinition {
+  AggregateColumnDefinition(std::optional<ColumnID> c, AggregateFunction f) : column(c), function(f) {}
+  std::optional<ColumnID> column;
+  AggregateFunction function;
+};
+
+class Aggregate final : public AbstractOperator {
+ public:
+  Aggregate(std::shared_ptr<const AbstractOperator> in, std::vector<AggregateColumnDefinition> aggregates,
+            std::vector<ColumnID> groupby_column_ids)
+      : AbstractOperator(OperatorType::Aggregate, std::move(in)),
+        _aggregates(std::move(aggregates)),
+        _groupby_column_ids(std::move(groupby_column_ids)) {
+    Assert(!(_aggregates.empty() && _groupby_column_ids.empty()),
+           "Neither aggregate nor groupby columns have been specified");
+  }
+  const std::string name() const override { return "Aggregate"; }
+  const std::vector<AggregateColumnDefinition>& aggregates() const { return _aggregates; }
+  const std::vector<ColumnID>& groupby_column_ids() const { return _groupby_column_ids; }
+
+ protected:
+  std::shared_ptr<const Table> _on_execute() override;
+
+ private:
+  std::vector<AggregateColumnDefinition> _aggregates;
+  std::vector<ColumnID> _groupby_column_ids;
+};
+
+// JoinHashTraits (reference src/lib/operators/join_hash/hash_traits.hpp:9-42) over data types.
+DataType join_hashed_type(DataType left, DataType right);
+
+}  // namespace hyrise

@@ -1,0 +1,184 @@
+#include "storage.hpp"
+
+#include <fstream>
+#include <sstream>
+
+namespace hyrise {
+
+BaseColumn::~BaseColumn() = default;
+
+ReferenceColumn::ReferenceColumn(std::shared_ptr<const Table> referenced_table, ColumnID referenced_column_id,
+                                 std::shared_ptr<const PosList> pos)
+    : BaseColumn(referenced_table->column_data_type(referenced_column_id)),
+      _referenced_table(std::move(referenced_table)),
+      _referenced_column_id(referenced_column_id),
+      _pos_list(std::move(pos)) {}
+
+// reference reference_column.cpp:23-33
+AllTypeVariant ReferenceColumn::operator[](ChunkOffset o) const {
+  const RowID row_id = _pos_list->at(o);
+  if (row_id.is_null()) return NullValue{};
+  const auto chunk = _referenced_table->get_chunk(row_id.chunk_id);
+  return (*chunk->get_column(_referenced_column_id))[row_id.chunk_offset];
+}
+
+void Chunk::append(const std::vector<AllTypeVariant>& values) {
+  Assert(values.size() == _columns.size(), "append: wrong number of values");
+  for (size_t i = 0; i < values.size(); ++i) _columns[i]->append(values[i]);
+}
+
+ColumnID Table::column_id_by_name(const std::string& name) const {
+  for (ColumnID i = 0; i < _defs.size(); ++i)
+    if (_defs[i].name == name) return i;
+  Fail("Couldn't find column '" + name + "'");
+}
+
+std::vector<std::string> Table::column_names() const {
+  std::vector<std::string> out;
+  for (const auto& d : _defs) out.push_back(d.name);
+  return out;
+}
+
+uint64_t Table::row_count() const {
+  uint64_t n = 0;
+  for (const auto& c : _chunks) n += c->size();
+  return n;
+}
+
+std::shared_ptr<BaseColumn> make_value_column(DataType t, bool nullable) {
+  std::shared_ptr<BaseColumn> out;
+  resolve_data_type(t, [&](auto tag) {
+    using T = decltype(tag);
+    out = std::make_shared<ValueColumn<T>>(nullable);
+  });
+  return out;
+}
+
+void Table::append_mutable_chunk() {
+  ChunkColumns cols;
+  for (const auto& d : _defs) cols.push_back(make_value_column(d.data_type, d.nullable));
+  _chunks.push_back(std::make_shared<Chunk>(std::move(cols)));
+}
+
+void Table::append(const std::vector<AllTypeVariant>& values) {
+  if (_chunks.empty() || _chunks.back()->size() >= _max_chunk_size) append_mutable_chunk();
+  _chunks.back()->append(values);
+}
+
+void Table::append_chunk(const ChunkColumns& columns) {
+  Assert(columns.size() == _defs.size(), "append_chunk: wrong number of columns");
+  const size_t n = columns.empty() ? 0 : columns[0]->size();
+  for (const auto& c : columns) {
+    Assert(c->size() == n, "Columns don't have the same length");
+    Assert(c->is_reference() == (_type == TableType::References), "Invalid column type");
+  }
+  _chunks.push_back(std::make_shared<Chunk>(columns));
+}
+
+AllTypeVariant Table::get_value(ColumnID column_id, uint64_t row) const {
+  for (const auto& c : _chunks) {
+    if (row < c->size()) return (*c->get_column(column_id))[static_cast<ChunkOffset>(row)];
+    row -= c->size();
+  }
+  Fail("Row does not exist.");
+}
+
+// reference dictionary_column/dictionary_encoder.hpp:57-130
+std::shared_ptr<BaseColumn> encode_dictionary(const BaseColumn& base) {
+  std::shared_ptr<BaseColumn> out;
+  resolve_data_type(base.data_type(), [&](auto tag) {
+    using T = decltype(tag);
+    const auto* vc = dynamic_cast<const ValueColumn<T>*>(&base);
+    Assert(vc != nullptr, "encode_dictionary needs a ValueColumn");
+    const auto& values = vc->values();
+    std::vector<T> dict;
+    dict.reserve(values.size());
+    for (size_t i = 0; i < values.size(); ++i)
+      if (!vc->is_null(static_cast<ChunkOffset>(i))) dict.push_back(values[i]);
+    std::sort(dict.begin(), dict.end());
+    dict.erase(std::unique(dict.begin(), dict.end()), dict.end());
+    dict.shrink_to_fit();
+    const auto null_value_id = static_cast<uint32_t>(dict.size());
+    std::vector<uint32_t> vids(values.size());
+    for (size_t i = 0; i < values.size(); ++i) {
+      if (vc->is_null(static_cast<ChunkOffset>(i))) {
+        vids[i] = null_value_id;
+      } else {
+        vids[i] = static_cast<uint32_t>(std::distance(dict.cbegin(), std::lower_bound(dict.cbegin(), dict.cend(), values[i])));
+      }
+    }
+    const uint32_t max_value = static_cast<uint32_t>(dict.size() + 1u);
+    auto av = std::make_shared<const AttributeVector>(vids, max_value);
+    out = std::make_shared<DictionaryColumn<T>>(std::make_shared<const std::vector<T>>(std::move(dict)), std::move(av),
+                                                null_value_id);
+  });
+  return out;
+}
+
+void ChunkEncoder::encode_chunks(const std::shared_ptr<Table>& table, const std::vector<ChunkID>& chunk_ids,
+                                 EncodingType encoding) {
+  Assert(table->type() == TableType::Data, "Only data tables can be encoded");
+  if (encoding == EncodingType::Unencoded) return;
+  if (encoding != EncodingType::Dictionary)
+    Fail("Encoding type not supported by the device path (only Unencoded and Dictionary)");
+  for (const auto chunk_id : chunk_ids) {
+    const auto chunk = table->get_chunk(chunk_id);
+    for (ColumnID c = 0; c < chunk->column_count(); ++c) {
+      const auto col = chunk->get_column(c);
+      if (col->encoding_type() == EncodingType::Dictionary) continue;
+      chunk->replace_column(c, encode_dictionary(*col));
+    }
+  }
+}
+
+void ChunkEncoder::encode_all_chunks(const std::shared_ptr<Table>& table, EncodingType encoding) {
+  std::vector<ChunkID> ids(table->chunk_count());
+  for (ChunkID i = 0; i < ids.size(); ++i) ids[i] = i;
+  encode_chunks(table, ids, encoding);
+}
+
+namespace {
+std::vector<std::string> split(const std::string& s, char delim) {
+  std::vector<std::string> out;
+  std::stringstream ss(s);
+  std::string item;
+  while (std::getline(ss, item, delim)) out.push_back(item);
+  return out;
+}
+}  // namespace
+
+// reference src/lib/utils/load_table.cpp:14-62
+std::shared_ptr<Table> load_table(const std::string& file_name, uint32_t chunk_size) {
+  std::ifstream infile(file_name);
+  Assert(infile.is_open(), "load_table: Could not find file " + file_name);
+  std::string line;
+  std::getline(infile, line);
+  const auto names = split(line, '|');
+  std::getline(infile, line);
+  auto types = split(line, '|');
+  TableColumnDefinitions defs;
+  std::vector<bool> nullable;
+  for (size_t i = 0; i < names.size(); ++i) {
+    const auto parts = split(types.at(i), '_');
+    const bool is_nullable = parts.size() > 1 && parts[1] == "null";
+    nullable.push_back(is_nullable);
+    defs.emplace_back(names[i], data_type_from_string(parts[0]), is_nullable);
+  }
+  auto table = std::make_shared<Table>(defs, TableType::Data, chunk_size);
+  while (std::getline(infile, line)) {
+    auto fields = split(line, '|');
+    std::vector<AllTypeVariant> values;
+    for (size_t i = 0; i < fields.size(); ++i) {
+      if (nullable[i] && fields[i] == "null")
+        values.emplace_back(NullValue{});
+      else
+        values.emplace_back(fields[i]);
+    }
+    // a trailing empty string field is dropped by getline-split; restore it
+    while (values.size() < defs.size()) values.emplace_back(std::string{});
+    table->append(values);
+  }
+  return table;
+}
+
+}  // namespace hyrise

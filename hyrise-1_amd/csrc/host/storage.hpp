@@ -1,0 +1,317 @@
+// Columnar storage mirror: Table -> Chunk -> {ValueColumn<T>, DictionaryColumn<T>, ReferenceColumn}.
+//
+// Same public surface and semantics as the reference's storage layer (the parts the hot path touches):
+//   Table          reference src/lib/storage/table.hpp:26-175, append_chunk table.cpp:143-170
+//   Chunk          reference src/lib/storage/chunk.hpp:41-160
+//   ValueColumn    reference src/lib/storage/value_column.hpp:15-73 (append: value_column.cpp:78-90)
+//   DictionaryColumn + DictionaryEncoder + FixedSizeByteAligned attribute vectors
+//                  reference src/lib/storage/dictionary_column.hpp:20-72, dictionary_column.cpp:75-95,
+//                  dictionary_column/dictionary_encoder.hpp:57-130, fixed_size_byte_aligned_compressor.cpp:21-43
+//   ReferenceColumn reference src/lib/storage/reference_column.hpp:19-50, reference_column.cpp:23-33
+//   load_table     reference src/lib/utils/load_table.cpp:14-62
+// Every column can carry a device-resident mirror (device.hpp) that GPU operators create on first use.
+#pragma once
+
+#include <algorithm>
+#include <memory>
+#include <mutex>
+#include <optional>
+#include <string>
+#include <vector>
+
+#include "types.hpp"
+
+namespace hyrise {
+
+class Table;
+struct DeviceColumn;  // device.hpp
+
+class BaseColumn : public std::enable_shared_from_this<BaseColumn> {
+ public:
+  explicit BaseColumn(DataType data_type) : _data_type(data_type) {}
+  virtual ~BaseColumn();
+
+  DataType data_type() const { return _data_type; }
+  virtual size_t size() const = 0;
+  virtual AllTypeVariant operator[](ChunkOffset chunk_offset) const = 0;
+  virtual void append(const AllTypeVariant& value) { Fail("Column is immutable"); }
+  virtual EncodingType encoding_type() const = 0;
+  virtual bool is_reference() const { return false; }
+
+  // Lazily created device mirror (owned by the column; invalidated by mutation).
+  std::shared_ptr<DeviceColumn> device_mirror() const {
+    std::lock_guard<std::mutex> lock(_device_mutex);
+    return _device;
+  }
+  void set_device_mirror(std::shared_ptr<DeviceColumn> d) const {
+    std::lock_guard<std::mutex> lock(_device_mutex);
+    _device = std::move(d);
+  }
+  // Returns the device mirror, creating it with create() under the column's lock on first use.
+  template <typename F>
+  std::shared_ptr<DeviceColumn> device_mirror_or_create(F&& create) const {
+    std::lock_guard<std::mutex> lock(_device_mutex);
+    if (!_device) _device = create();
+    return _device;
+  }
+
+ protected:
+  void invalidate_device() {
+    std::lock_guard<std::mutex> lock(_device_mutex);
+    _device.reset();
+  }
+  const DataType _data_type;
+  mutable std::mutex _device_mutex;
+  mutable std::shared_ptr<DeviceColumn> _device;
+};
+
+template <typename T>
+class ValueColumn final : public BaseColumn {
+ public:
+  explicit ValueColumn(bool nullable = false) : BaseColumn(data_type_from_type<T>()) {
+    if (nullable) _nulls.emplace();
+  }
+  ValueColumn(std::vector<T>&& values, std::optional<std::vector<uint8_t>>&& nulls)
+      : BaseColumn(data_type_from_type<T>()), _values(std::move(values)), _nulls(std::move(nulls)) {}
+
+  size_t size() const override { return _values.size(); }
+  EncodingType encoding_type() const override { return EncodingType::Unencoded; }
+
+  AllTypeVariant operator[](ChunkOffset o) const override {
+    if (_nulls && (*_nulls).at(o)) return NullValue{};
+    return _values.at(o);
+  }
+
+  void append(const AllTypeVariant& v) override {
+    invalidate_device();
+    const bool is_null = variant_is_null(v);
+    if (_nulls) {
+      _nulls->push_back(is_null ? 1 : 0);
+      _values.push_back(is_null ? T{} : type_cast<T>(v));
+      return;
+    }
+    Assert(!is_null, "ValueColumns is not nullable but value passed is null.");
+    _values.push_back(type_cast<T>(v));
+  }
+
+  bool is_nullable() const { return _nulls.has_value(); }
+  bool is_null(ChunkOffset o) const { return _nulls && (*_nulls)[o]; }
+  const std::vector<T>& values() const { return _values; }
+  std::vector<T>& values() {
+    invalidate_device();
+    return _values;
+  }
+  const std::vector<uint8_t>& null_values() const {
+    Assert(is_nullable(), "This ValueColumn does not support null values.");
+    return *_nulls;
+  }
+  std::vector<uint8_t>& null_values() {
+    Assert(is_nullable(), "This ValueColumn does not support null values.");
+    invalidate_device();
+    return *_nulls;
+  }
+
+ private:
+  std::vector<T> _values;
+  std::optional<std::vector<uint8_t>> _nulls;
+};
+
+// FixedSizeByteAligned attribute vector: uint8 / uint16 / uint32 value ids.
+class AttributeVector {
+ public:
+  AttributeVector() = default;
+  AttributeVector(const std::vector<uint32_t>& vids, uint32_t max_value) {
+    // reference fixed_size_byte_aligned_compressor.cpp:21-30: narrowest width that holds max_value
+    _width = max_value <= 0xFFu ? 1 : (max_value <= 0xFFFFu ? 2 : 4);
+    _size = vids.size();
+    _bytes.resize(_size * _width);
+    for (size_t i = 0; i < _size; ++i) {
+      const uint32_t v = vids[i];
+      std::memcpy(_bytes.data() + i * _width, &v, _width);  // little endian
+    }
+  }
+  AttributeVector(std::vector<uint8_t>&& bytes, int width, size_t size)
+      : _bytes(std::move(bytes)), _width(width), _size(size) {}
+
+  uint32_t get(size_t i) const {
+    switch (_width) {
+      case 1:
+        return _bytes[i];
+      case 2: {
+        uint16_t v;
+        std::memcpy(&v, _bytes.data() + 2 * i, 2);
+        return v;
+      }
+      default: {
+        uint32_t v;
+        std::memcpy(&v, _bytes.data() + 4 * i, 4);
+        return v;
+      }
+    }
+  }
+  int width() const { return _width; }
+  size_t size() const { return _size; }
+  const std::vector<uint8_t>& bytes() const { return _bytes; }
+
+ private:
+  std::vector<uint8_t> _bytes;
+  int _width = 1;
+  size_t _size = 0;
+};
+
+class BaseDictionaryColumn : public BaseColumn {
+ public:
+  using BaseColumn::BaseColumn;
+  virtual ValueID lower_bound(const AllTypeVariant& value) const = 0;
+  virtual ValueID upper_bound(const AllTypeVariant& value) const = 0;
+  virtual size_t unique_values_count() const = 0;
+  virtual ValueID null_value_id() const = 0;
+  virtual const AttributeVector& attribute_vector() const = 0;
+};
+
+template <typename T>
+class DictionaryColumn final : public BaseDictionaryColumn {
+ public:
+  DictionaryColumn(std::shared_ptr<const std::vector<T>> dictionary, std::shared_ptr<const AttributeVector> av,
+                   ValueID null_value_id)
+      : BaseDictionaryColumn(data_type_from_type<T>()),
+        _dictionary(std::move(dictionary)),
+        _attribute_vector(std::move(av)),
+        _null_value_id(null_value_id) {}
+
+  size_t size() const override { return _attribute_vector->size(); }
+  EncodingType encoding_type() const override { return EncodingType::Dictionary; }
+
+  AllTypeVariant operator[](ChunkOffset o) const override {
+    const ValueID vid = _attribute_vector->get(o);
+    if (vid == _null_value_id) return NullValue{};
+    return (*_dictionary)[vid];
+  }
+
+  // reference dictionary_column.cpp:75-95
+  ValueID lower_bound(const AllTypeVariant& value) const override {
+    Assert(!variant_is_null(value), "Null value passed.");
+    const T typed = type_cast<T>(value);
+    auto it = std::lower_bound(_dictionary->cbegin(), _dictionary->cend(), typed);
+    if (it == _dictionary->cend()) return INVALID_VALUE_ID;
+    return static_cast<ValueID>(std::distance(_dictionary->cbegin(), it));
+  }
+  ValueID upper_bound(const AllTypeVariant& value) const override {
+    Assert(!variant_is_null(value), "Null value passed.");
+    const T typed = type_cast<T>(value);
+    auto it = std::upper_bound(_dictionary->cbegin(), _dictionary->cend(), typed);
+    if (it == _dictionary->cend()) return INVALID_VALUE_ID;
+    return static_cast<ValueID>(std::distance(_dictionary->cbegin(), it));
+  }
+  size_t unique_values_count() const override { return _dictionary->size(); }
+  ValueID null_value_id() const override { return _null_value_id; }
+  const AttributeVector& attribute_vector() const override { return *_attribute_vector; }
+  const std::vector<T>& dictionary() const { return *_dictionary; }
+
+ private:
+  std::shared_ptr<const std::vector<T>> _dictionary;
+  std::shared_ptr<const AttributeVector> _attribute_vector;
+  ValueID _null_value_id;
+};
+
+class ReferenceColumn final : public BaseColumn {
+ public:
+  ReferenceColumn(std::shared_ptr<const Table> referenced_table, ColumnID referenced_column_id,
+                  std::shared_ptr<const PosList> pos);
+
+  size_t size() const override { return _pos_list->size(); }
+  EncodingType encoding_type() const override { return EncodingType::Unencoded; }
+  bool is_reference() const override { return true; }
+  AllTypeVariant operator[](ChunkOffset o) const override;
+
+  const std::shared_ptr<const PosList>& pos_list() const { return _pos_list; }
+  const std::shared_ptr<const Table>& referenced_table() const { return _referenced_table; }
+  ColumnID referenced_column_id() const { return _referenced_column_id; }
+
+ private:
+  std::shared_ptr<const Table> _referenced_table;
+  ColumnID _referenced_column_id;
+  std::shared_ptr<const PosList> _pos_list;
+};
+
+using ChunkColumns = std::vector<std::shared_ptr<BaseColumn>>;
+
+class Chunk {
+ public:
+  explicit Chunk(ChunkColumns columns) : _columns(std::move(columns)) {}
+  size_t size() const { return _columns.empty() ? 0 : _columns[0]->size(); }
+  uint16_t column_count() const { return static_cast<uint16_t>(_columns.size()); }
+  std::shared_ptr<BaseColumn> get_column(ColumnID id) const { return _columns.at(id); }
+  const ChunkColumns& columns() const { return _columns; }
+  // reference chunk.cpp:39-41
+  void replace_column(ColumnID id, std::shared_ptr<BaseColumn> c) { _columns.at(id) = std::move(c); }
+  void append(const std::vector<AllTypeVariant>& values);
+
+ private:
+  ChunkColumns _columns;
+};
+
+struct TableColumnDefinition {
+  TableColumnDefinition() = default;
+  TableColumnDefinition(std::string n, DataType t, bool null = false) : name(std::move(n)), data_type(t), nullable(null) {}
+  std::string name;
+  DataType data_type = DataType::Int;
+  bool nullable = false;
+};
+using TableColumnDefinitions = std::vector<TableColumnDefinition>;
+
+class Table {
+ public:
+  Table(TableColumnDefinitions defs, TableType type, uint32_t max_chunk_size = CHUNK_MAX_SIZE)
+      : _defs(std::move(defs)), _type(type), _max_chunk_size(max_chunk_size) {}
+
+  const TableColumnDefinitions& column_definitions() const { return _defs; }
+  TableType type() const { return _type; }
+  uint16_t column_count() const { return static_cast<uint16_t>(_defs.size()); }
+  const std::string& column_name(ColumnID id) const { return _defs.at(id).name; }
+  DataType column_data_type(ColumnID id) const { return _defs.at(id).data_type; }
+  bool column_is_nullable(ColumnID id) const { return _defs.at(id).nullable; }
+  ColumnID column_id_by_name(const std::string& name) const;
+  std::vector<std::string> column_names() const;
+
+  uint32_t max_chunk_size() const { return _max_chunk_size; }
+  uint32_t chunk_count() const { return static_cast<uint32_t>(_chunks.size()); }
+  uint64_t row_count() const;
+  std::shared_ptr<Chunk> get_chunk(ChunkID id) const { return _chunks.at(id); }
+  const std::vector<std::shared_ptr<Chunk>>& chunks() const { return _chunks; }
+
+  // reference table.cpp: append a row, opening a new chunk when the last one is full
+  void append(const std::vector<AllTypeVariant>& values);
+  void append_chunk(const ChunkColumns& columns);
+  void append_mutable_chunk();
+
+  AllTypeVariant get_value(ColumnID column_id, uint64_t row) const;
+
+  static std::shared_ptr<Table> create_dummy_table(const TableColumnDefinitions& defs) {
+    return std::make_shared<Table>(defs, TableType::Data);
+  }
+
+ private:
+  TableColumnDefinitions _defs;
+  TableType _type;
+  uint32_t _max_chunk_size;
+  std::vector<std::shared_ptr<Chunk>> _chunks;
+};
+
+// Creates an empty ValueColumn<T> for a data type.
+std::shared_ptr<BaseColumn> make_value_column(DataType t, bool nullable);
+
+// Dictionary encoding of one value column (reference dictionary_encoder.hpp:57-130).
+std::shared_ptr<BaseColumn> encode_dictionary(const BaseColumn& value_column);
+
+// ChunkEncoder (reference src/lib/storage/chunk_encoder.cpp): encode chunks of a data table. Only Unencoded and
+// Dictionary exist on the device path; other encodings are rejected.
+struct ChunkEncoder {
+  static void encode_chunks(const std::shared_ptr<Table>& table, const std::vector<ChunkID>& chunk_ids,
+                            EncodingType encoding);
+  static void encode_all_chunks(const std::shared_ptr<Table>& table, EncodingType encoding);
+};
+
+std::shared_ptr<Table> load_table(const std::string& file_name, uint32_t chunk_size = CHUNK_MAX_SIZE);
+
+}  // namespace hyrise

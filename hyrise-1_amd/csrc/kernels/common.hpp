@@ -1,0 +1,174 @@
+// Device-side building blocks shared by the gfx950 kernels: MurmurHash2, wave64 ballot/prefix primitives,
+// workgroup prefix sums and the decoupled look-back status words.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hyrise_amd.h"
+
+namespace hyk {
+
+constexpr int WAVE = 64;
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------------------------------------------------
+// MurmurHash2 (32 bit), as reference src/lib/utils/murmur_hash.cpp:21-75 computes it over the sizeof(T) bytes of
+// an arithmetic key (murmur_hash.hpp:11-14). Only 4- and 8-byte keys occur on the device path, so the tail switch
+// of the byte loop is never taken.
+// ------------------------------------------------------------------------------------------------------------
+__host__ __device__ inline uint32_t murmur_mix_word(uint32_t h, uint32_t k) {
+  const uint32_t m = 0x5bd1e995u;
+  k *= m;
+  k ^= k >> 24;
+  k *= m;
+  h *= m;
+  h ^= k;
+  return h;
+}
+
+__host__ __device__ inline uint32_t murmur_final(uint32_t h) {
+  const uint32_t m = 0x5bd1e995u;
+  h ^= h >> 13;
+  h *= m;
+  h ^= h >> 15;
+  return h;
+}
+
+__host__ __device__ inline uint32_t murmur2_u32(uint32_t key_bits, uint32_t seed) {
+  uint32_t h = seed ^ 4u;
+  h = murmur_mix_word(h, key_bits);
+  return murmur_final(h);
+}
+
+__host__ __device__ inline uint32_t murmur2_u64(uint64_t key_bits, uint32_t seed) {
+  uint32_t h = seed ^ 8u;
+  h = murmur_mix_word(h, static_cast<uint32_t>(key_bits));
+  h = murmur_mix_word(h, static_cast<uint32_t>(key_bits >> 32));
+  return murmur_final(h);
+}
+
+template <typename T>
+__host__ __device__ inline uint32_t murmur2(T key, uint32_t seed) {
+  if constexpr (sizeof(T) == 4) {
+    uint32_t bits;
+    __builtin_memcpy(&bits, &key, 4);
+    return murmur2_u32(bits, seed);
+  } else {
+    uint64_t bits;
+    __builtin_memcpy(&bits, &key, 8);
+    return murmur2_u64(bits, seed);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Wave64 helpers.
+// ------------------------------------------------------------------------------------------------------------
+__device__ inline int lane_id() { return __lane_id(); }
+
+__device__ inline uint64_t lanemask_lt() {
+  const int l = __lane_id();
+  return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+
+// Inclusive prefix sum over the 64 lanes of a wave.
+__device__ inline uint32_t wave_inclusive_sum(uint32_t v) {
+#pragma unroll
+  for (int d = 1; d < WAVE; d <<= 1) {
+    const uint32_t o = __shfl_up(v, d, WAVE);
+    if (__lane_id() >= d) v += o;
+  }
+  return v;
+}
+
+__device__ inline uint64_t wave_inclusive_sum64(uint64_t v) {
+#pragma unroll
+  for (int d = 1; d < WAVE; d <<= 1) {
+    const uint64_t o = __shfl_up(v, d, WAVE);
+    if (__lane_id() >= d) v += o;
+  }
+  return v;
+}
+
+__device__ inline uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, WAVE);
+  return v;
+}
+
+// Exclusive prefix over a workgroup of NT threads. Returns the exclusive prefix of v; *total = sum over the group.
+// scratch: NT/64 + 1 uint32 in LDS.
+template <int NT>
+__device__ inline uint32_t block_exclusive_sum(uint32_t v, uint32_t* scratch, uint32_t* total) {
+  constexpr int NW = NT / WAVE;
+  const int w = threadIdx.x / WAVE;
+  const uint32_t incl = wave_inclusive_sum(v);
+  if (__lane_id() == WAVE - 1) scratch[w] = incl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t run = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+      const uint32_t t = scratch[i];
+      scratch[i] = run;
+      run += t;
+    }
+    scratch[NW] = run;
+  }
+  __syncthreads();
+  const uint32_t res = scratch[w] + incl - v;
+  *total = scratch[NW];
+  __syncthreads();
+  return res;
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Decoupled look-back status words (single-pass chained scan across workgroups).
+//
+// Each word is one naturally aligned 8-byte {flag, value} granule written by ONE agent-scope relaxed atomic store
+// and polled by agent-scope relaxed atomic loads: the data is the flag, so no release/acquire fence is needed
+// (MI355X_MICROARCH.md "Valid forms", R2 granule). Words are zeroed by a memset before every launch. Tile ids are
+// handed out by an atomic ticket so a workgroup only ever waits on workgroups that are already running.
+// ------------------------------------------------------------------------------------------------------------
+constexpr uint64_t LB_FLAG_AGG = 1ull << 62;
+constexpr uint64_t LB_FLAG_PREFIX = 2ull << 62;
+constexpr uint64_t LB_VALUE_MASK = (1ull << 62) - 1;
+constexpr uint32_t LB_MAX_SPINS = 1u << 22;
+
+__device__ inline void lb_publish(uint64_t* word, uint64_t flag, uint64_t value) {
+  __hip_atomic_store(word, flag | value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ inline uint64_t lb_poll(const uint64_t* word) {
+  return __hip_atomic_load(const_cast<uint64_t*>(word), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Exclusive prefix for tile `tile`, looking back over tiles [first_tile, tile). Executed by one lane.
+// Returns false (and sets *error) if a predecessor never published within the spin bound.
+__device__ inline bool lb_lookback(const uint64_t* status, uint64_t first_tile, uint64_t tile, uint64_t* prefix,
+                                   uint32_t* error) {
+  uint64_t acc = 0;
+  uint64_t j = tile;
+  uint32_t spins = 0;
+  while (j > first_tile) {
+    const uint64_t s = lb_poll(&status[j - 1]);
+    const uint64_t flag = s & ~LB_VALUE_MASK;
+    if (flag == 0) {
+      if (++spins > LB_MAX_SPINS) {
+        __hip_atomic_store(error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *prefix = acc;
+        return false;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    acc += s & LB_VALUE_MASK;
+    if (flag == LB_FLAG_PREFIX) break;
+    --j;
+  }
+  *prefix = acc;
+  return true;
+}
+
+}  // namespace hyk

@@ -1,0 +1,729 @@
+// JoinHash kernels for gfx950: radix partitioning + per-partition LDS hash build/probe.
+//
+// The reference (src/lib/operators/join_hash.cpp) materializes {RowID, murmur2(v, 17), v} per row
+// (materialize_input, :203-285), partitions both sides by hash & (2^b - 1) with a stable, partition-major /
+// chunk-minor scatter (partition_radix_parallel, :287-355), builds one std::unordered_map per partition (build,
+// :127-185) and probes it partition by partition (probe / probe_semi_anti, :362-527). Its output order is therefore:
+// partition ascending, then probe rows in (chunk, offset) order, then build matches in (chunk, offset) order.
+//
+// This file reproduces that order exactly with an MI355X-shaped pipeline:
+//   pass 1  part1_hist / part1_scatter : read the join column straight from its chunks (value, dictionary, or
+//           through a PosList), murmur2-hash, stable scatter of 8-byte {key, payload} records by the HIGH digit of
+//           the partition id (up to 8 bits, 256 buckets). 8192-row tiles; per-wave match-any ranking keeps the
+//           scatter stable.
+//   pass 2  part2_hist / part2_scatter : inside every high-digit bucket, stable scatter by the LOW 8 bits. After
+//           pass 2 every radix partition is contiguous and in row order (MSD, so partition bounds fall out of the
+//           pass-2 histogram).
+//   join    join_partition : one workgroup per partition, taken in partition order by an atomic ticket. The build
+//           partition (~1-2k rows with the reference's radix-bit formula) is hashed into LDS; probe rows stream
+//           through it twice (count, then write) with a decoupled look-back across partitions in between, so the
+//           output of partition p starts right after partition p-1 — one contiguous pair of PosLists.
+// Roofline: HBM. Partition passes move 8 B/row per read or write; the join reads 8 B/row and writes 16 B/pair.
+#include <hip/hip_runtime.h>
+
+#include "common.hpp"
+
+namespace hyk {
+
+constexpr int PART_THREADS = 512;
+constexpr int PART_WAVES = PART_THREADS / WAVE;
+constexpr int PART_ITEMS = 16;                              // items per lane per tile
+constexpr int PART_TILE = PART_THREADS * PART_ITEMS;        // 8192 rows per tile
+constexpr int WAVE_SPAN = WAVE * PART_ITEMS;                // 1024 consecutive rows per wave
+constexpr uint32_t NULL_PAYLOAD = 0xFFFFFFFFu;
+
+template <typename H>
+struct __attribute__((aligned(sizeof(H) == 8 ? 16 : 8))) Rec {
+  H key;
+  uint32_t payload;
+};
+
+// Column chunk of one join side as the device sees it.
+struct SrcChunk {
+  const void* data;
+  const uint8_t* nulls;
+  const void* dictionary;
+  const hy_row_id* pos_list;  // reference chunk when != nullptr
+  uint32_t size;
+  uint32_t dictionary_size;
+  int32_t kind;
+  int32_t vid_width;
+  uint64_t row_begin;         // first row of this chunk in the side's row space
+};
+
+// Maps a 32-bit global row index of some table to its RowID.
+struct RowMap {
+  const uint64_t* row_begin;  // n_chunks + 1
+  uint32_t n_chunks;
+  uint32_t uniform;           // chunk size if every chunk but the last has it, else 0
+  uint64_t magic;             // floor(2^64 / uniform) + 1 (uniform >= 2)
+};
+
+__device__ __forceinline__ hy_row_id map_row(const RowMap& m, uint32_t idx) {
+  if (idx == NULL_PAYLOAD) return hy_row_id{0xFFFFFFFFu, 0xFFFFFFFFu};
+  if (m.uniform == 1) return hy_row_id{idx, 0u};
+  if (m.uniform != 0) {
+    const uint32_t q = static_cast<uint32_t>(__umul64hi(static_cast<uint64_t>(idx), m.magic));
+    return hy_row_id{q, idx - q * m.uniform};
+  }
+  uint32_t lo = 0, hi = m.n_chunks;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (m.row_begin[mid] <= idx)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  return hy_row_id{lo, static_cast<uint32_t>(idx - m.row_begin[lo])};
+}
+
+struct Side {
+  const SrcChunk* chunks;
+  uint32_t n_chunks;
+  const uint64_t* chunk_tile_begin;  // n_chunks + 1 (pass-1 tiles)
+  uint64_t n_tiles;
+  const SrcChunk* referenced;        // referenced column chunks (reference sides)
+  uint32_t n_referenced;
+  const uint64_t* referenced_row_begin;  // for fused dereference payloads
+  int32_t fuse_deref;                // payload = row in the referenced table instead of row in this table
+  int32_t keep_nulls;
+};
+
+template <typename T>
+__device__ __forceinline__ bool read_column_value(const SrcChunk& c, uint32_t off, T* v) {
+  if (c.kind == HY_COL_DICT) {
+    uint32_t vid;
+    if (c.vid_width == 1)
+      vid = static_cast<const uint8_t*>(c.data)[off];
+    else if (c.vid_width == 2)
+      vid = static_cast<const uint16_t*>(c.data)[off];
+    else
+      vid = static_cast<const uint32_t*>(c.data)[off];
+    if (vid >= c.dictionary_size) {
+      *v = T{};
+      return false;
+    }
+    *v = static_cast<const T*>(c.dictionary)[vid];
+    return true;
+  }
+  if (c.nulls != nullptr && c.nulls[off]) {
+    *v = T{};
+    return false;
+  }
+  *v = static_cast<const T*>(c.data)[off];
+  return true;
+}
+
+// Loads row `off` of chunk `c`: key (cast to the hashed type), payload, validity (NULLs are dropped unless
+// keep_nulls, as materialize_input does at join_hash.cpp:253).
+template <typename T, typename H>
+__device__ __forceinline__ bool load_row(const Side& s, const SrcChunk& c, uint32_t off, H* key, uint32_t* payload) {
+  T v;
+  bool valid;
+  if (c.pos_list != nullptr) {
+    const hy_row_id rid = c.pos_list[off];
+    if (rid.chunk_offset == 0xFFFFFFFFu) {
+      v = T{};
+      valid = false;
+      *payload = s.fuse_deref ? NULL_PAYLOAD : static_cast<uint32_t>(c.row_begin + off);
+    } else {
+      valid = read_column_value<T>(s.referenced[rid.chunk_id], rid.chunk_offset, &v);
+      *payload = s.fuse_deref ? static_cast<uint32_t>(s.referenced_row_begin[rid.chunk_id] + rid.chunk_offset)
+                              : static_cast<uint32_t>(c.row_begin + off);
+    }
+  } else {
+    valid = read_column_value<T>(c, off, &v);
+    *payload = static_cast<uint32_t>(c.row_begin + off);
+  }
+  *key = static_cast<H>(v);
+  return valid || s.keep_nulls;
+}
+
+struct Digit {
+  uint32_t mask;   // (1 << radix_bits) - 1
+  uint32_t shift;  // digit = (hash & mask) >> shift
+  uint32_t dmask;  // digit &= dmask
+  uint32_t seed;
+};
+
+template <typename H>
+__device__ __forceinline__ uint32_t digit_of(const Digit& dg, H key) {
+  return ((murmur2<H>(key, dg.seed) & dg.mask) >> dg.shift) & dg.dmask;
+}
+
+__device__ __forceinline__ uint32_t find_tile_owner(const uint64_t* begin, uint32_t n, uint64_t tile) {
+  uint32_t lo = 0, hi = n;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (begin[mid] <= tile)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+// Stable in-tile ranking by digit: wave w owns rows [w*1024, (w+1)*1024) of the tile, lane l handles row
+// k*64 + l at step k, so processing steps in order per wave and waves in order reproduces row order.
+// Returns rank of the item among the same-digit items of its wave that precede it, and updates the per-wave
+// digit counter.
+__device__ __forceinline__ uint32_t wave_rank(uint32_t digit, bool active, int dbits, uint32_t* wave_cnt) {
+  uint64_t peers = __ballot(active);
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    if (b < dbits) {
+      const uint64_t bb = __ballot(active && ((digit >> b) & 1u));
+      peers &= ((digit >> b) & 1u) ? bb : ~bb;
+    }
+  }
+  uint32_t rank = 0;
+  if (active) {
+    const uint32_t before = __popcll(peers & lanemask_lt());
+    rank = wave_cnt[digit] + before;
+  }
+  // all lanes read wave_cnt before anyone writes (LDS ops of one wave execute in order)
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  if (active) {
+    const uint64_t higher = peers & ~(lanemask_lt() | (1ull << __lane_id()));
+    if (higher == 0) wave_cnt[digit] += __popcll(peers);
+  }
+  return rank;
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Pass 1: from column chunks.
+// ------------------------------------------------------------------------------------------------------------
+template <typename T, typename H>
+__global__ __launch_bounds__(PART_THREADS) void part1_hist(Side s, Digit dg, uint32_t n_digits,
+                                                          uint32_t* __restrict__ hist) {
+  __shared__ uint32_t s_hist[256];
+  const uint64_t tile = blockIdx.x;
+  for (int i = threadIdx.x; i < 256; i += PART_THREADS) s_hist[i] = 0;
+  __syncthreads();
+  const uint32_t c = find_tile_owner(s.chunk_tile_begin, s.n_chunks, tile);
+  const SrcChunk ch = s.chunks[c];
+  const uint32_t base = static_cast<uint32_t>(tile - s.chunk_tile_begin[c]) * PART_TILE;
+  const int w = threadIdx.x / WAVE;
+  for (int k = 0; k < PART_ITEMS; ++k) {
+    const uint32_t off = base + w * WAVE_SPAN + k * WAVE + __lane_id();
+    if (off < ch.size) {
+      H key;
+      uint32_t payload;
+      if (load_row<T, H>(s, ch, off, &key, &payload)) atomicAdd(&s_hist[digit_of<H>(dg, key)], 1u);
+    }
+  }
+  __syncthreads();
+  for (uint32_t d = threadIdx.x; d < n_digits; d += PART_THREADS) hist[d * s.n_tiles + tile] = s_hist[d];
+}
+
+template <typename T, typename H>
+__global__ __launch_bounds__(PART_THREADS) void part1_scatter(Side s, Digit dg, int dbits, uint32_t n_digits,
+                                                             const uint32_t* __restrict__ offsets,
+                                                             Rec<H>* __restrict__ out) {
+  __shared__ uint32_t s_cnt[PART_WAVES][256];
+  const uint64_t tile = blockIdx.x;
+  for (int i = threadIdx.x; i < PART_WAVES * 256; i += PART_THREADS) (&s_cnt[0][0])[i] = 0;
+  __syncthreads();
+  const uint32_t c = find_tile_owner(s.chunk_tile_begin, s.n_chunks, tile);
+  const SrcChunk ch = s.chunks[c];
+  const uint32_t base = static_cast<uint32_t>(tile - s.chunk_tile_begin[c]) * PART_TILE;
+  const int w = threadIdx.x / WAVE;
+
+  H keys[PART_ITEMS];
+  uint32_t pays[PART_ITEMS];
+  uint32_t digs[PART_ITEMS];
+  uint32_t ranks[PART_ITEMS];
+  uint32_t act = 0;
+#pragma unroll
+  for (int k = 0; k < PART_ITEMS; ++k) {
+    const uint32_t off = base + w * WAVE_SPAN + k * WAVE + __lane_id();
+    bool a = false;
+    digs[k] = 0;
+    if (off < ch.size) {
+      a = load_row<T, H>(s, ch, off, &keys[k], &pays[k]);
+      if (a) digs[k] = digit_of<H>(dg, keys[k]);
+    }
+    act |= static_cast<uint32_t>(a) << k;
+    ranks[k] = wave_rank(digs[k], a, dbits, s_cnt[w]);
+  }
+  __syncthreads();
+  // exclusive prefix over waves per digit
+  for (uint32_t d = threadIdx.x; d < n_digits; d += PART_THREADS) {
+    uint32_t run = offsets[d * s.n_tiles + tile];
+#pragma unroll
+    for (int ww = 0; ww < PART_WAVES; ++ww) {
+      const uint32_t t = s_cnt[ww][d];
+      s_cnt[ww][d] = run;
+      run += t;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < PART_ITEMS; ++k) {
+    if ((act >> k) & 1u) {
+      const uint32_t pos = s_cnt[w][digs[k]] + ranks[k];
+      Rec<H> r;
+      r.key = keys[k];
+      r.payload = pays[k];
+      out[pos] = r;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Pass 2: records -> records, inside every pass-1 bucket (segment).
+// ------------------------------------------------------------------------------------------------------------
+struct Segs {
+  const uint32_t* seg_begin;        // n_segs + 1 record offsets
+  const uint64_t* seg_tile_begin;   // n_segs + 1 tile prefix (device-computed; grid is an upper bound)
+  uint32_t n_segs;
+};
+
+template <typename H>
+__global__ __launch_bounds__(PART_THREADS) void part2_hist(Segs sg, Digit dg, uint32_t n_digits,
+                                                          const Rec<H>* __restrict__ in, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t s_hist[256];
+  const uint64_t tile = blockIdx.x;
+  if (tile >= sg.seg_tile_begin[sg.n_segs]) return;
+  for (int i = threadIdx.x; i < 256; i += PART_THREADS) s_hist[i] = 0;
+  __syncthreads();
+  const uint32_t sgi = find_tile_owner(sg.seg_tile_begin, sg.n_segs, tile);
+  const uint32_t t_in = static_cast<uint32_t>(tile - sg.seg_tile_begin[sgi]);
+  const uint32_t nt = static_cast<uint32_t>(sg.seg_tile_begin[sgi + 1] - sg.seg_tile_begin[sgi]);
+  const uint32_t b0 = sg.seg_begin[sgi], b1 = sg.seg_begin[sgi + 1];
+  const int w = threadIdx.x / WAVE;
+  for (int k = 0; k < PART_ITEMS; ++k) {
+    const uint32_t r = b0 + t_in * PART_TILE + w * WAVE_SPAN + k * WAVE + __lane_id();
+    if (r < b1) atomicAdd(&s_hist[digit_of<H>(dg, in[r].key)], 1u);
+  }
+  __syncthreads();
+  const uint64_t hbase = sg.seg_tile_begin[sgi] * n_digits;
+  for (uint32_t d = threadIdx.x; d < n_digits; d += PART_THREADS) hist[hbase + d * nt + t_in] = s_hist[d];
+}
+
+template <typename H>
+__global__ __launch_bounds__(PART_THREADS) void part2_scatter(Segs sg, Digit dg, int dbits, uint32_t n_digits,
+                                                             const Rec<H>* __restrict__ in,
+                                                             const uint32_t* __restrict__ offsets,
+                                                             Rec<H>* __restrict__ out) {
+  __shared__ uint32_t s_cnt[PART_WAVES][256];
+  const uint64_t tile = blockIdx.x;
+  if (tile >= sg.seg_tile_begin[sg.n_segs]) return;
+  for (int i = threadIdx.x; i < PART_WAVES * 256; i += PART_THREADS) (&s_cnt[0][0])[i] = 0;
+  __syncthreads();
+  const uint32_t sgi = find_tile_owner(sg.seg_tile_begin, sg.n_segs, tile);
+  const uint32_t t_in = static_cast<uint32_t>(tile - sg.seg_tile_begin[sgi]);
+  const uint32_t nt = static_cast<uint32_t>(sg.seg_tile_begin[sgi + 1] - sg.seg_tile_begin[sgi]);
+  const uint32_t b0 = sg.seg_begin[sgi], b1 = sg.seg_begin[sgi + 1];
+  const int w = threadIdx.x / WAVE;
+  Rec<H> recs[PART_ITEMS];
+  uint32_t digs[PART_ITEMS];
+  uint32_t ranks[PART_ITEMS];
+  uint32_t act = 0;
+#pragma unroll
+  for (int k = 0; k < PART_ITEMS; ++k) {
+    const uint32_t r = b0 + t_in * PART_TILE + w * WAVE_SPAN + k * WAVE + __lane_id();
+    const bool a = r < b1;
+    digs[k] = 0;
+    if (a) {
+      recs[k] = in[r];
+      digs[k] = digit_of<H>(dg, recs[k].key);
+    }
+    act |= static_cast<uint32_t>(a) << k;
+    ranks[k] = wave_rank(digs[k], a, dbits, s_cnt[w]);
+  }
+  __syncthreads();
+  const uint64_t hbase = sg.seg_tile_begin[sgi] * n_digits;
+  for (uint32_t d = threadIdx.x; d < n_digits; d += PART_THREADS) {
+    uint32_t run = offsets[hbase + d * nt + t_in];
+#pragma unroll
+    for (int ww = 0; ww < PART_WAVES; ++ww) {
+      const uint32_t t = s_cnt[ww][d];
+      s_cnt[ww][d] = run;
+      run += t;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < PART_ITEMS; ++k)
+    if ((act >> k) & 1u) out[s_cnt[w][digs[k]] + ranks[k]] = recs[k];
+}
+
+// Partition bounds after pass 1 only (radix_bits <= 8): part_begin[d] = offsets[d * n_tiles].
+__global__ void bounds_single_pass(const uint32_t* __restrict__ offsets, uint64_t n_tiles, uint32_t n_parts,
+                                   const uint64_t* __restrict__ total, uint32_t* __restrict__ part_begin) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < n_parts) part_begin[p] = n_tiles == 0 ? 0u : offsets[p * n_tiles];
+  if (p == n_parts) part_begin[p] = static_cast<uint32_t>(*total);
+}
+
+// Segment bounds of pass 1 (same formula), plus the pass-2 tile prefix of every segment.
+__global__ void seg_bounds(const uint32_t* __restrict__ offsets, uint64_t n_tiles, uint32_t n_segs,
+                           const uint64_t* __restrict__ total, uint32_t* __restrict__ seg_begin) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < n_segs) seg_begin[p] = n_tiles == 0 ? 0u : offsets[p * n_tiles];
+  if (p == n_segs) seg_begin[p] = static_cast<uint32_t>(*total);
+}
+
+__global__ void seg_tiles(const uint32_t* __restrict__ seg_begin, uint32_t n_segs, uint64_t* __restrict__ seg_tile_begin) {
+  // single workgroup: sequential prefix over <= 256 segments
+  if (threadIdx.x == 0) {
+    uint64_t run = 0;
+    for (uint32_t s = 0; s < n_segs; ++s) {
+      seg_tile_begin[s] = run;
+      run += (seg_begin[s + 1] - seg_begin[s] + PART_TILE - 1) / PART_TILE;
+    }
+    seg_tile_begin[n_segs] = run;
+  }
+}
+
+// Partition bounds after pass 2: partition p = (seg << lo_bits) | d.
+__global__ void bounds_two_pass(const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ seg_begin,
+                                const uint64_t* __restrict__ seg_tile_begin, uint32_t n_segs, uint32_t lo_digits,
+                                const uint64_t* __restrict__ total, uint32_t* __restrict__ part_begin) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t n_parts = n_segs * lo_digits;
+  if (p < n_parts) {
+    const uint32_t sgi = p / lo_digits, d = p % lo_digits;
+    const uint64_t nt = seg_tile_begin[sgi + 1] - seg_tile_begin[sgi];
+    part_begin[p] = nt == 0 ? seg_begin[sgi] : offsets[seg_tile_begin[sgi] * lo_digits + d * nt];
+  }
+  if (p == n_parts) part_begin[p] = static_cast<uint32_t>(*total);
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Exclusive scan of a uint32 array (decoupled look-back, 8192 elements per workgroup).
+// ------------------------------------------------------------------------------------------------------------
+constexpr int SCAN_T = 512;
+constexpr int SCAN_PER = 16;
+constexpr int SCAN_BLOCK = SCAN_T * SCAN_PER;
+
+__global__ __launch_bounds__(SCAN_T) void exclusive_scan_u32(const uint32_t* __restrict__ in,
+                                                             uint32_t* __restrict__ out, uint64_t n,
+                                                             uint64_t* __restrict__ status, uint32_t* ticket,
+                                                             uint32_t* error, uint64_t* total_out) {
+  __shared__ uint32_t s_scratch[SCAN_T / WAVE + 1];
+  __shared__ uint64_t s_tile;
+  __shared__ uint64_t s_prefix;
+  if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
+  __syncthreads();
+  const uint64_t tile = s_tile;
+  const uint64_t n_tiles = (n + SCAN_BLOCK - 1) / SCAN_BLOCK;
+  if (tile >= n_tiles) return;
+  const uint64_t i0 = tile * SCAN_BLOCK + threadIdx.x * SCAN_PER;
+  uint32_t v[SCAN_PER];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int i = 0; i < SCAN_PER; ++i) {
+    v[i] = (i0 + i < n) ? in[i0 + i] : 0u;
+    sum += v[i];
+  }
+  uint32_t total;
+  const uint32_t local = block_exclusive_sum<SCAN_T>(sum, s_scratch, &total);
+  if (threadIdx.x == 0) {
+    uint64_t prefix = 0;
+    if (tile == 0) {
+      lb_publish(&status[0], LB_FLAG_PREFIX, total);
+    } else {
+      lb_publish(&status[tile], LB_FLAG_AGG, total);
+      lb_lookback(status, 0, tile, &prefix, error);
+      lb_publish(&status[tile], LB_FLAG_PREFIX, prefix + total);
+    }
+    s_prefix = prefix;
+    if (tile == n_tiles - 1 && total_out != nullptr) *total_out = prefix + total;
+  }
+  __syncthreads();
+  uint32_t run = static_cast<uint32_t>(s_prefix) + local;
+#pragma unroll
+  for (int i = 0; i < SCAN_PER; ++i) {
+    if (i0 + i < n) out[i0 + i] = run;
+    run += v[i];
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Per-partition build + probe.
+// ------------------------------------------------------------------------------------------------------------
+constexpr int JOIN_THREADS = 512;
+constexpr uint32_t SLOT_EMPTY = 0u;
+constexpr uint32_t SLOT_LOCKED = 0xFFFFFFFFu;
+
+template <typename H>
+struct __attribute__((aligned(sizeof(H) == 8 ? 16 : 8))) Slot {
+  uint32_t state;  // 0 empty, LOCKED while the key is written, else first build index + 1
+  H key;
+};
+
+struct JoinDesc {
+  const uint32_t* build_begin;  // n_parts + 1
+  const uint32_t* probe_begin;  // n_parts + 1
+  uint32_t n_parts;
+  uint32_t cap;                 // LDS hash slots (power of two)
+  uint32_t max_build;           // max build partition size (LDS arrays sized by it)
+  int32_t mode;
+  RowMap build_map;
+  RowMap probe_map;
+  uint64_t capacity;            // output capacity in pairs
+  uint64_t* status;             // n_parts look-back words
+  uint32_t* ticket;
+  uint32_t* error;
+  uint32_t* overflow;
+  uint64_t* total;              // total pairs (written by the last partition)
+};
+
+template <typename H>
+__device__ __forceinline__ uint32_t slot_hash(H key) {
+  if constexpr (sizeof(H) == 4) {
+    uint32_t b;
+    if constexpr (std::is_floating_point_v<H>) {
+      const H k = key == H(0) ? H(0) : key;  // -0.0 and 0.0 compare equal: hash them alike
+      __builtin_memcpy(&b, &k, 4);
+    } else {
+      __builtin_memcpy(&b, &key, 4);
+    }
+    return murmur_final(b * 0x9E3779B1u);
+  } else {
+    uint64_t b;
+    if constexpr (std::is_floating_point_v<H>) {
+      const H k = key == H(0) ? H(0) : key;
+      __builtin_memcpy(&b, &k, 8);
+    } else {
+      __builtin_memcpy(&b, &key, 8);
+    }
+    return murmur_final(static_cast<uint32_t>(b) * 0x9E3779B1u ^ static_cast<uint32_t>(b >> 32));
+  }
+}
+
+template <typename H>
+__global__ __launch_bounds__(JOIN_THREADS) void join_partition(JoinDesc d, const Rec<H>* __restrict__ build,
+                                                               const Rec<H>* __restrict__ probe,
+                                                               hy_row_id* __restrict__ out_build,
+                                                               hy_row_id* __restrict__ out_probe,
+                                                               uint64_t* __restrict__ part_out_begin,
+                                                               uint32_t* __restrict__ part_out_count) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  Slot<H>* slots = reinterpret_cast<Slot<H>*>(smem);
+  uint32_t* bpay = reinterpret_cast<uint32_t*>(smem + sizeof(Slot<H>) * d.cap);      // build payloads
+  uint16_t* cnt = reinterpret_cast<uint16_t*>(bpay + d.max_build);                    // per-slot counts
+  uint16_t* lbeg = cnt + d.cap;                                                         // per-slot list begin
+  uint16_t* eslot = lbeg + d.cap;                                                       // per-element slot
+  uint16_t* sorted = eslot + d.max_build;                                               // elements by slot
+  __shared__ uint32_t s_scratch[JOIN_THREADS / WAVE + 1];
+  __shared__ uint32_t s_part;
+  __shared__ uint32_t s_dup;
+  __shared__ uint64_t s_base;
+
+  if (threadIdx.x == 0) {
+    s_part = atomicAdd(d.ticket, 1u);
+    s_dup = 0;
+  }
+  for (uint32_t i = threadIdx.x; i < d.cap; i += JOIN_THREADS) {
+    slots[i].state = SLOT_EMPTY;
+    cnt[i] = 0;
+  }
+  __syncthreads();
+  const uint32_t p = s_part;
+  if (p >= d.n_parts) return;
+  const uint32_t bb = d.build_begin[p], nb = d.build_begin[p + 1] - bb;
+  const uint32_t pb = d.probe_begin[p], np = d.probe_begin[p + 1] - pb;
+  const uint32_t mask = d.cap - 1;
+  const int mode = d.mode;
+
+  // ---- build: insert keys, count multiplicities ----
+  for (uint32_t i = threadIdx.x; i < nb; i += JOIN_THREADS) {
+    const Rec<H> r = build[bb + i];
+    bpay[i] = r.payload;
+    uint32_t s = slot_hash<H>(r.key) & mask;
+    for (uint32_t guard = 0; guard <= d.cap * 64u; ++guard) {
+      const uint32_t st = __hip_atomic_load(&slots[s].state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (st == SLOT_EMPTY) {
+        uint32_t expected = SLOT_EMPTY;
+        if (__hip_atomic_compare_exchange_strong(&slots[s].state, &expected, SLOT_LOCKED, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+          slots[s].key = r.key;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          __hip_atomic_store(&slots[s].state, i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          break;
+        }
+        continue;
+      }
+      if (st == SLOT_LOCKED) continue;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      if (slots[s].key == r.key) {
+        s_dup = 1;
+        break;
+      }
+      s = (s + 1) & mask;
+    }
+    eslot[i] = static_cast<uint16_t>(s);
+    atomicAdd(reinterpret_cast<uint32_t*>(&cnt[s & ~1u]), (s & 1u) ? 0x10000u : 1u);
+  }
+  __syncthreads();
+  const bool dup = s_dup != 0;
+  if (dup) {
+    // list_begin = exclusive prefix of counts over slots; then place elements in slot order, stable.
+    uint32_t run = 0;
+    const uint32_t per = (d.cap + JOIN_THREADS - 1) / JOIN_THREADS;
+    const uint32_t s0 = threadIdx.x * per;
+    for (uint32_t k = 0; k < per; ++k)
+      if (s0 + k < d.cap) run += cnt[s0 + k];
+    uint32_t total;
+    uint32_t pre = block_exclusive_sum<JOIN_THREADS>(run, s_scratch, &total);
+    for (uint32_t k = 0; k < per; ++k)
+      if (s0 + k < d.cap) {
+        lbeg[s0 + k] = static_cast<uint16_t>(pre);
+        pre += cnt[s0 + k];
+      }
+    __syncthreads();
+    // wave 0 places elements in index order: per slot a running cursor kept in `cnt` (reset first)
+    for (uint32_t i = threadIdx.x; i < d.cap; i += JOIN_THREADS) cnt[i] = 0;
+    __syncthreads();
+    if (threadIdx.x < WAVE) {
+      for (uint32_t i0 = 0; i0 < nb; i0 += WAVE) {
+        const uint32_t i = i0 + __lane_id();
+        const bool a = i < nb;
+        const uint32_t s = a ? eslot[i] : 0u;
+        uint64_t peers = __ballot(a);
+        for (int b = 0; b < 16; ++b) {
+          const uint64_t bb2 = __ballot(a && ((s >> b) & 1u));
+          peers &= ((s >> b) & 1u) ? bb2 : ~bb2;
+        }
+        uint32_t pos = 0;
+        if (a) pos = lbeg[s] + cnt[s] + __popcll(peers & lanemask_lt());
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        if (a) {
+          sorted[pos] = static_cast<uint16_t>(i);
+          const uint64_t higher = peers & ~(lanemask_lt() | (1ull << __lane_id()));
+          if (higher == 0) cnt[s] = static_cast<uint16_t>(cnt[s] + __popcll(peers));
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- probe: lookup ----
+  auto lookup = [&](H key, uint32_t* first, uint32_t* count) {
+    uint32_t s = slot_hash<H>(key) & mask;
+    for (uint32_t guard = 0; guard <= d.cap; ++guard) {
+      const uint32_t st = slots[s].state;
+      if (st == SLOT_EMPTY) break;
+      if (slots[s].key == key) {
+        if (dup) {
+          *first = lbeg[s];
+          *count = cnt[s];
+        } else {
+          *first = st - 1;
+          *count = 1;
+        }
+        return;
+      }
+      s = (s + 1) & mask;
+    }
+    *first = 0;
+    *count = 0;
+  };
+  auto emitted = [&](uint32_t count) -> uint32_t {
+    switch (mode) {
+      case HY_JOIN_INNER:
+        return count;
+      case HY_JOIN_LEFT:
+      case HY_JOIN_RIGHT:
+        return count > 0 ? count : 1u;
+      case HY_JOIN_SEMI:
+        return count > 0 ? 1u : 0u;
+      case HY_JOIN_ANTI:
+        return count > 0 ? 0u : 1u;
+    }
+    return 0u;
+  };
+
+  // count phase
+  uint64_t my = 0;
+  for (uint32_t j = threadIdx.x; j < np; j += JOIN_THREADS) {
+    uint32_t f, c;
+    if (nb > 0)
+      lookup(probe[pb + j].key, &f, &c);
+    else
+      c = 0;
+    my += emitted(c);
+  }
+  uint32_t part_total32;
+  // per-thread counts fit 32 bits unless a single probe row matches > 4G rows
+  block_exclusive_sum<JOIN_THREADS>(static_cast<uint32_t>(my), s_scratch, &part_total32);
+  const uint64_t part_total = part_total32;
+
+  if (threadIdx.x == 0) {
+    uint64_t prefix = 0;
+    if (p == 0) {
+      lb_publish(&d.status[0], LB_FLAG_PREFIX, part_total);
+    } else {
+      lb_publish(&d.status[p], LB_FLAG_AGG, part_total);
+      lb_lookback(d.status, 0, p, &prefix, d.error);
+      lb_publish(&d.status[p], LB_FLAG_PREFIX, prefix + part_total);
+    }
+    s_base = prefix;
+    part_out_begin[p] = prefix;
+    part_out_count[p] = part_total32;
+    if (p == d.n_parts - 1) *d.total = prefix + part_total;
+    if (prefix + part_total > d.capacity) atomicOr(d.overflow, 1u);
+  }
+  __syncthreads();
+  const uint64_t base = s_base;
+  if (base + part_total > d.capacity) return;
+
+  // write phase: blocks of JOIN_THREADS probe rows, in order
+  uint64_t run = base;
+  for (uint32_t j0 = 0; j0 < np; j0 += JOIN_THREADS) {
+    const uint32_t j = j0 + threadIdx.x;
+    uint32_t f = 0, c = 0, e = 0;
+    uint32_t ppay = 0;
+    if (j < np) {
+      const Rec<H> r = probe[pb + j];
+      ppay = r.payload;
+      if (nb > 0) lookup(r.key, &f, &c);
+      e = emitted(c);
+    }
+    uint32_t blk_total;
+    const uint32_t off = block_exclusive_sum<JOIN_THREADS>(e, s_scratch, &blk_total);
+    if (e) {
+      const hy_row_id prow = map_row(d.probe_map, ppay);
+      uint64_t o = run + off;
+      if (mode == HY_JOIN_SEMI || mode == HY_JOIN_ANTI) {
+        out_probe[o] = prow;
+      } else if (c == 0) {
+        out_build[o] = hy_row_id{0xFFFFFFFFu, 0xFFFFFFFFu};
+        out_probe[o] = prow;
+      } else {
+        for (uint32_t m = 0; m < c; ++m, ++o) {
+          const uint32_t bi = dup ? sorted[f + m] : f;
+          out_build[o] = map_row(d.build_map, bpay[bi]);
+          out_probe[o] = prow;
+        }
+      }
+    }
+    run += blk_total;
+  }
+}
+
+__global__ void murmur_kernel_u32(const uint32_t* keys, uint64_t n, uint32_t seed, uint32_t* out) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    out[i] = murmur2_u32(keys[i], seed);
+}
+
+__global__ void murmur_kernel_u64(const uint64_t* keys, uint64_t n, uint32_t seed, uint32_t* out) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    out[i] = murmur2_u64(keys[i], seed);
+}
+
+// Dereference join outputs of a reference input through its per-chunk PosLists (write_output_columns,
+// join_hash.cpp:584-592): out[i] = row is NULL ? row : chunk_pos_lists[row.chunk_id][row.chunk_offset].
+__global__ void dereference_kernel(const hy_row_id* __restrict__ rows, uint64_t n,
+                                   const hy_row_id* const* __restrict__ chunk_pos_lists, hy_row_id* __restrict__ out) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const hy_row_id r = rows[i];
+    out[i] = r.chunk_offset == 0xFFFFFFFFu ? r : chunk_pos_lists[r.chunk_id][r.chunk_offset];
+  }
+}
+
+}  // namespace hyk

@@ -1,0 +1,280 @@
+// TableScan kernels for gfx950.
+//
+// One launch scans every chunk of one column class (dictionary u8/u16/u32 attribute vectors, or value columns of
+// one type) and writes, per chunk, the ascending list of matching chunk offsets — the PosList that
+// BaseTableScanImpl::_unary_scan_with_value builds per chunk (reference
+// src/lib/operators/table_scan/base_table_scan_impl.hpp:33-63).
+//
+// Layout: a tile is 4096 consecutive rows of one chunk; thread t of the 256-thread workgroup owns rows
+// [16t, 16t+16) and reads them with 16-byte vector loads (1 B/row for u8 vids -> one dwordx4 per lane).
+// Matches are compacted order-preservingly: per-thread popcount -> workgroup exclusive sum -> decoupled look-back
+// across the tiles of the same chunk -> offsets staged in LDS -> coalesced stores.
+// The roofline is HBM: vid_width bytes read per row + 4 bytes written per match.
+#include <hip/hip_runtime.h>
+
+#include "common.hpp"
+
+namespace hyk {
+
+constexpr int SCAN_THREADS = 256;
+constexpr int SCAN_ROWS_PER_THREAD = 16;
+constexpr int SCAN_TILE = SCAN_THREADS * SCAN_ROWS_PER_THREAD;  // 4096
+
+struct ScanLaunchDesc {
+  const hy_scan_chunk* chunks;       // device copy of this class's chunk descriptors
+  const uint64_t* chunk_tile_begin;  // n_chunks + 1 prefix of tile counts
+  const uint32_t* chunk_index;       // original chunk index (for counts[])
+  uint32_t n_chunks;
+  uint64_t n_tiles;
+  uint64_t* status;                  // n_tiles look-back words (zeroed)
+  uint32_t* ticket;                  // zeroed
+  uint32_t* error;                   // zeroed before the first launch of a call
+};
+
+template <typename T>
+struct ScanConst {
+  T value;
+};
+
+template <typename T>
+__device__ __forceinline__ bool cmp_op(int op, T v, T c) {
+  switch (op) {
+    case HY_OP_EQ:
+      return v == c;
+    case HY_OP_NE:
+      return v != c;
+    case HY_OP_LT:
+      return v < c;
+    case HY_OP_LE:
+      return v <= c;
+    case HY_OP_GT:
+      return v > c;
+    case HY_OP_GE:
+      return v >= c;
+    case HY_OP_ALL:
+      return true;
+    default:
+      return false;
+  }
+}
+
+// Loads 16 consecutive elements of E bytes starting at element `first` (16-byte aligned), elements past `n`
+// are returned as garbage and masked by the caller.
+template <typename E>
+__device__ __forceinline__ void load16(const E* __restrict__ base, uint32_t first, E (&out)[16]) {
+  constexpr int VECS = sizeof(E);  // 16 elements * sizeof(E) bytes / 16 bytes per vector
+  const u32x4* p = reinterpret_cast<const u32x4*>(base + first);
+  u32x4 tmp[VECS];
+#pragma unroll
+  for (int i = 0; i < VECS; ++i) tmp[i] = __builtin_nontemporal_load(p + i);
+  __builtin_memcpy(out, tmp, sizeof(tmp));
+}
+
+// E = element type read from memory (vid type for DICT, value type for VALUE); IS_DICT selects the semantics.
+template <typename E, bool IS_DICT>
+__global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanLaunchDesc d, ScanConst<E> constant,
+                                                           uint32_t* __restrict__ out_offsets,
+                                                           uint32_t* __restrict__ counts) {
+  __shared__ uint32_t s_stage[SCAN_TILE];
+  __shared__ uint32_t s_scratch[SCAN_THREADS / WAVE + 1];
+  __shared__ uint64_t s_tile;
+  __shared__ uint32_t s_chunk;
+  __shared__ uint64_t s_prefix;
+
+  if (threadIdx.x == 0) {
+    const uint64_t tile = atomicAdd(d.ticket, 1u);
+    // binary search: largest c with chunk_tile_begin[c] <= tile
+    uint32_t lo = 0, hi = d.n_chunks;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (d.chunk_tile_begin[mid] <= tile)
+        lo = mid;
+      else
+        hi = mid;
+    }
+    s_tile = tile;
+    s_chunk = lo;
+  }
+  __syncthreads();
+  const uint64_t tile = s_tile;
+  if (tile >= d.n_tiles) return;
+  const uint32_t c = s_chunk;
+  const hy_scan_chunk ch = d.chunks[c];
+  const uint64_t first_tile = d.chunk_tile_begin[c];
+  const uint32_t tile_in_chunk = static_cast<uint32_t>(tile - first_tile);
+  const uint32_t tile_row0 = tile_in_chunk * SCAN_TILE;
+  const uint32_t row0 = tile_row0 + threadIdx.x * SCAN_ROWS_PER_THREAD;
+  const uint32_t n = ch.column.size;
+
+  uint32_t mask = 0;
+  if (row0 < n && ch.op != HY_OP_NONE) {
+    E v[16];
+    load16(reinterpret_cast<const E*>(ch.column.data), row0, v);
+    const uint32_t valid = (n - row0) >= 16 ? 0xFFFFu : ((1u << (n - row0)) - 1u);
+    if constexpr (IS_DICT) {
+      const E null_vid = static_cast<E>(ch.column.dictionary_size);
+      const E s = static_cast<E>(ch.search_vid);
+      const int op = ch.op;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const bool m = (v[i] != null_vid) && cmp_op<E>(op, v[i], s);
+        mask |= static_cast<uint32_t>(m) << i;
+      }
+    } else {
+      uint8_t nl[16];
+      if (ch.column.nulls != nullptr) {
+        const u32x4 t = *reinterpret_cast<const u32x4*>(ch.column.nulls + row0);
+        __builtin_memcpy(nl, &t, 16);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) nl[i] = 0;
+      }
+      const int op = ch.op;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const bool m = (nl[i] == 0) && cmp_op<E>(op, v[i], constant.value);
+        mask |= static_cast<uint32_t>(m) << i;
+      }
+    }
+    mask &= valid;
+  }
+
+  uint32_t tile_total;
+  const uint32_t local = block_exclusive_sum<SCAN_THREADS>(__popc(mask), s_scratch, &tile_total);
+
+  // Decoupled look-back across the tiles of this chunk.
+  if (threadIdx.x == 0) {
+    uint64_t prefix = 0;
+    if (tile == first_tile) {
+      lb_publish(&d.status[tile], LB_FLAG_PREFIX, tile_total);
+    } else {
+      lb_publish(&d.status[tile], LB_FLAG_AGG, tile_total);
+      lb_lookback(d.status, first_tile, tile, &prefix, d.error);
+      lb_publish(&d.status[tile], LB_FLAG_PREFIX, prefix + tile_total);
+    }
+    s_prefix = prefix;
+    const uint64_t last_tile = d.chunk_tile_begin[c + 1] - 1;
+    if (tile == last_tile) counts[d.chunk_index[c]] = static_cast<uint32_t>(prefix + tile_total);
+  }
+
+  // Stage matching offsets in LDS in order, then store them coalesced.
+  uint32_t pos = local;
+  uint32_t m = mask;
+  while (m) {
+    const int i = __builtin_ctz(m);
+    m &= m - 1;
+    s_stage[pos++] = row0 + i;
+  }
+  __syncthreads();
+  uint32_t* out = out_offsets + ch.out_begin + s_prefix;
+  for (uint32_t i = threadIdx.x; i < tile_total; i += SCAN_THREADS) out[i] = s_stage[i];
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Reference-column scan: for each PosList position, gather the referenced value through the referenced chunk's
+// descriptor and compare; emit matching positions in PosList order.
+// ------------------------------------------------------------------------------------------------------------
+struct RefScanDesc {
+  const hy_row_id* pos_list;
+  uint64_t n;
+  const hy_scan_chunk* chunks;  // referenced chunks, indexed by chunk id
+  uint32_t n_chunks;
+  uint64_t n_tiles;
+  uint64_t* status;
+  uint32_t* ticket;
+  uint32_t* error;
+};
+
+template <typename T>
+__device__ __forceinline__ bool ref_match(const hy_scan_chunk& ch, uint32_t off, T constant) {
+  if (ch.op == HY_OP_NONE) return false;
+  if (ch.column.kind == HY_COL_DICT) {
+    uint32_t vid;
+    if (ch.column.vid_width == 1)
+      vid = reinterpret_cast<const uint8_t*>(ch.column.data)[off];
+    else if (ch.column.vid_width == 2)
+      vid = reinterpret_cast<const uint16_t*>(ch.column.data)[off];
+    else
+      vid = reinterpret_cast<const uint32_t*>(ch.column.data)[off];
+    if (vid == ch.column.dictionary_size) return false;
+    return cmp_op<uint32_t>(ch.op, vid, ch.search_vid);
+  }
+  if (ch.column.nulls != nullptr && ch.column.nulls[off]) return false;
+  const T v = reinterpret_cast<const T*>(ch.column.data)[off];
+  return cmp_op<T>(ch.op, v, constant);
+}
+
+template <typename T>
+__global__ __launch_bounds__(SCAN_THREADS) void ref_scan_kernel(RefScanDesc d, ScanConst<T> constant,
+                                                               uint32_t* __restrict__ out_positions,
+                                                               uint64_t* __restrict__ count) {
+  __shared__ uint32_t s_stage[SCAN_TILE];
+  __shared__ uint32_t s_scratch[SCAN_THREADS / WAVE + 1];
+  __shared__ uint64_t s_tile;
+  __shared__ uint64_t s_prefix;
+  if (threadIdx.x == 0) s_tile = atomicAdd(d.ticket, 1u);
+  __syncthreads();
+  const uint64_t tile = s_tile;
+  if (tile >= d.n_tiles) return;
+  const uint64_t row0 = tile * SCAN_TILE + threadIdx.x * SCAN_ROWS_PER_THREAD;
+
+  uint32_t mask = 0;
+#pragma unroll 4
+  for (int i = 0; i < SCAN_ROWS_PER_THREAD; ++i) {
+    const uint64_t r = row0 + i;
+    if (r < d.n) {
+      const hy_row_id rid = d.pos_list[r];
+      if (rid.chunk_offset != 0xFFFFFFFFu && rid.chunk_id < d.n_chunks) {
+        const hy_scan_chunk& ch = d.chunks[rid.chunk_id];
+        if (ref_match<T>(ch, rid.chunk_offset, constant.value)) mask |= 1u << i;
+      }
+    }
+  }
+
+  uint32_t tile_total;
+  const uint32_t local = block_exclusive_sum<SCAN_THREADS>(__popc(mask), s_scratch, &tile_total);
+  if (threadIdx.x == 0) {
+    uint64_t prefix = 0;
+    if (tile == 0) {
+      lb_publish(&d.status[tile], LB_FLAG_PREFIX, tile_total);
+    } else {
+      lb_publish(&d.status[tile], LB_FLAG_AGG, tile_total);
+      lb_lookback(d.status, 0, tile, &prefix, d.error);
+      lb_publish(&d.status[tile], LB_FLAG_PREFIX, prefix + tile_total);
+    }
+    s_prefix = prefix;
+    if (tile == d.n_tiles - 1) *count = prefix + tile_total;
+  }
+  uint32_t pos = local;
+  uint32_t m = mask;
+  while (m) {
+    const int i = __builtin_ctz(m);
+    m &= m - 1;
+    s_stage[pos++] = static_cast<uint32_t>(row0 + i);
+  }
+  __syncthreads();
+  uint32_t* out = out_positions + s_prefix;
+  for (uint32_t i = threadIdx.x; i < tile_total; i += SCAN_THREADS) out[i] = s_stage[i];
+}
+
+__global__ void gather_row_ids_kernel(const hy_row_id* __restrict__ pos_list, const uint32_t* __restrict__ positions,
+                                      uint64_t n, hy_row_id* __restrict__ out) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    out[i] = pos_list[positions[i]];
+}
+
+__global__ void first_seen_kernel(const hy_row_id* __restrict__ pos_list, uint64_t n, uint32_t n_chunks,
+                                  unsigned long long* __restrict__ first) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const hy_row_id r = pos_list[i];
+    if (r.chunk_offset != 0xFFFFFFFFu && r.chunk_id < n_chunks) atomicMin(&first[r.chunk_id], (unsigned long long)i);
+  }
+}
+
+__global__ void expand_row_ids_kernel(uint32_t chunk_id, const uint32_t* __restrict__ offsets, uint64_t n,
+                                      hy_row_id* __restrict__ out) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    out[i] = hy_row_id{chunk_id, offsets[i]};
+}
+
+}  // namespace hyk

@@ -1,0 +1,246 @@
+/*
+ * hyrise_amd.h — C-ABI of the MI355X (gfx950) execution layer for Hyrise's TableScan / JoinHash / Aggregate
+ * hot path.
+ *
+ * This is the drop-in boundary: the reference's operators keep their C++ surface
+ * (AbstractOperator::_on_execute(), src/lib/operators/abstract_operator.hpp:70-172) and call into these entry
+ * points for the per-chunk hot loops. Every entry point takes plain pointers and sizes, never throws, and returns
+ * an hy_status (0 = success). Device buffers are caller-owned; every launch takes an explicit stream and a
+ * caller-provided workspace whose size is queried first, so launches can be captured into hipGraphs.
+ *
+ * Which reference interface each entry point replaces is stated next to it (reference path:line).
+ */
+#ifndef HYRISE_AMD_H_
+#define HYRISE_AMD_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int hy_status;
+typedef void* hy_stream_t; /* hipStream_t */
+
+enum {
+  HY_OK = 0,
+  HY_ERR_INVALID_ARGUMENT = 1,
+  HY_ERR_DEVICE = 2,         /* a HIP runtime call failed; see hy_last_error_message() */
+  HY_ERR_WORKSPACE = 3,      /* workspace too small */
+  HY_ERR_ALIGNMENT = 4,      /* a device pointer is not 16-byte aligned */
+  HY_ERR_UNSUPPORTED = 5,    /* type / mode not implemented on the device path */
+  HY_ERR_CAPACITY = 6,       /* output capacity exceeded; *_required holds the needed size */
+  HY_ERR_KERNEL = 7          /* a kernel reported an internal failure (bounded spin expired) */
+};
+
+/* RowID, identical layout to reference src/lib/types.hpp:97-131 ({ChunkID chunk_id; ChunkOffset chunk_offset;}). */
+typedef struct hy_row_id {
+  uint32_t chunk_id;
+  uint32_t chunk_offset;
+} hy_row_id;
+
+/* Column data types (reference src/lib/all_type_variant.hpp data_types). */
+enum { HY_TYPE_INT32 = 1, HY_TYPE_INT64 = 2, HY_TYPE_FLOAT = 3, HY_TYPE_DOUBLE = 4 };
+
+/* ---------------------------------------------------------------------------------------------------------------
+ * Runtime
+ * ------------------------------------------------------------------------------------------------------------- */
+hy_status hy_get_device_count(int* count);
+hy_status hy_set_device(int device);
+hy_status hy_malloc(void** ptr, size_t bytes);
+hy_status hy_free(void* ptr);
+hy_status hy_memcpy_htod(void* dst, const void* src, size_t bytes, hy_stream_t stream);
+hy_status hy_memcpy_dtoh(void* dst, const void* src, size_t bytes, hy_stream_t stream);
+hy_status hy_memcpy_dtod(void* dst, const void* src, size_t bytes, hy_stream_t stream);
+hy_status hy_memset(void* dst, int value, size_t bytes, hy_stream_t stream);
+hy_status hy_stream_create(hy_stream_t* stream);
+hy_status hy_stream_destroy(hy_stream_t stream);
+hy_status hy_stream_synchronize(hy_stream_t stream);
+/* Thread-local message of the last failing call. */
+const char* hy_last_error_message(void);
+/* Build identification ("gfx950 …"). */
+const char* hy_build_info(void);
+
+/* ---------------------------------------------------------------------------------------------------------------
+ * Column chunk descriptors (device residency of the reference's per-chunk columns).
+ *
+ *   HY_COL_VALUE      ValueColumn<T>          reference src/lib/storage/value_column.hpp:15-73
+ *                     data = T[size], nulls = uint8[size] (1 = NULL) or NULL when the column is not nullable
+ *   HY_COL_DICT       DictionaryColumn<T>     reference src/lib/storage/dictionary_column.hpp:20-72
+ *                     data = attribute vector (uint8/16/32 per vid_width, FixedSizeByteAligned,
+ *                     reference vector_compression/fixed_size_byte_aligned/fixed_size_byte_aligned_compressor.cpp:21-43),
+ *                     dictionary = T[dictionary_size] sorted unique, null_value_id = dictionary_size
+ *                     (reference dictionary_column/dictionary_encoder.hpp:87)
+ *
+ * All device pointers must be 16-byte aligned; buffers must be readable up to the next multiple of 16 bytes.
+ * ------------------------------------------------------------------------------------------------------------- */
+enum { HY_COL_VALUE = 0, HY_COL_DICT = 1 };
+
+typedef struct hy_column_chunk {
+  const void* data;          /* values (VALUE) or attribute vector (DICT) */
+  const uint8_t* nulls;      /* VALUE: null flags or NULL; DICT: unused */
+  const void* dictionary;    /* DICT: sorted dictionary (device) */
+  uint32_t size;             /* rows in this chunk */
+  uint32_t dictionary_size;  /* DICT: number of dictionary entries (== null value id) */
+  int32_t kind;              /* HY_COL_VALUE / HY_COL_DICT */
+  int32_t vid_width;         /* DICT: 1, 2 or 4 bytes */
+} hy_column_chunk;
+
+/* ---------------------------------------------------------------------------------------------------------------
+ * TableScan (single column vs constant)
+ *
+ * Replaces the per-chunk hot loop BaseTableScanImpl::_unary_scan_with_value / _unary_scan
+ * (reference src/lib/operators/table_scan/base_table_scan_impl.hpp:33-63) as driven by
+ * SingleColumnTableScanImpl::handle_column (single_column_table_scan_impl.cpp:38-142) for all chunks of a table
+ * in ONE launch. The dictionary rewrite (search value id via lower/upper_bound and the all/none early-outs,
+ * single_column_table_scan_impl.cpp:145-205) is host work per chunk and arrives here as (op, search_vid).
+ *
+ * Output is order-preserving: for chunk c the matching chunk offsets are written ascending at
+ * out_offsets + out_begin[c] and counts[c] receives the number of matches, exactly the PosList the reference
+ * builds for that chunk ({c, offset} for each match).
+ * ------------------------------------------------------------------------------------------------------------- */
+enum {
+  HY_OP_EQ = 0, /* ==  */
+  HY_OP_NE = 1, /* !=  */
+  HY_OP_LT = 2, /* <   */
+  HY_OP_LE = 3, /* <=  */
+  HY_OP_GT = 4, /* >   */
+  HY_OP_GE = 5, /* >=  */
+  HY_OP_ALL = 6, /* every non-NULL row (dictionary "matches all" early-out) */
+  HY_OP_NONE = 7 /* no row (dictionary "matches none" early-out) */
+};
+
+typedef struct hy_scan_chunk {
+  hy_column_chunk column;
+  int32_t op;            /* HY_OP_*; for DICT chunks compared against search_vid */
+  uint32_t search_vid;   /* DICT: search value id (host-computed, reference _get_search_value_id) */
+  uint64_t out_begin;    /* first output slot of this chunk (capacity = column.size) */
+} hy_scan_chunk;
+
+/* Workspace bytes for a scan over chunks with the given sizes. */
+hy_status hy_table_scan_workspace_size(const uint32_t* chunk_sizes, uint32_t n_chunks, size_t* bytes);
+
+/*
+ * value_type: HY_TYPE_* of VALUE chunks (ignored for DICT chunks). constant: host pointer to one value of
+ * value_type (the type_cast<T>(right_value) of the reference). chunks: HOST array. out_offsets and counts: device.
+ */
+hy_status hy_table_scan(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_t value_type, const void* constant,
+                        uint32_t* out_offsets, uint32_t* counts, void* workspace, size_t workspace_bytes,
+                        hy_stream_t stream);
+
+/*
+ * Scan over a ReferenceColumn (reference BaseSingleColumnTableScanImpl::handle_column(const ReferenceColumn&),
+ * base_single_column_table_scan_impl.cpp:36-60): for each position i of pos_list (device RowIDs) whose RowID is
+ * not NULL, the referenced value is read from referenced_chunks[row.chunk_id] and compared. Positions of matches
+ * are written ascending to out_positions; *count (device) receives the number of matches. Per referenced chunk
+ * the predicate is given by ref_scan[row.chunk_id] (op + search_vid, because dictionaries differ per chunk).
+ * Group ordering of the reference's unordered_map over referenced chunks is applied by the caller
+ * (hy_stable_order_by_group).
+ */
+hy_status hy_reference_scan_workspace_size(uint64_t pos_list_size, size_t* bytes);
+hy_status hy_reference_scan(const hy_row_id* pos_list, uint64_t pos_list_size, const hy_scan_chunk* referenced_chunks,
+                            uint32_t n_referenced_chunks, int32_t value_type, const void* constant,
+                            uint32_t* out_positions, uint64_t* count, void* workspace, size_t workspace_bytes,
+                            hy_stream_t stream);
+
+/*
+ * out[i] = pos_list[positions[i]] for i < n (device gather; builds the filtered PosList of a reference-input
+ * scan, reference table_scan.cpp:124-134, and the dereference of write_output_columns, join_hash.cpp:584-592).
+ */
+hy_status hy_gather_row_ids(const hy_row_id* pos_list, const uint32_t* positions, uint64_t n, hy_row_id* out,
+                            hy_stream_t stream);
+
+/*
+ * first_seen[c] = smallest position i with pos_list[i].chunk_id == c (NULL RowIDs skipped), ~0 if none, for
+ * c < n_chunks. Gives the order in which split_pos_list_by_chunk_id (reference
+ * src/lib/storage/column_iterables/chunk_offset_mapping.cpp:5-21) first inserts each referenced chunk.
+ */
+hy_status hy_pos_list_chunk_first_seen(const hy_row_id* pos_list, uint64_t n, uint32_t n_chunks, uint64_t* first_seen,
+                                       hy_stream_t stream);
+
+/* out[i] = {chunk_id, offsets[i]} — expands a single-chunk offset list into reference RowIDs. */
+hy_status hy_expand_row_ids(uint32_t chunk_id, const uint32_t* offsets, uint64_t n, hy_row_id* out,
+                            hy_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------------------------
+ * Hashing (reference src/lib/utils/murmur_hash.cpp:21-75, seed 17 from join_hash.cpp:680)
+ * ------------------------------------------------------------------------------------------------------------- */
+/* out[i] = murmur_hash2(&keys[i], key_bytes, seed); key_bytes 4 or 8. */
+hy_status hy_murmur2(const void* keys, uint64_t n, uint32_t key_bytes, uint32_t seed, uint32_t* out,
+                     hy_stream_t stream);
+/* Radix bits of JoinHashImpl's constructor (join_hash.cpp:640-668) for a build side of build_rows rows. */
+uint32_t hy_join_radix_bits(uint64_t build_rows, uint32_t key_bytes);
+
+/* ---------------------------------------------------------------------------------------------------------------
+ * JoinHash (equi-join, radix partitioned)
+ *
+ * Replaces JoinHashImpl::_on_execute's materialize_input / partition_radix_parallel / build / probe
+ * (reference src/lib/operators/join_hash.cpp:203-527). One side of the join ("build" / "probe" after the
+ * reference's swap rule, join_hash.cpp:55-76) is described by a list of chunks. A chunk is either a column chunk
+ * of a data table, or — for a reference table — a device PosList into referenced column chunks.
+ *
+ * Output reproduces the reference exactly: one output chunk per radix partition p (ascending) with at least one
+ * emitted pair; inside a partition, probe rows in (chunk, offset) order and for each probe row its build matches
+ * in build (chunk, offset) order. partition_counts[p] = pairs of partition p, written at
+ * [partition_begin[p], partition_begin[p] + partition_counts[p]) of out_build / out_probe.
+ * Rows are emitted as RowIDs of the side's input table: (input chunk id, offset in that chunk / in the
+ * ReferenceColumn), like the reference before write_output_columns; NULL_ROW_ID for the outer side of a
+ * Left/Right join without match. Semi/Anti write only out_probe.
+ * ------------------------------------------------------------------------------------------------------------- */
+enum { HY_JOIN_INNER = 0, HY_JOIN_LEFT = 1, HY_JOIN_RIGHT = 2, HY_JOIN_SEMI = 5, HY_JOIN_ANTI = 6 };
+
+typedef struct hy_join_chunk {
+  hy_column_chunk column;      /* data-table chunk (pos_list == NULL) */
+  const hy_row_id* pos_list;   /* reference-table chunk: device PosList of this chunk, or NULL */
+  uint32_t size;               /* rows of this chunk (== column.size or PosList length) */
+  uint32_t chunk_id;           /* chunk id of this chunk in its table */
+} hy_join_chunk;
+
+typedef struct hy_join_side {
+  const hy_join_chunk* chunks;            /* HOST array, one per chunk of the side's table */
+  uint32_t n_chunks;
+  int32_t value_type;                     /* HY_TYPE_* of the join column */
+  const hy_column_chunk* referenced;      /* HOST array: column chunks of the referenced table (reference sides) */
+  uint32_t n_referenced;
+  /* reference sides only: 1 = emit RowIDs of the referenced table (fused write_output_columns dereference, valid
+   * when every output column of this side shares the join column's PosLists); 0 = emit RowIDs of the side's own
+   * table, to be dereferenced per PosList group with hy_dereference_row_ids. */
+  int32_t fuse_dereference;
+} hy_join_side;
+
+typedef struct hy_join_params {
+  int32_t mode;           /* HY_JOIN_* */
+  int32_t hashed_type;    /* HY_TYPE_* of JoinHashTraits<L,R>::HashType (hash_traits.hpp:9-42) */
+  uint32_t radix_bits;    /* normally hy_join_radix_bits(build rows) */
+  uint32_t seed;          /* 17 */
+} hy_join_params;
+
+typedef struct hy_join_result {
+  uint64_t total_pairs;        /* written by hy_join_hash */
+  uint64_t capacity_required;  /* set when HY_ERR_CAPACITY is returned */
+} hy_join_result;
+
+hy_status hy_join_hash_workspace_size(const hy_join_side* build, const hy_join_side* probe,
+                                      const hy_join_params* params, size_t* bytes);
+/*
+ * out_build / out_probe: device RowID arrays of capacity out_capacity pairs.
+ * partition_begin / partition_counts: device arrays of 2^radix_bits uint64 / uint32.
+ */
+hy_status hy_join_hash(const hy_join_side* build, const hy_join_side* probe, const hy_join_params* params,
+                       hy_row_id* out_build, hy_row_id* out_probe, uint64_t out_capacity, uint64_t* partition_begin,
+                       uint32_t* partition_counts, hy_join_result* result, void* workspace, size_t workspace_bytes,
+                       hy_stream_t stream);
+
+/*
+ * out[i] = rows[i] is NULL ? rows[i] : chunk_pos_lists[rows[i].chunk_id][rows[i].chunk_offset]
+ * (reference write_output_columns, join_hash.cpp:584-592). chunk_pos_lists: DEVICE array of device PosList pointers.
+ */
+hy_status hy_dereference_row_ids(const hy_row_id* rows, uint64_t n, const hy_row_id* const* chunk_pos_lists,
+                                 hy_row_id* out, hy_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HYRISE_AMD_H_ */

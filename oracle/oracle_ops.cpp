@@ -1,0 +1,922 @@
+// ORACLE — test infrastructure only. CPU restatement of the reference's TableScan / JoinHash / Aggregate, used by
+// tests/ as the parity checker and by bench.py as the timed CPU baseline (cpu_baseline.kind = "port"). Nothing in
+// the product (hyrise-1_amd/) links or calls this code.
+//
+// Pinned by: the reference's own fixtures (src/test/tables/{joinoperators,aggregateoperator}/*.tbl and the TableScan
+// expectations of src/test/operators/table_scan_test.cpp, copied as data into tests/golden/), the murmur golden
+// vectors produced by compiling the reference's src/lib/utils/murmur_hash.cpp (oracle/_ref), and TPC-H known answers
+// from the reference's vendored dbgen + sqlite3 (tests/golden/tpch_*).
+//
+// Each function follows the reference file:line it names. Boost/TBB are absent, so std containers stand in; where
+// the reference's output order depends on libstdc++'s std::unordered_map (split_pos_list_by_chunk_id, Aggregate
+// results) the same container type is used with the same insertion sequence.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <array>
+#include <cmath>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <optional>
+#include <set>
+#include <thread>
+#include <unordered_map>
+#include <variant>
+#include <vector>
+
+#include "operators.hpp"
+#include "storage.hpp"
+
+namespace py = pybind11;
+using namespace hyrise;
+
+namespace oracle {
+
+// ---------------------------------------------------------------------------------------------------------------
+// MurmurHash2, reference src/lib/utils/murmur_hash.cpp:21-75
+// ---------------------------------------------------------------------------------------------------------------
+unsigned int murmur_hash2(const void* key, unsigned int len, unsigned int seed) {
+  const unsigned int m = 0x5bd1e995;
+  const unsigned int r = 24;
+  unsigned int h = seed ^ len;
+  const auto* data = static_cast<const unsigned char*>(key);
+  while (len >= 4) {
+    unsigned int k;
+    std::memcpy(&k, data, sizeof(k));
+    k *= m;
+    k ^= k >> r;
+    k *= m;
+    h *= m;
+    h ^= k;
+    data += 4;
+    len -= 4;
+  }
+  switch (len) {
+    case 3:
+      h ^= data[2] << 16u;
+      [[fallthrough]];
+    case 2:
+      h ^= data[1] << 8u;
+      [[fallthrough]];
+    case 1:
+      h ^= data[0];
+      h *= m;
+  }
+  h ^= h >> 13u;
+  h *= m;
+  h ^= h >> 15u;
+  return h;
+}
+
+template <typename T>
+unsigned int murmur2(const T& key, unsigned int seed) {
+  if constexpr (std::is_same_v<T, std::string>) {
+    return murmur_hash2(key.c_str(), static_cast<unsigned int>(key.size()), seed);
+  } else {
+    return murmur_hash2(&key, sizeof(T), seed);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Column iteration (reference column iterables): value, is_null, chunk_offset. For a mapped iteration
+// (ChunkOffsetsList) chunk_offset is into_referencing.
+// ---------------------------------------------------------------------------------------------------------------
+template <typename T>
+struct Item {
+  T value;
+  bool is_null;
+  ChunkOffset chunk_offset;
+};
+
+template <typename T>
+T value_or_default(const AllTypeVariant& v) {
+  if (variant_is_null(v)) return T{};
+  return type_cast<T>(v);
+}
+
+// Iterate a data column (value / dictionary) of type T, optionally through mapped offsets.
+template <typename T, typename F>
+void for_each_data(const BaseColumn& col, const std::vector<std::pair<ChunkOffset, ChunkOffset>>* mapped, F&& f) {
+  auto get = [&](ChunkOffset o) -> std::pair<T, bool> {
+    if (const auto* vc = dynamic_cast<const ValueColumn<T>*>(&col)) {
+      const bool n = vc->is_null(o);
+      return {vc->values()[o], n};
+    }
+    const auto* dc = dynamic_cast<const DictionaryColumn<T>*>(&col);
+    Assert(dc != nullptr, "oracle: unsupported column type");
+    const ValueID vid = dc->attribute_vector().get(o);
+    if (vid == dc->null_value_id()) return {T{}, true};
+    return {dc->dictionary()[vid], false};
+  };
+  if (mapped) {
+    for (const auto& [into_referencing, into_referenced] : *mapped) {
+      const auto [v, n] = get(into_referenced);
+      f(Item<T>{v, n, into_referencing});
+    }
+  } else {
+    for (ChunkOffset o = 0; o < col.size(); ++o) {
+      const auto [v, n] = get(o);
+      f(Item<T>{v, n, o});
+    }
+  }
+}
+
+// Iterate any column as type T (reference create_iterable_from_column; ReferenceColumnIterable
+// reference_column/reference_column_iterable.hpp:59-90 dereferences with operator[] + type_cast).
+template <typename T, typename F>
+void for_each_any(const BaseColumn& col, F&& f) {
+  if (const auto* rc = dynamic_cast<const ReferenceColumn*>(&col)) {
+    const auto& pl = *rc->pos_list();
+    for (ChunkOffset o = 0; o < pl.size(); ++o) {
+      const RowID r = pl[o];
+      if (r.is_null()) {
+        f(Item<T>{T{}, true, o});
+        continue;
+      }
+      const auto v = (*rc->referenced_table()->get_chunk(r.chunk_id)->get_column(rc->referenced_column_id()))[r.chunk_offset];
+      if (variant_is_null(v))
+        f(Item<T>{T{}, true, o});
+      else
+        f(Item<T>{type_cast<T>(v), false, o});
+    }
+    return;
+  }
+  for_each_data<T>(col, nullptr, f);
+}
+
+template <typename F>
+void with_comparator(PredicateCondition c, F&& f) {  // reference type_comparison.hpp:100-123
+  switch (c) {
+    case PredicateCondition::Equals:
+      return f(std::equal_to<void>{});
+    case PredicateCondition::NotEquals:
+      return f(std::not_equal_to<void>{});
+    case PredicateCondition::LessThan:
+      return f(std::less<void>{});
+    case PredicateCondition::LessThanEquals:
+      return f(std::less_equal<void>{});
+    case PredicateCondition::GreaterThan:
+      return f(std::greater<void>{});
+    case PredicateCondition::GreaterThanEquals:
+      return f(std::greater_equal<void>{});
+    default:
+      Fail("Unsupported operator.");
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// TableScan: reference table_scan.cpp:78-164, single_column_table_scan_impl.cpp:23-205,
+// base_single_column_table_scan_impl.cpp:22-60, base_table_scan_impl.hpp:33-63, chunk_offset_mapping.cpp:5-21
+// ---------------------------------------------------------------------------------------------------------------
+using Mapped = std::vector<std::pair<ChunkOffset, ChunkOffset>>;
+
+void scan_data_column(const BaseColumn& col, DataType type, PredicateCondition cond, const AllTypeVariant& value,
+                      ChunkID chunk_id, const Mapped* mapped, PosList& out) {
+  if (const auto* dict = dynamic_cast<const BaseDictionaryColumn*>(&col)) {
+    ValueID svid;
+    switch (cond) {
+      case PredicateCondition::Equals:
+      case PredicateCondition::NotEquals:
+      case PredicateCondition::LessThan:
+      case PredicateCondition::GreaterThanEquals:
+        svid = dict->lower_bound(value);
+        break;
+      case PredicateCondition::LessThanEquals:
+      case PredicateCondition::GreaterThan:
+        svid = dict->upper_bound(value);
+        break;
+      default:
+        Fail("Unsupported comparison type encountered");
+    }
+    bool all = false, none = false;
+    switch (cond) {
+      case PredicateCondition::Equals:
+        all = svid != dict->upper_bound(value) && dict->unique_values_count() == 1u;
+        none = svid == dict->upper_bound(value);
+        break;
+      case PredicateCondition::NotEquals:
+        all = svid == dict->upper_bound(value);
+        none = svid == dict->upper_bound(value) && dict->unique_values_count() == 1u;
+        break;
+      case PredicateCondition::LessThan:
+      case PredicateCondition::LessThanEquals:
+        all = svid == INVALID_VALUE_ID;
+        none = svid == 0u;
+        break;
+      default:
+        all = svid == 0u;
+        none = svid == INVALID_VALUE_ID;
+        break;
+    }
+    const auto& av = dict->attribute_vector();
+    const ValueID null_vid = dict->null_value_id();
+    auto visit = [&](auto&& pred) {
+      auto one = [&](ChunkOffset into_referencing, ChunkOffset o) {
+        const ValueID vid = av.get(o);
+        if (vid == null_vid) return;
+        if (pred(vid)) out.emplace_back(chunk_id, into_referencing);
+      };
+      if (mapped)
+        for (const auto& [a, b] : *mapped) one(a, b);
+      else
+        for (ChunkOffset o = 0; o < col.size(); ++o) one(o, o);
+    };
+    if (all) {
+      visit([](ValueID) { return true; });
+      return;
+    }
+    if (none) return;
+    switch (cond) {
+      case PredicateCondition::Equals:
+        visit([&](ValueID v) { return v == svid; });
+        break;
+      case PredicateCondition::NotEquals:
+        visit([&](ValueID v) { return v != svid; });
+        break;
+      case PredicateCondition::LessThan:
+      case PredicateCondition::LessThanEquals:
+        visit([&](ValueID v) { return v < svid; });
+        break;
+      default:
+        visit([&](ValueID v) { return v >= svid; });
+        break;
+    }
+    return;
+  }
+  resolve_data_type(type, [&](auto tag) {
+    using T = decltype(tag);
+    const T c = type_cast<T>(value);
+    with_comparator(cond, [&](auto cmp) {
+      for_each_data<T>(col, mapped, [&](const Item<T>& it) {
+        if (it.is_null) return;
+        if (cmp(it.value, c)) out.emplace_back(chunk_id, it.chunk_offset);
+      });
+    });
+  });
+}
+
+std::shared_ptr<Table> table_scan(const std::shared_ptr<const Table>& in, ColumnID col, PredicateCondition cond,
+                                  const AllTypeVariant& value, const std::vector<ChunkID>& excluded) {
+  if (cond == PredicateCondition::Between) Fail("Unsupported comparison type encountered");
+  auto out = std::make_shared<Table>(in->column_definitions(), TableType::References);
+  const DataType type = in->column_data_type(col);
+  for (ChunkID chunk_id = 0; chunk_id < in->chunk_count(); ++chunk_id) {
+    if (std::find(excluded.begin(), excluded.end(), chunk_id) != excluded.end()) continue;
+    auto matches = std::make_shared<PosList>();
+    if (!variant_is_null(value)) {
+      const auto column = in->get_chunk(chunk_id)->get_column(col);
+      if (const auto* rc = dynamic_cast<const ReferenceColumn*>(column.get())) {
+        // split_pos_list_by_chunk_id: std::unordered_map<ChunkID, ChunkOffsetsList>
+        std::unordered_map<ChunkID, Mapped> by_chunk;
+        const auto& pl = *rc->pos_list();
+        for (ChunkOffset o = 0; o < pl.size(); ++o) {
+          const RowID r = pl[o];
+          if (r.is_null()) continue;
+          by_chunk[r.chunk_id].emplace_back(o, r.chunk_offset);
+        }
+        for (const auto& [ref_chunk, mapped] : by_chunk) {
+          const auto rcol = rc->referenced_table()->get_chunk(ref_chunk)->get_column(rc->referenced_column_id());
+          scan_data_column(*rcol, type, cond, value, chunk_id, &mapped, *matches);
+        }
+      } else {
+        scan_data_column(*column, type, cond, value, chunk_id, nullptr, *matches);
+      }
+    }
+    if (matches->empty()) continue;
+    ChunkColumns cols;
+    if (in->type() == TableType::References) {
+      std::map<std::shared_ptr<const PosList>, std::shared_ptr<PosList>> filtered;
+      const auto chunk = in->get_chunk(chunk_id);
+      for (ColumnID c = 0; c < in->column_count(); ++c) {
+        const auto rc = std::static_pointer_cast<const ReferenceColumn>(chunk->get_column(c));
+        auto& f = filtered[rc->pos_list()];
+        if (!f) {
+          f = std::make_shared<PosList>();
+          f->reserve(matches->size());
+          for (const auto& m : *matches) f->push_back((*rc->pos_list())[m.chunk_offset]);
+        }
+        cols.push_back(std::make_shared<ReferenceColumn>(rc->referenced_table(), rc->referenced_column_id(), f));
+      }
+    } else {
+      for (ColumnID c = 0; c < in->column_count(); ++c) cols.push_back(std::make_shared<ReferenceColumn>(in, c, matches));
+    }
+    out->append_chunk(cols);
+  }
+  return out;
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// JoinHash: reference join_hash.cpp:49-858
+// ---------------------------------------------------------------------------------------------------------------
+template <typename T>
+struct PartitionedElement {
+  RowID row_id = NULL_ROW_ID;
+  uint32_t partition_hash = 0;
+  T value{};
+};
+
+template <typename T>
+using Partition = std::vector<PartitionedElement<T>>;
+
+template <typename T>
+struct RadixContainer {
+  std::shared_ptr<Partition<T>> elements;
+  std::vector<size_t> partition_offsets;
+};
+
+// join_hash.cpp:640-668, same float arithmetic (sizeof(PosList) = 32, sizeof(RowID) = 8)
+uint32_t radix_bits(uint64_t build_rows, uint32_t left_type_size) {
+  const auto complete_hash_map_size = build_rows * (left_type_size + sizeof(void*)) + (build_rows / 2) * (32 + 2 * 8);
+  const auto adaption_factor = 2.0f;
+  const auto cluster_count = std::max(1.0f, (adaption_factor * complete_hash_map_size) / 256'000);
+  return static_cast<uint32_t>(std::ceil(std::log2(cluster_count)));
+}
+
+template <typename H, typename T>
+H hashed_cast(const T& v) {
+  if constexpr (std::is_same_v<H, T>) {
+    return v;
+  } else {
+    return type_cast<H>(AllTypeVariant{v});
+  }
+}
+
+// materialize_input, join_hash.cpp:203-285 (sequential over chunks; the per-chunk jobs write disjoint ranges)
+template <typename T, typename H>
+std::shared_ptr<Partition<T>> materialize_input(const std::shared_ptr<const Table>& in, ColumnID col,
+                                                std::vector<std::vector<size_t>>& histograms, size_t bits,
+                                                unsigned seed, bool keep_nulls, std::vector<size_t>& chunk_offsets) {
+  auto elements = std::make_shared<Partition<T>>(in->row_count());
+  const size_t num_partitions = size_t{1} << bits;
+  const size_t mask = static_cast<uint32_t>(std::pow(2, bits) - 1);
+  chunk_offsets.assign(in->chunk_count(), 0);
+  size_t off = 0;
+  for (ChunkID c = 0; c < in->chunk_count(); ++c) {
+    chunk_offsets[c] = off;
+    off += in->get_chunk(c)->get_column(col)->size();
+  }
+  histograms.assign(in->chunk_count(), std::vector<size_t>(num_partitions, 0));
+  for (ChunkID chunk_id = 0; chunk_id < in->chunk_count(); ++chunk_id) {
+    auto it = elements->begin() + chunk_offsets[chunk_id];
+    auto& hist = histograms[chunk_id];
+    const auto column = in->get_chunk(chunk_id)->get_column(col);
+    const bool is_ref = column->is_reference();
+    ChunkOffset ref_off = 0;
+    for_each_any<T>(*column, [&](const Item<T>& v) {
+      if (!v.is_null || keep_nulls) {
+        const uint32_t h = murmur2<H>(hashed_cast<H>(v.value), seed);
+        *(it++) = PartitionedElement<T>{RowID{chunk_id, is_ref ? ref_off : v.chunk_offset}, h, v.value};
+        hist[h & mask]++;
+      }
+      if (is_ref) ref_off++;
+    });
+  }
+  return elements;
+}
+
+// partition_radix_parallel, join_hash.cpp:287-355
+template <typename T>
+RadixContainer<T> partition_radix(const std::shared_ptr<Partition<T>>& materialized,
+                                  const std::vector<size_t>& chunk_offsets,
+                                  const std::vector<std::vector<size_t>>& histograms, size_t bits, bool keep_nulls) {
+  const size_t num_partitions = size_t{1} << bits;
+  const size_t mask = static_cast<uint32_t>(std::pow(2, bits) - 1);
+  auto output = std::make_shared<Partition<T>>(materialized->size());
+  RadixContainer<T> rc;
+  rc.elements = output;
+  rc.partition_offsets.resize(num_partitions + 1);
+  size_t offset = 0;
+  std::vector<std::vector<size_t>> out_off(chunk_offsets.size(), std::vector<size_t>(num_partitions));
+  for (size_t p = 0; p < num_partitions; ++p) {
+    rc.partition_offsets[p] = offset;
+    for (size_t c = 0; c < chunk_offsets.size(); ++c) {
+      out_off[c][p] = offset;
+      offset += histograms[c][p];
+    }
+  }
+  rc.partition_offsets[num_partitions] = offset;
+  for (size_t c = 0; c < chunk_offsets.size(); ++c) {
+    const size_t begin = chunk_offsets[c];
+    const size_t end = c + 1 < chunk_offsets.size() ? chunk_offsets[c + 1] : materialized->size();
+    for (size_t i = begin; i < end; ++i) {
+      const auto& e = (*materialized)[i];
+      if (!keep_nulls && e.row_id.chunk_offset == INVALID_CHUNK_OFFSET) continue;
+      (*output)[out_off[c][e.partition_hash & mask]++] = e;
+    }
+  }
+  return rc;
+}
+
+template <typename H>
+using HashTable = std::unordered_map<H, std::variant<RowID, PosList>>;
+
+template <typename L, typename H>
+std::vector<std::optional<HashTable<H>>> build(const RadixContainer<L>& rc) {  // join_hash.cpp:127-185
+  std::vector<std::optional<HashTable<H>>> tables(rc.partition_offsets.size() - 1);
+  for (size_t p = 0; p + 1 < rc.partition_offsets.size(); ++p) {
+    const size_t b = rc.partition_offsets[p], e = rc.partition_offsets[p + 1];
+    if (b == e) continue;
+    HashTable<H> ht(e - b);
+    for (size_t i = b; i < e; ++i) {
+      const auto& el = (*rc.elements)[i];
+      const H key = hashed_cast<H>(el.value);
+      auto it = ht.find(key);
+      if (it == ht.end()) {
+        ht[key] = el.row_id;
+      } else if (std::holds_alternative<RowID>(it->second)) {
+        ht[key] = PosList{std::get<RowID>(it->second), el.row_id};
+      } else {
+        std::get<PosList>(it->second).push_back(el.row_id);
+      }
+    }
+    tables[p] = std::move(ht);
+  }
+  return tables;
+}
+
+template <typename R, typename H>
+void probe(const RadixContainer<R>& rc, const std::vector<std::optional<HashTable<H>>>& tables,
+           std::vector<PosList>& left, std::vector<PosList>& right, JoinMode mode) {  // join_hash.cpp:362-466
+  for (size_t p = 0; p + 1 < rc.partition_offsets.size(); ++p) {
+    const size_t b = rc.partition_offsets[p], e = rc.partition_offsets[p + 1];
+    if (b == e) continue;
+    PosList l, r;
+    if (tables[p].has_value()) {
+      const auto& ht = *tables[p];
+      for (size_t i = b; i < e; ++i) {
+        const auto& row = (*rc.elements)[i];
+        if (mode == JoinMode::Inner && row.row_id.chunk_offset == INVALID_CHUNK_OFFSET) continue;
+        const auto it = ht.find(hashed_cast<H>(row.value));
+        if (it != ht.end()) {
+          if (std::holds_alternative<PosList>(it->second)) {
+            for (const auto rid : std::get<PosList>(it->second)) {
+              if (rid.chunk_offset != INVALID_CHUNK_OFFSET) {
+                l.push_back(rid);
+                r.push_back(row.row_id);
+              }
+            }
+          } else {
+            const auto rid = std::get<RowID>(it->second);
+            if (rid.chunk_offset != INVALID_CHUNK_OFFSET) {
+              l.push_back(rid);
+              r.push_back(row.row_id);
+            }
+          }
+        } else if (mode == JoinMode::Left || mode == JoinMode::Right) {
+          l.push_back(NULL_ROW_ID);
+          r.push_back(row.row_id);
+        }
+      }
+    } else if (mode == JoinMode::Left || mode == JoinMode::Right) {
+      for (size_t i = b; i < e; ++i) {
+        l.push_back(NULL_ROW_ID);
+        r.push_back((*rc.elements)[i].row_id);
+      }
+    }
+    if (!l.empty()) {
+      left[p] = std::move(l);
+      right[p] = std::move(r);
+    }
+  }
+}
+
+template <typename R, typename H>
+void probe_semi_anti(const RadixContainer<R>& rc, const std::vector<std::optional<HashTable<H>>>& tables,
+                     std::vector<PosList>& out, JoinMode mode) {  // join_hash.cpp:468-527
+  for (size_t p = 0; p + 1 < rc.partition_offsets.size(); ++p) {
+    const size_t b = rc.partition_offsets[p], e = rc.partition_offsets[p + 1];
+    if (b == e) continue;
+    PosList local;
+    if (tables[p].has_value()) {
+      for (size_t i = b; i < e; ++i) {
+        const auto& row = (*rc.elements)[i];
+        if (row.row_id.chunk_offset == INVALID_CHUNK_OFFSET) continue;
+        const auto it = tables[p]->find(hashed_cast<H>(row.value));
+        if ((mode == JoinMode::Semi && it != tables[p]->end()) || (mode == JoinMode::Anti && it == tables[p]->end()))
+          local.push_back(row.row_id);
+      }
+    } else if (mode == JoinMode::Anti) {
+      for (size_t i = b; i < e; ++i) local.push_back((*rc.elements)[i].row_id);
+    }
+    if (!local.empty()) out[p] = std::move(local);
+  }
+}
+
+using PosLists = std::vector<std::shared_ptr<const PosList>>;
+using PosListsByColumn = std::vector<std::shared_ptr<PosLists>>;
+
+PosListsByColumn setup_pos_lists_by_column(const std::shared_ptr<const Table>& t) {  // join_hash.cpp:533-562
+  std::map<PosLists, std::shared_ptr<PosLists>> shared;
+  PosListsByColumn out(t->column_count());
+  for (ColumnID c = 0; c < t->column_count(); ++c) {
+    auto v = std::make_shared<PosLists>(t->chunk_count());
+    for (ChunkID ch = 0; ch < t->chunk_count(); ++ch)
+      (*v)[ch] = std::static_pointer_cast<const ReferenceColumn>(t->get_chunk(ch)->get_column(c))->pos_list();
+    out[c] = shared.emplace(*v, v).first->second;
+  }
+  return out;
+}
+
+void write_output_columns(ChunkColumns& out, const std::shared_ptr<const Table>& in, const PosListsByColumn& by_col,
+                          const std::shared_ptr<PosList>& pos_list) {  // join_hash.cpp:564-613
+  std::map<std::shared_ptr<PosLists>, std::shared_ptr<PosList>> cache;
+  std::shared_ptr<Table> dummy;
+  for (ColumnID c = 0; c < in->column_count(); ++c) {
+    if (in->type() == TableType::References) {
+      if (in->chunk_count() > 0) {
+        const auto& lists = by_col[c];
+        auto it = cache.find(lists);
+        if (it == cache.end()) {
+          auto np = std::make_shared<PosList>(pos_list->size());
+          for (size_t i = 0; i < pos_list->size(); ++i) {
+            const RowID row = (*pos_list)[i];
+            (*np)[i] = row.chunk_offset == INVALID_CHUNK_OFFSET ? row : (*(*lists)[row.chunk_id])[row.chunk_offset];
+          }
+          it = cache.emplace(lists, np).first;
+        }
+        const auto rc = std::static_pointer_cast<const ReferenceColumn>(in->get_chunk(0)->get_column(c));
+        out.push_back(std::make_shared<ReferenceColumn>(rc->referenced_table(), rc->referenced_column_id(), it->second));
+      } else {
+        if (!dummy) dummy = Table::create_dummy_table(in->column_definitions());
+        out.push_back(std::make_shared<ReferenceColumn>(dummy, c, pos_list));
+      }
+    } else {
+      out.push_back(std::make_shared<ReferenceColumn>(in, c, pos_list));
+    }
+  }
+}
+
+template <typename L, typename R>
+std::shared_ptr<Table> join_impl(const std::shared_ptr<const Table>& left_in, const std::shared_ptr<const Table>& right_in,
+                                 JoinMode mode, std::pair<ColumnID, ColumnID> cols, bool swapped, uint32_t* bits_out) {
+  using H = std::conditional_t<
+      std::is_same_v<L, std::string> || std::is_same_v<R, std::string>, std::string,
+      std::conditional_t<std::is_floating_point_v<L> && std::is_floating_point_v<R>,
+                         std::conditional_t<(sizeof(L) < sizeof(R)), R, L>,
+                         std::conditional_t<std::is_integral_v<L> && std::is_integral_v<R>,
+                                            std::conditional_t<(sizeof(L) < sizeof(R)), R, L>,
+                                            std::conditional_t<std::is_floating_point_v<L>, L, R>>>>;
+  // _left = build, _right = probe
+  const size_t bits = radix_bits(left_in->row_count(), sizeof(L));
+  if (bits_out) *bits_out = static_cast<uint32_t>(bits);
+  TableColumnDefinitions defs;
+  if (swapped) {
+    defs = right_in->column_definitions();
+    if (!(mode == JoinMode::Semi || mode == JoinMode::Anti))
+      for (const auto& d : left_in->column_definitions()) defs.push_back(d);
+  } else {
+    defs = left_in->column_definitions();
+    for (const auto& d : right_in->column_definitions()) defs.push_back(d);
+  }
+  auto out = std::make_shared<Table>(defs, TableType::References);
+  const bool keep_nulls = mode == JoinMode::Left || mode == JoinMode::Right;
+  std::vector<std::vector<size_t>> hl, hr;
+  std::vector<size_t> ol, orr;
+  auto ml = materialize_input<L, H>(left_in, cols.first, hl, bits, 17, false, ol);
+  auto mr = materialize_input<R, H>(right_in, cols.second, hr, bits, 17, keep_nulls, orr);
+  auto rl = partition_radix<L>(ml, ol, hl, bits, false);
+  auto rr = partition_radix<R>(mr, orr, hr, bits, keep_nulls);
+  auto tables = build<L, H>(rl);
+  const size_t parts = rr.partition_offsets.size() - 1;
+  std::vector<PosList> lp(parts), rp(parts);
+  if (mode == JoinMode::Semi || mode == JoinMode::Anti)
+    probe_semi_anti<R, H>(rr, tables, rp, mode);
+  else
+    probe<R, H>(rr, tables, lp, rp, mode);
+  const bool only_right = swapped && (mode == JoinMode::Semi || mode == JoinMode::Anti);
+  PosListsByColumn lbc, rbc;
+  if (left_in->type() == TableType::References && !only_right) lbc = setup_pos_lists_by_column(left_in);
+  if (right_in->type() == TableType::References) rbc = setup_pos_lists_by_column(right_in);
+  for (size_t p = 0; p < parts; ++p) {
+    auto l = std::make_shared<PosList>(std::move(lp[p]));
+    auto r = std::make_shared<PosList>(std::move(rp[p]));
+    if (l->empty() && r->empty()) continue;
+    ChunkColumns oc;
+    if (swapped) {
+      write_output_columns(oc, right_in, rbc, r);
+      if (!only_right) write_output_columns(oc, left_in, lbc, l);
+    } else {
+      write_output_columns(oc, left_in, lbc, l);
+      write_output_columns(oc, right_in, rbc, r);
+    }
+    out->append_chunk(oc);
+  }
+  return out;
+}
+
+std::pair<std::shared_ptr<Table>, uint32_t> join_hash(const std::shared_ptr<const Table>& left,
+                                                      const std::shared_ptr<const Table>& right, JoinMode mode,
+                                                      std::pair<ColumnID, ColumnID> cols) {
+  bool swapped = (mode == JoinMode::Left || mode == JoinMode::Anti || mode == JoinMode::Semi);
+  if (!swapped && left->row_count() > right->row_count()) swapped = true;
+  const auto build_t = swapped ? right : left;
+  const auto probe_t = swapped ? left : right;
+  const auto adjusted = swapped ? std::make_pair(cols.second, cols.first) : cols;
+  std::shared_ptr<Table> out;
+  uint32_t bits = 0;
+  resolve_data_type(build_t->column_data_type(adjusted.first), [&](auto lt) {
+    resolve_data_type(probe_t->column_data_type(adjusted.second), [&](auto rt) {
+      out = join_impl<decltype(lt), decltype(rt)>(build_t, probe_t, mode, adjusted, swapped, &bits);
+    });
+  });
+  return {out, bits};
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Aggregate: reference aggregate.cpp:203-820, aggregate_traits.hpp:15-74
+// ---------------------------------------------------------------------------------------------------------------
+struct ArrayHash {  // boost::hash_range with boost::hash_combine (pre-1.81), aggregate.hpp:154-169
+  size_t operator()(const std::array<uint64_t, 2>& k) const {
+    size_t seed = 0;
+    for (auto v : k) seed ^= static_cast<size_t>(v) + 0x9e3779b9 + (seed << 6) + (seed >> 2);
+    return seed;
+  }
+};
+struct VecHash {
+  size_t operator()(const std::vector<uint64_t>& k) const {
+    size_t seed = 0;
+    for (auto v : k) seed ^= static_cast<size_t>(v) + 0x9e3779b9 + (seed << 6) + (seed >> 2);
+    return seed;
+  }
+};
+template <typename K>
+struct KeyHash {
+  using type = std::hash<K>;
+};
+template <>
+struct KeyHash<std::array<uint64_t, 2>> {
+  using type = ArrayHash;
+};
+template <>
+struct KeyHash<std::vector<uint64_t>> {
+  using type = VecHash;
+};
+
+struct AggResult {
+  std::optional<std::variant<int32_t, int64_t, float, double, std::string>> current;
+  size_t count = 0;
+  std::set<std::variant<int32_t, int64_t, float, double, std::string>> distinct;
+  RowID row_id;
+};
+
+template <typename K>
+using Results = std::unordered_map<K, AggResult, typename KeyHash<K>::type>;
+
+template <typename K>
+void set_key(K& key, size_t idx, uint64_t id) {
+  if constexpr (std::is_same_v<K, uint64_t>)
+    key = id;
+  else
+    key[idx] = id;
+}
+
+template <typename K>
+std::shared_ptr<Table> aggregate_impl(const std::shared_ptr<const Table>& in, const std::vector<AggregateColumnDefinition>& aggs,
+                                      const std::vector<ColumnID>& groupby) {
+  for (const auto& a : aggs) {
+    if (!a.column) {
+      if (a.function != AggregateFunction::Count) Fail("Aggregate: Asterisk is only valid with COUNT");
+    } else if (in->column_data_type(*a.column) == DataType::String &&
+               (a.function == AggregateFunction::Sum || a.function == AggregateFunction::Avg)) {
+      Fail("Aggregate: Cannot calculate SUM or AVG on string column");
+    }
+  }
+  // keys per chunk (aggregate.cpp:291-394)
+  std::vector<std::vector<K>> keys(in->chunk_count());
+  for (ChunkID c = 0; c < in->chunk_count(); ++c) {
+    if constexpr (std::is_same_v<K, std::vector<uint64_t>>)
+      keys[c].assign(in->get_chunk(c)->size(), K(groupby.size()));
+    else
+      keys[c].assign(in->get_chunk(c)->size(), K{});
+  }
+  for (size_t gi = 0; gi < groupby.size(); ++gi) {
+    resolve_data_type(in->column_data_type(groupby[gi]), [&](auto tag) {
+      using T = decltype(tag);
+      std::unordered_map<T, uint64_t> id_map;
+      uint64_t id_counter = 1;
+      for (ChunkID c = 0; c < in->chunk_count(); ++c) {
+        ChunkOffset o = 0;
+        for_each_any<T>(*in->get_chunk(c)->get_column(groupby[gi]), [&](const Item<T>& v) {
+          if (v.is_null) {
+            set_key(keys[c][o], gi, 0);
+          } else {
+            auto ins = id_map.try_emplace(v.value, id_counter);
+            set_key(keys[c][o], gi, ins.first->second);
+            if (ins.second) ++id_counter;
+          }
+          ++o;
+        });
+      }
+    });
+  }
+  // one results map per aggregate (+ one for DISTINCT / no-aggregate)
+  const size_t nres = aggs.empty() ? 1 : aggs.size();
+  std::vector<Results<K>> results(nres);
+  for (ChunkID c = 0; c < in->chunk_count(); ++c) {
+    const auto chunk = in->get_chunk(c);
+    if (aggs.empty()) {
+      for (ChunkOffset o = 0; o < chunk->size(); ++o) results[0][keys[c][o]].row_id = RowID{c, o};
+      continue;
+    }
+    for (size_t ai = 0; ai < aggs.size(); ++ai) {
+      const auto& a = aggs[ai];
+      auto& res = results[ai];
+      if (!a.column && a.function == AggregateFunction::Count) {
+        for (ChunkOffset o = 0; o < chunk->size(); ++o) {
+          auto& e = res[keys[c][o]];
+          e.row_id = RowID{c, o};
+          ++e.count;
+        }
+        continue;
+      }
+      resolve_data_type(in->column_data_type(*a.column), [&](auto tag) {
+        using T = decltype(tag);
+        ChunkOffset o = 0;
+        for_each_any<T>(*chunk->get_column(*a.column), [&](const Item<T>& v) {
+          auto& e = res[keys[c][o]];
+          e.row_id = RowID{c, o};
+          if (!v.is_null) {
+            switch (a.function) {
+              case AggregateFunction::Min:
+                if (!e.current || v.value < std::get<T>(*e.current)) e.current = v.value;
+                break;
+              case AggregateFunction::Max:
+                if (!e.current || v.value > std::get<T>(*e.current)) e.current = v.value;
+                break;
+              case AggregateFunction::Sum:
+              case AggregateFunction::Avg:
+                if constexpr (!std::is_same_v<T, std::string>) {
+                  // AggregateType: SUM int -> int64, SUM float -> double, AVG -> double
+                  if (a.function == AggregateFunction::Avg || std::is_floating_point_v<T>) {
+                    if (e.current)
+                      e.current = std::get<double>(*e.current) + v.value;
+                    else
+                      e.current = static_cast<double>(v.value);
+                  } else {
+                    if (e.current)
+                      e.current = std::get<int64_t>(*e.current) + v.value;
+                    else
+                      e.current = static_cast<int64_t>(v.value);
+                  }
+                }
+                break;
+              case AggregateFunction::CountDistinct:
+                e.distinct.insert(v.value);
+                break;
+              default:
+                break;
+            }
+            ++e.count;
+          }
+          ++o;
+        });
+      });
+    }
+  }
+  // output (aggregate.cpp:543-820)
+  TableColumnDefinitions defs;
+  std::vector<std::vector<AllTypeVariant>> columns;
+  for (const auto g : groupby) defs.emplace_back(in->column_name(g), in->column_data_type(g), true);
+  const auto& first = results[0];
+  std::vector<RowID> group_rows;
+  for (const auto& kv : first) group_rows.push_back(kv.second.row_id);
+  for (size_t gi = 0; gi < groupby.size(); ++gi) {
+    std::vector<AllTypeVariant> col;
+    for (const auto r : group_rows) col.push_back((*in->get_chunk(r.chunk_id)->get_column(groupby[gi]))[r.chunk_offset]);
+    columns.push_back(std::move(col));
+  }
+  for (size_t ai = 0; ai < aggs.size(); ++ai) {
+    const auto& a = aggs[ai];
+    const DataType in_type = a.column ? in->column_data_type(*a.column) : DataType::Int;
+    DataType out_type;
+    switch (a.function) {
+      case AggregateFunction::Count:
+      case AggregateFunction::CountDistinct:
+        out_type = DataType::Long;
+        break;
+      case AggregateFunction::Avg:
+        out_type = DataType::Double;
+        break;
+      case AggregateFunction::Sum:
+        out_type = (in_type == DataType::Float || in_type == DataType::Double) ? DataType::Double : DataType::Long;
+        break;
+      default:
+        out_type = in_type;
+    }
+    std::string name;
+    static const char* fn[] = {"MIN", "MAX", "SUM", "AVG", "COUNT", "COUNT"};
+    name = a.function == AggregateFunction::CountDistinct ? "COUNT(DISTINCT " : std::string(fn[int(a.function)]) + "(";
+    name += a.column ? in->column_name(*a.column) : "*";
+    name += ")";
+    const bool nullable = !(a.function == AggregateFunction::Count || a.function == AggregateFunction::CountDistinct);
+    defs.emplace_back(name, out_type, nullable);
+    std::vector<AllTypeVariant> col;
+    const auto& res = results[ai];
+    if (!res.empty()) {
+      for (const auto& kv : res) {
+        const auto& e = kv.second;
+        switch (a.function) {
+          case AggregateFunction::Count:
+            col.emplace_back(static_cast<int64_t>(e.count));
+            break;
+          case AggregateFunction::CountDistinct:
+            col.emplace_back(static_cast<int64_t>(e.distinct.size()));
+            break;
+          case AggregateFunction::Avg:
+            if (e.current)
+              col.emplace_back(std::get<double>(*e.current) / static_cast<double>(e.count));
+            else
+              col.emplace_back(NullValue{});
+            break;
+          default:
+            if (e.current)
+              std::visit([&](auto v) { col.emplace_back(v); }, *e.current);
+            else
+              col.emplace_back(NullValue{});
+        }
+      }
+    } else if (groupby.empty()) {
+      if (a.function == AggregateFunction::Count || a.function == AggregateFunction::CountDistinct)
+        col.emplace_back(int64_t{0});
+      else
+        col.emplace_back(NullValue{});
+    }
+    columns.push_back(std::move(col));
+  }
+  auto out = std::make_shared<Table>(defs, TableType::Data);
+  ChunkColumns cc;
+  for (size_t c = 0; c < defs.size(); ++c) {
+    auto vc = make_value_column(defs[c].data_type, defs[c].nullable);
+    for (const auto& v : columns[c]) vc->append(v);
+    cc.push_back(vc);
+  }
+  out->append_chunk(cc);
+  return out;
+}
+
+std::shared_ptr<Table> aggregate(const std::shared_ptr<const Table>& in, const std::vector<AggregateColumnDefinition>& aggs,
+                                 const std::vector<ColumnID>& groupby) {
+  Assert(!(aggs.empty() && groupby.empty()), "Neither aggregate nor groupby columns have been specified");
+  switch (groupby.size()) {
+    case 0:
+    case 1:
+      return aggregate_impl<uint64_t>(in, aggs, groupby);
+    case 2:
+      return aggregate_impl<std::array<uint64_t, 2>>(in, aggs, groupby);
+    default:
+      return aggregate_impl<std::vector<uint64_t>>(in, aggs, groupby);
+  }
+}
+
+}  // namespace oracle
+
+namespace {
+AllTypeVariant to_variant(const py::handle& o) {
+  if (o.is_none()) return NullValue{};
+  if (py::isinstance<py::int_>(o)) {
+    const auto v = o.cast<long long>();
+    if (v >= INT32_MIN && v <= INT32_MAX) return static_cast<int32_t>(v);
+    return static_cast<int64_t>(v);
+  }
+  if (py::isinstance<py::float_>(o)) return o.cast<double>();
+  if (py::isinstance<py::str>(o)) return o.cast<std::string>();
+  if (py::isinstance<py::tuple>(o) && py::len(o) == 2) {
+    const auto t = o[py::int_(0)].cast<std::string>();
+    const py::handle v = o[py::int_(1)];
+    if (t == "int") return v.cast<int32_t>();
+    if (t == "long") return v.cast<int64_t>();
+    if (t == "float") return v.cast<float>();
+    if (t == "double") return v.cast<double>();
+    if (t == "string") return v.cast<std::string>();
+  }
+  throw std::invalid_argument("cannot convert Python object to AllTypeVariant");
+}
+}  // namespace
+
+PYBIND11_MODULE(_hyrise_oracle, m) {
+  m.doc() = "ORACLE (test infrastructure): CPU restatement of the reference TableScan/JoinHash/Aggregate";
+  m.def("murmur2_int32", [](int32_t v, unsigned seed) { return oracle::murmur2<int32_t>(v, seed); });
+  m.def("murmur2_int64", [](int64_t v, unsigned seed) { return oracle::murmur2<int64_t>(v, seed); });
+  m.def("murmur2_float", [](float v, unsigned seed) { return oracle::murmur2<float>(v, seed); });
+  m.def("murmur2_double", [](double v, unsigned seed) { return oracle::murmur2<double>(v, seed); });
+  m.def("radix_bits", &oracle::radix_bits);
+  m.def("table_scan",
+        [](std::shared_ptr<Table> in, ColumnID col, PredicateCondition cond, py::object value,
+           std::vector<ChunkID> excluded) {
+          py::gil_scoped_release rel;
+          return oracle::table_scan(in, col, cond, to_variant(value), excluded);
+        },
+        py::arg("table"), py::arg("column_id"), py::arg("predicate_condition"), py::arg("value"),
+        py::arg("excluded_chunk_ids") = std::vector<ChunkID>{});
+  m.def("join_hash",
+        [](std::shared_ptr<Table> l, std::shared_ptr<Table> r, JoinMode mode, std::pair<ColumnID, ColumnID> cols) {
+          py::gil_scoped_release rel;
+          return oracle::join_hash(l, r, mode, cols);
+        });
+  m.def("aggregate", [](std::shared_ptr<Table> in, std::vector<AggregateColumnDefinition> aggs,
+                        std::vector<ColumnID> groupby) {
+    py::gil_scoped_release rel;
+    return oracle::aggregate(in, aggs, groupby);
+  });
+}

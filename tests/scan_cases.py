@@ -1,0 +1,114 @@
+"""TableScan cases of the reference's src/test/operators/table_scan_test.cpp (expected column-1 multisets copied
+from the test's inline vectors), shared by the oracle tests (CPU) and the device parity tests (GPU)."""
+from helpers import tbl, wrap
+
+ENCODINGS = ["Unencoded", "Dictionary"]
+
+
+def int_int_tables(hy, encoding):
+    """_int_int_compressed (chunk 7, chunks 0,1 encoded) and _int_int_partly_compressed (chunk 5, chunks 0,1)."""
+    t7 = hy.load_table(tbl("int_int_shuffled.tbl"), 7)
+    t5 = hy.load_table(tbl("int_int_shuffled_2.tbl"), 5)
+    enc = getattr(hy.EncodingType, encoding)
+    hy.encode_chunks(t7, [0, 1], enc)
+    hy.encode_chunks(t5, [0, 1], enc)
+    return wrap(hy, t7), wrap(hy, t5)
+
+
+def filtered_table(hy, partly):
+    """get_table_op_filtered: a reference table with a 'weird' PosList over the partly compressed table."""
+    t = hy.Table([("a", hy.DataType.Int, False), ("b", hy.DataType.Int, False)], hy.TableType.References, 5)
+    src = partly.get_output()
+    pl = [[2, 0], [1, 1], [1, 3], [0, 2], [2, 2], [0, 0], [0, 4]]
+    t.append_chunk([hy.ReferenceColumn(src, 0, pl), hy.ReferenceColumn(src, 1, pl)])
+    return wrap(hy, t)
+
+
+def to_referencing_table(hy, table):
+    pl = []
+    for c in range(table.chunk_count()):
+        for o in range(table.get_chunk(c).size()):
+            pl.append([c, o])
+    defs = [(n, t, False) for (n, t, _) in table.column_definitions()]
+    out = hy.Table(defs, hy.TableType.References)
+    out.append_chunk([hy.ReferenceColumn(table, c, pl) for c in range(table.column_count())])
+    return out
+
+
+C = None  # filled lazily with PredicateCondition names
+
+
+def compressed_column_cases():
+    # ScanOnCompressedColumn (table_scan_test.cpp:226-268), column a vs 6
+    return {
+        "Equals": [106, 106],
+        "NotEquals": [100, 102, 104, 108, 110, 112, 100, 102, 104, 108, 110, 112],
+        "LessThan": [100, 102, 104, 100, 102, 104],
+        "LessThanEquals": [100, 102, 104, 106, 100, 102, 104, 106],
+        "GreaterThan": [108, 110, 112, 108, 110, 112],
+        "GreaterThanEquals": [106, 108, 110, 112, 106, 108, 110, 112],
+    }
+
+
+def referenced_compressed_cases():
+    # ScanOnReferencedCompressedColumn (:269-305): scan1 b < 108, then a OP 4
+    return {
+        "Equals": [104, 104],
+        "NotEquals": [100, 102, 106, 100, 102, 106],
+        "LessThan": [100, 102, 100, 102],
+        "LessThanEquals": [100, 102, 104, 100, 102, 104],
+        "GreaterThan": [106, 106],
+        "GreaterThanEquals": [104, 106, 104, 106],
+    }
+
+
+def weird_pos_list_cases():
+    # ScanWeirdPosList (:312-331): column a vs 10
+    return {
+        "Equals": [110, 110],
+        "NotEquals": [100, 102, 106, 108, 112],
+        "LessThan": [100, 102, 106, 108],
+        "LessThanEquals": [100, 102, 106, 108, 110, 110],
+        "GreaterThan": [112],
+        "GreaterThanEquals": [110, 110, 112],
+    }
+
+
+ALL_ROWS = [100, 102, 104, 106, 108, 110, 112, 100, 102, 104, 106, 108, 110, 112]
+
+
+def greater_than_max_cases():  # :333-357, value 30
+    return {"Equals": [], "NotEquals": ALL_ROWS, "LessThan": ALL_ROWS, "LessThanEquals": ALL_ROWS,
+            "GreaterThan": [], "GreaterThanEquals": []}
+
+
+def less_than_min_cases():  # :359-381, value -10
+    return {"Equals": [], "NotEquals": ALL_ROWS, "LessThan": [], "LessThanEquals": [], "GreaterThan": ALL_ROWS,
+            "GreaterThanEquals": ALL_ROWS}
+
+
+def around_bounds_cases():  # ScanOnCompressedColumnAroundBounds, value 0
+    return {
+        "Equals": [100, 100],
+        "LessThan": [],
+        "LessThanEquals": [100, 100],
+        "GreaterThan": [102, 104, 106, 108, 110, 112, 102, 104, 106, 108, 110, 112],
+        "GreaterThanEquals": ALL_ROWS,
+        "NotEquals": [102, 104, 106, 108, 110, 112, 102, 104, 106, 108, 110, 112],
+    }
+
+
+def column_values(table, column_id):
+    out = []
+    for c in range(table.chunk_count()):
+        out.extend(table.get_chunk(c).get_column(column_id).values())
+    return out
+
+
+def dict_n_entries(hy, n, encoding):
+    """get_table_op_with_n_dict_entries: 0..n in one chunk."""
+    t = hy.Table([("a", hy.DataType.Int, False)], hy.TableType.Data)
+    for i in range(n + 1):
+        t.append([i])
+    hy.encode_chunks(t, [0], getattr(hy.EncodingType, encoding))
+    return wrap(hy, t)

@@ -1,0 +1,137 @@
+"""Device TableScan parity: bit-exact PosLists against the oracle on the reference's test setups and on seeded
+synthetic tables (all widths, NULLs, ragged chunks, reference inputs)."""
+import numpy as np
+import pytest
+
+import scan_cases as sc
+from helpers import assert_identical, assert_table_eq_unordered, tbl, wrap
+
+pytestmark = pytest.mark.gpu
+
+CONDS = ["Equals", "NotEquals", "LessThan", "LessThanEquals", "GreaterThan", "GreaterThanEquals"]
+
+
+def device_scan(hy, op, col, cond, value, excluded=None):
+    s = hy.TableScan(op, col, getattr(hy.PredicateCondition, cond), value)
+    if excluded:
+        s.set_excluded_chunk_ids(excluded)
+    s.execute()
+    return s
+
+
+def check(hy, oracle, op, col, cond, value, excluded=None):
+    s = device_scan(hy, op, col, cond, value, excluded)
+    exp = oracle.table_scan(op.get_output(), col, getattr(hy.PredicateCondition, cond), value, excluded or [])
+    assert_identical(s.get_output(), exp)
+    return s
+
+
+@pytest.mark.parametrize("encoding", sc.ENCODINGS)
+@pytest.mark.parametrize(
+    "cases,value",
+    [(sc.compressed_column_cases, 6), (sc.greater_than_max_cases, 30), (sc.less_than_min_cases, -10),
+     (sc.around_bounds_cases, 0)],
+)
+def test_scan_on_compressed_column(hy, oracle, encoding, cases, value):
+    full, partly = sc.int_int_tables(hy, encoding)
+    for cond, expected in cases().items():
+        for w in (full, partly):
+            s = check(hy, oracle, w, 0, cond, value)
+            assert sorted(sc.column_values(s.get_output(), 1)) == sorted(expected)
+
+
+@pytest.mark.parametrize("encoding", sc.ENCODINGS)
+def test_scan_on_referenced_compressed_column(hy, oracle, encoding):
+    full, partly = sc.int_int_tables(hy, encoding)
+    for cond, expected in sc.referenced_compressed_cases().items():
+        for w in (full, partly):
+            s1 = device_scan(hy, w, 1, "LessThan", 108)
+            s2 = check(hy, oracle, s1, 0, cond, 4)
+            assert sorted(sc.column_values(s2.get_output(), 1)) == sorted(expected)
+
+
+@pytest.mark.parametrize("encoding", sc.ENCODINGS)
+def test_scan_weird_pos_list(hy, oracle, encoding):
+    _, partly = sc.int_int_tables(hy, encoding)
+    w = sc.filtered_table(hy, partly)
+    for cond, expected in sc.weird_pos_list_cases().items():
+        s = check(hy, oracle, w, 0, cond, 10)
+        assert sorted(sc.column_values(s.get_output(), 1)) == sorted(expected)
+
+
+def test_double_scan_and_empty(hy, oracle):
+    w = wrap(hy, hy.load_table(tbl("int_float.tbl"), 2))
+    s1 = check(hy, oracle, w, 0, "GreaterThanEquals", 1234)
+    s2 = check(hy, oracle, s1, 1, "LessThan", 457.9)
+    assert_table_eq_unordered(s2.get_output(), hy.load_table(tbl("int_float_filtered.tbl"), 2))
+    e1 = check(hy, oracle, w, 0, "GreaterThan", 12345)
+    assert e1.get_output().row_count() == 0
+    e2 = check(hy, oracle, e1, 1, "Equals", 456.7)
+    assert e2.get_output().row_count() == 0
+
+
+def test_wide_dictionaries(hy, oracle):
+    w16 = sc.dict_n_entries(hy, (1 << 8) + 1, "Dictionary")
+    assert check(hy, oracle, w16, 0, "GreaterThan", 200).get_output().row_count() == 57
+    w32 = sc.dict_n_entries(hy, (1 << 16) + 1, "Dictionary")
+    assert check(hy, oracle, w32, 0, "GreaterThan", 65500).get_output().row_count() == 37
+
+
+def test_between_and_null_constant(hy, oracle):
+    w = wrap(hy, hy.load_table(tbl("int_int_w_null_8_rows.tbl"), 4))
+    with pytest.raises(RuntimeError):
+        device_scan(hy, w, 0, "Between", 6)
+    for cond in CONDS:
+        assert device_scan(hy, w, 1, cond, None).get_output().row_count() == 0
+
+
+def test_nullable_columns_all_predicates(hy, oracle):
+    for enc in (None, "Dictionary"):
+        t = hy.load_table(tbl("int_int_w_null_8_rows.tbl"), 4)
+        if enc:
+            hy.encode_all_chunks(t, hy.EncodingType.Dictionary)
+        w = wrap(hy, t)
+        for cond in CONDS:
+            for v in (12, 123, 1234, 0, 99999):
+                check(hy, oracle, w, 0, cond, v)
+                check(hy, oracle, w, 1, cond, v)
+        ref = wrap(hy, sc.to_referencing_table(hy, t))
+        for cond in CONDS:
+            check(hy, oracle, ref, 1, cond, 123)
+
+
+def synthetic(hy, rng, n, chunk, dtype, distinct, null_frac, encode):
+    dt = {"int": hy.DataType.Int, "long": hy.DataType.Long, "float": hy.DataType.Float,
+          "double": hy.DataType.Double}[dtype]
+    npt = {"int": np.int32, "long": np.int64, "float": np.float32, "double": np.float64}[dtype]
+    vals = rng.integers(0, distinct, n).astype(npt)
+    if dtype in ("float", "double"):
+        vals = (vals * 0.25).astype(npt)
+    nulls = (rng.random(n) < null_frac).astype(np.uint8) if null_frac else None
+    t = hy.Table.from_arrays([("a", dt, nulls is not None), ("b", hy.DataType.Int, False)],
+                             [vals, np.arange(n, dtype=np.int32)], [nulls, None], chunk)
+    if encode:
+        hy.encode_all_chunks(t, hy.EncodingType.Dictionary)
+    return t
+
+
+@pytest.mark.parametrize("dtype", ["int", "long", "float", "double"])
+@pytest.mark.parametrize("encode", [False, True])
+def test_synthetic_scans(hy, oracle, dtype, encode):
+    rng = np.random.default_rng(0x48595249)
+    # ragged chunk size (not a multiple of 16) exercises tail tiles; distinct counts hit u8 / u16 / u32 widths
+    for n, chunk, distinct in ((50_000, 10_007, 50), (70_000, 65_536, 300), (140_000, 70_000, 70_000)):
+        t = synthetic(hy, rng, n, chunk, dtype, distinct, 0.05, encode)
+        w = wrap(hy, t)
+        for cond in CONDS:
+            v = distinct // 3 if dtype in ("int", "long") else (distinct // 3) * 0.25
+            check(hy, oracle, w, 0, cond, v)
+        check(hy, oracle, w, 0, "LessThan", v, excluded=[1])
+
+
+def test_scan_then_reference_scan_large(hy, oracle):
+    rng = np.random.default_rng(7)
+    t = synthetic(hy, rng, 300_000, 100_000, "int", 50, 0.0, True)
+    w = wrap(hy, t)
+    s1 = check(hy, oracle, w, 0, "LessThan", 24)
+    check(hy, oracle, s1, 1, "GreaterThanEquals", 150_000)
