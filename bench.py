@@ -1,0 +1,300 @@
+"""Headline benchmark: rows/s of TableScan + JoinHash on TPC-H-shaped lineitem ⋈ orders (BASELINE.json metric).
+
+One step = the reference's query shape, on data already resident in HBM:
+    TableScan(lineitem, l_quantity < 24)            dictionary-encoded u8 attribute vectors, 100k-row chunks
+    JoinHash(orders, <scan output>, o_orderkey = l_orderkey, Inner)   orders builds (smaller side), the scan's
+                                                                       reference table probes
+Rows per step = |lineitem| + |orders| (base-table rows consumed). Everything runs through the C-ABI
+(include/hyrise_amd.h) on buffers owned by torch (device memory only; the C-ABI never sees a torch type).
+
+Multi-GPU (torchrun, one process per GPU): weak scaling. Rank r generates the r-th shard of an SF·N database
+(orders r*n..(r+1)*n and their lineitems), so lineitem and orders are co-partitioned by o_orderkey range and the join
+needs no exchange; the shards' outputs are the reference's per-partition output chunks, concatenated in rank order.
+"""
+import argparse
+import ctypes
+import importlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--sf", type=float, default=100.0, help="TPC-H scale factor per GPU")
+    p.add_argument("--chunk", type=int, default=100_000)
+    p.add_argument("--cpu-sf", type=float, default=20.0, help="scale factor of the bounded CPU-baseline sample")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+
+    hy = importlib.import_module("hyrise-1_amd")
+    synth = importlib.import_module("hyrise-1_amd.synth")
+    capi = hy.capi
+    L = capi.lib
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    capi.check(L.hy_set_device(dev.index), "hy_set_device")
+    stream = torch.cuda.current_stream().cuda_stream
+    chunk = args.chunk
+
+    # ---------------- data (resident in HBM before timing) ----------------
+    n_ord = synth.n_orders(args.sf)
+    first_order = rank * n_ord
+    okey, lines = synth.orders_torch(args.sf, dev, first_order=first_order)
+    # first lineitem row of this shard (not needed for values beyond the quantity stream): use order-based offset
+    lkey, qty = synth.lineitem_torch(okey, lines, first_row=first_order * 4)
+    del lines
+    n_li = lkey.numel()
+    vids, present = synth.dictionary_encode_small_domain(qty, chunk, 50)
+    del qty
+    present_h = present.cpu().numpy()
+    n_lchunks = (n_li + chunk - 1) // chunk
+    n_ochunks = (n_ord + chunk - 1) // chunk
+    # pad buffers so 16-byte vector loads of the last chunk stay in bounds
+    def padded(t, mult=64):
+        extra = (-t.numel()) % mult
+        return torch.cat([t, torch.zeros(extra, dtype=t.dtype, device=t.device)]) if extra else t
+
+    vids = padded(vids.contiguous())
+    lkey = padded(lkey.contiguous())
+    okey = padded(okey.contiguous())
+    torch.cuda.synchronize()
+
+    # ---------------- scan descriptors: l_quantity < 24 on dictionary chunks ----------------
+    # search value id = lower_bound(dictionary, 24) = number of distinct values < 24 in the chunk
+    # (single_column_table_scan_impl.cpp:145-205: LessThan -> all if INVALID, none if 0, else vid < svid)
+    scan_chunks = (capi.ScanChunk * n_lchunks)()
+    for c in range(n_lchunks):
+        size = min(chunk, n_li - c * chunk)
+        dsize = int(present_h[c].sum())
+        svid = int(present_h[c, :23].sum())
+        sc = scan_chunks[c]
+        sc.column.data = vids.data_ptr() + c * chunk
+        sc.column.size = size
+        sc.column.dictionary_size = dsize
+        sc.column.kind = capi.HY_COL_DICT
+        sc.column.vid_width = 1
+        sc.search_vid = svid
+        sc.op = capi.HY_OP_ALL if svid >= dsize else (capi.HY_OP_NONE if svid == 0 else capi.HY_OP_LT)
+        sc.out_begin = c * chunk
+    sizes = (ctypes.c_uint32 * n_lchunks)(*[min(chunk, n_li - c * chunk) for c in range(n_lchunks)])
+    chunk_ids = (ctypes.c_uint32 * n_lchunks)(*range(n_lchunks))
+    ws_bytes = ctypes.c_size_t(0)
+    capi.check(L.hy_table_scan_workspace_size(sizes, n_lchunks, ctypes.byref(ws_bytes)), "scan ws")
+    scan_ws = torch.empty(ws_bytes.value, dtype=torch.uint8, device=dev)
+    scan_rows = torch.empty(n_li * 2 + 64, dtype=torch.int32, device=dev)  # RowIDs (2 x u32)
+    scan_counts = torch.empty(n_lchunks, dtype=torch.int32, device=dev)
+    L.hy_table_scan_row_ids.restype = ctypes.c_int
+    L.hy_table_scan_row_ids.argtypes = [ctypes.POINTER(capi.ScanChunk), ctypes.c_uint32, ctypes.c_int32,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+
+    def run_scan():
+        capi.check(L.hy_table_scan_row_ids(scan_chunks, n_lchunks, capi.HY_TYPE_FLOAT, None, chunk_ids,
+                                           scan_rows.data_ptr(), scan_counts.data_ptr(), scan_ws.data_ptr(),
+                                           ws_bytes.value, stream), "hy_table_scan_row_ids")
+
+    # ---------------- join descriptors ----------------
+    build_chunks = (capi.JoinChunk * n_ochunks)()
+    for c in range(n_ochunks):
+        size = min(chunk, n_ord - c * chunk)
+        b = build_chunks[c]
+        b.column.data = okey.data_ptr() + 4 * c * chunk
+        b.column.size = size
+        b.column.kind = capi.HY_COL_VALUE
+        b.size = size
+        b.chunk_id = c
+    referenced = (capi.ColumnChunk * n_lchunks)()
+    for c in range(n_lchunks):
+        r = referenced[c]
+        r.data = lkey.data_ptr() + 4 * c * chunk
+        r.size = min(chunk, n_li - c * chunk)
+        r.kind = capi.HY_COL_VALUE
+    build_side = capi.JoinSide(build_chunks, n_ochunks, capi.HY_TYPE_INT32, None, 0, 0)
+    radix_bits = L.hy_join_radix_bits(n_ord, 4)
+    params = capi.JoinParams(capi.HY_JOIN_INNER, capi.HY_TYPE_INT32, radix_bits, 17)
+    n_parts = 1 << radix_bits
+    part_begin = torch.empty(n_parts, dtype=torch.int64, device=dev)
+    part_count = torch.empty(n_parts, dtype=torch.int32, device=dev)
+    state = {}
+
+    def probe_side_from_counts(counts_h):
+        nz = [c for c in range(n_lchunks) if counts_h[c] > 0]
+        pchunks = (capi.JoinChunk * len(nz))()
+        for k, c in enumerate(nz):
+            pc = pchunks[k]
+            pc.pos_list = scan_rows.data_ptr() + 8 * c * chunk
+            pc.size = int(counts_h[c])
+            pc.chunk_id = k
+        side = capi.JoinSide(pchunks, len(nz), capi.HY_TYPE_INT32, referenced, n_lchunks, 1)
+        return side, pchunks, int(sum(counts_h[c] for c in nz))
+
+    def run_join(counts_h):
+        side, keep, n_probe = probe_side_from_counts(counts_h)
+        if "ws" not in state:
+            wsb = ctypes.c_size_t(0)
+            capi.check(L.hy_join_hash_workspace_size(ctypes.byref(build_side), ctypes.byref(side),
+                                                     ctypes.byref(params), ctypes.byref(wsb)), "join ws")
+            state["ws"] = torch.empty(wsb.value, dtype=torch.uint8, device=dev)
+            state["out_b"] = torch.empty(2 * n_probe + 64, dtype=torch.int32, device=dev)
+            state["out_p"] = torch.empty(2 * n_probe + 64, dtype=torch.int32, device=dev)
+            state["cap"] = n_probe
+        res = capi.JoinResult()
+        capi.check(L.hy_join_hash(ctypes.byref(build_side), ctypes.byref(side), ctypes.byref(params),
+                                  state["out_b"].data_ptr(), state["out_p"].data_ptr(), state["cap"],
+                                  part_begin.data_ptr(), part_count.data_ptr(), ctypes.byref(res),
+                                  state["ws"].data_ptr(), state["ws"].numel(), stream), "hy_join_hash")
+        return n_probe, res.total_pairs
+
+    def step():
+        run_scan()
+        counts_h = scan_counts.cpu().numpy()  # D2H of per-chunk match counts (the output chunk layout)
+        return run_join(counts_h)
+
+    for _ in range(args.warmup):
+        n_probe, pairs = step()
+    torch.cuda.synchronize()
+
+    # ---------------- timed region ----------------
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    L.hy_kernel_stats_reset()
+    L.hy_kernel_stats_enable(1)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        n_probe, pairs = step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    L.hy_kernel_stats_enable(0)
+    if dist:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # ---------------- per-kernel device time (HIP events on the launch stream) ----------------
+    nk = ctypes.c_uint32(0)
+    L.hy_kernel_stats_collect(ctypes.byref(nk))
+    L.hy_kernel_stats_get.argtypes = [ctypes.c_uint32, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_uint64),
+                                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]
+    kernels = {}
+    for i in range(nk.value):
+        name, launches, total, units = ctypes.c_char_p(), ctypes.c_uint64(), ctypes.c_double(), ctypes.c_uint64()
+        L.hy_kernel_stats_get(i, ctypes.byref(name), ctypes.byref(launches), ctypes.byref(total), ctypes.byref(units))
+        kernels[name.value.decode()] = {"launches": launches.value, "ms_total": total.value}
+
+    K = args.steps
+    rows_per_step = n_li + n_ord
+    # algorithmic bytes per step for each kernel; 8-byte {key, payload} partition records
+    valid_build, valid_probe = n_ord, n_probe
+    alg = {
+        "scan_dict": n_li * 1 + n_probe * 8,
+        "part1_hist": valid_build * 4 + valid_probe * (8 + 4),
+        "part1_scatter": valid_build * (4 + 8) + valid_probe * (8 + 4 + 8),
+        "part2_hist": (valid_build + valid_probe) * 8,
+        "part2_scatter": (valid_build + valid_probe) * 16,
+        "join_partition": (valid_build + valid_probe) * 8 + pairs * 16,
+    }
+    for k, v in kernels.items():
+        per_launch_ms = v["ms_total"] / max(v["launches"], 1)
+        v["ms_per_launch"] = per_launch_ms
+        if k in alg:
+            launches_per_step = v["launches"] / K
+            v["alg_bytes_per_launch"] = alg[k] / launches_per_step
+            v["achieved_GBps"] = v["alg_bytes_per_launch"] / (per_launch_ms * 1e-3) / 1e9
+    dom = max((k for k in kernels if k in alg), key=lambda k: kernels[k]["ms_total"])
+    dk = kernels[dom]
+    roofline = {"bound": "hbm", "kernel": dom, "achieved": round(dk["achieved_GBps"], 1), "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": round(dk["achieved_GBps"] / HBM_PEAK_GBPS, 4), "traffic": None}
+    step_s = elapsed / K
+    # end-to-end algorithmic bytes (§8(d)): scan 1 B/row + 8 B/match; join 4 B/build + 4 B/probe + 16 B/pair
+    e2e_bytes = n_li * 1 + n_probe * 8 + n_ord * 4 + n_probe * 4 + pairs * 16
+    value = rows_per_step * world / step_s
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(hy, synth, args.cpu_sf, chunk)
+
+    if rank == 0:
+        line = {
+            "metric": "rows/sec TableScan+JoinHash, TPC-H SF100 lineitem⋈orders, 1/2/4/8 MI355X",
+            "value": round(value, 1),
+            "unit": "rows/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": round(step_s * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic (seeded counter-based TPC-H-shaped columns, resident in HBM)",
+            "config": {"workload": f"TableScan(l_quantity<24, dictionary u8) -> JoinHash(orders ⋈ scan, "
+                                   f"o_orderkey=l_orderkey, radix_bits={radix_bits})",
+                       "sf_per_gpu": args.sf, "lineitem_rows": n_li, "orders_rows": n_ord, "chunk_size": chunk,
+                       "scan_matches": n_probe, "join_pairs": int(pairs), "parallelism": f"chunk-sharded x{world}"},
+            "roofline": roofline,
+            "end_to_end": {"alg_bytes_per_step": e2e_bytes, "GBps": round(e2e_bytes / step_s / 1e9, 1),
+                           "frac_of_peak": round(e2e_bytes / step_s / 1e9 / HBM_PEAK_GBPS, 4)},
+            "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
+                        for k, v in kernels.items()},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    if dist:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(hy, synth, sf, chunk):
+    """The oracle (CPU restatement of the reference operators, single thread) on a bounded sample of the same
+    workload: TableScan(l_quantity < 24) on dictionary-encoded lineitem, then JoinHash(orders, scan output)."""
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import helpers
+
+    oracle = helpers.load_oracle()
+    okey, lines = synth.orders_numpy(sf)
+    lkey, qty = synth.lineitem_numpy(okey, lines)
+    orders = hy.Table.from_arrays([("o_orderkey", hy.DataType.Int, False)], [okey], [], chunk)
+    lineitem = hy.Table.from_arrays([("l_orderkey", hy.DataType.Int, False), ("l_quantity", hy.DataType.Float, False)],
+                                    [lkey, qty.astype(np.float32)], [], chunk)
+    hy.encode_all_chunks(lineitem, hy.EncodingType.Dictionary)
+    t0 = time.perf_counter()
+    scan = oracle.table_scan(lineitem, 1, hy.PredicateCondition.LessThan, 24, [])
+    join, _bits = oracle.join_hash(orders, scan, hy.JoinMode.Inner, (0, 0))
+    dt = time.perf_counter() - t0
+    rows = lineitem.row_count() + orders.row_count()
+    return {"value": round(rows / dt, 1), "unit": "rows/s", "cores": 1, "kind": "port",
+            "sample": f"SF{sf}: {lineitem.row_count()} lineitem + {orders.row_count()} orders rows, "
+                      f"scan {scan.row_count()} matches, join {join.row_count()} pairs, {dt:.2f} s"}
+
+
+if __name__ == "__main__":
+    main()

@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <mutex>
 #include <vector>
 
 #include "hyrise_amd.h"
@@ -47,6 +48,58 @@ struct Carver {
     used += count * sizeof(T);
     if (base && used > cap) ok = false;
     return p;
+  }
+};
+
+// ---- per-kernel timing (HIP events on the launching stream), enabled by hy_kernel_stats_enable ----
+struct KernelTiming {
+  std::string name;
+  hipEvent_t start, stop;
+  uint64_t units;
+};
+std::mutex g_kt_mutex;
+bool g_kt_enabled = false;
+std::vector<KernelTiming> g_kt_pending;
+std::vector<hipEvent_t> g_kt_pool;
+struct KStat {
+  uint64_t count = 0;
+  double total_ms = 0;
+  uint64_t units = 0;
+};
+std::vector<std::pair<std::string, KStat>> g_kt_stats;
+
+hipEvent_t kt_event() {
+  if (!g_kt_pool.empty()) {
+    hipEvent_t e = g_kt_pool.back();
+    g_kt_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  hipEventCreate(&e);
+  return e;
+}
+
+// Brackets one kernel launch: KTimer t("name", stream, units); launch; t.done();
+struct KTimer {
+  bool on;
+  KernelTiming kt;
+  hipStream_t s;
+  KTimer(const char* name, hipStream_t stream, uint64_t units) : on(false), s(stream) {
+    std::lock_guard<std::mutex> lock(g_kt_mutex);
+    if (!g_kt_enabled) return;
+    on = true;
+    kt.name = name;
+    kt.units = units;
+    kt.start = kt_event();
+    kt.stop = kt_event();
+    hipEventRecord(kt.start, s);
+  }
+  void done() {
+    if (!on) return;
+    hipEventRecord(kt.stop, s);
+    std::lock_guard<std::mutex> lock(g_kt_mutex);
+    g_kt_pending.push_back(kt);
+    on = false;
   }
 };
 
@@ -127,6 +180,58 @@ hy_status hy_stream_synchronize(hy_stream_t stream) {
 
 const char* hy_last_error_message(void) { return g_last_error.c_str(); }
 
+hy_status hy_kernel_stats_enable(int enable) {
+  std::lock_guard<std::mutex> lock(g_kt_mutex);
+  g_kt_enabled = enable != 0;
+  return HY_OK;
+}
+
+hy_status hy_kernel_stats_reset(void) {
+  std::lock_guard<std::mutex> lock(g_kt_mutex);
+  for (auto& k : g_kt_pending) {
+    hipEventSynchronize(k.stop);
+    g_kt_pool.push_back(k.start);
+    g_kt_pool.push_back(k.stop);
+  }
+  g_kt_pending.clear();
+  g_kt_stats.clear();
+  return HY_OK;
+}
+
+// Resolves all recorded launches (waits for them) and returns the number of distinct kernels.
+hy_status hy_kernel_stats_collect(uint32_t* n_kernels) {
+  std::lock_guard<std::mutex> lock(g_kt_mutex);
+  for (auto& k : g_kt_pending) {
+    HY_HIP(hipEventSynchronize(k.stop));
+    float ms = 0;
+    HY_HIP(hipEventElapsedTime(&ms, k.start, k.stop));
+    auto it = std::find_if(g_kt_stats.begin(), g_kt_stats.end(), [&](const auto& e) { return e.first == k.name; });
+    if (it == g_kt_stats.end()) {
+      g_kt_stats.emplace_back(k.name, KStat{});
+      it = g_kt_stats.end() - 1;
+    }
+    it->second.count += 1;
+    it->second.total_ms += ms;
+    it->second.units += k.units;
+    g_kt_pool.push_back(k.start);
+    g_kt_pool.push_back(k.stop);
+  }
+  g_kt_pending.clear();
+  if (n_kernels) *n_kernels = static_cast<uint32_t>(g_kt_stats.size());
+  return HY_OK;
+}
+
+hy_status hy_kernel_stats_get(uint32_t index, const char** name, uint64_t* launches, double* total_ms,
+                              uint64_t* units) {
+  std::lock_guard<std::mutex> lock(g_kt_mutex);
+  if (index >= g_kt_stats.size()) return fail(HY_ERR_INVALID_ARGUMENT, "kernel stats index");
+  *name = g_kt_stats[index].first.c_str();
+  *launches = g_kt_stats[index].second.count;
+  *total_ms = g_kt_stats[index].second.total_ms;
+  *units = g_kt_stats[index].second.units;
+  return HY_OK;
+}
+
 const char* hy_build_info(void) { return "hyrise-amd gfx950 (CDNA4) HIP kernels: table_scan, reference_scan, join_hash"; }
 
 }  // extern "C"
@@ -153,13 +258,15 @@ int scan_class(const hy_scan_chunk& c) {
 
 uint64_t scan_tiles(uint32_t size) { return (uint64_t(size) + hyk::SCAN_TILE - 1) / hyk::SCAN_TILE; }
 
-template <typename E, bool DICT>
-hy_status launch_scan(const hyk::ScanLaunchDesc& d, const void* constant, uint32_t* out, uint32_t* counts,
+template <typename E, bool DICT, bool OUT_ROWID>
+hy_status launch_scan(const hyk::ScanLaunchDesc& d, const void* constant, void* out, uint32_t* counts,
                       hipStream_t s) {
   hyk::ScanConst<E> c{};
   if (!DICT && constant) std::memcpy(&c.value, constant, sizeof(E));
-  hipLaunchKernelGGL((hyk::scan_kernel<E, DICT>), dim3(static_cast<uint32_t>(d.n_tiles)), dim3(hyk::SCAN_THREADS), 0,
-                     s, d, c, out, counts);
+  KTimer t(DICT ? "scan_dict" : "scan_value", s, d.n_rows);
+  hipLaunchKernelGGL((hyk::scan_kernel<E, DICT, OUT_ROWID>), dim3(static_cast<uint32_t>(d.n_tiles)),
+                     dim3(hyk::SCAN_THREADS), 0, s, d, c, out, counts);
+  t.done();
   HY_HIP(hipGetLastError());
   return HY_OK;
 }
@@ -169,6 +276,7 @@ size_t scan_class_bytes(uint32_t n_chunks, uint64_t n_tiles) {
   Carver cv{nullptr, 0};
   cv.take<hy_scan_chunk>(n_chunks);
   cv.take<uint64_t>(n_chunks + 1);
+  cv.take<uint32_t>(n_chunks);
   cv.take<uint32_t>(n_chunks);
   cv.take<uint64_t>(n_tiles + 1);
   cv.take<uint32_t>(64);
@@ -188,9 +296,13 @@ hy_status hy_table_scan_workspace_size(const uint32_t* chunk_sizes, uint32_t n_c
   return HY_OK;
 }
 
-hy_status hy_table_scan(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_t value_type, const void* constant,
-                        uint32_t* out_offsets, uint32_t* counts, void* workspace, size_t workspace_bytes,
-                        hy_stream_t stream) {
+}  // extern "C"
+
+namespace {
+template <bool OUT_ROWID>
+hy_status table_scan_impl(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_t value_type, const void* constant,
+                          void* out_offsets, uint32_t* counts, const uint32_t* chunk_ids, void* workspace,
+                          size_t workspace_bytes, hy_stream_t stream) {
   if (n_chunks == 0) return HY_OK;
   if (!chunks || !out_offsets || !counts) return fail(HY_ERR_INVALID_ARGUMENT, "null argument");
   hipStream_t s = S(stream);
@@ -214,6 +326,7 @@ hy_status hy_table_scan(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_t 
   // host staging must outlive the async copies: keep everything until the stream is synchronized below
   std::vector<std::vector<hy_scan_chunk>> h_chunks(SC_COUNT);
   std::vector<std::vector<uint64_t>> h_tiles(SC_COUNT);
+  std::vector<std::vector<uint32_t>> h_cids(SC_COUNT);
   uint32_t* error = nullptr;
   for (int cls = 0; cls < SC_COUNT; ++cls) {
     const auto& idx = by_class[cls];
@@ -223,9 +336,10 @@ hy_status hy_table_scan(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_t 
     auto& ht = h_tiles[cls];
     hc.resize(nc);
     ht.resize(nc + 1);
-    uint64_t run = 0;
+    uint64_t run = 0, rows = 0;
     for (uint32_t k = 0; k < nc; ++k) {
       hc[k] = chunks[idx[k]];
+      rows += hc[k].column.size;
       ht[k] = run;
       run += hc[k].op == HY_OP_NONE ? 0 : scan_tiles(hc[k].column.size);
     }
@@ -234,6 +348,7 @@ hy_status hy_table_scan(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_t 
     auto* dch = cv.take<hy_scan_chunk>(nc);
     auto* dti = cv.take<uint64_t>(nc + 1);
     auto* dix = cv.take<uint32_t>(nc);
+    auto* dcid = cv.take<uint32_t>(nc);
     auto* dst = cv.take<uint64_t>(run + 1);
     auto* dmisc = cv.take<uint32_t>(64);
     if (!cv.ok) return fail(HY_ERR_WORKSPACE, "scan workspace too small");
@@ -244,12 +359,18 @@ hy_status hy_table_scan(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_t 
     HY_HIP(hipMemcpyAsync(dch, hc.data(), sizeof(hy_scan_chunk) * nc, hipMemcpyHostToDevice, s));
     HY_HIP(hipMemcpyAsync(dti, ht.data(), sizeof(uint64_t) * (nc + 1), hipMemcpyHostToDevice, s));
     HY_HIP(hipMemcpyAsync(dix, idx.data(), sizeof(uint32_t) * nc, hipMemcpyHostToDevice, s));
+    auto& hcid = h_cids[cls];
+    hcid.resize(nc);
+    for (uint32_t k = 0; k < nc; ++k) hcid[k] = chunk_ids ? chunk_ids[idx[k]] : idx[k];
+    HY_HIP(hipMemcpyAsync(dcid, hcid.data(), sizeof(uint32_t) * nc, hipMemcpyHostToDevice, s));
     HY_HIP(hipMemsetAsync(dst, 0, sizeof(uint64_t) * (run + 1), s));
     HY_HIP(hipMemsetAsync(dmisc, 0, 4, s));
     if (run == 0) continue;
     d.chunks = dch;
     d.chunk_tile_begin = dti;
     d.chunk_index = dix;
+    d.chunk_ids = dcid;
+    d.n_rows = rows;
     d.n_chunks = nc;
     d.n_tiles = run;
     d.status = dst;
@@ -258,27 +379,27 @@ hy_status hy_table_scan(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_t 
     hy_status st = HY_OK;
     switch (cls) {
       case SC_DICT8:
-        st = launch_scan<uint8_t, true>(d, nullptr, out_offsets, counts, s);
+        st = launch_scan<uint8_t, true, OUT_ROWID>(d, nullptr, out_offsets, counts, s);
         break;
       case SC_DICT16:
-        st = launch_scan<uint16_t, true>(d, nullptr, out_offsets, counts, s);
+        st = launch_scan<uint16_t, true, OUT_ROWID>(d, nullptr, out_offsets, counts, s);
         break;
       case SC_DICT32:
-        st = launch_scan<uint32_t, true>(d, nullptr, out_offsets, counts, s);
+        st = launch_scan<uint32_t, true, OUT_ROWID>(d, nullptr, out_offsets, counts, s);
         break;
       case SC_VALUE:
         switch (value_type) {
           case HY_TYPE_INT32:
-            st = launch_scan<int32_t, false>(d, constant, out_offsets, counts, s);
+            st = launch_scan<int32_t, false, OUT_ROWID>(d, constant, out_offsets, counts, s);
             break;
           case HY_TYPE_INT64:
-            st = launch_scan<int64_t, false>(d, constant, out_offsets, counts, s);
+            st = launch_scan<int64_t, false, OUT_ROWID>(d, constant, out_offsets, counts, s);
             break;
           case HY_TYPE_FLOAT:
-            st = launch_scan<float, false>(d, constant, out_offsets, counts, s);
+            st = launch_scan<float, false, OUT_ROWID>(d, constant, out_offsets, counts, s);
             break;
           case HY_TYPE_DOUBLE:
-            st = launch_scan<double, false>(d, constant, out_offsets, counts, s);
+            st = launch_scan<double, false, OUT_ROWID>(d, constant, out_offsets, counts, s);
             break;
         }
         break;
@@ -292,6 +413,23 @@ hy_status hy_table_scan(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_t 
   HY_HIP(hipStreamSynchronize(s));
   if (herr) return fail(HY_ERR_KERNEL, "scan look-back did not complete");
   return HY_OK;
+}
+}  // namespace
+
+extern "C" {
+
+hy_status hy_table_scan(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_t value_type, const void* constant,
+                        uint32_t* out_offsets, uint32_t* counts, void* workspace, size_t workspace_bytes,
+                        hy_stream_t stream) {
+  return table_scan_impl<false>(chunks, n_chunks, value_type, constant, out_offsets, counts, nullptr, workspace,
+                                workspace_bytes, stream);
+}
+
+hy_status hy_table_scan_row_ids(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_t value_type,
+                                const void* constant, const uint32_t* chunk_ids, hy_row_id* out_rows, uint32_t* counts,
+                                void* workspace, size_t workspace_bytes, hy_stream_t stream) {
+  return table_scan_impl<true>(chunks, n_chunks, value_type, constant, out_rows, counts, chunk_ids, workspace,
+                               workspace_bytes, stream);
 }
 
 hy_status hy_reference_scan_workspace_size(uint64_t pos_list_size, size_t* bytes) {
@@ -594,8 +732,12 @@ hy_status run_scan(const uint32_t* in, uint32_t* out, uint64_t n, const Common& 
   if (tiles + 1 > c.scan_status_words) return fail(HY_ERR_WORKSPACE, "scan status");
   HY_HIP(hipMemsetAsync(c.scan_status, 0, sizeof(uint64_t) * (tiles + 1), s));
   HY_HIP(hipMemsetAsync(c.misc, 0, 4, s));
-  hipLaunchKernelGGL(hyk::exclusive_scan_u32, dim3(static_cast<uint32_t>(tiles)), dim3(hyk::SCAN_T), 0, s, in, out, n,
+  {
+      KTimer kt_("exclusive_scan", s, n);
+      hipLaunchKernelGGL(hyk::exclusive_scan_u32, dim3(static_cast<uint32_t>(tiles)), dim3(hyk::SCAN_T), 0, s, in, out, n,
                      c.scan_status, c.misc, c.misc + 1, total_out);
+      kt_.done();
+    }
   HY_HIP(hipGetLastError());
   return HY_OK;
 }
@@ -622,13 +764,21 @@ hy_status partition_side(const SidePlan& p, const SideBufs<H>& b, const Geometry
   const uint64_t* total_dev = side_total;
   HY_HIP(hipMemsetAsync(side_total, 0, 8, s));
   if (p.n_tiles1 > 0) {
-    hipLaunchKernelGGL((hyk::part1_hist<T, H>), dim3(static_cast<uint32_t>(p.n_tiles1)), dim3(hyk::PART_THREADS), 0, s,
+    {
+      KTimer kt_("part1_hist", s, p.n_rows);
+      hipLaunchKernelGGL((hyk::part1_hist<T, H>), dim3(static_cast<uint32_t>(p.n_tiles1)), dim3(hyk::PART_THREADS), 0, s,
                        sd, d1, g.n_digits1, b.hist1);
+      kt_.done();
+    }
     HY_HIP(hipGetLastError());
     hy_status st = run_scan(b.hist1, b.off1, h1n, c, s, side_total);
     if (st != HY_OK) return st;
-    hipLaunchKernelGGL((hyk::part1_scatter<T, H>), dim3(static_cast<uint32_t>(p.n_tiles1)), dim3(hyk::PART_THREADS), 0,
+    {
+      KTimer kt_("part1_scatter", s, p.n_rows);
+      hipLaunchKernelGGL((hyk::part1_scatter<T, H>), dim3(static_cast<uint32_t>(p.n_tiles1)), dim3(hyk::PART_THREADS), 0,
                        s, sd, d1, dbits1, g.n_digits1, b.off1, b.rec1);
+      kt_.done();
+    }
     HY_HIP(hipGetLastError());
   }
 
@@ -647,13 +797,21 @@ hy_status partition_side(const SidePlan& p, const SideBufs<H>& b, const Geometry
   hyk::Segs sg{b.seg_begin, b.seg_tile_begin, g.n_digits1};
   hyk::Digit d2{mask, 0u, 0xFFu, seed};
   const uint64_t grid2 = b.max_tiles2;
-  hipLaunchKernelGGL((hyk::part2_hist<H>), dim3(static_cast<uint32_t>(grid2)), dim3(hyk::PART_THREADS), 0, s, sg, d2,
+  {
+      KTimer kt_("part2_hist", s, p.n_rows);
+      hipLaunchKernelGGL((hyk::part2_hist<H>), dim3(static_cast<uint32_t>(grid2)), dim3(hyk::PART_THREADS), 0, s, sg, d2,
                      256u, b.rec1, b.hist2);
+      kt_.done();
+    }
   HY_HIP(hipGetLastError());
   hy_status st = run_scan(b.hist2, b.off2, grid2 * 256, c, s);
   if (st != HY_OK) return st;
-  hipLaunchKernelGGL((hyk::part2_scatter<H>), dim3(static_cast<uint32_t>(grid2)), dim3(hyk::PART_THREADS), 0, s, sg,
+  {
+      KTimer kt_("part2_scatter", s, p.n_rows);
+      hipLaunchKernelGGL((hyk::part2_scatter<H>), dim3(static_cast<uint32_t>(grid2)), dim3(hyk::PART_THREADS), 0, s, sg,
                      d2, 8, 256u, b.rec1, b.off2, b.rec2);
+      kt_.done();
+    }
   HY_HIP(hipGetLastError());
   hipLaunchKernelGGL(hyk::bounds_two_pass, dim3((n_parts + 1 + 255) / 256), dim3(256), 0, s, b.off2, b.seg_begin,
                      b.seg_tile_begin, g.n_digits1, 256u, total_dev, b.part_begin);
@@ -722,21 +880,29 @@ hy_status join_typed(const SidePlan& bp, const SidePlan& pp, const hy_join_param
   HY_HIP(hipMemcpyAsync(hb.data(), bb.part_begin, sizeof(uint32_t) * (n_parts + 1), hipMemcpyDeviceToHost, s));
   HY_HIP(hipStreamSynchronize(s));
   uint32_t max_build = 0;
+  uint64_t build_total = hb[n_parts];
   for (uint32_t i = 0; i < n_parts; ++i) max_build = std::max(max_build, hb[i + 1] - hb[i]);
-  uint32_t cap = 64;
-  while (cap < max_build + max_build / 2 + 1) cap <<= 1;
-  const size_t lds = sizeof(hyk::Slot<H>) * cap + 4 * size_t(max_build) + 2 * size_t(cap) * 2 +
-                     2 * size_t(max_build) * 2 + 64;
-  if (max_build > 65535 || lds > 150 * 1024)
+  if (max_build > 65535)
     return fail(HY_ERR_UNSUPPORTED, "build partition of " + std::to_string(max_build) +
-                                        " rows exceeds the LDS hash table (skewed join keys)");
+                                        " rows exceeds 65535 (heavily skewed join keys)");
+  // LDS budget: two 512-thread workgroups per CU; larger (skewed) partitions use a global-memory table
+  constexpr size_t kLdsBudget = 78 * 1024;
+  uint32_t lds_max = max_build;
+  while (lds_max > 0 && hyk::table_bytes<H>(lds_max) > kLdsBudget) lds_max = lds_max * 7 / 8;
+  const size_t lds = hyk::table_bytes<H>(lds_max);
+  void* global_ws = nullptr;
+  if (lds_max < max_build) {
+    const size_t gbytes = build_total * (sizeof(hyk::Slot<H>) * 3 / 2 + 18) + size_t(n_parts) * 64 * sizeof(hyk::Slot<H>) +
+                          hyk::table_bytes<H>(max_build) + 4096;
+    HY_HIP(hipMallocAsync(&global_ws, gbytes, s));
+  }
 
   hyk::JoinDesc jd{};
   jd.build_begin = bb.part_begin;
   jd.probe_begin = pb.part_begin;
   jd.n_parts = n_parts;
-  jd.cap = cap;
-  jd.max_build = std::max<uint32_t>(max_build, 1);
+  jd.lds_max_build = lds_max;
+  jd.global_ws = global_ws;
   jd.mode = prm->mode;
   jd.build_map = bp.fuse ? make_map(bb.ref_row_begin, bp.ref_row_begin) : make_map(bb.row_begin, bp.row_begin);
   jd.probe_map = pp.fuse ? make_map(pb.ref_row_begin, pp.ref_row_begin) : make_map(pb.row_begin, pp.row_begin);
@@ -749,13 +915,18 @@ hy_status join_typed(const SidePlan& bp, const SidePlan& pp, const hy_join_param
   HY_HIP(hipMemsetAsync(c.join_status, 0, sizeof(uint64_t) * n_parts, s));
   HY_HIP(hipMemsetAsync(c.misc, 0, 64 * 4, s));
   HY_HIP(hipMemsetAsync(c.totals, 0, 8 * 2, s));
-  hipLaunchKernelGGL((hyk::join_partition<H>), dim3(n_parts), dim3(hyk::JOIN_THREADS), lds, s, jd, brec, precs,
+  {
+      KTimer kt_("join_partition", s, bp.n_rows + pp.n_rows);
+      hipLaunchKernelGGL((hyk::join_partition<H>), dim3(n_parts), dim3(hyk::JOIN_THREADS), lds, s, jd, brec, precs,
                      out_build, out_probe, partition_begin, partition_counts);
+      kt_.done();
+    }
   HY_HIP(hipGetLastError());
   uint32_t flags[4] = {0, 0, 0, 0};
   uint64_t total = 0;
   HY_HIP(hipMemcpyAsync(flags, c.misc, 16, hipMemcpyDeviceToHost, s));
   HY_HIP(hipMemcpyAsync(&total, c.totals + 1, 8, hipMemcpyDeviceToHost, s));
+  if (global_ws) HY_HIP(hipFreeAsync(global_ws, s));
   HY_HIP(hipStreamSynchronize(s));
   if (flags[1]) return fail(HY_ERR_KERNEL, "join look-back did not complete");
   if (result) {

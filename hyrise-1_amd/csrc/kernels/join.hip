@@ -89,8 +89,11 @@ struct Side {
   int32_t keep_nulls;
 };
 
+// NULL rows: a ValueColumn read directly yields its stored value (value_column_iterable), a dictionary column and
+// any row reached through a ReferenceColumn yield T{} (dictionary_column_iterable.hpp:80,
+// reference_column_iterable.hpp:60-86). The value only matters for outer joins, which keep NULL probe rows.
 template <typename T>
-__device__ __forceinline__ bool read_column_value(const SrcChunk& c, uint32_t off, T* v) {
+__device__ __forceinline__ bool read_column_value(const SrcChunk& c, uint32_t off, T* v, bool stored_null_value) {
   if (c.kind == HY_COL_DICT) {
     uint32_t vid;
     if (c.vid_width == 1)
@@ -107,7 +110,7 @@ __device__ __forceinline__ bool read_column_value(const SrcChunk& c, uint32_t of
     return true;
   }
   if (c.nulls != nullptr && c.nulls[off]) {
-    *v = T{};
+    *v = stored_null_value ? static_cast<const T*>(c.data)[off] : T{};
     return false;
   }
   *v = static_cast<const T*>(c.data)[off];
@@ -127,12 +130,12 @@ __device__ __forceinline__ bool load_row(const Side& s, const SrcChunk& c, uint3
       valid = false;
       *payload = s.fuse_deref ? NULL_PAYLOAD : static_cast<uint32_t>(c.row_begin + off);
     } else {
-      valid = read_column_value<T>(s.referenced[rid.chunk_id], rid.chunk_offset, &v);
+      valid = read_column_value<T>(s.referenced[rid.chunk_id], rid.chunk_offset, &v, false);
       *payload = s.fuse_deref ? static_cast<uint32_t>(s.referenced_row_begin[rid.chunk_id] + rid.chunk_offset)
                               : static_cast<uint32_t>(c.row_begin + off);
     }
   } else {
-    valid = read_column_value<T>(c, off, &v);
+    valid = read_column_value<T>(c, off, &v, true);
     *payload = static_cast<uint32_t>(c.row_begin + off);
   }
   *key = static_cast<H>(v);
@@ -443,6 +446,10 @@ __global__ __launch_bounds__(SCAN_T) void exclusive_scan_u32(const uint32_t* __r
 
 // ------------------------------------------------------------------------------------------------------------
 // Per-partition build + probe.
+//
+// Partition p's hash table has cap_p = n + n/2 + 1 slots (open addressing, linear probing, slot = fastrange of a
+// key hash independent of the radix bits). It lives in LDS when the partition fits the launch's LDS budget and
+// otherwise in a global workspace slice (skewed keys), so any partition size is handled.
 // ------------------------------------------------------------------------------------------------------------
 constexpr int JOIN_THREADS = 512;
 constexpr uint32_t SLOT_EMPTY = 0u;
@@ -458,8 +465,7 @@ struct JoinDesc {
   const uint32_t* build_begin;  // n_parts + 1
   const uint32_t* probe_begin;  // n_parts + 1
   uint32_t n_parts;
-  uint32_t cap;                 // LDS hash slots (power of two)
-  uint32_t max_build;           // max build partition size (LDS arrays sized by it)
+  uint32_t lds_max_build;       // partitions up to this size use LDS
   int32_t mode;
   RowMap build_map;
   RowMap probe_map;
@@ -469,80 +475,72 @@ struct JoinDesc {
   uint32_t* error;
   uint32_t* overflow;
   uint64_t* total;              // total pairs (written by the last partition)
+  void* global_ws;              // tables of partitions above lds_max_build
 };
 
+__host__ __device__ inline uint32_t slot_cap(uint32_t nb) { return nb + nb / 2 + 1; }
+
+// bytes of the per-partition table for nb build rows (LDS and global layouts are identical)
 template <typename H>
-__device__ __forceinline__ uint32_t slot_hash(H key) {
-  if constexpr (sizeof(H) == 4) {
-    uint32_t b;
-    if constexpr (std::is_floating_point_v<H>) {
-      const H k = key == H(0) ? H(0) : key;  // -0.0 and 0.0 compare equal: hash them alike
-      __builtin_memcpy(&b, &k, 4);
-    } else {
-      __builtin_memcpy(&b, &key, 4);
-    }
-    return murmur_final(b * 0x9E3779B1u);
-  } else {
-    uint64_t b;
-    if constexpr (std::is_floating_point_v<H>) {
-      const H k = key == H(0) ? H(0) : key;
-      __builtin_memcpy(&b, &k, 8);
-    } else {
-      __builtin_memcpy(&b, &key, 8);
-    }
-    return murmur_final(static_cast<uint32_t>(b) * 0x9E3779B1u ^ static_cast<uint32_t>(b >> 32));
-  }
+__host__ __device__ inline size_t table_bytes(uint32_t nb) {
+  const size_t cap = slot_cap(nb);
+  size_t b = sizeof(Slot<H>) * cap;        // slots
+  b += 4 * size_t(nb);                      // build payloads
+  b += 4 * ((cap + 1) / 2);                 // per-slot counts (u16, packed for 32-bit atomics)
+  b += 2 * cap;                             // per-slot list begin
+  b += 2 * size_t(nb) * 2;                  // element slot + sorted element list
+  return (b + 15) & ~size_t(15);
 }
 
 template <typename H>
-__global__ __launch_bounds__(JOIN_THREADS) void join_partition(JoinDesc d, const Rec<H>* __restrict__ build,
-                                                               const Rec<H>* __restrict__ probe,
-                                                               hy_row_id* __restrict__ out_build,
-                                                               hy_row_id* __restrict__ out_probe,
-                                                               uint64_t* __restrict__ part_out_begin,
-                                                               uint32_t* __restrict__ part_out_count) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  Slot<H>* slots = reinterpret_cast<Slot<H>*>(smem);
-  uint32_t* bpay = reinterpret_cast<uint32_t*>(smem + sizeof(Slot<H>) * d.cap);      // build payloads
-  uint16_t* cnt = reinterpret_cast<uint16_t*>(bpay + d.max_build);                    // per-slot counts
-  uint16_t* lbeg = cnt + d.cap;                                                         // per-slot list begin
-  uint16_t* eslot = lbeg + d.cap;                                                       // per-element slot
-  uint16_t* sorted = eslot + d.max_build;                                               // elements by slot
-  __shared__ uint32_t s_scratch[JOIN_THREADS / WAVE + 1];
-  __shared__ uint32_t s_part;
-  __shared__ uint32_t s_dup;
-  __shared__ uint64_t s_base;
+__device__ __forceinline__ uint32_t slot_hash(H key) {
+  uint64_t b = 0;
+  H k = key;
+  if constexpr (std::is_floating_point_v<H>) {
+    if (k == H(0)) k = H(0);  // -0.0 and 0.0 compare equal: hash them alike
+  }
+  __builtin_memcpy(&b, &k, sizeof(H));
+  return murmur_final(static_cast<uint32_t>(b) * 0x9E3779B1u ^ static_cast<uint32_t>(b >> 32) * 0x85EBCA77u);
+}
 
-  if (threadIdx.x == 0) {
-    s_part = atomicAdd(d.ticket, 1u);
-    s_dup = 0;
-  }
-  for (uint32_t i = threadIdx.x; i < d.cap; i += JOIN_THREADS) {
-    slots[i].state = SLOT_EMPTY;
-    cnt[i] = 0;
-  }
-  __syncthreads();
-  const uint32_t p = s_part;
-  if (p >= d.n_parts) return;
+template <typename H, bool GLOBAL>
+__device__ void process_partition(const JoinDesc& d, uint32_t p, unsigned char* base, const Rec<H>* __restrict__ build,
+                                  const Rec<H>* __restrict__ probe, hy_row_id* __restrict__ out_build,
+                                  hy_row_id* __restrict__ out_probe, uint64_t* __restrict__ part_out_begin,
+                                  uint32_t* __restrict__ part_out_count, uint32_t* s_scratch, uint32_t* s_flag,
+                                  uint64_t* s_base) {
   const uint32_t bb = d.build_begin[p], nb = d.build_begin[p + 1] - bb;
   const uint32_t pb = d.probe_begin[p], np = d.probe_begin[p + 1] - pb;
-  const uint32_t mask = d.cap - 1;
+  const uint32_t cap = slot_cap(nb);
+  Slot<H>* slots = reinterpret_cast<Slot<H>*>(base);
+  uint32_t* bpay = reinterpret_cast<uint32_t*>(base + sizeof(Slot<H>) * cap);
+  uint32_t* cnt32 = bpay + nb;
+  uint16_t* cnt = reinterpret_cast<uint16_t*>(cnt32);
+  uint16_t* lbeg = reinterpret_cast<uint16_t*>(cnt32 + (cap + 1) / 2);
+  uint16_t* eslot = lbeg + cap;
+  uint16_t* sorted = eslot + nb;
+  constexpr int SCOPE = GLOBAL ? __HIP_MEMORY_SCOPE_WORKGROUP : __HIP_MEMORY_SCOPE_WORKGROUP;
   const int mode = d.mode;
+
+  for (uint32_t i = threadIdx.x; i < cap; i += JOIN_THREADS) slots[i].state = SLOT_EMPTY;
+  for (uint32_t i = threadIdx.x; i < (cap + 1) / 2; i += JOIN_THREADS) cnt32[i] = 0;
+  if (threadIdx.x == 0) *s_flag = 0;
+  __syncthreads();
 
   // ---- build: insert keys, count multiplicities ----
   for (uint32_t i = threadIdx.x; i < nb; i += JOIN_THREADS) {
     const Rec<H> r = build[bb + i];
     bpay[i] = r.payload;
-    uint32_t s = slot_hash<H>(r.key) & mask;
-    for (uint32_t guard = 0; guard <= d.cap * 64u; ++guard) {
-      const uint32_t st = __hip_atomic_load(&slots[s].state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    uint32_t s = static_cast<uint32_t>((static_cast<uint64_t>(slot_hash<H>(r.key)) * cap) >> 32);
+    for (uint32_t guard = 0; guard <= cap * 64u; ++guard) {
+      const uint32_t st = __hip_atomic_load(&slots[s].state, __ATOMIC_RELAXED, SCOPE);
       if (st == SLOT_EMPTY) {
         uint32_t expected = SLOT_EMPTY;
         if (__hip_atomic_compare_exchange_strong(&slots[s].state, &expected, SLOT_LOCKED, __ATOMIC_RELAXED,
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                                                 __ATOMIC_RELAXED, SCOPE)) {
           slots[s].key = r.key;
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-          __hip_atomic_store(&slots[s].state, i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_store(&slots[s].state, i + 1, __ATOMIC_RELAXED, SCOPE);
           break;
         }
         continue;
@@ -550,34 +548,34 @@ __global__ __launch_bounds__(JOIN_THREADS) void join_partition(JoinDesc d, const
       if (st == SLOT_LOCKED) continue;
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       if (slots[s].key == r.key) {
-        s_dup = 1;
+        *s_flag = 1;
         break;
       }
-      s = (s + 1) & mask;
+      s = (s + 1 == cap) ? 0 : s + 1;
     }
     eslot[i] = static_cast<uint16_t>(s);
-    atomicAdd(reinterpret_cast<uint32_t*>(&cnt[s & ~1u]), (s & 1u) ? 0x10000u : 1u);
+    atomicAdd(&cnt32[s >> 1], (s & 1u) ? 0x10000u : 1u);
   }
   __syncthreads();
-  const bool dup = s_dup != 0;
+  const bool dup = *s_flag != 0;
   if (dup) {
     // list_begin = exclusive prefix of counts over slots; then place elements in slot order, stable.
     uint32_t run = 0;
-    const uint32_t per = (d.cap + JOIN_THREADS - 1) / JOIN_THREADS;
+    const uint32_t per = (cap + JOIN_THREADS - 1) / JOIN_THREADS;
     const uint32_t s0 = threadIdx.x * per;
     for (uint32_t k = 0; k < per; ++k)
-      if (s0 + k < d.cap) run += cnt[s0 + k];
+      if (s0 + k < cap) run += cnt[s0 + k];
     uint32_t total;
     uint32_t pre = block_exclusive_sum<JOIN_THREADS>(run, s_scratch, &total);
     for (uint32_t k = 0; k < per; ++k)
-      if (s0 + k < d.cap) {
+      if (s0 + k < cap) {
         lbeg[s0 + k] = static_cast<uint16_t>(pre);
         pre += cnt[s0 + k];
       }
     __syncthreads();
-    // wave 0 places elements in index order: per slot a running cursor kept in `cnt` (reset first)
-    for (uint32_t i = threadIdx.x; i < d.cap; i += JOIN_THREADS) cnt[i] = 0;
+    for (uint32_t i = threadIdx.x; i < (cap + 1) / 2; i += JOIN_THREADS) cnt32[i] = 0;
     __syncthreads();
+    // wave 0 places elements in index order with a running per-slot cursor (rebuilds `cnt`)
     if (threadIdx.x < WAVE) {
       for (uint32_t i0 = 0; i0 < nb; i0 += WAVE) {
         const uint32_t i = i0 + __lane_id();
@@ -588,26 +586,30 @@ __global__ __launch_bounds__(JOIN_THREADS) void join_partition(JoinDesc d, const
           const uint64_t bb2 = __ballot(a && ((s >> b) & 1u));
           peers &= ((s >> b) & 1u) ? bb2 : ~bb2;
         }
-        uint32_t pos = 0;
-        if (a) pos = lbeg[s] + cnt[s] + __popcll(peers & lanemask_lt());
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        if (a) {
-          sorted[pos] = static_cast<uint16_t>(i);
-          const uint64_t higher = peers & ~(lanemask_lt() | (1ull << __lane_id()));
-          if (higher == 0) cnt[s] = static_cast<uint16_t>(cnt[s] + __popcll(peers));
+        // the highest peer advances the slot's cursor atomically (coherent in LDS and in global memory) and
+        // broadcasts the old value to its peers
+        const int leader = a ? 63 - __builtin_clzll(peers) : 0;
+        uint32_t old = 0;
+        if (a && __lane_id() == leader) {
+          const uint32_t w = atomicAdd(&cnt32[s >> 1], (s & 1u) ? (uint32_t(__popcll(peers)) << 16)
+                                                                 : uint32_t(__popcll(peers)));
+          old = (s & 1u) ? (w >> 16) : (w & 0xFFFFu);
         }
-        __builtin_amdgcn_s_waitcnt(0xC07F);
+        const uint32_t base_pos = __shfl(old, leader, WAVE);
+        if (a) sorted[lbeg[s] + base_pos + __popcll(peers & lanemask_lt())] = static_cast<uint16_t>(i);
       }
     }
     __syncthreads();
   }
 
-  // ---- probe: lookup ----
   auto lookup = [&](H key, uint32_t* first, uint32_t* count) {
-    uint32_t s = slot_hash<H>(key) & mask;
-    for (uint32_t guard = 0; guard <= d.cap; ++guard) {
+    *first = 0;
+    *count = 0;
+    if (nb == 0) return;
+    uint32_t s = static_cast<uint32_t>((static_cast<uint64_t>(slot_hash<H>(key)) * cap) >> 32);
+    for (uint32_t guard = 0; guard <= cap; ++guard) {
       const uint32_t st = slots[s].state;
-      if (st == SLOT_EMPTY) break;
+      if (st == SLOT_EMPTY) return;
       if (slots[s].key == key) {
         if (dup) {
           *first = lbeg[s];
@@ -618,10 +620,8 @@ __global__ __launch_bounds__(JOIN_THREADS) void join_partition(JoinDesc d, const
         }
         return;
       }
-      s = (s + 1) & mask;
+      s = (s + 1 == cap) ? 0 : s + 1;
     }
-    *first = 0;
-    *count = 0;
   };
   auto emitted = [&](uint32_t count) -> uint32_t {
     switch (mode) {
@@ -638,19 +638,15 @@ __global__ __launch_bounds__(JOIN_THREADS) void join_partition(JoinDesc d, const
     return 0u;
   };
 
-  // count phase
-  uint64_t my = 0;
+  // ---- probe, count phase ----
+  uint32_t my = 0;
   for (uint32_t j = threadIdx.x; j < np; j += JOIN_THREADS) {
     uint32_t f, c;
-    if (nb > 0)
-      lookup(probe[pb + j].key, &f, &c);
-    else
-      c = 0;
+    lookup(probe[pb + j].key, &f, &c);
     my += emitted(c);
   }
   uint32_t part_total32;
-  // per-thread counts fit 32 bits unless a single probe row matches > 4G rows
-  block_exclusive_sum<JOIN_THREADS>(static_cast<uint32_t>(my), s_scratch, &part_total32);
+  block_exclusive_sum<JOIN_THREADS>(my, s_scratch, &part_total32);
   const uint64_t part_total = part_total32;
 
   if (threadIdx.x == 0) {
@@ -662,18 +658,18 @@ __global__ __launch_bounds__(JOIN_THREADS) void join_partition(JoinDesc d, const
       lb_lookback(d.status, 0, p, &prefix, d.error);
       lb_publish(&d.status[p], LB_FLAG_PREFIX, prefix + part_total);
     }
-    s_base = prefix;
+    *s_base = prefix;
     part_out_begin[p] = prefix;
     part_out_count[p] = part_total32;
     if (p == d.n_parts - 1) *d.total = prefix + part_total;
     if (prefix + part_total > d.capacity) atomicOr(d.overflow, 1u);
   }
   __syncthreads();
-  const uint64_t base = s_base;
-  if (base + part_total > d.capacity) return;
+  const uint64_t obase = *s_base;
+  if (obase + part_total > d.capacity) return;
 
-  // write phase: blocks of JOIN_THREADS probe rows, in order
-  uint64_t run = base;
+  // ---- probe, write phase: blocks of JOIN_THREADS probe rows, in order ----
+  uint64_t run = obase;
   for (uint32_t j0 = 0; j0 < np; j0 += JOIN_THREADS) {
     const uint32_t j = j0 + threadIdx.x;
     uint32_t f = 0, c = 0, e = 0;
@@ -681,7 +677,7 @@ __global__ __launch_bounds__(JOIN_THREADS) void join_partition(JoinDesc d, const
     if (j < np) {
       const Rec<H> r = probe[pb + j];
       ppay = r.payload;
-      if (nb > 0) lookup(r.key, &f, &c);
+      lookup(r.key, &f, &c);
       e = emitted(c);
     }
     uint32_t blk_total;
@@ -703,6 +699,36 @@ __global__ __launch_bounds__(JOIN_THREADS) void join_partition(JoinDesc d, const
       }
     }
     run += blk_total;
+  }
+}
+
+template <typename H>
+__global__ __launch_bounds__(JOIN_THREADS) void join_partition(JoinDesc d, const Rec<H>* __restrict__ build,
+                                                               const Rec<H>* __restrict__ probe,
+                                                               hy_row_id* __restrict__ out_build,
+                                                               hy_row_id* __restrict__ out_probe,
+                                                               uint64_t* __restrict__ part_out_begin,
+                                                               uint32_t* __restrict__ part_out_count) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ uint32_t s_scratch[JOIN_THREADS / WAVE + 1];
+  __shared__ uint32_t s_part;
+  __shared__ uint32_t s_flag;
+  __shared__ uint64_t s_base;
+  if (threadIdx.x == 0) s_part = atomicAdd(d.ticket, 1u);
+  __syncthreads();
+  const uint32_t p = s_part;
+  if (p >= d.n_parts) return;
+  const uint32_t bb = d.build_begin[p], nb = d.build_begin[p + 1] - bb;
+  if (nb <= d.lds_max_build) {
+    process_partition<H, false>(d, p, smem, build, probe, out_build, out_probe, part_out_begin, part_out_count,
+                                s_scratch, &s_flag, &s_base);
+  } else {
+    // global slice: element offset bb, slot offset bb + bb/2 + p (see table_bytes / slot_cap)
+    unsigned char* g = static_cast<unsigned char*>(d.global_ws) +
+                       (static_cast<size_t>(bb) * (sizeof(Slot<H>) * 3 / 2 + 18) + size_t(p) * 64 * sizeof(Slot<H>));
+    g = reinterpret_cast<unsigned char*>((reinterpret_cast<uintptr_t>(g) + 15) & ~uintptr_t(15));
+    process_partition<H, true>(d, p, g, build, probe, out_build, out_probe, part_out_begin, part_out_count, s_scratch,
+                               &s_flag, &s_base);
   }
 }
 

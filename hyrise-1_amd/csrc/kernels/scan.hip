@@ -24,6 +24,8 @@ struct ScanLaunchDesc {
   const hy_scan_chunk* chunks;       // device copy of this class's chunk descriptors
   const uint64_t* chunk_tile_begin;  // n_chunks + 1 prefix of tile counts
   const uint32_t* chunk_index;       // original chunk index (for counts[])
+  const uint32_t* chunk_ids;         // chunk id written into RowID outputs
+  uint64_t n_rows;
   uint32_t n_chunks;
   uint64_t n_tiles;
   uint64_t* status;                  // n_tiles look-back words (zeroed)
@@ -71,9 +73,10 @@ __device__ __forceinline__ void load16(const E* __restrict__ base, uint32_t firs
 }
 
 // E = element type read from memory (vid type for DICT, value type for VALUE); IS_DICT selects the semantics.
-template <typename E, bool IS_DICT>
+// OUT_ROWID: write reference RowIDs {chunk_id, offset} (8 B) instead of chunk offsets (4 B).
+template <typename E, bool IS_DICT, bool OUT_ROWID>
 __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanLaunchDesc d, ScanConst<E> constant,
-                                                           uint32_t* __restrict__ out_offsets,
+                                                           void* __restrict__ out_any,
                                                            uint32_t* __restrict__ counts) {
   __shared__ uint32_t s_stage[SCAN_TILE];
   __shared__ uint32_t s_scratch[SCAN_THREADS / WAVE + 1];
@@ -166,8 +169,14 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanLaunchDesc d, Sc
     s_stage[pos++] = row0 + i;
   }
   __syncthreads();
-  uint32_t* out = out_offsets + ch.out_begin + s_prefix;
-  for (uint32_t i = threadIdx.x; i < tile_total; i += SCAN_THREADS) out[i] = s_stage[i];
+  if constexpr (OUT_ROWID) {
+    const uint32_t cid = d.chunk_ids[c];
+    hy_row_id* out = static_cast<hy_row_id*>(out_any) + ch.out_begin + s_prefix;
+    for (uint32_t i = threadIdx.x; i < tile_total; i += SCAN_THREADS) out[i] = hy_row_id{cid, s_stage[i]};
+  } else {
+    uint32_t* out = static_cast<uint32_t*>(out_any) + ch.out_begin + s_prefix;
+    for (uint32_t i = threadIdx.x; i < tile_total; i += SCAN_THREADS) out[i] = s_stage[i];
+  }
 }
 
 // ------------------------------------------------------------------------------------------------------------

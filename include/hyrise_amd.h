@@ -57,6 +57,16 @@ hy_status hy_memset(void* dst, int value, size_t bytes, hy_stream_t stream);
 hy_status hy_stream_create(hy_stream_t* stream);
 hy_status hy_stream_destroy(hy_stream_t stream);
 hy_status hy_stream_synchronize(hy_stream_t stream);
+/*
+ * Per-kernel device timing (HIP events recorded around every launch on its stream; off by default).
+ * collect() waits for the recorded launches and aggregates them per kernel name; get() reads one aggregate:
+ * launches, summed device milliseconds, summed work units (rows or pairs the launches processed).
+ */
+hy_status hy_kernel_stats_enable(int enable);
+hy_status hy_kernel_stats_reset(void);
+hy_status hy_kernel_stats_collect(uint32_t* n_kernels);
+hy_status hy_kernel_stats_get(uint32_t index, const char** name, uint64_t* launches, double* total_ms,
+                              uint64_t* units);
 /* Thread-local message of the last failing call. */
 const char* hy_last_error_message(void);
 /* Build identification ("gfx950 …"). */
@@ -128,6 +138,14 @@ hy_status hy_table_scan_workspace_size(const uint32_t* chunk_sizes, uint32_t n_c
 hy_status hy_table_scan(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_t value_type, const void* constant,
                         uint32_t* out_offsets, uint32_t* counts, void* workspace, size_t workspace_bytes,
                         hy_stream_t stream);
+
+/*
+ * Same scan, writing reference RowIDs {chunk_ids[c], offset} (8 B each) at out_rows + out_begin[c] — the PosList
+ * of the output chunk as the reference stores it (used by fused Scan -> Join pipelines). chunk_ids: HOST array.
+ */
+hy_status hy_table_scan_row_ids(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_t value_type,
+                                const void* constant, const uint32_t* chunk_ids, hy_row_id* out_rows, uint32_t* counts,
+                                void* workspace, size_t workspace_bytes, hy_stream_t stream);
 
 /*
  * Scan over a ReferenceColumn (reference BaseSingleColumnTableScanImpl::handle_column(const ReferenceColumn&),

@@ -87,3 +87,17 @@ def test_float_keys(hy, oracle):
     j.execute()
     exp, _ = oracle.join_hash(a, b, hy.JoinMode.Inner, (0, 0))
     assert_identical(j.get_output(), exp)
+
+
+@pytest.mark.parametrize("mode", ["Inner", "Left", "Semi", "Anti"])
+def test_skewed_keys_use_global_tables(hy, oracle, mode):
+    # a few hot keys put >10k build rows into one radix partition: beyond the LDS budget -> global-memory table
+    rng = np.random.default_rng(5)
+    build = np.where(rng.random(12_000) < 0.9, 42, rng.integers(0, 1000, 12_000)).astype(np.int32)
+    probe = rng.integers(0, 1200, 3_000).astype(np.int32)
+    a = hy.Table.from_arrays([("k", hy.DataType.Int, False)], [probe], [], 1_000)
+    b = hy.Table.from_arrays([("k", hy.DataType.Int, False)], [build], [], 5_000)
+    j = hy.JoinHash(wrap(hy, a), wrap(hy, b), getattr(hy.JoinMode, mode), (0, 0), hy.PredicateCondition.Equals)
+    j.execute()
+    exp, _ = oracle.join_hash(a, b, getattr(hy.JoinMode, mode), (0, 0))
+    assert_identical(j.get_output(), exp)
