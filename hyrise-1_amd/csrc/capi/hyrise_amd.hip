@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <mutex>
@@ -882,27 +883,19 @@ hy_status join_typed(const SidePlan& bp, const SidePlan& pp, const hy_join_param
   uint32_t max_build = 0;
   uint64_t build_total = hb[n_parts];
   for (uint32_t i = 0; i < n_parts; ++i) max_build = std::max(max_build, hb[i + 1] - hb[i]);
-  if (max_build > 65535)
-    return fail(HY_ERR_UNSUPPORTED, "build partition of " + std::to_string(max_build) +
-                                        " rows exceeds 65535 (heavily skewed join keys)");
-  // LDS budget: two 512-thread workgroups per CU; larger (skewed) partitions use a global-memory table
-  constexpr size_t kLdsBudget = 78 * 1024;
-  uint32_t lds_max = max_build;
-  while (lds_max > 0 && hyk::table_bytes<H>(lds_max) > kLdsBudget) lds_max = lds_max * 7 / 8;
+  // LDS budget: four 512-thread workgroups per CU (40 KiB each); a partition with more build rows than one table
+  // holds (skewed keys) is processed as several LDS sub-tables in sequence
+  size_t kLdsBudget = 40 * 1024;
+  if (const char* e = std::getenv("HY_JOIN_LDS_BUDGET")) kLdsBudget = std::strtoull(e, nullptr, 10);  // test knob
+  uint32_t lds_max = std::max<uint32_t>(max_build, 1);
+  while (lds_max > 16 && hyk::table_bytes<H>(lds_max) > kLdsBudget) lds_max = lds_max * 7 / 8;
   const size_t lds = hyk::table_bytes<H>(lds_max);
-  void* global_ws = nullptr;
-  if (lds_max < max_build) {
-    const size_t gbytes = build_total * (sizeof(hyk::Slot<H>) * 3 / 2 + 18) + size_t(n_parts) * 64 * sizeof(hyk::Slot<H>) +
-                          hyk::table_bytes<H>(max_build) + 4096;
-    HY_HIP(hipMallocAsync(&global_ws, gbytes, s));
-  }
 
   hyk::JoinDesc jd{};
   jd.build_begin = bb.part_begin;
   jd.probe_begin = pb.part_begin;
   jd.n_parts = n_parts;
   jd.lds_max_build = lds_max;
-  jd.global_ws = global_ws;
   jd.mode = prm->mode;
   jd.build_map = bp.fuse ? make_map(bb.ref_row_begin, bp.ref_row_begin) : make_map(bb.row_begin, bp.row_begin);
   jd.probe_map = pp.fuse ? make_map(pb.ref_row_begin, pp.ref_row_begin) : make_map(pb.row_begin, pp.row_begin);
@@ -926,7 +919,6 @@ hy_status join_typed(const SidePlan& bp, const SidePlan& pp, const hy_join_param
   uint64_t total = 0;
   HY_HIP(hipMemcpyAsync(flags, c.misc, 16, hipMemcpyDeviceToHost, s));
   HY_HIP(hipMemcpyAsync(&total, c.totals + 1, 8, hipMemcpyDeviceToHost, s));
-  if (global_ws) HY_HIP(hipFreeAsync(global_ws, s));
   HY_HIP(hipStreamSynchronize(s));
   if (flags[1]) return fail(HY_ERR_KERNEL, "join look-back did not complete");
   if (result) {

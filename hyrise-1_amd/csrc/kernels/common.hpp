@@ -171,4 +171,43 @@ __device__ inline bool lb_lookback(const uint64_t* status, uint64_t first_tile, 
   return true;
 }
 
+__device__ inline uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, WAVE);
+  return v;
+}
+
+// Wave-parallel look-back: executed by ALL 64 lanes of one wave. Each round polls the 64 nearest unresolved
+// predecessors at once; it stops at the nearest inclusive PREFIX (or the segment start [first_tile]) and sums the
+// aggregates in between. Returns the exclusive prefix of `tile` (same value in every lane).
+__device__ inline uint64_t lb_lookback_wave(const uint64_t* status, uint64_t first_tile, uint64_t tile,
+                                            uint32_t* error) {
+  const int lane = __lane_id();
+  uint64_t acc = 0;
+  int64_t hi = static_cast<int64_t>(tile) - 1;
+  uint32_t spins = 0;
+  while (hi >= static_cast<int64_t>(first_tile)) {
+    const int64_t j = hi - lane;
+    uint64_t v = LB_FLAG_PREFIX;  // before the segment start: inclusive prefix 0
+    if (j >= static_cast<int64_t>(first_tile)) v = lb_poll(&status[j]);
+    const uint64_t flag = v & ~LB_VALUE_MASK;
+    const uint64_t pmask = __ballot(flag == LB_FLAG_PREFIX);
+    const int stop = pmask ? __builtin_ctzll(pmask) : 63;
+    const uint64_t upto = stop == 63 ? ~0ull : ((2ull << stop) - 1);
+    if (__ballot(flag == 0) & upto) {
+      if (++spins > LB_MAX_SPINS) {
+        if (lane == 0) __hip_atomic_store(error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return acc;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    const uint64_t mine = (lane <= stop && j >= static_cast<int64_t>(first_tile)) ? (v & LB_VALUE_MASK) : 0;
+    acc += wave_sum64(mine);
+    if (pmask) break;
+    hi -= WAVE;
+  }
+  return acc;
+}
+
 }  // namespace hyk

@@ -423,17 +423,19 @@ __global__ __launch_bounds__(SCAN_T) void exclusive_scan_u32(const uint32_t* __r
   }
   uint32_t total;
   const uint32_t local = block_exclusive_sum<SCAN_T>(sum, s_scratch, &total);
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < WAVE) {
     uint64_t prefix = 0;
     if (tile == 0) {
-      lb_publish(&status[0], LB_FLAG_PREFIX, total);
+      if (threadIdx.x == 0) lb_publish(&status[0], LB_FLAG_PREFIX, total);
     } else {
-      lb_publish(&status[tile], LB_FLAG_AGG, total);
-      lb_lookback(status, 0, tile, &prefix, error);
-      lb_publish(&status[tile], LB_FLAG_PREFIX, prefix + total);
+      if (threadIdx.x == 0) lb_publish(&status[tile], LB_FLAG_AGG, total);
+      prefix = lb_lookback_wave(status, 0, tile, error);
+      if (threadIdx.x == 0) lb_publish(&status[tile], LB_FLAG_PREFIX, prefix + total);
     }
-    s_prefix = prefix;
-    if (tile == n_tiles - 1 && total_out != nullptr) *total_out = prefix + total;
+    if (threadIdx.x == 0) {
+      s_prefix = prefix;
+      if (tile == n_tiles - 1 && total_out != nullptr) *total_out = prefix + total;
+    }
   }
   __syncthreads();
   uint32_t run = static_cast<uint32_t>(s_prefix) + local;
@@ -445,19 +447,32 @@ __global__ __launch_bounds__(SCAN_T) void exclusive_scan_u32(const uint32_t* __r
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// Per-partition build + probe.
+// Per-partition build + probe, entirely in LDS.
 //
-// Partition p's hash table has cap_p = n + n/2 + 1 slots (open addressing, linear probing, slot = fastrange of a
-// key hash independent of the radix bits). It lives in LDS when the partition fits the launch's LDS budget and
-// otherwise in a global workspace slice (skewed keys), so any partition size is handled.
+// A hash table over up to L = lds_max_build build rows has cap = n + n/2 + 1 slots (open addressing, linear
+// probing, slot = fastrange of a key hash independent of the radix bits). A slot holds {state, key}: state = 1 +
+// payload of the row that claimed it, plus a per-slot count. A key with one build row needs nothing else; a key
+// with several build rows is expanded by re-reading the table's build records in order, which reproduces the
+// reference's insertion-ordered PosList (join_hash.cpp:158-175).
+//
+// A partition with more than L build rows (skewed keys) is processed as consecutive sub-tables of L rows each:
+// every probe row's match count is summed over the sub-tables, and its matches are written sub-table by sub-table,
+// which is again build order. Nothing ever leaves LDS.
+//
+// Probe records are loaded once into registers (8 per thread, 4096 per pass) with all loads in flight, matched,
+// counted, and - after the decoupled look-back across partitions has fixed this partition's output offset -
+// written without re-reading them.
 // ------------------------------------------------------------------------------------------------------------
 constexpr int JOIN_THREADS = 512;
+constexpr int JOIN_WAVES = JOIN_THREADS / WAVE;
+constexpr int JP_PER = 8;                          // probe records per thread per pass
+constexpr int JP_PASS = JP_PER * JOIN_THREADS;     // 4096
 constexpr uint32_t SLOT_EMPTY = 0u;
 constexpr uint32_t SLOT_LOCKED = 0xFFFFFFFFu;
 
 template <typename H>
 struct __attribute__((aligned(sizeof(H) == 8 ? 16 : 8))) Slot {
-  uint32_t state;  // 0 empty, LOCKED while the key is written, else first build index + 1
+  uint32_t state;  // 0 empty, LOCKED while the key is written, else 1 + payload of the claiming build row
   H key;
 };
 
@@ -465,7 +480,7 @@ struct JoinDesc {
   const uint32_t* build_begin;  // n_parts + 1
   const uint32_t* probe_begin;  // n_parts + 1
   uint32_t n_parts;
-  uint32_t lds_max_build;       // partitions up to this size use LDS
+  uint32_t lds_max_build;       // rows per LDS table (larger partitions use several sub-tables)
   int32_t mode;
   RowMap build_map;
   RowMap probe_map;
@@ -475,20 +490,16 @@ struct JoinDesc {
   uint32_t* error;
   uint32_t* overflow;
   uint64_t* total;              // total pairs (written by the last partition)
-  void* global_ws;              // tables of partitions above lds_max_build
 };
 
 __host__ __device__ inline uint32_t slot_cap(uint32_t nb) { return nb + nb / 2 + 1; }
 
-// bytes of the per-partition table for nb build rows (LDS and global layouts are identical)
+// LDS bytes of a table over nb build rows
 template <typename H>
 __host__ __device__ inline size_t table_bytes(uint32_t nb) {
   const size_t cap = slot_cap(nb);
-  size_t b = sizeof(Slot<H>) * cap;        // slots
-  b += 4 * size_t(nb);                      // build payloads
-  b += 4 * ((cap + 1) / 2);                 // per-slot counts (u16, packed for 32-bit atomics)
-  b += 2 * cap;                             // per-slot list begin
-  b += 2 * size_t(nb) * 2;                  // element slot + sorted element list
+  size_t b = sizeof(Slot<H>) * cap;  // slots
+  b += 4 * ((cap + 1) / 2);           // per-slot counts (u16, packed for 32-bit atomics)
   return (b + 15) & ~size_t(15);
 }
 
@@ -503,202 +514,366 @@ __device__ __forceinline__ uint32_t slot_hash(H key) {
   return murmur_final(static_cast<uint32_t>(b) * 0x9E3779B1u ^ static_cast<uint32_t>(b >> 32) * 0x85EBCA77u);
 }
 
-template <typename H, bool GLOBAL>
-__device__ void process_partition(const JoinDesc& d, uint32_t p, unsigned char* base, const Rec<H>* __restrict__ build,
-                                  const Rec<H>* __restrict__ probe, hy_row_id* __restrict__ out_build,
-                                  hy_row_id* __restrict__ out_probe, uint64_t* __restrict__ part_out_begin,
-                                  uint32_t* __restrict__ part_out_count, uint32_t* s_scratch, uint32_t* s_flag,
-                                  uint64_t* s_base) {
-  const uint32_t bb = d.build_begin[p], nb = d.build_begin[p + 1] - bb;
-  const uint32_t pb = d.probe_begin[p], np = d.probe_begin[p + 1] - pb;
-  const uint32_t cap = slot_cap(nb);
-  Slot<H>* slots = reinterpret_cast<Slot<H>*>(base);
-  uint32_t* bpay = reinterpret_cast<uint32_t*>(base + sizeof(Slot<H>) * cap);
-  uint32_t* cnt32 = bpay + nb;
-  uint16_t* cnt = reinterpret_cast<uint16_t*>(cnt32);
-  uint16_t* lbeg = reinterpret_cast<uint16_t*>(cnt32 + (cap + 1) / 2);
-  uint16_t* eslot = lbeg + cap;
-  uint16_t* sorted = eslot + nb;
-  constexpr int SCOPE = GLOBAL ? __HIP_MEMORY_SCOPE_WORKGROUP : __HIP_MEMORY_SCOPE_WORKGROUP;
-  const int mode = d.mode;
+__device__ __forceinline__ uint32_t emitted_for(int mode, uint32_t count) {
+  switch (mode) {
+    case HY_JOIN_INNER:
+      return count;
+    case HY_JOIN_LEFT:
+    case HY_JOIN_RIGHT:
+      return count > 0 ? count : 1u;
+    case HY_JOIN_SEMI:
+      return count > 0 ? 1u : 0u;
+    case HY_JOIN_ANTI:
+      return count > 0 ? 0u : 1u;
+  }
+  return 0u;
+}
 
+// Builds the LDS table over build records [b0, b0 + n). Ends with a barrier.
+template <typename H>
+__device__ __forceinline__ void build_table(Slot<H>* slots, uint32_t* cnt32, uint32_t cap,
+                                            const Rec<H>* __restrict__ build, uint32_t b0, uint32_t n, uint32_t* error) {
   for (uint32_t i = threadIdx.x; i < cap; i += JOIN_THREADS) slots[i].state = SLOT_EMPTY;
-  for (uint32_t i = threadIdx.x; i < (cap + 1) / 2; i += JOIN_THREADS) cnt32[i] = 0;
-  if (threadIdx.x == 0) *s_flag = 0;
+  for (uint32_t i = threadIdx.x; i < (cap + 1) / 2; i += JOIN_THREADS) cnt32[i] = 0u;
   __syncthreads();
-
-  // ---- build: insert keys, count multiplicities ----
-  for (uint32_t i = threadIdx.x; i < nb; i += JOIN_THREADS) {
-    const Rec<H> r = build[bb + i];
-    bpay[i] = r.payload;
-    uint32_t s = static_cast<uint32_t>((static_cast<uint64_t>(slot_hash<H>(r.key)) * cap) >> 32);
-    for (uint32_t guard = 0; guard <= cap * 64u; ++guard) {
-      const uint32_t st = __hip_atomic_load(&slots[s].state, __ATOMIC_RELAXED, SCOPE);
+  uint32_t i = threadIdx.x;
+  Rec<H> cur;
+  if (i < n) cur = build[b0 + i];
+  while (i < n) {
+    const uint32_t inext = i + JOIN_THREADS;
+    Rec<H> nxt;
+    if (inext < n) nxt = build[b0 + inext];  // next record's load in flight while inserting
+    uint32_t s = static_cast<uint32_t>((static_cast<uint64_t>(slot_hash<H>(cur.key)) * cap) >> 32);
+    // The claiming lane finishes its whole publication (key, state, count) inside the iteration in which its CAS
+    // succeeds, before any lane of the wave loops back: a lane that lost the race never spins on a LOCKED slot
+    // whose owner is a masked-off lane of its own wave.
+    bool done = false;
+    for (uint32_t guard = 0; !done && guard <= cap * 64u; ++guard) {
+      const uint32_t st = __hip_atomic_load(&slots[s].state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      bool won = false;
       if (st == SLOT_EMPTY) {
         uint32_t expected = SLOT_EMPTY;
-        if (__hip_atomic_compare_exchange_strong(&slots[s].state, &expected, SLOT_LOCKED, __ATOMIC_RELAXED,
-                                                 __ATOMIC_RELAXED, SCOPE)) {
-          slots[s].key = r.key;
+        won = __hip_atomic_compare_exchange_strong(&slots[s].state, &expected, SLOT_LOCKED, __ATOMIC_RELAXED,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (won) {
+          slots[s].key = cur.key;
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-          __hip_atomic_store(&slots[s].state, i + 1, __ATOMIC_RELAXED, SCOPE);
-          break;
+          __hip_atomic_store(&slots[s].state, cur.payload + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          atomicAdd(&cnt32[s >> 1], (s & 1u) ? 0x10000u : 1u);
         }
-        continue;
       }
-      if (st == SLOT_LOCKED) continue;
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      if (slots[s].key == r.key) {
-        *s_flag = 1;
-        break;
+      if (won) {
+        done = true;
+      } else if (st != SLOT_EMPTY && st != SLOT_LOCKED) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if (slots[s].key == cur.key) {
+          atomicAdd(&cnt32[s >> 1], (s & 1u) ? 0x10000u : 1u);
+          done = true;
+        } else {
+          s = (s + 1 == cap) ? 0 : s + 1;
+        }
       }
-      s = (s + 1 == cap) ? 0 : s + 1;
+      // else: lost the CAS or the slot is being published by another wave -> re-read the same slot
     }
-    eslot[i] = static_cast<uint16_t>(s);
-    atomicAdd(&cnt32[s >> 1], (s & 1u) ? 0x10000u : 1u);
+    if (!done) atomicOr(error, 2u);  // livelock guard (reported as a kernel failure)
+    cur = nxt;
+    i = inext;
   }
   __syncthreads();
-  const bool dup = *s_flag != 0;
-  if (dup) {
-    // list_begin = exclusive prefix of counts over slots; then place elements in slot order, stable.
-    uint32_t run = 0;
-    const uint32_t per = (cap + JOIN_THREADS - 1) / JOIN_THREADS;
-    const uint32_t s0 = threadIdx.x * per;
-    for (uint32_t k = 0; k < per; ++k)
-      if (s0 + k < cap) run += cnt[s0 + k];
-    uint32_t total;
-    uint32_t pre = block_exclusive_sum<JOIN_THREADS>(run, s_scratch, &total);
-    for (uint32_t k = 0; k < per; ++k)
-      if (s0 + k < cap) {
-        lbeg[s0 + k] = static_cast<uint16_t>(pre);
-        pre += cnt[s0 + k];
-      }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < (cap + 1) / 2; i += JOIN_THREADS) cnt32[i] = 0;
-    __syncthreads();
-    // wave 0 places elements in index order with a running per-slot cursor (rebuilds `cnt`)
-    if (threadIdx.x < WAVE) {
-      for (uint32_t i0 = 0; i0 < nb; i0 += WAVE) {
-        const uint32_t i = i0 + __lane_id();
-        const bool a = i < nb;
-        const uint32_t s = a ? eslot[i] : 0u;
-        uint64_t peers = __ballot(a);
-        for (int b = 0; b < 16; ++b) {
-          const uint64_t bb2 = __ballot(a && ((s >> b) & 1u));
-          peers &= ((s >> b) & 1u) ? bb2 : ~bb2;
-        }
-        // the highest peer advances the slot's cursor atomically (coherent in LDS and in global memory) and
-        // broadcasts the old value to its peers
-        const int leader = a ? 63 - __builtin_clzll(peers) : 0;
-        uint32_t old = 0;
-        if (a && __lane_id() == leader) {
-          const uint32_t w = atomicAdd(&cnt32[s >> 1], (s & 1u) ? (uint32_t(__popcll(peers)) << 16)
-                                                                 : uint32_t(__popcll(peers)));
-          old = (s & 1u) ? (w >> 16) : (w & 0xFFFFu);
-        }
-        const uint32_t base_pos = __shfl(old, leader, WAVE);
-        if (a) sorted[lbeg[s] + base_pos + __popcll(peers & lanemask_lt())] = static_cast<uint16_t>(i);
-      }
+}
+
+// (state, count) of key in the table (count = build rows with this key)
+template <typename H>
+__device__ __forceinline__ void table_lookup(const Slot<H>* slots, const uint32_t* cnt32, uint32_t cap, H key,
+                                             uint32_t* state, uint32_t* count) {
+  *state = 0;
+  *count = 0;
+  uint32_t s = static_cast<uint32_t>((static_cast<uint64_t>(slot_hash<H>(key)) * cap) >> 32);
+  for (uint32_t guard = 0; guard <= cap; ++guard) {
+    const Slot<H> sl = slots[s];
+    if (sl.state == SLOT_EMPTY) return;
+    if (sl.key == key) {
+      *state = sl.state;
+      *count = (cnt32[s >> 1] >> ((s & 1u) * 16)) & 0xFFFFu;
+      return;
     }
-    __syncthreads();
+    s = (s + 1 == cap) ? 0 : s + 1;
   }
+}
 
-  auto lookup = [&](H key, uint32_t* first, uint32_t* count) {
-    *first = 0;
-    *count = 0;
-    if (nb == 0) return;
-    uint32_t s = static_cast<uint32_t>((static_cast<uint64_t>(slot_hash<H>(key)) * cap) >> 32);
-    for (uint32_t guard = 0; guard <= cap; ++guard) {
-      const uint32_t st = slots[s].state;
-      if (st == SLOT_EMPTY) return;
-      if (slots[s].key == key) {
-        if (dup) {
-          *first = lbeg[s];
-          *count = cnt[s];
-        } else {
-          *first = st - 1;
-          *count = 1;
-        }
-        return;
-      }
-      s = (s + 1 == cap) ? 0 : s + 1;
-    }
-  };
-  auto emitted = [&](uint32_t count) -> uint32_t {
-    switch (mode) {
-      case HY_JOIN_INNER:
-        return count;
-      case HY_JOIN_LEFT:
-      case HY_JOIN_RIGHT:
-        return count > 0 ? count : 1u;
-      case HY_JOIN_SEMI:
-        return count > 0 ? 1u : 0u;
-      case HY_JOIN_ANTI:
-        return count > 0 ? 0u : 1u;
-    }
-    return 0u;
-  };
-
-  // ---- probe, count phase ----
-  uint32_t my = 0;
-  for (uint32_t j = threadIdx.x; j < np; j += JOIN_THREADS) {
-    uint32_t f, c;
-    lookup(probe[pb + j].key, &f, &c);
-    my += emitted(c);
-  }
-  uint32_t part_total32;
-  block_exclusive_sum<JOIN_THREADS>(my, s_scratch, &part_total32);
-  const uint64_t part_total = part_total32;
-
-  if (threadIdx.x == 0) {
+// Decoupled look-back across partitions (ticket order = partition order). Returns this partition's output offset;
+// the block must not write when offset + total exceeds the capacity (the overflow flag is raised instead).
+__device__ __forceinline__ uint64_t partition_base(const JoinDesc& d, uint32_t p, uint32_t part_total,
+                                                   uint64_t* __restrict__ part_out_begin,
+                                                   uint32_t* __restrict__ part_out_count, uint64_t* s_base) {
+  if (threadIdx.x < WAVE) {
     uint64_t prefix = 0;
     if (p == 0) {
-      lb_publish(&d.status[0], LB_FLAG_PREFIX, part_total);
+      if (threadIdx.x == 0) lb_publish(&d.status[0], LB_FLAG_PREFIX, part_total);
     } else {
-      lb_publish(&d.status[p], LB_FLAG_AGG, part_total);
-      lb_lookback(d.status, 0, p, &prefix, d.error);
-      lb_publish(&d.status[p], LB_FLAG_PREFIX, prefix + part_total);
+      if (threadIdx.x == 0) lb_publish(&d.status[p], LB_FLAG_AGG, part_total);
+      prefix = lb_lookback_wave(d.status, 0, p, d.error);
+      if (threadIdx.x == 0) lb_publish(&d.status[p], LB_FLAG_PREFIX, prefix + part_total);
     }
-    *s_base = prefix;
-    part_out_begin[p] = prefix;
-    part_out_count[p] = part_total32;
-    if (p == d.n_parts - 1) *d.total = prefix + part_total;
-    if (prefix + part_total > d.capacity) atomicOr(d.overflow, 1u);
+    if (threadIdx.x == 0) {
+      *s_base = prefix;
+      part_out_begin[p] = prefix;
+      part_out_count[p] = part_total;
+      if (p == d.n_parts - 1) *d.total = prefix + part_total;
+      if (prefix + part_total > d.capacity) atomicOr(d.overflow, 1u);
+    }
   }
   __syncthreads();
-  const uint64_t obase = *s_base;
+  return *s_base;
+}
+
+// Output offsets of one pass's records (k, thread): records (k' < k) first, then waves (w' < w), then lanes.
+// Leaves per-(k, wave) offsets in s_tot (valid until the caller's next barrier) and returns the pass total; a
+// record's position is then record_pos(e, k, s_tot).
+template <int JP, typename EF>
+__device__ __forceinline__ uint32_t pass_offsets(EF e_of, uint32_t* s_tot) {
+  const int lane = __lane_id();
+  const int w = threadIdx.x / WAVE;
+#pragma unroll
+  for (int k = 0; k < JP; ++k) {
+    const uint32_t incl = wave_inclusive_sum(e_of(k));
+    if (lane == WAVE - 1) s_tot[k * JOIN_WAVES + w] = incl;
+  }
+  __syncthreads();
+  if (threadIdx.x < WAVE) {  // exclusive prefix over the JP * JOIN_WAVES wave totals, (k, w) order
+    constexpr int N = JP * JOIN_WAVES;
+    constexpr int PER_LANE = (N + WAVE - 1) / WAVE;
+    uint32_t v[PER_LANE], sum = 0;
+#pragma unroll
+    for (int q = 0; q < PER_LANE; ++q) {
+      const int idx = lane * PER_LANE + q;
+      v[q] = idx < N ? s_tot[idx] : 0u;
+      sum += v[q];
+    }
+    const uint32_t incl = wave_inclusive_sum(sum);
+    uint32_t runl = incl - sum;
+#pragma unroll
+    for (int q = 0; q < PER_LANE; ++q) {
+      const int idx = lane * PER_LANE + q;
+      if (idx < N) s_tot[idx] = runl;
+      runl += v[q];
+    }
+    if (lane == WAVE - 1) s_tot[N] = incl;
+  }
+  __syncthreads();
+  return s_tot[JP * JOIN_WAVES];
+}
+
+template <int JP>
+__device__ __forceinline__ uint32_t record_pos(uint32_t e, int k, const uint32_t* s_tot) {
+  return s_tot[k * JOIN_WAVES + threadIdx.x / WAVE] + wave_inclusive_sum(e) - e;
+}
+
+// Writes the build rows with `key` among build records [b0, b0 + n) in order, each paired with prow.
+template <typename H>
+__device__ __forceinline__ void write_duplicates(const JoinDesc& d, const Rec<H>* __restrict__ build, uint32_t b0,
+                                                 uint32_t n, H key, uint32_t count, hy_row_id prow, uint64_t o,
+                                                 hy_row_id* __restrict__ out_build, hy_row_id* __restrict__ out_probe) {
+  for (uint32_t i = 0, m = 0; i < n && m < count; ++i) {
+    const Rec<H> br = build[b0 + i];
+    if (br.key == key) {
+      out_build[o] = map_row(d.build_map, br.payload);
+      out_probe[o] = prow;
+      ++o;
+      ++m;
+    }
+  }
+}
+
+// A partition whose build side fits one LDS table (the common case): the table is built once and every probe
+// record's (state, count) stays in registers from counting to writing.
+template <typename H>
+__device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t p, unsigned char* smem,
+                                                    const Rec<H>* __restrict__ build,
+                                                    const Rec<H>* __restrict__ probe, hy_row_id* __restrict__ out_build,
+                                                    hy_row_id* __restrict__ out_probe,
+                                                    uint64_t* __restrict__ part_out_begin,
+                                                    uint32_t* __restrict__ part_out_count, uint32_t* s_tot,
+                                                    uint64_t* s_base) {
+  const uint32_t bb = d.build_begin[p], nb = d.build_begin[p + 1] - bb;
+  const uint32_t pb = d.probe_begin[p], np = d.probe_begin[p + 1] - pb;
+  const int mode = d.mode;
+  const uint32_t cap = slot_cap(nb);
+  Slot<H>* slots = reinterpret_cast<Slot<H>*>(smem);
+  uint32_t* cnt32 = reinterpret_cast<uint32_t*>(smem + sizeof(Slot<H>) * cap);
+  build_table<H>(slots, cnt32, cap, build, bb, nb, d.error);
+
+  const uint32_t n_pass = (np + JP_PASS - 1) / JP_PASS;
+  Rec<H> pr[JP_PER];
+  uint32_t pst[JP_PER], pcn[JP_PER];
+  auto load_and_match = [&](uint32_t pass) {
+#pragma unroll
+    for (int k = 0; k < JP_PER; ++k) {
+      const uint32_t j = pass * JP_PASS + k * JOIN_THREADS + threadIdx.x;
+      if (j < np) pr[k] = probe[pb + j];
+    }
+#pragma unroll
+    for (int k = 0; k < JP_PER; ++k) {
+      const uint32_t j = pass * JP_PASS + k * JOIN_THREADS + threadIdx.x;
+      pst[k] = 0;
+      pcn[k] = 0;
+      if (j < np && nb > 0) table_lookup<H>(slots, cnt32, cap, pr[k].key, &pst[k], &pcn[k]);
+    }
+  };
+
+  uint32_t my = 0;
+  for (uint32_t pass = 0; pass < n_pass; ++pass) {
+    load_and_match(pass);
+#pragma unroll
+    for (int k = 0; k < JP_PER; ++k) {
+      const uint32_t j = pass * JP_PASS + k * JOIN_THREADS + threadIdx.x;
+      if (j < np) my += emitted_for(mode, pcn[k]);
+    }
+  }
+  uint32_t part_total;
+  block_exclusive_sum<JOIN_THREADS>(my, s_tot, &part_total);
+  const uint64_t obase = partition_base(d, p, part_total, part_out_begin, part_out_count, s_base);
   if (obase + part_total > d.capacity) return;
 
-  // ---- probe, write phase: blocks of JOIN_THREADS probe rows, in order ----
   uint64_t run = obase;
-  for (uint32_t j0 = 0; j0 < np; j0 += JOIN_THREADS) {
-    const uint32_t j = j0 + threadIdx.x;
-    uint32_t f = 0, c = 0, e = 0;
-    uint32_t ppay = 0;
-    if (j < np) {
-      const Rec<H> r = probe[pb + j];
-      ppay = r.payload;
-      lookup(r.key, &f, &c);
-      e = emitted(c);
-    }
-    uint32_t blk_total;
-    const uint32_t off = block_exclusive_sum<JOIN_THREADS>(e, s_scratch, &blk_total);
-    if (e) {
-      const hy_row_id prow = map_row(d.probe_map, ppay);
-      uint64_t o = run + off;
+  for (uint32_t pass = 0; pass < n_pass; ++pass) {
+    if (n_pass > 1) load_and_match(pass);  // a single pass still holds its records and matches in registers
+    auto e_of = [&](int k) {
+      const uint32_t j = pass * JP_PASS + k * JOIN_THREADS + threadIdx.x;
+      return j < np ? emitted_for(mode, pcn[k]) : 0u;
+    };
+    const uint32_t pass_total = pass_offsets<JP_PER>(e_of, s_tot);
+#pragma unroll
+    for (int k = 0; k < JP_PER; ++k) {
+      const uint32_t e = e_of(k);
+      const uint64_t o = run + record_pos<JP_PER>(e, k, s_tot);
+      if (e == 0) continue;
+      const hy_row_id prow = map_row(d.probe_map, pr[k].payload);
       if (mode == HY_JOIN_SEMI || mode == HY_JOIN_ANTI) {
         out_probe[o] = prow;
-      } else if (c == 0) {
+      } else if (pcn[k] == 0) {  // outer: probe row without a match
         out_build[o] = hy_row_id{0xFFFFFFFFu, 0xFFFFFFFFu};
         out_probe[o] = prow;
+      } else if (pcn[k] == 1) {
+        out_build[o] = map_row(d.build_map, pst[k] - 1);
+        out_probe[o] = prow;
       } else {
-        for (uint32_t m = 0; m < c; ++m, ++o) {
-          const uint32_t bi = dup ? sorted[f + m] : f;
-          out_build[o] = map_row(d.build_map, bpay[bi]);
-          out_probe[o] = prow;
-        }
+        write_duplicates<H>(d, build, bb, nb, pr[k].key, pcn[k], prow, o, out_build, out_probe);
       }
     }
-    run += blk_total;
+    run += pass_total;
+    __syncthreads();  // s_tot is reused by the next pass
+  }
+}
+
+// A partition with more build rows than one LDS table holds (skewed keys): consecutive sub-tables of L build rows.
+// Counts are summed over the sub-tables; matches are written sub-table by sub-table, i.e. in build order. Each
+// probe pass rebuilds the sub-tables twice (count, write), a cost only skewed partitions pay.
+template <typename H>
+__device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t p, unsigned char* smem,
+                                                  const Rec<H>* __restrict__ build, const Rec<H>* __restrict__ probe,
+                                                  hy_row_id* __restrict__ out_build, hy_row_id* __restrict__ out_probe,
+                                                  uint64_t* __restrict__ part_out_begin,
+                                                  uint32_t* __restrict__ part_out_count, uint32_t* s_tot,
+                                                  uint64_t* s_base) {
+  const uint32_t bb = d.build_begin[p], nb = d.build_begin[p + 1] - bb;
+  const uint32_t pb = d.probe_begin[p], np = d.probe_begin[p + 1] - pb;
+  const uint32_t L = d.lds_max_build;
+  const uint32_t n_sub = (nb + L - 1) / L;
+  const int mode = d.mode;
+  Slot<H>* slots = reinterpret_cast<Slot<H>*>(smem);
+  auto cnt_of = [&](uint32_t c) { return reinterpret_cast<uint32_t*>(smem + sizeof(Slot<H>) * c); };
+  constexpr int JS = 2;  // probe records per thread per pass (fewer than JP_PER: keeps this rare path's registers
+                        // within the fast path's budget)
+  constexpr uint32_t JS_PASS = JS * JOIN_THREADS;
+  const uint32_t n_pass = (np + JS_PASS - 1) / JS_PASS;
+
+  Rec<H> pr[JS];
+  uint32_t pcn[JS];
+  auto load_and_count = [&](uint32_t pass) {
+#pragma unroll
+    for (int k = 0; k < JS; ++k) {
+      const uint32_t j = pass * JS_PASS + k * JOIN_THREADS + threadIdx.x;
+      if (j < np) pr[k] = probe[pb + j];
+      pcn[k] = 0;
+    }
+    for (uint32_t sub = 0; sub < n_sub; ++sub) {
+      const uint32_t b0 = bb + sub * L, n = (sub + 1 == n_sub) ? nb - sub * L : L, c = slot_cap(n);
+      build_table<H>(slots, cnt_of(c), c, build, b0, n, d.error);
+#pragma unroll
+      for (int k = 0; k < JS; ++k) {
+        const uint32_t j = pass * JS_PASS + k * JOIN_THREADS + threadIdx.x;
+        if (j < np) {
+          uint32_t st, cnt;
+          table_lookup<H>(slots, cnt_of(c), c, pr[k].key, &st, &cnt);
+          pcn[k] += cnt;
+        }
+      }
+      __syncthreads();  // before the next table overwrites LDS
+    }
+  };
+
+  uint32_t my = 0;
+  for (uint32_t pass = 0; pass < n_pass; ++pass) {
+    load_and_count(pass);
+#pragma unroll
+    for (int k = 0; k < JS; ++k) {
+      const uint32_t j = pass * JS_PASS + k * JOIN_THREADS + threadIdx.x;
+      if (j < np) my += emitted_for(mode, pcn[k]);
+    }
+  }
+  uint32_t part_total;
+  block_exclusive_sum<JOIN_THREADS>(my, s_tot, &part_total);
+  const uint64_t obase = partition_base(d, p, part_total, part_out_begin, part_out_count, s_base);
+  if (obase + part_total > d.capacity) return;
+
+  uint64_t run = obase;
+  for (uint32_t pass = 0; pass < n_pass; ++pass) {
+    if (n_pass > 1) load_and_count(pass);
+    auto e_of = [&](int k) {
+      const uint32_t j = pass * JS_PASS + k * JOIN_THREADS + threadIdx.x;
+      return j < np ? emitted_for(mode, pcn[k]) : 0u;
+    };
+    const uint32_t pass_total = pass_offsets<JS>(e_of, s_tot);
+    uint32_t pos[JS];
+#pragma unroll
+    for (int k = 0; k < JS; ++k) {
+      const uint32_t e = e_of(k);
+      pos[k] = record_pos<JS>(e, k, s_tot);
+      if (e == 0) continue;
+      if (mode == HY_JOIN_SEMI || mode == HY_JOIN_ANTI) {
+        out_probe[run + pos[k]] = map_row(d.probe_map, pr[k].payload);
+      } else if (pcn[k] == 0) {
+        out_build[run + pos[k]] = hy_row_id{0xFFFFFFFFu, 0xFFFFFFFFu};
+        out_probe[run + pos[k]] = map_row(d.probe_map, pr[k].payload);
+      }
+    }
+    __syncthreads();  // s_tot consumed; LDS table region free
+    if (mode != HY_JOIN_SEMI && mode != HY_JOIN_ANTI) {
+      for (uint32_t sub = 0; sub < n_sub; ++sub) {
+        const uint32_t b0 = bb + sub * L, n = (sub + 1 == n_sub) ? nb - sub * L : L, c = slot_cap(n);
+        build_table<H>(slots, cnt_of(c), c, build, b0, n, d.error);
+#pragma unroll
+        for (int k = 0; k < JS; ++k) {
+          const uint32_t j = pass * JS_PASS + k * JOIN_THREADS + threadIdx.x;
+          if (j >= np || pcn[k] == 0) continue;
+          uint32_t st, cnt;
+          table_lookup<H>(slots, cnt_of(c), c, pr[k].key, &st, &cnt);
+          if (cnt == 0) continue;
+          const hy_row_id prow = map_row(d.probe_map, pr[k].payload);
+          const uint64_t o = run + pos[k];
+          if (cnt == 1) {
+            out_build[o] = map_row(d.build_map, st - 1);
+            out_probe[o] = prow;
+          } else {
+            write_duplicates<H>(d, build, b0, n, pr[k].key, cnt, prow, o, out_build, out_probe);
+          }
+          pos[k] += cnt;
+        }
+        __syncthreads();  // before the next table overwrites LDS
+      }
+    }
+    run += pass_total;
   }
 }
 
@@ -710,26 +885,19 @@ __global__ __launch_bounds__(JOIN_THREADS) void join_partition(JoinDesc d, const
                                                                uint64_t* __restrict__ part_out_begin,
                                                                uint32_t* __restrict__ part_out_count) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ uint32_t s_scratch[JOIN_THREADS / WAVE + 1];
+  __shared__ uint32_t s_tot[JP_PER * JOIN_WAVES + 1];
   __shared__ uint32_t s_part;
-  __shared__ uint32_t s_flag;
   __shared__ uint64_t s_base;
   if (threadIdx.x == 0) s_part = atomicAdd(d.ticket, 1u);
   __syncthreads();
   const uint32_t p = s_part;
   if (p >= d.n_parts) return;
-  const uint32_t bb = d.build_begin[p], nb = d.build_begin[p + 1] - bb;
-  if (nb <= d.lds_max_build) {
-    process_partition<H, false>(d, p, smem, build, probe, out_build, out_probe, part_out_begin, part_out_count,
-                                s_scratch, &s_flag, &s_base);
-  } else {
-    // global slice: element offset bb, slot offset bb + bb/2 + p (see table_bytes / slot_cap)
-    unsigned char* g = static_cast<unsigned char*>(d.global_ws) +
-                       (static_cast<size_t>(bb) * (sizeof(Slot<H>) * 3 / 2 + 18) + size_t(p) * 64 * sizeof(Slot<H>));
-    g = reinterpret_cast<unsigned char*>((reinterpret_cast<uintptr_t>(g) + 15) & ~uintptr_t(15));
-    process_partition<H, true>(d, p, g, build, probe, out_build, out_probe, part_out_begin, part_out_count, s_scratch,
-                               &s_flag, &s_base);
-  }
+  if (d.build_begin[p + 1] - d.build_begin[p] <= d.lds_max_build)
+    partition_one_table<H>(d, p, smem, build, probe, out_build, out_probe, part_out_begin, part_out_count, s_tot,
+                           &s_base);
+  else
+    partition_sub_tables<H>(d, p, smem, build, probe, out_build, out_probe, part_out_begin, part_out_count, s_tot,
+                            &s_base);
 }
 
 __global__ void murmur_kernel_u32(const uint32_t* keys, uint64_t n, uint32_t seed, uint32_t* out) {

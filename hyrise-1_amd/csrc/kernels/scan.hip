@@ -145,19 +145,21 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanLaunchDesc d, Sc
   uint32_t tile_total;
   const uint32_t local = block_exclusive_sum<SCAN_THREADS>(__popc(mask), s_scratch, &tile_total);
 
-  // Decoupled look-back across the tiles of this chunk.
-  if (threadIdx.x == 0) {
+  // Decoupled look-back across the tiles of this chunk (wave 0, 64 predecessors per poll).
+  if (threadIdx.x < WAVE) {
     uint64_t prefix = 0;
     if (tile == first_tile) {
-      lb_publish(&d.status[tile], LB_FLAG_PREFIX, tile_total);
+      if (threadIdx.x == 0) lb_publish(&d.status[tile], LB_FLAG_PREFIX, tile_total);
     } else {
-      lb_publish(&d.status[tile], LB_FLAG_AGG, tile_total);
-      lb_lookback(d.status, first_tile, tile, &prefix, d.error);
-      lb_publish(&d.status[tile], LB_FLAG_PREFIX, prefix + tile_total);
+      if (threadIdx.x == 0) lb_publish(&d.status[tile], LB_FLAG_AGG, tile_total);
+      prefix = lb_lookback_wave(d.status, first_tile, tile, d.error);
+      if (threadIdx.x == 0) lb_publish(&d.status[tile], LB_FLAG_PREFIX, prefix + tile_total);
     }
-    s_prefix = prefix;
-    const uint64_t last_tile = d.chunk_tile_begin[c + 1] - 1;
-    if (tile == last_tile) counts[d.chunk_index[c]] = static_cast<uint32_t>(prefix + tile_total);
+    if (threadIdx.x == 0) {
+      s_prefix = prefix;
+      const uint64_t last_tile = d.chunk_tile_begin[c + 1] - 1;
+      if (tile == last_tile) counts[d.chunk_index[c]] = static_cast<uint32_t>(prefix + tile_total);
+    }
   }
 
   // Stage matching offsets in LDS in order, then store them coalesced.
@@ -242,17 +244,19 @@ __global__ __launch_bounds__(SCAN_THREADS) void ref_scan_kernel(RefScanDesc d, S
 
   uint32_t tile_total;
   const uint32_t local = block_exclusive_sum<SCAN_THREADS>(__popc(mask), s_scratch, &tile_total);
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < WAVE) {
     uint64_t prefix = 0;
     if (tile == 0) {
-      lb_publish(&d.status[tile], LB_FLAG_PREFIX, tile_total);
+      if (threadIdx.x == 0) lb_publish(&d.status[tile], LB_FLAG_PREFIX, tile_total);
     } else {
-      lb_publish(&d.status[tile], LB_FLAG_AGG, tile_total);
-      lb_lookback(d.status, 0, tile, &prefix, d.error);
-      lb_publish(&d.status[tile], LB_FLAG_PREFIX, prefix + tile_total);
+      if (threadIdx.x == 0) lb_publish(&d.status[tile], LB_FLAG_AGG, tile_total);
+      prefix = lb_lookback_wave(d.status, 0, tile, d.error);
+      if (threadIdx.x == 0) lb_publish(&d.status[tile], LB_FLAG_PREFIX, prefix + tile_total);
     }
-    s_prefix = prefix;
-    if (tile == d.n_tiles - 1) *count = prefix + tile_total;
+    if (threadIdx.x == 0) {
+      s_prefix = prefix;
+      if (tile == d.n_tiles - 1) *count = prefix + tile_total;
+    }
   }
   uint32_t pos = local;
   uint32_t m = mask;

@@ -58,8 +58,13 @@ def test_orders_lineitem_join(hy, oracle, n_orders, chunk):
     assert_identical(j2.get_output(), exp2)
 
 
+@pytest.mark.parametrize("lds_budget", [None, 1024])
 @pytest.mark.parametrize("mode", ["Inner", "Left", "Right", "Semi", "Anti"])
-def test_duplicates_and_nulls(hy, oracle, mode):
+def test_duplicates_and_nulls(hy, oracle, mode, lds_budget, monkeypatch):
+    # lds_budget=1024 caps every LDS hash table at a few dozen build rows, so every partition runs as a chain of
+    # sub-tables (the skewed-partition path) while the expected output stays the reference's
+    if lds_budget is not None:
+        monkeypatch.setenv("HY_JOIN_LDS_BUDGET", str(lds_budget))
     rng = np.random.default_rng(11)
     n1, n2 = 30_000, 50_000
     k1 = rng.integers(0, 8_000, n1).astype(np.int64)
@@ -90,8 +95,8 @@ def test_float_keys(hy, oracle):
 
 
 @pytest.mark.parametrize("mode", ["Inner", "Left", "Semi", "Anti"])
-def test_skewed_keys_use_global_tables(hy, oracle, mode):
-    # a few hot keys put >10k build rows into one radix partition: beyond the LDS budget -> global-memory table
+def test_skewed_keys_use_sub_tables(hy, oracle, mode):
+    # a few hot keys put >10k build rows into one radix partition: beyond one LDS table -> chained sub-tables
     rng = np.random.default_rng(5)
     build = np.where(rng.random(12_000) < 0.9, 42, rng.integers(0, 1000, 12_000)).astype(np.int32)
     probe = rng.integers(0, 1200, 3_000).astype(np.int32)
