@@ -14,6 +14,7 @@ needs no exchange; the shards' outputs are the reference's per-partition output 
 import argparse
 import ctypes
 import importlib
+import glob
 import json
 import os
 import sys
@@ -232,6 +233,10 @@ def main():
     dk = kernels[dom]
     roofline = {"bound": "hbm", "kernel": dom, "achieved": round(dk["achieved_GBps"], 1), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(dk["achieved_GBps"] / HBM_PEAK_GBPS, 4), "traffic": None}
+    traffic, traffic_src = committed_traffic(dom, args.sf, chunk, world)
+    if traffic is not None:
+        roofline["traffic"] = round(traffic)
+        roofline["traffic_source"] = traffic_src
     step_s = elapsed / K
     # end-to-end algorithmic bytes (§8(d)): scan 1 B/row + 8 B/match; join 4 B/build + 4 B/probe + 16 B/pair
     e2e_bytes = n_li * 1 + n_probe * 8 + n_ord * 4 + n_probe * 4 + pairs * 16
@@ -269,6 +274,27 @@ def main():
         print(json.dumps(line))
     if dist:
         dist.destroy_process_group()
+
+
+# bench.py's kernel-table names -> the HIP kernel function names rocprofv3 reports
+ROCPROF_NAME = {"scan_dict": "scan_kernel", "scan_value": "scan_kernel"}
+
+
+def committed_traffic(kernel, sf, chunk, world):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary of this configuration
+    (profiles/rNN_rocprof_sf<SF>_summary.json, written by tools/profile_bench.sh: FETCH_SIZE x2 + WRITE_SIZE as the
+    MI355X guide prescribes). The counters need their own rocprofv3 passes, so they are not re-collected here; the
+    summary named in traffic_source is the evidence. None if no summary matches (other scale factor or N>1)."""
+    if world != 1 or chunk != 100_000:
+        return None, None
+    here = os.path.dirname(os.path.abspath(__file__))
+    files = sorted(glob.glob(os.path.join(here, "profiles", f"r*_rocprof_sf{sf:g}_summary.json")))
+    for f in reversed(files):
+        with open(f) as fh:
+            k = json.load(fh).get("kernels", {}).get(ROCPROF_NAME.get(kernel, kernel), {})
+        if "hbm_bytes_per_launch" in k:
+            return k["hbm_bytes_per_launch"], os.path.relpath(f, here)
+    return None, None
 
 
 def cpu_baseline(hy, synth, sf, chunk):
