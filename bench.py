@@ -35,6 +35,9 @@ def parse():
     p.add_argument("--chunk", type=int, default=100_000)
     p.add_argument("--cpu-sf", type=float, default=20.0, help="scale factor of the bounded CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--join-trace", default=None,
+                   help="debug: after the timed region run one traced step and write per-partition join phase "
+                        "durations (us) to this .npz (hy_debug_set_join_trace)")
     return p.parse_args()
 
 
@@ -193,6 +196,16 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     L.hy_kernel_stats_enable(0)
+    if args.join_trace and rank == 0:
+        import numpy as np
+        trace = torch.zeros(5 * (1 << radix_bits), dtype=torch.int64, device=dev)
+        L.hy_debug_set_join_trace.argtypes = [ctypes.c_void_p]
+        L.hy_debug_set_join_trace(trace.data_ptr())
+        step()
+        torch.cuda.synchronize()
+        L.hy_debug_set_join_trace(None)
+        t = trace.view(-1, 5).cpu().numpy().astype(np.float64) / 100.0  # 100 MHz device clock -> us
+        np.savez(args.join_trace, stamps_us=t, out_pairs=part_count.cpu().numpy())
     if dist:
         dist.barrier()
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)

@@ -59,6 +59,7 @@ struct KernelTiming {
   uint64_t units;
 };
 std::mutex g_kt_mutex;
+uint64_t* g_join_trace = nullptr;  // hy_debug_set_join_trace
 bool g_kt_enabled = false;
 std::vector<KernelTiming> g_kt_pending;
 std::vector<hipEvent_t> g_kt_pool;
@@ -180,6 +181,11 @@ hy_status hy_stream_synchronize(hy_stream_t stream) {
 }
 
 const char* hy_last_error_message(void) { return g_last_error.c_str(); }
+
+hy_status hy_debug_set_join_trace(uint64_t* device_trace) {
+  g_join_trace = device_trace;
+  return HY_OK;
+}
 
 hy_status hy_kernel_stats_enable(int enable) {
   std::lock_guard<std::mutex> lock(g_kt_mutex);
@@ -877,12 +883,18 @@ hy_status join_typed(const SidePlan& bp, const SidePlan& pp, const hy_join_param
 
   // largest build partition decides the LDS table size
   const uint32_t n_parts = 1u << g.bits;
-  std::vector<uint32_t> hb(n_parts + 1);
+  std::vector<uint32_t> hb(n_parts + 1), hp(n_parts + 1);
   HY_HIP(hipMemcpyAsync(hb.data(), bb.part_begin, sizeof(uint32_t) * (n_parts + 1), hipMemcpyDeviceToHost, s));
+  HY_HIP(hipMemcpyAsync(hp.data(), pb.part_begin, sizeof(uint32_t) * (n_parts + 1), hipMemcpyDeviceToHost, s));
   HY_HIP(hipStreamSynchronize(s));
-  uint32_t max_build = 0;
+  uint32_t max_build = 0, max_probe = 0;
   uint64_t build_total = hb[n_parts];
-  for (uint32_t i = 0; i < n_parts; ++i) max_build = std::max(max_build, hb[i + 1] - hb[i]);
+  for (uint32_t i = 0; i < n_parts; ++i) {
+    max_build = std::max(max_build, hb[i + 1] - hb[i]);
+    max_probe = std::max(max_probe, hp[i + 1] - hp[i]);
+  }
+  // probe records per thread per pass: 8, or 12 when the largest probe partition needs more than one 8-record pass
+  const bool wide = max_probe > static_cast<uint32_t>(hyk::JP_PER * hyk::JOIN_THREADS);
   // LDS budget: four 512-thread workgroups per CU (40 KiB each); a partition with more build rows than one table
   // holds (skewed keys) is processed as several LDS sub-tables in sequence
   size_t kLdsBudget = 40 * 1024;
@@ -900,18 +912,23 @@ hy_status join_typed(const SidePlan& bp, const SidePlan& pp, const hy_join_param
   jd.build_map = bp.fuse ? make_map(bb.ref_row_begin, bp.ref_row_begin) : make_map(bb.row_begin, bp.row_begin);
   jd.probe_map = pp.fuse ? make_map(pb.ref_row_begin, pp.ref_row_begin) : make_map(pb.row_begin, pp.row_begin);
   jd.capacity = out_capacity;
-  jd.status = c.join_status;
-  jd.ticket = c.misc + 4;
   jd.error = c.misc + 1;
   jd.overflow = c.misc + 2;
   jd.total = c.totals + 1;
+  jd.trace = g_join_trace;
   HY_HIP(hipMemsetAsync(c.join_status, 0, sizeof(uint64_t) * n_parts, s));
   HY_HIP(hipMemsetAsync(c.misc, 0, 64 * 4, s));
   HY_HIP(hipMemsetAsync(c.totals, 0, 8 * 2, s));
   {
       KTimer kt_("join_partition", s, bp.n_rows + pp.n_rows);
-      hipLaunchKernelGGL((hyk::join_partition<H>), dim3(n_parts), dim3(hyk::JOIN_THREADS), lds, s, jd, brec, precs,
-                     out_build, out_probe, partition_begin, partition_counts);
+      auto launch = [&](auto kernel) {
+        hipLaunchKernelGGL(kernel, dim3(n_parts), dim3(hyk::JOIN_THREADS), lds, s, jd, brec, precs, out_build,
+                           out_probe, partition_begin, partition_counts);
+      };
+      if (jd.trace)  // debug phase-trace instance (hy_debug_set_join_trace)
+        wide ? launch(hyk::join_partition<H, true, 12>) : launch(hyk::join_partition<H, true, hyk::JP_PER>);
+      else
+        wide ? launch(hyk::join_partition<H, false, 12>) : launch(hyk::join_partition<H, false, hyk::JP_PER>);
       kt_.done();
     }
   HY_HIP(hipGetLastError());

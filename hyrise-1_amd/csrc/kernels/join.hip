@@ -459,9 +459,9 @@ __global__ __launch_bounds__(SCAN_T) void exclusive_scan_u32(const uint32_t* __r
 // every probe row's match count is summed over the sub-tables, and its matches are written sub-table by sub-table,
 // which is again build order. Nothing ever leaves LDS.
 //
-// Probe records are loaded once into registers (8 per thread, 4096 per pass) with all loads in flight, matched,
-// counted, and - after the decoupled look-back across partitions has fixed this partition's output offset -
-// written without re-reading them.
+// Probe records are loaded once into registers (JP per thread per pass; the host picks JP so that a typical
+// partition is one pass) with all loads in flight, matched, counted, and - once one atomic add has reserved the
+// partition's output range - written without re-reading them.
 // ------------------------------------------------------------------------------------------------------------
 constexpr int JOIN_THREADS = 512;
 constexpr int JOIN_WAVES = JOIN_THREADS / WAVE;
@@ -485,11 +485,10 @@ struct JoinDesc {
   RowMap build_map;
   RowMap probe_map;
   uint64_t capacity;            // output capacity in pairs
-  uint64_t* status;             // n_parts look-back words
-  uint32_t* ticket;
   uint32_t* error;
   uint32_t* overflow;
   uint64_t* total;              // total pairs (written by the last partition)
+  uint64_t* trace;              // debug phase stamps (hy_debug_set_join_trace) or null
 };
 
 __host__ __device__ inline uint32_t slot_cap(uint32_t nb) { return nb + nb / 2 + 1; }
@@ -514,6 +513,13 @@ __device__ __forceinline__ uint32_t slot_hash(H key) {
   return murmur_final(static_cast<uint32_t>(b) * 0x9E3779B1u ^ static_cast<uint32_t>(b >> 32) * 0x85EBCA77u);
 }
 
+template <bool TRACE>
+__device__ __forceinline__ void trace_stamp(const JoinDesc& d, uint32_t p, int i) {
+  if constexpr (TRACE) {
+    if (threadIdx.x == 0) d.trace[5ull * p + i] = wall_clock64();
+  }
+}
+
 __device__ __forceinline__ uint32_t emitted_for(int mode, uint32_t count) {
   switch (mode) {
     case HY_JOIN_INNER:
@@ -529,57 +535,91 @@ __device__ __forceinline__ uint32_t emitted_for(int mode, uint32_t count) {
   return 0u;
 }
 
-// Builds the LDS table over build records [b0, b0 + n). Ends with a barrier.
+// Inserts one build record. The claiming lane finishes its whole publication (key, state, count) inside the
+// iteration in which its CAS succeeds, before any lane of the wave loops back: a lane that lost the race never spins
+// on a LOCKED slot whose owner is a masked-off lane of its own wave.
+template <typename H>
+__device__ __forceinline__ void table_insert(Slot<H>* slots, uint32_t* cnt32, uint32_t cap, const Rec<H>& rec,
+                                             uint32_t* error) {
+  uint32_t s = static_cast<uint32_t>((static_cast<uint64_t>(slot_hash<H>(rec.key)) * cap) >> 32);
+  bool done = false;
+  for (uint32_t guard = 0; !done && guard <= cap * 64u; ++guard) {
+    const uint32_t st = __hip_atomic_load(&slots[s].state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    bool won = false;
+    if (st == SLOT_EMPTY) {
+      uint32_t expected = SLOT_EMPTY;
+      won = __hip_atomic_compare_exchange_strong(&slots[s].state, &expected, SLOT_LOCKED, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (won) {
+        slots[s].key = rec.key;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __hip_atomic_store(&slots[s].state, rec.payload + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        atomicAdd(&cnt32[s >> 1], (s & 1u) ? 0x10000u : 1u);
+      }
+    }
+    if (won) {
+      done = true;
+    } else if (st != SLOT_EMPTY && st != SLOT_LOCKED) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      if (slots[s].key == rec.key) {
+        atomicAdd(&cnt32[s >> 1], (s & 1u) ? 0x10000u : 1u);
+        done = true;
+      } else {
+        s = (s + 1 == cap) ? 0 : s + 1;
+      }
+    }
+    // else: lost the CAS or the slot is being published by another wave -> re-read the same slot
+  }
+  if (!done) atomicOr(error, 2u);  // livelock guard (reported as a kernel failure)
+}
+
+// Builds the LDS table over build records [b0, b0 + n). Each thread holds up to BUILD_PER records whose loads are
+// all in flight together - the first batch's while the table is being cleared. Insertion order is irrelevant: a
+// slot's state names the row of a single-row key, and multi-row keys are expanded in build order from the records.
+// Ends with a barrier.
+constexpr int BUILD_PER = 6;  // >= the largest 4-byte-key table in the default 40 KiB budget / JOIN_THREADS
 template <typename H>
 __device__ __forceinline__ void build_table(Slot<H>* slots, uint32_t* cnt32, uint32_t cap,
                                             const Rec<H>* __restrict__ build, uint32_t b0, uint32_t n, uint32_t* error) {
+  Rec<H> r[BUILD_PER];
+  auto load_batch = [&](uint32_t base) {
+#pragma unroll
+    for (int q = 0; q < BUILD_PER; ++q) {
+      const uint32_t i = base + q * JOIN_THREADS + threadIdx.x;
+      if (i < n) r[q] = build[b0 + i];
+    }
+  };
+  load_batch(0);
   for (uint32_t i = threadIdx.x; i < cap; i += JOIN_THREADS) slots[i].state = SLOT_EMPTY;
   for (uint32_t i = threadIdx.x; i < (cap + 1) / 2; i += JOIN_THREADS) cnt32[i] = 0u;
   __syncthreads();
-  uint32_t i = threadIdx.x;
-  Rec<H> cur;
-  if (i < n) cur = build[b0 + i];
-  while (i < n) {
-    const uint32_t inext = i + JOIN_THREADS;
-    Rec<H> nxt;
-    if (inext < n) nxt = build[b0 + inext];  // next record's load in flight while inserting
-    uint32_t s = static_cast<uint32_t>((static_cast<uint64_t>(slot_hash<H>(cur.key)) * cap) >> 32);
-    // The claiming lane finishes its whole publication (key, state, count) inside the iteration in which its CAS
-    // succeeds, before any lane of the wave loops back: a lane that lost the race never spins on a LOCKED slot
-    // whose owner is a masked-off lane of its own wave.
-    bool done = false;
-    for (uint32_t guard = 0; !done && guard <= cap * 64u; ++guard) {
-      const uint32_t st = __hip_atomic_load(&slots[s].state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      bool won = false;
-      if (st == SLOT_EMPTY) {
-        uint32_t expected = SLOT_EMPTY;
-        won = __hip_atomic_compare_exchange_strong(&slots[s].state, &expected, SLOT_LOCKED, __ATOMIC_RELAXED,
-                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (won) {
-          slots[s].key = cur.key;
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-          __hip_atomic_store(&slots[s].state, cur.payload + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          atomicAdd(&cnt32[s >> 1], (s & 1u) ? 0x10000u : 1u);
-        }
-      }
-      if (won) {
-        done = true;
-      } else if (st != SLOT_EMPTY && st != SLOT_LOCKED) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        if (slots[s].key == cur.key) {
-          atomicAdd(&cnt32[s >> 1], (s & 1u) ? 0x10000u : 1u);
-          done = true;
-        } else {
-          s = (s + 1 == cap) ? 0 : s + 1;
-        }
-      }
-      // else: lost the CAS or the slot is being published by another wave -> re-read the same slot
+  for (uint32_t base = 0; base < n; base += BUILD_PER * JOIN_THREADS) {
+    if (base) load_batch(base);
+#pragma unroll
+    for (int q = 0; q < BUILD_PER; ++q) {
+      if (base + q * JOIN_THREADS + threadIdx.x < n) table_insert<H>(slots, cnt32, cap, r[q], error);
     }
-    if (!done) atomicOr(error, 2u);  // livelock guard (reported as a kernel failure)
-    cur = nxt;
-    i = inext;
   }
   __syncthreads();
+}
+
+constexpr uint32_t NO_SLOT = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint32_t slot_count(const uint32_t* cnt32, uint32_t s) {
+  return (cnt32[s >> 1] >> ((s & 1u) * 16)) & 0xFFFFu;
+}
+
+// slot holding key, or NO_SLOT
+template <typename H>
+__device__ __forceinline__ uint32_t table_find(const Slot<H>* slots, uint32_t cap, H key) {
+  uint32_t s = static_cast<uint32_t>((static_cast<uint64_t>(slot_hash<H>(key)) * cap) >> 32);
+  for (uint32_t guard = 0; guard <= cap; ++guard) {
+    const Slot<H> sl = slots[s];
+    if (sl.state == SLOT_EMPTY) return NO_SLOT;
+    if (sl.key == key) return s;
+    s = (s + 1 == cap) ? 0 : s + 1;
+  }
+  return NO_SLOT;
 }
 
 // (state, count) of key in the table (count = build rows with this key)
@@ -601,27 +641,22 @@ __device__ __forceinline__ void table_lookup(const Slot<H>* slots, const uint32_
   }
 }
 
-// Decoupled look-back across partitions (ticket order = partition order). Returns this partition's output offset;
-// the block must not write when offset + total exceeds the capacity (the overflow flag is raised instead).
-__device__ __forceinline__ uint64_t partition_base(const JoinDesc& d, uint32_t p, uint32_t part_total,
-                                                   uint64_t* __restrict__ part_out_begin,
-                                                   uint32_t* __restrict__ part_out_count, uint64_t* s_base) {
-  if (threadIdx.x < WAVE) {
-    uint64_t prefix = 0;
-    if (p == 0) {
-      if (threadIdx.x == 0) lb_publish(&d.status[0], LB_FLAG_PREFIX, part_total);
-    } else {
-      if (threadIdx.x == 0) lb_publish(&d.status[p], LB_FLAG_AGG, part_total);
-      prefix = lb_lookback_wave(d.status, 0, p, d.error);
-      if (threadIdx.x == 0) lb_publish(&d.status[p], LB_FLAG_PREFIX, prefix + part_total);
-    }
-    if (threadIdx.x == 0) {
-      *s_base = prefix;
-      part_out_begin[p] = prefix;
-      part_out_count[p] = part_total;
-      if (p == d.n_parts - 1) *d.total = prefix + part_total;
-      if (prefix + part_total > d.capacity) atomicOr(d.overflow, 1u);
-    }
+// Reserves this partition's output range with one atomic add on the running total. The reference emits one output
+// chunk per partition, each with its own PosList (join_hash.cpp:571-590), so partition ranges need not follow
+// partition order in the buffer: part_out_begin/count locate each one. Nothing waits on another partition.
+// Returns the range start; the block must not write when it ends beyond the capacity (overflow is raised instead,
+// and *total still reaches the exact number of pairs required).
+__device__ __forceinline__ uint64_t allocate_output(const JoinDesc& d, uint32_t p, uint32_t part_total,
+                                                    uint64_t* __restrict__ part_out_begin,
+                                                    uint32_t* __restrict__ part_out_count, uint64_t* s_base) {
+  if (threadIdx.x == 0) {
+    const uint64_t base =
+        part_total ? atomicAdd(reinterpret_cast<unsigned long long*>(d.total), static_cast<unsigned long long>(part_total))
+                   : 0ull;
+    *s_base = base;
+    part_out_begin[p] = base;
+    part_out_count[p] = part_total;
+    if (base + part_total > d.capacity) atomicOr(d.overflow, 1u);
   }
   __syncthreads();
   return *s_base;
@@ -687,7 +722,7 @@ __device__ __forceinline__ void write_duplicates(const JoinDesc& d, const Rec<H>
 
 // A partition whose build side fits one LDS table (the common case): the table is built once and every probe
 // record's (state, count) stays in registers from counting to writing.
-template <typename H>
+template <typename H, bool TRACE, int JP>
 __device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t p, unsigned char* smem,
                                                     const Rec<H>* __restrict__ build,
                                                     const Rec<H>* __restrict__ probe, hy_row_id* __restrict__ out_build,
@@ -702,63 +737,71 @@ __device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t 
   Slot<H>* slots = reinterpret_cast<Slot<H>*>(smem);
   uint32_t* cnt32 = reinterpret_cast<uint32_t*>(smem + sizeof(Slot<H>) * cap);
   build_table<H>(slots, cnt32, cap, build, bb, nb, d.error);
+  trace_stamp<TRACE>(d, p, 1);
 
-  const uint32_t n_pass = (np + JP_PASS - 1) / JP_PASS;
-  Rec<H> pr[JP_PER];
-  uint32_t pst[JP_PER], pcn[JP_PER];
+  // Per probe record only its payload and matched slot stay in registers; count, state and key are re-read from
+  // the LDS table when needed.
+  constexpr uint32_t JP_PASS_ = JP * JOIN_THREADS;
+  const uint32_t n_pass = (np + JP_PASS_ - 1) / JP_PASS_;
+  uint32_t ppay[JP], pslot[JP];
   auto load_and_match = [&](uint32_t pass) {
+    Rec<H> pr[JP];
 #pragma unroll
-    for (int k = 0; k < JP_PER; ++k) {
-      const uint32_t j = pass * JP_PASS + k * JOIN_THREADS + threadIdx.x;
+    for (int k = 0; k < JP; ++k) {
+      const uint32_t j = pass * JP_PASS_ + k * JOIN_THREADS + threadIdx.x;
       if (j < np) pr[k] = probe[pb + j];
     }
 #pragma unroll
-    for (int k = 0; k < JP_PER; ++k) {
-      const uint32_t j = pass * JP_PASS + k * JOIN_THREADS + threadIdx.x;
-      pst[k] = 0;
-      pcn[k] = 0;
-      if (j < np && nb > 0) table_lookup<H>(slots, cnt32, cap, pr[k].key, &pst[k], &pcn[k]);
+    for (int k = 0; k < JP; ++k) {
+      const uint32_t j = pass * JP_PASS_ + k * JOIN_THREADS + threadIdx.x;
+      ppay[k] = pr[k].payload;
+      pslot[k] = (j < np && nb > 0) ? table_find<H>(slots, cap, pr[k].key) : NO_SLOT;
     }
   };
+  auto count_of = [&](uint32_t slot) { return slot == NO_SLOT ? 0u : slot_count(cnt32, slot); };
 
   uint32_t my = 0;
   for (uint32_t pass = 0; pass < n_pass; ++pass) {
     load_and_match(pass);
 #pragma unroll
-    for (int k = 0; k < JP_PER; ++k) {
-      const uint32_t j = pass * JP_PASS + k * JOIN_THREADS + threadIdx.x;
-      if (j < np) my += emitted_for(mode, pcn[k]);
+    for (int k = 0; k < JP; ++k) {
+      const uint32_t j = pass * JP_PASS_ + k * JOIN_THREADS + threadIdx.x;
+      if (j < np) my += emitted_for(mode, count_of(pslot[k]));
     }
   }
+  trace_stamp<TRACE>(d, p, 2);
   uint32_t part_total;
   block_exclusive_sum<JOIN_THREADS>(my, s_tot, &part_total);
-  const uint64_t obase = partition_base(d, p, part_total, part_out_begin, part_out_count, s_base);
+  const uint64_t obase = allocate_output(d, p, part_total, part_out_begin, part_out_count, s_base);
+  trace_stamp<TRACE>(d, p, 3);
   if (obase + part_total > d.capacity) return;
 
   uint64_t run = obase;
   for (uint32_t pass = 0; pass < n_pass; ++pass) {
     if (n_pass > 1) load_and_match(pass);  // a single pass still holds its records and matches in registers
     auto e_of = [&](int k) {
-      const uint32_t j = pass * JP_PASS + k * JOIN_THREADS + threadIdx.x;
-      return j < np ? emitted_for(mode, pcn[k]) : 0u;
+      const uint32_t j = pass * JP_PASS_ + k * JOIN_THREADS + threadIdx.x;
+      return j < np ? emitted_for(mode, count_of(pslot[k])) : 0u;
     };
-    const uint32_t pass_total = pass_offsets<JP_PER>(e_of, s_tot);
+    const uint32_t pass_total = pass_offsets<JP>(e_of, s_tot);
 #pragma unroll
-    for (int k = 0; k < JP_PER; ++k) {
-      const uint32_t e = e_of(k);
-      const uint64_t o = run + record_pos<JP_PER>(e, k, s_tot);
+    for (int k = 0; k < JP; ++k) {
+      const uint32_t c = count_of(pslot[k]);
+      const uint32_t j = pass * JP_PASS_ + k * JOIN_THREADS + threadIdx.x;
+      const uint32_t e = j < np ? emitted_for(mode, c) : 0u;
+      const uint64_t o = run + record_pos<JP>(e, k, s_tot);
       if (e == 0) continue;
-      const hy_row_id prow = map_row(d.probe_map, pr[k].payload);
+      const hy_row_id prow = map_row(d.probe_map, ppay[k]);
       if (mode == HY_JOIN_SEMI || mode == HY_JOIN_ANTI) {
         out_probe[o] = prow;
-      } else if (pcn[k] == 0) {  // outer: probe row without a match
+      } else if (c == 0) {  // outer: probe row without a match
         out_build[o] = hy_row_id{0xFFFFFFFFu, 0xFFFFFFFFu};
         out_probe[o] = prow;
-      } else if (pcn[k] == 1) {
-        out_build[o] = map_row(d.build_map, pst[k] - 1);
+      } else if (c == 1) {
+        out_build[o] = map_row(d.build_map, slots[pslot[k]].state - 1);
         out_probe[o] = prow;
       } else {
-        write_duplicates<H>(d, build, bb, nb, pr[k].key, pcn[k], prow, o, out_build, out_probe);
+        write_duplicates<H>(d, build, bb, nb, slots[pslot[k]].key, c, prow, o, out_build, out_probe);
       }
     }
     run += pass_total;
@@ -769,7 +812,7 @@ __device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t 
 // A partition with more build rows than one LDS table holds (skewed keys): consecutive sub-tables of L build rows.
 // Counts are summed over the sub-tables; matches are written sub-table by sub-table, i.e. in build order. Each
 // probe pass rebuilds the sub-tables twice (count, write), a cost only skewed partitions pay.
-template <typename H>
+template <typename H, bool TRACE>
 __device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t p, unsigned char* smem,
                                                   const Rec<H>* __restrict__ build, const Rec<H>* __restrict__ probe,
                                                   hy_row_id* __restrict__ out_build, hy_row_id* __restrict__ out_probe,
@@ -822,9 +865,11 @@ __device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t
       if (j < np) my += emitted_for(mode, pcn[k]);
     }
   }
+  trace_stamp<TRACE>(d, p, 2);
   uint32_t part_total;
   block_exclusive_sum<JOIN_THREADS>(my, s_tot, &part_total);
-  const uint64_t obase = partition_base(d, p, part_total, part_out_begin, part_out_count, s_base);
+  const uint64_t obase = allocate_output(d, p, part_total, part_out_begin, part_out_count, s_base);
+  trace_stamp<TRACE>(d, p, 3);
   if (obase + part_total > d.capacity) return;
 
   uint64_t run = obase;
@@ -877,7 +922,7 @@ __device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t
   }
 }
 
-template <typename H>
+template <typename H, bool TRACE, int JP>
 __global__ __launch_bounds__(JOIN_THREADS) void join_partition(JoinDesc d, const Rec<H>* __restrict__ build,
                                                                const Rec<H>* __restrict__ probe,
                                                                hy_row_id* __restrict__ out_build,
@@ -885,19 +930,18 @@ __global__ __launch_bounds__(JOIN_THREADS) void join_partition(JoinDesc d, const
                                                                uint64_t* __restrict__ part_out_begin,
                                                                uint32_t* __restrict__ part_out_count) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ uint32_t s_tot[JP_PER * JOIN_WAVES + 1];
-  __shared__ uint32_t s_part;
+  __shared__ uint32_t s_tot[(JP > JP_PER ? JP : JP_PER) * JOIN_WAVES + 1];
   __shared__ uint64_t s_base;
-  if (threadIdx.x == 0) s_part = atomicAdd(d.ticket, 1u);
-  __syncthreads();
-  const uint32_t p = s_part;
+  const uint32_t p = blockIdx.x;
   if (p >= d.n_parts) return;
+  trace_stamp<TRACE>(d, p, 0);
   if (d.build_begin[p + 1] - d.build_begin[p] <= d.lds_max_build)
-    partition_one_table<H>(d, p, smem, build, probe, out_build, out_probe, part_out_begin, part_out_count, s_tot,
+    partition_one_table<H, TRACE, JP>(d, p, smem, build, probe, out_build, out_probe, part_out_begin, part_out_count, s_tot,
                            &s_base);
   else
-    partition_sub_tables<H>(d, p, smem, build, probe, out_build, out_probe, part_out_begin, part_out_count, s_tot,
+    partition_sub_tables<H, TRACE>(d, p, smem, build, probe, out_build, out_probe, part_out_begin, part_out_count, s_tot,
                             &s_base);
+  trace_stamp<TRACE>(d, p, 4);
 }
 
 __global__ void murmur_kernel_u32(const uint32_t* keys, uint64_t n, uint32_t seed, uint32_t* out) {

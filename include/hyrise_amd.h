@@ -67,6 +67,12 @@ hy_status hy_kernel_stats_reset(void);
 hy_status hy_kernel_stats_collect(uint32_t* n_kernels);
 hy_status hy_kernel_stats_get(uint32_t index, const char** name, uint64_t* launches, double* total_ms,
                               uint64_t* units);
+/*
+ * Debug: per-partition phase trace of the next hy_join_hash calls (NULL turns it off). When set, the first thread
+ * of each partition's workgroup stores 5 wall-clock stamps (100 MHz device clock) at trace[5 * partition + i]:
+ * entry, table built, probe counted, output offset known (look-back done), exit. Costs one scalar branch.
+ */
+hy_status hy_debug_set_join_trace(uint64_t* device_trace);
 /* Thread-local message of the last failing call. */
 const char* hy_last_error_message(void);
 /* Build identification ("gfx950 …"). */
