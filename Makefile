@@ -13,15 +13,24 @@ EXTSUF    := $(shell $(PY) -c "import sysconfig;print(sysconfig.get_config_var('
 CXXFLAGS  := -std=c++17 -O2 -fPIC -Wall -Wno-unused-function -Iinclude -I$(CSRC)/host
 HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude
 
-HOST_SRC  := $(CSRC)/host/storage.cpp $(CSRC)/host/device.cpp $(CSRC)/host/operators.cpp
+HOST_SRC  := $(CSRC)/host/storage.cpp $(CSRC)/host/device.cpp $(CSRC)/host/operators.cpp $(CSRC)/host/aggregate.cpp
 HOST_HDR  := $(wildcard $(CSRC)/host/*.hpp) include/hyrise_amd.h
-KERN_SRC  := $(CSRC)/capi/hyrise_amd.hip $(wildcard $(CSRC)/kernels/*.hip) $(wildcard $(CSRC)/kernels/*.hpp)
 
 all: $(LIB)/libhyrise_amd.so $(LIB)/libhyrise_host.so $(LIB)/_hyrise_host$(EXTSUF)
 
-$(LIB)/libhyrise_amd.so: $(KERN_SRC) include/hyrise_amd.h
+CAPI_HDR  := include/hyrise_amd.h $(CSRC)/capi/capi_common.hpp $(CSRC)/kernels/common.hpp
+
+# one object per C-ABI translation unit (they compile in parallel under make -j)
+$(LIB)/hyrise_amd.o: $(CSRC)/capi/hyrise_amd.hip $(CSRC)/kernels/scan.hip $(CSRC)/kernels/join.hip $(CAPI_HDR)
 	@mkdir -p $(LIB)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(CSRC)/capi/hyrise_amd.hip
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIB)/hyrise_amd_aggregate.o: $(CSRC)/capi/hyrise_amd_aggregate.hip $(CSRC)/kernels/aggregate.hip $(CAPI_HDR)
+	@mkdir -p $(LIB)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIB)/libhyrise_amd.so: $(LIB)/hyrise_amd.o $(LIB)/hyrise_amd_aggregate.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 $(LIB)/libhyrise_host.so: $(HOST_SRC) $(HOST_HDR) $(LIB)/libhyrise_amd.so
 	$(CXX) $(CXXFLAGS) -shared -o $@ $(HOST_SRC) -L$(LIB) -lhyrise_amd -Wl,-rpath,'$$ORIGIN'

@@ -19,6 +19,8 @@ HY_TYPE_INT32, HY_TYPE_INT64, HY_TYPE_FLOAT, HY_TYPE_DOUBLE = 1, 2, 3, 4
 HY_COL_VALUE, HY_COL_DICT = 0, 1
 HY_OP_EQ, HY_OP_NE, HY_OP_LT, HY_OP_LE, HY_OP_GT, HY_OP_GE, HY_OP_ALL, HY_OP_NONE = range(8)
 HY_JOIN_INNER, HY_JOIN_LEFT, HY_JOIN_RIGHT, HY_JOIN_SEMI, HY_JOIN_ANTI = 0, 1, 2, 5, 6
+HY_AGG_MIN, HY_AGG_MAX, HY_AGG_SUM, HY_AGG_AVG, HY_AGG_COUNT, HY_AGG_COUNT_DISTINCT = range(6)
+HY_AGG_MAX_AGGREGATES = 16
 
 
 class RowID(ctypes.Structure):
@@ -56,6 +58,34 @@ class JoinResult(ctypes.Structure):
     _fields_ = [("total_pairs", ctypes.c_uint64), ("capacity_required", ctypes.c_uint64)]
 
 
+class AggColumn(ctypes.Structure):
+    _fields_ = [("value_type", ctypes.c_int32), ("pos_group", ctypes.c_int32), ("chunks", ctypes.POINTER(ColumnChunk)),
+                ("n_chunks", ctypes.c_uint32), ("domain", ctypes.c_uint32)]
+
+
+class AggInput(ctypes.Structure):
+    _fields_ = [("n_chunks", ctypes.c_uint32), ("chunk_sizes", ctypes.POINTER(ctypes.c_uint32)),
+                ("pos_lists", ctypes.POINTER(ctypes.c_void_p)), ("n_pos_groups", ctypes.c_uint32),
+                ("columns", ctypes.POINTER(AggColumn)), ("n_columns", ctypes.c_uint32)]
+
+
+class AggDef(ctypes.Structure):
+    _fields_ = [("function", ctypes.c_int32), ("column", ctypes.c_int32)]
+
+
+class AggParams(ctypes.Structure):
+    _fields_ = [("groupby", ctypes.POINTER(ctypes.c_int32)), ("n_groupby", ctypes.c_uint32),
+                ("aggregates", ctypes.POINTER(AggDef)), ("n_aggregates", ctypes.c_uint32),
+                ("group_bound", ctypes.c_uint64)]
+
+
+class AggLayout(ctypes.Structure):
+    _fields_ = [("words", ctypes.c_uint32), ("dense", ctypes.c_uint32),
+                ("agg_word", ctypes.c_uint32 * HY_AGG_MAX_AGGREGATES),
+                ("agg_emin", ctypes.c_int32 * HY_AGG_MAX_AGGREGATES),
+                ("agg_limbs", ctypes.c_uint32 * HY_AGG_MAX_AGGREGATES)]
+
+
 _sigs = {
     "hy_get_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "hy_set_device": (ctypes.c_int, [ctypes.c_int]),
@@ -77,6 +107,16 @@ _sigs = {
                                     ctypes.c_void_p]),
     "hy_expand_row_ids": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                          ctypes.c_void_p]),
+    "hy_aggregate_layout": (ctypes.c_int, [ctypes.POINTER(AggInput), ctypes.POINTER(AggParams),
+                                           ctypes.POINTER(AggLayout)]),
+    "hy_aggregate_workspace_size": (ctypes.c_int, [ctypes.POINTER(AggInput), ctypes.POINTER(AggParams),
+                                                   ctypes.POINTER(ctypes.c_size_t)]),
+    "hy_aggregate": (ctypes.c_int, [ctypes.POINTER(AggInput), ctypes.POINTER(AggParams), ctypes.c_void_p,
+                                    ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p,
+                                    ctypes.c_size_t, ctypes.c_void_p]),
+    "hy_agg_float_sum": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32, ctypes.c_int32,
+                                        ctypes.c_uint64, ctypes.POINTER(ctypes.c_double)]),
+    "hy_agg_decode_ordered": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_int32]),
 }
 for _name, (_res, _args) in _sigs.items():
     _f = getattr(lib, _name)
@@ -96,7 +136,7 @@ def check(status, what=""):
 def declared_symbols():
     """Entry points declared in include/hyrise_amd.h."""
     text = open(HEADER_PATH).read()
-    return sorted(set(re.findall(r"^\s*(?:hy_status|uint32_t|const char\*)\s+(hy_\w+)\s*\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:hy_status|uint32_t|uint64_t|const char\*)\s+(hy_\w+)\s*\(", text, re.M)))
 
 
 def device_count():

@@ -1,0 +1,107 @@
+// Shared host-side plumbing of the C-ABI translation units: error reporting, workspace carving and per-kernel
+// HIP-event timing. State lives in hyrise_amd.hip; every other TU only includes this header.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "hyrise_amd.h"
+
+namespace hyc {
+
+extern thread_local std::string g_last_error;
+
+inline hy_status fail(hy_status code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define HY_HIP(call)                                                                                       \
+  do {                                                                                                     \
+    hipError_t e_ = (call);                                                                                \
+    if (e_ != hipSuccess) return ::hyc::fail(HY_ERR_DEVICE, std::string(#call) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+inline hipStream_t S(hy_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// Bump allocator over the caller's workspace. Every carve is 256-byte aligned.
+struct Carver {
+  char* base;
+  size_t cap;
+  size_t used = 0;
+  bool ok = true;
+  template <typename T>
+  T* take(size_t count) {
+    used = (used + 255) & ~size_t(255);
+    T* p = reinterpret_cast<T*>(base ? base + used : nullptr);
+    used += count * sizeof(T);
+    if (base && used > cap) ok = false;
+    return p;
+  }
+};
+
+// ---- per-kernel timing (HIP events on the launching stream), enabled by hy_kernel_stats_enable ----
+struct KernelTiming {
+  std::string name;
+  hipEvent_t start, stop;
+  uint64_t units;
+};
+struct KStat {
+  uint64_t count = 0;
+  double total_ms = 0;
+  uint64_t units = 0;
+};
+extern std::mutex g_kt_mutex;
+extern uint64_t* g_join_trace;  // hy_debug_set_join_trace
+extern bool g_kt_enabled;
+extern std::vector<KernelTiming> g_kt_pending;
+extern std::vector<hipEvent_t> g_kt_pool;
+extern std::vector<std::pair<std::string, KStat>> g_kt_stats;
+
+inline hipEvent_t kt_event() {
+  if (!g_kt_pool.empty()) {
+    hipEvent_t e = g_kt_pool.back();
+    g_kt_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+// Brackets one kernel launch: KTimer t("name", stream, units); launch; t.done();
+struct KTimer {
+  bool on;
+  KernelTiming kt;
+  hipStream_t s;
+  KTimer(const char* name, hipStream_t stream, uint64_t units) : on(false), s(stream) {
+    std::lock_guard<std::mutex> lock(g_kt_mutex);
+    if (!g_kt_enabled) return;
+    on = true;
+    kt.name = name;
+    kt.units = units;
+    kt.start = kt_event();
+    kt.stop = kt_event();
+    (void)hipEventRecord(kt.start, s);
+  }
+  void done() {
+    if (!on) return;
+    (void)hipEventRecord(kt.stop, s);
+    std::lock_guard<std::mutex> lock(g_kt_mutex);
+    g_kt_pending.push_back(kt);
+    on = false;
+  }
+};
+
+inline int grid_for(uint64_t n, int threads) {
+  const uint64_t g = (n + threads - 1) / threads;
+  return static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(g, 256 * 16)));
+}
+
+}  // namespace hyc

@@ -1,0 +1,378 @@
+// C-ABI implementation of the Aggregate entry points (include/hyrise_amd.h): record layout, workspace carving,
+// dense / hash path selection and the launches of kernels/aggregate.hip. Host helpers round exact limb sums.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "capi_common.hpp"
+#include "../kernels/aggregate.hip"
+
+using namespace hyc;
+
+namespace {
+
+uint64_t next_pow2(uint64_t v) {
+  uint64_t p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+struct AggPlan {
+  hyk::AggDesc d{};
+  std::vector<int32_t> word_op;
+  hy_agg_layout layout{};
+  uint64_t rows = 0;
+  uint64_t n_tiles = 0;
+  uint32_t dense_groups = 0;  // > 0: dense path
+  uint64_t cap = 0, dcap = 0;
+  bool distinct = false;
+};
+
+hy_status make_plan(const hy_agg_input* in, const hy_agg_params* p, AggPlan* plan) {
+  if (!in || !p || !plan) return fail(HY_ERR_INVALID_ARGUMENT, "null argument");
+  if (in->n_columns > hyk::AGG_MAX_COLUMNS) return fail(HY_ERR_UNSUPPORTED, "too many aggregate input columns");
+  if (p->n_groupby > hyk::AGG_MAX_GROUPBY) return fail(HY_ERR_UNSUPPORTED, "too many group-by columns");
+  if (p->n_aggregates > hyk::AGG_MAX_AGGREGATES) return fail(HY_ERR_UNSUPPORTED, "too many aggregates");
+  if (in->n_pos_groups > hyk::AGG_MAX_POS_GROUPS) return fail(HY_ERR_UNSUPPORTED, "too many PosList groups");
+  if (in->n_pos_groups && in->n_chunks && !in->pos_lists) return fail(HY_ERR_INVALID_ARGUMENT, "pos_lists missing");
+  if (in->n_chunks && !in->chunk_sizes) return fail(HY_ERR_INVALID_ARGUMENT, "chunk_sizes missing");
+  auto& d = plan->d;
+  d.n_cols = in->n_columns;
+  d.n_fns = p->n_aggregates;
+  d.n_gb = p->n_groupby;
+  d.n_pos_groups = in->n_pos_groups;
+  d.n_chunks = in->n_chunks;
+  for (uint32_t j = 0; j < in->n_columns; ++j) {
+    const auto& c = in->columns[j];
+    if (c.value_type < HY_TYPE_INT32 || c.value_type > HY_TYPE_DOUBLE) return fail(HY_ERR_UNSUPPORTED, "column type");
+    if (c.pos_group >= static_cast<int32_t>(in->n_pos_groups)) return fail(HY_ERR_INVALID_ARGUMENT, "pos_group");
+    if (c.pos_group < 0 && c.n_chunks != in->n_chunks)
+      return fail(HY_ERR_INVALID_ARGUMENT, "data column must have one chunk per input chunk");
+    d.cols[j].type = c.value_type;
+    d.cols[j].pos_group = c.pos_group;
+    d.cols[j].domain = c.domain;
+  }
+  // record layout
+  const uint32_t H = p->n_groupby;
+  uint32_t w = H + hyk::AGG_HDR_WORDS;
+  plan->word_op.assign(w, hyk::WOP_KEY);
+  plan->word_op[H + hyk::AGG_HDR_FIRST] = hyk::WOP_MIN;
+  plan->word_op[H + hyk::AGG_HDR_LAST] = hyk::WOP_MAX;
+  plan->word_op[H + hyk::AGG_HDR_ROWS] = hyk::WOP_ADD;
+  auto& L = plan->layout;
+  for (uint32_t a = 0; a < p->n_aggregates; ++a) {
+    const auto& def = p->aggregates[a];
+    auto& fn = d.fns[a];
+    fn.function = def.function;
+    fn.column = def.column;
+    fn.word = w;
+    fn.limbs = 0;
+    L.agg_word[a] = w;
+    L.agg_emin[a] = 0;
+    L.agg_limbs[a] = 0;
+    if (def.function < HY_AGG_MIN || def.function > HY_AGG_COUNT_DISTINCT)
+      return fail(HY_ERR_INVALID_ARGUMENT, "aggregate function");
+    if (def.column < 0) {
+      if (def.function != HY_AGG_COUNT) return fail(HY_ERR_INVALID_ARGUMENT, "only COUNT may have no column");
+      continue;  // COUNT(*): the rows word
+    }
+    if (def.column >= static_cast<int32_t>(in->n_columns)) return fail(HY_ERR_INVALID_ARGUMENT, "aggregate column");
+    const int32_t type = in->columns[def.column].value_type;
+    plan->word_op.push_back(hyk::WOP_ADD);  // count
+    switch (def.function) {
+      case HY_AGG_MIN:
+        plan->word_op.push_back(hyk::WOP_MIN);
+        break;
+      case HY_AGG_MAX:
+        plan->word_op.push_back(hyk::WOP_MAX);
+        break;
+      case HY_AGG_SUM:
+      case HY_AGG_AVG:
+        if (type == HY_TYPE_FLOAT || type == HY_TYPE_DOUBLE) {
+          const bool f = type == HY_TYPE_FLOAT;
+          fn.limbs = f ? hyk::FLOAT_LIMBS : hyk::DOUBLE_LIMBS;
+          L.agg_limbs[a] = fn.limbs;
+          L.agg_emin[a] = f ? hyk::FLOAT_EMIN : hyk::DOUBLE_EMIN;
+          plan->word_op.push_back(hyk::WOP_OR);
+          for (int l = 0; l < fn.limbs; ++l) plan->word_op.push_back(hyk::WOP_ADD);
+        } else {
+          plan->word_op.push_back(hyk::WOP_ADD);
+        }
+        break;
+      case HY_AGG_COUNT_DISTINCT:
+        plan->distinct = true;
+        break;
+      default:
+        break;
+    }
+    w = static_cast<uint32_t>(plan->word_op.size());
+  }
+  d.words = static_cast<uint32_t>(plan->word_op.size());
+  L.words = d.words;
+  for (uint32_t j = 0; j < p->n_groupby; ++j) {
+    if (p->groupby[j] < 0 || p->groupby[j] >= static_cast<int32_t>(in->n_columns))
+      return fail(HY_ERR_INVALID_ARGUMENT, "group-by column");
+    d.gb[j] = p->groupby[j];
+  }
+  // rows and tiles
+  for (uint32_t c = 0; c < in->n_chunks; ++c) {
+    plan->rows += in->chunk_sizes[c];
+    plan->n_tiles += (in->chunk_sizes[c] + hyk::AGG_TILE - 1) / hyk::AGG_TILE;
+  }
+  d.n_tiles = plan->n_tiles;
+  // dense path: every group-by column has a code domain, the mixed-radix index fits a wave's 64 lanes and the
+  // records fit the LDS budget
+  uint64_t groups = 1;
+  bool dense = !plan->distinct;
+  for (uint32_t j = 0; j < p->n_groupby && dense; ++j) {
+    const auto& c = in->columns[p->groupby[j]];
+    if (c.domain == 0 || (c.value_type != HY_TYPE_INT32 && c.value_type != HY_TYPE_INT64)) dense = false;
+    groups *= static_cast<uint64_t>(c.domain) + 1;
+    if (groups > hyk::AGG_DENSE_MAX) dense = false;
+  }
+  if (dense && groups * d.words > hyk::AGG_DENSE_LDS_WORDS) dense = false;
+  if (dense) {
+    uint32_t stride = 1;
+    for (uint32_t j = 0; j < p->n_groupby; ++j) {
+      auto& col = d.cols[d.gb[j]];
+      col.stride = stride;
+      stride *= col.domain + 1;
+    }
+    plan->dense_groups = static_cast<uint32_t>(groups);
+  }
+  L.dense = dense ? 1 : 0;
+  const uint64_t bound = p->group_bound ? std::min<uint64_t>(p->group_bound, plan->rows) : plan->rows;
+  plan->cap = next_pow2(std::max<uint64_t>(64, 2 * bound));
+  plan->dcap = plan->distinct ? next_pow2(std::max<uint64_t>(64, 2 * plan->rows * p->n_aggregates)) : 0;
+  return HY_OK;
+}
+
+// Workspace carve (sizes only when base == nullptr).
+struct AggWs {
+  uint32_t* sizes;
+  uint64_t* row_begin;
+  uint64_t* tile_begin;
+  const hy_row_id** pos_lists;
+  hy_column_chunk* chunks[hyk::AGG_MAX_COLUMNS];
+  int32_t* word_op;
+  uint32_t* misc;  // [0] error, [2..3] n_out (u64)
+  uint32_t* state;
+  unsigned long long* records;
+  uint32_t* dstate;
+  unsigned long long* dkeys;
+};
+
+void carve(Carver& cv, const hy_agg_input* in, const AggPlan& plan, AggWs* w) {
+  w->sizes = cv.take<uint32_t>(std::max<uint32_t>(1, in->n_chunks));
+  w->row_begin = cv.take<uint64_t>(in->n_chunks + 1);
+  w->tile_begin = cv.take<uint64_t>(in->n_chunks + 1);
+  w->pos_lists = cv.take<const hy_row_id*>(std::max<uint64_t>(1, uint64_t(in->n_pos_groups) * in->n_chunks));
+  for (uint32_t j = 0; j < in->n_columns; ++j)
+    w->chunks[j] = cv.take<hy_column_chunk>(std::max<uint32_t>(1, in->columns[j].n_chunks));
+  w->word_op = cv.take<int32_t>(plan.word_op.size());
+  w->misc = cv.take<uint32_t>(64);
+  if (plan.dense_groups) {
+    w->state = nullptr;
+    w->records = cv.take<unsigned long long>(uint64_t(plan.dense_groups) * plan.d.words);
+    w->dstate = nullptr;
+    w->dkeys = nullptr;
+  } else {
+    w->state = cv.take<uint32_t>(plan.cap);
+    w->records = cv.take<unsigned long long>(plan.cap * plan.d.words);
+    w->dstate = plan.dcap ? cv.take<uint32_t>(plan.dcap) : nullptr;
+    w->dkeys = plan.dcap ? cv.take<unsigned long long>(2 * plan.dcap) : nullptr;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+hy_status hy_aggregate_layout(const hy_agg_input* input, const hy_agg_params* params, hy_agg_layout* layout) {
+  if (!layout) return fail(HY_ERR_INVALID_ARGUMENT, "null layout");
+  AggPlan plan;
+  const hy_status st = make_plan(input, params, &plan);
+  if (st != HY_OK) return st;
+  *layout = plan.layout;
+  return HY_OK;
+}
+
+hy_status hy_aggregate_workspace_size(const hy_agg_input* input, const hy_agg_params* params, size_t* bytes) {
+  if (!bytes) return fail(HY_ERR_INVALID_ARGUMENT, "null bytes");
+  AggPlan plan;
+  const hy_status st = make_plan(input, params, &plan);
+  if (st != HY_OK) return st;
+  Carver cv{nullptr, 0};
+  AggWs w;
+  carve(cv, input, plan, &w);
+  *bytes = cv.used + 256;
+  return HY_OK;
+}
+
+hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, uint64_t* out_records,
+                       uint64_t out_capacity, uint64_t* n_groups, void* workspace, size_t workspace_bytes,
+                       hy_stream_t stream) {
+  if (!n_groups) return fail(HY_ERR_INVALID_ARGUMENT, "null n_groups");
+  AggPlan plan;
+  hy_status st = make_plan(input, params, &plan);
+  if (st != HY_OK) return st;
+  hipStream_t s = S(stream);
+  Carver cv{static_cast<char*>(workspace), workspace_bytes};
+  AggWs w;
+  carve(cv, input, plan, &w);
+  if (!cv.ok || !workspace) return fail(HY_ERR_WORKSPACE, "aggregate workspace too small");
+  auto& d = plan.d;
+  // descriptors
+  std::vector<uint64_t> row_begin(input->n_chunks + 1, 0), tile_begin(input->n_chunks + 1, 0);
+  for (uint32_t c = 0; c < input->n_chunks; ++c) {
+    row_begin[c + 1] = row_begin[c] + input->chunk_sizes[c];
+    tile_begin[c + 1] = tile_begin[c] + (input->chunk_sizes[c] + hyk::AGG_TILE - 1) / hyk::AGG_TILE;
+  }
+  if (input->n_chunks) {
+    HY_HIP(hipMemcpyAsync(w.sizes, input->chunk_sizes, 4 * input->n_chunks, hipMemcpyHostToDevice, s));
+    HY_HIP(hipMemcpyAsync(w.row_begin, row_begin.data(), 8 * row_begin.size(), hipMemcpyHostToDevice, s));
+    HY_HIP(hipMemcpyAsync(w.tile_begin, tile_begin.data(), 8 * tile_begin.size(), hipMemcpyHostToDevice, s));
+  }
+  const uint64_t n_pl = uint64_t(input->n_pos_groups) * input->n_chunks;
+  if (n_pl) HY_HIP(hipMemcpyAsync(w.pos_lists, input->pos_lists, sizeof(void*) * n_pl, hipMemcpyHostToDevice, s));
+  for (uint32_t j = 0; j < input->n_columns; ++j) {
+    const auto& c = input->columns[j];
+    for (uint32_t k = 0; k < c.n_chunks; ++k) {
+      const auto& ch = c.chunks[k];
+      if (ch.size && !ch.data) return fail(HY_ERR_INVALID_ARGUMENT, "column chunk without data");
+      if (ch.kind == HY_COL_DICT && ch.vid_width != 1 && ch.vid_width != 2 && ch.vid_width != 4)
+        return fail(HY_ERR_INVALID_ARGUMENT, "vid width");
+    }
+    if (c.n_chunks)
+      HY_HIP(hipMemcpyAsync(w.chunks[j], c.chunks, sizeof(hy_column_chunk) * c.n_chunks, hipMemcpyHostToDevice, s));
+    d.cols[j].chunks = w.chunks[j];
+  }
+  HY_HIP(hipMemcpyAsync(w.word_op, plan.word_op.data(), 4 * plan.word_op.size(), hipMemcpyHostToDevice, s));
+  HY_HIP(hipMemsetAsync(w.misc, 0, 256, s));
+  d.pos_lists = w.pos_lists;
+  d.chunk_size = w.sizes;
+  d.chunk_row_begin = w.row_begin;
+  d.chunk_tile_begin = w.tile_begin;
+  d.word_op = w.word_op;
+  d.error = w.misc;
+  auto* n_out = reinterpret_cast<unsigned long long*>(w.misc + 2);
+  auto* out = reinterpret_cast<unsigned long long*>(out_records);
+
+  if (plan.dense_groups) {
+    const uint64_t nw = uint64_t(plan.dense_groups) * d.words;
+    hipLaunchKernelGGL(hyk::agg_init_records, dim3(grid_for(nw, 256)), dim3(256), 0, s, w.records,
+                       uint64_t(plan.dense_groups), d.words, w.word_op);
+    HY_HIP(hipGetLastError());
+    if (plan.n_tiles) {
+      const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(plan.n_tiles, 256 * 8));
+      KTimer t("agg_dense_rows", s, plan.rows);
+      hipLaunchKernelGGL(hyk::agg_dense_rows, dim3(grid), dim3(hyk::AGG_THREADS), 0, s, d, plan.dense_groups,
+                         w.records);
+      t.done();
+      HY_HIP(hipGetLastError());
+    }
+    hipLaunchKernelGGL(hyk::agg_dense_compact, dim3((plan.dense_groups + 63) / 64), dim3(64), 0, s, d,
+                       plan.dense_groups, w.records, out, out_capacity, n_out);
+    HY_HIP(hipGetLastError());
+  } else {
+    hyk::AggTable t{w.state, w.records, plan.cap, w.dstate, w.dkeys, plan.dcap};
+    HY_HIP(hipMemsetAsync(w.state, 0, 4 * plan.cap, s));
+    if (plan.dcap) HY_HIP(hipMemsetAsync(w.dstate, 0, 4 * plan.dcap, s));
+    if (plan.n_tiles) {
+      KTimer kt("agg_hash_rows", s, plan.rows);
+      hipLaunchKernelGGL(hyk::agg_hash_rows, dim3(static_cast<uint32_t>(plan.n_tiles)), dim3(hyk::AGG_THREADS), 0, s,
+                         d, t);
+      kt.done();
+      HY_HIP(hipGetLastError());
+    }
+    hipLaunchKernelGGL(hyk::agg_hash_compact, dim3(grid_for(plan.cap, 256)), dim3(256), 0, s, d, t, out, out_capacity,
+                       n_out);
+    HY_HIP(hipGetLastError());
+  }
+  uint32_t misc[4] = {0, 0, 0, 0};
+  HY_HIP(hipMemcpyAsync(misc, w.misc, 16, hipMemcpyDeviceToHost, s));
+  HY_HIP(hipStreamSynchronize(s));
+  uint64_t n = 0;
+  std::memcpy(&n, misc + 2, 8);
+  *n_groups = n;
+  if (misc[0] & 2u) return fail(HY_ERR_INVALID_ARGUMENT, "dense group-by code outside its domain");
+  if (misc[0] & 1u) return fail(HY_ERR_KERNEL, "aggregate hash table full (group_bound too small?)");
+  if (n > out_capacity) return fail(HY_ERR_CAPACITY, "more groups than out_capacity");
+  return HY_OK;
+}
+
+hy_status hy_agg_float_sum(const uint64_t* limbs, uint32_t n_limbs, int32_t emin, uint64_t special, double* out) {
+  if (!out || (n_limbs && !limbs)) return fail(HY_ERR_INVALID_ARGUMENT, "null argument");
+  if ((special & 4u) || ((special & 1u) && (special & 2u))) {
+    *out = NAN;
+    return HY_OK;
+  }
+  if (special & 1u) {
+    *out = INFINITY;
+    return HY_OK;
+  }
+  if (special & 2u) {
+    *out = -INFINITY;
+    return HY_OK;
+  }
+  // carry-normalise the signed limbs into base-2^32 digits of a two's complement integer
+  std::vector<uint32_t> dig(n_limbs + 3, 0);
+  __int128 carry = 0;
+  for (uint32_t i = 0; i < n_limbs + 3; ++i) {
+    const __int128 t = carry + (i < n_limbs ? static_cast<__int128>(static_cast<int64_t>(limbs[i])) : 0);
+    dig[i] = static_cast<uint32_t>(static_cast<unsigned __int128>(t) & 0xFFFFFFFFu);
+    carry = t >> 32;  // arithmetic
+  }
+  const bool neg = carry < 0;
+  if (neg) {  // magnitude = two's complement negation
+    uint64_t c = 1;
+    for (auto& x : dig) {
+      const uint64_t v = static_cast<uint64_t>(static_cast<uint32_t>(~x)) + c;
+      x = static_cast<uint32_t>(v);
+      c = v >> 32;
+    }
+  }
+  int top = static_cast<int>(dig.size()) - 1;
+  while (top >= 0 && dig[top] == 0) --top;
+  if (top < 0) {
+    *out = 0.0;
+    return HY_OK;
+  }
+  // 64-bit window below the leading one, plus sticky bits
+  const int lead = 31 - __builtin_clz(dig[top]);
+  const int64_t msb = static_cast<int64_t>(top) * 32 + lead;  // bit index of the leading one
+  auto bit_at = [&](int64_t b) -> uint64_t {
+    if (b < 0) return 0;
+    return (dig[b >> 5] >> (b & 31)) & 1u;
+  };
+  uint64_t m = 0;
+  for (int64_t b = msb; b > msb - 64; --b) m = (m << 1) | bit_at(b);
+  bool sticky = false;
+  for (int64_t b = msb - 64; b >= 0 && !sticky; --b) sticky = bit_at(b) != 0;
+  // round the 64-bit window to 53 bits, nearest-even
+  const uint64_t low = m & 0x7FFu;
+  uint64_t mant = m >> 11;
+  if (low > 0x400u || (low == 0x400u && (sticky || (mant & 1u)))) ++mant;
+  const double v = std::ldexp(static_cast<double>(mant), static_cast<int>(msb - 52 + emin));
+  *out = neg ? -v : v;
+  return HY_OK;
+}
+
+uint64_t hy_agg_decode_ordered(uint64_t o, int32_t value_type) {
+  switch (value_type) {
+    case HY_TYPE_INT32:
+      return static_cast<uint32_t>(o) ^ 0x80000000u;
+    case HY_TYPE_INT64:
+      return o ^ (1ull << 63);
+    case HY_TYPE_FLOAT: {
+      const uint32_t b = static_cast<uint32_t>(o);
+      return (b & 0x80000000u) ? (b & 0x7FFFFFFFu) : static_cast<uint32_t>(~b);
+    }
+    default:
+      return (o >> 63) ? (o & ~(1ull << 63)) : ~o;
+  }
+}
+
+}  // extern "C"

@@ -307,5 +307,6 @@ PYBIND11_MODULE(_hyrise_host, m) {
   py::class_<Aggregate, AbstractOperator, std::shared_ptr<Aggregate>>(m, "Aggregate")
       .def(py::init<std::shared_ptr<const AbstractOperator>, std::vector<AggregateColumnDefinition>,
                     std::vector<ColumnID>>(),
-           py::arg("input"), py::arg("aggregates"), py::arg("groupby_column_ids"));
+           py::arg("input"), py::arg("aggregates"), py::arg("groupby_column_ids"))
+      .def("used_dense_path", &Aggregate::used_dense_path);
 }

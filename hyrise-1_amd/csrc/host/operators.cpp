@@ -582,8 +582,4 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
   return output;
 }
 
-std::shared_ptr<const Table> Aggregate::_on_execute() {
-  Fail("hyrise-amd: Aggregate device path not built yet");
-}
-
 }  // namespace hyrise

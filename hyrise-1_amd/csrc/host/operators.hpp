@@ -145,6 +145,8 @@ class Aggregate final : public AbstractOperator {
   const std::string name() const override { return "Aggregate"; }
   const std::vector<AggregateColumnDefinition>& aggregates() const { return _aggregates; }
   const std::vector<ColumnID>& groupby_column_ids() const { return _groupby_column_ids; }
+  // device path of the last execution: true = dense (code-indexed LDS records), false = hash table in HBM
+  bool used_dense_path() const { return _used_dense_path; }
 
  protected:
   std::shared_ptr<const Table> _on_execute() override;
@@ -152,6 +154,7 @@ class Aggregate final : public AbstractOperator {
  private:
   std::vector<AggregateColumnDefinition> _aggregates;
   std::vector<ColumnID> _groupby_column_ids;
+  bool _used_dense_path = false;
 };
 
 // JoinHashTraits (reference src/lib/operators/join_hash/hash_traits.hpp:9-42) over data types.

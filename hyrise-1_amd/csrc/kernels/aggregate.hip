@@ -1,0 +1,595 @@
+// Aggregate kernels for gfx950: GROUP BY + MIN / MAX / SUM / AVG / COUNT / COUNT(*) / COUNT(DISTINCT).
+//
+// The reference (src/lib/operators/aggregate.cpp) first maps every group-by value to a first-seen id per column
+// (:291-394), then, chunk by chunk and aggregate by aggregate, upserts results[key] in a std::unordered_map and folds
+// the row's value in (_aggregate_column, :133-249, traits aggregate_traits.hpp:15-74). Its output order is the
+// unordered_map's, its group values are read back at each group's LAST row (:543-566, _write_groupby_output).
+//
+// Here one pass over the input rows produces, per group, a record of 64-bit words:
+//   [0, n_gb)     key words: the group-by values' bits (0 when NULL), floats with -0.0 folded into +0.0
+//   n_gb          NULL mask of the key columns
+//   n_gb + 1      first row (smallest input row index of the group)  -> reproduces the reference's insertion order
+//   n_gb + 2      last row  (largest input row index)                -> the row the reference reads group values at
+//   n_gb + 3      rows (COUNT(*))
+//   then per aggregate, at its first word w:
+//     COUNT(col) / COUNT(DISTINCT col):  w = count
+//     SUM/AVG of int32/int64:            w = non-NULL count, w+1 = int64 sum (two's complement wrap, like the
+//                                        reference's int64 accumulator)
+//     SUM/AVG of float/double:           w = non-NULL count, w+1 = non-finite flags (1 +inf, 2 -inf, 4 NaN),
+//                                        w+2.. = exact fixed-point sum: limb i holds a signed sum of 32-bit pieces of
+//                                        weight 2^(32 i + emin) (float: 9 limbs, emin -149; double: 66, emin -1074).
+//                                        Integer atomics make it exact and order-independent; the host rounds it
+//                                        once to double (hy_agg_float_sum).
+//     MIN / MAX:                         w = non-NULL count, w+1 = order-preserving bits of the extreme value
+// Group records are combined with per-word operations (ADD / MIN / MAX / OR), so any split of the rows over
+// workgroups gives the same result.
+//
+// Two kernels:
+//   agg_dense_rows  every group-by column arrives as small integer codes (host-built code dictionaries), so the
+//                   group is a mixed-radix index < 64. Each wave folds 64 rows per step with ballots (counts, first /
+//                   last row) and 64-bit butterfly reductions (sums, min/max), one lane updates the workgroup's LDS
+//                   records; a workgroup flushes its records to HBM with a handful of atomics at the end. This is the
+//                   TPC-H Q1 shape (4 groups over 6e8 rows): HBM-bound on the column reads.
+//   agg_hash_rows   general keys: a global open-addressing table of group records in HBM (linear probing, claim by
+//                   CAS, record initialised before the slot is published), accumulators updated with global atomics.
+//                   COUNT(DISTINCT) inserts (group slot, aggregate, value) into a second global set.
+#include <hip/hip_runtime.h>
+
+#include "common.hpp"
+
+namespace hyk {
+
+constexpr int AGG_MAX_COLUMNS = 16;
+constexpr int AGG_MAX_GROUPBY = 8;
+constexpr int AGG_MAX_AGGREGATES = 16;
+constexpr int AGG_MAX_POS_GROUPS = 8;
+constexpr int AGG_DENSE_MAX = 64;
+constexpr int AGG_THREADS = 256;
+constexpr int AGG_ITEMS = 16;                           // rows per lane per tile
+constexpr int AGG_TILE = AGG_THREADS * AGG_ITEMS;       // 4096 rows
+constexpr int AGG_WAVE_SPAN = WAVE * AGG_ITEMS;         // 1024 consecutive rows per wave
+constexpr int AGG_DENSE_LDS_WORDS = 6144;               // 48 KiB of group records per workgroup
+
+enum : int32_t { WOP_KEY = 0, WOP_ADD = 1, WOP_MIN = 2, WOP_MAX = 3, WOP_OR = 4 };
+enum : int32_t { AGG_HDR_NULLS = 0, AGG_HDR_FIRST = 1, AGG_HDR_LAST = 2, AGG_HDR_ROWS = 3, AGG_HDR_WORDS = 4 };
+
+constexpr int FLOAT_LIMBS = 9;
+constexpr int FLOAT_EMIN = -149;
+constexpr int DOUBLE_LIMBS = 66;
+constexpr int DOUBLE_EMIN = -1074;
+
+struct AggCol {
+  const hy_column_chunk* chunks;  // device array: per input chunk (data input) or per referenced chunk
+  int32_t type;                   // HY_TYPE_*
+  int32_t pos_group;              // -1: read at (input chunk, offset); else through pos_lists[pos_group]
+  uint32_t domain;                // dense grouping: codes in [0, domain), NULL -> domain
+  uint32_t stride;                // dense grouping: weight of this column's code in the group index
+};
+
+struct AggFn {
+  int32_t function;  // HY_AGG_*
+  int32_t column;    // index into cols, -1 for COUNT(*)
+  uint32_t word;     // first word of this aggregate in a group record
+  int32_t limbs;     // float/double SUM/AVG: limbs of the fixed-point accumulator, else 0
+};
+
+struct AggDesc {
+  AggCol cols[AGG_MAX_COLUMNS];
+  AggFn fns[AGG_MAX_AGGREGATES];
+  int32_t gb[AGG_MAX_GROUPBY];       // group-by entries (indexes into cols)
+  uint32_t n_cols, n_fns, n_gb, n_pos_groups;
+  const hy_row_id* const* pos_lists; // device: pos_lists[g * n_chunks + c]
+  const uint32_t* chunk_size;        // device: rows per input chunk
+  const uint64_t* chunk_row_begin;   // device: n_chunks + 1
+  const uint64_t* chunk_tile_begin;  // device: n_chunks + 1
+  uint32_t n_chunks;
+  uint64_t n_tiles;
+  uint32_t words;                    // words per group record
+  const int32_t* word_op;            // device: WOP_* per record word
+  uint32_t* error;                   // bit 0: table full / livelock guard, bit 1: dense code out of range
+};
+
+__host__ __device__ inline uint64_t word_init(int32_t op) { return op == WOP_MIN ? ~0ull : 0ull; }
+
+// ------------------------------------------------------------------------------------------------------------
+// Column reads
+// ------------------------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool is_wide(int32_t type) { return type == HY_TYPE_INT64 || type == HY_TYPE_DOUBLE; }
+
+// Raw bits of row `off` of a column chunk (zero-extended for 4-byte types); false for NULL. Dictionary NULL is
+// value id == dictionary size (dictionary_encoder.hpp:87); a ValueColumn NULL is its null flag.
+__device__ __forceinline__ bool load_bits(const hy_column_chunk& c, uint32_t off, bool wide, uint64_t* bits) {
+  if (c.kind == HY_COL_DICT) {
+    uint32_t vid;
+    if (c.vid_width == 1)
+      vid = static_cast<const uint8_t*>(c.data)[off];
+    else if (c.vid_width == 2)
+      vid = static_cast<const uint16_t*>(c.data)[off];
+    else
+      vid = static_cast<const uint32_t*>(c.data)[off];
+    if (vid >= c.dictionary_size) {
+      *bits = 0;
+      return false;
+    }
+    *bits = wide ? static_cast<const uint64_t*>(c.dictionary)[vid] : static_cast<const uint32_t*>(c.dictionary)[vid];
+    return true;
+  }
+  if (c.nulls != nullptr && c.nulls[off]) {
+    *bits = 0;
+    return false;
+  }
+  *bits = wide ? static_cast<const uint64_t*>(c.data)[off] : static_cast<const uint32_t*>(c.data)[off];
+  return true;
+}
+
+// RowIDs of one input row in every PosList group (reference input); NULL RowIDs read as NULL values
+// (reference_column_iterable.hpp:60-86).
+struct RowRefs {
+  hy_row_id rid[AGG_MAX_POS_GROUPS];
+};
+
+__device__ __forceinline__ void load_refs(const AggDesc& d, uint32_t c, uint32_t off, RowRefs* r) {
+  for (uint32_t g = 0; g < d.n_pos_groups; ++g) r->rid[g] = d.pos_lists[static_cast<uint64_t>(g) * d.n_chunks + c][off];
+}
+
+__device__ __forceinline__ bool read_col(const AggDesc& d, const AggCol& col, uint32_t c, uint32_t off,
+                                         const RowRefs& refs, uint64_t* bits) {
+  const bool wide = is_wide(col.type);
+  if (col.pos_group < 0) return load_bits(col.chunks[c], off, wide, bits);
+  const hy_row_id rid = refs.rid[col.pos_group];
+  if (rid.chunk_offset == 0xFFFFFFFFu) {
+    *bits = 0;
+    return false;
+  }
+  return load_bits(col.chunks[rid.chunk_id], rid.chunk_offset, wide, bits);
+}
+
+// Key word of a group-by value: raw bits, with -0.0 folded into +0.0 (they are one key of std::unordered_map<float>).
+__device__ __forceinline__ uint64_t key_bits(uint64_t bits, int32_t type) {
+  if (type == HY_TYPE_FLOAT && bits == 0x80000000ull) return 0;
+  if (type == HY_TYPE_DOUBLE && bits == 0x8000000000000000ull) return 0;
+  return bits;
+}
+
+// Order-preserving unsigned image of a value (MIN / MAX with unsigned 64-bit atomics).
+__device__ __forceinline__ uint64_t ordered_bits(uint64_t bits, int32_t type) {
+  switch (type) {
+    case HY_TYPE_INT32:
+      return static_cast<uint32_t>(bits) ^ 0x80000000u;
+    case HY_TYPE_INT64:
+      return bits ^ (1ull << 63);
+    case HY_TYPE_FLOAT: {
+      const uint32_t b = static_cast<uint32_t>(bits);
+      return (b & 0x80000000u) ? static_cast<uint32_t>(~b) : (b | 0x80000000u);
+    }
+    default:
+      return (bits >> 63) ? ~bits : (bits | (1ull << 63));
+  }
+}
+
+__device__ __forceinline__ int64_t int_value(uint64_t bits, int32_t type) {
+  return type == HY_TYPE_INT32 ? static_cast<int64_t>(static_cast<int32_t>(static_cast<uint32_t>(bits)))
+                               : static_cast<int64_t>(bits);
+}
+
+// Exact fixed-point pieces of a float / double: value = sum_k part[k] * 2^(32 (i0 + k) + emin). Returns the number of
+// pieces (0 for zero / non-finite; *special receives the non-finite flag).
+__device__ __forceinline__ int float_parts(uint64_t bits, int32_t type, int* i0, int64_t part[3], uint32_t* special) {
+  *special = 0;
+  bool neg;
+  uint32_t shift;
+  unsigned __int128 c;
+  if (type == HY_TYPE_FLOAT) {
+    const uint32_t b = static_cast<uint32_t>(bits);
+    const uint32_t e = (b >> 23) & 0xFFu;
+    uint32_t m = b & 0x7FFFFFu;
+    neg = (b >> 31) != 0;
+    if (e == 0xFFu) {
+      *special = m ? 4u : (neg ? 2u : 1u);
+      return 0;
+    }
+    if (e == 0 && m == 0) return 0;
+    if (e) m |= 0x800000u;
+    shift = e ? e - 1 : 0;  // value = m * 2^(shift + FLOAT_EMIN)
+    c = static_cast<unsigned __int128>(m) << (shift & 31u);
+  } else {
+    const uint64_t e = (bits >> 52) & 0x7FFull;
+    uint64_t m = bits & 0xFFFFFFFFFFFFFull;
+    neg = (bits >> 63) != 0;
+    if (e == 0x7FFull) {
+      *special = m ? 4u : (neg ? 2u : 1u);
+      return 0;
+    }
+    if (e == 0 && m == 0) return 0;
+    if (e) m |= 1ull << 52;
+    shift = e ? static_cast<uint32_t>(e) - 1 : 0;  // value = m * 2^(shift + DOUBLE_EMIN)
+    c = static_cast<unsigned __int128>(m) << (shift & 31u);
+  }
+  *i0 = static_cast<int>(shift >> 5);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int64_t p = static_cast<int64_t>(static_cast<uint32_t>(c >> (32 * k)));
+    part[k] = neg ? -p : p;
+  }
+  return type == HY_TYPE_FLOAT ? 2 : 3;
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Wave reductions (64 lanes, 64-bit)
+// ------------------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v |= __shfl_xor(v, d, WAVE);
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_min64(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint64_t o = __shfl_xor(v, d, WAVE);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_max64(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint64_t o = __shfl_xor(v, d, WAVE);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v = min(v, __shfl_xor(v, d, WAVE));
+  return v;
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v = max(v, __shfl_xor(v, d, WAVE));
+  return v;
+}
+
+// Applies one word operation atomically (LDS or global, by address space of p).
+__device__ __forceinline__ void word_apply(unsigned long long* p, int32_t op, uint64_t v) {
+  switch (op) {
+    case WOP_ADD:
+      if (v) atomicAdd(p, static_cast<unsigned long long>(v));
+      break;
+    case WOP_MIN:
+      if (v != ~0ull) atomicMin(p, static_cast<unsigned long long>(v));
+      break;
+    case WOP_MAX:
+      if (v) atomicMax(p, static_cast<unsigned long long>(v));
+      break;
+    case WOP_OR:
+      if (v) atomicOr(p, static_cast<unsigned long long>(v));
+      break;
+    default:
+      break;
+  }
+}
+
+__device__ __forceinline__ uint32_t agg_tile_chunk(const AggDesc& d, uint64_t tile) {
+  uint32_t lo = 0, hi = d.n_chunks;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (d.chunk_tile_begin[mid] <= tile)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Dense grouping
+// ------------------------------------------------------------------------------------------------------------
+__global__ void agg_init_records(unsigned long long* __restrict__ rec, uint64_t n_records, uint32_t words,
+                                 const int32_t* __restrict__ word_op) {
+  const uint64_t n = n_records * words;
+  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+    rec[i] = word_init(word_op[i % words]);
+}
+
+__global__ __launch_bounds__(AGG_THREADS) void agg_dense_rows(AggDesc d, uint32_t n_groups,
+                                                             unsigned long long* __restrict__ records) {
+  __shared__ unsigned long long s_rec[AGG_DENSE_LDS_WORDS];
+  const uint32_t words = d.words;
+  const uint32_t n_words = n_groups * words;
+  for (uint32_t i = threadIdx.x; i < n_words; i += AGG_THREADS) s_rec[i] = word_init(d.word_op[i % words]);
+  __syncthreads();
+  const int lane = __lane_id();
+  const int w = threadIdx.x / WAVE;
+  const uint32_t H = d.n_gb;  // header starts after the key words
+
+  for (uint64_t tile = blockIdx.x; tile < d.n_tiles; tile += gridDim.x) {
+    const uint32_t c = agg_tile_chunk(d, tile);
+    const uint32_t size = d.chunk_size[c];
+    const uint32_t base = static_cast<uint32_t>(tile - d.chunk_tile_begin[c]) * AGG_TILE + w * AGG_WAVE_SPAN;
+    const uint64_t row0 = d.chunk_row_begin[c];
+    for (int k = 0; k < AGG_ITEMS; ++k) {
+      const uint32_t off0 = base + k * WAVE;
+      if (off0 >= size) break;  // wave-uniform
+      const uint32_t off = off0 + lane;
+      const bool active = off < size;
+      RowRefs refs;
+      if (active) load_refs(d, c, off, &refs);
+      // group index
+      uint32_t g = 0;
+      if (active) {
+        for (uint32_t j = 0; j < d.n_gb; ++j) {
+          const AggCol& col = d.cols[d.gb[j]];
+          uint64_t bits;
+          uint32_t code = col.domain;
+          if (read_col(d, col, c, off, refs, &bits)) {
+            code = static_cast<uint32_t>(bits);
+            if (code >= col.domain) {
+              atomicOr(d.error, 2u);
+              code = col.domain;
+            }
+          }
+          g += code * col.stride;
+        }
+      }
+      uint64_t present = wave_or64(active ? (1ull << g) : 0ull);
+      // values of every aggregate's column for this row
+      uint64_t vbits[AGG_MAX_AGGREGATES];
+      uint32_t valid = 0;
+      for (uint32_t f = 0; f < d.n_fns; ++f) {
+        vbits[f] = 0;
+        const AggFn fn = d.fns[f];
+        if (active && fn.column >= 0 && read_col(d, d.cols[fn.column], c, off, refs, &vbits[f])) valid |= 1u << f;
+      }
+      while (present) {
+        const uint32_t gg = static_cast<uint32_t>(__builtin_ctzll(present));
+        present &= present - 1;
+        const bool mine = active && g == gg;
+        const uint64_t m = __ballot(mine);
+        unsigned long long* rec = s_rec + gg * words;
+        if (lane == 0) {
+          atomicAdd(rec + H + AGG_HDR_ROWS, static_cast<unsigned long long>(__popcll(m)));
+          atomicMin(rec + H + AGG_HDR_FIRST, static_cast<unsigned long long>(row0 + off0 + __builtin_ctzll(m)));
+          atomicMax(rec + H + AGG_HDR_LAST, static_cast<unsigned long long>(row0 + off0 + 63 - __builtin_clzll(m)));
+        }
+        for (uint32_t f = 0; f < d.n_fns; ++f) {
+          const AggFn fn = d.fns[f];
+          if (fn.column < 0) continue;  // COUNT(*) = rows
+          const bool in = mine && ((valid >> f) & 1u);
+          const uint64_t cnt = __popcll(__ballot(in));
+          if (lane == 0 && cnt) atomicAdd(rec + fn.word, static_cast<unsigned long long>(cnt));
+          if (cnt == 0 || fn.function == HY_AGG_COUNT) continue;
+          const int32_t type = d.cols[fn.column].type;
+          if (fn.function == HY_AGG_MIN || fn.function == HY_AGG_MAX) {
+            const bool is_min = fn.function == HY_AGG_MIN;
+            const uint64_t ob = in ? ordered_bits(vbits[f], type) : (is_min ? ~0ull : 0ull);
+            const uint64_t r = is_min ? wave_min64(ob) : wave_max64(ob);
+            if (lane == 0) {
+              if (is_min)
+                atomicMin(rec + fn.word + 1, static_cast<unsigned long long>(r));
+              else
+                atomicMax(rec + fn.word + 1, static_cast<unsigned long long>(r));
+            }
+          } else if (fn.limbs == 0) {  // SUM / AVG of integers
+            const uint64_t s = wave_sum64(in ? static_cast<uint64_t>(int_value(vbits[f], type)) : 0ull);
+            if (lane == 0 && s) atomicAdd(rec + fn.word + 1, static_cast<unsigned long long>(s));
+          } else {  // SUM / AVG of floats: exact limbs
+            int i0 = 0;
+            int64_t part[3] = {0, 0, 0};
+            uint32_t special = 0;
+            const int np = in ? float_parts(vbits[f], type, &i0, part, &special) : 0;
+            const uint64_t sp = wave_or64(special);
+            if (lane == 0 && sp) atomicOr(rec + fn.word + 1, static_cast<unsigned long long>(sp));
+            const int lo = wave_min_i(np ? i0 : 0x7FFFFFFF);
+            const int hi = wave_max_i(np ? i0 + np - 1 : -1);
+            for (int l = lo; l <= hi; ++l) {
+              const int k = l - i0;
+              const int64_t v = (np && k >= 0 && k < np) ? part[k] : 0;
+              const uint64_t s = wave_sum64(static_cast<uint64_t>(v));
+              if (lane == 0 && s) atomicAdd(rec + fn.word + 2 + l, static_cast<unsigned long long>(s));
+            }
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n_words; i += AGG_THREADS) {
+    const int32_t op = d.word_op[i % words];
+    word_apply(records + i, op, s_rec[i]);
+  }
+}
+
+// Dense records -> compact group records with their key words (code per group-by column, NULL code = domain).
+__global__ void agg_dense_compact(AggDesc d, uint32_t n_groups, const unsigned long long* __restrict__ records,
+                                  unsigned long long* __restrict__ out, uint64_t capacity,
+                                  unsigned long long* __restrict__ n_out) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_groups) return;
+  const unsigned long long* rec = records + static_cast<uint64_t>(g) * d.words;
+  if (rec[d.n_gb + AGG_HDR_ROWS] == 0) return;
+  const uint64_t idx = atomicAdd(n_out, 1ull);
+  if (idx >= capacity) return;
+  unsigned long long* o = out + idx * d.words;
+  for (uint32_t i = 0; i < d.words; ++i) o[i] = rec[i];
+  uint64_t nulls = 0;
+  for (uint32_t j = 0; j < d.n_gb; ++j) {
+    const AggCol& col = d.cols[d.gb[j]];
+    const uint32_t code = (g / col.stride) % (col.domain + 1);
+    o[j] = code == col.domain ? 0ull : code;
+    if (code == col.domain) nulls |= 1ull << j;
+  }
+  o[d.n_gb + AGG_HDR_NULLS] = nulls;
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Hash grouping
+// ------------------------------------------------------------------------------------------------------------
+constexpr uint32_t HSLOT_EMPTY = 0, HSLOT_LOCKED = 1, HSLOT_READY = 2;
+
+struct AggTable {
+  uint32_t* state;                 // cap
+  unsigned long long* records;     // cap * words
+  uint64_t cap;                    // power of two
+  // COUNT(DISTINCT) set: keys (slot << 8 | aggregate, value bits)
+  uint32_t* dstate;
+  unsigned long long* dkeys;       // dcap * 2
+  uint64_t dcap;
+};
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+
+// Returns the slot of the group with the given key words, inserting it (record initialised) if new; ~0 on failure.
+__device__ __forceinline__ uint64_t group_slot(const AggDesc& d, const AggTable& t, const uint64_t* key, uint32_t nk) {
+  uint64_t h = 0x9E3779B97F4A7C15ull;
+  for (uint32_t i = 0; i < nk; ++i) h = mix64(h ^ key[i]);
+  uint64_t s = h & (t.cap - 1);
+  for (uint64_t guard = 0; guard < t.cap * 4; ++guard) {
+    const uint32_t st = __hip_atomic_load(&t.state[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    if (st == HSLOT_EMPTY) {
+      uint32_t expected = HSLOT_EMPTY;
+      if (__hip_atomic_compare_exchange_strong(&t.state[s], &expected, HSLOT_LOCKED, __ATOMIC_RELAXED,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        unsigned long long* rec = t.records + s * d.words;
+        for (uint32_t i = 0; i < nk; ++i) rec[i] = key[i];
+        for (uint32_t i = nk; i < d.words; ++i) rec[i] = word_init(d.word_op[i]);
+        __hip_atomic_store(&t.state[s], HSLOT_READY, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        return s;
+      }
+      continue;  // lost the race: re-read the same slot
+    }
+    if (st == HSLOT_LOCKED) {
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    const unsigned long long* rec = t.records + s * d.words;
+    bool eq = true;
+    for (uint32_t i = 0; i < nk; ++i) eq = eq && (rec[i] == key[i]);
+    if (eq) return s;
+    s = (s + 1) & (t.cap - 1);
+  }
+  atomicOr(d.error, 1u);
+  return ~0ull;
+}
+
+// true if (tag, value) was not in the distinct set yet
+__device__ __forceinline__ bool distinct_insert(const AggDesc& d, const AggTable& t, uint64_t tag, uint64_t value) {
+  uint64_t s = mix64(tag * 0x9E3779B97F4A7C15ull ^ mix64(value)) & (t.dcap - 1);
+  for (uint64_t guard = 0; guard < t.dcap * 4; ++guard) {
+    const uint32_t st = __hip_atomic_load(&t.dstate[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    if (st == HSLOT_EMPTY) {
+      uint32_t expected = HSLOT_EMPTY;
+      if (__hip_atomic_compare_exchange_strong(&t.dstate[s], &expected, HSLOT_LOCKED, __ATOMIC_RELAXED,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        t.dkeys[2 * s] = tag;
+        t.dkeys[2 * s + 1] = value;
+        __hip_atomic_store(&t.dstate[s], HSLOT_READY, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        return true;
+      }
+      continue;
+    }
+    if (st == HSLOT_LOCKED) {
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    if (t.dkeys[2 * s] == tag && t.dkeys[2 * s + 1] == value) return false;
+    s = (s + 1) & (t.dcap - 1);
+  }
+  atomicOr(d.error, 1u);
+  return false;
+}
+
+__global__ __launch_bounds__(AGG_THREADS) void agg_hash_rows(AggDesc d, AggTable t) {
+  const uint64_t tile = blockIdx.x;
+  if (tile >= d.n_tiles) return;
+  const uint32_t c = agg_tile_chunk(d, tile);
+  const uint32_t size = d.chunk_size[c];
+  const uint64_t row0 = d.chunk_row_begin[c];
+  const uint32_t base = static_cast<uint32_t>(tile - d.chunk_tile_begin[c]) * AGG_TILE;
+  const uint32_t H = d.n_gb;
+  for (int k = 0; k < AGG_ITEMS; ++k) {
+    const uint32_t off = base + k * AGG_THREADS + threadIdx.x;
+    if (off >= size) continue;
+    RowRefs refs;
+    load_refs(d, c, off, &refs);
+    uint64_t key[AGG_MAX_GROUPBY + 1];
+    uint64_t nulls = 0;
+    for (uint32_t j = 0; j < d.n_gb; ++j) {
+      const AggCol& col = d.cols[d.gb[j]];
+      uint64_t bits;
+      if (read_col(d, col, c, off, refs, &bits)) {
+        key[j] = key_bits(bits, col.type);
+      } else {
+        key[j] = 0;
+        nulls |= 1ull << j;
+      }
+    }
+    key[d.n_gb] = nulls;
+    const uint64_t s = group_slot(d, t, key, d.n_gb + 1);
+    if (s == ~0ull) return;
+    unsigned long long* rec = t.records + s * d.words;
+    const uint64_t row = row0 + off;
+    atomicAdd(rec + H + AGG_HDR_ROWS, 1ull);
+    atomicMin(rec + H + AGG_HDR_FIRST, static_cast<unsigned long long>(row));
+    atomicMax(rec + H + AGG_HDR_LAST, static_cast<unsigned long long>(row));
+    for (uint32_t f = 0; f < d.n_fns; ++f) {
+      const AggFn fn = d.fns[f];
+      if (fn.column < 0) continue;
+      const int32_t type = d.cols[fn.column].type;
+      uint64_t bits;
+      if (!read_col(d, d.cols[fn.column], c, off, refs, &bits)) continue;
+      switch (fn.function) {
+        case HY_AGG_COUNT:
+          atomicAdd(rec + fn.word, 1ull);
+          break;
+        case HY_AGG_COUNT_DISTINCT:
+          if (distinct_insert(d, t, (s << 8) | f, key_bits(bits, type))) atomicAdd(rec + fn.word, 1ull);
+          break;
+        case HY_AGG_MIN:
+          atomicAdd(rec + fn.word, 1ull);
+          atomicMin(rec + fn.word + 1, static_cast<unsigned long long>(ordered_bits(bits, type)));
+          break;
+        case HY_AGG_MAX:
+          atomicAdd(rec + fn.word, 1ull);
+          atomicMax(rec + fn.word + 1, static_cast<unsigned long long>(ordered_bits(bits, type)));
+          break;
+        default:  // SUM / AVG
+          atomicAdd(rec + fn.word, 1ull);
+          if (fn.limbs == 0) {
+            atomicAdd(rec + fn.word + 1, static_cast<unsigned long long>(int_value(bits, type)));
+          } else {
+            int i0 = 0;
+            int64_t part[3];
+            uint32_t special = 0;
+            const int np = float_parts(bits, type, &i0, part, &special);
+            if (special) atomicOr(rec + fn.word + 1, static_cast<unsigned long long>(special));
+            for (int q = 0; q < np; ++q)
+              if (part[q]) atomicAdd(rec + fn.word + 2 + i0 + q, static_cast<unsigned long long>(part[q]));
+          }
+          break;
+      }
+    }
+  }
+}
+
+__global__ void agg_hash_compact(AggDesc d, AggTable t, unsigned long long* __restrict__ out, uint64_t capacity,
+                                 unsigned long long* __restrict__ n_out) {
+  for (uint64_t s = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; s < t.cap;
+       s += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    if (t.state[s] != HSLOT_READY) continue;
+    const uint64_t idx = atomicAdd(n_out, 1ull);
+    if (idx >= capacity) continue;
+    const unsigned long long* rec = t.records + s * d.words;
+    unsigned long long* o = out + idx * d.words;
+    for (uint32_t i = 0; i < d.words; ++i) o[i] = rec[i];
+  }
+}
+
+}  // namespace hyk

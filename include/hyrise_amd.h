@@ -263,6 +263,89 @@ hy_status hy_join_hash(const hy_join_side* build, const hy_join_side* probe, con
 hy_status hy_dereference_row_ids(const hy_row_id* rows, uint64_t n, const hy_row_id* const* chunk_pos_lists,
                                  hy_row_id* out, hy_stream_t stream);
 
+
+/* ---------------------------------------------------------------------------------------------------------------
+ * Aggregate (GROUP BY + MIN / MAX / SUM / AVG / COUNT / COUNT(*) / COUNT(DISTINCT))
+ *
+ * Replaces Aggregate::_aggregate's group-id phase and the per-chunk aggregate loops (reference
+ * src/lib/operators/aggregate.cpp:291-498, AggregateFunctionBuilder :133-249, traits
+ * operators/aggregate/aggregate_traits.hpp:15-74) for all chunks of the input in one pass. The output is one
+ * record of 64-bit words per group; the caller (the Aggregate operator) orders the groups the way the reference's
+ * std::unordered_map iterates them (from the first-row words) and writes the output columns
+ * (write_aggregate_values / _write_groupby_output, aggregate.cpp:622-820).
+ *
+ * Record layout (hy_aggregate_layout reports the word offsets):
+ *   [0, n_groupby)  key words: group-by value bits (4-byte types zero-extended, -0.0 folded into 0.0), 0 if NULL
+ *   n_groupby + 0   NULL mask of the group-by values (bit j = group-by j is NULL)
+ *   n_groupby + 1   first row: smallest input row index of the group (input rows are numbered chunk by chunk)
+ *   n_groupby + 2   last row: largest input row index of the group
+ *   n_groupby + 3   rows of the group (= COUNT(*))
+ *   per aggregate a at word agg_word[a]:
+ *     COUNT, COUNT(DISTINCT): count
+ *     MIN, MAX:               non-NULL count, order-preserving bits of the extreme value (hy_agg_decode_ordered)
+ *     SUM, AVG of integers:   non-NULL count, int64 sum (two's complement)
+ *     SUM, AVG of floats:     non-NULL count, non-finite flags (1 +inf, 2 -inf, 4 NaN), then agg_limbs[a] signed
+ *                             64-bit limbs; limb i has weight 2^(32 i + agg_emin[a]). hy_agg_float_sum rounds the
+ *                             exact sum once to double.
+ *     COUNT(*):               no words (use the rows word)
+ * In dense mode (every group-by column arrives as integer codes with a domain, product of (domain + 1) <= 64) the
+ * key words of a group are its codes.
+ * ------------------------------------------------------------------------------------------------------------- */
+enum { HY_AGG_MIN = 0, HY_AGG_MAX = 1, HY_AGG_SUM = 2, HY_AGG_AVG = 3, HY_AGG_COUNT = 4, HY_AGG_COUNT_DISTINCT = 5 };
+enum { HY_AGG_MAX_COLUMNS = 16, HY_AGG_MAX_GROUPBY = 8, HY_AGG_MAX_AGGREGATES = 16, HY_AGG_MAX_POS_GROUPS = 8 };
+
+typedef struct hy_agg_column {
+  int32_t value_type;                /* HY_TYPE_* of the values (string columns arrive as HY_TYPE_INT32 codes) */
+  int32_t pos_group;                 /* -1: data input (chunks[c] is input chunk c); else the PosList group through
+                                        which this column's values are referenced (chunks[] = referenced chunks) */
+  const hy_column_chunk* chunks;     /* HOST array of n_chunks device column chunks */
+  uint32_t n_chunks;
+  uint32_t domain;                   /* group-by only: 0, or every non-NULL value is an integer code < domain */
+} hy_agg_column;
+
+typedef struct hy_agg_input {
+  uint32_t n_chunks;                 /* input chunks */
+  const uint32_t* chunk_sizes;       /* HOST: rows per input chunk (PosList length for reference input) */
+  const hy_row_id* const* pos_lists; /* HOST: n_pos_groups * n_chunks device PosLists, [g * n_chunks + c] */
+  uint32_t n_pos_groups;
+  const hy_agg_column* columns;      /* HOST */
+  uint32_t n_columns;
+} hy_agg_input;
+
+typedef struct hy_agg_def {
+  int32_t function;                  /* HY_AGG_* */
+  int32_t column;                    /* index into hy_agg_input.columns; -1 for COUNT(*) */
+} hy_agg_def;
+
+typedef struct hy_agg_params {
+  const int32_t* groupby;            /* HOST: indexes into hy_agg_input.columns */
+  uint32_t n_groupby;
+  const hy_agg_def* aggregates;      /* HOST */
+  uint32_t n_aggregates;
+  uint64_t group_bound;              /* upper bound on the number of groups; 0 = number of input rows */
+} hy_agg_params;
+
+typedef struct hy_agg_layout {
+  uint32_t words;                            /* 64-bit words per group record */
+  uint32_t dense;                            /* 1 if the dense (code-indexed) path is used */
+  uint32_t agg_word[HY_AGG_MAX_AGGREGATES];
+  int32_t agg_emin[HY_AGG_MAX_AGGREGATES];
+  uint32_t agg_limbs[HY_AGG_MAX_AGGREGATES];
+} hy_agg_layout;
+
+hy_status hy_aggregate_layout(const hy_agg_input* input, const hy_agg_params* params, hy_agg_layout* layout);
+hy_status hy_aggregate_workspace_size(const hy_agg_input* input, const hy_agg_params* params, size_t* bytes);
+/*
+ * out_records: device, out_capacity * layout.words words. *n_groups (host) receives the number of groups; the call
+ * synchronizes the stream. HY_ERR_CAPACITY if more than out_capacity groups (*n_groups holds the number needed).
+ */
+hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, uint64_t* out_records,
+                       uint64_t out_capacity, uint64_t* n_groups, void* workspace, size_t workspace_bytes,
+                       hy_stream_t stream);
+/* Host helpers: the correctly rounded double of an exact limb sum, and the value bits behind an ordered word. */
+hy_status hy_agg_float_sum(const uint64_t* limbs, uint32_t n_limbs, int32_t emin, uint64_t special, double* out);
+uint64_t hy_agg_decode_ordered(uint64_t ordered, int32_t value_type);
+
 #ifdef __cplusplus
 }
 #endif

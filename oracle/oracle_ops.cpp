@@ -777,7 +777,9 @@ std::shared_ptr<Table> aggregate_impl(const std::shared_ptr<const Table>& in, co
   // output (aggregate.cpp:543-820)
   TableColumnDefinitions defs;
   std::vector<std::vector<AllTypeVariant>> columns;
-  for (const auto g : groupby) defs.emplace_back(in->column_name(g), in->column_data_type(g), true);
+  // aggregate.cpp:544-551: the definition says not nullable (TableColumnDefinition's default), the ValueColumn is
+  // created nullable
+  for (const auto g : groupby) defs.emplace_back(in->column_name(g), in->column_data_type(g), false);
   const auto& first = results[0];
   std::vector<RowID> group_rows;
   for (const auto& kv : first) group_rows.push_back(kv.second.row_id);
@@ -847,7 +849,7 @@ std::shared_ptr<Table> aggregate_impl(const std::shared_ptr<const Table>& in, co
   auto out = std::make_shared<Table>(defs, TableType::Data);
   ChunkColumns cc;
   for (size_t c = 0; c < defs.size(); ++c) {
-    auto vc = make_value_column(defs[c].data_type, defs[c].nullable);
+    auto vc = make_value_column(defs[c].data_type, c < groupby.size() ? true : defs[c].nullable);
     for (const auto& v : columns[c]) vc->append(v);
     cc.push_back(vc);
   }

@@ -4,8 +4,12 @@ import subprocess
 import sys
 
 cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Iinclude", "-c",
-       "hyrise-1_amd/csrc/capi/hyrise_amd.hip", "-o", "/tmp/_res.o", "-Rpass-analysis=kernel-resource-usage"]
-out = subprocess.run(cmd, capture_output=True, text=True).stderr
+       "TU", "-o", "/tmp/_res.o", "-Rpass-analysis=kernel-resource-usage"]
+out = ""
+for tu in ("hyrise-1_amd/csrc/capi/hyrise_amd.hip", "hyrise-1_amd/csrc/capi/hyrise_amd_aggregate.hip"):
+    if len(sys.argv) > 2 and sys.argv[2] not in tu:
+        continue
+    out += subprocess.run([tu if a == "TU" else a for a in cmd], capture_output=True, text=True).stderr
 cur = None
 rows = []
 for line in out.splitlines():
