@@ -1,0 +1,65 @@
+"""MurmurHash2 (seed 17) golden vectors of the reference's own murmur_hash.cpp (tests/golden/murmur2_seed17.json):
+the oracle reproduces them, the reference source compiled by oracle/Makefile (oracle/_ref, when present) agrees with
+the oracle on a sweep, and the device kernel (hy_murmur2) reproduces them on the GPU."""
+import ctypes
+import glob
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+from helpers import GOLDEN, ROOT
+
+GOLD = json.load(open(os.path.join(GOLDEN, "murmur2_seed17.json")))
+
+
+def test_oracle_matches_golden(oracle):
+    for k, v in GOLD["int32"].items():
+        assert oracle.murmur2_int32(int(k), 17) == int(v, 16), k
+    for k, v in GOLD["float"].items():
+        assert oracle.murmur2_float(float(k), 17) == int(v, 16), k
+    for k, v in GOLD["int64"].items():
+        assert oracle.murmur2_int64(int(k), 17) == int(v, 16), k
+
+
+def test_oracle_matches_reference_build(oracle):
+    cands = glob.glob(os.path.join(ROOT, "oracle", "_ref", "libref_murmur.so"))
+    if not cands:
+        pytest.skip("reference murmur_hash.cpp not built here (oracle/_ref needs /root/reference)")
+    ref = ctypes.CDLL(cands[0])
+    for fn in ("ref_murmur2_int32", "ref_murmur2_int64", "ref_murmur2_float", "ref_murmur2_double"):
+        getattr(ref, fn).restype = ctypes.c_uint
+    ref.ref_murmur2_int32.argtypes = [ctypes.c_int32, ctypes.c_uint]
+    ref.ref_murmur2_int64.argtypes = [ctypes.c_int64, ctypes.c_uint]
+    ref.ref_murmur2_float.argtypes = [ctypes.c_float, ctypes.c_uint]
+    ref.ref_murmur2_double.argtypes = [ctypes.c_double, ctypes.c_uint]
+    rng = random.Random(17)
+    for _ in range(2000):
+        i32 = rng.randrange(-(2**31), 2**31)
+        i64 = rng.randrange(-(2**63), 2**63)
+        f = float(np.float32(rng.uniform(-1e6, 1e6)))
+        seed = rng.choice([17, 0, 12345])
+        assert oracle.murmur2_int32(i32, seed) == ref.ref_murmur2_int32(i32, seed)
+        assert oracle.murmur2_int64(i64, seed) == ref.ref_murmur2_int64(i64, seed)
+        assert oracle.murmur2_float(f, seed) == ref.ref_murmur2_float(f, seed)
+        assert oracle.murmur2_double(f, seed) == ref.ref_murmur2_double(f, seed)
+
+
+@pytest.mark.gpu
+def test_device_murmur_matches_golden(hy):
+    import torch
+
+    keys32 = torch.tensor([int(k) for k in GOLD["int32"]] + [int(np.float32(24.0).view(np.int32))],
+                          dtype=torch.int32, device="cuda")
+    out = torch.empty(keys32.numel(), dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    hy.capi.check(hy.capi.lib.hy_murmur2(keys32.data_ptr(), keys32.numel(), 4, 17, out.data_ptr(), stream), "murmur")
+    torch.cuda.synchronize()
+    want = [int(v, 16) for v in GOLD["int32"].values()] + [int(GOLD["float"]["24.0"], 16)]
+    assert [int(x) & 0xFFFFFFFF for x in out.cpu().tolist()] == want
+    keys64 = torch.tensor([1], dtype=torch.int64, device="cuda")
+    hy.capi.check(hy.capi.lib.hy_murmur2(keys64.data_ptr(), 1, 8, 17, out.data_ptr(), stream), "murmur")
+    torch.cuda.synchronize()
+    assert int(out[0].item()) & 0xFFFFFFFF == int(GOLD["int64"]["1"], 16)
