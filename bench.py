@@ -147,16 +147,20 @@ def main():
     part_count = torch.empty(n_parts, dtype=torch.int32, device=dev)
     state = {}
 
+    import numpy as np
+    jc_dtype = np.dtype(capi.JoinChunk)
+
     def probe_side_from_counts(counts_h):
-        nz = [c for c in range(n_lchunks) if counts_h[c] > 0]
-        pchunks = (capi.JoinChunk * len(nz))()
-        for k, c in enumerate(nz):
-            pc = pchunks[k]
-            pc.pos_list = scan_rows.data_ptr() + 8 * c * chunk
-            pc.size = int(counts_h[c])
-            pc.chunk_id = k
-        side = capi.JoinSide(pchunks, len(nz), capi.HY_TYPE_INT32, referenced, n_lchunks, 1)
-        return side, pchunks, int(sum(counts_h[c] for c in nz))
+        # the scan's output table: one chunk (PosList) per input chunk with >= 1 match (table_scan.cpp:99); built with
+        # numpy so the host side of a step costs what the C++ operator's loop would, not a Python loop
+        nz = np.nonzero(counts_h > 0)[0]
+        pchunks = np.zeros(len(nz), jc_dtype)
+        pchunks["pos_list"] = scan_rows.data_ptr() + 8 * chunk * nz.astype(np.uint64)
+        pchunks["size"] = counts_h[nz]
+        pchunks["chunk_id"] = np.arange(len(nz), dtype=np.uint32)
+        side = capi.JoinSide(pchunks.ctypes.data_as(ctypes.POINTER(capi.JoinChunk)), len(nz), capi.HY_TYPE_INT32,
+                             referenced, n_lchunks, 1)
+        return side, pchunks, int(counts_h[nz].sum())
 
     def run_join(counts_h):
         side, keep, n_probe = probe_side_from_counts(counts_h)

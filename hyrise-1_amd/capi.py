@@ -92,6 +92,10 @@ _sigs = {
     "hy_last_error_message": (ctypes.c_char_p, []),
     "hy_build_info": (ctypes.c_char_p, []),
     "hy_stream_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
+    "hy_malloc": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]),
+    "hy_free": (ctypes.c_int, [ctypes.c_void_p]),
+    "hy_memcpy_htod": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "hy_memcpy_dtoh": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
     "hy_table_scan_workspace_size": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_size_t)]),
     "hy_table_scan": (ctypes.c_int, [ctypes.POINTER(ScanChunk), ctypes.c_uint32, ctypes.c_int32, ctypes.c_void_p,
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
@@ -143,3 +147,25 @@ def device_count():
     n = ctypes.c_int(0)
     check(lib.hy_get_device_count(ctypes.byref(n)), "hy_get_device_count")
     return n.value
+
+
+class DeviceArray:
+    """A numpy array mirrored in device memory through the C-ABI's own allocator (tests; no torch involved)."""
+
+    def __init__(self, host):
+        import numpy as np
+
+        self.host = np.ascontiguousarray(host)
+        self.ptr = ctypes.c_void_p()
+        check(lib.hy_malloc(ctypes.byref(self.ptr), max(16, self.host.nbytes)), "hy_malloc")
+        check(lib.hy_memcpy_htod(self.ptr, self.host.ctypes.data, self.host.nbytes, None), "hy_memcpy_htod")
+        check(lib.hy_stream_synchronize(None), "sync")
+
+    def fetch(self):
+        check(lib.hy_memcpy_dtoh(self.host.ctypes.data, self.ptr, self.host.nbytes, None), "hy_memcpy_dtoh")
+        check(lib.hy_stream_synchronize(None), "sync")
+        return self.host
+
+    def __del__(self):
+        if getattr(self, "ptr", None) and self.ptr.value:
+            lib.hy_free(self.ptr)

@@ -205,6 +205,7 @@ size_t scan_class_bytes(uint32_t n_chunks, uint64_t n_tiles) {
   cv.take<uint32_t>(n_chunks);
   cv.take<uint32_t>(n_chunks);
   cv.take<uint64_t>(n_tiles + 1);
+  cv.take<uint32_t>(n_tiles + 1);
   cv.take<uint32_t>(64);
   return cv.used + 256;
 }
@@ -276,6 +277,7 @@ hy_status table_scan_impl(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_
     auto* dix = cv.take<uint32_t>(nc);
     auto* dcid = cv.take<uint32_t>(nc);
     auto* dst = cv.take<uint64_t>(run + 1);
+    auto* downer = cv.take<uint32_t>(run + 1);
     auto* dmisc = cv.take<uint32_t>(64);
     if (!cv.ok) return fail(HY_ERR_WORKSPACE, "scan workspace too small");
     if (!error) {
@@ -292,6 +294,9 @@ hy_status table_scan_impl(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_
     HY_HIP(hipMemsetAsync(dst, 0, sizeof(uint64_t) * (run + 1), s));
     HY_HIP(hipMemsetAsync(dmisc, 0, 4, s));
     if (run == 0) continue;
+    hipLaunchKernelGGL(hyk::fill_tile_owner, dim3((nc + 255) / 256), dim3(256), 0, s, dti, nc, downer);
+    HY_HIP(hipGetLastError());
+    d.tile_chunk = downer;
     d.chunks = dch;
     d.chunk_tile_begin = dti;
     d.chunk_index = dix;
@@ -411,8 +416,14 @@ hy_status hy_reference_scan(const hy_row_id* pos_list, uint64_t pos_list_size, c
     case HY_TYPE_DOUBLE:
       st = go(double{});
       break;
-    default:
-      return fail(HY_ERR_UNSUPPORTED, "reference scan type");
+    default: {
+      // non-numeric columns (strings) are only scanned through their dictionaries: the comparison is on value ids
+      for (uint32_t i = 0; i < n_referenced_chunks; ++i)
+        if (referenced_chunks[i].column.kind != HY_COL_DICT && referenced_chunks[i].op != HY_OP_NONE)
+          return fail(HY_ERR_UNSUPPORTED, "reference scan of an unencoded non-numeric column");
+      st = go(int32_t{});
+      break;
+    }
   }
   if (st != HY_OK) return st;
   uint32_t herr = 0;
@@ -579,6 +590,8 @@ struct SideBufs {
   uint32_t* hist2;
   uint32_t* off2;
   uint32_t* part_begin;
+  uint32_t* tile_owner1;
+  uint32_t* tile_owner2;
   uint64_t max_tiles2;
 };
 
@@ -625,6 +638,8 @@ void carve_side(Carver& cv, const SidePlan& p, const Geometry& g, SideBufs<H>& b
     b.off2 = nullptr;
   }
   b.part_begin = cv.take<uint32_t>((1u << g.bits) + 1);
+  b.tile_owner1 = cv.take<uint32_t>(std::max<uint64_t>(1, p.n_tiles1));
+  b.tile_owner2 = g.two_pass ? cv.take<uint32_t>(b.max_tiles2) : nullptr;
 }
 
 struct Common {
@@ -675,6 +690,7 @@ hy_status partition_side(const SidePlan& p, const SideBufs<H>& b, const Geometry
   sd.chunks = b.chunks;
   sd.n_chunks = static_cast<uint32_t>(p.chunks.size());
   sd.chunk_tile_begin = b.tile_begin;
+  sd.tile_chunk = b.tile_owner1;
   sd.n_tiles = p.n_tiles1;
   sd.referenced = b.referenced;
   sd.n_referenced = static_cast<uint32_t>(p.referenced.size());
@@ -690,6 +706,9 @@ hy_status partition_side(const SidePlan& p, const SideBufs<H>& b, const Geometry
   const uint64_t* total_dev = side_total;
   HY_HIP(hipMemsetAsync(side_total, 0, 8, s));
   if (p.n_tiles1 > 0) {
+    hipLaunchKernelGGL(hyk::fill_tile_owner, dim3((sd.n_chunks + 255) / 256), dim3(256), 0, s, b.tile_begin,
+                       sd.n_chunks, b.tile_owner1);
+    HY_HIP(hipGetLastError());
     {
       KTimer kt_("part1_hist", s, p.n_rows);
       hipLaunchKernelGGL((hyk::part1_hist<T, H>), dim3(static_cast<uint32_t>(p.n_tiles1)), dim3(hyk::PART_THREADS), 0, s,
@@ -720,7 +739,9 @@ hy_status partition_side(const SidePlan& p, const SideBufs<H>& b, const Geometry
   HY_HIP(hipGetLastError());
   hipLaunchKernelGGL(hyk::seg_tiles, dim3(1), dim3(64), 0, s, b.seg_begin, g.n_digits1, b.seg_tile_begin);
   HY_HIP(hipGetLastError());
-  hyk::Segs sg{b.seg_begin, b.seg_tile_begin, g.n_digits1};
+  hipLaunchKernelGGL(hyk::fill_tile_owner, dim3(1), dim3(256), 0, s, b.seg_tile_begin, g.n_digits1, b.tile_owner2);
+  HY_HIP(hipGetLastError());
+  hyk::Segs sg{b.seg_begin, b.seg_tile_begin, b.tile_owner2, g.n_digits1};
   hyk::Digit d2{mask, 0u, 0xFFu, seed};
   const uint64_t grid2 = b.max_tiles2;
   {

@@ -154,6 +154,7 @@ struct AggWs {
   uint32_t* sizes;
   uint64_t* row_begin;
   uint64_t* tile_begin;
+  uint32_t* tile_owner;
   const hy_row_id** pos_lists;
   hy_column_chunk* chunks[hyk::AGG_MAX_COLUMNS];
   int32_t* word_op;
@@ -168,6 +169,7 @@ void carve(Carver& cv, const hy_agg_input* in, const AggPlan& plan, AggWs* w) {
   w->sizes = cv.take<uint32_t>(std::max<uint32_t>(1, in->n_chunks));
   w->row_begin = cv.take<uint64_t>(in->n_chunks + 1);
   w->tile_begin = cv.take<uint64_t>(in->n_chunks + 1);
+  w->tile_owner = cv.take<uint32_t>(std::max<uint64_t>(1, plan.n_tiles));
   w->pos_lists = cv.take<const hy_row_id*>(std::max<uint64_t>(1, uint64_t(in->n_pos_groups) * in->n_chunks));
   for (uint32_t j = 0; j < in->n_columns; ++j)
     w->chunks[j] = cv.take<hy_column_chunk>(std::max<uint32_t>(1, in->columns[j].n_chunks));
@@ -255,6 +257,12 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
   d.chunk_size = w.sizes;
   d.chunk_row_begin = w.row_begin;
   d.chunk_tile_begin = w.tile_begin;
+  d.tile_chunk = w.tile_owner;
+  if (plan.n_tiles) {
+    hipLaunchKernelGGL(hyk::fill_tile_owner, dim3((input->n_chunks + 255) / 256), dim3(256), 0, s, w.tile_begin,
+                       input->n_chunks, w.tile_owner);
+    HY_HIP(hipGetLastError());
+  }
   d.word_op = w.word_op;
   d.error = w.misc;
   auto* n_out = reinterpret_cast<unsigned long long*>(w.misc + 2);

@@ -82,6 +82,7 @@ struct AggDesc {
   const uint32_t* chunk_size;        // device: rows per input chunk
   const uint64_t* chunk_row_begin;   // device: n_chunks + 1
   const uint64_t* chunk_tile_begin;  // device: n_chunks + 1
+  const uint32_t* tile_chunk;        // device: chunk of each tile
   uint32_t n_chunks;
   uint64_t n_tiles;
   uint32_t words;                    // words per group record
@@ -269,17 +270,7 @@ __device__ __forceinline__ void word_apply(unsigned long long* p, int32_t op, ui
   }
 }
 
-__device__ __forceinline__ uint32_t agg_tile_chunk(const AggDesc& d, uint64_t tile) {
-  uint32_t lo = 0, hi = d.n_chunks;
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (d.chunk_tile_begin[mid] <= tile)
-      lo = mid;
-    else
-      hi = mid;
-  }
-  return lo;
-}
+__device__ __forceinline__ uint32_t agg_tile_chunk(const AggDesc& d, uint64_t tile) { return d.tile_chunk[tile]; }
 
 // ------------------------------------------------------------------------------------------------------------
 // Dense grouping

@@ -210,4 +210,11 @@ __device__ inline uint64_t lb_lookback_wave(const uint64_t* status, uint64_t fir
   return acc;
 }
 
+// owner[t] = c for every tile t in [begin[c], begin[c+1]), c < n: lets a workgroup find its chunk / segment with one
+// load instead of a dependent binary search over the prefix (each step of which is a global-memory round trip).
+static __global__ void fill_tile_owner(const uint64_t* __restrict__ begin, uint32_t n, uint32_t* __restrict__ owner) {
+  for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x)
+    for (uint64_t t = begin[c]; t < begin[c + 1]; ++t) owner[t] = c;
+}
+
 }  // namespace hyk

@@ -81,6 +81,7 @@ struct Side {
   const SrcChunk* chunks;
   uint32_t n_chunks;
   const uint64_t* chunk_tile_begin;  // n_chunks + 1 (pass-1 tiles)
+  const uint32_t* tile_chunk;        // n_tiles: chunk of each pass-1 tile
   uint64_t n_tiles;
   const SrcChunk* referenced;        // referenced column chunks (reference sides)
   uint32_t n_referenced;
@@ -203,7 +204,7 @@ __global__ __launch_bounds__(PART_THREADS) void part1_hist(Side s, Digit dg, uin
   const uint64_t tile = blockIdx.x;
   for (int i = threadIdx.x; i < 256; i += PART_THREADS) s_hist[i] = 0;
   __syncthreads();
-  const uint32_t c = find_tile_owner(s.chunk_tile_begin, s.n_chunks, tile);
+  const uint32_t c = s.tile_chunk[tile];
   const SrcChunk ch = s.chunks[c];
   const uint32_t base = static_cast<uint32_t>(tile - s.chunk_tile_begin[c]) * PART_TILE;
   const int w = threadIdx.x / WAVE;
@@ -227,7 +228,7 @@ __global__ __launch_bounds__(PART_THREADS) void part1_scatter(Side s, Digit dg, 
   const uint64_t tile = blockIdx.x;
   for (int i = threadIdx.x; i < PART_WAVES * 256; i += PART_THREADS) (&s_cnt[0][0])[i] = 0;
   __syncthreads();
-  const uint32_t c = find_tile_owner(s.chunk_tile_begin, s.n_chunks, tile);
+  const uint32_t c = s.tile_chunk[tile];
   const SrcChunk ch = s.chunks[c];
   const uint32_t base = static_cast<uint32_t>(tile - s.chunk_tile_begin[c]) * PART_TILE;
   const int w = threadIdx.x / WAVE;
@@ -279,6 +280,7 @@ __global__ __launch_bounds__(PART_THREADS) void part1_scatter(Side s, Digit dg, 
 struct Segs {
   const uint32_t* seg_begin;        // n_segs + 1 record offsets
   const uint64_t* seg_tile_begin;   // n_segs + 1 tile prefix (device-computed; grid is an upper bound)
+  const uint32_t* tile_seg;         // segment of each pass-2 tile
   uint32_t n_segs;
 };
 
@@ -290,7 +292,7 @@ __global__ __launch_bounds__(PART_THREADS) void part2_hist(Segs sg, Digit dg, ui
   if (tile >= sg.seg_tile_begin[sg.n_segs]) return;
   for (int i = threadIdx.x; i < 256; i += PART_THREADS) s_hist[i] = 0;
   __syncthreads();
-  const uint32_t sgi = find_tile_owner(sg.seg_tile_begin, sg.n_segs, tile);
+  const uint32_t sgi = sg.tile_seg[tile];
   const uint32_t t_in = static_cast<uint32_t>(tile - sg.seg_tile_begin[sgi]);
   const uint32_t nt = static_cast<uint32_t>(sg.seg_tile_begin[sgi + 1] - sg.seg_tile_begin[sgi]);
   const uint32_t b0 = sg.seg_begin[sgi], b1 = sg.seg_begin[sgi + 1];
@@ -314,7 +316,7 @@ __global__ __launch_bounds__(PART_THREADS) void part2_scatter(Segs sg, Digit dg,
   if (tile >= sg.seg_tile_begin[sg.n_segs]) return;
   for (int i = threadIdx.x; i < PART_WAVES * 256; i += PART_THREADS) (&s_cnt[0][0])[i] = 0;
   __syncthreads();
-  const uint32_t sgi = find_tile_owner(sg.seg_tile_begin, sg.n_segs, tile);
+  const uint32_t sgi = sg.tile_seg[tile];
   const uint32_t t_in = static_cast<uint32_t>(tile - sg.seg_tile_begin[sgi]);
   const uint32_t nt = static_cast<uint32_t>(sg.seg_tile_begin[sgi + 1] - sg.seg_tile_begin[sgi]);
   const uint32_t b0 = sg.seg_begin[sgi], b1 = sg.seg_begin[sgi + 1];

@@ -23,6 +23,7 @@ constexpr int SCAN_TILE = SCAN_THREADS * SCAN_ROWS_PER_THREAD;  // 4096
 struct ScanLaunchDesc {
   const hy_scan_chunk* chunks;       // device copy of this class's chunk descriptors
   const uint64_t* chunk_tile_begin;  // n_chunks + 1 prefix of tile counts
+  const uint32_t* tile_chunk;        // n_tiles: chunk of each tile (fill_tile_owner)
   const uint32_t* chunk_index;       // original chunk index (for counts[])
   const uint32_t* chunk_ids;         // chunk id written into RowID outputs
   uint64_t n_rows;
@@ -86,17 +87,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanLaunchDesc d, Sc
 
   if (threadIdx.x == 0) {
     const uint64_t tile = atomicAdd(d.ticket, 1u);
-    // binary search: largest c with chunk_tile_begin[c] <= tile
-    uint32_t lo = 0, hi = d.n_chunks;
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (d.chunk_tile_begin[mid] <= tile)
-        lo = mid;
-      else
-        hi = mid;
-    }
     s_tile = tile;
-    s_chunk = lo;
+    s_chunk = tile < d.n_tiles ? d.tile_chunk[tile] : 0u;
   }
   __syncthreads();
   const uint64_t tile = s_tile;
