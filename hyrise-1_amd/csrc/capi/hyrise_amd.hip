@@ -839,7 +839,7 @@ hy_status join_typed(const SidePlan& bp, const SidePlan& pp, const hy_join_param
   // holds (skewed keys) is processed as several LDS sub-tables in sequence
   size_t kLdsBudget = 40 * 1024;
   if (const char* e = std::getenv("HY_JOIN_LDS_BUDGET")) kLdsBudget = std::strtoull(e, nullptr, 10);  // test knob
-  uint32_t lds_max = std::max<uint32_t>(max_build, 1);
+  uint32_t lds_max = std::min<uint32_t>(std::max<uint32_t>(max_build, 1), hyk::LDS_MAX_ROWS);
   while (lds_max > 16 && hyk::table_bytes<H>(lds_max) > kLdsBudget) lds_max = lds_max * 7 / 8;
   const size_t lds = hyk::table_bytes<H>(lds_max);
 

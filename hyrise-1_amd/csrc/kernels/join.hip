@@ -25,10 +25,10 @@
 
 namespace hyk {
 
-constexpr int PART_THREADS = 512;
+constexpr int PART_THREADS = 256;
 constexpr int PART_WAVES = PART_THREADS / WAVE;
 constexpr int PART_ITEMS = 16;                              // items per lane per tile
-constexpr int PART_TILE = PART_THREADS * PART_ITEMS;        // 8192 rows per tile
+constexpr int PART_TILE = PART_THREADS * PART_ITEMS;        // 4096 rows per tile
 constexpr int WAVE_SPAN = WAVE * PART_ITEMS;                // 1024 consecutive rows per wave
 constexpr uint32_t NULL_PAYLOAD = 0xFFFFFFFFu;
 
@@ -235,20 +235,19 @@ __global__ __launch_bounds__(PART_THREADS) void part1_scatter(Side s, Digit dg, 
 
   H keys[PART_ITEMS];
   uint32_t pays[PART_ITEMS];
-  uint32_t digs[PART_ITEMS];
-  uint32_t ranks[PART_ITEMS];
+  uint32_t dr[PART_ITEMS];  // digit << 24 | rank within the wave (rank < WAVE_SPAN)
   uint32_t act = 0;
 #pragma unroll
   for (int k = 0; k < PART_ITEMS; ++k) {
     const uint32_t off = base + w * WAVE_SPAN + k * WAVE + __lane_id();
     bool a = false;
-    digs[k] = 0;
+    uint32_t dig = 0;
     if (off < ch.size) {
       a = load_row<T, H>(s, ch, off, &keys[k], &pays[k]);
-      if (a) digs[k] = digit_of<H>(dg, keys[k]);
+      if (a) dig = digit_of<H>(dg, keys[k]);
     }
     act |= static_cast<uint32_t>(a) << k;
-    ranks[k] = wave_rank(digs[k], a, dbits, s_cnt[w]);
+    dr[k] = (dig << 24) | wave_rank(dig, a, dbits, s_cnt[w]);
   }
   __syncthreads();
   // exclusive prefix over waves per digit
@@ -265,7 +264,7 @@ __global__ __launch_bounds__(PART_THREADS) void part1_scatter(Side s, Digit dg, 
 #pragma unroll
   for (int k = 0; k < PART_ITEMS; ++k) {
     if ((act >> k) & 1u) {
-      const uint32_t pos = s_cnt[w][digs[k]] + ranks[k];
+      const uint32_t pos = s_cnt[w][dr[k] >> 24] + (dr[k] & 0xFFFFFFu);
       Rec<H> r;
       r.key = keys[k];
       r.payload = pays[k];
@@ -322,20 +321,19 @@ __global__ __launch_bounds__(PART_THREADS) void part2_scatter(Segs sg, Digit dg,
   const uint32_t b0 = sg.seg_begin[sgi], b1 = sg.seg_begin[sgi + 1];
   const int w = threadIdx.x / WAVE;
   Rec<H> recs[PART_ITEMS];
-  uint32_t digs[PART_ITEMS];
-  uint32_t ranks[PART_ITEMS];
+  uint32_t dr[PART_ITEMS];  // digit << 24 | rank within the wave
   uint32_t act = 0;
 #pragma unroll
   for (int k = 0; k < PART_ITEMS; ++k) {
     const uint32_t r = b0 + t_in * PART_TILE + w * WAVE_SPAN + k * WAVE + __lane_id();
     const bool a = r < b1;
-    digs[k] = 0;
+    uint32_t dig = 0;
     if (a) {
       recs[k] = in[r];
-      digs[k] = digit_of<H>(dg, recs[k].key);
+      dig = digit_of<H>(dg, recs[k].key);
     }
     act |= static_cast<uint32_t>(a) << k;
-    ranks[k] = wave_rank(digs[k], a, dbits, s_cnt[w]);
+    dr[k] = (dig << 24) | wave_rank(dig, a, dbits, s_cnt[w]);
   }
   __syncthreads();
   const uint64_t hbase = sg.seg_tile_begin[sgi] * n_digits;
@@ -351,7 +349,7 @@ __global__ __launch_bounds__(PART_THREADS) void part2_scatter(Segs sg, Digit dg,
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < PART_ITEMS; ++k)
-    if ((act >> k) & 1u) out[s_cnt[w][digs[k]] + ranks[k]] = recs[k];
+    if ((act >> k) & 1u) out[s_cnt[w][dr[k] >> 24] + (dr[k] & 0xFFFFFFu)] = recs[k];
 }
 
 // Partition bounds after pass 1 only (radix_bits <= 8): part_begin[d] = offsets[d * n_tiles].
@@ -448,14 +446,16 @@ __global__ __launch_bounds__(SCAN_T) void exclusive_scan_u32(const uint32_t* __r
   }
 }
 
-// ------------------------------------------------------------------------------------------------------------
 // Per-partition build + probe, entirely in LDS.
 //
-// A hash table over up to L = lds_max_build build rows has cap = n + n/2 + 1 slots (open addressing, linear
-// probing, slot = fastrange of a key hash independent of the radix bits). A slot holds {state, key}: state = 1 +
-// payload of the row that claimed it, plus a per-slot count. A key with one build row needs nothing else; a key
-// with several build rows is expanded by re-reading the table's build records in order, which reproduces the
-// reference's insertion-ordered PosList (join_hash.cpp:158-175).
+// The build records of a partition (up to L = lds_max_build of them) are placed in a bucketed LDS table by a
+// counting sort: NB = nb buckets chosen by a key hash independent of the radix bits; pass 1 adds 1 to its bucket's
+// size for every record (fire-and-forget LDS adds), a block scan turns sizes into bucket starts, pass 2 claims a slot
+// per record with one returning LDS add and stores {key, payload} there. Bucket b then holds entries
+// [end[b-1], end[b]). No CAS loops, locks or fences: all inserts of a thread are independent LDS operations.
+// A lookup scans one bucket (about two entries) and yields (matches, first matching entry). A key with one build
+// row needs nothing else; a key with several build rows is expanded by re-reading the partition's build records in
+// order, which reproduces the reference's insertion-ordered PosList (join_hash.cpp:158-175).
 //
 // A partition with more than L build rows (skewed keys) is processed as consecutive sub-tables of L rows each:
 // every probe row's match count is summed over the sub-tables, and its matches are written sub-table by sub-table,
@@ -469,14 +469,7 @@ constexpr int JOIN_THREADS = 512;
 constexpr int JOIN_WAVES = JOIN_THREADS / WAVE;
 constexpr int JP_PER = 8;                          // probe records per thread per pass
 constexpr int JP_PASS = JP_PER * JOIN_THREADS;     // 4096
-constexpr uint32_t SLOT_EMPTY = 0u;
-constexpr uint32_t SLOT_LOCKED = 0xFFFFFFFFu;
-
-template <typename H>
-struct __attribute__((aligned(sizeof(H) == 8 ? 16 : 8))) Slot {
-  uint32_t state;  // 0 empty, LOCKED while the key is written, else 1 + payload of the claiming build row
-  H key;
-};
+constexpr uint32_t LDS_MAX_ROWS = 0xFFFFu;         // entry indexes and counts of one table fit 16 bits
 
 struct JoinDesc {
   const uint32_t* build_begin;  // n_parts + 1
@@ -493,15 +486,30 @@ struct JoinDesc {
   uint64_t* trace;              // debug phase stamps (hy_debug_set_join_trace) or null
 };
 
-__host__ __device__ inline uint32_t slot_cap(uint32_t nb) { return nb + nb / 2 + 1; }
+template <typename H>
+struct BTable {
+  Rec<H>* ents;   // nb entries, bucket by bucket
+  uint32_t* end;  // NB bucket ends
+  uint32_t nb;
+  uint32_t NB;
+};
+
+__host__ __device__ inline size_t align16(size_t b) { return (b + 15) & ~size_t(15); }
 
 // LDS bytes of a table over nb build rows
 template <typename H>
 __host__ __device__ inline size_t table_bytes(uint32_t nb) {
-  const size_t cap = slot_cap(nb);
-  size_t b = sizeof(Slot<H>) * cap;  // slots
-  b += 4 * ((cap + 1) / 2);           // per-slot counts (u16, packed for 32-bit atomics)
-  return (b + 15) & ~size_t(15);
+  return align16(sizeof(Rec<H>) * nb) + align16(4 * size_t(nb ? nb : 1));
+}
+
+template <typename H>
+__device__ __forceinline__ BTable<H> table_at(unsigned char* smem, uint32_t nb) {
+  BTable<H> t;
+  t.nb = nb;
+  t.NB = nb ? nb : 1;
+  t.ents = reinterpret_cast<Rec<H>*>(smem);
+  t.end = reinterpret_cast<uint32_t*>(smem + align16(sizeof(Rec<H>) * nb));
+  return t;
 }
 
 template <typename H>
@@ -537,52 +545,19 @@ __device__ __forceinline__ uint32_t emitted_for(int mode, uint32_t count) {
   return 0u;
 }
 
-// Inserts one build record. The claiming lane finishes its whole publication (key, state, count) inside the
-// iteration in which its CAS succeeds, before any lane of the wave loops back: a lane that lost the race never spins
-// on a LOCKED slot whose owner is a masked-off lane of its own wave.
 template <typename H>
-__device__ __forceinline__ void table_insert(Slot<H>* slots, uint32_t* cnt32, uint32_t cap, const Rec<H>& rec,
-                                             uint32_t* error) {
-  uint32_t s = static_cast<uint32_t>((static_cast<uint64_t>(slot_hash<H>(rec.key)) * cap) >> 32);
-  bool done = false;
-  for (uint32_t guard = 0; !done && guard <= cap * 64u; ++guard) {
-    const uint32_t st = __hip_atomic_load(&slots[s].state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    bool won = false;
-    if (st == SLOT_EMPTY) {
-      uint32_t expected = SLOT_EMPTY;
-      won = __hip_atomic_compare_exchange_strong(&slots[s].state, &expected, SLOT_LOCKED, __ATOMIC_RELAXED,
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (won) {
-        slots[s].key = rec.key;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __hip_atomic_store(&slots[s].state, rec.payload + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        atomicAdd(&cnt32[s >> 1], (s & 1u) ? 0x10000u : 1u);
-      }
-    }
-    if (won) {
-      done = true;
-    } else if (st != SLOT_EMPTY && st != SLOT_LOCKED) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      if (slots[s].key == rec.key) {
-        atomicAdd(&cnt32[s >> 1], (s & 1u) ? 0x10000u : 1u);
-        done = true;
-      } else {
-        s = (s + 1 == cap) ? 0 : s + 1;
-      }
-    }
-    // else: lost the CAS or the slot is being published by another wave -> re-read the same slot
-  }
-  if (!done) atomicOr(error, 2u);  // livelock guard (reported as a kernel failure)
+__device__ __forceinline__ uint32_t bucket_of(H key, uint32_t NB) {
+  return static_cast<uint32_t>((static_cast<uint64_t>(slot_hash<H>(key)) * NB) >> 32);
 }
 
-// Builds the LDS table over build records [b0, b0 + n). Each thread holds up to BUILD_PER records whose loads are
-// all in flight together - the first batch's while the table is being cleared. Insertion order is irrelevant: a
-// slot's state names the row of a single-row key, and multi-row keys are expanded in build order from the records.
-// Ends with a barrier.
-constexpr int BUILD_PER = 6;  // >= the largest 4-byte-key table in the default 40 KiB budget / JOIN_THREADS
+// Builds the LDS table over build records [b0, b0 + n) (n <= LDS_MAX_ROWS). Each thread holds up to BUILD_PER
+// records whose loads are all in flight together - the first batch's while the bucket sizes are being cleared. A
+// partition larger than one batch re-reads its records (from L2) for the second counting-sort pass. Ends with a
+// barrier.
+constexpr int BUILD_PER = 6;  // >= the largest 4-byte-key table in the default LDS budget / JOIN_THREADS
 template <typename H>
-__device__ __forceinline__ void build_table(Slot<H>* slots, uint32_t* cnt32, uint32_t cap,
-                                            const Rec<H>* __restrict__ build, uint32_t b0, uint32_t n, uint32_t* error) {
+__device__ __forceinline__ void build_table(const BTable<H>& t, const Rec<H>* __restrict__ build, uint32_t b0,
+                                            uint32_t n, uint32_t* s_scratch) {
   Rec<H> r[BUILD_PER];
   auto load_batch = [&](uint32_t base) {
 #pragma unroll
@@ -591,57 +566,63 @@ __device__ __forceinline__ void build_table(Slot<H>* slots, uint32_t* cnt32, uin
       if (i < n) r[q] = build[b0 + i];
     }
   };
+  constexpr uint32_t BATCH = BUILD_PER * JOIN_THREADS;
   load_batch(0);
-  for (uint32_t i = threadIdx.x; i < cap; i += JOIN_THREADS) slots[i].state = SLOT_EMPTY;
-  for (uint32_t i = threadIdx.x; i < (cap + 1) / 2; i += JOIN_THREADS) cnt32[i] = 0u;
+  for (uint32_t i = threadIdx.x; i < t.NB; i += JOIN_THREADS) t.end[i] = 0;
   __syncthreads();
-  for (uint32_t base = 0; base < n; base += BUILD_PER * JOIN_THREADS) {
+  // pass 1: bucket sizes
+  for (uint32_t base = 0; base < n; base += BATCH) {
     if (base) load_batch(base);
 #pragma unroll
+    for (int q = 0; q < BUILD_PER; ++q)
+      if (base + q * JOIN_THREADS + threadIdx.x < n) atomicAdd(&t.end[bucket_of<H>(r[q].key, t.NB)], 1u);
+  }
+  __syncthreads();
+  // bucket sizes -> bucket starts (each thread owns a contiguous run of buckets)
+  const uint32_t per = (t.NB + JOIN_THREADS - 1) / JOIN_THREADS;
+  const uint32_t lo = threadIdx.x * per, hi = min(lo + per, t.NB);
+  uint32_t sum = 0;
+  for (uint32_t i = lo; i < hi; ++i) sum += t.end[i];
+  uint32_t total;
+  uint32_t run = block_exclusive_sum<JOIN_THREADS>(sum, s_scratch, &total);
+  for (uint32_t i = lo; i < hi; ++i) {
+    const uint32_t c = t.end[i];
+    t.end[i] = run;
+    run += c;
+  }
+  __syncthreads();
+  // pass 2: claim slots; afterwards end[b] is the end of bucket b
+  for (uint32_t base = 0; base < n; base += BATCH) {
+    if (base || n > BATCH) load_batch(base);
+#pragma unroll
     for (int q = 0; q < BUILD_PER; ++q) {
-      if (base + q * JOIN_THREADS + threadIdx.x < n) table_insert<H>(slots, cnt32, cap, r[q], error);
+      if (base + q * JOIN_THREADS + threadIdx.x < n) {
+        const uint32_t pos = atomicAdd(&t.end[bucket_of<H>(r[q].key, t.NB)], 1u);
+        t.ents[pos] = r[q];
+      }
     }
   }
   __syncthreads();
 }
 
-constexpr uint32_t NO_SLOT = 0xFFFFFFFFu;
-
-__device__ __forceinline__ uint32_t slot_count(const uint32_t* cnt32, uint32_t s) {
-  return (cnt32[s >> 1] >> ((s & 1u) * 16)) & 0xFFFFu;
-}
-
-// slot holding key, or NO_SLOT
+// Matches of key in the table, packed as (count << 16) | index of the first matching entry; 0 = no match.
 template <typename H>
-__device__ __forceinline__ uint32_t table_find(const Slot<H>* slots, uint32_t cap, H key) {
-  uint32_t s = static_cast<uint32_t>((static_cast<uint64_t>(slot_hash<H>(key)) * cap) >> 32);
-  for (uint32_t guard = 0; guard <= cap; ++guard) {
-    const Slot<H> sl = slots[s];
-    if (sl.state == SLOT_EMPTY) return NO_SLOT;
-    if (sl.key == key) return s;
-    s = (s + 1 == cap) ? 0 : s + 1;
-  }
-  return NO_SLOT;
-}
-
-// (state, count) of key in the table (count = build rows with this key)
-template <typename H>
-__device__ __forceinline__ void table_lookup(const Slot<H>* slots, const uint32_t* cnt32, uint32_t cap, H key,
-                                             uint32_t* state, uint32_t* count) {
-  *state = 0;
-  *count = 0;
-  uint32_t s = static_cast<uint32_t>((static_cast<uint64_t>(slot_hash<H>(key)) * cap) >> 32);
-  for (uint32_t guard = 0; guard <= cap; ++guard) {
-    const Slot<H> sl = slots[s];
-    if (sl.state == SLOT_EMPTY) return;
-    if (sl.key == key) {
-      *state = sl.state;
-      *count = (cnt32[s >> 1] >> ((s & 1u) * 16)) & 0xFFFFu;
-      return;
+__device__ __forceinline__ uint32_t table_lookup(const BTable<H>& t, H key) {
+  if (t.nb == 0) return 0u;
+  const uint32_t b = bucket_of<H>(key, t.NB);
+  const uint32_t lo = b ? t.end[b - 1] : 0u, hi = t.end[b];
+  uint32_t count = 0, first = 0;
+  for (uint32_t i = lo; i < hi; ++i) {
+    if (t.ents[i].key == key) {
+      if (count == 0) first = i;
+      ++count;
     }
-    s = (s + 1 == cap) ? 0 : s + 1;
   }
+  return (count << 16) | first;
 }
+
+__device__ __forceinline__ uint32_t info_count(uint32_t info) { return info >> 16; }
+__device__ __forceinline__ uint32_t info_index(uint32_t info) { return info & 0xFFFFu; }
 
 // Reserves this partition's output range with one atomic add on the running total. The reference emits one output
 // chunk per partition, each with its own PosList (join_hash.cpp:571-590), so partition ranges need not follow
@@ -723,7 +704,7 @@ __device__ __forceinline__ void write_duplicates(const JoinDesc& d, const Rec<H>
 }
 
 // A partition whose build side fits one LDS table (the common case): the table is built once and every probe
-// record's (state, count) stays in registers from counting to writing.
+// record's (count, first entry) stays in registers from counting to writing.
 template <typename H, bool TRACE, int JP>
 __device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t p, unsigned char* smem,
                                                     const Rec<H>* __restrict__ build,
@@ -735,17 +716,14 @@ __device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t 
   const uint32_t bb = d.build_begin[p], nb = d.build_begin[p + 1] - bb;
   const uint32_t pb = d.probe_begin[p], np = d.probe_begin[p + 1] - pb;
   const int mode = d.mode;
-  const uint32_t cap = slot_cap(nb);
-  Slot<H>* slots = reinterpret_cast<Slot<H>*>(smem);
-  uint32_t* cnt32 = reinterpret_cast<uint32_t*>(smem + sizeof(Slot<H>) * cap);
-  build_table<H>(slots, cnt32, cap, build, bb, nb, d.error);
+  const BTable<H> t = table_at<H>(smem, nb);
+  build_table<H>(t, build, bb, nb, s_tot);
   trace_stamp<TRACE>(d, p, 1);
 
-  // Per probe record only its payload and matched slot stay in registers; count, state and key are re-read from
-  // the LDS table when needed.
+  // Per probe record only its payload and match info (count << 16 | first entry) stay in registers.
   constexpr uint32_t JP_PASS_ = JP * JOIN_THREADS;
   const uint32_t n_pass = (np + JP_PASS_ - 1) / JP_PASS_;
-  uint32_t ppay[JP], pslot[JP];
+  uint32_t ppay[JP], pinfo[JP];
   auto load_and_match = [&](uint32_t pass) {
     Rec<H> pr[JP];
 #pragma unroll
@@ -757,10 +735,9 @@ __device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t 
     for (int k = 0; k < JP; ++k) {
       const uint32_t j = pass * JP_PASS_ + k * JOIN_THREADS + threadIdx.x;
       ppay[k] = pr[k].payload;
-      pslot[k] = (j < np && nb > 0) ? table_find<H>(slots, cap, pr[k].key) : NO_SLOT;
+      pinfo[k] = j < np ? table_lookup<H>(t, pr[k].key) : 0u;
     }
   };
-  auto count_of = [&](uint32_t slot) { return slot == NO_SLOT ? 0u : slot_count(cnt32, slot); };
 
   uint32_t my = 0;
   for (uint32_t pass = 0; pass < n_pass; ++pass) {
@@ -768,7 +745,7 @@ __device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t 
 #pragma unroll
     for (int k = 0; k < JP; ++k) {
       const uint32_t j = pass * JP_PASS_ + k * JOIN_THREADS + threadIdx.x;
-      if (j < np) my += emitted_for(mode, count_of(pslot[k]));
+      if (j < np) my += emitted_for(mode, info_count(pinfo[k]));
     }
   }
   trace_stamp<TRACE>(d, p, 2);
@@ -783,12 +760,12 @@ __device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t 
     if (n_pass > 1) load_and_match(pass);  // a single pass still holds its records and matches in registers
     auto e_of = [&](int k) {
       const uint32_t j = pass * JP_PASS_ + k * JOIN_THREADS + threadIdx.x;
-      return j < np ? emitted_for(mode, count_of(pslot[k])) : 0u;
+      return j < np ? emitted_for(mode, info_count(pinfo[k])) : 0u;
     };
     const uint32_t pass_total = pass_offsets<JP>(e_of, s_tot);
 #pragma unroll
     for (int k = 0; k < JP; ++k) {
-      const uint32_t c = count_of(pslot[k]);
+      const uint32_t c = info_count(pinfo[k]);
       const uint32_t j = pass * JP_PASS_ + k * JOIN_THREADS + threadIdx.x;
       const uint32_t e = j < np ? emitted_for(mode, c) : 0u;
       const uint64_t o = run + record_pos<JP>(e, k, s_tot);
@@ -800,10 +777,10 @@ __device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t 
         out_build[o] = hy_row_id{0xFFFFFFFFu, 0xFFFFFFFFu};
         out_probe[o] = prow;
       } else if (c == 1) {
-        out_build[o] = map_row(d.build_map, slots[pslot[k]].state - 1);
+        out_build[o] = map_row(d.build_map, t.ents[info_index(pinfo[k])].payload);
         out_probe[o] = prow;
       } else {
-        write_duplicates<H>(d, build, bb, nb, slots[pslot[k]].key, c, prow, o, out_build, out_probe);
+        write_duplicates<H>(d, build, bb, nb, t.ents[info_index(pinfo[k])].key, c, prow, o, out_build, out_probe);
       }
     }
     run += pass_total;
@@ -826,8 +803,6 @@ __device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t
   const uint32_t L = d.lds_max_build;
   const uint32_t n_sub = (nb + L - 1) / L;
   const int mode = d.mode;
-  Slot<H>* slots = reinterpret_cast<Slot<H>*>(smem);
-  auto cnt_of = [&](uint32_t c) { return reinterpret_cast<uint32_t*>(smem + sizeof(Slot<H>) * c); };
   constexpr int JS = 2;  // probe records per thread per pass (fewer than JP_PER: keeps this rare path's registers
                         // within the fast path's budget)
   constexpr uint32_t JS_PASS = JS * JOIN_THREADS;
@@ -843,16 +818,13 @@ __device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t
       pcn[k] = 0;
     }
     for (uint32_t sub = 0; sub < n_sub; ++sub) {
-      const uint32_t b0 = bb + sub * L, n = (sub + 1 == n_sub) ? nb - sub * L : L, c = slot_cap(n);
-      build_table<H>(slots, cnt_of(c), c, build, b0, n, d.error);
+      const uint32_t b0 = bb + sub * L, n = (sub + 1 == n_sub) ? nb - sub * L : L;
+      const BTable<H> t = table_at<H>(smem, n);
+      build_table<H>(t, build, b0, n, s_tot);
 #pragma unroll
       for (int k = 0; k < JS; ++k) {
         const uint32_t j = pass * JS_PASS + k * JOIN_THREADS + threadIdx.x;
-        if (j < np) {
-          uint32_t st, cnt;
-          table_lookup<H>(slots, cnt_of(c), c, pr[k].key, &st, &cnt);
-          pcn[k] += cnt;
-        }
+        if (j < np) pcn[k] += info_count(table_lookup<H>(t, pr[k].key));
       }
       __syncthreads();  // before the next table overwrites LDS
     }
@@ -898,19 +870,20 @@ __device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t
     __syncthreads();  // s_tot consumed; LDS table region free
     if (mode != HY_JOIN_SEMI && mode != HY_JOIN_ANTI) {
       for (uint32_t sub = 0; sub < n_sub; ++sub) {
-        const uint32_t b0 = bb + sub * L, n = (sub + 1 == n_sub) ? nb - sub * L : L, c = slot_cap(n);
-        build_table<H>(slots, cnt_of(c), c, build, b0, n, d.error);
+        const uint32_t b0 = bb + sub * L, n = (sub + 1 == n_sub) ? nb - sub * L : L;
+        const BTable<H> t = table_at<H>(smem, n);
+        build_table<H>(t, build, b0, n, s_tot);
 #pragma unroll
         for (int k = 0; k < JS; ++k) {
           const uint32_t j = pass * JS_PASS + k * JOIN_THREADS + threadIdx.x;
           if (j >= np || pcn[k] == 0) continue;
-          uint32_t st, cnt;
-          table_lookup<H>(slots, cnt_of(c), c, pr[k].key, &st, &cnt);
+          const uint32_t info = table_lookup<H>(t, pr[k].key);
+          const uint32_t cnt = info_count(info);
           if (cnt == 0) continue;
           const hy_row_id prow = map_row(d.probe_map, pr[k].payload);
           const uint64_t o = run + pos[k];
           if (cnt == 1) {
-            out_build[o] = map_row(d.build_map, st - 1);
+            out_build[o] = map_row(d.build_map, t.ents[info_index(info)].payload);
             out_probe[o] = prow;
           } else {
             write_duplicates<H>(d, build, b0, n, pr[k].key, cnt, prow, o, out_build, out_probe);
