@@ -133,6 +133,7 @@ def main():
         b.column.kind = capi.HY_COL_VALUE
         b.size = size
         b.chunk_id = c
+        b.single_chunk = capi.HY_MIXED_CHUNKS
     referenced = (capi.ColumnChunk * n_lchunks)()
     for c in range(n_lchunks):
         r = referenced[c]
@@ -158,6 +159,7 @@ def main():
         pchunks["pos_list"] = scan_rows.data_ptr() + 8 * chunk * nz.astype(np.uint64)
         pchunks["size"] = counts_h[nz]
         pchunks["chunk_id"] = np.arange(len(nz), dtype=np.uint32)
+        pchunks["single_chunk"] = nz  # scan output chunk k references lineitem chunk nz[k] only
         side = capi.JoinSide(pchunks.ctypes.data_as(ctypes.POINTER(capi.JoinChunk)), len(nz), capi.HY_TYPE_INT32,
                              referenced, n_lchunks, 1)
         return side, pchunks, int(counts_h[nz].sum())

@@ -38,9 +38,12 @@ class ScanChunk(ctypes.Structure):
                 ("out_begin", ctypes.c_uint64)]
 
 
+HY_MIXED_CHUNKS = 0xFFFFFFFF
+
+
 class JoinChunk(ctypes.Structure):
     _fields_ = [("column", ColumnChunk), ("pos_list", ctypes.c_void_p), ("size", ctypes.c_uint32),
-                ("chunk_id", ctypes.c_uint32)]
+                ("chunk_id", ctypes.c_uint32), ("single_chunk", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
 class JoinSide(ctypes.Structure):

@@ -523,8 +523,10 @@ uint32_t uniform_of(const std::vector<uint64_t>& row_begin) {
   return static_cast<uint32_t>(u);
 }
 
-hyk::SrcChunk src_from(const hy_column_chunk& c, const hy_row_id* pos_list, uint32_t size, uint64_t row_begin) {
+hyk::SrcChunk src_from(const hy_column_chunk& c, const hy_row_id* pos_list, uint32_t size, uint64_t row_begin,
+                       uint32_t single_chunk = HY_MIXED_CHUNKS) {
   hyk::SrcChunk s{};
+  s.single_chunk = single_chunk;
   s.data = c.data;
   s.nulls = c.nulls;
   s.dictionary = c.dictionary;
@@ -547,7 +549,7 @@ hy_status plan_side(const hy_join_side* side, SidePlan& p) {
   for (uint32_t i = 0; i < side->n_chunks; ++i) {
     const hy_join_chunk& c = side->chunks[i];
     if (c.pos_list) is_ref = true;
-    p.chunks[i] = src_from(c.column, c.pos_list, c.size, rows);
+    p.chunks[i] = src_from(c.column, c.pos_list, c.size, rows, c.single_chunk);
     p.row_begin[i] = rows;
     p.tile_begin[i] = tiles;
     rows += c.size;
@@ -568,6 +570,9 @@ hy_status plan_side(const hy_join_side* side, SidePlan& p) {
       rr += side->referenced[i].size;
     }
     p.ref_row_begin[side->n_referenced] = rr;
+    for (const auto& c : p.chunks)
+      if (c.pos_list && c.single_chunk != HY_MIXED_CHUNKS && c.single_chunk >= side->n_referenced)
+        return fail(HY_ERR_INVALID_ARGUMENT, "single_chunk outside the referenced chunks");
     if (rr >= 0xFFFFFFFFull) return fail(HY_ERR_UNSUPPORTED, "referenced table exceeds 2^32-1 rows");
   }
   return HY_OK;

@@ -249,6 +249,7 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
     for (size_t k = 0; k < descs.size(); ++k) {
       if (views[k].second == 0) continue;  // reference table_scan.cpp:99: no empty output chunks
       auto pl = pos_list_from_device(rows, views[k].first, views[k].second);
+      pl->set_single_chunk_id(chunk_ids[k]);
       ChunkColumns cols;
       for (ColumnID col = 0; col < in_table->column_count(); ++col)
         cols.push_back(std::make_shared<ReferenceColumn>(in_table, col, pl));
@@ -332,6 +333,7 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
                  "hy_gather_row_ids");
         hy_check(hy_stream_synchronize(s), "sync");
         f = pos_list_from_device(rows, 0, total);
+        f->set_single_chunk_id(rc->pos_list()->single_chunk_id());  // a filtered PosList stays within its chunk
       }
       cols.push_back(std::make_shared<ReferenceColumn>(rc->referenced_table(), rc->referenced_column_id(), f));
     }
@@ -389,6 +391,7 @@ JoinSideInput describe_side(const std::shared_ptr<const Table>& table, ColumnID 
     const auto column = table->get_chunk(c)->get_column(column_id);
     hy_join_chunk jc{};
     jc.chunk_id = c;
+    jc.single_chunk = HY_MIXED_CHUNKS;
     jc.size = static_cast<uint32_t>(column->size());
     if (is_ref) {
       const auto rc = std::static_pointer_cast<const ReferenceColumn>(column);
@@ -399,6 +402,7 @@ JoinSideInput describe_side(const std::shared_ptr<const Table>& table, ColumnID 
       Assert(rc->referenced_table() == referenced && rc->referenced_column_id() == rcol,
              "hyrise-amd: a join column referencing several tables is not supported");
       jc.pos_list = device_pos_list(*rc->pos_list())->ptr();
+      if (rc->pos_list()->single_chunk_id() != INVALID_CHUNK_ID) jc.single_chunk = rc->pos_list()->single_chunk_id();
     } else {
       jc.column = device_column(*column)->desc;
     }

@@ -74,8 +74,15 @@ class PosList : public std::vector<RowID> {
   std::shared_ptr<DevicePosList> device_mirror() const { return std::atomic_load(&_device); }
   void set_device_mirror(std::shared_ptr<DevicePosList> d) const { std::atomic_store(&_device, std::move(d)); }
 
+  // The only chunk every non-NULL RowID points into, when the producer knows it (a TableScan over a data table emits
+  // one PosList per input chunk); INVALID_CHUNK_ID when unknown or mixed. Lets GPU consumers read that chunk's
+  // descriptor once per workgroup instead of once per row.
+  ChunkID single_chunk_id() const { return _single_chunk_id; }
+  void set_single_chunk_id(ChunkID c) { _single_chunk_id = c; }
+
  private:
   mutable std::shared_ptr<DevicePosList> _device;
+  ChunkID _single_chunk_id = INVALID_CHUNK_ID;
 };
 
 enum class DataType : uint8_t { Null, Int, Long, Float, Double, String };

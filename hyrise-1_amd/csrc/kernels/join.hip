@@ -44,6 +44,7 @@ struct SrcChunk {
   const uint8_t* nulls;
   const void* dictionary;
   const hy_row_id* pos_list;  // reference chunk when != nullptr
+  uint32_t single_chunk;      // reference chunk: the only referenced chunk id, or HY_MIXED_CHUNKS
   uint32_t size;
   uint32_t dictionary_size;
   int32_t kind;
@@ -143,6 +144,43 @@ __device__ __forceinline__ bool load_row(const Side& s, const SrcChunk& c, uint3
   return valid || s.keep_nulls;
 }
 
+// Loads the PART_ITEMS rows of this lane in a wave's span (row base + k * WAVE + lane for item k): keys (cast to the
+// hashed type) and payloads; returns the mask of items that take part (valid rows, NULLs only when keep_nulls, as
+// materialize_input does at join_hash.cpp:253). A reference chunk whose PosList references a single chunk (known
+// from its producer, hy_join_chunk.single_chunk) reads that chunk's descriptor once with scalar loads instead of once
+// per lane and row.
+template <typename T, typename H>
+__device__ __forceinline__ uint32_t load_items(const Side& s, const SrcChunk& ch, uint32_t base, H (&keys)[PART_ITEMS],
+                                               uint32_t (&pays)[PART_ITEMS]) {
+  uint32_t act = 0;
+  if (ch.pos_list != nullptr && ch.single_chunk != HY_MIXED_CHUNKS) {
+    const SrcChunk rc = s.referenced[ch.single_chunk];
+    const uint64_t rrow = s.fuse_deref ? s.referenced_row_begin[ch.single_chunk] : 0;
+#pragma unroll
+    for (int k = 0; k < PART_ITEMS; ++k) {
+      const uint32_t off = base + k * WAVE + __lane_id();
+      if (off >= ch.size) continue;
+      const hy_row_id rid = ch.pos_list[off];
+      const bool has = rid.chunk_offset != 0xFFFFFFFFu;
+      T v = T{};
+      const bool valid = has && read_column_value<T>(rc, rid.chunk_offset, &v, false);
+      if (s.fuse_deref)
+        pays[k] = has ? static_cast<uint32_t>(rrow + rid.chunk_offset) : NULL_PAYLOAD;
+      else
+        pays[k] = static_cast<uint32_t>(ch.row_begin + off);
+      keys[k] = static_cast<H>(v);
+      if (valid || s.keep_nulls) act |= 1u << k;
+    }
+    return act;
+  }
+#pragma unroll
+  for (int k = 0; k < PART_ITEMS; ++k) {
+    const uint32_t off = base + k * WAVE + __lane_id();
+    if (off < ch.size && load_row<T, H>(s, ch, off, &keys[k], &pays[k])) act |= 1u << k;
+  }
+  return act;
+}
+
 struct Digit {
   uint32_t mask;   // (1 << radix_bits) - 1
   uint32_t shift;  // digit = (hash & mask) >> shift
@@ -194,6 +232,47 @@ __device__ __forceinline__ uint32_t wave_rank(uint32_t digit, bool active, int d
   return rank;
 }
 
+// LDS-staged scatter of one tile's records. On entry s_cnt[w][d] holds wave w's count of digit d and dr[k] = digit << 24
+// | rank of item k among its wave's same-digit items (wave_rank). The tile's records are first placed in LDS in
+// (digit, wave, rank) order - the order they take in the output - and then stored from consecutive LDS entries by
+// consecutive lanes, so each bucket's run of the tile is written with coalesced stores instead of one scattered 8-byte
+// store per lane. goff(d) = output position of this tile's first digit-d record.
+static_assert(PART_THREADS >= 256, "one thread per digit");
+template <typename H, typename GOFF>
+__device__ __forceinline__ void staged_scatter(const Rec<H> (&recs)[PART_ITEMS], uint32_t act,
+                                               const uint32_t (&dr)[PART_ITEMS], uint32_t (*s_cnt)[256],
+                                               uint32_t* s_delta, Rec<H>* s_stage, uint32_t* s_scratch,
+                                               uint32_t n_digits, const Digit& dg, GOFF goff, Rec<H>* __restrict__ out) {
+  const int w = threadIdx.x / WAVE;
+  __syncthreads();  // every wave's counts are in s_cnt
+  const uint32_t d = threadIdx.x;
+  uint32_t tot = 0;
+  if (d < n_digits) {
+#pragma unroll
+    for (int ww = 0; ww < PART_WAVES; ++ww) {
+      const uint32_t t = s_cnt[ww][d];
+      s_cnt[ww][d] = tot;
+      tot += t;
+    }
+  }
+  uint32_t total;
+  const uint32_t loc = block_exclusive_sum<PART_THREADS>(tot, s_scratch, &total);  // tile-local start of digit d
+  if (d < n_digits) {
+#pragma unroll
+    for (int ww = 0; ww < PART_WAVES; ++ww) s_cnt[ww][d] += loc;
+    s_delta[d] = goff(d) - loc;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < PART_ITEMS; ++k)
+    if ((act >> k) & 1u) s_stage[s_cnt[w][dr[k] >> 24] + (dr[k] & 0xFFFFFFu)] = recs[k];
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < total; i += PART_THREADS) {
+    const Rec<H> r = s_stage[i];
+    out[i + s_delta[digit_of<H>(dg, r.key)]] = r;
+  }
+}
+
 // ------------------------------------------------------------------------------------------------------------
 // Pass 1: from column chunks.
 // ------------------------------------------------------------------------------------------------------------
@@ -208,14 +287,12 @@ __global__ __launch_bounds__(PART_THREADS) void part1_hist(Side s, Digit dg, uin
   const SrcChunk ch = s.chunks[c];
   const uint32_t base = static_cast<uint32_t>(tile - s.chunk_tile_begin[c]) * PART_TILE;
   const int w = threadIdx.x / WAVE;
-  for (int k = 0; k < PART_ITEMS; ++k) {
-    const uint32_t off = base + w * WAVE_SPAN + k * WAVE + __lane_id();
-    if (off < ch.size) {
-      H key;
-      uint32_t payload;
-      if (load_row<T, H>(s, ch, off, &key, &payload)) atomicAdd(&s_hist[digit_of<H>(dg, key)], 1u);
-    }
-  }
+  H keys[PART_ITEMS];
+  uint32_t pays[PART_ITEMS];
+  const uint32_t act = load_items<T, H>(s, ch, base + w * WAVE_SPAN, keys, pays);
+#pragma unroll
+  for (int k = 0; k < PART_ITEMS; ++k)
+    if ((act >> k) & 1u) atomicAdd(&s_hist[digit_of<H>(dg, keys[k])], 1u);
   __syncthreads();
   for (uint32_t d = threadIdx.x; d < n_digits; d += PART_THREADS) hist[d * s.n_tiles + tile] = s_hist[d];
 }
@@ -225,6 +302,9 @@ __global__ __launch_bounds__(PART_THREADS) void part1_scatter(Side s, Digit dg, 
                                                              const uint32_t* __restrict__ offsets,
                                                              Rec<H>* __restrict__ out) {
   __shared__ uint32_t s_cnt[PART_WAVES][256];
+  __shared__ uint32_t s_delta[256];
+  __shared__ uint32_t s_scratch[PART_WAVES + 1];
+  __shared__ Rec<H> s_stage[PART_TILE];
   const uint64_t tile = blockIdx.x;
   for (int i = threadIdx.x; i < PART_WAVES * 256; i += PART_THREADS) (&s_cnt[0][0])[i] = 0;
   __syncthreads();
@@ -236,41 +316,18 @@ __global__ __launch_bounds__(PART_THREADS) void part1_scatter(Side s, Digit dg, 
   H keys[PART_ITEMS];
   uint32_t pays[PART_ITEMS];
   uint32_t dr[PART_ITEMS];  // digit << 24 | rank within the wave (rank < WAVE_SPAN)
-  uint32_t act = 0;
+  const uint32_t act = load_items<T, H>(s, ch, base + w * WAVE_SPAN, keys, pays);
+  Rec<H> recs[PART_ITEMS];
 #pragma unroll
   for (int k = 0; k < PART_ITEMS; ++k) {
-    const uint32_t off = base + w * WAVE_SPAN + k * WAVE + __lane_id();
-    bool a = false;
-    uint32_t dig = 0;
-    if (off < ch.size) {
-      a = load_row<T, H>(s, ch, off, &keys[k], &pays[k]);
-      if (a) dig = digit_of<H>(dg, keys[k]);
-    }
-    act |= static_cast<uint32_t>(a) << k;
+    const bool a = (act >> k) & 1u;
+    const uint32_t dig = a ? digit_of<H>(dg, keys[k]) : 0u;
     dr[k] = (dig << 24) | wave_rank(dig, a, dbits, s_cnt[w]);
+    recs[k].key = keys[k];
+    recs[k].payload = pays[k];
   }
-  __syncthreads();
-  // exclusive prefix over waves per digit
-  for (uint32_t d = threadIdx.x; d < n_digits; d += PART_THREADS) {
-    uint32_t run = offsets[d * s.n_tiles + tile];
-#pragma unroll
-    for (int ww = 0; ww < PART_WAVES; ++ww) {
-      const uint32_t t = s_cnt[ww][d];
-      s_cnt[ww][d] = run;
-      run += t;
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < PART_ITEMS; ++k) {
-    if ((act >> k) & 1u) {
-      const uint32_t pos = s_cnt[w][dr[k] >> 24] + (dr[k] & 0xFFFFFFu);
-      Rec<H> r;
-      r.key = keys[k];
-      r.payload = pays[k];
-      out[pos] = r;
-    }
-  }
+  staged_scatter<H>(recs, act, dr, s_cnt, s_delta, s_stage, s_scratch, n_digits, dg,
+                    [&](uint32_t d) { return offsets[d * s.n_tiles + tile]; }, out);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -311,6 +368,9 @@ __global__ __launch_bounds__(PART_THREADS) void part2_scatter(Segs sg, Digit dg,
                                                              const uint32_t* __restrict__ offsets,
                                                              Rec<H>* __restrict__ out) {
   __shared__ uint32_t s_cnt[PART_WAVES][256];
+  __shared__ uint32_t s_delta[256];
+  __shared__ uint32_t s_scratch[PART_WAVES + 1];
+  __shared__ Rec<H> s_stage[PART_TILE];
   const uint64_t tile = blockIdx.x;
   if (tile >= sg.seg_tile_begin[sg.n_segs]) return;
   for (int i = threadIdx.x; i < PART_WAVES * 256; i += PART_THREADS) (&s_cnt[0][0])[i] = 0;
@@ -326,30 +386,20 @@ __global__ __launch_bounds__(PART_THREADS) void part2_scatter(Segs sg, Digit dg,
 #pragma unroll
   for (int k = 0; k < PART_ITEMS; ++k) {
     const uint32_t r = b0 + t_in * PART_TILE + w * WAVE_SPAN + k * WAVE + __lane_id();
-    const bool a = r < b1;
-    uint32_t dig = 0;
-    if (a) {
+    if (r < b1) {
       recs[k] = in[r];
-      dig = digit_of<H>(dg, recs[k].key);
+      act |= 1u << k;
     }
-    act |= static_cast<uint32_t>(a) << k;
+  }
+#pragma unroll
+  for (int k = 0; k < PART_ITEMS; ++k) {
+    const bool a = (act >> k) & 1u;
+    const uint32_t dig = a ? digit_of<H>(dg, recs[k].key) : 0u;
     dr[k] = (dig << 24) | wave_rank(dig, a, dbits, s_cnt[w]);
   }
-  __syncthreads();
   const uint64_t hbase = sg.seg_tile_begin[sgi] * n_digits;
-  for (uint32_t d = threadIdx.x; d < n_digits; d += PART_THREADS) {
-    uint32_t run = offsets[hbase + d * nt + t_in];
-#pragma unroll
-    for (int ww = 0; ww < PART_WAVES; ++ww) {
-      const uint32_t t = s_cnt[ww][d];
-      s_cnt[ww][d] = run;
-      run += t;
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < PART_ITEMS; ++k)
-    if ((act >> k) & 1u) out[s_cnt[w][dr[k] >> 24] + (dr[k] & 0xFFFFFFu)] = recs[k];
+  staged_scatter<H>(recs, act, dr, s_cnt, s_delta, s_stage, s_scratch, n_digits, dg,
+                    [&](uint32_t d) { return offsets[hbase + d * nt + t_in]; }, out);
 }
 
 // Partition bounds after pass 1 only (radix_bits <= 8): part_begin[d] = offsets[d * n_tiles].
@@ -654,8 +704,10 @@ __device__ __forceinline__ uint32_t pass_offsets(EF e_of, uint32_t* s_tot) {
   const int w = threadIdx.x / WAVE;
 #pragma unroll
   for (int k = 0; k < JP; ++k) {
-    const uint32_t incl = wave_inclusive_sum(e_of(k));
-    if (lane == WAVE - 1) s_tot[k * JOIN_WAVES + w] = incl;
+    const uint32_t e = e_of(k);
+    // common case (unique build keys): every record emits 0 or 1 pairs -> a ballot count is the wave total
+    const uint32_t total = __ballot(e > 1) ? wave_sum(e) : static_cast<uint32_t>(__popcll(__ballot(e != 0)));
+    if (lane == 0) s_tot[k * JOIN_WAVES + w] = total;
   }
   __syncthreads();
   if (threadIdx.x < WAVE) {  // exclusive prefix over the JP * JOIN_WAVES wave totals, (k, w) order
@@ -684,7 +736,9 @@ __device__ __forceinline__ uint32_t pass_offsets(EF e_of, uint32_t* s_tot) {
 
 template <int JP>
 __device__ __forceinline__ uint32_t record_pos(uint32_t e, int k, const uint32_t* s_tot) {
-  return s_tot[k * JOIN_WAVES + threadIdx.x / WAVE] + wave_inclusive_sum(e) - e;
+  const uint32_t before = __ballot(e > 1) ? wave_inclusive_sum(e) - e
+                                          : static_cast<uint32_t>(__popcll(__ballot(e != 0) & lanemask_lt()));
+  return s_tot[k * JOIN_WAVES + threadIdx.x / WAVE] + before;
 }
 
 // Writes the build rows with `key` among build records [b0, b0 + n) in order, each paired with prow.

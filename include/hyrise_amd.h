@@ -214,11 +214,17 @@ uint32_t hy_join_radix_bits(uint64_t build_rows, uint32_t key_bytes);
  * ------------------------------------------------------------------------------------------------------------- */
 enum { HY_JOIN_INNER = 0, HY_JOIN_LEFT = 1, HY_JOIN_RIGHT = 2, HY_JOIN_SEMI = 5, HY_JOIN_ANTI = 6 };
 
+#define HY_MIXED_CHUNKS 0xFFFFFFFFu
+
 typedef struct hy_join_chunk {
   hy_column_chunk column;      /* data-table chunk (pos_list == NULL) */
   const hy_row_id* pos_list;   /* reference-table chunk: device PosList of this chunk, or NULL */
   uint32_t size;               /* rows of this chunk (== column.size or PosList length) */
   uint32_t chunk_id;           /* chunk id of this chunk in its table */
+  uint32_t single_chunk;       /* reference chunk: id of the only referenced chunk when every non-NULL RowID of
+                                  pos_list points into it (e.g. a TableScan output over a data table), else
+                                  HY_MIXED_CHUNKS. Zero-initialised descriptors must set it. */
+  uint32_t reserved;
 } hy_join_chunk;
 
 typedef struct hy_join_side {
