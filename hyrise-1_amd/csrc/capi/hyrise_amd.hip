@@ -184,6 +184,21 @@ int scan_class(const hy_scan_chunk& c) {
 
 uint64_t scan_tiles(uint32_t size) { return (uint64_t(size) + hyk::SCAN_TILE - 1) / hyk::SCAN_TILE; }
 
+// tiles per scan workgroup for a column class (hyk::seg_tiles<E> of the class's element type)
+int class_seg(int cls, int32_t value_type) {
+  switch (cls) {
+    case SC_DICT8:
+      return hyk::seg_tiles<uint8_t>();
+    case SC_DICT16:
+      return hyk::seg_tiles<uint16_t>();
+    case SC_DICT32:
+      return hyk::seg_tiles<uint32_t>();
+    default:
+      return (value_type == HY_TYPE_INT64 || value_type == HY_TYPE_DOUBLE) ? hyk::seg_tiles<int64_t>()
+                                                                          : hyk::seg_tiles<int32_t>();
+  }
+}
+
 template <typename E, bool DICT, bool OUT_ROWID>
 hy_status launch_scan(const hyk::ScanLaunchDesc& d, const void* constant, void* out, uint32_t* counts,
                       hipStream_t s) {
@@ -268,7 +283,8 @@ hy_status table_scan_impl(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_
       hc[k] = chunks[idx[k]];
       rows += hc[k].column.size;
       ht[k] = run;
-      run += hc[k].op == HY_OP_NONE ? 0 : scan_tiles(hc[k].column.size);
+      const uint64_t seg = static_cast<uint64_t>(class_seg(cls, value_type));
+      run += hc[k].op == HY_OP_NONE ? 0 : (scan_tiles(hc[k].column.size) + seg - 1) / seg;  // segments
     }
     ht[nc] = run;
     hyk::ScanLaunchDesc d{};

@@ -73,6 +73,41 @@ __device__ __forceinline__ void load16(const E* __restrict__ base, uint32_t firs
   __builtin_memcpy(out, tmp, sizeof(tmp));
 }
 
+// Tiles per workgroup ("segment"): 128 bytes of loads in flight per lane whatever the element width.
+template <typename E>
+__host__ __device__ constexpr int seg_tiles() {
+  return sizeof(E) >= 8 ? 1 : static_cast<int>(8 / sizeof(E));
+}
+
+// Match mask of the 16 rows [row0, row0 + 16) of chunk ch (bit i = row row0 + i matches).
+template <typename E, bool IS_DICT>
+__device__ __forceinline__ uint32_t match_mask(const hy_scan_chunk& ch, uint32_t row0, const E (&v)[16],
+                                               const u32x4& nulls, const ScanConst<E>& constant) {
+  const uint32_t n = ch.column.size;
+  if (row0 >= n || ch.op == HY_OP_NONE) return 0u;
+  uint32_t mask = 0;
+  const uint32_t valid = (n - row0) >= 16 ? 0xFFFFu : ((1u << (n - row0)) - 1u);
+  const int op = ch.op;
+  if constexpr (IS_DICT) {
+    const E null_vid = static_cast<E>(ch.column.dictionary_size);
+    const E s = static_cast<E>(ch.search_vid);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const bool m = (v[i] != null_vid) && cmp_op<E>(op, v[i], s);
+      mask |= static_cast<uint32_t>(m) << i;
+    }
+  } else {
+    uint8_t nl[16];
+    __builtin_memcpy(nl, &nulls, 16);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const bool m = (nl[i] == 0) && cmp_op<E>(op, v[i], constant.value);
+      mask |= static_cast<uint32_t>(m) << i;
+    }
+  }
+  return mask & valid;
+}
+
 // E = element type read from memory (vid type for DICT, value type for VALUE); IS_DICT selects the semantics.
 // OUT_ROWID: write reference RowIDs {chunk_id, offset} (8 B) instead of chunk offsets (4 B).
 template <typename E, bool IS_DICT, bool OUT_ROWID>
@@ -96,80 +131,81 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanLaunchDesc d, Sc
   const uint32_t c = s_chunk;
   const hy_scan_chunk ch = d.chunks[c];
   const uint64_t first_tile = d.chunk_tile_begin[c];
+  // (for this kernel d.chunk_tile_begin / d.tile_chunk / d.n_tiles / d.status count segments of SEG tiles)
+  constexpr int SEG = seg_tiles<E>();
   const uint32_t tile_in_chunk = static_cast<uint32_t>(tile - first_tile);
-  const uint32_t tile_row0 = tile_in_chunk * SCAN_TILE;
-  const uint32_t row0 = tile_row0 + threadIdx.x * SCAN_ROWS_PER_THREAD;
+  const uint32_t tile_row0 = tile_in_chunk * (SEG * SCAN_TILE);
   const uint32_t n = ch.column.size;
 
-  uint32_t mask = 0;
-  if (row0 < n && ch.op != HY_OP_NONE) {
-    E v[16];
-    load16(reinterpret_cast<const E*>(ch.column.data), row0, v);
-    const uint32_t valid = (n - row0) >= 16 ? 0xFFFFu : ((1u << (n - row0)) - 1u);
-    if constexpr (IS_DICT) {
-      const E null_vid = static_cast<E>(ch.column.dictionary_size);
-      const E s = static_cast<E>(ch.search_vid);
-      const int op = ch.op;
+  // One workgroup = one segment of SEG consecutive tiles of this chunk: all SEG loads per lane are issued up front,
+  // the per-lane 16-bit match masks stay in registers, the segment's count is chained to its predecessors by one
+  // decoupled look-back, and the tiles' offsets are then compacted tile by tile through LDS into coalesced stores.
+  uint32_t masks[SEG];
+  {
+    E v[SEG][16];
+    u32x4 nl[SEG];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const bool m = (v[i] != null_vid) && cmp_op<E>(op, v[i], s);
-        mask |= static_cast<uint32_t>(m) << i;
-      }
-    } else {
-      uint8_t nl[16];
-      if (ch.column.nulls != nullptr) {
-        const u32x4 t = *reinterpret_cast<const u32x4*>(ch.column.nulls + row0);
-        __builtin_memcpy(nl, &t, 16);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) nl[i] = 0;
-      }
-      const int op = ch.op;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const bool m = (nl[i] == 0) && cmp_op<E>(op, v[i], constant.value);
-        mask |= static_cast<uint32_t>(m) << i;
+    for (int t = 0; t < SEG; ++t) {
+      const uint32_t r0 = tile_row0 + t * SCAN_TILE + threadIdx.x * SCAN_ROWS_PER_THREAD;
+      nl[t] = u32x4{0u, 0u, 0u, 0u};
+      if (r0 < n && ch.op != HY_OP_NONE) {
+        load16(reinterpret_cast<const E*>(ch.column.data), r0, v[t]);
+        if (!IS_DICT && ch.column.nulls != nullptr) nl[t] = *reinterpret_cast<const u32x4*>(ch.column.nulls + r0);
       }
     }
-    mask &= valid;
+#pragma unroll
+    for (int t = 0; t < SEG; ++t)
+      masks[t] = match_mask<E, IS_DICT>(ch, tile_row0 + t * SCAN_TILE + threadIdx.x * SCAN_ROWS_PER_THREAD, v[t],
+                                        nl[t], constant);
   }
+  uint32_t mine = 0;
+#pragma unroll
+  for (int t = 0; t < SEG; ++t) mine += __popc(masks[t]);
+  uint32_t seg_total;
+  block_exclusive_sum<SCAN_THREADS>(mine, s_scratch, &seg_total);
 
-  uint32_t tile_total;
-  const uint32_t local = block_exclusive_sum<SCAN_THREADS>(__popc(mask), s_scratch, &tile_total);
-
-  // Decoupled look-back across the tiles of this chunk (wave 0, 64 predecessors per poll).
+  // Decoupled look-back across the segments of this chunk (wave 0, 64 predecessors per poll).
   if (threadIdx.x < WAVE) {
     uint64_t prefix = 0;
     if (tile == first_tile) {
-      if (threadIdx.x == 0) lb_publish(&d.status[tile], LB_FLAG_PREFIX, tile_total);
+      if (threadIdx.x == 0) lb_publish(&d.status[tile], LB_FLAG_PREFIX, seg_total);
     } else {
-      if (threadIdx.x == 0) lb_publish(&d.status[tile], LB_FLAG_AGG, tile_total);
+      if (threadIdx.x == 0) lb_publish(&d.status[tile], LB_FLAG_AGG, seg_total);
       prefix = lb_lookback_wave(d.status, first_tile, tile, d.error);
-      if (threadIdx.x == 0) lb_publish(&d.status[tile], LB_FLAG_PREFIX, prefix + tile_total);
+      if (threadIdx.x == 0) lb_publish(&d.status[tile], LB_FLAG_PREFIX, prefix + seg_total);
     }
     if (threadIdx.x == 0) {
       s_prefix = prefix;
       const uint64_t last_tile = d.chunk_tile_begin[c + 1] - 1;
-      if (tile == last_tile) counts[d.chunk_index[c]] = static_cast<uint32_t>(prefix + tile_total);
+      if (tile == last_tile) counts[d.chunk_index[c]] = static_cast<uint32_t>(prefix + seg_total);
     }
   }
-
-  // Stage matching offsets in LDS in order, then store them coalesced.
-  uint32_t pos = local;
-  uint32_t m = mask;
-  while (m) {
-    const int i = __builtin_ctz(m);
-    m &= m - 1;
-    s_stage[pos++] = row0 + i;
-  }
   __syncthreads();
-  if constexpr (OUT_ROWID) {
-    const uint32_t cid = d.chunk_ids[c];
-    hy_row_id* out = static_cast<hy_row_id*>(out_any) + ch.out_begin + s_prefix;
-    for (uint32_t i = threadIdx.x; i < tile_total; i += SCAN_THREADS) out[i] = hy_row_id{cid, s_stage[i]};
-  } else {
-    uint32_t* out = static_cast<uint32_t*>(out_any) + ch.out_begin + s_prefix;
-    for (uint32_t i = threadIdx.x; i < tile_total; i += SCAN_THREADS) out[i] = s_stage[i];
+  uint64_t run = ch.out_begin + s_prefix;
+  const uint32_t cid = OUT_ROWID ? d.chunk_ids[c] : 0u;
+#pragma unroll
+  for (int t = 0; t < SEG; ++t) {
+    if (tile_row0 + t * SCAN_TILE >= n) break;  // uniform
+    const uint32_t r0 = tile_row0 + t * SCAN_TILE + threadIdx.x * SCAN_ROWS_PER_THREAD;
+    uint32_t tile_total;
+    uint32_t pos = block_exclusive_sum<SCAN_THREADS>(__popc(masks[t]), s_scratch, &tile_total);
+    // stage matching offsets in LDS in order, then store them coalesced
+    uint32_t m = masks[t];
+    while (m) {
+      const int i = __builtin_ctz(m);
+      m &= m - 1;
+      s_stage[pos++] = r0 + i;
+    }
+    __syncthreads();
+    if constexpr (OUT_ROWID) {
+      hy_row_id* out = static_cast<hy_row_id*>(out_any) + run;
+      for (uint32_t i = threadIdx.x; i < tile_total; i += SCAN_THREADS) out[i] = hy_row_id{cid, s_stage[i]};
+    } else {
+      uint32_t* out = static_cast<uint32_t*>(out_any) + run;
+      for (uint32_t i = threadIdx.x; i < tile_total; i += SCAN_THREADS) out[i] = s_stage[i];
+    }
+    run += tile_total;
+    __syncthreads();  // s_stage is refilled by the next tile
   }
 }
 
