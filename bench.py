@@ -235,10 +235,14 @@ def main():
     valid_build, valid_probe = n_ord, n_probe
     alg = {
         "scan_dict": n_li * 1 + n_probe * 8,
-        "part1_hist": valid_build * 4 + valid_probe * (8 + 4),
-        "part1_scatter": valid_build * (4 + 8) + valid_probe * (8 + 4 + 8),
-        "part2_hist": (valid_build + valid_probe) * 8,
-        "part2_scatter": (valid_build + valid_probe) * 16,
+        "part1_hist.build": valid_build * 4,
+        "part1_hist.probe": valid_probe * (8 + 4),
+        "part1_scatter.build": valid_build * (4 + 8),
+        "part1_scatter.probe": valid_probe * (8 + 4 + 8),
+        "part2_hist.build": valid_build * 8,
+        "part2_hist.probe": valid_probe * 8,
+        "part2_scatter.build": valid_build * 16,
+        "part2_scatter.probe": valid_probe * 16,
         "join_partition": (valid_build + valid_probe) * 8 + pairs * 16,
     }
     for k, v in kernels.items():
@@ -304,7 +308,7 @@ def committed_traffic(kernel, sf, chunk, world):
     (profiles/rNN_rocprof_sf<SF>_summary.json, written by tools/profile_bench.sh: FETCH_SIZE x2 + WRITE_SIZE as the
     MI355X guide prescribes). The counters need their own rocprofv3 passes, so they are not re-collected here; the
     summary named in traffic_source is the evidence. None if no summary matches (other scale factor or N>1)."""
-    if world != 1 or chunk != 100_000:
+    if world != 1 or chunk != 100_000 or "." in kernel:  # per-side timers have no per-side rocprof counters
         return None, None
     here = os.path.dirname(os.path.abspath(__file__))
     files = sorted(glob.glob(os.path.join(here, "profiles", f"r*_rocprof_sf{sf:g}_summary.json")))

@@ -705,7 +705,7 @@ hy_status run_scan(const uint32_t* in, uint32_t* out, uint64_t n, const Common& 
 }
 
 template <typename T, typename H>
-hy_status partition_side(const SidePlan& p, const SideBufs<H>& b, const Geometry& g, uint32_t seed, bool keep_nulls,
+hy_status partition_side(const char* side_tag, const SidePlan& p, const SideBufs<H>& b, const Geometry& g, uint32_t seed, bool keep_nulls,
                          const Common& c, uint64_t* side_total, hipStream_t s, hyk::Rec<H>** final_recs) {
   hyk::Side sd{};
   sd.chunks = b.chunks;
@@ -731,7 +731,7 @@ hy_status partition_side(const SidePlan& p, const SideBufs<H>& b, const Geometry
                        sd.n_chunks, b.tile_owner1);
     HY_HIP(hipGetLastError());
     {
-      KTimer kt_("part1_hist", s, p.n_rows);
+      KTimer kt_((std::string("part1_hist.") + side_tag).c_str(), s, p.n_rows);
       hipLaunchKernelGGL((hyk::part1_hist<T, H>), dim3(static_cast<uint32_t>(p.n_tiles1)), dim3(hyk::PART_THREADS), 0, s,
                        sd, d1, g.n_digits1, b.hist1);
       kt_.done();
@@ -740,7 +740,7 @@ hy_status partition_side(const SidePlan& p, const SideBufs<H>& b, const Geometry
     hy_status st = run_scan(b.hist1, b.off1, h1n, c, s, side_total);
     if (st != HY_OK) return st;
     {
-      KTimer kt_("part1_scatter", s, p.n_rows);
+      KTimer kt_((std::string("part1_scatter.") + side_tag).c_str(), s, p.n_rows);
       hipLaunchKernelGGL((hyk::part1_scatter<T, H>), dim3(static_cast<uint32_t>(p.n_tiles1)), dim3(hyk::PART_THREADS), 0,
                        s, sd, d1, dbits1, g.n_digits1, b.off1, b.rec1);
       kt_.done();
@@ -766,7 +766,7 @@ hy_status partition_side(const SidePlan& p, const SideBufs<H>& b, const Geometry
   hyk::Digit d2{mask, 0u, 0xFFu, seed};
   const uint64_t grid2 = b.max_tiles2;
   {
-      KTimer kt_("part2_hist", s, p.n_rows);
+      KTimer kt_((std::string("part2_hist.") + side_tag).c_str(), s, p.n_rows);
       hipLaunchKernelGGL((hyk::part2_hist<H>), dim3(static_cast<uint32_t>(grid2)), dim3(hyk::PART_THREADS), 0, s, sg, d2,
                      256u, b.rec1, b.hist2);
       kt_.done();
@@ -775,7 +775,7 @@ hy_status partition_side(const SidePlan& p, const SideBufs<H>& b, const Geometry
   hy_status st = run_scan(b.hist2, b.off2, grid2 * 256, c, s);
   if (st != HY_OK) return st;
   {
-      KTimer kt_("part2_scatter", s, p.n_rows);
+      KTimer kt_((std::string("part2_scatter.") + side_tag).c_str(), s, p.n_rows);
       hipLaunchKernelGGL((hyk::part2_scatter<H>), dim3(static_cast<uint32_t>(grid2)), dim3(hyk::PART_THREADS), 0, s, sg,
                      d2, 8, 256u, b.rec1, b.off2, b.rec2);
       kt_.done();
@@ -837,9 +837,9 @@ hy_status join_typed(const SidePlan& bp, const SidePlan& pp, const hy_join_param
   const bool keep_nulls = prm->mode == HY_JOIN_LEFT || prm->mode == HY_JOIN_RIGHT;
   hyk::Rec<H>* brec = nullptr;
   hyk::Rec<H>* precs = nullptr;
-  hy_status st = partition_side<TB, H>(bp, bb, g, prm->seed, false, c, c.totals + 2, s, &brec);
+  hy_status st = partition_side<TB, H>("build", bp, bb, g, prm->seed, false, c, c.totals + 2, s, &brec);
   if (st != HY_OK) return st;
-  st = partition_side<TP, H>(pp, pb, g, prm->seed, keep_nulls, c, c.totals + 3, s, &precs);
+  st = partition_side<TP, H>("probe", pp, pb, g, prm->seed, keep_nulls, c, c.totals + 3, s, &precs);
   if (st != HY_OK) return st;
 
   // largest build partition decides the LDS table size

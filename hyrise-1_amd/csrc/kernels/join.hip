@@ -153,19 +153,62 @@ template <typename T, typename H>
 __device__ __forceinline__ uint32_t load_items(const Side& s, const SrcChunk& ch, uint32_t base, H (&keys)[PART_ITEMS],
                                                uint32_t (&pays)[PART_ITEMS]) {
   uint32_t act = 0;
+  // Fast paths issue all PART_ITEMS loads of a phase before using any of them (the general per-item path below
+  // serialises each item's dependent loads).
+  if (ch.pos_list == nullptr && ch.kind == HY_COL_VALUE && ch.nulls == nullptr) {
+    const T* data = static_cast<const T*>(ch.data);
+    T v[PART_ITEMS];
+#pragma unroll
+    for (int k = 0; k < PART_ITEMS; ++k) {
+      const uint32_t off = base + k * WAVE + __lane_id();
+      v[k] = off < ch.size ? data[off] : T{};
+    }
+#pragma unroll
+    for (int k = 0; k < PART_ITEMS; ++k) {
+      const uint32_t off = base + k * WAVE + __lane_id();
+      keys[k] = static_cast<H>(v[k]);
+      pays[k] = static_cast<uint32_t>(ch.row_begin + off);
+      if (off < ch.size) act |= 1u << k;
+    }
+    return act;
+  }
   if (ch.pos_list != nullptr && ch.single_chunk != HY_MIXED_CHUNKS) {
     const SrcChunk rc = s.referenced[ch.single_chunk];
     const uint64_t rrow = s.fuse_deref ? s.referenced_row_begin[ch.single_chunk] : 0;
+    hy_row_id rid[PART_ITEMS];
+#pragma unroll
+    for (int k = 0; k < PART_ITEMS; ++k) {
+      const uint32_t off = base + k * WAVE + __lane_id();
+      rid[k] = off < ch.size ? ch.pos_list[off] : hy_row_id{0xFFFFFFFFu, 0xFFFFFFFFu};
+    }
+    if (rc.kind == HY_COL_VALUE && rc.nulls == nullptr) {
+      const T* data = static_cast<const T*>(rc.data);
+      T v[PART_ITEMS];
+#pragma unroll
+      for (int k = 0; k < PART_ITEMS; ++k) v[k] = rid[k].chunk_offset != 0xFFFFFFFFu ? data[rid[k].chunk_offset] : T{};
+#pragma unroll
+      for (int k = 0; k < PART_ITEMS; ++k) {
+        const uint32_t off = base + k * WAVE + __lane_id();
+        const bool has = rid[k].chunk_offset != 0xFFFFFFFFu;
+        if (s.fuse_deref)
+          pays[k] = has ? static_cast<uint32_t>(rrow + rid[k].chunk_offset) : NULL_PAYLOAD;
+        else
+          pays[k] = static_cast<uint32_t>(ch.row_begin + off);
+        keys[k] = static_cast<H>(v[k]);
+        if (off < ch.size && (has || s.keep_nulls)) act |= 1u << k;
+      }
+      return act;
+    }
 #pragma unroll
     for (int k = 0; k < PART_ITEMS; ++k) {
       const uint32_t off = base + k * WAVE + __lane_id();
       if (off >= ch.size) continue;
-      const hy_row_id rid = ch.pos_list[off];
-      const bool has = rid.chunk_offset != 0xFFFFFFFFu;
+      const hy_row_id rid1 = rid[k];
+      const bool has = rid1.chunk_offset != 0xFFFFFFFFu;
       T v = T{};
-      const bool valid = has && read_column_value<T>(rc, rid.chunk_offset, &v, false);
+      const bool valid = has && read_column_value<T>(rc, rid1.chunk_offset, &v, false);
       if (s.fuse_deref)
-        pays[k] = has ? static_cast<uint32_t>(rrow + rid.chunk_offset) : NULL_PAYLOAD;
+        pays[k] = has ? static_cast<uint32_t>(rrow + rid1.chunk_offset) : NULL_PAYLOAD;
       else
         pays[k] = static_cast<uint32_t>(ch.row_begin + off);
       keys[k] = static_cast<H>(v);
