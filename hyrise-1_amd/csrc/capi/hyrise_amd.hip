@@ -887,9 +887,9 @@ hy_status join_typed(const SidePlan& bp, const SidePlan& pp, const hy_join_param
                            out_probe, partition_begin, partition_counts);
       };
       if (jd.trace)  // debug phase-trace instance (hy_debug_set_join_trace)
-        wide ? launch(hyk::join_partition<H, true, 12>) : launch(hyk::join_partition<H, true, hyk::JP_PER>);
+        wide ? launch(hyk::join_partition<H, true, 6>) : launch(hyk::join_partition<H, true, hyk::JP_PER>);
       else
-        wide ? launch(hyk::join_partition<H, false, 12>) : launch(hyk::join_partition<H, false, hyk::JP_PER>);
+        wide ? launch(hyk::join_partition<H, false, 6>) : launch(hyk::join_partition<H, false, hyk::JP_PER>);
       kt_.done();
     }
   HY_HIP(hipGetLastError());

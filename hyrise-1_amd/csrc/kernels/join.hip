@@ -558,9 +558,9 @@ __global__ __launch_bounds__(SCAN_T) void exclusive_scan_u32(const uint32_t* __r
 // partition is one pass) with all loads in flight, matched, counted, and - once one atomic add has reserved the
 // partition's output range - written without re-reading them.
 // ------------------------------------------------------------------------------------------------------------
-constexpr int JOIN_THREADS = 512;
+constexpr int JOIN_THREADS = 1024;
 constexpr int JOIN_WAVES = JOIN_THREADS / WAVE;
-constexpr int JP_PER = 8;                          // probe records per thread per pass
+constexpr int JP_PER = 4;                          // probe records per thread per pass
 constexpr int JP_PASS = JP_PER * JOIN_THREADS;     // 4096
 constexpr uint32_t LDS_MAX_ROWS = 0xFFFFu;         // entry indexes and counts of one table fit 16 bits
 
@@ -647,7 +647,7 @@ __device__ __forceinline__ uint32_t bucket_of(H key, uint32_t NB) {
 // records whose loads are all in flight together - the first batch's while the bucket sizes are being cleared. A
 // partition larger than one batch re-reads its records (from L2) for the second counting-sort pass. Ends with a
 // barrier.
-constexpr int BUILD_PER = 6;  // >= the largest 4-byte-key table in the default LDS budget / JOIN_THREADS
+constexpr int BUILD_PER = 3;  // >= the largest 4-byte-key table in the default LDS budget / JOIN_THREADS
 template <typename H>
 __device__ __forceinline__ void build_table(const BTable<H>& t, const Rec<H>* __restrict__ build, uint32_t b0,
                                             uint32_t n, uint32_t* s_scratch) {
@@ -995,7 +995,7 @@ __device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t
 }
 
 template <typename H, bool TRACE, int JP>
-__global__ __launch_bounds__(JOIN_THREADS) void join_partition(JoinDesc d, const Rec<H>* __restrict__ build,
+__global__ __launch_bounds__(JOIN_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void join_partition(JoinDesc d, const Rec<H>* __restrict__ build,
                                                                const Rec<H>* __restrict__ probe,
                                                                hy_row_id* __restrict__ out_build,
                                                                hy_row_id* __restrict__ out_probe,
