@@ -308,13 +308,13 @@ def committed_traffic(kernel, sf, chunk, world):
     (profiles/rNN_rocprof_sf<SF>_summary.json, written by tools/profile_bench.sh: FETCH_SIZE x2 + WRITE_SIZE as the
     MI355X guide prescribes). The counters need their own rocprofv3 passes, so they are not re-collected here; the
     summary named in traffic_source is the evidence. None if no summary matches (other scale factor or N>1)."""
-    if world != 1 or chunk != 100_000 or "." in kernel:  # per-side timers have no per-side rocprof counters
+    if world != 1 or chunk != 100_000:
         return None, None
     here = os.path.dirname(os.path.abspath(__file__))
     files = sorted(glob.glob(os.path.join(here, "profiles", f"r*_rocprof_sf{sf:g}_summary.json")))
     for f in reversed(files):
         with open(f) as fh:
-            k = json.load(fh).get("kernels", {}).get(ROCPROF_NAME.get(kernel, kernel), {})
+            k = json.load(fh).get("kernels", {}).get(ROCPROF_NAME.get(kernel, kernel), {})  # part*.build/.probe split
         if "hbm_bytes_per_launch" in k:
             return k["hbm_bytes_per_launch"], os.path.relpath(f, here)
     return None, None

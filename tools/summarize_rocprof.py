@@ -40,6 +40,19 @@ def main(out):
                 acc[k][1] += float(row["TotalDurationNs"])
         for k, (calls, tot) in acc.items():
             res["kernels"].setdefault(k, {}).update(calls=calls, avg_ns=tot / calls, total_ns=tot)
+    trace = one(os.path.join(out, "trace", "**", "*kernel_trace.csv"))
+    if trace:  # per-side average durations of the partition kernels (launch order: build, probe)
+        durs = defaultdict(list)
+        with open(trace) as f:
+            for row in csv.DictReader(f):
+                k = short(row["Kernel_Name"])
+                if k.startswith(("part1_", "part2_")):
+                    durs[k].append((int(row["Dispatch_Id"]), int(row["End_Timestamp"]) - int(row["Start_Timestamp"])))
+        for k, v in durs.items():
+            v.sort()
+            for tag, sel in ((".build", v[0::2]), (".probe", v[1::2])):
+                if sel:
+                    res["kernels"].setdefault(k + tag, {}).update(calls=len(sel), avg_ns=sum(x for _, x in sel) / len(sel))
     for counter, scale in (("FETCH_SIZE", 2.0), ("WRITE_SIZE", 1.0)):
         f = one(os.path.join(out, counter, "**", "*counter_collection.csv"))
         if not f:
@@ -56,6 +69,11 @@ def main(out):
         by_kernel = defaultdict(list)
         for d, v in per_dispatch.items():
             by_kernel[names[d]].append(v * 1024.0 * scale)
+        # partition kernels run once per join side, build first: split their launches into .build / .probe
+        for k in [k for k in by_kernel if k.startswith(("part1_", "part2_"))]:
+            ordered = [v for d, v in sorted(((int(d), v) for d, v in per_dispatch.items() if names[d] == k))]
+            by_kernel[k + ".build"] = [v * 1024.0 * scale for v in ordered[0::2]]
+            by_kernel[k + ".probe"] = [v * 1024.0 * scale for v in ordered[1::2]]
         key = "hbm_read_bytes_per_launch" if counter == "FETCH_SIZE" else "hbm_write_bytes_per_launch"
         for k, vals in by_kernel.items():
             res["kernels"].setdefault(k, {})[key] = sum(vals) / len(vals)
