@@ -49,7 +49,7 @@ class JoinChunk(ctypes.Structure):
 class JoinSide(ctypes.Structure):
     _fields_ = [("chunks", ctypes.POINTER(JoinChunk)), ("n_chunks", ctypes.c_uint32), ("value_type", ctypes.c_int32),
                 ("referenced", ctypes.POINTER(ColumnChunk)), ("n_referenced", ctypes.c_uint32),
-                ("fuse_dereference", ctypes.c_int32)]
+                ("fuse_dereference", ctypes.c_int32), ("referenced_chunk_base", ctypes.c_uint32)]
 
 
 class JoinParams(ctypes.Structure):
@@ -124,6 +124,22 @@ _sigs = {
     "hy_agg_float_sum": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32, ctypes.c_int32,
                                         ctypes.c_uint64, ctypes.POINTER(ctypes.c_double)]),
     "hy_agg_decode_ordered": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_int32]),
+    "hy_join_exchange_bucket_bits": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32]),
+    "hy_join_exchange_partition_workspace_size": (ctypes.c_int, [ctypes.POINTER(JoinSide), ctypes.POINTER(JoinParams),
+                                                                 ctypes.c_uint32, ctypes.POINTER(ctypes.c_size_t)]),
+    "hy_join_exchange_partition": (ctypes.c_int, [ctypes.POINTER(JoinSide), ctypes.POINTER(JoinParams), ctypes.c_int32,
+                                                  ctypes.c_uint32, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
+                                                  ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "hy_join_exchange_join_workspace_size": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64),
+                                                            ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32,
+                                                            ctypes.c_uint32, ctypes.POINTER(JoinParams),
+                                                            ctypes.POINTER(ctypes.c_size_t)]),
+    "hy_join_exchange_join": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p,
+                                             ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32, ctypes.c_uint32,
+                                             ctypes.c_uint32, ctypes.POINTER(JoinParams), ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.POINTER(JoinResult), ctypes.c_void_p, ctypes.c_size_t,
+                                             ctypes.c_void_p]),
 }
 for _name, (_res, _args) in _sigs.items():
     _f = getattr(lib, _name)

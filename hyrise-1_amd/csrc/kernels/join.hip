@@ -32,10 +32,12 @@ constexpr int PART_TILE = PART_THREADS * PART_ITEMS;        // 4096 rows per til
 constexpr int WAVE_SPAN = WAVE * PART_ITEMS;                // 1024 consecutive rows per wave
 constexpr uint32_t NULL_PAYLOAD = 0xFFFFFFFFu;
 
-template <typename H>
-struct __attribute__((aligned(sizeof(H) == 8 ? 16 : 8))) Rec {
+// Partition record: join key (hashed type) + payload. Single-GPU payload = 32-bit row index in the side's row space
+// (8 B records for 4-byte keys); exchange records of the distributed join carry the row's global RowID (16 B).
+template <typename H, typename P = uint32_t>
+struct __attribute__((aligned(sizeof(H) == 8 || sizeof(P) == 8 ? 16 : 8))) Rec {
   H key;
-  uint32_t payload;
+  P payload;
 };
 
 // Column chunk of one join side as the device sees it.
@@ -44,7 +46,8 @@ struct SrcChunk {
   const uint8_t* nulls;
   const void* dictionary;
   const hy_row_id* pos_list;  // reference chunk when != nullptr
-  uint32_t single_chunk;      // reference chunk: the only referenced chunk id, or HY_MIXED_CHUNKS
+  uint32_t single_chunk;      // reference chunk: the only referenced chunk (index into Side::referenced), or HY_MIXED_CHUNKS
+  uint32_t chunk_id;          // chunk id written into RowID payloads (distributed join: global chunk id)
   uint32_t size;
   uint32_t dictionary_size;
   int32_t kind;
@@ -78,6 +81,25 @@ __device__ __forceinline__ hy_row_id map_row(const RowMap& m, uint32_t idx) {
   return hy_row_id{lo, static_cast<uint32_t>(idx - m.row_begin[lo])};
 }
 
+// RowID payloads (exchange records) already are the output RowIDs.
+__device__ __forceinline__ hy_row_id map_row(const RowMap&, hy_row_id rid) { return rid; }
+
+// Payload of row `off` of chunk c itself, and of a referenced row (fused dereference).
+template <typename P>
+__device__ __forceinline__ P own_payload(uint64_t row_begin, uint32_t chunk_id, uint32_t off) {
+  if constexpr (std::is_same_v<P, hy_row_id>)
+    return hy_row_id{chunk_id, off};
+  else
+    return static_cast<uint32_t>(row_begin + off);
+}
+template <typename P>
+__device__ __forceinline__ P ref_payload(bool has, const hy_row_id& rid, uint64_t ref_row_begin) {
+  if constexpr (std::is_same_v<P, hy_row_id>)
+    return has ? rid : hy_row_id{0xFFFFFFFFu, 0xFFFFFFFFu};
+  else
+    return has ? static_cast<uint32_t>(ref_row_begin + rid.chunk_offset) : NULL_PAYLOAD;
+}
+
 struct Side {
   const SrcChunk* chunks;
   uint32_t n_chunks;
@@ -89,6 +111,7 @@ struct Side {
   const uint64_t* referenced_row_begin;  // for fused dereference payloads
   int32_t fuse_deref;                // payload = row in the referenced table instead of row in this table
   int32_t keep_nulls;
+  uint32_t ref_base;                 // RowIDs in PosLists name referenced chunk ref_base + i for Side::referenced[i]
 };
 
 // NULL rows: a ValueColumn read directly yields its stored value (value_column_iterable), a dictionary column and
@@ -121,8 +144,8 @@ __device__ __forceinline__ bool read_column_value(const SrcChunk& c, uint32_t of
 
 // Loads row `off` of chunk `c`: key (cast to the hashed type), payload, validity (NULLs are dropped unless
 // keep_nulls, as materialize_input does at join_hash.cpp:253).
-template <typename T, typename H>
-__device__ __forceinline__ bool load_row(const Side& s, const SrcChunk& c, uint32_t off, H* key, uint32_t* payload) {
+template <typename T, typename H, typename P>
+__device__ __forceinline__ bool load_row(const Side& s, const SrcChunk& c, uint32_t off, H* key, P* payload) {
   T v;
   bool valid;
   if (c.pos_list != nullptr) {
@@ -130,15 +153,16 @@ __device__ __forceinline__ bool load_row(const Side& s, const SrcChunk& c, uint3
     if (rid.chunk_offset == 0xFFFFFFFFu) {
       v = T{};
       valid = false;
-      *payload = s.fuse_deref ? NULL_PAYLOAD : static_cast<uint32_t>(c.row_begin + off);
+      *payload = s.fuse_deref ? ref_payload<P>(false, rid, 0) : own_payload<P>(c.row_begin, c.chunk_id, off);
     } else {
-      valid = read_column_value<T>(s.referenced[rid.chunk_id], rid.chunk_offset, &v, false);
-      *payload = s.fuse_deref ? static_cast<uint32_t>(s.referenced_row_begin[rid.chunk_id] + rid.chunk_offset)
-                              : static_cast<uint32_t>(c.row_begin + off);
+      const uint32_t rc = rid.chunk_id - s.ref_base;
+      valid = read_column_value<T>(s.referenced[rc], rid.chunk_offset, &v, false);
+      *payload = s.fuse_deref ? ref_payload<P>(true, rid, s.referenced_row_begin[rc])
+                              : own_payload<P>(c.row_begin, c.chunk_id, off);
     }
   } else {
     valid = read_column_value<T>(c, off, &v, true);
-    *payload = static_cast<uint32_t>(c.row_begin + off);
+    *payload = own_payload<P>(c.row_begin, c.chunk_id, off);
   }
   *key = static_cast<H>(v);
   return valid || s.keep_nulls;
@@ -149,9 +173,9 @@ __device__ __forceinline__ bool load_row(const Side& s, const SrcChunk& c, uint3
 // materialize_input does at join_hash.cpp:253). A reference chunk whose PosList references a single chunk (known
 // from its producer, hy_join_chunk.single_chunk) reads that chunk's descriptor once with scalar loads instead of once
 // per lane and row.
-template <typename T, typename H>
+template <typename T, typename H, typename P>
 __device__ __forceinline__ uint32_t load_items(const Side& s, const SrcChunk& ch, uint32_t base, H (&keys)[PART_ITEMS],
-                                               uint32_t (&pays)[PART_ITEMS]) {
+                                               P (&pays)[PART_ITEMS]) {
   uint32_t act = 0;
   // Fast paths issue all PART_ITEMS loads of a phase before using any of them (the general per-item path below
   // serialises each item's dependent loads).
@@ -167,7 +191,7 @@ __device__ __forceinline__ uint32_t load_items(const Side& s, const SrcChunk& ch
     for (int k = 0; k < PART_ITEMS; ++k) {
       const uint32_t off = base + k * WAVE + __lane_id();
       keys[k] = static_cast<H>(v[k]);
-      pays[k] = static_cast<uint32_t>(ch.row_begin + off);
+      pays[k] = own_payload<P>(ch.row_begin, ch.chunk_id, off);
       if (off < ch.size) act |= 1u << k;
     }
     return act;
@@ -190,10 +214,7 @@ __device__ __forceinline__ uint32_t load_items(const Side& s, const SrcChunk& ch
       for (int k = 0; k < PART_ITEMS; ++k) {
         const uint32_t off = base + k * WAVE + __lane_id();
         const bool has = rid[k].chunk_offset != 0xFFFFFFFFu;
-        if (s.fuse_deref)
-          pays[k] = has ? static_cast<uint32_t>(rrow + rid[k].chunk_offset) : NULL_PAYLOAD;
-        else
-          pays[k] = static_cast<uint32_t>(ch.row_begin + off);
+        pays[k] = s.fuse_deref ? ref_payload<P>(has, rid[k], rrow) : own_payload<P>(ch.row_begin, ch.chunk_id, off);
         keys[k] = static_cast<H>(v[k]);
         if (off < ch.size && (has || s.keep_nulls)) act |= 1u << k;
       }
@@ -207,10 +228,7 @@ __device__ __forceinline__ uint32_t load_items(const Side& s, const SrcChunk& ch
       const bool has = rid1.chunk_offset != 0xFFFFFFFFu;
       T v = T{};
       const bool valid = has && read_column_value<T>(rc, rid1.chunk_offset, &v, false);
-      if (s.fuse_deref)
-        pays[k] = has ? static_cast<uint32_t>(rrow + rid1.chunk_offset) : NULL_PAYLOAD;
-      else
-        pays[k] = static_cast<uint32_t>(ch.row_begin + off);
+      pays[k] = s.fuse_deref ? ref_payload<P>(has, rid1, rrow) : own_payload<P>(ch.row_begin, ch.chunk_id, off);
       keys[k] = static_cast<H>(v);
       if (valid || s.keep_nulls) act |= 1u << k;
     }
@@ -219,7 +237,7 @@ __device__ __forceinline__ uint32_t load_items(const Side& s, const SrcChunk& ch
 #pragma unroll
   for (int k = 0; k < PART_ITEMS; ++k) {
     const uint32_t off = base + k * WAVE + __lane_id();
-    if (off < ch.size && load_row<T, H>(s, ch, off, &keys[k], &pays[k])) act |= 1u << k;
+    if (off < ch.size && load_row<T, H, P>(s, ch, off, &keys[k], &pays[k])) act |= 1u << k;
   }
   return act;
 }
@@ -281,11 +299,11 @@ __device__ __forceinline__ uint32_t wave_rank(uint32_t digit, bool active, int d
 // consecutive lanes, so each bucket's run of the tile is written with coalesced stores instead of one scattered 8-byte
 // store per lane. goff(d) = output position of this tile's first digit-d record.
 static_assert(PART_THREADS >= 256, "one thread per digit");
-template <typename H, typename GOFF>
-__device__ __forceinline__ void staged_scatter(const Rec<H> (&recs)[PART_ITEMS], uint32_t act,
+template <typename H, typename P, typename GOFF>
+__device__ __forceinline__ void staged_scatter(const Rec<H, P> (&recs)[PART_ITEMS], uint32_t act,
                                                const uint32_t (&dr)[PART_ITEMS], uint32_t (*s_cnt)[256],
-                                               uint32_t* s_delta, Rec<H>* s_stage, uint32_t* s_scratch,
-                                               uint32_t n_digits, const Digit& dg, GOFF goff, Rec<H>* __restrict__ out) {
+                                               uint32_t* s_delta, Rec<H, P>* s_stage, uint32_t* s_scratch,
+                                               uint32_t n_digits, const Digit& dg, GOFF goff, Rec<H, P>* __restrict__ out) {
   const int w = threadIdx.x / WAVE;
   __syncthreads();  // every wave's counts are in s_cnt
   const uint32_t d = threadIdx.x;
@@ -311,7 +329,7 @@ __device__ __forceinline__ void staged_scatter(const Rec<H> (&recs)[PART_ITEMS],
     if ((act >> k) & 1u) s_stage[s_cnt[w][dr[k] >> 24] + (dr[k] & 0xFFFFFFu)] = recs[k];
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < total; i += PART_THREADS) {
-    const Rec<H> r = s_stage[i];
+    const Rec<H, P> r = s_stage[i];
     out[i + s_delta[digit_of<H>(dg, r.key)]] = r;
   }
 }
@@ -332,7 +350,7 @@ __global__ __launch_bounds__(PART_THREADS) void part1_hist(Side s, Digit dg, uin
   const int w = threadIdx.x / WAVE;
   H keys[PART_ITEMS];
   uint32_t pays[PART_ITEMS];
-  const uint32_t act = load_items<T, H>(s, ch, base + w * WAVE_SPAN, keys, pays);
+  const uint32_t act = load_items<T, H, uint32_t>(s, ch, base + w * WAVE_SPAN, keys, pays);
 #pragma unroll
   for (int k = 0; k < PART_ITEMS; ++k)
     if ((act >> k) & 1u) atomicAdd(&s_hist[digit_of<H>(dg, keys[k])], 1u);
@@ -340,14 +358,14 @@ __global__ __launch_bounds__(PART_THREADS) void part1_hist(Side s, Digit dg, uin
   for (uint32_t d = threadIdx.x; d < n_digits; d += PART_THREADS) hist[d * s.n_tiles + tile] = s_hist[d];
 }
 
-template <typename T, typename H>
+template <typename T, typename H, typename P>
 __global__ __launch_bounds__(PART_THREADS) void part1_scatter(Side s, Digit dg, int dbits, uint32_t n_digits,
                                                              const uint32_t* __restrict__ offsets,
-                                                             Rec<H>* __restrict__ out) {
+                                                             Rec<H, P>* __restrict__ out) {
   __shared__ uint32_t s_cnt[PART_WAVES][256];
   __shared__ uint32_t s_delta[256];
   __shared__ uint32_t s_scratch[PART_WAVES + 1];
-  __shared__ Rec<H> s_stage[PART_TILE];
+  __shared__ Rec<H, P> s_stage[PART_TILE];
   const uint64_t tile = blockIdx.x;
   for (int i = threadIdx.x; i < PART_WAVES * 256; i += PART_THREADS) (&s_cnt[0][0])[i] = 0;
   __syncthreads();
@@ -357,10 +375,10 @@ __global__ __launch_bounds__(PART_THREADS) void part1_scatter(Side s, Digit dg, 
   const int w = threadIdx.x / WAVE;
 
   H keys[PART_ITEMS];
-  uint32_t pays[PART_ITEMS];
+  P pays[PART_ITEMS];
   uint32_t dr[PART_ITEMS];  // digit << 24 | rank within the wave (rank < WAVE_SPAN)
-  const uint32_t act = load_items<T, H>(s, ch, base + w * WAVE_SPAN, keys, pays);
-  Rec<H> recs[PART_ITEMS];
+  const uint32_t act = load_items<T, H, P>(s, ch, base + w * WAVE_SPAN, keys, pays);
+  Rec<H, P> recs[PART_ITEMS];
 #pragma unroll
   for (int k = 0; k < PART_ITEMS; ++k) {
     const bool a = (act >> k) & 1u;
@@ -369,23 +387,43 @@ __global__ __launch_bounds__(PART_THREADS) void part1_scatter(Side s, Digit dg, 
     recs[k].key = keys[k];
     recs[k].payload = pays[k];
   }
-  staged_scatter<H>(recs, act, dr, s_cnt, s_delta, s_stage, s_scratch, n_digits, dg,
+  staged_scatter<H, P>(recs, act, dr, s_cnt, s_delta, s_stage, s_scratch, n_digits, dg,
                     [&](uint32_t d) { return offsets[d * s.n_tiles + tile]; }, out);
 }
 
 // ------------------------------------------------------------------------------------------------------------
 // Pass 2: records -> records, inside every pass-1 bucket (segment).
 // ------------------------------------------------------------------------------------------------------------
+// Pass-2 segments. Single-GPU: the pass-1 buckets, contiguous (seg_begin[i], seg_begin[i+1]) with the histogram of
+// segment i at [seg_tile_begin[i] * n_digits, ...) digit-major. Distributed join (receiver): one segment per
+// (bucket, sender) run of the received buffer, listed bucket-major / sender-minor; seg_end gives each run's end, and
+// the histogram of a segment is interleaved with the other senders' runs of its bucket - entry (digit d, tile t) at
+// seg_hbase[i] + d * seg_stride[i] + seg_toff[i] + t - so that the exclusive scan orders the output by (bucket, digit,
+// sender, tile): the reference's (partition, chunk, offset) order across ranks.
 struct Segs {
-  const uint32_t* seg_begin;        // n_segs + 1 record offsets
-  const uint64_t* seg_tile_begin;   // n_segs + 1 tile prefix (device-computed; grid is an upper bound)
+  const uint32_t* seg_begin;        // record offset of each segment (n_segs + 1 entries when seg_end is null)
+  const uint64_t* seg_tile_begin;   // n_segs + 1 tile prefix (grid is an upper bound)
   const uint32_t* tile_seg;         // segment of each pass-2 tile
   uint32_t n_segs;
+  const uint32_t* seg_end;          // null: seg_begin[i + 1]
+  const uint64_t* seg_hbase;        // null: seg_tile_begin[i] * n_digits
+  const uint32_t* seg_stride;       // null: the segment's tile count
+  const uint32_t* seg_toff;         // null: 0
 };
 
-template <typename H>
+__device__ __forceinline__ void seg_geometry(const Segs& sg, uint32_t sgi, uint32_t n_digits, uint32_t* b0, uint32_t* b1,
+                                             uint64_t* hbase, uint32_t* stride, uint32_t* toff) {
+  const uint32_t nt = static_cast<uint32_t>(sg.seg_tile_begin[sgi + 1] - sg.seg_tile_begin[sgi]);
+  *b0 = sg.seg_begin[sgi];
+  *b1 = sg.seg_end ? sg.seg_end[sgi] : sg.seg_begin[sgi + 1];
+  *hbase = sg.seg_hbase ? sg.seg_hbase[sgi] : sg.seg_tile_begin[sgi] * n_digits;
+  *stride = sg.seg_stride ? sg.seg_stride[sgi] : nt;
+  *toff = sg.seg_toff ? sg.seg_toff[sgi] : 0u;
+}
+
+template <typename H, typename P>
 __global__ __launch_bounds__(PART_THREADS) void part2_hist(Segs sg, Digit dg, uint32_t n_digits,
-                                                          const Rec<H>* __restrict__ in, uint32_t* __restrict__ hist) {
+                                                          const Rec<H, P>* __restrict__ in, uint32_t* __restrict__ hist) {
   __shared__ uint32_t s_hist[256];
   const uint64_t tile = blockIdx.x;
   if (tile >= sg.seg_tile_begin[sg.n_segs]) return;
@@ -393,37 +431,38 @@ __global__ __launch_bounds__(PART_THREADS) void part2_hist(Segs sg, Digit dg, ui
   __syncthreads();
   const uint32_t sgi = sg.tile_seg[tile];
   const uint32_t t_in = static_cast<uint32_t>(tile - sg.seg_tile_begin[sgi]);
-  const uint32_t nt = static_cast<uint32_t>(sg.seg_tile_begin[sgi + 1] - sg.seg_tile_begin[sgi]);
-  const uint32_t b0 = sg.seg_begin[sgi], b1 = sg.seg_begin[sgi + 1];
+  uint32_t b0, b1, stride, toff;
+  uint64_t hbase;
+  seg_geometry(sg, sgi, n_digits, &b0, &b1, &hbase, &stride, &toff);
   const int w = threadIdx.x / WAVE;
   for (int k = 0; k < PART_ITEMS; ++k) {
     const uint32_t r = b0 + t_in * PART_TILE + w * WAVE_SPAN + k * WAVE + __lane_id();
     if (r < b1) atomicAdd(&s_hist[digit_of<H>(dg, in[r].key)], 1u);
   }
   __syncthreads();
-  const uint64_t hbase = sg.seg_tile_begin[sgi] * n_digits;
-  for (uint32_t d = threadIdx.x; d < n_digits; d += PART_THREADS) hist[hbase + d * nt + t_in] = s_hist[d];
+  for (uint32_t d = threadIdx.x; d < n_digits; d += PART_THREADS) hist[hbase + d * stride + toff + t_in] = s_hist[d];
 }
 
-template <typename H>
+template <typename H, typename P>
 __global__ __launch_bounds__(PART_THREADS) void part2_scatter(Segs sg, Digit dg, int dbits, uint32_t n_digits,
-                                                             const Rec<H>* __restrict__ in,
+                                                             const Rec<H, P>* __restrict__ in,
                                                              const uint32_t* __restrict__ offsets,
-                                                             Rec<H>* __restrict__ out) {
+                                                             Rec<H, P>* __restrict__ out) {
   __shared__ uint32_t s_cnt[PART_WAVES][256];
   __shared__ uint32_t s_delta[256];
   __shared__ uint32_t s_scratch[PART_WAVES + 1];
-  __shared__ Rec<H> s_stage[PART_TILE];
+  __shared__ Rec<H, P> s_stage[PART_TILE];
   const uint64_t tile = blockIdx.x;
   if (tile >= sg.seg_tile_begin[sg.n_segs]) return;
   for (int i = threadIdx.x; i < PART_WAVES * 256; i += PART_THREADS) (&s_cnt[0][0])[i] = 0;
   __syncthreads();
   const uint32_t sgi = sg.tile_seg[tile];
   const uint32_t t_in = static_cast<uint32_t>(tile - sg.seg_tile_begin[sgi]);
-  const uint32_t nt = static_cast<uint32_t>(sg.seg_tile_begin[sgi + 1] - sg.seg_tile_begin[sgi]);
-  const uint32_t b0 = sg.seg_begin[sgi], b1 = sg.seg_begin[sgi + 1];
+  uint32_t b0, b1, stride, toff;
+  uint64_t hbase;
+  seg_geometry(sg, sgi, n_digits, &b0, &b1, &hbase, &stride, &toff);
   const int w = threadIdx.x / WAVE;
-  Rec<H> recs[PART_ITEMS];
+  Rec<H, P> recs[PART_ITEMS];
   uint32_t dr[PART_ITEMS];  // digit << 24 | rank within the wave
   uint32_t act = 0;
 #pragma unroll
@@ -440,20 +479,12 @@ __global__ __launch_bounds__(PART_THREADS) void part2_scatter(Segs sg, Digit dg,
     const uint32_t dig = a ? digit_of<H>(dg, recs[k].key) : 0u;
     dr[k] = (dig << 24) | wave_rank(dig, a, dbits, s_cnt[w]);
   }
-  const uint64_t hbase = sg.seg_tile_begin[sgi] * n_digits;
-  staged_scatter<H>(recs, act, dr, s_cnt, s_delta, s_stage, s_scratch, n_digits, dg,
-                    [&](uint32_t d) { return offsets[hbase + d * nt + t_in]; }, out);
+  staged_scatter<H, P>(recs, act, dr, s_cnt, s_delta, s_stage, s_scratch, n_digits, dg,
+                       [&](uint32_t d) { return offsets[hbase + d * stride + toff + t_in]; }, out);
 }
 
-// Partition bounds after pass 1 only (radix_bits <= 8): part_begin[d] = offsets[d * n_tiles].
-__global__ void bounds_single_pass(const uint32_t* __restrict__ offsets, uint64_t n_tiles, uint32_t n_parts,
-                                   const uint64_t* __restrict__ total, uint32_t* __restrict__ part_begin) {
-  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p < n_parts) part_begin[p] = n_tiles == 0 ? 0u : offsets[p * n_tiles];
-  if (p == n_parts) part_begin[p] = static_cast<uint32_t>(*total);
-}
-
-// Segment bounds of pass 1 (same formula), plus the pass-2 tile prefix of every segment.
+// Bucket bounds after the pass from column chunks (histogram laid out digit-major over tiles):
+// seg_begin[d] = offsets[d * n_tiles] (output position of the first digit-d record), seg_begin[n_digits] = total.
 __global__ void seg_bounds(const uint32_t* __restrict__ offsets, uint64_t n_tiles, uint32_t n_segs,
                            const uint64_t* __restrict__ total, uint32_t* __restrict__ seg_begin) {
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -461,30 +492,46 @@ __global__ void seg_bounds(const uint32_t* __restrict__ offsets, uint64_t n_tile
   if (p == n_segs) seg_begin[p] = static_cast<uint32_t>(*total);
 }
 
-__global__ void seg_tiles(const uint32_t* __restrict__ seg_begin, uint32_t n_segs, uint64_t* __restrict__ seg_tile_begin) {
-  // single workgroup: sequential prefix over <= 256 segments
-  if (threadIdx.x == 0) {
-    uint64_t run = 0;
-    for (uint32_t s = 0; s < n_segs; ++s) {
-      seg_tile_begin[s] = run;
-      run += (seg_begin[s + 1] - seg_begin[s] + PART_TILE - 1) / PART_TILE;
-    }
-    seg_tile_begin[n_segs] = run;
+// Tiles of every segment of a record pass (counts, then an exclusive scan and widen_prefix give seg_tile_begin).
+__global__ void seg_tile_counts(const uint32_t* __restrict__ seg_begin, const uint32_t* __restrict__ seg_end,
+                                uint32_t n_segs, uint32_t* __restrict__ counts) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_segs; i += gridDim.x * blockDim.x) {
+    const uint32_t b1 = seg_end ? seg_end[i] : seg_begin[i + 1];
+    counts[i] = (b1 - seg_begin[i] + PART_TILE - 1) / PART_TILE;
   }
 }
 
-// Partition bounds after pass 2: partition p = (seg << lo_bits) | d.
-__global__ void bounds_two_pass(const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ seg_begin,
-                                const uint64_t* __restrict__ seg_tile_begin, uint32_t n_segs, uint32_t lo_digits,
-                                const uint64_t* __restrict__ total, uint32_t* __restrict__ part_begin) {
-  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t n_parts = n_segs * lo_digits;
-  if (p < n_parts) {
-    const uint32_t sgi = p / lo_digits, d = p % lo_digits;
-    const uint64_t nt = seg_tile_begin[sgi + 1] - seg_tile_begin[sgi];
-    part_begin[p] = nt == 0 ? seg_begin[sgi] : offsets[seg_tile_begin[sgi] * lo_digits + d * nt];
+__global__ void widen_prefix(const uint32_t* __restrict__ excl, uint32_t n, const uint64_t* __restrict__ total,
+                             uint64_t* __restrict__ out) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += gridDim.x * blockDim.x)
+    out[i] = i < n ? static_cast<uint64_t>(excl[i]) : *total;
+}
+
+// Bounds after a record pass: group g (a segment, or for the distributed receiver a bucket whose runs from all
+// senders are interleaved in the histogram) splits into n_digits parts; bounds[g * n_digits + d] = output position
+// of its first digit-d record, bounds[n_groups * n_digits] = total. Null group arrays: a group is segment g itself
+// (histogram at seg_tile_begin[g] * n_digits, output starting where its input starts).
+struct Groups {
+  const uint64_t* hbase;
+  const uint32_t* tiles;
+  const uint32_t* out_begin;
+};
+
+__global__ void pass_bounds(const uint32_t* __restrict__ offsets, Segs sg, Groups gr, uint32_t n_groups,
+                            uint32_t n_digits, const uint64_t* __restrict__ total, uint32_t* __restrict__ bounds) {
+  const uint64_t n = static_cast<uint64_t>(n_groups) * n_digits;
+  for (uint64_t p = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; p <= n;
+       p += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    if (p == n) {
+      bounds[p] = static_cast<uint32_t>(*total);
+      continue;
+    }
+    const uint32_t g = static_cast<uint32_t>(p / n_digits), d = static_cast<uint32_t>(p % n_digits);
+    const uint64_t hb = gr.hbase ? gr.hbase[g] : sg.seg_tile_begin[g] * n_digits;
+    const uint64_t nt = gr.tiles ? gr.tiles[g] : sg.seg_tile_begin[g + 1] - sg.seg_tile_begin[g];
+    const uint32_t ob = gr.out_begin ? gr.out_begin[g] : sg.seg_begin[g];
+    bounds[p] = nt == 0 ? ob : offsets[hb + d * nt];
   }
-  if (p == n_parts) part_begin[p] = static_cast<uint32_t>(*total);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -579,9 +626,9 @@ struct JoinDesc {
   uint64_t* trace;              // debug phase stamps (hy_debug_set_join_trace) or null
 };
 
-template <typename H>
+template <typename H, typename P>
 struct BTable {
-  Rec<H>* ents;   // nb entries, bucket by bucket
+  Rec<H, P>* ents;   // nb entries, bucket by bucket
   uint32_t* end;  // NB bucket ends
   uint32_t nb;
   uint32_t NB;
@@ -590,18 +637,18 @@ struct BTable {
 __host__ __device__ inline size_t align16(size_t b) { return (b + 15) & ~size_t(15); }
 
 // LDS bytes of a table over nb build rows
-template <typename H>
+template <typename H, typename P>
 __host__ __device__ inline size_t table_bytes(uint32_t nb) {
-  return align16(sizeof(Rec<H>) * nb) + align16(4 * size_t(nb ? nb : 1));
+  return align16(sizeof(Rec<H, P>) * nb) + align16(4 * size_t(nb ? nb : 1));
 }
 
-template <typename H>
-__device__ __forceinline__ BTable<H> table_at(unsigned char* smem, uint32_t nb) {
-  BTable<H> t;
+template <typename H, typename P>
+__device__ __forceinline__ BTable<H, P> table_at(unsigned char* smem, uint32_t nb) {
+  BTable<H, P> t;
   t.nb = nb;
   t.NB = nb ? nb : 1;
-  t.ents = reinterpret_cast<Rec<H>*>(smem);
-  t.end = reinterpret_cast<uint32_t*>(smem + align16(sizeof(Rec<H>) * nb));
+  t.ents = reinterpret_cast<Rec<H, P>*>(smem);
+  t.end = reinterpret_cast<uint32_t*>(smem + align16(sizeof(Rec<H, P>) * nb));
   return t;
 }
 
@@ -648,10 +695,10 @@ __device__ __forceinline__ uint32_t bucket_of(H key, uint32_t NB) {
 // partition larger than one batch re-reads its records (from L2) for the second counting-sort pass. Ends with a
 // barrier.
 constexpr int BUILD_PER = 3;  // >= the largest 4-byte-key table in the default LDS budget / JOIN_THREADS
-template <typename H>
-__device__ __forceinline__ void build_table(const BTable<H>& t, const Rec<H>* __restrict__ build, uint32_t b0,
+template <typename H, typename P>
+__device__ __forceinline__ void build_table(const BTable<H, P>& t, const Rec<H, P>* __restrict__ build, uint32_t b0,
                                             uint32_t n, uint32_t* s_scratch) {
-  Rec<H> r[BUILD_PER];
+  Rec<H, P> r[BUILD_PER];
   auto load_batch = [&](uint32_t base) {
 #pragma unroll
     for (int q = 0; q < BUILD_PER; ++q) {
@@ -699,8 +746,8 @@ __device__ __forceinline__ void build_table(const BTable<H>& t, const Rec<H>* __
 }
 
 // Matches of key in the table, packed as (count << 16) | index of the first matching entry; 0 = no match.
-template <typename H>
-__device__ __forceinline__ uint32_t table_lookup(const BTable<H>& t, H key) {
+template <typename H, typename P>
+__device__ __forceinline__ uint32_t table_lookup(const BTable<H, P>& t, H key) {
   if (t.nb == 0) return 0u;
   const uint32_t b = bucket_of<H>(key, t.NB);
   const uint32_t lo = b ? t.end[b - 1] : 0u, hi = t.end[b];
@@ -785,12 +832,12 @@ __device__ __forceinline__ uint32_t record_pos(uint32_t e, int k, const uint32_t
 }
 
 // Writes the build rows with `key` among build records [b0, b0 + n) in order, each paired with prow.
-template <typename H>
-__device__ __forceinline__ void write_duplicates(const JoinDesc& d, const Rec<H>* __restrict__ build, uint32_t b0,
+template <typename H, typename P>
+__device__ __forceinline__ void write_duplicates(const JoinDesc& d, const Rec<H, P>* __restrict__ build, uint32_t b0,
                                                  uint32_t n, H key, uint32_t count, hy_row_id prow, uint64_t o,
                                                  hy_row_id* __restrict__ out_build, hy_row_id* __restrict__ out_probe) {
   for (uint32_t i = 0, m = 0; i < n && m < count; ++i) {
-    const Rec<H> br = build[b0 + i];
+    const Rec<H, P> br = build[b0 + i];
     if (br.key == key) {
       out_build[o] = map_row(d.build_map, br.payload);
       out_probe[o] = prow;
@@ -802,10 +849,10 @@ __device__ __forceinline__ void write_duplicates(const JoinDesc& d, const Rec<H>
 
 // A partition whose build side fits one LDS table (the common case): the table is built once and every probe
 // record's (count, first entry) stays in registers from counting to writing.
-template <typename H, bool TRACE, int JP>
+template <typename H, typename P, bool TRACE, int JP>
 __device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t p, unsigned char* smem,
-                                                    const Rec<H>* __restrict__ build,
-                                                    const Rec<H>* __restrict__ probe, hy_row_id* __restrict__ out_build,
+                                                    const Rec<H, P>* __restrict__ build,
+                                                    const Rec<H, P>* __restrict__ probe, hy_row_id* __restrict__ out_build,
                                                     hy_row_id* __restrict__ out_probe,
                                                     uint64_t* __restrict__ part_out_begin,
                                                     uint32_t* __restrict__ part_out_count, uint32_t* s_tot,
@@ -813,16 +860,17 @@ __device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t 
   const uint32_t bb = d.build_begin[p], nb = d.build_begin[p + 1] - bb;
   const uint32_t pb = d.probe_begin[p], np = d.probe_begin[p + 1] - pb;
   const int mode = d.mode;
-  const BTable<H> t = table_at<H>(smem, nb);
-  build_table<H>(t, build, bb, nb, s_tot);
+  const BTable<H, P> t = table_at<H, P>(smem, nb);
+  build_table<H, P>(t, build, bb, nb, s_tot);
   trace_stamp<TRACE>(d, p, 1);
 
   // Per probe record only its payload and match info (count << 16 | first entry) stay in registers.
   constexpr uint32_t JP_PASS_ = JP * JOIN_THREADS;
   const uint32_t n_pass = (np + JP_PASS_ - 1) / JP_PASS_;
-  uint32_t ppay[JP], pinfo[JP];
+  P ppay[JP];
+  uint32_t pinfo[JP];
   auto load_and_match = [&](uint32_t pass) {
-    Rec<H> pr[JP];
+    Rec<H, P> pr[JP];
 #pragma unroll
     for (int k = 0; k < JP; ++k) {
       const uint32_t j = pass * JP_PASS_ + k * JOIN_THREADS + threadIdx.x;
@@ -832,7 +880,7 @@ __device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t 
     for (int k = 0; k < JP; ++k) {
       const uint32_t j = pass * JP_PASS_ + k * JOIN_THREADS + threadIdx.x;
       ppay[k] = pr[k].payload;
-      pinfo[k] = j < np ? table_lookup<H>(t, pr[k].key) : 0u;
+      pinfo[k] = j < np ? table_lookup<H, P>(t, pr[k].key) : 0u;
     }
   };
 
@@ -877,7 +925,7 @@ __device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t 
         out_build[o] = map_row(d.build_map, t.ents[info_index(pinfo[k])].payload);
         out_probe[o] = prow;
       } else {
-        write_duplicates<H>(d, build, bb, nb, t.ents[info_index(pinfo[k])].key, c, prow, o, out_build, out_probe);
+        write_duplicates<H, P>(d, build, bb, nb, t.ents[info_index(pinfo[k])].key, c, prow, o, out_build, out_probe);
       }
     }
     run += pass_total;
@@ -888,9 +936,9 @@ __device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t 
 // A partition with more build rows than one LDS table holds (skewed keys): consecutive sub-tables of L build rows.
 // Counts are summed over the sub-tables; matches are written sub-table by sub-table, i.e. in build order. Each
 // probe pass rebuilds the sub-tables twice (count, write), a cost only skewed partitions pay.
-template <typename H, bool TRACE>
+template <typename H, typename P, bool TRACE>
 __device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t p, unsigned char* smem,
-                                                  const Rec<H>* __restrict__ build, const Rec<H>* __restrict__ probe,
+                                                  const Rec<H, P>* __restrict__ build, const Rec<H, P>* __restrict__ probe,
                                                   hy_row_id* __restrict__ out_build, hy_row_id* __restrict__ out_probe,
                                                   uint64_t* __restrict__ part_out_begin,
                                                   uint32_t* __restrict__ part_out_count, uint32_t* s_tot,
@@ -905,7 +953,7 @@ __device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t
   constexpr uint32_t JS_PASS = JS * JOIN_THREADS;
   const uint32_t n_pass = (np + JS_PASS - 1) / JS_PASS;
 
-  Rec<H> pr[JS];
+  Rec<H, P> pr[JS];
   uint32_t pcn[JS];
   auto load_and_count = [&](uint32_t pass) {
 #pragma unroll
@@ -916,12 +964,12 @@ __device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t
     }
     for (uint32_t sub = 0; sub < n_sub; ++sub) {
       const uint32_t b0 = bb + sub * L, n = (sub + 1 == n_sub) ? nb - sub * L : L;
-      const BTable<H> t = table_at<H>(smem, n);
-      build_table<H>(t, build, b0, n, s_tot);
+      const BTable<H, P> t = table_at<H, P>(smem, n);
+      build_table<H, P>(t, build, b0, n, s_tot);
 #pragma unroll
       for (int k = 0; k < JS; ++k) {
         const uint32_t j = pass * JS_PASS + k * JOIN_THREADS + threadIdx.x;
-        if (j < np) pcn[k] += info_count(table_lookup<H>(t, pr[k].key));
+        if (j < np) pcn[k] += info_count(table_lookup<H, P>(t, pr[k].key));
       }
       __syncthreads();  // before the next table overwrites LDS
     }
@@ -968,13 +1016,13 @@ __device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t
     if (mode != HY_JOIN_SEMI && mode != HY_JOIN_ANTI) {
       for (uint32_t sub = 0; sub < n_sub; ++sub) {
         const uint32_t b0 = bb + sub * L, n = (sub + 1 == n_sub) ? nb - sub * L : L;
-        const BTable<H> t = table_at<H>(smem, n);
-        build_table<H>(t, build, b0, n, s_tot);
+        const BTable<H, P> t = table_at<H, P>(smem, n);
+        build_table<H, P>(t, build, b0, n, s_tot);
 #pragma unroll
         for (int k = 0; k < JS; ++k) {
           const uint32_t j = pass * JS_PASS + k * JOIN_THREADS + threadIdx.x;
           if (j >= np || pcn[k] == 0) continue;
-          const uint32_t info = table_lookup<H>(t, pr[k].key);
+          const uint32_t info = table_lookup<H, P>(t, pr[k].key);
           const uint32_t cnt = info_count(info);
           if (cnt == 0) continue;
           const hy_row_id prow = map_row(d.probe_map, pr[k].payload);
@@ -983,7 +1031,7 @@ __device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t
             out_build[o] = map_row(d.build_map, t.ents[info_index(info)].payload);
             out_probe[o] = prow;
           } else {
-            write_duplicates<H>(d, build, b0, n, pr[k].key, cnt, prow, o, out_build, out_probe);
+            write_duplicates<H, P>(d, build, b0, n, pr[k].key, cnt, prow, o, out_build, out_probe);
           }
           pos[k] += cnt;
         }
@@ -994,9 +1042,9 @@ __device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t
   }
 }
 
-template <typename H, bool TRACE, int JP>
-__global__ __launch_bounds__(JOIN_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void join_partition(JoinDesc d, const Rec<H>* __restrict__ build,
-                                                               const Rec<H>* __restrict__ probe,
+template <typename H, typename P, bool TRACE, int JP>
+__global__ __launch_bounds__(JOIN_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void join_partition(JoinDesc d, const Rec<H, P>* __restrict__ build,
+                                                               const Rec<H, P>* __restrict__ probe,
                                                                hy_row_id* __restrict__ out_build,
                                                                hy_row_id* __restrict__ out_probe,
                                                                uint64_t* __restrict__ part_out_begin,
@@ -1008,10 +1056,10 @@ __global__ __launch_bounds__(JOIN_THREADS) __attribute__((amdgpu_waves_per_eu(8,
   if (p >= d.n_parts) return;
   trace_stamp<TRACE>(d, p, 0);
   if (d.build_begin[p + 1] - d.build_begin[p] <= d.lds_max_build)
-    partition_one_table<H, TRACE, JP>(d, p, smem, build, probe, out_build, out_probe, part_out_begin, part_out_count, s_tot,
+    partition_one_table<H, P, TRACE, JP>(d, p, smem, build, probe, out_build, out_probe, part_out_begin, part_out_count, s_tot,
                            &s_base);
   else
-    partition_sub_tables<H, TRACE>(d, p, smem, build, probe, out_build, out_probe, part_out_begin, part_out_count, s_tot,
+    partition_sub_tables<H, P, TRACE>(d, p, smem, build, probe, out_build, out_probe, part_out_begin, part_out_count, s_tot,
                             &s_base);
   trace_stamp<TRACE>(d, p, 4);
 }

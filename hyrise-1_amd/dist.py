@@ -1,0 +1,130 @@
+"""Distributed JoinHash across the GPUs of one node: one process per GPU, chunks sharded by
+contiguous chunk ranges, one exchange step.
+
+    step 1  every rank, each side: hy_join_exchange_partition -> 16-byte exchange records {key, global RowID}
+            grouped by first-digit bucket of the GLOBAL radix partition, plus per-bucket counts
+    counts  all_gather of the per-bucket counts (B <= 256 integers per rank and side)
+    records all_to_all_single over RCCL/xGMI: rank r receives, sender by sender, every record of the buckets it owns
+    step 2  every rank: hy_join_exchange_join -> remaining radix passes + LDS build/probe of its partitions
+
+The ranks' outputs, concatenated in rank order, are the single-node JoinHash output: one output chunk per radix
+partition in ascending order, probe rows in (chunk, offset) order, build matches in build order (join_hash.cpp).
+
+The collective plumbing (split sizes, count matrices) is plain Python over torch.distributed so it runs on RCCL for
+the GPU path and on gloo for the CPU tests; the records themselves are opaque int64 pairs.
+"""
+import ctypes
+
+import numpy as np
+
+RECORD_BYTES = 16
+
+
+def bucket_bits(capi, radix_bits, world):
+    return int(capi.lib.hy_join_exchange_bucket_bits(radix_bits, world))
+
+
+def owned_buckets(n_buckets, rank, world):
+    """Rank r owns first-digit buckets [r * B // N, (r + 1) * B // N) (include/hyrise_amd.h)."""
+    return rank * n_buckets // world, (rank + 1) * n_buckets // world
+
+
+def exchange_plan(all_counts, rank, world):
+    """all_counts[s][b] = rows of bucket b on sender s (every rank's counts, from all_gather).
+    Returns (send_rows[d], recv_rows[s], recv_matrix[s][j]) for this rank: rows sent to each destination rank, rows
+    received from each sender, and per sender the counts of this rank's local buckets j."""
+    all_counts = np.asarray(all_counts, dtype=np.int64)
+    n_buckets = all_counts.shape[1]
+    send = []
+    for d in range(world):
+        lo, hi = owned_buckets(n_buckets, d, world)
+        send.append(int(all_counts[rank, lo:hi].sum()))
+    lo, hi = owned_buckets(n_buckets, rank, world)
+    recv_matrix = all_counts[:, lo:hi].copy()
+    recv = [int(x) for x in recv_matrix.sum(axis=1)]
+    return send, recv, recv_matrix
+
+
+def exchange_records(dist, records, bucket_counts, rank, world, device=None):
+    """Routes this rank's exchange records (int64 tensor, 2 words per record, grouped by bucket) to their owners.
+    Returns (received records, recv_matrix[s][j])."""
+    import torch
+
+    counts = torch.as_tensor(np.asarray(bucket_counts, dtype=np.int64), device=device)
+    gathered = [torch.empty_like(counts) for _ in range(world)]
+    dist.all_gather(gathered, counts)
+    all_counts = np.stack([g.cpu().numpy() for g in gathered])
+    send, recv, recv_matrix = exchange_plan(all_counts, rank, world)
+    words = RECORD_BYTES // 8
+    out = torch.empty(sum(recv) * words, dtype=torch.int64, device=records.device)
+    dist.all_to_all_single(out, records[: sum(send) * words], [r * words for r in recv], [s * words for s in send])
+    return out, recv_matrix
+
+
+class ExchangeJoin:
+    """The two C-ABI steps of the distributed JoinHash on device buffers owned by torch tensors."""
+
+    def __init__(self, capi, radix_bits, world, hashed_type, mode=0, seed=17):
+        self.capi = capi
+        self.lib = capi.lib
+        self.world = world
+        self.params = capi.JoinParams(mode, hashed_type, radix_bits, seed)
+        self.bits = radix_bits
+        self.first_bits = bucket_bits(capi, radix_bits, world)
+        self.n_buckets = 1 << self.first_bits
+        self._ws = {}
+
+    def _workspace(self, key, nbytes, device):
+        import torch
+
+        t = self._ws.get(key)
+        if t is None or t.numel() < nbytes:
+            t = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=device)
+            self._ws[key] = t
+        return t
+
+    def partition(self, side, n_rows, keep_nulls, stream, device, key="side"):
+        """Step 1 for one side: returns (records int64 tensor [2 * n_rows], bucket counts np.uint64[B])."""
+        import torch
+
+        lib, capi = self.lib, self.capi
+        wsb = ctypes.c_size_t(0)
+        capi.check(lib.hy_join_exchange_partition_workspace_size(ctypes.byref(side), ctypes.byref(self.params),
+                                                                  self.world, ctypes.byref(wsb)), "exchange ws")
+        ws = self._workspace(key, wsb.value, device)
+        recs = self._workspace(key + ".recs", max(1, n_rows) * RECORD_BYTES, device)
+        counts = (ctypes.c_uint64 * self.n_buckets)()
+        capi.check(lib.hy_join_exchange_partition(ctypes.byref(side), ctypes.byref(self.params), int(keep_nulls),
+                                                  self.world, recs.data_ptr(), counts, ws.data_ptr(), ws.numel(),
+                                                  stream), "hy_join_exchange_partition")
+        return recs[: n_rows * RECORD_BYTES].view(torch.int64), np.frombuffer(counts, dtype=np.uint64).copy()
+
+    def join(self, build_recs, build_matrix, probe_recs, probe_matrix, rank, stream, device, capacity=None):
+        """Step 2: returns (out_build, out_probe, part_begin, part_count, total_pairs) - RowID tensors (int32 pairs)
+        and per local partition the output range."""
+        import torch
+
+        lib, capi = self.lib, self.capi
+        first, last = owned_buckets(self.n_buckets, rank, self.world)
+        nb = last - first
+        bc = np.ascontiguousarray(build_matrix, dtype=np.uint64)
+        pc = np.ascontiguousarray(probe_matrix, dtype=np.uint64)
+        bcp = bc.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+        pcp = pc.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+        wsb = ctypes.c_size_t(0)
+        capi.check(lib.hy_join_exchange_join_workspace_size(bcp, pcp, self.world, nb, ctypes.byref(self.params),
+                                                             ctypes.byref(wsb)), "exchange join ws")
+        ws = self._workspace("join", wsb.value, device)
+        n_parts = nb << (self.bits - self.first_bits)
+        if capacity is None:
+            capacity = int(pc.sum()) + int(bc.sum()) + 16
+        out_b = self._workspace("out_b", capacity * 8, device)
+        out_p = self._workspace("out_p", capacity * 8, device)
+        part_begin = torch.empty(max(1, n_parts), dtype=torch.int64, device=device)
+        part_count = torch.empty(max(1, n_parts), dtype=torch.int32, device=device)
+        res = capi.JoinResult()
+        capi.check(lib.hy_join_exchange_join(build_recs.data_ptr(), bcp, probe_recs.data_ptr(), pcp, self.world,
+                                             first, nb, ctypes.byref(self.params), out_b.data_ptr(), out_p.data_ptr(),
+                                             capacity, part_begin.data_ptr(), part_count.data_ptr(), ctypes.byref(res),
+                                             ws.data_ptr(), ws.numel(), stream), "hy_join_exchange_join")
+        return out_b, out_p, part_begin[:n_parts], part_count[:n_parts], res.total_pairs

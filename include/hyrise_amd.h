@@ -237,6 +237,9 @@ typedef struct hy_join_side {
    * when every output column of this side shares the join column's PosLists); 0 = emit RowIDs of the side's own
    * table, to be dereferenced per PosList group with hy_dereference_row_ids. */
   int32_t fuse_dereference;
+  /* reference sides: RowIDs in the PosLists name referenced chunk referenced_chunk_base + i for referenced[i] (a
+   * rank of the distributed join holds a range of a table's chunks under their global ids); 0 otherwise */
+  uint32_t referenced_chunk_base;
 } hy_join_side;
 
 typedef struct hy_join_params {
@@ -261,6 +264,41 @@ hy_status hy_join_hash(const hy_join_side* build, const hy_join_side* probe, con
                        hy_row_id* out_build, hy_row_id* out_probe, uint64_t out_capacity, uint64_t* partition_begin,
                        uint32_t* partition_counts, hy_join_result* result, void* workspace, size_t workspace_bytes,
                        hy_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------------------------
+ * Distributed JoinHash (one process per GPU; an RCCL all-to-all of records between the two steps)
+ *
+ * The radix partition id of a row (murmur2(key, seed) & (2^radix_bits - 1), radix_bits from the GLOBAL build size) is
+ * split into digits from the most significant; the first digit has B = 2^w0 >= n_ranks buckets and rank r owns buckets
+ * [r * B / n_ranks, (r + 1) * B / n_ranks) - hence a contiguous range of partitions, and the ranks' outputs
+ * concatenated in rank order are the reference's output (join_hash.cpp:829-855: one chunk per partition, ascending).
+ *
+ * Step 1, every rank, each side: hy_join_exchange_partition writes the rank's rows of the side as 16-byte exchange
+ * records {key (hashed type, 8-byte aligned), RowID} grouped by first-digit bucket (stable: row order inside a bucket)
+ * and bucket_counts[b] (host, B entries). The RowID is the row's own (chunk_id of its hy_join_chunk, offset) or, for
+ * a fused reference side, the referenced RowID from its PosList. The records for rank r are one contiguous range.
+ * Step 2, every rank, after all-to-all (received buffer = the senders' ranges in sender order; counts[s * n_buckets +
+ * j] = rows of local bucket j from sender s): hy_join_exchange_join partitions the received records further (stable,
+ * bucket-major then sender then row order) and runs the LDS build/probe of the rank's n_buckets << (radix_bits - w0)
+ * partitions. partition_begin / partition_counts as for hy_join_hash, indexed by local partition.
+ * ------------------------------------------------------------------------------------------------------------- */
+#define HY_EXCHANGE_RECORD_BYTES 16
+hy_status hy_join_exchange_partition_workspace_size(const hy_join_side* side, const hy_join_params* params,
+                                                    uint32_t n_ranks, size_t* bytes);
+hy_status hy_join_exchange_partition(const hy_join_side* side, const hy_join_params* params, int32_t keep_nulls,
+                                     uint32_t n_ranks, void* out_records, uint64_t* bucket_counts, void* workspace,
+                                     size_t workspace_bytes, hy_stream_t stream);
+hy_status hy_join_exchange_join_workspace_size(const uint64_t* build_counts, const uint64_t* probe_counts,
+                                               uint32_t n_senders, uint32_t n_buckets, const hy_join_params* params,
+                                               size_t* bytes);
+hy_status hy_join_exchange_join(const void* build_records, const uint64_t* build_counts, const void* probe_records,
+                                const uint64_t* probe_counts, uint32_t n_senders, uint32_t first_bucket,
+                                uint32_t n_buckets, const hy_join_params* params, hy_row_id* out_build,
+                                hy_row_id* out_probe, uint64_t out_capacity, uint64_t* partition_begin,
+                                uint32_t* partition_counts, hy_join_result* result, void* workspace,
+                                size_t workspace_bytes, hy_stream_t stream);
+/* First-digit width of the distributed join's radix plan (buckets = 2^width). */
+uint32_t hy_join_exchange_bucket_bits(uint32_t radix_bits, uint32_t n_ranks);
 
 /*
  * out[i] = rows[i] is NULL ? rows[i] : chunk_pos_lists[rows[i].chunk_id][rows[i].chunk_offset]
