@@ -7,9 +7,11 @@ One step = the reference's query shape, on data already resident in HBM:
 Rows per step = |lineitem| + |orders| (base-table rows consumed). Everything runs through the C-ABI
 (include/hyrise_amd.h) on buffers owned by torch (device memory only; the C-ABI never sees a torch type).
 
-Multi-GPU (torchrun, one process per GPU): weak scaling. Rank r generates the r-th shard of an SF·N database
-(orders r*n..(r+1)*n and their lineitems), so lineitem and orders are co-partitioned by o_orderkey range and the join
-needs no exchange; the shards' outputs are the reference's per-partition output chunks, concatenated in rank order.
+Multi-GPU (torchrun, one process per GPU): weak scaling. Rank r holds the r-th shard of an SF·N database (its chunk
+range of orders and lineitem under global chunk ids) and scans it locally. The join is the distributed JoinHash of
+SURVEY.md 8(e): the radix bits come from the GLOBAL build size, both sides are partitioned by the first radix digit,
+records {key, global RowID} are exchanged with one RCCL all-to-all per side over xGMI, and every rank joins the
+partitions it owns (hyrise-1_amd/dist.py); the ranks' outputs concatenated in rank order are the single-node output.
 """
 import argparse
 import ctypes
@@ -35,6 +37,8 @@ def parse():
     p.add_argument("--chunk", type=int, default=100_000)
     p.add_argument("--cpu-sf", type=float, default=20.0, help="scale factor of the bounded CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--dist-backend", default="nccl",
+                   help="nccl (RCCL; one GPU per rank) or gloo (host-staged exchange: rehearsal of N ranks on one GPU)")
     p.add_argument("--join-trace", default=None,
                    help="debug: after the timed region run one traced step and write per-partition join phase "
                         "durations (us) to this .npz (hy_debug_set_join_trace)")
@@ -57,8 +61,12 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            torch.cuda.set_device(local % torch.cuda.device_count())
+            dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -79,6 +87,11 @@ def main():
     present_h = present.cpu().numpy()
     n_lchunks = (n_li + chunk - 1) // chunk
     n_ochunks = (n_ord + chunk - 1) // chunk
+    l_stride, o_stride = n_lchunks, n_ochunks  # global chunk id stride per rank (shards differ by a chunk or so)
+    if dist:
+        t = torch.tensor([n_lchunks, n_ochunks], dtype=torch.int64, device=dev if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        l_stride, o_stride = int(t[0]), int(t[1])
     # pad buffers so 16-byte vector loads of the last chunk stay in bounds
     def padded(t, mult=64):
         extra = (-t.numel()) % mult
@@ -107,7 +120,9 @@ def main():
         sc.op = capi.HY_OP_ALL if svid >= dsize else (capi.HY_OP_NONE if svid == 0 else capi.HY_OP_LT)
         sc.out_begin = c * chunk
     sizes = (ctypes.c_uint32 * n_lchunks)(*[min(chunk, n_li - c * chunk) for c in range(n_lchunks)])
-    chunk_ids = (ctypes.c_uint32 * n_lchunks)(*range(n_lchunks))
+    # global chunk ids: rank r holds lineitem chunks [r * n_lchunks, (r + 1) * n_lchunks) (every shard has the same SF)
+    l_base, o_base = rank * l_stride, rank * o_stride
+    chunk_ids = (ctypes.c_uint32 * n_lchunks)(*range(l_base, l_base + n_lchunks))
     ws_bytes = ctypes.c_size_t(0)
     capi.check(L.hy_table_scan_workspace_size(sizes, n_lchunks, ctypes.byref(ws_bytes)), "scan ws")
     scan_ws = torch.empty(ws_bytes.value, dtype=torch.uint8, device=dev)
@@ -132,7 +147,7 @@ def main():
         b.column.size = size
         b.column.kind = capi.HY_COL_VALUE
         b.size = size
-        b.chunk_id = c
+        b.chunk_id = o_base + c
         b.single_chunk = capi.HY_MIXED_CHUNKS
     referenced = (capi.ColumnChunk * n_lchunks)()
     for c in range(n_lchunks):
@@ -140,8 +155,9 @@ def main():
         r.data = lkey.data_ptr() + 4 * c * chunk
         r.size = min(chunk, n_li - c * chunk)
         r.kind = capi.HY_COL_VALUE
-    build_side = capi.JoinSide(build_chunks, n_ochunks, capi.HY_TYPE_INT32, None, 0, 0)
-    radix_bits = L.hy_join_radix_bits(n_ord, 4)
+    build_side = capi.JoinSide(build_chunks, n_ochunks, capi.HY_TYPE_INT32, None, 0, 0, 0)
+    # the reference's radix bits for the GLOBAL build side (join_hash.cpp:640-668)
+    radix_bits = L.hy_join_radix_bits(n_ord * world, 4)
     params = capi.JoinParams(capi.HY_JOIN_INNER, capi.HY_TYPE_INT32, radix_bits, 17)
     n_parts = 1 << radix_bits
     part_begin = torch.empty(n_parts, dtype=torch.int64, device=dev)
@@ -161,7 +177,7 @@ def main():
         pchunks["chunk_id"] = np.arange(len(nz), dtype=np.uint32)
         pchunks["single_chunk"] = nz  # scan output chunk k references lineitem chunk nz[k] only
         side = capi.JoinSide(pchunks.ctypes.data_as(ctypes.POINTER(capi.JoinChunk)), len(nz), capi.HY_TYPE_INT32,
-                             referenced, n_lchunks, 1)
+                             referenced, n_lchunks, 1, l_base)
         return side, pchunks, int(counts_h[nz].sum())
 
     def run_join(counts_h):
@@ -181,10 +197,29 @@ def main():
                                   state["ws"].data_ptr(), state["ws"].numel(), stream), "hy_join_hash")
         return n_probe, res.total_pairs
 
+    xj = None
+    if world > 1:
+        hdist = importlib.import_module("hyrise-1_amd.dist")
+        xj = hdist.ExchangeJoin(capi, radix_bits, world, capi.HY_TYPE_INT32, capi.HY_JOIN_INNER, 17)
+
+    def run_join_distributed(counts_h):
+        # partition both sides by the first radix digit, RCCL all-to-all over xGMI, then the
+        # remaining passes + LDS build/probe of this rank's partitions
+        side, keep, n_probe = probe_side_from_counts(counts_h)
+        brec, bcnt = xj.partition(build_side, n_ord, False, stream, dev, key="build")
+        precs, pcnt = xj.partition(side, n_probe, False, stream, dev, key="probe")
+        xdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
+        brecv, bmat = hdist.exchange_records(dist, brec.to(xdev), bcnt, rank, world, device=xdev)
+        precv, pmat = hdist.exchange_records(dist, precs.to(xdev), pcnt, rank, world, device=xdev)
+        brecv, precv = brecv.to(dev), precv.to(dev)
+        out = xj.join(brecv, bmat, precv, pmat, rank, stream, dev)
+        state["recv_rows"] = (int(bmat.sum()), int(pmat.sum()))
+        return n_probe, out[4]
+
     def step():
         run_scan()
         counts_h = scan_counts.cpu().numpy()  # D2H of per-chunk match counts (the output chunk layout)
-        return run_join(counts_h)
+        return run_join_distributed(counts_h) if xj else run_join(counts_h)
 
     for _ in range(args.warmup):
         n_probe, pairs = step()
@@ -202,7 +237,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     L.hy_kernel_stats_enable(0)
-    if args.join_trace and rank == 0:
+    if args.join_trace and rank == 0 and world == 1:
         import numpy as np
         trace = torch.zeros(5 * (1 << radix_bits), dtype=torch.int64, device=dev)
         L.hy_debug_set_join_trace.argtypes = [ctypes.c_void_p]
@@ -214,9 +249,16 @@ def main():
         np.savez(args.join_trace, stamps_us=t, out_pairs=part_count.cpu().numpy())
     if dist:
         dist.barrier()
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        # whole-job totals: rows processed, scan matches and join pairs summed over ranks
+        tot = torch.tensor([n_li, n_ord, n_probe, pairs], dtype=torch.int64,
+                           device=dev if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        g_li, g_ord, g_probe, g_pairs = (int(x) for x in tot.tolist())
+    else:
+        g_li, g_ord, g_probe, g_pairs = n_li, n_ord, n_probe, int(pairs)
 
     # ---------------- per-kernel device time (HIP events on the launch stream) ----------------
     nk = ctypes.c_uint32(0)
@@ -233,6 +275,7 @@ def main():
     rows_per_step = n_li + n_ord
     # algorithmic bytes per step for each kernel; 8-byte {key, payload} partition records
     valid_build, valid_probe = n_ord, n_probe
+    recv_build, recv_probe = state.get("recv_rows", (n_ord, n_probe))  # rows this rank joins after the exchange
     alg = {
         "scan_dict": n_li * 1 + n_probe * 8,
         "part1_hist.build": valid_build * 4,
@@ -243,7 +286,7 @@ def main():
         "part2_hist.probe": valid_probe * 8,
         "part2_scatter.build": valid_build * 16,
         "part2_scatter.probe": valid_probe * 16,
-        "join_partition": (valid_build + valid_probe) * 8 + pairs * 16,
+        "join_partition": (recv_build + recv_probe) * 8 + pairs * 16,
     }
     for k, v in kernels.items():
         per_launch_ms = v["ms_total"] / max(v["launches"], 1)
@@ -263,7 +306,7 @@ def main():
     step_s = elapsed / K
     # end-to-end algorithmic bytes (§8(d)): scan 1 B/row + 8 B/match; join 4 B/build + 4 B/probe + 16 B/pair
     e2e_bytes = n_li * 1 + n_probe * 8 + n_ord * 4 + n_probe * 4 + pairs * 16
-    value = rows_per_step * world / step_s
+    value = (g_li + g_ord) / step_s
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -285,8 +328,10 @@ def main():
             "data": "synthetic (seeded counter-based TPC-H-shaped columns, resident in HBM)",
             "config": {"workload": f"TableScan(l_quantity<24, dictionary u8) -> JoinHash(orders ⋈ scan, "
                                    f"o_orderkey=l_orderkey, radix_bits={radix_bits})",
-                       "sf_per_gpu": args.sf, "lineitem_rows": n_li, "orders_rows": n_ord, "chunk_size": chunk,
-                       "scan_matches": n_probe, "join_pairs": int(pairs), "parallelism": f"chunk-sharded x{world}"},
+                       "sf_per_gpu": args.sf, "lineitem_rows": g_li, "orders_rows": g_ord, "chunk_size": chunk,
+                       "scan_matches": g_probe, "join_pairs": g_pairs,
+                       "parallelism": f"chunk-sharded x{world}" + (f", RCCL all-to-all radix exchange"
+                                                                    if world > 1 else "")},
             "roofline": roofline,
             "end_to_end": {"alg_bytes_per_step": e2e_bytes, "GBps": round(e2e_bytes / step_s / 1e9, 1),
                            "frac_of_peak": round(e2e_bytes / step_s / 1e9 / HBM_PEAK_GBPS, 4)},
