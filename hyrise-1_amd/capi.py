@@ -9,7 +9,8 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libhyrise_amd.so")
+# HY_AMD_LIB: an alternative build of the same library (kernel-variant experiments); default the in-tree build
+LIB_PATH = os.environ.get("HY_AMD_LIB") or os.path.join(_HERE, "_lib", "libhyrise_amd.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "hyrise_amd.h")
 
 lib = ctypes.CDLL(LIB_PATH)

@@ -515,6 +515,25 @@ uint32_t hy_join_radix_bits(uint64_t build_rows, uint32_t key_bytes) {
 // ================================================================================================================
 namespace {
 
+// Tiles per span of the pass from column chunks (sub1) and of the record passes (sub2); HY_PART_SUB1 / HY_PART_SUB2
+// override them (tuning). Read once: workspace sizes and launches must agree.
+uint32_t sub_from_env(const char* name, uint32_t dflt) {
+  const char* e = std::getenv(name);
+  const long v = e ? std::strtol(e, nullptr, 10) : 0;
+  return v >= 1 && v <= hyk::PART_SUB_MAX ? static_cast<uint32_t>(v) : dflt;
+}
+uint32_t sub1() {
+  static const uint32_t v = sub_from_env("HY_PART_SUB1", 2);
+  return v;
+}
+uint32_t sub2() {
+  static const uint32_t v = sub_from_env("HY_PART_SUB2", 1);
+  return v;
+}
+uint64_t span1() { return uint64_t(sub1()) * hyk::PART_TILE; }
+uint64_t span2() { return uint64_t(sub2()) * hyk::PART_TILE; }
+
+
 struct SidePlan {
   uint64_t n_rows = 0;
   uint64_t n_tiles1 = 0;
@@ -572,7 +591,7 @@ hy_status plan_side(const hy_join_side* side, SidePlan& p) {
     p.row_begin[i] = rows;
     p.tile_begin[i] = tiles;
     rows += c.size;
-    tiles += (uint64_t(c.size) + hyk::PART_TILE - 1) / hyk::PART_TILE;
+    tiles += (uint64_t(c.size) + span1() - 1) / span1();
   }
   p.row_begin[side->n_chunks] = rows;
   p.tile_begin[side->n_chunks] = tiles;
@@ -653,7 +672,7 @@ void pass_sizes(const SideSizes& z, const std::vector<uint32_t>& w, uint64_t fir
       *hist_words = std::max(*hist_words, digits * z.tiles1);
       *max_tiles = std::max(*max_tiles, z.tiles1);
     } else {
-      const uint64_t t = (z.rows + hyk::PART_TILE - 1) / hyk::PART_TILE + segs;
+      const uint64_t t = (z.rows + span2() - 1) / span2() + segs;
       *hist_words = std::max(*hist_words, digits * t);
       *max_tiles = std::max(*max_tiles, t);
       segs *= digits;
@@ -723,6 +742,21 @@ hy_status run_scan(const uint32_t* in, uint32_t* out, uint64_t n, const Common& 
 
 uint32_t full_mask(uint32_t bits) { return bits >= 32 ? 0xFFFFFFFFu : ((1u << bits) - 1u); }
 
+// The load path every chunk of the side allows (hyk::LP_*): lean kernels for the all-value and all-single-chunk
+// reference sides, the general one otherwise.
+int load_path(const SidePlan& p) {
+  bool value = true, ref1 = true;
+  for (const auto& c : p.chunks) {
+    if (c.size == 0) continue;
+    value = value && c.pos_list == nullptr && c.kind == HY_COL_VALUE && c.nulls == nullptr;
+    ref1 = ref1 && c.pos_list != nullptr && c.single_chunk != HY_MIXED_CHUNKS &&
+           p.referenced[c.single_chunk].kind == HY_COL_VALUE && p.referenced[c.single_chunk].nulls == nullptr &&
+           p.referenced[c.single_chunk].size > 0;
+  }
+  if (value) return hyk::LP_VALUE;
+  return ref1 ? hyk::LP_REF1 : hyk::LP_ANY;
+}
+
 // Pass 0: from column chunks into b.recA (or `out`), bucket bounds into b.segA (2^w0 buckets).
 template <typename T, typename H, typename P>
 hy_status pass0_side(const char* side_tag, const SidePlan& p, const SideBufs<H, P>& b, uint32_t bits, uint32_t w0,
@@ -740,6 +774,7 @@ hy_status pass0_side(const char* side_tag, const SidePlan& p, const SideBufs<H, 
   sd.fuse_deref = p.fuse;
   sd.keep_nulls = keep_nulls ? 1 : 0;
   sd.ref_base = ref_base;
+  sd.sub = sub1();
   const uint32_t n_digits = 1u << w0;
   hyk::Digit d0{full_mask(bits), bits - w0, n_digits - 1u, seed};
   HY_HIP(hipMemsetAsync(b.total, 0, 8, s));
@@ -747,10 +782,14 @@ hy_status pass0_side(const char* side_tag, const SidePlan& p, const SideBufs<H, 
     hipLaunchKernelGGL(hyk::fill_tile_owner, dim3((sd.n_chunks + 255) / 256), dim3(256), 0, s, b.tile_begin,
                        sd.n_chunks, b.tile_owner);
     HY_HIP(hipGetLastError());
+    const int lp = load_path(p);
     {
       KTimer kt_((std::string("part1_hist.") + side_tag).c_str(), s, p.n_rows);
-      hipLaunchKernelGGL((hyk::part1_hist<T, H>), dim3(static_cast<uint32_t>(p.n_tiles1)), dim3(hyk::PART_THREADS), 0,
-                         s, sd, d0, n_digits, b.hist);
+      auto kern = lp == hyk::LP_VALUE  ? hyk::part1_hist<T, H, hyk::LP_VALUE>
+                  : lp == hyk::LP_REF1 ? hyk::part1_hist<T, H, hyk::LP_REF1>
+                                       : hyk::part1_hist<T, H, hyk::LP_ANY>;
+      hipLaunchKernelGGL(kern, dim3(static_cast<uint32_t>(p.n_tiles1)), dim3(hyk::PART_THREADS), 0, s, sd, d0,
+                         n_digits, b.hist);
       kt_.done();
     }
     HY_HIP(hipGetLastError());
@@ -758,8 +797,11 @@ hy_status pass0_side(const char* side_tag, const SidePlan& p, const SideBufs<H, 
     if (st != HY_OK) return st;
     {
       KTimer kt_((std::string("part1_scatter.") + side_tag).c_str(), s, p.n_rows);
-      hipLaunchKernelGGL((hyk::part1_scatter<T, H, P>), dim3(static_cast<uint32_t>(p.n_tiles1)),
-                         dim3(hyk::PART_THREADS), 0, s, sd, d0, static_cast<int>(w0), n_digits, b.off, out);
+      auto kern = lp == hyk::LP_VALUE  ? hyk::part1_scatter<T, H, P, hyk::LP_VALUE>
+                  : lp == hyk::LP_REF1 ? hyk::part1_scatter<T, H, P, hyk::LP_REF1>
+                                       : hyk::part1_scatter<T, H, P, hyk::LP_ANY>;
+      hipLaunchKernelGGL(kern, dim3(static_cast<uint32_t>(p.n_tiles1)), dim3(hyk::PART_THREADS), 0, s, sd, d0,
+                         static_cast<int>(w0), n_digits, b.off, out);
       kt_.done();
     }
     HY_HIP(hipGetLastError());
@@ -816,7 +858,7 @@ hy_status local_passes(const char* side_tag, SideBufs<H, P>& b, const std::vecto
   for (size_t i = first; i < w.size(); ++i) {
     below -= w[i];
     hipLaunchKernelGGL(hyk::seg_tile_counts, dim3(grid_for(n_segs, 256)), dim3(256), 0, s, seg, nullptr,
-                       static_cast<uint32_t>(n_segs), b.tile_counts);
+                       static_cast<uint32_t>(n_segs), span2(), b.tile_counts);
     HY_HIP(hipGetLastError());
     hy_status st = run_scan(b.tile_counts, b.tile_excl, n_segs, c, s, c.totals + 4);
     if (st != HY_OK) return st;
@@ -826,8 +868,9 @@ hy_status local_passes(const char* side_tag, SideBufs<H, P>& b, const std::vecto
     hipLaunchKernelGGL(hyk::fill_tile_owner, dim3(grid_for(n_segs, 256)), dim3(256), 0, s, b.seg_tile_begin,
                        static_cast<uint32_t>(n_segs), b.tile_owner);
     HY_HIP(hipGetLastError());
-    const uint64_t grid = rows ? (rows + hyk::PART_TILE - 1) / hyk::PART_TILE + n_segs : 0;
-    hyk::Segs sg{seg, b.seg_tile_begin, b.tile_owner, static_cast<uint32_t>(n_segs), nullptr, nullptr, nullptr, nullptr};
+    const uint64_t grid = rows ? (rows + span2() - 1) / span2() + n_segs : 0;
+    hyk::Segs sg{seg,     b.seg_tile_begin, b.tile_owner, static_cast<uint32_t>(n_segs), nullptr, nullptr, nullptr,
+                 nullptr, sub2()};
     st = record_pass<H, P>(side_tag, b, sg, hyk::Groups{nullptr, nullptr, nullptr}, static_cast<uint32_t>(n_segs), grid,
                            bits, below, w[i], seed, in, spare, total, seg_spare, c, s, rows);
     if (st != HY_OK) return st;
@@ -1064,7 +1107,7 @@ RecvPlan recv_plan(const uint64_t* counts, uint32_t n_senders, uint32_t nb, uint
       run_in_sender[s] += cnt;
       r.seg_begin[q] = static_cast<uint32_t>(b0);
       r.seg_end[q] = static_cast<uint32_t>(b0 + cnt);
-      const uint32_t t = static_cast<uint32_t>((cnt + hyk::PART_TILE - 1) / hyk::PART_TILE);
+      const uint32_t t = static_cast<uint32_t>((cnt + span2() - 1) / span2());
       r.seg_tile_begin[q] = tiles;
       r.seg_toff[q] = gt;
       tiles += t;
@@ -1135,7 +1178,8 @@ hy_status recv_side(const char* tag, const RecvPlan& r, RecvBufs<H>& rb, const s
   }
   const uint32_t w1 = w.size() > 1 ? w[1] : 0;  // one digit only: a stable merge of the senders' runs
   const uint32_t shift = bits - w[0] - w1;
-  hyk::Segs sg{rb.seg_begin, rb.seg_tile_begin, rb.owner, nseg, rb.seg_end, rb.seg_hbase, rb.seg_stride, rb.seg_toff};
+  hyk::Segs sg{rb.seg_begin, rb.seg_tile_begin, rb.owner,    nseg,   rb.seg_end,
+               rb.seg_hbase, rb.seg_stride,     rb.seg_toff, sub2()};
   hyk::Groups gr{rb.group_hbase, rb.group_tiles, rb.group_out};
   // the merge pass must not write through a stale histogram entry: hist words are exactly the groups' tiles x digits
   hy_status st = record_pass<H, hy_row_id>(tag, rb.b, sg, gr, nb, r.tiles, bits, shift, w1, seed, in, rb.b.recA,
@@ -1154,7 +1198,7 @@ size_t exchange_join_bytes(const RecvPlan& rbp, const RecvPlan& rpp, uint32_t bi
   carve_recv<H>(cv, rpp, bits, w, nb, n_senders, b);
   Common c;
   const uint64_t max_scan = std::max({rbp.hist_words * 2, rpp.hist_words * 2, (uint64_t(1) << bits) + 1,
-                                      (rbp.rows + rpp.rows) / hyk::PART_TILE * 256 + uint64_t(nb) * n_senders * 256});
+                                      (rbp.rows + rpp.rows) / span2() * 256 + uint64_t(nb) * n_senders * 256});
   carve_common(cv, max_scan, bits, &c);
   return cv.used + 256;
 }
@@ -1348,7 +1392,7 @@ hy_status hy_join_exchange_join(const void* build_records, const uint64_t* build
     Common c{};
     const uint64_t max_scan =
         std::max({rbp.hist_words * 2, rpp.hist_words * 2, (uint64_t(1) << bits) + 1,
-                  (rbp.rows + rpp.rows) / hyk::PART_TILE * 256 + uint64_t(n_buckets) * n_senders * 256});
+                  (rbp.rows + rpp.rows) / span2() * 256 + uint64_t(n_buckets) * n_senders * 256});
     carve_common(cv, max_scan, bits, &c);
     if (!cv.ok) return fail(HY_ERR_WORKSPACE, "exchange join workspace too small");
     using R = hyk::Rec<H, hy_row_id>;

@@ -30,6 +30,11 @@ constexpr int PART_WAVES = PART_THREADS / WAVE;
 constexpr int PART_ITEMS = 16;                              // items per lane per tile
 constexpr int PART_TILE = PART_THREADS * PART_ITEMS;        // 4096 rows per tile
 constexpr int WAVE_SPAN = WAVE * PART_ITEMS;                // 1024 consecutive rows per wave
+// A partition workgroup handles one SPAN of `sub` consecutive tiles (a per-pass launch parameter), one after the
+// other, carrying each digit's output position from tile to tile in a register. Histograms and their scans are per
+// span, so the per-digit offset tables are `sub` times smaller than per-tile ones (their strided 4-byte entries cost
+// a cache line each); a larger span has fewer tiles in flight per CU, so the host picks it per pass.
+constexpr int PART_SUB_MAX = 16;
 constexpr uint32_t NULL_PAYLOAD = 0xFFFFFFFFu;
 
 // Partition record: join key (hashed type) + payload. Single-GPU payload = 32-bit row index in the side's row space
@@ -112,6 +117,7 @@ struct Side {
   int32_t fuse_deref;                // payload = row in the referenced table instead of row in this table
   int32_t keep_nulls;
   uint32_t ref_base;                 // RowIDs in PosLists name referenced chunk ref_base + i for Side::referenced[i]
+  uint32_t sub;                      // tiles per span
 };
 
 // NULL rows: a ValueColumn read directly yields its stored value (value_column_iterable), a dictionary column and
@@ -173,46 +179,54 @@ __device__ __forceinline__ bool load_row(const Side& s, const SrcChunk& c, uint3
 // materialize_input does at join_hash.cpp:253). A reference chunk whose PosList references a single chunk (known
 // from its producer, hy_join_chunk.single_chunk) reads that chunk's descriptor once with scalar loads instead of once
 // per lane and row.
-template <typename T, typename H, typename P>
+// Load paths a side can be specialised for (the host picks one per side; LP_ANY decides per chunk).
+constexpr int LP_ANY = 0;    // any mix of value / dictionary / reference chunks, NULLs
+constexpr int LP_VALUE = 1;  // every chunk a ValueColumn without NULLs
+constexpr int LP_REF1 = 2;   // every chunk a PosList into one ValueColumn chunk without NULLs (single_chunk set)
+
+template <typename T, typename H, typename P, int LP = LP_ANY>
 __device__ __forceinline__ uint32_t load_items(const Side& s, const SrcChunk& ch, uint32_t base, H (&keys)[PART_ITEMS],
                                                P (&pays)[PART_ITEMS]) {
   uint32_t act = 0;
+  // Row offsets are recomputed per tile: hoisting the 16 lane offsets out of a span's tile loop costs registers.
+  uint32_t lane0 = __lane_id();
+  asm volatile("" : "+v"(lane0));
+  base += lane0;
   // Fast paths issue all PART_ITEMS loads of a phase before using any of them (the general per-item path below
-  // serialises each item's dependent loads).
-  if (ch.pos_list == nullptr && ch.kind == HY_COL_VALUE && ch.nulls == nullptr) {
+  // serialises each item's dependent loads). Their loads are unconditional, from clamped addresses: a load under
+  // `if (in range)` becomes its own exec-masked block with a full wait after it, i.e. PART_ITEMS serial round trips.
+  // Items outside the chunk are masked out of `act`; their keys and payloads are never used.
+  if (LP == LP_VALUE || (LP == LP_ANY && ch.pos_list == nullptr && ch.kind == HY_COL_VALUE && ch.nulls == nullptr)) {
     const T* data = static_cast<const T*>(ch.data);
+    const uint32_t last = ch.size - 1;  // a tile exists only for a non-empty chunk
     T v[PART_ITEMS];
 #pragma unroll
-    for (int k = 0; k < PART_ITEMS; ++k) {
-      const uint32_t off = base + k * WAVE + __lane_id();
-      v[k] = off < ch.size ? data[off] : T{};
-    }
+    for (int k = 0; k < PART_ITEMS; ++k) v[k] = data[min(base + k * WAVE, last)];
 #pragma unroll
     for (int k = 0; k < PART_ITEMS; ++k) {
-      const uint32_t off = base + k * WAVE + __lane_id();
+      const uint32_t off = base + k * WAVE;
       keys[k] = static_cast<H>(v[k]);
       pays[k] = own_payload<P>(ch.row_begin, ch.chunk_id, off);
       if (off < ch.size) act |= 1u << k;
     }
     return act;
   }
-  if (ch.pos_list != nullptr && ch.single_chunk != HY_MIXED_CHUNKS) {
+  if (LP == LP_REF1 || (LP == LP_ANY && ch.pos_list != nullptr && ch.single_chunk != HY_MIXED_CHUNKS)) {
     const SrcChunk rc = s.referenced[ch.single_chunk];
     const uint64_t rrow = s.fuse_deref ? s.referenced_row_begin[ch.single_chunk] : 0;
+    const uint32_t last = ch.size - 1;
     hy_row_id rid[PART_ITEMS];
 #pragma unroll
-    for (int k = 0; k < PART_ITEMS; ++k) {
-      const uint32_t off = base + k * WAVE + __lane_id();
-      rid[k] = off < ch.size ? ch.pos_list[off] : hy_row_id{0xFFFFFFFFu, 0xFFFFFFFFu};
-    }
-    if (rc.kind == HY_COL_VALUE && rc.nulls == nullptr) {
+    for (int k = 0; k < PART_ITEMS; ++k) rid[k] = ch.pos_list[min(base + k * WAVE, last)];
+    // LP_REF1 is chosen only for non-empty referenced chunks, so offset 0 is a valid stand-in for NULL rows.
+    if (LP == LP_REF1 || (rc.kind == HY_COL_VALUE && rc.nulls == nullptr && rc.size > 0)) {
       const T* data = static_cast<const T*>(rc.data);
       T v[PART_ITEMS];
 #pragma unroll
-      for (int k = 0; k < PART_ITEMS; ++k) v[k] = rid[k].chunk_offset != 0xFFFFFFFFu ? data[rid[k].chunk_offset] : T{};
+      for (int k = 0; k < PART_ITEMS; ++k) v[k] = data[rid[k].chunk_offset != 0xFFFFFFFFu ? rid[k].chunk_offset : 0u];
 #pragma unroll
       for (int k = 0; k < PART_ITEMS; ++k) {
-        const uint32_t off = base + k * WAVE + __lane_id();
+        const uint32_t off = base + k * WAVE;
         const bool has = rid[k].chunk_offset != 0xFFFFFFFFu;
         pays[k] = s.fuse_deref ? ref_payload<P>(has, rid[k], rrow) : own_payload<P>(ch.row_begin, ch.chunk_id, off);
         keys[k] = static_cast<H>(v[k]);
@@ -220,9 +234,10 @@ __device__ __forceinline__ uint32_t load_items(const Side& s, const SrcChunk& ch
       }
       return act;
     }
+    if constexpr (LP != LP_ANY) return act;
 #pragma unroll
     for (int k = 0; k < PART_ITEMS; ++k) {
-      const uint32_t off = base + k * WAVE + __lane_id();
+      const uint32_t off = base + k * WAVE;
       if (off >= ch.size) continue;
       const hy_row_id rid1 = rid[k];
       const bool has = rid1.chunk_offset != 0xFFFFFFFFu;
@@ -234,10 +249,12 @@ __device__ __forceinline__ uint32_t load_items(const Side& s, const SrcChunk& ch
     }
     return act;
   }
+  if constexpr (LP == LP_ANY) {
 #pragma unroll
-  for (int k = 0; k < PART_ITEMS; ++k) {
-    const uint32_t off = base + k * WAVE + __lane_id();
-    if (off < ch.size && load_row<T, H, P>(s, ch, off, &keys[k], &pays[k])) act |= 1u << k;
+    for (int k = 0; k < PART_ITEMS; ++k) {
+      const uint32_t off = base + k * WAVE;
+      if (off < ch.size && load_row<T, H, P>(s, ch, off, &keys[k], &pays[k])) act |= 1u << k;
+    }
   }
   return act;
 }
@@ -297,13 +314,15 @@ __device__ __forceinline__ uint32_t wave_rank(uint32_t digit, bool active, int d
 // | rank of item k among its wave's same-digit items (wave_rank). The tile's records are first placed in LDS in
 // (digit, wave, rank) order - the order they take in the output - and then stored from consecutive LDS entries by
 // consecutive lanes, so each bucket's run of the tile is written with coalesced stores instead of one scattered 8-byte
-// store per lane. goff(d) = output position of this tile's first digit-d record.
+// store per lane. Thread d holds run = output position of this tile's first digit-d record and advances it by the
+// tile's digit-d count.
 static_assert(PART_THREADS >= 256, "one thread per digit");
-template <typename H, typename P, typename GOFF>
+template <typename H, typename P>
 __device__ __forceinline__ void staged_scatter(const Rec<H, P> (&recs)[PART_ITEMS], uint32_t act,
                                                const uint32_t (&dr)[PART_ITEMS], uint32_t (*s_cnt)[256],
                                                uint32_t* s_delta, Rec<H, P>* s_stage, uint32_t* s_scratch,
-                                               uint32_t n_digits, const Digit& dg, GOFF goff, Rec<H, P>* __restrict__ out) {
+                                               uint32_t n_digits, const Digit& dg, uint32_t& run,
+                                               Rec<H, P>* __restrict__ out) {
   const int w = threadIdx.x / WAVE;
   __syncthreads();  // every wave's counts are in s_cnt
   const uint32_t d = threadIdx.x;
@@ -321,7 +340,8 @@ __device__ __forceinline__ void staged_scatter(const Rec<H, P> (&recs)[PART_ITEM
   if (d < n_digits) {
 #pragma unroll
     for (int ww = 0; ww < PART_WAVES; ++ww) s_cnt[ww][d] += loc;
-    s_delta[d] = goff(d) - loc;
+    s_delta[d] = run - loc;
+    run += tot;
   }
   __syncthreads();
 #pragma unroll
@@ -334,31 +354,44 @@ __device__ __forceinline__ void staged_scatter(const Rec<H, P> (&recs)[PART_ITEM
   }
 }
 
+// Zeroes this wave's digit counters (only the wave itself uses its row before the next block barrier).
+__device__ __forceinline__ void clear_wave_counts(uint32_t* wave_cnt) {
+#pragma unroll
+  for (int i = 0; i < 256 / WAVE; ++i) wave_cnt[i * WAVE + __lane_id()] = 0;
+}
+
 // ------------------------------------------------------------------------------------------------------------
 // Pass 1: from column chunks.
 // ------------------------------------------------------------------------------------------------------------
-template <typename T, typename H>
+template <typename T, typename H, int LP>
 __global__ __launch_bounds__(PART_THREADS) void part1_hist(Side s, Digit dg, uint32_t n_digits,
                                                           uint32_t* __restrict__ hist) {
   __shared__ uint32_t s_hist[256];
-  const uint64_t tile = blockIdx.x;
+  const uint64_t tile = blockIdx.x;  // span
   for (int i = threadIdx.x; i < 256; i += PART_THREADS) s_hist[i] = 0;
   __syncthreads();
   const uint32_t c = s.tile_chunk[tile];
   const SrcChunk ch = s.chunks[c];
-  const uint32_t base = static_cast<uint32_t>(tile - s.chunk_tile_begin[c]) * PART_TILE;
+  const uint32_t base = static_cast<uint32_t>(tile - s.chunk_tile_begin[c]) * (s.sub * PART_TILE);
+  const uint32_t n_sub = min(s.sub, (ch.size - base + PART_TILE - 1) / PART_TILE);
   const int w = threadIdx.x / WAVE;
-  H keys[PART_ITEMS];
-  uint32_t pays[PART_ITEMS];
-  const uint32_t act = load_items<T, H, uint32_t>(s, ch, base + w * WAVE_SPAN, keys, pays);
+#pragma unroll 1
+  for (uint32_t j = 0; j < n_sub; ++j) {
+    H keys[PART_ITEMS];
+    uint32_t pays[PART_ITEMS];
+    const uint32_t act = load_items<T, H, uint32_t, LP>(s, ch, base + j * PART_TILE + w * WAVE_SPAN, keys, pays);
+    uint32_t dig[PART_ITEMS];
 #pragma unroll
-  for (int k = 0; k < PART_ITEMS; ++k)
-    if ((act >> k) & 1u) atomicAdd(&s_hist[digit_of<H>(dg, keys[k])], 1u);
+    for (int k = 0; k < PART_ITEMS; ++k) dig[k] = digit_of<H>(dg, keys[k]);
+#pragma unroll
+    for (int k = 0; k < PART_ITEMS; ++k)
+      if ((act >> k) & 1u) atomicAdd(&s_hist[dig[k]], 1u);
+  }
   __syncthreads();
   for (uint32_t d = threadIdx.x; d < n_digits; d += PART_THREADS) hist[d * s.n_tiles + tile] = s_hist[d];
 }
 
-template <typename T, typename H, typename P>
+template <typename T, typename H, typename P, int LP>
 __global__ __launch_bounds__(PART_THREADS) void part1_scatter(Side s, Digit dg, int dbits, uint32_t n_digits,
                                                              const uint32_t* __restrict__ offsets,
                                                              Rec<H, P>* __restrict__ out) {
@@ -366,29 +399,32 @@ __global__ __launch_bounds__(PART_THREADS) void part1_scatter(Side s, Digit dg, 
   __shared__ uint32_t s_delta[256];
   __shared__ uint32_t s_scratch[PART_WAVES + 1];
   __shared__ Rec<H, P> s_stage[PART_TILE];
-  const uint64_t tile = blockIdx.x;
-  for (int i = threadIdx.x; i < PART_WAVES * 256; i += PART_THREADS) (&s_cnt[0][0])[i] = 0;
-  __syncthreads();
+  const uint64_t tile = blockIdx.x;  // span
   const uint32_t c = s.tile_chunk[tile];
   const SrcChunk ch = s.chunks[c];
-  const uint32_t base = static_cast<uint32_t>(tile - s.chunk_tile_begin[c]) * PART_TILE;
+  const uint32_t base = static_cast<uint32_t>(tile - s.chunk_tile_begin[c]) * (s.sub * PART_TILE);
+  const uint32_t n_sub = min(s.sub, (ch.size - base + PART_TILE - 1) / PART_TILE);
   const int w = threadIdx.x / WAVE;
+  uint32_t run = threadIdx.x < n_digits ? offsets[threadIdx.x * s.n_tiles + tile] : 0u;
 
-  H keys[PART_ITEMS];
-  P pays[PART_ITEMS];
-  uint32_t dr[PART_ITEMS];  // digit << 24 | rank within the wave (rank < WAVE_SPAN)
-  const uint32_t act = load_items<T, H, P>(s, ch, base + w * WAVE_SPAN, keys, pays);
-  Rec<H, P> recs[PART_ITEMS];
+#pragma unroll 1
+  for (uint32_t j = 0; j < n_sub; ++j) {
+    clear_wave_counts(s_cnt[w]);
+    H keys[PART_ITEMS];
+    P pays[PART_ITEMS];
+    uint32_t dr[PART_ITEMS];  // digit << 24 | rank within the wave (rank < WAVE_SPAN)
+    const uint32_t act = load_items<T, H, P, LP>(s, ch, base + j * PART_TILE + w * WAVE_SPAN, keys, pays);
+    Rec<H, P> recs[PART_ITEMS];
 #pragma unroll
-  for (int k = 0; k < PART_ITEMS; ++k) {
-    const bool a = (act >> k) & 1u;
-    const uint32_t dig = a ? digit_of<H>(dg, keys[k]) : 0u;
-    dr[k] = (dig << 24) | wave_rank(dig, a, dbits, s_cnt[w]);
-    recs[k].key = keys[k];
-    recs[k].payload = pays[k];
+    for (int k = 0; k < PART_ITEMS; ++k) {
+      const bool a = (act >> k) & 1u;
+      const uint32_t dig = a ? digit_of<H>(dg, keys[k]) : 0u;
+      dr[k] = (dig << 24) | wave_rank(dig, a, dbits, s_cnt[w]);
+      recs[k].key = keys[k];
+      recs[k].payload = pays[k];
+    }
+    staged_scatter<H, P>(recs, act, dr, s_cnt, s_delta, s_stage, s_scratch, n_digits, dg, run, out);
   }
-  staged_scatter<H, P>(recs, act, dr, s_cnt, s_delta, s_stage, s_scratch, n_digits, dg,
-                    [&](uint32_t d) { return offsets[d * s.n_tiles + tile]; }, out);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -409,6 +445,7 @@ struct Segs {
   const uint64_t* seg_hbase;        // null: seg_tile_begin[i] * n_digits
   const uint32_t* seg_stride;       // null: the segment's tile count
   const uint32_t* seg_toff;         // null: 0
+  uint32_t sub;                     // tiles per span
 };
 
 __device__ __forceinline__ void seg_geometry(const Segs& sg, uint32_t sgi, uint32_t n_digits, uint32_t* b0, uint32_t* b1,
@@ -435,9 +472,18 @@ __global__ __launch_bounds__(PART_THREADS) void part2_hist(Segs sg, Digit dg, ui
   uint64_t hbase;
   seg_geometry(sg, sgi, n_digits, &b0, &b1, &hbase, &stride, &toff);
   const int w = threadIdx.x / WAVE;
-  for (int k = 0; k < PART_ITEMS; ++k) {
-    const uint32_t r = b0 + t_in * PART_TILE + w * WAVE_SPAN + k * WAVE + __lane_id();
-    if (r < b1) atomicAdd(&s_hist[digit_of<H>(dg, in[r].key)], 1u);
+  const uint32_t sb = b0 + t_in * (sg.sub * PART_TILE);
+  const uint32_t n_sub = min(sg.sub, (b1 - sb + PART_TILE - 1) / PART_TILE);
+#pragma unroll 1
+  for (uint32_t j = 0; j < n_sub; ++j) {
+    // unconditional loads from clamped rows (see load_items), then the counts of the rows in range
+    const uint32_t r0 = sb + j * PART_TILE + w * WAVE_SPAN + __lane_id();
+    uint32_t dig[PART_ITEMS];
+#pragma unroll
+    for (int k = 0; k < PART_ITEMS; ++k) dig[k] = digit_of<H>(dg, in[min(r0 + k * WAVE, b1 - 1)].key);
+#pragma unroll
+    for (int k = 0; k < PART_ITEMS; ++k)
+      if (r0 + k * WAVE < b1) atomicAdd(&s_hist[dig[k]], 1u);
   }
   __syncthreads();
   for (uint32_t d = threadIdx.x; d < n_digits; d += PART_THREADS) hist[hbase + d * stride + toff + t_in] = s_hist[d];
@@ -452,35 +498,37 @@ __global__ __launch_bounds__(PART_THREADS) void part2_scatter(Segs sg, Digit dg,
   __shared__ uint32_t s_delta[256];
   __shared__ uint32_t s_scratch[PART_WAVES + 1];
   __shared__ Rec<H, P> s_stage[PART_TILE];
-  const uint64_t tile = blockIdx.x;
+  const uint64_t tile = blockIdx.x;  // span
   if (tile >= sg.seg_tile_begin[sg.n_segs]) return;
-  for (int i = threadIdx.x; i < PART_WAVES * 256; i += PART_THREADS) (&s_cnt[0][0])[i] = 0;
-  __syncthreads();
   const uint32_t sgi = sg.tile_seg[tile];
   const uint32_t t_in = static_cast<uint32_t>(tile - sg.seg_tile_begin[sgi]);
   uint32_t b0, b1, stride, toff;
   uint64_t hbase;
   seg_geometry(sg, sgi, n_digits, &b0, &b1, &hbase, &stride, &toff);
   const int w = threadIdx.x / WAVE;
-  Rec<H, P> recs[PART_ITEMS];
-  uint32_t dr[PART_ITEMS];  // digit << 24 | rank within the wave
-  uint32_t act = 0;
+  const uint32_t sb = b0 + t_in * (sg.sub * PART_TILE);
+  const uint32_t n_sub = min(sg.sub, (b1 - sb + PART_TILE - 1) / PART_TILE);
+  uint32_t run = threadIdx.x < n_digits ? offsets[hbase + threadIdx.x * stride + toff + t_in] : 0u;
+#pragma unroll 1
+  for (uint32_t j = 0; j < n_sub; ++j) {
+    clear_wave_counts(s_cnt[w]);
+    Rec<H, P> recs[PART_ITEMS];
+    uint32_t dr[PART_ITEMS];  // digit << 24 | rank within the wave
+    uint32_t act = 0;
+    const uint32_t r0 = sb + j * PART_TILE + w * WAVE_SPAN + __lane_id();
 #pragma unroll
-  for (int k = 0; k < PART_ITEMS; ++k) {
-    const uint32_t r = b0 + t_in * PART_TILE + w * WAVE_SPAN + k * WAVE + __lane_id();
-    if (r < b1) {
-      recs[k] = in[r];
-      act |= 1u << k;
+    for (int k = 0; k < PART_ITEMS; ++k) recs[k] = in[min(r0 + k * WAVE, b1 - 1)];  // unconditional (see load_items)
+#pragma unroll
+    for (int k = 0; k < PART_ITEMS; ++k)
+      if (r0 + k * WAVE < b1) act |= 1u << k;
+#pragma unroll
+    for (int k = 0; k < PART_ITEMS; ++k) {
+      const bool a = (act >> k) & 1u;
+      const uint32_t dig = a ? digit_of<H>(dg, recs[k].key) : 0u;
+      dr[k] = (dig << 24) | wave_rank(dig, a, dbits, s_cnt[w]);
     }
+    staged_scatter<H, P>(recs, act, dr, s_cnt, s_delta, s_stage, s_scratch, n_digits, dg, run, out);
   }
-#pragma unroll
-  for (int k = 0; k < PART_ITEMS; ++k) {
-    const bool a = (act >> k) & 1u;
-    const uint32_t dig = a ? digit_of<H>(dg, recs[k].key) : 0u;
-    dr[k] = (dig << 24) | wave_rank(dig, a, dbits, s_cnt[w]);
-  }
-  staged_scatter<H, P>(recs, act, dr, s_cnt, s_delta, s_stage, s_scratch, n_digits, dg,
-                       [&](uint32_t d) { return offsets[hbase + d * stride + toff + t_in]; }, out);
 }
 
 // Bucket bounds after the pass from column chunks (histogram laid out digit-major over tiles):
@@ -494,10 +542,10 @@ __global__ void seg_bounds(const uint32_t* __restrict__ offsets, uint64_t n_tile
 
 // Tiles of every segment of a record pass (counts, then an exclusive scan and widen_prefix give seg_tile_begin).
 __global__ void seg_tile_counts(const uint32_t* __restrict__ seg_begin, const uint32_t* __restrict__ seg_end,
-                                uint32_t n_segs, uint32_t* __restrict__ counts) {
+                                uint32_t n_segs, uint32_t span, uint32_t* __restrict__ counts) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_segs; i += gridDim.x * blockDim.x) {
     const uint32_t b1 = seg_end ? seg_end[i] : seg_begin[i + 1];
-    counts[i] = (b1 - seg_begin[i] + PART_TILE - 1) / PART_TILE;
+    counts[i] = (b1 - seg_begin[i] + span - 1) / span;
   }
 }
 
