@@ -523,7 +523,7 @@ uint32_t sub_from_env(const char* name, uint32_t dflt) {
   return v >= 1 && v <= hyk::PART_SUB_MAX ? static_cast<uint32_t>(v) : dflt;
 }
 uint32_t sub1() {
-  static const uint32_t v = sub_from_env("HY_PART_SUB1", 2);
+  static const uint32_t v = sub_from_env("HY_PART_SUB1", 1);
   return v;
 }
 uint32_t sub2() {

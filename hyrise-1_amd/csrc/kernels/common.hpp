@@ -67,6 +67,16 @@ __host__ __device__ inline uint32_t murmur2(T key, uint32_t seed) {
 // ------------------------------------------------------------------------------------------------------------
 __device__ inline int lane_id() { return __lane_id(); }
 
+// XCD-aware workgroup -> tile map. Workgroups are dispatched round-robin over the 8 XCDs (workgroup b on XCD b % 8);
+// this hands XCD x a contiguous range of tiles, taken in order. Neighbouring tiles then run on the same XCD at about
+// the same time, so the 128-B lines they share at the edges of their output runs are completed in one L2 instead of
+// being written back half-filled from two. A bijection on [0, n) for any n.
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t n) {
+  constexpr uint32_t X = 8;
+  const uint32_t q = n / X, r = n % X, x = b % X;
+  return x * q + min(x, r) + b / X;
+}
+
 __device__ inline uint64_t lanemask_lt() {
   const int l = __lane_id();
   return l == 0 ? 0ull : (~0ull >> (64 - l));

@@ -9,8 +9,9 @@
 // This file reproduces that order exactly with an MI355X-shaped pipeline:
 //   pass 1  part1_hist / part1_scatter : read the join column straight from its chunks (value, dictionary, or
 //           through a PosList), murmur2-hash, stable scatter of 8-byte {key, payload} records by the HIGH digit of
-//           the partition id (up to 8 bits, 256 buckets). 8192-row tiles; per-wave match-any ranking keeps the
-//           scatter stable.
+//           the partition id (up to 8 bits, 256 buckets). 4096-row tiles; a per-wave match-any ranking (LDS lane
+//           masks) keeps the scatter stable; tiles are mapped to XCDs in contiguous ranges so neighbouring tiles'
+//           shared output lines are completed in one L2.
 //   pass 2  part2_hist / part2_scatter : inside every high-digit bucket, stable scatter by the LOW 8 bits. After
 //           pass 2 every radix partition is contiguous and in row order (MSD, so partition bounds fall out of the
 //           pass-2 histogram).
@@ -31,9 +32,10 @@ constexpr int PART_ITEMS = 16;                              // items per lane pe
 constexpr int PART_TILE = PART_THREADS * PART_ITEMS;        // 4096 rows per tile
 constexpr int WAVE_SPAN = WAVE * PART_ITEMS;                // 1024 consecutive rows per wave
 // A partition workgroup handles one SPAN of `sub` consecutive tiles (a per-pass launch parameter), one after the
-// other, carrying each digit's output position from tile to tile in a register. Histograms and their scans are per
-// span, so the per-digit offset tables are `sub` times smaller than per-tile ones (their strided 4-byte entries cost
-// a cache line each); a larger span has fewer tiles in flight per CU, so the host picks it per pass.
+// other, carrying each digit's output position from tile to tile in a register; histograms and their scans are per
+// span. Measured on MI355X (SF100 bench): with the XCD-aware tile map (xcd_tile) one tile per span is fastest - a
+// workgroup working through several tiles in sequence keeps fewer loads in flight than several workgroups do - so
+// the host default is sub = 1 (HY_PART_SUB1 / HY_PART_SUB2 override it).
 constexpr int PART_SUB_MAX = 16;
 constexpr uint32_t NULL_PAYLOAD = 0xFFFFFFFFu;
 
@@ -310,6 +312,33 @@ __device__ __forceinline__ uint32_t wave_rank(uint32_t digit, bool active, int d
   return rank;
 }
 
+// The same ranking without per-bit ballots: each active lane ORs its lane bit into its digit's 64-bit mask in LDS
+// and reads the mask back - the set of lanes holding the same digit (a match-any) - then clears it. LDS instructions
+// of one wave execute in order, so the read sees every lane's OR and the next item starts from a cleared mask. Three
+// LDS operations replace the 8 ballots and ~60 vector instructions per item of wave_rank (the partition passes were
+// VALU-bound on them).
+__device__ __forceinline__ uint32_t wave_rank_lds(uint32_t digit, bool active, uint64_t* wave_mask, uint32_t* wave_cnt) {
+  uint32_t rank = 0;
+  if (active) {
+    const uint64_t me = 1ull << __lane_id();
+    __hip_atomic_fetch_or(&wave_mask[digit], me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const uint64_t peers = __hip_atomic_load(&wave_mask[digit], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_store(&wave_mask[digit], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const uint32_t c = __hip_atomic_load(&wave_cnt[digit], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    rank = c + static_cast<uint32_t>(__popcll(peers & (me - 1)));
+    if ((peers & ~((me << 1) - 1)) == 0)  // highest lane of the group advances the counter
+      __hip_atomic_store(&wave_cnt[digit], c + static_cast<uint32_t>(__popcll(peers)), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  return rank;
+}
+
+// Zeroes this wave's 256 digit masks (the wave alone uses them until the next block barrier).
+__device__ __forceinline__ void clear_wave_masks(uint64_t* wave_mask) {
+#pragma unroll
+  for (int i = 0; i < 256 / WAVE; ++i) wave_mask[i * WAVE + __lane_id()] = 0;
+}
+
 // LDS-staged scatter of one tile's records. On entry s_cnt[w][d] holds wave w's count of digit d and dr[k] = digit << 24
 // | rank of item k among its wave's same-digit items (wave_rank). The tile's records are first placed in LDS in
 // (digit, wave, rank) order - the order they take in the output - and then stored from consecutive LDS entries by
@@ -317,6 +346,7 @@ __device__ __forceinline__ uint32_t wave_rank(uint32_t digit, bool active, int d
 // store per lane. Thread d holds run = output position of this tile's first digit-d record and advances it by the
 // tile's digit-d count.
 static_assert(PART_THREADS >= 256, "one thread per digit");
+static_assert(PART_TILE * 8 >= PART_WAVES * 256 * 8, "ranking masks fit the staging area");
 template <typename H, typename P>
 __device__ __forceinline__ void staged_scatter(const Rec<H, P> (&recs)[PART_ITEMS], uint32_t act,
                                                const uint32_t (&dr)[PART_ITEMS], uint32_t (*s_cnt)[256],
@@ -367,7 +397,7 @@ template <typename T, typename H, int LP>
 __global__ __launch_bounds__(PART_THREADS) void part1_hist(Side s, Digit dg, uint32_t n_digits,
                                                           uint32_t* __restrict__ hist) {
   __shared__ uint32_t s_hist[256];
-  const uint64_t tile = blockIdx.x;  // span
+  const uint64_t tile = xcd_tile(blockIdx.x, gridDim.x);  // span
   for (int i = threadIdx.x; i < 256; i += PART_THREADS) s_hist[i] = 0;
   __syncthreads();
   const uint32_t c = s.tile_chunk[tile];
@@ -392,14 +422,14 @@ __global__ __launch_bounds__(PART_THREADS) void part1_hist(Side s, Digit dg, uin
 }
 
 template <typename T, typename H, typename P, int LP>
-__global__ __launch_bounds__(PART_THREADS) void part1_scatter(Side s, Digit dg, int dbits, uint32_t n_digits,
+__global__ __launch_bounds__(PART_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void part1_scatter(Side s, Digit dg, int dbits, uint32_t n_digits,
                                                              const uint32_t* __restrict__ offsets,
                                                              Rec<H, P>* __restrict__ out) {
   __shared__ uint32_t s_cnt[PART_WAVES][256];
   __shared__ uint32_t s_delta[256];
   __shared__ uint32_t s_scratch[PART_WAVES + 1];
   __shared__ Rec<H, P> s_stage[PART_TILE];
-  const uint64_t tile = blockIdx.x;  // span
+  const uint64_t tile = xcd_tile(blockIdx.x, gridDim.x);  // span
   const uint32_t c = s.tile_chunk[tile];
   const SrcChunk ch = s.chunks[c];
   const uint32_t base = static_cast<uint32_t>(tile - s.chunk_tile_begin[c]) * (s.sub * PART_TILE);
@@ -407,9 +437,12 @@ __global__ __launch_bounds__(PART_THREADS) void part1_scatter(Side s, Digit dg, 
   const int w = threadIdx.x / WAVE;
   uint32_t run = threadIdx.x < n_digits ? offsets[threadIdx.x * s.n_tiles + tile] : 0u;
 
+  uint64_t* s_mask = reinterpret_cast<uint64_t*>(s_stage) + w * 256;  // ranking masks alias the staging area
 #pragma unroll 1
   for (uint32_t j = 0; j < n_sub; ++j) {
+    if (j) __syncthreads();  // the previous tile's write-out has read s_stage
     clear_wave_counts(s_cnt[w]);
+    clear_wave_masks(s_mask);
     H keys[PART_ITEMS];
     P pays[PART_ITEMS];
     uint32_t dr[PART_ITEMS];  // digit << 24 | rank within the wave (rank < WAVE_SPAN)
@@ -419,7 +452,7 @@ __global__ __launch_bounds__(PART_THREADS) void part1_scatter(Side s, Digit dg, 
     for (int k = 0; k < PART_ITEMS; ++k) {
       const bool a = (act >> k) & 1u;
       const uint32_t dig = a ? digit_of<H>(dg, keys[k]) : 0u;
-      dr[k] = (dig << 24) | wave_rank(dig, a, dbits, s_cnt[w]);
+      dr[k] = (dig << 24) | wave_rank_lds(dig, a, s_mask, s_cnt[w]);
       recs[k].key = keys[k];
       recs[k].payload = pays[k];
     }
@@ -462,7 +495,7 @@ template <typename H, typename P>
 __global__ __launch_bounds__(PART_THREADS) void part2_hist(Segs sg, Digit dg, uint32_t n_digits,
                                                           const Rec<H, P>* __restrict__ in, uint32_t* __restrict__ hist) {
   __shared__ uint32_t s_hist[256];
-  const uint64_t tile = blockIdx.x;
+  const uint64_t tile = xcd_tile(blockIdx.x, gridDim.x);
   if (tile >= sg.seg_tile_begin[sg.n_segs]) return;
   for (int i = threadIdx.x; i < 256; i += PART_THREADS) s_hist[i] = 0;
   __syncthreads();
@@ -498,7 +531,7 @@ __global__ __launch_bounds__(PART_THREADS) void part2_scatter(Segs sg, Digit dg,
   __shared__ uint32_t s_delta[256];
   __shared__ uint32_t s_scratch[PART_WAVES + 1];
   __shared__ Rec<H, P> s_stage[PART_TILE];
-  const uint64_t tile = blockIdx.x;  // span
+  const uint64_t tile = xcd_tile(blockIdx.x, gridDim.x);  // span
   if (tile >= sg.seg_tile_begin[sg.n_segs]) return;
   const uint32_t sgi = sg.tile_seg[tile];
   const uint32_t t_in = static_cast<uint32_t>(tile - sg.seg_tile_begin[sgi]);
@@ -509,9 +542,12 @@ __global__ __launch_bounds__(PART_THREADS) void part2_scatter(Segs sg, Digit dg,
   const uint32_t sb = b0 + t_in * (sg.sub * PART_TILE);
   const uint32_t n_sub = min(sg.sub, (b1 - sb + PART_TILE - 1) / PART_TILE);
   uint32_t run = threadIdx.x < n_digits ? offsets[hbase + threadIdx.x * stride + toff + t_in] : 0u;
+  uint64_t* s_mask = reinterpret_cast<uint64_t*>(s_stage) + w * 256;  // ranking masks alias the staging area
 #pragma unroll 1
   for (uint32_t j = 0; j < n_sub; ++j) {
+    if (j) __syncthreads();  // the previous tile's write-out has read s_stage
     clear_wave_counts(s_cnt[w]);
+    clear_wave_masks(s_mask);
     Rec<H, P> recs[PART_ITEMS];
     uint32_t dr[PART_ITEMS];  // digit << 24 | rank within the wave
     uint32_t act = 0;
@@ -525,7 +561,7 @@ __global__ __launch_bounds__(PART_THREADS) void part2_scatter(Segs sg, Digit dg,
     for (int k = 0; k < PART_ITEMS; ++k) {
       const bool a = (act >> k) & 1u;
       const uint32_t dig = a ? digit_of<H>(dg, recs[k].key) : 0u;
-      dr[k] = (dig << 24) | wave_rank(dig, a, dbits, s_cnt[w]);
+      dr[k] = (dig << 24) | wave_rank_lds(dig, a, s_mask, s_cnt[w]);
     }
     staged_scatter<H, P>(recs, act, dr, s_cnt, s_delta, s_stage, s_scratch, n_digits, dg, run, out);
   }
