@@ -733,8 +733,10 @@ hy_status run_scan(const uint32_t* in, uint32_t* out, uint64_t n, const Common& 
   HY_HIP(hipMemsetAsync(c.scan_status, 0, sizeof(uint64_t) * (tiles + 1), s));
   HY_HIP(hipMemsetAsync(c.misc, 0, 4, s));
   KTimer kt_("exclusive_scan", s, n);
-  hipLaunchKernelGGL(hyk::exclusive_scan_u32, dim3(static_cast<uint32_t>(tiles)), dim3(hyk::SCAN_T), 0, s, in, out, n,
-                     c.scan_status, c.misc, c.misc + 1, total_out);
+  const bool vec = reinterpret_cast<uintptr_t>(in) % 16 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0;
+  hipLaunchKernelGGL(vec ? hyk::exclusive_scan_u32<true> : hyk::exclusive_scan_u32<false>,
+                     dim3(static_cast<uint32_t>(tiles)), dim3(hyk::SCAN_T), 0, s, in, out, n, c.scan_status, c.misc,
+                     c.misc + 1, total_out);
   kt_.done();
   HY_HIP(hipGetLastError());
   return HY_OK;

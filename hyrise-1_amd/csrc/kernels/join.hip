@@ -625,10 +625,15 @@ constexpr int SCAN_T = 512;
 constexpr int SCAN_PER = 16;
 constexpr int SCAN_BLOCK = SCAN_T * SCAN_PER;
 
+// Lane t of the workgroup holds the four 4-element groups at (k * SCAN_T + t) * 4, k = 0..3: every load and store
+// instruction of a wave then moves 1 KB of consecutive words (16 B per lane). The block's prefix runs over the
+// groups in (k, t) order - four workgroup scans - followed by the decoupled look-back across blocks.
+template <bool VEC>
 __global__ __launch_bounds__(SCAN_T) void exclusive_scan_u32(const uint32_t* __restrict__ in,
                                                              uint32_t* __restrict__ out, uint64_t n,
                                                              uint64_t* __restrict__ status, uint32_t* ticket,
                                                              uint32_t* error, uint64_t* total_out) {
+  static_assert(SCAN_PER == 16, "four groups of four per lane");
   __shared__ uint32_t s_scratch[SCAN_T / WAVE + 1];
   __shared__ uint64_t s_tile;
   __shared__ uint64_t s_prefix;
@@ -637,16 +642,28 @@ __global__ __launch_bounds__(SCAN_T) void exclusive_scan_u32(const uint32_t* __r
   const uint64_t tile = s_tile;
   const uint64_t n_tiles = (n + SCAN_BLOCK - 1) / SCAN_BLOCK;
   if (tile >= n_tiles) return;
-  const uint64_t i0 = tile * SCAN_BLOCK + threadIdx.x * SCAN_PER;
-  uint32_t v[SCAN_PER];
-  uint32_t sum = 0;
+  const uint64_t base = tile * SCAN_BLOCK;
+  const bool full = VEC && base + SCAN_BLOCK <= n;
+  uint4 v[4];
 #pragma unroll
-  for (int i = 0; i < SCAN_PER; ++i) {
-    v[i] = (i0 + i < n) ? in[i0 + i] : 0u;
-    sum += v[i];
+  for (int k = 0; k < 4; ++k) {
+    const uint64_t e = base + (static_cast<uint64_t>(k) * SCAN_T + threadIdx.x) * 4;
+    if (full) {
+      v[k] = reinterpret_cast<const uint4*>(in + e)[0];
+    } else {
+      v[k].x = e < n ? in[e] : 0u;
+      v[k].y = e + 1 < n ? in[e + 1] : 0u;
+      v[k].z = e + 2 < n ? in[e + 2] : 0u;
+      v[k].w = e + 3 < n ? in[e + 3] : 0u;
+    }
   }
-  uint32_t total;
-  const uint32_t local = block_exclusive_sum<SCAN_T>(sum, s_scratch, &total);
+  uint32_t loc[4], total = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint32_t tk;
+    loc[k] = block_exclusive_sum<SCAN_T>(v[k].x + v[k].y + v[k].z + v[k].w, s_scratch, &tk) + total;
+    total += tk;
+  }
   if (threadIdx.x < WAVE) {
     uint64_t prefix = 0;
     if (tile == 0) {
@@ -662,11 +679,23 @@ __global__ __launch_bounds__(SCAN_T) void exclusive_scan_u32(const uint32_t* __r
     }
   }
   __syncthreads();
-  uint32_t run = static_cast<uint32_t>(s_prefix) + local;
+  const uint32_t pre = static_cast<uint32_t>(s_prefix);
 #pragma unroll
-  for (int i = 0; i < SCAN_PER; ++i) {
-    if (i0 + i < n) out[i0 + i] = run;
-    run += v[i];
+  for (int k = 0; k < 4; ++k) {
+    const uint64_t e = base + (static_cast<uint64_t>(k) * SCAN_T + threadIdx.x) * 4;
+    uint4 o;
+    o.x = pre + loc[k];
+    o.y = o.x + v[k].x;
+    o.z = o.y + v[k].y;
+    o.w = o.z + v[k].z;
+    if (full) {
+      reinterpret_cast<uint4*>(out + e)[0] = o;
+    } else {
+      if (e < n) out[e] = o.x;
+      if (e + 1 < n) out[e + 1] = o.y;
+      if (e + 2 < n) out[e + 2] = o.z;
+      if (e + 3 < n) out[e + 3] = o.w;
+    }
   }
 }
 
