@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -53,6 +54,21 @@ hy_status make_plan(const hy_agg_input* in, const hy_agg_params* p, AggPlan* pla
     d.cols[j].type = c.value_type;
     d.cols[j].pos_group = c.pos_group;
     d.cols[j].domain = c.domain;
+    // one encoding across the column's chunks (agg_dense_span reads columns with uniform control flow)
+    int32_t kind = c.n_chunks ? c.chunks[0].kind : HY_COL_VALUE;
+    int32_t width = 0, nulls = 0;
+    for (uint32_t k = 0; k < c.n_chunks; ++k) {
+      const auto& ch = c.chunks[k];
+      if (ch.kind != kind) kind = -1;
+      if (ch.kind == HY_COL_DICT) {
+        if (width == 0) width = ch.vid_width;
+        if (ch.vid_width != width) kind = -1;
+      }
+      if (ch.nulls) nulls = 1;
+    }
+    d.cols[j].ukind = kind;
+    d.cols[j].uwidth = width;
+    d.cols[j].unulls = nulls;
   }
   // record layout
   const uint32_t H = p->n_groupby;
@@ -273,7 +289,20 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
     hipLaunchKernelGGL(hyk::agg_init_records, dim3(grid_for(nw, 256)), dim3(256), 0, s, w.records,
                        uint64_t(plan.dense_groups), d.words, w.word_op);
     HY_HIP(hipGetLastError());
-    if (plan.n_tiles) {
+    // agg_dense_span (batched column reads, per-span register folding) unless a column mixes encodings or the
+    // input has several PosList groups; HY_AGG_DENSE_ROWS=1 forces the per-64-row kernel (test knob)
+    bool span = input->n_pos_groups <= 1;
+    for (uint32_t j = 0; j < input->n_columns; ++j) span = span && d.cols[j].ukind >= 0;
+    if (const char* e = std::getenv("HY_AGG_DENSE_ROWS")) span = span && std::atoi(e) == 0;
+    if (plan.n_tiles && span) {
+      const size_t lds = sizeof(unsigned long long) * plan.dense_groups * d.words;
+      const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(plan.n_tiles, 256 * 16));
+      KTimer t("agg_dense_span", s, plan.rows);
+      hipLaunchKernelGGL(hyk::agg_dense_span, dim3(grid), dim3(hyk::AGG_THREADS), lds, s, d, plan.dense_groups,
+                         w.records);
+      t.done();
+      HY_HIP(hipGetLastError());
+    } else if (plan.n_tiles) {
       const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(plan.n_tiles, 256 * 8));
       KTimer t("agg_dense_rows", s, plan.rows);
       hipLaunchKernelGGL(hyk::agg_dense_rows, dim3(grid), dim3(hyk::AGG_THREADS), 0, s, d, plan.dense_groups,

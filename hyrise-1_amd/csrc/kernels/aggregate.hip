@@ -64,6 +64,9 @@ struct AggCol {
   int32_t pos_group;              // -1: read at (input chunk, offset); else through pos_lists[pos_group]
   uint32_t domain;                // dense grouping: codes in [0, domain), NULL -> domain
   uint32_t stride;                // dense grouping: weight of this column's code in the group index
+  int32_t ukind;                  // HY_COL_* shared by every chunk of the column, -1 if mixed (host-computed)
+  int32_t uwidth;                 // dictionary chunks: the vid width they all share (0 if mixed)
+  int32_t unulls;                 // value chunks: some chunk has NULL flags
 };
 
 struct AggFn {
@@ -388,6 +391,276 @@ __global__ __launch_bounds__(AGG_THREADS) void agg_dense_rows(AggDesc d, uint32_
   for (uint32_t i = threadIdx.x; i < n_words; i += AGG_THREADS) {
     const int32_t op = d.word_op[i % words];
     word_apply(records + i, op, s_rec[i]);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// agg_dense_span: the dense path restructured for memory-level parallelism (TPC-H 1 shape). A wave owns a span of
+// AGG_WAVE_SPAN = 1024 rows; lane l holds rows span + 64 k + l for k < 16 (coalesced per k). Every column is read
+// for all 16 rows in phases (RowIDs, chunk descriptors, values, dictionary entries), so 16 independent loads per lane
+// are in flight at each step instead of one dependent chain per row. Per group present in the span, each lane first
+// folds its 16 rows in registers (counts, sums, min/max, limb pieces) and the wave then reduces once - 16x fewer
+// cross-lane reductions than per-64-row ballots. Requires: at most one PosList group and every used column with one
+// encoding (kind / vid width) across its chunks (AggCol::ukind); the host falls back to agg_dense_rows otherwise.
+// Results are word-for-word those of agg_dense_rows (the same ADD / MIN / MAX / OR combination of the same values).
+// ------------------------------------------------------------------------------------------------------------
+constexpr int SPAN_K = 4;  // rows per lane per step: a wave span is AGG_ITEMS / SPAN_K steps (register budget)
+
+// Loads the values of column col for the 16 rows of this lane; returns the non-NULL mask (bit k).
+__device__ __forceinline__ uint32_t span_load(const AggDesc& d, const AggCol& col, uint32_t c, uint32_t base,
+                                              uint32_t act, const hy_row_id (&rid)[SPAN_K], uint64_t (&b)[SPAN_K]) {
+  const bool wide = is_wide(col.type);
+  const int lane = __lane_id();
+  uint32_t ok = act;
+  uint32_t off[SPAN_K];
+  uint32_t cc = c;  // chunk whose descriptor serves every row of the step when `uniform`
+  bool uniform = true;
+  if (col.pos_group < 0) {
+#pragma unroll
+    for (int k = 0; k < SPAN_K; ++k) off[k] = base + k * WAVE + lane;
+  } else {
+    // scan outputs reference one chunk per PosList: then the descriptor is wave-uniform (scalar loads, no per-row
+    // descriptor round trip); otherwise rows are read one by one through their own chunk's descriptor
+    cc = __builtin_amdgcn_readfirstlane(rid[0].chunk_id);
+    bool same = true;
+#pragma unroll
+    for (int k = 0; k < SPAN_K; ++k) {
+      off[k] = rid[k].chunk_offset;
+      if ((act >> k) & 1u) same = same && rid[k].chunk_id == cc && rid[k].chunk_offset != 0xFFFFFFFFu;
+    }
+    uniform = __ballot(!same) == 0ull;
+  }
+  if (!uniform) {
+#pragma unroll
+    for (int k = 0; k < SPAN_K; ++k) {
+      b[k] = 0;
+      if (!((ok >> k) & 1u)) continue;
+      if (rid[k].chunk_offset == 0xFFFFFFFFu || !load_bits(col.chunks[rid[k].chunk_id], off[k], wide, &b[k]))
+        ok &= ~(1u << k);
+    }
+    return ok;
+  }
+  const hy_column_chunk& ch = col.chunks[cc];
+  if (col.ukind == HY_COL_DICT) {
+    const void* data = ch.data;
+    const void* dict = ch.dictionary;
+    const uint32_t dsz = ch.dictionary_size;
+    uint32_t vid[SPAN_K];
+#pragma unroll
+    for (int k = 0; k < SPAN_K; ++k) {
+      vid[k] = 0xFFFFFFFFu;
+      if ((ok >> k) & 1u) {
+        if (col.uwidth == 1)
+          vid[k] = static_cast<const uint8_t*>(data)[off[k]];
+        else if (col.uwidth == 2)
+          vid[k] = static_cast<const uint16_t*>(data)[off[k]];
+        else
+          vid[k] = static_cast<const uint32_t*>(data)[off[k]];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < SPAN_K; ++k) {
+      b[k] = 0;
+      if (((ok >> k) & 1u) && vid[k] < dsz)
+        b[k] = wide ? static_cast<const uint64_t*>(dict)[vid[k]] : static_cast<const uint32_t*>(dict)[vid[k]];
+      else
+        ok &= ~(1u << k);
+    }
+  } else {
+    const void* data = ch.data;
+    const uint8_t* nul = col.unulls ? ch.nulls : nullptr;
+    uint8_t nf[SPAN_K];
+#pragma unroll
+    for (int k = 0; k < SPAN_K; ++k) {
+      b[k] = 0;
+      nf[k] = 0;
+      if ((ok >> k) & 1u) {
+        b[k] = wide ? static_cast<const uint64_t*>(data)[off[k]] : static_cast<const uint32_t*>(data)[off[k]];
+        if (nul != nullptr) nf[k] = nul[off[k]];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < SPAN_K; ++k)
+      if (nf[k]) {
+        ok &= ~(1u << k);
+        b[k] = 0;
+      }
+  }
+  return ok;
+}
+
+__global__ __launch_bounds__(AGG_THREADS) void agg_dense_span(AggDesc d, uint32_t n_groups,
+                                                             unsigned long long* __restrict__ records) {
+  extern __shared__ unsigned long long s_recd[];
+  const uint32_t words = d.words;
+  const uint32_t n_words = n_groups * words;
+  for (uint32_t i = threadIdx.x; i < n_words; i += AGG_THREADS) s_recd[i] = word_init(d.word_op[i % words]);
+  __syncthreads();
+  const int lane = __lane_id();
+  const int w = threadIdx.x / WAVE;
+  const uint32_t H = d.n_gb;
+
+  for (uint64_t tile = blockIdx.x; tile < d.n_tiles; tile += gridDim.x) {
+    const uint32_t c = agg_tile_chunk(d, tile);
+    const uint32_t size = d.chunk_size[c];
+    const uint32_t span = static_cast<uint32_t>(tile - d.chunk_tile_begin[c]) * AGG_TILE + w * AGG_WAVE_SPAN;
+    const uint64_t row0 = d.chunk_row_begin[c];
+    for (int h = 0; h < AGG_ITEMS / SPAN_K; ++h) {
+    const uint32_t base = span + h * SPAN_K * WAVE;
+    if (base >= size) break;  // wave-uniform
+    uint32_t act = 0;
+#pragma unroll
+    for (int k = 0; k < SPAN_K; ++k)
+      if (base + k * WAVE + lane < size) act |= 1u << k;
+    hy_row_id rid[SPAN_K];
+    if (d.n_pos_groups) {
+      const hy_row_id* pl = d.pos_lists[c];
+#pragma unroll
+      for (int k = 0; k < SPAN_K; ++k)
+        rid[k] = ((act >> k) & 1u) ? pl[base + k * WAVE + lane] : hy_row_id{0xFFFFFFFFu, 0xFFFFFFFFu};
+    }
+    // group index of every row
+    uint8_t g[SPAN_K];
+#pragma unroll
+    for (int k = 0; k < SPAN_K; ++k) g[k] = 0;
+    for (uint32_t j = 0; j < d.n_gb; ++j) {
+      const AggCol& col = d.cols[d.gb[j]];
+      uint64_t b[SPAN_K];
+      const uint32_t ok = span_load(d, col, c, base, act, rid, b);
+      bool bad = false;
+#pragma unroll
+      for (int k = 0; k < SPAN_K; ++k) {
+        uint32_t code = col.domain;
+        if ((ok >> k) & 1u) {
+          code = static_cast<uint32_t>(b[k]);
+          if (code >= col.domain) {
+            bad = true;
+            code = col.domain;
+          }
+        }
+        g[k] = static_cast<uint8_t>(g[k] + code * col.stride);
+      }
+      if (bad) atomicOr(d.error, 2u);
+    }
+    uint64_t mine_groups = 0;
+#pragma unroll
+    for (int k = 0; k < SPAN_K; ++k)
+      if ((act >> k) & 1u) mine_groups |= 1ull << g[k];
+    const uint64_t span_groups = wave_or64(mine_groups);
+    // header words: rows, first row, last row
+    for (uint64_t pg = span_groups; pg;) {
+      const uint32_t gg = static_cast<uint32_t>(__builtin_ctzll(pg));
+      pg &= pg - 1;
+      uint32_t cnt = 0;
+      uint64_t first = ~0ull, last = 0;
+#pragma unroll
+      for (int k = 0; k < SPAN_K; ++k) {
+        if (((act >> k) & 1u) && g[k] == gg) {
+          const uint64_t row = row0 + base + k * WAVE + lane;
+          ++cnt;
+          first = row < first ? row : first;
+          last = row > last ? row : last;
+        }
+      }
+      const uint32_t rows = wave_sum(cnt);
+      first = wave_min64(first);
+      last = wave_max64(last);
+      if (lane == 0) {
+        unsigned long long* rec = s_recd + gg * words;
+        atomicAdd(rec + H + AGG_HDR_ROWS, static_cast<unsigned long long>(rows));
+        atomicMin(rec + H + AGG_HDR_FIRST, static_cast<unsigned long long>(first));
+        atomicMax(rec + H + AGG_HDR_LAST, static_cast<unsigned long long>(last));
+      }
+    }
+    // aggregates
+    for (uint32_t f = 0; f < d.n_fns; ++f) {
+      const AggFn fn = d.fns[f];
+      if (fn.column < 0) continue;  // COUNT(*) = rows
+      const AggCol& col = d.cols[fn.column];
+      uint64_t b[SPAN_K];
+      const uint32_t ok = span_load(d, col, c, base, act, rid, b);
+      const int32_t type = col.type;
+      for (uint64_t pg = span_groups; pg;) {
+        const uint32_t gg = static_cast<uint32_t>(__builtin_ctzll(pg));
+        pg &= pg - 1;
+        uint32_t inm = 0;
+#pragma unroll
+        for (int k = 0; k < SPAN_K; ++k)
+          if (((ok >> k) & 1u) && g[k] == gg) inm |= 1u << k;
+        const uint32_t cnt = wave_sum(static_cast<uint32_t>(__popc(inm)));
+        unsigned long long* rec = s_recd + gg * words;
+        if (lane == 0 && cnt) atomicAdd(rec + fn.word, static_cast<unsigned long long>(cnt));
+        if (cnt == 0 || fn.function == HY_AGG_COUNT) continue;
+        if (fn.function == HY_AGG_MIN || fn.function == HY_AGG_MAX) {
+          const bool is_min = fn.function == HY_AGG_MIN;
+          uint64_t r = is_min ? ~0ull : 0ull;
+#pragma unroll
+          for (int k = 0; k < SPAN_K; ++k) {
+            if ((inm >> k) & 1u) {
+              const uint64_t ob = ordered_bits(b[k], type);
+              r = is_min ? (ob < r ? ob : r) : (ob > r ? ob : r);
+            }
+          }
+          r = is_min ? wave_min64(r) : wave_max64(r);
+          if (lane == 0) {
+            if (is_min)
+              atomicMin(rec + fn.word + 1, static_cast<unsigned long long>(r));
+            else
+              atomicMax(rec + fn.word + 1, static_cast<unsigned long long>(r));
+          }
+        } else if (fn.limbs == 0) {  // SUM / AVG of integers (two's complement wrap, like agg_dense_rows)
+          uint64_t s = 0;
+#pragma unroll
+          for (int k = 0; k < SPAN_K; ++k)
+            if ((inm >> k) & 1u) s += static_cast<uint64_t>(int_value(b[k], type));
+          s = wave_sum64(s);
+          if (lane == 0 && s) atomicAdd(rec + fn.word + 1, static_cast<unsigned long long>(s));
+        } else {  // SUM / AVG of floats: exact limbs; each row's pieces are split once, then summed per limb
+          uint32_t special = 0;
+          int lo = 0x7FFFFFFF, hi = -1;
+          int i0s[SPAN_K];
+          int64_t pc[SPAN_K][3];
+#pragma unroll
+          for (int k = 0; k < SPAN_K; ++k) {
+            i0s[k] = -4;  // no piece of this row matches any limb
+            pc[k][0] = pc[k][1] = pc[k][2] = 0;
+            if ((inm >> k) & 1u) {
+              int i0 = 0;
+              uint32_t sp = 0;
+              const int np = float_parts(b[k], type, &i0, pc[k], &sp);
+              special |= sp;
+              if (np) {
+                i0s[k] = i0;
+                lo = min(lo, i0);
+                hi = max(hi, i0 + np - 1);
+              } else {
+                pc[k][0] = pc[k][1] = pc[k][2] = 0;
+              }
+            }
+          }
+          const uint64_t spw = wave_or64(special);
+          if (lane == 0 && spw) atomicOr(rec + fn.word + 1, static_cast<unsigned long long>(spw));
+          lo = wave_min_i(lo);
+          hi = wave_max_i(hi);
+          for (int l = lo; l <= hi; ++l) {
+            int64_t s = 0;
+#pragma unroll
+            for (int k = 0; k < SPAN_K; ++k) {
+              const int q = l - i0s[k];
+              s += q == 0 ? pc[k][0] : (q == 1 ? pc[k][1] : (q == 2 ? pc[k][2] : 0));
+            }
+            const uint64_t ws = wave_sum64(static_cast<uint64_t>(s));
+            if (lane == 0 && ws) atomicAdd(rec + fn.word + 2 + l, static_cast<unsigned long long>(ws));
+          }
+        }
+      }
+    }
+    }  // steps of the span
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n_words; i += AGG_THREADS) {
+    const int32_t op = d.word_op[i % words];
+    word_apply(records + i, op, s_recd[i]);
   }
 }
 

@@ -75,6 +75,50 @@ def lineitem_torch(okey, lines, first_row=0, seed=SEED):
     return lkey, qty.to(torch.int32)
 
 
+def _umod_torch(h, m):
+    """(h mod 2^64) % m for int64 tensors holding uint64 bit patterns."""
+    import torch
+
+    return torch.remainder(torch.remainder(h, m) + torch.where(h < 0, (1 << 64) % m, 0), m)
+
+
+# days since 1970-01-01 (dbgen's date range, dss.h STARTDATE / CURRENTDATE / ENDDATE - 151)
+DATE_1992_01_01, DATE_1995_06_17, DATE_1998_08_02, DATE_1998_09_02 = 8035, 9298, 10440, 10471
+
+
+def lineitem_q1_torch(sf, device, seed=SEED):
+    """The lineitem columns TPC-H 1 reads, TPC-H-shaped (dbgen dss.h / build.c value ranges), as torch tensors:
+    l_shipdate int32 days (o_orderdate + 1..121, o_orderdate uniform 1992-01-01..1998-08-02), l_returnflag code
+    (A=0, N=1, R=2: R/A when the receipt date l_shipdate + 1..30 is <= 1995-06-17, else N), l_linestatus code (F=0,
+    O=1: O when l_shipdate > 1995-06-17), l_quantity 1..50, l_extendedprice int64 cents = quantity x retail price
+    (900.00..2100.00), l_discount 0..10 (hundredths). Works on any torch device (the CPU baseline uses the same
+    generator on a smaller scale factor)."""
+    import torch
+
+    okey, lines = orders_torch(sf, device, seed=seed)
+    i = torch.arange(1, okey.numel() + 1, dtype=torch.int64, device=device)
+    odate = DATE_1992_01_01 + _umod_torch(_splitmix64_torch(i ^ (seed ^ 0x0D47)), DATE_1998_08_02 - DATE_1992_01_01 + 1)
+    odate = torch.repeat_interleave(odate, lines)
+    del okey, i
+    _, qty = lineitem_torch(torch.zeros(lines.numel(), dtype=torch.int32, device=device), lines)
+    del lines
+    n = qty.numel()
+    r = torch.arange(n, dtype=torch.int64, device=device)
+    h = _splitmix64_torch(r ^ (seed ^ 0x5344))
+    ship = odate + 1 + _umod_torch(h, 121)
+    del odate
+    receipt = ship + 1 + torch.remainder(h >> 8, 30)  # h >> 8 may be negative: arithmetic shift, remainder >= 0
+    rflag = torch.where(receipt <= DATE_1995_06_17, torch.where((h >> 20) & 1 == 1, 2, 0), 1).to(torch.int32)
+    del receipt
+    lstatus = (ship > DATE_1995_06_17).to(torch.int32)
+    h = _splitmix64_torch(r ^ (seed ^ 0x5052))
+    retail = 90_000 + _umod_torch(h, 120_001)
+    price = qty.to(torch.int64) * retail
+    disc = torch.remainder(h >> 24, 11).to(torch.int32)
+    return {"l_shipdate": ship.to(torch.int32), "l_returnflag": rflag, "l_linestatus": lstatus, "l_quantity": qty,
+            "l_extendedprice": price, "l_discount": disc}
+
+
 def dictionary_encode_small_domain(values_np_or_torch, chunk, domain):
     """Per-chunk dictionary encoding of values in [1, domain] (FixedSizeByteAligned u8 when domain < 255):
     returns (vids u8, present[chunks, domain] bool). vid = rank of the value among the chunk's distinct values,
