@@ -113,6 +113,7 @@ hy_status make_plan(const hy_agg_input* in, const hy_agg_params* p, AggPlan* pla
           L.agg_emin[a] = f ? hyk::FLOAT_EMIN : hyk::DOUBLE_EMIN;
           plan->word_op.push_back(hyk::WOP_OR);
           for (int l = 0; l < fn.limbs; ++l) plan->word_op.push_back(hyk::WOP_ADD);
+          plan->word_op.push_back(hyk::WOP_ADD);  // integer-valued rows (agg_dense_span; zero when flushed)
         } else {
           plan->word_op.push_back(hyk::WOP_ADD);
         }

@@ -404,6 +404,48 @@ __global__ __launch_bounds__(AGG_THREADS) void agg_dense_rows(AggDesc d, uint32_
 // encoding (kind / vid width) across its chunks (AggCol::ukind); the host falls back to agg_dense_rows otherwise.
 // Results are word-for-word those of agg_dense_rows (the same ADD / MIN / MAX / OR combination of the same values).
 // ------------------------------------------------------------------------------------------------------------
+// A float / double that is an integer of small magnitude (|v| <= 2^24, resp. 2^31): its int64 value. Such rows of a
+// float SUM are summed exactly in one int64 word (no overflow below 2^32 rows).
+__device__ __forceinline__ bool small_integer(uint64_t bits, int32_t type, int64_t* iv) {
+  if (type == HY_TYPE_FLOAT) {
+    float f;
+    const uint32_t b = static_cast<uint32_t>(bits);
+    __builtin_memcpy(&f, &b, 4);
+    if (!(fabsf(f) <= 16777216.0f) || f != truncf(f)) return false;
+    *iv = static_cast<int64_t>(f);
+    return true;
+  }
+  double x;
+  __builtin_memcpy(&x, &bits, 8);
+  if (!(fabs(x) <= 2147483648.0) || x != trunc(x)) return false;
+  *iv = static_cast<int64_t>(x);
+  return true;
+}
+
+// Adds the exact int64 word of every float SUM / AVG (integer-valued rows) into its limbs and clears it: value I has
+// weight 2^0 = 2^(32 i + o + emin) with i = (-emin) / 32, o = (-emin) % 32. One thread per (group, aggregate).
+__device__ __forceinline__ void span_fold_int_words(const AggDesc& d, uint32_t n_groups, unsigned long long* rec) {
+  for (uint32_t t = threadIdx.x; t < n_groups * d.n_fns; t += AGG_THREADS) {
+    const uint32_t gg = t / d.n_fns;
+    const AggFn fn = d.fns[t % d.n_fns];
+    if (fn.column < 0 || fn.limbs == 0) continue;
+    unsigned long long* r = rec + gg * d.words;
+    const int64_t I = static_cast<int64_t>(r[fn.word + 2 + fn.limbs]);
+    if (I == 0) continue;
+    r[fn.word + 2 + fn.limbs] = 0;
+    const int p = fn.limbs == FLOAT_LIMBS ? -FLOAT_EMIN : -DOUBLE_EMIN;
+    const unsigned __int128 u = static_cast<unsigned __int128>(I < 0 ? 0ull - static_cast<uint64_t>(I)
+                                                                        : static_cast<uint64_t>(I))
+                                << (p & 31);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int64_t piece = static_cast<int64_t>(static_cast<uint32_t>(u >> (32 * k)));
+      const int l = (p >> 5) + k;
+      if (piece && l < fn.limbs) r[fn.word + 2 + l] += static_cast<uint64_t>(I < 0 ? -piece : piece);
+    }
+  }
+}
+
 constexpr int SPAN_K = 4;  // rows per lane per step: a wave span is AGG_ITEMS / SPAN_K steps (register budget)
 
 // Loads the values of column col for the 16 rows of this lane; returns the non-NULL mask (bit k).
@@ -616,6 +658,26 @@ __global__ __launch_bounds__(AGG_THREADS) void agg_dense_span(AggDesc d, uint32_
           s = wave_sum64(s);
           if (lane == 0 && s) atomicAdd(rec + fn.word + 1, static_cast<unsigned long long>(s));
         } else {  // SUM / AVG of floats: exact limbs; each row's pieces are split once, then summed per limb
+          // integer-valued rows (TPC-H quantities, cents) skip the limbs: an exact int64 word, folded into the
+          // limbs when the workgroup flushes (span_fold_int_words); only the other rows are split into pieces
+          {
+            uint64_t isum = 0;
+            uint32_t frac = 0;
+#pragma unroll
+            for (int k = 0; k < SPAN_K; ++k) {
+              if ((inm >> k) & 1u) {
+                int64_t iv;
+                if (small_integer(b[k], type, &iv))
+                  isum += static_cast<uint64_t>(iv);
+                else
+                  frac |= 1u << k;
+              }
+            }
+            isum = wave_sum64(isum);
+            if (lane == 0 && isum) atomicAdd(rec + fn.word + 2 + fn.limbs, static_cast<unsigned long long>(isum));
+            if (__ballot(frac != 0) == 0ull) continue;
+            inm = frac;
+          }
           uint32_t special = 0;
           int lo = 0x7FFFFFFF, hi = -1;
           int i0s[SPAN_K];
@@ -657,6 +719,8 @@ __global__ __launch_bounds__(AGG_THREADS) void agg_dense_span(AggDesc d, uint32_
     }
     }  // steps of the span
   }
+  __syncthreads();
+  span_fold_int_words(d, n_groups, s_recd);
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < n_words; i += AGG_THREADS) {
     const int32_t op = d.word_op[i % words];

@@ -330,7 +330,8 @@ hy_status hy_dereference_row_ids(const hy_row_id* rows, uint64_t n, const hy_row
  *     SUM, AVG of integers:   non-NULL count, int64 sum (two's complement)
  *     SUM, AVG of floats:     non-NULL count, non-finite flags (1 +inf, 2 -inf, 4 NaN), then agg_limbs[a] signed
  *                             64-bit limbs; limb i has weight 2^(32 i + agg_emin[a]). hy_agg_float_sum rounds the
- *                             exact sum once to double.
+ *                             exact sum once to double. One more word follows the limbs (device scratch for
+ *                             integer-valued rows, always 0 in returned records).
  *     COUNT(*):               no words (use the rows word)
  * In dense mode (every group-by column arrives as integer codes with a domain, product of (domain + 1) <= 64) the
  * key words of a group are its codes.
