@@ -143,3 +143,39 @@ def test_empty_input(hy, oracle):
         aggs = [(1, "Max"), (2, "Sum"), (None, "Count"), (1, "CountDistinct")]
         out = run_device(hy, empty, aggs, gb)
         assert_identical(out, oracle.aggregate(empty, ac.agg_defs(hy, aggs), gb))
+
+
+@pytest.mark.parametrize("reference_input", [False, True])
+def test_dense_span_float_sums_mixed_integer_rows(hy, oracle, monkeypatch, reference_input):
+    """agg_dense_span sums integer-valued float rows in an int64 word and the others in limbs; the folded result must
+    be the exact sum rounded once (== math.fsum) and word-for-word the per-64-row kernel's (HY_AGG_DENSE_ROWS=1)."""
+    rng = np.random.default_rng(17)
+    n = 250_000
+    g = rng.integers(0, 4, n).astype(np.int32)
+    ints = rng.integers(-60, 61, n).astype(np.float32)
+    f = np.where(rng.random(n) < 0.7, ints, (rng.standard_normal(n) * 100).astype(np.float32)).astype(np.float32)
+    big = rng.integers(-(1 << 40), 1 << 40, n).astype(np.float64)  # integers above 2^31 take the limb path
+    d = np.where(rng.random(n) < 0.5, rng.integers(-1000, 1000, n).astype(np.float64), big)
+    d = np.where(rng.random(n) < 0.1, d + 0.25, d)
+    nulls = (rng.random(n) < 0.05).astype(np.uint8)
+    t = hy.Table.from_arrays([("g", hy.DataType.Int, False), ("f", hy.DataType.Float, True),
+                              ("d", hy.DataType.Double, False)], [g, f, d], [None, nulls, None], 60_000)
+    hy.encode_chunks(t, list(range(t.chunk_count())), hy.EncodingType.Dictionary)
+    src = oracle.table_scan(t, 0, hy.PredicateCondition.GreaterThanEquals, 0, []) if reference_input else t
+    aggs = [(1, "Sum"), (2, "Sum"), (1, "Avg"), (2, "Avg"), (None, "Count")]
+
+    def run():
+        op = hy.Aggregate(wrap(hy, src), ac.agg_defs(hy, aggs), [0])
+        op.execute()
+        assert op.used_dense_path()
+        return op.get_output()
+
+    out = run()
+    monkeypatch.setenv("HY_AGG_DENSE_ROWS", "1")
+    out_rows_kernel = run()
+    monkeypatch.delenv("HY_AGG_DENSE_ROWS")
+    assert_identical(out, out_rows_kernel)
+    for row in out.rows():
+        sel = g == row[0]
+        assert row[1] == math.fsum(f[sel & (nulls == 0)].astype(np.float64))
+        assert row[2] == math.fsum(d[sel])
