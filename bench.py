@@ -555,6 +555,18 @@ def main_q1(args):
     dom = max((k for k in kernels if k in alg), key=lambda k: kernels[k]["ms_total"])
     dk = kernels[dom]
     step_s = elapsed / K
+    roofline = {"bound": "hbm", "kernel": dom, "achieved": round(dk["achieved_GBps"], 1), "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": round(dk["achieved_GBps"] / HBM_PEAK_GBPS, 4), "traffic": None}
+    # HBM bytes per launch from the newest committed PMC summary of this workload (tools: rocprofv3 --pmc FETCH_SIZE /
+    # WRITE_SIZE passes of `bench.py --workload q1`, summarized by tools/summarize_rocprof.py)
+    if chunk == 100_000:
+        for f in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_rocprof_q1_sf{args.sf:g}_summary.json")))):
+            with open(f) as fh:
+                kk = json.load(fh).get("kernels", {}).get(dom if dom != "scan_value" else "scan_kernel", {})
+            if "hbm_bytes_per_launch" in kk:
+                roofline["traffic"] = round(kk["hbm_bytes_per_launch"])
+                roofline["traffic_source"] = os.path.relpath(f, ROOT)
+                break
     cpu = None if args.no_cpu_baseline else cpu_baseline_q1(hy, synth, args.cpu_sf / 10, chunk)
     line = {
         "metric": "rows/sec TableScan+Aggregate, TPC-H 1 on lineitem (BASELINE.json configs[3])",
@@ -566,8 +578,7 @@ def main_q1(args):
                    "sf": args.sf, "lineitem_rows": n, "chunk_size": chunk, "scan_matches": n_match,
                    "groups": n_groups, "parallelism": "single GPU"},
         "check": {"ok": bool(ok), "groups": groups},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(dk["achieved_GBps"], 1), "peak": HBM_PEAK_GBPS,
-                     "unit": "GB/s", "frac": round(dk["achieved_GBps"] / HBM_PEAK_GBPS, 4), "traffic": None},
+        "roofline": roofline,
         "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                     for k, v in kernels.items()},
         "cpu_baseline": cpu,
