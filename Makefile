@@ -29,7 +29,14 @@ $(LIB)/hyrise_amd_aggregate.o: $(CSRC)/capi/hyrise_amd_aggregate.hip $(CSRC)/ker
 	@mkdir -p $(LIB)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
-$(LIB)/libhyrise_amd.so: $(LIB)/hyrise_amd.o $(LIB)/hyrise_amd_aggregate.o
+JOIN_TUS   := join join_i32 join_i64 join_f32 join_f64
+JOIN_OBJS  := $(patsubst %,$(LIB)/hyrise_amd_%.o,$(JOIN_TUS))
+
+$(JOIN_OBJS): $(LIB)/hyrise_amd_%.o: $(CSRC)/capi/hyrise_amd_%.hip $(CSRC)/capi/join_host.hpp $(CSRC)/kernels/join.hip $(CAPI_HDR)
+	@mkdir -p $(LIB)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIB)/libhyrise_amd.so: $(LIB)/hyrise_amd.o $(LIB)/hyrise_amd_aggregate.o $(JOIN_OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 $(LIB)/libhyrise_host.so: $(HOST_SRC) $(HOST_HDR) $(LIB)/libhyrise_amd.so

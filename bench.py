@@ -35,7 +35,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--sf", type=float, default=100.0, help="TPC-H scale factor per GPU")
     p.add_argument("--chunk", type=int, default=100_000)
-    p.add_argument("--cpu-sf", type=float, default=20.0, help="scale factor of the bounded CPU-baseline sample")
+    p.add_argument("--cpu-sf", type=float, default=10.0, help="scale factor of the bounded CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (RCCL; one GPU per rank) or gloo (host-staged exchange: rehearsal of N ranks on one GPU)")
@@ -43,6 +43,10 @@ def parse():
                    help="join: the headline TableScan+JoinHash (BASELINE.json metric); q1: BASELINE config 4, "
                         "TableScan(l_shipdate) -> Aggregate of TPC-H 1 on one GPU")
     p.add_argument("--q1-aggs", default=None, help="debug: comma-separated subset of Q1_AGGS indexes (q1 workload)")
+    p.add_argument("--unfused", action="store_true",
+                   help="run TableScan and JoinHash as two C-ABI calls (hy_table_scan_row_ids, hy_join_hash) instead "
+                        "of the fused hy_scan_join_hash (A/B of the fusion; single GPU)")
+    p.add_argument("--probe-gb", type=float, default=4.0, help="buffer size of the measured HBM roofline probe")
     p.add_argument("--join-trace", default=None,
                    help="debug: after the timed region run one traced step and write per-partition join phase "
                         "durations (us) to this .npz (hy_debug_set_join_trace)")
@@ -222,7 +226,49 @@ def main():
         state["recv_rows"] = (int(bmat.sum()), int(pmat.sum()))
         return n_probe, out[4]
 
+    # ---------------- fused TableScan -> JoinHash (hy_scan_join_hash): the scan predicate runs inside the join's
+    # first radix pass over lineitem's chunks; the scan output (per-chunk offset lists) is written by the same pass ----
+    probe_chunks = (capi.JoinChunk * n_lchunks)()
+    for c in range(n_lchunks):
+        pc = probe_chunks[c]
+        pc.column = referenced[c]
+        pc.size = referenced[c].size
+        pc.chunk_id = l_base + c
+        pc.single_chunk = capi.HY_MIXED_CHUNKS
+    probe_data_side = capi.JoinSide(probe_chunks, n_lchunks, capi.HY_TYPE_INT32, None, 0, 0, 0)
+    scan_off = torch.empty(n_li + 64, dtype=torch.int32, device=dev)
+    scan_begin = torch.zeros(n_lchunks + 1, dtype=torch.int64, device=dev)
+    pfilter = capi.JoinFilter(scan_chunks, capi.HY_TYPE_FLOAT, None, scan_off.data_ptr(), scan_begin.data_ptr())
+
+    def run_fused():
+        if "fws" not in state:
+            wsb = ctypes.c_size_t(0)
+            capi.check(L.hy_scan_join_hash_workspace_size(ctypes.byref(build_side), None, ctypes.byref(probe_data_side),
+                                                          ctypes.byref(pfilter), ctypes.byref(params),
+                                                          ctypes.byref(wsb)), "fused ws")
+            state["fws"] = torch.empty(wsb.value, dtype=torch.uint8, device=dev)
+            state["fcap"] = n_li + 64  # pairs <= probe rows for the unique orders keys; HY_ERR_CAPACITY grows it
+            state["fout_b"] = torch.empty(2 * state["fcap"], dtype=torch.int32, device=dev)
+            state["fout_p"] = torch.empty(2 * state["fcap"], dtype=torch.int32, device=dev)
+        res = capi.JoinResult()
+        st = L.hy_scan_join_hash(ctypes.byref(build_side), None, ctypes.byref(probe_data_side), ctypes.byref(pfilter),
+                                 ctypes.byref(params), state["fout_b"].data_ptr(), state["fout_p"].data_ptr(),
+                                 state["fcap"], part_begin.data_ptr(), part_count.data_ptr(), ctypes.byref(res),
+                                 state["fws"].data_ptr(), state["fws"].numel(), stream)
+        if st == capi.HY_ERR_CAPACITY:
+            state["fcap"] = res.capacity_required + 64
+            state["fout_b"] = torch.empty(2 * state["fcap"], dtype=torch.int32, device=dev)
+            state["fout_p"] = torch.empty(2 * state["fcap"], dtype=torch.int32, device=dev)
+            return run_fused()
+        capi.check(st, "hy_scan_join_hash")
+        return res.total_pairs
+
+    fused = world == 1 and not args.unfused
+
     def step():
+        if fused:
+            pairs = run_fused()
+            return None, pairs  # scan matches are read once after the timed region (scan_begin[-1])
         run_scan()
         counts_h = scan_counts.cpu().numpy()  # D2H of per-chunk match counts (the output chunk layout)
         return run_join_distributed(counts_h) if xj else run_join(counts_h)
@@ -243,6 +289,8 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     L.hy_kernel_stats_enable(0)
+    if fused:
+        n_probe = int(scan_begin[-1].item())
     if args.join_trace and rank == 0 and world == 1:
         import numpy as np
         trace = torch.zeros(5 * (1 << radix_bits), dtype=torch.int64, device=dev)
@@ -278,41 +326,62 @@ def main():
         kernels[name.value.decode()] = {"launches": launches.value, "ms_total": total.value}
 
     K = args.steps
-    rows_per_step = n_li + n_ord
-    # algorithmic bytes per step for each kernel; 8-byte {key, payload} partition records
-    valid_build, valid_probe = n_ord, n_probe
+    # algorithmic bytes: scan 1 B/row read + 4 B/match written (chunk offsets; 8 B RowIDs on the
+    # unfused path); JoinHash 4 B/build row + 4 B/probe row read + 16 B/pair written. Partition passes are overhead:
+    # for them the table lists the bytes each kernel must move (records 8 B, digit bytes 1 B), not algorithmic bytes.
     recv_build, recv_probe = state.get("recv_rows", (n_ord, n_probe))  # rows this rank joins after the exchange
-    alg = {
-        "scan_dict": n_li * 1 + n_probe * 8,
-        "part1_hist.build": valid_build * 4,
-        "part1_hist.probe": valid_probe * (8 + 4),
-        "part1_scatter.build": valid_build * (4 + 8),
-        "part1_scatter.probe": valid_probe * (8 + 4 + 8),
-        "part2_hist.build": valid_build * 8,
-        "part2_hist.probe": valid_probe * 8,
-        "part2_scatter.build": valid_build * 16,
-        "part2_scatter.probe": valid_probe * 16,
-        "join_partition": (recv_build + recv_probe) * 8 + pairs * 16,
-    }
+    scan_out_b = 4 if fused else 8
+    e2e_bytes = n_li * 1 + n_probe * scan_out_b + n_ord * 4 + n_probe * 4 + int(pairs) * 16
+    if fused:
+        moved = {
+            "part1_hist.probe": n_li * 5,
+            "part1_scatter.probe": n_li * 5 + n_probe * (8 + 4 + 1),
+            "part2_hist.probe": n_probe * 1,
+            "part2_scatter.probe": n_probe * 16,
+        }
+    else:
+        moved = {
+            "scan_dict": n_li * 1 + n_probe * 8,
+            "part1_hist.probe": n_probe * (8 + 4),
+            "part1_scatter.probe": n_probe * (8 + 4 + 8),
+            "part2_hist.probe": n_probe * 8,
+            "part2_scatter.probe": n_probe * 16,
+        }
+    moved.update({
+        "part1_hist.build": n_ord * 4,
+        "part1_scatter.build": n_ord * (4 + 8 + 1),
+        "part2_hist.build": n_ord * (1 if fused else 8),
+        "part2_scatter.build": n_ord * 16,
+        # the join kernel's algorithmic bytes exactly as 8(d) counts JoinHash
+        "join_partition": recv_build * 4 + recv_probe * 4 + int(pairs) * 16,
+    })
     for k, v in kernels.items():
         per_launch_ms = v["ms_total"] / max(v["launches"], 1)
         v["ms_per_launch"] = per_launch_ms
-        if k in alg:
+        if k in moved:
             launches_per_step = v["launches"] / K
-            v["alg_bytes_per_launch"] = alg[k] / launches_per_step
-            v["achieved_GBps"] = v["alg_bytes_per_launch"] / (per_launch_ms * 1e-3) / 1e9
-    dom = max((k for k in kernels if k in alg), key=lambda k: kernels[k]["ms_total"])
+            v["bytes_per_launch"] = moved[k] / launches_per_step
+            v["achieved_GBps"] = v["bytes_per_launch"] / (per_launch_ms * 1e-3) / 1e9
+    step_s = elapsed / K
+    value = (g_li + g_ord) / step_s
+    peak, probe = measured_roofline(L, capi, torch, dev, stream, args.probe_gb)
+    dom = max((k for k in kernels if k in moved), key=lambda k: kernels[k]["ms_total"])
     dk = kernels[dom]
-    roofline = {"bound": "hbm", "kernel": dom, "achieved": round(dk["achieved_GBps"], 1), "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s", "frac": round(dk["achieved_GBps"] / HBM_PEAK_GBPS, 4), "traffic": None}
-    traffic, traffic_src = committed_traffic(dom, args.sf, chunk, world)
+    e2e_gbps = e2e_bytes / step_s / 1e9
+    # headline roofline: the whole step's algorithmic bytes over its time, against the HBM bandwidth measured in this
+    # run; the dominant kernel's own line follows (its rocprofv3 average is in profiles/)
+    roofline = {"bound": "hbm", "scope": "end-to-end step (TableScan + JoinHash, algorithmic bytes of SURVEY 8(d))",
+                "achieved": round(e2e_gbps, 1), "peak": round(peak, 1), "unit": "GB/s",
+                "frac": round(e2e_gbps / peak, 4), "alg_bytes_per_step": e2e_bytes, "traffic": None,
+                "peak_source": "measured in this run (hy_stream_bandwidth_probe, best of read / copy)",
+                "frac_of_spec_8000": round(e2e_gbps / HBM_PEAK_GBPS, 4)}
+    traffic, traffic_src = committed_traffic_step(args.sf, chunk, world, fused)
     if traffic is not None:
         roofline["traffic"] = round(traffic)
         roofline["traffic_source"] = traffic_src
-    step_s = elapsed / K
-    # end-to-end algorithmic bytes (§8(d)): scan 1 B/row + 8 B/match; join 4 B/build + 4 B/probe + 16 B/pair
-    e2e_bytes = n_li * 1 + n_probe * 8 + n_ord * 4 + n_probe * 4 + pairs * 16
-    value = (g_li + g_ord) / step_s
+    kernel_roofline = {"kernel": dom, "achieved": round(dk["achieved_GBps"], 1), "peak": round(peak, 1),
+                       "unit": "GB/s", "frac": round(dk["achieved_GBps"] / peak, 4),
+                       "ms_per_launch": round(dk["ms_per_launch"], 4), "bytes_per_launch": dk["bytes_per_launch"]}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -334,13 +403,14 @@ def main():
             "data": "synthetic (seeded counter-based TPC-H-shaped columns, resident in HBM)",
             "config": {"workload": f"TableScan(l_quantity<24, dictionary u8) -> JoinHash(orders ⋈ scan, "
                                    f"o_orderkey=l_orderkey, radix_bits={radix_bits})",
+                       "path": "fused hy_scan_join_hash" if fused else "hy_table_scan_row_ids + hy_join_hash",
                        "sf_per_gpu": args.sf, "lineitem_rows": g_li, "orders_rows": g_ord, "chunk_size": chunk,
                        "scan_matches": g_probe, "join_pairs": g_pairs,
                        "parallelism": f"chunk-sharded x{world}" + (f", RCCL all-to-all radix exchange"
                                                                     if world > 1 else "")},
             "roofline": roofline,
-            "end_to_end": {"alg_bytes_per_step": e2e_bytes, "GBps": round(e2e_bytes / step_s / 1e9, 1),
-                           "frac_of_peak": round(e2e_bytes / step_s / 1e9 / HBM_PEAK_GBPS, 4)},
+            "kernel_roofline": kernel_roofline,
+            "hbm_probe": probe,
             "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                         for k, v in kernels.items()},
             "cpu_baseline": cpu,
@@ -633,29 +703,101 @@ def committed_traffic(kernel, sf, chunk, world):
     return None, None
 
 
-def cpu_baseline(hy, synth, sf, chunk):
-    """The oracle (CPU restatement of the reference operators, single thread) on a bounded sample of the same
-    workload: TableScan(l_quantity < 24) on dictionary-encoded lineitem, then JoinHash(orders, scan output)."""
+def measured_roofline(L, capi, torch, dev, stream, gb):
+    """HBM bandwidth measured in this run with the library's streaming read and copy kernels (best of 5 each, 16-B
+    nontemporal accesses): the denominator of roofline.frac."""
+    n = int(gb * 1e9) // 16 * 16
+    src = torch.empty(n // 4, dtype=torch.int32, device=dev).fill_(1)
+    dst = torch.empty(n // 4, dtype=torch.int32, device=dev)
+    out = {}
+    for name, mode, traffic in (("read", capi.HY_PROBE_READ, n), ("copy", capi.HY_PROBE_COPY, 2 * n)):
+        best = 0.0
+        for _ in range(6):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            capi.check(L.hy_stream_bandwidth_probe(src.data_ptr(), dst.data_ptr(), n, mode, stream), "probe")
+            e1.record()
+            torch.cuda.synchronize()
+            best = max(best, traffic / (e0.elapsed_time(e1) * 1e-3) / 1e9)
+        out[name + "_GBps"] = round(best, 1)
+    del src, dst
+    out["bytes"] = n
+    return max(out["read_GBps"], out["copy_GBps"]), out
+
+
+def committed_traffic_step(sf, chunk, world, fused):
+    """HBM bytes per step (all kernels) from the newest committed PMC summary of this configuration
+    (profiles/rNN_rocprof_sf<SF>[_fused]_summary.json, tools/profile_bench.sh: FETCH_SIZE x2 + WRITE_SIZE per the
+    MI355X guide). None if no summary matches."""
+    if world != 1 or chunk != 100_000:
+        return None, None
+    here = os.path.dirname(os.path.abspath(__file__))
+    pat = f"r*_rocprof_sf{sf:g}_fused_summary.json" if fused else f"r*_rocprof_sf{sf:g}_summary.json"
+    for f in reversed(sorted(glob.glob(os.path.join(here, "profiles", pat)))):
+        with open(f) as fh:
+            d = json.load(fh)
+        if "hbm_bytes_per_step" in d:
+            return d["hbm_bytes_per_step"], os.path.relpath(f, here)
+    return None, None
+
+
+def host_cpu():
+    """(threads to use, CPU model): the CPUs this process may run on, capped by OMP_NUM_THREADS (the GPU box's share
+    of a larger machine)."""
+    n = len(os.sched_getaffinity(0))
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        n = min(n, int(os.environ["OMP_NUM_THREADS"]))
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return max(1, n), model
+
+
+def cpu_baseline(hy, synth, sf, chunk, runs=5):
+    """The oracle (CPU restatement of the reference operators with the reference's per-chunk / per-partition jobs)
+    on a bounded sample of the same workload: TableScan(l_quantity < 24) on dictionary-encoded lineitem, then
+    JoinHash(orders, scan output). Median of `runs` warm runs on all host cores of this process, and on 1 core at a
+    fifth of the sample."""
     import numpy as np
 
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import helpers
 
     oracle = helpers.load_oracle()
-    okey, lines = synth.orders_numpy(sf)
-    lkey, qty = synth.lineitem_numpy(okey, lines)
-    orders = hy.Table.from_arrays([("o_orderkey", hy.DataType.Int, False)], [okey], [], chunk)
-    lineitem = hy.Table.from_arrays([("l_orderkey", hy.DataType.Int, False), ("l_quantity", hy.DataType.Float, False)],
-                                    [lkey, qty.astype(np.float32)], [], chunk)
-    hy.encode_all_chunks(lineitem, hy.EncodingType.Dictionary)
-    t0 = time.perf_counter()
-    scan = oracle.table_scan(lineitem, 1, hy.PredicateCondition.LessThan, 24, [])
-    join, _bits = oracle.join_hash(orders, scan, hy.JoinMode.Inner, (0, 0))
-    dt = time.perf_counter() - t0
-    rows = lineitem.row_count() + orders.row_count()
-    return {"value": round(rows / dt, 1), "unit": "rows/s", "cores": 1, "kind": "port",
-            "sample": f"SF{sf}: {lineitem.row_count()} lineitem + {orders.row_count()} orders rows, "
-                      f"scan {scan.row_count()} matches, join {join.row_count()} pairs, {dt:.2f} s"}
+    threads, model = host_cpu()
+    out = {"unit": "rows/s", "kind": "port", "cpu_model": model, "nproc": os.cpu_count()}
+    for label, n_threads, sample_sf in (("all_cores", threads, sf), ("one_core", 1, sf / 5)):
+        okey, lines = synth.orders_numpy(sample_sf)
+        lkey, qty = synth.lineitem_numpy(okey, lines)
+        orders = hy.Table.from_arrays([("o_orderkey", hy.DataType.Int, False)], [okey], [], chunk)
+        lineitem = hy.Table.from_arrays([("l_orderkey", hy.DataType.Int, False),
+                                         ("l_quantity", hy.DataType.Float, False)],
+                                        [lkey, qty.astype(np.float32)], [], chunk)
+        hy.encode_all_chunks(lineitem, hy.EncodingType.Dictionary)
+        oracle.set_threads(n_threads)
+        times = []
+        for _ in range(runs + 1):  # the first run warms caches and allocators
+            t0 = time.perf_counter()
+            scan = oracle.table_scan(lineitem, 1, hy.PredicateCondition.LessThan, 24, [])
+            join, _bits = oracle.join_hash(orders, scan, hy.JoinMode.Inner, (0, 0))
+            times.append(time.perf_counter() - t0)
+        oracle.set_threads(1)
+        med = sorted(times[1:])[len(times[1:]) // 2]
+        rows = lineitem.row_count() + orders.row_count()
+        out[label] = {"value": round(rows / med, 1), "cores": n_threads, "median_s": round(med, 3),
+                      "runs_s": [round(t, 3) for t in times[1:]],
+                      "sample": f"SF{sample_sf:g}: {lineitem.row_count()} lineitem + {orders.row_count()} orders "
+                                f"rows, scan {scan.row_count()} matches, join {join.row_count()} pairs"}
+        del orders, lineitem, scan, join
+    out["value"], out["cores"] = out["all_cores"]["value"], out["all_cores"]["cores"]
+    out["sample"] = out["all_cores"]["sample"] + f"; median of {runs}"
+    return out
 
 
 if __name__ == "__main__":

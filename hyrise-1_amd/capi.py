@@ -22,6 +22,7 @@ HY_OP_EQ, HY_OP_NE, HY_OP_LT, HY_OP_LE, HY_OP_GT, HY_OP_GE, HY_OP_ALL, HY_OP_NON
 HY_JOIN_INNER, HY_JOIN_LEFT, HY_JOIN_RIGHT, HY_JOIN_SEMI, HY_JOIN_ANTI = 0, 1, 2, 5, 6
 HY_AGG_MIN, HY_AGG_MAX, HY_AGG_SUM, HY_AGG_AVG, HY_AGG_COUNT, HY_AGG_COUNT_DISTINCT = range(6)
 HY_AGG_MAX_AGGREGATES = 16
+HY_PROBE_READ, HY_PROBE_COPY = 0, 1
 
 
 class RowID(ctypes.Structure):
@@ -51,6 +52,11 @@ class JoinSide(ctypes.Structure):
     _fields_ = [("chunks", ctypes.POINTER(JoinChunk)), ("n_chunks", ctypes.c_uint32), ("value_type", ctypes.c_int32),
                 ("referenced", ctypes.POINTER(ColumnChunk)), ("n_referenced", ctypes.c_uint32),
                 ("fuse_dereference", ctypes.c_int32), ("referenced_chunk_base", ctypes.c_uint32)]
+
+
+class JoinFilter(ctypes.Structure):
+    _fields_ = [("chunks", ctypes.POINTER(ScanChunk)), ("value_type", ctypes.c_int32), ("constant", ctypes.c_void_p),
+                ("out_offsets", ctypes.c_void_p), ("out_chunk_begin", ctypes.c_void_p)]
 
 
 class JoinParams(ctypes.Structure):
@@ -113,6 +119,16 @@ _sigs = {
                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                     ctypes.c_void_p, ctypes.POINTER(JoinResult), ctypes.c_void_p, ctypes.c_size_t,
                                     ctypes.c_void_p]),
+    "hy_scan_join_hash_workspace_size": (ctypes.c_int, [ctypes.POINTER(JoinSide), ctypes.POINTER(JoinFilter),
+                                                        ctypes.POINTER(JoinSide), ctypes.POINTER(JoinFilter),
+                                                        ctypes.POINTER(JoinParams), ctypes.POINTER(ctypes.c_size_t)]),
+    "hy_scan_join_hash": (ctypes.c_int, [ctypes.POINTER(JoinSide), ctypes.POINTER(JoinFilter), ctypes.POINTER(JoinSide),
+                                         ctypes.POINTER(JoinFilter), ctypes.POINTER(JoinParams), ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.POINTER(JoinResult), ctypes.c_void_p, ctypes.c_size_t,
+                                         ctypes.c_void_p]),
+    "hy_stream_bandwidth_probe": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int32,
+                                                 ctypes.c_void_p]),
     "hy_expand_row_ids": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                          ctypes.c_void_p]),
     "hy_aggregate_layout": (ctypes.c_int, [ctypes.POINTER(AggInput), ctypes.POINTER(AggParams),

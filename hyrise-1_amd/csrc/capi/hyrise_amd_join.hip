@@ -1,0 +1,234 @@
+// C entry points of JoinHash (include/hyrise_amd.h): argument checks and the dispatch on the hashed type to the
+// per-type translation units (hyrise_amd_join_*.hip, join_host.hpp).
+#include "join_host.hpp"
+
+using namespace hyc;
+using namespace hyj;
+
+namespace {
+
+hy_status prepare(const hy_join_side* build, const hy_join_filter* build_filter, const hy_join_side* probe,
+                  const hy_join_filter* probe_filter, const hy_join_params* params, SidePlan& bp, SidePlan& pp) {
+  if (!params) return fail(HY_ERR_INVALID_ARGUMENT, "params");
+  if (params->radix_bits > 24) return fail(HY_ERR_UNSUPPORTED, "radix_bits > 24");
+  if (!(params->mode == HY_JOIN_INNER || params->mode == HY_JOIN_LEFT || params->mode == HY_JOIN_RIGHT ||
+        params->mode == HY_JOIN_SEMI || params->mode == HY_JOIN_ANTI))
+    return fail(HY_ERR_UNSUPPORTED, "join mode");
+  hy_status st = plan_side(build, bp);
+  if (st != HY_OK) return st;
+  st = plan_side(probe, pp);
+  if (st != HY_OK) return st;
+  st = plan_filter(build_filter, bp, build->value_type, params->hashed_type);
+  if (st != HY_OK) return st;
+  st = plan_filter(probe_filter, pp, probe->value_type, params->hashed_type);
+  if (st != HY_OK) return st;
+  // fuse the dereference when the side is a reference table (one PosList per chunk shared by the join column)
+  bp.fuse = (!bp.referenced.empty() && build->fuse_dereference) ? 1 : 0;
+  pp.fuse = (!pp.referenced.empty() && probe->fuse_dereference) ? 1 : 0;
+  if (!type_bytes(build->value_type) || !type_bytes(probe->value_type) || !type_bytes(params->hashed_type))
+    return fail(HY_ERR_UNSUPPORTED, "join column type");
+  return HY_OK;
+}
+
+size_t join_bytes_any(int32_t hashed, const SidePlan& bp, const SidePlan& pp, uint32_t bits) {
+  switch (hashed) {
+    case HY_TYPE_INT32:
+      return join_bytes_i32(bp, pp, bits);
+    case HY_TYPE_INT64:
+      return join_bytes_i64(bp, pp, bits);
+    case HY_TYPE_FLOAT:
+      return join_bytes_f32(bp, pp, bits);
+    default:
+      return join_bytes_f64(bp, pp, bits);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+hy_status hy_scan_join_hash_workspace_size(const hy_join_side* build, const hy_join_filter* build_filter,
+                                           const hy_join_side* probe, const hy_join_filter* probe_filter,
+                                           const hy_join_params* params, size_t* bytes) {
+  if (!bytes) return fail(HY_ERR_INVALID_ARGUMENT, "bytes");
+  SidePlan bp, pp;
+  hy_status st = prepare(build, build_filter, probe, probe_filter, params, bp, pp);
+  if (st != HY_OK) return st;
+  *bytes = join_bytes_any(params->hashed_type, bp, pp, params->radix_bits);
+  return HY_OK;
+}
+
+hy_status hy_scan_join_hash(const hy_join_side* build, const hy_join_filter* build_filter, const hy_join_side* probe,
+                            const hy_join_filter* probe_filter, const hy_join_params* params, hy_row_id* out_build,
+                            hy_row_id* out_probe, uint64_t out_capacity, uint64_t* partition_begin,
+                            uint32_t* partition_counts, hy_join_result* result, void* workspace,
+                            size_t workspace_bytes, hy_stream_t stream) {
+  SidePlan bp, pp;
+  hy_status st = prepare(build, build_filter, probe, probe_filter, params, bp, pp);
+  if (st != HY_OK) return st;
+  if (!partition_begin || !partition_counts) return fail(HY_ERR_INVALID_ARGUMENT, "partition arrays");
+  hipStream_t s = S(stream);
+  switch (params->hashed_type) {
+    case HY_TYPE_INT32:
+      return join_i32(bp, pp, build->value_type, probe->value_type, params, out_build, out_probe, out_capacity,
+                      partition_begin, partition_counts, result, workspace, workspace_bytes, s);
+    case HY_TYPE_INT64:
+      return join_i64(bp, pp, build->value_type, probe->value_type, params, out_build, out_probe, out_capacity,
+                      partition_begin, partition_counts, result, workspace, workspace_bytes, s);
+    case HY_TYPE_FLOAT:
+      return join_f32(bp, pp, build->value_type, probe->value_type, params, out_build, out_probe, out_capacity,
+                      partition_begin, partition_counts, result, workspace, workspace_bytes, s);
+    default:
+      return join_f64(bp, pp, build->value_type, probe->value_type, params, out_build, out_probe, out_capacity,
+                      partition_begin, partition_counts, result, workspace, workspace_bytes, s);
+  }
+}
+
+hy_status hy_join_hash_workspace_size(const hy_join_side* build, const hy_join_side* probe,
+                                      const hy_join_params* params, size_t* bytes) {
+  return hy_scan_join_hash_workspace_size(build, nullptr, probe, nullptr, params, bytes);
+}
+
+hy_status hy_join_hash(const hy_join_side* build, const hy_join_side* probe, const hy_join_params* params,
+                       hy_row_id* out_build, hy_row_id* out_probe, uint64_t out_capacity, uint64_t* partition_begin,
+                       uint32_t* partition_counts, hy_join_result* result, void* workspace, size_t workspace_bytes,
+                       hy_stream_t stream) {
+  return hy_scan_join_hash(build, nullptr, probe, nullptr, params, out_build, out_probe, out_capacity,
+                           partition_begin, partition_counts, result, workspace, workspace_bytes, stream);
+}
+
+hy_status hy_join_exchange_partition_workspace_size(const hy_join_side* side, const hy_join_params* params,
+                                                    uint32_t n_ranks, size_t* bytes) {
+  if (!bytes || !params || n_ranks == 0) return fail(HY_ERR_INVALID_ARGUMENT, "null argument");
+  SidePlan p;
+  hy_status st = plan_side(side, p);
+  if (st != HY_OK) return st;
+  const auto w = digit_plan(params->radix_bits, ceil_log2(n_ranks));
+  if (w.empty() || (1u << w[0]) < n_ranks) return fail(HY_ERR_UNSUPPORTED, "radix bits too few for the ranks");
+  switch (params->hashed_type) {
+    case HY_TYPE_INT32:
+      *bytes = exchange_partition_bytes_i32(p, params->radix_bits, w);
+      break;
+    case HY_TYPE_INT64:
+      *bytes = exchange_partition_bytes_i64(p, params->radix_bits, w);
+      break;
+    case HY_TYPE_FLOAT:
+      *bytes = exchange_partition_bytes_f32(p, params->radix_bits, w);
+      break;
+    case HY_TYPE_DOUBLE:
+      *bytes = exchange_partition_bytes_f64(p, params->radix_bits, w);
+      break;
+    default:
+      return fail(HY_ERR_UNSUPPORTED, "hashed type");
+  }
+  return HY_OK;
+}
+
+hy_status hy_join_exchange_partition(const hy_join_side* side, const hy_join_params* params, int32_t keep_nulls,
+                                     uint32_t n_ranks, void* out_records, uint64_t* bucket_counts, void* workspace,
+                                     size_t workspace_bytes, hy_stream_t stream) {
+  if (!params || !bucket_counts || n_ranks == 0) return fail(HY_ERR_INVALID_ARGUMENT, "null argument");
+  if (params->radix_bits > 24) return fail(HY_ERR_UNSUPPORTED, "radix_bits > 24");
+  SidePlan p;
+  hy_status st = plan_side(side, p);
+  if (st != HY_OK) return st;
+  p.fuse = (!p.referenced.empty() && side->fuse_dereference) ? 1 : 0;
+  const auto w = digit_plan(params->radix_bits, ceil_log2(n_ranks));
+  if (w.empty() || (1u << w[0]) < n_ranks) return fail(HY_ERR_UNSUPPORTED, "radix bits too few for the ranks");
+  if (p.n_rows && !out_records) return fail(HY_ERR_INVALID_ARGUMENT, "out_records");
+  hipStream_t s = S(stream);
+  switch (params->hashed_type) {
+    case HY_TYPE_INT32:
+      return exchange_partition_i32(p, side->value_type, params, keep_nulls, w, out_records, bucket_counts, workspace,
+                                    workspace_bytes, s);
+    case HY_TYPE_INT64:
+      return exchange_partition_i64(p, side->value_type, params, keep_nulls, w, out_records, bucket_counts, workspace,
+                                    workspace_bytes, s);
+    case HY_TYPE_FLOAT:
+      return exchange_partition_f32(p, side->value_type, params, keep_nulls, w, out_records, bucket_counts, workspace,
+                                    workspace_bytes, s);
+    case HY_TYPE_DOUBLE:
+      return exchange_partition_f64(p, side->value_type, params, keep_nulls, w, out_records, bucket_counts, workspace,
+                                    workspace_bytes, s);
+  }
+  return fail(HY_ERR_UNSUPPORTED, "hashed type");
+}
+
+hy_status hy_join_exchange_join_workspace_size(const uint64_t* build_counts, const uint64_t* probe_counts,
+                                               uint32_t n_senders, uint32_t n_buckets, const hy_join_params* params,
+                                               size_t* bytes) {
+  if (!bytes || !params || !build_counts || !probe_counts || n_senders == 0)
+    return fail(HY_ERR_INVALID_ARGUMENT, "null argument");
+  const uint32_t bits = params->radix_bits;
+  const auto w = digit_plan(bits, ceil_log2(n_senders));
+  if (w.empty()) return fail(HY_ERR_UNSUPPORTED, "radix_bits 0");
+  const uint32_t digits = 1u << (w.size() > 1 ? w[1] : 0);
+  const RecvPlan rb = recv_plan(build_counts, n_senders, n_buckets, digits);
+  const RecvPlan rp = recv_plan(probe_counts, n_senders, n_buckets, digits);
+  switch (params->hashed_type) {
+    case HY_TYPE_INT32:
+      *bytes = exchange_join_bytes_i32(rb, rp, bits, w, n_buckets, n_senders);
+      break;
+    case HY_TYPE_INT64:
+      *bytes = exchange_join_bytes_i64(rb, rp, bits, w, n_buckets, n_senders);
+      break;
+    case HY_TYPE_FLOAT:
+      *bytes = exchange_join_bytes_f32(rb, rp, bits, w, n_buckets, n_senders);
+      break;
+    case HY_TYPE_DOUBLE:
+      *bytes = exchange_join_bytes_f64(rb, rp, bits, w, n_buckets, n_senders);
+      break;
+    default:
+      return fail(HY_ERR_UNSUPPORTED, "hashed type");
+  }
+  return HY_OK;
+}
+
+hy_status hy_join_exchange_join(const void* build_records, const uint64_t* build_counts, const void* probe_records,
+                                const uint64_t* probe_counts, uint32_t n_senders, uint32_t first_bucket,
+                                uint32_t n_buckets, const hy_join_params* params, hy_row_id* out_build,
+                                hy_row_id* out_probe, uint64_t out_capacity, uint64_t* partition_begin,
+                                uint32_t* partition_counts, hy_join_result* result, void* workspace,
+                                size_t workspace_bytes, hy_stream_t stream) {
+  if (!params || !build_counts || !probe_counts || n_senders == 0 || !partition_begin || !partition_counts)
+    return fail(HY_ERR_INVALID_ARGUMENT, "null argument");
+  if (params->radix_bits > 24) return fail(HY_ERR_UNSUPPORTED, "radix_bits > 24");
+  if (!(params->mode == HY_JOIN_INNER || params->mode == HY_JOIN_LEFT || params->mode == HY_JOIN_RIGHT ||
+        params->mode == HY_JOIN_SEMI || params->mode == HY_JOIN_ANTI))
+    return fail(HY_ERR_UNSUPPORTED, "join mode");
+  const uint32_t bits = params->radix_bits;
+  const auto w = digit_plan(bits, ceil_log2(n_senders));
+  if (w.empty() || first_bucket + n_buckets > (1u << w[0])) return fail(HY_ERR_INVALID_ARGUMENT, "bucket range");
+  const uint32_t digits = 1u << (w.size() > 1 ? w[1] : 0);
+  const RecvPlan rbp = recv_plan(build_counts, n_senders, n_buckets, digits);
+  const RecvPlan rpp = recv_plan(probe_counts, n_senders, n_buckets, digits);
+  if (rbp.rows >= 0xFFFFFFFFull || rpp.rows >= 0xFFFFFFFFull)
+    return fail(HY_ERR_UNSUPPORTED, "received side exceeds 2^32-1 rows");
+  hipStream_t s = S(stream);
+  switch (params->hashed_type) {
+    case HY_TYPE_INT32:
+      return exchange_join_i32(build_records, probe_records, rbp, rpp, n_senders, n_buckets, w, params, out_build,
+                               out_probe, out_capacity, partition_begin, partition_counts, result, workspace,
+                               workspace_bytes, s);
+    case HY_TYPE_INT64:
+      return exchange_join_i64(build_records, probe_records, rbp, rpp, n_senders, n_buckets, w, params, out_build,
+                               out_probe, out_capacity, partition_begin, partition_counts, result, workspace,
+                               workspace_bytes, s);
+    case HY_TYPE_FLOAT:
+      return exchange_join_f32(build_records, probe_records, rbp, rpp, n_senders, n_buckets, w, params, out_build,
+                               out_probe, out_capacity, partition_begin, partition_counts, result, workspace,
+                               workspace_bytes, s);
+    case HY_TYPE_DOUBLE:
+      return exchange_join_f64(build_records, probe_records, rbp, rpp, n_senders, n_buckets, w, params, out_build,
+                               out_probe, out_capacity, partition_begin, partition_counts, result, workspace,
+                               workspace_bytes, s);
+  }
+  return fail(HY_ERR_UNSUPPORTED, "hashed type");
+}
+
+uint32_t hy_join_exchange_bucket_bits(uint32_t radix_bits, uint32_t n_ranks) {
+  const auto w = digit_plan(radix_bits, ceil_log2(std::max<uint32_t>(1, n_ranks)));
+  return w.empty() ? 0u : w[0];
+}
+
+}  // extern "C"

@@ -1,0 +1,1070 @@
+// Host orchestration of the JoinHash kernels (kernels/join.hip): side plans, workspace carving, the radix passes and
+// the per-partition LDS build/probe launch. Shared by the per-hashed-type translation units (hyrise_amd_join_*.hip),
+// which instantiate it for one hashed type each so that `make -j` compiles them in parallel; the C entry points
+// (hyrise_amd_join.hip) dispatch on the hashed type.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "hyrise_amd.h"
+#include "../kernels/common.hpp"
+#include "../kernels/join.hip"
+#include "capi_common.hpp"
+
+namespace hyj {
+
+using namespace hyc;
+
+// Tiles per span of the pass from column chunks (sub1) and of the record passes (sub2); HY_PART_SUB1 / HY_PART_SUB2
+// override them (tuning). Read once: workspace sizes and launches must agree.
+inline uint32_t sub_from_env(const char* name, uint32_t dflt) {
+  const char* e = std::getenv(name);
+  const long v = e ? std::strtol(e, nullptr, 10) : 0;
+  return v >= 1 && v <= hyk::PART_SUB_MAX ? static_cast<uint32_t>(v) : dflt;
+}
+inline uint32_t sub1() {
+  static const uint32_t v = sub_from_env("HY_PART_SUB1", 1);
+  return v;
+}
+// Spans of a side with a fused TableScan: two tiles, so that part1_spread's spans hold about as many matches as
+// a record pass's tile (measured on MI355X at SF100: 1.70 ms for part1_spread vs 2.52 ms with one-tile spans);
+// HY_PART_SUB_FILTERED overrides it.
+inline uint32_t sub_filtered() {
+  static const uint32_t v = sub_from_env("HY_PART_SUB_FILTERED", 2);
+  return v;
+}
+inline uint32_t sub2() {
+  static const uint32_t v = sub_from_env("HY_PART_SUB2", 1);
+  return v;
+}
+inline uint64_t span1() { return uint64_t(sub1()) * hyk::PART_TILE; }
+inline uint64_t span2() { return uint64_t(sub2()) * hyk::PART_TILE; }
+
+struct SidePlan {
+  uint64_t n_rows = 0;
+  uint64_t n_tiles1 = 0;
+  uint32_t sub = 1;                      // tiles per pass-0 span
+  std::vector<hyk::SrcChunk> chunks;
+  std::vector<uint64_t> tile_begin;
+  std::vector<uint64_t> row_begin;       // this table
+  std::vector<hyk::SrcChunk> referenced;
+  std::vector<uint64_t> ref_row_begin;   // referenced table
+  int32_t fuse = 0;
+  uint32_t ref_base = 0;                 // referenced_chunk_base of the side
+  // fused TableScan (hy_join_filter): predicate chunk per side chunk
+  bool filtered = false;
+  std::vector<hy_scan_chunk> filter;
+  int32_t filter_type = 0;
+  uint64_t filter_const = 0;
+  uint32_t* scan_out = nullptr;
+  uint64_t* scan_chunk_begin = nullptr;
+};
+
+inline uint32_t uniform_of(const std::vector<uint64_t>& row_begin) {
+  const size_t n = row_begin.size() - 1;
+  if (n == 0) return 0;
+  if (n == 1) return static_cast<uint32_t>(std::max<uint64_t>(row_begin[1], 1));
+  const uint64_t u = row_begin[1] - row_begin[0];
+  if (u == 0) return 0;
+  for (size_t i = 1; i + 1 < n; ++i)
+    if (row_begin[i + 1] - row_begin[i] != u) return 0;
+  if (row_begin[n] - row_begin[n - 1] > u) return 0;
+  return static_cast<uint32_t>(u);
+}
+
+inline hyk::SrcChunk src_from(const hy_column_chunk& c, const hy_row_id* pos_list, uint32_t size, uint64_t row_begin,
+                              uint32_t single_chunk = HY_MIXED_CHUNKS) {
+  hyk::SrcChunk s{};
+  s.single_chunk = single_chunk;
+  s.data = c.data;
+  s.nulls = c.nulls;
+  s.dictionary = c.dictionary;
+  s.pos_list = pos_list;
+  s.size = size;
+  s.dictionary_size = c.dictionary_size;
+  s.kind = c.kind;
+  s.vid_width = c.vid_width;
+  s.row_begin = row_begin;
+  return s;
+}
+
+inline int type_bytes(int32_t t) {
+  return (t == HY_TYPE_INT32 || t == HY_TYPE_FLOAT) ? 4 : (t == HY_TYPE_INT64 || t == HY_TYPE_DOUBLE) ? 8 : 0;
+}
+
+// Pass-0 spans of the side's chunks (a span never crosses a chunk).
+inline void plan_spans(SidePlan& p, uint32_t sub) {
+  p.sub = sub;
+  const uint64_t span = uint64_t(sub) * hyk::PART_TILE;
+  uint64_t tiles = 0;
+  for (size_t i = 0; i < p.chunks.size(); ++i) {
+    p.tile_begin[i] = tiles;
+    tiles += (uint64_t(p.chunks[i].size) + span - 1) / span;
+  }
+  p.tile_begin[p.chunks.size()] = tiles;
+  p.n_tiles1 = tiles;
+}
+
+inline hy_status plan_side(const hy_join_side* side, SidePlan& p) {
+  if (!side || (side->n_chunks && !side->chunks)) return fail(HY_ERR_INVALID_ARGUMENT, "join side");
+  p.ref_base = side->referenced_chunk_base;
+  p.chunks.resize(side->n_chunks);
+  p.tile_begin.resize(side->n_chunks + 1);
+  p.row_begin.resize(side->n_chunks + 1);
+  bool is_ref = false;
+  uint64_t rows = 0;
+  for (uint32_t i = 0; i < side->n_chunks; ++i) {
+    const hy_join_chunk& c = side->chunks[i];
+    if (c.pos_list) is_ref = true;
+    p.chunks[i] = src_from(c.column, c.pos_list, c.size, rows, c.single_chunk);
+    p.chunks[i].chunk_id = c.chunk_id;
+    p.row_begin[i] = rows;
+    rows += c.size;
+  }
+  p.row_begin[side->n_chunks] = rows;
+  p.n_rows = rows;
+  plan_spans(p, sub1());
+  if (rows >= 0xFFFFFFFFull) return fail(HY_ERR_UNSUPPORTED, "join side exceeds 2^32-1 rows");
+  if (is_ref) {
+    p.referenced.resize(side->n_referenced);
+    p.ref_row_begin.resize(side->n_referenced + 1);
+    uint64_t rr = 0;
+    for (uint32_t i = 0; i < side->n_referenced; ++i) {
+      p.referenced[i] = src_from(side->referenced[i], nullptr, side->referenced[i].size, rr);
+      p.ref_row_begin[i] = rr;
+      rr += side->referenced[i].size;
+    }
+    p.ref_row_begin[side->n_referenced] = rr;
+    for (const auto& c : p.chunks)
+      if (c.pos_list && c.single_chunk != HY_MIXED_CHUNKS && c.single_chunk >= side->n_referenced)
+        return fail(HY_ERR_INVALID_ARGUMENT, "single_chunk outside the referenced chunks");
+    if (rr >= 0xFFFFFFFFull) return fail(HY_ERR_UNSUPPORTED, "referenced table exceeds 2^32-1 rows");
+  }
+  return HY_OK;
+}
+
+// Attaches a fused TableScan predicate to a data-table side.
+inline hy_status plan_filter(const hy_join_filter* f, SidePlan& p, int32_t column_type, int32_t hashed_type) {
+  if (f == nullptr) return HY_OK;
+  if (column_type != hashed_type)
+    return fail(HY_ERR_UNSUPPORTED, "a fused scan needs the side's join column to have the hashed type");
+  if (p.chunks.size() && !f->chunks) return fail(HY_ERR_INVALID_ARGUMENT, "filter chunks");
+  if (p.n_rows >= 0x7FFFFFFFull) return fail(HY_ERR_UNSUPPORTED, "filtered join side exceeds 2^31-1 rows");
+  p.filtered = true;
+  p.filter.assign(f->chunks, f->chunks + p.chunks.size());
+  p.filter_type = f->value_type;
+  p.scan_out = f->out_offsets;
+  p.scan_chunk_begin = f->out_chunk_begin;
+  bool value = false;
+  for (size_t i = 0; i < p.chunks.size(); ++i) {
+    if (p.chunks[i].pos_list) return fail(HY_ERR_UNSUPPORTED, "a filtered join side must be a data table");
+    const hy_scan_chunk& sc = p.filter[i];
+    if (sc.column.size != p.chunks[i].size) return fail(HY_ERR_INVALID_ARGUMENT, "filter chunk size != join chunk size");
+    if (sc.column.size && !aligned16(sc.column.data)) return fail(HY_ERR_ALIGNMENT, "filter data not 16-byte aligned");
+    if (sc.column.kind == HY_COL_DICT) {
+      if (sc.column.vid_width != 1 && sc.column.vid_width != 2 && sc.column.vid_width != 4)
+        return fail(HY_ERR_INVALID_ARGUMENT, "filter vid width");
+    } else if (sc.op != HY_OP_NONE) {
+      value = true;
+    }
+  }
+  plan_spans(p, sub_filtered());
+  if (value) {
+    const int tb = type_bytes(f->value_type);
+    if (!tb) return fail(HY_ERR_UNSUPPORTED, "filter value type");
+    if (!f->constant) return fail(HY_ERR_INVALID_ARGUMENT, "filter constant");
+    std::memcpy(&p.filter_const, f->constant, tb);
+  }
+  return HY_OK;
+}
+
+// Radix digits from the most significant: the partition id has `bits` bits; the first digit may be narrower than 8 so
+// that the others are 8 bits wide; min_top forces the first digit to be at least that wide (the distributed join
+// assigns whole first-digit buckets to ranks).
+inline std::vector<uint32_t> digit_plan(uint32_t bits, uint32_t min_top) {
+  std::vector<uint32_t> w;
+  if (bits == 0) return w;
+  uint32_t top = bits - 8 * ((bits - 1) / 8);
+  if (top < min_top) top = std::min(min_top, bits);
+  w.push_back(top);
+  uint32_t rest = bits - top;
+  if (rest) {
+    const uint32_t q = (rest + 7) / 8;
+    w.push_back(rest - 8 * (q - 1));
+    for (uint32_t i = 1; i < q; ++i) w.push_back(8);
+  }
+  return w;
+}
+
+// Device pointers of one side inside the workspace.
+template <typename H, typename P = uint32_t>
+struct SideBufs {
+  hyk::SrcChunk* chunks;
+  uint64_t* tile_begin;
+  uint64_t* row_begin;
+  hyk::SrcChunk* referenced;
+  uint64_t* ref_row_begin;
+  hy_scan_chunk* filter;     // fused TableScan predicate chunks (filtered sides)
+  uint32_t* hist;            // histogram of the current pass (largest pass)
+  uint32_t* off;             // its exclusive scan
+  hyk::Rec<H, P>* recA;
+  hyk::Rec<H, P>* recB;      // filtered sides: first the gapped per-span records of part1_compact
+  uint32_t* span_count;      // filtered sides: matches per pass-0 span
+  uint8_t* digA;             // next-pass digit bytes beside recA / recB (sides with more than one pass)
+  uint8_t* digB;
+  uint32_t* segA;            // segment / partition bounds, ping-pong (2^bits + 1 entries)
+  uint32_t* segB;
+  uint64_t* seg_tile_begin;  // 2^bits + 1
+  uint32_t* tile_counts;     // 2^bits
+  uint32_t* tile_excl;       // 2^bits
+  uint32_t* tile_owner;      // largest pass's tiles
+  uint64_t* total;           // rows taking part (device)
+  uint64_t* grand_total;     // total of a fused-scan histogram (records + scan matches)
+};
+
+struct SideSizes {
+  uint64_t rows = 0, tiles1 = 0;   // pass-0 spans (0: the side starts from received records)
+  uint32_t sub = 1;                // tiles per pass-0 span
+  size_t n_chunks = 0, n_referenced = 0;
+  bool filtered = false;           // one more histogram row in pass 0 (the scan's matches)
+  bool digit_bytes = false;        // next-digit byte arrays (single-GPU sides with more than one pass)
+};
+
+// Largest histogram of any pass, and the largest tile count of any record pass.
+inline void pass_sizes(const SideSizes& z, const std::vector<uint32_t>& w, uint64_t first_segs, uint64_t* hist_words,
+                       uint64_t* max_tiles) {
+  *hist_words = 1;
+  *max_tiles = 1;
+  uint64_t segs = first_segs;
+  for (size_t i = 0; i < w.size(); ++i) {
+    const uint64_t digits = 1ull << w[i];
+    if (i == 0 && z.tiles1) {
+      *hist_words = std::max(*hist_words, (digits + (z.filtered ? 1 : 0)) * z.tiles1);
+      *max_tiles = std::max(*max_tiles, z.tiles1);
+    } else {
+      const uint64_t t = (z.rows + span2() - 1) / span2() + segs;
+      *hist_words = std::max(*hist_words, digits * t);
+      *max_tiles = std::max(*max_tiles, t);
+      segs *= digits;
+      continue;
+    }
+    segs = digits;
+  }
+}
+
+template <typename H, typename P>
+void carve_side(Carver& cv, const SideSizes& z, uint32_t bits, const std::vector<uint32_t>& w, uint64_t first_segs,
+                bool own_recA, SideBufs<H, P>& b) {
+  b.chunks = cv.take<hyk::SrcChunk>(std::max<size_t>(1, z.n_chunks));
+  b.tile_begin = cv.take<uint64_t>(z.n_chunks + 1);
+  b.row_begin = cv.take<uint64_t>(z.n_chunks + 1);
+  b.referenced = cv.take<hyk::SrcChunk>(std::max<size_t>(1, z.n_referenced));
+  b.ref_row_begin = cv.take<uint64_t>(z.n_referenced + 1);
+  b.filter = z.filtered ? cv.take<hy_scan_chunk>(std::max<size_t>(1, z.n_chunks)) : nullptr;
+  uint64_t hist_words, max_tiles;
+  pass_sizes(z, w, first_segs, &hist_words, &max_tiles);
+  b.hist = cv.take<uint32_t>(hist_words);
+  b.off = cv.take<uint32_t>(hist_words);
+  b.recA = own_recA ? cv.take<hyk::Rec<H, P>>(std::max<uint64_t>(1, z.rows)) : nullptr;
+  b.recB = cv.take<hyk::Rec<H, P>>(std::max<uint64_t>(1, z.filtered ? std::max(z.rows, z.tiles1 * z.sub * hyk::PART_TILE) : z.rows));
+  b.span_count = z.filtered ? cv.take<uint32_t>(std::max<uint64_t>(1, z.tiles1)) : nullptr;
+  b.digA = z.digit_bytes ? cv.take<uint8_t>(std::max<uint64_t>(16, z.rows)) : nullptr;
+  b.digB = z.digit_bytes ? cv.take<uint8_t>(std::max<uint64_t>(16, z.rows)) : nullptr;
+  const uint64_t parts = (uint64_t(1) << bits) + 1;
+  b.segA = cv.take<uint32_t>(parts);
+  b.segB = cv.take<uint32_t>(parts);
+  b.seg_tile_begin = cv.take<uint64_t>(parts);
+  b.tile_counts = cv.take<uint32_t>(parts);
+  b.tile_excl = cv.take<uint32_t>(parts);
+  b.tile_owner = cv.take<uint32_t>(max_tiles);
+  b.total = cv.take<uint64_t>(1);
+  b.grand_total = cv.take<uint64_t>(1);
+}
+
+struct Common {
+  uint64_t* scan_status;
+  uint64_t scan_status_words;
+  uint32_t* misc;  // [0] ticket [1] error [2] overflow ...
+  uint64_t* totals;
+  uint64_t* join_status;
+};
+
+inline void carve_common(Carver& cv, uint64_t max_scan, uint32_t bits, Common* c) {
+  c->scan_status_words = max_scan / hyk::SCAN_BLOCK + 2;
+  c->scan_status = cv.take<uint64_t>(c->scan_status_words);
+  c->misc = cv.take<uint32_t>(64);
+  c->totals = cv.take<uint64_t>(8);
+  c->join_status = cv.take<uint64_t>((uint64_t(1) << bits) + 1);
+}
+
+inline hy_status run_scan(const uint32_t* in, uint32_t* out, uint64_t n, const Common& c, hipStream_t s,
+                          uint64_t* total_out = nullptr) {
+  if (n == 0) {
+    if (total_out) HY_HIP(hipMemsetAsync(total_out, 0, 8, s));
+    return HY_OK;
+  }
+  const uint64_t tiles = (n + hyk::SCAN_BLOCK - 1) / hyk::SCAN_BLOCK;
+  if (tiles + 1 > c.scan_status_words) return fail(HY_ERR_WORKSPACE, "scan status");
+  HY_HIP(hipMemsetAsync(c.scan_status, 0, sizeof(uint64_t) * (tiles + 1), s));
+  HY_HIP(hipMemsetAsync(c.misc, 0, 4, s));
+  KTimer kt_("exclusive_scan", s, n);
+  const bool vec = reinterpret_cast<uintptr_t>(in) % 16 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0;
+  hipLaunchKernelGGL(vec ? hyk::exclusive_scan_u32<true> : hyk::exclusive_scan_u32<false>,
+                     dim3(static_cast<uint32_t>(tiles)), dim3(hyk::SCAN_T), 0, s, in, out, n, c.scan_status, c.misc,
+                     c.misc + 1, total_out);
+  kt_.done();
+  HY_HIP(hipGetLastError());
+  return HY_OK;
+}
+
+inline uint32_t full_mask(uint32_t bits) { return bits >= 32 ? 0xFFFFFFFFu : ((1u << bits) - 1u); }
+
+// The load path every chunk of the side allows (hyk::LP_*): lean kernels for the all-value and all-single-chunk
+// reference sides, the general one otherwise.
+inline int load_path(const SidePlan& p) {
+  bool value = true, ref1 = true;
+  for (const auto& c : p.chunks) {
+    if (c.size == 0) continue;
+    value = value && c.pos_list == nullptr && c.kind == HY_COL_VALUE && c.nulls == nullptr;
+    ref1 = ref1 && c.pos_list != nullptr && c.single_chunk != HY_MIXED_CHUNKS &&
+           p.referenced[c.single_chunk].kind == HY_COL_VALUE && p.referenced[c.single_chunk].nulls == nullptr &&
+           p.referenced[c.single_chunk].size > 0;
+  }
+  if (value) return hyk::LP_VALUE;
+  return ref1 ? hyk::LP_REF1 : hyk::LP_ANY;
+}
+
+// Next-pass digit of pass i of the plan w (bits [shift, shift + w[i + 1])), or none.
+inline hyk::NextDigit next_digit(const std::vector<uint32_t>& w, size_t i, uint32_t bits, uint8_t* bytes) {
+  if (bytes == nullptr || i + 1 >= w.size()) return hyk::NextDigit{nullptr, 0, 0};
+  uint32_t above = 0;
+  for (size_t j = 0; j <= i + 1; ++j) above += w[j];
+  return hyk::NextDigit{bytes, bits - above, (1u << w[i + 1]) - 1u};
+}
+
+// The filter kind every predicate chunk of a filtered side allows (hyk::FK_*).
+inline int filter_kind(const SidePlan& p) {
+  if (!p.filtered) return hyk::FK_NONE;
+  int width = 0;
+  for (const auto& f : p.filter) {
+    if (f.op == HY_OP_NONE || f.column.size == 0) continue;
+    if (f.column.kind != HY_COL_DICT) return hyk::FK_ANY;
+    if (width && width != f.column.vid_width) return hyk::FK_ANY;
+    width = f.column.vid_width;
+  }
+  return width == 2 ? hyk::FK_DICT16 : width == 4 ? hyk::FK_DICT32 : width == 1 ? hyk::FK_DICT8 : hyk::FK_ANY;
+}
+
+// Pass 0 of a side with a fused TableScan: part1_compact (predicate + join column -> gapped row-order records in
+// recB, histograms, span counts), the histogram scan, then part1_spread (scan output + stable scatter into `out`).
+template <typename T, typename H, int LP, int FK>
+hy_status launch_filtered_pass0(const char* side_tag, const SidePlan& p, const hyk::Side& sd, const hyk::Digit& d0,
+                                const hyk::NextDigit& nd, uint32_t w0, uint32_t n_digits, SideBufs<H, uint32_t>& b,
+                                const Common& c, hipStream_t s, hyk::Rec<H, uint32_t>* out) {
+  const dim3 grid(static_cast<uint32_t>(p.n_tiles1));
+  {
+    KTimer kt_((std::string("part1_compact.") + side_tag).c_str(), s, p.n_rows);
+    hipLaunchKernelGGL((hyk::part1_compact<T, H, LP, FK>), grid, dim3(hyk::PART_THREADS), 0, s, sd, d0, n_digits,
+                       b.hist, b.span_count, b.recB);
+    kt_.done();
+  }
+  HY_HIP(hipGetLastError());
+  hy_status st = run_scan(b.hist, b.off, uint64_t(n_digits + 1) * p.n_tiles1, c, s, b.grand_total);
+  if (st != HY_OK) return st;
+  hipLaunchKernelGGL(hyk::fused_scan_totals, dim3(grid_for(p.chunks.size() + 1, 256)), dim3(256), 0, s, b.off,
+                     p.n_tiles1, n_digits, b.grand_total, b.tile_begin, static_cast<uint32_t>(p.chunks.size()), b.total,
+                     p.scan_chunk_begin);
+  HY_HIP(hipGetLastError());
+  {
+    KTimer kt_((std::string("part1_spread.") + side_tag).c_str(), s, p.n_rows);
+    hipLaunchKernelGGL((hyk::part1_spread<H>), grid, dim3(hyk::PART_THREADS), 0, s, sd, d0, nd, static_cast<int>(w0),
+                       n_digits, b.off, b.span_count, b.recB, out);
+    kt_.done();
+  }
+  HY_HIP(hipGetLastError());
+  return HY_OK;
+}
+
+template <typename T, typename H, typename P, int LP>
+hy_status launch_pass0(const char* side_tag, const SidePlan& p, const hyk::Side& sd, const hyk::Digit& d0,
+                       const hyk::NextDigit& nd, uint32_t w0, uint32_t n_digits, SideBufs<H, P>& b, const Common& c,
+                       hipStream_t s, hyk::Rec<H, P>* out) {
+  const bool filt = p.filtered;
+  const int fk = filter_kind(p);
+  if constexpr (LP != hyk::LP_REF1 && std::is_same_v<T, H> && std::is_same_v<P, uint32_t>) {
+    switch (fk) {
+      case hyk::FK_DICT8:
+        return launch_filtered_pass0<T, H, LP, hyk::FK_DICT8>(side_tag, p, sd, d0, nd, w0, n_digits, b, c, s, out);
+      case hyk::FK_DICT16:
+        return launch_filtered_pass0<T, H, LP, hyk::FK_DICT16>(side_tag, p, sd, d0, nd, w0, n_digits, b, c, s, out);
+      case hyk::FK_DICT32:
+        return launch_filtered_pass0<T, H, LP, hyk::FK_DICT32>(side_tag, p, sd, d0, nd, w0, n_digits, b, c, s, out);
+      case hyk::FK_ANY:
+        return launch_filtered_pass0<T, H, LP, hyk::FK_ANY>(side_tag, p, sd, d0, nd, w0, n_digits, b, c, s, out);
+      default:
+        break;
+    }
+  }
+  if (filt) return fail(HY_ERR_UNSUPPORTED, "fused scan on a side whose join column type is not the hashed type");
+  const dim3 grid(static_cast<uint32_t>(p.n_tiles1));
+  {
+    KTimer kt_((std::string("part1_hist.") + side_tag).c_str(), s, p.n_rows);
+    hipLaunchKernelGGL((hyk::part1_hist<T, H, LP>), grid, dim3(hyk::PART_THREADS), 0, s, sd, d0, n_digits, b.hist);
+    kt_.done();
+  }
+  HY_HIP(hipGetLastError());
+  hy_status st = run_scan(b.hist, b.off, uint64_t(n_digits) * p.n_tiles1, c, s, b.total);
+  if (st != HY_OK) return st;
+  {
+    KTimer kt_((std::string("part1_scatter.") + side_tag).c_str(), s, p.n_rows);
+    hipLaunchKernelGGL((hyk::part1_scatter<T, H, P, LP>), grid, dim3(hyk::PART_THREADS), 0, s, sd, d0, nd,
+                       static_cast<int>(w0), n_digits, b.off, out);
+    kt_.done();
+  }
+  HY_HIP(hipGetLastError());
+  return HY_OK;
+}
+
+// Pass 0: from column chunks into `out`, bucket bounds into b.segA (2^w0 buckets); next-digit bytes into nd.
+template <typename T, typename H, typename P>
+hy_status pass0_side(const char* side_tag, const SidePlan& p, SideBufs<H, P>& b, uint32_t bits, uint32_t w0,
+                     uint32_t seed, bool keep_nulls, uint32_t ref_base, const hyk::NextDigit& nd, const Common& c,
+                     hipStream_t s, hyk::Rec<H, P>* out) {
+  hyk::Side sd{};
+  sd.chunks = b.chunks;
+  sd.n_chunks = static_cast<uint32_t>(p.chunks.size());
+  sd.chunk_tile_begin = b.tile_begin;
+  sd.tile_chunk = b.tile_owner;
+  sd.n_tiles = p.n_tiles1;
+  sd.referenced = b.referenced;
+  sd.n_referenced = static_cast<uint32_t>(p.referenced.size());
+  sd.referenced_row_begin = b.ref_row_begin;
+  sd.fuse_deref = p.fuse;
+  sd.keep_nulls = keep_nulls ? 1 : 0;
+  sd.ref_base = ref_base;
+  sd.sub = p.sub;
+  sd.filter = p.filtered ? b.filter : nullptr;
+  sd.filter_const = p.filter_const;
+  sd.filter_type = p.filter_type;
+  sd.scan_out = p.scan_out;
+  const uint32_t n_digits = 1u << w0;
+  hyk::Digit d0{full_mask(bits), bits - w0, n_digits - 1u, seed};
+  HY_HIP(hipMemsetAsync(b.total, 0, 8, s));
+  if (p.filtered && p.scan_chunk_begin) HY_HIP(hipMemsetAsync(p.scan_chunk_begin, 0, 8 * (p.chunks.size() + 1), s));
+  if (p.n_tiles1 > 0) {
+    hipLaunchKernelGGL(hyk::fill_tile_owner, dim3((sd.n_chunks + 255) / 256), dim3(256), 0, s, b.tile_begin,
+                       sd.n_chunks, b.tile_owner);
+    HY_HIP(hipGetLastError());
+    const int lp = load_path(p);
+    hy_status st;
+    if (lp == hyk::LP_VALUE)
+      st = launch_pass0<T, H, P, hyk::LP_VALUE>(side_tag, p, sd, d0, nd, w0, n_digits, b, c, s, out);
+    else if (lp == hyk::LP_REF1)
+      st = launch_pass0<T, H, P, hyk::LP_REF1>(side_tag, p, sd, d0, nd, w0, n_digits, b, c, s, out);
+    else
+      st = launch_pass0<T, H, P, hyk::LP_ANY>(side_tag, p, sd, d0, nd, w0, n_digits, b, c, s, out);
+    if (st != HY_OK) return st;
+  }
+  hipLaunchKernelGGL(hyk::seg_bounds, dim3((n_digits + 1 + 255) / 256), dim3(256), 0, s, b.off, p.n_tiles1, n_digits,
+                     b.total, b.segA);
+  HY_HIP(hipGetLastError());
+  return HY_OK;
+}
+
+// One record pass over segments sg (tile prefix and owners filled, grid = an upper bound of its tiles): histogram
+// (from the digit bytes dig_in when the previous pass wrote them, else from the records), scan, stable scatter by digit
+// (bits [shift, shift + w)) writing the next pass's digit bytes (nd), then the bounds of the n_groups * 2^w parts.
+template <typename H, typename P>
+hy_status record_pass(const char* side_tag, const SideBufs<H, P>& b, const hyk::Segs& sg, const hyk::Groups& gr,
+                      uint32_t n_groups, uint64_t grid, uint32_t bits, uint32_t shift, uint32_t w, uint32_t seed,
+                      const hyk::Rec<H, P>* in, const uint8_t* dig_in, const hyk::NextDigit& nd, hyk::Rec<H, P>* out,
+                      const uint64_t* total, uint32_t* bounds, const Common& c, hipStream_t s, uint64_t rows) {
+  const uint32_t n_digits = 1u << w;
+  hyk::Digit dg{full_mask(bits), shift, n_digits - 1u, seed};
+  if (grid) {
+    {
+      KTimer kt_((std::string("part2_hist.") + side_tag).c_str(), s, rows);
+      if (dig_in)
+        hipLaunchKernelGGL(hyk::part2_hist_bytes, dim3(static_cast<uint32_t>(grid)), dim3(hyk::PART_THREADS), 0, s,
+                           sg, n_digits, dig_in, b.hist);
+      else
+        hipLaunchKernelGGL((hyk::part2_hist<H, P>), dim3(static_cast<uint32_t>(grid)), dim3(hyk::PART_THREADS), 0, s,
+                           sg, dg, n_digits, in, b.hist);
+      kt_.done();
+    }
+    HY_HIP(hipGetLastError());
+    hy_status st = run_scan(b.hist, b.off, grid * n_digits, c, s);
+    if (st != HY_OK) return st;
+    {
+      KTimer kt_((std::string("part2_scatter.") + side_tag).c_str(), s, rows);
+      hipLaunchKernelGGL((hyk::part2_scatter<H, P>), dim3(static_cast<uint32_t>(grid)), dim3(hyk::PART_THREADS), 0, s,
+                         sg, dg, nd, static_cast<int>(w), n_digits, in, b.off, out);
+      kt_.done();
+    }
+    HY_HIP(hipGetLastError());
+  }
+  const uint64_t nb = uint64_t(n_groups) * n_digits + 1;
+  hipLaunchKernelGGL(hyk::pass_bounds, dim3(grid_for(nb, 256)), dim3(256), 0, s, b.off, sg, gr, n_groups, n_digits,
+                     total, bounds);
+  HY_HIP(hipGetLastError());
+  return HY_OK;
+}
+
+// Record passes over contiguous segments (bounds in `seg`, n_segs of them) for digits w[first..]: ping-pong between
+// the two record buffers (and, when dig_in is given, the two digit-byte buffers). On return *recs / *bounds hold the
+// final records and partition bounds.
+template <typename H, typename P>
+hy_status local_passes(const char* side_tag, SideBufs<H, P>& b, const std::vector<uint32_t>& w, size_t first,
+                       uint32_t bits, uint32_t seed, hyk::Rec<H, P>* in, hyk::Rec<H, P>* spare, const uint8_t* dig_in,
+                       uint8_t* dig_spare, uint32_t* seg, uint32_t* seg_spare, uint64_t n_segs,
+                       const uint64_t* total, uint64_t rows, const Common& c, hipStream_t s, hyk::Rec<H, P>** recs,
+                       uint32_t** bounds) {
+  uint32_t below = 0;
+  for (size_t i = first; i < w.size(); ++i) below += w[i];
+  for (size_t i = first; i < w.size(); ++i) {
+    below -= w[i];
+    hipLaunchKernelGGL(hyk::seg_tile_counts, dim3(grid_for(n_segs, 256)), dim3(256), 0, s, seg, nullptr,
+                       static_cast<uint32_t>(n_segs), span2(), b.tile_counts);
+    HY_HIP(hipGetLastError());
+    hy_status st = run_scan(b.tile_counts, b.tile_excl, n_segs, c, s, c.totals + 4);
+    if (st != HY_OK) return st;
+    hipLaunchKernelGGL(hyk::widen_prefix, dim3(grid_for(n_segs + 1, 256)), dim3(256), 0, s, b.tile_excl,
+                       static_cast<uint32_t>(n_segs), c.totals + 4, b.seg_tile_begin);
+    HY_HIP(hipGetLastError());
+    hipLaunchKernelGGL(hyk::fill_tile_owner, dim3(grid_for(n_segs, 256)), dim3(256), 0, s, b.seg_tile_begin,
+                       static_cast<uint32_t>(n_segs), b.tile_owner);
+    HY_HIP(hipGetLastError());
+    const uint64_t grid = rows ? (rows + span2() - 1) / span2() + n_segs : 0;
+    hyk::Segs sg{seg,     b.seg_tile_begin, b.tile_owner, static_cast<uint32_t>(n_segs), nullptr, nullptr, nullptr,
+                 nullptr, sub2()};
+    const hyk::NextDigit nd = next_digit(w, i, bits, dig_in ? dig_spare : nullptr);
+    st = record_pass<H, P>(side_tag, b, sg, hyk::Groups{nullptr, nullptr, nullptr}, static_cast<uint32_t>(n_segs), grid,
+                           bits, below, w[i], seed, in, dig_in, nd, spare, total, seg_spare, c, s, rows);
+    if (st != HY_OK) return st;
+    std::swap(in, spare);
+    std::swap(seg, seg_spare);
+    if (nd.bytes) {
+      uint8_t* written = nd.bytes;
+      dig_spare = const_cast<uint8_t*>(dig_in);
+      dig_in = written;
+    } else {
+      dig_in = nullptr;
+    }
+    n_segs <<= w[i];
+  }
+  *recs = in;
+  *bounds = seg;
+  return HY_OK;
+}
+
+inline hyk::RowMap make_map(const uint64_t* dev_row_begin, const std::vector<uint64_t>& host_row_begin) {
+  hyk::RowMap m{};
+  m.row_begin = dev_row_begin;
+  m.n_chunks = static_cast<uint32_t>(host_row_begin.size() - 1);
+  m.uniform = uniform_of(host_row_begin);
+  m.magic = 0;
+  if (m.uniform >= 2) {
+    // floor(2^64 / u) + 1
+    const unsigned __int128 two64 = static_cast<unsigned __int128>(1) << 64;
+    m.magic = static_cast<uint64_t>(two64 / m.uniform) + 1;
+  }
+  return m;
+}
+
+// LDS rows of one build table: a fixed budget (two 1024-thread workgroups per CU), so the launch needs no partition
+// sizes from the device; a partition with more build rows than one table holds (skewed keys) is processed as several
+// LDS sub-tables in sequence.
+template <typename H, typename P>
+uint32_t lds_table_rows() {
+  size_t budget = sizeof(hyk::Rec<H, P>) > 8 ? 72 * 1024 : 40 * 1024;
+  if (const char* e = std::getenv("HY_JOIN_LDS_BUDGET")) budget = std::strtoull(e, nullptr, 10);  // test knob
+  uint32_t rows = hyk::LDS_MAX_ROWS;
+  while (rows > 16 && hyk::table_bytes<H, P>(rows) > budget) rows = rows * 7 / 8;
+  return rows;
+}
+
+// Per-partition LDS build/probe over partitioned records (partition bounds on the device). probe_rows_hint: an
+// upper bound of the probe rows; it picks the probe records per thread (JP) from the average partition.
+template <typename H, typename P>
+hy_status run_join_partitions(const uint32_t* build_begin, const uint32_t* probe_begin, uint32_t n_parts,
+                              const hyk::Rec<H, P>* brec, const hyk::Rec<H, P>* precs, const hyk::RowMap& bmap,
+                              const hyk::RowMap& pmap, int32_t mode, hy_row_id* out_build, hy_row_id* out_probe,
+                              uint64_t out_capacity, uint64_t* partition_begin, uint32_t* partition_counts,
+                              hy_join_result* result, const Common& c, hipStream_t s, uint64_t units,
+                              uint64_t probe_rows_hint) {
+  constexpr int NT = hyk::JOIN_THREADS;
+  // probe records per thread per pass: the wide variant (6) when the average partition needs more than 3/4 of JP_PER
+  const uint64_t avg_probe = n_parts ? probe_rows_hint / n_parts : 0;
+  const bool wide = avg_probe > static_cast<uint64_t>(3 * hyk::JP_PER * NT / 4);
+  const uint32_t lds_max = lds_table_rows<H, P>();
+  const size_t lds = hyk::table_bytes<H, P>(lds_max);
+
+  hyk::JoinDesc jd{};
+  jd.build_begin = build_begin;
+  jd.probe_begin = probe_begin;
+  jd.n_parts = n_parts;
+  jd.lds_max_build = lds_max;
+  jd.mode = mode;
+  jd.build_map = bmap;
+  jd.probe_map = pmap;
+  jd.capacity = out_capacity;
+  jd.error = c.misc + 1;
+  jd.overflow = c.misc + 2;
+  jd.total = c.totals + 1;
+  jd.trace = g_join_trace;
+  HY_HIP(hipMemsetAsync(c.misc, 0, 64 * 4, s));
+  HY_HIP(hipMemsetAsync(c.totals, 0, 8 * 2, s));
+  if (n_parts) {
+    KTimer kt_("join_partition", s, units);
+    auto launch = [&](auto kernel) {
+      hipLaunchKernelGGL(kernel, dim3(n_parts), dim3(NT), lds, s, jd, brec, precs, out_build, out_probe,
+                         partition_begin, partition_counts);
+    };
+    if (jd.trace)  // debug phase-trace instance (hy_debug_set_join_trace)
+      wide ? launch(hyk::join_partition<H, P, true, 6, NT>) : launch(hyk::join_partition<H, P, true, 4, NT>);
+    else
+      wide ? launch(hyk::join_partition<H, P, false, 6, NT>) : launch(hyk::join_partition<H, P, false, 4, NT>);
+    kt_.done();
+  }
+  HY_HIP(hipGetLastError());
+  uint32_t flags[4] = {0, 0, 0, 0};
+  uint64_t total = 0;
+  HY_HIP(hipMemcpyAsync(flags, c.misc, 16, hipMemcpyDeviceToHost, s));
+  HY_HIP(hipMemcpyAsync(&total, c.totals + 1, 8, hipMemcpyDeviceToHost, s));
+  HY_HIP(hipStreamSynchronize(s));
+  if (flags[1]) return fail(HY_ERR_KERNEL, "join look-back did not complete");
+  if (result) {
+    result->total_pairs = total;
+    result->capacity_required = total;
+  }
+  if (flags[2] || total > out_capacity)
+    return fail(HY_ERR_CAPACITY, "join output needs " + std::to_string(total) + " pairs");
+  return HY_OK;
+}
+
+inline SideSizes sizes_of(const SidePlan& p, bool digit_bytes) {
+  SideSizes z;
+  z.rows = p.n_rows;
+  z.tiles1 = p.n_tiles1;
+  z.sub = p.sub;
+  z.n_chunks = p.chunks.size();
+  z.n_referenced = p.referenced.size();
+  z.filtered = p.filtered;
+  z.digit_bytes = digit_bytes;
+  return z;
+}
+
+template <typename H>
+size_t join_bytes(const SidePlan& bp, const SidePlan& pp, uint32_t bits) {
+  const auto w = digit_plan(bits, 0);
+  const bool db = w.size() > 1;
+  Carver cv{nullptr, 0};
+  SideBufs<H> a, b;
+  carve_side<H, uint32_t>(cv, sizes_of(bp, db), bits, w, 1, true, a);
+  carve_side<H, uint32_t>(cv, sizes_of(pp, db), bits, w, 1, true, b);
+  uint64_t ha, hb, t;
+  pass_sizes(sizes_of(bp, db), w, 1, &ha, &t);
+  pass_sizes(sizes_of(pp, db), w, 1, &hb, &t);
+  Common c;
+  carve_common(cv, std::max({ha, hb, (uint64_t(1) << bits) + 1}), bits, &c);
+  return cv.used + 256;
+}
+
+template <typename H, typename P>
+hy_status upload_side(const SidePlan& p, const SideBufs<H, P>& b, hipStream_t s) {
+  auto upload = [&](auto* dst, const auto& v) -> hy_status {
+    if (!v.empty()) HY_HIP(hipMemcpyAsync(dst, v.data(), sizeof(v[0]) * v.size(), hipMemcpyHostToDevice, s));
+    return HY_OK;
+  };
+  if (upload(b.chunks, p.chunks) || upload(b.tile_begin, p.tile_begin) || upload(b.row_begin, p.row_begin) ||
+      upload(b.referenced, p.referenced) || upload(b.ref_row_begin, p.ref_row_begin))
+    return HY_ERR_DEVICE;
+  if (p.filtered && upload(b.filter, p.filter)) return HY_ERR_DEVICE;
+  return HY_OK;
+}
+
+template <typename TB, typename TP, typename H>
+hy_status join_typed(const SidePlan& bp, const SidePlan& pp, const hy_join_params* prm, hy_row_id* out_build,
+                     hy_row_id* out_probe, uint64_t out_capacity, uint64_t* partition_begin,
+                     uint32_t* partition_counts, hy_join_result* result, void* workspace, size_t workspace_bytes,
+                     hipStream_t s) {
+  const uint32_t bits = prm->radix_bits;
+  if (workspace_bytes < join_bytes<H>(bp, pp, bits)) return fail(HY_ERR_WORKSPACE, "join workspace too small");
+  const auto w = digit_plan(bits, 0);
+  const bool db = w.size() > 1;
+  Carver cv{static_cast<char*>(workspace), workspace_bytes};
+  SideBufs<H> bb, pb;
+  carve_side<H, uint32_t>(cv, sizes_of(bp, db), bits, w, 1, true, bb);
+  carve_side<H, uint32_t>(cv, sizes_of(pp, db), bits, w, 1, true, pb);
+  uint64_t ha, hb2, t;
+  pass_sizes(sizes_of(bp, db), w, 1, &ha, &t);
+  pass_sizes(sizes_of(pp, db), w, 1, &hb2, &t);
+  Common c{};
+  carve_common(cv, std::max({ha, hb2, (uint64_t(1) << bits) + 1}), bits, &c);
+  if (!cv.ok) return fail(HY_ERR_WORKSPACE, "join workspace too small");
+  if (upload_side(bp, bb, s) || upload_side(pp, pb, s)) return HY_ERR_DEVICE;
+  const bool keep_nulls = prm->mode == HY_JOIN_LEFT || prm->mode == HY_JOIN_RIGHT;
+
+  hyk::Rec<H>* recs[2] = {nullptr, nullptr};
+  uint32_t* bounds[2] = {nullptr, nullptr};
+  for (int side = 0; side < 2; ++side) {
+    const SidePlan& p = side == 0 ? bp : pp;
+    SideBufs<H>& b = side == 0 ? bb : pb;
+    const char* tag = side == 0 ? "build" : "probe";
+    const hyk::NextDigit nd = next_digit(w, 0, bits, b.digA);
+    hy_status st = side == 0
+                       ? pass0_side<TB, H, uint32_t>(tag, p, b, bits, w.empty() ? 0 : w[0], prm->seed, false,
+                                                     p.ref_base, nd, c, s, b.recA)
+                       : pass0_side<TP, H, uint32_t>(tag, p, b, bits, w.empty() ? 0 : w[0], prm->seed, keep_nulls,
+                                                     p.ref_base, nd, c, s, b.recA);
+    if (st != HY_OK) return st;
+    st = local_passes<H, uint32_t>(tag, b, w, 1, bits, prm->seed, b.recA, b.recB, nd.bytes, b.digB, b.segA, b.segB,
+                                   w.empty() ? 1 : (1ull << w[0]), b.total, p.n_rows, c, s, &recs[side], &bounds[side]);
+    if (st != HY_OK) return st;
+  }
+  // filtered sides emit RowIDs of their data table (the scan's PosLists dereferenced, write_output_columns)
+  const hyk::RowMap bmap = bp.fuse ? make_map(bb.ref_row_begin, bp.ref_row_begin) : make_map(bb.row_begin, bp.row_begin);
+  const hyk::RowMap pmap = pp.fuse ? make_map(pb.ref_row_begin, pp.ref_row_begin) : make_map(pb.row_begin, pp.row_begin);
+  return run_join_partitions<H, uint32_t>(bounds[0], bounds[1], 1u << bits, recs[0], recs[1], bmap, pmap, prm->mode,
+                                          out_build, out_probe, out_capacity, partition_begin, partition_counts,
+                                          result, c, s, bp.n_rows + pp.n_rows, pp.n_rows);
+}
+
+template <typename F>
+hy_status dispatch_type(int32_t t, F&& f) {
+  switch (t) {
+    case HY_TYPE_INT32:
+      return f(int32_t{});
+    case HY_TYPE_INT64:
+      return f(int64_t{});
+    case HY_TYPE_FLOAT:
+      return f(float{});
+    case HY_TYPE_DOUBLE:
+      return f(double{});
+  }
+  return fail(HY_ERR_UNSUPPORTED, "join column type");
+}
+
+// Only hashed types reachable through JoinHashTraits (hash_traits.hpp:9-42) are instantiated.
+template <typename T, typename H>
+constexpr bool reachable() {
+  return (sizeof(H) >= sizeof(T) || std::is_floating_point_v<H>) &&
+         !(std::is_floating_point_v<T> && !std::is_floating_point_v<H>);
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Distributed JoinHash: exchange records are Rec<H, hy_row_id> (16 bytes: key, global RowID).
+// ---------------------------------------------------------------------------------------------------------------
+inline uint32_t ceil_log2(uint32_t n) {
+  uint32_t b = 0;
+  while ((1u << b) < n) ++b;
+  return b;
+}
+
+template <typename H>
+size_t exchange_partition_bytes(const SidePlan& p, uint32_t bits, const std::vector<uint32_t>& w) {
+  Carver cv{nullptr, 0};
+  SideBufs<H, hy_row_id> b;
+  SideSizes z = sizes_of(p, false);
+  carve_side<H, hy_row_id>(cv, z, bits, std::vector<uint32_t>(w.begin(), w.begin() + 1), 1, false, b);
+  Common c;
+  carve_common(cv, std::max<uint64_t>((1ull << w[0]) * std::max<uint64_t>(1, p.n_tiles1), 2), bits, &c);
+  return cv.used + 256;
+}
+
+// Receiver geometry of one side: runs (bucket j, sender s) of the received buffer, listed j-major.
+struct RecvPlan {
+  uint64_t rows = 0, tiles = 0;
+  std::vector<uint32_t> seg_begin, seg_end, seg_stride, seg_toff;
+  std::vector<uint64_t> seg_tile_begin, seg_hbase, group_hbase;
+  std::vector<uint32_t> group_tiles, group_out;
+  uint64_t hist_words = 1;
+};
+
+inline RecvPlan recv_plan(const uint64_t* counts, uint32_t n_senders, uint32_t nb, uint32_t digits) {
+  RecvPlan r;
+  std::vector<uint64_t> sender_base(n_senders + 1, 0);
+  for (uint32_t s = 0; s < n_senders; ++s) {
+    uint64_t n = 0;
+    for (uint32_t j = 0; j < nb; ++j) n += counts[uint64_t(s) * nb + j];
+    sender_base[s + 1] = sender_base[s] + n;
+  }
+  r.rows = sender_base[n_senders];
+  const uint32_t nseg = nb * n_senders;
+  r.seg_begin.resize(nseg);
+  r.seg_end.resize(nseg);
+  r.seg_stride.resize(nseg);
+  r.seg_toff.resize(nseg);
+  r.seg_hbase.resize(nseg);
+  r.seg_tile_begin.resize(nseg + 1);
+  r.group_hbase.resize(nb);
+  r.group_tiles.resize(nb);
+  r.group_out.resize(nb);
+  std::vector<uint64_t> run_in_sender(n_senders, 0);
+  uint64_t tiles = 0, hbase = 0, out = 0;
+  for (uint32_t j = 0; j < nb; ++j) {
+    uint32_t gt = 0;
+    r.group_out[j] = static_cast<uint32_t>(out);
+    for (uint32_t s = 0; s < n_senders; ++s) {
+      const uint64_t cnt = counts[uint64_t(s) * nb + j];
+      const uint32_t q = j * n_senders + s;
+      const uint64_t b0 = sender_base[s] + run_in_sender[s];
+      run_in_sender[s] += cnt;
+      r.seg_begin[q] = static_cast<uint32_t>(b0);
+      r.seg_end[q] = static_cast<uint32_t>(b0 + cnt);
+      const uint32_t t = static_cast<uint32_t>((cnt + span2() - 1) / span2());
+      r.seg_tile_begin[q] = tiles;
+      r.seg_toff[q] = gt;
+      tiles += t;
+      gt += t;
+      out += cnt;
+    }
+    r.group_tiles[j] = gt;
+    r.group_hbase[j] = hbase;
+    for (uint32_t s = 0; s < n_senders; ++s) {
+      r.seg_hbase[j * n_senders + s] = hbase;
+      r.seg_stride[j * n_senders + s] = gt;
+    }
+    hbase += uint64_t(gt) * digits;
+  }
+  r.seg_tile_begin[nseg] = tiles;
+  r.tiles = tiles;
+  r.hist_words = std::max<uint64_t>(1, hbase);
+  return r;
+}
+
+// Receiver device buffers of one side.
+template <typename H>
+struct RecvBufs {
+  SideBufs<H, hy_row_id> b;
+  uint32_t *seg_begin, *seg_end, *seg_stride, *seg_toff, *group_tiles, *group_out, *owner;
+  uint64_t *seg_tile_begin, *seg_hbase, *group_hbase;
+};
+
+template <typename H>
+void carve_recv(Carver& cv, const RecvPlan& r, uint32_t bits, const std::vector<uint32_t>& w, uint32_t nb,
+                uint32_t n_senders, RecvBufs<H>& rb) {
+  SideSizes z;
+  z.rows = r.rows;
+  std::vector<uint32_t> tail(w.begin() + 1, w.end());
+  if (tail.empty()) tail.push_back(0);
+  carve_side<H, hy_row_id>(cv, z, bits, tail, uint64_t(nb) * n_senders, true, rb.b);
+  const uint32_t nseg = std::max<uint32_t>(1, nb * n_senders);
+  rb.seg_begin = cv.take<uint32_t>(nseg);
+  rb.seg_end = cv.take<uint32_t>(nseg);
+  rb.seg_stride = cv.take<uint32_t>(nseg);
+  rb.seg_toff = cv.take<uint32_t>(nseg);
+  rb.seg_tile_begin = cv.take<uint64_t>(nseg + 1);
+  rb.seg_hbase = cv.take<uint64_t>(nseg);
+  rb.group_hbase = cv.take<uint64_t>(std::max<uint32_t>(1, nb));
+  rb.group_tiles = cv.take<uint32_t>(std::max<uint32_t>(1, nb));
+  rb.group_out = cv.take<uint32_t>(std::max<uint32_t>(1, nb));
+  rb.owner = cv.take<uint32_t>(std::max<uint64_t>(1, r.tiles));
+}
+
+template <typename H>
+hy_status recv_side(const char* tag, const RecvPlan& r, RecvBufs<H>& rb, const std::vector<uint32_t>& w, uint32_t bits,
+                    uint32_t nb, uint32_t n_senders, uint32_t seed, const hyk::Rec<H, hy_row_id>* in,
+                    const Common& c, hipStream_t s, hyk::Rec<H, hy_row_id>** recs, uint32_t** bounds) {
+  auto up = [&](auto* dst, const auto& v) -> hy_status {
+    if (!v.empty()) HY_HIP(hipMemcpyAsync(dst, v.data(), sizeof(v[0]) * v.size(), hipMemcpyHostToDevice, s));
+    return HY_OK;
+  };
+  if (up(rb.seg_begin, r.seg_begin) || up(rb.seg_end, r.seg_end) || up(rb.seg_stride, r.seg_stride) ||
+      up(rb.seg_toff, r.seg_toff) || up(rb.seg_tile_begin, r.seg_tile_begin) || up(rb.seg_hbase, r.seg_hbase) ||
+      up(rb.group_hbase, r.group_hbase) || up(rb.group_tiles, r.group_tiles) || up(rb.group_out, r.group_out))
+    return HY_ERR_DEVICE;
+  HY_HIP(hipMemcpyAsync(rb.b.total, &r.rows, 8, hipMemcpyHostToDevice, s));
+  const uint32_t nseg = nb * n_senders;
+  if (r.tiles) {
+    hipLaunchKernelGGL(hyk::fill_tile_owner, dim3(grid_for(nseg, 256)), dim3(256), 0, s, rb.seg_tile_begin, nseg,
+                       rb.owner);
+    HY_HIP(hipGetLastError());
+  }
+  const uint32_t w1 = w.size() > 1 ? w[1] : 0;  // one digit only: a stable merge of the senders' runs
+  const uint32_t shift = bits - w[0] - w1;
+  hyk::Segs sg{rb.seg_begin, rb.seg_tile_begin, rb.owner,    nseg,   rb.seg_end,
+               rb.seg_hbase, rb.seg_stride,     rb.seg_toff, sub2()};
+  hyk::Groups gr{rb.group_hbase, rb.group_tiles, rb.group_out};
+  // the merge pass must not write through a stale histogram entry: hist words are exactly the groups' tiles x digits
+  hy_status st = record_pass<H, hy_row_id>(tag, rb.b, sg, gr, nb, r.tiles, bits, shift, w1, seed, in, nullptr,
+                                           hyk::NextDigit{nullptr, 0, 0}, rb.b.recA, rb.b.total, rb.b.segA, c, s,
+                                           r.rows);
+  if (st != HY_OK) return st;
+  return local_passes<H, hy_row_id>(tag, rb.b, w, 2, bits, seed, rb.b.recA, rb.b.recB, nullptr, nullptr, rb.b.segA,
+                                    rb.b.segB, uint64_t(nb) << w1, rb.b.total, r.rows, c, s, recs, bounds);
+}
+
+template <typename H>
+size_t exchange_join_bytes(const RecvPlan& rbp, const RecvPlan& rpp, uint32_t bits, const std::vector<uint32_t>& w,
+                           uint32_t nb, uint32_t n_senders) {
+  Carver cv{nullptr, 0};
+  RecvBufs<H> a, b;
+  carve_recv<H>(cv, rbp, bits, w, nb, n_senders, a);
+  carve_recv<H>(cv, rpp, bits, w, nb, n_senders, b);
+  Common c;
+  const uint64_t max_scan = std::max({rbp.hist_words * 2, rpp.hist_words * 2, (uint64_t(1) << bits) + 1,
+                                      (rbp.rows + rpp.rows) / span2() * 256 + uint64_t(nb) * n_senders * 256});
+  carve_common(cv, max_scan, bits, &c);
+  return cv.used + 256;
+}
+
+template <typename H>
+hy_status exchange_partition_for_hashed(const SidePlan& p, int32_t value_type, const hy_join_params* params,
+                                        int32_t keep_nulls, const std::vector<uint32_t>& w, void* out_records,
+                                        uint64_t* bucket_counts, void* workspace, size_t workspace_bytes,
+                                        hipStream_t s) {
+  const uint32_t bits = params->radix_bits;
+  const uint32_t T = 1u << w[0];
+  return dispatch_type(value_type, [&](auto ttag) -> hy_status {
+    using T_ = decltype(ttag);
+    if constexpr (reachable<T_, H>()) {
+      if (workspace_bytes < exchange_partition_bytes<H>(p, bits, w)) return fail(HY_ERR_WORKSPACE, "workspace");
+      Carver cv{static_cast<char*>(workspace), workspace_bytes};
+      SideBufs<H, hy_row_id> b;
+      carve_side<H, hy_row_id>(cv, sizes_of(p, false), bits, std::vector<uint32_t>(w.begin(), w.begin() + 1), 1,
+                               false, b);
+      Common c{};
+      carve_common(cv, std::max<uint64_t>(uint64_t(T) * std::max<uint64_t>(1, p.n_tiles1), 2), bits, &c);
+      if (!cv.ok) return fail(HY_ERR_WORKSPACE, "workspace");
+      if (upload_side(p, b, s)) return HY_ERR_DEVICE;
+      hy_status st2 = pass0_side<T_, H, hy_row_id>("exchange", p, b, bits, w[0], params->seed, keep_nulls != 0,
+                                                   p.ref_base, hyk::NextDigit{nullptr, 0, 0}, c, s,
+                                                   static_cast<hyk::Rec<H, hy_row_id>*>(out_records));
+      if (st2 != HY_OK) return st2;
+      std::vector<uint32_t> bounds(T + 1);
+      HY_HIP(hipMemcpyAsync(bounds.data(), b.segA, 4 * (T + 1), hipMemcpyDeviceToHost, s));
+      HY_HIP(hipStreamSynchronize(s));
+      for (uint32_t i = 0; i < T; ++i) bucket_counts[i] = bounds[i + 1] - bounds[i];
+      return HY_OK;
+    } else {
+      return fail(HY_ERR_UNSUPPORTED, "hashed type not reachable from the column type");
+    }
+  });
+}
+
+template <typename H>
+hy_status exchange_join_for_hashed(const void* build_records, const void* probe_records, const RecvPlan& rbp,
+                                   const RecvPlan& rpp, uint32_t n_senders, uint32_t n_buckets,
+                                   const std::vector<uint32_t>& w, const hy_join_params* params, hy_row_id* out_build,
+                                   hy_row_id* out_probe, uint64_t out_capacity, uint64_t* partition_begin,
+                                   uint32_t* partition_counts, hy_join_result* result, void* workspace,
+                                   size_t workspace_bytes, hipStream_t s) {
+  const uint32_t bits = params->radix_bits;
+  if (workspace_bytes < exchange_join_bytes<H>(rbp, rpp, bits, w, n_buckets, n_senders))
+    return fail(HY_ERR_WORKSPACE, "exchange join workspace too small");
+  Carver cv{static_cast<char*>(workspace), workspace_bytes};
+  RecvBufs<H> rb, rp;
+  carve_recv<H>(cv, rbp, bits, w, n_buckets, n_senders, rb);
+  carve_recv<H>(cv, rpp, bits, w, n_buckets, n_senders, rp);
+  Common c{};
+  const uint64_t max_scan = std::max({rbp.hist_words * 2, rpp.hist_words * 2, (uint64_t(1) << bits) + 1,
+                                      (rbp.rows + rpp.rows) / span2() * 256 + uint64_t(n_buckets) * n_senders * 256});
+  carve_common(cv, max_scan, bits, &c);
+  if (!cv.ok) return fail(HY_ERR_WORKSPACE, "exchange join workspace too small");
+  using R = hyk::Rec<H, hy_row_id>;
+  R* recs[2] = {nullptr, nullptr};
+  uint32_t* bounds[2] = {nullptr, nullptr};
+  hy_status st = recv_side<H>("build", rbp, rb, w, bits, n_buckets, n_senders, params->seed,
+                              static_cast<const R*>(build_records), c, s, &recs[0], &bounds[0]);
+  if (st != HY_OK) return st;
+  st = recv_side<H>("probe", rpp, rp, w, bits, n_buckets, n_senders, params->seed,
+                    static_cast<const R*>(probe_records), c, s, &recs[1], &bounds[1]);
+  if (st != HY_OK) return st;
+  const uint32_t n_parts = n_buckets << (bits - w[0]);
+  return run_join_partitions<H, hy_row_id>(bounds[0], bounds[1], n_parts, recs[0], recs[1], hyk::RowMap{},
+                                           hyk::RowMap{}, params->mode, out_build, out_probe, out_capacity,
+                                           partition_begin, partition_counts, result, c, s, rbp.rows + rpp.rows,
+                                           rpp.rows);
+}
+
+template <typename H>
+hy_status join_for_hashed(const SidePlan& bp, const SidePlan& pp, int32_t build_type, int32_t probe_type,
+                          const hy_join_params* params, hy_row_id* out_build, hy_row_id* out_probe,
+                          uint64_t out_capacity, uint64_t* partition_begin, uint32_t* partition_counts,
+                          hy_join_result* result, void* workspace, size_t workspace_bytes, hipStream_t s) {
+  return dispatch_type(build_type, [&](auto btag) -> hy_status {
+    using TB = decltype(btag);
+    return dispatch_type(probe_type, [&](auto ptag) -> hy_status {
+      using TP = decltype(ptag);
+      if constexpr (reachable<TB, H>() && reachable<TP, H>()) {
+        return join_typed<TB, TP, H>(bp, pp, params, out_build, out_probe, out_capacity, partition_begin,
+                                     partition_counts, result, workspace, workspace_bytes, s);
+      } else {
+        return fail(HY_ERR_UNSUPPORTED, "hashed type not reachable from column types");
+      }
+    });
+  });
+}
+
+// Per-hashed-type entry points (one translation unit each).
+#define HYJ_DECLARE(SUFFIX, H)                                                                                      \
+  hy_status join_##SUFFIX(const SidePlan& bp, const SidePlan& pp, int32_t build_type, int32_t probe_type,           \
+                          const hy_join_params* params, hy_row_id* out_build, hy_row_id* out_probe,               \
+                          uint64_t out_capacity, uint64_t* partition_begin, uint32_t* partition_counts,           \
+                          hy_join_result* result, void* workspace, size_t workspace_bytes, hipStream_t s);    \
+  size_t join_bytes_##SUFFIX(const SidePlan& bp, const SidePlan& pp, uint32_t bits);                               \
+  size_t exchange_partition_bytes_##SUFFIX(const SidePlan& p, uint32_t bits, const std::vector<uint32_t>& w);        \
+  size_t exchange_join_bytes_##SUFFIX(const RecvPlan& rbp, const RecvPlan& rpp, uint32_t bits,                      \
+                                      const std::vector<uint32_t>& w, uint32_t nb, uint32_t n_senders);             \
+  hy_status exchange_partition_##SUFFIX(const SidePlan& p, int32_t value_type, const hy_join_params* params,        \
+                                        int32_t keep_nulls, const std::vector<uint32_t>& w, void* out_records,      \
+                                        uint64_t* bucket_counts, void* workspace, size_t workspace_bytes,           \
+                                        hipStream_t s);                                                             \
+  hy_status exchange_join_##SUFFIX(const void* build_records, const void* probe_records, const RecvPlan& rbp,      \
+                                   const RecvPlan& rpp, uint32_t n_senders, uint32_t n_buckets,                    \
+                                   const std::vector<uint32_t>& w, const hy_join_params* params,                   \
+                                   hy_row_id* out_build, hy_row_id* out_probe, uint64_t out_capacity,              \
+                                   uint64_t* partition_begin, uint32_t* partition_counts, hy_join_result* result,  \
+                                   void* workspace, size_t workspace_bytes, hipStream_t s);
+HYJ_DECLARE(i32, int32_t)
+HYJ_DECLARE(i64, int64_t)
+HYJ_DECLARE(f32, float)
+HYJ_DECLARE(f64, double)
+#undef HYJ_DECLARE
+
+#define HYJ_DEFINE(SUFFIX, H)                                                                                       \
+  hy_status join_##SUFFIX(const SidePlan& bp, const SidePlan& pp, int32_t build_type, int32_t probe_type,           \
+                          const hy_join_params* params, hy_row_id* out_build, hy_row_id* out_probe,               \
+                          uint64_t out_capacity, uint64_t* partition_begin, uint32_t* partition_counts,           \
+                          hy_join_result* result, void* workspace, size_t workspace_bytes, hipStream_t s) {       \
+    return join_for_hashed<H>(bp, pp, build_type, probe_type, params, out_build, out_probe, out_capacity,         \
+                              partition_begin, partition_counts, result, workspace, workspace_bytes, s);          \
+  }                                                                                                                 \
+  size_t join_bytes_##SUFFIX(const SidePlan& bp, const SidePlan& pp, uint32_t bits) {                               \
+    return join_bytes<H>(bp, pp, bits);                                                                             \
+  }                                                                                                                 \
+  size_t exchange_partition_bytes_##SUFFIX(const SidePlan& p, uint32_t bits, const std::vector<uint32_t>& w) {       \
+    return exchange_partition_bytes<H>(p, bits, w);                                                                 \
+  }                                                                                                                 \
+  size_t exchange_join_bytes_##SUFFIX(const RecvPlan& rbp, const RecvPlan& rpp, uint32_t bits,                      \
+                                      const std::vector<uint32_t>& w, uint32_t nb, uint32_t n_senders) {            \
+    return exchange_join_bytes<H>(rbp, rpp, bits, w, nb, n_senders);                                                \
+  }                                                                                                                 \
+  hy_status exchange_partition_##SUFFIX(const SidePlan& p, int32_t value_type, const hy_join_params* params,        \
+                                        int32_t keep_nulls, const std::vector<uint32_t>& w, void* out_records,      \
+                                        uint64_t* bucket_counts, void* workspace, size_t workspace_bytes,           \
+                                        hipStream_t s) {                                                            \
+    return exchange_partition_for_hashed<H>(p, value_type, params, keep_nulls, w, out_records, bucket_counts,       \
+                                            workspace, workspace_bytes, s);                                         \
+  }                                                                                                                 \
+  hy_status exchange_join_##SUFFIX(const void* build_records, const void* probe_records, const RecvPlan& rbp,      \
+                                   const RecvPlan& rpp, uint32_t n_senders, uint32_t n_buckets,                    \
+                                   const std::vector<uint32_t>& w, const hy_join_params* params,                   \
+                                   hy_row_id* out_build, hy_row_id* out_probe, uint64_t out_capacity,              \
+                                   uint64_t* partition_begin, uint32_t* partition_counts, hy_join_result* result,  \
+                                   void* workspace, size_t workspace_bytes, hipStream_t s) {                        \
+    return exchange_join_for_hashed<H>(build_records, probe_records, rbp, rpp, n_senders, n_buckets, w, params,     \
+                                       out_build, out_probe, out_capacity, partition_begin, partition_counts,      \
+                                       result, workspace, workspace_bytes, s);                                      \
+  }
+
+}  // namespace hyj

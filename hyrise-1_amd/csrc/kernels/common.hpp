@@ -62,6 +62,30 @@ __host__ __device__ inline uint32_t murmur2(T key, uint32_t seed) {
   }
 }
 
+// Predicate of one row (HY_OP_*): value compare of the reference's with_comparator (type_comparison.hpp:100-123), or
+// the value-id compare of the dictionary rewrite (single_column_table_scan_impl.hpp:52-76).
+template <typename T>
+__device__ __forceinline__ bool cmp_op(int op, T v, T c) {
+  switch (op) {
+    case HY_OP_EQ:
+      return v == c;
+    case HY_OP_NE:
+      return v != c;
+    case HY_OP_LT:
+      return v < c;
+    case HY_OP_LE:
+      return v <= c;
+    case HY_OP_GT:
+      return v > c;
+    case HY_OP_GE:
+      return v >= c;
+    case HY_OP_ALL:
+      return true;
+    default:
+      return false;
+  }
+}
+
 // ------------------------------------------------------------------------------------------------------------
 // Wave64 helpers.
 // ------------------------------------------------------------------------------------------------------------

@@ -120,6 +120,12 @@ struct Side {
   int32_t keep_nulls;
   uint32_t ref_base;                 // RowIDs in PosLists name referenced chunk ref_base + i for Side::referenced[i]
   uint32_t sub;                      // tiles per span
+  // Fused TableScan (hy_scan_join_hash): the predicate column's chunk c is filter[c]; a row takes part only if it
+  // matches. Matching chunk offsets are written chunk by chunk to scan_out (the scan's output, row order).
+  const hy_scan_chunk* filter;       // device, n_chunks entries, or null
+  uint64_t filter_const;             // type_cast<T>(constant) bits for VALUE predicate chunks
+  int32_t filter_type;               // HY_TYPE_* of VALUE predicate chunks
+  uint32_t* scan_out;
 };
 
 // NULL rows: a ValueColumn read directly yields its stored value (value_column_iterable), a dictionary column and
@@ -169,7 +175,9 @@ __device__ __forceinline__ bool load_row(const Side& s, const SrcChunk& c, uint3
                               : own_payload<P>(c.row_begin, c.chunk_id, off);
     }
   } else {
-    valid = read_column_value<T>(c, off, &v, true);
+    // a filtered side stands for the scan's output, a reference table: its NULL rows read as T{} like any row reached
+    // through a ReferenceColumn (they only matter to outer joins, which partition them by that value)
+    valid = read_column_value<T>(c, off, &v, s.filter == nullptr);
     *payload = own_payload<P>(c.row_begin, c.chunk_id, off);
   }
   *key = static_cast<H>(v);
@@ -261,6 +269,78 @@ __device__ __forceinline__ uint32_t load_items(const Side& s, const SrcChunk& ch
   return act;
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// Fused TableScan predicate (reference SingleColumnTableScanImpl, single_column_table_scan_impl.cpp:38-205, with the
+// dictionary rewrite done on the host per chunk): match mask of this lane's PART_ITEMS rows base + k * WAVE + lane of
+// predicate chunk f (rows >= f.column.size are 0). Loads are unconditional from clamped rows (see load_items).
+// ------------------------------------------------------------------------------------------------------------
+template <typename E, bool DICT>
+__device__ __forceinline__ uint32_t filter_items_t(const hy_scan_chunk& f, uint32_t base, uint64_t cbits) {
+  const E* data = static_cast<const E*>(f.column.data);
+  const uint32_t n = f.column.size, last = n - 1;
+  E v[PART_ITEMS];
+#pragma unroll
+  for (int k = 0; k < PART_ITEMS; ++k) v[k] = data[min(base + k * WAVE, last)];
+  uint32_t m = 0;
+  const int op = f.op;
+  if constexpr (DICT) {
+    const E null_vid = static_cast<E>(f.column.dictionary_size);
+    const E s = static_cast<E>(f.search_vid);
+#pragma unroll
+    for (int k = 0; k < PART_ITEMS; ++k) m |= static_cast<uint32_t>(v[k] != null_vid && cmp_op<E>(op, v[k], s)) << k;
+  } else {
+    E c;
+    __builtin_memcpy(&c, &cbits, sizeof(E));
+    if (f.column.nulls != nullptr) {
+      uint8_t nl[PART_ITEMS];
+#pragma unroll
+      for (int k = 0; k < PART_ITEMS; ++k) nl[k] = f.column.nulls[min(base + k * WAVE, last)];
+#pragma unroll
+      for (int k = 0; k < PART_ITEMS; ++k) m |= static_cast<uint32_t>(nl[k] == 0 && cmp_op<E>(op, v[k], c)) << k;
+    } else {
+#pragma unroll
+      for (int k = 0; k < PART_ITEMS; ++k) m |= static_cast<uint32_t>(cmp_op<E>(op, v[k], c)) << k;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < PART_ITEMS; ++k)
+    if (base + k * WAVE >= n) m &= ~(1u << k);
+  return m;
+}
+
+// Filter kinds a side can be specialised for (the host picks one per side from its predicate chunks): every chunk
+// dictionary-encoded with 1-, 2- or 4-byte value ids, or anything (value columns of any type, mixed widths).
+constexpr int FK_NONE = 0;
+constexpr int FK_DICT8 = 1;
+constexpr int FK_DICT16 = 2;
+constexpr int FK_DICT32 = 3;
+constexpr int FK_ANY = 4;
+
+template <int FK>
+__device__ __forceinline__ uint32_t filter_items(const Side& s, uint32_t c, uint32_t base) {
+  const hy_scan_chunk f = s.filter[c];
+  base += __lane_id();
+  if (f.op == HY_OP_NONE || f.column.size == 0) return 0u;
+  if constexpr (FK == FK_DICT8) return filter_items_t<uint8_t, true>(f, base, 0);
+  if constexpr (FK == FK_DICT16) return filter_items_t<uint16_t, true>(f, base, 0);
+  if constexpr (FK == FK_DICT32) return filter_items_t<uint32_t, true>(f, base, 0);
+  if (f.column.kind == HY_COL_DICT) {
+    if (f.column.vid_width == 1) return filter_items_t<uint8_t, true>(f, base, 0);
+    if (f.column.vid_width == 2) return filter_items_t<uint16_t, true>(f, base, 0);
+    return filter_items_t<uint32_t, true>(f, base, 0);
+  }
+  switch (s.filter_type) {
+    case HY_TYPE_INT32:
+      return filter_items_t<int32_t, false>(f, base, s.filter_const);
+    case HY_TYPE_INT64:
+      return filter_items_t<int64_t, false>(f, base, s.filter_const);
+    case HY_TYPE_FLOAT:
+      return filter_items_t<float, false>(f, base, s.filter_const);
+    default:
+      return filter_items_t<double, false>(f, base, s.filter_const);
+  }
+}
+
 struct Digit {
   uint32_t mask;   // (1 << radix_bits) - 1
   uint32_t shift;  // digit = (hash & mask) >> shift
@@ -272,6 +352,14 @@ template <typename H>
 __device__ __forceinline__ uint32_t digit_of(const Digit& dg, H key) {
   return ((murmur2<H>(key, dg.seed) & dg.mask) >> dg.shift) & dg.dmask;
 }
+
+// The next pass's digit of each record, written beside the records so that the next histogram reads one byte per
+// record instead of the record (and its hash). bytes == null: no next pass.
+struct NextDigit {
+  uint8_t* bytes;
+  uint32_t shift;
+  uint32_t dmask;
+};
 
 __device__ __forceinline__ uint32_t find_tile_owner(const uint64_t* begin, uint32_t n, uint64_t tile) {
   uint32_t lo = 0, hi = n;
@@ -351,8 +439,8 @@ template <typename H, typename P>
 __device__ __forceinline__ void staged_scatter(const Rec<H, P> (&recs)[PART_ITEMS], uint32_t act,
                                                const uint32_t (&dr)[PART_ITEMS], uint32_t (*s_cnt)[256],
                                                uint32_t* s_delta, Rec<H, P>* s_stage, uint32_t* s_scratch,
-                                               uint32_t n_digits, const Digit& dg, uint32_t& run,
-                                               Rec<H, P>* __restrict__ out) {
+                                               uint32_t n_digits, const Digit& dg, const NextDigit& nd,
+                                               uint32_t& run, Rec<H, P>* __restrict__ out) {
   const int w = threadIdx.x / WAVE;
   __syncthreads();  // every wave's counts are in s_cnt
   const uint32_t d = threadIdx.x;
@@ -380,7 +468,10 @@ __device__ __forceinline__ void staged_scatter(const Rec<H, P> (&recs)[PART_ITEM
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < total; i += PART_THREADS) {
     const Rec<H, P> r = s_stage[i];
-    out[i + s_delta[digit_of<H>(dg, r.key)]] = r;
+    const uint32_t h = murmur2<H>(r.key, dg.seed) & dg.mask;
+    const uint32_t o = i + s_delta[(h >> dg.shift) & dg.dmask];
+    out[o] = r;
+    if (nd.bytes != nullptr) nd.bytes[o] = static_cast<uint8_t>((h >> nd.shift) & nd.dmask);
   }
 }
 
@@ -393,6 +484,7 @@ __device__ __forceinline__ void clear_wave_counts(uint32_t* wave_cnt) {
 // ------------------------------------------------------------------------------------------------------------
 // Pass 1: from column chunks.
 // ------------------------------------------------------------------------------------------------------------
+// Histogram rows: hist[d * n_tiles + tile] = rows of span `tile` with digit d.
 template <typename T, typename H, int LP>
 __global__ __launch_bounds__(PART_THREADS) void part1_hist(Side s, Digit dg, uint32_t n_digits,
                                                           uint32_t* __restrict__ hist) {
@@ -422,9 +514,9 @@ __global__ __launch_bounds__(PART_THREADS) void part1_hist(Side s, Digit dg, uin
 }
 
 template <typename T, typename H, typename P, int LP>
-__global__ __launch_bounds__(PART_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void part1_scatter(Side s, Digit dg, int dbits, uint32_t n_digits,
-                                                             const uint32_t* __restrict__ offsets,
-                                                             Rec<H, P>* __restrict__ out) {
+__global__ __launch_bounds__(PART_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void part1_scatter(
+    Side s, Digit dg, NextDigit nd, int dbits, uint32_t n_digits, const uint32_t* __restrict__ offsets,
+    Rec<H, P>* __restrict__ out) {
   __shared__ uint32_t s_cnt[PART_WAVES][256];
   __shared__ uint32_t s_delta[256];
   __shared__ uint32_t s_scratch[PART_WAVES + 1];
@@ -456,7 +548,130 @@ __global__ __launch_bounds__(PART_THREADS) __attribute__((amdgpu_waves_per_eu(4)
       recs[k].key = keys[k];
       recs[k].payload = pays[k];
     }
-    staged_scatter<H, P>(recs, act, dr, s_cnt, s_delta, s_stage, s_scratch, n_digits, dg, run, out);
+    staged_scatter<H, P>(recs, act, dr, s_cnt, s_delta, s_stage, s_scratch, n_digits, dg, nd, run, out);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Pass 1 of a side with a fused TableScan, in two streaming kernels:
+//   part1_compact: evaluates the predicate and reads the join column of every row of a span once, writes the span's
+//     matching rows as records in row order into the span's own slot of a gapped buffer (slot = span * SPAN
+//     records; no prefix across spans is needed), counts them per digit (histogram rows as part1_hist, plus the scan
+//     row) and per span (span_count). A matching row whose join key is NULL (and does not take part: no keep_nulls)
+//     is still a scan match; its record carries NULL_FLAG in the payload and no digit.
+//   part1_spread: reads each span's records back (coalesced), writes the scan's output (chunk offsets, in row order)
+//     and scatters the taking-part records by digit exactly as part1_scatter would (stable LDS-staged scatter).
+// Traffic per matched row is one 8-byte record more than the single fused scatter, but both kernels are plain
+// streams, while the single kernel's load -> rank -> stage -> store chain per tile left it latency-bound.
+// ------------------------------------------------------------------------------------------------------------
+constexpr uint32_t NULL_FLAG = 0x80000000u;  // payloads of filtered sides are row indexes < 2^31
+
+template <typename T, typename H, int LP, int FK>
+__global__ __launch_bounds__(PART_THREADS) void part1_compact(Side s, Digit dg, uint32_t n_digits,
+                                                             uint32_t* __restrict__ hist, uint32_t* __restrict__ span_count,
+                                                             Rec<H, uint32_t>* __restrict__ gap_out) {
+  __shared__ uint32_t s_hist[257];
+  __shared__ uint32_t s_sc[WAVE + 1];
+  const uint64_t tile = xcd_tile(blockIdx.x, gridDim.x);  // span
+  for (int i = threadIdx.x; i < 257; i += PART_THREADS) s_hist[i] = 0;
+  const uint32_t c = s.tile_chunk[tile];
+  const SrcChunk ch = s.chunks[c];
+  const uint32_t base = static_cast<uint32_t>(tile - s.chunk_tile_begin[c]) * (s.sub * PART_TILE);
+  const uint32_t n_sub = min(s.sub, (ch.size - base + PART_TILE - 1) / PART_TILE);
+  const int w = threadIdx.x / WAVE, lane = __lane_id();
+  Rec<H, uint32_t>* out = gap_out + tile * (static_cast<uint64_t>(s.sub) * PART_TILE);
+  uint32_t run = 0;
+  __syncthreads();
+#pragma unroll 1
+  for (uint32_t j = 0; j < n_sub; ++j) {
+    const uint32_t rb = base + j * PART_TILE + w * WAVE_SPAN;
+    const uint32_t m = filter_items<FK>(s, c, rb);
+    H keys[PART_ITEMS];
+    uint32_t pays[PART_ITEMS];
+    const uint32_t act = load_items<T, H, uint32_t, LP>(s, ch, rb, keys, pays) & m;
+#pragma unroll
+    for (int k = 0; k < PART_ITEMS; ++k)
+      if ((act >> k) & 1u) atomicAdd(&s_hist[digit_of<H>(dg, keys[k])], 1u);
+    // row-order compaction of the matches: (wave, item) ballot counts -> prefix -> lane rank
+#pragma unroll
+    for (int k = 0; k < PART_ITEMS; ++k) {
+      const uint64_t b = __ballot((m >> k) & 1u);
+      if (lane == 0) s_sc[w * PART_ITEMS + k] = static_cast<uint32_t>(__popcll(b));
+    }
+    __syncthreads();
+    if (threadIdx.x < WAVE) {
+      const uint32_t v = s_sc[threadIdx.x];
+      const uint32_t incl = wave_inclusive_sum(v);
+      s_sc[threadIdx.x] = incl - v;
+      if (threadIdx.x == WAVE - 1) s_sc[WAVE] = incl;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PART_ITEMS; ++k) {
+      const uint64_t b = __ballot((m >> k) & 1u);
+      if ((m >> k) & 1u) {
+        Rec<H, uint32_t> r;
+        r.key = keys[k];
+        r.payload = pays[k] | (((act >> k) & 1u) ? 0u : NULL_FLAG);
+        out[run + s_sc[w * PART_ITEMS + k] + static_cast<uint32_t>(__popcll(b & lanemask_lt()))] = r;
+      }
+    }
+    run += s_sc[WAVE];
+    __syncthreads();  // s_sc is rewritten by the next tile
+  }
+  for (uint32_t d = threadIdx.x; d < n_digits; d += PART_THREADS) hist[d * s.n_tiles + tile] = s_hist[d];
+  if (threadIdx.x == 0) {
+    hist[n_digits * s.n_tiles + tile] = run;
+    span_count[tile] = run;
+  }
+}
+
+template <typename H>
+__global__ __launch_bounds__(PART_THREADS) void part1_spread(Side s, Digit dg, NextDigit nd, int dbits,
+                                                            uint32_t n_digits, const uint32_t* __restrict__ offsets,
+                                                            const uint32_t* __restrict__ span_count,
+                                                            const Rec<H, uint32_t>* __restrict__ gap_in,
+                                                            Rec<H, uint32_t>* __restrict__ out) {
+  __shared__ uint32_t s_cnt[PART_WAVES][256];
+  __shared__ uint32_t s_delta[256];
+  __shared__ uint32_t s_scratch[PART_WAVES + 1];
+  __shared__ Rec<H, uint32_t> s_stage[PART_TILE];
+  const uint64_t tile = xcd_tile(blockIdx.x, gridDim.x);  // span
+  const uint32_t n = span_count[tile];
+  const uint32_t c = s.tile_chunk[tile];
+  const uint32_t row0 = static_cast<uint32_t>(s.chunks[c].row_begin);  // payload -> chunk offset
+  const Rec<H, uint32_t>* in = gap_in + tile * (static_cast<uint64_t>(s.sub) * PART_TILE);
+  const int w = threadIdx.x / WAVE;
+  uint32_t run = threadIdx.x < n_digits ? offsets[threadIdx.x * s.n_tiles + tile] : 0u;
+  const uint32_t srun = offsets[n_digits * s.n_tiles + tile] - offsets[n_digits * s.n_tiles];
+  uint64_t* s_mask = reinterpret_cast<uint64_t*>(s_stage) + w * 256;  // ranking masks alias the staging area
+  const uint32_t n_sub = (n + PART_TILE - 1) / PART_TILE;
+#pragma unroll 1
+  for (uint32_t j = 0; j < n_sub; ++j) {
+    if (j) __syncthreads();  // the previous tile's write-out has read s_stage
+    clear_wave_counts(s_cnt[w]);
+    clear_wave_masks(s_mask);
+    Rec<H, uint32_t> recs[PART_ITEMS];
+    uint32_t dr[PART_ITEMS];
+    uint32_t act = 0;
+    const uint32_t r0 = j * PART_TILE + w * WAVE_SPAN + __lane_id();
+#pragma unroll
+    for (int k = 0; k < PART_ITEMS; ++k) recs[k] = in[min(r0 + k * WAVE, n - 1)];  // unconditional (see load_items)
+#pragma unroll
+    for (int k = 0; k < PART_ITEMS; ++k) {
+      const uint32_t i = r0 + k * WAVE;
+      if (i < n) {
+        if (s.scan_out != nullptr) s.scan_out[srun + i] = (recs[k].payload & ~NULL_FLAG) - row0;
+        if (!(recs[k].payload & NULL_FLAG)) act |= 1u << k;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < PART_ITEMS; ++k) {
+      const bool a = (act >> k) & 1u;
+      const uint32_t dig = a ? digit_of<H>(dg, recs[k].key) : 0u;
+      dr[k] = (dig << 24) | wave_rank_lds(dig, a, s_mask, s_cnt[w]);
+    }
+    staged_scatter<H, uint32_t>(recs, act, dr, s_cnt, s_delta, s_stage, s_scratch, n_digits, dg, nd, run, out);
   }
 }
 
@@ -495,8 +710,9 @@ template <typename H, typename P>
 __global__ __launch_bounds__(PART_THREADS) void part2_hist(Segs sg, Digit dg, uint32_t n_digits,
                                                           const Rec<H, P>* __restrict__ in, uint32_t* __restrict__ hist) {
   __shared__ uint32_t s_hist[256];
-  const uint64_t tile = xcd_tile(blockIdx.x, gridDim.x);
-  if (tile >= sg.seg_tile_begin[sg.n_segs]) return;
+  const uint32_t n_real = static_cast<uint32_t>(sg.seg_tile_begin[sg.n_segs]);
+  if (blockIdx.x >= n_real) return;
+  const uint64_t tile = xcd_tile(blockIdx.x, n_real);  // XCD-contiguous over the tiles that exist
   for (int i = threadIdx.x; i < 256; i += PART_THREADS) s_hist[i] = 0;
   __syncthreads();
   const uint32_t sgi = sg.tile_seg[tile];
@@ -523,16 +739,17 @@ __global__ __launch_bounds__(PART_THREADS) void part2_hist(Segs sg, Digit dg, ui
 }
 
 template <typename H, typename P>
-__global__ __launch_bounds__(PART_THREADS) void part2_scatter(Segs sg, Digit dg, int dbits, uint32_t n_digits,
-                                                             const Rec<H, P>* __restrict__ in,
+__global__ __launch_bounds__(PART_THREADS) void part2_scatter(Segs sg, Digit dg, NextDigit nd, int dbits,
+                                                             uint32_t n_digits, const Rec<H, P>* __restrict__ in,
                                                              const uint32_t* __restrict__ offsets,
                                                              Rec<H, P>* __restrict__ out) {
   __shared__ uint32_t s_cnt[PART_WAVES][256];
   __shared__ uint32_t s_delta[256];
   __shared__ uint32_t s_scratch[PART_WAVES + 1];
   __shared__ Rec<H, P> s_stage[PART_TILE];
-  const uint64_t tile = xcd_tile(blockIdx.x, gridDim.x);  // span
-  if (tile >= sg.seg_tile_begin[sg.n_segs]) return;
+  const uint32_t n_real = static_cast<uint32_t>(sg.seg_tile_begin[sg.n_segs]);
+  if (blockIdx.x >= n_real) return;
+  const uint64_t tile = xcd_tile(blockIdx.x, n_real);  // span; XCD-contiguous over the tiles that exist
   const uint32_t sgi = sg.tile_seg[tile];
   const uint32_t t_in = static_cast<uint32_t>(tile - sg.seg_tile_begin[sgi]);
   uint32_t b0, b1, stride, toff;
@@ -563,13 +780,64 @@ __global__ __launch_bounds__(PART_THREADS) void part2_scatter(Segs sg, Digit dg,
       const uint32_t dig = a ? digit_of<H>(dg, recs[k].key) : 0u;
       dr[k] = (dig << 24) | wave_rank_lds(dig, a, s_mask, s_cnt[w]);
     }
-    staged_scatter<H, P>(recs, act, dr, s_cnt, s_delta, s_stage, s_scratch, n_digits, dg, run, out);
+    staged_scatter<H, P>(recs, act, dr, s_cnt, s_delta, s_stage, s_scratch, n_digits, dg, nd, run, out);
+  }
+}
+
+// part2_hist from the digit bytes the previous pass wrote beside the records (1 B per record instead of the record
+// and its hash); same tiles and histogram layout as part2_hist.
+static __global__ __launch_bounds__(PART_THREADS) void part2_hist_bytes(Segs sg, uint32_t n_digits,
+                                                                const uint8_t* __restrict__ dig,
+                                                                uint32_t* __restrict__ hist) {
+  __shared__ uint32_t s_hist[256];
+  const uint32_t n_real = static_cast<uint32_t>(sg.seg_tile_begin[sg.n_segs]);
+  if (blockIdx.x >= n_real) return;
+  const uint64_t tile = xcd_tile(blockIdx.x, n_real);  // XCD-contiguous over the tiles that exist
+  for (int i = threadIdx.x; i < 256; i += PART_THREADS) s_hist[i] = 0;
+  __syncthreads();
+  const uint32_t sgi = sg.tile_seg[tile];
+  const uint32_t t_in = static_cast<uint32_t>(tile - sg.seg_tile_begin[sgi]);
+  uint32_t b0, b1, stride, toff;
+  uint64_t hbase;
+  seg_geometry(sg, sgi, n_digits, &b0, &b1, &hbase, &stride, &toff);
+  const int w = threadIdx.x / WAVE;
+  const uint32_t sb = b0 + t_in * (sg.sub * PART_TILE);
+  const uint32_t n_sub = min(sg.sub, (b1 - sb + PART_TILE - 1) / PART_TILE);
+#pragma unroll 1
+  for (uint32_t j = 0; j < n_sub; ++j) {
+    const uint32_t r0 = sb + j * PART_TILE + w * WAVE_SPAN + __lane_id();
+    uint32_t d[PART_ITEMS];
+#pragma unroll
+    for (int k = 0; k < PART_ITEMS; ++k) d[k] = dig[min(r0 + k * WAVE, b1 - 1)];
+#pragma unroll
+    for (int k = 0; k < PART_ITEMS; ++k)
+      if (r0 + k * WAVE < b1) atomicAdd(&s_hist[d[k]], 1u);
+  }
+  __syncthreads();
+  for (uint32_t d = threadIdx.x; d < n_digits; d += PART_THREADS) hist[hbase + d * stride + toff + t_in] = s_hist[d];
+}
+
+// After the exclusive scan of a fused-scan histogram (part1_compact: (n_digits + 1) rows over n_tiles spans): records = first
+// entry of the scan row, matches = grand total - records; chunk c's matches start at the scan-row prefix of its first
+// span (chunks without spans take the next chunk's start). Writes the record total (for the bucket bounds), the
+// scan's per-chunk begins (n_chunks + 1, in matches) and its total.
+static __global__ void fused_scan_totals(const uint32_t* __restrict__ offsets, uint64_t n_tiles, uint32_t n_digits,
+                                  const uint64_t* __restrict__ grand_total, const uint64_t* __restrict__ chunk_tile_begin,
+                                  uint32_t n_chunks, uint64_t* __restrict__ record_total,
+                                  uint64_t* __restrict__ chunk_begin) {
+  const uint64_t row = static_cast<uint64_t>(n_digits) * n_tiles;
+  const uint64_t records = n_tiles ? offsets[row] : 0u;
+  for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c <= n_chunks; c += gridDim.x * blockDim.x) {
+    const uint64_t t = chunk_tile_begin[c];
+    const uint64_t v = t < n_tiles ? offsets[row + t] : *grand_total;
+    if (chunk_begin != nullptr) chunk_begin[c] = v - records;
+    if (c == 0) *record_total = records;
   }
 }
 
 // Bucket bounds after the pass from column chunks (histogram laid out digit-major over tiles):
 // seg_begin[d] = offsets[d * n_tiles] (output position of the first digit-d record), seg_begin[n_digits] = total.
-__global__ void seg_bounds(const uint32_t* __restrict__ offsets, uint64_t n_tiles, uint32_t n_segs,
+static __global__ void seg_bounds(const uint32_t* __restrict__ offsets, uint64_t n_tiles, uint32_t n_segs,
                            const uint64_t* __restrict__ total, uint32_t* __restrict__ seg_begin) {
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p < n_segs) seg_begin[p] = n_tiles == 0 ? 0u : offsets[p * n_tiles];
@@ -577,7 +845,7 @@ __global__ void seg_bounds(const uint32_t* __restrict__ offsets, uint64_t n_tile
 }
 
 // Tiles of every segment of a record pass (counts, then an exclusive scan and widen_prefix give seg_tile_begin).
-__global__ void seg_tile_counts(const uint32_t* __restrict__ seg_begin, const uint32_t* __restrict__ seg_end,
+static __global__ void seg_tile_counts(const uint32_t* __restrict__ seg_begin, const uint32_t* __restrict__ seg_end,
                                 uint32_t n_segs, uint32_t span, uint32_t* __restrict__ counts) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_segs; i += gridDim.x * blockDim.x) {
     const uint32_t b1 = seg_end ? seg_end[i] : seg_begin[i + 1];
@@ -585,7 +853,7 @@ __global__ void seg_tile_counts(const uint32_t* __restrict__ seg_begin, const ui
   }
 }
 
-__global__ void widen_prefix(const uint32_t* __restrict__ excl, uint32_t n, const uint64_t* __restrict__ total,
+static __global__ void widen_prefix(const uint32_t* __restrict__ excl, uint32_t n, const uint64_t* __restrict__ total,
                              uint64_t* __restrict__ out) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += gridDim.x * blockDim.x)
     out[i] = i < n ? static_cast<uint64_t>(excl[i]) : *total;
@@ -601,7 +869,7 @@ struct Groups {
   const uint32_t* out_begin;
 };
 
-__global__ void pass_bounds(const uint32_t* __restrict__ offsets, Segs sg, Groups gr, uint32_t n_groups,
+static __global__ void pass_bounds(const uint32_t* __restrict__ offsets, Segs sg, Groups gr, uint32_t n_groups,
                             uint32_t n_digits, const uint64_t* __restrict__ total, uint32_t* __restrict__ bounds) {
   const uint64_t n = static_cast<uint64_t>(n_groups) * n_digits;
   for (uint64_t p = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; p <= n;
@@ -718,10 +986,10 @@ __global__ __launch_bounds__(SCAN_T) void exclusive_scan_u32(const uint32_t* __r
 // partition is one pass) with all loads in flight, matched, counted, and - once one atomic add has reserved the
 // partition's output range - written without re-reading them.
 // ------------------------------------------------------------------------------------------------------------
+// join_partition runs one 1024-thread workgroup per partition, two per CU. (Measured on MI355X at SF100: 256-thread
+// workgroups, four per CU by LDS, took 4.4 ms against 1.86 ms - the per-partition phases got longer, not overlapped.)
 constexpr int JOIN_THREADS = 1024;
-constexpr int JOIN_WAVES = JOIN_THREADS / WAVE;
-constexpr int JP_PER = 4;                          // probe records per thread per pass
-constexpr int JP_PASS = JP_PER * JOIN_THREADS;     // 4096
+constexpr int JP_PER = 4;                          // probe records per thread per pass (1024-thread workgroups)
 constexpr uint32_t LDS_MAX_ROWS = 0xFFFFu;         // entry indexes and counts of one table fit 16 bits
 
 struct JoinDesc {
@@ -803,41 +1071,44 @@ __device__ __forceinline__ uint32_t bucket_of(H key, uint32_t NB) {
   return static_cast<uint32_t>((static_cast<uint64_t>(slot_hash<H>(key)) * NB) >> 32);
 }
 
-// Builds the LDS table over build records [b0, b0 + n) (n <= LDS_MAX_ROWS). Each thread holds up to BUILD_PER
+// Builds the LDS table over build records [b0, b0 + n) (n <= LDS_MAX_ROWS). Each thread holds up to build_per<NT>()
 // records whose loads are all in flight together - the first batch's while the bucket sizes are being cleared. A
 // partition larger than one batch re-reads its records (from L2) for the second counting-sort pass. Ends with a
 // barrier.
-constexpr int BUILD_PER = 3;  // >= the largest 4-byte-key table in the default LDS budget / JOIN_THREADS
-template <typename H, typename P>
+template <int NT>
+constexpr int build_per() {  // >= the largest 4-byte-key table in the default LDS budget / NT
+  return NT >= 1024 ? 3 : 14;
+}
+template <typename H, typename P, int NT>
 __device__ __forceinline__ void build_table(const BTable<H, P>& t, const Rec<H, P>* __restrict__ build, uint32_t b0,
                                             uint32_t n, uint32_t* s_scratch) {
-  Rec<H, P> r[BUILD_PER];
+  Rec<H, P> r[build_per<NT>()];
   auto load_batch = [&](uint32_t base) {
 #pragma unroll
-    for (int q = 0; q < BUILD_PER; ++q) {
-      const uint32_t i = base + q * JOIN_THREADS + threadIdx.x;
+    for (int q = 0; q < build_per<NT>(); ++q) {
+      const uint32_t i = base + q * NT + threadIdx.x;
       if (i < n) r[q] = build[b0 + i];
     }
   };
-  constexpr uint32_t BATCH = BUILD_PER * JOIN_THREADS;
+  constexpr uint32_t BATCH = build_per<NT>() * NT;
   load_batch(0);
-  for (uint32_t i = threadIdx.x; i < t.NB; i += JOIN_THREADS) t.end[i] = 0;
+  for (uint32_t i = threadIdx.x; i < t.NB; i += NT) t.end[i] = 0;
   __syncthreads();
   // pass 1: bucket sizes
   for (uint32_t base = 0; base < n; base += BATCH) {
     if (base) load_batch(base);
 #pragma unroll
-    for (int q = 0; q < BUILD_PER; ++q)
-      if (base + q * JOIN_THREADS + threadIdx.x < n) atomicAdd(&t.end[bucket_of<H>(r[q].key, t.NB)], 1u);
+    for (int q = 0; q < build_per<NT>(); ++q)
+      if (base + q * NT + threadIdx.x < n) atomicAdd(&t.end[bucket_of<H>(r[q].key, t.NB)], 1u);
   }
   __syncthreads();
   // bucket sizes -> bucket starts (each thread owns a contiguous run of buckets)
-  const uint32_t per = (t.NB + JOIN_THREADS - 1) / JOIN_THREADS;
+  const uint32_t per = (t.NB + NT - 1) / NT;
   const uint32_t lo = threadIdx.x * per, hi = min(lo + per, t.NB);
   uint32_t sum = 0;
   for (uint32_t i = lo; i < hi; ++i) sum += t.end[i];
   uint32_t total;
-  uint32_t run = block_exclusive_sum<JOIN_THREADS>(sum, s_scratch, &total);
+  uint32_t run = block_exclusive_sum<NT>(sum, s_scratch, &total);
   for (uint32_t i = lo; i < hi; ++i) {
     const uint32_t c = t.end[i];
     t.end[i] = run;
@@ -848,8 +1119,8 @@ __device__ __forceinline__ void build_table(const BTable<H, P>& t, const Rec<H, 
   for (uint32_t base = 0; base < n; base += BATCH) {
     if (base || n > BATCH) load_batch(base);
 #pragma unroll
-    for (int q = 0; q < BUILD_PER; ++q) {
-      if (base + q * JOIN_THREADS + threadIdx.x < n) {
+    for (int q = 0; q < build_per<NT>(); ++q) {
+      if (base + q * NT + threadIdx.x < n) {
         const uint32_t pos = atomicAdd(&t.end[bucket_of<H>(r[q].key, t.NB)], 1u);
         t.ents[pos] = r[q];
       }
@@ -901,7 +1172,7 @@ __device__ __forceinline__ uint64_t allocate_output(const JoinDesc& d, uint32_t 
 // Output offsets of one pass's records (k, thread): records (k' < k) first, then waves (w' < w), then lanes.
 // Leaves per-(k, wave) offsets in s_tot (valid until the caller's next barrier) and returns the pass total; a
 // record's position is then record_pos(e, k, s_tot).
-template <int JP, typename EF>
+template <int JP, int NT, typename EF>
 __device__ __forceinline__ uint32_t pass_offsets(EF e_of, uint32_t* s_tot) {
   const int lane = __lane_id();
   const int w = threadIdx.x / WAVE;
@@ -910,11 +1181,11 @@ __device__ __forceinline__ uint32_t pass_offsets(EF e_of, uint32_t* s_tot) {
     const uint32_t e = e_of(k);
     // common case (unique build keys): every record emits 0 or 1 pairs -> a ballot count is the wave total
     const uint32_t total = __ballot(e > 1) ? wave_sum(e) : static_cast<uint32_t>(__popcll(__ballot(e != 0)));
-    if (lane == 0) s_tot[k * JOIN_WAVES + w] = total;
+    if (lane == 0) s_tot[k * (NT / WAVE) + w] = total;
   }
   __syncthreads();
-  if (threadIdx.x < WAVE) {  // exclusive prefix over the JP * JOIN_WAVES wave totals, (k, w) order
-    constexpr int N = JP * JOIN_WAVES;
+  if (threadIdx.x < WAVE) {  // exclusive prefix over the JP * (NT / WAVE) wave totals, (k, w) order
+    constexpr int N = JP * (NT / WAVE);
     constexpr int PER_LANE = (N + WAVE - 1) / WAVE;
     uint32_t v[PER_LANE], sum = 0;
 #pragma unroll
@@ -934,14 +1205,14 @@ __device__ __forceinline__ uint32_t pass_offsets(EF e_of, uint32_t* s_tot) {
     if (lane == WAVE - 1) s_tot[N] = incl;
   }
   __syncthreads();
-  return s_tot[JP * JOIN_WAVES];
+  return s_tot[JP * (NT / WAVE)];
 }
 
-template <int JP>
+template <int JP, int NT>
 __device__ __forceinline__ uint32_t record_pos(uint32_t e, int k, const uint32_t* s_tot) {
   const uint32_t before = __ballot(e > 1) ? wave_inclusive_sum(e) - e
                                           : static_cast<uint32_t>(__popcll(__ballot(e != 0) & lanemask_lt()));
-  return s_tot[k * JOIN_WAVES + threadIdx.x / WAVE] + before;
+  return s_tot[k * (NT / WAVE) + threadIdx.x / WAVE] + before;
 }
 
 // Writes the build rows with `key` among build records [b0, b0 + n) in order, each paired with prow.
@@ -962,7 +1233,7 @@ __device__ __forceinline__ void write_duplicates(const JoinDesc& d, const Rec<H,
 
 // A partition whose build side fits one LDS table (the common case): the table is built once and every probe
 // record's (count, first entry) stays in registers from counting to writing.
-template <typename H, typename P, bool TRACE, int JP>
+template <typename H, typename P, bool TRACE, int JP, int NT>
 __device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t p, unsigned char* smem,
                                                     const Rec<H, P>* __restrict__ build,
                                                     const Rec<H, P>* __restrict__ probe, hy_row_id* __restrict__ out_build,
@@ -974,11 +1245,11 @@ __device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t 
   const uint32_t pb = d.probe_begin[p], np = d.probe_begin[p + 1] - pb;
   const int mode = d.mode;
   const BTable<H, P> t = table_at<H, P>(smem, nb);
-  build_table<H, P>(t, build, bb, nb, s_tot);
+  build_table<H, P, NT>(t, build, bb, nb, s_tot);
   trace_stamp<TRACE>(d, p, 1);
 
   // Per probe record only its payload and match info (count << 16 | first entry) stay in registers.
-  constexpr uint32_t JP_PASS_ = JP * JOIN_THREADS;
+  constexpr uint32_t JP_PASS_ = JP * NT;
   const uint32_t n_pass = (np + JP_PASS_ - 1) / JP_PASS_;
   P ppay[JP];
   uint32_t pinfo[JP];
@@ -986,12 +1257,12 @@ __device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t 
     Rec<H, P> pr[JP];
 #pragma unroll
     for (int k = 0; k < JP; ++k) {
-      const uint32_t j = pass * JP_PASS_ + k * JOIN_THREADS + threadIdx.x;
+      const uint32_t j = pass * JP_PASS_ + k * NT + threadIdx.x;
       if (j < np) pr[k] = probe[pb + j];
     }
 #pragma unroll
     for (int k = 0; k < JP; ++k) {
-      const uint32_t j = pass * JP_PASS_ + k * JOIN_THREADS + threadIdx.x;
+      const uint32_t j = pass * JP_PASS_ + k * NT + threadIdx.x;
       ppay[k] = pr[k].payload;
       pinfo[k] = j < np ? table_lookup<H, P>(t, pr[k].key) : 0u;
     }
@@ -1002,13 +1273,13 @@ __device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t 
     load_and_match(pass);
 #pragma unroll
     for (int k = 0; k < JP; ++k) {
-      const uint32_t j = pass * JP_PASS_ + k * JOIN_THREADS + threadIdx.x;
+      const uint32_t j = pass * JP_PASS_ + k * NT + threadIdx.x;
       if (j < np) my += emitted_for(mode, info_count(pinfo[k]));
     }
   }
   trace_stamp<TRACE>(d, p, 2);
   uint32_t part_total;
-  block_exclusive_sum<JOIN_THREADS>(my, s_tot, &part_total);
+  block_exclusive_sum<NT>(my, s_tot, &part_total);
   const uint64_t obase = allocate_output(d, p, part_total, part_out_begin, part_out_count, s_base);
   trace_stamp<TRACE>(d, p, 3);
   if (obase + part_total > d.capacity) return;
@@ -1017,16 +1288,16 @@ __device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t 
   for (uint32_t pass = 0; pass < n_pass; ++pass) {
     if (n_pass > 1) load_and_match(pass);  // a single pass still holds its records and matches in registers
     auto e_of = [&](int k) {
-      const uint32_t j = pass * JP_PASS_ + k * JOIN_THREADS + threadIdx.x;
+      const uint32_t j = pass * JP_PASS_ + k * NT + threadIdx.x;
       return j < np ? emitted_for(mode, info_count(pinfo[k])) : 0u;
     };
-    const uint32_t pass_total = pass_offsets<JP>(e_of, s_tot);
+    const uint32_t pass_total = pass_offsets<JP, NT>(e_of, s_tot);
 #pragma unroll
     for (int k = 0; k < JP; ++k) {
       const uint32_t c = info_count(pinfo[k]);
-      const uint32_t j = pass * JP_PASS_ + k * JOIN_THREADS + threadIdx.x;
+      const uint32_t j = pass * JP_PASS_ + k * NT + threadIdx.x;
       const uint32_t e = j < np ? emitted_for(mode, c) : 0u;
-      const uint64_t o = run + record_pos<JP>(e, k, s_tot);
+      const uint64_t o = run + record_pos<JP, NT>(e, k, s_tot);
       if (e == 0) continue;
       const hy_row_id prow = map_row(d.probe_map, ppay[k]);
       if (mode == HY_JOIN_SEMI || mode == HY_JOIN_ANTI) {
@@ -1049,7 +1320,7 @@ __device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t 
 // A partition with more build rows than one LDS table holds (skewed keys): consecutive sub-tables of L build rows.
 // Counts are summed over the sub-tables; matches are written sub-table by sub-table, i.e. in build order. Each
 // probe pass rebuilds the sub-tables twice (count, write), a cost only skewed partitions pay.
-template <typename H, typename P, bool TRACE>
+template <typename H, typename P, bool TRACE, int NT>
 __device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t p, unsigned char* smem,
                                                   const Rec<H, P>* __restrict__ build, const Rec<H, P>* __restrict__ probe,
                                                   hy_row_id* __restrict__ out_build, hy_row_id* __restrict__ out_probe,
@@ -1061,9 +1332,9 @@ __device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t
   const uint32_t L = d.lds_max_build;
   const uint32_t n_sub = (nb + L - 1) / L;
   const int mode = d.mode;
-  constexpr int JS = 2;  // probe records per thread per pass (fewer than JP_PER: keeps this rare path's registers
-                        // within the fast path's budget)
-  constexpr uint32_t JS_PASS = JS * JOIN_THREADS;
+  constexpr int JS = NT >= 1024 ? 2 : 8;  // probe records per thread per pass (few: keeps this rare path's
+                                         // registers within the fast path's budget)
+  constexpr uint32_t JS_PASS = JS * NT;
   const uint32_t n_pass = (np + JS_PASS - 1) / JS_PASS;
 
   Rec<H, P> pr[JS];
@@ -1071,17 +1342,17 @@ __device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t
   auto load_and_count = [&](uint32_t pass) {
 #pragma unroll
     for (int k = 0; k < JS; ++k) {
-      const uint32_t j = pass * JS_PASS + k * JOIN_THREADS + threadIdx.x;
+      const uint32_t j = pass * JS_PASS + k * NT + threadIdx.x;
       if (j < np) pr[k] = probe[pb + j];
       pcn[k] = 0;
     }
     for (uint32_t sub = 0; sub < n_sub; ++sub) {
       const uint32_t b0 = bb + sub * L, n = (sub + 1 == n_sub) ? nb - sub * L : L;
       const BTable<H, P> t = table_at<H, P>(smem, n);
-      build_table<H, P>(t, build, b0, n, s_tot);
+      build_table<H, P, NT>(t, build, b0, n, s_tot);
 #pragma unroll
       for (int k = 0; k < JS; ++k) {
-        const uint32_t j = pass * JS_PASS + k * JOIN_THREADS + threadIdx.x;
+        const uint32_t j = pass * JS_PASS + k * NT + threadIdx.x;
         if (j < np) pcn[k] += info_count(table_lookup<H, P>(t, pr[k].key));
       }
       __syncthreads();  // before the next table overwrites LDS
@@ -1093,13 +1364,13 @@ __device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t
     load_and_count(pass);
 #pragma unroll
     for (int k = 0; k < JS; ++k) {
-      const uint32_t j = pass * JS_PASS + k * JOIN_THREADS + threadIdx.x;
+      const uint32_t j = pass * JS_PASS + k * NT + threadIdx.x;
       if (j < np) my += emitted_for(mode, pcn[k]);
     }
   }
   trace_stamp<TRACE>(d, p, 2);
   uint32_t part_total;
-  block_exclusive_sum<JOIN_THREADS>(my, s_tot, &part_total);
+  block_exclusive_sum<NT>(my, s_tot, &part_total);
   const uint64_t obase = allocate_output(d, p, part_total, part_out_begin, part_out_count, s_base);
   trace_stamp<TRACE>(d, p, 3);
   if (obase + part_total > d.capacity) return;
@@ -1108,15 +1379,15 @@ __device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t
   for (uint32_t pass = 0; pass < n_pass; ++pass) {
     if (n_pass > 1) load_and_count(pass);
     auto e_of = [&](int k) {
-      const uint32_t j = pass * JS_PASS + k * JOIN_THREADS + threadIdx.x;
+      const uint32_t j = pass * JS_PASS + k * NT + threadIdx.x;
       return j < np ? emitted_for(mode, pcn[k]) : 0u;
     };
-    const uint32_t pass_total = pass_offsets<JS>(e_of, s_tot);
+    const uint32_t pass_total = pass_offsets<JS, NT>(e_of, s_tot);
     uint32_t pos[JS];
 #pragma unroll
     for (int k = 0; k < JS; ++k) {
       const uint32_t e = e_of(k);
-      pos[k] = record_pos<JS>(e, k, s_tot);
+      pos[k] = record_pos<JS, NT>(e, k, s_tot);
       if (e == 0) continue;
       if (mode == HY_JOIN_SEMI || mode == HY_JOIN_ANTI) {
         out_probe[run + pos[k]] = map_row(d.probe_map, pr[k].payload);
@@ -1130,10 +1401,10 @@ __device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t
       for (uint32_t sub = 0; sub < n_sub; ++sub) {
         const uint32_t b0 = bb + sub * L, n = (sub + 1 == n_sub) ? nb - sub * L : L;
         const BTable<H, P> t = table_at<H, P>(smem, n);
-        build_table<H, P>(t, build, b0, n, s_tot);
+        build_table<H, P, NT>(t, build, b0, n, s_tot);
 #pragma unroll
         for (int k = 0; k < JS; ++k) {
-          const uint32_t j = pass * JS_PASS + k * JOIN_THREADS + threadIdx.x;
+          const uint32_t j = pass * JS_PASS + k * NT + threadIdx.x;
           if (j >= np || pcn[k] == 0) continue;
           const uint32_t info = table_lookup<H, P>(t, pr[k].key);
           const uint32_t cnt = info_count(info);
@@ -1155,41 +1426,40 @@ __device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t
   }
 }
 
-template <typename H, typename P, bool TRACE, int JP>
-__global__ __launch_bounds__(JOIN_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void join_partition(JoinDesc d, const Rec<H, P>* __restrict__ build,
-                                                               const Rec<H, P>* __restrict__ probe,
-                                                               hy_row_id* __restrict__ out_build,
-                                                               hy_row_id* __restrict__ out_probe,
-                                                               uint64_t* __restrict__ part_out_begin,
-                                                               uint32_t* __restrict__ part_out_count) {
+template <typename H, typename P, bool TRACE, int JP, int NT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT >= 1024 ? 8 : 4, 8))) void join_partition(
+    JoinDesc d, const Rec<H, P>* __restrict__ build, const Rec<H, P>* __restrict__ probe,
+    hy_row_id* __restrict__ out_build, hy_row_id* __restrict__ out_probe, uint64_t* __restrict__ part_out_begin,
+    uint32_t* __restrict__ part_out_count) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ uint32_t s_tot[(JP > JP_PER ? JP : JP_PER) * JOIN_WAVES + 1];
+  constexpr int JS = NT >= 1024 ? 2 : 8;
+  __shared__ uint32_t s_tot[(JP > JS ? JP : JS) * (NT / WAVE) + 1];
   __shared__ uint64_t s_base;
   const uint32_t p = blockIdx.x;
   if (p >= d.n_parts) return;
   trace_stamp<TRACE>(d, p, 0);
   if (d.build_begin[p + 1] - d.build_begin[p] <= d.lds_max_build)
-    partition_one_table<H, P, TRACE, JP>(d, p, smem, build, probe, out_build, out_probe, part_out_begin, part_out_count, s_tot,
-                           &s_base);
+    partition_one_table<H, P, TRACE, JP, NT>(d, p, smem, build, probe, out_build, out_probe, part_out_begin,
+                                             part_out_count, s_tot, &s_base);
   else
-    partition_sub_tables<H, P, TRACE>(d, p, smem, build, probe, out_build, out_probe, part_out_begin, part_out_count, s_tot,
-                            &s_base);
+    partition_sub_tables<H, P, TRACE, NT>(d, p, smem, build, probe, out_build, out_probe, part_out_begin,
+                                          part_out_count, s_tot, &s_base);
   trace_stamp<TRACE>(d, p, 4);
 }
 
-__global__ void murmur_kernel_u32(const uint32_t* keys, uint64_t n, uint32_t seed, uint32_t* out) {
+static __global__ void murmur_kernel_u32(const uint32_t* keys, uint64_t n, uint32_t seed, uint32_t* out) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     out[i] = murmur2_u32(keys[i], seed);
 }
 
-__global__ void murmur_kernel_u64(const uint64_t* keys, uint64_t n, uint32_t seed, uint32_t* out) {
+static __global__ void murmur_kernel_u64(const uint64_t* keys, uint64_t n, uint32_t seed, uint32_t* out) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     out[i] = murmur2_u64(keys[i], seed);
 }
 
 // Dereference join outputs of a reference input through its per-chunk PosLists (write_output_columns,
 // join_hash.cpp:584-592): out[i] = row is NULL ? row : chunk_pos_lists[row.chunk_id][row.chunk_offset].
-__global__ void dereference_kernel(const hy_row_id* __restrict__ rows, uint64_t n,
+static __global__ void dereference_kernel(const hy_row_id* __restrict__ rows, uint64_t n,
                                    const hy_row_id* const* __restrict__ chunk_pos_lists, hy_row_id* __restrict__ out) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const hy_row_id r = rows[i];

@@ -39,28 +39,6 @@ struct ScanConst {
   T value;
 };
 
-template <typename T>
-__device__ __forceinline__ bool cmp_op(int op, T v, T c) {
-  switch (op) {
-    case HY_OP_EQ:
-      return v == c;
-    case HY_OP_NE:
-      return v != c;
-    case HY_OP_LT:
-      return v < c;
-    case HY_OP_LE:
-      return v <= c;
-    case HY_OP_GT:
-      return v > c;
-    case HY_OP_GE:
-      return v >= c;
-    case HY_OP_ALL:
-      return true;
-    default:
-      return false;
-  }
-}
-
 // Loads 16 consecutive elements of E bytes starting at element `first` (16-byte aligned), elements past `n`
 // are returned as garbage and masked by the caller.
 template <typename E>

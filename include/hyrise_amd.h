@@ -73,6 +73,14 @@ hy_status hy_kernel_stats_get(uint32_t index, const char** name, uint64_t* launc
  * entry, table built, probe counted, output offset known (look-back done), exit. Costs one scalar branch.
  */
 hy_status hy_debug_set_join_trace(uint64_t* device_trace);
+/*
+ * Measured HBM roofline (the denominator of the bench's roofline fraction): HY_PROBE_READ streams
+ * `bytes` from src (dst: a scratch buffer of 256 * 32 * 256 * 4 bytes, written only by a practically impossible
+ * branch); HY_PROBE_COPY copies `bytes` from src to dst (2 * bytes of traffic). 16-byte nontemporal accesses, four in
+ * flight per lane, a grid of up to 8192 workgroups. Launch only; time it with events on `stream`.
+ */
+enum { HY_PROBE_READ = 0, HY_PROBE_COPY = 1 };
+hy_status hy_stream_bandwidth_probe(const void* src, void* dst, uint64_t bytes, int32_t mode, hy_stream_t stream);
 /* Thread-local message of the last failing call. */
 const char* hy_last_error_message(void);
 /* Build identification ("gfx950 …"). */
@@ -264,6 +272,41 @@ hy_status hy_join_hash(const hy_join_side* build, const hy_join_side* probe, con
                        hy_row_id* out_build, hy_row_id* out_probe, uint64_t out_capacity, uint64_t* partition_begin,
                        uint32_t* partition_counts, hy_join_result* result, void* workspace, size_t workspace_bytes,
                        hy_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------------------------
+ * Fused TableScan -> JoinHash.
+ *
+ * The plan TableScan(T, col OP value) -> JoinHash(..., <scan output>, ...) (reference lqp_translator.cpp:169 / :330,
+ * table_scan.cpp:78-164 feeding join_hash.cpp:49-858) executed as one device pipeline: the scan predicate of a join
+ * side is evaluated inside the join's first radix pass, which reads the data table's chunks directly, so the scan's
+ * output is never re-read to gather the join column. The result is exactly that of the two operators:
+ *   - out_offsets / out_chunk_begin: the TableScan's output, chunk by chunk - the matching chunk offsets of chunk c
+ *     (ascending, base_table_scan_impl.hpp:50-63) at out_offsets[out_chunk_begin[c], out_chunk_begin[c + 1]); chunk c
+ *     of the side is an output chunk of the scan iff it has a match (table_scan.cpp:99), and its PosList is
+ *     {chunk_id of side chunk c, offset} for each offset;
+ *   - the join output (as hy_join_hash) with the filtered side's RowIDs naming rows of the DATA table, i.e. the
+ *     JoinHash output already dereferenced through the scan's PosLists (write_output_columns, join_hash.cpp:584-592).
+ * The side must be a data table (no PosLists); its chunks and the predicate chunks correspond one to one (the
+ * predicate column is another column of the same table). Either filter may be NULL (no scan on that side);
+ * out_offsets / out_chunk_begin may be NULL when only the join output is wanted.
+ * ------------------------------------------------------------------------------------------------------------- */
+typedef struct hy_join_filter {
+  const hy_scan_chunk* chunks;  /* HOST array, one per chunk of the side: the predicate column's chunk (op, search_vid
+                                   from the host dictionary rewrite exactly as for hy_table_scan; out_begin unused) */
+  int32_t value_type;           /* HY_TYPE_* of VALUE predicate chunks */
+  const void* constant;         /* HOST pointer to the constant of VALUE predicate chunks (type_cast<T>(value)) */
+  uint32_t* out_offsets;        /* device, capacity = side rows, or NULL */
+  uint64_t* out_chunk_begin;    /* device, n_chunks + 1 entries, or NULL */
+} hy_join_filter;
+
+hy_status hy_scan_join_hash_workspace_size(const hy_join_side* build, const hy_join_filter* build_filter,
+                                           const hy_join_side* probe, const hy_join_filter* probe_filter,
+                                           const hy_join_params* params, size_t* bytes);
+hy_status hy_scan_join_hash(const hy_join_side* build, const hy_join_filter* build_filter, const hy_join_side* probe,
+                            const hy_join_filter* probe_filter, const hy_join_params* params, hy_row_id* out_build,
+                            hy_row_id* out_probe, uint64_t out_capacity, uint64_t* partition_begin,
+                            uint32_t* partition_counts, hy_join_result* result, void* workspace,
+                            size_t workspace_bytes, hy_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------------------------
  * Distributed JoinHash (one process per GPU; an RCCL all-to-all of records between the two steps)

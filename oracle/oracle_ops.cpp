@@ -14,6 +14,7 @@
 #include <pybind11/stl.h>
 
 #include <array>
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <functional>
@@ -32,6 +33,28 @@ namespace py = pybind11;
 using namespace hyrise;
 
 namespace oracle {
+
+// The reference runs one JobTask per chunk (TableScan table_scan.cpp:92-159; JoinHash materialize / scatter
+// join_hash.cpp:237-280, :324-350) and one per radix partition (build :139-180, probe :377-463) on its scheduler's
+// workers. parallel_for(n, f) runs f(0..n-1) as such tasks on g_threads threads (1 = inline, the tests' default: the
+// reference runs inline without a scheduler, abstract_task.cpp:59-67). Only the bench's CPU baseline raises it.
+int g_threads = 1;
+
+template <typename F>
+void parallel_for(size_t n, F&& f) {
+  if (g_threads <= 1 || n <= 1) {
+    for (size_t i = 0; i < n; ++i) f(i);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  std::vector<std::thread> workers;
+  const size_t t = std::min<size_t>(static_cast<size_t>(g_threads), n);
+  for (size_t k = 0; k < t; ++k)
+    workers.emplace_back([&] {
+      for (size_t i; (i = next.fetch_add(1)) < n;) f(i);
+    });
+  for (auto& w : workers) w.join();
+}
 
 // ---------------------------------------------------------------------------------------------------------------
 // MurmurHash2, reference src/lib/utils/murmur_hash.cpp:21-75
@@ -261,9 +284,13 @@ std::shared_ptr<Table> table_scan(const std::shared_ptr<const Table>& in, Column
   if (cond == PredicateCondition::Between) Fail("Unsupported comparison type encountered");
   auto out = std::make_shared<Table>(in->column_definitions(), TableType::References);
   const DataType type = in->column_data_type(col);
-  for (ChunkID chunk_id = 0; chunk_id < in->chunk_count(); ++chunk_id) {
-    if (std::find(excluded.begin(), excluded.end(), chunk_id) != excluded.end()) continue;
+  // per-chunk jobs (table_scan.cpp:92-159); chunks are appended in input-chunk order as without a scheduler
+  std::vector<std::shared_ptr<PosList>> chunk_matches(in->chunk_count());
+  parallel_for(in->chunk_count(), [&](size_t ci) {
+    const ChunkID chunk_id = static_cast<ChunkID>(ci);
     auto matches = std::make_shared<PosList>();
+    chunk_matches[ci] = matches;
+    if (std::find(excluded.begin(), excluded.end(), chunk_id) != excluded.end()) return;
     if (!variant_is_null(value)) {
       const auto column = in->get_chunk(chunk_id)->get_column(col);
       if (const auto* rc = dynamic_cast<const ReferenceColumn*>(column.get())) {
@@ -283,6 +310,9 @@ std::shared_ptr<Table> table_scan(const std::shared_ptr<const Table>& in, Column
         scan_data_column(*column, type, cond, value, chunk_id, nullptr, *matches);
       }
     }
+  });
+  for (ChunkID chunk_id = 0; chunk_id < in->chunk_count(); ++chunk_id) {
+    const auto& matches = chunk_matches[chunk_id];
     if (matches->empty()) continue;
     ChunkColumns cols;
     if (in->type() == TableType::References) {
@@ -357,7 +387,8 @@ std::shared_ptr<Partition<T>> materialize_input(const std::shared_ptr<const Tabl
     off += in->get_chunk(c)->get_column(col)->size();
   }
   histograms.assign(in->chunk_count(), std::vector<size_t>(num_partitions, 0));
-  for (ChunkID chunk_id = 0; chunk_id < in->chunk_count(); ++chunk_id) {
+  parallel_for(in->chunk_count(), [&](size_t ci) {  // per-chunk jobs, join_hash.cpp:237-280
+    const ChunkID chunk_id = static_cast<ChunkID>(ci);
     auto it = elements->begin() + chunk_offsets[chunk_id];
     auto& hist = histograms[chunk_id];
     const auto column = in->get_chunk(chunk_id)->get_column(col);
@@ -371,7 +402,7 @@ std::shared_ptr<Partition<T>> materialize_input(const std::shared_ptr<const Tabl
       }
       if (is_ref) ref_off++;
     });
-  }
+  });
   return elements;
 }
 
@@ -396,7 +427,7 @@ RadixContainer<T> partition_radix(const std::shared_ptr<Partition<T>>& materiali
     }
   }
   rc.partition_offsets[num_partitions] = offset;
-  for (size_t c = 0; c < chunk_offsets.size(); ++c) {
+  parallel_for(chunk_offsets.size(), [&](size_t c) {  // per-chunk scatter jobs, join_hash.cpp:324-350
     const size_t begin = chunk_offsets[c];
     const size_t end = c + 1 < chunk_offsets.size() ? chunk_offsets[c + 1] : materialized->size();
     for (size_t i = begin; i < end; ++i) {
@@ -404,7 +435,7 @@ RadixContainer<T> partition_radix(const std::shared_ptr<Partition<T>>& materiali
       if (!keep_nulls && e.row_id.chunk_offset == INVALID_CHUNK_OFFSET) continue;
       (*output)[out_off[c][e.partition_hash & mask]++] = e;
     }
-  }
+  });
   return rc;
 }
 
@@ -414,9 +445,9 @@ using HashTable = std::unordered_map<H, std::variant<RowID, PosList>>;
 template <typename L, typename H>
 std::vector<std::optional<HashTable<H>>> build(const RadixContainer<L>& rc) {  // join_hash.cpp:127-185
   std::vector<std::optional<HashTable<H>>> tables(rc.partition_offsets.size() - 1);
-  for (size_t p = 0; p + 1 < rc.partition_offsets.size(); ++p) {
+  parallel_for(tables.size(), [&](size_t p) {  // per-partition jobs, join_hash.cpp:139-180
     const size_t b = rc.partition_offsets[p], e = rc.partition_offsets[p + 1];
-    if (b == e) continue;
+    if (b == e) return;
     HashTable<H> ht(e - b);
     for (size_t i = b; i < e; ++i) {
       const auto& el = (*rc.elements)[i];
@@ -431,16 +462,16 @@ std::vector<std::optional<HashTable<H>>> build(const RadixContainer<L>& rc) {  /
       }
     }
     tables[p] = std::move(ht);
-  }
+  });
   return tables;
 }
 
 template <typename R, typename H>
 void probe(const RadixContainer<R>& rc, const std::vector<std::optional<HashTable<H>>>& tables,
            std::vector<PosList>& left, std::vector<PosList>& right, JoinMode mode) {  // join_hash.cpp:362-466
-  for (size_t p = 0; p + 1 < rc.partition_offsets.size(); ++p) {
+  parallel_for(rc.partition_offsets.size() - 1, [&](size_t p) {  // per-partition jobs, join_hash.cpp:377-463
     const size_t b = rc.partition_offsets[p], e = rc.partition_offsets[p + 1];
-    if (b == e) continue;
+    if (b == e) return;
     PosList l, r;
     if (tables[p].has_value()) {
       const auto& ht = *tables[p];
@@ -478,15 +509,15 @@ void probe(const RadixContainer<R>& rc, const std::vector<std::optional<HashTabl
       left[p] = std::move(l);
       right[p] = std::move(r);
     }
-  }
+  });
 }
 
 template <typename R, typename H>
 void probe_semi_anti(const RadixContainer<R>& rc, const std::vector<std::optional<HashTable<H>>>& tables,
                      std::vector<PosList>& out, JoinMode mode) {  // join_hash.cpp:468-527
-  for (size_t p = 0; p + 1 < rc.partition_offsets.size(); ++p) {
+  parallel_for(rc.partition_offsets.size() - 1, [&](size_t p) {
     const size_t b = rc.partition_offsets[p], e = rc.partition_offsets[p + 1];
-    if (b == e) continue;
+    if (b == e) return;
     PosList local;
     if (tables[p].has_value()) {
       for (size_t i = b; i < e; ++i) {
@@ -500,7 +531,7 @@ void probe_semi_anti(const RadixContainer<R>& rc, const std::vector<std::optiona
       for (size_t i = b; i < e; ++i) local.push_back((*rc.elements)[i].row_id);
     }
     if (!local.empty()) out[p] = std::move(local);
-  }
+  });
 }
 
 using PosLists = std::vector<std::shared_ptr<const PosList>>;
@@ -903,6 +934,9 @@ PYBIND11_MODULE(_hyrise_oracle, m) {
   m.def("murmur2_float", [](float v, unsigned seed) { return oracle::murmur2<float>(v, seed); });
   m.def("murmur2_double", [](double v, unsigned seed) { return oracle::murmur2<double>(v, seed); });
   m.def("radix_bits", &oracle::radix_bits);
+  m.def("set_threads", [](int n) { oracle::g_threads = std::max(1, n); },
+        "worker threads of the per-chunk / per-partition jobs (bench CPU baseline; tests keep 1)");
+  m.def("threads", []() { return oracle::g_threads; });
   m.def("table_scan",
         [](std::shared_ptr<Table> in, ColumnID col, PredicateCondition cond, py::object value,
            std::vector<ChunkID> excluded) {

@@ -1,0 +1,144 @@
+"""Fused TableScan -> JoinHash (hy_scan_join_hash) against the oracle's TableScan followed by its JoinHash on the scan
+output (reference table_scan.cpp:78-164 then join_hash.cpp:49-858 + write_output_columns :564-613): the scan's
+per-chunk offset lists, and every partition's build / probe PosLists RowID for RowID, for value and dictionary
+predicate columns, NULLs in the predicate and join columns, filters on either or both sides and every join mode."""
+import ctypes
+import zlib
+
+import numpy as np
+import pytest
+
+import device_tables as dt
+
+pytestmark = pytest.mark.gpu
+
+
+def orders_lineitem(rng, n_orders, key_nulls):
+    i = np.arange(1, n_orders + 1, dtype=np.int64)
+    okey = (((i >> 3) << 5) + (i & 7)).astype(np.int32)  # dbgen sparse order keys (build.c)
+    okey = np.concatenate([okey, okey[rng.integers(0, n_orders, n_orders // 9)]])  # duplicate build keys
+    lkey = np.repeat(okey[:n_orders], rng.integers(1, 8, n_orders))
+    lkey = np.concatenate([lkey, rng.integers(-500, 0, lkey.size // 40).astype(np.int32)])  # unmatched probe rows
+    rng.shuffle(lkey)
+    lkey = lkey.astype(np.int32)
+    qty = rng.integers(1, 51, lkey.size).astype(np.float32)
+    qty_nulls = (rng.random(lkey.size) < 0.02).astype(np.uint8)
+    lkey_nulls = (rng.random(lkey.size) < 0.03).astype(np.uint8) if key_nulls else None
+    ostatus = rng.integers(0, 10, okey.size).astype(np.int32)
+    return okey, ostatus, lkey, lkey_nulls, qty, qty_nulls
+
+
+def run_fused(hy, build, bfilt, probe, pfilt, params, cap):
+    capi, L = hy.capi, hy.capi.lib
+    wsb = ctypes.c_size_t()
+    bf = ctypes.byref(bfilt) if bfilt is not None else None
+    pf = ctypes.byref(pfilt) if pfilt is not None else None
+    capi.check(L.hy_scan_join_hash_workspace_size(ctypes.byref(build), bf, ctypes.byref(probe), pf,
+                                                  ctypes.byref(params), ctypes.byref(wsb)), "ws")
+    ws = capi.DeviceArray(np.zeros(wsb.value, np.uint8))
+    ob, op = capi.DeviceArray(np.zeros(cap * 2, np.uint32)), capi.DeviceArray(np.zeros(cap * 2, np.uint32))
+    n_parts = 1 << params.radix_bits
+    pbeg, pcnt = capi.DeviceArray(np.zeros(n_parts, np.uint64)), capi.DeviceArray(np.zeros(n_parts, np.uint32))
+    res = capi.JoinResult()
+    capi.check(L.hy_scan_join_hash(ctypes.byref(build), bf, ctypes.byref(probe), pf, ctypes.byref(params), ob.ptr,
+                                   op.ptr, cap, pbeg.ptr, pcnt.ptr, ctypes.byref(res), ws.ptr, wsb.value, None),
+               "hy_scan_join_hash")
+    ob, op = ob.fetch().reshape(-1, 2), op.fetch().reshape(-1, 2)
+    return [(ob[b:b + c], op[b:b + c]) for b, c in zip(pbeg.fetch().astype(np.int64), pcnt.fetch().astype(np.int64))]
+
+
+class Filter:
+    """hy_join_filter for `column cond value` on a DeviceColumn, with its output buffers."""
+
+    def __init__(self, capi, col, cond, value):
+        self.chunks = col.scan_chunks(cond, value)
+        self.const = col.constant(value)
+        n = max(16, col.values.size)
+        self.out = capi.DeviceArray(np.zeros(n, np.uint32))
+        self.begin = capi.DeviceArray(np.zeros(col.n_chunks + 1, np.uint64))
+        self.f = capi.JoinFilter(self.chunks, dt.HY_TYPES[col.values.dtype], self.const.ctypes.data, self.out.ptr.value,
+                                 self.begin.ptr.value)
+
+    def scan_output(self):
+        off, beg = self.out.fetch(), self.begin.fetch().astype(np.int64)
+        return [off[beg[c]:beg[c + 1]] for c in range(beg.size - 1)]
+
+
+def check_scan(expected_scan, filt):
+    """The fused scan's per-chunk offset lists equal the TableScan output chunks (chunks with >= 1 match)."""
+    got = [(c, o) for c, o in enumerate(filt.scan_output()) if o.size]
+    assert len(got) == expected_scan.chunk_count()
+    for k, (c, offs) in enumerate(got):
+        pl = expected_scan.get_chunk(k).get_column(0).pos_list()
+        assert (pl[:, 0] == c).all(), f"scan output chunk {k}"
+        assert np.array_equal(pl[:, 1], offs), f"scan output chunk {k}: offsets differ"
+
+
+def check_join(expected, parts, build_cols, probe_first, semi_anti):
+    """Partition p's PosLists equal output chunk k of the oracle's JoinHash (non-empty partitions, ascending)."""
+    nonempty = [(b, p) for b, p in parts if p.shape[0]]
+    assert len(nonempty) == expected.chunk_count()
+    for k, (b, p) in enumerate(nonempty):
+        ch = expected.get_chunk(k)
+        pcol = 0 if (probe_first or semi_anti) else build_cols
+        assert np.array_equal(ch.get_column(pcol).pos_list(), p), f"partition chunk {k}: probe RowIDs"
+        if not semi_anti:
+            bcol = (ch.column_count() - build_cols) if probe_first else 0
+            assert np.array_equal(ch.get_column(bcol).pos_list(), b), f"partition chunk {k}: build RowIDs"
+
+
+@pytest.mark.parametrize("mode", ["Inner", "Left", "Right", "Semi", "Anti"])
+@pytest.mark.parametrize("qty_enc,key_enc,key_nulls", [("Dictionary", "Unencoded", False),
+                                                       ("Unencoded", "Unencoded", True),
+                                                       ("Dictionary", "Dictionary", True)])
+@pytest.mark.parametrize("build_filter", [False, True])
+def test_scan_join_matches_operators(hy, oracle, mode, qty_enc, key_enc, key_nulls, build_filter):
+    capi = hy.capi
+    rng = np.random.default_rng(zlib.crc32(repr((mode, qty_enc, key_enc, key_nulls, build_filter)).encode()))
+    okey, ostatus, lkey, lkey_nulls, qty, qty_nulls = orders_lineitem(rng, 40_000, key_nulls)
+    lchunk, ochunk = 9_000, 7_000
+    lineitem = hy.Table.from_arrays([("l_orderkey", hy.DataType.Int, key_nulls), ("l_quantity", hy.DataType.Float, True)],
+                                    [lkey, qty], [lkey_nulls, qty_nulls], lchunk)
+    orders = hy.Table.from_arrays([("o_orderkey", hy.DataType.Int, False), ("o_status", hy.DataType.Int, False)],
+                                  [okey, ostatus], [], ochunk)
+    scan_l = oracle.table_scan(lineitem, 1, hy.PredicateCondition.LessThan, 24.0, [])
+    left = oracle.table_scan(orders, 1, hy.PredicateCondition.GreaterThanEquals, 3, []) if build_filter else orders
+    jm = getattr(hy.JoinMode, mode)
+    expected, bits = oracle.join_hash(left, scan_l, jm, (0, 0))
+
+    lk = dt.DeviceColumn(capi, lkey, lkey_nulls, lchunk, key_enc)
+    lq = dt.DeviceColumn(capi, qty, qty_nulls, lchunk, qty_enc)
+    ok = dt.DeviceColumn(capi, okey, None, ochunk, "Unencoded")
+    os_ = dt.DeviceColumn(capi, ostatus, None, ochunk, "Dictionary")
+    lf = Filter(capi, lq, "LessThan", 24.0)
+    of = Filter(capi, os_, "GreaterThanEquals", 3) if build_filter else None
+    # the reference's swap rule on the scan outputs' row counts (join_hash.cpp:55-76)
+    swapped = mode in ("Left", "Semi", "Anti") or left.row_count() > scan_l.row_count()
+    o_side, l_side = dt.join_side(capi, ok), dt.join_side(capi, lk)
+    o_f, l_f = (of.f if of else None), lf.f
+    params = capi.JoinParams({"Inner": 0, "Left": 1, "Right": 2, "Semi": 5, "Anti": 6}[mode], capi.HY_TYPE_INT32, bits,
+                             17)
+    cap = okey.size * 3 + lkey.size + 16
+    if swapped:  # the scan output (left input's role after the swap: build = right input)
+        parts = run_fused(hy, l_side, l_f, o_side, o_f, params, cap)
+    else:
+        parts = run_fused(hy, o_side, o_f, l_side, l_f, params, cap)
+    check_scan(scan_l, lf)
+    if of is not None:
+        check_scan(left, of)
+    check_join(expected, parts, 2, swapped, mode in ("Semi", "Anti"))
+
+
+def test_scan_join_empty_and_all_none(hy, oracle):
+    """Predicates matching nothing (dictionary early-out) and a side without rows."""
+    capi = hy.capi
+    rng = np.random.default_rng(5)
+    okey, ostatus, lkey, _, qty, qty_nulls = orders_lineitem(rng, 5_000, False)
+    lk = dt.DeviceColumn(capi, lkey, None, 4_000, "Unencoded")
+    lq = dt.DeviceColumn(capi, qty, qty_nulls, 4_000, "Dictionary")
+    ok = dt.DeviceColumn(capi, okey, None, 3_000, "Unencoded")
+    lf = Filter(capi, lq, "LessThan", -1.0)
+    params = capi.JoinParams(0, capi.HY_TYPE_INT32, capi.lib.hy_join_radix_bits(okey.size, 4), 17)
+    parts = run_fused(hy, dt.join_side(capi, ok), None, dt.join_side(capi, lk), lf.f, params, okey.size + 16)
+    assert sum(p.shape[0] for _, p in parts) == 0
+    assert all(o.size == 0 for o in lf.scan_output())

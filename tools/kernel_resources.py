@@ -6,7 +6,8 @@ import sys
 cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Iinclude", "-c",
        "TU", "-o", "/tmp/_res.o", "-Rpass-analysis=kernel-resource-usage"]
 out = ""
-for tu in ("hyrise-1_amd/csrc/capi/hyrise_amd.hip", "hyrise-1_amd/csrc/capi/hyrise_amd_aggregate.hip"):
+for tu in ("hyrise-1_amd/csrc/capi/hyrise_amd.hip", "hyrise-1_amd/csrc/capi/hyrise_amd_aggregate.hip",
+           "hyrise-1_amd/csrc/capi/hyrise_amd_join_i32.hip"):
     if len(sys.argv) > 2 and sys.argv[2] not in tu:
         continue
     out += subprocess.run([tu if a == "TU" else a for a in cmd], capture_output=True, text=True).stderr
