@@ -13,7 +13,8 @@ EXTSUF    := $(shell $(PY) -c "import sysconfig;print(sysconfig.get_config_var('
 CXXFLAGS  := -std=c++17 -O2 -fPIC -Wall -Wno-unused-function -Iinclude -I$(CSRC)/host
 HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude
 
-HOST_SRC  := $(CSRC)/host/storage.cpp $(CSRC)/host/device.cpp $(CSRC)/host/operators.cpp $(CSRC)/host/aggregate.cpp
+HOST_SRC  := $(CSRC)/host/storage.cpp $(CSRC)/host/device.cpp $(CSRC)/host/operators.cpp $(CSRC)/host/aggregate.cpp \
+             $(CSRC)/host/projection.cpp
 HOST_HDR  := $(wildcard $(CSRC)/host/*.hpp) include/hyrise_amd.h
 
 all: $(LIB)/libhyrise_amd.so $(LIB)/libhyrise_host.so $(LIB)/_hyrise_host$(EXTSUF)
@@ -25,7 +26,7 @@ $(LIB)/hyrise_amd.o: $(CSRC)/capi/hyrise_amd.hip $(CSRC)/kernels/scan.hip $(CSRC
 	@mkdir -p $(LIB)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
-$(LIB)/hyrise_amd_aggregate.o: $(CSRC)/capi/hyrise_amd_aggregate.hip $(CSRC)/kernels/aggregate.hip $(CAPI_HDR)
+$(LIB)/hyrise_amd_aggregate.o: $(CSRC)/capi/hyrise_amd_aggregate.hip $(CSRC)/kernels/aggregate.hip $(CSRC)/kernels/projection.hip $(CAPI_HDR)
 	@mkdir -p $(LIB)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 

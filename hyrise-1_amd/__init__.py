@@ -52,6 +52,13 @@ TableScan = _host.TableScan
 JoinHash = _host.JoinHash
 Aggregate = _host.Aggregate
 AggregateColumnDefinition = _host.AggregateColumnDefinition
+Projection = _host.Projection
+ArithmeticOperator = _host.ArithmeticOperator
+AbstractExpression = _host.AbstractExpression
+PQPColumnExpression = _host.PQPColumnExpression
+ValueExpression = _host.ValueExpression
+ArithmeticExpression = _host.ArithmeticExpression
+expression_common_type = _host.expression_common_type
 LogicError = _host.LogicError
 load_table = _host.load_table
 encode_chunks = _host.encode_chunks

@@ -9,6 +9,7 @@
 
 #include "capi_common.hpp"
 #include "../kernels/aggregate.hip"
+#include "../kernels/projection.hip"
 
 using namespace hyc;
 
@@ -338,6 +339,159 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
   if (misc[0] & 2u) return fail(HY_ERR_INVALID_ARGUMENT, "dense group-by code outside its domain");
   if (misc[0] & 1u) return fail(HY_ERR_KERNEL, "aggregate hash table full (group_bound too small?)");
   if (n > out_capacity) return fail(HY_ERR_CAPACITY, "more groups than out_capacity");
+  return HY_OK;
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Projection (expression evaluation over an aggregate-style input)
+// ---------------------------------------------------------------------------------------------------------------
+namespace {
+
+struct ProjWs {
+  uint32_t* sizes;
+  uint64_t* row_begin;
+  uint64_t* tile_begin;
+  uint32_t* tile_owner;
+  const hy_row_id** pos_lists;
+  hy_column_chunk* chunks[hyk::AGG_MAX_COLUMNS];
+};
+
+uint64_t proj_tiles(const hy_agg_input* in) {
+  uint64_t t = 0;
+  for (uint32_t c = 0; c < in->n_chunks; ++c) t += (in->chunk_sizes[c] + hyk::PROJ_TILE - 1) / hyk::PROJ_TILE;
+  return t;
+}
+
+void carve_proj(Carver& cv, const hy_agg_input* in, ProjWs* w) {
+  w->sizes = cv.take<uint32_t>(std::max<uint32_t>(1, in->n_chunks));
+  w->row_begin = cv.take<uint64_t>(in->n_chunks + 1);
+  w->tile_begin = cv.take<uint64_t>(in->n_chunks + 1);
+  w->tile_owner = cv.take<uint32_t>(std::max<uint64_t>(1, proj_tiles(in)));
+  w->pos_lists = cv.take<const hy_row_id*>(std::max<uint64_t>(1, uint64_t(in->n_pos_groups) * in->n_chunks));
+  for (uint32_t j = 0; j < in->n_columns; ++j)
+    w->chunks[j] = cv.take<hy_column_chunk>(std::max<uint32_t>(1, in->columns[j].n_chunks));
+}
+
+hy_status check_proj_input(const hy_agg_input* in) {
+  if (!in) return fail(HY_ERR_INVALID_ARGUMENT, "null input");
+  if (in->n_columns > hyk::AGG_MAX_COLUMNS) return fail(HY_ERR_UNSUPPORTED, "too many projection input columns");
+  if (in->n_pos_groups > hyk::AGG_MAX_POS_GROUPS) return fail(HY_ERR_UNSUPPORTED, "too many PosList groups");
+  if (in->n_chunks && !in->chunk_sizes) return fail(HY_ERR_INVALID_ARGUMENT, "chunk_sizes missing");
+  if (in->n_pos_groups && in->n_chunks && !in->pos_lists) return fail(HY_ERR_INVALID_ARGUMENT, "pos_lists missing");
+  for (uint32_t j = 0; j < in->n_columns; ++j) {
+    const auto& c = in->columns[j];
+    if (c.value_type < HY_TYPE_INT32 || c.value_type > HY_TYPE_DOUBLE) return fail(HY_ERR_UNSUPPORTED, "column type");
+    if (c.pos_group >= static_cast<int32_t>(in->n_pos_groups)) return fail(HY_ERR_INVALID_ARGUMENT, "pos_group");
+    if (c.pos_group < 0 && c.n_chunks != in->n_chunks)
+      return fail(HY_ERR_INVALID_ARGUMENT, "data column must have one chunk per input chunk");
+  }
+  return HY_OK;
+}
+
+}  // namespace
+
+hy_status hy_projection_workspace_size(const hy_agg_input* input, size_t* bytes) {
+  if (!bytes) return fail(HY_ERR_INVALID_ARGUMENT, "null bytes");
+  hy_status st = check_proj_input(input);
+  if (st != HY_OK) return st;
+  Carver cv{nullptr, 0};
+  ProjWs w;
+  carve_proj(cv, input, &w);
+  *bytes = cv.used + 256;
+  return HY_OK;
+}
+
+hy_status hy_projection(const hy_agg_input* input, const hy_expr_node* program, uint32_t n_nodes, void* out_values,
+                        uint8_t* out_nulls, void* workspace, size_t workspace_bytes, hy_stream_t stream) {
+  hy_status st = check_proj_input(input);
+  if (st != HY_OK) return st;
+  if (!program || n_nodes == 0 || n_nodes > HY_EXPR_MAX_NODES) return fail(HY_ERR_INVALID_ARGUMENT, "program size");
+  // validate the postfix program: stack depth, column indexes, types
+  hyk::ExprProgram prog{};
+  int depth = 0;
+  for (uint32_t i = 0; i < n_nodes; ++i) {
+    const hy_expr_node& nd = program[i];
+    prog.nodes[i] = nd;
+    const bool typed = nd.type >= HY_TYPE_INT32 && nd.type <= HY_TYPE_DOUBLE;
+    switch (nd.kind) {
+      case HY_EXPR_COLUMN:
+        if (nd.column < 0 || nd.column >= static_cast<int32_t>(input->n_columns))
+          return fail(HY_ERR_INVALID_ARGUMENT, "expression column");
+        if (nd.type != input->columns[nd.column].value_type) return fail(HY_ERR_INVALID_ARGUMENT, "column node type");
+        ++depth;
+        break;
+      case HY_EXPR_VALUE:
+        if (!typed && nd.type != 0) return fail(HY_ERR_INVALID_ARGUMENT, "literal type");
+        ++depth;
+        break;
+      case HY_EXPR_ADD:
+      case HY_EXPR_SUB:
+      case HY_EXPR_MUL:
+      case HY_EXPR_DIV:
+      case HY_EXPR_MOD:
+        if (depth < 2) return fail(HY_ERR_INVALID_ARGUMENT, "expression stack underflow");
+        if (!typed || nd.calc_type < HY_TYPE_INT32 || nd.calc_type > HY_TYPE_DOUBLE)
+          return fail(HY_ERR_INVALID_ARGUMENT, "arithmetic node types");
+        --depth;
+        break;
+      default:
+        return fail(HY_ERR_INVALID_ARGUMENT, "expression node kind");
+    }
+    if (depth > HY_EXPR_MAX_DEPTH) return fail(HY_ERR_UNSUPPORTED, "expression deeper than HY_EXPR_MAX_DEPTH");
+  }
+  if (depth != 1) return fail(HY_ERR_INVALID_ARGUMENT, "program does not leave one value");
+  prog.n_nodes = n_nodes;
+  prog.out_type = program[n_nodes - 1].type;
+  if (prog.out_type == 0) return fail(HY_ERR_UNSUPPORTED, "an all-NULL expression has no column type");
+  const uint64_t tiles = proj_tiles(input);
+  if (tiles == 0) return HY_OK;
+  if (!out_values) return fail(HY_ERR_INVALID_ARGUMENT, "out_values");
+  hipStream_t s = S(stream);
+  Carver cv{static_cast<char*>(workspace), workspace_bytes};
+  ProjWs w;
+  carve_proj(cv, input, &w);
+  if (!cv.ok || !workspace) return fail(HY_ERR_WORKSPACE, "projection workspace too small");
+  std::vector<uint64_t> row_begin(input->n_chunks + 1, 0), tile_begin(input->n_chunks + 1, 0);
+  for (uint32_t c = 0; c < input->n_chunks; ++c) {
+    row_begin[c + 1] = row_begin[c] + input->chunk_sizes[c];
+    tile_begin[c + 1] = tile_begin[c] + (input->chunk_sizes[c] + hyk::PROJ_TILE - 1) / hyk::PROJ_TILE;
+  }
+  HY_HIP(hipMemcpyAsync(w.sizes, input->chunk_sizes, 4 * input->n_chunks, hipMemcpyHostToDevice, s));
+  HY_HIP(hipMemcpyAsync(w.row_begin, row_begin.data(), 8 * row_begin.size(), hipMemcpyHostToDevice, s));
+  HY_HIP(hipMemcpyAsync(w.tile_begin, tile_begin.data(), 8 * tile_begin.size(), hipMemcpyHostToDevice, s));
+  const uint64_t n_pl = uint64_t(input->n_pos_groups) * input->n_chunks;
+  if (n_pl) HY_HIP(hipMemcpyAsync(w.pos_lists, input->pos_lists, sizeof(void*) * n_pl, hipMemcpyHostToDevice, s));
+  hyk::AggDesc d{};
+  d.n_cols = input->n_columns;
+  d.n_pos_groups = input->n_pos_groups;
+  d.n_chunks = input->n_chunks;
+  d.n_tiles = tiles;
+  for (uint32_t j = 0; j < input->n_columns; ++j) {
+    const auto& c = input->columns[j];
+    for (uint32_t k = 0; k < c.n_chunks; ++k)
+      if (c.chunks[k].size && !c.chunks[k].data) return fail(HY_ERR_INVALID_ARGUMENT, "column chunk without data");
+    if (c.n_chunks)
+      HY_HIP(hipMemcpyAsync(w.chunks[j], c.chunks, sizeof(hy_column_chunk) * c.n_chunks, hipMemcpyHostToDevice, s));
+    d.cols[j].chunks = w.chunks[j];
+    d.cols[j].type = c.value_type;
+    d.cols[j].pos_group = c.pos_group;
+  }
+  d.pos_lists = w.pos_lists;
+  d.chunk_size = w.sizes;
+  d.chunk_row_begin = w.row_begin;
+  d.chunk_tile_begin = w.tile_begin;
+  d.tile_chunk = w.tile_owner;
+  hipLaunchKernelGGL(hyk::fill_tile_owner, dim3((input->n_chunks + 255) / 256), dim3(256), 0, s, w.tile_begin,
+                     input->n_chunks, w.tile_owner);
+  HY_HIP(hipGetLastError());
+  uint64_t rows = row_begin[input->n_chunks];
+  KTimer t("projection", s, rows);
+  hipLaunchKernelGGL(hyk::projection_kernel, dim3(static_cast<uint32_t>(tiles)), dim3(hyk::AGG_THREADS), 0, s, d, prog,
+                     out_values, out_nulls);
+  t.done();
+  HY_HIP(hipGetLastError());
+  // host staging above must outlive the async copies
+  HY_HIP(hipStreamSynchronize(s));
   return HY_OK;
 }
 

@@ -41,6 +41,15 @@ inline uint32_t sub_filtered() {
   static const uint32_t v = sub_from_env("HY_PART_SUB_FILTERED", 2);
   return v;
 }
+// Next-digit bytes beside the records of a pass that has a successor (HY_DIGIT_BYTES=0 turns them off: the next
+// histogram then reads the records and re-hashes them).
+inline bool digit_bytes_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("HY_DIGIT_BYTES");
+    return !(e && std::strtol(e, nullptr, 10) == 0);
+  }();
+  return v;
+}
 inline uint32_t sub2() {
   static const uint32_t v = sub_from_env("HY_PART_SUB2", 1);
   return v;
@@ -665,7 +674,7 @@ inline SideSizes sizes_of(const SidePlan& p, bool digit_bytes) {
 template <typename H>
 size_t join_bytes(const SidePlan& bp, const SidePlan& pp, uint32_t bits) {
   const auto w = digit_plan(bits, 0);
-  const bool db = w.size() > 1;
+  const bool db = w.size() > 1 && digit_bytes_enabled();
   Carver cv{nullptr, 0};
   SideBufs<H> a, b;
   carve_side<H, uint32_t>(cv, sizes_of(bp, db), bits, w, 1, true, a);
@@ -699,7 +708,7 @@ hy_status join_typed(const SidePlan& bp, const SidePlan& pp, const hy_join_param
   const uint32_t bits = prm->radix_bits;
   if (workspace_bytes < join_bytes<H>(bp, pp, bits)) return fail(HY_ERR_WORKSPACE, "join workspace too small");
   const auto w = digit_plan(bits, 0);
-  const bool db = w.size() > 1;
+  const bool db = w.size() > 1 && digit_bytes_enabled();
   Carver cv{static_cast<char*>(workspace), workspace_bytes};
   SideBufs<H> bb, pb;
   carve_side<H, uint32_t>(cv, sizes_of(bp, db), bits, w, 1, true, bb);

@@ -309,4 +309,42 @@ PYBIND11_MODULE(_hyrise_host, m) {
                     std::vector<ColumnID>>(),
            py::arg("input"), py::arg("aggregates"), py::arg("groupby_column_ids"))
       .def("used_dense_path", &Aggregate::used_dense_path);
+
+  // ---- Projection and its expressions (reference expression/*.hpp, operators/projection.hpp)
+  py::enum_<ArithmeticOperator>(m, "ArithmeticOperator")
+      .value("Addition", ArithmeticOperator::Addition)
+      .value("Subtraction", ArithmeticOperator::Subtraction)
+      .value("Multiplication", ArithmeticOperator::Multiplication)
+      .value("Division", ArithmeticOperator::Division)
+      .value("Modulo", ArithmeticOperator::Modulo);
+  py::class_<AbstractExpression, std::shared_ptr<AbstractExpression>>(m, "AbstractExpression")
+      .def("data_type", &AbstractExpression::data_type)
+      .def("is_nullable", &AbstractExpression::is_nullable)
+      .def("as_column_name", &AbstractExpression::as_column_name);
+  py::class_<PQPColumnExpression, AbstractExpression, std::shared_ptr<PQPColumnExpression>>(m, "PQPColumnExpression")
+      .def(py::init<ColumnID, DataType, bool, std::string>(), py::arg("column_id"), py::arg("data_type"),
+           py::arg("nullable"), py::arg("column_name"))
+      .def_static("from_table", &PQPColumnExpression::from_table, py::arg("table"), py::arg("column_id"))
+      .def_readonly("column_id", &PQPColumnExpression::column_id);
+  py::class_<ValueExpression, AbstractExpression, std::shared_ptr<ValueExpression>>(m, "ValueExpression")
+      .def(py::init([](py::object v) { return std::make_shared<ValueExpression>(to_variant(v)); }), py::arg("value"))
+      .def(py::init([](py::object v, DataType t) {
+             // a literal of an explicit type (Python numbers are int32/int64/double otherwise)
+             AllTypeVariant var = to_variant(v);
+             if (!variant_is_null(var)) resolve_data_type(t, [&](auto tag) { var = type_cast<decltype(tag)>(var); });
+             return std::make_shared<ValueExpression>(var);
+           }),
+           py::arg("value"), py::arg("data_type"))
+      .def_property_readonly("value", [](const ValueExpression& e) { return to_py(e.value); });
+  py::class_<ArithmeticExpression, AbstractExpression, std::shared_ptr<ArithmeticExpression>>(m, "ArithmeticExpression")
+      .def(py::init<ArithmeticOperator, std::shared_ptr<AbstractExpression>, std::shared_ptr<AbstractExpression>>(),
+           py::arg("arithmetic_operator"), py::arg("left_operand"), py::arg("right_operand"))
+      .def_readonly("arithmetic_operator", &ArithmeticExpression::arithmetic_operator)
+      .def("left_operand", &ArithmeticExpression::left_operand)
+      .def("right_operand", &ArithmeticExpression::right_operand);
+  m.def("expression_common_type", &expression_common_type);
+  py::class_<Projection, AbstractOperator, std::shared_ptr<Projection>>(m, "Projection")
+      .def(py::init<std::shared_ptr<const AbstractOperator>, std::vector<std::shared_ptr<AbstractExpression>>>(),
+           py::arg("input"), py::arg("expressions"))
+      .def_readonly("expressions", &Projection::expressions);
 }

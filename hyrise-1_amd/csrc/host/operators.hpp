@@ -20,11 +20,12 @@
 #include <vector>
 
 #include "device.hpp"
+#include "expression.hpp"
 #include "storage.hpp"
 
 namespace hyrise {
 
-enum class OperatorType { TableWrapper, TableScan, JoinHash, Aggregate, Mock };
+enum class OperatorType { TableWrapper, TableScan, JoinHash, Aggregate, Projection, Mock };
 
 struct OperatorPerformanceData {
   uint64_t walltime_ns = 0;  // reference operator_performance_data.hpp:15
@@ -155,6 +156,22 @@ class Aggregate final : public AbstractOperator {
   std::vector<AggregateColumnDefinition> _aggregates;
   std::vector<ColumnID> _groupby_column_ids;
   bool _used_dense_path = false;
+};
+
+// Projection(in, expressions): reference src/lib/operators/projection.hpp:20-50, projection.cpp:39-87. One output
+// column per expression; PQPColumn expressions forward the input column when the output table type equals the
+// input's (a projection of columns only keeps the input's type; anything computed makes a Data table). Arithmetic
+// expressions are evaluated on the device (hy_projection), one launch per expression over all chunks.
+class Projection final : public AbstractOperator {
+ public:
+  Projection(std::shared_ptr<const AbstractOperator> in, std::vector<std::shared_ptr<AbstractExpression>> expressions)
+      : AbstractOperator(OperatorType::Projection, std::move(in)), expressions(std::move(expressions)) {}
+  const std::string name() const override { return "Projection"; }
+
+  const std::vector<std::shared_ptr<AbstractExpression>> expressions;
+
+ protected:
+  std::shared_ptr<const Table> _on_execute() override;
 };
 
 // JoinHashTraits (reference src/lib/operators/join_hash/hash_traits.hpp:9-42) over data types.

@@ -430,6 +430,38 @@ hy_status hy_aggregate_workspace_size(const hy_agg_input* input, const hy_agg_pa
 hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, uint64_t* out_records,
                        uint64_t out_capacity, uint64_t* n_groups, void* workspace, size_t workspace_bytes,
                        hy_stream_t stream);
+/* ---------------------------------------------------------------------------------------------------------------
+ * Projection of arithmetic expressions (reference src/lib/operators/projection.cpp:39-87 evaluating
+ * ArithmeticExpression / PQPColumnExpression / ValueExpression through ExpressionEvaluator,
+ * expression/evaluation/expression_evaluator.cpp:105-120, :795-830, expression_functors.hpp:104-180).
+ *
+ * The expression is a postfix program over the columns of a hy_agg_input (data chunks or columns referenced through
+ * PosList groups, exactly as for hy_aggregate). Every node carries the reference's types:
+ *   type       the node's result type: a column's / literal's type; for arithmetic expression_common_type(l, r)
+ *              (expression/expression_utils.cpp:116-136)
+ *   calc_type  arithmetic only: the type the operation runs in, std::common_type of the operands' types (the
+ *              functors compute Functor<std::common_type_t<A, B>>(a, b) and assign it to the result type)
+ * NULL logic: + - * are NULL if an operand is NULL; / and % also when the divisor is 0 (integral % or fmod).
+ * A NULL literal is a VALUE node with type 0 (every row NULL).
+ * Output: values[r] (result type) and nulls[r] (1 = NULL; may be NULL when the expression is not nullable) for input
+ * row r, rows numbered chunk by chunk. Values of NULL rows are unspecified.
+ * ------------------------------------------------------------------------------------------------------------- */
+enum { HY_EXPR_COLUMN = 0, HY_EXPR_VALUE = 1, HY_EXPR_ADD = 2, HY_EXPR_SUB = 3, HY_EXPR_MUL = 4, HY_EXPR_DIV = 5,
+       HY_EXPR_MOD = 6 };
+enum { HY_EXPR_MAX_NODES = 32, HY_EXPR_MAX_DEPTH = 8 };
+
+typedef struct hy_expr_node {
+  int32_t kind;       /* HY_EXPR_* */
+  int32_t type;       /* HY_TYPE_* of the node's value (0: NULL literal) */
+  int32_t calc_type;  /* arithmetic: HY_TYPE_* the operation is computed in */
+  int32_t column;     /* COLUMN: index into hy_agg_input.columns */
+  uint64_t value;     /* VALUE: the literal's bits in `type` (int32/float in the low 4 bytes) */
+} hy_expr_node;
+
+hy_status hy_projection_workspace_size(const hy_agg_input* input, size_t* bytes);
+hy_status hy_projection(const hy_agg_input* input, const hy_expr_node* program, uint32_t n_nodes, void* out_values,
+                        uint8_t* out_nulls, void* workspace, size_t workspace_bytes, hy_stream_t stream);
+
 /* Host helpers: the correctly rounded double of an exact limb sum, and the value bits behind an ordered word. */
 hy_status hy_agg_float_sum(const uint64_t* limbs, uint32_t n_limbs, int32_t emin, uint64_t special, double* out);
 uint64_t hy_agg_decode_ordered(uint64_t ordered, int32_t value_type);

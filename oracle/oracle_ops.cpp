@@ -902,6 +902,173 @@ std::shared_ptr<Table> aggregate(const std::shared_ptr<const Table>& in, const s
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Projection: reference operators/projection.cpp:39-87 with ExpressionEvaluator's arithmetic
+// (expression_evaluator.cpp:105-120 _evaluate_arithmetic_expression, :795-830 _evaluate_binary_with_default_null_logic,
+// expression_functors.hpp:104-180 STLArithmeticFunctorWrapper / DivisionEvaluator / ModuloEvaluator).
+// Each node evaluates to typed values + NULL flags for the rows of one chunk; arithmetic computes
+// Functor<std::common_type_t<A, B>>{}(a, b) and stores it as the expression's data type.
+// ---------------------------------------------------------------------------------------------------------------
+template <typename T>
+struct ExprValues {
+  std::vector<T> values;
+  std::vector<uint8_t> nulls;  // 1 = NULL
+};
+struct AllNull {
+  size_t size = 0;
+};
+using ExprAny = std::variant<AllNull, ExprValues<int32_t>, ExprValues<int64_t>, ExprValues<float>, ExprValues<double>>;
+
+template <typename F>
+void with_data_type(DataType t, F&& f) {
+  switch (t) {
+    case DataType::Int:
+      return f(int32_t{});
+    case DataType::Long:
+      return f(int64_t{});
+    case DataType::Float:
+      return f(float{});
+    case DataType::Double:
+      return f(double{});
+    default:
+      Fail("oracle projection: unsupported data type");
+  }
+}
+
+ExprAny evaluate(const AbstractExpression& e, const Table& in, ChunkID chunk_id) {
+  const size_t n = in.get_chunk(chunk_id)->size();
+  if (e.type == ExpressionType::PQPColumn) {
+    const auto column = in.get_chunk(chunk_id)->get_column(static_cast<const PQPColumnExpression&>(e).column_id);
+    ExprAny out;
+    with_data_type(e.data_type(), [&](auto tag) {
+      using T = decltype(tag);
+      ExprValues<T> r;
+      r.values.resize(n);
+      r.nulls.resize(n);
+      for (ChunkOffset o = 0; o < n; ++o) {  // BaseColumn::operator[] (through the PosList for a ReferenceColumn)
+        const auto v = (*column)[o];
+        if (variant_is_null(v)) {
+          r.nulls[o] = 1;
+        } else {
+          r.values[o] = std::get<T>(v);
+        }
+      }
+      out = std::move(r);
+    });
+    return out;
+  }
+  if (e.type == ExpressionType::Value) {
+    const auto& value = static_cast<const ValueExpression&>(e).value;
+    if (variant_is_null(value)) return AllNull{n};
+    ExprAny out;
+    with_data_type(e.data_type(), [&](auto tag) {
+      using T = decltype(tag);
+      out = ExprValues<T>{std::vector<T>(n, std::get<T>(value)), std::vector<uint8_t>(n, 0)};
+    });
+    return out;
+  }
+  const auto& a = static_cast<const ArithmeticExpression&>(e);
+  const ExprAny left = evaluate(*a.left_operand(), in, chunk_id);
+  const ExprAny right = evaluate(*a.right_operand(), in, chunk_id);
+  ExprAny out = AllNull{n};
+  if (std::holds_alternative<AllNull>(left) || std::holds_alternative<AllNull>(right)) return out;
+  with_data_type(e.data_type(), [&](auto rtag) {
+    using R = decltype(rtag);
+    std::visit(
+        [&](const auto& l, const auto& r) {
+          using LV = std::decay_t<decltype(l)>;
+          using RV = std::decay_t<decltype(r)>;
+          if constexpr (!std::is_same_v<LV, AllNull> && !std::is_same_v<RV, AllNull>) {
+            using A = typename std::decay_t<decltype(l.values)>::value_type;
+            using B = typename std::decay_t<decltype(r.values)>::value_type;
+            using C = std::common_type_t<A, B>;
+            ExprValues<R> res;
+            res.values.resize(n);
+            res.nulls.resize(n);
+            for (size_t i = 0; i < n; ++i) {
+              res.nulls[i] = l.nulls[i] || r.nulls[i];
+              if (res.nulls[i]) continue;
+              const C x = static_cast<C>(l.values[i]), y = static_cast<C>(r.values[i]);
+              switch (a.arithmetic_operator) {
+                case ArithmeticOperator::Addition:
+                  res.values[i] = static_cast<R>(std::plus<C>{}(x, y));
+                  break;
+                case ArithmeticOperator::Subtraction:
+                  res.values[i] = static_cast<R>(std::minus<C>{}(x, y));
+                  break;
+                case ArithmeticOperator::Multiplication:
+                  res.values[i] = static_cast<R>(std::multiplies<C>{}(x, y));
+                  break;
+                case ArithmeticOperator::Division:
+                  if (r.values[i] == 0)
+                    res.nulls[i] = 1;
+                  else
+                    res.values[i] = static_cast<R>(l.values[i] / r.values[i]);
+                  break;
+                case ArithmeticOperator::Modulo:
+                  if (r.values[i] == 0) {
+                    res.nulls[i] = 1;
+                  } else if constexpr (std::is_integral_v<A> && std::is_integral_v<B>) {
+                    res.values[i] = static_cast<R>(l.values[i] % r.values[i]);
+                  } else {
+                    res.values[i] = static_cast<R>(std::fmod(l.values[i], r.values[i]));
+                  }
+                  break;
+              }
+            }
+            out = std::move(res);
+          }
+        },
+        left, right);
+  });
+  return out;
+}
+
+std::shared_ptr<Table> projection(const std::shared_ptr<const Table>& in,
+                                  const std::vector<std::shared_ptr<AbstractExpression>>& expressions) {
+  TableColumnDefinitions defs;
+  for (const auto& e : expressions) defs.emplace_back(e->as_column_name(), e->data_type(), e->is_nullable());
+  const bool only_columns = std::all_of(expressions.begin(), expressions.end(),
+                                        [](const auto& e) { return e->type == ExpressionType::PQPColumn; });
+  const auto output_type = only_columns ? in->type() : TableType::Data;
+  const bool forward = in->type() == output_type;
+  auto out = std::make_shared<Table>(defs, output_type, in->max_chunk_size());
+  for (ChunkID c = 0; c < in->chunk_count(); ++c) {
+    ChunkColumns cols;
+    for (const auto& e : expressions) {
+      if (e->type == ExpressionType::PQPColumn && forward) {
+        cols.push_back(std::const_pointer_cast<BaseColumn>(
+            in->get_chunk(c)->get_column(static_cast<const PQPColumnExpression&>(*e).column_id)));
+        continue;
+      }
+      if (e->data_type() == DataType::String) {  // a string column of a reference input, materialized
+        const auto src = in->get_chunk(c)->get_column(static_cast<const PQPColumnExpression&>(*e).column_id);
+        auto dst = std::make_shared<ValueColumn<std::string>>(e->is_nullable());
+        for (ChunkOffset o = 0; o < src->size(); ++o) dst->append((*src)[o]);
+        cols.push_back(dst);
+        continue;
+      }
+      const ExprAny r = evaluate(*e, *in, c);
+      with_data_type(e->data_type(), [&](auto tag) {
+        using T = decltype(tag);
+        std::vector<T> values(in->get_chunk(c)->size());
+        std::vector<uint8_t> nulls(values.size(), 1);
+        if (const auto* v = std::get_if<ExprValues<T>>(&r)) {
+          values = v->values;
+          nulls = v->nulls;
+        }
+        for (size_t i = 0; i < values.size(); ++i)
+          if (nulls[i]) values[i] = T{};
+        std::optional<std::vector<uint8_t>> nv;
+        if (e->is_nullable()) nv = std::move(nulls);
+        cols.push_back(std::make_shared<ValueColumn<T>>(std::move(values), std::move(nv)));
+      });
+    }
+    out->append_chunk(cols);
+  }
+  return out;
+}
+
 }  // namespace oracle
 
 namespace {
@@ -950,6 +1117,10 @@ PYBIND11_MODULE(_hyrise_oracle, m) {
           py::gil_scoped_release rel;
           return oracle::join_hash(l, r, mode, cols);
         });
+  m.def("projection", [](std::shared_ptr<Table> in, std::vector<std::shared_ptr<AbstractExpression>> exprs) {
+    py::gil_scoped_release rel;
+    return oracle::projection(in, exprs);
+  });
   m.def("aggregate", [](std::shared_ptr<Table> in, std::vector<AggregateColumnDefinition> aggs,
                         std::vector<ColumnID> groupby) {
     py::gil_scoped_release rel;
