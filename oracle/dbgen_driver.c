@@ -1,9 +1,10 @@
 /*
  * Driver over the reference's vendored TPC-H dbgen (third_party/tpch-dbgen, compiled where it lies by
- * oracle/Makefile `ref`; never copied). Generates ORDERS and LINEITEM exactly as the reference's
+ * oracle/Makefile `ref`; never copied). Generates CUSTOMER, then ORDERS and LINEITEM exactly as the reference's
  * TpchDbGenerator::generate does (src/benchmarklib/tpch/tpch_db_generator.cpp:203-236: dbgen_reset_seeds, then per
- * order row_start / mk_order / row_stop, money through convert_money) and prints the columns the hot-path fixtures
- * use as tab-separated text:
+ * row row_start / mk_cust or mk_order / row_stop, money through convert_money) and prints the columns the hot-path
+ * fixtures use as tab-separated text:
+ *   C <c_custkey> <c_mktsegment>
  *   O <o_orderkey> <o_custkey> <o_orderdate> <o_shippriority>
  *   L <l_orderkey> <l_quantity> <l_extendedprice> <l_discount> <l_tax> <l_returnflag> <l_linestatus> <l_shipdate>
  * Floats are printed with %.9g (round-trips float32).
@@ -26,7 +27,16 @@ static float convert_money(DSS_HUGE cents) {
 int main(int argc, char** argv) {
   const float sf = argc > 1 ? (float)atof(argv[1]) : 0.01f;
   static order_t order;
+  static customer_t cust;
   dbgen_reset_seeds();
+  /* tpch_db_generator.cpp:206-214 */
+  const size_t customer_count = (size_t)(tdefs[CUST].base * sf);
+  for (size_t i = 0; i < customer_count; ++i) {
+    row_start(CUST);
+    mk_cust((DSS_HUGE)(i + 1), &cust);
+    row_stop(CUST);
+    printf("C\t%lld\t%s\n", (long long)cust.custkey, cust.mktsegment);
+  }
   const size_t order_count = (size_t)(tdefs[ORDER].base * sf);
   for (size_t i = 0; i < order_count; ++i) {
     row_start(ORDER);
