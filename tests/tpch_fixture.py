@@ -1,4 +1,4 @@
-"""TPC-H SF0.01 ORDERS / LINEITEM from the committed dbgen fixture (tests/golden/tpch_sf0.01.npz, made by
+"""TPC-H SF0.01 CUSTOMER / ORDERS / LINEITEM from the committed dbgen fixture (tests/golden/tpch_sf0.01.npz, made by
 tests/golden/make_tpch_fixture.py) as host tables with the reference schema types (tpch_db_generator.cpp:20-27:
 keys int, money and quantity float, flags and dates strings), chunked by 10,000 rows like tpch_test.cpp:56."""
 import json
@@ -37,6 +37,15 @@ def tables(hy, encode=True):
         hy.encode_all_chunks(lineitem, hy.EncodingType.Dictionary)
         hy.encode_all_chunks(orders, hy.EncodingType.Dictionary)
     return orders, lineitem
+
+
+def customer_table(hy, encode=True):
+    a = arrays()
+    customer = hy.Table.from_arrays([("c_custkey", hy.DataType.Int, False), ("c_mktsegment", hy.DataType.String, False)],
+                                    [a["c_custkey"], a["c_mktsegment"].astype(str)], [], CHUNK)
+    if encode:
+        hy.encode_all_chunks(customer, hy.EncodingType.Dictionary)
+    return customer
 
 
 Q1_GROUPBY = [5, 6]
