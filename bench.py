@@ -39,9 +39,10 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (RCCL; one GPU per rank) or gloo (host-staged exchange: rehearsal of N ranks on one GPU)")
-    p.add_argument("--workload", choices=["join", "q1"], default="join",
+    p.add_argument("--workload", choices=["join", "q1", "q3"], default="join",
                    help="join: the headline TableScan+JoinHash (BASELINE.json metric); q1: BASELINE config 4, "
-                        "TableScan(l_shipdate) -> Aggregate of TPC-H 1 on one GPU")
+                        "TableScan(l_shipdate) -> Aggregate of TPC-H 1 on one GPU; q3: BASELINE config 5 at N=1, "
+                        "TPC-H 3 Scan -> Join -> Join -> Projection -> Aggregate (bench_tpch.py)")
     p.add_argument("--q1-aggs", default=None, help="debug: comma-separated subset of Q1_AGGS indexes (q1 workload)")
     p.add_argument("--unfused", action="store_true",
                    help="run TableScan and JoinHash as two C-ABI calls (hy_table_scan_row_ids, hy_join_hash) instead "
@@ -57,6 +58,10 @@ def main():
     args = parse()
     if args.workload == "q1":
         return main_q1(args)
+    if args.workload == "q3":
+        import bench_tpch
+
+        return bench_tpch.main_q3(args)
     import torch
 
     hy = importlib.import_module("hyrise-1_amd")

@@ -1,0 +1,464 @@
+"""TPC-H 3 on one GPU (BASELINE.json configs[4] at N=1): `python bench.py --workload q3`.
+
+One step is the reference's plan for tpch_queries.cpp:101-106, on columns resident in HBM, through the C-ABI:
+
+    TableScan(customer, c_mktsegment = 'BUILDING')                       hy_table_scan_row_ids (dictionary u8)
+    JoinHash(<customer scan>, TableScan(orders, o_orderdate < 1995-03-15), c_custkey = o_custkey)
+                                                                          hy_scan_join_hash: the orders scan runs
+                                                                          inside the join's first partition pass
+    JoinHash(<that join>, TableScan(lineitem, l_shipdate > 1995-03-15), o_orderkey = l_orderkey)
+                                                                          hy_scan_join_hash, same fusion
+    Projection(l_orderkey, o_orderdate, o_shippriority, l_extendedprice * (1 - l_discount))   hy_projection x 4
+    Aggregate(GROUP BY l_orderkey, o_orderdate, o_shippriority; SUM(revenue))                  hy_aggregate
+
+The builds are the smaller inputs (the reference's swap rule, join_hash.cpp:55-76; checked after the run), radix bits
+come from the build input's row count (join_hash.cpp:640-668), so the step reads the customer scan's per-chunk counts
+and each join's partition bounds back to the host, as the operators would. A join's output chunks are its non-empty
+radix partitions in ascending order (write_output_columns). The second join's build side dereferences the first join's
+orders PosLists (the orders columns of the join output); the customer columns are not read after the first join
+(the reference's column pruning). ORDER BY / LIMIT (Sort) is outside the hot path.
+
+Dates are int32 days in per-chunk dictionaries (u16 value ids, the reference's default Dictionary encoding; ISO date
+strings order like their days), c_mktsegment is a u8 dictionary of its five codes, keys are unencoded int32 columns.
+Rows/s counts the base rows consumed (customer + orders + lineitem). The result is checked against torch on the same
+columns: match and pair counts, group count and every sampled group's SUM exactly (an order's revenue is a sum of
+<= 7 float products, exact in double).
+"""
+import ctypes
+import importlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+INVALID_VALUE_ID = 0xFFFFFFFF
+
+
+def dict_predicate(capi, lb, ub, dict_size, cond):
+    """(op, search_vid) for a dictionary chunk, from lower_bound / upper_bound value ids of the constant
+    (single_column_table_scan_impl.cpp:145-205 via operators.cpp dictionary_predicate; INVALID when at the end)."""
+    lb = INVALID_VALUE_ID if lb >= dict_size else lb
+    ub = INVALID_VALUE_ID if ub >= dict_size else ub
+    svid = ub if cond in ("LessThanEquals", "GreaterThan") else lb
+    one = dict_size == 1
+    if cond == "Equals":
+        all_, none = svid != ub and one, svid == ub
+    elif cond in ("LessThan", "LessThanEquals"):
+        all_, none = svid == INVALID_VALUE_ID, svid == 0
+    else:
+        all_, none = svid == 0, svid == INVALID_VALUE_ID
+    if all_:
+        return capi.HY_OP_ALL, svid
+    if none:
+        return capi.HY_OP_NONE, svid
+    return {"Equals": capi.HY_OP_EQ, "LessThan": capi.HY_OP_LT, "LessThanEquals": capi.HY_OP_LT}.get(
+        cond, capi.HY_OP_GE), svid
+
+
+class DictColumn:
+    """A chunked integer column dictionary-encoded per chunk on the device (vids u8 / u16 by dictionary size)."""
+
+    def __init__(self, torch, synth, capi, values, chunk, lo, domain):
+        vids, present = synth.dictionary_encode_chunks(values, chunk, lo, domain)
+        n = values.numel()
+        self.n_chunks = present.shape[0]
+        self.sizes = [min(chunk, n - c * chunk) for c in range(self.n_chunks)]
+        dsize = present.sum(dim=1)
+        # dictionaries: dict[c, rank] = lo + value index, one row of `domain` int32 per chunk
+        rank = torch.cumsum(present.to(torch.int32), dim=1) - 1
+        rows, js = torch.nonzero(present, as_tuple=True)
+        self.dicts = torch.zeros(self.n_chunks, domain, dtype=torch.int32, device=values.device)
+        self.dicts[rows, rank[rows, js].long()] = (lo + js).to(torch.int32)
+        self.cum = torch.cumsum(present.to(torch.int64), dim=1).cpu().numpy()  # cum[c, j] = #values <= lo + j
+        self.dsize = dsize.cpu().numpy()
+        self.lo, self.domain = lo, domain
+        wide = self.dsize > 0xFF
+        self.v16 = torch.cat([vids.to(torch.int16), torch.zeros(64, dtype=torch.int16, device=values.device)])
+        self.v8 = torch.cat([vids.to(torch.uint8), torch.zeros(64, dtype=torch.uint8, device=values.device)]) \
+            if not wide.all() else None
+        self.desc = (capi.ColumnChunk * self.n_chunks)()
+        for c in range(self.n_chunks):
+            d = self.desc[c]
+            w = 2 if wide[c] else 1
+            d.data = (self.v16.data_ptr() + 2 * c * chunk) if w == 2 else (self.v8.data_ptr() + c * chunk)
+            d.size = self.sizes[c]
+            d.kind, d.vid_width = capi.HY_COL_DICT, w
+            d.dictionary = self.dicts.data_ptr() + 4 * domain * c
+            d.dictionary_size = int(self.dsize[c])
+
+    def scan_chunks(self, capi, cond, value):
+        arr = (capi.ScanChunk * self.n_chunks)()
+        j = value - self.lo
+        for c in range(self.n_chunks):
+            lb = int(self.cum[c, j - 1]) if 0 < j <= self.domain else (0 if j <= 0 else int(self.dsize[c]))
+            ub = int(self.cum[c, j]) if 0 <= j < self.domain else (0 if j < 0 else int(self.dsize[c]))
+            s = arr[c]
+            s.column = self.desc[c]
+            s.op, s.search_vid = dict_predicate(capi, lb, ub, int(self.dsize[c]), cond)
+        return arr
+
+
+def value_chunks(capi, t, chunk, width):
+    n = t.numel() - 64
+    n_chunks = (n + chunk - 1) // chunk
+    arr = (capi.ColumnChunk * n_chunks)()
+    for c in range(n_chunks):
+        arr[c].data = t.data_ptr() + width * c * chunk
+        arr[c].size = min(chunk, n - c * chunk)
+        arr[c].kind = capi.HY_COL_VALUE
+    return arr
+
+
+def data_side(capi, cols, value_type):
+    arr = (capi.JoinChunk * len(cols))()
+    for c in range(len(cols)):
+        arr[c].column = cols[c]
+        arr[c].size = cols[c].size
+        arr[c].chunk_id = c
+        arr[c].single_chunk = capi.HY_MIXED_CHUNKS
+    side = capi.JoinSide(arr, len(cols), value_type, None, 0, 0, 0)
+    side._keep = arr
+    return side
+
+
+def expr_column(capi, col, vtype):
+    return capi.ExprNode(capi.HY_EXPR_COLUMN, vtype, 0, col, 0)
+
+
+def main_q3(args):
+    import numpy as np
+    import torch
+
+    if int(os.environ.get("WORLD_SIZE", "1")) != 1:
+        raise SystemExit("--workload q3 runs on one GPU (BASELINE.json configs[4] at N=1)")
+    sys.path.insert(0, ROOT)
+    hy = importlib.import_module("hyrise-1_amd")
+    synth = importlib.import_module("hyrise-1_amd.synth")
+    capi = hy.capi
+    L = capi.lib
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    capi.check(L.hy_set_device(0), "hy_set_device")
+    stream = torch.cuda.current_stream().cuda_stream
+    chunk = args.chunk
+    D = synth.DATE_1995_03_15
+    I32, F32 = capi.HY_TYPE_INT32, capi.HY_TYPE_FLOAT
+
+    # ---------------- data ----------------
+    cols = synth.q3_columns(args.sf, dev)
+    n_cust, n_ord, n_li = (cols[k].numel() for k in ("c_custkey", "o_orderkey", "l_orderkey"))
+    # expected result (torch on the same columns)
+    seg_ok = cols["c_mktsegment"] == 1  # BUILDING
+    o_date_ok = cols["o_orderdate"] < D
+    o_ok = o_date_ok & seg_ok[cols["o_custkey"].long() - 1]
+    l_date_ok = cols["l_shipdate"] > D
+    l_ok = l_date_ok & o_ok[cols["l_order_index"]]
+    exp = {"customer_matches": int(seg_ok.sum()), "orders_matches": int(o_date_ok.sum()),
+           "lineitem_matches": int(l_date_ok.sum()), "join1_pairs": int(o_ok.sum()), "join2_pairs": int(l_ok.sum())}
+    rev = cols["l_extendedprice"] * (1 - cols["l_discount"])  # float32, as the projection computes it
+    order_rev = torch.zeros(n_ord, dtype=torch.float64, device=dev).index_add_(
+        0, cols["l_order_index"][l_ok], rev[l_ok].to(torch.float64))
+    order_hit = torch.zeros(n_ord, dtype=torch.bool, device=dev)
+    order_hit[cols["l_order_index"][l_ok]] = True
+    exp["groups"] = int(order_hit.sum())
+    del seg_ok, o_date_ok, o_ok, l_date_ok, l_ok, rev
+
+    def padded(t):
+        return torch.cat([t.contiguous(), torch.zeros(64, dtype=t.dtype, device=t.device)])
+
+    seg = DictColumn(torch, synth, capi, cols["c_mktsegment"], chunk, 0, 5)
+    odate = DictColumn(torch, synth, capi, cols["o_orderdate"], chunk, synth.DATE_1992_01_01,
+                       synth.DATE_1998_08_02 - synth.DATE_1992_01_01 + 1)
+    ship = DictColumn(torch, synth, capi, cols["l_shipdate"], chunk, synth.DATE_1992_01_01,
+                      synth.DATE_1998_08_02 + 121 - synth.DATE_1992_01_01 + 1)
+    ckey, ocust, okey = padded(cols["c_custkey"]), padded(cols["o_custkey"]), padded(cols["o_orderkey"])
+    oprio, lkey = padded(cols["o_shippriority"]), padded(cols["l_orderkey"])
+    price, disc = padded(cols["l_extendedprice"]), padded(cols["l_discount"])
+    del cols
+    torch.cuda.synchronize()
+    ckey_c, ocust_c, okey_c = (value_chunks(capi, t, chunk, 4) for t in (ckey, ocust, okey))
+    oprio_c, lkey_c, price_c, disc_c = (value_chunks(capi, t, chunk, 4) for t in (oprio, lkey, price, disc))
+    n_cc, n_oc, n_lc = len(ckey_c), len(okey_c), len(lkey_c)
+
+    # ---------------- operators' fixed descriptors ----------------
+    cscan = seg.scan_chunks(capi, "Equals", 1)
+    for c in range(n_cc):
+        cscan[c].out_begin = c * chunk
+    c_ids = (ctypes.c_uint32 * n_cc)(*range(n_cc))
+    wsb = ctypes.c_size_t(0)
+    capi.check(L.hy_table_scan_workspace_size((ctypes.c_uint32 * n_cc)(*seg.sizes), n_cc, ctypes.byref(wsb)), "ws")
+    c_ws = torch.empty(max(16, wsb.value), dtype=torch.uint8, device=dev)
+    c_rows = torch.empty(2 * n_cust + 64, dtype=torch.int32, device=dev)
+    c_counts = torch.empty(n_cc, dtype=torch.int32, device=dev)
+    L.hy_table_scan_row_ids.restype = ctypes.c_int
+    L.hy_table_scan_row_ids.argtypes = [ctypes.POINTER(capi.ScanChunk), ctypes.c_uint32, ctypes.c_int32,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+
+    orders_side = data_side(capi, ocust_c, I32)
+    li_side = data_side(capi, lkey_c, I32)
+    o_off = torch.empty(n_ord + 64, dtype=torch.int32, device=dev)
+    o_begin = torch.zeros(n_oc + 1, dtype=torch.int64, device=dev)
+    ofilter = capi.JoinFilter(odate.scan_chunks(capi, "LessThan", D), I32, None, o_off.data_ptr(), o_begin.data_ptr())
+    l_off = torch.empty(n_li + 64, dtype=torch.int32, device=dev)
+    l_begin = torch.zeros(n_lc + 1, dtype=torch.int64, device=dev)
+    lfilter = capi.JoinFilter(ship.scan_chunks(capi, "GreaterThan", D), I32, None, l_off.data_ptr(),
+                              l_begin.data_ptr())
+    jc_dtype = np.dtype(capi.JoinChunk)
+    cc_dtype = np.dtype(capi.ColumnChunk)
+    state = {"ws": {}, "cap": {}}
+
+    def workspace(key, query):
+        if key not in state["ws"]:
+            b = ctypes.c_size_t(0)
+            capi.check(query(ctypes.byref(b)), "workspace size")
+            state["ws"][key] = torch.empty(max(16, b.value), dtype=torch.uint8, device=dev)
+        return state["ws"][key]
+
+    def out_pairs(tag, cap):
+        if state["cap"].get(tag, (0,))[0] < cap:
+            state["cap"][tag] = (cap, torch.empty(2 * cap, dtype=torch.int32, device=dev),
+                                 torch.empty(2 * cap, dtype=torch.int32, device=dev))
+        return state["cap"][tag]
+
+    def ref_side(pos_base, begins, counts, single, referenced, n_referenced):
+        """A reference input's join side: chunk k = PosList pos_base + 8 * begins[k] of counts[k] RowIDs."""
+        arr = np.zeros(len(counts), jc_dtype)
+        arr["pos_list"] = pos_base + 8 * begins.astype(np.uint64)
+        arr["size"] = counts
+        arr["chunk_id"] = np.arange(len(counts), dtype=np.uint32)
+        arr["single_chunk"] = single
+        side = capi.JoinSide(arr.ctypes.data_as(ctypes.POINTER(capi.JoinChunk)), len(counts), I32, referenced,
+                             n_referenced, 1, 0)
+        side._keep = arr
+        return side
+
+    def join(tag, build, probe, pfilter, bits, cap_hint):
+        params = capi.JoinParams(capi.HY_JOIN_INNER, I32, bits, 17)
+        ws = workspace((tag, bits, build.n_chunks), lambda b: L.hy_scan_join_hash_workspace_size(
+            ctypes.byref(build), None, ctypes.byref(probe), ctypes.byref(pfilter), ctypes.byref(params), b))
+        pb = torch.empty(1 << bits, dtype=torch.int64, device=dev)
+        pc = torch.empty(1 << bits, dtype=torch.int32, device=dev)
+        while True:
+            cap, ob, op = out_pairs(tag, cap_hint)
+            res = capi.JoinResult()
+            st = L.hy_scan_join_hash(ctypes.byref(build), None, ctypes.byref(probe), ctypes.byref(pfilter),
+                                     ctypes.byref(params), ob.data_ptr(), op.data_ptr(), cap, pb.data_ptr(),
+                                     pc.data_ptr(), ctypes.byref(res), ws.data_ptr(), ws.numel(), stream)
+            if st != capi.HY_ERR_CAPACITY:
+                capi.check(st, "hy_scan_join_hash " + tag)
+                break
+            cap_hint = res.capacity_required + 64
+        pb_h, pc_h = pb.cpu().numpy(), pc.cpu().numpy()
+        nz = np.nonzero(pc_h)[0]
+        return ob, op, pb_h[nz], pc_h[nz].astype(np.uint32), res.total_pairs
+
+    proj_cols = (capi.AggColumn * 5)()
+    for j, (vt, g, ch) in enumerate([(I32, 1, lkey_c), (I32, 0, odate.desc), (I32, 0, oprio_c), (F32, 1, price_c),
+                                     (F32, 1, disc_c)]):
+        proj_cols[j].value_type, proj_cols[j].pos_group, proj_cols[j].chunks, proj_cols[j].n_chunks = vt, g, ch, len(ch)
+    programs = [[expr_column(capi, 0, I32)], [expr_column(capi, 1, I32)], [expr_column(capi, 2, I32)],
+                [expr_column(capi, 3, F32), capi.ExprNode(capi.HY_EXPR_VALUE, I32, 0, 0, 1),
+                 expr_column(capi, 4, F32), capi.ExprNode(capi.HY_EXPR_SUB, F32, F32, 0, 0),
+                 capi.ExprNode(capi.HY_EXPR_MUL, F32, F32, 0, 0)]]
+    programs = [(capi.ExprNode * len(p))(*p) for p in programs]
+    groupby = (ctypes.c_int32 * 3)(0, 1, 2)
+    agg_defs = (capi.AggDef * 1)(capi.AggDef(capi.HY_AGG_SUM, 3))
+    agg_params = capi.AggParams(groupby, 3, agg_defs, 1, 0)
+
+    def step():
+        # TableScan(customer, c_mktsegment = 'BUILDING'): its output's chunk layout decides the join's build input
+        capi.check(L.hy_table_scan_row_ids(cscan, n_cc, I32, None, c_ids, c_rows.data_ptr(), c_counts.data_ptr(),
+                                           c_ws.data_ptr(), c_ws.numel(), stream), "customer scan")
+        cc = c_counts.cpu().numpy()
+        nz = np.nonzero(cc)[0]
+        c_match = int(cc.sum())
+        build1 = ref_side(c_rows.data_ptr(), nz.astype(np.uint64) * chunk, cc[nz].astype(np.uint32),
+                          nz.astype(np.uint32), ckey_c, n_cc)
+        j1b, j1p, b1, n1, pairs1 = join("j1", build1, orders_side, ofilter, L.hy_join_radix_bits(c_match, 4),
+                                        n_ord // 4 + 64)
+        build2 = ref_side(j1p.data_ptr(), b1, n1, capi.HY_MIXED_CHUNKS, okey_c, n_oc)
+        j2b, j2p, b2, n2, pairs2 = join("j2", build2, li_side, lfilter, L.hy_join_radix_bits(pairs1, 4),
+                                        n_li // 32 + 64)
+        # Projection over the join output (chunks = non-empty partitions; PosList groups: orders, lineitem)
+        k = len(n2)
+        sizes_np = np.ascontiguousarray(n2, dtype=np.uint32)
+        pls_np = np.concatenate([j2b.data_ptr() + 8 * b2.astype(np.uint64), j2p.data_ptr() + 8 * b2.astype(np.uint64)])
+        sizes = sizes_np.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+        pls = pls_np.ctypes.data_as(ctypes.POINTER(ctypes.c_void_p))
+        pin = capi.AggInput(k, sizes, pls, 2, proj_cols, 5)
+        pws = workspace(("proj", k), lambda b: L.hy_projection_workspace_size(ctypes.byref(pin), b))
+        if state.get("proj_rows", 0) < pairs2:
+            state["proj_rows"] = pairs2
+            state["proj"] = torch.empty(4, pairs2 + 64, dtype=torch.int32, device=dev)
+        proj = state["proj"]
+        for j, prog in enumerate(programs):
+            capi.check(L.hy_projection(ctypes.byref(pin), prog, len(prog), proj[j].data_ptr(), None, pws.data_ptr(),
+                                       pws.numel(), stream), "hy_projection")
+        # Aggregate over the projection's output (a data table with the join output's chunking)
+        rb = np.concatenate([[0], np.cumsum(n2.astype(np.int64))])[:-1].astype(np.uint64)
+        acols = (capi.AggColumn * 4)()
+        keep = []
+        for j, vt in enumerate([I32, I32, I32, F32]):
+            ch = np.zeros(max(1, k), cc_dtype)
+            ch["data"][:k] = proj[j].data_ptr() + 4 * rb
+            ch["size"][:k] = n2
+            ch["kind"] = capi.HY_COL_VALUE
+            keep.append(ch)
+            acols[j].value_type, acols[j].pos_group, acols[j].n_chunks = vt, -1, k
+            acols[j].chunks = ch.ctypes.data_as(ctypes.POINTER(capi.ColumnChunk))
+        ain = capi.AggInput(k, sizes, None, 0, acols, 4)
+        if "layout" not in state:
+            lay = capi.AggLayout()
+            capi.check(L.hy_aggregate_layout(ctypes.byref(ain), ctypes.byref(agg_params), ctypes.byref(lay)), "layout")
+            state["layout"] = lay
+        words = state["layout"].words
+        aws = workspace(("agg", k, pairs2), lambda b: L.hy_aggregate_workspace_size(ctypes.byref(ain),
+                                                                                     ctypes.byref(agg_params), b))
+        if state.get("agg_cap", 0) < pairs2 + 1:
+            state["agg_cap"] = pairs2 + 1
+            state["agg_out"] = torch.empty((pairs2 + 1) * words, dtype=torch.int64, device=dev)
+        ng = ctypes.c_uint64(0)
+        capi.check(L.hy_aggregate(ctypes.byref(ain), ctypes.byref(agg_params), state["agg_out"].data_ptr(),
+                                  state["agg_cap"], ctypes.byref(ng), aws.data_ptr(), aws.numel(), stream),
+                   "hy_aggregate")
+        return {"customer_matches": c_match, "join1_pairs": int(pairs1), "join2_pairs": int(pairs2),
+                "groups": int(ng.value)}
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    L.hy_kernel_stats_reset()
+    L.hy_kernel_stats_enable(1)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        got = step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    L.hy_kernel_stats_enable(0)
+    got["orders_matches"] = int(o_begin[-1].item())
+    got["lineitem_matches"] = int(l_begin[-1].item())
+
+    # ---------------- check ----------------
+    lay = state["layout"]
+    rec = state["agg_out"].view(-1, lay.words)[:got["groups"]].cpu().numpy().view(np.uint64)
+    ok = got == exp
+    # the reference's swap rule kept the builds on the smaller inputs
+    ok &= got["customer_matches"] <= got["orders_matches"] and got["join1_pairs"] <= got["lineitem_matches"]
+    rng = np.random.default_rng(3)
+    sample = rng.choice(rec.shape[0], size=min(2000, rec.shape[0]), replace=False) if rec.shape[0] else []
+    order_rev_h = order_rev.cpu().numpy()
+    w = lay.agg_word[0]
+    for g in sample:
+        r = rec[g]
+        key = int(np.int32(np.uint32(r[0])))
+        oi = ((key >> 5) << 3) + (key & 7) - 1  # inverse of the dbgen sparse order key
+        limbs = (ctypes.c_uint64 * lay.agg_limbs[0])(*[int(x) for x in r[w + 2:w + 2 + lay.agg_limbs[0]]])
+        s = ctypes.c_double(0)
+        capi.check(L.hy_agg_float_sum(limbs, lay.agg_limbs[0], lay.agg_emin[0], int(r[w + 1]), ctypes.byref(s)))
+        ok &= s.value == order_rev_h[oi]
+    if not ok:
+        raise SystemExit(f"q3 result mismatch: {got} vs {exp}")
+
+    from bench import kernel_stats, measured_roofline, host_cpu  # noqa: E402  (shared helpers)
+
+    kernels = kernel_stats(L)
+    K = args.steps
+    step_s = elapsed / K
+    # algorithmic bytes (SURVEY.md 8(d) per operator): scans 1 B (u8 vids) / 2 B (u16 vids) per row read + output
+    # (8 B RowIDs customer, 4 B offsets for the fused scans); JoinHash 4 B per build row + 4 B per probe row + 16 B
+    # per pair; Projection per row 2 RowIDs + 4 x 4 B read... (16 + 20) in, 16 out; Aggregate per row 16 B in
+    cm, om, lm = got["customer_matches"], got["orders_matches"], got["lineitem_matches"]
+    p1, p2 = got["join1_pairs"], got["join2_pairs"]
+    alg = {"scans": n_cust * 1 + cm * 8 + n_ord * 2 + om * 4 + n_li * 2 + lm * 4,
+           "join1": cm * 4 + om * 4 + p1 * 16, "join2": p1 * 4 + lm * 4 + p2 * 16,
+           "projection": p2 * (16 + 20 + 16), "aggregate": p2 * 16}
+    e2e = sum(alg.values())
+    peak, probe = measured_roofline(L, capi, torch, dev, stream, args.probe_gb)
+    for v in kernels.values():
+        v["ms_per_launch"] = v["ms_total"] / max(v["launches"], 1)
+    dom = max(kernels, key=lambda k: kernels[k]["ms_total"])
+    roofline = {"bound": "hbm", "scope": "end-to-end step (algorithmic bytes of SURVEY 8(d) per operator)",
+                "achieved": round(e2e / step_s / 1e9, 1), "peak": round(peak, 1), "unit": "GB/s",
+                "frac": round(e2e / step_s / 1e9 / peak, 4), "alg_bytes_per_step": e2e, "alg_bytes": alg,
+                "traffic": None, "peak_source": "measured in this run (hy_stream_bandwidth_probe, best of read / copy)",
+                "dominant_kernel": dom, "dominant_ms_per_step": round(kernels[dom]["ms_total"] / K, 4)}
+    cpu = None if args.no_cpu_baseline else cpu_baseline_q3(hy, synth, args.cpu_sf, chunk, host_cpu)
+    line = {
+        "metric": "rows/sec TPC-H 3 (Scan -> JoinHash -> JoinHash -> Projection -> Aggregate), one MI355X",
+        "value": round((n_cust + n_ord + n_li) / step_s, 1), "unit": "rows/s", "n_gpus": 1, "steps": K,
+        "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "int32/f32", "data": "synthetic (seeded counter-based TPC-H-shaped columns, "
+                                                           "resident in HBM)",
+        "config": {"workload": "TPC-H 3 (tpch_queries.cpp:101-106) without ORDER BY/LIMIT", "sf": args.sf,
+                   "customer_rows": n_cust, "orders_rows": n_ord, "lineitem_rows": n_li, "chunk_size": chunk,
+                   **got, "parallelism": "single GPU"},
+        "check": {"ok": bool(ok), "expected": exp, "sampled_groups": len(sample)},
+        "roofline": roofline,
+        "hbm_probe": probe,
+        "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
+                    for k, v in kernels.items()},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line))
+
+
+def cpu_baseline_q3(hy, synth, sf, chunk, host_cpu, runs=5):
+    """The oracle's Q3 operator chain (same plan, the reference's per-chunk / per-partition jobs) on a bounded sample
+    of the same synthetic columns (dictionary-encoded like the reference default). Median of `runs` on all host cores
+    of this process at SF `sf`, and on one core at a fifth of it."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import helpers
+
+    oracle = helpers.load_oracle()
+    threads, model = host_cpu()
+    I, F = hy.DataType.Int, hy.DataType.Float
+    P, A, O, V = (hy.PQPColumnExpression.from_table, hy.ArithmeticExpression, hy.ArithmeticOperator,
+                  hy.ValueExpression)
+    D = synth.DATE_1995_03_15
+    cond = hy.PredicateCondition
+    out = {"unit": "rows/s", "kind": "port", "cpu_model": model, "nproc": os.cpu_count()}
+    for label, n_threads, sample_sf in (("all_cores", threads, sf), ("one_core", 1, sf / 5)):
+        c = {k: v.numpy() for k, v in synth.q3_columns(sample_sf, "cpu").items()}
+        customer = hy.Table.from_arrays([("c_custkey", I, False), ("c_mktsegment", I, False)],
+                                        [c["c_custkey"], c["c_mktsegment"]], [], chunk)
+        orders = hy.Table.from_arrays([("o_orderkey", I, False), ("o_custkey", I, False), ("o_orderdate", I, False),
+                                       ("o_shippriority", I, False)],
+                                      [c["o_orderkey"], c["o_custkey"], c["o_orderdate"], c["o_shippriority"]], [],
+                                      chunk)
+        lineitem = hy.Table.from_arrays([("l_orderkey", I, False), ("l_extendedprice", F, False),
+                                         ("l_discount", F, False), ("l_shipdate", I, False)],
+                                        [c["l_orderkey"], c["l_extendedprice"], c["l_discount"], c["l_shipdate"]], [],
+                                        chunk)
+        del c
+        for t in (customer, orders, lineitem):
+            hy.encode_all_chunks(t, hy.EncodingType.Dictionary)
+
+        def run():
+            cs = oracle.table_scan(customer, 1, cond.Equals, 1, [])
+            os_ = oracle.table_scan(orders, 2, cond.LessThan, D, [])
+            ls = oracle.table_scan(lineitem, 3, cond.GreaterThan, D, [])
+            j1, _ = oracle.join_hash(cs, os_, hy.JoinMode.Inner, (0, 1))
+            j2, _ = oracle.join_hash(j1, ls, hy.JoinMode.Inner, (2, 0))
+            p = oracle.projection(j2, [P(j2, 6), P(j2, 4), P(j2, 5),
+                                       A(O.Multiplication, P(j2, 7), A(O.Subtraction, V(1), P(j2, 8)))])
+            return oracle.aggregate(p, [hy.AggregateColumnDefinition(3, hy.AggregateFunction.Sum)], [0, 1, 2])
+
+        rows = customer.row_count() + orders.row_count() + lineitem.row_count()
+        oracle.set_threads(n_threads)
+        times = []
+        for _ in range(runs + 1):  # the first run warms caches and allocators
+            t0 = time.perf_counter()
+            agg = run()
+            times.append(time.perf_counter() - t0)
+        oracle.set_threads(1)
+        med = sorted(times[1:])[len(times[1:]) // 2]
+        out[label] = {"value": round(rows / med, 1), "cores": n_threads, "median_s": round(med, 3),
+                      "runs_s": [round(t, 3) for t in times[1:]],
+                      "sample": f"SF{sample_sf:g}: {customer.row_count()} customer + {orders.row_count()} orders + "
+                                f"{lineitem.row_count()} lineitem rows, {agg.row_count()} groups"}
+        del customer, orders, lineitem, agg
+    out["value"], out["cores"] = out["all_cores"]["value"], out["all_cores"]["cores"]
+    out["sample"] = out["all_cores"]["sample"] + f"; median of {runs}"
+    return out

@@ -23,6 +23,7 @@ HY_JOIN_INNER, HY_JOIN_LEFT, HY_JOIN_RIGHT, HY_JOIN_SEMI, HY_JOIN_ANTI = 0, 1, 2
 HY_AGG_MIN, HY_AGG_MAX, HY_AGG_SUM, HY_AGG_AVG, HY_AGG_COUNT, HY_AGG_COUNT_DISTINCT = range(6)
 HY_AGG_MAX_AGGREGATES = 16
 HY_PROBE_READ, HY_PROBE_COPY = 0, 1
+HY_EXPR_COLUMN, HY_EXPR_VALUE, HY_EXPR_ADD, HY_EXPR_SUB, HY_EXPR_MUL, HY_EXPR_DIV, HY_EXPR_MOD = range(7)
 
 
 class RowID(ctypes.Structure):
@@ -96,6 +97,11 @@ class AggLayout(ctypes.Structure):
                 ("agg_limbs", ctypes.c_uint32 * HY_AGG_MAX_AGGREGATES)]
 
 
+class ExprNode(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("type", ctypes.c_int32), ("calc_type", ctypes.c_int32),
+                ("column", ctypes.c_int32), ("value", ctypes.c_uint64)]
+
+
 _sigs = {
     "hy_get_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "hy_set_device": (ctypes.c_int, [ctypes.c_int]),
@@ -138,6 +144,10 @@ _sigs = {
     "hy_aggregate": (ctypes.c_int, [ctypes.POINTER(AggInput), ctypes.POINTER(AggParams), ctypes.c_void_p,
                                     ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p,
                                     ctypes.c_size_t, ctypes.c_void_p]),
+    "hy_projection_workspace_size": (ctypes.c_int, [ctypes.POINTER(AggInput), ctypes.POINTER(ctypes.c_size_t)]),
+    "hy_projection": (ctypes.c_int, [ctypes.POINTER(AggInput), ctypes.POINTER(ExprNode), ctypes.c_uint32,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                     ctypes.c_void_p]),
     "hy_agg_float_sum": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32, ctypes.c_int32,
                                         ctypes.c_uint64, ctypes.POINTER(ctypes.c_double)]),
     "hy_agg_decode_ordered": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_int32]),

@@ -319,10 +319,12 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
     hyk::AggTable t{w.state, w.records, plan.cap, w.dstate, w.dkeys, plan.dcap};
     HY_HIP(hipMemsetAsync(w.state, 0, 4 * plan.cap, s));
     if (plan.dcap) HY_HIP(hipMemsetAsync(w.dstate, 0, 4 * plan.dcap, s));
-    if (plan.n_tiles) {
-      KTimer kt("agg_hash_rows", s, plan.rows);
-      hipLaunchKernelGGL(hyk::agg_hash_rows, dim3(static_cast<uint32_t>(plan.n_tiles)), dim3(hyk::AGG_THREADS), 0, s,
-                         d, t);
+    if (plan.rows) {
+      KTimer kt("agg_hash_runs", s, plan.rows);
+      const uint32_t items = hyk::flat_items(plan.rows);  // tiles over global rows
+      const uint64_t tile_rows = uint64_t(hyk::AGG_THREADS) * items;
+      hipLaunchKernelGGL(hyk::agg_hash_runs, dim3(static_cast<uint32_t>((plan.rows + tile_rows - 1) / tile_rows)),
+                         dim3(hyk::AGG_THREADS), 0, s, d, t, plan.rows, items);
       kt.done();
       HY_HIP(hipGetLastError());
     }
@@ -348,25 +350,13 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
 namespace {
 
 struct ProjWs {
-  uint32_t* sizes;
   uint64_t* row_begin;
-  uint64_t* tile_begin;
-  uint32_t* tile_owner;
   const hy_row_id** pos_lists;
   hy_column_chunk* chunks[hyk::AGG_MAX_COLUMNS];
 };
 
-uint64_t proj_tiles(const hy_agg_input* in) {
-  uint64_t t = 0;
-  for (uint32_t c = 0; c < in->n_chunks; ++c) t += (in->chunk_sizes[c] + hyk::PROJ_TILE - 1) / hyk::PROJ_TILE;
-  return t;
-}
-
 void carve_proj(Carver& cv, const hy_agg_input* in, ProjWs* w) {
-  w->sizes = cv.take<uint32_t>(std::max<uint32_t>(1, in->n_chunks));
   w->row_begin = cv.take<uint64_t>(in->n_chunks + 1);
-  w->tile_begin = cv.take<uint64_t>(in->n_chunks + 1);
-  w->tile_owner = cv.take<uint32_t>(std::max<uint64_t>(1, proj_tiles(in)));
   w->pos_lists = cv.take<const hy_row_id*>(std::max<uint64_t>(1, uint64_t(in->n_pos_groups) * in->n_chunks));
   for (uint32_t j = 0; j < in->n_columns; ++j)
     w->chunks[j] = cv.take<hy_column_chunk>(std::max<uint32_t>(1, in->columns[j].n_chunks));
@@ -443,22 +433,19 @@ hy_status hy_projection(const hy_agg_input* input, const hy_expr_node* program, 
   prog.n_nodes = n_nodes;
   prog.out_type = program[n_nodes - 1].type;
   if (prog.out_type == 0) return fail(HY_ERR_UNSUPPORTED, "an all-NULL expression has no column type");
-  const uint64_t tiles = proj_tiles(input);
-  if (tiles == 0) return HY_OK;
+  std::vector<uint64_t> row_begin(input->n_chunks + 1, 0);
+  for (uint32_t c = 0; c < input->n_chunks; ++c) row_begin[c + 1] = row_begin[c] + input->chunk_sizes[c];
+  const uint64_t rows = row_begin[input->n_chunks];
+  if (rows == 0) return HY_OK;
+  const uint32_t items = hyk::flat_items(rows);  // tiles over global rows
+  const uint64_t tiles = (rows + uint64_t(hyk::AGG_THREADS) * items - 1) / (uint64_t(hyk::AGG_THREADS) * items);
   if (!out_values) return fail(HY_ERR_INVALID_ARGUMENT, "out_values");
   hipStream_t s = S(stream);
   Carver cv{static_cast<char*>(workspace), workspace_bytes};
   ProjWs w;
   carve_proj(cv, input, &w);
   if (!cv.ok || !workspace) return fail(HY_ERR_WORKSPACE, "projection workspace too small");
-  std::vector<uint64_t> row_begin(input->n_chunks + 1, 0), tile_begin(input->n_chunks + 1, 0);
-  for (uint32_t c = 0; c < input->n_chunks; ++c) {
-    row_begin[c + 1] = row_begin[c] + input->chunk_sizes[c];
-    tile_begin[c + 1] = tile_begin[c] + (input->chunk_sizes[c] + hyk::PROJ_TILE - 1) / hyk::PROJ_TILE;
-  }
-  HY_HIP(hipMemcpyAsync(w.sizes, input->chunk_sizes, 4 * input->n_chunks, hipMemcpyHostToDevice, s));
   HY_HIP(hipMemcpyAsync(w.row_begin, row_begin.data(), 8 * row_begin.size(), hipMemcpyHostToDevice, s));
-  HY_HIP(hipMemcpyAsync(w.tile_begin, tile_begin.data(), 8 * tile_begin.size(), hipMemcpyHostToDevice, s));
   const uint64_t n_pl = uint64_t(input->n_pos_groups) * input->n_chunks;
   if (n_pl) HY_HIP(hipMemcpyAsync(w.pos_lists, input->pos_lists, sizeof(void*) * n_pl, hipMemcpyHostToDevice, s));
   hyk::AggDesc d{};
@@ -477,17 +464,10 @@ hy_status hy_projection(const hy_agg_input* input, const hy_expr_node* program, 
     d.cols[j].pos_group = c.pos_group;
   }
   d.pos_lists = w.pos_lists;
-  d.chunk_size = w.sizes;
   d.chunk_row_begin = w.row_begin;
-  d.chunk_tile_begin = w.tile_begin;
-  d.tile_chunk = w.tile_owner;
-  hipLaunchKernelGGL(hyk::fill_tile_owner, dim3((input->n_chunks + 255) / 256), dim3(256), 0, s, w.tile_begin,
-                     input->n_chunks, w.tile_owner);
-  HY_HIP(hipGetLastError());
-  uint64_t rows = row_begin[input->n_chunks];
   KTimer t("projection", s, rows);
   hipLaunchKernelGGL(hyk::projection_kernel, dim3(static_cast<uint32_t>(tiles)), dim3(hyk::AGG_THREADS), 0, s, d, prog,
-                     out_values, out_nulls);
+                     out_values, out_nulls, rows, items);
   t.done();
   HY_HIP(hipGetLastError());
   // host staging above must outlive the async copies

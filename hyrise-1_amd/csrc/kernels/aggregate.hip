@@ -30,9 +30,10 @@
 //                   last row) and 64-bit butterfly reductions (sums, min/max), one lane updates the workgroup's LDS
 //                   records; a workgroup flushes its records to HBM with a handful of atomics at the end. This is the
 //                   TPC-H Q1 shape (4 groups over 6e8 rows): HBM-bound on the column reads.
-//   agg_hash_rows   general keys: a global open-addressing table of group records in HBM (linear probing, claim by
-//                   CAS, record initialised before the slot is published), accumulators updated with global atomics.
-//                   COUNT(DISTINCT) inserts (group slot, aggregate, value) into a second global set.
+//   agg_hash_runs   general keys: a global open-addressing table of group records in HBM (linear probing, claim by
+//                   CAS, record initialised before the slot is published), accumulators updated with global atomics,
+//                   once per run of equal keys inside a wave. COUNT(DISTINCT) inserts (group slot, aggregate, value)
+//                   into a second global set.
 #include <hip/hip_runtime.h>
 
 #include "common.hpp"
@@ -774,21 +775,35 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
   return x;
 }
 
+// Group table visibility (MI355X_MICROARCH.md, inter-workgroup visibility: the "8-B agent atomics on both sides"
+// form). Every table word another workgroup reads in this launch is written and read with 8-B relaxed agent-scope
+// atomics (sc1 stores / loads, coherent per location across XCDs), the claimer drains its stores (s_waitcnt
+// vmcnt(0)) before it publishes the slot as READY, and readers load the keys only after they saw READY. No release /
+// acquire fences: at agent scope those are an L2 writeback / L1 invalidate (microseconds each), once per group.
+__device__ __forceinline__ uint64_t table_load(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void table_store(unsigned long long* p, uint64_t v) {
+  __hip_atomic_store(p, static_cast<unsigned long long>(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 // Returns the slot of the group with the given key words, inserting it (record initialised) if new; ~0 on failure.
 __device__ __forceinline__ uint64_t group_slot(const AggDesc& d, const AggTable& t, const uint64_t* key, uint32_t nk) {
   uint64_t h = 0x9E3779B97F4A7C15ull;
   for (uint32_t i = 0; i < nk; ++i) h = mix64(h ^ key[i]);
   uint64_t s = h & (t.cap - 1);
   for (uint64_t guard = 0; guard < t.cap * 4; ++guard) {
-    const uint32_t st = __hip_atomic_load(&t.state[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t st = __hip_atomic_load(&t.state[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (st == HSLOT_EMPTY) {
       uint32_t expected = HSLOT_EMPTY;
       if (__hip_atomic_compare_exchange_strong(&t.state[s], &expected, HSLOT_LOCKED, __ATOMIC_RELAXED,
                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
         unsigned long long* rec = t.records + s * d.words;
-        for (uint32_t i = 0; i < nk; ++i) rec[i] = key[i];
-        for (uint32_t i = nk; i < d.words; ++i) rec[i] = word_init(d.word_op[i]);
-        __hip_atomic_store(&t.state[s], HSLOT_READY, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        for (uint32_t i = 0; i < nk; ++i) table_store(rec + i, key[i]);
+        for (uint32_t i = nk; i < d.words; ++i) table_store(rec + i, word_init(d.word_op[i]));
+        drain_stores();
+        __hip_atomic_store(&t.state[s], HSLOT_READY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return s;
       }
       continue;  // lost the race: re-read the same slot
@@ -799,7 +814,7 @@ __device__ __forceinline__ uint64_t group_slot(const AggDesc& d, const AggTable&
     }
     const unsigned long long* rec = t.records + s * d.words;
     bool eq = true;
-    for (uint32_t i = 0; i < nk; ++i) eq = eq && (rec[i] == key[i]);
+    for (uint32_t i = 0; i < nk; ++i) eq = eq && (table_load(rec + i) == key[i]);
     if (eq) return s;
     s = (s + 1) & (t.cap - 1);
   }
@@ -811,14 +826,15 @@ __device__ __forceinline__ uint64_t group_slot(const AggDesc& d, const AggTable&
 __device__ __forceinline__ bool distinct_insert(const AggDesc& d, const AggTable& t, uint64_t tag, uint64_t value) {
   uint64_t s = mix64(tag * 0x9E3779B97F4A7C15ull ^ mix64(value)) & (t.dcap - 1);
   for (uint64_t guard = 0; guard < t.dcap * 4; ++guard) {
-    const uint32_t st = __hip_atomic_load(&t.dstate[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t st = __hip_atomic_load(&t.dstate[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (st == HSLOT_EMPTY) {
       uint32_t expected = HSLOT_EMPTY;
       if (__hip_atomic_compare_exchange_strong(&t.dstate[s], &expected, HSLOT_LOCKED, __ATOMIC_RELAXED,
                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-        t.dkeys[2 * s] = tag;
-        t.dkeys[2 * s + 1] = value;
-        __hip_atomic_store(&t.dstate[s], HSLOT_READY, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        table_store(t.dkeys + 2 * s, tag);
+        table_store(t.dkeys + 2 * s + 1, value);
+        drain_stores();
+        __hip_atomic_store(&t.dstate[s], HSLOT_READY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return true;
       }
       continue;
@@ -827,81 +843,167 @@ __device__ __forceinline__ bool distinct_insert(const AggDesc& d, const AggTable
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
-    if (t.dkeys[2 * s] == tag && t.dkeys[2 * s + 1] == value) return false;
+    if (table_load(t.dkeys + 2 * s) == tag && table_load(t.dkeys + 2 * s + 1) == value) return false;
     s = (s + 1) & (t.dcap - 1);
   }
   atomicOr(d.error, 1u);
   return false;
 }
 
-__global__ __launch_bounds__(AGG_THREADS) void agg_hash_rows(AggDesc d, AggTable t) {
-  const uint64_t tile = blockIdx.x;
-  if (tile >= d.n_tiles) return;
-  const uint32_t c = agg_tile_chunk(d, tile);
-  const uint32_t size = d.chunk_size[c];
-  const uint64_t row0 = d.chunk_row_begin[c];
-  const uint32_t base = static_cast<uint32_t>(tile - d.chunk_tile_begin[c]) * AGG_TILE;
+// Flat row mapping (kernels whose tiles run over the input's global row numbers, so that many small chunks, e.g. a
+// join output's radix partitions, do not leave most lanes of a chunk-aligned tile idle): chunk of global row r, the
+// last chunk whose first row is <= r (empty chunks are skipped by construction).
+__device__ __forceinline__ uint32_t row_chunk(const AggDesc& d, uint64_t r) {
+  uint32_t lo = 0, hi = d.n_chunks;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (d.chunk_row_begin[mid] <= r) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+// The same for a row after the row whose chunk is c (rows only move forward within a lane).
+__device__ __forceinline__ uint32_t advance_chunk(const AggDesc& d, uint32_t c, uint64_t r) {
+  while (d.chunk_row_begin[c + 1] <= r) ++c;
+  return c;
+}
+
+// Inclusive scan inside runs of lanes: lane i combines lanes [start, i] of its run.
+template <typename T, typename Op>
+__device__ __forceinline__ T run_scan(T v, int start, Op op) {
+  const int lane = __lane_id();
+#pragma unroll
+  for (int dd = 1; dd < WAVE; dd <<= 1) {
+    const T o = __shfl_up(v, dd, WAVE);
+    if (lane - dd >= start) v = op(v, o);
+  }
+  return v;
+}
+
+// Hash grouping. The 64 lanes of a wave hold 64 consecutive input rows; lanes whose group-by keys equal their left
+// neighbour's form a run (rows of one group arriving together, e.g. the lines of one order after a join on the order
+// key). Every run is folded inside the wave (segmented shuffle scans) and applied to its group record once, by the
+// run's last lane: one table lookup and one set of atomics per run instead of per row. Float SUM/AVG runs whose values
+// share a limb window are folded exactly in that window (integer limb parts); other runs add per row. The record
+// words are combined by ADD / MIN / MAX / OR, so the result is the same for any order and any run split.
+// Rows per lane of a flat tile: enough tiles to give every CU several workgroups, at most AGG_ITEMS.
+inline uint32_t flat_items(uint64_t rows) {
+  const uint64_t want_tiles = 256ull * 8;
+  const uint64_t items = (rows + uint64_t(AGG_THREADS) * want_tiles - 1) / (uint64_t(AGG_THREADS) * want_tiles);
+  return static_cast<uint32_t>(items < 1 ? 1 : (items > AGG_ITEMS ? AGG_ITEMS : items));
+}
+
+__global__ __launch_bounds__(AGG_THREADS) void agg_hash_runs(AggDesc d, AggTable t, uint64_t total_rows,
+                                                             uint32_t items) {
+  const int lane = __lane_id();
+  const uint64_t tile_row0 = static_cast<uint64_t>(blockIdx.x) * AGG_THREADS * items;
   const uint32_t H = d.n_gb;
-  for (int k = 0; k < AGG_ITEMS; ++k) {
-    const uint32_t off = base + k * AGG_THREADS + threadIdx.x;
-    if (off >= size) continue;
+  uint32_t c = 0;
+  bool have_c = false;
+  for (uint32_t k = 0; k < items; ++k) {
+    const uint64_t wave_row0 = tile_row0 + static_cast<uint64_t>(k) * AGG_THREADS + (threadIdx.x & ~(WAVE - 1u));
+    if (wave_row0 >= total_rows) break;  // wave-uniform
+    const uint64_t row = wave_row0 + lane;
+    const bool valid = row < total_rows;
+    uint32_t off = 0;
     RowRefs refs;
-    load_refs(d, c, off, &refs);
     uint64_t key[AGG_MAX_GROUPBY + 1];
-    uint64_t nulls = 0;
-    for (uint32_t j = 0; j < d.n_gb; ++j) {
-      const AggCol& col = d.cols[d.gb[j]];
-      uint64_t bits;
-      if (read_col(d, col, c, off, refs, &bits)) {
-        key[j] = key_bits(bits, col.type);
-      } else {
-        key[j] = 0;
-        nulls |= 1ull << j;
+    for (uint32_t j = 0; j <= H; ++j) key[j] = 0;
+    if (valid) {
+      c = have_c ? advance_chunk(d, c, row) : row_chunk(d, row);
+      have_c = true;
+      off = static_cast<uint32_t>(row - d.chunk_row_begin[c]);
+      if (d.n_pos_groups) load_refs(d, c, off, &refs);
+      uint64_t nulls = 0;
+      for (uint32_t j = 0; j < H; ++j) {
+        const AggCol& col = d.cols[d.gb[j]];
+        uint64_t bits;
+        if (read_col(d, col, c, off, refs, &bits)) key[j] = key_bits(bits, col.type);
+        else nulls |= 1ull << j;
       }
+      key[H] = nulls;
     }
-    key[d.n_gb] = nulls;
-    const uint64_t s = group_slot(d, t, key, d.n_gb + 1);
-    if (s == ~0ull) return;
-    unsigned long long* rec = t.records + s * d.words;
-    const uint64_t row = row0 + off;
-    atomicAdd(rec + H + AGG_HDR_ROWS, 1ull);
-    atomicMin(rec + H + AGG_HDR_FIRST, static_cast<unsigned long long>(row));
-    atomicMax(rec + H + AGG_HDR_LAST, static_cast<unsigned long long>(row));
+    // runs: a lane starts a run unless it is valid and its keys equal the previous lane's (invalid lanes, a suffix
+    // of the wave, are runs of their own and do nothing)
+    bool same = valid && lane > 0;
+    for (uint32_t j = 0; j <= H; ++j) {
+      const uint64_t prev = __shfl_up(key[j], 1, WAVE);
+      same = same && prev == key[j];
+    }
+    const uint64_t heads = __ballot(!same);
+    const uint64_t upto = (2ull << lane) - 1;  // lanes [0, lane] (all lanes for lane 63)
+    const int start = 63 - __builtin_clzll(heads & upto);
+    const uint64_t after = heads & ~upto;
+    const int end = after ? __builtin_ctzll(after) - 1 : WAVE - 1;
+    const uint64_t run_mask = (end == WAVE - 1 ? ~0ull : ((2ull << end) - 1)) & ~((1ull << start) - 1);
+    const bool tail = valid && end == lane;
+    uint64_t s = ~0ull;
+    if (tail) s = group_slot(d, t, key, H + 1);
+    s = __shfl(s, end, WAVE);  // the run's slot, in every lane of the run
+    unsigned long long* rec = (valid && s != ~0ull) ? t.records + s * d.words : nullptr;
+    if (tail && rec) {
+      atomicAdd(rec + H + AGG_HDR_ROWS, static_cast<unsigned long long>(end - start + 1));
+      atomicMin(rec + H + AGG_HDR_FIRST, static_cast<unsigned long long>(row - (lane - start)));
+      atomicMax(rec + H + AGG_HDR_LAST, static_cast<unsigned long long>(row));
+    }
     for (uint32_t f = 0; f < d.n_fns; ++f) {
       const AggFn fn = d.fns[f];
       if (fn.column < 0) continue;
       const int32_t type = d.cols[fn.column].type;
-      uint64_t bits;
-      if (!read_col(d, d.cols[fn.column], c, off, refs, &bits)) continue;
-      switch (fn.function) {
-        case HY_AGG_COUNT:
-          atomicAdd(rec + fn.word, 1ull);
-          break;
-        case HY_AGG_COUNT_DISTINCT:
-          if (distinct_insert(d, t, (s << 8) | f, key_bits(bits, type))) atomicAdd(rec + fn.word, 1ull);
-          break;
-        case HY_AGG_MIN:
-          atomicAdd(rec + fn.word, 1ull);
-          atomicMin(rec + fn.word + 1, static_cast<unsigned long long>(ordered_bits(bits, type)));
-          break;
-        case HY_AGG_MAX:
-          atomicAdd(rec + fn.word, 1ull);
-          atomicMax(rec + fn.word + 1, static_cast<unsigned long long>(ordered_bits(bits, type)));
-          break;
-        default:  // SUM / AVG
-          atomicAdd(rec + fn.word, 1ull);
-          if (fn.limbs == 0) {
-            atomicAdd(rec + fn.word + 1, static_cast<unsigned long long>(int_value(bits, type)));
-          } else {
-            int i0 = 0;
-            int64_t part[3];
-            uint32_t special = 0;
-            const int np = float_parts(bits, type, &i0, part, &special);
-            if (special) atomicOr(rec + fn.word + 1, static_cast<unsigned long long>(special));
-            for (int q = 0; q < np; ++q)
-              if (part[q]) atomicAdd(rec + fn.word + 2 + i0 + q, static_cast<unsigned long long>(part[q]));
-          }
-          break;
+      uint64_t bits = 0;
+      const bool ok = rec != nullptr && read_col(d, d.cols[fn.column], c, off, refs, &bits);
+      const uint32_t cnt = __popcll(__ballot(ok) & run_mask);
+      if (fn.function == HY_AGG_COUNT_DISTINCT) {
+        if (ok && distinct_insert(d, t, (s << 8) | f, key_bits(bits, type))) atomicAdd(rec + fn.word, 1ull);
+        continue;
+      }
+      if (tail && rec && cnt) atomicAdd(rec + fn.word, static_cast<unsigned long long>(cnt));
+      if (fn.function == HY_AGG_COUNT) continue;
+      if (fn.function == HY_AGG_MIN || fn.function == HY_AGG_MAX) {
+        const bool mx = fn.function == HY_AGG_MAX;
+        uint64_t v = ok ? ordered_bits(bits, type) : (mx ? 0ull : ~0ull);
+        v = mx ? run_scan(v, start, [](uint64_t a, uint64_t b) { return a > b ? a : b; })
+               : run_scan(v, start, [](uint64_t a, uint64_t b) { return a < b ? a : b; });
+        if (tail && rec && cnt) {
+          if (mx) atomicMax(rec + fn.word + 1, static_cast<unsigned long long>(v));
+          else atomicMin(rec + fn.word + 1, static_cast<unsigned long long>(v));
+        }
+        continue;
+      }
+      if (fn.limbs == 0) {  // SUM / AVG of integers
+        uint64_t v = ok ? static_cast<uint64_t>(int_value(bits, type)) : 0ull;
+        v = run_scan(v, start, [](uint64_t a, uint64_t b) { return a + b; });
+        if (tail && rec && v) atomicAdd(rec + fn.word + 1, static_cast<unsigned long long>(v));
+        continue;
+      }
+      // SUM / AVG of floats
+      int i0 = 0;
+      int64_t part[3] = {0, 0, 0};
+      uint32_t special = 0;
+      const int np = ok ? float_parts(bits, type, &i0, part, &special) : 0;
+      const uint64_t sp = run_scan(static_cast<uint64_t>(special), start, [](uint64_t a, uint64_t b) { return a | b; });
+      if (tail && rec && sp) atomicOr(rec + fn.word + 1, static_cast<unsigned long long>(sp));
+      const bool has = np > 0;
+      int lo = run_scan(has ? i0 : 0x7FFFFFFF, start, [](int a, int b) { return a < b ? a : b; });
+      int hi = run_scan(has ? i0 : -1, start, [](int a, int b) { return a > b ? a : b; });
+      lo = __shfl(lo, end, WAVE);
+      hi = __shfl(hi, end, WAVE);
+      if (hi - lo <= 1) {  // the run's parts fit limbs [lo, lo + np]: fold them exactly, one atomic per limb
+        const int rel = has ? i0 - lo : 0;
+        const int W = type == HY_TYPE_FLOAT ? 3 : 4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (q >= W) break;
+          int64_t v = 0;
+          if (has) v = rel == 0 ? (q < 3 ? part[q] : 0) : (q >= 1 ? part[q - 1] : 0);
+          v = static_cast<int64_t>(
+              run_scan(static_cast<uint64_t>(v), start, [](uint64_t a, uint64_t b) { return a + b; }));
+          if (tail && rec && v && lo + q < fn.limbs)
+            atomicAdd(rec + fn.word + 2 + lo + q, static_cast<unsigned long long>(v));
+        }
+      } else if (has) {
+        for (int q = 0; q < np; ++q)
+          if (part[q]) atomicAdd(rec + fn.word + 2 + i0 + q, static_cast<unsigned long long>(part[q]));
       }
     }
   }

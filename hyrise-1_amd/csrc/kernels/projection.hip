@@ -6,8 +6,9 @@
 // data type (expression_functors.hpp:104-180), NULL if an operand is NULL (_evaluate_default_null_logic,
 // expression_evaluator.cpp:795-830) and, for / and %, if the divisor is 0.
 //
-// Layout: one 4096-row tile per workgroup, 16 rows per lane (row = tile base + k * 256 + thread), so every column
-// read and the result store are coalesced across a wave. Columns are read through the Aggregate's column model
+// Layout: one tile of the input's global rows per workgroup (tiles cross chunk boundaries, so many small chunks such
+// as a join output's partitions keep every lane busy), `items` rows per lane (row = tile base + k * 256 + thread; up
+// to 16, fewer for small inputs so that the grid still covers the CUs), so the result store is coalesced per wave. Columns are read through the Aggregate's column model
 // (value / dictionary chunks, or referenced chunks through PosList groups). The program is interpreted with a
 // per-lane value stack; its control flow is uniform (the same program for every row), so there is no divergence.
 // Roofline: HBM (the read column bytes + result bytes per row).
@@ -143,22 +144,21 @@ __device__ __forceinline__ uint64_t expr_arith(int32_t op, int32_t calc, uint64_
   }
 }
 
-constexpr int PROJ_ITEMS = 16;
-constexpr int PROJ_TILE = AGG_THREADS * PROJ_ITEMS;
 
 __global__ __launch_bounds__(AGG_THREADS) void projection_kernel(AggDesc d, ExprProgram prog, void* __restrict__ out,
-                                                                uint8_t* __restrict__ out_nulls) {
-  const uint64_t tile = blockIdx.x;
-  if (tile >= d.n_tiles) return;
-  const uint32_t c = d.tile_chunk[tile];
-  const uint32_t size = d.chunk_size[c];
-  const uint32_t base = static_cast<uint32_t>(tile - d.chunk_tile_begin[c]) * PROJ_TILE;
-  const uint64_t row0 = d.chunk_row_begin[c];
+                                                                uint8_t* __restrict__ out_nulls, uint64_t total_rows,
+                                                                uint32_t items) {
+  const uint64_t tile_row0 = static_cast<uint64_t>(blockIdx.x) * AGG_THREADS * items;
   const bool wide_out = is_wide(prog.out_type);
+  uint32_t c = 0;
+  bool have_c = false;
 #pragma unroll 1
-  for (int k = 0; k < PROJ_ITEMS; ++k) {
-    const uint32_t off = base + k * AGG_THREADS + threadIdx.x;
-    if (off >= size) break;
+  for (uint32_t k = 0; k < items; ++k) {
+    const uint64_t row = tile_row0 + static_cast<uint64_t>(k) * AGG_THREADS + threadIdx.x;
+    if (row >= total_rows) break;
+    c = have_c ? advance_chunk(d, c, row) : row_chunk(d, row);
+    have_c = true;
+    const uint32_t off = static_cast<uint32_t>(row - d.chunk_row_begin[c]);
     RowRefs refs;
     if (d.n_pos_groups) load_refs(d, c, off, &refs);
     // value stack in registers: every slot access is an unrolled compare against the (uniform) stack pointer, so the
@@ -211,7 +211,6 @@ __global__ __launch_bounds__(AGG_THREADS) void projection_kernel(AggDesc d, Expr
       }
     }
     const uint64_t r = val[0];
-    const uint64_t row = row0 + off;
     if (wide_out)
       static_cast<uint64_t*>(out)[row] = r;
     else

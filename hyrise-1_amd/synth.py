@@ -148,3 +148,72 @@ def dictionary_encode_small_domain(values_np_or_torch, chunk, domain):
     present[:, 0] = 0
     rank = np.cumsum(present, axis=1) - 1
     return rank[cid, v].astype(np.uint8), present[:, 1:].astype(bool)
+
+
+CUSTOMERS_PER_SF = 150_000
+# c_mktsegment codes in dictionary order (dbgen c_mseg_set: AUTOMOBILE, BUILDING, FURNITURE, HOUSEHOLD, MACHINERY)
+MKTSEGMENTS = ["AUTOMOBILE", "BUILDING", "FURNITURE", "HOUSEHOLD", "MACHINERY"]
+DATE_1995_03_15 = 9204  # TPC-H 3's date (days since 1970-01-01)
+
+
+def n_customers(sf):
+    return int(round(CUSTOMERS_PER_SF * sf))
+
+
+def q3_columns(sf, device, seed=SEED):
+    """The columns TPC-H 3 reads (tpch_queries.cpp:101-106), TPC-H-shaped (dbgen build.c / dss.h ranges), as torch
+    tensors on `device`:
+      customer: c_custkey 1..150k*SF, c_mktsegment code 0..4 (uniform, MKTSEGMENTS order)
+      orders:   o_orderkey (dbgen sparse keys), o_custkey uniform over the custkeys that are not multiples of 3 (dbgen
+                leaves every third customer without orders), o_orderdate int32 days uniform 1992-01-01..1998-08-02,
+                o_shippriority 0 (dbgen writes 0)
+      lineitem: 1..7 lines per order, l_orderkey = parent key, l_shipdate = o_orderdate + 1..121,
+                l_extendedprice = l_quantity x retail price (900.00..2100.00) and l_discount 0.00..0.10 as float32
+                (the reference schema's float columns, tpch_db_generator.cpp:20-27)
+    plus `l_order_index` (row index of the parent order, for the expected-result check)."""
+    import torch
+
+    n_cust = n_customers(sf)
+    ci = torch.arange(1, n_cust + 1, dtype=torch.int64, device=device)
+    seg = _umod_torch(_splitmix64_torch(ci ^ (seed ^ 0x4353)), 5).to(torch.int32)
+    okey, lines = orders_torch(sf, device, seed=seed)
+    n_ord = okey.numel()
+    i = torch.arange(1, n_ord + 1, dtype=torch.int64, device=device)
+    odate = DATE_1992_01_01 + _umod_torch(_splitmix64_torch(i ^ (seed ^ 0x0D47)), DATE_1998_08_02 - DATE_1992_01_01 + 1)
+    k = _umod_torch(_splitmix64_torch(i ^ (seed ^ 0x4F43)), max(1, (n_cust // 3) * 2))
+    ocust = (k // 2) * 3 + (k % 2) + 1
+    del i, k
+    lkey, qty = lineitem_torch(okey, lines, seed=seed)
+    oidx = torch.repeat_interleave(torch.arange(n_ord, dtype=torch.int64, device=device), lines)
+    n = lkey.numel()
+    r = torch.arange(n, dtype=torch.int64, device=device)
+    h = _splitmix64_torch(r ^ (seed ^ 0x5344))
+    ship = odate[oidx] + 1 + _umod_torch(h, 121)
+    h = _splitmix64_torch(r ^ (seed ^ 0x5052))
+    del r
+    retail = 90_000 + _umod_torch(h, 120_001)
+    price = ((qty.to(torch.int64) * retail).to(torch.float64) / 100.0).to(torch.float32)
+    disc = (torch.remainder(h >> 24, 11).to(torch.float64) / 100.0).to(torch.float32)
+    del h, retail, qty
+    return {"c_custkey": ci.to(torch.int32), "c_mktsegment": seg,
+            "o_orderkey": okey, "o_custkey": ocust.to(torch.int32), "o_orderdate": odate.to(torch.int32),
+            "o_shippriority": torch.zeros(n_ord, dtype=torch.int32, device=device),
+            "l_orderkey": lkey, "l_shipdate": ship.to(torch.int32), "l_extendedprice": price, "l_discount": disc,
+            "l_order_index": oidx}
+
+
+def dictionary_encode_chunks(values, chunk, lo, domain):
+    """Per-chunk dictionary encoding of integer values in [lo, lo + domain) (DictionaryEncoder: sorted distinct
+    values, vid = rank; dictionary_encoder.hpp:57-130) on the values' torch device. Returns (vids int32, present
+    [chunks, domain] bool): dictionary of chunk c = lo + nonzero(present[c]), vid width from its size."""
+    import torch
+
+    n = values.numel()
+    n_chunks = (n + chunk - 1) // chunk
+    cid = torch.arange(n, device=values.device, dtype=torch.int64) // chunk
+    v = (values.to(torch.int64) - lo)
+    present = torch.zeros(n_chunks, domain, dtype=torch.int32, device=values.device)
+    present.index_put_((cid, v), torch.ones_like(cid, dtype=torch.int32), accumulate=False)
+    rank = torch.cumsum(present, dim=1) - 1
+    vids = rank[cid, v].to(torch.int32)
+    return vids, present.bool()
