@@ -41,9 +41,8 @@ def parse():
                    help="nccl (RCCL; one GPU per rank) or gloo (host-staged exchange: rehearsal of N ranks on one GPU)")
     p.add_argument("--workload", choices=["join", "q1", "q3"], default="join",
                    help="join: the headline TableScan+JoinHash (BASELINE.json metric); q1: BASELINE config 4, "
-                        "TableScan(l_shipdate) -> Aggregate of TPC-H 1 on one GPU; q3: BASELINE config 5 at N=1, "
+                        "TPC-H 1 TableScan -> Projection -> Aggregate (8 aggregates) on one GPU; q3: BASELINE config 5 at N=1, "
                         "TPC-H 3 Scan -> Join -> Join -> Projection -> Aggregate (bench_tpch.py)")
-    p.add_argument("--q1-aggs", default=None, help="debug: comma-separated subset of Q1_AGGS indexes (q1 workload)")
     p.add_argument("--unfused", action="store_true",
                    help="run TableScan and JoinHash as two C-ABI calls (hy_table_scan_row_ids, hy_join_hash) instead "
                         "of the fused hy_scan_join_hash (A/B of the fusion; single GPU)")
@@ -56,12 +55,10 @@ def parse():
 
 def main():
     args = parse()
-    if args.workload == "q1":
-        return main_q1(args)
-    if args.workload == "q3":
+    if args.workload in ("q1", "q3"):
         import bench_tpch
 
-        return bench_tpch.main_q3(args)
+        return bench_tpch.main_q1(args) if args.workload == "q1" else bench_tpch.main_q3(args)
     import torch
 
     hy = importlib.import_module("hyrise-1_amd")
@@ -437,254 +434,6 @@ def kernel_stats(L):
         L.hy_kernel_stats_get(i, ctypes.byref(name), ctypes.byref(launches), ctypes.byref(total), ctypes.byref(units))
         out[name.value.decode()] = {"launches": launches.value, "ms_total": total.value}
     return out
-
-
-# TPC-H 1's aggregates that need no projection (l_extendedprice * (1 - l_discount) etc. are SURVEY.md 8(f) rank 1):
-# (function, column index into the aggregate's input columns; -1 = COUNT(*))
-Q1_AGGS = [("SUM", 2), ("SUM", 3), ("AVG", 2), ("AVG", 3), ("AVG", 4), ("COUNT", -1)]
-
-
-def main_q1(args):
-    """BASELINE.json config 4 on one GPU: TableScan(l_shipdate <= 1998-09-02) on the int32 value column, then
-    Aggregate(scan output) GROUP BY l_returnflag, l_linestatus (dictionary u8 codes) with SUM/AVG(l_quantity)
-    (dictionary u8 over float dictionaries, the reference schema's type), SUM/AVG(l_extendedprice) (int64 cents),
-    AVG(l_discount) (int32 hundredths) and COUNT(*). The aggregate reads every column through the scan's PosLists
-    (reference input, aggregate.cpp:291-498 over ReferenceColumns). One step = scan + aggregate; rows/s counts the
-    lineitem rows scanned. Results are checked against torch group sums of the same columns (exact integers)."""
-    import numpy as np
-    import torch
-
-    if int(os.environ.get("WORLD_SIZE", "1")) != 1:
-        raise SystemExit("--workload q1 is the single-GPU config (BASELINE.json configs[3])")
-    hy = importlib.import_module("hyrise-1_amd")
-    synth = importlib.import_module("hyrise-1_amd.synth")
-    capi = hy.capi
-    L = capi.lib
-    torch.cuda.set_device(0)
-    dev = torch.device("cuda", 0)
-    capi.check(L.hy_set_device(0), "hy_set_device")
-    stream = torch.cuda.current_stream().cuda_stream
-    chunk = args.chunk
-
-    cols = synth.lineitem_q1_torch(args.sf, dev)
-    n = cols["l_shipdate"].numel()
-    n_chunks = (n + chunk - 1) // chunk
-    sizes_l = [min(chunk, n - c * chunk) for c in range(n_chunks)]
-
-    def padded(t, mult=64):
-        extra = (-t.numel()) % mult
-        return torch.cat([t, torch.zeros(extra, dtype=t.dtype, device=t.device)]) if extra else t
-
-    # per-chunk dictionary encoding (DictionaryEncoder: sorted distinct values, vid = rank, u8 attribute vectors)
-    def dict_encode(values, domain, dict_values):
-        vids, present = synth.dictionary_encode_small_domain(values + 1, chunk, domain)
-        pres = present.cpu().numpy()
-        dicts = np.zeros((n_chunks, domain), dtype=dict_values.dtype)
-        for c in range(n_chunks):
-            v = dict_values[pres[c]]
-            dicts[c, :v.size] = v
-        return padded(vids.contiguous()), torch.from_numpy(dicts).to(dev), pres.sum(axis=1)
-
-    rf_v, rf_d, rf_n = dict_encode(cols["l_returnflag"], 3, np.arange(3, dtype=np.int32))
-    ls_v, ls_d, ls_n = dict_encode(cols["l_linestatus"], 2, np.arange(2, dtype=np.int32))
-    qt_v, qt_d, qt_n = dict_encode(cols["l_quantity"] - 1, 50, np.arange(1, 51, dtype=np.float32))
-    ship = padded(cols["l_shipdate"].contiguous())
-    price = padded(cols["l_extendedprice"].contiguous())
-    disc = padded(cols["l_discount"].contiguous())
-
-    # expected results (exact integer group sums of the same data, on the device with torch)
-    mask = cols["l_shipdate"] <= synth.DATE_1998_09_02
-    gkey = (cols["l_returnflag"] * 2 + cols["l_linestatus"]).to(torch.int64)[mask]
-    exp = {}
-    for name, v in (("count", torch.ones_like(gkey)), ("qty", cols["l_quantity"].to(torch.int64)[mask]),
-                    ("price", cols["l_extendedprice"][mask]), ("disc", cols["l_discount"].to(torch.int64)[mask])):
-        exp[name] = torch.zeros(6, dtype=torch.int64, device=dev).scatter_add_(0, gkey, v).cpu().tolist()
-    n_match_exp = int(mask.sum())
-    del cols, mask, gkey
-    torch.cuda.synchronize()
-
-    # ---- scan: l_shipdate <= 1998-09-02 on int32 value chunks -> RowIDs ----
-    scan_chunks = (capi.ScanChunk * n_chunks)()
-    for c in range(n_chunks):
-        sc = scan_chunks[c]
-        sc.column.data = ship.data_ptr() + 4 * c * chunk
-        sc.column.size = sizes_l[c]
-        sc.column.kind = capi.HY_COL_VALUE
-        sc.op = capi.HY_OP_LE
-        sc.out_begin = c * chunk
-    sizes = (ctypes.c_uint32 * n_chunks)(*sizes_l)
-    chunk_ids = (ctypes.c_uint32 * n_chunks)(*range(n_chunks))
-    ws_bytes = ctypes.c_size_t(0)
-    capi.check(L.hy_table_scan_workspace_size(sizes, n_chunks, ctypes.byref(ws_bytes)), "scan ws")
-    scan_ws = torch.empty(ws_bytes.value, dtype=torch.uint8, device=dev)
-    scan_rows = torch.empty(n * 2 + 64, dtype=torch.int32, device=dev)
-    scan_counts = torch.empty(n_chunks, dtype=torch.int32, device=dev)
-    L.hy_table_scan_row_ids.restype = ctypes.c_int
-    L.hy_table_scan_row_ids.argtypes = [ctypes.POINTER(capi.ScanChunk), ctypes.c_uint32, ctypes.c_int32,
-                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                        ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
-    constant = ctypes.c_int32(synth.DATE_1998_09_02)
-
-    # ---- aggregate input: columns over the referenced lineitem chunks, PosLists = scan output chunks ----
-    def ref_chunks(data, width, dicts=None, dsizes=None):
-        arr = (capi.ColumnChunk * n_chunks)()
-        for c in range(n_chunks):
-            ch = arr[c]
-            ch.data = data.data_ptr() + width * c * chunk
-            ch.size = sizes_l[c]
-            if dicts is not None:
-                ch.kind = capi.HY_COL_DICT
-                ch.vid_width = 1
-                ch.dictionary = dicts.data_ptr() + dicts.element_size() * dicts.shape[1] * c
-                ch.dictionary_size = int(dsizes[c])
-            else:
-                ch.kind = capi.HY_COL_VALUE
-        return arr
-
-    col_chunks = [ref_chunks(rf_v, 1, rf_d, rf_n), ref_chunks(ls_v, 1, ls_d, ls_n), ref_chunks(qt_v, 1, qt_d, qt_n),
-                  ref_chunks(price, 8), ref_chunks(disc, 4)]
-    agg_cols = (capi.AggColumn * 5)()
-    for j, (vt, dom) in enumerate([(capi.HY_TYPE_INT32, 3), (capi.HY_TYPE_INT32, 2), (capi.HY_TYPE_FLOAT, 0),
-                                   (capi.HY_TYPE_INT64, 0), (capi.HY_TYPE_INT32, 0)]):
-        agg_cols[j].value_type, agg_cols[j].pos_group, agg_cols[j].domain = vt, 0, dom
-        agg_cols[j].chunks = col_chunks[j]
-        agg_cols[j].n_chunks = n_chunks
-    groupby = (ctypes.c_int32 * 2)(0, 1)
-    aggs = [Q1_AGGS[int(i)] for i in args.q1_aggs.split(",")] if args.q1_aggs else Q1_AGGS
-    defs = (capi.AggDef * len(aggs))()
-    for a, (f, col) in enumerate(aggs):
-        defs[a].function, defs[a].column = getattr(capi, "HY_AGG_" + f), col
-    params = capi.AggParams(groupby, 2, defs, len(aggs), 64)
-    out_cap = 64
-    state = {}
-
-    def agg_input(counts_h):
-        nz = np.nonzero(counts_h > 0)[0]
-        csz = (ctypes.c_uint32 * len(nz))(*counts_h[nz].tolist())
-        pls = (ctypes.c_void_p * len(nz))(*[scan_rows.data_ptr() + 8 * chunk * int(c) for c in nz])
-        return capi.AggInput(len(nz), csz, pls, 1, agg_cols, 5), (csz, pls), int(counts_h[nz].sum())
-
-    def step():
-        capi.check(L.hy_table_scan_row_ids(scan_chunks, n_chunks, capi.HY_TYPE_INT32, ctypes.byref(constant),
-                                           chunk_ids, scan_rows.data_ptr(), scan_counts.data_ptr(),
-                                           scan_ws.data_ptr(), ws_bytes.value, stream), "hy_table_scan_row_ids")
-        counts_h = scan_counts.cpu().numpy()  # the scan output's chunk layout
-        inp, keep, n_match = agg_input(counts_h)
-        if "ws" not in state:
-            wsb = ctypes.c_size_t(0)
-            capi.check(L.hy_aggregate_workspace_size(ctypes.byref(inp), ctypes.byref(params), ctypes.byref(wsb)), "ws")
-            state["ws"] = torch.empty(wsb.value, dtype=torch.uint8, device=dev)
-            lay = capi.AggLayout()
-            capi.check(L.hy_aggregate_layout(ctypes.byref(inp), ctypes.byref(params), ctypes.byref(lay)), "layout")
-            state["layout"] = lay
-            state["out"] = torch.empty(out_cap * lay.words, dtype=torch.int64, device=dev)
-        ng = ctypes.c_uint64(0)
-        capi.check(L.hy_aggregate(ctypes.byref(inp), ctypes.byref(params), state["out"].data_ptr(), out_cap,
-                                  ctypes.byref(ng), state["ws"].data_ptr(), state["ws"].numel(), stream), "hy_aggregate")
-        return n_match, ng.value
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    L.hy_kernel_stats_reset()
-    L.hy_kernel_stats_enable(1)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        n_match, n_groups = step()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    L.hy_kernel_stats_enable(0)
-
-    # ---- check the groups against the exact torch sums ----
-    lay = state["layout"]
-    rec = state["out"].view(-1, lay.words)[:n_groups].cpu().numpy().view(np.uint64)
-    ok = n_match == n_match_exp
-    groups = {}
-    for r in (rec if aggs is Q1_AGGS else []):
-        g = int(r[0]) * 2 + int(r[1])
-        w_q, w_p, w_d = lay.agg_word[0], lay.agg_word[1], lay.agg_word[4]
-        limbs = (ctypes.c_uint64 * lay.agg_limbs[0])(*[int(x) for x in r[w_q + 2:w_q + 2 + lay.agg_limbs[0]]])
-        qsum = ctypes.c_double(0)
-        capi.check(L.hy_agg_float_sum(limbs, lay.agg_limbs[0], lay.agg_emin[0], int(r[w_q + 1]), ctypes.byref(qsum)))
-        rows = int(r[5])
-        psum, dsum = int(np.int64(r[w_p + 1])), int(np.int64(r[w_d + 1]))
-        ok &= rows == exp["count"][g] and qsum.value == exp["qty"][g] and psum == exp["price"][g] \
-            and dsum == exp["disc"][g]
-        groups["ANR"[int(r[0])] + "FO"[int(r[1])]] = {
-            "count": rows, "sum_qty": qsum.value, "sum_base_price": psum / 100.0, "avg_disc": dsum / 100.0 / rows}
-    ok &= n_groups == sum(1 for c in exp["count"] if c)
-    ok &= aggs is Q1_AGGS or args.no_cpu_baseline  # a debug subset is not checked
-    if not ok:
-        raise SystemExit(f"q1 result mismatch: {groups} vs {exp}")
-
-    kernels = kernel_stats(L)
-    K = args.steps
-    # algorithmic bytes (SURVEY.md 8(d)): scan 4 B/row read + 8 B/match RowID written; aggregate per matched row the
-    # RowID (8 B) + returnflag, linestatus, quantity vids (1 B each) + extendedprice (8 B) + discount (4 B) = 23 B
-    alg = {"scan_value": n * 4 + n_match * 8, "agg_dense_rows": n_match * 23, "agg_dense_span": n_match * 23}
-    for k, v in kernels.items():
-        v["ms_per_launch"] = v["ms_total"] / max(v["launches"], 1)
-        if k in alg:
-            v["alg_bytes_per_launch"] = alg[k] / (v["launches"] / K)
-            v["achieved_GBps"] = v["alg_bytes_per_launch"] / (v["ms_per_launch"] * 1e-3) / 1e9
-    dom = max((k for k in kernels if k in alg), key=lambda k: kernels[k]["ms_total"])
-    dk = kernels[dom]
-    step_s = elapsed / K
-    roofline = {"bound": "hbm", "kernel": dom, "achieved": round(dk["achieved_GBps"], 1), "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s", "frac": round(dk["achieved_GBps"] / HBM_PEAK_GBPS, 4), "traffic": None}
-    # HBM bytes per launch from the newest committed PMC summary of this workload (tools: rocprofv3 --pmc FETCH_SIZE /
-    # WRITE_SIZE passes of `bench.py --workload q1`, summarized by tools/summarize_rocprof.py)
-    if chunk == 100_000:
-        for f in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_rocprof_q1_sf{args.sf:g}_summary.json")))):
-            with open(f) as fh:
-                kk = json.load(fh).get("kernels", {}).get(dom if dom != "scan_value" else "scan_kernel", {})
-            if "hbm_bytes_per_launch" in kk:
-                roofline["traffic"] = round(kk["hbm_bytes_per_launch"])
-                roofline["traffic_source"] = os.path.relpath(f, ROOT)
-                break
-    cpu = None if args.no_cpu_baseline else cpu_baseline_q1(hy, synth, args.cpu_sf / 10, chunk)
-    line = {
-        "metric": "rows/sec TableScan+Aggregate, TPC-H 1 on lineitem (BASELINE.json configs[3])",
-        "value": round(n / step_s, 1), "unit": "rows/s", "n_gpus": 1, "steps": K, "warmup": args.warmup,
-        "ms_per_step": round(step_s * 1e3, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "int64/f32-exact", "data": "synthetic (seeded counter-based TPC-H-shaped columns, resident in HBM)",
-        "config": {"workload": "TableScan(l_shipdate <= 1998-09-02, int32 value) -> Aggregate(GROUP BY l_returnflag, "
-                               "l_linestatus; SUM/AVG l_quantity, SUM/AVG l_extendedprice, AVG l_discount, COUNT(*))",
-                   "sf": args.sf, "lineitem_rows": n, "chunk_size": chunk, "scan_matches": n_match,
-                   "groups": n_groups, "parallelism": "single GPU"},
-        "check": {"ok": bool(ok), "groups": groups},
-        "roofline": roofline,
-        "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
-                    for k, v in kernels.items()},
-        "cpu_baseline": cpu,
-    }
-    print(json.dumps(line))
-
-
-def cpu_baseline_q1(hy, synth, sf, chunk):
-    """The oracle's TableScan + Aggregate (single thread) on a bounded sample of the same TPC-H 1 workload."""
-    import numpy as np
-
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import helpers
-
-    oracle = helpers.load_oracle()
-    cols = {k: v.numpy() for k, v in synth.lineitem_q1_torch(sf, "cpu").items()}
-    t = hy.Table.from_arrays([("l_returnflag", hy.DataType.Int, False), ("l_linestatus", hy.DataType.Int, False),
-                              ("l_quantity", hy.DataType.Float, False), ("l_extendedprice", hy.DataType.Long, False),
-                              ("l_discount", hy.DataType.Int, False), ("l_shipdate", hy.DataType.Int, False)],
-                             [cols["l_returnflag"], cols["l_linestatus"], cols["l_quantity"].astype(np.float32),
-                              cols["l_extendedprice"], cols["l_discount"], cols["l_shipdate"]], [], chunk)
-    hy.encode_all_chunks(t, hy.EncodingType.Dictionary)
-    aggs = [hy.AggregateColumnDefinition(None if c < 0 else c, getattr(hy.AggregateFunction, f.capitalize()))
-            for f, c in Q1_AGGS]
-    t0 = time.perf_counter()
-    scan = oracle.table_scan(t, 5, hy.PredicateCondition.LessThanEquals, synth.DATE_1998_09_02, [])
-    out = oracle.aggregate(scan, aggs, [0, 1])
-    dt = time.perf_counter() - t0
-    return {"value": round(t.row_count() / dt, 1), "unit": "rows/s", "cores": 1, "kind": "port",
-            "sample": f"SF{sf}: {t.row_count()} lineitem rows (all columns dictionary-encoded, the reference default), "
-                      f"scan {scan.row_count()} matches, {out.row_count()} groups, {dt:.2f} s"}
 
 
 # bench.py's kernel-table names -> the HIP kernel function names rocprofv3 reports

@@ -59,7 +59,9 @@ def dict_predicate(capi, lb, ub, dict_size, cond):
 class DictColumn:
     """A chunked integer column dictionary-encoded per chunk on the device (vids u8 / u16 by dictionary size)."""
 
-    def __init__(self, torch, synth, capi, values, chunk, lo, domain):
+    def __init__(self, torch, synth, capi, values, chunk, lo, domain, dict_values=None):
+        """values: integer codes in [lo, lo + domain); the dictionary holds the codes themselves (int32), or
+        dict_values[code - lo] (e.g. float32 values whose order is the codes' order)."""
         vids, present = synth.dictionary_encode_chunks(values, chunk, lo, domain)
         n = values.numel()
         self.n_chunks = present.shape[0]
@@ -68,8 +70,10 @@ class DictColumn:
         # dictionaries: dict[c, rank] = lo + value index, one row of `domain` int32 per chunk
         rank = torch.cumsum(present.to(torch.int32), dim=1) - 1
         rows, js = torch.nonzero(present, as_tuple=True)
-        self.dicts = torch.zeros(self.n_chunks, domain, dtype=torch.int32, device=values.device)
-        self.dicts[rows, rank[rows, js].long()] = (lo + js).to(torch.int32)
+        dv = (torch.arange(lo, lo + domain, dtype=torch.int32, device=values.device) if dict_values is None
+              else dict_values.to(values.device))
+        self.dicts = torch.zeros(self.n_chunks, domain, dtype=dv.dtype, device=values.device)
+        self.dicts[rows, rank[rows, js].long()] = dv[js]
         self.cum = torch.cumsum(present.to(torch.int64), dim=1).cpu().numpy()  # cum[c, j] = #values <= lo + j
         self.dsize = dsize.cpu().numpy()
         self.lo, self.domain = lo, domain
@@ -459,6 +463,292 @@ def cpu_baseline_q3(hy, synth, sf, chunk, host_cpu, runs=5):
                       "sample": f"SF{sample_sf:g}: {customer.row_count()} customer + {orders.row_count()} orders + "
                                 f"{lineitem.row_count()} lineitem rows, {agg.row_count()} groups"}
         del customer, orders, lineitem, agg
+    out["value"], out["cores"] = out["all_cores"]["value"], out["all_cores"]["cores"]
+    out["sample"] = out["all_cores"]["sample"] + f"; median of {runs}"
+    return out
+
+
+# TPC-H 1 (tpch_queries.cpp:36-44): SELECT list over the scan, by aggregate-input column index
+Q1_AGGS = [("SUM", 2), ("SUM", 3), ("SUM", 4), ("SUM", 5), ("AVG", 2), ("AVG", 3), ("AVG", 6), ("COUNT", -1)]
+
+
+def main_q1(args):
+    """BASELINE.json configs[3] on one GPU: TPC-H 1 with all eight aggregates on the reference schema's types.
+
+    One step:
+        TableScan(lineitem, l_shipdate <= 1998-09-02)          hy_table_scan_row_ids (dictionary u16 dates)
+        Projection(l_extendedprice * (1 - l_discount), l_extendedprice * (1 - l_discount) * (1 + l_tax))
+                                                                hy_projection x 2 (float, as the reference computes)
+        Aggregate(GROUP BY l_returnflag, l_linestatus; SUM(l_quantity), SUM(l_extendedprice), SUM(disc_price),
+                  SUM(charge), AVG(l_quantity), AVG(l_extendedprice), AVG(l_discount), COUNT(*))   hy_aggregate
+    The reference's Projection materialises all seven SELECT-list inputs into a data table (projection.cpp:52-85);
+    here only the two computed columns are materialised and the aggregate reads the five plain columns through the
+    scan's PosLists (same values, one materialisation less). Float SUM/AVG are exact (rounded once); they are checked
+    against float64 torch sums of the same float32 values (relative 1e-9), counts and SUM(l_quantity) exactly."""
+    import numpy as np
+    import torch
+
+    if int(os.environ.get("WORLD_SIZE", "1")) != 1:
+        raise SystemExit("--workload q1 is the single-GPU config (BASELINE.json configs[3])")
+    sys.path.insert(0, ROOT)
+    hy = importlib.import_module("hyrise-1_amd")
+    synth = importlib.import_module("hyrise-1_amd.synth")
+    capi = hy.capi
+    L = capi.lib
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    capi.check(L.hy_set_device(0), "hy_set_device")
+    stream = torch.cuda.current_stream().cuda_stream
+    chunk = args.chunk
+    I32, F32 = capi.HY_TYPE_INT32, capi.HY_TYPE_FLOAT
+    D = synth.DATE_1998_09_02
+
+    cols = synth.q1_columns(args.sf, dev)
+    n = cols["l_shipdate"].numel()
+    # expected results (torch, same columns)
+    print(f"q1: {n} lineitem rows generated", file=sys.stderr, flush=True)
+    mask = cols["l_shipdate"] <= D
+    gkey = torch.where(mask, cols["l_returnflag"] * 2 + cols["l_linestatus"], -1)
+    price, disc, tax = cols["l_extendedprice"], cols["l_discount"], cols["l_tax"]
+    dp = price * (1 - disc)  # float32, as the projection computes it
+    ch = dp * (1 + tax)
+    # per-group masked reductions (a 6-slot index_add_ would be 6e8 contended float64 atomics)
+    sel = [gkey == g for g in range(6)]
+
+    def gsum(v):
+        return [float(torch.sum(torch.where(m, v.to(torch.float64), 0.0))) for m in sel]
+
+    exp = {"count": [int(m.sum()) for m in sel], "qty": gsum(cols["l_quantity"]), "price": gsum(price),
+           "disc_price": gsum(dp), "charge": gsum(ch), "disc": gsum(disc)}
+    n_match_exp = int(mask.sum())
+    del mask, gkey, dp, ch, sel
+    print("q1: expected results computed", file=sys.stderr, flush=True)
+    codes = lambda v, scale: torch.round(v.to(torch.float64) * scale).to(torch.int32)
+    ship = DictColumn(torch, synth, capi, cols["l_shipdate"], chunk, synth.DATE_1992_01_01,
+                      synth.DATE_1998_08_02 + 121 - synth.DATE_1992_01_01 + 1)
+    rf = DictColumn(torch, synth, capi, cols["l_returnflag"], chunk, 0, 3)
+    ls = DictColumn(torch, synth, capi, cols["l_linestatus"], chunk, 0, 2)
+    qty = DictColumn(torch, synth, capi, codes(cols["l_quantity"], 1), chunk, 1, 50,
+                     torch.arange(1, 51, dtype=torch.float32))
+    dsc = DictColumn(torch, synth, capi, codes(disc, 100), chunk, 0, 11,
+                     (torch.arange(11, dtype=torch.float64) / 100).to(torch.float32))
+    tx = DictColumn(torch, synth, capi, codes(tax, 100), chunk, 0, 9,
+                    (torch.arange(9, dtype=torch.float64) / 100).to(torch.float32))
+    price_t = torch.cat([price.contiguous(), torch.zeros(64, dtype=torch.float32, device=dev)])
+    del cols, price, disc, tax
+    torch.cuda.synchronize()
+    price_c = value_chunks(capi, price_t, chunk, 4)
+    n_chunks = len(price_c)
+
+    scan = ship.scan_chunks(capi, "LessThanEquals", D)
+    for c in range(n_chunks):
+        scan[c].out_begin = c * chunk
+    ids = (ctypes.c_uint32 * n_chunks)(*range(n_chunks))
+    wsb = ctypes.c_size_t(0)
+    capi.check(L.hy_table_scan_workspace_size((ctypes.c_uint32 * n_chunks)(*ship.sizes), n_chunks,
+                                              ctypes.byref(wsb)), "scan ws")
+    scan_ws = torch.empty(max(16, wsb.value), dtype=torch.uint8, device=dev)
+    rows_t = torch.empty(2 * n + 64, dtype=torch.int32, device=dev)
+    counts_t = torch.empty(n_chunks, dtype=torch.int32, device=dev)
+    L.hy_table_scan_row_ids.restype = ctypes.c_int
+    L.hy_table_scan_row_ids.argtypes = [ctypes.POINTER(capi.ScanChunk), ctypes.c_uint32, ctypes.c_int32,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    proj_cols = (capi.AggColumn * 3)()
+    for j, (vt, chs) in enumerate([(F32, price_c), (F32, dsc.desc), (F32, tx.desc)]):
+        proj_cols[j].value_type, proj_cols[j].pos_group, proj_cols[j].chunks, proj_cols[j].n_chunks = vt, 0, chs, \
+            n_chunks
+    N = capi.ExprNode
+    one = N(capi.HY_EXPR_VALUE, I32, 0, 0, 1)
+    disc_price = [N(capi.HY_EXPR_COLUMN, F32, 0, 0, 0), one, N(capi.HY_EXPR_COLUMN, F32, 0, 1, 0),
+                  N(capi.HY_EXPR_SUB, F32, F32, 0, 0), N(capi.HY_EXPR_MUL, F32, F32, 0, 0)]
+    charge = disc_price + [one, N(capi.HY_EXPR_COLUMN, F32, 0, 2, 0), N(capi.HY_EXPR_ADD, F32, F32, 0, 0),
+                           N(capi.HY_EXPR_MUL, F32, F32, 0, 0)]
+    programs = [(N * len(p))(*p) for p in (disc_price, charge)]
+    proj_out = torch.empty(2, n + 64, dtype=torch.float32, device=dev)
+    agg_cols = (capi.AggColumn * 7)()
+    ref_cols = {0: (I32, rf.desc, 3), 1: (I32, ls.desc, 2), 2: (F32, qty.desc, 0), 3: (F32, price_c, 0),
+                6: (F32, dsc.desc, 0)}
+    for j, (vt, chs, dom) in ref_cols.items():
+        agg_cols[j].value_type, agg_cols[j].pos_group, agg_cols[j].chunks = vt, 0, chs
+        agg_cols[j].n_chunks, agg_cols[j].domain = n_chunks, dom
+    groupby = (ctypes.c_int32 * 2)(0, 1)
+    defs = (capi.AggDef * len(Q1_AGGS))(*[capi.AggDef(getattr(capi, "HY_AGG_" + f), col) for f, col in Q1_AGGS])
+    params = capi.AggParams(groupby, 2, defs, len(Q1_AGGS), 64)
+    cc_dtype = np.dtype(capi.ColumnChunk)
+    state = {}
+
+    def step():
+        capi.check(L.hy_table_scan_row_ids(scan, n_chunks, I32, None, ids, rows_t.data_ptr(), counts_t.data_ptr(),
+                                           scan_ws.data_ptr(), scan_ws.numel(), stream), "scan")
+        cnt = counts_t.cpu().numpy()
+        nz = np.nonzero(cnt)[0]
+        k = len(nz)
+        sizes_np = np.ascontiguousarray(cnt[nz], dtype=np.uint32)
+        pls_np = (rows_t.data_ptr() + 8 * chunk * nz.astype(np.uint64)).astype(np.uint64)
+        sizes = sizes_np.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+        pls = pls_np.ctypes.data_as(ctypes.POINTER(ctypes.c_void_p))
+        pin = capi.AggInput(k, sizes, pls, 1, proj_cols, 3)
+        if "pws" not in state:
+            b = ctypes.c_size_t(0)
+            capi.check(L.hy_projection_workspace_size(ctypes.byref(pin), ctypes.byref(b)), "proj ws")
+            state["pws"] = torch.empty(max(16, b.value), dtype=torch.uint8, device=dev)
+        pws = state["pws"]
+        for j, prog in enumerate(programs):
+            capi.check(L.hy_projection(ctypes.byref(pin), prog, len(prog), proj_out[j].data_ptr(), None,
+                                       pws.data_ptr(), pws.numel(), stream), "hy_projection")
+        rb = np.concatenate([[0], np.cumsum(sizes_np.astype(np.int64))])[:-1].astype(np.uint64)
+        keep = []
+        for j in (4, 5):  # the projection's columns: data chunks aligned with the scan output's chunks
+            chs = np.zeros(max(1, k), cc_dtype)
+            chs["data"][:k] = proj_out[j - 4].data_ptr() + 4 * rb
+            chs["size"][:k] = sizes_np
+            chs["kind"] = capi.HY_COL_VALUE
+            keep.append(chs)
+            agg_cols[j].value_type, agg_cols[j].pos_group, agg_cols[j].n_chunks = F32, -1, k
+            agg_cols[j].chunks = chs.ctypes.data_as(ctypes.POINTER(capi.ColumnChunk))
+        ain = capi.AggInput(k, sizes, pls, 1, agg_cols, 7)
+        if "ws" not in state:
+            b = ctypes.c_size_t(0)
+            capi.check(L.hy_aggregate_workspace_size(ctypes.byref(ain), ctypes.byref(params), ctypes.byref(b)), "ws")
+            state["ws"] = torch.empty(b.value, dtype=torch.uint8, device=dev)
+            lay = capi.AggLayout()
+            capi.check(L.hy_aggregate_layout(ctypes.byref(ain), ctypes.byref(params), ctypes.byref(lay)), "layout")
+            state["layout"] = lay
+            state["out"] = torch.empty(64 * lay.words, dtype=torch.int64, device=dev)
+        ng = ctypes.c_uint64(0)
+        capi.check(L.hy_aggregate(ctypes.byref(ain), ctypes.byref(params), state["out"].data_ptr(), 64,
+                                  ctypes.byref(ng), state["ws"].data_ptr(), state["ws"].numel(), stream),
+                   "hy_aggregate")
+        return int(sizes_np.sum()), ng.value
+
+    print("q1: columns encoded, running", file=sys.stderr, flush=True)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    L.hy_kernel_stats_reset()
+    L.hy_kernel_stats_enable(1)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        n_match, n_groups = step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    L.hy_kernel_stats_enable(0)
+
+    # ---- check ----
+    lay = state["layout"]
+    rec = state["out"].view(-1, lay.words)[:n_groups].cpu().numpy().view(np.uint64)
+
+    def fsum(r, a):
+        w = lay.agg_word[a]
+        limbs = (ctypes.c_uint64 * lay.agg_limbs[a])(*[int(x) for x in r[w + 2:w + 2 + lay.agg_limbs[a]]])
+        out = ctypes.c_double(0)
+        capi.check(L.hy_agg_float_sum(limbs, lay.agg_limbs[a], lay.agg_emin[a], int(r[w + 1]), ctypes.byref(out)))
+        return out.value
+
+    close = lambda a, b: abs(a - b) <= 1e-9 * max(1.0, abs(b))
+    ok = n_match == n_match_exp and n_groups == sum(1 for c in exp["count"] if c)
+    groups = {}
+    for r in rec:
+        g = int(r[0]) * 2 + int(r[1])
+        rows = int(r[5])
+        vals = {"sum_qty": fsum(r, 0), "sum_base_price": fsum(r, 1), "sum_disc_price": fsum(r, 2),
+                "sum_charge": fsum(r, 3), "count_order": rows}
+        vals["avg_qty"], vals["avg_price"] = vals["sum_qty"] / rows, vals["sum_base_price"] / rows
+        vals["avg_disc"] = fsum(r, 6) / rows
+        ok &= rows == exp["count"][g] and vals["sum_qty"] == exp["qty"][g]
+        ok &= close(vals["sum_base_price"], exp["price"][g]) and close(vals["sum_disc_price"], exp["disc_price"][g])
+        ok &= close(vals["sum_charge"], exp["charge"][g]) and close(fsum(r, 6), exp["disc"][g])
+        groups["ANR"[int(r[0])] + "FO"[int(r[1])]] = vals
+    if not ok:
+        raise SystemExit(f"q1 result mismatch: {groups} vs {exp}")
+
+    from bench import kernel_stats, measured_roofline, host_cpu  # noqa: E402  (shared helpers)
+
+    kernels = kernel_stats(L)
+    K = args.steps
+    step_s = elapsed / K
+    # algorithmic bytes (SURVEY.md 8(d)): scan 2 B/row (u16 date vids) + 8 B/match RowID; projection per match RowID
+    # 8 B + price 4 B + discount 1 B (+ tax 1 B) + result 4 B; aggregate per match RowID 8 B + flags, quantity,
+    # discount vids 1 B each + price 4 B + the two projected columns 4 B each
+    alg = {"scan_dict": n * 2 + n_match * 8, "projection": n_match * (17 + 18), "agg_dense_span": n_match * 24}
+    e2e = sum(alg.values())
+    for k, v in kernels.items():
+        v["ms_per_launch"] = v["ms_total"] / max(v["launches"], 1)
+        if k in alg:
+            v["alg_bytes_per_step"] = alg[k]
+            v["achieved_GBps"] = alg[k] / (v["ms_total"] / K * 1e-3) / 1e9
+    peak, probe = measured_roofline(L, capi, torch, dev, stream, args.probe_gb)
+    dom = max(kernels, key=lambda k: kernels[k]["ms_total"])
+    roofline = {"bound": "hbm", "scope": "end-to-end step (algorithmic bytes of SURVEY 8(d) per operator)",
+                "achieved": round(e2e / step_s / 1e9, 1), "peak": round(peak, 1), "unit": "GB/s",
+                "frac": round(e2e / step_s / 1e9 / peak, 4), "alg_bytes_per_step": e2e, "alg_bytes": alg,
+                "traffic": None, "peak_source": "measured in this run (hy_stream_bandwidth_probe, best of read / copy)",
+                "dominant_kernel": dom, "dominant_ms_per_step": round(kernels[dom]["ms_total"] / K, 4)}
+    # the reference Aggregate runs ~1e6 rows/s per core: a tenth of --cpu-sf keeps the sample near 10-30 s
+    cpu = None if args.no_cpu_baseline else cpu_baseline_q1(hy, synth, args.cpu_sf / 10, chunk, host_cpu)
+    line = {
+        "metric": "rows/sec TableScan+Projection+Aggregate, TPC-H 1 on lineitem (BASELINE.json configs[3])",
+        "value": round(n / step_s, 1), "unit": "rows/s", "n_gpus": 1, "steps": K, "warmup": args.warmup,
+        "ms_per_step": round(step_s * 1e3, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f32 (exact sums)", "data": "synthetic (seeded counter-based TPC-H-shaped columns, resident in HBM)",
+        "config": {"workload": "TPC-H 1 (tpch_queries.cpp:36-44) without ORDER BY: scan l_shipdate <= 1998-09-02, "
+                               "8 aggregates GROUP BY l_returnflag, l_linestatus", "sf": args.sf, "lineitem_rows": n,
+                   "chunk_size": chunk, "scan_matches": n_match, "groups": n_groups, "parallelism": "single GPU"},
+        "check": {"ok": bool(ok), "groups": groups},
+        "roofline": roofline,
+        "hbm_probe": probe,
+        "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
+                    for k, v in kernels.items()},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line))
+
+
+def cpu_baseline_q1(hy, synth, sf, chunk, host_cpu, runs=5):
+    """The oracle's TPC-H 1 chain (TableScan -> Projection of the seven SELECT-list inputs -> Aggregate, the
+    reference's plan and per-chunk jobs) on a bounded sample of the same columns, dictionary-encoded like the reference
+    default. Median of `runs` on all host cores of this process at SF `sf`, and on one core at a fifth of it."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import helpers
+
+    oracle = helpers.load_oracle()
+    threads, model = host_cpu()
+    I, F = hy.DataType.Int, hy.DataType.Float
+    P, A, O, V = (hy.PQPColumnExpression.from_table, hy.ArithmeticExpression, hy.ArithmeticOperator,
+                  hy.ValueExpression)
+    out = {"unit": "rows/s", "kind": "port", "cpu_model": model, "nproc": os.cpu_count()}
+    for label, n_threads, sample_sf in (("all_cores", threads, sf), ("one_core", 1, sf / 5)):
+        print(f"q1 cpu baseline: {label} SF{sample_sf:g}", file=sys.stderr, flush=True)
+        c = {k: v.numpy() for k, v in synth.q1_columns(sample_sf, "cpu").items()}
+        names = ["l_returnflag", "l_linestatus", "l_quantity", "l_extendedprice", "l_discount", "l_tax", "l_shipdate"]
+        types = [I, I, F, F, F, F, I]
+        t = hy.Table.from_arrays([(nm, ty, False) for nm, ty in zip(names, types)], [c[nm] for nm in names], [],
+                                 chunk)
+        del c
+        hy.encode_all_chunks(t, hy.EncodingType.Dictionary)
+        aggs = [hy.AggregateColumnDefinition(None if col < 0 else col, getattr(hy.AggregateFunction, f.capitalize()))
+                for f, col in Q1_AGGS]
+
+        def run():
+            s = oracle.table_scan(t, 6, hy.PredicateCondition.LessThanEquals, synth.DATE_1998_09_02, [])
+            dp = A(O.Multiplication, P(s, 3), A(O.Subtraction, V(1), P(s, 4)))
+            p = oracle.projection(s, [P(s, 0), P(s, 1), P(s, 2), P(s, 3), dp,
+                                      A(O.Multiplication, dp, A(O.Addition, V(1), P(s, 5))), P(s, 4)])
+            return oracle.aggregate(p, aggs, [0, 1])
+
+        oracle.set_threads(n_threads)
+        times = []
+        for _ in range(runs + 1):
+            t0 = time.perf_counter()
+            agg = run()
+            times.append(time.perf_counter() - t0)
+        oracle.set_threads(1)
+        med = sorted(times[1:])[len(times[1:]) // 2]
+        out[label] = {"value": round(t.row_count() / med, 1), "cores": n_threads, "median_s": round(med, 3),
+                      "runs_s": [round(x, 3) for x in times[1:]],
+                      "sample": f"SF{sample_sf:g}: {t.row_count()} lineitem rows, {agg.row_count()} groups"}
+        del t, agg
     out["value"], out["cores"] = out["all_cores"]["value"], out["all_cores"]["cores"]
     out["sample"] = out["all_cores"]["sample"] + f"; median of {runs}"
     return out

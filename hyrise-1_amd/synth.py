@@ -217,3 +217,24 @@ def dictionary_encode_chunks(values, chunk, lo, domain):
     rank = torch.cumsum(present, dim=1) - 1
     vids = rank[cid, v].to(torch.int32)
     return vids, present.bool()
+
+
+def q1_columns(sf, device, seed=SEED):
+    """The lineitem columns TPC-H 1 reads with the reference schema's types (tpch_db_generator.cpp:20-27):
+    l_quantity, l_extendedprice, l_discount, l_tax as float32 (quantity 1..50, price = quantity x retail
+    900.00..2100.00, discount 0.00..0.10, tax 0.00..0.08), l_returnflag / l_linestatus codes (A=0, N=1, R=2 / F=0,
+    O=1) and l_shipdate int32 days, from the same generator as lineitem_q1_torch (same rows, same flags and dates)."""
+    import torch
+
+    c = lineitem_q1_torch(sf, device, seed=seed)
+    n = c["l_shipdate"].numel()
+    r = torch.arange(n, dtype=torch.int64, device=device)
+    h = _splitmix64_torch(r ^ (seed ^ 0x5052))
+    retail = 90_000 + _umod_torch(h, 120_001)
+    price = ((c["l_quantity"].to(torch.int64) * retail).to(torch.float64) / 100.0).to(torch.float32)
+    disc = (c["l_discount"].to(torch.float64) / 100.0).to(torch.float32)
+    h = _splitmix64_torch(r ^ (seed ^ 0x5441))
+    tax = (_umod_torch(h, 9).to(torch.float64) / 100.0).to(torch.float32)
+    return {"l_returnflag": c["l_returnflag"], "l_linestatus": c["l_linestatus"],
+            "l_quantity": c["l_quantity"].to(torch.float32), "l_extendedprice": price, "l_discount": disc,
+            "l_tax": tax, "l_shipdate": c["l_shipdate"]}
