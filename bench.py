@@ -4,14 +4,13 @@ One step = the reference's query shape, on data already resident in HBM:
     TableScan(lineitem, l_quantity < 24)            dictionary-encoded u8 attribute vectors, 100k-row chunks
     JoinHash(orders, <scan output>, o_orderkey = l_orderkey, Inner)   orders builds (smaller side), the scan's
                                                                        reference table probes
-Rows per step = |lineitem| + |orders| (base-table rows consumed). Everything runs through the C-ABI
-(include/hyrise_amd.h) on buffers owned by torch (device memory only; the C-ABI never sees a torch type).
+executed as the fused hy_scan_join_hash (the scan predicate runs inside the join's first radix pass; --unfused runs
+the two C-ABI calls). Rows per step = |lineitem| + |orders| (base-table rows consumed). Everything runs through the
+C-ABI (include/hyrise_amd.h) on buffers owned by torch (device memory only; the C-ABI never sees a torch type).
 
-Multi-GPU (torchrun, one process per GPU): weak scaling. Rank r holds the r-th shard of an SF·N database (its chunk
-range of orders and lineitem under global chunk ids) and scans it locally. The join is the distributed JoinHash of
-SURVEY.md 8(e): the radix bits come from the GLOBAL build size, both sides are partitioned by the first radix digit,
-records {key, global RowID} are exchanged with one RCCL all-to-all per side over xGMI, and every rank joins the
-partitions it owns (hyrise-1_amd/dist.py); the ranks' outputs concatenated in rank order are the single-node output.
+Multi-GPU (torchrun, one process per GPU): bench_dist.py - strong scaling by default (the SF database split over the
+ranks), the scan fused into the distributed JoinHash's exchange partition, 8-byte records over one RCCL all-to-all
+per side. --workload q1 / q3: bench_tpch.py (BASELINE.json configs[3] / configs[4] at N=1).
 """
 import argparse
 import ctypes
@@ -33,7 +32,11 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--sf", type=float, default=100.0, help="TPC-H scale factor per GPU")
+    p.add_argument("--sf", type=float, default=100.0,
+                   help="TPC-H scale factor of the database (strong scaling) or per GPU (--scaling weak)")
+    p.add_argument("--scaling", choices=["strong", "weak"], default=None,
+                   help="N>1: strong (default; the --sf database split over the ranks, BASELINE.json's metric) or "
+                        "weak (--sf per rank)")
     p.add_argument("--chunk", type=int, default=100_000)
     p.add_argument("--cpu-sf", type=float, default=10.0, help="scale factor of the bounded CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -59,6 +62,10 @@ def main():
         import bench_tpch
 
         return bench_tpch.main_q1(args) if args.workload == "q1" else bench_tpch.main_q3(args)
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        import bench_dist
+
+        return bench_dist.main_distributed(args)
     import torch
 
     hy = importlib.import_module("hyrise-1_amd")
@@ -66,21 +73,8 @@ def main():
     capi = hy.capi
     L = capi.lib
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        if args.dist_backend == "nccl":
-            torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            torch.cuda.set_device(local % torch.cuda.device_count())
-            dist.init_process_group("gloo")
-    else:
-        torch.cuda.set_device(0)
+    world, rank = 1, 0  # N > 1: bench_dist.py
+    torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
     capi.check(L.hy_set_device(dev.index), "hy_set_device")
     stream = torch.cuda.current_stream().cuda_stream
@@ -88,10 +82,8 @@ def main():
 
     # ---------------- data (resident in HBM before timing) ----------------
     n_ord = synth.n_orders(args.sf)
-    first_order = rank * n_ord
-    okey, lines = synth.orders_torch(args.sf, dev, first_order=first_order)
-    # first lineitem row of this shard (not needed for values beyond the quantity stream): use order-based offset
-    lkey, qty = synth.lineitem_torch(okey, lines, first_row=first_order * 4)
+    okey, lines = synth.orders_torch(args.sf, dev)
+    lkey, qty = synth.lineitem_torch(okey, lines)
     del lines
     n_li = lkey.numel()
     vids, present = synth.dictionary_encode_small_domain(qty, chunk, 50)
@@ -99,11 +91,6 @@ def main():
     present_h = present.cpu().numpy()
     n_lchunks = (n_li + chunk - 1) // chunk
     n_ochunks = (n_ord + chunk - 1) // chunk
-    l_stride, o_stride = n_lchunks, n_ochunks  # global chunk id stride per rank (shards differ by a chunk or so)
-    if dist:
-        t = torch.tensor([n_lchunks, n_ochunks], dtype=torch.int64, device=dev if args.dist_backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        l_stride, o_stride = int(t[0]), int(t[1])
     # pad buffers so 16-byte vector loads of the last chunk stay in bounds
     def padded(t, mult=64):
         extra = (-t.numel()) % mult
@@ -132,8 +119,7 @@ def main():
         sc.op = capi.HY_OP_ALL if svid >= dsize else (capi.HY_OP_NONE if svid == 0 else capi.HY_OP_LT)
         sc.out_begin = c * chunk
     sizes = (ctypes.c_uint32 * n_lchunks)(*[min(chunk, n_li - c * chunk) for c in range(n_lchunks)])
-    # global chunk ids: rank r holds lineitem chunks [r * n_lchunks, (r + 1) * n_lchunks) (every shard has the same SF)
-    l_base, o_base = rank * l_stride, rank * o_stride
+    l_base, o_base = 0, 0
     chunk_ids = (ctypes.c_uint32 * n_lchunks)(*range(l_base, l_base + n_lchunks))
     ws_bytes = ctypes.c_size_t(0)
     capi.check(L.hy_table_scan_workspace_size(sizes, n_lchunks, ctypes.byref(ws_bytes)), "scan ws")
@@ -168,8 +154,7 @@ def main():
         r.size = min(chunk, n_li - c * chunk)
         r.kind = capi.HY_COL_VALUE
     build_side = capi.JoinSide(build_chunks, n_ochunks, capi.HY_TYPE_INT32, None, 0, 0, 0)
-    # the reference's radix bits for the GLOBAL build side (join_hash.cpp:640-668)
-    radix_bits = L.hy_join_radix_bits(n_ord * world, 4)
+    radix_bits = L.hy_join_radix_bits(n_ord, 4)  # join_hash.cpp:640-668
     params = capi.JoinParams(capi.HY_JOIN_INNER, capi.HY_TYPE_INT32, radix_bits, 17)
     n_parts = 1 << radix_bits
     part_begin = torch.empty(n_parts, dtype=torch.int64, device=dev)
@@ -209,25 +194,6 @@ def main():
                                   state["ws"].data_ptr(), state["ws"].numel(), stream), "hy_join_hash")
         return n_probe, res.total_pairs
 
-    xj = None
-    if world > 1:
-        hdist = importlib.import_module("hyrise-1_amd.dist")
-        xj = hdist.ExchangeJoin(capi, radix_bits, world, capi.HY_TYPE_INT32, capi.HY_JOIN_INNER, 17)
-
-    def run_join_distributed(counts_h):
-        # partition both sides by the first radix digit, RCCL all-to-all over xGMI, then the
-        # remaining passes + LDS build/probe of this rank's partitions
-        side, keep, n_probe = probe_side_from_counts(counts_h)
-        brec, bcnt = xj.partition(build_side, n_ord, False, stream, dev, key="build")
-        precs, pcnt = xj.partition(side, n_probe, False, stream, dev, key="probe")
-        xdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
-        brecv, bmat = hdist.exchange_records(dist, brec.to(xdev), bcnt, rank, world, device=xdev)
-        precv, pmat = hdist.exchange_records(dist, precs.to(xdev), pcnt, rank, world, device=xdev)
-        brecv, precv = brecv.to(dev), precv.to(dev)
-        out = xj.join(brecv, bmat, precv, pmat, rank, stream, dev)
-        state["recv_rows"] = (int(bmat.sum()), int(pmat.sum()))
-        return n_probe, out[4]
-
     # ---------------- fused TableScan -> JoinHash (hy_scan_join_hash): the scan predicate runs inside the join's
     # first radix pass over lineitem's chunks; the scan output (per-chunk offset lists) is written by the same pass ----
     probe_chunks = (capi.JoinChunk * n_lchunks)()
@@ -265,7 +231,7 @@ def main():
         capi.check(st, "hy_scan_join_hash")
         return res.total_pairs
 
-    fused = world == 1 and not args.unfused
+    fused = not args.unfused
 
     def step():
         if fused:
@@ -273,15 +239,13 @@ def main():
             return None, pairs  # scan matches are read once after the timed region (scan_begin[-1])
         run_scan()
         counts_h = scan_counts.cpu().numpy()  # D2H of per-chunk match counts (the output chunk layout)
-        return run_join_distributed(counts_h) if xj else run_join(counts_h)
+        return run_join(counts_h)
 
     for _ in range(args.warmup):
         n_probe, pairs = step()
     torch.cuda.synchronize()
 
     # ---------------- timed region ----------------
-    if dist:
-        dist.barrier()
     torch.cuda.synchronize()
     L.hy_kernel_stats_reset()
     L.hy_kernel_stats_enable(1)
@@ -293,7 +257,7 @@ def main():
     L.hy_kernel_stats_enable(0)
     if fused:
         n_probe = int(scan_begin[-1].item())
-    if args.join_trace and rank == 0 and world == 1:
+    if args.join_trace:
         import numpy as np
         trace = torch.zeros(5 * (1 << radix_bits), dtype=torch.int64, device=dev)
         L.hy_debug_set_join_trace.argtypes = [ctypes.c_void_p]
@@ -303,18 +267,7 @@ def main():
         L.hy_debug_set_join_trace(None)
         t = trace.view(-1, 5).cpu().numpy().astype(np.float64) / 100.0  # 100 MHz device clock -> us
         np.savez(args.join_trace, stamps_us=t, out_pairs=part_count.cpu().numpy())
-    if dist:
-        dist.barrier()
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        # whole-job totals: rows processed, scan matches and join pairs summed over ranks
-        tot = torch.tensor([n_li, n_ord, n_probe, pairs], dtype=torch.int64,
-                           device=dev if args.dist_backend == "nccl" else "cpu")
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        g_li, g_ord, g_probe, g_pairs = (int(x) for x in tot.tolist())
-    else:
-        g_li, g_ord, g_probe, g_pairs = n_li, n_ord, n_probe, int(pairs)
+    g_li, g_ord, g_probe, g_pairs = n_li, n_ord, n_probe, int(pairs)
 
     # ---------------- per-kernel device time (HIP events on the launch stream) ----------------
     nk = ctypes.c_uint32(0)
@@ -331,7 +284,7 @@ def main():
     # algorithmic bytes: scan 1 B/row read + 4 B/match written (chunk offsets; 8 B RowIDs on the
     # unfused path); JoinHash 4 B/build row + 4 B/probe row read + 16 B/pair written. Partition passes are overhead:
     # for them the table lists the bytes each kernel must move (records 8 B, digit bytes 1 B), not algorithmic bytes.
-    recv_build, recv_probe = state.get("recv_rows", (n_ord, n_probe))  # rows this rank joins after the exchange
+    recv_build, recv_probe = n_ord, n_probe
     scan_out_b = 4 if fused else 8
     e2e_bytes = n_li * 1 + n_probe * scan_out_b + n_ord * 4 + n_probe * 4 + int(pairs) * 16
     if fused:
@@ -399,17 +352,16 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(step_s * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling or "strong",
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic (seeded counter-based TPC-H-shaped columns, resident in HBM)",
             "config": {"workload": f"TableScan(l_quantity<24, dictionary u8) -> JoinHash(orders ⋈ scan, "
                                    f"o_orderkey=l_orderkey, radix_bits={radix_bits})",
                        "path": "fused hy_scan_join_hash" if fused else "hy_table_scan_row_ids + hy_join_hash",
-                       "sf_per_gpu": args.sf, "lineitem_rows": g_li, "orders_rows": g_ord, "chunk_size": chunk,
+                       "sf_total": args.sf, "lineitem_rows": g_li, "orders_rows": g_ord, "chunk_size": chunk,
                        "scan_matches": g_probe, "join_pairs": g_pairs,
-                       "parallelism": f"chunk-sharded x{world}" + (f", RCCL all-to-all radix exchange"
-                                                                    if world > 1 else "")},
+                       "parallelism": "single GPU"},
             "roofline": roofline,
             "kernel_roofline": kernel_roofline,
             "hbm_probe": probe,
@@ -418,8 +370,6 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))
-    if dist:
-        dist.destroy_process_group()
 
 
 def kernel_stats(L):

@@ -167,6 +167,28 @@ _sigs = {
                                              ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
                                              ctypes.POINTER(JoinResult), ctypes.c_void_p, ctypes.c_size_t,
                                              ctypes.c_void_p]),
+    "hy_join_exchange_row_record_bytes": (ctypes.c_uint32, [ctypes.c_int32]),
+    "hy_scan_join_exchange_partition_workspace_size": (ctypes.c_int, [ctypes.POINTER(JoinSide),
+                                                                      ctypes.POINTER(JoinFilter),
+                                                                      ctypes.POINTER(JoinParams), ctypes.c_uint32,
+                                                                      ctypes.POINTER(ctypes.c_size_t)]),
+    "hy_scan_join_exchange_partition": (ctypes.c_int, [ctypes.POINTER(JoinSide), ctypes.POINTER(JoinFilter),
+                                                       ctypes.POINTER(JoinParams), ctypes.c_int32, ctypes.c_uint32,
+                                                       ctypes.c_uint64, ctypes.c_void_p,
+                                                       ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p,
+                                                       ctypes.c_size_t, ctypes.c_void_p]),
+    "hy_join_exchange_join_rows_workspace_size": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64),
+                                                                 ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32,
+                                                                 ctypes.c_uint32, ctypes.POINTER(JoinParams),
+                                                                 ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                                                 ctypes.c_uint32, ctypes.POINTER(ctypes.c_size_t)]),
+    "hy_join_exchange_join_rows": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p,
+                                                  ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32, ctypes.c_uint32,
+                                                  ctypes.c_uint32, ctypes.POINTER(JoinParams), ctypes.c_void_p,
+                                                  ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                                  ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                                  ctypes.POINTER(JoinResult), ctypes.c_void_p, ctypes.c_size_t,
+                                                  ctypes.c_void_p]),
 }
 for _name, (_res, _args) in _sigs.items():
     _f = getattr(lib, _name)

@@ -226,6 +226,180 @@ hy_status hy_join_exchange_join(const void* build_records, const uint64_t* build
   return fail(HY_ERR_UNSUPPORTED, "hashed type");
 }
 
+// ---- row-index exchange records {key, uint32 global row} ----
+uint32_t hy_join_exchange_row_record_bytes(int32_t hashed_type) {
+  return (hashed_type == HY_TYPE_INT32 || hashed_type == HY_TYPE_FLOAT) ? 8u : 16u;
+}
+
+namespace {
+
+hy_status plan_row_side(const hy_join_side* side, const hy_join_filter* filter, const hy_join_params* params,
+                        uint32_t n_ranks, uint64_t row_base, SidePlan& p, std::vector<uint32_t>& w) {
+  if (!params || n_ranks == 0) return fail(HY_ERR_INVALID_ARGUMENT, "null argument");
+  if (params->radix_bits > 24) return fail(HY_ERR_UNSUPPORTED, "radix_bits > 24");
+  hy_status st = plan_side(side, p);
+  if (st != HY_OK) return st;
+  for (const auto& c : p.chunks)
+    if (c.pos_list) return fail(HY_ERR_UNSUPPORTED, "row-index exchange records need a data-table side");
+  st = plan_filter(filter, p, side->value_type, params->hashed_type);
+  if (st != HY_OK) return st;
+  if (p.n_rows + row_base >= (p.filtered ? 0x7FFFFFFFull : 0xFFFFFFFFull))
+    return fail(HY_ERR_UNSUPPORTED, "global row indexes exceed the 32-bit record payload");
+  for (auto& c : p.chunks) c.row_begin += row_base;  // payload = global row index
+  w = digit_plan(params->radix_bits, ceil_log2(n_ranks));
+  if (w.empty() || (1u << w[0]) < n_ranks) return fail(HY_ERR_UNSUPPORTED, "radix bits too few for the ranks");
+  return HY_OK;
+}
+
+}  // namespace
+
+hy_status hy_scan_join_exchange_partition_workspace_size(const hy_join_side* side, const hy_join_filter* filter,
+                                                         const hy_join_params* params, uint32_t n_ranks,
+                                                         size_t* bytes) {
+  if (!bytes) return fail(HY_ERR_INVALID_ARGUMENT, "bytes");
+  SidePlan p;
+  std::vector<uint32_t> w;
+  hy_status st = plan_row_side(side, filter, params, n_ranks, 0, p, w);
+  if (st != HY_OK) return st;
+  switch (params->hashed_type) {
+    case HY_TYPE_INT32:
+      *bytes = exchange_partition_rows_bytes_i32(p, params->radix_bits, w);
+      return HY_OK;
+    case HY_TYPE_INT64:
+      *bytes = exchange_partition_rows_bytes_i64(p, params->radix_bits, w);
+      return HY_OK;
+    case HY_TYPE_FLOAT:
+      *bytes = exchange_partition_rows_bytes_f32(p, params->radix_bits, w);
+      return HY_OK;
+    case HY_TYPE_DOUBLE:
+      *bytes = exchange_partition_rows_bytes_f64(p, params->radix_bits, w);
+      return HY_OK;
+  }
+  return fail(HY_ERR_UNSUPPORTED, "hashed type");
+}
+
+hy_status hy_scan_join_exchange_partition(const hy_join_side* side, const hy_join_filter* filter,
+                                          const hy_join_params* params, int32_t keep_nulls, uint32_t n_ranks,
+                                          uint64_t row_base, void* out_records, uint64_t* bucket_counts,
+                                          void* workspace, size_t workspace_bytes, hy_stream_t stream) {
+  if (!bucket_counts) return fail(HY_ERR_INVALID_ARGUMENT, "bucket_counts");
+  SidePlan p;
+  std::vector<uint32_t> w;
+  hy_status st = plan_row_side(side, filter, params, n_ranks, row_base, p, w);
+  if (st != HY_OK) return st;
+  if (p.n_rows && !out_records) return fail(HY_ERR_INVALID_ARGUMENT, "out_records");
+  hipStream_t s = S(stream);
+  switch (params->hashed_type) {
+    case HY_TYPE_INT32:
+      return exchange_partition_rows_i32(p, side->value_type, params, keep_nulls, w, out_records, bucket_counts,
+                                         workspace, workspace_bytes, s);
+    case HY_TYPE_INT64:
+      return exchange_partition_rows_i64(p, side->value_type, params, keep_nulls, w, out_records, bucket_counts,
+                                         workspace, workspace_bytes, s);
+    case HY_TYPE_FLOAT:
+      return exchange_partition_rows_f32(p, side->value_type, params, keep_nulls, w, out_records, bucket_counts,
+                                         workspace, workspace_bytes, s);
+    case HY_TYPE_DOUBLE:
+      return exchange_partition_rows_f64(p, side->value_type, params, keep_nulls, w, out_records, bucket_counts,
+                                         workspace, workspace_bytes, s);
+  }
+  return fail(HY_ERR_UNSUPPORTED, "hashed type");
+}
+
+namespace {
+
+hy_status plan_row_join(const uint64_t* build_counts, const uint64_t* probe_counts, uint32_t n_senders,
+                        uint32_t first_bucket, uint32_t n_buckets, const hy_join_params* params,
+                        const uint32_t* build_chunk_sizes, uint32_t n_build_chunks, const uint32_t* probe_chunk_sizes,
+                        uint32_t n_probe_chunks, RecvPlan& rbp, RecvPlan& rpp, std::vector<uint32_t>& w, Layouts& lay) {
+  if (!params || !build_counts || !probe_counts || n_senders == 0) return fail(HY_ERR_INVALID_ARGUMENT, "null argument");
+  if ((n_build_chunks && !build_chunk_sizes) || (n_probe_chunks && !probe_chunk_sizes))
+    return fail(HY_ERR_INVALID_ARGUMENT, "chunk layouts");
+  if (params->radix_bits > 24) return fail(HY_ERR_UNSUPPORTED, "radix_bits > 24");
+  if (!(params->mode == HY_JOIN_INNER || params->mode == HY_JOIN_LEFT || params->mode == HY_JOIN_RIGHT ||
+        params->mode == HY_JOIN_SEMI || params->mode == HY_JOIN_ANTI))
+    return fail(HY_ERR_UNSUPPORTED, "join mode");
+  w = digit_plan(params->radix_bits, ceil_log2(n_senders));
+  if (w.empty() || first_bucket + n_buckets > (1u << w[0])) return fail(HY_ERR_INVALID_ARGUMENT, "bucket range");
+  const uint32_t digits = 1u << (w.size() > 1 ? w[1] : 0);
+  rbp = recv_plan(build_counts, n_senders, n_buckets, digits);
+  rpp = recv_plan(probe_counts, n_senders, n_buckets, digits);
+  if (rbp.rows >= 0xFFFFFFFFull || rpp.rows >= 0xFFFFFFFFull)
+    return fail(HY_ERR_UNSUPPORTED, "received side exceeds 2^32-1 rows");
+  lay.build_rows = layout_rows(build_chunk_sizes, n_build_chunks);
+  lay.probe_rows = layout_rows(probe_chunk_sizes, n_probe_chunks);
+  return HY_OK;
+}
+
+}  // namespace
+
+hy_status hy_join_exchange_join_rows_workspace_size(const uint64_t* build_counts, const uint64_t* probe_counts,
+                                                    uint32_t n_senders, uint32_t n_buckets,
+                                                    const hy_join_params* params, const uint32_t* build_chunk_sizes,
+                                                    uint32_t n_build_chunks, const uint32_t* probe_chunk_sizes,
+                                                    uint32_t n_probe_chunks, size_t* bytes) {
+  if (!bytes) return fail(HY_ERR_INVALID_ARGUMENT, "bytes");
+  RecvPlan rb, rp;
+  std::vector<uint32_t> w;
+  Layouts lay;
+  hy_status st = plan_row_join(build_counts, probe_counts, n_senders, 0, n_buckets, params, build_chunk_sizes,
+                               n_build_chunks, probe_chunk_sizes, n_probe_chunks, rb, rp, w, lay);
+  if (st != HY_OK) return st;
+  const uint32_t bits = params->radix_bits;
+  switch (params->hashed_type) {
+    case HY_TYPE_INT32:
+      *bytes = exchange_join_rows_bytes_i32(rb, rp, bits, w, n_buckets, n_senders, lay);
+      return HY_OK;
+    case HY_TYPE_INT64:
+      *bytes = exchange_join_rows_bytes_i64(rb, rp, bits, w, n_buckets, n_senders, lay);
+      return HY_OK;
+    case HY_TYPE_FLOAT:
+      *bytes = exchange_join_rows_bytes_f32(rb, rp, bits, w, n_buckets, n_senders, lay);
+      return HY_OK;
+    case HY_TYPE_DOUBLE:
+      *bytes = exchange_join_rows_bytes_f64(rb, rp, bits, w, n_buckets, n_senders, lay);
+      return HY_OK;
+  }
+  return fail(HY_ERR_UNSUPPORTED, "hashed type");
+}
+
+hy_status hy_join_exchange_join_rows(const void* build_records, const uint64_t* build_counts,
+                                     const void* probe_records, const uint64_t* probe_counts, uint32_t n_senders,
+                                     uint32_t first_bucket, uint32_t n_buckets, const hy_join_params* params,
+                                     const uint32_t* build_chunk_sizes, uint32_t n_build_chunks,
+                                     const uint32_t* probe_chunk_sizes, uint32_t n_probe_chunks,
+                                     hy_row_id* out_build, hy_row_id* out_probe, uint64_t out_capacity,
+                                     uint64_t* partition_begin, uint32_t* partition_counts, hy_join_result* result,
+                                     void* workspace, size_t workspace_bytes, hy_stream_t stream) {
+  if (!partition_begin || !partition_counts) return fail(HY_ERR_INVALID_ARGUMENT, "partition arrays");
+  RecvPlan rb, rp;
+  std::vector<uint32_t> w;
+  Layouts lay;
+  hy_status st = plan_row_join(build_counts, probe_counts, n_senders, first_bucket, n_buckets, params,
+                               build_chunk_sizes, n_build_chunks, probe_chunk_sizes, n_probe_chunks, rb, rp, w, lay);
+  if (st != HY_OK) return st;
+  hipStream_t s = S(stream);
+  switch (params->hashed_type) {
+    case HY_TYPE_INT32:
+      return exchange_join_rows_i32(build_records, probe_records, rb, rp, n_senders, n_buckets, w, params, out_build,
+                                    out_probe, out_capacity, partition_begin, partition_counts, result, workspace,
+                                    workspace_bytes, s, lay);
+    case HY_TYPE_INT64:
+      return exchange_join_rows_i64(build_records, probe_records, rb, rp, n_senders, n_buckets, w, params, out_build,
+                                    out_probe, out_capacity, partition_begin, partition_counts, result, workspace,
+                                    workspace_bytes, s, lay);
+    case HY_TYPE_FLOAT:
+      return exchange_join_rows_f32(build_records, probe_records, rb, rp, n_senders, n_buckets, w, params, out_build,
+                                    out_probe, out_capacity, partition_begin, partition_counts, result, workspace,
+                                    workspace_bytes, s, lay);
+    case HY_TYPE_DOUBLE:
+      return exchange_join_rows_f64(build_records, probe_records, rb, rp, n_senders, n_buckets, w, params, out_build,
+                                    out_probe, out_capacity, partition_begin, partition_counts, result, workspace,
+                                    workspace_bytes, s, lay);
+  }
+  return fail(HY_ERR_UNSUPPORTED, "hashed type");
+}
+
 uint32_t hy_join_exchange_bucket_bits(uint32_t radix_bits, uint32_t n_ranks) {
   const auto w = digit_plan(radix_bits, ceil_log2(std::max<uint32_t>(1, n_ranks)));
   return w.empty() ? 0u : w[0];

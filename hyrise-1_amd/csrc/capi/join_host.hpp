@@ -778,12 +778,12 @@ inline uint32_t ceil_log2(uint32_t n) {
   return b;
 }
 
-template <typename H>
+template <typename H, typename P = hy_row_id>
 size_t exchange_partition_bytes(const SidePlan& p, uint32_t bits, const std::vector<uint32_t>& w) {
   Carver cv{nullptr, 0};
-  SideBufs<H, hy_row_id> b;
+  SideBufs<H, P> b;
   SideSizes z = sizes_of(p, false);
-  carve_side<H, hy_row_id>(cv, z, bits, std::vector<uint32_t>(w.begin(), w.begin() + 1), 1, false, b);
+  carve_side<H, P>(cv, z, bits, std::vector<uint32_t>(w.begin(), w.begin() + 1), 1, false, b);
   Common c;
   carve_common(cv, std::max<uint64_t>((1ull << w[0]) * std::max<uint64_t>(1, p.n_tiles1), 2), bits, &c);
   return cv.used + 256;
@@ -851,21 +851,21 @@ inline RecvPlan recv_plan(const uint64_t* counts, uint32_t n_senders, uint32_t n
 }
 
 // Receiver device buffers of one side.
-template <typename H>
+template <typename H, typename P = hy_row_id>
 struct RecvBufs {
-  SideBufs<H, hy_row_id> b;
+  SideBufs<H, P> b;
   uint32_t *seg_begin, *seg_end, *seg_stride, *seg_toff, *group_tiles, *group_out, *owner;
   uint64_t *seg_tile_begin, *seg_hbase, *group_hbase;
 };
 
-template <typename H>
+template <typename H, typename P = hy_row_id>
 void carve_recv(Carver& cv, const RecvPlan& r, uint32_t bits, const std::vector<uint32_t>& w, uint32_t nb,
-                uint32_t n_senders, RecvBufs<H>& rb) {
+                uint32_t n_senders, RecvBufs<H, P>& rb) {
   SideSizes z;
   z.rows = r.rows;
   std::vector<uint32_t> tail(w.begin() + 1, w.end());
   if (tail.empty()) tail.push_back(0);
-  carve_side<H, hy_row_id>(cv, z, bits, tail, uint64_t(nb) * n_senders, true, rb.b);
+  carve_side<H, P>(cv, z, bits, tail, uint64_t(nb) * n_senders, true, rb.b);
   const uint32_t nseg = std::max<uint32_t>(1, nb * n_senders);
   rb.seg_begin = cv.take<uint32_t>(nseg);
   rb.seg_end = cv.take<uint32_t>(nseg);
@@ -879,10 +879,10 @@ void carve_recv(Carver& cv, const RecvPlan& r, uint32_t bits, const std::vector<
   rb.owner = cv.take<uint32_t>(std::max<uint64_t>(1, r.tiles));
 }
 
-template <typename H>
-hy_status recv_side(const char* tag, const RecvPlan& r, RecvBufs<H>& rb, const std::vector<uint32_t>& w, uint32_t bits,
-                    uint32_t nb, uint32_t n_senders, uint32_t seed, const hyk::Rec<H, hy_row_id>* in,
-                    const Common& c, hipStream_t s, hyk::Rec<H, hy_row_id>** recs, uint32_t** bounds) {
+template <typename H, typename P = hy_row_id>
+hy_status recv_side(const char* tag, const RecvPlan& r, RecvBufs<H, P>& rb, const std::vector<uint32_t>& w,
+                    uint32_t bits, uint32_t nb, uint32_t n_senders, uint32_t seed, const hyk::Rec<H, P>* in,
+                    const Common& c, hipStream_t s, hyk::Rec<H, P>** recs, uint32_t** bounds) {
   auto up = [&](auto* dst, const auto& v) -> hy_status {
     if (!v.empty()) HY_HIP(hipMemcpyAsync(dst, v.data(), sizeof(v[0]) * v.size(), hipMemcpyHostToDevice, s));
     return HY_OK;
@@ -904,21 +904,33 @@ hy_status recv_side(const char* tag, const RecvPlan& r, RecvBufs<H>& rb, const s
                rb.seg_hbase, rb.seg_stride,     rb.seg_toff, sub2()};
   hyk::Groups gr{rb.group_hbase, rb.group_tiles, rb.group_out};
   // the merge pass must not write through a stale histogram entry: hist words are exactly the groups' tiles x digits
-  hy_status st = record_pass<H, hy_row_id>(tag, rb.b, sg, gr, nb, r.tiles, bits, shift, w1, seed, in, nullptr,
-                                           hyk::NextDigit{nullptr, 0, 0}, rb.b.recA, rb.b.total, rb.b.segA, c, s,
-                                           r.rows);
+  hy_status st = record_pass<H, P>(tag, rb.b, sg, gr, nb, r.tiles, bits, shift, w1, seed, in, nullptr,
+                                   hyk::NextDigit{nullptr, 0, 0}, rb.b.recA, rb.b.total, rb.b.segA, c, s, r.rows);
   if (st != HY_OK) return st;
-  return local_passes<H, hy_row_id>(tag, rb.b, w, 2, bits, seed, rb.b.recA, rb.b.recB, nullptr, nullptr, rb.b.segA,
-                                    rb.b.segB, uint64_t(nb) << w1, rb.b.total, r.rows, c, s, recs, bounds);
+  return local_passes<H, P>(tag, rb.b, w, 2, bits, seed, rb.b.recA, rb.b.recB, nullptr, nullptr, rb.b.segA, rb.b.segB,
+                            uint64_t(nb) << w1, rb.b.total, r.rows, c, s, recs, bounds);
 }
 
-template <typename H>
+// Global chunk layouts of the two tables (row-index exchange records): device row_begin arrays of the RowMaps.
+struct Layouts {
+  std::vector<uint64_t> build_rows, probe_rows;  // row_begin (n_chunks + 1 each); empty for RowID records
+};
+
+inline std::vector<uint64_t> layout_rows(const uint32_t* sizes, uint32_t n) {
+  std::vector<uint64_t> r(n + 1, 0);
+  for (uint32_t i = 0; i < n; ++i) r[i + 1] = r[i] + sizes[i];
+  return r;
+}
+
+template <typename H, typename P = hy_row_id>
 size_t exchange_join_bytes(const RecvPlan& rbp, const RecvPlan& rpp, uint32_t bits, const std::vector<uint32_t>& w,
-                           uint32_t nb, uint32_t n_senders) {
+                           uint32_t nb, uint32_t n_senders, const Layouts& lay = Layouts{}) {
   Carver cv{nullptr, 0};
-  RecvBufs<H> a, b;
-  carve_recv<H>(cv, rbp, bits, w, nb, n_senders, a);
-  carve_recv<H>(cv, rpp, bits, w, nb, n_senders, b);
+  RecvBufs<H, P> a, b;
+  carve_recv<H, P>(cv, rbp, bits, w, nb, n_senders, a);
+  carve_recv<H, P>(cv, rpp, bits, w, nb, n_senders, b);
+  cv.take<uint64_t>(lay.build_rows.size() + 1);
+  cv.take<uint64_t>(lay.probe_rows.size() + 1);
   Common c;
   const uint64_t max_scan = std::max({rbp.hist_words * 2, rpp.hist_words * 2, (uint64_t(1) << bits) + 1,
                                       (rbp.rows + rpp.rows) / span2() * 256 + uint64_t(nb) * n_senders * 256});
@@ -926,7 +938,7 @@ size_t exchange_join_bytes(const RecvPlan& rbp, const RecvPlan& rpp, uint32_t bi
   return cv.used + 256;
 }
 
-template <typename H>
+template <typename H, typename P = hy_row_id>
 hy_status exchange_partition_for_hashed(const SidePlan& p, int32_t value_type, const hy_join_params* params,
                                         int32_t keep_nulls, const std::vector<uint32_t>& w, void* out_records,
                                         uint64_t* bucket_counts, void* workspace, size_t workspace_bytes,
@@ -936,18 +948,17 @@ hy_status exchange_partition_for_hashed(const SidePlan& p, int32_t value_type, c
   return dispatch_type(value_type, [&](auto ttag) -> hy_status {
     using T_ = decltype(ttag);
     if constexpr (reachable<T_, H>()) {
-      if (workspace_bytes < exchange_partition_bytes<H>(p, bits, w)) return fail(HY_ERR_WORKSPACE, "workspace");
+      if (workspace_bytes < exchange_partition_bytes<H, P>(p, bits, w)) return fail(HY_ERR_WORKSPACE, "workspace");
       Carver cv{static_cast<char*>(workspace), workspace_bytes};
-      SideBufs<H, hy_row_id> b;
-      carve_side<H, hy_row_id>(cv, sizes_of(p, false), bits, std::vector<uint32_t>(w.begin(), w.begin() + 1), 1,
-                               false, b);
+      SideBufs<H, P> b;
+      carve_side<H, P>(cv, sizes_of(p, false), bits, std::vector<uint32_t>(w.begin(), w.begin() + 1), 1, false, b);
       Common c{};
       carve_common(cv, std::max<uint64_t>(uint64_t(T) * std::max<uint64_t>(1, p.n_tiles1), 2), bits, &c);
       if (!cv.ok) return fail(HY_ERR_WORKSPACE, "workspace");
       if (upload_side(p, b, s)) return HY_ERR_DEVICE;
-      hy_status st2 = pass0_side<T_, H, hy_row_id>("exchange", p, b, bits, w[0], params->seed, keep_nulls != 0,
-                                                   p.ref_base, hyk::NextDigit{nullptr, 0, 0}, c, s,
-                                                   static_cast<hyk::Rec<H, hy_row_id>*>(out_records));
+      hy_status st2 = pass0_side<T_, H, P>("exchange", p, b, bits, w[0], params->seed, keep_nulls != 0, p.ref_base,
+                                           hyk::NextDigit{nullptr, 0, 0}, c, s,
+                                           static_cast<hyk::Rec<H, P>*>(out_records));
       if (st2 != HY_OK) return st2;
       std::vector<uint32_t> bounds(T + 1);
       HY_HIP(hipMemcpyAsync(bounds.data(), b.segA, 4 * (T + 1), hipMemcpyDeviceToHost, s));
@@ -960,39 +971,47 @@ hy_status exchange_partition_for_hashed(const SidePlan& p, int32_t value_type, c
   });
 }
 
-template <typename H>
+template <typename H, typename P = hy_row_id>
 hy_status exchange_join_for_hashed(const void* build_records, const void* probe_records, const RecvPlan& rbp,
                                    const RecvPlan& rpp, uint32_t n_senders, uint32_t n_buckets,
                                    const std::vector<uint32_t>& w, const hy_join_params* params, hy_row_id* out_build,
                                    hy_row_id* out_probe, uint64_t out_capacity, uint64_t* partition_begin,
                                    uint32_t* partition_counts, hy_join_result* result, void* workspace,
-                                   size_t workspace_bytes, hipStream_t s) {
+                                   size_t workspace_bytes, hipStream_t s, const Layouts& lay = Layouts{}) {
   const uint32_t bits = params->radix_bits;
-  if (workspace_bytes < exchange_join_bytes<H>(rbp, rpp, bits, w, n_buckets, n_senders))
+  if (workspace_bytes < exchange_join_bytes<H, P>(rbp, rpp, bits, w, n_buckets, n_senders, lay))
     return fail(HY_ERR_WORKSPACE, "exchange join workspace too small");
   Carver cv{static_cast<char*>(workspace), workspace_bytes};
-  RecvBufs<H> rb, rp;
-  carve_recv<H>(cv, rbp, bits, w, n_buckets, n_senders, rb);
-  carve_recv<H>(cv, rpp, bits, w, n_buckets, n_senders, rp);
+  RecvBufs<H, P> rb, rp;
+  carve_recv<H, P>(cv, rbp, bits, w, n_buckets, n_senders, rb);
+  carve_recv<H, P>(cv, rpp, bits, w, n_buckets, n_senders, rp);
+  uint64_t* b_rows = cv.take<uint64_t>(lay.build_rows.size() + 1);
+  uint64_t* p_rows = cv.take<uint64_t>(lay.probe_rows.size() + 1);
   Common c{};
   const uint64_t max_scan = std::max({rbp.hist_words * 2, rpp.hist_words * 2, (uint64_t(1) << bits) + 1,
                                       (rbp.rows + rpp.rows) / span2() * 256 + uint64_t(n_buckets) * n_senders * 256});
   carve_common(cv, max_scan, bits, &c);
   if (!cv.ok) return fail(HY_ERR_WORKSPACE, "exchange join workspace too small");
-  using R = hyk::Rec<H, hy_row_id>;
+  using R = hyk::Rec<H, P>;
   R* recs[2] = {nullptr, nullptr};
   uint32_t* bounds[2] = {nullptr, nullptr};
-  hy_status st = recv_side<H>("build", rbp, rb, w, bits, n_buckets, n_senders, params->seed,
-                              static_cast<const R*>(build_records), c, s, &recs[0], &bounds[0]);
+  hy_status st = recv_side<H, P>("build", rbp, rb, w, bits, n_buckets, n_senders, params->seed,
+                                 static_cast<const R*>(build_records), c, s, &recs[0], &bounds[0]);
   if (st != HY_OK) return st;
-  st = recv_side<H>("probe", rpp, rp, w, bits, n_buckets, n_senders, params->seed,
-                    static_cast<const R*>(probe_records), c, s, &recs[1], &bounds[1]);
+  st = recv_side<H, P>("probe", rpp, rp, w, bits, n_buckets, n_senders, params->seed,
+                       static_cast<const R*>(probe_records), c, s, &recs[1], &bounds[1]);
   if (st != HY_OK) return st;
   const uint32_t n_parts = n_buckets << (bits - w[0]);
-  return run_join_partitions<H, hy_row_id>(bounds[0], bounds[1], n_parts, recs[0], recs[1], hyk::RowMap{},
-                                           hyk::RowMap{}, params->mode, out_build, out_probe, out_capacity,
-                                           partition_begin, partition_counts, result, c, s, rbp.rows + rpp.rows,
-                                           rpp.rows);
+  hyk::RowMap bmap{}, pmap{};
+  if constexpr (std::is_same_v<P, uint32_t>) {  // global row indexes -> RowIDs of the global chunk layouts
+    HY_HIP(hipMemcpyAsync(b_rows, lay.build_rows.data(), 8 * lay.build_rows.size(), hipMemcpyHostToDevice, s));
+    HY_HIP(hipMemcpyAsync(p_rows, lay.probe_rows.data(), 8 * lay.probe_rows.size(), hipMemcpyHostToDevice, s));
+    bmap = make_map(b_rows, lay.build_rows);
+    pmap = make_map(p_rows, lay.probe_rows);
+  }
+  return run_join_partitions<H, P>(bounds[0], bounds[1], n_parts, recs[0], recs[1], bmap, pmap, params->mode,
+                                   out_build, out_probe, out_capacity, partition_begin, partition_counts, result, c, s,
+                                   rbp.rows + rpp.rows, rpp.rows);
 }
 
 template <typename H>
@@ -1033,7 +1052,22 @@ hy_status join_for_hashed(const SidePlan& bp, const SidePlan& pp, int32_t build_
                                    const std::vector<uint32_t>& w, const hy_join_params* params,                   \
                                    hy_row_id* out_build, hy_row_id* out_probe, uint64_t out_capacity,              \
                                    uint64_t* partition_begin, uint32_t* partition_counts, hy_join_result* result,  \
-                                   void* workspace, size_t workspace_bytes, hipStream_t s);
+                                   void* workspace, size_t workspace_bytes, hipStream_t s);                        \
+  size_t exchange_partition_rows_bytes_##SUFFIX(const SidePlan& p, uint32_t bits, const std::vector<uint32_t>& w);   \
+  size_t exchange_join_rows_bytes_##SUFFIX(const RecvPlan& rbp, const RecvPlan& rpp, uint32_t bits,                 \
+                                           const std::vector<uint32_t>& w, uint32_t nb, uint32_t n_senders,         \
+                                           const Layouts& lay);                                                     \
+  hy_status exchange_partition_rows_##SUFFIX(const SidePlan& p, int32_t value_type, const hy_join_params* params,   \
+                                             int32_t keep_nulls, const std::vector<uint32_t>& w, void* out_records, \
+                                             uint64_t* bucket_counts, void* workspace, size_t workspace_bytes,      \
+                                             hipStream_t s);                                                        \
+  hy_status exchange_join_rows_##SUFFIX(const void* build_records, const void* probe_records, const RecvPlan& rbp, \
+                                        const RecvPlan& rpp, uint32_t n_senders, uint32_t n_buckets,               \
+                                        const std::vector<uint32_t>& w, const hy_join_params* params,              \
+                                        hy_row_id* out_build, hy_row_id* out_probe, uint64_t out_capacity,         \
+                                        uint64_t* partition_begin, uint32_t* partition_counts,                     \
+                                        hy_join_result* result, void* workspace, size_t workspace_bytes,           \
+                                        hipStream_t s, const Layouts& lay);
 HYJ_DECLARE(i32, int32_t)
 HYJ_DECLARE(i64, int64_t)
 HYJ_DECLARE(f32, float)
@@ -1074,6 +1108,32 @@ HYJ_DECLARE(f64, double)
     return exchange_join_for_hashed<H>(build_records, probe_records, rbp, rpp, n_senders, n_buckets, w, params,     \
                                        out_build, out_probe, out_capacity, partition_begin, partition_counts,      \
                                        result, workspace, workspace_bytes, s);                                      \
+  }                                                                                                                 \
+  size_t exchange_partition_rows_bytes_##SUFFIX(const SidePlan& p, uint32_t bits, const std::vector<uint32_t>& w) {  \
+    return exchange_partition_bytes<H, uint32_t>(p, bits, w);                                                       \
+  }                                                                                                                 \
+  size_t exchange_join_rows_bytes_##SUFFIX(const RecvPlan& rbp, const RecvPlan& rpp, uint32_t bits,                 \
+                                           const std::vector<uint32_t>& w, uint32_t nb, uint32_t n_senders,         \
+                                           const Layouts& lay) {                                                    \
+    return exchange_join_bytes<H, uint32_t>(rbp, rpp, bits, w, nb, n_senders, lay);                                 \
+  }                                                                                                                 \
+  hy_status exchange_partition_rows_##SUFFIX(const SidePlan& p, int32_t value_type, const hy_join_params* params,   \
+                                             int32_t keep_nulls, const std::vector<uint32_t>& w, void* out_records, \
+                                             uint64_t* bucket_counts, void* workspace, size_t workspace_bytes,      \
+                                             hipStream_t s) {                                                       \
+    return exchange_partition_for_hashed<H, uint32_t>(p, value_type, params, keep_nulls, w, out_records,            \
+                                                      bucket_counts, workspace, workspace_bytes, s);                \
+  }                                                                                                                 \
+  hy_status exchange_join_rows_##SUFFIX(const void* build_records, const void* probe_records, const RecvPlan& rbp, \
+                                        const RecvPlan& rpp, uint32_t n_senders, uint32_t n_buckets,               \
+                                        const std::vector<uint32_t>& w, const hy_join_params* params,              \
+                                        hy_row_id* out_build, hy_row_id* out_probe, uint64_t out_capacity,         \
+                                        uint64_t* partition_begin, uint32_t* partition_counts,                     \
+                                        hy_join_result* result, void* workspace, size_t workspace_bytes,           \
+                                        hipStream_t s, const Layouts& lay) {                                       \
+    return exchange_join_for_hashed<H, uint32_t>(build_records, probe_records, rbp, rpp, n_senders, n_buckets, w,   \
+                                                 params, out_build, out_probe, out_capacity, partition_begin,      \
+                                                 partition_counts, result, workspace, workspace_bytes, s, lay);    \
   }
 
 }  // namespace hyj

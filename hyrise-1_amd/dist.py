@@ -1,11 +1,14 @@
 """Distributed JoinHash across the GPUs of one node: one process per GPU, chunks sharded by
 contiguous chunk ranges, one exchange step.
 
-    step 1  every rank, each side: hy_join_exchange_partition -> 16-byte exchange records {key, global RowID}
-            grouped by first-digit bucket of the GLOBAL radix partition, plus per-bucket counts
+    step 1  every rank, each side: hy_scan_join_exchange_partition -> 8-byte exchange records {int32 key, global row
+            index} (data-table sides, optionally with the side's TableScan fused in) or hy_join_exchange_partition ->
+            16-byte records {key, global RowID} (reference sides), grouped by first-digit bucket of the GLOBAL radix
+            partition, plus per-bucket counts
     counts  all_gather of the per-bucket counts (B <= 256 integers per rank and side)
     records all_to_all_single over RCCL/xGMI: rank r receives, sender by sender, every record of the buckets it owns
-    step 2  every rank: hy_join_exchange_join -> remaining radix passes + LDS build/probe of its partitions
+    step 2  every rank: hy_join_exchange_join_rows / hy_join_exchange_join -> remaining radix passes + LDS
+            build/probe of its partitions
 
 The ranks' outputs, concatenated in rank order, are the single-node JoinHash output: one output chunk per radix
 partition in ascending order, probe rows in (chunk, offset) order, build matches in build order (join_hash.cpp).
@@ -45,9 +48,9 @@ def exchange_plan(all_counts, rank, world):
     return send, recv, recv_matrix
 
 
-def exchange_records(dist, records, bucket_counts, rank, world, device=None):
-    """Routes this rank's exchange records (int64 tensor, 2 words per record, grouped by bucket) to their owners.
-    Returns (received records, recv_matrix[s][j])."""
+def exchange_records(dist, records, bucket_counts, rank, world, device=None, record_bytes=RECORD_BYTES):
+    """Routes this rank's exchange records (int64 tensor of record_bytes / 8 words per record, grouped by bucket) to
+    their owners. Returns (received records, recv_matrix[s][j])."""
     import torch
 
     counts = torch.as_tensor(np.asarray(bucket_counts, dtype=np.int64), device=device)
@@ -55,16 +58,20 @@ def exchange_records(dist, records, bucket_counts, rank, world, device=None):
     dist.all_gather(gathered, counts)
     all_counts = np.stack([g.cpu().numpy() for g in gathered])
     send, recv, recv_matrix = exchange_plan(all_counts, rank, world)
-    words = RECORD_BYTES // 8
+    words = record_bytes // 8
     out = torch.empty(sum(recv) * words, dtype=torch.int64, device=records.device)
     dist.all_to_all_single(out, records[: sum(send) * words], [r * words for r in recv], [s * words for s in send])
     return out, recv_matrix
 
 
 class ExchangeJoin:
-    """The two C-ABI steps of the distributed JoinHash on device buffers owned by torch tensors."""
+    """The two C-ABI steps of the distributed JoinHash on device buffers owned by torch tensors.
 
-    def __init__(self, capi, radix_bits, world, hashed_type, mode=0, seed=17):
+    rows=True: row-index records (hy_scan_join_exchange_partition / hy_join_exchange_join_rows) for data-table
+    sides, with build_layout / probe_layout the global tables' chunk sizes (global chunk-id order)."""
+
+    def __init__(self, capi, radix_bits, world, hashed_type, mode=0, seed=17, rows=False, build_layout=None,
+                 probe_layout=None):
         self.capi = capi
         self.lib = capi.lib
         self.world = world
@@ -72,6 +79,10 @@ class ExchangeJoin:
         self.bits = radix_bits
         self.first_bits = bucket_bits(capi, radix_bits, world)
         self.n_buckets = 1 << self.first_bits
+        self.rows = rows
+        self.record_bytes = int(capi.lib.hy_join_exchange_row_record_bytes(hashed_type)) if rows else RECORD_BYTES
+        self.layouts = [np.ascontiguousarray(np.asarray(x if x is not None else [], dtype=np.uint32))
+                        for x in (build_layout, probe_layout)]
         self._ws = {}
 
     def _workspace(self, key, nbytes, device):
@@ -83,21 +94,37 @@ class ExchangeJoin:
             self._ws[key] = t
         return t
 
-    def partition(self, side, n_rows, keep_nulls, stream, device, key="side"):
-        """Step 1 for one side: returns (records int64 tensor [2 * n_rows], bucket counts np.uint64[B])."""
+    def partition(self, side, n_rows, keep_nulls, stream, device, key="side", filt=None, row_base=0):
+        """Step 1 for one side: returns (records int64 tensor, bucket counts np.uint64[B]). Row-index mode: the
+        records of the rows taking part (all rows, or the fused scan's matches with filt), payload row_base + row."""
         import torch
 
         lib, capi = self.lib, self.capi
         wsb = ctypes.c_size_t(0)
-        capi.check(lib.hy_join_exchange_partition_workspace_size(ctypes.byref(side), ctypes.byref(self.params),
-                                                                  self.world, ctypes.byref(wsb)), "exchange ws")
+        fp = ctypes.byref(filt) if filt is not None else None
+        if self.rows:
+            capi.check(lib.hy_scan_join_exchange_partition_workspace_size(ctypes.byref(side), fp,
+                                                                           ctypes.byref(self.params), self.world,
+                                                                           ctypes.byref(wsb)), "exchange ws")
+        else:
+            capi.check(lib.hy_join_exchange_partition_workspace_size(ctypes.byref(side), ctypes.byref(self.params),
+                                                                      self.world, ctypes.byref(wsb)), "exchange ws")
         ws = self._workspace(key, wsb.value, device)
-        recs = self._workspace(key + ".recs", max(1, n_rows) * RECORD_BYTES, device)
+        rb = self.record_bytes
+        recs = self._workspace(key + ".recs", max(1, n_rows) * rb + 64, device)
         counts = (ctypes.c_uint64 * self.n_buckets)()
-        capi.check(lib.hy_join_exchange_partition(ctypes.byref(side), ctypes.byref(self.params), int(keep_nulls),
-                                                  self.world, recs.data_ptr(), counts, ws.data_ptr(), ws.numel(),
-                                                  stream), "hy_join_exchange_partition")
-        return recs[: n_rows * RECORD_BYTES].view(torch.int64), np.frombuffer(counts, dtype=np.uint64).copy()
+        if self.rows:
+            capi.check(lib.hy_scan_join_exchange_partition(ctypes.byref(side), fp, ctypes.byref(self.params),
+                                                           int(keep_nulls), self.world, row_base, recs.data_ptr(),
+                                                           counts, ws.data_ptr(), ws.numel(), stream),
+                       "hy_scan_join_exchange_partition")
+        else:
+            capi.check(lib.hy_join_exchange_partition(ctypes.byref(side), ctypes.byref(self.params), int(keep_nulls),
+                                                      self.world, recs.data_ptr(), counts, ws.data_ptr(), ws.numel(),
+                                                      stream), "hy_join_exchange_partition")
+        counts = np.frombuffer(counts, dtype=np.uint64).copy()
+        n_out = int(counts.sum())
+        return recs[: n_out * rb].view(torch.int64), counts
 
     def join(self, build_recs, build_matrix, probe_recs, probe_matrix, rank, stream, device, capacity=None):
         """Step 2: returns (out_build, out_probe, part_begin, part_count, total_pairs) - RowID tensors (int32 pairs)
@@ -112,8 +139,14 @@ class ExchangeJoin:
         bcp = bc.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
         pcp = pc.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
         wsb = ctypes.c_size_t(0)
-        capi.check(lib.hy_join_exchange_join_workspace_size(bcp, pcp, self.world, nb, ctypes.byref(self.params),
-                                                             ctypes.byref(wsb)), "exchange join ws")
+        bl, pl = self.layouts
+        if self.rows:
+            capi.check(lib.hy_join_exchange_join_rows_workspace_size(bcp, pcp, self.world, nb, ctypes.byref(self.params),
+                                                                      bl.ctypes.data, bl.size, pl.ctypes.data, pl.size,
+                                                                      ctypes.byref(wsb)), "exchange join ws")
+        else:
+            capi.check(lib.hy_join_exchange_join_workspace_size(bcp, pcp, self.world, nb, ctypes.byref(self.params),
+                                                                 ctypes.byref(wsb)), "exchange join ws")
         ws = self._workspace("join", wsb.value, device)
         n_parts = nb << (self.bits - self.first_bits)
         if capacity is None:
@@ -123,8 +156,17 @@ class ExchangeJoin:
         part_begin = torch.empty(max(1, n_parts), dtype=torch.int64, device=device)
         part_count = torch.empty(max(1, n_parts), dtype=torch.int32, device=device)
         res = capi.JoinResult()
-        capi.check(lib.hy_join_exchange_join(build_recs.data_ptr(), bcp, probe_recs.data_ptr(), pcp, self.world,
-                                             first, nb, ctypes.byref(self.params), out_b.data_ptr(), out_p.data_ptr(),
-                                             capacity, part_begin.data_ptr(), part_count.data_ptr(), ctypes.byref(res),
-                                             ws.data_ptr(), ws.numel(), stream), "hy_join_exchange_join")
+        if self.rows:
+            capi.check(lib.hy_join_exchange_join_rows(build_recs.data_ptr(), bcp, probe_recs.data_ptr(), pcp,
+                                                      self.world, first, nb, ctypes.byref(self.params), bl.ctypes.data,
+                                                      bl.size, pl.ctypes.data, pl.size, out_b.data_ptr(),
+                                                      out_p.data_ptr(), capacity, part_begin.data_ptr(),
+                                                      part_count.data_ptr(), ctypes.byref(res), ws.data_ptr(),
+                                                      ws.numel(), stream), "hy_join_exchange_join_rows")
+        else:
+            capi.check(lib.hy_join_exchange_join(build_recs.data_ptr(), bcp, probe_recs.data_ptr(), pcp, self.world,
+                                                 first, nb, ctypes.byref(self.params), out_b.data_ptr(),
+                                                 out_p.data_ptr(), capacity, part_begin.data_ptr(),
+                                                 part_count.data_ptr(), ctypes.byref(res), ws.data_ptr(), ws.numel(),
+                                                 stream), "hy_join_exchange_join")
         return out_b, out_p, part_begin[:n_parts], part_count[:n_parts], res.total_pairs

@@ -238,3 +238,42 @@ def q1_columns(sf, device, seed=SEED):
     return {"l_returnflag": c["l_returnflag"], "l_linestatus": c["l_linestatus"],
             "l_quantity": c["l_quantity"].to(torch.float32), "l_extendedprice": price, "l_discount": disc,
             "l_tax": tax, "l_shipdate": c["l_shipdate"]}
+
+
+def shard_torch(sf, chunk, rank, world, device, seed=SEED):
+    """Rank `rank`'s chunk-aligned shard of the SF `sf` orders / lineitem tables (contiguous global chunk ranges, rank
+    r holding chunks [r * C / N, (r + 1) * C / N) of each table), generated from global row indexes so that the
+    union of the shards is exactly orders_torch / lineitem_torch of the whole table for any N. Returns a dict with
+    o_orderkey, l_orderkey, l_quantity (this shard), o_row_base / l_row_base (global index of the shard's first
+    row), o_chunk_lo / l_chunk_lo (its first global chunk id) and o_layout / l_layout (every global chunk's size)."""
+    import torch
+
+    n_ord = n_orders(sf)
+    i = torch.arange(1, n_ord + 1, dtype=torch.int64, device=device)
+    lines = _umod_torch(_splitmix64_torch(i ^ seed), 7) + 1
+    del i
+    ends = torch.cumsum(lines, 0)  # global lineitem row after each order's last line
+    del lines
+    n_li = int(ends[-1]) if n_ord else 0
+
+    def chunks(n):
+        return (n + chunk - 1) // chunk
+
+    def layout(n):
+        return [min(chunk, n - c * chunk) for c in range(chunks(n))]
+
+    out = {"o_layout": layout(n_ord), "l_layout": layout(n_li)}
+    for t, n in (("o", n_ord), ("l", n_li)):
+        c_lo, c_hi = rank * chunks(n) // world, (rank + 1) * chunks(n) // world
+        out[t + "_chunk_lo"], out[t + "_chunk_hi"] = c_lo, c_hi
+        out[t + "_row_base"], out[t + "_row_end"] = c_lo * chunk, min(c_hi * chunk, n)
+    o = torch.arange(out["o_row_base"] + 1, out["o_row_end"] + 1, dtype=torch.int64, device=device)
+    out["o_orderkey"] = (((o >> 3) << 5) + (o & 7)).to(torch.int32)
+    del o
+    r = torch.arange(out["l_row_base"], out["l_row_end"], dtype=torch.int64, device=device)
+    oi = torch.searchsorted(ends, r, right=True) + 1  # 1-based order index of each line
+    del ends
+    out["l_orderkey"] = (((oi >> 3) << 5) + (oi & 7)).to(torch.int32)
+    del oi
+    out["l_quantity"] = (_umod_torch(_splitmix64_torch(r ^ (seed ^ 0x5155)), 50) + 1).to(torch.int32)
+    return out

@@ -344,6 +344,38 @@ hy_status hy_join_exchange_join(const void* build_records, const uint64_t* build
 uint32_t hy_join_exchange_bucket_bits(uint32_t radix_bits, uint32_t n_ranks);
 
 /*
+ * Row-index exchange records (the default for data-table sides): {key (hashed type), uint32 global row index}, 8 bytes
+ * for 4-byte hashed types (16 for 8-byte ones, alignment) - half the xGMI bytes of the RowID records above. The global
+ * row index is row_base + the row's index in the side (chunks in order); every rank passes the index of its shard's
+ * first row in the global table, so indexes are unique across ranks (< 2^32, < 2^31 with a fused scan).
+ * hy_scan_join_exchange_partition is step 1 for a data-table side with an optional fused TableScan (filter as for
+ * hy_scan_join_hash; its out_offsets / out_chunk_begin receive the scan output of this shard).
+ * hy_join_exchange_join_rows is step 2; the global tables' chunk layouts (chunk sizes in global chunk-id order) turn
+ * the received row indexes into the output RowIDs {global chunk id, offset}.
+ */
+uint32_t hy_join_exchange_row_record_bytes(int32_t hashed_type);
+hy_status hy_scan_join_exchange_partition_workspace_size(const hy_join_side* side, const hy_join_filter* filter,
+                                                         const hy_join_params* params, uint32_t n_ranks,
+                                                         size_t* bytes);
+hy_status hy_scan_join_exchange_partition(const hy_join_side* side, const hy_join_filter* filter,
+                                          const hy_join_params* params, int32_t keep_nulls, uint32_t n_ranks,
+                                          uint64_t row_base, void* out_records, uint64_t* bucket_counts,
+                                          void* workspace, size_t workspace_bytes, hy_stream_t stream);
+hy_status hy_join_exchange_join_rows_workspace_size(const uint64_t* build_counts, const uint64_t* probe_counts,
+                                                    uint32_t n_senders, uint32_t n_buckets,
+                                                    const hy_join_params* params, const uint32_t* build_chunk_sizes,
+                                                    uint32_t n_build_chunks, const uint32_t* probe_chunk_sizes,
+                                                    uint32_t n_probe_chunks, size_t* bytes);
+hy_status hy_join_exchange_join_rows(const void* build_records, const uint64_t* build_counts,
+                                     const void* probe_records, const uint64_t* probe_counts, uint32_t n_senders,
+                                     uint32_t first_bucket, uint32_t n_buckets, const hy_join_params* params,
+                                     const uint32_t* build_chunk_sizes, uint32_t n_build_chunks,
+                                     const uint32_t* probe_chunk_sizes, uint32_t n_probe_chunks,
+                                     hy_row_id* out_build, hy_row_id* out_probe, uint64_t out_capacity,
+                                     uint64_t* partition_begin, uint32_t* partition_counts, hy_join_result* result,
+                                     void* workspace, size_t workspace_bytes, hy_stream_t stream);
+
+/*
  * out[i] = rows[i] is NULL ? rows[i] : chunk_pos_lists[rows[i].chunk_id][rows[i].chunk_offset]
  * (reference write_output_columns, join_hash.cpp:584-592). chunk_pos_lists: DEVICE array of device PosList pointers.
  */

@@ -7,6 +7,8 @@ import ctypes
 import numpy as np
 import pytest
 
+import device_tables as dt
+
 pytestmark = pytest.mark.gpu
 
 REC = 16
@@ -137,6 +139,142 @@ def test_exchange_join_equals_single_gpu(hy, world, mode):
     params = capi.JoinParams(getattr(capi, "HY_JOIN_" + mode), capi.HY_TYPE_INT32, bits, 17)
     want = single_gpu(hy, build, probe, params, okey.size, lkey.size)
     got = distributed(hy, build, probe, params, world, dist)
+    assert len(got) == len(want) == 1 << bits
+    for p, ((wb, wp), (gb, gp)) in enumerate(zip(want, got)):
+        assert np.array_equal(wp, gp), f"partition {p}: probe RowIDs differ"
+        if mode == "INNER":
+            assert np.array_equal(wb, gb), f"partition {p}: build RowIDs differ"
+
+
+def scan_filter(capi, col, chunk_ids, cond, value):
+    """hy_join_filter over the chunks chunk_ids of a DeviceColumn, with its own scan-output buffers."""
+    full = col.scan_chunks(cond, value)
+    arr = (capi.ScanChunk * max(1, len(chunk_ids)))()
+    for k, c in enumerate(chunk_ids):
+        arr[k] = full[c]
+    rows = sum(col.chunk_size(c) for c in chunk_ids)
+    out = capi.DeviceArray(np.zeros(max(16, rows), np.uint32))
+    begin = capi.DeviceArray(np.zeros(len(chunk_ids) + 1, np.uint64))
+    const = col.constant(value)
+    f = capi.JoinFilter(arr, dt.HY_TYPES[col.values.dtype], const.ctypes.data, out.ptr.value, begin.ptr.value)
+    f._keep = (arr, out, begin, const)
+    return f, out, begin
+
+
+def distributed_rows(hy, build, probe, qty, params, world, dist, cond, value):
+    """Row-index exchange (8-byte records) with the probe side's TableScan fused into step 1."""
+    capi, L = hy.capi, hy.capi.lib
+    T = 1 << dist.bucket_bits(capi, params.radix_bits, world)
+    rec_bytes = L.hy_join_exchange_row_record_bytes(params.hashed_type)
+    shard = lambda n: [list(range(r * n // world, (r + 1) * n // world)) for r in range(world)]
+    layouts = {name: np.array([tab.dev[c].host.size for c in range(tab.n_chunks)], np.uint32)
+               for name, tab in (("build", build), ("probe", probe))}
+    recs, counts, scans = {}, {}, []
+    for name, tab in (("build", build), ("probe", probe)):
+        for r, cids in enumerate(shard(tab.n_chunks)):
+            side = tab.side(cids)
+            row_base = sum(tab.dev[c].host.size for c in range(cids[0])) if cids else 0
+            rows = sum(tab.dev[c].host.size for c in cids)
+            filt = None
+            if name == "probe":
+                filt, out, begin = scan_filter(capi, qty, cids, cond, value)
+            fp = ctypes.byref(filt) if filt is not None else None
+            wsb = ctypes.c_size_t()
+            capi.check(L.hy_scan_join_exchange_partition_workspace_size(ctypes.byref(side), fp, ctypes.byref(params),
+                                                                        world, ctypes.byref(wsb)), "ws")
+            ws = capi.DeviceArray(np.zeros(max(16, wsb.value), np.uint8))
+            buf = capi.DeviceArray(np.zeros(max(1, rows) * rec_bytes + 64, np.uint8))
+            cnt = (ctypes.c_uint64 * T)()
+            capi.check(L.hy_scan_join_exchange_partition(ctypes.byref(side), fp, ctypes.byref(params), 0, world,
+                                                         row_base, buf.ptr, cnt, ws.ptr, wsb.value, None), "partition")
+            counts[name, r] = np.frombuffer(cnt, np.uint64).astype(np.int64)
+            n_out = int(counts[name, r].sum())
+            recs[name, r] = buf.fetch()[: n_out * rec_bytes].reshape(-1, rec_bytes)
+            if name == "build":
+                assert n_out == rows
+            else:
+                off, beg = out.fetch(), begin.fetch().astype(np.int64)
+                scans += [off[beg[k]:beg[k + 1]] for k in range(len(cids))]
+                assert n_out == beg[-1]
+    parts = []
+    for d in range(world):
+        lo, hi = dist.owned_buckets(T, d, world)
+        recv, mats = {}, {}
+        for name in ("build", "probe"):
+            chunks, mat = [], []
+            for s in range(world):
+                c = counts[name, s]
+                begin = c[:lo].sum()
+                chunks.append(recs[name, s][begin:begin + c[lo:hi].sum()])
+                mat.append(c[lo:hi])
+            cat = np.concatenate(chunks) if chunks else np.zeros((0, rec_bytes), np.uint8)
+            recv[name] = capi.DeviceArray(np.ascontiguousarray(cat) if cat.size else np.zeros(16, np.uint8))
+            mats[name] = np.ascontiguousarray(np.array(mat, dtype=np.uint64))
+        bc = mats["build"].ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+        pc = mats["probe"].ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+        bl, pl = layouts["build"], layouts["probe"]
+        wsb = ctypes.c_size_t()
+        capi.check(L.hy_join_exchange_join_rows_workspace_size(bc, pc, world, hi - lo, ctypes.byref(params),
+                                                               bl.ctypes.data, bl.size, pl.ctypes.data, pl.size,
+                                                               ctypes.byref(wsb)), "ws")
+        ws = capi.DeviceArray(np.zeros(wsb.value, np.uint8))
+        cap = int(mats["build"].sum()) * 2 + int(mats["probe"].sum()) + 16
+        ob, op = capi.DeviceArray(np.zeros(cap * 2, np.uint32)), capi.DeviceArray(np.zeros(cap * 2, np.uint32))
+        n_parts = (hi - lo) << (params.radix_bits - dist.bucket_bits(capi, params.radix_bits, world))
+        pbeg = capi.DeviceArray(np.zeros(max(1, n_parts), np.uint64))
+        pcnt = capi.DeviceArray(np.zeros(max(1, n_parts), np.uint32))
+        res = capi.JoinResult()
+        capi.check(L.hy_join_exchange_join_rows(recv["build"].ptr, bc, recv["probe"].ptr, pc, world, lo, hi - lo,
+                                                ctypes.byref(params), bl.ctypes.data, bl.size, pl.ctypes.data, pl.size,
+                                                ob.ptr, op.ptr, cap, pbeg.ptr, pcnt.ptr, ctypes.byref(res), ws.ptr,
+                                                wsb.value, None), "exchange join rows")
+        ob, op = ob.fetch().reshape(-1, 2), op.fetch().reshape(-1, 2)
+        pb, pn = pbeg.fetch()[:n_parts].astype(np.int64), pcnt.fetch()[:n_parts].astype(np.int64)
+        parts += [(ob[b:b + c], op[b:b + c]) for b, c in zip(pb, pn)]
+    return parts, scans
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("mode", ["INNER", "SEMI"])
+def test_row_exchange_with_fused_scan_equals_single_gpu(hy, world, mode):
+    """8-byte row-index records, the probe side's TableScan (l_quantity < 24 on a dictionary column) fused into the
+    exchange partition: the ranks' outputs equal the single-GPU hy_scan_join_hash, and the shards' scan outputs
+    concatenated equal its scan output."""
+    import importlib
+
+    dist = importlib.import_module("hyrise-1_amd.dist")
+    capi, L = hy.capi, hy.capi.lib
+    rng = np.random.default_rng(world * 11 + len(mode))
+    okey, lkey = tables(50_000, rng, dup=(mode == "INNER"))
+    chunk = 9_000
+    qty = rng.integers(1, 51, lkey.size).astype(np.float32)
+    build, probe = Sides(hy, okey, 7_000), Sides(hy, lkey, chunk)
+    qcol = dt.DeviceColumn(capi, qty, None, chunk, "Dictionary")
+    bits = max(L.hy_join_radix_bits(okey.size, 4), 9)
+    params = capi.JoinParams(getattr(capi, "HY_JOIN_" + mode), capi.HY_TYPE_INT32, bits, 17)
+    # single GPU: hy_scan_join_hash with the same filter
+    bs, ps = build.side(range(build.n_chunks)), probe.side(range(probe.n_chunks))
+    filt, out, begin = scan_filter(capi, qcol, list(range(probe.n_chunks)), "LessThan", 24.0)
+    wsb = ctypes.c_size_t()
+    capi.check(L.hy_scan_join_hash_workspace_size(ctypes.byref(bs), None, ctypes.byref(ps), ctypes.byref(filt),
+                                                  ctypes.byref(params), ctypes.byref(wsb)), "ws")
+    ws = capi.DeviceArray(np.zeros(wsb.value, np.uint8))
+    cap = okey.size * 2 + lkey.size + 16
+    ob, op = capi.DeviceArray(np.zeros(cap * 2, np.uint32)), capi.DeviceArray(np.zeros(cap * 2, np.uint32))
+    pbeg = capi.DeviceArray(np.zeros(1 << bits, np.uint64))
+    pcnt = capi.DeviceArray(np.zeros(1 << bits, np.uint32))
+    res = capi.JoinResult()
+    capi.check(L.hy_scan_join_hash(ctypes.byref(bs), None, ctypes.byref(ps), ctypes.byref(filt), ctypes.byref(params),
+                                   ob.ptr, op.ptr, cap, pbeg.ptr, pcnt.ptr, ctypes.byref(res), ws.ptr, wsb.value, None),
+               "hy_scan_join_hash")
+    ob, op = ob.fetch().reshape(-1, 2), op.fetch().reshape(-1, 2)
+    want = [(ob[b:b + c], op[b:b + c]) for b, c in zip(pbeg.fetch().astype(np.int64), pcnt.fetch().astype(np.int64))]
+    off, beg = out.fetch(), begin.fetch().astype(np.int64)
+    want_scan = [off[beg[k]:beg[k + 1]] for k in range(probe.n_chunks)]
+    got, got_scan = distributed_rows(hy, build, probe, qcol, params, world, dist, "LessThan", 24.0)
+    assert len(got_scan) == len(want_scan)
+    for k, (a, b) in enumerate(zip(got_scan, want_scan)):
+        assert np.array_equal(a, b), f"scan output chunk {k}"
     assert len(got) == len(want) == 1 << bits
     for p, ((wb, wp), (gb, gp)) in enumerate(zip(want, got)):
         assert np.array_equal(wp, gp), f"partition {p}: probe RowIDs differ"
