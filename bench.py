@@ -46,6 +46,12 @@ def parse():
                    help="join: the headline TableScan+JoinHash (BASELINE.json metric); q1: BASELINE config 4, "
                         "TPC-H 1 TableScan -> Projection -> Aggregate (8 aggregates) on one GPU; q3: BASELINE config 5 at N=1, "
                         "TPC-H 3 Scan -> Join -> Join -> Projection -> Aggregate (bench_tpch.py)")
+    p.add_argument("--q1-materialize", action="store_true",
+                   help="q1: materialise the two arithmetic expressions with hy_projection before the aggregate "
+                        "(the reference's plan shape) instead of evaluating them inside it (A/B)")
+    p.add_argument("--through-operators", action="store_true",
+                   help="time the headline step through TableScan / JoinHash::_on_execute (the drop-in operators, "
+                        "bench_ops.py) instead of the C-ABI")
     p.add_argument("--unfused", action="store_true",
                    help="run TableScan and JoinHash as two C-ABI calls (hy_table_scan_row_ids, hy_join_hash) instead "
                         "of the fused hy_scan_join_hash (A/B of the fusion; single GPU)")
@@ -58,6 +64,10 @@ def parse():
 
 def main():
     args = parse()
+    if args.through_operators:
+        import bench_ops
+
+        return bench_ops.main_operators(args)
     if args.workload in ("q1", "q3"):
         import bench_tpch
 

@@ -1,0 +1,77 @@
+"""The headline step through the drop-in operators (`python bench.py --through-operators`): what a Hyrise process
+linking the library executes - TableScan::_on_execute then JoinHash::_on_execute (csrc/host/operators.cpp, the
+reference constructors and output tables), not the C-ABI directly.
+
+One step (SF --sf, chunks of --chunk rows, l_quantity dictionary-encoded, keys unencoded - the same database as the
+C-ABI bench):
+    scan = TableScan(lineitem, l_quantity < 24)        -> reference table, one lazy PosList per input chunk
+    join = JoinHash(orders, scan, Inner, o_orderkey = l_orderkey)  -> reference table, one chunk per radix partition
+and a synchronize of the operator stream (the outputs are produced asynchronously; their PosLists are copied to the
+host only when host code reads them). The column chunks' HBM mirrors are created by the warmup steps, as they would be
+by the first query over the tables. Rows/s counts the base rows consumed, as the C-ABI bench does.
+"""
+import importlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+
+
+def main_operators(args):
+    import numpy as np
+    import torch
+
+    sys.path.insert(0, ROOT)
+    hy = importlib.import_module("hyrise-1_amd")
+    synth = importlib.import_module("hyrise-1_amd.synth")
+    torch.cuda.set_device(0)
+    chunk = args.chunk
+    okey, lines = synth.orders_numpy(args.sf)
+    lkey, qty = synth.lineitem_numpy(okey, lines)
+    del lines
+    t0 = time.perf_counter()
+    orders = hy.Table.from_arrays([("o_orderkey", hy.DataType.Int, False)], [okey], [], chunk)
+    lineitem = hy.Table.from_arrays([("l_orderkey", hy.DataType.Int, False), ("l_quantity", hy.DataType.Float, False)],
+                                    [lkey, qty.astype(np.float32)], [], chunk)
+    n_ord, n_li = len(okey), len(lkey)
+    del okey, lkey, qty
+    hy.encode_columns(lineitem, [1], hy.EncodingType.Dictionary)
+    setup_s = time.perf_counter() - t0
+    print(f"operators: tables built and encoded in {setup_s:.1f} s", file=sys.stderr, flush=True)
+    o, l = hy.TableWrapper(orders), hy.TableWrapper(lineitem)
+    o.execute()
+    l.execute()
+
+    def step():
+        scan = hy.TableScan(l, 1, hy.PredicateCondition.LessThan, 24)
+        scan.execute()
+        join = hy.JoinHash(o, scan, hy.JoinMode.Inner, (0, 0), hy.PredicateCondition.Equals)
+        join.execute()
+        hy.synchronize()
+        return scan, join
+
+    for _ in range(args.warmup):
+        step()
+    times = []
+    for _ in range(args.steps):
+        t0 = time.perf_counter()
+        scan, join = step()
+        times.append(time.perf_counter() - t0)
+    step_s = sum(times) / len(times)
+    out = join.get_output()
+    matches = scan.get_output().row_count()
+    line = {
+        "metric": "rows/sec TableScan+JoinHash through the operators (TableScan/JoinHash::_on_execute), "
+                  "TPC-H lineitem⋈orders",
+        "value": round((n_li + n_ord) / step_s, 1), "unit": "rows/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 3),
+        "ms_per_step_runs": [round(t * 1e3, 3) for t in times], "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "int32", "data": "synthetic (seeded counter-based TPC-H-shaped columns)",
+        "config": {"workload": "TableScan(l_quantity<24) -> JoinHash(orders, scan) via _on_execute", "sf": args.sf,
+                   "lineitem_rows": n_li, "orders_rows": n_ord, "chunk_size": chunk, "scan_matches": matches,
+                   "join_pairs": out.row_count(), "join_output_chunks": out.chunk_count(),
+                   "setup_s": round(setup_s, 1), "parallelism": "single GPU"},
+    }
+    print(json.dumps(line))

@@ -318,15 +318,21 @@ def main_q3(args):
             capi.check(L.hy_aggregate_layout(ctypes.byref(ain), ctypes.byref(agg_params), ctypes.byref(lay)), "layout")
             state["layout"] = lay
         words = state["layout"].words
-        aws = workspace(("agg", k, pairs2), lambda b: L.hy_aggregate_workspace_size(ctypes.byref(ain),
-                                                                                     ctypes.byref(agg_params), b))
+        aws = workspace(("agg", k, pairs2, agg_params.group_bound), lambda b: L.hy_aggregate_workspace_size(
+            ctypes.byref(ain), ctypes.byref(agg_params), b))
         if state.get("agg_cap", 0) < pairs2 + 1:
             state["agg_cap"] = pairs2 + 1
             state["agg_out"] = torch.empty((pairs2 + 1) * words, dtype=torch.int64, device=dev)
         ng = ctypes.c_uint64(0)
-        capi.check(L.hy_aggregate(ctypes.byref(ain), ctypes.byref(agg_params), state["agg_out"].data_ptr(),
-                                  state["agg_cap"], ctypes.byref(ng), aws.data_ptr(), aws.numel(), stream),
-                   "hy_aggregate")
+        while True:
+            st = L.hy_aggregate(ctypes.byref(ain), ctypes.byref(agg_params), state["agg_out"].data_ptr(),
+                                state["agg_cap"], ctypes.byref(ng), aws.data_ptr(), aws.numel(), stream)
+            if st != capi.HY_ERR_GROUP_BOUND:
+                break
+            agg_params.group_bound = ng.value  # more groups than the table was sized for: grow it
+            aws = workspace(("agg", k, pairs2, ng.value), lambda b: L.hy_aggregate_workspace_size(
+                ctypes.byref(ain), ctypes.byref(agg_params), b))
+        capi.check(st, "hy_aggregate")
         return {"customer_matches": c_match, "join1_pairs": int(pairs1), "join2_pairs": int(pairs2),
                 "groups": int(ng.value)}
 
@@ -477,14 +483,15 @@ def main_q1(args):
 
     One step:
         TableScan(lineitem, l_shipdate <= 1998-09-02)          hy_table_scan_row_ids (dictionary u16 dates)
-        Projection(l_extendedprice * (1 - l_discount), l_extendedprice * (1 - l_discount) * (1 + l_tax))
-                                                                hy_projection x 2 (float, as the reference computes)
+        Projection(l_extendedprice * (1 - l_discount), l_extendedprice * (1 - l_discount) * (1 + l_tax)) fused into
         Aggregate(GROUP BY l_returnflag, l_linestatus; SUM(l_quantity), SUM(l_extendedprice), SUM(disc_price),
                   SUM(charge), AVG(l_quantity), AVG(l_extendedprice), AVG(l_discount), COUNT(*))   hy_aggregate
-    The reference's Projection materialises all seven SELECT-list inputs into a data table (projection.cpp:52-85);
-    here only the two computed columns are materialised and the aggregate reads the five plain columns through the
-    scan's PosLists (same values, one materialisation less). Float SUM/AVG are exact (rounded once); they are checked
-    against float64 torch sums of the same float32 values (relative 1e-9), counts and SUM(l_quantity) exactly."""
+    The reference's Projection materialises all seven SELECT-list inputs into a data table (projection.cpp:52-85)
+    that the Aggregate then reads; here the two arithmetic expressions are expression columns of hy_aggregate,
+    evaluated (in float, as the reference computes them) in the aggregation kernel, and every column is read through
+    the scan's PosLists once - nothing is materialised. --q1-materialize runs the two hy_projection launches first
+    instead (A/B). Float SUM/AVG are exact (rounded once); they are checked against float64 torch sums of the same
+    float32 values (relative 1e-9), counts and SUM(l_quantity) exactly."""
     import numpy as np
     import torch
 
@@ -565,13 +572,18 @@ def main_q1(args):
     charge = disc_price + [one, N(capi.HY_EXPR_COLUMN, F32, 0, 2, 0), N(capi.HY_EXPR_ADD, F32, F32, 0, 0),
                            N(capi.HY_EXPR_MUL, F32, F32, 0, 0)]
     programs = [(N * len(p))(*p) for p in (disc_price, charge)]
-    proj_out = torch.empty(2, n + 64, dtype=torch.float32, device=dev)
-    agg_cols = (capi.AggColumn * 7)()
+    proj_out = torch.empty(2, n + 64, dtype=torch.float32, device=dev) if args.q1_materialize else None
+    agg_cols = (capi.AggColumn * 8)()
     ref_cols = {0: (I32, rf.desc, 3), 1: (I32, ls.desc, 2), 2: (F32, qty.desc, 0), 3: (F32, price_c, 0),
-                6: (F32, dsc.desc, 0)}
+                6: (F32, dsc.desc, 0), 7: (F32, tx.desc, 0)}
     for j, (vt, chs, dom) in ref_cols.items():
         agg_cols[j].value_type, agg_cols[j].pos_group, agg_cols[j].chunks = vt, 0, chs
         agg_cols[j].n_chunks, agg_cols[j].domain = n_chunks, dom
+    # expression columns 4 and 5 over the aggregate input's columns 3 (price), 6 (discount), 7 (tax)
+    col = lambda j: N(capi.HY_EXPR_COLUMN, F32, 0, j, 0)
+    agg_dp = [col(3), one, col(6), N(capi.HY_EXPR_SUB, F32, F32, 0, 0), N(capi.HY_EXPR_MUL, F32, F32, 0, 0)]
+    agg_ch = agg_dp + [one, col(7), N(capi.HY_EXPR_ADD, F32, F32, 0, 0), N(capi.HY_EXPR_MUL, F32, F32, 0, 0)]
+    agg_programs = [(N * len(p))(*p) for p in (agg_dp, agg_ch)]
     groupby = (ctypes.c_int32 * 2)(0, 1)
     defs = (capi.AggDef * len(Q1_AGGS))(*[capi.AggDef(getattr(capi, "HY_AGG_" + f), col) for f, col in Q1_AGGS])
     params = capi.AggParams(groupby, 2, defs, len(Q1_AGGS), 64)
@@ -588,26 +600,32 @@ def main_q1(args):
         pls_np = (rows_t.data_ptr() + 8 * chunk * nz.astype(np.uint64)).astype(np.uint64)
         sizes = sizes_np.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
         pls = pls_np.ctypes.data_as(ctypes.POINTER(ctypes.c_void_p))
-        pin = capi.AggInput(k, sizes, pls, 1, proj_cols, 3)
-        if "pws" not in state:
-            b = ctypes.c_size_t(0)
-            capi.check(L.hy_projection_workspace_size(ctypes.byref(pin), ctypes.byref(b)), "proj ws")
-            state["pws"] = torch.empty(max(16, b.value), dtype=torch.uint8, device=dev)
-        pws = state["pws"]
-        for j, prog in enumerate(programs):
-            capi.check(L.hy_projection(ctypes.byref(pin), prog, len(prog), proj_out[j].data_ptr(), None,
-                                       pws.data_ptr(), pws.numel(), stream), "hy_projection")
-        rb = np.concatenate([[0], np.cumsum(sizes_np.astype(np.int64))])[:-1].astype(np.uint64)
         keep = []
-        for j in (4, 5):  # the projection's columns: data chunks aligned with the scan output's chunks
-            chs = np.zeros(max(1, k), cc_dtype)
-            chs["data"][:k] = proj_out[j - 4].data_ptr() + 4 * rb
-            chs["size"][:k] = sizes_np
-            chs["kind"] = capi.HY_COL_VALUE
-            keep.append(chs)
-            agg_cols[j].value_type, agg_cols[j].pos_group, agg_cols[j].n_chunks = F32, -1, k
-            agg_cols[j].chunks = chs.ctypes.data_as(ctypes.POINTER(capi.ColumnChunk))
-        ain = capi.AggInput(k, sizes, pls, 1, agg_cols, 7)
+        if args.q1_materialize:
+            pin = capi.AggInput(k, sizes, pls, 1, proj_cols, 3)
+            if "pws" not in state:
+                b = ctypes.c_size_t(0)
+                capi.check(L.hy_projection_workspace_size(ctypes.byref(pin), ctypes.byref(b)), "proj ws")
+                state["pws"] = torch.empty(max(16, b.value), dtype=torch.uint8, device=dev)
+            pws = state["pws"]
+            for j, prog in enumerate(programs):
+                capi.check(L.hy_projection(ctypes.byref(pin), prog, len(prog), proj_out[j].data_ptr(), None,
+                                           pws.data_ptr(), pws.numel(), stream), "hy_projection")
+            rb = np.concatenate([[0], np.cumsum(sizes_np.astype(np.int64))])[:-1].astype(np.uint64)
+            for j in (4, 5):  # the projection's columns: data chunks aligned with the scan output's chunks
+                chs = np.zeros(max(1, k), cc_dtype)
+                chs["data"][:k] = proj_out[j - 4].data_ptr() + 4 * rb
+                chs["size"][:k] = sizes_np
+                chs["kind"] = capi.HY_COL_VALUE
+                keep.append(chs)
+                agg_cols[j].value_type, agg_cols[j].pos_group, agg_cols[j].n_chunks = F32, -1, k
+                agg_cols[j].chunks = chs.ctypes.data_as(ctypes.POINTER(capi.ColumnChunk))
+                agg_cols[j].program, agg_cols[j].n_nodes = None, 0
+        else:
+            for j, prog in ((4, agg_programs[0]), (5, agg_programs[1])):
+                agg_cols[j].value_type, agg_cols[j].pos_group, agg_cols[j].n_chunks = F32, -1, 0
+                agg_cols[j].program, agg_cols[j].n_nodes = prog, len(prog)
+        ain = capi.AggInput(k, sizes, pls, 1, agg_cols, 8)
         if "ws" not in state:
             b = ctypes.c_size_t(0)
             capi.check(L.hy_aggregate_workspace_size(ctypes.byref(ain), ctypes.byref(params), ctypes.byref(b)), "ws")
@@ -668,11 +686,13 @@ def main_q1(args):
     kernels = kernel_stats(L)
     K = args.steps
     step_s = elapsed / K
-    # algorithmic bytes: scan 2 B/row (u16 date vids) + 8 B/match RowID; projection per match RowID
-    # 8 B + price 4 B + discount 1 B (+ tax 1 B) + result 4 B; aggregate per match RowID 8 B + flags, quantity,
-    # discount vids 1 B each + price 4 B + the two projected columns 4 B each
-    alg = {"scan_dict": n * 2 + n_match * 8, "projection": n_match * (17 + 18), "agg_dense_span": n_match * 24}
-    e2e = sum(alg.values())
+    # algorithmic bytes, independent of the path: scan 2 B/row (u16 date vids) + 8 B/match RowID;
+    # aggregate (with its projection) per match: RowID 8 B + returnflag, linestatus, quantity, discount, tax vids 1 B
+    # each + price 4 B = 17 B. Per kernel: the bytes that kernel must move on the path taken.
+    e2e_parts = {"scan": n * 2 + n_match * 8, "aggregate": n_match * 17}
+    alg = {"scan_dict": n * 2 + n_match * 8, "projection": n_match * (17 + 18), "agg_dense_span": n_match * 24,
+           "agg_dense_fused": n_match * 17}
+    e2e = sum(e2e_parts.values())
     for k, v in kernels.items():
         v["ms_per_launch"] = v["ms_total"] / max(v["launches"], 1)
         if k in alg:
@@ -682,7 +702,7 @@ def main_q1(args):
     dom = max(kernels, key=lambda k: kernels[k]["ms_total"])
     roofline = {"bound": "hbm", "scope": "end-to-end step (algorithmic bytes of SURVEY 8(d) per operator)",
                 "achieved": round(e2e / step_s / 1e9, 1), "peak": round(peak, 1), "unit": "GB/s",
-                "frac": round(e2e / step_s / 1e9 / peak, 4), "alg_bytes_per_step": e2e, "alg_bytes": alg,
+                "frac": round(e2e / step_s / 1e9 / peak, 4), "alg_bytes_per_step": e2e, "alg_bytes": e2e_parts,
                 "traffic": None, "peak_source": "measured in this run (hy_stream_bandwidth_probe, best of read / copy)",
                 "dominant_kernel": dom, "dominant_ms_per_step": round(kernels[dom]["ms_total"] / K, 4)}
     # the reference Aggregate runs ~1e6 rows/s per core: a tenth of --cpu-sf keeps the sample near 10-30 s

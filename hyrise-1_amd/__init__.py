@@ -63,6 +63,8 @@ LogicError = _host.LogicError
 load_table = _host.load_table
 encode_chunks = _host.encode_chunks
 encode_all_chunks = _host.encode_all_chunks
+encode_columns = _host.encode_columns
+synchronize = _host.synchronize
 join_hashed_type = _host.join_hashed_type
 join_radix_bits = _host.join_radix_bits
 device_count = _host.device_count

@@ -15,7 +15,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "hyrise_amd.h")
 
 lib = ctypes.CDLL(LIB_PATH)
 
-HY_OK, HY_ERR_CAPACITY = 0, 6
+HY_OK, HY_ERR_CAPACITY, HY_ERR_GROUP_BOUND = 0, 6, 8
 HY_TYPE_INT32, HY_TYPE_INT64, HY_TYPE_FLOAT, HY_TYPE_DOUBLE = 1, 2, 3, 4
 HY_COL_VALUE, HY_COL_DICT = 0, 1
 HY_OP_EQ, HY_OP_NE, HY_OP_LT, HY_OP_LE, HY_OP_GT, HY_OP_GE, HY_OP_ALL, HY_OP_NONE = range(8)
@@ -69,9 +69,15 @@ class JoinResult(ctypes.Structure):
     _fields_ = [("total_pairs", ctypes.c_uint64), ("capacity_required", ctypes.c_uint64)]
 
 
+class ExprNode(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("type", ctypes.c_int32), ("calc_type", ctypes.c_int32),
+                ("column", ctypes.c_int32), ("value", ctypes.c_uint64)]
+
+
 class AggColumn(ctypes.Structure):
     _fields_ = [("value_type", ctypes.c_int32), ("pos_group", ctypes.c_int32), ("chunks", ctypes.POINTER(ColumnChunk)),
-                ("n_chunks", ctypes.c_uint32), ("domain", ctypes.c_uint32)]
+                ("n_chunks", ctypes.c_uint32), ("domain", ctypes.c_uint32), ("program", ctypes.POINTER(ExprNode)),
+                ("n_nodes", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
 class AggInput(ctypes.Structure):
@@ -95,11 +101,6 @@ class AggLayout(ctypes.Structure):
                 ("agg_word", ctypes.c_uint32 * HY_AGG_MAX_AGGREGATES),
                 ("agg_emin", ctypes.c_int32 * HY_AGG_MAX_AGGREGATES),
                 ("agg_limbs", ctypes.c_uint32 * HY_AGG_MAX_AGGREGATES)]
-
-
-class ExprNode(ctypes.Structure):
-    _fields_ = [("kind", ctypes.c_int32), ("type", ctypes.c_int32), ("calc_type", ctypes.c_int32),
-                ("column", ctypes.c_int32), ("value", ctypes.c_uint64)]
 
 
 _sigs = {

@@ -10,6 +10,7 @@
 #include "capi_common.hpp"
 #include "../kernels/aggregate.hip"
 #include "../kernels/projection.hip"
+#include "../kernels/aggregate_fused.hip"
 
 using namespace hyc;
 
@@ -21,6 +22,54 @@ uint64_t next_pow2(uint64_t v) {
   return p;
 }
 
+// Validates a postfix program over the plain (non-expression) columns of `in` and copies it into *out.
+hy_status validate_program(const hy_agg_input* in, const hy_expr_node* program, uint32_t n_nodes,
+                           hyk::ExprProgram* out, int* max_depth = nullptr) {
+  if (!program || n_nodes == 0 || n_nodes > HY_EXPR_MAX_NODES) return fail(HY_ERR_INVALID_ARGUMENT, "program size");
+  *out = hyk::ExprProgram{};
+  int depth = 0, deepest = 0;
+  for (uint32_t i = 0; i < n_nodes; ++i) {
+    const hy_expr_node& nd = program[i];
+    out->nodes[i] = nd;
+    const bool typed = nd.type >= HY_TYPE_INT32 && nd.type <= HY_TYPE_DOUBLE;
+    switch (nd.kind) {
+      case HY_EXPR_COLUMN:
+        if (nd.column < 0 || nd.column >= static_cast<int32_t>(in->n_columns))
+          return fail(HY_ERR_INVALID_ARGUMENT, "expression column");
+        if (in->columns[nd.column].n_nodes) return fail(HY_ERR_INVALID_ARGUMENT, "expression over an expression");
+        if (nd.type != in->columns[nd.column].value_type) return fail(HY_ERR_INVALID_ARGUMENT, "column node type");
+        ++depth;
+        break;
+      case HY_EXPR_VALUE:
+        if (!typed && nd.type != 0) return fail(HY_ERR_INVALID_ARGUMENT, "literal type");
+        ++depth;
+        break;
+      case HY_EXPR_ADD:
+      case HY_EXPR_SUB:
+      case HY_EXPR_MUL:
+      case HY_EXPR_DIV:
+      case HY_EXPR_MOD:
+        if (depth < 2) return fail(HY_ERR_INVALID_ARGUMENT, "expression stack underflow");
+        if (!typed || nd.calc_type < HY_TYPE_INT32 || nd.calc_type > HY_TYPE_DOUBLE)
+          return fail(HY_ERR_INVALID_ARGUMENT, "arithmetic node types");
+        --depth;
+        break;
+      default:
+        return fail(HY_ERR_INVALID_ARGUMENT, "expression node kind");
+    }
+    if (depth > HY_EXPR_MAX_DEPTH) return fail(HY_ERR_UNSUPPORTED, "expression deeper than HY_EXPR_MAX_DEPTH");
+    deepest = std::max(deepest, depth);
+  }
+  if (depth != 1) return fail(HY_ERR_INVALID_ARGUMENT, "program does not leave one value");
+  out->n_nodes = n_nodes;
+  out->out_type = program[n_nodes - 1].type;
+  if (out->out_type == 0) return fail(HY_ERR_UNSUPPORTED, "an all-NULL expression has no column type");
+  if (max_depth) *max_depth = deepest;
+  return HY_OK;
+}
+
+inline bool four_bytes(int32_t t) { return t == HY_TYPE_INT32 || t == HY_TYPE_FLOAT; }
+
 struct AggPlan {
   hyk::AggDesc d{};
   std::vector<int32_t> word_op;
@@ -29,8 +78,124 @@ struct AggPlan {
   uint64_t n_tiles = 0;
   uint32_t dense_groups = 0;  // > 0: dense path
   uint64_t cap = 0, dcap = 0;
+  uint64_t max_groups = 0;
   bool distinct = false;
+  std::vector<uint32_t> expr_cols;         // input columns that are expressions
+  std::vector<hyk::ExprProgram> exprs;     // their programs (same order)
+  bool fused = false;                      // agg_dense_fused (expressions evaluated in the kernel)
+  bool materialize = false;                // else: expression columns materialised first (projection kernel)
+  hyk::FusedPlan fp{};
+  std::vector<hyk::FqOp> fused_nodes;      // fp.progs on the host
 };
+
+// agg_dense_fused applies: the dense path; at most one PosList group; int32 group-by columns; every aggregate over a
+// 4-byte plain column or a 4-byte expression of 4-byte plain columns (stack <= FQ_DEPTH); <= FQ_SLOTS slots; no
+// COUNT(DISTINCT). HY_AGG_FUSED=0 disables it (tests compare the paths).
+void plan_fused(const hy_agg_input* in, const hy_agg_params* p, AggPlan* plan) {
+  if (const char* e = std::getenv("HY_AGG_FUSED"))
+    if (std::atoi(e) == 0) return;
+  if (!plan->dense_groups || plan->distinct || in->n_pos_groups > 1 || p->n_groupby > hyk::FQ_MAX_GB) return;
+  for (uint32_t j = 0; j < p->n_groupby; ++j) {
+    const auto& c = in->columns[p->groupby[j]];
+    if (c.n_nodes || c.value_type != HY_TYPE_INT32) return;
+  }
+  auto& fp = plan->fp;
+  fp = hyk::FusedPlan{};
+  std::vector<int32_t> slot_of(in->n_columns, -1);
+  auto plain_slot = [&](uint32_t col) -> int32_t {
+    if (slot_of[col] >= 0) return slot_of[col];
+    if (fp.n_slots >= hyk::FQ_SLOTS || !four_bytes(in->columns[col].value_type)) return -1;
+    const int32_t sl = fp.n_slots++;
+    fp.slot_col[sl] = static_cast<int32_t>(col);
+    fp.slot_prog[sl] = -1;
+    fp.slot_type[sl] = in->columns[col].value_type;
+    return slot_of[col] = sl;
+  };
+  std::vector<int32_t> expr_slot(in->n_columns, -1);
+  for (uint32_t a = 0; a < p->n_aggregates; ++a) {
+    const auto& def = p->aggregates[a];
+    fp.fn_slot[a] = -1;
+    if (def.column < 0) continue;
+    const auto& c = in->columns[def.column];
+    if (!four_bytes(c.value_type)) return;
+    if (!c.n_nodes) {
+      if ((fp.fn_slot[a] = plain_slot(def.column)) < 0) return;
+      continue;
+    }
+    if (expr_slot[def.column] < 0) {
+      int depth = 0;
+      hyk::ExprProgram prog;
+      if (validate_program(in, c.program, c.n_nodes, &prog, &depth) != HY_OK || depth > hyk::FQ_DEPTH) return;
+      // compile to FqOps: every value 4 bytes; the stack's types are tracked here, so the kernel only converts the
+      // operands flagged per op
+      std::vector<hyk::FqOp> nodes;
+      std::vector<int32_t> types;  // 0 = NULL literal
+      for (uint32_t i = 0; i < c.n_nodes; ++i) {
+        const hy_expr_node& nd = c.program[i];
+        hyk::FqOp op{nd.kind, 0, 0, 0};
+        if (nd.kind == HY_EXPR_COLUMN) {
+          if (!four_bytes(nd.type) || (op.arg = plain_slot(static_cast<uint32_t>(nd.column))) < 0) return;
+          types.push_back(nd.type);
+        } else if (nd.kind == HY_EXPR_VALUE) {
+          if (nd.type != 0 && !four_bytes(nd.type)) return;
+          op.arg = nd.type == 0 ? 1 : 0;
+          op.lit = static_cast<uint32_t>(nd.value);
+          types.push_back(nd.type);
+        } else {
+          if (!four_bytes(nd.calc_type) || nd.type != nd.calc_type) return;
+          const int32_t tb = types.back();
+          types.pop_back();
+          const int32_t ta = types.back();
+          types.pop_back();
+          op.calc = nd.calc_type;
+          if (nd.calc_type == HY_TYPE_FLOAT) op.arg = (ta == HY_TYPE_INT32 ? 1 : 0) | (tb == HY_TYPE_INT32 ? 2 : 0);
+          else if (ta == HY_TYPE_FLOAT || tb == HY_TYPE_FLOAT) return;  // float operand of an int32 op
+          types.push_back(nd.type);
+        }
+        nodes.push_back(op);
+      }
+      if (fp.n_slots >= hyk::FQ_SLOTS) return;
+      const int32_t sl = fp.n_slots++;
+      fp.slot_col[sl] = -1;
+      fp.slot_prog[sl] = static_cast<int32_t>(plan->fused_nodes.size());
+      fp.slot_nodes[sl] = static_cast<int32_t>(nodes.size());
+      fp.slot_type[sl] = c.value_type;
+      plan->fused_nodes.insert(plan->fused_nodes.end(), nodes.begin(), nodes.end());
+      expr_slot[def.column] = sl;
+    }
+    fp.fn_slot[a] = expr_slot[def.column];
+  }
+  for (uint32_t a = 0; a < p->n_aggregates; ++a)  // float sums use the float limb layout only
+    if (plan->d.fns[a].limbs && plan->d.fns[a].limbs != hyk::FLOAT_LIMBS) return;
+  plan->fused = true;
+}
+
+// Record bytes a hash table may take without a caller-given bound (at load 1/2: 2 slots per expected group).
+constexpr uint64_t DEFAULT_RECORD_BUDGET = 2ull << 30;
+
+// Groups the hash table is sized for: the caller's bound, else the product of the group-by columns' distinct-value
+// bounds when every group-by column is dictionary-encoded (sum of its chunks' dictionary sizes + NULL), else as many
+// groups as DEFAULT_RECORD_BUDGET holds (at least 2^20); never more than the rows.
+uint64_t group_bound_of(const hy_agg_input* in, const hy_agg_params* p, uint64_t rows, uint32_t words) {
+  if (p->group_bound) return std::min<uint64_t>(p->group_bound, std::max<uint64_t>(rows, 1));
+  uint64_t bound = 1;
+  bool dict = p->n_groupby > 0;
+  for (uint32_t j = 0; j < p->n_groupby && dict; ++j) {
+    const auto& c = in->columns[p->groupby[j]];
+    uint64_t distinct = 1;  // NULL
+    for (uint32_t k = 0; k < c.n_chunks && dict; ++k) {
+      if (c.chunks[k].kind != HY_COL_DICT) dict = false;
+      distinct += c.chunks[k].dictionary_size;
+    }
+    bound = std::min<uint64_t>(bound * std::min<uint64_t>(distinct, rows + 1), rows + 1);
+  }
+  if (p->n_groupby == 0) return 1;
+  const uint64_t per_group = 2ull * 8 * std::max(words, 1u);
+  const char* knob = std::getenv("HY_AGG_RECORD_BUDGET");  // test knob: a small table, to exercise the retry
+  const uint64_t budget = knob ? std::max<uint64_t>(1, std::strtoull(knob, nullptr, 10) / per_group)
+                               : std::max<uint64_t>(1ull << 20, DEFAULT_RECORD_BUDGET / per_group);
+  return std::min<uint64_t>(std::max<uint64_t>(rows, 1), dict ? bound : budget);
+}
 
 hy_status make_plan(const hy_agg_input* in, const hy_agg_params* p, AggPlan* plan) {
   if (!in || !p || !plan) return fail(HY_ERR_INVALID_ARGUMENT, "null argument");
@@ -49,6 +214,22 @@ hy_status make_plan(const hy_agg_input* in, const hy_agg_params* p, AggPlan* pla
   for (uint32_t j = 0; j < in->n_columns; ++j) {
     const auto& c = in->columns[j];
     if (c.value_type < HY_TYPE_INT32 || c.value_type > HY_TYPE_DOUBLE) return fail(HY_ERR_UNSUPPORTED, "column type");
+    if (c.n_nodes) {  // expression column: evaluated in the kernel (fused) or materialised first
+      hyk::ExprProgram prog;
+      const hy_status st = validate_program(in, c.program, c.n_nodes, &prog);
+      if (st != HY_OK) return st;
+      if (prog.out_type != c.value_type) return fail(HY_ERR_INVALID_ARGUMENT, "expression column type");
+      for (uint32_t g = 0; g < p->n_groupby; ++g)
+        if (p->groupby[g] == static_cast<int32_t>(j)) return fail(HY_ERR_UNSUPPORTED, "GROUP BY an expression column");
+      plan->expr_cols.push_back(j);
+      plan->exprs.push_back(prog);
+      d.cols[j].type = c.value_type;
+      d.cols[j].pos_group = -1;
+      d.cols[j].ukind = HY_COL_VALUE;  // as materialised (the fused kernel reads slots instead)
+      d.cols[j].uwidth = 0;
+      d.cols[j].unulls = 1;
+      continue;
+    }
     if (c.pos_group >= static_cast<int32_t>(in->n_pos_groups)) return fail(HY_ERR_INVALID_ARGUMENT, "pos_group");
     if (c.pos_group < 0 && c.n_chunks != in->n_chunks)
       return fail(HY_ERR_INVALID_ARGUMENT, "data column must have one chunk per input chunk");
@@ -161,8 +342,10 @@ hy_status make_plan(const hy_agg_input* in, const hy_agg_params* p, AggPlan* pla
     plan->dense_groups = static_cast<uint32_t>(groups);
   }
   L.dense = dense ? 1 : 0;
-  const uint64_t bound = p->group_bound ? std::min<uint64_t>(p->group_bound, plan->rows) : plan->rows;
-  plan->cap = next_pow2(std::max<uint64_t>(64, 2 * bound));
+  plan_fused(in, p, plan);
+  plan->materialize = !plan->fused && !plan->expr_cols.empty();
+  plan->cap = next_pow2(std::max<uint64_t>(64, 2 * group_bound_of(in, p, plan->rows, d.words)));
+  plan->max_groups = plan->cap / 4 * 3;  // load factor limit: past it the insert reports HY_ERR_GROUP_BOUND
   plan->dcap = plan->distinct ? next_pow2(std::max<uint64_t>(64, 2 * plan->rows * p->n_aggregates)) : 0;
   return HY_OK;
 }
@@ -177,6 +360,10 @@ struct AggWs {
   hy_column_chunk* chunks[hyk::AGG_MAX_COLUMNS];
   int32_t* word_op;
   uint32_t* misc;  // [0] error, [2..3] n_out (u64)
+  unsigned long long* inserted;  // hash path: hyk::INSERT_SHARDS insert counters
+  hyk::FqOp* fused_nodes;        // agg_dense_fused: its expression ops
+  void* mat_values[hyk::AGG_MAX_COLUMNS];    // materialised expression columns
+  uint8_t* mat_nulls[hyk::AGG_MAX_COLUMNS];
   uint32_t* state;
   unsigned long long* records;
   uint32_t* dstate;
@@ -189,10 +376,18 @@ void carve(Carver& cv, const hy_agg_input* in, const AggPlan& plan, AggWs* w) {
   w->tile_begin = cv.take<uint64_t>(in->n_chunks + 1);
   w->tile_owner = cv.take<uint32_t>(std::max<uint64_t>(1, plan.n_tiles));
   w->pos_lists = cv.take<const hy_row_id*>(std::max<uint64_t>(1, uint64_t(in->n_pos_groups) * in->n_chunks));
-  for (uint32_t j = 0; j < in->n_columns; ++j)
-    w->chunks[j] = cv.take<hy_column_chunk>(std::max<uint32_t>(1, in->columns[j].n_chunks));
+  for (uint32_t j = 0; j < in->n_columns; ++j)  // expression columns: one materialised chunk per input chunk
+    w->chunks[j] = cv.take<hy_column_chunk>(
+        std::max<uint32_t>(1, in->columns[j].n_nodes ? in->n_chunks : in->columns[j].n_chunks));
   w->word_op = cv.take<int32_t>(plan.word_op.size());
+  w->fused_nodes = cv.take<hyk::FqOp>(std::max<size_t>(1, plan.fused_nodes.size()));
+  for (uint32_t e = 0; e < plan.expr_cols.size(); ++e) {
+    const uint32_t j = plan.expr_cols[e];
+    w->mat_values[j] = plan.materialize ? cv.take<uint64_t>(std::max<uint64_t>(2, plan.rows)) : nullptr;
+    w->mat_nulls[j] = plan.materialize ? cv.take<uint8_t>(std::max<uint64_t>(16, plan.rows)) : nullptr;
+  }
   w->misc = cv.take<uint32_t>(64);
+  w->inserted = cv.take<unsigned long long>(hyk::INSERT_SHARDS);
   if (plan.dense_groups) {
     w->state = nullptr;
     w->records = cv.take<unsigned long long>(uint64_t(plan.dense_groups) * plan.d.words);
@@ -259,13 +454,13 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
   if (n_pl) HY_HIP(hipMemcpyAsync(w.pos_lists, input->pos_lists, sizeof(void*) * n_pl, hipMemcpyHostToDevice, s));
   for (uint32_t j = 0; j < input->n_columns; ++j) {
     const auto& c = input->columns[j];
-    for (uint32_t k = 0; k < c.n_chunks; ++k) {
+    for (uint32_t k = 0; k < (c.n_nodes ? 0u : c.n_chunks); ++k) {
       const auto& ch = c.chunks[k];
       if (ch.size && !ch.data) return fail(HY_ERR_INVALID_ARGUMENT, "column chunk without data");
       if (ch.kind == HY_COL_DICT && ch.vid_width != 1 && ch.vid_width != 2 && ch.vid_width != 4)
         return fail(HY_ERR_INVALID_ARGUMENT, "vid width");
     }
-    if (c.n_chunks)
+    if (c.n_chunks && !c.n_nodes)
       HY_HIP(hipMemcpyAsync(w.chunks[j], c.chunks, sizeof(hy_column_chunk) * c.n_chunks, hipMemcpyHostToDevice, s));
     d.cols[j].chunks = w.chunks[j];
   }
@@ -285,8 +480,53 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
   d.error = w.misc;
   auto* n_out = reinterpret_cast<unsigned long long*>(w.misc + 2);
   auto* out = reinterpret_cast<unsigned long long*>(out_records);
+  // expression columns outside the fused kernel: materialised (projection kernel over the same input), then read as
+  // data columns with NULL flags
+  std::vector<std::vector<hy_column_chunk>> mat_chunks(plan.expr_cols.size());
+  for (uint32_t e = 0; e < plan.expr_cols.size() && plan.materialize && plan.rows; ++e) {
+    const uint32_t j = plan.expr_cols[e];
+    const uint32_t items = hyk::flat_items(plan.rows);
+    const uint64_t tile_rows = uint64_t(hyk::AGG_THREADS) * items;
+    hipLaunchKernelGGL(hyk::projection_kernel, dim3(static_cast<uint32_t>((plan.rows + tile_rows - 1) / tile_rows)),
+                       dim3(hyk::AGG_THREADS), 0, s, d, plan.exprs[e], w.mat_values[j], w.mat_nulls[j], plan.rows,
+                       items);
+    HY_HIP(hipGetLastError());
+    const int bytes = (plan.exprs[e].out_type == HY_TYPE_INT64 || plan.exprs[e].out_type == HY_TYPE_DOUBLE) ? 8 : 4;
+    auto& chs = mat_chunks[e];
+    chs.resize(input->n_chunks);
+    for (uint32_t c = 0; c < input->n_chunks; ++c) {
+      chs[c] = hy_column_chunk{};
+      chs[c].data = static_cast<char*>(w.mat_values[j]) + bytes * row_begin[c];
+      chs[c].nulls = w.mat_nulls[j] + row_begin[c];
+      chs[c].size = input->chunk_sizes[c];
+      chs[c].kind = HY_COL_VALUE;
+    }
+    HY_HIP(hipMemcpyAsync(w.chunks[j], chs.data(), sizeof(hy_column_chunk) * chs.size(), hipMemcpyHostToDevice, s));
+  }
 
-  if (plan.dense_groups) {
+  if (plan.fused && plan.dense_groups) {
+    const uint64_t nw = uint64_t(plan.dense_groups) * d.words;
+    hipLaunchKernelGGL(hyk::agg_init_records, dim3(grid_for(nw, 256)), dim3(256), 0, s, w.records,
+                       uint64_t(plan.dense_groups), d.words, w.word_op);
+    HY_HIP(hipGetLastError());
+    if (!plan.fused_nodes.empty())
+      HY_HIP(hipMemcpyAsync(w.fused_nodes, plan.fused_nodes.data(), sizeof(hyk::FqOp) * plan.fused_nodes.size(),
+                            hipMemcpyHostToDevice, s));
+    hyk::FusedPlan fp = plan.fp;
+    fp.progs = w.fused_nodes;
+    if (plan.n_tiles) {
+      const size_t lds = sizeof(unsigned long long) * plan.dense_groups * d.words;
+      const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(plan.n_tiles, 256 * 16));
+      KTimer t("agg_dense_fused", s, plan.rows);
+      hipLaunchKernelGGL(hyk::agg_dense_fused, dim3(grid), dim3(hyk::AGG_THREADS), lds, s, d, fp, plan.dense_groups,
+                         w.records);
+      t.done();
+      HY_HIP(hipGetLastError());
+    }
+    hipLaunchKernelGGL(hyk::agg_dense_compact, dim3((plan.dense_groups + 63) / 64), dim3(64), 0, s, d,
+                       plan.dense_groups, w.records, out, out_capacity, n_out);
+    HY_HIP(hipGetLastError());
+  } else if (plan.dense_groups) {
     const uint64_t nw = uint64_t(plan.dense_groups) * d.words;
     hipLaunchKernelGGL(hyk::agg_init_records, dim3(grid_for(nw, 256)), dim3(256), 0, s, w.records,
                        uint64_t(plan.dense_groups), d.words, w.word_op);
@@ -316,8 +556,11 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
                        plan.dense_groups, w.records, out, out_capacity, n_out);
     HY_HIP(hipGetLastError());
   } else {
-    hyk::AggTable t{w.state, w.records, plan.cap, w.dstate, w.dkeys, plan.dcap};
+    hyk::AggTable t{w.state, w.records, plan.cap, w.dstate, w.dkeys, plan.dcap, w.inserted,
+                    // per counter: its share of the load limit, with slack for the uneven split of slots
+                    (plan.max_groups + hyk::INSERT_SHARDS - 1) / hyk::INSERT_SHARDS * 5 / 4 + 4};
     HY_HIP(hipMemsetAsync(w.state, 0, 4 * plan.cap, s));
+    HY_HIP(hipMemsetAsync(w.inserted, 0, 8 * hyk::INSERT_SHARDS, s));
     if (plan.dcap) HY_HIP(hipMemsetAsync(w.dstate, 0, 4 * plan.dcap, s));
     if (plan.rows) {
       KTimer kt("agg_hash_runs", s, plan.rows);
@@ -339,7 +582,11 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
   std::memcpy(&n, misc + 2, 8);
   *n_groups = n;
   if (misc[0] & 2u) return fail(HY_ERR_INVALID_ARGUMENT, "dense group-by code outside its domain");
-  if (misc[0] & 1u) return fail(HY_ERR_KERNEL, "aggregate hash table full (group_bound too small?)");
+  if (misc[0] & 4u) {  // more groups than the table was sized for: suggest a bound 4x larger
+    *n_groups = std::min<uint64_t>(std::max<uint64_t>(plan.rows, 1), std::max<uint64_t>(64, plan.cap / 2) * 4);
+    return fail(HY_ERR_GROUP_BOUND, "more groups than group_bound; retry with *n_groups");
+  }
+  if (misc[0] & 1u) return fail(HY_ERR_KERNEL, "aggregate hash table probe did not terminate");
   if (n > out_capacity) return fail(HY_ERR_CAPACITY, "more groups than out_capacity");
   return HY_OK;
 }

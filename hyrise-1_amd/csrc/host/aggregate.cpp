@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <array>
 #include <map>
+#include <memory>
 #include <numeric>
 #include <unordered_map>
 
@@ -324,24 +325,34 @@ std::shared_ptr<const Table> Aggregate::_on_execute() {
   _used_dense_path = layout.dense != 0;
   size_t ws_bytes = 0;
   hy_check(hy_aggregate_workspace_size(&hin, &prm, &ws_bytes), "hy_aggregate_workspace_size");
-  DeviceBuffer ws(ws_bytes);
+  auto ws = std::make_unique<DeviceBuffer>(ws_bytes, s);
   uint64_t capacity = std::max<uint64_t>(1, std::min<uint64_t>(in->row_count(), layout.dense ? 64 : 1u << 16));
   uint64_t n_groups = 0;
   std::vector<uint64_t> rec;
-  for (int attempt = 0; attempt < 2; ++attempt) {
-    DeviceBuffer out(capacity * layout.words * 8);
+  // retries: a larger output capacity (HY_ERR_CAPACITY) or a larger hash table (HY_ERR_GROUP_BOUND: the device
+  // table is sized for params.group_bound groups, derived from the inputs when 0, and grows 4x per retry)
+  bool done = false;
+  for (int attempt = 0; attempt < 16 && !done; ++attempt) {
+    DeviceBuffer out(capacity * layout.words * 8, s);
     const hy_status st =
-        hy_aggregate(&hin, &prm, out.as<uint64_t>(), capacity, &n_groups, ws.get(), ws_bytes, s);
-    if (st == HY_ERR_CAPACITY && attempt == 0) {
+        hy_aggregate(&hin, &prm, out.as<uint64_t>(), capacity, &n_groups, ws->get(), ws_bytes, s);
+    if (st == HY_ERR_CAPACITY) {
       capacity = n_groups;
+      continue;
+    }
+    if (st == HY_ERR_GROUP_BOUND) {
+      prm.group_bound = n_groups;
+      hy_check(hy_aggregate_workspace_size(&hin, &prm, &ws_bytes), "hy_aggregate_workspace_size");
+      ws = std::make_unique<DeviceBuffer>(ws_bytes, s);
       continue;
     }
     hy_check(st, "hy_aggregate");
     rec.resize(n_groups * layout.words);
     hy_check(hy_memcpy_dtoh(rec.data(), out.get(), rec.size() * 8, s), "dtoh");
     hy_check(hy_stream_synchronize(s), "sync");
-    break;
+    done = true;
   }
+  if (!done) Fail("hyrise-amd: hy_aggregate did not converge on an output capacity / group bound");
 
   // ---- reference row order
   const uint32_t W = layout.words, NG = prm.n_groupby;

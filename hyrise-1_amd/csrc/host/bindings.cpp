@@ -260,6 +260,9 @@ PYBIND11_MODULE(_hyrise_host, m) {
   m.def("load_table", &load_table, py::arg("file_name"), py::arg("chunk_size") = CHUNK_MAX_SIZE);
   m.def("encode_chunks", &ChunkEncoder::encode_chunks);
   m.def("encode_all_chunks", &ChunkEncoder::encode_all_chunks);
+  m.def("encode_columns", &ChunkEncoder::encode_columns);
+  m.def("synchronize", []() { hy_check(hy_stream_synchronize(operator_stream()), "hy_stream_synchronize"); },
+        "Waits for the calling thread's operator stream (operator outputs are produced asynchronously).");
   m.def("join_hashed_type", &join_hashed_type);
   m.def("join_radix_bits", [](uint64_t rows, uint32_t key_bytes) { return hy_join_radix_bits(rows, key_bytes); });
   m.def("device_count", []() {

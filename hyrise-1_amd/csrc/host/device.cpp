@@ -20,6 +20,52 @@ std::shared_ptr<DeviceBuffer> upload(const void* host, size_t bytes, hy_stream_t
 }
 }  // namespace
 
+namespace {
+// size classes: powers of two from 4 KiB; at most TEMP_CACHE_BYTES kept per thread
+constexpr size_t TEMP_CACHE_BYTES = size_t(8) << 30;
+struct TempCache {
+  std::vector<std::pair<size_t, void*>> free_blocks;  // (block bytes, ptr)
+  size_t cached = 0;
+  ~TempCache() {
+    for (auto& b : free_blocks) hy_free(b.second);
+  }
+};
+TempCache& temp_cache() {
+  thread_local TempCache c;
+  return c;
+}
+}  // namespace
+
+void* temp_block_acquire(size_t bytes, size_t* block_bytes) {
+  size_t b = 4096;
+  while (b < bytes) b <<= 1;
+  auto& c = temp_cache();
+  for (size_t i = 0; i < c.free_blocks.size(); ++i) {
+    if (c.free_blocks[i].first == b) {
+      void* p = c.free_blocks[i].second;
+      c.free_blocks[i] = c.free_blocks.back();
+      c.free_blocks.pop_back();
+      c.cached -= b;
+      *block_bytes = b;
+      return p;
+    }
+  }
+  void* p = nullptr;
+  hy_check(hy_malloc(&p, b), "hy_malloc");
+  *block_bytes = b;
+  return p;
+}
+
+void temp_block_release(void* ptr, size_t block_bytes) {
+  auto& c = temp_cache();
+  if (c.cached + block_bytes > TEMP_CACHE_BYTES) {
+    hy_free(ptr);
+    return;
+  }
+  c.free_blocks.emplace_back(block_bytes, ptr);
+  c.cached += block_bytes;
+}
+
 void require_device() {
   int n = 0;
   hy_get_device_count(&n);
@@ -106,13 +152,19 @@ std::shared_ptr<DevicePosList> device_pos_list(const PosList& pos_list) {
   return d;
 }
 
+namespace {
+// the lazy PosLists' host copy (PosList::host): stream-ordered after the kernels that wrote the RowIDs
+void fetch_pos_list(const PosList& pos_list, RowID* dst) {
+  const auto d = pos_list.device_mirror();
+  if (!d) throw std::logic_error("lazy PosList without a device mirror");
+  hy_stream_t s = operator_stream();
+  hy_check(hy_memcpy_dtoh(dst, d->ptr(), pos_list.size() * sizeof(RowID), s), "hy_memcpy_dtoh");
+  hy_check(hy_stream_synchronize(s), "hy_stream_synchronize");
+}
+}  // namespace
+
 std::shared_ptr<PosList> pos_list_from_device(std::shared_ptr<DeviceBuffer> rows, uint64_t offset, uint64_t n) {
-  auto pl = std::make_shared<PosList>(n);
-  if (n) {
-    hy_stream_t s = operator_stream();
-    hy_check(hy_memcpy_dtoh(pl->data(), rows->as<RowID>() + offset, n * sizeof(RowID), s), "hy_memcpy_dtoh");
-    hy_check(hy_stream_synchronize(s), "hy_stream_synchronize");
-  }
+  auto pl = PosList::lazy(n, &fetch_pos_list);  // host RowIDs copied on first host access
   // device mirror: a view into the shared buffer (kept alive by the shared_ptr)
   auto d = std::make_shared<DevicePosList>();
   d->size = n;

@@ -19,15 +19,27 @@ inline void hy_check(hy_status st, const char* what) {
   if (st != HY_OK) Fail(std::string(what) + " failed (" + std::to_string(st) + "): " + hy_last_error_message());
 }
 
-// Owning device allocation.
+// Per-thread cache of device blocks for operator-scoped temporaries (workspaces, offsets, counts). A block goes
+// back to the cache of the thread that releases it and is only handed out again on that thread, whose operator work
+// is ordered on that thread's stream - so a reused block is never written before the kernels that read it finished,
+// and releasing it neither frees device memory nor waits for the device (hipFree synchronises the whole device).
+void* temp_block_acquire(size_t bytes, size_t* block_bytes);
+void temp_block_release(void* ptr, size_t block_bytes);
+
+// Owning device allocation. Temporary (the `stream` constructor): a block of the calling thread's cache, for buffers
+// used only by that thread's operator stream while the operator runs; otherwise a plain allocation for buffers that
+// outlive the operator (column mirrors, the RowIDs behind output PosLists).
 class DeviceBuffer {
  public:
   DeviceBuffer() = default;
   explicit DeviceBuffer(size_t bytes) : _bytes(bytes) {
     if (bytes) hy_check(hy_malloc(&_ptr, bytes), "hy_malloc");
   }
+  DeviceBuffer(size_t bytes, hy_stream_t /*operator stream*/) : _bytes(bytes), _temp(true) {
+    if (bytes) _ptr = temp_block_acquire(bytes, &_block);
+  }
   ~DeviceBuffer() {
-    if (_ptr) hy_free(_ptr);
+    if (_ptr) _temp ? temp_block_release(_ptr, _block) : static_cast<void>(hy_free(_ptr));
   }
   DeviceBuffer(const DeviceBuffer&) = delete;
   DeviceBuffer& operator=(const DeviceBuffer&) = delete;
@@ -41,6 +53,8 @@ class DeviceBuffer {
  private:
   void* _ptr = nullptr;
   size_t _bytes = 0;
+  size_t _block = 0;
+  bool _temp = false;
 };
 
 // Per-thread stream for operator execution (operators may run concurrently on scheduler workers).
@@ -70,7 +84,7 @@ std::shared_ptr<DeviceColumn> device_column(const BaseColumn& column);
 // Returns (uploading on first use) the device mirror of a PosList.
 std::shared_ptr<DevicePosList> device_pos_list(const PosList& pos_list);
 
-// Creates a PosList whose host content and device mirror are both filled from a device RowID array.
+// Creates a lazy PosList over a device RowID array (its device mirror; host RowIDs copied on first host access).
 std::shared_ptr<PosList> pos_list_from_device(std::shared_ptr<DeviceBuffer> rows, uint64_t offset, uint64_t n);
 
 int32_t hy_type_of(DataType t);

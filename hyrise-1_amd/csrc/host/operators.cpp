@@ -222,9 +222,9 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
     size_t ws_bytes = 0;
     hy_check(hy_table_scan_workspace_size(sizes.data(), static_cast<uint32_t>(sizes.size()), &ws_bytes),
              "hy_table_scan_workspace_size");
-    DeviceBuffer ws(ws_bytes);
-    DeviceBuffer offsets(std::max<uint64_t>(total, 1) * 4);
-    DeviceBuffer counts(descs.size() * 4);
+    DeviceBuffer ws(ws_bytes, s);
+    DeviceBuffer offsets(std::max<uint64_t>(total, 1) * 4, s);
+    DeviceBuffer counts(descs.size() * 4, s);
     hy_check(hy_table_scan(descs.data(), static_cast<uint32_t>(descs.size()), hy_type_of(col_type), constant.bytes,
                            offsets.as<uint32_t>(), counts.as<uint32_t>(), ws.get(), ws_bytes, s),
              "hy_table_scan");
@@ -245,7 +245,7 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
       views.emplace_back(pos, h_counts[k]);
       pos += h_counts[k];
     }
-    hy_check(hy_stream_synchronize(s), "sync");
+    // output PosLists are lazy views of `rows` (no copy to the host, no wait: later work is ordered on the stream)
     for (size_t k = 0; k < descs.size(); ++k) {
       if (views[k].second == 0) continue;  // reference table_scan.cpp:99: no empty output chunks
       auto pl = pos_list_from_device(rows, views[k].first, views[k].second);
@@ -276,7 +276,7 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
     const uint64_t m = pos_list.size();
 
     // distinct referenced chunks in order of first appearance -> the reference's unordered_map iteration order
-    DeviceBuffer first(std::max<size_t>(rtable->chunk_count(), 1) * 8);
+    DeviceBuffer first(std::max<size_t>(rtable->chunk_count(), 1) * 8, s);
     hy_check(hy_pos_list_chunk_first_seen(dpl->ptr(), m, rtable->chunk_count(), first.as<uint64_t>(), s),
              "hy_pos_list_chunk_first_seen");
     std::vector<uint64_t> h_first(rtable->chunk_count());
@@ -290,9 +290,9 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
 
     size_t ws_bytes = 0;
     hy_check(hy_reference_scan_workspace_size(m, &ws_bytes), "hy_reference_scan_workspace_size");
-    DeviceBuffer ws(ws_bytes);
-    DeviceBuffer positions(std::max<uint64_t>(m, 1) * 4);
-    DeviceBuffer count(8);
+    DeviceBuffer ws(ws_bytes, s);
+    DeviceBuffer positions(std::max<uint64_t>(m, 1) * 4, s);
+    DeviceBuffer count(8, s);
     uint64_t total = 0;
     if (groups.size() <= 1) {
       hy_check(hy_reference_scan(dpl->ptr(), m, rdesc.data(), static_cast<uint32_t>(rdesc.size()), hy_type_of(col_type),
@@ -443,11 +443,14 @@ int32_t join_mode(JoinMode m) {
   return HY_JOIN_INNER;
 }
 
-// write_output_columns (join_hash.cpp:564-613) for one side of one partition.
+// write_output_columns (join_hash.cpp:564-613) for one side of one partition. PosLists are lazy views: of the
+// join's output RowIDs, or - for a reference input - of that side's RowIDs dereferenced through one PosList group,
+// computed once for all partitions (rows [0, rows_used) of the output buffer) by a single launch.
 void write_output_columns(ChunkColumns& out, const std::shared_ptr<const Table>& input_table, const JoinSideInput& side,
-                          const std::shared_ptr<DeviceBuffer>& rows, uint64_t offset, uint64_t n,
+                          const std::shared_ptr<DeviceBuffer>& rows, uint64_t offset, uint64_t n, uint64_t rows_used,
                           std::map<std::pair<int, uint64_t>, std::shared_ptr<PosList>>& cache,
                           std::vector<std::shared_ptr<DeviceBuffer>>& group_ptr_arrays,
+                          std::vector<std::shared_ptr<DeviceBuffer>>& group_deref,
                           std::shared_ptr<Table>& dummy_table) {
   hy_stream_t s = operator_stream();
   if (input_table->type() == TableType::Data) {
@@ -473,19 +476,19 @@ void write_output_columns(ChunkColumns& out, const std::shared_ptr<const Table>&
     } else {
       auto& cached = cache[{g, offset}];
       if (!cached) {
-        if (!group_ptr_arrays[g]) {
+        if (!group_deref[g]) {
           std::vector<const hy_row_id*> ptrs;
           for (const auto& p : side.groups[g]) ptrs.push_back(device_pos_list(*p)->ptr());
           group_ptr_arrays[g] = std::make_shared<DeviceBuffer>(ptrs.size() * sizeof(void*));
           hy_check(hy_memcpy_htod(group_ptr_arrays[g]->get(), ptrs.data(), ptrs.size() * sizeof(void*), s), "htod");
-          hy_check(hy_stream_synchronize(s), "sync");
+          hy_check(hy_stream_synchronize(s), "sync");  // `ptrs` is pageable host memory
+          group_deref[g] = std::make_shared<DeviceBuffer>(std::max<uint64_t>(rows_used, 1) * sizeof(RowID));
+          hy_check(hy_dereference_row_ids(rows->as<hy_row_id>(), rows_used,
+                                          group_ptr_arrays[g]->as<const hy_row_id* const>(),
+                                          group_deref[g]->as<hy_row_id>(), s),
+                   "hy_dereference_row_ids");
         }
-        auto deref = std::make_shared<DeviceBuffer>(std::max<uint64_t>(n, 1) * sizeof(RowID));
-        hy_check(hy_dereference_row_ids(rows->as<hy_row_id>() + offset, n,
-                                        group_ptr_arrays[g]->as<const hy_row_id* const>(), deref->as<hy_row_id>(), s),
-                 "hy_dereference_row_ids");
-        hy_check(hy_stream_synchronize(s), "sync");
-        cached = pos_list_from_device(deref, 0, n);
+        cached = pos_list_from_device(group_deref[g], offset, n);
       }
       pl = cached;
     }
@@ -543,9 +546,9 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
 
   size_t ws_bytes = 0;
   hy_check(hy_join_hash_workspace_size(&b, &p, &prm, &ws_bytes), "hy_join_hash_workspace_size");
-  DeviceBuffer ws(ws_bytes);
+  DeviceBuffer ws(ws_bytes, s);
   const uint32_t n_parts = 1u << prm.radix_bits;
-  DeviceBuffer part_begin(8 * n_parts), part_count(4 * n_parts);
+  DeviceBuffer part_begin(8 * n_parts, s), part_count(4 * n_parts, s);
   uint64_t capacity = std::max<uint64_t>(probe_table->row_count() + build_table->row_count(), 16);
   std::shared_ptr<DeviceBuffer> out_b, out_p;
   hy_join_result res{};
@@ -569,17 +572,23 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
 
   std::map<std::pair<int, uint64_t>, std::shared_ptr<PosList>> bcache, pcache;
   std::vector<std::shared_ptr<DeviceBuffer>> bptrs(bside.groups.size()), pptrs(pside.groups.size());
+  std::vector<std::shared_ptr<DeviceBuffer>> bderef(bside.groups.size()), pderef(pside.groups.size());
   std::shared_ptr<Table> bdummy, pdummy;
+  uint64_t used = 0;  // the output range the partitions occupy
+  for (uint32_t part = 0; part < n_parts; ++part)
+    if (h_count[part]) used = std::max<uint64_t>(used, h_begin[part] + h_count[part]);
   for (uint32_t part = 0; part < n_parts; ++part) {
     const uint64_t n = h_count[part];
     if (n == 0) continue;  // join_hash.cpp:835-837
     ChunkColumns cols;
+    const uint64_t b0 = h_begin[part];
     if (inputs_swapped) {
-      write_output_columns(cols, probe_table, pside, out_p, h_begin[part], n, pcache, pptrs, pdummy);
-      if (!semi_anti) write_output_columns(cols, build_table, bside, out_b, h_begin[part], n, bcache, bptrs, bdummy);
+      write_output_columns(cols, probe_table, pside, out_p, b0, n, used, pcache, pptrs, pderef, pdummy);
+      if (!semi_anti)
+        write_output_columns(cols, build_table, bside, out_b, b0, n, used, bcache, bptrs, bderef, bdummy);
     } else {
-      write_output_columns(cols, build_table, bside, out_b, h_begin[part], n, bcache, bptrs, bdummy);
-      write_output_columns(cols, probe_table, pside, out_p, h_begin[part], n, pcache, pptrs, pdummy);
+      write_output_columns(cols, build_table, bside, out_b, b0, n, used, bcache, bptrs, bderef, bdummy);
+      write_output_columns(cols, probe_table, pside, out_p, b0, n, used, pcache, pptrs, pderef, pdummy);
     }
     output->append_chunk(cols);
   }

@@ -259,7 +259,7 @@ std::vector<std::shared_ptr<BaseColumn>> evaluate_on_device(const AbstractExpres
   auto nulls = nullable ? std::make_shared<DeviceBuffer>(std::max<uint64_t>(rows, 1) + 16) : nullptr;
   size_t ws_bytes = 0;
   hy_check(hy_projection_workspace_size(&hin, &ws_bytes), "hy_projection_workspace_size");
-  DeviceBuffer ws(ws_bytes);
+  DeviceBuffer ws(ws_bytes, s);
   hy_check(hy_projection(&hin, prog.data(), static_cast<uint32_t>(prog.size()), values->get(),
                          nulls ? nulls->as<uint8_t>() : nullptr, ws.get(), ws_bytes, s),
            "hy_projection");

@@ -1,5 +1,8 @@
 #include "storage.hpp"
 
+#include <atomic>
+#include <thread>
+
 #include <fstream>
 #include <sstream>
 
@@ -129,6 +132,31 @@ void ChunkEncoder::encode_chunks(const std::shared_ptr<Table>& table, const std:
       chunk->replace_column(c, encode_dictionary(*col));
     }
   }
+}
+
+void ChunkEncoder::encode_columns(const std::shared_ptr<Table>& table, const std::vector<ColumnID>& column_ids,
+                                  EncodingType encoding) {
+  Assert(table->type() == TableType::Data, "Only data tables can be encoded");
+  if (encoding == EncodingType::Unencoded) return;
+  if (encoding != EncodingType::Dictionary)
+    Fail("Encoding type not supported by the device path (only Unencoded and Dictionary)");
+  // chunks are independent: encoded in parallel (the reference encodes chunk by chunk in jobs as well)
+  const ChunkID n = table->chunk_count();
+  const unsigned workers = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  std::atomic<ChunkID> next{0};
+  auto work = [&]() {
+    for (ChunkID c; (c = next.fetch_add(1)) < n;) {
+      const auto chunk = table->get_chunk(c);
+      for (const auto col_id : column_ids) {
+        const auto col = chunk->get_column(col_id);
+        if (col->encoding_type() != EncodingType::Dictionary) chunk->replace_column(col_id, encode_dictionary(*col));
+      }
+    }
+  };
+  std::vector<std::thread> pool;
+  for (unsigned i = 1; i < workers; ++i) pool.emplace_back(work);
+  work();
+  for (auto& t : pool) t.join();
 }
 
 void ChunkEncoder::encode_all_chunks(const std::shared_ptr<Table>& table, EncodingType encoding) {

@@ -310,6 +310,9 @@ struct ChunkEncoder {
   static void encode_chunks(const std::shared_ptr<Table>& table, const std::vector<ChunkID>& chunk_ids,
                             EncodingType encoding);
   static void encode_all_chunks(const std::shared_ptr<Table>& table, EncodingType encoding);
+  // every chunk's columns column_ids (the others stay as they are); chunks in parallel
+  static void encode_columns(const std::shared_ptr<Table>& table, const std::vector<ColumnID>& column_ids,
+                             EncodingType encoding);
 };
 
 std::shared_ptr<Table> load_table(const std::string& file_name, uint32_t chunk_size = CHUNK_MAX_SIZE);

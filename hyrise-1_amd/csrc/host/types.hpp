@@ -21,6 +21,7 @@
 #include <cstring>
 #include <limits>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <variant>
@@ -62,14 +63,47 @@ inline const RowID NULL_ROW_ID = RowID{INVALID_CHUNK_ID, INVALID_CHUNK_OFFSET};
 
 struct DevicePosList;  // device.hpp
 
+class PosList;
+// Copies a device-produced PosList's RowIDs to `dst` (the device layer's function, device.cpp). Carried by each lazy
+// PosList, so code in another shared object (the oracle module) reading it calls the producer's copy routine.
+using PosListFetch = void (*)(const PosList& pos_list, RowID* dst);
+
 // PosList: host vector of RowIDs (the reference's pmr_vector<RowID>) plus an optional device-resident mirror
 // in the same 8-byte layout, so that a downstream GPU operator does not re-upload what an upstream GPU
-// operator produced.
+// operator produced. A PosList a GPU operator produces is lazy: it knows its size and holds only the device mirror;
+// the host RowIDs are copied down on the first host access (element, iterator or data()), so an operator chain that
+// stays on the device never waits for a device-to-host copy per output chunk.
 class PosList : public std::vector<RowID> {
+  using Base = std::vector<RowID>;
+
  public:
-  using std::vector<RowID>::vector;
+  using Base::vector;
   PosList() = default;
-  explicit PosList(std::vector<RowID>&& v) : std::vector<RowID>(std::move(v)) {}
+  explicit PosList(std::vector<RowID>&& v) : Base(std::move(v)) {}
+
+  // A PosList of n RowIDs that live on the device (its mirror is set by the producer; fetch copies them down).
+  static std::shared_ptr<PosList> lazy(size_t n, PosListFetch fetch) {
+    auto p = std::make_shared<PosList>();
+    p->_lazy_size = n;
+    p->_lazy = n > 0;
+    p->_fetch = fetch;
+    return p;
+  }
+  bool is_lazy() const { return _lazy; }
+
+  size_t size() const { return _lazy ? _lazy_size : Base::size(); }
+  bool empty() const { return size() == 0; }
+  const RowID& operator[](size_t i) const { return host()[i]; }
+  RowID& operator[](size_t i) { return host()[i]; }
+  const RowID& at(size_t i) const { return host().at(i); }
+  const RowID* data() const { return host().data(); }
+  RowID* data() { return host().data(); }
+  Base::const_iterator begin() const { return host().begin(); }
+  Base::const_iterator end() const { return host().end(); }
+  Base::iterator begin() { return host().begin(); }
+  Base::iterator end() { return host().end(); }
+  const RowID& front() const { return host().front(); }
+  const RowID& back() const { return host().back(); }
 
   std::shared_ptr<DevicePosList> device_mirror() const { return std::atomic_load(&_device); }
   void set_device_mirror(std::shared_ptr<DevicePosList> d) const { std::atomic_store(&_device, std::move(d)); }
@@ -81,8 +115,25 @@ class PosList : public std::vector<RowID> {
   void set_single_chunk_id(ChunkID c) { _single_chunk_id = c; }
 
  private:
+  Base& host() const {
+    auto& self = const_cast<PosList&>(*this);
+    if (_lazy) {
+      static std::mutex m;
+      std::lock_guard<std::mutex> lock(m);
+      if (_lazy) {
+        self.Base::resize(_lazy_size);
+        _fetch(*this, self.Base::data());
+        _lazy = false;
+      }
+    }
+    return self;
+  }
+
   mutable std::shared_ptr<DevicePosList> _device;
   ChunkID _single_chunk_id = INVALID_CHUNK_ID;
+  size_t _lazy_size = 0;
+  mutable bool _lazy = false;
+  PosListFetch _fetch = nullptr;
 };
 
 enum class DataType : uint8_t { Null, Int, Long, Float, Double, String };

@@ -403,7 +403,8 @@ __global__ __launch_bounds__(AGG_THREADS) void agg_dense_rows(AggDesc d, uint32_
 // folds its 16 rows in registers (counts, sums, min/max, limb pieces) and the wave then reduces once - 16x fewer
 // cross-lane reductions than per-64-row ballots. Requires: at most one PosList group and every used column with one
 // encoding (kind / vid width) across its chunks (AggCol::ukind); the host falls back to agg_dense_rows otherwise.
-// Results are word-for-word those of agg_dense_rows (the same ADD / MIN / MAX / OR combination of the same values).
+// Results are the same exact sums as agg_dense_rows (the same decoded values; integer-valued float rows are folded
+// into the limbs as normalised pieces by span_fold_int_words, so individual limb words may differ).
 // ------------------------------------------------------------------------------------------------------------
 // A float / double that is an integer of small magnitude (|v| <= 2^24, resp. 2^31): its int64 value. Such rows of a
 // float SUM are summed exactly in one int64 word (no overflow below 2^32 rows).
@@ -764,7 +765,13 @@ struct AggTable {
   uint32_t* dstate;
   unsigned long long* dkeys;       // dcap * 2
   uint64_t dcap;
+  unsigned long long* inserted;    // groups inserted so far, INSERT_SHARDS counters (by slot; no single hot word)
+  uint64_t max_per_shard;          // load limit per counter: an insert past it sets error bit 2 (HY_ERR_GROUP_BOUND)
 };
+
+constexpr uint32_t INSERT_SHARDS = 64;
+
+constexpr uint64_t LOCK_SPIN_LIMIT = 1ull << 22;  // waits on a slot being initialised (not probe steps)
 
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {
   x ^= x >> 33;
@@ -793,30 +800,41 @@ __device__ __forceinline__ uint64_t group_slot(const AggDesc& d, const AggTable&
   uint64_t h = 0x9E3779B97F4A7C15ull;
   for (uint32_t i = 0; i < nk; ++i) h = mix64(h ^ key[i]);
   uint64_t s = h & (t.cap - 1);
-  for (uint64_t guard = 0; guard < t.cap * 4; ++guard) {
+  // a READY slot's state word carries a tag of the key's hash (>= HSLOT_READY): other keys are skipped without
+  // loading their key words
+  const uint32_t tag = static_cast<uint32_t>(h >> 32) | HSLOT_READY;
+  uint64_t probes = 0, spins = 0;
+  while (probes < t.cap && spins < LOCK_SPIN_LIMIT) {
     const uint32_t st = __hip_atomic_load(&t.state[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (st == HSLOT_EMPTY) {
       uint32_t expected = HSLOT_EMPTY;
       if (__hip_atomic_compare_exchange_strong(&t.state[s], &expected, HSLOT_LOCKED, __ATOMIC_RELAXED,
                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        // past the load limit the table still works (the record is inserted) but the call reports
+        // HY_ERR_GROUP_BOUND, and the caller re-runs with a larger table
+        if (atomicAdd(t.inserted + (s & (INSERT_SHARDS - 1)), 1ull) >= t.max_per_shard) atomicOr(d.error, 4u);
         unsigned long long* rec = t.records + s * d.words;
         for (uint32_t i = 0; i < nk; ++i) table_store(rec + i, key[i]);
         for (uint32_t i = nk; i < d.words; ++i) table_store(rec + i, word_init(d.word_op[i]));
         drain_stores();
-        __hip_atomic_store(&t.state[s], HSLOT_READY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&t.state[s], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return s;
       }
       continue;  // lost the race: re-read the same slot
     }
     if (st == HSLOT_LOCKED) {
+      ++spins;
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
-    const unsigned long long* rec = t.records + s * d.words;
-    bool eq = true;
-    for (uint32_t i = 0; i < nk; ++i) eq = eq && (table_load(rec + i) == key[i]);
-    if (eq) return s;
+    if (st == tag) {
+      const unsigned long long* rec = t.records + s * d.words;
+      uint64_t diff = 0;  // every key word loaded at once (no short-circuit chain of dependent loads)
+      for (uint32_t i = 0; i < nk; ++i) diff |= table_load(rec + i) ^ key[i];
+      if (diff == 0) return s;
+    }
     s = (s + 1) & (t.cap - 1);
+    ++probes;
   }
   atomicOr(d.error, 1u);
   return ~0ull;
@@ -825,7 +843,8 @@ __device__ __forceinline__ uint64_t group_slot(const AggDesc& d, const AggTable&
 // true if (tag, value) was not in the distinct set yet
 __device__ __forceinline__ bool distinct_insert(const AggDesc& d, const AggTable& t, uint64_t tag, uint64_t value) {
   uint64_t s = mix64(tag * 0x9E3779B97F4A7C15ull ^ mix64(value)) & (t.dcap - 1);
-  for (uint64_t guard = 0; guard < t.dcap * 4; ++guard) {
+  uint64_t probes = 0, spins = 0;
+  while (probes < t.dcap && spins < LOCK_SPIN_LIMIT) {
     const uint32_t st = __hip_atomic_load(&t.dstate[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (st == HSLOT_EMPTY) {
       uint32_t expected = HSLOT_EMPTY;
@@ -840,11 +859,13 @@ __device__ __forceinline__ bool distinct_insert(const AggDesc& d, const AggTable
       continue;
     }
     if (st == HSLOT_LOCKED) {
+      ++spins;
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
     if (table_load(t.dkeys + 2 * s) == tag && table_load(t.dkeys + 2 * s + 1) == value) return false;
     s = (s + 1) & (t.dcap - 1);
+    ++probes;
   }
   atomicOr(d.error, 1u);
   return false;
@@ -1013,7 +1034,7 @@ __global__ void agg_hash_compact(AggDesc d, AggTable t, unsigned long long* __re
                                  unsigned long long* __restrict__ n_out) {
   for (uint64_t s = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; s < t.cap;
        s += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
-    if (t.state[s] != HSLOT_READY) continue;
+    if (t.state[s] < HSLOT_READY) continue;  // READY slots hold a hash tag >= HSLOT_READY
     const uint64_t idx = atomicAdd(n_out, 1ull);
     if (idx >= capacity) continue;
     const unsigned long long* rec = t.records + s * d.words;

@@ -96,10 +96,13 @@ class ExchangeJoin:
 
     def partition(self, side, n_rows, keep_nulls, stream, device, key="side", filt=None, row_base=0):
         """Step 1 for one side: returns (records int64 tensor, bucket counts np.uint64[B]). Row-index mode: the
-        records of the rows taking part (all rows, or the fused scan's matches with filt), payload row_base + row."""
+        records of the rows taking part (all rows, or the fused scan's matches with filt), payload row_base + row.
+        keep_nulls None: from the join mode (NULL keys take part in LEFT / RIGHT joins, join_hash.cpp:468-527)."""
         import torch
 
         lib, capi = self.lib, self.capi
+        if keep_nulls is None:
+            keep_nulls = self.params.mode in (capi.HY_JOIN_LEFT, capi.HY_JOIN_RIGHT)
         wsb = ctypes.c_size_t(0)
         fp = ctypes.byref(filt) if filt is not None else None
         if self.rows:
@@ -157,16 +160,18 @@ class ExchangeJoin:
         part_count = torch.empty(max(1, n_parts), dtype=torch.int32, device=device)
         res = capi.JoinResult()
         if self.rows:
-            capi.check(lib.hy_join_exchange_join_rows(build_recs.data_ptr(), bcp, probe_recs.data_ptr(), pcp,
-                                                      self.world, first, nb, ctypes.byref(self.params), bl.ctypes.data,
-                                                      bl.size, pl.ctypes.data, pl.size, out_b.data_ptr(),
-                                                      out_p.data_ptr(), capacity, part_begin.data_ptr(),
-                                                      part_count.data_ptr(), ctypes.byref(res), ws.data_ptr(),
-                                                      ws.numel(), stream), "hy_join_exchange_join_rows")
+            st = lib.hy_join_exchange_join_rows(build_recs.data_ptr(), bcp, probe_recs.data_ptr(), pcp, self.world,
+                                                first, nb, ctypes.byref(self.params), bl.ctypes.data, bl.size,
+                                                pl.ctypes.data, pl.size, out_b.data_ptr(), out_p.data_ptr(), capacity,
+                                                part_begin.data_ptr(), part_count.data_ptr(), ctypes.byref(res),
+                                                ws.data_ptr(), ws.numel(), stream)
         else:
-            capi.check(lib.hy_join_exchange_join(build_recs.data_ptr(), bcp, probe_recs.data_ptr(), pcp, self.world,
-                                                 first, nb, ctypes.byref(self.params), out_b.data_ptr(),
-                                                 out_p.data_ptr(), capacity, part_begin.data_ptr(),
-                                                 part_count.data_ptr(), ctypes.byref(res), ws.data_ptr(), ws.numel(),
-                                                 stream), "hy_join_exchange_join")
+            st = lib.hy_join_exchange_join(build_recs.data_ptr(), bcp, probe_recs.data_ptr(), pcp, self.world, first,
+                                           nb, ctypes.byref(self.params), out_b.data_ptr(), out_p.data_ptr(),
+                                           capacity, part_begin.data_ptr(), part_count.data_ptr(), ctypes.byref(res),
+                                           ws.data_ptr(), ws.numel(), stream)
+        if st == capi.HY_ERR_CAPACITY:  # more pairs than the first guess (repeated build keys): exact size known
+            return self.join(build_recs, build_matrix, probe_recs, probe_matrix, rank, stream, device,
+                             capacity=res.capacity_required + 16)
+        capi.check(st, "hy_join_exchange_join")
         return out_b, out_p, part_begin[:n_parts], part_count[:n_parts], res.total_pairs

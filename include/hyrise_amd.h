@@ -31,7 +31,9 @@ enum {
   HY_ERR_ALIGNMENT = 4,      /* a device pointer is not 16-byte aligned */
   HY_ERR_UNSUPPORTED = 5,    /* type / mode not implemented on the device path */
   HY_ERR_CAPACITY = 6,       /* output capacity exceeded; *_required holds the needed size */
-  HY_ERR_KERNEL = 7          /* a kernel reported an internal failure (bounded spin expired) */
+  HY_ERR_KERNEL = 7,         /* a kernel reported an internal failure (bounded spin expired) */
+  HY_ERR_GROUP_BOUND = 8     /* hy_aggregate: more groups than params->group_bound allows; *n_groups holds the
+                                group_bound to retry with (re-query the workspace size) */
 };
 
 /* RowID, identical layout to reference src/lib/types.hpp:97-131 ({ChunkID chunk_id; ChunkOffset chunk_offset;}). */
@@ -411,6 +413,20 @@ hy_status hy_dereference_row_ids(const hy_row_id* rows, uint64_t n, const hy_row
  * In dense mode (every group-by column arrives as integer codes with a domain, product of (domain + 1) <= 64) the
  * key words of a group are its codes.
  * ------------------------------------------------------------------------------------------------------------- */
+/* Expression nodes (postfix programs) of hy_projection and of expression columns of hy_aggregate; see the Projection
+ * section below for their semantics. */
+enum { HY_EXPR_COLUMN = 0, HY_EXPR_VALUE = 1, HY_EXPR_ADD = 2, HY_EXPR_SUB = 3, HY_EXPR_MUL = 4, HY_EXPR_DIV = 5,
+       HY_EXPR_MOD = 6 };
+enum { HY_EXPR_MAX_NODES = 32, HY_EXPR_MAX_DEPTH = 8 };
+
+typedef struct hy_expr_node {
+  int32_t kind;       /* HY_EXPR_* */
+  int32_t type;       /* HY_TYPE_* of the node's value (0: NULL literal) */
+  int32_t calc_type;  /* arithmetic: HY_TYPE_* the operation is computed in */
+  int32_t column;     /* COLUMN: index into hy_agg_input.columns */
+  uint64_t value;     /* VALUE: the literal's bits in `type` (int32/float in the low 4 bytes) */
+} hy_expr_node;
+
 enum { HY_AGG_MIN = 0, HY_AGG_MAX = 1, HY_AGG_SUM = 2, HY_AGG_AVG = 3, HY_AGG_COUNT = 4, HY_AGG_COUNT_DISTINCT = 5 };
 enum { HY_AGG_MAX_COLUMNS = 16, HY_AGG_MAX_GROUPBY = 8, HY_AGG_MAX_AGGREGATES = 16, HY_AGG_MAX_POS_GROUPS = 8 };
 
@@ -421,6 +437,12 @@ typedef struct hy_agg_column {
   const hy_column_chunk* chunks;     /* HOST array of n_chunks device column chunks */
   uint32_t n_chunks;
   uint32_t domain;                   /* group-by only: 0, or every non-NULL value is an integer code < domain */
+  /* Expression column (n_nodes > 0): each row's value is the postfix program over the input's other, plain columns
+   * (hy_expr_node semantics of hy_projection: the reference's Projection feeding the Aggregate, evaluated inside the
+   * aggregation instead of materialised); value_type = the program's result type; chunks / pos_group unused. */
+  const hy_expr_node* program;       /* HOST array of n_nodes nodes, or NULL */
+  uint32_t n_nodes;
+  uint32_t reserved;
 } hy_agg_column;
 
 typedef struct hy_agg_input {
@@ -442,7 +464,11 @@ typedef struct hy_agg_params {
   uint32_t n_groupby;
   const hy_agg_def* aggregates;      /* HOST */
   uint32_t n_aggregates;
-  uint64_t group_bound;              /* upper bound on the number of groups; 0 = number of input rows */
+  uint64_t group_bound;              /* expected number of groups (sizes the hash table); 0 = derived: the product
+                                        of the group-by columns' dictionary sizes when every group-by column is
+                                        dictionary-encoded, else min(rows, the groups 2 GiB of records hold,
+                                        at least 2^20). Exceeding it returns
+                                        HY_ERR_GROUP_BOUND with a larger bound; the call has no other effect. */
 } hy_agg_params;
 
 typedef struct hy_agg_layout {
@@ -478,18 +504,6 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
  * Output: values[r] (result type) and nulls[r] (1 = NULL; may be NULL when the expression is not nullable) for input
  * row r, rows numbered chunk by chunk. Values of NULL rows are unspecified.
  * ------------------------------------------------------------------------------------------------------------- */
-enum { HY_EXPR_COLUMN = 0, HY_EXPR_VALUE = 1, HY_EXPR_ADD = 2, HY_EXPR_SUB = 3, HY_EXPR_MUL = 4, HY_EXPR_DIV = 5,
-       HY_EXPR_MOD = 6 };
-enum { HY_EXPR_MAX_NODES = 32, HY_EXPR_MAX_DEPTH = 8 };
-
-typedef struct hy_expr_node {
-  int32_t kind;       /* HY_EXPR_* */
-  int32_t type;       /* HY_TYPE_* of the node's value (0: NULL literal) */
-  int32_t calc_type;  /* arithmetic: HY_TYPE_* the operation is computed in */
-  int32_t column;     /* COLUMN: index into hy_agg_input.columns */
-  uint64_t value;     /* VALUE: the literal's bits in `type` (int32/float in the low 4 bytes) */
-} hy_expr_node;
-
 hy_status hy_projection_workspace_size(const hy_agg_input* input, size_t* bytes);
 hy_status hy_projection(const hy_agg_input* input, const hy_expr_node* program, uint32_t n_nodes, void* out_values,
                         uint8_t* out_nulls, void* workspace, size_t workspace_bytes, hy_stream_t stream);

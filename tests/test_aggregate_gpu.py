@@ -148,7 +148,7 @@ def test_empty_input(hy, oracle):
 @pytest.mark.parametrize("reference_input", [False, True])
 def test_dense_span_float_sums_mixed_integer_rows(hy, oracle, monkeypatch, reference_input):
     """agg_dense_span sums integer-valued float rows in an int64 word and the others in limbs; the folded result must
-    be the exact sum rounded once (== math.fsum) and word-for-word the per-64-row kernel's (HY_AGG_DENSE_ROWS=1)."""
+    be the exact sum rounded once (== math.fsum) and decode to the per-64-row kernel's results (HY_AGG_DENSE_ROWS=1)."""
     rng = np.random.default_rng(17)
     n = 250_000
     g = rng.integers(0, 4, n).astype(np.int32)
@@ -179,3 +179,21 @@ def test_dense_span_float_sums_mixed_integer_rows(hy, oracle, monkeypatch, refer
         sel = g == row[0]
         assert row[1] == math.fsum(f[sel & (nulls == 0)].astype(np.float64))
         assert row[2] == math.fsum(d[sel])
+
+
+def test_hash_aggregate_grows_past_its_group_bound(hy, oracle, monkeypatch):
+    """More groups than the hash table was sized for (HY_AGG_RECORD_BUDGET shrinks the derived bound to a few
+    thousand groups): hy_aggregate reports HY_ERR_GROUP_BOUND, the operator retries with 4x larger tables, and the
+    result equals the reference Aggregate's (groups in first-appearance order)."""
+    monkeypatch.setenv("HY_AGG_RECORD_BUDGET", str(1 << 20))
+    rng = np.random.default_rng(23)
+    n = 600_000
+    keys = rng.permutation(n).astype(np.int64) * 3 - 7
+    vals = rng.integers(-1000, 1000, n).astype(np.int32)
+    t = hy.Table.from_arrays([("k", hy.DataType.Long, False), ("v", hy.DataType.Int, False)], [keys, vals], [],
+                             100_000)
+    aggs = [(1, "Sum"), (None, "Count")]
+    op = hy.Aggregate(wrap(hy, t), ac.agg_defs(hy, aggs), [0])
+    op.execute()
+    assert not op.used_dense_path()
+    assert_identical(op.get_output(), oracle.aggregate(t, ac.agg_defs(hy, aggs), [0]))
