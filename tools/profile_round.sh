@@ -1,0 +1,29 @@
+#!/bin/bash
+# Round profiles of the three bench workloads on the GPU box (run through gpurun from the repo root):
+# per workload one rocprofv3 --kernel-trace --stats pass over the bench command, then separate FETCH_SIZE and
+# WRITE_SIZE PMC passes (one counter each, restricted to the framework's kernels), summarised by
+# tools/summarize_rocprof.py with the PMC runs' step count (HBM bytes per step). Each pass has its own time limit.
+# usage: tools/profile_round.sh <tag, e.g. r02>
+set -e -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=${1:-r02}
+export TMPDIR=/tmp
+cd /tmp
+run() {  # name, bench args
+  local name=$1
+  shift
+  local OUT=$R/gpurun_out/prof_$name
+  mkdir -p "$OUT"
+  timeout -s KILL 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run -f csv -- \
+    python3 "$R/bench.py" "$@" --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/bench_under_trace.json" 2> "$OUT/trace.err"
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -s KILL 400 rocprofv3 --pmc $c --kernel-include-regex 'hyk::' -d "$OUT/$c" -o run -f csv -- \
+      python3 "$R/bench.py" "$@" --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/bench_under_$c.json" 2> "$OUT/$c.err"
+  done
+  python3 "$R/tools/summarize_rocprof.py" "$OUT" 3 > "$R/gpurun_out/${TAG}_rocprof_${name}_summary.json"
+  cp "$OUT"/trace/run_kernel_stats.csv "$R/gpurun_out/${TAG}_rocprof_${name}_kernel_stats.csv"
+  echo "profiled $name"
+}
+run sf100_fused
+run q1_sf100 --workload q1
+run q3_sf100 --workload q3

@@ -28,7 +28,14 @@ def one(pattern):
     return files[-1] if files else None
 
 
-def main(out):
+def split_sides(launches, steps):
+    """True when the launches alternate build / probe sides (an even count per step)."""
+    if steps:
+        return launches % (2 * steps) == 0
+    return launches % 2 == 0
+
+
+def main(out, steps=None):
     res = {"kernels": {}}
     stats = one(os.path.join(out, "trace", "**", "*kernel_stats.csv"))
     if stats:
@@ -49,6 +56,8 @@ def main(out):
                 if k.startswith(("part1_", "part2_")):
                     durs[k].append((int(row["Dispatch_Id"]), int(row["End_Timestamp"]) - int(row["Start_Timestamp"])))
         for k, v in durs.items():
+            if not split_sides(len(v), None):
+                continue
             v.sort()
             for tag, sel in ((".build", v[0::2]), (".probe", v[1::2])):
                 if sel:
@@ -69,8 +78,9 @@ def main(out):
         by_kernel = defaultdict(list)
         for d, v in per_dispatch.items():
             by_kernel[names[d]].append(v * 1024.0 * scale)
-        # partition kernels run once per join side, build first: split their launches into .build / .probe
-        for k in [k for k in by_kernel if k.startswith(("part1_", "part2_"))]:
+        # partition kernels run once per join side, build first: split their launches into .build / .probe (only when
+        # a step launches them a multiple of twice - the fused path partitions both sides in one launch)
+        for k in [k for k in by_kernel if k.startswith(("part1_", "part2_")) and split_sides(len(by_kernel[k]), steps)]:
             ordered = [v for d, v in sorted(((int(d), v) for d, v in per_dispatch.items() if names[d] == k))]
             by_kernel[k + ".build"] = [v * 1024.0 * scale for v in ordered[0::2]]
             by_kernel[k + ".probe"] = [v * 1024.0 * scale for v in ordered[1::2]]
@@ -81,9 +91,17 @@ def main(out):
     for k, v in res["kernels"].items():
         if "hbm_read_bytes_per_launch" in v and "hbm_write_bytes_per_launch" in v:
             v["hbm_bytes_per_launch"] = v["hbm_read_bytes_per_launch"] + v["hbm_write_bytes_per_launch"]
+    if steps:  # the PMC runs' steps (warmup + timed): HBM bytes of one step over every kernel of the path
+        total = 0.0
+        for k, v in res["kernels"].items():
+            if k.startswith("stream_") or k.endswith((".build", ".probe")) or "hbm_bytes_per_launch" not in v:
+                continue  # the roofline probe is not part of a step; .build/.probe split the same launches
+            total += v["hbm_bytes_per_launch"] * v.get("hbm_read_bytes_launches", 0)
+        res["hbm_bytes_per_step"] = total / steps
+        res["pmc_steps"] = steps
     res["corrections"] = "FETCH_SIZE x2 (gfx950 128-B requests tallied at 64 B), WRITE_SIZE x1; KiB -> bytes"
     print(json.dumps(res, indent=1, sort_keys=True))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else None)
