@@ -11,6 +11,7 @@
 #include "../kernels/aggregate.hip"
 #include "../kernels/projection.hip"
 #include "../kernels/aggregate_fused.hip"
+#include "../kernels/aggregate_lanes.hip"
 
 using namespace hyc;
 
@@ -86,6 +87,10 @@ struct AggPlan {
   bool materialize = false;                // else: expression columns materialised first (projection kernel)
   hyk::FusedPlan fp{};
   std::vector<hyk::FqOp> fused_nodes;      // fp.progs on the host
+  bool lanes = false;                      // agg_dense_lanes first, agg_dense_fused over the steps it defers
+  hyk::LaneTables lt{};                    // agg_dense_lanes' tables (copied to the workspace)
+  std::vector<hyk::LnTerm> lane_terms;     // lp.terms on the host
+  std::vector<int32_t> lane_cols;          // input column of each loaded column
 };
 
 // agg_dense_fused applies: the dense path; at most one PosList group; int32 group-by columns; every aggregate over a
@@ -170,6 +175,166 @@ void plan_fused(const hy_agg_input* in, const hy_agg_params* p, AggPlan* plan) {
   plan->fused = true;
 }
 
+// agg_dense_lanes applies on top of agg_dense_fused: no MIN / MAX; every loaded column (group-by columns, columns
+// of SUM / AVG / COUNT inputs and of their expressions) 4 bytes wide, read through the single PosList group (or
+// directly for a data input), its chunks dictionary-encoded or value chunks (with or without NULL flags); a group-by
+// column is not also summed; every SUM / AVG / COUNT input compiles to a chain (LnTerm) of + - *; <= LN_COLS columns, <= LN_SUMS
+// inputs, <= LN_TERMS terms. HY_AGG_LANES=0 disables it (tests compare the paths).
+void plan_lanes(const hy_agg_input* in, const hy_agg_params* p, AggPlan* plan) {
+  if (!plan->fused) return;
+  if (const char* e = std::getenv("HY_AGG_LANES"))
+    if (std::atoi(e) == 0) return;
+  auto& lp = plan->lt;
+  lp = hyk::LaneTables{};
+  auto& terms = plan->lane_terms;
+  terms.clear();
+  const int32_t H = static_cast<int32_t>(p->n_groupby);
+  const int32_t want_pg = in->n_pos_groups ? 0 : -1;
+  std::vector<int32_t> load_of(in->n_columns, -1);
+  plan->lane_cols.clear();
+  auto load = [&](int32_t col) -> int32_t {
+    if (col < 0 || col >= static_cast<int32_t>(in->n_columns)) return -1;
+    if (load_of[col] >= 0) return load_of[col];
+    const auto& c = in->columns[col];
+    if (c.n_nodes || !four_bytes(c.value_type) || c.pos_group != want_pg || lp.n_load >= hyk::LN_COLS) return -1;
+    for (uint32_t k = 0; k < c.n_chunks; ++k) {
+      const auto& ch = c.chunks[k];
+      if (ch.kind == HY_COL_DICT && ch.vid_width != 1 && ch.vid_width != 2 && ch.vid_width != 4) return -1;
+    }
+    plan->lane_cols.push_back(col);
+    return load_of[col] = lp.n_load++;
+  };
+  if (H > hyk::FQ_MAX_GB) return;
+  for (int32_t j = 0; j < H; ++j) {
+    if (load(p->groupby[j]) != j) return;
+    lp.gb_domain[j] = plan->d.cols[p->groupby[j]].domain;
+    lp.gb_stride[j] = plan->d.cols[p->groupby[j]].stride;
+  }
+  // an input's chain: postfix program -> terms (see hyk::LnTerm)
+  struct Ent {
+    int form;  // 0 column, 1 literal, 2 literal op column / column op literal, 3 chain
+    hyk::LnTerm t;
+    std::vector<hyk::LnTerm> chain;
+    int32_t type;
+  };
+  auto term_col = [&](int32_t col, int32_t type, Ent* e) -> bool {
+    const int32_t li = load(col);
+    if (li < H) return false;  // not loadable, or a group-by column
+    *e = Ent{0, hyk::LnTerm{hyk::LN_TERM_COL, 0, li, 0, 0, 0, 0, 0}, {}, type};
+    return true;
+  };
+  auto compile = [&](uint32_t colidx, std::vector<hyk::LnTerm>* out, bool* is_float) -> bool {
+    const auto& c = in->columns[colidx];
+    Ent res;
+    if (!c.n_nodes) {
+      if (!term_col(static_cast<int32_t>(colidx), c.value_type, &res)) return false;
+    } else {
+      std::vector<Ent> st;
+      for (uint32_t i = 0; i < c.n_nodes; ++i) {
+        const hy_expr_node& nd = c.program[i];
+        if (nd.kind == HY_EXPR_COLUMN) {
+          Ent e;
+          if (!term_col(nd.column, nd.type, &e)) return false;
+          st.push_back(e);
+          continue;
+        }
+        if (nd.kind == HY_EXPR_VALUE) {
+          if (nd.type == 0) return false;  // NULL literal
+          st.push_back(Ent{1, hyk::LnTerm{hyk::LN_TERM_LIT, 0, 0, static_cast<uint32_t>(nd.value), 0, 0, 0, 0}, {},
+                           nd.type});
+          continue;
+        }
+        if (st.size() < 2) return false;
+        Ent b = st.back();
+        st.pop_back();
+        Ent a = st.back();
+        st.pop_back();
+        const int32_t calc = nd.calc_type;
+        if (nd.kind != HY_EXPR_ADD && nd.kind != HY_EXPR_SUB && nd.kind != HY_EXPR_MUL) return false;  // / % -> fused
+        auto conv = [&](Ent& e) -> bool {  // an int32 operand of a float operation converts (columns, literals)
+          if (e.type == calc) return true;
+          if (e.type != HY_TYPE_INT32 || calc != HY_TYPE_FLOAT) return false;
+          if (e.form == 0) {
+            e.t.cvt = 1;
+          } else if (e.form == 1) {
+            const float f = static_cast<float>(static_cast<int32_t>(e.t.lit));
+            std::memcpy(&e.t.lit, &f, 4);
+          } else {
+            return false;
+          }
+          e.type = calc;
+          return true;
+        };
+        if (!four_bytes(calc) || nd.type != calc || !conv(a) || !conv(b)) return false;
+        Ent r;
+        r.type = nd.type;
+        if (a.form <= 1 && b.form <= 1) {
+          if (a.form == 1 && b.form == 1) return false;  // literal op literal
+          if (a.form == 0 && b.form == 0) {
+            r.form = 3;
+            b.t.comb = nd.kind;
+            r.chain = {a.t, b.t};
+          } else {
+            r.form = 2;
+            r.t = a.form == 0 ? hyk::LnTerm{hyk::LN_TERM_COL_LIT, nd.kind, a.t.col, b.t.lit, a.t.cvt, 0, 0, 0}
+                              : hyk::LnTerm{hyk::LN_TERM_LIT_COL, nd.kind, b.t.col, a.t.lit, b.t.cvt, 0, 0, 0};
+          }
+        } else if (a.form == 3 && b.form == 3) {
+          return false;
+        } else if (a.form == 3) {
+          r = a;
+          b.t.comb = nd.kind;
+          b.t.rev = 0;
+          r.chain.push_back(b.t);
+        } else if (b.form == 3) {
+          r = b;
+          a.t.comb = nd.kind;
+          a.t.rev = 1;
+          r.chain.push_back(a.t);
+        } else {
+          r.form = 3;
+          b.t.comb = nd.kind;
+          r.chain = {a.t, b.t};
+        }
+        r.type = nd.type;
+        st.push_back(r);
+      }
+      if (st.size() != 1) return false;
+      res = st.back();
+    }
+    *out = res.form == 3 ? res.chain : std::vector<hyk::LnTerm>{res.t};
+    *is_float = res.type == HY_TYPE_FLOAT;
+    return true;
+  };
+  std::vector<int32_t> sum_of(in->n_columns, -1);
+  for (uint32_t a = 0; a < p->n_aggregates; ++a) {
+    const auto& def = p->aggregates[a];
+    if (def.column < 0) continue;  // COUNT(*)
+    lp.cnt_word[lp.n_cnt++] = plan->d.fns[a].word;
+    if (def.function != HY_AGG_SUM && def.function != HY_AGG_AVG && def.function != HY_AGG_COUNT) return;
+    int32_t& si = sum_of[def.column];
+    if (si < 0) {
+      std::vector<hyk::LnTerm> chain;
+      bool fl = false;
+      if (lp.n_sums >= hyk::LN_SUMS || !compile(static_cast<uint32_t>(def.column), &chain, &fl)) return;
+      if (terms.size() + chain.size() > static_cast<size_t>(hyk::LN_TERMS)) return;
+      si = lp.n_sums++;
+      lp.sum_kind[si] = hyk::LN_SUM_CHECK;
+      lp.sum_float[si] = fl ? 1 : 0;
+      lp.sum_first[si] = static_cast<int32_t>(terms.size());
+      lp.sum_len[si] = static_cast<int32_t>(chain.size());
+      terms.insert(terms.end(), chain.begin(), chain.end());
+    }
+    if (def.function != HY_AGG_COUNT) {
+      lp.sum_kind[si] = lp.sum_float[si] ? hyk::LN_SUM_FLOAT : hyk::LN_SUM_INT;
+      if (lp.sum_nfn[si] >= hyk::LN_SUM_FNS) return;
+      lp.sum_word[si][lp.sum_nfn[si]++] = plan->d.fns[a].word;
+      lp.sum_limbs[si] = plan->d.fns[a].limbs;
+    }
+  }
+  plan->lanes = true;
+}
+
 // Record bytes a hash table may take without a caller-given bound (at load 1/2: 2 slots per expected group).
 constexpr uint64_t DEFAULT_RECORD_BUDGET = 2ull << 30;
 
@@ -195,6 +360,31 @@ uint64_t group_bound_of(const hy_agg_input* in, const hy_agg_params* p, uint64_t
   const uint64_t budget = knob ? std::max<uint64_t>(1, std::strtoull(knob, nullptr, 10) / per_group)
                                : std::max<uint64_t>(1ull << 20, DEFAULT_RECORD_BUDGET / per_group);
   return std::min<uint64_t>(std::max<uint64_t>(rows, 1), dict ? bound : budget);
+}
+
+inline uint32_t p_groupby(const hy_agg_params* p) { return p->n_groupby; }
+
+// agg_dense_lanes<n_sums>
+void launch_lanes(int n_sums, uint32_t grid, size_t lds, hipStream_t s, const hyk::AggDesc& d,
+                  const hyk::LanePlan& lp, unsigned long long* records) {
+  switch (n_sums) {
+#define HY_LANES_CASE(N)                                                                                         \
+  case N:                                                                                                        \
+    hipLaunchKernelGGL(hyk::agg_dense_lanes<N>, dim3(grid), dim3(hyk::AGG_THREADS), lds, s, d, lp, records); \
+    break;
+    HY_LANES_CASE(0)
+    HY_LANES_CASE(1)
+    HY_LANES_CASE(2)
+    HY_LANES_CASE(3)
+    HY_LANES_CASE(4)
+    HY_LANES_CASE(5)
+    HY_LANES_CASE(6)
+    HY_LANES_CASE(7)
+    HY_LANES_CASE(8)
+#undef HY_LANES_CASE
+    default:
+      break;
+  }
 }
 
 hy_status make_plan(const hy_agg_input* in, const hy_agg_params* p, AggPlan* plan) {
@@ -343,6 +533,7 @@ hy_status make_plan(const hy_agg_input* in, const hy_agg_params* p, AggPlan* pla
   }
   L.dense = dense ? 1 : 0;
   plan_fused(in, p, plan);
+  plan_lanes(in, p, plan);
   plan->materialize = !plan->fused && !plan->expr_cols.empty();
   plan->cap = next_pow2(std::max<uint64_t>(64, 2 * group_bound_of(in, p, plan->rows, d.words)));
   plan->max_groups = plan->cap / 4 * 3;  // load factor limit: past it the insert reports HY_ERR_GROUP_BOUND
@@ -362,6 +553,9 @@ struct AggWs {
   uint32_t* misc;  // [0] error, [2..3] n_out (u64)
   unsigned long long* inserted;  // hash path: hyk::INSERT_SHARDS insert counters
   hyk::FqOp* fused_nodes;        // agg_dense_fused: its expression ops
+  hyk::LnTerm* lane_terms;       // agg_dense_lanes: its chains
+  uint32_t* deferred;            // agg_dense_lanes: steps left to agg_dense_fused
+  hyk::LaneTables* lane_tables;
   void* mat_values[hyk::AGG_MAX_COLUMNS];    // materialised expression columns
   uint8_t* mat_nulls[hyk::AGG_MAX_COLUMNS];
   uint32_t* state;
@@ -381,6 +575,9 @@ void carve(Carver& cv, const hy_agg_input* in, const AggPlan& plan, AggWs* w) {
         std::max<uint32_t>(1, in->columns[j].n_nodes ? in->n_chunks : in->columns[j].n_chunks));
   w->word_op = cv.take<int32_t>(plan.word_op.size());
   w->fused_nodes = cv.take<hyk::FqOp>(std::max<size_t>(1, plan.fused_nodes.size()));
+  w->lane_terms = cv.take<hyk::LnTerm>(std::max<size_t>(1, plan.lane_terms.size()));
+  w->lane_tables = cv.take<hyk::LaneTables>(1);
+  w->deferred = cv.take<uint32_t>(plan.lanes ? std::max<uint64_t>(1, plan.n_tiles * hyk::FQ_STEPS_PER_TILE) : 1);
   for (uint32_t e = 0; e < plan.expr_cols.size(); ++e) {
     const uint32_t j = plan.expr_cols[e];
     w->mat_values[j] = plan.materialize ? cv.take<uint64_t>(std::max<uint64_t>(2, plan.rows)) : nullptr;
@@ -514,12 +711,35 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
                             hipMemcpyHostToDevice, s));
     hyk::FusedPlan fp = plan.fp;
     fp.progs = w.fused_nodes;
-    if (plan.n_tiles) {
-      const size_t lds = sizeof(unsigned long long) * plan.dense_groups * d.words;
+    const size_t lds = sizeof(unsigned long long) * plan.dense_groups * d.words;
+    if (plan.n_tiles && plan.lanes) {
+      // per-lane accumulation; the steps it cannot take (NULLs, non-finite values, ...) are listed for the fused
+      // kernel, which then runs over that list only (misc[8] = its length, zeroed above)
+      hyk::LaneTables lt = plan.lt;
+      for (int32_t li = 0; li < lt.n_load; ++li) lt.load_chunks[li] = d.cols[plan.lane_cols[li]].chunks;
+      HY_HIP(hipMemcpyAsync(w.lane_tables, &lt, sizeof(lt), hipMemcpyHostToDevice, s));
+      HY_HIP(hipMemcpyAsync(w.lane_terms, plan.lane_terms.data(), sizeof(hyk::LnTerm) * plan.lane_terms.size(),
+                            hipMemcpyHostToDevice, s));
+      const hyk::LanePlan lp{lt.n_load, lt.n_sums, w.lane_tables, w.lane_terms, w.deferred, w.misc + 8};
+      const size_t vlds = size_t(hyk::AGG_THREADS / hyk::WAVE) *
+                          hyk::ln_wave_lds(lt.n_load - static_cast<int>(params->n_groupby), lt.n_sums);
+      const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(plan.n_tiles, 256 * 8));
+      {
+        KTimer t("agg_dense_lanes", s, plan.rows);
+        launch_lanes(lp.n_sums, grid, vlds, s, d, lp, w.records);
+        t.done();
+      }
+      HY_HIP(hipGetLastError());
+      KTimer t("agg_dense_fused.deferred", s, 0);
+      hipLaunchKernelGGL(hyk::agg_dense_fused, dim3(256), dim3(hyk::AGG_THREADS), lds, s, d, fp, plan.dense_groups,
+                         w.records, static_cast<const uint32_t*>(w.deferred), static_cast<const uint32_t*>(w.misc + 8));
+      t.done();
+      HY_HIP(hipGetLastError());
+    } else if (plan.n_tiles) {
       const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(plan.n_tiles, 256 * 16));
       KTimer t("agg_dense_fused", s, plan.rows);
       hipLaunchKernelGGL(hyk::agg_dense_fused, dim3(grid), dim3(hyk::AGG_THREADS), lds, s, d, fp, plan.dense_groups,
-                         w.records);
+                         w.records, static_cast<const uint32_t*>(nullptr), static_cast<const uint32_t*>(nullptr));
       t.done();
       HY_HIP(hipGetLastError());
     }

@@ -178,25 +178,17 @@ __device__ __forceinline__ void fq_add_scaled(unsigned long long* limbs, int n_l
   }
 }
 
-__global__ __launch_bounds__(AGG_THREADS) void agg_dense_fused(AggDesc d, FusedPlan fp, uint32_t n_groups,
-                                                              unsigned long long* __restrict__ records) {
-  extern __shared__ unsigned long long s_recf[];
+// One step of a wave: the FQ_R * WAVE rows [base, base + FQ_R * WAVE) of input chunk c (base < the chunk's size),
+// folded into the workgroup's LDS records.
+__device__ __forceinline__ void fused_step(const AggDesc& d, const FusedPlan& fp, unsigned long long* s_recf,
+                                           uint32_t c, uint32_t base) {
   const uint32_t words = d.words;
-  const uint32_t n_words = n_groups * words;
-  for (uint32_t i = threadIdx.x; i < n_words; i += AGG_THREADS) s_recf[i] = word_init(d.word_op[i % words]);
-  __syncthreads();
   const int lane = __lane_id();
-  const int w = threadIdx.x / WAVE;
   const uint32_t H = d.n_gb;
-
-  for (uint64_t tile = blockIdx.x; tile < d.n_tiles; tile += gridDim.x) {
-    const uint32_t c = agg_tile_chunk(d, tile);
-    const uint32_t size = d.chunk_size[c];
-    const uint32_t span = static_cast<uint32_t>(tile - d.chunk_tile_begin[c]) * AGG_TILE + w * AGG_WAVE_SPAN;
-    const uint64_t row0 = d.chunk_row_begin[c];
-    for (int h = 0; h < AGG_ITEMS / FQ_R; ++h) {
-      const uint32_t base = span + h * FQ_R * WAVE;
-      if (base >= size) break;  // wave-uniform
+  const uint32_t size = d.chunk_size[c];
+  const uint64_t row0 = d.chunk_row_begin[c];
+  {
+    {
       uint32_t act = 0;
 #pragma unroll
       for (int k = 0; k < FQ_R; ++k)
@@ -509,7 +501,48 @@ __global__ __launch_bounds__(AGG_THREADS) void agg_dense_fused(AggDesc d, FusedP
           }
         }
       }
-    }  // steps of the span
+    }
+  }
+}
+
+// Step id of the deferred-step lists (agg_dense_lanes): tile * 16 + wave * 4 + step of the wave's span.
+constexpr int FQ_STEPS_PER_TILE = (AGG_THREADS / WAVE) * (AGG_ITEMS / FQ_R);
+
+// Every step of the input (steps == nullptr), or only the n_steps[0] steps listed in `steps` (the ones
+// agg_dense_lanes deferred), spread over the grid's waves.
+__global__ __launch_bounds__(AGG_THREADS) void agg_dense_fused(AggDesc d, FusedPlan fp, uint32_t n_groups,
+                                                              unsigned long long* __restrict__ records,
+                                                              const uint32_t* __restrict__ steps,
+                                                              const uint32_t* __restrict__ n_steps) {
+  extern __shared__ unsigned long long s_recf[];
+  const uint32_t words = d.words;
+  const uint32_t n_words = n_groups * words;
+  for (uint32_t i = threadIdx.x; i < n_words; i += AGG_THREADS) s_recf[i] = word_init(d.word_op[i % words]);
+  __syncthreads();
+  const int w = threadIdx.x / WAVE;
+  if (steps == nullptr) {
+    for (uint64_t tile = blockIdx.x; tile < d.n_tiles; tile += gridDim.x) {
+      const uint32_t c = agg_tile_chunk(d, tile);
+      const uint32_t size = d.chunk_size[c];
+      const uint32_t span = static_cast<uint32_t>(tile - d.chunk_tile_begin[c]) * AGG_TILE + w * AGG_WAVE_SPAN;
+      for (int h = 0; h < AGG_ITEMS / FQ_R; ++h) {
+        const uint32_t base = span + h * FQ_R * WAVE;
+        if (base >= size) break;  // wave-uniform
+        fused_step(d, fp, s_recf, c, base);
+      }
+    }
+  } else {
+    const uint32_t n = *n_steps;
+    const uint32_t waves = gridDim.x * (AGG_THREADS / WAVE);
+    for (uint32_t i = blockIdx.x * (AGG_THREADS / WAVE) + w; i < n; i += waves) {
+      const uint32_t id = steps[i];
+      const uint64_t tile = id / FQ_STEPS_PER_TILE;
+      const uint32_t r = id % FQ_STEPS_PER_TILE;
+      const uint32_t c = agg_tile_chunk(d, tile);
+      const uint32_t base = static_cast<uint32_t>(tile - d.chunk_tile_begin[c]) * AGG_TILE +
+                            (r / (AGG_ITEMS / FQ_R)) * AGG_WAVE_SPAN + (r % (AGG_ITEMS / FQ_R)) * FQ_R * WAVE;
+      fused_step(d, fp, s_recf, c, base);
+    }
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < n_words; i += AGG_THREADS) {

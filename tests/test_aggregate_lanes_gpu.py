@@ -1,0 +1,240 @@
+"""agg_dense_lanes (csrc/kernels/aggregate_lanes.hip): the dense Aggregate accumulating per lane, with the Projection's
++ - * expressions evaluated as chains - TPC-H 1's SUM / AVG / COUNT shape (reference projection.cpp:39-87 feeding
+aggregate.cpp:133-249). Every case runs hy_aggregate twice - lanes path (default) and HY_AGG_LANES=0 (agg_dense_fused
+over every step) - and checks both against numpy: float32 expressions as the reference's functors compute them,
+counts exact, float SUM / AVG equal to the exactly rounded sum (math.fsum), int32 sums exact. The data cases drive the
+kernel's exits: clean Q1-shaped columns (every step on the lanes path), NULLs, tiny / huge / non-finite / denormal
+values, negative and zero values (steps deferred to agg_dense_fused or re-based), more groups than a wave's table,
+int32 sums and COUNT(col); data and reference inputs (PosLists into one chunk, and mixing chunks)."""
+import ctypes
+import math
+import zlib
+
+import numpy as np
+import pytest
+
+import device_tables as dt
+
+pytestmark = pytest.mark.gpu
+
+N, CHUNK = 60_000, 9_000
+
+# [rf, ls, qty, price, dp = price * (1 - disc), ch = dp * (1 + tax), disc, tax, iq (int32), iexpr = iq * 3 - 7 (int32)]
+AGGS = [("SUM", 2), ("SUM", 3), ("SUM", 4), ("SUM", 5), ("AVG", 2), ("AVG", 3), ("AVG", 6), ("COUNT", -1),
+        ("SUM", 8), ("AVG", 9), ("COUNT", 7)]
+
+
+def columns(rng, case):
+    rf_dom, ls_dom = (8, 4) if case == "many_groups" else (3, 2)
+    rf = rng.integers(0, rf_dom, N).astype(np.int32)
+    ls = rng.integers(0, ls_dom, N).astype(np.int32)
+    if case == "clustered":  # one group per 5000 rows: the table refills as codes change
+        rf = ((np.arange(N) // 5000) % 3).astype(np.int32)
+        ls = ((np.arange(N) // 7000) % 2).astype(np.int32)
+    qty = rng.integers(1, 51, N).astype(np.float32)
+    price = (rng.integers(90_000, 210_001, N) * qty.astype(np.int64) / 100.0).astype(np.float32)
+    disc = (rng.integers(0, 11, N) / 100.0).astype(np.float32)
+    tax = (rng.integers(0, 9, N) / 100.0).astype(np.float32)
+    iq = rng.integers(-1000, 1000, N).astype(np.int32)
+    price_n = np.zeros(N, np.uint8)
+    disc_n = np.zeros(N, np.uint8)
+    if case == "nulls":
+        price_n = (rng.random(N) < 0.002).astype(np.uint8)
+        disc_n = (rng.random(N) < 0.001).astype(np.uint8)
+    elif case == "odd_values":  # steps leave the window / hold non-finite, denormal, negative, zero values
+        price[rng.random(N) < 0.0005] = np.float32(-3.5e-30)
+        price[rng.random(N) < 0.0005] = np.float32(7.0e25)
+        price[rng.random(N) < 0.0002] = np.float32(1.0e-41)  # denormal
+        price[rng.random(N) < 0.001] = np.float32(0.0)
+        price[rng.random(N) < 0.001] *= np.float32(-1)
+        qty[rng.random(N) < 0.0001] = np.float32(np.inf)
+    elif case == "wide_range":  # every step spans more binades than one window: re-based or deferred steps
+        price = (rng.standard_normal(N) * np.exp2(rng.integers(-40, 40, N))).astype(np.float32)
+    elif case == "drift":  # magnitudes drift upwards chunk by chunk: re-bases as the largest exponent grows
+        price = (price * np.exp2(np.arange(N) // 3000)).astype(np.float32)
+    return rf, ls, qty, price, disc, tax, iq, price_n, disc_n, (rf_dom, ls_dom)
+
+
+def expected(cols, rows):
+    rf, ls, qty, price, disc, tax, iq, price_n, disc_n, _ = cols
+    one = np.float32(1)
+    with np.errstate(all="ignore"):
+        dp = (price * (one - disc)).astype(np.float32)
+        ch = (dp * (one + tax)).astype(np.float32)
+    ie = (iq.astype(np.int64) * 3 - 7).astype(np.int32)
+    dp_null = (price_n | disc_n).astype(bool)
+    out = {}
+    for r in rows:
+        g = (int(rf[r]), int(ls[r]))
+        e = out.setdefault(g, {"rows": 0, 2: [], 3: [], 4: [], 5: [], 6: [], 7: 0, 8: [], 9: []})
+        e["rows"] += 1
+        e[2].append(float(qty[r]))
+        e[8].append(int(iq[r]))
+        e[9].append(int(ie[r]))
+        if not price_n[r]:
+            e[3].append(float(price[r]))
+        if not dp_null[r]:
+            e[4].append(float(dp[r]))
+            e[5].append(float(ch[r]))
+        if not disc_n[r]:
+            e[6].append(float(disc[r]))
+        e[7] += 1  # tax has no NULLs
+    return out
+
+
+def fsum_inf(vals):
+    if any(math.isnan(v) for v in vals) or (any(v == math.inf for v in vals) and any(v == -math.inf for v in vals)):
+        return math.nan
+    if any(math.isinf(v) for v in vals):
+        return next(v for v in vals if math.isinf(v))
+    return math.fsum(vals)
+
+
+def run(hy, dcols, pos_lists, sizes, doms):
+    capi, L = hy.capi, hy.capi.lib
+    I32, F32 = capi.HY_TYPE_INT32, capi.HY_TYPE_FLOAT
+    N_ = capi.ExprNode
+    col = lambda j, t=F32: N_(capi.HY_EXPR_COLUMN, t, 0, j, 0)
+    one = N_(capi.HY_EXPR_VALUE, I32, 0, 0, 1)
+    dp = [col(3), one, col(6), N_(capi.HY_EXPR_SUB, F32, F32, 0, 0), N_(capi.HY_EXPR_MUL, F32, F32, 0, 0)]
+    ch = dp + [one, col(7), N_(capi.HY_EXPR_ADD, F32, F32, 0, 0), N_(capi.HY_EXPR_MUL, F32, F32, 0, 0)]
+    ie = [col(8, I32), N_(capi.HY_EXPR_VALUE, I32, 0, 0, 3), N_(capi.HY_EXPR_MUL, I32, I32, 0, 0),
+          N_(capi.HY_EXPR_VALUE, I32, 0, 0, 7), N_(capi.HY_EXPR_SUB, I32, I32, 0, 0)]
+    progs = [(N_ * len(p))(*p) for p in (dp, ch, ie)]
+    n_chunks = len(sizes)
+    ac = (capi.AggColumn * 10)()
+    pg = 0 if pos_lists is not None else -1
+    specs = {0: (I32, dcols[0], doms[0]), 1: (I32, dcols[1], doms[1]), 2: (F32, dcols[2], 0),
+             3: (F32, dcols[3], 0), 6: (F32, dcols[4], 0), 7: (F32, dcols[5], 0), 8: (I32, dcols[6], 0)}
+    keep = []
+    for j, (vt, c, dom) in specs.items():
+        arr = (capi.ColumnChunk * len(c.descs))(*c.descs)
+        keep.append(arr)
+        ac[j].value_type, ac[j].pos_group, ac[j].chunks, ac[j].n_chunks, ac[j].domain = vt, pg, arr, len(c.descs), dom
+    for j, p, t in ((4, progs[0], F32), (5, progs[1], F32), (9, progs[2], I32)):
+        ac[j].value_type, ac[j].pos_group, ac[j].program, ac[j].n_nodes = t, -1, p, len(p)
+    csz = (ctypes.c_uint32 * n_chunks)(*sizes)
+    pls = (ctypes.c_void_p * max(1, n_chunks))(*([p.ptr.value for p in pos_lists] if pos_lists is not None else []))
+    inp = capi.AggInput(n_chunks, csz, pls if pos_lists is not None else None, 1 if pos_lists is not None else 0,
+                        ac, 10)
+    gb = (ctypes.c_int32 * 2)(0, 1)
+    defs = (capi.AggDef * len(AGGS))(*[capi.AggDef(getattr(capi, "HY_AGG_" + f), c) for f, c in AGGS])
+    prm = capi.AggParams(gb, 2, defs, len(AGGS), 0)
+    lay = capi.AggLayout()
+    capi.check(L.hy_aggregate_layout(ctypes.byref(inp), ctypes.byref(prm), ctypes.byref(lay)), "layout")
+    assert lay.dense == 1
+    wsb = ctypes.c_size_t()
+    capi.check(L.hy_aggregate_workspace_size(ctypes.byref(inp), ctypes.byref(prm), ctypes.byref(wsb)), "ws")
+    ws = capi.DeviceArray(np.zeros(wsb.value, np.uint8))
+    out = capi.DeviceArray(np.zeros(64 * lay.words, np.uint64))
+    ng = ctypes.c_uint64()
+    capi.check(L.hy_aggregate(ctypes.byref(inp), ctypes.byref(prm), out.ptr, 64, ctypes.byref(ng), ws.ptr, wsb.value,
+                              None), "hy_aggregate")
+    rec = out.fetch().reshape(-1, lay.words)[:ng.value]
+    res = {}
+    for r in rec:
+        g = (int(r[0]), int(r[1]))
+        vals = {"rows": int(r[2 + 3])}
+        for a, (f, c) in enumerate(AGGS):
+            wd = lay.agg_word[a]
+            if c < 0:
+                continue
+            if f == "COUNT":
+                vals[a] = int(r[wd])
+            elif lay.agg_limbs[a] == 0:  # int32 input: int64 sum
+                vals[a] = (int(r[wd]), int(np.array([r[wd + 1]], np.uint64).view(np.int64)[0]))
+            else:
+                limbs = (ctypes.c_uint64 * lay.agg_limbs[a])(*[int(x) for x in r[wd + 2:wd + 2 + lay.agg_limbs[a]]])
+                sm = ctypes.c_double()
+                capi.check(L.hy_agg_float_sum(limbs, lay.agg_limbs[a], lay.agg_emin[a], int(r[wd + 1]),
+                                              ctypes.byref(sm)))
+                vals[a] = (int(r[wd]), sm.value)
+        res[g] = vals
+    return res
+
+
+def same_float(a, b):
+    return (math.isnan(a) and math.isnan(b)) or a == b
+
+
+def check(res, exp):
+    assert set(res) == set(exp)
+    for g, e in exp.items():
+        r = res[g]
+        assert r["rows"] == e["rows"], g
+        for a, (f, c) in enumerate(AGGS):
+            if c < 0:
+                continue
+            if f == "COUNT":
+                assert r[a] == (e[c] if c == 7 else len(e[c])), (g, f, c)
+                continue
+            vals = e[c]
+            assert r[a][0] == len(vals), (g, f, c)
+            if c in (8, 9):
+                assert r[a][1] == sum(vals), (g, f, c)
+            else:
+                assert same_float(r[a][1], fsum_inf(vals)), (g, f, c, r[a][1], fsum_inf(vals))
+
+
+def kernels_ran(L):
+    n = ctypes.c_uint32()
+    L.hy_kernel_stats_collect(ctypes.byref(n))
+    names = set()
+    for i in range(n.value):
+        nm, la, ms = ctypes.c_char_p(), ctypes.c_uint64(), ctypes.c_double()
+        un = ctypes.c_uint64()
+        L.hy_kernel_stats_get(i, ctypes.byref(nm), ctypes.byref(la), ctypes.byref(ms), ctypes.byref(un))
+        names.add(nm.value.decode())
+    return names
+
+
+@pytest.mark.parametrize("case", ["clean", "nulls", "odd_values", "wide_range", "drift", "many_groups", "clustered"])
+@pytest.mark.parametrize("input_kind", ["data", "reference", "reference_mixed"])
+def test_lanes_path(hy, monkeypatch, case, input_kind):
+    capi = hy.capi
+    L = capi.lib
+    rng = np.random.default_rng(zlib.crc32(f"lanes/{case}/{input_kind}".encode()))
+    cols = columns(rng, case)
+    rf, ls, qty, price, disc, tax, iq, price_n, disc_n, doms = cols
+    dcols = [dt.DeviceColumn(capi, rf, None, CHUNK, "Dictionary"), dt.DeviceColumn(capi, ls, None, CHUNK, "Dictionary"),
+             dt.DeviceColumn(capi, qty, None, CHUNK, "Dictionary"),
+             dt.DeviceColumn(capi, price, price_n, CHUNK, "Dictionary" if case == "nulls" else "Unencoded"),
+             dt.DeviceColumn(capi, disc, disc_n, CHUNK, "Dictionary"), dt.DeviceColumn(capi, tax, None, CHUNK,
+                                                                                       "Dictionary"),
+             dt.DeviceColumn(capi, iq, None, CHUNK, "Unencoded")]
+    n_chunks = dcols[0].n_chunks
+    if input_kind == "data":
+        rows = list(range(N))
+        pos, sizes = None, [dcols[0].chunk_size(c) for c in range(n_chunks)]
+    else:
+        pos, sizes, rows = [], [], []
+        for c in range(n_chunks):
+            offs = np.nonzero(rng.random(dcols[0].chunk_size(c)) < 0.7)[0].astype(np.uint32)
+            if input_kind == "reference_mixed":  # this chunk's PosList also references the next chunk
+                nxt = (c + 1) % n_chunks
+                more = np.nonzero(rng.random(dcols[0].chunk_size(nxt)) < 0.05)[0].astype(np.uint32)
+                ids = np.concatenate([np.full(offs.size, c, np.uint32), np.full(more.size, nxt, np.uint32)])
+                offs = np.concatenate([offs, more])
+                order = np.argsort(rng.random(ids.size) + np.where(ids == c, 0.0, 0.3), kind="stable")
+                ids, offs = ids[order], offs[order]
+            else:
+                ids = np.full(offs.size, c, np.uint32)
+            pl = np.stack([ids, offs], axis=1).astype(np.uint32)
+            pos.append(capi.DeviceArray(pl.reshape(-1) if pl.size else np.zeros(2, np.uint32)))
+            sizes.append(pl.shape[0])
+            rows += [int(i) * CHUNK + int(o) for i, o in zip(ids, offs)]
+    exp = expected(cols, rows)
+    L.hy_kernel_stats_enable(1)
+    L.hy_kernel_stats_reset()
+    res_lanes = run(hy, dcols, pos, sizes, doms)
+    ran = kernels_ran(L)
+    L.hy_kernel_stats_enable(0)
+    assert "agg_dense_lanes" in ran, ran
+    check(res_lanes, exp)
+    monkeypatch.setenv("HY_AGG_LANES", "0")
+    res_fused = run(hy, dcols, pos, sizes, doms)
+    check(res_fused, exp)
+    assert res_lanes == res_fused or all(
+        all(same_float(x[1], y[1]) if isinstance(x, tuple) else x == y for x, y in zip(res_lanes[g].values(),
+                                                                                       res_fused[g].values()))
+        for g in res_lanes)
