@@ -364,13 +364,31 @@ uint64_t group_bound_of(const hy_agg_input* in, const hy_agg_params* p, uint64_t
 
 inline uint32_t p_groupby(const hy_agg_params* p) { return p->n_groupby; }
 
-// agg_dense_lanes<n_sums>
-void launch_lanes(int n_sums, uint32_t grid, size_t lds, hipStream_t s, const hyk::AggDesc& d,
+// agg_dense_lanes<n_sums> on a persistent grid: as many workgroups as are resident at once (more would leave a
+// partly filled last round of workgroups - each works through many tiles in turn).
+template <int N>
+void launch_lanes_n(uint64_t n_tiles, size_t lds, hipStream_t s, const hyk::AggDesc& d, const hyk::LanePlan& lp,
+                    unsigned long long* records) {
+  static int resident = 0;  // per instantiation; LDS per workgroup is small next to the VGPR limit
+  if (resident == 0) {
+    int per_cu = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hyk::agg_dense_lanes<N>, hyk::AGG_THREADS, lds) !=
+            hipSuccess ||
+        hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      per_cu = 3, cus = 256;
+    resident = std::max(1, per_cu) * std::max(1, cus);
+  }
+  const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(n_tiles, static_cast<uint64_t>(resident)));
+  hipLaunchKernelGGL(hyk::agg_dense_lanes<N>, dim3(grid), dim3(hyk::AGG_THREADS), lds, s, d, lp, records);
+}
+
+void launch_lanes(int n_sums, uint64_t n_tiles, size_t lds, hipStream_t s, const hyk::AggDesc& d,
                   const hyk::LanePlan& lp, unsigned long long* records) {
   switch (n_sums) {
-#define HY_LANES_CASE(N)                                                                                         \
-  case N:                                                                                                        \
-    hipLaunchKernelGGL(hyk::agg_dense_lanes<N>, dim3(grid), dim3(hyk::AGG_THREADS), lds, s, d, lp, records); \
+#define HY_LANES_CASE(N)                                    \
+  case N:                                                   \
+    launch_lanes_n<N>(n_tiles, lds, s, d, lp, records);     \
     break;
     HY_LANES_CASE(0)
     HY_LANES_CASE(1)
@@ -723,10 +741,9 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
       const hyk::LanePlan lp{lt.n_load, lt.n_sums, w.lane_tables, w.lane_terms, w.deferred, w.misc + 8};
       const size_t vlds = size_t(hyk::AGG_THREADS / hyk::WAVE) *
                           hyk::ln_wave_lds(lt.n_load - static_cast<int>(params->n_groupby), lt.n_sums);
-      const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(plan.n_tiles, 256 * 8));
       {
         KTimer t("agg_dense_lanes", s, plan.rows);
-        launch_lanes(lp.n_sums, grid, vlds, s, d, lp, w.records);
+        launch_lanes(lp.n_sums, plan.n_tiles, vlds, s, d, lp, w.records);
         t.done();
       }
       HY_HIP(hipGetLastError());

@@ -85,7 +85,7 @@ struct LanePlan {
 // Per-wave LDS of agg_dense_lanes: the step's loaded values (read by the chains at run-time column indices), the
 // flush's staging of one group's lane partial sums, and the per-group rows / first / last row (updated by lane 0).
 struct LnHeader {
-  unsigned long long rows, first, last, pad;
+  unsigned long long rows, first, last, pad;  // rows: unused (the lanes count them)
 };
 __host__ __device__ inline size_t ln_wave_lds(int n_store, int n_sums) {
   return size_t(n_store) * WAVE * 16 + size_t(n_sums) * WAVE * 8 + LN_GROUPS * sizeof(LnHeader) + LN_SUMS * 4;
@@ -122,6 +122,29 @@ __device__ __forceinline__ void ln_apply(int32_t op, bool fl, const uint32_t (&a
   }
 }
 
+// Read-only, wave-uniform data (the plan's tables and terms, the chunk descriptors) read through the constant address
+// space: scalar loads. Through a generic pointer the compiler cannot rule out the kernel's own stores and emits
+// vector loads with VGPR address arithmetic (~170 loads per step).
+template <class X>
+using ln_cptr = const __attribute__((address_space(4))) X*;
+template <class X>
+__device__ __forceinline__ ln_cptr<X> ln_const(const X* p) {
+  return (ln_cptr<X>)(p);
+}
+
+// Column data in the global address space: global loads with a uniform (SGPR) base and 32-bit lane offsets instead
+// of flat loads with 64-bit VGPR addresses.
+using ln_gword = const __attribute__((address_space(1))) uint32_t*;
+__device__ __forceinline__ uint32_t ln_load_word(uintptr_t base, uint32_t byte_off) {
+  return *reinterpret_cast<ln_gword>(base + byte_off);
+}
+// Element `i` of a 1-, 2- or 4-byte wide array (wave-uniform width), zero-extended.
+__device__ __forceinline__ uint32_t ln_load_elem(uintptr_t base, uint32_t i, uint32_t width) {
+  if (width == 1) return *reinterpret_cast<const __attribute__((address_space(1))) uint8_t*>(base + i);
+  if (width == 2) return *reinterpret_cast<const __attribute__((address_space(1))) uint16_t*>(base + 2ull * i);
+  return *reinterpret_cast<ln_gword>(base + 4ull * i);
+}
+
 __device__ __forceinline__ uint64_t ln_uniform64(uint64_t v) {
   const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
   const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
@@ -137,13 +160,13 @@ constexpr uint32_t LN_NO_ROW = 0xFFFFFFFEu;  // group code of inactive rows: mat
 // Folds a wave's lane partial sums and its per-entry rows / first / last into the group records; keeps the table.
 template <int NS, int NA>
 __device__ __forceinline__ void ln_flush(const AggDesc& d, const LanePlan& lp, unsigned long long* records,
-                                         double (&acc)[LN_GROUPS][NA], const int32_t (&tab)[LN_GROUPS],
-                                         const int32_t (&fbase)[NA], double* stage, LnHeader* hdr, int32_t* sbase,
-                                         uint32_t* since) {
+                                         double (&acc)[LN_GROUPS][NA], uint32_t (&cnt)[LN_GROUPS],
+                                         const int32_t (&tab)[LN_GROUPS], const int32_t (&fbase)[NA], double* stage,
+                                         LnHeader* hdr, int32_t* sbase, uint32_t* first_set, uint32_t* since) {
   const int lane = __lane_id();
   const uint32_t H = d.n_gb;
   const uint32_t words = d.words;
-  const LaneTables* T = lp.t;
+  const ln_cptr<LaneTables> T = ln_const(lp.t);
   if (lane == 0) {
 #pragma unroll
     for (int s = 0; s < NS; ++s) sbase[s] = fbase[s];
@@ -152,13 +175,15 @@ __device__ __forceinline__ void ln_flush(const AggDesc& d, const LanePlan& lp, u
   for (int j = 0; j < LN_GROUPS; ++j) {
     if (tab[j] < 0) continue;
     unsigned long long* rec = records + static_cast<uint64_t>(tab[j]) * words;
+    const unsigned long long rows = fq_wave_sum(cnt[j]);
+    cnt[j] = 0;
     if (lane == 0) {
       const LnHeader hd = hdr[j];
-      if (hd.rows) {
-        atomicAdd(rec + H + AGG_HDR_ROWS, hd.rows);
+      if (rows) {
+        atomicAdd(rec + H + AGG_HDR_ROWS, rows);
         atomicMin(rec + H + AGG_HDR_FIRST, hd.first);
         atomicMax(rec + H + AGG_HDR_LAST, hd.last);
-        for (int f = 0; f < T->n_cnt; ++f) atomicAdd(rec + T->cnt_word[f], hd.rows);  // non-NULL counts
+        for (int f = 0; f < T->n_cnt; ++f) atomicAdd(rec + T->cnt_word[f], rows);  // non-NULL counts
       }
       hdr[j] = LnHeader{0, ~0ull, 0, 0};
     }
@@ -186,6 +211,7 @@ __device__ __forceinline__ void ln_flush(const AggDesc& d, const LanePlan& lp, u
       }
     }
   }
+  *first_set = 0;
   *since = 0;
 }
 
@@ -198,7 +224,7 @@ __device__ __forceinline__ bool ln_window_ok(const LanePlan& lp, const uint32_t 
   bool ok = true;
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    if (lp.t->sum_kind[s] != LN_SUM_FLOAT) continue;
+    if (ln_const(lp.t)->sum_kind[s] != LN_SUM_FLOAT) continue;
     if (fbase[s] < 0) {
       uint32_t em = 0;
 #pragma unroll
@@ -225,7 +251,8 @@ __device__ __forceinline__ bool ln_window_ok(const LanePlan& lp, const uint32_t 
 }
 
 template <int NS>
-__global__ __launch_bounds__(AGG_THREADS) void agg_dense_lanes(AggDesc d, LanePlan lp,
+// 3 waves per SIMD (<= 168 VGPRs): measured best on MI355X - 4 spills, 2 leaves too little latency hiding.
+__global__ __launch_bounds__(AGG_THREADS) __attribute__((amdgpu_waves_per_eu(3))) void agg_dense_lanes(AggDesc d, LanePlan lp,
                                                               unsigned long long* __restrict__ records) {
   constexpr int NA = NS > 0 ? NS : 1;
   extern __shared__ __align__(16) unsigned char s_lanes[];
@@ -238,15 +265,19 @@ __global__ __launch_bounds__(AGG_THREADS) void agg_dense_lanes(AggDesc d, LanePl
   double* stage = reinterpret_cast<double*>(vals + n_store * WAVE);  // [sum][lane]
   LnHeader* hdr = reinterpret_cast<LnHeader*>(stage + NS * WAVE);    // [table entry]
   int32_t* sbase = reinterpret_cast<int32_t*>(hdr + LN_GROUPS);       // [sum]
-  const LaneTables* T = lp.t;
+  const ln_cptr<LaneTables> T = ln_const(lp.t);
+  const ln_cptr<LnTerm> terms = ln_const(lp.terms);
   if (lane < LN_GROUPS) hdr[lane] = LnHeader{0, ~0ull, 0, 0};
 
   double acc[LN_GROUPS][NA];
+  uint32_t cnt[LN_GROUPS];  // the lane's rows per table entry
   int32_t tab[LN_GROUPS];
   int32_t fbase[NA];
+  uint32_t first_set = 0;   // bit j: hdr[j].first holds the flush period's first row of entry j
 #pragma unroll
   for (int j = 0; j < LN_GROUPS; ++j) {
     tab[j] = -1;
+    cnt[j] = 0;
 #pragma unroll
     for (int s = 0; s < NA; ++s) acc[j][s] = 0.0;
   }
@@ -271,10 +302,15 @@ __global__ __launch_bounds__(AGG_THREADS) void agg_dense_lanes(AggDesc d, LanePl
       uint32_t off[FQ_R];
       uint32_t cc = c;
       if (d.n_pos_groups) {
-        const hy_row_id* pl = d.pos_lists[c];
+        const uintptr_t pl = reinterpret_cast<uintptr_t>(ln_const(d.pos_lists)[c]);
         hy_row_id rid[FQ_R];
 #pragma unroll
-        for (int k = 0; k < FQ_R; ++k) rid[k] = pl[min(base + k * WAVE + lane, size - 1)];
+        for (int k = 0; k < FQ_R; ++k) {
+          const uint32_t i = min(base + k * WAVE + lane, size - 1);
+          const unsigned long long q = *reinterpret_cast<const __attribute__((address_space(1))) unsigned long long*>(
+              pl + 8ull * i);
+          rid[k] = hy_row_id{static_cast<uint32_t>(q), static_cast<uint32_t>(q >> 32)};
+        }
         cc = __builtin_amdgcn_readfirstlane(rid[0].chunk_id);
         bool same = true;
 #pragma unroll
@@ -290,18 +326,16 @@ __global__ __launch_bounds__(AGG_THREADS) void agg_dense_lanes(AggDesc d, LanePl
 #pragma unroll
         for (int k = 0; k < FQ_R; ++k) off[k] = ((act >> k) & 1u) ? base + k * WAVE + lane : 0u;
       }
-      // loads: every column's 4-byte word holding the row's value / vid first (one batch in flight), then vids ->
-      // dictionary values
+      // loads: every column's value / vid first (one batch in flight), then vids -> dictionary values
       uint32_t raw[LN_COLS][FQ_R];
 #pragma unroll
       for (int li = 0; li < LN_COLS; ++li) {
         if (li >= lp.n_load) break;
-        const hy_column_chunk& ch = T->load_chunks[li][cc];
+        const auto& ch = ln_const(T->load_chunks[li])[cc];
         const uint32_t wb = ch.kind == HY_COL_DICT ? static_cast<uint32_t>(ch.vid_width) : 4u;
         const uintptr_t p0 = reinterpret_cast<uintptr_t>(ch.data);
 #pragma unroll
-        for (int k = 0; k < FQ_R; ++k)
-          raw[li][k] = *reinterpret_cast<const uint32_t*>((p0 + static_cast<uintptr_t>(off[k]) * wb) & ~uintptr_t(3));
+        for (int k = 0; k < FQ_R; ++k) raw[li][k] = ln_load_elem(p0, off[k], wb);
       }
       uint32_t g[FQ_R] = {0, 0, 0, 0};
       uint32_t nulls = 0;  // rows with a NULL in a non-group-by column
@@ -309,34 +343,25 @@ __global__ __launch_bounds__(AGG_THREADS) void agg_dense_lanes(AggDesc d, LanePl
 #pragma unroll
       for (int li = 0; li < LN_COLS; ++li) {
         if (li >= lp.n_load) break;
-        const hy_column_chunk& ch = T->load_chunks[li][cc];
+        const auto& ch = ln_const(T->load_chunks[li])[cc];
         const bool dict = ch.kind == HY_COL_DICT;
-        const uint32_t wb = dict ? static_cast<uint32_t>(ch.vid_width) : 4u;
-        const uint32_t mask = wb == 4 ? 0xFFFFFFFFu : (1u << (8 * wb)) - 1u;
-        const uintptr_t p0 = reinterpret_cast<uintptr_t>(ch.data);
         uint32_t v[FQ_R];
         uint32_t nl = 0;
 #pragma unroll
-        for (int k = 0; k < FQ_R; ++k) {
-          const uint32_t sh = static_cast<uint32_t>((p0 + static_cast<uintptr_t>(off[k]) * wb) & 3u) * 8u;
-          v[k] = (raw[li][k] >> sh) & mask;
-        }
+        for (int k = 0; k < FQ_R; ++k) v[k] = raw[li][k];
         if (dict) {
-          const uint32_t* dv = static_cast<const uint32_t*>(ch.dictionary);
+          const uintptr_t dv = reinterpret_cast<uintptr_t>(ch.dictionary);
 #pragma unroll
           for (int k = 0; k < FQ_R; ++k) {
             const bool isnull = v[k] >= ch.dictionary_size;
             if (isnull) nl |= 1u << k;
-            v[k] = dv[isnull ? 0u : v[k]];
+            v[k] = ln_load_word(dv, (isnull ? 0u : v[k]) * 4u);
           }
         } else if (ch.nulls != nullptr) {  // nullable value column: its NULL flag bytes
           const uintptr_t n0 = reinterpret_cast<uintptr_t>(ch.nulls);
 #pragma unroll
-          for (int k = 0; k < FQ_R; ++k) {
-            const uintptr_t pb = n0 + off[k];
-            const uint32_t word = *reinterpret_cast<const uint32_t*>(pb & ~uintptr_t(3));
-            if ((word >> ((pb & 3u) * 8u)) & 0xFFu) nl |= 1u << k;
-          }
+          for (int k = 0; k < FQ_R; ++k)
+            if (ln_load_elem(n0, off[k], 1)) nl |= 1u << k;
         }
         if (li < FQ_MAX_GB && static_cast<uint32_t>(li) < H) {
           const uint32_t domain = T->gb_domain[li < FQ_MAX_GB ? li : 0];
@@ -389,7 +414,7 @@ __global__ __launch_bounds__(AGG_THREADS) void agg_dense_lanes(AggDesc d, LanePl
           }
           uint64_t need = present & ~have;
           if (__popcll(need) > free_slots) {  // flush and refill
-            ln_flush<NS, NA>(d, lp, records, acc, tab, fbase, stage, hdr, sbase, &since);
+            ln_flush<NS, NA>(d, lp, records, acc, cnt, tab, fbase, stage, hdr, sbase, &first_set, &since);
 #pragma unroll
             for (int j = 0; j < LN_GROUPS; ++j) tab[j] = -1;
             need = present;
@@ -415,7 +440,14 @@ __global__ __launch_bounds__(AGG_THREADS) void agg_dense_lanes(AggDesc d, LanePl
         const int t0 = T->sum_first[s], tn = T->sum_len[s];
 #pragma unroll 1
         for (int t = 0; t < tn; ++t) {
-          const LnTerm tm = lp.terms[t0 + t];
+          LnTerm tm;  // field by field (a constant-address-space struct has no copy constructor)
+          tm.kind = terms[t0 + t].kind;
+          tm.op = terms[t0 + t].op;
+          tm.col = terms[t0 + t].col;
+          tm.lit = terms[t0 + t].lit;
+          tm.cvt = terms[t0 + t].cvt;
+          tm.comb = terms[t0 + t].comb;
+          tm.rev = terms[t0 + t].rev;
           uint32_t x[FQ_R];
           if (tm.kind == LN_TERM_LIT) {
 #pragma unroll
@@ -451,7 +483,7 @@ __global__ __launch_bounds__(AGG_THREADS) void agg_dense_lanes(AggDesc d, LanePl
       bool hard = false;
       if (!ln_window_ok<NS, NA>(lp, r, act, fbase, &hard) && !hard) {
         // re-base: flush, drop the bases and take them from this step
-        ln_flush<NS, NA>(d, lp, records, acc, tab, fbase, stage, hdr, sbase, &since);
+        ln_flush<NS, NA>(d, lp, records, acc, cnt, tab, fbase, stage, hdr, sbase, &first_set, &since);
 #pragma unroll
         for (int s = 0; s < NA; ++s) fbase[s] = -1;
         if (!ln_window_ok<NS, NA>(lp, r, act, fbase, &hard)) hard = true;
@@ -460,7 +492,8 @@ __global__ __launch_bounds__(AGG_THREADS) void agg_dense_lanes(AggDesc d, LanePl
         ln_defer(lp, step_id);
         continue;
       }
-      // accumulate: row k's values into its group's lane accumulators (one branch per table entry)
+      // accumulate: acc[j][s] = fma(m, x, acc[j][s]) with m = 1.0 for the rows of entry j, else 0.0 - exactly the
+      // (exact, see above) sum, without a branch per entry; the lane's row counts likewise
 #pragma unroll
       for (int k = 0; k < FQ_R; ++k) {
         double xv[NA];
@@ -470,37 +503,37 @@ __global__ __launch_bounds__(AGG_THREADS) void agg_dense_lanes(AggDesc d, LanePl
                                   : static_cast<double>(static_cast<int32_t>(r[s][k]));
 #pragma unroll
         for (int j = 0; j < LN_GROUPS; ++j) {
-          if (tab[j] >= 0 && g[k] == static_cast<uint32_t>(tab[j])) {
+          const bool in = g[k] == static_cast<uint32_t>(tab[j]);  // empty entries (-1) match no row
+          const double m = static_cast<double>(static_cast<uint32_t>(in));  // (a select would become select + add)
+          cnt[j] += in ? 1u : 0u;
 #pragma unroll
-            for (int s = 0; s < NS; ++s) acc[j][s] += xv[s];
-          }
+          for (int s = 0; s < NS; ++s) acc[j][s] = __builtin_fma(m, xv[s], acc[j][s]);
         }
       }
-      // rows, first and last row per entry (ballots; row k * 64 + lane of the step); lane 0 keeps them in LDS
+      // first row (once per flush period) and last row per entry; lane 0 keeps them in LDS
 #pragma unroll
       for (int j = 0; j < LN_GROUPS; ++j) {
         if (tab[j] < 0) continue;
-        uint64_t n = 0, fr = ~0ull, ls = 0;
+        uint64_t mk[FQ_R];
 #pragma unroll
-        for (int k = 0; k < FQ_R; ++k) {
-          const uint64_t m = __ballot(g[k] == static_cast<uint32_t>(tab[j]));
-          if (m) {
-            const uint64_t r0 = row0 + base + k * WAVE;
-            n += __popcll(m);
-            fr = min(fr, r0 + __builtin_ctzll(m));
-            ls = r0 + 63 - __builtin_clzll(m);
-          }
-        }
-        if (n && lane == 0) {
-          atomicAdd(&hdr[j].rows, static_cast<unsigned long long>(n));
-          atomicMin(&hdr[j].first, static_cast<unsigned long long>(fr));
-          atomicMax(&hdr[j].last, static_cast<unsigned long long>(ls));
+        for (int k = 0; k < FQ_R; ++k) mk[k] = __ballot(g[k] == static_cast<uint32_t>(tab[j]));
+        if ((mk[0] | mk[1] | mk[2] | mk[3]) == 0) continue;
+        const uint64_t rb = row0 + base;
+        const int kl = mk[3] ? 3 : mk[2] ? 2 : mk[1] ? 1 : 0;
+        const uint64_t ml = mk[3] ? mk[3] : mk[2] ? mk[2] : mk[1] ? mk[1] : mk[0];
+        const uint64_t ls = rb + kl * WAVE + 63 - __builtin_clzll(ml);
+        if (lane == 0) atomicMax(&hdr[j].last, static_cast<unsigned long long>(ls));
+        if (!((first_set >> j) & 1u)) {
+          const int kf = mk[0] ? 0 : mk[1] ? 1 : mk[2] ? 2 : 3;
+          const uint64_t mf = mk[0] ? mk[0] : mk[1] ? mk[1] : mk[2] ? mk[2] : mk[3];
+          if (lane == 0) atomicMin(&hdr[j].first, static_cast<unsigned long long>(rb + kf * WAVE + __builtin_ctzll(mf)));
+          first_set |= 1u << j;
         }
       }
-      if (++since >= LN_FLUSH_STEPS) ln_flush<NS, NA>(d, lp, records, acc, tab, fbase, stage, hdr, sbase, &since);
+      if (++since >= LN_FLUSH_STEPS) ln_flush<NS, NA>(d, lp, records, acc, cnt, tab, fbase, stage, hdr, sbase, &first_set, &since);
     }
   }
-  ln_flush<NS, NA>(d, lp, records, acc, tab, fbase, stage, hdr, sbase, &since);
+  ln_flush<NS, NA>(d, lp, records, acc, cnt, tab, fbase, stage, hdr, sbase, &first_set, &since);
 }
 
 }  // namespace hyk
