@@ -38,7 +38,11 @@ $(JOIN_OBJS): $(LIB)/hyrise_amd_%.o: $(CSRC)/capi/hyrise_amd_%.hip $(CSRC)/capi/
 	@mkdir -p $(LIB)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
-$(LIB)/libhyrise_amd.so: $(LIB)/hyrise_amd.o $(LIB)/hyrise_amd_aggregate.o $(JOIN_OBJS)
+$(LIB)/hyrise_amd_order.o: $(CSRC)/capi/hyrise_amd_order.hip $(CAPI_HDR)
+	@mkdir -p $(LIB)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIB)/libhyrise_amd.so: $(LIB)/hyrise_amd.o $(LIB)/hyrise_amd_aggregate.o $(LIB)/hyrise_amd_order.o $(JOIN_OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 $(LIB)/libhyrise_host.so: $(HOST_SRC) $(HOST_HDR) $(LIB)/libhyrise_amd.so

@@ -672,7 +672,7 @@ inline SideSizes sizes_of(const SidePlan& p, bool digit_bytes) {
 }
 
 template <typename H>
-size_t join_bytes(const SidePlan& bp, const SidePlan& pp, uint32_t bits) {
+size_t classic_join_bytes(const SidePlan& bp, const SidePlan& pp, uint32_t bits) {
   const auto w = digit_plan(bits, 0);
   const bool db = w.size() > 1 && digit_bytes_enabled();
   Carver cv{nullptr, 0};
@@ -700,13 +700,328 @@ hy_status upload_side(const SidePlan& p, const SideBufs<H, P>& b, hipStream_t s)
   return HY_OK;
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Single-pass first radix pass (hyk::part1_onepass) for plans of two or more digits: one read of the column chunks
+// writes the pass-1 buckets as NCLASS gapped regions each; the first record pass reads them as interleaved segments
+// (the distributed receiver's geometry, computed on the device by hyk::onepass_geometry) and writes compact records.
+// Opt-in (HY_ONEPASS=1): measured on MI355X at SF100 it is SLOWER than the two-read path (probe side 2.9-3.4 ms vs
+// 3.0 ms for part1_compact + part1_spread, build 0.78-0.94 vs 0.71 ms; per-class tickets vs a static order and 1-16
+// predecessors per look-back round trip all measured, profiles/r02g_onepass_variants.txt): a workgroup waiting on its
+// predecessors' digit counts holds its slot, so fewer loads are in flight than in the two streaming kernels. A region
+// overflow (skewed keys) falls back to the two-read path.
+// ---------------------------------------------------------------------------------------------------------------
+inline bool onepass_enabled() {
+  const char* e = std::getenv("HY_ONEPASS");
+  return e && std::strtol(e, nullptr, 10) != 0;
+}
+
+struct OnepassGeo {
+  uint64_t cap = 0;                 // records per (bucket, class) region
+  uint64_t gapped = 0;              // records of the gapped buffer
+  uint32_t grid = 0;
+  uint32_t class_begin[hyk::NCLASS + 1] = {};
+};
+
+// Classes = NCLASS balanced contiguous tile ranges; cap = the expected records of a region if every row of the
+// largest class took part, with 1/8 slack plus one tile (HY_ONEPASS_CAP_DIV overrides the slack divisor: tests).
+inline OnepassGeo onepass_geo(const SidePlan& p, uint32_t n_digits0) {
+  OnepassGeo g;
+  const uint64_t n = p.n_tiles1, q = n / hyk::NCLASS, r = n % hyk::NCLASS;
+  for (uint32_t x = 0; x <= hyk::NCLASS; ++x) g.class_begin[x] = static_cast<uint32_t>(x * q + std::min<uint64_t>(x, r));
+  const uint64_t max_tiles = q + (r ? 1 : 0);
+  g.grid = static_cast<uint32_t>(max_tiles * hyk::NCLASS);
+  const uint64_t class_rows = max_tiles * hyk::PART_TILE;
+  uint64_t div = 8;
+  if (const char* e = std::getenv("HY_ONEPASS_CAP_DIV")) div = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
+  const uint64_t expect = (class_rows + n_digits0 - 1) / n_digits0;
+  g.cap = std::min<uint64_t>(class_rows, expect + expect / div + (div > 1000 ? 0 : hyk::PART_TILE));
+  if (const char* e = std::getenv("HY_ONEPASS_CAP")) g.cap = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
+  g.gapped = g.cap * n_digits0 * hyk::NCLASS;
+  return g;
+}
+
+inline bool onepass_ok(const SidePlan& p, const std::vector<uint32_t>& w) {
+  if (!onepass_enabled() || w.size() < 2 || p.n_tiles1 == 0) return false;
+  return onepass_geo(p, 1u << w[0]).gapped < (uint64_t(1) << 31);
+}
+
+template <typename H>
+struct OneBufs {
+  SideBufs<H> b;
+  uint32_t *class_begin, *ticket, *status, *class_count, *flags, *match_count, *tile_off;
+  uint64_t* match_bits;
+  uint32_t *seg_begin, *seg_end, *seg_stride, *seg_toff, *group_tiles, *group_out, *owner;
+  uint64_t *seg_tile_begin, *seg_hbase, *group_hbase;
+  uint64_t hist_words = 1, max_tiles = 1;
+};
+
+template <typename H>
+void carve_onepass(Carver& cv, const SidePlan& p, uint32_t bits, const std::vector<uint32_t>& w, OneBufs<H>& o) {
+  const uint32_t nd0 = 1u << w[0];
+  const OnepassGeo g = onepass_geo(p, nd0);
+  const uint64_t nseg = uint64_t(nd0) * hyk::NCLASS;
+  const uint64_t row_tiles = p.n_rows / span2() + 1;
+  o.hist_words = (row_tiles + nseg) * (uint64_t(1) << w[1]);
+  o.max_tiles = std::max<uint64_t>(p.n_tiles1, row_tiles + nseg);
+  uint64_t segs = uint64_t(nd0) << w[1];
+  for (size_t i = 2; i < w.size(); ++i) {
+    o.hist_words = std::max(o.hist_words, (row_tiles + segs) * (uint64_t(1) << w[i]));
+    o.max_tiles = std::max(o.max_tiles, row_tiles + segs);
+    segs <<= w[i];
+  }
+  SideBufs<H>& b = o.b;
+  b.chunks = cv.take<hyk::SrcChunk>(std::max<size_t>(1, p.chunks.size()));
+  b.tile_begin = cv.take<uint64_t>(p.chunks.size() + 1);
+  b.row_begin = cv.take<uint64_t>(p.chunks.size() + 1);
+  b.referenced = cv.take<hyk::SrcChunk>(std::max<size_t>(1, p.referenced.size()));
+  b.ref_row_begin = cv.take<uint64_t>(p.referenced.size() + 1);
+  b.filter = p.filtered ? cv.take<hy_scan_chunk>(std::max<size_t>(1, p.chunks.size())) : nullptr;
+  b.hist = cv.take<uint32_t>(o.hist_words);
+  b.off = cv.take<uint32_t>(o.hist_words);
+  b.recA = cv.take<hyk::Rec<H>>(std::max<uint64_t>(1, g.gapped));
+  b.recB = cv.take<hyk::Rec<H>>(std::max<uint64_t>(1, p.n_rows));
+  b.span_count = nullptr;
+  b.digA = cv.take<uint8_t>(std::max<uint64_t>(16, g.gapped));
+  b.digB = cv.take<uint8_t>(std::max<uint64_t>(16, p.n_rows));
+  const uint64_t parts = (uint64_t(1) << bits) + 1;
+  b.segA = cv.take<uint32_t>(parts);
+  b.segB = cv.take<uint32_t>(parts);
+  b.seg_tile_begin = cv.take<uint64_t>(parts);
+  b.tile_counts = cv.take<uint32_t>(parts);
+  b.tile_excl = cv.take<uint32_t>(parts);
+  b.tile_owner = cv.take<uint32_t>(o.max_tiles);
+  b.total = cv.take<uint64_t>(1);
+  b.grand_total = cv.take<uint64_t>(1);
+  o.class_begin = cv.take<uint32_t>(hyk::NCLASS + 1);
+  o.ticket = cv.take<uint32_t>(hyk::NCLASS);
+  o.status = cv.take<uint32_t>(p.n_tiles1 * 256);
+  o.class_count = cv.take<uint32_t>(hyk::NCLASS * 256);
+  o.flags = cv.take<uint32_t>(1);
+  const bool scan = p.filtered && p.scan_out != nullptr;
+  o.match_bits = scan ? cv.take<uint64_t>(p.n_tiles1 * hyk::PART_WAVES * hyk::PART_ITEMS) : nullptr;
+  o.match_count = scan ? cv.take<uint32_t>(p.n_tiles1) : nullptr;
+  o.tile_off = scan ? cv.take<uint32_t>(p.n_tiles1) : nullptr;
+  o.seg_begin = cv.take<uint32_t>(nseg);
+  o.seg_end = cv.take<uint32_t>(nseg);
+  o.seg_stride = cv.take<uint32_t>(nseg);
+  o.seg_toff = cv.take<uint32_t>(nseg);
+  o.seg_hbase = cv.take<uint64_t>(nseg);
+  o.seg_tile_begin = cv.take<uint64_t>(nseg + 1);
+  o.group_hbase = cv.take<uint64_t>(nd0);
+  o.group_tiles = cv.take<uint32_t>(nd0);
+  o.group_out = cv.take<uint32_t>(nd0);
+  o.owner = cv.take<uint32_t>(row_tiles + nseg);
+}
+
+template <typename H>
+size_t onepass_bytes(const SidePlan& bp, const SidePlan& pp, uint32_t bits) {
+  const auto w = digit_plan(bits, 0);
+  Carver cv{nullptr, 0};
+  OneBufs<H> a, b;
+  carve_onepass<H>(cv, bp, bits, w, a);
+  carve_onepass<H>(cv, pp, bits, w, b);
+  Common c;
+  carve_common(cv, std::max({a.hist_words, b.hist_words, bp.n_tiles1, pp.n_tiles1, (uint64_t(1) << bits) + 1}), bits,
+               &c);
+  return cv.used + 256;
+}
+
+// The side's pass 0 (part1_onepass), the fused scan's output, the first record pass over the gapped regions and the
+// remaining record passes. *flags_host receives the overflow / look-back flags once the stream has synchronised.
+template <typename T, typename H, int LP, int FK>
+hy_status onepass_launch(const char* tag, const hyk::Side& sd, const hyk::Digit& d0, const hyk::NextDigit& nd,
+                         uint32_t n_digits, const hyk::OnePass& op, uint32_t grid, hyk::Rec<H>* out, hipStream_t s,
+                         uint64_t rows) {
+  KTimer kt_((std::string("part1_onepass.") + tag).c_str(), s, rows);
+  hipLaunchKernelGGL((hyk::part1_onepass<T, H, LP, FK>), dim3(grid), dim3(hyk::PART_THREADS), 0, s, sd, d0, nd,
+                     n_digits, op, out);
+  kt_.done();
+  HY_HIP(hipGetLastError());
+  return HY_OK;
+}
+
+template <typename T, typename H>
+hy_status onepass_side(const char* tag, const SidePlan& p, OneBufs<H>& o, uint32_t bits, const std::vector<uint32_t>& w,
+                       uint32_t seed, bool keep_nulls, const Common& c, hipStream_t s, uint32_t* flags_host,
+                       hyk::Rec<H>** recs, uint32_t** bounds) {
+  SideBufs<H>& b = o.b;
+  const uint32_t nd0 = 1u << w[0], w1 = w[1];
+  const OnepassGeo g = onepass_geo(p, nd0);
+  HY_HIP(hipMemcpyAsync(o.class_begin, g.class_begin, sizeof(g.class_begin), hipMemcpyHostToDevice, s));
+  HY_HIP(hipMemsetAsync(o.ticket, 0, 4 * hyk::NCLASS, s));
+  HY_HIP(hipMemsetAsync(o.status, 0, 4 * 256 * p.n_tiles1, s));
+  HY_HIP(hipMemsetAsync(o.class_count, 0, 4 * 256 * hyk::NCLASS, s));
+  HY_HIP(hipMemsetAsync(o.flags, 0, 4, s));
+  if (p.filtered && p.scan_chunk_begin) HY_HIP(hipMemsetAsync(p.scan_chunk_begin, 0, 8 * (p.chunks.size() + 1), s));
+  hyk::Side sd{};
+  sd.chunks = b.chunks;
+  sd.n_chunks = static_cast<uint32_t>(p.chunks.size());
+  sd.chunk_tile_begin = b.tile_begin;
+  sd.tile_chunk = b.tile_owner;
+  sd.n_tiles = p.n_tiles1;
+  sd.referenced = b.referenced;
+  sd.n_referenced = static_cast<uint32_t>(p.referenced.size());
+  sd.referenced_row_begin = b.ref_row_begin;
+  sd.fuse_deref = p.fuse;
+  sd.keep_nulls = keep_nulls ? 1 : 0;
+  sd.ref_base = p.ref_base;
+  sd.sub = 1;
+  sd.filter = p.filtered ? b.filter : nullptr;
+  sd.filter_const = p.filter_const;
+  sd.filter_type = p.filter_type;
+  sd.scan_out = p.scan_out;
+  hipLaunchKernelGGL(hyk::fill_tile_owner, dim3((sd.n_chunks + 255) / 256), dim3(256), 0, s, b.tile_begin, sd.n_chunks,
+                     b.tile_owner);
+  HY_HIP(hipGetLastError());
+  const hyk::Digit d0{full_mask(bits), bits - w[0], nd0 - 1u, seed};
+  const hyk::NextDigit nd = next_digit(w, 0, bits, b.digA);
+  static const uint32_t win = [] {
+    const char* e = std::getenv("HY_ONEPASS_WIN");
+    const long v = e ? std::strtol(e, nullptr, 10) : 1;
+    return static_cast<uint32_t>(std::min<long>(std::max<long>(v, 1), hyk::LB_WIN));
+  }();
+  static const uint32_t static_order = std::getenv("HY_ONEPASS_STATIC") ? 1u : 0u;
+  const hyk::OnePass op{o.class_begin, o.ticket,      o.status, o.class_count, g.cap, o.flags,
+                        o.match_bits,  o.match_count, win,      static_order};
+  const int lp = load_path(p);
+  hy_status st = HY_OK;
+  if (p.filtered) {
+    if constexpr (std::is_same_v<T, H>) {
+      const int fk = filter_kind(p);
+      auto go = [&](auto fk_tag) {
+        constexpr int FK = decltype(fk_tag)::value;
+        return lp == hyk::LP_VALUE
+                   ? onepass_launch<T, H, hyk::LP_VALUE, FK>(tag, sd, d0, nd, nd0, op, g.grid, b.recA, s, p.n_rows)
+                   : onepass_launch<T, H, hyk::LP_ANY, FK>(tag, sd, d0, nd, nd0, op, g.grid, b.recA, s, p.n_rows);
+      };
+      if (fk == hyk::FK_DICT8)
+        st = go(std::integral_constant<int, hyk::FK_DICT8>{});
+      else if (fk == hyk::FK_DICT16)
+        st = go(std::integral_constant<int, hyk::FK_DICT16>{});
+      else if (fk == hyk::FK_DICT32)
+        st = go(std::integral_constant<int, hyk::FK_DICT32>{});
+      else
+        st = go(std::integral_constant<int, hyk::FK_ANY>{});
+    } else {
+      return fail(HY_ERR_UNSUPPORTED, "fused scan on a side whose join column type is not the hashed type");
+    }
+  } else if (lp == hyk::LP_VALUE) {
+    st = onepass_launch<T, H, hyk::LP_VALUE, hyk::FK_NONE>(tag, sd, d0, nd, nd0, op, g.grid, b.recA, s, p.n_rows);
+  } else if (lp == hyk::LP_REF1) {
+    st = onepass_launch<T, H, hyk::LP_REF1, hyk::FK_NONE>(tag, sd, d0, nd, nd0, op, g.grid, b.recA, s, p.n_rows);
+  } else {
+    st = onepass_launch<T, H, hyk::LP_ANY, hyk::FK_NONE>(tag, sd, d0, nd, nd0, op, g.grid, b.recA, s, p.n_rows);
+  }
+  if (st != HY_OK) return st;
+  if (o.match_bits != nullptr) {  // the fused scan's output
+    st = run_scan(o.match_count, o.tile_off, p.n_tiles1, c, s, b.grand_total);
+    if (st != HY_OK) return st;
+    KTimer kt_((std::string("part1_scan_expand.") + tag).c_str(), s, p.n_rows);
+    hipLaunchKernelGGL(hyk::part1_scan_expand, dim3(static_cast<uint32_t>(p.n_tiles1)), dim3(hyk::PART_THREADS), 0, s,
+                       sd, o.match_bits, o.tile_off, b.grand_total, p.scan_chunk_begin);
+    kt_.done();
+    HY_HIP(hipGetLastError());
+  }
+  HY_HIP(hipMemcpyAsync(flags_host, o.flags, 4, hipMemcpyDeviceToHost, s));
+  const uint32_t nseg = nd0 * hyk::NCLASS;
+  hipLaunchKernelGGL(hyk::onepass_geometry, dim3(1), dim3(256), 0, s, o.class_count, nd0, g.cap, span2(), 1u << w1,
+                     o.seg_begin, o.seg_end, o.seg_stride, o.seg_toff, o.seg_hbase, o.seg_tile_begin, o.group_hbase,
+                     o.group_tiles, o.group_out, b.total);
+  HY_HIP(hipGetLastError());
+  hipLaunchKernelGGL(hyk::fill_tile_owner, dim3(grid_for(nseg, 256)), dim3(256), 0, s, o.seg_tile_begin, nseg, o.owner);
+  HY_HIP(hipGetLastError());
+  const hyk::Segs sg{o.seg_begin, o.seg_tile_begin, o.owner, nseg, o.seg_end, o.seg_hbase, o.seg_stride, o.seg_toff,
+                     sub2()};
+  const hyk::Groups gr{o.group_hbase, o.group_tiles, o.group_out};
+  const uint64_t grid = p.n_rows / span2() + 1 + nseg;
+  const hyk::NextDigit nd1 = next_digit(w, 1, bits, b.digB);
+  st = record_pass<H, uint32_t>(tag, b, sg, gr, nd0, grid, bits, bits - w[0] - w1, w1, seed, b.recA, b.digA, nd1, b.recB,
+                                b.total, b.segA, c, s, p.n_rows);
+  if (st != HY_OK) return st;
+  if (w.size() == 2) {
+    *recs = b.recB;
+    *bounds = b.segA;
+    return HY_OK;
+  }
+  return local_passes<H, uint32_t>(tag, b, w, 2, bits, seed, b.recB, b.recA, b.digB, b.digA, b.segA, b.segB,
+                                   uint64_t(nd0) << w1, b.total, p.n_rows, c, s, recs, bounds);
+}
+
+// Both sides through onepass_side, then the partition joins. *overflow = the sides' flags (nonzero: results invalid,
+// the caller reruns the two-read path).
 template <typename TB, typename TP, typename H>
-hy_status join_typed(const SidePlan& bp, const SidePlan& pp, const hy_join_params* prm, hy_row_id* out_build,
+hy_status join_typed_onepass(const SidePlan& bp, const SidePlan& pp, const hy_join_params* prm, hy_row_id* out_build,
+                             hy_row_id* out_probe, uint64_t out_capacity, uint64_t* partition_begin,
+                             uint32_t* partition_counts, hy_join_result* result, void* workspace,
+                             size_t workspace_bytes, hipStream_t s, uint32_t* overflow) {
+  const uint32_t bits = prm->radix_bits;
+  const auto w = digit_plan(bits, 0);
+  Carver cv{static_cast<char*>(workspace), workspace_bytes};
+  OneBufs<H> ob, op;
+  carve_onepass<H>(cv, bp, bits, w, ob);
+  carve_onepass<H>(cv, pp, bits, w, op);
+  Common c{};
+  carve_common(cv, std::max({ob.hist_words, op.hist_words, bp.n_tiles1, pp.n_tiles1, (uint64_t(1) << bits) + 1}), bits,
+               &c);
+  if (!cv.ok) return fail(HY_ERR_WORKSPACE, "join workspace too small");
+  if (upload_side(bp, ob.b, s) || upload_side(pp, op.b, s)) return HY_ERR_DEVICE;
+  const bool keep_nulls = prm->mode == HY_JOIN_LEFT || prm->mode == HY_JOIN_RIGHT;
+  static thread_local uint32_t flags[2];
+  flags[0] = flags[1] = 0;
+  hyk::Rec<H>* recs[2] = {nullptr, nullptr};
+  uint32_t* bounds[2] = {nullptr, nullptr};
+  hy_status st = onepass_side<TB, H>("build", bp, ob, bits, w, prm->seed, false, c, s, &flags[0], &recs[0], &bounds[0]);
+  if (st != HY_OK) return st;
+  st = onepass_side<TP, H>("probe", pp, op, bits, w, prm->seed, keep_nulls, c, s, &flags[1], &recs[1], &bounds[1]);
+  if (st != HY_OK) return st;
+  const hyk::RowMap bmap = bp.fuse ? make_map(ob.b.ref_row_begin, bp.ref_row_begin) : make_map(ob.b.row_begin, bp.row_begin);
+  const hyk::RowMap pmap = pp.fuse ? make_map(op.b.ref_row_begin, pp.ref_row_begin) : make_map(op.b.row_begin, pp.row_begin);
+  st = run_join_partitions<H, uint32_t>(bounds[0], bounds[1], 1u << bits, recs[0], recs[1], bmap, pmap, prm->mode,
+                                        out_build, out_probe, out_capacity, partition_begin, partition_counts, result,
+                                        c, s, bp.n_rows + pp.n_rows, pp.n_rows);
+  HY_HIP(hipStreamSynchronize(s));  // the flags' copies (run_join_partitions has synchronised on success)
+  *overflow = flags[0] | flags[1];
+  return st;
+}
+
+// Pass-0 spans of one tile each (part1_onepass handles one tile per workgroup).
+inline SidePlan one_tile_spans(const SidePlan& p) {
+  SidePlan q = p;
+  plan_spans(q, 1);
+  return q;
+}
+
+// Workspace of a single-GPU join: enough for the single-pass path (when it applies) and for its fallback.
+template <typename H>
+size_t join_bytes(const SidePlan& bp, const SidePlan& pp, uint32_t bits) {
+  size_t n = classic_join_bytes<H>(bp, pp, bits);
+  const auto w = digit_plan(bits, 0);
+  const SidePlan b1 = one_tile_spans(bp), p1 = one_tile_spans(pp);
+  if (onepass_ok(b1, w) && onepass_ok(p1, w)) n = std::max(n, onepass_bytes<H>(b1, p1, bits));
+  return n;
+}
+
+template <typename TB, typename TP, typename H>
+hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join_params* prm, hy_row_id* out_build,
                      hy_row_id* out_probe, uint64_t out_capacity, uint64_t* partition_begin,
                      uint32_t* partition_counts, hy_join_result* result, void* workspace, size_t workspace_bytes,
                      hipStream_t s) {
   const uint32_t bits = prm->radix_bits;
-  if (workspace_bytes < join_bytes<H>(bp, pp, bits)) return fail(HY_ERR_WORKSPACE, "join workspace too small");
+  {
+    const auto w = digit_plan(bits, 0);
+    const SidePlan b1 = one_tile_spans(bp_in), p1 = one_tile_spans(pp_in);
+    if (onepass_ok(b1, w) && onepass_ok(p1, w) && workspace_bytes >= onepass_bytes<H>(b1, p1, bits)) {
+      uint32_t overflow = 0;
+      const hy_status st = join_typed_onepass<TB, TP, H>(b1, p1, prm, out_build, out_probe, out_capacity,
+                                                         partition_begin, partition_counts, result, workspace,
+                                                         workspace_bytes, s, &overflow);
+      if (overflow == 0) return st;
+      // a gapped region overflowed (or a look-back timed out): the two-read path below recomputes everything
+    }
+  }
+  const SidePlan& bp = bp_in;
+  const SidePlan& pp = pp_in;
+  if (workspace_bytes < classic_join_bytes<H>(bp, pp, bits)) return fail(HY_ERR_WORKSPACE, "join workspace too small");
   const auto w = digit_plan(bits, 0);
   const bool db = w.size() > 1 && digit_bytes_enabled();
   Carver cv{static_cast<char*>(workspace), workspace_bytes};

@@ -301,22 +301,27 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
       hy_check(hy_memcpy_dtoh(&total, count.get(), 8, s), "dtoh");
       hy_check(hy_stream_synchronize(s), "sync");
     } else {
-      // one pass per referenced chunk, in the unordered_map's iteration order (positions ascending inside each)
-      if (groups.size() > 64)
-        Fail("hyrise-amd: reference scan over a PosList spanning more than 64 chunks is not supported yet");
-      for (const auto g : groups) {
-        auto masked = rdesc;
-        for (ChunkID r = 0; r < masked.size(); ++r)
-          if (r != g) masked[r].op = HY_OP_NONE;
-        hy_check(hy_reference_scan(dpl->ptr(), m, masked.data(), static_cast<uint32_t>(masked.size()),
-                                   hy_type_of(col_type), constant.bytes, positions.as<uint32_t>() + total,
-                                   count.as<uint64_t>(), ws.get(), ws_bytes, s),
-                 "hy_reference_scan");
-        uint64_t n = 0;
-        hy_check(hy_memcpy_dtoh(&n, count.get(), 8, s), "dtoh");
-        hy_check(hy_stream_synchronize(s), "sync");
-        total += n;
-      }
+      // all referenced chunks in one scan (ascending positions), then the matches reordered into the unordered_map's
+      // group order (positions ascending inside each group) by one stable sort on the device
+      DeviceBuffer asc(std::max<uint64_t>(m, 1) * 4, s);
+      hy_check(hy_reference_scan(dpl->ptr(), m, rdesc.data(), static_cast<uint32_t>(rdesc.size()), hy_type_of(col_type),
+                                 constant.bytes, asc.as<uint32_t>(), count.as<uint64_t>(), ws.get(), ws_bytes, s),
+               "hy_reference_scan");
+      hy_check(hy_memcpy_dtoh(&total, count.get(), 8, s), "dtoh");
+      hy_check(hy_stream_synchronize(s), "sync");
+      std::vector<uint32_t> rank(rtable->chunk_count(), 0);
+      for (size_t g = 0; g < groups.size(); ++g) rank[groups[g]] = static_cast<uint32_t>(g);
+      DeviceBuffer d_rank(rank.size() * 4, s);
+      hy_check(hy_memcpy_htod(d_rank.get(), rank.data(), rank.size() * 4, s), "htod");
+      size_t ob = 0;
+      hy_check(hy_reference_scan_order_workspace_size(total, static_cast<uint32_t>(groups.size()), &ob),
+               "hy_reference_scan_order_workspace_size");
+      DeviceBuffer ows(ob, s);
+      hy_check(hy_reference_scan_order(dpl->ptr(), asc.as<uint32_t>(), total, d_rank.as<uint32_t>(),
+                                       static_cast<uint32_t>(rank.size()), static_cast<uint32_t>(groups.size()),
+                                       positions.as<uint32_t>(), ows.get(), ob, s),
+               "hy_reference_scan_order");
+      hy_check(hy_stream_synchronize(s), "sync");  // d_rank / asc / ows are released at scope end
     }
     if (total == 0) continue;
     // filtered PosLists, shared per distinct input PosList (table_scan.cpp:115-145)

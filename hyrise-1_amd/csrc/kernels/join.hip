@@ -676,6 +676,260 @@ __global__ __launch_bounds__(PART_THREADS) void part1_spread(Side s, Digit dg, N
 }
 
 // ------------------------------------------------------------------------------------------------------------
+// Single-pass first radix pass (part1_onepass): the histogram, its prefix across tiles and the stable scatter in ONE
+// read of the column chunks (and of the fused scan's predicate column), instead of part1_hist + scan + part1_scatter
+// (two reads) or part1_compact + scan + part1_spread (one read plus a gapped write and re-read of the records).
+//
+// The pass-0 tiles are split into NCLASS contiguous ranges ("classes"); workgroups of class x (blockIdx % NCLASS: the
+// blocks that share an XCD, so a range's neighbouring tiles complete their shared output lines in one L2) take the
+// class's tiles in order from a per-class atomic ticket. Every tile publishes its 256 digit counts as look-back
+// granules and resolves, per digit, the count of the same digit in the class's earlier tiles (a decoupled look-back
+// per digit, one thread per digit) - so no tile waits on another class. Class x writes digit d's records into their
+// own region (d * NCLASS + x) * cap of a gapped buffer, in row order. The regions of digit d, taken in class order,
+// are exactly the stable pass-1 bucket d; the next record pass reads them as NCLASS segments per bucket (the
+// interleaved-segment geometry of the distributed receiver) and writes compact output. A region that would exceed
+// `cap` (skewed keys) sets the overflow flag and the tile writes nothing; the host then runs the two-read path.
+//
+// The fused TableScan's output cannot be placed in the same pass without a prefix over ALL earlier tiles (a wait
+// across classes), so the pass writes each tile's match bitmask (one 64-bit ballot per wave and item, 512 B per
+// tile) and match count; part1_scan_expand turns them into the scan's chunk offsets after a scan of the counts.
+// ------------------------------------------------------------------------------------------------------------
+constexpr uint32_t NCLASS = 8;
+constexpr uint32_t LB32_AGG = 1u << 30;
+constexpr uint32_t LB32_PREFIX = 2u << 30;
+constexpr uint32_t LB32_VALUE = (1u << 30) - 1;
+constexpr int LB_WIN = 16;  // predecessors polled per look-back round trip
+
+struct OnePass {
+  const uint32_t* class_begin;  // NCLASS + 1 tile bounds of the classes
+  uint32_t* ticket;             // NCLASS counters (zeroed before the launch)
+  uint32_t* status;             // n_tiles * 256 look-back granules (zeroed before the launch)
+  uint32_t* class_count;        // NCLASS * 256: records of digit d in class x (zeroed before the launch)
+  uint64_t cap;                 // records per (digit, class) region
+  uint32_t* flags;              // [0] bit 0: a region overflowed, bit 1: a look-back timed out
+  uint64_t* match_bits;         // n_tiles * 64 ballots (filtered sides with a scan output), or null
+  uint32_t* match_count;        // n_tiles match counts (filtered sides with a scan output), or null
+  uint32_t win;                 // predecessors polled per look-back round trip (1..LB_WIN)
+  uint32_t static_order;        // 1: tile = blockIdx / NCLASS instead of the per-class ticket (experiment)
+};
+
+template <typename T, typename H, int LP, int FK>
+__global__ __launch_bounds__(PART_THREADS) void part1_onepass(Side s, Digit dg, NextDigit nd, uint32_t n_digits,
+                                                             OnePass op, Rec<H, uint32_t>* __restrict__ out) {
+  __shared__ uint32_t s_cnt[PART_WAVES][256];
+  __shared__ uint32_t s_delta[256];
+  __shared__ uint32_t s_scratch[PART_WAVES + 1];
+  __shared__ Rec<H, uint32_t> s_stage[PART_TILE];
+  __shared__ uint32_t s_tile;
+  __shared__ uint32_t s_bad;
+  const uint32_t x = blockIdx.x % NCLASS;
+  const uint32_t c0 = op.class_begin[x], n_cls = op.class_begin[x + 1] - c0;
+  if (threadIdx.x == 0) {
+    s_tile = op.static_order ? blockIdx.x / NCLASS : atomicAdd(&op.ticket[x], 1u);
+    s_bad = 0;
+  }
+  __syncthreads();
+  const uint32_t i = s_tile;
+  if (i >= n_cls) return;
+  const uint64_t tile = c0 + i;
+  const uint32_t c = s.tile_chunk[tile];
+  const SrcChunk ch = s.chunks[c];
+  const uint32_t base = static_cast<uint32_t>(tile - s.chunk_tile_begin[c]) * PART_TILE;
+  const int w = threadIdx.x / WAVE, lane = __lane_id();
+  uint64_t* s_mask = reinterpret_cast<uint64_t*>(s_stage) + w * 256;  // ranking masks alias the staging area
+  clear_wave_counts(s_cnt[w]);
+  clear_wave_masks(s_mask);
+  const uint32_t rb = base + w * WAVE_SPAN;
+  uint32_t m = 0xFFFFu;
+  if constexpr (FK != FK_NONE) {
+    m = filter_items<FK>(s, c, rb);
+    if (op.match_bits != nullptr) {
+      uint32_t cnt = 0;
+#pragma unroll
+      for (int k = 0; k < PART_ITEMS; ++k) {
+        const uint64_t b = __ballot((m >> k) & 1u);
+        if (lane == k) op.match_bits[tile * (PART_WAVES * PART_ITEMS) + w * PART_ITEMS + k] = b;
+        cnt += static_cast<uint32_t>(__popcll(b));
+      }
+      if (lane == 0) s_scratch[w] = cnt;
+    }
+  }
+  H keys[PART_ITEMS];
+  uint32_t pays[PART_ITEMS];
+  const uint32_t act = load_items<T, H, uint32_t, LP>(s, ch, rb, keys, pays) & m;
+  Rec<H, uint32_t> recs[PART_ITEMS];
+  uint32_t dr[PART_ITEMS];
+#pragma unroll
+  for (int k = 0; k < PART_ITEMS; ++k) {
+    const bool a = (act >> k) & 1u;
+    const uint32_t dig = a ? digit_of<H>(dg, keys[k]) : 0u;
+    dr[k] = (dig << 24) | wave_rank_lds(dig, a, s_mask, s_cnt[w]);
+    recs[k].key = keys[k];
+    recs[k].payload = pays[k];
+  }
+  __syncthreads();  // every wave's digit counts (and match counts) are in LDS
+  if constexpr (FK != FK_NONE) {
+    if (op.match_count != nullptr && threadIdx.x == 0) {
+      uint32_t t = 0;
+#pragma unroll
+      for (int ww = 0; ww < PART_WAVES; ++ww) t += s_scratch[ww];
+      op.match_count[tile] = t;
+    }
+  }
+  // per digit: publish this tile's count, resolve the class-local prefix of the earlier tiles, publish the inclusive
+  const uint32_t d = threadIdx.x;
+  uint32_t run = 0;
+  if (d < n_digits) {
+    uint32_t tot = 0;
+#pragma unroll
+    for (int ww = 0; ww < PART_WAVES; ++ww) tot += s_cnt[ww][d];
+    uint32_t* st = op.status + tile * 256 + d;
+    uint32_t prefix = 0;
+    if (i == 0) {
+      __hip_atomic_store(st, LB32_PREFIX | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_store(st, LB32_AGG | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // windowed walk: LB_WIN predecessors polled with independent loads per round trip, summed up to the nearest
+      // inclusive prefix; a not-yet-published predecessor ends the round (the sum so far is kept) and is re-polled
+      uint64_t j = tile;  // tiles [c0, j) remain to be resolved
+      uint32_t spins = 0;
+      bool done = false;
+      while (!done && j > c0) {
+        uint32_t v[LB_WIN];
+#pragma unroll
+        for (int k = 0; k < LB_WIN; ++k)
+          v[k] = (k < op.win && j - k > c0) ? __hip_atomic_load(op.status + (j - 1 - k) * 256 + d, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT)
+                              : (j - k > c0 ? 0u : LB32_PREFIX);  // before the class start: inclusive prefix 0
+        uint32_t k = 0;
+        for (; k < op.win; ++k) {
+          const uint32_t f = v[k] & ~LB32_VALUE;
+          if (f == 0) break;
+          prefix += v[k] & LB32_VALUE;
+          if (f == LB32_PREFIX) {
+            done = true;
+            break;
+          }
+        }
+        if (done) break;
+        j -= k;
+        if (k < op.win) {  // predecessor j - 1 has not published yet
+          if (++spins > LB_MAX_SPINS) {
+            atomicOr(op.flags, 2u);
+            s_bad = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      __hip_atomic_store(st, LB32_PREFIX | (prefix + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (i == n_cls - 1) op.class_count[x * 256 + d] = prefix + tot;
+    if (prefix + tot > op.cap) {
+      atomicOr(op.flags, 1u);
+      s_bad = 1;
+    }
+    run = static_cast<uint32_t>((static_cast<uint64_t>(d) * NCLASS + x) * op.cap) + prefix;
+  }
+  __syncthreads();
+  if (s_bad) return;  // the host falls back to the two-read path; nothing of this tile is written
+  staged_scatter<H, uint32_t>(recs, act, dr, s_cnt, s_delta, s_stage, s_scratch, n_digits, dg, nd, run, out);
+}
+
+// The fused scan's output from part1_onepass's per-tile match bitmasks: tile_off = exclusive scan of the match
+// counts (matches in row order), each matching row's chunk offset written at its position; chunk_begin[c] = position
+// of chunk c's first match (n_chunks + 1 entries).
+static __global__ __launch_bounds__(PART_THREADS) void part1_scan_expand(Side s, const uint64_t* __restrict__ bits,
+                                                                       const uint32_t* __restrict__ tile_off,
+                                                                       const uint64_t* __restrict__ total,
+                                                                       uint64_t* __restrict__ chunk_begin) {
+  __shared__ uint32_t s_w[PART_WAVES + 1];
+  __shared__ uint32_t s_out[PART_TILE];
+  const uint64_t tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int w = threadIdx.x / WAVE, lane = __lane_id();
+  const uint32_t c = s.tile_chunk[tile];
+  const uint32_t base = static_cast<uint32_t>(tile - s.chunk_tile_begin[c]) * PART_TILE + w * WAVE_SPAN;
+  uint64_t b[PART_ITEMS];
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int k = 0; k < PART_ITEMS; ++k) {
+    b[k] = bits[tile * (PART_WAVES * PART_ITEMS) + w * PART_ITEMS + k];
+    cnt += static_cast<uint32_t>(__popcll(b[k]));
+  }
+  if (lane == 0) s_w[w] = cnt;
+  const uint32_t pos0 = tile_off[tile];
+  __syncthreads();
+  uint32_t pos = 0, n = 0;
+  for (int ww = 0; ww < PART_WAVES; ++ww) {
+    if (ww < w) pos += s_w[ww];
+    n += s_w[ww];
+  }
+  // the tile's offsets in row order into LDS, then written out by consecutive lanes (coalesced)
+#pragma unroll
+  for (int k = 0; k < PART_ITEMS; ++k) {
+    if ((b[k] >> lane) & 1u) s_out[pos + __popcll(b[k] & lanemask_lt())] = base + k * WAVE + lane;
+    pos += static_cast<uint32_t>(__popcll(b[k]));
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += PART_THREADS) s.scan_out[pos0 + i] = s_out[i];
+  if (chunk_begin != nullptr && blockIdx.x == 0) {
+    for (uint32_t cc = threadIdx.x; cc <= s.n_chunks; cc += PART_THREADS) {
+      const uint64_t t = s.chunk_tile_begin[cc];
+      chunk_begin[cc] = t < s.n_tiles ? tile_off[t] : *total;
+    }
+  }
+}
+
+// Geometry of the record pass that follows part1_onepass (one workgroup, thread g = pass-1 bucket g): the NCLASS
+// regions of bucket g are its segments g * NCLASS + x (begin = region start, end = begin + count), their tiles of
+// `span` records are interleaved in the histogram by (bucket, digit, class, tile) - the layout record_pass takes for
+// the distributed receiver's (bucket, sender) runs - and the bucket's output starts at the count of all earlier
+// buckets. Writes the segment / group arrays, the tile prefix (n_segs + 1) and the record total.
+static __global__ __launch_bounds__(256) void onepass_geometry(const uint32_t* __restrict__ class_count, uint32_t n_groups,
+                                                               uint64_t cap, uint32_t span, uint32_t next_digits,
+                                                               uint32_t* seg_begin, uint32_t* seg_end,
+                                                               uint32_t* seg_stride, uint32_t* seg_toff,
+                                                               uint64_t* seg_hbase, uint64_t* seg_tile_begin,
+                                                               uint64_t* group_hbase, uint32_t* group_tiles,
+                                                               uint32_t* group_out, uint64_t* total) {
+  __shared__ uint32_t s_scratch[256 / WAVE + 1];
+  const uint32_t g = threadIdx.x;
+  uint32_t cnt[NCLASS], gt = 0, gc = 0;
+#pragma unroll
+  for (uint32_t x = 0; x < NCLASS; ++x) {
+    cnt[x] = g < n_groups ? static_cast<uint32_t>(min<uint64_t>(class_count[x * 256 + g], cap)) : 0u;
+    gt += (cnt[x] + span - 1) / span;
+    gc += cnt[x];
+  }
+  uint32_t tiles_total, rows_total;
+  const uint32_t tile_base = block_exclusive_sum<256>(gt, s_scratch, &tiles_total);
+  const uint32_t out_base = block_exclusive_sum<256>(gc, s_scratch, &rows_total);
+  if (g < n_groups) {
+    const uint64_t hb = static_cast<uint64_t>(tile_base) * next_digits;
+    uint32_t toff = 0;
+#pragma unroll
+    for (uint32_t x = 0; x < NCLASS; ++x) {
+      const uint32_t q = g * NCLASS + x;
+      const uint32_t b0 = static_cast<uint32_t>(static_cast<uint64_t>(q) * cap);
+      seg_begin[q] = b0;
+      seg_end[q] = b0 + cnt[x];
+      seg_stride[q] = gt;
+      seg_toff[q] = toff;
+      seg_hbase[q] = hb;
+      seg_tile_begin[q] = tile_base + toff;
+      toff += (cnt[x] + span - 1) / span;
+    }
+    group_hbase[g] = hb;
+    group_tiles[g] = gt;
+    group_out[g] = out_base;
+  }
+  if (g == 0) {
+    seg_tile_begin[n_groups * NCLASS] = tiles_total;
+    *total = rows_total;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
 // Pass 2: records -> records, inside every pass-1 bucket (segment).
 // ------------------------------------------------------------------------------------------------------------
 // Pass-2 segments. Single-GPU: the pass-1 buckets, contiguous (seg_begin[i], seg_begin[i+1]) with the histogram of

@@ -186,6 +186,21 @@ hy_status hy_gather_row_ids(const hy_row_id* pos_list, const uint32_t* positions
                             hy_stream_t stream);
 
 /*
+ * Reference-input TableScan over a PosList referencing several chunks, in the reference's output order: the
+ * reference splits the PosList by referenced chunk into a std::unordered_map (split_pos_list_by_chunk_id,
+ * chunk_offset_mapping.cpp:5-21) and emits the matches group by group in the map's iteration order, positions
+ * ascending inside a group (base_single_column_table_scan_impl.cpp:36-60). Given the ascending match positions of
+ * ONE hy_reference_scan over all chunks, writes them to out_positions ordered by (chunk_rank[referenced chunk id],
+ * position): chunk_rank (device, n_chunks entries, values < n_ranks) is the group order the host replays
+ * (std::unordered_map iteration order). One launch and one stable radix sort instead of one scan per group.
+ */
+hy_status hy_reference_scan_order_workspace_size(uint64_t n, uint32_t n_ranks, size_t* bytes);
+hy_status hy_reference_scan_order(const hy_row_id* pos_list, const uint32_t* positions, uint64_t n,
+                                  const uint32_t* chunk_rank, uint32_t n_chunks, uint32_t n_ranks,
+                                  uint32_t* out_positions, void* workspace, size_t workspace_bytes,
+                                  hy_stream_t stream);
+
+/*
  * first_seen[c] = smallest position i with pos_list[i].chunk_id == c (NULL RowIDs skipped), ~0 if none, for
  * c < n_chunks. Gives the order in which split_pos_list_by_chunk_id (reference
  * src/lib/storage/column_iterables/chunk_offset_mapping.cpp:5-21) first inserts each referenced chunk.

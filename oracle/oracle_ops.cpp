@@ -580,7 +580,8 @@ void write_output_columns(ChunkColumns& out, const std::shared_ptr<const Table>&
 
 template <typename L, typename R>
 std::shared_ptr<Table> join_impl(const std::shared_ptr<const Table>& left_in, const std::shared_ptr<const Table>& right_in,
-                                 JoinMode mode, std::pair<ColumnID, ColumnID> cols, bool swapped, uint32_t* bits_out) {
+                                 JoinMode mode, std::pair<ColumnID, ColumnID> cols, bool swapped, uint32_t* bits_out,
+                                 uint32_t force_bits) {
   using H = std::conditional_t<
       std::is_same_v<L, std::string> || std::is_same_v<R, std::string>, std::string,
       std::conditional_t<std::is_floating_point_v<L> && std::is_floating_point_v<R>,
@@ -589,7 +590,7 @@ std::shared_ptr<Table> join_impl(const std::shared_ptr<const Table>& left_in, co
                                             std::conditional_t<(sizeof(L) < sizeof(R)), R, L>,
                                             std::conditional_t<std::is_floating_point_v<L>, L, R>>>>;
   // _left = build, _right = probe
-  const size_t bits = radix_bits(left_in->row_count(), sizeof(L));
+  const size_t bits = force_bits ? force_bits : radix_bits(left_in->row_count(), sizeof(L));
   if (bits_out) *bits_out = static_cast<uint32_t>(bits);
   TableColumnDefinitions defs;
   if (swapped) {
@@ -638,7 +639,7 @@ std::shared_ptr<Table> join_impl(const std::shared_ptr<const Table>& left_in, co
 
 std::pair<std::shared_ptr<Table>, uint32_t> join_hash(const std::shared_ptr<const Table>& left,
                                                       const std::shared_ptr<const Table>& right, JoinMode mode,
-                                                      std::pair<ColumnID, ColumnID> cols) {
+                                                      std::pair<ColumnID, ColumnID> cols, uint32_t force_bits = 0) {
   bool swapped = (mode == JoinMode::Left || mode == JoinMode::Anti || mode == JoinMode::Semi);
   if (!swapped && left->row_count() > right->row_count()) swapped = true;
   const auto build_t = swapped ? right : left;
@@ -648,7 +649,7 @@ std::pair<std::shared_ptr<Table>, uint32_t> join_hash(const std::shared_ptr<cons
   uint32_t bits = 0;
   resolve_data_type(build_t->column_data_type(adjusted.first), [&](auto lt) {
     resolve_data_type(probe_t->column_data_type(adjusted.second), [&](auto rt) {
-      out = join_impl<decltype(lt), decltype(rt)>(build_t, probe_t, mode, adjusted, swapped, &bits);
+      out = join_impl<decltype(lt), decltype(rt)>(build_t, probe_t, mode, adjusted, swapped, &bits, force_bits);
     });
   });
   return {out, bits};
@@ -1113,10 +1114,13 @@ PYBIND11_MODULE(_hyrise_oracle, m) {
         py::arg("table"), py::arg("column_id"), py::arg("predicate_condition"), py::arg("value"),
         py::arg("excluded_chunk_ids") = std::vector<ChunkID>{});
   m.def("join_hash",
-        [](std::shared_ptr<Table> l, std::shared_ptr<Table> r, JoinMode mode, std::pair<ColumnID, ColumnID> cols) {
+        [](std::shared_ptr<Table> l, std::shared_ptr<Table> r, JoinMode mode, std::pair<ColumnID, ColumnID> cols,
+           uint32_t radix_bits) {
           py::gil_scoped_release rel;
-          return oracle::join_hash(l, r, mode, cols);
-        });
+          return oracle::join_hash(l, r, mode, cols, radix_bits);
+        },
+        py::arg("left"), py::arg("right"), py::arg("mode"), py::arg("cols"),
+        py::arg("radix_bits") = 0);  // 0: the reference formula (join_hash.cpp:640-668); else the constructor's value
   m.def("projection", [](std::shared_ptr<Table> in, std::vector<std::shared_ptr<AbstractExpression>> exprs) {
     py::gil_scoped_release rel;
     return oracle::projection(in, exprs);

@@ -106,3 +106,25 @@ def test_skewed_keys_use_sub_tables(hy, oracle, mode):
     j.execute()
     exp, _ = oracle.join_hash(a, b, getattr(hy.JoinMode, mode), (0, 0))
     assert_identical(j.get_output(), exp)
+
+
+@pytest.mark.parametrize("cond,value", [("LessThan", 24), ("GreaterThanEquals", 7)])
+def test_scan_over_join_output(hy, oracle, cond, value):
+    """TableScan over a JoinHash output: every output chunk's PosList references hundreds of lineitem chunks, so the
+    scan runs in the reference's split_pos_list_by_chunk_id group order (chunk_offset_mapping.cpp:5-21,
+    base_single_column_table_scan_impl.cpp:36-60) - one device scan plus the stable group-order sort
+    (hy_reference_scan_order) - and equals the oracle's scan of the oracle's join, RowID for RowID."""
+    rng = np.random.default_rng(11)
+    orders, lineitem = orders_lineitem(hy, 60_000, 700, rng)
+    hy.encode_all_chunks(lineitem, hy.EncodingType.Dictionary)
+    o, l = wrap(hy, orders), wrap(hy, lineitem)
+    j = hy.JoinHash(o, l, hy.JoinMode.Inner, (0, 0), hy.PredicateCondition.Equals)
+    j.execute()
+    exp_j, _ = oracle.join_hash(orders, lineitem, hy.JoinMode.Inner, (0, 0))
+    assert_identical(j.get_output(), exp_j)
+    pc = getattr(hy.PredicateCondition, cond)
+    s = hy.TableScan(j, 2, pc, value)  # l_quantity of the join output (orders' column first)
+    s.execute()
+    exp_s = oracle.table_scan(exp_j, 2, pc, value, [])
+    assert exp_s.row_count() > 0
+    assert_identical(s.get_output(), exp_s)

@@ -142,3 +142,47 @@ def test_scan_join_empty_and_all_none(hy, oracle):
     parts = run_fused(hy, dt.join_side(capi, ok), None, dt.join_side(capi, lk), lf.f, params, okey.size + 16)
     assert sum(p.shape[0] for _, p in parts) == 0
     assert all(o.size == 0 for o in lf.scan_output())
+
+
+@pytest.mark.parametrize("bits", [12, 16, 20])
+@pytest.mark.parametrize("mode", ["Inner", "Left", "Semi"])
+@pytest.mark.parametrize("key_enc,filtered", [("Unencoded", True), ("Dictionary", True), ("Unencoded", False)])
+@pytest.mark.parametrize("onepass,cap", [(False, None), (True, None), (True, "64")])
+def test_multi_digit_plans(hy, oracle, monkeypatch, bits, mode, key_enc, filtered, onepass, cap):
+    """Radix plans of two and three digits through the default two-read first pass, the opt-in single-pass first
+    radix pass (HY_ONEPASS=1, part1_onepass: gapped per-class bucket regions, look-back per digit) and, with
+    HY_ONEPASS_CAP=64, its overflow fallback: scan output and every partition's PosLists equal the oracle's at the
+    same radix bits (the reference constructor's radix_bits, join_hash.hpp:28)."""
+    if onepass:
+        monkeypatch.setenv("HY_ONEPASS", "1")
+    if cap is not None:
+        monkeypatch.setenv("HY_ONEPASS_CAP", cap)
+    capi = hy.capi
+    rng = np.random.default_rng(zlib.crc32(repr((bits, mode, key_enc, filtered)).encode()))
+    okey, ostatus, lkey, lkey_nulls, qty, qty_nulls = orders_lineitem(rng, 30_000, True)
+    lchunk, ochunk = 6_000, 5_000
+    lineitem = hy.Table.from_arrays([("l_orderkey", hy.DataType.Int, True), ("l_quantity", hy.DataType.Float, True)],
+                                    [lkey, qty], [lkey_nulls, qty_nulls], lchunk)
+    orders = hy.Table.from_arrays([("o_orderkey", hy.DataType.Int, False), ("o_status", hy.DataType.Int, False)],
+                                  [okey, ostatus], [], ochunk)
+    probe_t = oracle.table_scan(lineitem, 1, hy.PredicateCondition.LessThan, 24.0, []) if filtered else lineitem
+    jm = getattr(hy.JoinMode, mode)
+    # orders (the smaller input) builds for Inner; Left / Semi swap so that lineitem's rows are the build side
+    expected, used = oracle.join_hash(orders, probe_t, jm, (0, 0), radix_bits=bits)
+    assert used == bits
+    lk = dt.DeviceColumn(capi, lkey, lkey_nulls, lchunk, key_enc)
+    lq = dt.DeviceColumn(capi, qty, qty_nulls, lchunk, "Dictionary")
+    ok = dt.DeviceColumn(capi, okey, None, ochunk, "Unencoded")
+    lf = Filter(capi, lq, "LessThan", 24.0) if filtered else None
+    swapped = mode in ("Left", "Semi") or orders.row_count() > probe_t.row_count()
+    params = capi.JoinParams({"Inner": 0, "Left": 1, "Semi": 5}[mode], capi.HY_TYPE_INT32, bits, 17)
+    cap_pairs = okey.size * 3 + lkey.size + 16
+    o_side, l_side = dt.join_side(capi, ok), dt.join_side(capi, lk)
+    l_f = lf.f if lf else None
+    if swapped:
+        parts = run_fused(hy, l_side, l_f, o_side, None, params, cap_pairs)
+    else:
+        parts = run_fused(hy, o_side, None, l_side, l_f, params, cap_pairs)
+    if lf is not None:
+        check_scan(probe_t, lf)
+    check_join(expected, parts, 2, swapped, mode == "Semi")
