@@ -17,7 +17,11 @@ HOST_SRC  := $(CSRC)/host/storage.cpp $(CSRC)/host/device.cpp $(CSRC)/host/opera
              $(CSRC)/host/projection.cpp
 HOST_HDR  := $(wildcard $(CSRC)/host/*.hpp) include/hyrise_amd.h
 
-all: $(LIB)/libhyrise_amd.so $(LIB)/libhyrise_host.so $(LIB)/_hyrise_host$(EXTSUF)
+all: $(LIB)/libhyrise_amd.so $(LIB)/libhyrise_host.so $(LIB)/_hyrise_host$(EXTSUF) $(LIB)/exchange_check
+
+# native (no Python, no torch) check of the C-ABI RCCL exchange, run by tests/test_dist_join_gpu.py on the GPU
+$(LIB)/exchange_check: tests/native/exchange_check.cpp include/hyrise_amd.h $(LIB)/libhyrise_amd.so
+	$(HIPCC) -std=c++17 -O2 -Iinclude -o $@ $< -L$(LIB) -lhyrise_amd -Wl,-rpath,'$$ORIGIN'
 
 CAPI_HDR  := include/hyrise_amd.h $(CSRC)/capi/capi_common.hpp $(CSRC)/kernels/common.hpp
 
@@ -42,8 +46,13 @@ $(LIB)/hyrise_amd_order.o: $(CSRC)/capi/hyrise_amd_order.hip $(CAPI_HDR)
 	@mkdir -p $(LIB)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
-$(LIB)/libhyrise_amd.so: $(LIB)/hyrise_amd.o $(LIB)/hyrise_amd_aggregate.o $(LIB)/hyrise_amd_order.o $(JOIN_OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+$(LIB)/hyrise_amd_comm.o: $(CSRC)/capi/hyrise_amd_comm.hip $(CAPI_HDR)
+	@mkdir -p $(LIB)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIB)/libhyrise_amd.so: $(LIB)/hyrise_amd.o $(LIB)/hyrise_amd_aggregate.o $(LIB)/hyrise_amd_order.o \
+                         $(LIB)/hyrise_amd_comm.o $(JOIN_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 $(LIB)/libhyrise_host.so: $(HOST_SRC) $(HOST_HDR) $(LIB)/libhyrise_amd.so
 	$(CXX) $(CXXFLAGS) -shared -o $@ $(HOST_SRC) -L$(LIB) -lhyrise_amd -Wl,-rpath,'$$ORIGIN'

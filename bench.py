@@ -42,6 +42,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (RCCL; one GPU per rank) or gloo (host-staged exchange: rehearsal of N ranks on one GPU)")
+    p.add_argument("--transport", choices=["capi", "torch"], default="torch",
+                   help="N>1 over RCCL: torch's all_to_all (default: torch bundles its own RCCL / HIP runtime) or the "
+                        "library's own communicator (hy_join_exchange_counts/records, the C++ integration's path)")
     p.add_argument("--workload", choices=["join", "q1", "q3"], default="join",
                    help="join: the headline TableScan+JoinHash (BASELINE.json metric); q1: BASELINE config 4, "
                         "TPC-H 1 TableScan -> Projection -> Aggregate (8 aggregates) on one GPU; q3: BASELINE config 5 at N=1, "
@@ -72,7 +75,7 @@ def main():
         import bench_tpch
 
         return bench_tpch.main_q1(args) if args.workload == "q1" else bench_tpch.main_q3(args)
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 or os.environ.get("HY_BENCH_DIST"):  # (env: rehearse at N = 1)
         import bench_dist
 
         return bench_dist.main_distributed(args)

@@ -111,14 +111,27 @@ def main_distributed(args):
                             build_layout=sh["o_layout"], probe_layout=sh["l_layout"])
     rb = xj.record_bytes
     state = {}
+    # RCCL transport: the library's own communicator (default) or torch.distributed's all_to_all (--transport torch)
+    rx, transport_note = None, "torch all_to_all"
+    if args.dist_backend == "nccl" and args.transport == "capi":
+        try:
+            rx = hdist.RcclExchange(capi, dist, rank, world, dev)
+            transport_note = "hy_join_exchange_counts/records (C-ABI RCCL communicator)"
+        except Exception as e:  # noqa: BLE001 - recorded in the bench line, the run continues on torch's RCCL
+            transport_note = f"torch all_to_all (C-ABI communicator failed: {e})"
 
     def step():
         brec, bcnt = xj.partition(build_side, n_ord, False, stream, dev, key="build", row_base=sh["o_row_base"])
         precs, pcnt = xj.partition(probe_side, n_li, False, stream, dev, key="probe", filt=pfilter,
                                    row_base=sh["l_row_base"])
-        brecv, bmat = hdist.exchange_records(dist, brec.to(xdev), bcnt, rank, world, device=xdev, record_bytes=rb)
-        precv, pmat = hdist.exchange_records(dist, precs.to(xdev), pcnt, rank, world, device=xdev, record_bytes=rb)
-        brecv, precv = brecv.to(dev), precv.to(dev)
+        if rx is not None:  # the C-ABI's RCCL exchange (hy_join_exchange_counts / _records)
+            brecv, bmat = rx.exchange(brec, bcnt, rb, stream)
+            precv, pmat = rx.exchange(precs, pcnt, rb, stream)
+        else:
+            brecv, bmat = hdist.exchange_records(dist, brec.to(xdev), bcnt, rank, world, device=xdev, record_bytes=rb)
+            precv, pmat = hdist.exchange_records(dist, precs.to(xdev), pcnt, rank, world, device=xdev,
+                                                 record_bytes=rb)
+            brecv, precv = brecv.to(dev), precv.to(dev)
         out = xj.join(brecv, bmat, precv, pmat, rank, stream, dev)
         state["recv_rows"] = (int(bmat.sum()), int(pmat.sum()))
         state["sent_bytes"] = (int(bcnt.sum()) + int(pcnt.sum())) * rb
@@ -174,7 +187,7 @@ def main_distributed(args):
             "config": {"workload": f"TableScan(l_quantity<24, dictionary u8) fused into the exchange partition -> "
                                    f"distributed JoinHash(orders ⋈ scan, o_orderkey=l_orderkey, "
                                    f"radix_bits={radix_bits})",
-                       "path": "hy_scan_join_exchange_partition + all_to_all + hy_join_exchange_join_rows",
+                       "path": "hy_scan_join_exchange_partition + " + transport_note + " + hy_join_exchange_join_rows",
                        "sf_total": global_sf, "lineitem_rows": n_li_g, "orders_rows": n_ord_g, "chunk_size": chunk,
                        "scan_matches": g_probe, "join_pairs": g_pairs, "record_bytes": rb,
                        "exchange_bytes_per_step": g_sent,
@@ -189,4 +202,6 @@ def main_distributed(args):
             "cpu_baseline": None,
         }
         print(json.dumps(line))
+    if rx is not None:
+        rx.close()
     dist.destroy_process_group()

@@ -190,7 +190,22 @@ _sigs = {
                                                   ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
                                                   ctypes.POINTER(JoinResult), ctypes.c_void_p, ctypes.c_size_t,
                                                   ctypes.c_void_p]),
+    "hy_comm_get_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
+    "hy_comm_init": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32]),
+    "hy_comm_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "hy_join_exchange_counts": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32,
+                                               ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p]),
+    "hy_join_exchange_records": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                                ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32, ctypes.c_void_p,
+                                                ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
+                                                ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p]),
+    "hy_reference_scan_order_workspace_size": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32,
+                                                              ctypes.POINTER(ctypes.c_size_t)]),
+    "hy_reference_scan_order": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                               ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.c_size_t, ctypes.c_void_p]),
 }
+HY_COMM_ID_BYTES = 128
 for _name, (_res, _args) in _sigs.items():
     _f = getattr(lib, _name)
     _f.restype = _res

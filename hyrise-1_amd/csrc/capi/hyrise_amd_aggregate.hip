@@ -2,6 +2,8 @@
 // dense / hash path selection and the launches of kernels/aggregate.hip. Host helpers round exact limb sums.
 #include <hip/hip_runtime.h>
 
+#include <unordered_map>
+
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -1013,6 +1015,98 @@ hy_status hy_agg_float_sum(const uint64_t* limbs, uint32_t n_limbs, int32_t emin
   if (low > 0x400u || (low == 0x400u && (sticky || (mant & 1u)))) ++mant;
   const double v = std::ldexp(static_cast<double>(mant), static_cast<int>(msb - 52 + emin));
   *out = neg ? -v : v;
+  return HY_OK;
+}
+
+// Merge of partial aggregates (the multi-GPU Aggregate: each rank aggregates its chunk range, the ranks' records are
+// all-gathered and merged here). Exact: counts and integer sums add; float sums add limb by limb in 128-bit and are
+// carry-normalised back into the layout's limbs (the exact sum of the parts, so hy_agg_float_sum of the merged record
+// equals that of a single-GPU aggregate over all rows); MIN / MAX take the extreme order-preserving bits of the parts
+// with values; the first / last row words take the parts' row bases (global row numbering) and combine by min / max.
+hy_status hy_aggregate_merge(const hy_agg_params* params, const hy_agg_layout* layout, const uint64_t* const* parts,
+                             const uint64_t* part_groups, const uint64_t* part_row_base, uint32_t n_parts,
+                             uint64_t* out, uint64_t out_capacity, uint64_t* n_out) {
+  if (!params || !layout || !n_out || (n_parts && (!parts || !part_groups))) return fail(HY_ERR_INVALID_ARGUMENT, "null");
+  const uint32_t W = layout->words, G = params->n_groupby;
+  for (uint32_t a = 0; a < params->n_aggregates; ++a)
+    if (params->aggregates[a].function == HY_AGG_COUNT_DISTINCT)
+      return fail(HY_ERR_UNSUPPORTED, "COUNT(DISTINCT) partials cannot be merged from counts");
+  std::vector<std::vector<uint64_t>> merged;
+  std::vector<std::vector<__int128>> wide;  // per merged group: float-sum limbs summed in 128 bits
+  std::unordered_map<std::string, size_t> index;
+  for (uint32_t p = 0; p < n_parts; ++p) {
+    const uint64_t base = part_row_base ? part_row_base[p] : 0;
+    for (uint64_t g = 0; g < part_groups[p]; ++g) {
+      const uint64_t* r = parts[p] + g * W;
+      const std::string key(reinterpret_cast<const char*>(r), 8 * (G + 1));  // key words + NULL mask
+      auto it = index.find(key);
+      if (it == index.end()) {
+        it = index.emplace(key, merged.size()).first;
+        std::vector<uint64_t> m(r, r + W);
+        m[G + 1] += base;
+        m[G + 2] += base;
+        merged.push_back(std::move(m));
+        std::vector<__int128> wl;
+        for (uint32_t a = 0; a < params->n_aggregates; ++a)
+          for (uint32_t i = 0; i < layout->agg_limbs[a]; ++i)
+            wl.push_back(static_cast<__int128>(static_cast<int64_t>(r[layout->agg_word[a] + 2 + i])));
+        wide.push_back(std::move(wl));
+        continue;
+      }
+      auto& m = merged[it->second];
+      auto& wl = wide[it->second];
+      m[G + 1] = std::min(m[G + 1], r[G + 1] + base);
+      m[G + 2] = std::max(m[G + 2], r[G + 2] + base);
+      m[G + 3] += r[G + 3];
+      size_t li = 0;
+      for (uint32_t a = 0; a < params->n_aggregates; ++a) {
+        const int32_t f = params->aggregates[a].function;
+        const uint32_t w = layout->agg_word[a];
+        if (params->aggregates[a].column < 0) continue;  // COUNT(*): the rows word
+        if (f == HY_AGG_COUNT) {
+          m[w] += r[w];
+        } else if (f == HY_AGG_MIN || f == HY_AGG_MAX) {
+          if (r[w] != 0) {
+            if (m[w] == 0)
+              m[w + 1] = r[w + 1];
+            else
+              m[w + 1] = f == HY_AGG_MIN ? std::min(m[w + 1], r[w + 1]) : std::max(m[w + 1], r[w + 1]);
+          }
+          m[w] += r[w];
+        } else if (layout->agg_limbs[a] == 0) {  // integer SUM / AVG
+          m[w] += r[w];
+          m[w + 1] += r[w + 1];
+        } else {  // float SUM / AVG
+          m[w] += r[w];
+          m[w + 1] |= r[w + 1];
+          for (uint32_t i = 0; i < layout->agg_limbs[a]; ++i)
+            wl[li + i] += static_cast<__int128>(static_cast<int64_t>(r[w + 2 + i]));
+        }
+        li += layout->agg_limbs[a];
+      }
+    }
+  }
+  *n_out = merged.size();
+  if (merged.size() > out_capacity) return fail(HY_ERR_CAPACITY, "merged groups exceed out_capacity");
+  for (size_t g = 0; g < merged.size(); ++g) {
+    auto& m = merged[g];
+    size_t li = 0;
+    for (uint32_t a = 0; a < params->n_aggregates; ++a) {
+      const uint32_t n = layout->agg_limbs[a], w = layout->agg_word[a];
+      __int128 carry = 0;
+      for (uint32_t i = 0; i < n; ++i) {  // base-2^32 digits, the remaining carry in the top limb
+        const __int128 t = carry + wide[g][li + i];
+        if (i + 1 < n) {
+          m[w + 2 + i] = static_cast<uint64_t>(t & 0xFFFFFFFF);
+          carry = t >> 32;
+        } else {
+          m[w + 2 + i] = static_cast<uint64_t>(static_cast<int64_t>(t));
+        }
+      }
+      li += n;
+    }
+    if (out) std::memcpy(out + g * W, m.data(), 8ull * W);
+  }
   return HY_OK;
 }
 

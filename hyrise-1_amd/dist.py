@@ -64,6 +64,57 @@ def exchange_records(dist, records, bucket_counts, rank, world, device=None, rec
     return out, recv_matrix
 
 
+class RcclExchange:
+    """The exchange step through the C-ABI's own RCCL communicator (hy_comm_init, hy_join_exchange_counts,
+    hy_join_exchange_records): what a C++ Hyrise process linking libhyrise_amd.so calls. torch.distributed only hands
+    rank 0's 128-byte communicator id to the other ranks. Opt-in from Python (bench.py --transport capi): a torch
+    process also loads torch's bundled RCCL and HIP runtime under the same sonames, and which one libhyrise_amd.so's
+    RCCL calls resolve to depends on load order; the native check (tests/native/exchange_check.cpp) runs without
+    torch."""
+
+    def __init__(self, capi, dist, rank, world, device):
+        import torch
+
+        self.capi, self.lib, self.rank, self.world = capi, capi.lib, rank, world
+        cid = (ctypes.c_char * capi.HY_COMM_ID_BYTES)()
+        if rank == 0:
+            capi.check(self.lib.hy_comm_get_unique_id(cid), "hy_comm_get_unique_id")
+        t = torch.tensor(list(bytes(cid)), dtype=torch.uint8, device=device)
+        dist.broadcast(t, 0)
+        cid = (ctypes.c_char * capi.HY_COMM_ID_BYTES)(*t.cpu().tolist())
+        self.comm = ctypes.c_void_p()
+        capi.check(self.lib.hy_comm_init(ctypes.byref(self.comm), world, cid, rank), "hy_comm_init")
+
+    def close(self):
+        if self.comm:
+            self.capi.check(self.lib.hy_comm_destroy(self.comm), "hy_comm_destroy")
+            self.comm = ctypes.c_void_p()
+
+    def exchange(self, records, bucket_counts, record_bytes, stream, out=None):
+        """Same contract as exchange_records: returns (received records as int64 words, recv_matrix[s][j])."""
+        import torch
+
+        capi, lib = self.capi, self.lib
+        nb = len(bucket_counts)
+        counts = (ctypes.c_uint64 * nb)(*[int(x) for x in bucket_counts])
+        all_counts = (ctypes.c_uint64 * (nb * self.world))()
+        capi.check(lib.hy_join_exchange_counts(self.comm, counts, nb, all_counts, stream), "hy_join_exchange_counts")
+        _, recv, recv_matrix = exchange_plan(np.frombuffer(all_counts, dtype=np.uint64).reshape(self.world, nb),
+                                             self.rank, self.world)
+        words = record_bytes // 8
+        if out is None or out.numel() < max(1, sum(recv)) * words:
+            out = torch.empty(max(1, sum(recv)) * words, dtype=torch.int64, device=records.device)
+        lo, hi = owned_buckets(nb, self.rank, self.world)
+        rc = (ctypes.c_uint64 * max(1, self.world * (hi - lo)))()
+        rows = ctypes.c_uint64()
+        capi.check(lib.hy_join_exchange_records(self.comm, records.data_ptr(), record_bytes, all_counts, nb,
+                                                out.data_ptr(), out.numel() // words, rc, ctypes.byref(rows), stream),
+                   "hy_join_exchange_records")
+        got = np.frombuffer(rc, dtype=np.uint64)[: self.world * (hi - lo)].reshape(self.world, hi - lo)
+        assert np.array_equal(got.astype(np.int64), recv_matrix.astype(np.int64))
+        return out[: int(rows.value) * words], recv_matrix
+
+
 class ExchangeJoin:
     """The two C-ABI steps of the distributed JoinHash on device buffers owned by torch tensors.
 

@@ -393,6 +393,35 @@ hy_status hy_join_exchange_join_rows(const void* build_records, const uint64_t* 
                                      void* workspace, size_t workspace_bytes, hy_stream_t stream);
 
 /*
+ * The exchange step between step 1 and step 2 over RCCL (xGMI), so that a C++ process runs the distributed join
+ * without another runtime. One communicator per process (one process per GPU): rank 0 calls hy_comm_get_unique_id
+ * and hands the 128 bytes to the other ranks over the host's own channel (the reference's network layer or a TCP
+ * store), then every rank calls hy_comm_init on its device. Per side:
+ *   hy_join_exchange_counts   all-gather of the B bucket counts (host in, host out: all_counts[s * B + b], N * B
+ *                             entries; synchronises the stream);
+ *   hy_join_exchange_records  sends this rank's records (grouped by bucket, as step 1 wrote them) to the buckets'
+ *                             owners and receives, sender after sender, the records of its own buckets into
+ *                             recv_records (device, recv_capacity records of record_bytes each); recv_counts (host,
+ *                             N * n_local_buckets) is exactly the counts matrix step 2 takes; *recv_rows = rows
+ *                             received. HY_ERR_CAPACITY (with *recv_rows set, nothing sent) if the buffer is too small.
+ * Asynchronous on `stream` like the other entry points; RCCL's send/recv round is stream-ordered.
+ */
+#define HY_COMM_ID_BYTES 128
+typedef struct hy_comm_id {
+  char bytes[HY_COMM_ID_BYTES];
+} hy_comm_id;
+typedef struct hy_comm_s* hy_comm_t;
+hy_status hy_comm_get_unique_id(hy_comm_id* id);
+hy_status hy_comm_init(hy_comm_t* comm, int32_t n_ranks, const hy_comm_id* id, int32_t rank);
+hy_status hy_comm_destroy(hy_comm_t comm);
+hy_status hy_join_exchange_counts(hy_comm_t comm, const uint64_t* bucket_counts, uint32_t n_buckets,
+                                  uint64_t* all_counts, hy_stream_t stream);
+hy_status hy_join_exchange_records(hy_comm_t comm, const void* records, uint32_t record_bytes,
+                                   const uint64_t* all_counts, uint32_t n_buckets, void* recv_records,
+                                   uint64_t recv_capacity, uint64_t* recv_counts, uint64_t* recv_rows,
+                                   hy_stream_t stream);
+
+/*
  * out[i] = rows[i] is NULL ? rows[i] : chunk_pos_lists[rows[i].chunk_id][rows[i].chunk_offset]
  * (reference write_output_columns, join_hash.cpp:584-592). chunk_pos_lists: DEVICE array of device PosList pointers.
  */
@@ -524,6 +553,17 @@ hy_status hy_projection(const hy_agg_input* input, const hy_expr_node* program, 
                         uint8_t* out_nulls, void* workspace, size_t workspace_bytes, hy_stream_t stream);
 
 /* Host helpers: the correctly rounded double of an exact limb sum, and the value bits behind an ordered word. */
+/*
+ * Multi-GPU Aggregate: merges the group records of n_parts partial aggregates (same params / layout; parts[p]: HOST
+ * records of part p, part_groups[p] of them; part_row_base[p]: added to the first / last row words, the part's first
+ * row in the global row numbering; may be NULL) into out (HOST, out_capacity records). Exact: counts and integer sums
+ * add, float-sum limbs add and are carry-normalised (hy_agg_float_sum of a merged record = that of one aggregate over
+ * all rows), MIN / MAX combine the parts that have values. COUNT(DISTINCT) -> HY_ERR_UNSUPPORTED. Groups appear in
+ * order of first appearance over the parts; *n_out = merged groups (HY_ERR_CAPACITY if more than out_capacity).
+ */
+hy_status hy_aggregate_merge(const hy_agg_params* params, const hy_agg_layout* layout, const uint64_t* const* parts,
+                             const uint64_t* part_groups, const uint64_t* part_row_base, uint32_t n_parts,
+                             uint64_t* out, uint64_t out_capacity, uint64_t* n_out);
 hy_status hy_agg_float_sum(const uint64_t* limbs, uint32_t n_limbs, int32_t emin, uint64_t special, double* out);
 uint64_t hy_agg_decode_ordered(uint64_t ordered, int32_t value_type);
 

@@ -280,3 +280,21 @@ def test_row_exchange_with_fused_scan_equals_single_gpu(hy, world, mode):
         assert np.array_equal(wp, gp), f"partition {p}: probe RowIDs differ"
         if mode == "INNER":
             assert np.array_equal(wb, gb), f"partition {p}: build RowIDs differ"
+
+
+
+def test_rccl_exchange_entry_points_native():
+    """The C-ABI's RCCL exchange (hy_comm_init, hy_join_exchange_counts, hy_join_exchange_records) from a native
+    process that links only libhyrise_amd.so - the C++ Hyrise integration: one-rank communicator, counts all-gathered,
+    records routed in bucket order with the step-2 counts matrix, HY_ERR_CAPACITY with the exact row count for a
+    too-small buffer (tests/native/exchange_check.cpp, built by `make`). More ranks need more GPUs (RCCL refuses two
+    ranks on one device); a torch process carries its own RCCL and HIP runtime, so bench_dist.py uses torch's
+    all_to_all there by default."""
+    import os
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "hyrise-1_amd", "_lib",
+                       "exchange_check")
+    assert os.path.exists(exe), "build with make"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=90)
+    assert r.returncode == 0 and "exchange_check ok" in r.stdout, r.stdout + r.stderr
