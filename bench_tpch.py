@@ -495,23 +495,36 @@ def main_q1(args):
     import numpy as np
     import torch
 
-    if int(os.environ.get("WORLD_SIZE", "1")) != 1:
-        raise SystemExit("--workload q1 is the single-GPU config (BASELINE.json configs[3])")
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
     sys.path.insert(0, ROOT)
     hy = importlib.import_module("hyrise-1_amd")
     synth = importlib.import_module("hyrise-1_amd.synth")
     capi = hy.capi
     L = capi.lib
-    torch.cuda.set_device(0)
-    dev = torch.device("cuda", 0)
-    capi.check(L.hy_set_device(0), "hy_set_device")
+    dist = None
+    if world > 1:  # multi-GPU Aggregate: chunk ranges per rank, partial records all-gathered and merged exactly
+        import torch.distributed as dist
+
+        if args.dist_backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            torch.cuda.set_device(local % torch.cuda.device_count())
+            dist.init_process_group("gloo")
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    xdev = dev if (dist is None or args.dist_backend == "nccl") else torch.device("cpu")
+    capi.check(L.hy_set_device(dev.index), "hy_set_device")
     stream = torch.cuda.current_stream().cuda_stream
     chunk = args.chunk
     I32, F32 = capi.HY_TYPE_INT32, capi.HY_TYPE_FLOAT
     D = synth.DATE_1998_09_02
 
     cols = synth.q1_columns(args.sf, dev)
-    n = cols["l_shipdate"].numel()
+    n = cols["l_shipdate"].numel()  # rows of the whole table (all ranks)
     # expected results (torch, same columns)
     print(f"q1: {n} lineitem rows generated", file=sys.stderr, flush=True)
     mask = cols["l_shipdate"] <= D
@@ -530,6 +543,15 @@ def main_q1(args):
     n_match_exp = int(mask.sum())
     del mask, gkey, dp, ch, sel
     print("q1: expected results computed", file=sys.stderr, flush=True)
+    # this rank's shard: global chunks [rank * C / N, (rank + 1) * C / N) (strong scaling over the SF database)
+    n_chunks_g = (n + chunk - 1) // chunk
+    c_lo, c_hi = rank * n_chunks_g // world, (rank + 1) * n_chunks_g // world
+    row_lo, row_hi = c_lo * chunk, min(n, c_hi * chunk)
+    if world > 1:
+        cols = {k: v[row_lo:row_hi].contiguous() for k, v in cols.items()}
+        torch.cuda.empty_cache()
+    n_local = row_hi - row_lo
+    price, disc, tax = cols["l_extendedprice"], cols["l_discount"], cols["l_tax"]
     codes = lambda v, scale: torch.round(v.to(torch.float64) * scale).to(torch.int32)
     ship = DictColumn(torch, synth, capi, cols["l_shipdate"], chunk, synth.DATE_1992_01_01,
                       synth.DATE_1998_08_02 + 121 - synth.DATE_1992_01_01 + 1)
@@ -555,7 +577,7 @@ def main_q1(args):
     capi.check(L.hy_table_scan_workspace_size((ctypes.c_uint32 * n_chunks)(*ship.sizes), n_chunks,
                                               ctypes.byref(wsb)), "scan ws")
     scan_ws = torch.empty(max(16, wsb.value), dtype=torch.uint8, device=dev)
-    rows_t = torch.empty(2 * n + 64, dtype=torch.int32, device=dev)
+    rows_t = torch.empty(2 * n_local + 64, dtype=torch.int32, device=dev)
     counts_t = torch.empty(n_chunks, dtype=torch.int32, device=dev)
     L.hy_table_scan_row_ids.restype = ctypes.c_int
     L.hy_table_scan_row_ids.argtypes = [ctypes.POINTER(capi.ScanChunk), ctypes.c_uint32, ctypes.c_int32,
@@ -638,11 +660,36 @@ def main_q1(args):
         capi.check(L.hy_aggregate(ctypes.byref(ain), ctypes.byref(params), state["out"].data_ptr(), 64,
                                   ctypes.byref(ng), state["ws"].data_ptr(), state["ws"].numel(), stream),
                    "hy_aggregate")
-        return int(sizes_np.sum()), ng.value
+        if world == 1:
+            state["records"] = None
+            return int(sizes_np.sum()), ng.value
+        # all-gather of the ranks' partial records (64 x words each, groups count in front) and the exact merge
+        words = state["layout"].words
+        buf = torch.empty(1 + 64 * words, dtype=torch.int64, device=dev)
+        buf[0] = int(ng.value)
+        buf[1:] = state["out"][:64 * words]
+        buf = buf.to(xdev)
+        parts = [torch.empty_like(buf) for _ in range(world)]
+        dist.all_gather(parts, buf)
+        host = [np.ascontiguousarray(t.cpu().numpy().view(np.uint64)) for t in parts]
+        ptrs = (ctypes.POINTER(ctypes.c_uint64) * world)(*[h[1:].ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+                                                           for h in host])
+        ngs = (ctypes.c_uint64 * world)(*[int(h[0]) for h in host])
+        bases = (ctypes.c_uint64 * world)(*[min(n, (r * n_chunks_g // world) * chunk) for r in range(world)])
+        merged = np.zeros((64, words), np.uint64)
+        n_out = ctypes.c_uint64()
+        capi.check(L.hy_aggregate_merge(ctypes.byref(params), ctypes.byref(state["layout"]), ptrs, ngs, bases, world,
+                                        merged.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), 64,
+                                        ctypes.byref(n_out)), "hy_aggregate_merge")
+        state["records"] = merged[:n_out.value]
+        return int(sizes_np.sum()), n_out.value
 
     print("q1: columns encoded, running", file=sys.stderr, flush=True)
     for _ in range(args.warmup):
         step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
     torch.cuda.synchronize()
     L.hy_kernel_stats_reset()
     L.hy_kernel_stats_enable(1)
@@ -650,12 +697,25 @@ def main_q1(args):
     for _ in range(args.steps):
         n_match, n_groups = step()
     torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     L.hy_kernel_stats_enable(0)
+    if dist is not None:  # max over ranks; scan matches summed over ranks
+        t = torch.tensor([elapsed], dtype=torch.float64, device=xdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        m = torch.tensor([n_match], dtype=torch.int64, device=xdev)
+        dist.all_reduce(m, op=dist.ReduceOp.SUM)
+        n_match = int(m.item())
 
     # ---- check ----
     lay = state["layout"]
-    rec = state["out"].view(-1, lay.words)[:n_groups].cpu().numpy().view(np.uint64)
+    if state["records"] is not None:
+        rec = state["records"]
+    else:
+        rec = state["out"].view(-1, lay.words)[:n_groups].cpu().numpy().view(np.uint64)
 
     def fsum(r, a):
         w = lay.agg_word[a]
@@ -680,6 +740,9 @@ def main_q1(args):
         groups["ANR"[int(r[0])] + "FO"[int(r[1])]] = vals
     if not ok:
         raise SystemExit(f"q1 result mismatch: {groups} vs {exp}")
+    if rank != 0:
+        dist.destroy_process_group()
+        return
 
     from bench import kernel_stats, measured_roofline, host_cpu  # noqa: E402  (shared helpers)
 
@@ -706,15 +769,20 @@ def main_q1(args):
                 "traffic": None, "peak_source": "measured in this run (hy_stream_bandwidth_probe, best of read / copy)",
                 "dominant_kernel": dom, "dominant_ms_per_step": round(kernels[dom]["ms_total"] / K, 4)}
     # the reference Aggregate runs ~1e6 rows/s per core: a tenth of --cpu-sf keeps the sample near 10-30 s
-    cpu = None if args.no_cpu_baseline else cpu_baseline_q1(hy, synth, args.cpu_sf / 10, chunk, host_cpu)
+    cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline_q1(hy, synth, args.cpu_sf / 10, chunk,
+                                                                            host_cpu)
     line = {
         "metric": "rows/sec TableScan+Projection+Aggregate, TPC-H 1 on lineitem (BASELINE.json configs[3])",
-        "value": round(n / step_s, 1), "unit": "rows/s", "n_gpus": 1, "steps": K, "warmup": args.warmup,
-        "ms_per_step": round(step_s * 1e3, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "value": round(n / step_s, 1), "unit": "rows/s", "n_gpus": world, "steps": K, "warmup": args.warmup,
+        "ms_per_step": round(step_s * 1e3, 3), "higher_is_better": True,
+        "scaling": "strong" if world > 1 else "weak", "vs_baseline": None,
         "dtype": "f32 (exact sums)", "data": "synthetic (seeded counter-based TPC-H-shaped columns, resident in HBM)",
         "config": {"workload": "TPC-H 1 (tpch_queries.cpp:36-44) without ORDER BY: scan l_shipdate <= 1998-09-02, "
                                "8 aggregates GROUP BY l_returnflag, l_linestatus", "sf": args.sf, "lineitem_rows": n,
-                   "chunk_size": chunk, "scan_matches": n_match, "groups": n_groups, "parallelism": "single GPU"},
+                   "chunk_size": chunk, "scan_matches": n_match, "groups": n_groups,
+                   "parallelism": "single GPU" if world == 1 else
+                   f"chunk-sharded x{world}: per-rank scan + aggregate, all-gather of partial records, exact merge "
+                   f"(hy_aggregate_merge)"},
         "check": {"ok": bool(ok), "groups": groups},
         "roofline": roofline,
         "hbm_probe": probe,
@@ -723,6 +791,8 @@ def main_q1(args):
         "cpu_baseline": cpu,
     }
     print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
 
 
 def cpu_baseline_q1(hy, synth, sf, chunk, host_cpu, runs=5):

@@ -190,6 +190,11 @@ _sigs = {
                                                   ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
                                                   ctypes.POINTER(JoinResult), ctypes.c_void_p, ctypes.c_size_t,
                                                   ctypes.c_void_p]),
+    "hy_aggregate_merge": (ctypes.c_int, [ctypes.POINTER(AggParams), ctypes.POINTER(AggLayout),
+                                          ctypes.POINTER(ctypes.POINTER(ctypes.c_uint64)),
+                                          ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                          ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint64,
+                                          ctypes.POINTER(ctypes.c_uint64)]),
     "hy_comm_get_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
     "hy_comm_init": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32]),
     "hy_comm_destroy": (ctypes.c_int, [ctypes.c_void_p]),

@@ -90,8 +90,11 @@ def fsum_inf(vals):
     return math.fsum(vals)
 
 
-def run(hy, dcols, pos_lists, sizes, doms):
+def run(hy, dcols, pos_lists, sizes, doms, part=None, raw=False):
+    """hy_aggregate over the input (or over input chunks [lo, hi) with part=(lo, hi)); raw: (records, layout,
+    params) instead of the decoded results."""
     capi, L = hy.capi, hy.capi.lib
+    lo, hi = part if part is not None else (0, len(sizes))
     I32, F32 = capi.HY_TYPE_INT32, capi.HY_TYPE_FLOAT
     N_ = capi.ExprNode
     col = lambda j, t=F32: N_(capi.HY_EXPR_COLUMN, t, 0, j, 0)
@@ -101,6 +104,7 @@ def run(hy, dcols, pos_lists, sizes, doms):
     ie = [col(8, I32), N_(capi.HY_EXPR_VALUE, I32, 0, 0, 3), N_(capi.HY_EXPR_MUL, I32, I32, 0, 0),
           N_(capi.HY_EXPR_VALUE, I32, 0, 0, 7), N_(capi.HY_EXPR_SUB, I32, I32, 0, 0)]
     progs = [(N_ * len(p))(*p) for p in (dp, ch, ie)]
+    sizes = sizes[lo:hi]
     n_chunks = len(sizes)
     ac = (capi.AggColumn * 10)()
     pg = 0 if pos_lists is not None else -1
@@ -108,13 +112,15 @@ def run(hy, dcols, pos_lists, sizes, doms):
              3: (F32, dcols[3], 0), 6: (F32, dcols[4], 0), 7: (F32, dcols[5], 0), 8: (I32, dcols[6], 0)}
     keep = []
     for j, (vt, c, dom) in specs.items():
-        arr = (capi.ColumnChunk * len(c.descs))(*c.descs)
+        descs = c.descs if pos_lists is not None else c.descs[lo:hi]
+        arr = (capi.ColumnChunk * len(descs))(*descs)
         keep.append(arr)
-        ac[j].value_type, ac[j].pos_group, ac[j].chunks, ac[j].n_chunks, ac[j].domain = vt, pg, arr, len(c.descs), dom
+        ac[j].value_type, ac[j].pos_group, ac[j].chunks, ac[j].n_chunks, ac[j].domain = vt, pg, arr, len(descs), dom
     for j, p, t in ((4, progs[0], F32), (5, progs[1], F32), (9, progs[2], I32)):
         ac[j].value_type, ac[j].pos_group, ac[j].program, ac[j].n_nodes = t, -1, p, len(p)
     csz = (ctypes.c_uint32 * n_chunks)(*sizes)
-    pls = (ctypes.c_void_p * max(1, n_chunks))(*([p.ptr.value for p in pos_lists] if pos_lists is not None else []))
+    pls = (ctypes.c_void_p * max(1, n_chunks))(*([p.ptr.value for p in pos_lists[lo:hi]] if pos_lists is not None
+                                                  else []))
     inp = capi.AggInput(n_chunks, csz, pls if pos_lists is not None else None, 1 if pos_lists is not None else 0,
                         ac, 10)
     gb = (ctypes.c_int32 * 2)(0, 1)
@@ -131,6 +137,13 @@ def run(hy, dcols, pos_lists, sizes, doms):
     capi.check(L.hy_aggregate(ctypes.byref(inp), ctypes.byref(prm), out.ptr, 64, ctypes.byref(ng), ws.ptr, wsb.value,
                               None), "hy_aggregate")
     rec = out.fetch().reshape(-1, lay.words)[:ng.value]
+    if raw:
+        return rec, lay, prm, (defs, gb)
+    return decode(hy, rec, lay)
+
+
+def decode(hy, rec, lay):
+    capi, L = hy.capi, hy.capi.lib
     res = {}
     for r in rec:
         g = (int(r[0]), int(r[1]))
@@ -238,3 +251,53 @@ def test_lanes_path(hy, monkeypatch, case, input_kind):
         all(same_float(x[1], y[1]) if isinstance(x, tuple) else x == y for x, y in zip(res_lanes[g].values(),
                                                                                        res_fused[g].values()))
         for g in res_lanes)
+
+
+@pytest.mark.parametrize("case", ["clean", "odd_values", "wide_range", "many_groups"])
+@pytest.mark.parametrize("n_parts", [2, 3, 7])
+def test_merge_of_partial_aggregates(hy, case, n_parts):
+    """The multi-GPU Aggregate's merge (hy_aggregate_merge): the input's chunks split into contiguous ranges (one per
+    rank), each aggregated alone, the partial records merged with the ranges' first global rows - equal to ONE
+    aggregate over all chunks: same groups, first / last row words, counts, int sums, and float sums decoding to the
+    same exactly rounded double (exact limb merge)."""
+    capi, L = hy.capi, hy.capi.lib
+    rng = np.random.default_rng(zlib.crc32(f"merge/{case}/{n_parts}".encode()))
+    cols = columns(rng, case)
+    rf, ls, qty, price, disc, tax, iq, price_n, disc_n, doms = cols
+    dcols = [dt.DeviceColumn(capi, rf, None, CHUNK, "Dictionary"), dt.DeviceColumn(capi, ls, None, CHUNK, "Dictionary"),
+             dt.DeviceColumn(capi, qty, None, CHUNK, "Dictionary"),
+             dt.DeviceColumn(capi, price, price_n if price_n.any() else None, CHUNK, "Unencoded"),
+             dt.DeviceColumn(capi, disc, disc_n if disc_n.any() else None, CHUNK, "Dictionary"),
+             dt.DeviceColumn(capi, tax, None, CHUNK, "Dictionary"), dt.DeviceColumn(capi, iq, None, CHUNK, "Unencoded")]
+    sizes = [d.size for d in dcols[0].descs]
+    whole, lay, prm, _keep = run(hy, dcols, None, sizes, doms, raw=True)
+    bounds = np.linspace(0, len(sizes), n_parts + 1).astype(int)
+    parts, keep = [], []
+    for p in range(n_parts):
+        rec, _, _, k = run(hy, dcols, None, sizes, doms, part=(bounds[p], bounds[p + 1]), raw=True)
+        parts.append(np.ascontiguousarray(rec, dtype=np.uint64))
+        keep.append(k)
+    ptrs = (ctypes.POINTER(ctypes.c_uint64) * n_parts)(*[p.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+                                                         for p in parts])
+    ngs = (ctypes.c_uint64 * n_parts)(*[p.shape[0] for p in parts])
+    bases = (ctypes.c_uint64 * n_parts)(*[int(sum(sizes[:bounds[p]])) for p in range(n_parts)])
+    out = np.zeros((64, lay.words), np.uint64)
+    n_out = ctypes.c_uint64()
+    capi.check(L.hy_aggregate_merge(ctypes.byref(prm), ctypes.byref(lay), ptrs, ngs, bases, n_parts,
+                                    out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), 64, ctypes.byref(n_out)),
+               "hy_aggregate_merge")
+    merged = out[:n_out.value]
+    assert n_out.value == whole.shape[0]
+    by_key = lambda recs: {(int(r[0]), int(r[1])): r for r in recs}
+    mw, ww = by_key(merged), by_key(whole)
+    assert set(mw) == set(ww)
+    for g in ww:  # NULL mask, first row, last row, rows
+        assert np.array_equal(mw[g][2:6], ww[g][2:6]), g
+    dm, dw = decode(hy, merged, lay), decode(hy, whole, lay)
+    for g, vals in dw.items():
+        for k, v in vals.items():
+            a = dm[g][k]
+            if isinstance(v, tuple) and isinstance(v[1], float):
+                assert a[0] == v[0] and same_float(a[1], v[1]), (g, k, a, v)
+            else:
+                assert a == v, (g, k, a, v)
