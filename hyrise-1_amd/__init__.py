@@ -61,6 +61,9 @@ ArithmeticExpression = _host.ArithmeticExpression
 expression_common_type = _host.expression_common_type
 LogicError = _host.LogicError
 load_table = _host.load_table
+import_binary = _host.import_binary
+export_binary = _host.export_binary
+load_to_device = _host.load_to_device
 encode_chunks = _host.encode_chunks
 encode_all_chunks = _host.encode_all_chunks
 encode_columns = _host.encode_columns

@@ -62,6 +62,33 @@ hy_status hy_free(void* ptr) {
   return HY_OK;
 }
 
+// Stream-ordered allocations from the device's default memory pool, which keeps freed memory (release threshold =
+// unlimited) for the next allocation instead of returning it to the driver: operator outputs of several GB per query
+// step are then not a hipMalloc + hipFree (and the device-wide synchronisation hipFree implies) each time.
+hy_status hy_malloc_async(void** ptr, size_t bytes, hy_stream_t stream) {
+  if (!ptr) return fail(HY_ERR_INVALID_ARGUMENT, "ptr is NULL");
+  static std::once_flag once;
+  static hipError_t pool_err = hipSuccess;
+  std::call_once(once, [] {
+    int dev = 0;
+    hipMemPool_t pool;
+    pool_err = hipGetDevice(&dev);
+    if (pool_err == hipSuccess) pool_err = hipDeviceGetDefaultMemPool(&pool, dev);
+    if (pool_err == hipSuccess) {
+      uint64_t threshold = UINT64_MAX;
+      pool_err = hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &threshold);
+    }
+  });
+  HY_HIP(pool_err);
+  HY_HIP(hipMallocAsync(ptr, std::max<size_t>(256, (bytes + 255) & ~size_t(255)), S(stream)));
+  return HY_OK;
+}
+
+hy_status hy_free_async(void* ptr, hy_stream_t stream) {
+  if (ptr) HY_HIP(hipFreeAsync(ptr, S(stream)));
+  return HY_OK;
+}
+
 hy_status hy_memcpy_htod(void* dst, const void* src, size_t bytes, hy_stream_t stream) {
   if (bytes) HY_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, S(stream)));
   return HY_OK;

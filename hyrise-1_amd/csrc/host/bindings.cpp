@@ -258,6 +258,10 @@ PYBIND11_MODULE(_hyrise_host, m) {
       });
 
   m.def("load_table", &load_table, py::arg("file_name"), py::arg("chunk_size") = CHUNK_MAX_SIZE);
+  m.def("import_binary", &import_binary, py::arg("filename"));
+  m.def("export_binary", [](std::shared_ptr<Table> t, const std::string& f) { export_binary(t, f); },
+        py::arg("table"), py::arg("filename"));
+  m.def("load_to_device", [](std::shared_ptr<Table> t) { load_to_device(t); }, py::arg("table"));
   m.def("encode_chunks", &ChunkEncoder::encode_chunks);
   m.def("encode_all_chunks", &ChunkEncoder::encode_all_chunks);
   m.def("encode_columns", &ChunkEncoder::encode_columns);

@@ -24,6 +24,7 @@ inline void hy_check(hy_status st, const char* what) {
 // is ordered on that thread's stream - so a reused block is never written before the kernels that read it finished,
 // and releasing it neither frees device memory nor waits for the device (hipFree synchronises the whole device).
 void* temp_block_acquire(size_t bytes, size_t* block_bytes);
+hy_stream_t operator_stream();
 void temp_block_release(void* ptr, size_t block_bytes);
 
 // Owning device allocation. Temporary (the `stream` constructor): a block of the calling thread's cache, for buffers
@@ -32,14 +33,16 @@ void temp_block_release(void* ptr, size_t block_bytes);
 class DeviceBuffer {
  public:
   DeviceBuffer() = default;
+  // long-lived buffers (operator outputs): stream-ordered on this thread's operator stream, from the device pool
   explicit DeviceBuffer(size_t bytes) : _bytes(bytes) {
-    if (bytes) hy_check(hy_malloc(&_ptr, bytes), "hy_malloc");
+    if (bytes) hy_check(hy_malloc_async(&_ptr, bytes, operator_stream()), "hy_malloc_async");
   }
   DeviceBuffer(size_t bytes, hy_stream_t /*operator stream*/) : _bytes(bytes), _temp(true) {
     if (bytes) _ptr = temp_block_acquire(bytes, &_block);
   }
   ~DeviceBuffer() {
-    if (_ptr) _temp ? temp_block_release(_ptr, _block) : static_cast<void>(hy_free(_ptr));
+    // freed on the null stream: ordered after the work of every (blocking) operator stream that may still read it
+    if (_ptr) _temp ? temp_block_release(_ptr, _block) : static_cast<void>(hy_free_async(_ptr, nullptr));
   }
   DeviceBuffer(const DeviceBuffer&) = delete;
   DeviceBuffer& operator=(const DeviceBuffer&) = delete;

@@ -1,10 +1,28 @@
 #include "operators.hpp"
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <numeric>
 #include <unordered_map>
 
 namespace hyrise {
+
+namespace {
+// HY_OP_TRACE=1: host wall time of operator phases on stderr (where an operator step's time goes)
+struct PhaseTrace {
+  const char* op;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  bool on = std::getenv("HY_OP_TRACE") != nullptr;
+  void mark(const char* phase) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[op] %s %s %.3f ms\n", op, phase, std::chrono::duration<double, std::milli>(now - t).count());
+    t = now;
+  }
+};
+}  // namespace
 
 // reference abstract_operator.cpp:25-54
 void AbstractOperator::execute() {
@@ -203,6 +221,7 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
   _performance_data.rows_in = in_table->row_count();
 
   if (in_table->type() == TableType::Data) {
+    PhaseTrace tr{"TableScan"};
     std::vector<hy_scan_chunk> descs;
     std::vector<ChunkID> chunk_ids;
     std::vector<uint32_t> sizes;
@@ -223,28 +242,20 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
     hy_check(hy_table_scan_workspace_size(sizes.data(), static_cast<uint32_t>(sizes.size()), &ws_bytes),
              "hy_table_scan_workspace_size");
     DeviceBuffer ws(ws_bytes, s);
-    DeviceBuffer offsets(std::max<uint64_t>(total, 1) * 4, s);
+    // one launch writes every chunk's output RowIDs {chunk id, offset} at its input row range of `rows` (the PosLists
+    // the output chunks share), so no per-chunk expansion launch follows
+    auto rows = std::make_shared<DeviceBuffer>(std::max<uint64_t>(total, 1) * sizeof(RowID));
     DeviceBuffer counts(descs.size() * 4, s);
-    hy_check(hy_table_scan(descs.data(), static_cast<uint32_t>(descs.size()), hy_type_of(col_type), constant.bytes,
-                           offsets.as<uint32_t>(), counts.as<uint32_t>(), ws.get(), ws_bytes, s),
-             "hy_table_scan");
+    hy_check(hy_table_scan_row_ids(descs.data(), static_cast<uint32_t>(descs.size()), hy_type_of(col_type),
+                                   constant.bytes, chunk_ids.data(), rows->as<hy_row_id>(), counts.as<uint32_t>(),
+                                   ws.get(), ws_bytes, s),
+             "hy_table_scan_row_ids");
     std::vector<uint32_t> h_counts(descs.size());
     hy_check(hy_memcpy_dtoh(h_counts.data(), counts.get(), 4 * descs.size(), s), "hy_memcpy_dtoh");
     hy_check(hy_stream_synchronize(s), "sync");
-    uint64_t matches = 0;
-    for (auto c : h_counts) matches += c;
-    // device RowIDs for all matches (so downstream GPU operators reuse them), then the host PosLists
-    auto rows = std::make_shared<DeviceBuffer>(std::max<uint64_t>(matches, 1) * sizeof(RowID));
-    uint64_t pos = 0;
+    tr.mark("descriptors + scan + sync");
     std::vector<std::pair<uint64_t, uint32_t>> views;  // (offset, count) per chunk
-    for (size_t k = 0; k < descs.size(); ++k) {
-      if (h_counts[k])
-        hy_check(hy_expand_row_ids(chunk_ids[k], offsets.as<uint32_t>() + descs[k].out_begin, h_counts[k],
-                                   rows->as<hy_row_id>() + pos, s),
-                 "hy_expand_row_ids");
-      views.emplace_back(pos, h_counts[k]);
-      pos += h_counts[k];
-    }
+    for (size_t k = 0; k < descs.size(); ++k) views.emplace_back(descs[k].out_begin, h_counts[k]);
     // output PosLists are lazy views of `rows` (no copy to the host, no wait: later work is ordered on the stream)
     for (size_t k = 0; k < descs.size(); ++k) {
       if (views[k].second == 0) continue;  // reference table_scan.cpp:99: no empty output chunks
@@ -255,6 +266,7 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
         cols.push_back(std::make_shared<ReferenceColumn>(in_table, col, pl));
       output->append_chunk(cols);
     }
+    tr.mark("output chunks");
     return output;
   }
 
@@ -534,6 +546,7 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
   require_device();
   hy_stream_t s = operator_stream();
   _performance_data.rows_in = build_table->row_count() + probe_table->row_count();
+  PhaseTrace tr{"JoinHash"};
 
   JoinSideInput bside = describe_side(build_table, build_col);
   JoinSideInput pside = describe_side(probe_table, probe_col);
@@ -549,6 +562,7 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
   prm.seed = 17;
   _used_radix_bits = prm.radix_bits;
 
+  tr.mark("describe sides");
   size_t ws_bytes = 0;
   hy_check(hy_join_hash_workspace_size(&b, &p, &prm, &ws_bytes), "hy_join_hash_workspace_size");
   DeviceBuffer ws(ws_bytes, s);
@@ -574,6 +588,7 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
   hy_check(hy_memcpy_dtoh(h_begin.data(), part_begin.get(), 8 * n_parts, s), "dtoh");
   hy_check(hy_memcpy_dtoh(h_count.data(), part_count.get(), 4 * n_parts, s), "dtoh");
   hy_check(hy_stream_synchronize(s), "sync");
+  tr.mark("join kernels + partition counts");
 
   std::map<std::pair<int, uint64_t>, std::shared_ptr<PosList>> bcache, pcache;
   std::vector<std::shared_ptr<DeviceBuffer>> bptrs(bside.groups.size()), pptrs(pside.groups.size());
@@ -597,6 +612,7 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
     }
     output->append_chunk(cols);
   }
+  tr.mark("output chunks");
   return output;
 }
 

@@ -177,4 +177,10 @@ class Projection final : public AbstractOperator {
 // JoinHashTraits (reference src/lib/operators/join_hash/hash_traits.hpp:9-42) over data types.
 DataType join_hashed_type(DataType left, DataType right);
 
+// Binary table files (reference ImportBinary / ExportBinary, import_binary.cpp / export_binary.cpp): chunks keep their
+// stored encoding; load_to_device creates every numeric column chunk's HBM mirror (the file's bytes).
+std::shared_ptr<Table> import_binary(const std::string& filename);
+void export_binary(const std::shared_ptr<const Table>& table, const std::string& filename);
+void load_to_device(const std::shared_ptr<const Table>& table);
+
 }  // namespace hyrise

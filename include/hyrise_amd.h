@@ -52,6 +52,10 @@ hy_status hy_get_device_count(int* count);
 hy_status hy_set_device(int device);
 hy_status hy_malloc(void** ptr, size_t bytes);
 hy_status hy_free(void* ptr);
+/* Stream-ordered allocation from the device's memory pool (kept across frees): for operator outputs that live as
+ * long as their table. Freed memory is reused by later allocations ordered after the free on `stream`. */
+hy_status hy_malloc_async(void** ptr, size_t bytes, hy_stream_t stream);
+hy_status hy_free_async(void* ptr, hy_stream_t stream);
 hy_status hy_memcpy_htod(void* dst, const void* src, size_t bytes, hy_stream_t stream);
 hy_status hy_memcpy_dtoh(void* dst, const void* src, size_t bytes, hy_stream_t stream);
 hy_status hy_memcpy_dtod(void* dst, const void* src, size_t bytes, hy_stream_t stream);
@@ -170,7 +174,7 @@ hy_status hy_table_scan_row_ids(const hy_scan_chunk* chunks, uint32_t n_chunks, 
  * are written ascending to out_positions; *count (device) receives the number of matches. Per referenced chunk
  * the predicate is given by ref_scan[row.chunk_id] (op + search_vid, because dictionaries differ per chunk).
  * Group ordering of the reference's unordered_map over referenced chunks is applied by the caller
- * (hy_stable_order_by_group).
+ * (hy_reference_scan_order).
  */
 hy_status hy_reference_scan_workspace_size(uint64_t pos_list_size, size_t* bytes);
 hy_status hy_reference_scan(const hy_row_id* pos_list, uint64_t pos_list_size, const hy_scan_chunk* referenced_chunks,
