@@ -5,6 +5,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <numeric>
+#include <thread>
 #include <unordered_map>
 
 namespace hyrise {
@@ -469,7 +470,6 @@ void write_output_columns(ChunkColumns& out, const std::shared_ptr<const Table>&
                           std::vector<std::shared_ptr<DeviceBuffer>>& group_ptr_arrays,
                           std::vector<std::shared_ptr<DeviceBuffer>>& group_deref,
                           std::shared_ptr<Table>& dummy_table) {
-  hy_stream_t s = operator_stream();
   if (input_table->type() == TableType::Data) {
     auto pl = pos_list_from_device(rows, offset, n);
     for (ColumnID col = 0; col < input_table->column_count(); ++col)
@@ -493,7 +493,8 @@ void write_output_columns(ChunkColumns& out, const std::shared_ptr<const Table>&
     } else {
       auto& cached = cache[{g, offset}];
       if (!cached) {
-        if (!group_deref[g]) {
+        if (!group_deref[g]) {  // (first partition only: the caller builds it before the parallel ones)
+          hy_stream_t s = operator_stream();
           std::vector<const hy_row_id*> ptrs;
           for (const auto& p : side.groups[g]) ptrs.push_back(device_pos_list(*p)->ptr());
           group_ptr_arrays[g] = std::make_shared<DeviceBuffer>(ptrs.size() * sizeof(void*));
@@ -590,28 +591,50 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
   hy_check(hy_stream_synchronize(s), "sync");
   tr.mark("join kernels + partition counts");
 
-  std::map<std::pair<int, uint64_t>, std::shared_ptr<PosList>> bcache, pcache;
   std::vector<std::shared_ptr<DeviceBuffer>> bptrs(bside.groups.size()), pptrs(pside.groups.size());
   std::vector<std::shared_ptr<DeviceBuffer>> bderef(bside.groups.size()), pderef(pside.groups.size());
   std::shared_ptr<Table> bdummy, pdummy;
   uint64_t used = 0;  // the output range the partitions occupy
-  for (uint32_t part = 0; part < n_parts; ++part)
-    if (h_count[part]) used = std::max<uint64_t>(used, h_begin[part] + h_count[part]);
+  std::vector<uint32_t> nonempty;  // join_hash.cpp:835-837: no chunk for an empty partition
   for (uint32_t part = 0; part < n_parts; ++part) {
-    const uint64_t n = h_count[part];
-    if (n == 0) continue;  // join_hash.cpp:835-837
+    if (!h_count[part]) continue;
+    used = std::max<uint64_t>(used, h_begin[part] + h_count[part]);
+    nonempty.push_back(part);
+  }
+  // One output chunk per non-empty partition (join_hash.cpp:829-855), built on several host threads: the first
+  // partition alone (it creates the shared per-side buffers: dereferenced RowIDs, dummy tables), then the rest in
+  // contiguous ranges; the chunks are appended in partition order.
+  auto build_chunk = [&](uint32_t part) {
+    std::map<std::pair<int, uint64_t>, std::shared_ptr<PosList>> bcache, pcache;  // PosLists shared in the chunk
     ChunkColumns cols;
-    const uint64_t b0 = h_begin[part];
+    cols.reserve(output->column_count());
+    const uint64_t n = h_count[part], b0 = h_begin[part];
     if (inputs_swapped) {
       write_output_columns(cols, probe_table, pside, out_p, b0, n, used, pcache, pptrs, pderef, pdummy);
-      if (!semi_anti)
-        write_output_columns(cols, build_table, bside, out_b, b0, n, used, bcache, bptrs, bderef, bdummy);
+      if (!semi_anti) write_output_columns(cols, build_table, bside, out_b, b0, n, used, bcache, bptrs, bderef, bdummy);
     } else {
       write_output_columns(cols, build_table, bside, out_b, b0, n, used, bcache, bptrs, bderef, bdummy);
       write_output_columns(cols, probe_table, pside, out_p, b0, n, used, pcache, pptrs, pderef, pdummy);
     }
-    output->append_chunk(cols);
+    return std::make_shared<Chunk>(std::move(cols));
+  };
+  std::vector<std::shared_ptr<Chunk>> chunks(nonempty.size());
+  if (!nonempty.empty()) chunks[0] = build_chunk(nonempty[0]);
+  const size_t rest = nonempty.size() > 1 ? nonempty.size() - 1 : 0;
+  const unsigned workers =
+      rest < 4096 ? 1u : std::max(1u, std::min<unsigned>(16u, std::thread::hardware_concurrency()));
+  auto run_range = [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) chunks[i] = build_chunk(nonempty[i]);
+  };
+  if (workers == 1) {
+    run_range(1, nonempty.size());
+  } else {
+    std::vector<std::thread> pool;
+    for (unsigned w = 0; w < workers; ++w)
+      pool.emplace_back(run_range, 1 + rest * w / workers, 1 + rest * (w + 1) / workers);
+    for (auto& t : pool) t.join();
   }
+  output->append_chunks(std::move(chunks));
   tr.mark("output chunks");
   return output;
 }

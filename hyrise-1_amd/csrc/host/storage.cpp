@@ -78,6 +78,22 @@ void Table::append_chunk(const ChunkColumns& columns) {
   _chunks.push_back(std::make_shared<Chunk>(columns));
 }
 
+void Table::append_chunks(std::vector<std::shared_ptr<Chunk>>&& chunks) {
+  for (const auto& ch : chunks) {
+    Assert(ch->column_count() == _defs.size(), "append_chunk: wrong number of columns");
+    for (const auto& c : ch->columns()) {
+      Assert(c->size() == ch->size(), "Columns don't have the same length");
+      Assert(c->is_reference() == (_type == TableType::References), "Invalid column type");
+    }
+  }
+  if (_chunks.empty()) {
+    _chunks = std::move(chunks);
+  } else {
+    _chunks.reserve(_chunks.size() + chunks.size());
+    for (auto& ch : chunks) _chunks.push_back(std::move(ch));
+  }
+}
+
 AllTypeVariant Table::get_value(ColumnID column_id, uint64_t row) const {
   for (const auto& c : _chunks) {
     if (row < c->size()) return (*c->get_column(column_id))[static_cast<ChunkOffset>(row)];

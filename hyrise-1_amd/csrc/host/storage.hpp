@@ -283,6 +283,8 @@ class Table {
   // reference table.cpp: append a row, opening a new chunk when the last one is full
   void append(const std::vector<AllTypeVariant>& values);
   void append_chunk(const ChunkColumns& columns);
+  // chunks an operator built (possibly on several threads), appended in order; same checks as append_chunk
+  void append_chunks(std::vector<std::shared_ptr<Chunk>>&& chunks);
   void append_mutable_chunk();
 
   AllTypeVariant get_value(ColumnID column_id, uint64_t row) const;
