@@ -62,7 +62,7 @@ class JoinFilter(ctypes.Structure):
 
 class JoinParams(ctypes.Structure):
     _fields_ = [("mode", ctypes.c_int32), ("hashed_type", ctypes.c_int32), ("radix_bits", ctypes.c_uint32),
-                ("seed", ctypes.c_uint32)]
+                ("seed", ctypes.c_uint32), ("key_hash", ctypes.c_void_p)]
 
 
 class JoinResult(ctypes.Structure):
@@ -195,6 +195,7 @@ _sigs = {
                                           ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                                           ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint64,
                                           ctypes.POINTER(ctypes.c_uint64)]),
+    "hy_murmur2_bytes": (ctypes.c_uint32, [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32]),
     "hy_comm_get_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
     "hy_comm_init": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32]),
     "hy_comm_destroy": (ctypes.c_int, [ctypes.c_void_p]),

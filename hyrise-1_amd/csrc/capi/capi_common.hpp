@@ -59,6 +59,7 @@ struct KStat {
 };
 extern std::mutex g_kt_mutex;
 extern uint64_t* g_join_trace;  // hy_debug_set_join_trace
+extern thread_local const uint32_t* g_key_hash;  // hy_join_params.key_hash of the join running on this thread
 extern bool g_kt_enabled;
 extern std::vector<KernelTiming> g_kt_pending;
 extern std::vector<hipEvent_t> g_kt_pool;

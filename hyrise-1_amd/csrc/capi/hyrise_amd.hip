@@ -23,6 +23,7 @@ namespace hyc {
 thread_local std::string g_last_error;
 std::mutex g_kt_mutex;
 uint64_t* g_join_trace = nullptr;
+thread_local const uint32_t* g_key_hash = nullptr;
 bool g_kt_enabled = false;
 std::vector<KernelTiming> g_kt_pending;
 std::vector<hipEvent_t> g_kt_pool;
@@ -508,6 +509,31 @@ hy_status hy_expand_row_ids(uint32_t chunk_id, const uint32_t* offsets, uint64_t
 // ================================================================================================================
 // Hashing
 // ================================================================================================================
+// MurmurHash2 over a byte string (reference murmur_hash.cpp:21-73; std::string keys, murmur_hash.hpp:16-20): the
+// partitioning hash of string join keys, computed once per distinct string by the JoinHash operator.
+uint32_t hy_murmur2_bytes(const void* bytes, uint32_t len, uint32_t seed) {
+  const uint32_t m = 0x5bd1e995u;
+  uint32_t h = seed ^ len;
+  const auto* data = static_cast<const unsigned char*>(bytes);
+  for (; len >= 4; data += 4, len -= 4) {
+    uint32_t k;
+    std::memcpy(&k, data, 4);
+    h = hyk::murmur_mix_word(h, k);
+  }
+  switch (len) {
+    case 3:
+      h ^= static_cast<uint32_t>(data[2]) << 16;
+      [[fallthrough]];
+    case 2:
+      h ^= static_cast<uint32_t>(data[1]) << 8;
+      [[fallthrough]];
+    case 1:
+      h ^= data[0];
+      h *= m;
+  }
+  return hyk::murmur_final(h);
+}
+
 hy_status hy_murmur2(const void* keys, uint64_t n, uint32_t key_bytes, uint32_t seed, uint32_t* out,
                      hy_stream_t stream) {
   if (n == 0) return HY_OK;

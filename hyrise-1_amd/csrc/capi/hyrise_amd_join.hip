@@ -67,7 +67,13 @@ hy_status hy_scan_join_hash(const hy_join_side* build, const hy_join_filter* bui
   hy_status st = prepare(build, build_filter, probe, probe_filter, params, bp, pp);
   if (st != HY_OK) return st;
   if (!partition_begin || !partition_counts) return fail(HY_ERR_INVALID_ARGUMENT, "partition arrays");
+  if (params->key_hash && params->hashed_type != HY_TYPE_INT32)
+    return fail(HY_ERR_INVALID_ARGUMENT, "key_hash needs int32 key ids");
   hipStream_t s = S(stream);
+  struct KeyHashScope {  // the kernels' Digit carries it (join_host.hpp)
+    explicit KeyHashScope(const uint32_t* k) { g_key_hash = k; }
+    ~KeyHashScope() { g_key_hash = nullptr; }
+  } key_hash_scope(params->key_hash);
   switch (params->hashed_type) {
     case HY_TYPE_INT32:
       return join_i32(bp, pp, build->value_type, probe->value_type, params, out_build, out_probe, out_capacity,
@@ -129,6 +135,7 @@ hy_status hy_join_exchange_partition(const hy_join_side* side, const hy_join_par
                                      size_t workspace_bytes, hy_stream_t stream) {
   if (!params || !bucket_counts || n_ranks == 0) return fail(HY_ERR_INVALID_ARGUMENT, "null argument");
   if (params->radix_bits > 24) return fail(HY_ERR_UNSUPPORTED, "radix_bits > 24");
+  if (params->key_hash) return fail(HY_ERR_UNSUPPORTED, "string join keys in the distributed join");
   SidePlan p;
   hy_status st = plan_side(side, p);
   if (st != HY_OK) return st;
@@ -283,6 +290,7 @@ hy_status hy_scan_join_exchange_partition(const hy_join_side* side, const hy_joi
                                           uint64_t row_base, void* out_records, uint64_t* bucket_counts,
                                           void* workspace, size_t workspace_bytes, hy_stream_t stream) {
   if (!bucket_counts) return fail(HY_ERR_INVALID_ARGUMENT, "bucket_counts");
+  if (params && params->key_hash) return fail(HY_ERR_UNSUPPORTED, "string join keys in the distributed join");
   SidePlan p;
   std::vector<uint32_t> w;
   hy_status st = plan_row_side(side, filter, params, n_ranks, row_base, p, w);

@@ -465,7 +465,7 @@ hy_status pass0_side(const char* side_tag, const SidePlan& p, SideBufs<H, P>& b,
   sd.filter_type = p.filter_type;
   sd.scan_out = p.scan_out;
   const uint32_t n_digits = 1u << w0;
-  hyk::Digit d0{full_mask(bits), bits - w0, n_digits - 1u, seed};
+  hyk::Digit d0{full_mask(bits), bits - w0, n_digits - 1u, seed, g_key_hash};
   HY_HIP(hipMemsetAsync(b.total, 0, 8, s));
   if (p.filtered && p.scan_chunk_begin) HY_HIP(hipMemsetAsync(p.scan_chunk_begin, 0, 8 * (p.chunks.size() + 1), s));
   if (p.n_tiles1 > 0) {
@@ -497,7 +497,7 @@ hy_status record_pass(const char* side_tag, const SideBufs<H, P>& b, const hyk::
                       const hyk::Rec<H, P>* in, const uint8_t* dig_in, const hyk::NextDigit& nd, hyk::Rec<H, P>* out,
                       const uint64_t* total, uint32_t* bounds, const Common& c, hipStream_t s, uint64_t rows) {
   const uint32_t n_digits = 1u << w;
-  hyk::Digit dg{full_mask(bits), shift, n_digits - 1u, seed};
+  hyk::Digit dg{full_mask(bits), shift, n_digits - 1u, seed, g_key_hash};
   if (grid) {
     {
       KTimer kt_((std::string("part2_hist.") + side_tag).c_str(), s, rows);
@@ -873,7 +873,7 @@ hy_status onepass_side(const char* tag, const SidePlan& p, OneBufs<H>& o, uint32
   hipLaunchKernelGGL(hyk::fill_tile_owner, dim3((sd.n_chunks + 255) / 256), dim3(256), 0, s, b.tile_begin, sd.n_chunks,
                      b.tile_owner);
   HY_HIP(hipGetLastError());
-  const hyk::Digit d0{full_mask(bits), bits - w[0], nd0 - 1u, seed};
+  const hyk::Digit d0{full_mask(bits), bits - w[0], nd0 - 1u, seed, g_key_hash};
   const hyk::NextDigit nd = next_digit(w, 0, bits, b.digA);
   static const uint32_t win = [] {
     const char* e = std::getenv("HY_ONEPASS_WIN");

@@ -5,7 +5,6 @@
 #include <cstdio>
 #include <cstdlib>
 #include <numeric>
-#include <thread>
 #include <unordered_map>
 
 namespace hyrise {
@@ -385,7 +384,89 @@ struct JoinSideInput {
   int join_group = -1;
 };
 
-JoinSideInput describe_side(const std::shared_ptr<const Table>& table, ColumnID column_id) {
+// String join keys (JoinHashTraits HashType std::string, hash_traits.hpp:36-41; the other side lexically cast):
+// every distinct string of both sides gets an int32 id ("" = 0, the value NULL rows carry), the device joins the ids,
+// and key_hash[id] = murmur2(string, 17) (murmur_hash.hpp:16-20) makes the radix partitioning the reference's. The
+// id columns are built on the host per column chunk (the device holds no string bytes): dictionary chunks map their
+// dictionary once and each row through its value id, other chunks row by row.
+struct StringKeys {
+  std::unordered_map<std::string, int32_t> ids{{"", 0}};
+  std::vector<uint32_t> hashes{hy_murmur2_bytes("", 0, 17)};
+  std::vector<std::shared_ptr<DeviceBuffer>> keep;  // id / NULL-flag chunks (alive until the join has run)
+  std::shared_ptr<DeviceBuffer> d_hashes;
+
+  int32_t id_of(const std::string& v) {
+    auto it = ids.find(v);
+    if (it != ids.end()) return it->second;
+    const auto id = static_cast<int32_t>(hashes.size());
+    ids.emplace(v, id);
+    hashes.push_back(hy_murmur2_bytes(v.data(), static_cast<uint32_t>(v.size()), 17));
+    return id;
+  }
+
+  hy_column_chunk map(const BaseColumn& column) {
+    const size_t n = column.size();
+    std::vector<int32_t> vals(std::max<size_t>(n, 1) + 4, 0);
+    std::vector<uint8_t> nulls(std::max<size_t>(n, 1) + 16, 0);
+    bool any_null = false;
+    if (const auto* dict = dynamic_cast<const BaseDictionaryColumn*>(&column)) {
+      std::vector<int32_t> entry(dict->unique_values_count());
+      for (size_t v = 0; v < entry.size(); ++v)  // the dictionary's values through the column's operator[]
+        entry[v] = -1;
+      const auto& av = dict->attribute_vector();
+      for (size_t i = 0; i < n; ++i) {
+        const uint32_t vid = av.get(i);
+        if (vid >= entry.size()) {
+          nulls[i] = 1;
+          any_null = true;
+          continue;
+        }
+        if (entry[vid] < 0) entry[vid] = id_of(type_cast<std::string>(column[static_cast<ChunkOffset>(i)]));
+        vals[i] = entry[vid];
+      }
+    } else {
+      for (size_t i = 0; i < n; ++i) {
+        const auto v = column[static_cast<ChunkOffset>(i)];
+        if (variant_is_null(v)) {
+          nulls[i] = 1;
+          any_null = true;
+        } else {
+          vals[i] = id_of(type_cast<std::string>(v));
+        }
+      }
+    }
+    hy_stream_t s = operator_stream();
+    auto d_vals = std::make_shared<DeviceBuffer>(vals.size() * 4);
+    hy_check(hy_memcpy_htod(d_vals->get(), vals.data(), vals.size() * 4, s), "htod");
+    keep.push_back(d_vals);
+    hy_column_chunk c{};
+    c.data = d_vals->get();
+    c.size = static_cast<uint32_t>(n);
+    c.kind = HY_COL_VALUE;
+    if (any_null) {
+      auto d_nulls = std::make_shared<DeviceBuffer>(nulls.size());
+      hy_check(hy_memcpy_htod(d_nulls->get(), nulls.data(), nulls.size(), s), "htod");
+      keep.push_back(d_nulls);
+      c.nulls = static_cast<const uint8_t*>(d_nulls->get());
+    }
+    hy_check(hy_stream_synchronize(s), "sync");  // the host vectors are pageable
+    return c;
+  }
+
+  const uint32_t* upload_hashes() {
+    hy_stream_t s = operator_stream();
+    d_hashes = std::make_shared<DeviceBuffer>(hashes.size() * 4);
+    hy_check(hy_memcpy_htod(d_hashes->get(), hashes.data(), hashes.size() * 4, s), "htod");
+    hy_check(hy_stream_synchronize(s), "sync");
+    return d_hashes->as<uint32_t>();
+  }
+};
+
+JoinSideInput describe_side(const std::shared_ptr<const Table>& table, ColumnID column_id,
+                            StringKeys* strings = nullptr) {
+  auto chunk_desc = [&](const BaseColumn& column) {
+    return strings ? strings->map(column) : device_column(column)->desc;
+  };
   JoinSideInput in;
   const bool is_ref = table->type() == TableType::References;
   if (is_ref) {
@@ -422,13 +503,13 @@ JoinSideInput describe_side(const std::shared_ptr<const Table>& table, ColumnID 
       jc.pos_list = device_pos_list(*rc->pos_list())->ptr();
       if (rc->pos_list()->single_chunk_id() != INVALID_CHUNK_ID) jc.single_chunk = rc->pos_list()->single_chunk_id();
     } else {
-      jc.column = device_column(*column)->desc;
+      jc.column = chunk_desc(*column);
     }
     in.chunks.push_back(jc);
   }
   if (referenced) {
     for (ChunkID r = 0; r < referenced->chunk_count(); ++r)
-      in.referenced.push_back(device_column(*referenced->get_chunk(r)->get_column(rcol))->desc);
+      in.referenced.push_back(chunk_desc(*referenced->get_chunk(r)->get_column(rcol)));
     // fuse the dereference when every column shares the join column's PosLists and referenced table
     bool fuse = true;
     for (ColumnID col = 0; col < table->column_count() && fuse; ++col) {
@@ -530,8 +611,7 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
   const DataType build_type = build_table->column_data_type(build_col);
   const DataType probe_type = probe_table->column_data_type(probe_col);
   const DataType hashed = join_hashed_type(build_type, probe_type);
-  if (hashed == DataType::String)
-    Fail("hyrise-amd: JoinHash on string columns is not supported by the device path");
+  const bool string_keys = hashed == DataType::String;
 
   const bool semi_anti = _mode == JoinMode::Semi || _mode == JoinMode::Anti;
   TableColumnDefinitions defs;
@@ -549,17 +629,23 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
   _performance_data.rows_in = build_table->row_count() + probe_table->row_count();
   PhaseTrace tr{"JoinHash"};
 
-  JoinSideInput bside = describe_side(build_table, build_col);
-  JoinSideInput pside = describe_side(probe_table, probe_col);
-  hy_join_side b{bside.chunks.data(), static_cast<uint32_t>(bside.chunks.size()), hy_type_of(build_type),
+  StringKeys strings;
+  JoinSideInput bside = describe_side(build_table, build_col, string_keys ? &strings : nullptr);
+  JoinSideInput pside = describe_side(probe_table, probe_col, string_keys ? &strings : nullptr);
+  const int32_t btype = string_keys ? HY_TYPE_INT32 : hy_type_of(build_type);
+  const int32_t ptype = string_keys ? HY_TYPE_INT32 : hy_type_of(probe_type);
+  hy_join_side b{bside.chunks.data(), static_cast<uint32_t>(bside.chunks.size()), btype,
                  bside.referenced.data(), static_cast<uint32_t>(bside.referenced.size()), bside.fuse};
-  hy_join_side p{pside.chunks.data(), static_cast<uint32_t>(pside.chunks.size()), hy_type_of(probe_type),
+  hy_join_side p{pside.chunks.data(), static_cast<uint32_t>(pside.chunks.size()), ptype,
                  pside.referenced.data(), static_cast<uint32_t>(pside.referenced.size()), pside.fuse};
   hy_join_params prm{};
   prm.mode = join_mode(_mode);
-  prm.hashed_type = hy_type_of(hashed);
+  prm.hashed_type = string_keys ? HY_TYPE_INT32 : hy_type_of(hashed);
+  if (string_keys) prm.key_hash = strings.upload_hashes();
   // the constructor's radix_bits is ignored and recomputed from the build side (join_hash.cpp:640-668)
-  prm.radix_bits = hy_join_radix_bits(build_table->row_count(), static_cast<uint32_t>(data_type_size(build_type)));
+  // sizeof(LeftType) of the build column's type; a std::string is 32 bytes in libstdc++
+  const uint32_t build_size = build_type == DataType::String ? 32u : static_cast<uint32_t>(data_type_size(build_type));
+  prm.radix_bits = hy_join_radix_bits(build_table->row_count(), build_size);
   prm.seed = 17;
   _used_radix_bits = prm.radix_bits;
 
@@ -601,9 +687,9 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
     used = std::max<uint64_t>(used, h_begin[part] + h_count[part]);
     nonempty.push_back(part);
   }
-  // One output chunk per non-empty partition (join_hash.cpp:829-855), built on several host threads: the first
-  // partition alone (it creates the shared per-side buffers: dereferenced RowIDs, dummy tables), then the rest in
-  // contiguous ranges; the chunks are appended in partition order.
+  // One output chunk per non-empty partition (join_hash.cpp:829-855), in partition order. (Built serially: on
+  // several host threads the chunks' shared_ptr copies of the same tables and buffers contend on their reference
+  // counts - measured 87 ms against 28 ms serial for 65,536 chunks at SF100.)
   auto build_chunk = [&](uint32_t part) {
     std::map<std::pair<int, uint64_t>, std::shared_ptr<PosList>> bcache, pcache;  // PosLists shared in the chunk
     ChunkColumns cols;
@@ -618,22 +704,9 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
     }
     return std::make_shared<Chunk>(std::move(cols));
   };
-  std::vector<std::shared_ptr<Chunk>> chunks(nonempty.size());
-  if (!nonempty.empty()) chunks[0] = build_chunk(nonempty[0]);
-  const size_t rest = nonempty.size() > 1 ? nonempty.size() - 1 : 0;
-  const unsigned workers =
-      rest < 4096 ? 1u : std::max(1u, std::min<unsigned>(16u, std::thread::hardware_concurrency()));
-  auto run_range = [&](size_t lo, size_t hi) {
-    for (size_t i = lo; i < hi; ++i) chunks[i] = build_chunk(nonempty[i]);
-  };
-  if (workers == 1) {
-    run_range(1, nonempty.size());
-  } else {
-    std::vector<std::thread> pool;
-    for (unsigned w = 0; w < workers; ++w)
-      pool.emplace_back(run_range, 1 + rest * w / workers, 1 + rest * (w + 1) / workers);
-    for (auto& t : pool) t.join();
-  }
+  std::vector<std::shared_ptr<Chunk>> chunks;
+  chunks.reserve(nonempty.size());
+  for (const auto part : nonempty) chunks.push_back(build_chunk(part));
   output->append_chunks(std::move(chunks));
   tr.mark("output chunks");
   return output;

@@ -346,11 +346,23 @@ struct Digit {
   uint32_t shift;  // digit = (hash & mask) >> shift
   uint32_t dmask;  // digit &= dmask
   uint32_t seed;
+  // string join keys (hy_join_params.key_hash): int32 keys are ids of distinct strings and key_hash[id] is the
+  // string's murmur2 (murmur_hash.hpp:16-20), so partitioning follows the reference's string hashes; else null
+  const uint32_t* key_hash;
 };
+
+// The partitioning hash of a key: murmur2 over its bytes (join_hash.cpp:253), or the precomputed string hash.
+template <typename H>
+__device__ __forceinline__ uint32_t key_hash_of(const Digit& dg, H key) {
+  if constexpr (std::is_same_v<H, int32_t>) {
+    if (dg.key_hash != nullptr) return dg.key_hash[static_cast<uint32_t>(key)];
+  }
+  return murmur2<H>(key, dg.seed);
+}
 
 template <typename H>
 __device__ __forceinline__ uint32_t digit_of(const Digit& dg, H key) {
-  return ((murmur2<H>(key, dg.seed) & dg.mask) >> dg.shift) & dg.dmask;
+  return ((key_hash_of<H>(dg, key) & dg.mask) >> dg.shift) & dg.dmask;
 }
 
 // The next pass's digit of each record, written beside the records so that the next histogram reads one byte per
@@ -468,7 +480,7 @@ __device__ __forceinline__ void staged_scatter(const Rec<H, P> (&recs)[PART_ITEM
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < total; i += PART_THREADS) {
     const Rec<H, P> r = s_stage[i];
-    const uint32_t h = murmur2<H>(r.key, dg.seed) & dg.mask;
+    const uint32_t h = key_hash_of<H>(dg, r.key) & dg.mask;
     const uint32_t o = i + s_delta[(h >> dg.shift) & dg.dmask];
     out[o] = r;
     if (nd.bytes != nullptr) nd.bytes[o] = static_cast<uint8_t>((h >> nd.shift) & nd.dmask);

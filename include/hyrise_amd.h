@@ -220,6 +220,8 @@ hy_status hy_expand_row_ids(uint32_t chunk_id, const uint32_t* offsets, uint64_t
  * Hashing (reference src/lib/utils/murmur_hash.cpp:21-75, seed 17 from join_hash.cpp:680)
  * ------------------------------------------------------------------------------------------------------------- */
 /* out[i] = murmur_hash2(&keys[i], key_bytes, seed); key_bytes 4 or 8. */
+/* MurmurHash2 of a byte string (murmur_hash.cpp:21-73), host function: the hash of a std::string key. */
+uint32_t hy_murmur2_bytes(const void* bytes, uint32_t len, uint32_t seed);
 hy_status hy_murmur2(const void* keys, uint64_t n, uint32_t key_bytes, uint32_t seed, uint32_t* out,
                      hy_stream_t stream);
 /* Radix bits of JoinHashImpl's constructor (join_hash.cpp:640-668) for a build side of build_rows rows. */
@@ -276,6 +278,11 @@ typedef struct hy_join_params {
   int32_t hashed_type;    /* HY_TYPE_* of JoinHashTraits<L,R>::HashType (hash_traits.hpp:9-42) */
   uint32_t radix_bits;    /* normally hy_join_radix_bits(build rows) */
   uint32_t seed;          /* 17 */
+  /* String join keys (JoinHashTraits HashType std::string, hash_traits.hpp:36-41): NULL, or a device table of
+   * murmur2 hashes of distinct strings (hy_murmur2_bytes): the sides' int32 values are then ids into it (equal
+   * strings, equal ids) and a row's partition follows key_hash[id] - the reference's hash of the string. Single-GPU
+   * joins only (hy_join_hash / hy_scan_join_hash). */
+  const uint32_t* key_hash;
 } hy_join_params;
 
 typedef struct hy_join_result {

@@ -58,3 +58,25 @@ def test_device_murmur_matches_golden(hy):
     keys64 = DA(np.array([1], np.int64))
     hy.capi.check(hy.capi.lib.hy_murmur2(keys64.ptr, 1, 8, 17, out.ptr, None), "murmur")
     assert int(out.fetch()[0]) == int(GOLD["int64"]["1"], 16)
+
+
+def test_string_murmur_matches_reference_file(hy):
+    """hy_murmur2_bytes (the hash of std::string join keys) equals the reference's murmur_hash2 compiled where it
+    lies (oracle/_ref), over empty, short (1-3 tail bytes) and long strings; skipped without the reference build."""
+    import ctypes
+    import os
+
+    ref = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref",
+                       "libref_murmur.so")
+    if not os.path.exists(ref):
+        import pytest
+        pytest.skip("reference murmur_hash.cpp not built here")
+    lib = ctypes.CDLL(ref)
+    fn = getattr(lib, "ref_murmur_hash2", None)
+    if fn is None:
+        import pytest
+        pytest.skip("shim has no byte-string entry point")
+    fn.restype = ctypes.c_uint32
+    fn.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32]
+    for s in [b"", b"a", b"ab", b"abc", b"abcd", b"This", b"is a test", b"CCCCCCCCCCCCCCC", bytes(range(1, 200))]:
+        assert hy.capi.lib.hy_murmur2_bytes(s, len(s), 17) == fn(s, len(s), 17), s
