@@ -49,6 +49,9 @@ def parse():
                    help="join: the headline TableScan+JoinHash (BASELINE.json metric); q1: BASELINE config 4, "
                         "TPC-H 1 TableScan -> Projection -> Aggregate (8 aggregates) on one GPU; q3: BASELINE config 5 at N=1, "
                         "TPC-H 3 Scan -> Join -> Join -> Projection -> Aggregate (bench_tpch.py)")
+    p.add_argument("--q1-unfused", action="store_true",
+                   help="q1: TableScan to PosLists, then the Aggregate over them (default: the scan fused into the "
+                        "aggregate, hy_agg_input.filter)")
     p.add_argument("--q1-materialize", action="store_true",
                    help="q1: materialise the two arithmetic expressions with hy_projection before the aggregate "
                         "(the reference's plan shape) instead of evaluating them inside it (A/B)")

@@ -673,7 +673,39 @@ def main_q1(args):
     cc_dtype = np.dtype(capi.ColumnChunk)
     state = {}
 
+    # fused plan (default): the TableScan's predicate evaluated inside the aggregate over the data chunks
+    fused_scan = not (args.q1_unfused or args.q1_materialize)
+    if fused_scan:
+        data_cols = (capi.AggColumn * 8)()
+        for j, (vt, chs, dom) in ref_cols.items():
+            data_cols[j].value_type, data_cols[j].pos_group, data_cols[j].chunks = vt, -1, chs
+            data_cols[j].n_chunks, data_cols[j].domain = n_chunks, dom
+        for j, prog in ((4, agg_programs[0]), (5, agg_programs[1])):
+            data_cols[j].value_type, data_cols[j].pos_group, data_cols[j].n_chunks = F32, -1, 0
+            data_cols[j].program, data_cols[j].n_nodes = prog, len(prog)
+        all_sizes = (ctypes.c_uint32 * n_chunks)(*ship.sizes)
+        fin = capi.AggInput(n_chunks, all_sizes, None, 0, data_cols, 8)
+        fin.filter, fin.filter_value_type, fin.filter_constant = scan, I32, None
+
+    def step_fused():
+        if "ws" not in state:
+            b = ctypes.c_size_t(0)
+            capi.check(L.hy_aggregate_workspace_size(ctypes.byref(fin), ctypes.byref(params), ctypes.byref(b)), "ws")
+            state["ws"] = torch.empty(b.value, dtype=torch.uint8, device=dev)
+            lay = capi.AggLayout()
+            capi.check(L.hy_aggregate_layout(ctypes.byref(fin), ctypes.byref(params), ctypes.byref(lay)), "layout")
+            state["layout"] = lay
+            state["out"] = torch.empty(64 * lay.words, dtype=torch.int64, device=dev)
+        ng = ctypes.c_uint64(0)
+        capi.check(L.hy_aggregate(ctypes.byref(fin), ctypes.byref(params), state["out"].data_ptr(), 64,
+                                  ctypes.byref(ng), state["ws"].data_ptr(), state["ws"].numel(), stream),
+                   "hy_aggregate (fused scan)")
+        return ng
+
     def step():
+        if fused_scan:
+            ng = step_fused()
+            return merge_or_local(ng, None)
         capi.check(L.hy_table_scan_row_ids(scan, n_chunks, I32, None, ids, rows_t.data_ptr(), counts_t.data_ptr(),
                                            scan_ws.data_ptr(), scan_ws.numel(), stream), "scan")
         cnt = counts_t.cpu().numpy()
@@ -721,9 +753,14 @@ def main_q1(args):
         capi.check(L.hy_aggregate(ctypes.byref(ain), ctypes.byref(params), state["out"].data_ptr(), 64,
                                   ctypes.byref(ng), state["ws"].data_ptr(), state["ws"].numel(), stream),
                    "hy_aggregate")
+        return merge_or_local(ng, int(sizes_np.sum()))
+
+    def merge_or_local(ng, n_match):
+        """This rank's groups (one GPU), or the all-gathered and merged groups of every rank. n_match None: the
+        fused scan's matches, counted from the records' rows words after the timed steps."""
         if world == 1:
             state["records"] = None
-            return int(sizes_np.sum()), ng.value
+            return n_match, ng.value
         # all-gather of the ranks' partial records (64 x words each, groups count in front) and the exact merge
         words = state["layout"].words
         buf = torch.empty(1 + 64 * words, dtype=torch.int64, device=dev)
@@ -743,7 +780,7 @@ def main_q1(args):
                                         merged.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), 64,
                                         ctypes.byref(n_out)), "hy_aggregate_merge")
         state["records"] = merged[:n_out.value]
-        return int(sizes_np.sum()), n_out.value
+        return n_match, n_out.value
 
     print("q1: columns encoded, running", file=sys.stderr, flush=True)
     for _ in range(args.warmup):
@@ -767,9 +804,10 @@ def main_q1(args):
         t = torch.tensor([elapsed], dtype=torch.float64, device=xdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        m = torch.tensor([n_match], dtype=torch.int64, device=xdev)
-        dist.all_reduce(m, op=dist.ReduceOp.SUM)
-        n_match = int(m.item())
+        if n_match is not None:  # (fused scan: counted from the merged records below)
+            m = torch.tensor([n_match], dtype=torch.int64, device=xdev)
+            dist.all_reduce(m, op=dist.ReduceOp.SUM)
+            n_match = int(m.item())
 
     # ---- check ----
     lay = state["layout"]
@@ -777,6 +815,8 @@ def main_q1(args):
         rec = state["records"]
     else:
         rec = state["out"].view(-1, lay.words)[:n_groups].cpu().numpy().view(np.uint64)
+    if fused_scan:  # the scan's matches = the groups' rows (every matching row is in exactly one group)
+        n_match = int(sum(int(r[5]) for r in rec))
 
     def fsum(r, a):
         w = lay.agg_word[a]
@@ -814,8 +854,12 @@ def main_q1(args):
     # aggregate (with its projection) per match: RowID 8 B + returnflag, linestatus, quantity, discount, tax vids 1 B
     # each + price 4 B = 17 B. Per kernel: the bytes that kernel must move on the path taken.
     e2e_parts = {"scan": n * 2 + n_match * 8, "aggregate": n_match * 17}
+    if fused_scan:  # no PosList in the fused plan: predicate 2 B/row + the 9 B of columns per matching row
+        e2e_parts = {"scan": n * 2, "aggregate": n_match * 9}
     alg = {"scan_dict": n * 2 + n_match * 8, "projection": n_match * (17 + 18), "agg_dense_span": n_match * 24,
            "agg_dense_fused": n_match * 17}
+    if fused_scan:
+        alg["agg_dense_lanes"] = n * 2 + n_match * 9
     e2e = sum(e2e_parts.values())
     for k, v in kernels.items():
         v["ms_per_launch"] = v["ms_total"] / max(v["launches"], 1)
@@ -841,6 +885,9 @@ def main_q1(args):
         "config": {"workload": "TPC-H 1 (tpch_queries.cpp:36-44) without ORDER BY: scan l_shipdate <= 1998-09-02, "
                                "8 aggregates GROUP BY l_returnflag, l_linestatus", "sf": args.sf, "lineitem_rows": n,
                    "chunk_size": chunk, "scan_matches": n_match, "groups": n_groups,
+                   "path": "TableScan fused into the aggregate (hy_agg_input.filter)" if fused_scan else
+                   ("hy_table_scan_row_ids -> hy_projection x2 -> hy_aggregate" if args.q1_materialize else
+                    "hy_table_scan_row_ids -> hy_aggregate with expression columns"),
                    "parallelism": "single GPU" if world == 1 else
                    f"chunk-sharded x{world}: per-rank scan + aggregate, all-gather of partial records, exact merge "
                    f"(hy_aggregate_merge)"},

@@ -83,7 +83,9 @@ class AggColumn(ctypes.Structure):
 class AggInput(ctypes.Structure):
     _fields_ = [("n_chunks", ctypes.c_uint32), ("chunk_sizes", ctypes.POINTER(ctypes.c_uint32)),
                 ("pos_lists", ctypes.POINTER(ctypes.c_void_p)), ("n_pos_groups", ctypes.c_uint32),
-                ("columns", ctypes.POINTER(AggColumn)), ("n_columns", ctypes.c_uint32)]
+                ("columns", ctypes.POINTER(AggColumn)), ("n_columns", ctypes.c_uint32),
+                ("filter", ctypes.POINTER(ScanChunk)), ("filter_value_type", ctypes.c_int32),
+                ("filter_constant", ctypes.c_void_p)]
 
 
 class AggDef(ctypes.Structure):

@@ -576,6 +576,7 @@ struct AggWs {
   hyk::LnTerm* lane_terms;       // agg_dense_lanes: its chains
   uint32_t* deferred;            // agg_dense_lanes: steps left to agg_dense_fused
   hyk::LaneTables* lane_tables;
+  hy_scan_chunk* filter;         // fused TableScan predicate chunks
   void* mat_values[hyk::AGG_MAX_COLUMNS];    // materialised expression columns
   uint8_t* mat_nulls[hyk::AGG_MAX_COLUMNS];
   uint32_t* state;
@@ -597,6 +598,7 @@ void carve(Carver& cv, const hy_agg_input* in, const AggPlan& plan, AggWs* w) {
   w->fused_nodes = cv.take<hyk::FqOp>(std::max<size_t>(1, plan.fused_nodes.size()));
   w->lane_terms = cv.take<hyk::LnTerm>(std::max<size_t>(1, plan.lane_terms.size()));
   w->lane_tables = cv.take<hyk::LaneTables>(1);
+  w->filter = cv.take<hy_scan_chunk>(in->filter ? std::max<uint32_t>(1, in->n_chunks) : 1);
   w->deferred = cv.take<uint32_t>(plan.lanes ? std::max<uint64_t>(1, plan.n_tiles * hyk::FQ_STEPS_PER_TILE) : 1);
   for (uint32_t e = 0; e < plan.expr_cols.size(); ++e) {
     const uint32_t j = plan.expr_cols[e];
@@ -618,6 +620,27 @@ void carve(Carver& cv, const hy_agg_input* in, const AggPlan& plan, AggWs* w) {
   }
 }
 
+// The fused TableScan of hy_agg_input.filter: data input on the dense expression path (agg_dense_lanes /
+// agg_dense_fused apply it); predicate chunks as hy_table_scan validates them.
+hy_status check_filter(const hy_agg_input* in, const AggPlan& plan) {
+  if (!in->filter) return HY_OK;
+  if (in->n_pos_groups != 0 || !plan.fused || !plan.dense_groups)
+    return fail(HY_ERR_UNSUPPORTED, "a fused scan needs a data input on the dense aggregate path");
+  for (uint32_t c = 0; c < in->n_chunks; ++c) {
+    const hy_scan_chunk& f = in->filter[c];
+    if (f.column.size != in->chunk_sizes[c]) return fail(HY_ERR_INVALID_ARGUMENT, "filter chunk size != input chunk");
+    if (f.op == HY_OP_NONE || f.column.size == 0) continue;
+    if (!f.column.data) return fail(HY_ERR_INVALID_ARGUMENT, "filter chunk without data");
+    if (f.column.kind == HY_COL_DICT) {
+      if (f.column.vid_width != 1 && f.column.vid_width != 2 && f.column.vid_width != 4)
+        return fail(HY_ERR_INVALID_ARGUMENT, "filter vid width");
+    } else if (!in->filter_constant || (in->filter_value_type < HY_TYPE_INT32 || in->filter_value_type > HY_TYPE_DOUBLE)) {
+      return fail(HY_ERR_INVALID_ARGUMENT, "filter constant / value type");
+    }
+  }
+  return HY_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -634,7 +657,9 @@ hy_status hy_aggregate_layout(const hy_agg_input* input, const hy_agg_params* pa
 hy_status hy_aggregate_workspace_size(const hy_agg_input* input, const hy_agg_params* params, size_t* bytes) {
   if (!bytes) return fail(HY_ERR_INVALID_ARGUMENT, "null bytes");
   AggPlan plan;
-  const hy_status st = make_plan(input, params, &plan);
+  hy_status st = make_plan(input, params, &plan);
+  if (st != HY_OK) return st;
+  st = check_filter(input, plan);
   if (st != HY_OK) return st;
   Carver cv{nullptr, 0};
   AggWs w;
@@ -649,6 +674,8 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
   if (!n_groups) return fail(HY_ERR_INVALID_ARGUMENT, "null n_groups");
   AggPlan plan;
   hy_status st = make_plan(input, params, &plan);
+  if (st != HY_OK) return st;
+  st = check_filter(input, plan);
   if (st != HY_OK) return st;
   hipStream_t s = S(stream);
   Carver cv{static_cast<char*>(workspace), workspace_bytes};
@@ -695,6 +722,16 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
   }
   d.word_op = w.word_op;
   d.error = w.misc;
+  if (input->filter && input->n_chunks) {
+    HY_HIP(hipMemcpyAsync(w.filter, input->filter, sizeof(hy_scan_chunk) * input->n_chunks, hipMemcpyHostToDevice, s));
+    d.filter = w.filter;
+    d.filter_type = input->filter_value_type;
+    d.filter_cbits = 0;
+    if (input->filter_constant) {
+      const bool wide = input->filter_value_type == HY_TYPE_INT64 || input->filter_value_type == HY_TYPE_DOUBLE;
+      std::memcpy(&d.filter_cbits, input->filter_constant, wide ? 8 : 4);
+    }
+  }
   auto* n_out = reinterpret_cast<unsigned long long*>(w.misc + 2);
   auto* out = reinterpret_cast<unsigned long long*>(out_records);
   // expression columns outside the fused kernel: materialised (projection kernel over the same input), then read as

@@ -92,7 +92,71 @@ struct AggDesc {
   uint32_t words;                    // words per group record
   const int32_t* word_op;            // device: WOP_* per record word
   uint32_t* error;                   // bit 0: table full / livelock guard, bit 1: dense code out of range
+  // fused TableScan (hy_agg_input.filter, data input only): a row takes part only if the predicate column's chunk c
+  // (filter[c]: op + search_vid of the host's dictionary rewrite, or a value compare with filter_cbits) matches
+  const hy_scan_chunk* filter;
+  uint64_t filter_cbits;
+  int32_t filter_type;
 };
+
+// Match mask of the FQ-style rows base + k * WAVE + lane (k < R) of input chunk c under the fused scan predicate
+// (reference SingleColumnTableScanImpl, single_column_table_scan_impl.cpp:38-205); rows past the chunk are 0.
+template <int R>
+__device__ __forceinline__ uint32_t agg_filter_mask(const AggDesc& d, uint32_t c, uint32_t base) {
+  const hy_scan_chunk f = d.filter[c];
+  const uint32_t n = f.column.size;
+  if (f.op == HY_OP_NONE || n == 0) return 0u;
+  const uint32_t lane = __lane_id();
+  uint32_t m = 0;
+  if (f.column.kind == HY_COL_DICT) {
+    const uint32_t w = static_cast<uint32_t>(f.column.vid_width);
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const uint32_t i = min(base + k * WAVE + lane, n - 1);
+      const uint32_t vid = w == 1 ? static_cast<const uint8_t*>(f.column.data)[i]
+                           : w == 2 ? static_cast<const uint16_t*>(f.column.data)[i]
+                                    : static_cast<const uint32_t*>(f.column.data)[i];
+      m |= static_cast<uint32_t>(vid != f.column.dictionary_size && cmp_op<uint32_t>(f.op, vid, f.search_vid)) << k;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const uint32_t i = min(base + k * WAVE + lane, n - 1);
+      const bool nul = f.column.nulls != nullptr && f.column.nulls[i];
+      bool hit = false;
+      switch (d.filter_type) {
+        case HY_TYPE_INT32: {
+          int32_t c0;
+          __builtin_memcpy(&c0, &d.filter_cbits, 4);
+          hit = cmp_op<int32_t>(f.op, static_cast<const int32_t*>(f.column.data)[i], c0);
+          break;
+        }
+        case HY_TYPE_INT64: {
+          int64_t c0;
+          __builtin_memcpy(&c0, &d.filter_cbits, 8);
+          hit = cmp_op<int64_t>(f.op, static_cast<const int64_t*>(f.column.data)[i], c0);
+          break;
+        }
+        case HY_TYPE_FLOAT: {
+          float c0;
+          __builtin_memcpy(&c0, &d.filter_cbits, 4);
+          hit = cmp_op<float>(f.op, static_cast<const float*>(f.column.data)[i], c0);
+          break;
+        }
+        default: {
+          double c0;
+          __builtin_memcpy(&c0, &d.filter_cbits, 8);
+          hit = cmp_op<double>(f.op, static_cast<const double*>(f.column.data)[i], c0);
+        }
+      }
+      m |= static_cast<uint32_t>(hit && !nul) << k;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < R; ++k)
+    if (base + k * WAVE + lane >= n) m &= ~(1u << k);
+  return m;
+}
 
 __host__ __device__ inline uint64_t word_init(int32_t op) { return op == WOP_MIN ? ~0ull : 0ull; }
 

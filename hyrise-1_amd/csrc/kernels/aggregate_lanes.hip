@@ -323,6 +323,7 @@ __global__ __launch_bounds__(AGG_THREADS) __attribute__((amdgpu_waves_per_eu(3))
           continue;
         }
       } else {
+        if (d.filter != nullptr) act &= agg_filter_mask<FQ_R>(d, c, base);  // fused TableScan
 #pragma unroll
         for (int k = 0; k < FQ_R; ++k) off[k] = ((act >> k) & 1u) ? base + k * WAVE + lane : 0u;
       }

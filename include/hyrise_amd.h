@@ -507,6 +507,15 @@ typedef struct hy_agg_input {
   uint32_t n_pos_groups;
   const hy_agg_column* columns;      /* HOST */
   uint32_t n_columns;
+  /* Fused TableScan (the plan TableScan -> [Projection ->] Aggregate as one pass, reference table_scan.cpp:78-164
+   * feeding aggregate.cpp:291-498): NULL, or - for a data input (n_pos_groups == 0) on the dense expression path -
+   * one predicate chunk per input chunk (hy_scan_chunk as for hy_table_scan: op + search_vid of the host's dictionary
+   * rewrite, or a value compare with *filter_constant of filter_value_type). Rows that do not match take no part,
+   * exactly as if the Aggregate read the scan's output; the first / last row words number the input's rows (an
+   * order-preserving renumbering of the scan output's). Other paths return HY_ERR_UNSUPPORTED. */
+  const hy_scan_chunk* filter;       /* HOST, n_chunks entries */
+  int32_t filter_value_type;
+  const void* filter_constant;       /* HOST */
 } hy_agg_input;
 
 typedef struct hy_agg_def {

@@ -90,7 +90,7 @@ def fsum_inf(vals):
     return math.fsum(vals)
 
 
-def run(hy, dcols, pos_lists, sizes, doms, part=None, raw=False):
+def run(hy, dcols, pos_lists, sizes, doms, part=None, raw=False, filt=None):
     """hy_aggregate over the input (or over input chunks [lo, hi) with part=(lo, hi)); raw: (records, layout,
     params) instead of the decoded results."""
     capi, L = hy.capi, hy.capi.lib
@@ -123,6 +123,8 @@ def run(hy, dcols, pos_lists, sizes, doms, part=None, raw=False):
                                                   else []))
     inp = capi.AggInput(n_chunks, csz, pls if pos_lists is not None else None, 1 if pos_lists is not None else 0,
                         ac, 10)
+    if filt is not None:  # fused TableScan: (ScanChunk array, value type, constant array)
+        inp.filter, inp.filter_value_type, inp.filter_constant = filt[0], filt[1], filt[2].ctypes.data
     gb = (ctypes.c_int32 * 2)(0, 1)
     defs = (capi.AggDef * len(AGGS))(*[capi.AggDef(getattr(capi, "HY_AGG_" + f), c) for f, c in AGGS])
     prm = capi.AggParams(gb, 2, defs, len(AGGS), 0)
@@ -301,3 +303,30 @@ def test_merge_of_partial_aggregates(hy, case, n_parts):
                 assert a[0] == v[0] and same_float(a[1], v[1]), (g, k, a, v)
             else:
                 assert a == v, (g, k, a, v)
+
+
+@pytest.mark.parametrize("pred_enc,cond,value", [("Dictionary", "LessThanEquals", 300), ("Unencoded", "LessThan", 250),
+                                                 ("Dictionary", "GreaterThan", 1000), ("Dictionary", "LessThan", 0)])
+@pytest.mark.parametrize("case", ["clean", "nulls", "odd_values"])
+def test_fused_scan_filter(hy, case, pred_enc, cond, value):
+    """hy_aggregate with a fused TableScan (hy_agg_input.filter) over a data input: every aggregate equals the
+    aggregate of exactly the matching rows (numpy over the predicate's rows) - TPC-H 1's Scan -> Aggregate in one
+    pass, the lanes path and the steps it defers to agg_dense_fused (NULLs, odd values) alike; predicates with all,
+    some and no matches, dictionary (u16 vids: value ids compared after the host's dictionary rewrite) and value."""
+    capi = hy.capi
+    rng = np.random.default_rng(zlib.crc32(f"filter/{case}/{pred_enc}/{cond}/{value}".encode()))
+    cols = columns(rng, case)
+    rf, ls, qty, price, disc, tax, iq, price_n, disc_n, doms = cols
+    ship = rng.integers(0, 1000, N).astype(np.int32)  # > 256 distinct values: 2-byte value ids
+    dcols = [dt.DeviceColumn(capi, rf, None, CHUNK, "Dictionary"), dt.DeviceColumn(capi, ls, None, CHUNK, "Dictionary"),
+             dt.DeviceColumn(capi, qty, None, CHUNK, "Dictionary"),
+             dt.DeviceColumn(capi, price, price_n, CHUNK, "Dictionary" if case == "nulls" else "Unencoded"),
+             dt.DeviceColumn(capi, disc, disc_n, CHUNK, "Dictionary"),
+             dt.DeviceColumn(capi, tax, None, CHUNK, "Dictionary"), dt.DeviceColumn(capi, iq, None, CHUNK, "Unencoded")]
+    pred = dt.DeviceColumn(capi, ship, None, CHUNK, pred_enc)
+    chunks = pred.scan_chunks(cond, value)
+    sizes = [d.size for d in dcols[0].descs]
+    res = run(hy, dcols, None, sizes, doms, filt=(chunks, capi.HY_TYPE_INT32, pred.constant(value)))
+    op = {"LessThanEquals": np.less_equal, "LessThan": np.less, "GreaterThan": np.greater}[cond]
+    rows = list(np.nonzero(op(ship, value))[0])
+    check(res, expected(cols, rows))
