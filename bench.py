@@ -32,7 +32,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--sf", type=float, default=100.0,
+    p.add_argument("--sf", type=float, default=None,
                    help="TPC-H scale factor of the database (strong scaling) or per GPU (--scaling weak)")
     p.add_argument("--scaling", choices=["strong", "weak"], default=None,
                    help="N>1: strong (default; the --sf database split over the ranks, BASELINE.json's metric) or "
@@ -45,13 +45,16 @@ def parse():
     p.add_argument("--transport", choices=["capi", "torch"], default="torch",
                    help="N>1 over RCCL: torch's all_to_all (default: torch bundles its own RCCL / HIP runtime) or the "
                         "library's own communicator (hy_join_exchange_counts/records, the C++ integration's path)")
-    p.add_argument("--workload", choices=["join", "q1", "q3"], default="join",
+    p.add_argument("--workload", choices=["join", "q1", "q3", "scan", "join-only"], default="join",
                    help="join: the headline TableScan+JoinHash (BASELINE.json metric); q1: BASELINE config 4, "
                         "TPC-H 1 TableScan -> Projection -> Aggregate (8 aggregates) on one GPU; q3: BASELINE config 5 at N=1, "
-                        "TPC-H 3 Scan -> Join -> Join -> Projection -> Aggregate (bench_tpch.py)")
-    p.add_argument("--q1-unfused", action="store_true",
-                   help="q1: TableScan to PosLists, then the Aggregate over them (default: the scan fused into the "
-                        "aggregate, hy_agg_input.filter)")
+                        "TPC-H 3 Scan -> Join -> Join -> Projection -> Aggregate (bench_tpch.py); scan: config 2, the "
+                        "TableScan l_quantity<24 alone (SF10 default); join-only: config 3, JoinHash lineitem x orders "
+                        "over all lineitem rows (SF10 default)")
+    p.add_argument("--q1-fused", action="store_true",
+                   help="q1: the TableScan fused into the aggregate (hy_agg_input.filter) instead of the reference plan "
+                        "(scan to PosLists, aggregate over them); measured no faster at SF100 (11.2 vs 11.0 ms): the "
+                        "aggregation kernel is latency-bound, not bound by the RowID bytes the fusion saves")
     p.add_argument("--q1-materialize", action="store_true",
                    help="q1: materialise the two arithmetic expressions with hy_projection before the aggregate "
                         "(the reference's plan shape) instead of evaluating them inside it (A/B)")
@@ -65,7 +68,10 @@ def parse():
     p.add_argument("--join-trace", default=None,
                    help="debug: after the timed region run one traced step and write per-partition join phase "
                         "durations (us) to this .npz (hy_debug_set_join_trace)")
-    return p.parse_args()
+    args = p.parse_args()
+    if args.sf is None:  # BASELINE.json: configs 2 and 3 are quoted at SF10, the others at SF100
+        args.sf = 10.0 if args.workload in ("scan", "join-only") else 100.0
+    return args
 
 
 def main():
@@ -247,9 +253,32 @@ def main():
         capi.check(st, "hy_scan_join_hash")
         return res.total_pairs
 
-    fused = not args.unfused
+    fused = not args.unfused and args.workload == "join"
+    mode = args.workload  # "join" (headline), "scan" (config 2) or "join-only" (config 3)
+
+    def run_join_only():
+        # JoinHash lineitem ⋈ orders over every lineitem row (BASELINE.json configs[2]): data tables on both sides
+        if "jws" not in state:
+            wsb = ctypes.c_size_t(0)
+            capi.check(L.hy_join_hash_workspace_size(ctypes.byref(build_side), ctypes.byref(probe_data_side),
+                                                     ctypes.byref(params), ctypes.byref(wsb)), "join ws")
+            state["jws"] = torch.empty(wsb.value, dtype=torch.uint8, device=dev)
+            state["jcap"] = n_li + 64
+            state["jout_b"] = torch.empty(2 * state["jcap"], dtype=torch.int32, device=dev)
+            state["jout_p"] = torch.empty(2 * state["jcap"], dtype=torch.int32, device=dev)
+        res = capi.JoinResult()
+        capi.check(L.hy_join_hash(ctypes.byref(build_side), ctypes.byref(probe_data_side), ctypes.byref(params),
+                                  state["jout_b"].data_ptr(), state["jout_p"].data_ptr(), state["jcap"],
+                                  part_begin.data_ptr(), part_count.data_ptr(), ctypes.byref(res),
+                                  state["jws"].data_ptr(), state["jws"].numel(), stream), "hy_join_hash")
+        return n_li, res.total_pairs
 
     def step():
+        if mode == "scan":  # the TableScan operator's step: RowIDs + per-chunk match counts to the host
+            run_scan()
+            return int(scan_counts.cpu().numpy().astype(np.int64).sum()), 0
+        if mode == "join-only":
+            return run_join_only()
         if fused:
             pairs = run_fused()
             return None, pairs  # scan matches are read once after the timed region (scan_begin[-1])
@@ -303,6 +332,10 @@ def main():
     recv_build, recv_probe = n_ord, n_probe
     scan_out_b = 4 if fused else 8
     e2e_bytes = n_li * 1 + n_probe * scan_out_b + n_ord * 4 + n_probe * 4 + int(pairs) * 16
+    if mode == "scan":
+        e2e_bytes = n_li * 1 + n_probe * 8  # u8 value ids read, 8-byte RowIDs written
+    elif mode == "join-only":
+        e2e_bytes = n_ord * 4 + n_li * 4 + int(pairs) * 16
     if fused:
         moved = {
             "part1_hist.probe": n_li * 5,
@@ -318,6 +351,11 @@ def main():
             "part2_hist.probe": n_probe * 8,
             "part2_scatter.probe": n_probe * 16,
         }
+    if mode == "scan":
+        moved = {"scan_dict": n_li * 1 + n_probe * 8}
+    elif mode == "join-only":
+        moved = {"part1_hist.probe": n_li * 4, "part1_scatter.probe": n_li * (4 + 8 + 1),
+                 "part2_hist.probe": n_li * 1, "part2_scatter.probe": n_li * 16}
     moved.update({
         "part1_hist.build": n_ord * 4,
         "part1_scatter.build": n_ord * (4 + 8 + 1),
@@ -334,7 +372,7 @@ def main():
             v["bytes_per_launch"] = moved[k] / launches_per_step
             v["achieved_GBps"] = v["bytes_per_launch"] / (per_launch_ms * 1e-3) / 1e9
     step_s = elapsed / K
-    value = (g_li + g_ord) / step_s
+    value = (g_li + (0 if mode == "scan" else g_ord)) / step_s
     peak, probe = measured_roofline(L, capi, torch, dev, stream, args.probe_gb)
     dom = max((k for k in kernels if k in moved), key=lambda k: kernels[k]["ms_total"])
     dk = kernels[dom]
@@ -346,7 +384,7 @@ def main():
                 "frac": round(e2e_gbps / peak, 4), "alg_bytes_per_step": e2e_bytes, "traffic": None,
                 "peak_source": "measured in this run (hy_stream_bandwidth_probe, best of read / copy)",
                 "frac_of_spec_8000": round(e2e_gbps / HBM_PEAK_GBPS, 4)}
-    traffic, traffic_src = committed_traffic_step(args.sf, chunk, world, fused)
+    traffic, traffic_src = committed_traffic_step(args.sf, chunk, world, fused) if mode == "join" else (None, None)
     if traffic is not None:
         roofline["traffic"] = round(traffic)
         roofline["traffic_source"] = traffic_src
@@ -355,7 +393,7 @@ def main():
                        "ms_per_launch": round(dk["ms_per_launch"], 4), "bytes_per_launch": dk["bytes_per_launch"]}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and mode == "join":
         cpu = cpu_baseline(hy, synth, args.cpu_sf, chunk)
 
     if rank == 0:
@@ -385,6 +423,21 @@ def main():
                         for k, v in kernels.items()},
             "cpu_baseline": cpu,
         }
+        if mode == "scan":  # BASELINE.json configs[1]
+            line["metric"] = "rows/sec TableScan lineitem.l_quantity<24, dictionary-encoded, one MI355X"
+            line["config"] = {"workload": "TableScan(l_quantity<24, dictionary u8) alone (BASELINE.json configs[1])",
+                              "path": "hy_table_scan_row_ids + per-chunk counts to the host", "sf": args.sf,
+                              "lineitem_rows": g_li, "chunk_size": chunk, "scan_matches": g_probe,
+                              "parallelism": "single GPU"}
+            line["roofline"]["scope"] = "TableScan step (1 B/row value ids read + 8 B/match RowIDs written)"
+        elif mode == "join-only":  # BASELINE.json configs[2]
+            line["metric"] = "rows/sec JoinHash lineitem⋈orders on l_orderkey, one MI355X"
+            line["config"] = {"workload": f"JoinHash(orders ⋈ lineitem, o_orderkey=l_orderkey, radix_bits={radix_bits}) "
+                                          f"over every lineitem row (BASELINE.json configs[2])",
+                              "path": "hy_join_hash (data tables on both sides)", "sf": args.sf,
+                              "lineitem_rows": g_li, "orders_rows": g_ord, "chunk_size": chunk, "join_pairs": g_pairs,
+                              "parallelism": "single GPU"}
+            line["roofline"]["scope"] = "JoinHash step (SURVEY 8(d): 4 B/build row + 4 B/probe row + 16 B/pair)"
         print(json.dumps(line))
 
 

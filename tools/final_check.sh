@@ -1,0 +1,10 @@
+set -e
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/fin_pytest.txt 2>&1
+timeout -k 10 200 python bench.py > $O/fin_bench.json 2> $O/fin_bench.err
+timeout -k 10 200 python bench.py --workload scan --no-cpu-baseline > $O/fin_scan.json 2>> $O/fin_bench.err
+timeout -k 10 200 python bench.py --workload join-only --no-cpu-baseline > $O/fin_joinonly.json 2>> $O/fin_bench.err
+timeout -k 10 300 python bench.py --workload q1 > $O/fin_q1.json 2>> $O/fin_bench.err
+timeout -k 10 300 python bench.py --workload q3 > $O/fin_q3.json 2>> $O/fin_bench.err
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/fin_smoke.txt 2>&1
