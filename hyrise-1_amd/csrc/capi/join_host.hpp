@@ -50,6 +50,20 @@ inline bool digit_bytes_enabled() {
   }();
   return v;
 }
+// Probe-side Bloom prefilter (hyk::bloom_filter_act) of INNER / SEMI joins whose build side is much smaller than the
+// probe side (probe rows >= 16x build rows: most probe rows are expected to find no partner, as in TPC-H 3's joins;
+// a foreign-key join like the headline's, probe / build ~ 4, keeps the plain path). 16 bits per build key.
+// HY_JOIN_BLOOM=0 / 1 turns it off / on regardless of the ratio. Returns the filter's words (0: none).
+inline uint64_t bloom_words(uint64_t build_rows, uint64_t probe_rows) {
+  const char* e = std::getenv("HY_JOIN_BLOOM");
+  const bool force = e && std::strtol(e, nullptr, 10) == 1;
+  if ((e && std::strtol(e, nullptr, 10) == 0) || build_rows == 0) return 0;
+  if (!force && probe_rows < 16 * build_rows) return 0;
+  uint64_t w = 1024;
+  while (w < build_rows / 2 && w < (uint64_t(1) << 31)) w <<= 1;
+  return w;
+}
+
 inline uint32_t sub2() {
   static const uint32_t v = sub_from_env("HY_PART_SUB2", 1);
   return v;
@@ -446,7 +460,7 @@ hy_status launch_pass0(const char* side_tag, const SidePlan& p, const hyk::Side&
 template <typename T, typename H, typename P>
 hy_status pass0_side(const char* side_tag, const SidePlan& p, SideBufs<H, P>& b, uint32_t bits, uint32_t w0,
                      uint32_t seed, bool keep_nulls, uint32_t ref_base, const hyk::NextDigit& nd, const Common& c,
-                     hipStream_t s, hyk::Rec<H, P>* out) {
+                     hipStream_t s, hyk::Rec<H, P>* out, const uint32_t* bloom = nullptr, uint64_t bloom_n = 0) {
   hyk::Side sd{};
   sd.chunks = b.chunks;
   sd.n_chunks = static_cast<uint32_t>(p.chunks.size());
@@ -464,6 +478,8 @@ hy_status pass0_side(const char* side_tag, const SidePlan& p, SideBufs<H, P>& b,
   sd.filter_const = p.filter_const;
   sd.filter_type = p.filter_type;
   sd.scan_out = p.scan_out;
+  sd.bloom = bloom;
+  sd.bloom_mask = bloom ? static_cast<uint32_t>(bloom_n - 1) : 0u;
   const uint32_t n_digits = 1u << w0;
   hyk::Digit d0{full_mask(bits), bits - w0, n_digits - 1u, seed, g_key_hash};
   HY_HIP(hipMemsetAsync(b.total, 0, 8, s));
@@ -684,6 +700,7 @@ size_t classic_join_bytes(const SidePlan& bp, const SidePlan& pp, uint32_t bits)
   pass_sizes(sizes_of(pp, db), w, 1, &hb, &t);
   Common c;
   carve_common(cv, std::max({ha, hb, (uint64_t(1) << bits) + 1}), bits, &c);
+  cv.take<uint32_t>(std::max<uint64_t>(1, bloom_words(bp.n_rows, pp.n_rows)));
   return cv.used + 256;
 }
 
@@ -1033,9 +1050,12 @@ hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join
   pass_sizes(sizes_of(pp, db), w, 1, &hb2, &t);
   Common c{};
   carve_common(cv, std::max({ha, hb2, (uint64_t(1) << bits) + 1}), bits, &c);
+  const uint64_t bloom_n = bloom_words(bp.n_rows, pp.n_rows);
+  uint32_t* bloom = cv.take<uint32_t>(std::max<uint64_t>(1, bloom_n));
   if (!cv.ok) return fail(HY_ERR_WORKSPACE, "join workspace too small");
   if (upload_side(bp, bb, s) || upload_side(pp, pb, s)) return HY_ERR_DEVICE;
   const bool keep_nulls = prm->mode == HY_JOIN_LEFT || prm->mode == HY_JOIN_RIGHT;
+  const bool use_bloom = bloom_n && (prm->mode == HY_JOIN_INNER || prm->mode == HY_JOIN_SEMI);
 
   hyk::Rec<H>* recs[2] = {nullptr, nullptr};
   uint32_t* bounds[2] = {nullptr, nullptr};
@@ -1048,11 +1068,20 @@ hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join
                        ? pass0_side<TB, H, uint32_t>(tag, p, b, bits, w.empty() ? 0 : w[0], prm->seed, false,
                                                      p.ref_base, nd, c, s, b.recA)
                        : pass0_side<TP, H, uint32_t>(tag, p, b, bits, w.empty() ? 0 : w[0], prm->seed, keep_nulls,
-                                                     p.ref_base, nd, c, s, b.recA);
+                                                     p.ref_base, nd, c, s, b.recA, use_bloom ? bloom : nullptr,
+                                                     bloom_n);
     if (st != HY_OK) return st;
     st = local_passes<H, uint32_t>(tag, b, w, 1, bits, prm->seed, b.recA, b.recB, nd.bytes, b.digB, b.segA, b.segB,
                                    w.empty() ? 1 : (1ull << w[0]), b.total, p.n_rows, c, s, &recs[side], &bounds[side]);
     if (st != HY_OK) return st;
+    if (side == 0 && use_bloom) {  // the probe side's prefilter over the build side's keys (its records)
+      HY_HIP(hipMemsetAsync(bloom, 0, 4 * bloom_n, s));
+      KTimer kt_("bloom_build", s, p.n_rows);
+      hipLaunchKernelGGL(hyk::bloom_build<H>, dim3(static_cast<uint32_t>(std::min<uint64_t>(grid_for(p.n_rows, 256), 4096))),
+                         dim3(256), 0, s, recs[0], b.total, bloom, static_cast<uint32_t>(bloom_n - 1));
+      kt_.done();
+      HY_HIP(hipGetLastError());
+    }
   }
   // filtered sides emit RowIDs of their data table (the scan's PosLists dereferenced, write_output_columns)
   const hyk::RowMap bmap = bp.fuse ? make_map(bb.ref_row_begin, bp.ref_row_begin) : make_map(bb.row_begin, bp.row_begin);

@@ -126,7 +126,55 @@ struct Side {
   uint64_t filter_const;             // type_cast<T>(constant) bits for VALUE predicate chunks
   int32_t filter_type;               // HY_TYPE_* of VALUE predicate chunks
   uint32_t* scan_out;
+  // Probe-side prefilter of a selective INNER / SEMI join (null: none): a blocked Bloom filter over the build keys;
+  // a probe row whose key is certainly absent takes no part - it could produce no output, and dropping it keeps the
+  // stable order of the others (the reference's output is unchanged). The fused scan's output still lists it.
+  const uint32_t* bloom;
+  uint32_t bloom_mask;  // words - 1 (power of two)
 };
+
+// Bloom filter words: one 32-bit word per key selected by a hash independent of the partition and bucket hashes,
+// two bits set in it.
+template <typename H>
+__device__ __forceinline__ uint2 bloom_slot(H key, uint32_t mask) {
+  uint64_t b = 0;
+  H k = key;
+  if constexpr (std::is_floating_point_v<H>) {
+    if (k == H(0)) k = H(0);  // -0.0 and 0.0 are equal keys
+  }
+  __builtin_memcpy(&b, &k, sizeof(H));
+  const uint64_t h = (b ^ 0x9E3779B97F4A7C15ull) * 0xD6E8FEB86659FD93ull;
+  const uint32_t hi = static_cast<uint32_t>(h >> 32);
+  return make_uint2(static_cast<uint32_t>(h) & mask, (1u << (hi & 31u)) | (1u << ((hi >> 5) & 31u)));
+}
+
+template <typename H>
+__device__ __forceinline__ uint32_t bloom_filter_act(const Side& s, const H (&keys)[PART_ITEMS], uint32_t act) {
+  if (s.bloom == nullptr) return act;
+  uint32_t words[PART_ITEMS];
+  uint32_t bits[PART_ITEMS];
+#pragma unroll
+  for (int k = 0; k < PART_ITEMS; ++k) {  // all loads in flight before any test
+    const uint2 sl = bloom_slot<H>(keys[k], s.bloom_mask);
+    bits[k] = sl.y;
+    words[k] = ((act >> k) & 1u) ? s.bloom[sl.x] : sl.y;
+  }
+#pragma unroll
+  for (int k = 0; k < PART_ITEMS; ++k)
+    if ((words[k] & bits[k]) != bits[k]) act &= ~(1u << k);
+  return act;
+}
+
+template <typename H>
+static __global__ void bloom_build(const Rec<H, uint32_t>* __restrict__ recs, const uint64_t* __restrict__ n,
+                                   uint32_t* __restrict__ bloom, uint32_t mask) {
+  const uint64_t total = *n;
+  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const uint2 sl = bloom_slot<H>(recs[i].key, mask);
+    atomicOr(bloom + sl.x, sl.y);
+  }
+}
 
 // NULL rows: a ValueColumn read directly yields its stored value (value_column_iterable), a dictionary column and
 // any row reached through a ReferenceColumn yield T{} (dictionary_column_iterable.hpp:80,
@@ -513,7 +561,8 @@ __global__ __launch_bounds__(PART_THREADS) void part1_hist(Side s, Digit dg, uin
   for (uint32_t j = 0; j < n_sub; ++j) {
     H keys[PART_ITEMS];
     uint32_t pays[PART_ITEMS];
-    const uint32_t act = load_items<T, H, uint32_t, LP>(s, ch, base + j * PART_TILE + w * WAVE_SPAN, keys, pays);
+    const uint32_t act =
+        bloom_filter_act<H>(s, keys, load_items<T, H, uint32_t, LP>(s, ch, base + j * PART_TILE + w * WAVE_SPAN, keys, pays));
     uint32_t dig[PART_ITEMS];
 #pragma unroll
     for (int k = 0; k < PART_ITEMS; ++k) dig[k] = digit_of<H>(dg, keys[k]);
@@ -550,7 +599,8 @@ __global__ __launch_bounds__(PART_THREADS) __attribute__((amdgpu_waves_per_eu(4)
     H keys[PART_ITEMS];
     P pays[PART_ITEMS];
     uint32_t dr[PART_ITEMS];  // digit << 24 | rank within the wave (rank < WAVE_SPAN)
-    const uint32_t act = load_items<T, H, P, LP>(s, ch, base + j * PART_TILE + w * WAVE_SPAN, keys, pays);
+    const uint32_t act =
+        bloom_filter_act<H>(s, keys, load_items<T, H, P, LP>(s, ch, base + j * PART_TILE + w * WAVE_SPAN, keys, pays));
     Rec<H, P> recs[PART_ITEMS];
 #pragma unroll
     for (int k = 0; k < PART_ITEMS; ++k) {
@@ -600,7 +650,7 @@ __global__ __launch_bounds__(PART_THREADS) void part1_compact(Side s, Digit dg, 
     const uint32_t m = filter_items<FK>(s, c, rb);
     H keys[PART_ITEMS];
     uint32_t pays[PART_ITEMS];
-    const uint32_t act = load_items<T, H, uint32_t, LP>(s, ch, rb, keys, pays) & m;
+    const uint32_t act = bloom_filter_act<H>(s, keys, load_items<T, H, uint32_t, LP>(s, ch, rb, keys, pays) & m);
 #pragma unroll
     for (int k = 0; k < PART_ITEMS; ++k)
       if ((act >> k) & 1u) atomicAdd(&s_hist[digit_of<H>(dg, keys[k])], 1u);

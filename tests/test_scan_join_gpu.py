@@ -92,7 +92,9 @@ def check_join(expected, parts, build_cols, probe_first, semi_anti):
                                                        ("Unencoded", "Unencoded", True),
                                                        ("Dictionary", "Dictionary", True)])
 @pytest.mark.parametrize("build_filter", [False, True])
-def test_scan_join_matches_operators(hy, oracle, mode, qty_enc, key_enc, key_nulls, build_filter):
+@pytest.mark.parametrize("bloom", [False, True])
+def test_scan_join_matches_operators(hy, oracle, monkeypatch, mode, qty_enc, key_enc, key_nulls, build_filter, bloom):
+    monkeypatch.setenv("HY_JOIN_BLOOM", "1" if bloom else "0")  # probe-side Bloom prefilter (INNER / SEMI only)
     capi = hy.capi
     rng = np.random.default_rng(zlib.crc32(repr((mode, qty_enc, key_enc, key_nulls, build_filter)).encode()))
     okey, ostatus, lkey, lkey_nulls, qty, qty_nulls = orders_lineitem(rng, 40_000, key_nulls)
@@ -186,3 +188,36 @@ def test_multi_digit_plans(hy, oracle, monkeypatch, bits, mode, key_enc, filtere
     if lf is not None:
         check_scan(probe_t, lf)
     check_join(expected, parts, 2, swapped, mode == "Semi")
+
+
+
+@pytest.mark.parametrize("mode", ["Inner", "Semi", "Left", "Anti"])
+@pytest.mark.parametrize("bloom", ["0", "1", None])
+def test_selective_join_bloom_prefilter(hy, oracle, monkeypatch, mode, bloom):
+    """A small build side against a large probe side where ~90% of the probe keys have no partner (TPC-H 3's shape):
+    the default heuristic (probe >= 16x build) enables the probe-side Bloom prefilter for INNER / SEMI, which drops
+    probe rows before partitioning; the output PosLists equal the oracle's, with the prefilter forced on, off and by
+    the heuristic."""
+    if bloom is not None:
+        monkeypatch.setenv("HY_JOIN_BLOOM", bloom)
+    else:
+        monkeypatch.delenv("HY_JOIN_BLOOM", raising=False)
+    capi = hy.capi
+    rng = np.random.default_rng(zlib.crc32(f"bloom/{mode}/{bloom}".encode()))
+    okey = rng.choice(np.arange(1, 200_000, dtype=np.int32), 4_000, replace=False)
+    okey = np.concatenate([okey, okey[:300]])  # duplicate build keys
+    lkey = rng.integers(1, 40_000, 150_000).astype(np.int32)  # ~10% of them find a partner
+    lineitem = hy.Table.from_arrays([("l_orderkey", hy.DataType.Int, False)], [lkey], [], 20_000)
+    orders = hy.Table.from_arrays([("o_orderkey", hy.DataType.Int, False)], [okey], [], 3_000)
+    jm = getattr(hy.JoinMode, mode)
+    expected, bits = oracle.join_hash(orders, lineitem, jm, (0, 0))
+    lk = dt.DeviceColumn(capi, lkey, None, 20_000, "Unencoded")
+    ok = dt.DeviceColumn(capi, okey, None, 3_000, "Unencoded")
+    swapped = mode in ("Left", "Semi", "Anti")
+    params = capi.JoinParams({"Inner": 0, "Left": 1, "Semi": 5, "Anti": 6}[mode], capi.HY_TYPE_INT32, bits, 17)
+    cap = okey.size * 4 + lkey.size + 16
+    if swapped:
+        parts = run_fused(hy, dt.join_side(capi, lk), None, dt.join_side(capi, ok), None, params, cap)
+    else:
+        parts = run_fused(hy, dt.join_side(capi, ok), None, dt.join_side(capi, lk), None, params, cap)
+    check_join(expected, parts, 1, swapped, mode in ("Semi", "Anti"))
