@@ -304,7 +304,17 @@ def main_q3(args):
     agg_defs = (capi.AggDef * 1)(capi.AggDef(capi.HY_AGG_SUM, 3))
     agg_params = capi.AggParams(groupby, 3, agg_defs, 1, 0)
 
+    trace_q3 = os.environ.get("HY_Q3_TRACE") is not None  # host wall time per operator (each ends synchronised)
+
+    def mark(label, t=[0.0]):
+        if trace_q3:
+            now = time.perf_counter()
+            if label != "start":
+                print(f"[q3] {label} {1e3 * (now - t[0]):.3f} ms", file=sys.stderr)
+            t[0] = now
+
     def step():
+        mark("start")
         # TableScan(customer, c_mktsegment = 'BUILDING'): its output's chunk layout decides the join's build input
         capi.check(L.hy_table_scan_row_ids(cscan, n_cc, I32, None, c_ids, c_rows.data_ptr(), c_counts.data_ptr(),
                                            c_ws.data_ptr(), c_ws.numel(), stream), "customer scan")
@@ -315,9 +325,11 @@ def main_q3(args):
                           nz.astype(np.uint32), ckey_c, n_cc)
         j1b, j1p, b1, n1, pairs1 = join("j1", build1, orders_side, ofilter, L.hy_join_radix_bits(c_match, 4),
                                         n_ord // 4 + 64)
+        mark("customer scan + join 1")
         build2 = ref_side(j1p.data_ptr(), b1, n1, capi.HY_MIXED_CHUNKS, okey_c, n_oc)
         j2b, j2p, b2, n2, pairs2 = join("j2", build2, li_side, lfilter, L.hy_join_radix_bits(pairs1, 4),
                                         n_li // 32 + 64)
+        mark("join 2")
         # Projection over the join output (chunks = non-empty partitions; PosList groups: orders, lineitem)
         k = len(n2)
         sizes_np = np.ascontiguousarray(n2, dtype=np.uint32)
@@ -333,6 +345,7 @@ def main_q3(args):
         for j, prog in enumerate(programs):
             capi.check(L.hy_projection(ctypes.byref(pin), prog, len(prog), proj[j].data_ptr(), None, pws.data_ptr(),
                                        pws.numel(), stream), "hy_projection")
+        mark("projection")
         # Aggregate over the projection's output (a data table with the join output's chunking)
         rb = np.concatenate([[0], np.cumsum(n2.astype(np.int64))])[:-1].astype(np.uint64)
         acols = (capi.AggColumn * 4)()
@@ -366,6 +379,7 @@ def main_q3(args):
             aws = workspace(("agg", k, pairs2, ng.value), lambda b: L.hy_aggregate_workspace_size(
                 ctypes.byref(ain), ctypes.byref(agg_params), b))
         capi.check(st, "hy_aggregate")
+        mark("aggregate")
         return {"customer_matches": c_match, "join1_pairs": int(pairs1), "join2_pairs": int(pairs2),
                 "groups": int(ng.value)}
 

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstring>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -29,6 +30,44 @@ inline hy_status fail(hy_status code, const std::string& msg) {
 inline hipStream_t S(hy_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// Host -> device copies of the descriptors a call builds on the host (chunk / side / column tables, offsets): staged
+// through a per-thread pinned ring so that hipMemcpyAsync is a real asynchronous DMA (a pageable source makes the
+// runtime stage it synchronously, at a fraction of the bandwidth - measurable with tens of thousands of chunks), and
+// so that the source may go out of scope right after the call. The ring wraps after a device synchronisation, which
+// every earlier copy out of it has then completed.
+struct PinnedRing {
+  char* buf = nullptr;
+  size_t cap = 0, used = 0;
+  ~PinnedRing() {
+    if (buf) (void)hipHostFree(buf);
+  }
+};
+inline hy_status staged_htod(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  if (bytes == 0) return HY_OK;
+  thread_local PinnedRing ring;
+  const size_t need = (bytes + 255) & ~size_t(255);
+  if (ring.used + need > ring.cap) {
+    HY_HIP(hipDeviceSynchronize());  // every copy out of the ring has completed
+    if (need > ring.cap) {
+      if (ring.buf) HY_HIP(hipHostFree(ring.buf));
+      ring.buf = nullptr;
+      ring.cap = std::max<size_t>(size_t(16) << 20, 2 * need);
+      HY_HIP(hipHostMalloc(reinterpret_cast<void**>(&ring.buf), ring.cap, hipHostMallocDefault));
+    }
+    ring.used = 0;
+  }
+  char* stage = ring.buf + ring.used;
+  std::memcpy(stage, src, bytes);
+  ring.used += need;
+  HY_HIP(hipMemcpyAsync(dst, stage, bytes, hipMemcpyHostToDevice, s));
+  return HY_OK;
+}
+#define HY_STAGE(dst, src, bytes, stream)                                              \
+  do {                                                                                 \
+    const hy_status st_ = ::hyc::staged_htod((dst), (src), (bytes), (stream));         \
+    if (st_ != HY_OK) return st_;                                                      \
+  } while (0)
 
 // Bump allocator over the caller's workspace. Every carve is 256-byte aligned.
 struct Carver {

@@ -328,13 +328,13 @@ hy_status table_scan_impl(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_
       error = dmisc + 1;
       HY_HIP(hipMemsetAsync(error, 0, 4, s));
     }
-    HY_HIP(hipMemcpyAsync(dch, hc.data(), sizeof(hy_scan_chunk) * nc, hipMemcpyHostToDevice, s));
-    HY_HIP(hipMemcpyAsync(dti, ht.data(), sizeof(uint64_t) * (nc + 1), hipMemcpyHostToDevice, s));
-    HY_HIP(hipMemcpyAsync(dix, idx.data(), sizeof(uint32_t) * nc, hipMemcpyHostToDevice, s));
+    HY_STAGE(dch, hc.data(), sizeof(hy_scan_chunk) * nc, s);
+    HY_STAGE(dti, ht.data(), sizeof(uint64_t) * (nc + 1), s);
+    HY_STAGE(dix, idx.data(), sizeof(uint32_t) * nc, s);
     auto& hcid = h_cids[cls];
     hcid.resize(nc);
     for (uint32_t k = 0; k < nc; ++k) hcid[k] = chunk_ids ? chunk_ids[idx[k]] : idx[k];
-    HY_HIP(hipMemcpyAsync(dcid, hcid.data(), sizeof(uint32_t) * nc, hipMemcpyHostToDevice, s));
+    HY_STAGE(dcid, hcid.data(), sizeof(uint32_t) * nc, s);
     HY_HIP(hipMemsetAsync(dst, 0, sizeof(uint64_t) * (run + 1), s));
     HY_HIP(hipMemsetAsync(dmisc, 0, 4, s));
     if (run == 0) continue;
@@ -435,7 +435,7 @@ hy_status hy_reference_scan(const hy_row_id* pos_list, uint64_t pos_list_size, c
   if (!cv.ok) return fail(HY_ERR_WORKSPACE, "reference scan workspace too small");
   HY_HIP(hipMemsetAsync(dst, 0, sizeof(uint64_t) * (tiles + 1), s));
   HY_HIP(hipMemsetAsync(dmisc, 0, 256, s));
-  HY_HIP(hipMemcpyAsync(dch, referenced_chunks, sizeof(hy_scan_chunk) * n_referenced_chunks, hipMemcpyHostToDevice, s));
+  HY_STAGE(dch, referenced_chunks, sizeof(hy_scan_chunk) * n_referenced_chunks, s);
   hyk::RefScanDesc d{pos_list, pos_list_size, dch, n_referenced_chunks, tiles, dst, dmisc, dmisc + 1};
   auto go = [&](auto tag) -> hy_status {
     using T = decltype(tag);

@@ -690,12 +690,12 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
     tile_begin[c + 1] = tile_begin[c] + (input->chunk_sizes[c] + hyk::AGG_TILE - 1) / hyk::AGG_TILE;
   }
   if (input->n_chunks) {
-    HY_HIP(hipMemcpyAsync(w.sizes, input->chunk_sizes, 4 * input->n_chunks, hipMemcpyHostToDevice, s));
-    HY_HIP(hipMemcpyAsync(w.row_begin, row_begin.data(), 8 * row_begin.size(), hipMemcpyHostToDevice, s));
-    HY_HIP(hipMemcpyAsync(w.tile_begin, tile_begin.data(), 8 * tile_begin.size(), hipMemcpyHostToDevice, s));
+    HY_STAGE(w.sizes, input->chunk_sizes, 4 * input->n_chunks, s);
+    HY_STAGE(w.row_begin, row_begin.data(), 8 * row_begin.size(), s);
+    HY_STAGE(w.tile_begin, tile_begin.data(), 8 * tile_begin.size(), s);
   }
   const uint64_t n_pl = uint64_t(input->n_pos_groups) * input->n_chunks;
-  if (n_pl) HY_HIP(hipMemcpyAsync(w.pos_lists, input->pos_lists, sizeof(void*) * n_pl, hipMemcpyHostToDevice, s));
+  if (n_pl) HY_STAGE(w.pos_lists, input->pos_lists, sizeof(void*) * n_pl, s);
   for (uint32_t j = 0; j < input->n_columns; ++j) {
     const auto& c = input->columns[j];
     for (uint32_t k = 0; k < (c.n_nodes ? 0u : c.n_chunks); ++k) {
@@ -705,10 +705,10 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
         return fail(HY_ERR_INVALID_ARGUMENT, "vid width");
     }
     if (c.n_chunks && !c.n_nodes)
-      HY_HIP(hipMemcpyAsync(w.chunks[j], c.chunks, sizeof(hy_column_chunk) * c.n_chunks, hipMemcpyHostToDevice, s));
+      HY_STAGE(w.chunks[j], c.chunks, sizeof(hy_column_chunk) * c.n_chunks, s);
     d.cols[j].chunks = w.chunks[j];
   }
-  HY_HIP(hipMemcpyAsync(w.word_op, plan.word_op.data(), 4 * plan.word_op.size(), hipMemcpyHostToDevice, s));
+  HY_STAGE(w.word_op, plan.word_op.data(), 4 * plan.word_op.size(), s);
   HY_HIP(hipMemsetAsync(w.misc, 0, 256, s));
   d.pos_lists = w.pos_lists;
   d.chunk_size = w.sizes;
@@ -723,7 +723,7 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
   d.word_op = w.word_op;
   d.error = w.misc;
   if (input->filter && input->n_chunks) {
-    HY_HIP(hipMemcpyAsync(w.filter, input->filter, sizeof(hy_scan_chunk) * input->n_chunks, hipMemcpyHostToDevice, s));
+    HY_STAGE(w.filter, input->filter, sizeof(hy_scan_chunk) * input->n_chunks, s);
     d.filter = w.filter;
     d.filter_type = input->filter_value_type;
     d.filter_cbits = 0;
@@ -755,7 +755,7 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
       chs[c].size = input->chunk_sizes[c];
       chs[c].kind = HY_COL_VALUE;
     }
-    HY_HIP(hipMemcpyAsync(w.chunks[j], chs.data(), sizeof(hy_column_chunk) * chs.size(), hipMemcpyHostToDevice, s));
+    HY_STAGE(w.chunks[j], chs.data(), sizeof(hy_column_chunk) * chs.size(), s);
   }
 
   if (plan.fused && plan.dense_groups) {
@@ -764,8 +764,7 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
                        uint64_t(plan.dense_groups), d.words, w.word_op);
     HY_HIP(hipGetLastError());
     if (!plan.fused_nodes.empty())
-      HY_HIP(hipMemcpyAsync(w.fused_nodes, plan.fused_nodes.data(), sizeof(hyk::FqOp) * plan.fused_nodes.size(),
-                            hipMemcpyHostToDevice, s));
+      HY_STAGE(w.fused_nodes, plan.fused_nodes.data(), sizeof(hyk::FqOp) * plan.fused_nodes.size(), s);
     hyk::FusedPlan fp = plan.fp;
     fp.progs = w.fused_nodes;
     const size_t lds = sizeof(unsigned long long) * plan.dense_groups * d.words;
@@ -774,9 +773,8 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
       // kernel, which then runs over that list only (misc[8] = its length, zeroed above)
       hyk::LaneTables lt = plan.lt;
       for (int32_t li = 0; li < lt.n_load; ++li) lt.load_chunks[li] = d.cols[plan.lane_cols[li]].chunks;
-      HY_HIP(hipMemcpyAsync(w.lane_tables, &lt, sizeof(lt), hipMemcpyHostToDevice, s));
-      HY_HIP(hipMemcpyAsync(w.lane_terms, plan.lane_terms.data(), sizeof(hyk::LnTerm) * plan.lane_terms.size(),
-                            hipMemcpyHostToDevice, s));
+      HY_STAGE(w.lane_tables, &lt, sizeof(lt), s);
+      HY_STAGE(w.lane_terms, plan.lane_terms.data(), sizeof(hyk::LnTerm) * plan.lane_terms.size(), s);
       const hyk::LanePlan lp{lt.n_load, lt.n_sums, w.lane_tables, w.lane_terms, w.deferred, w.misc + 8};
       const size_t vlds = size_t(hyk::AGG_THREADS / hyk::WAVE) *
                           hyk::ln_wave_lds(lt.n_load - static_cast<int>(params->n_groupby), lt.n_sums);
@@ -968,9 +966,9 @@ hy_status hy_projection(const hy_agg_input* input, const hy_expr_node* program, 
   ProjWs w;
   carve_proj(cv, input, &w);
   if (!cv.ok || !workspace) return fail(HY_ERR_WORKSPACE, "projection workspace too small");
-  HY_HIP(hipMemcpyAsync(w.row_begin, row_begin.data(), 8 * row_begin.size(), hipMemcpyHostToDevice, s));
+  HY_STAGE(w.row_begin, row_begin.data(), 8 * row_begin.size(), s);
   const uint64_t n_pl = uint64_t(input->n_pos_groups) * input->n_chunks;
-  if (n_pl) HY_HIP(hipMemcpyAsync(w.pos_lists, input->pos_lists, sizeof(void*) * n_pl, hipMemcpyHostToDevice, s));
+  if (n_pl) HY_STAGE(w.pos_lists, input->pos_lists, sizeof(void*) * n_pl, s);
   hyk::AggDesc d{};
   d.n_cols = input->n_columns;
   d.n_pos_groups = input->n_pos_groups;
@@ -981,7 +979,7 @@ hy_status hy_projection(const hy_agg_input* input, const hy_expr_node* program, 
     for (uint32_t k = 0; k < c.n_chunks; ++k)
       if (c.chunks[k].size && !c.chunks[k].data) return fail(HY_ERR_INVALID_ARGUMENT, "column chunk without data");
     if (c.n_chunks)
-      HY_HIP(hipMemcpyAsync(w.chunks[j], c.chunks, sizeof(hy_column_chunk) * c.n_chunks, hipMemcpyHostToDevice, s));
+      HY_STAGE(w.chunks[j], c.chunks, sizeof(hy_column_chunk) * c.n_chunks, s);
     d.cols[j].chunks = w.chunks[j];
     d.cols[j].type = c.value_type;
     d.cols[j].pos_group = c.pos_group;

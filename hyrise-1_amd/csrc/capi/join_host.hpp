@@ -707,7 +707,7 @@ size_t classic_join_bytes(const SidePlan& bp, const SidePlan& pp, uint32_t bits)
 template <typename H, typename P>
 hy_status upload_side(const SidePlan& p, const SideBufs<H, P>& b, hipStream_t s) {
   auto upload = [&](auto* dst, const auto& v) -> hy_status {
-    if (!v.empty()) HY_HIP(hipMemcpyAsync(dst, v.data(), sizeof(v[0]) * v.size(), hipMemcpyHostToDevice, s));
+    if (!v.empty()) HY_STAGE(dst, v.data(), sizeof(v[0]) * v.size(), s);
     return HY_OK;
   };
   if (upload(b.chunks, p.chunks) || upload(b.tile_begin, p.tile_begin) || upload(b.row_begin, p.row_begin) ||
@@ -864,7 +864,7 @@ hy_status onepass_side(const char* tag, const SidePlan& p, OneBufs<H>& o, uint32
   SideBufs<H>& b = o.b;
   const uint32_t nd0 = 1u << w[0], w1 = w[1];
   const OnepassGeo g = onepass_geo(p, nd0);
-  HY_HIP(hipMemcpyAsync(o.class_begin, g.class_begin, sizeof(g.class_begin), hipMemcpyHostToDevice, s));
+  HY_STAGE(o.class_begin, g.class_begin, sizeof(g.class_begin), s);
   HY_HIP(hipMemsetAsync(o.ticket, 0, 4 * hyk::NCLASS, s));
   HY_HIP(hipMemsetAsync(o.status, 0, 4 * 256 * p.n_tiles1, s));
   HY_HIP(hipMemsetAsync(o.class_count, 0, 4 * 256 * hyk::NCLASS, s));
@@ -1228,14 +1228,14 @@ hy_status recv_side(const char* tag, const RecvPlan& r, RecvBufs<H, P>& rb, cons
                     uint32_t bits, uint32_t nb, uint32_t n_senders, uint32_t seed, const hyk::Rec<H, P>* in,
                     const Common& c, hipStream_t s, hyk::Rec<H, P>** recs, uint32_t** bounds) {
   auto up = [&](auto* dst, const auto& v) -> hy_status {
-    if (!v.empty()) HY_HIP(hipMemcpyAsync(dst, v.data(), sizeof(v[0]) * v.size(), hipMemcpyHostToDevice, s));
+    if (!v.empty()) HY_STAGE(dst, v.data(), sizeof(v[0]) * v.size(), s);
     return HY_OK;
   };
   if (up(rb.seg_begin, r.seg_begin) || up(rb.seg_end, r.seg_end) || up(rb.seg_stride, r.seg_stride) ||
       up(rb.seg_toff, r.seg_toff) || up(rb.seg_tile_begin, r.seg_tile_begin) || up(rb.seg_hbase, r.seg_hbase) ||
       up(rb.group_hbase, r.group_hbase) || up(rb.group_tiles, r.group_tiles) || up(rb.group_out, r.group_out))
     return HY_ERR_DEVICE;
-  HY_HIP(hipMemcpyAsync(rb.b.total, &r.rows, 8, hipMemcpyHostToDevice, s));
+  HY_STAGE(rb.b.total, &r.rows, 8, s);
   const uint32_t nseg = nb * n_senders;
   if (r.tiles) {
     hipLaunchKernelGGL(hyk::fill_tile_owner, dim3(grid_for(nseg, 256)), dim3(256), 0, s, rb.seg_tile_begin, nseg,
@@ -1348,8 +1348,8 @@ hy_status exchange_join_for_hashed(const void* build_records, const void* probe_
   const uint32_t n_parts = n_buckets << (bits - w[0]);
   hyk::RowMap bmap{}, pmap{};
   if constexpr (std::is_same_v<P, uint32_t>) {  // global row indexes -> RowIDs of the global chunk layouts
-    HY_HIP(hipMemcpyAsync(b_rows, lay.build_rows.data(), 8 * lay.build_rows.size(), hipMemcpyHostToDevice, s));
-    HY_HIP(hipMemcpyAsync(p_rows, lay.probe_rows.data(), 8 * lay.probe_rows.size(), hipMemcpyHostToDevice, s));
+    HY_STAGE(b_rows, lay.build_rows.data(), 8 * lay.build_rows.size(), s);
+    HY_STAGE(p_rows, lay.probe_rows.data(), 8 * lay.probe_rows.size(), s);
     bmap = make_map(b_rows, lay.build_rows);
     pmap = make_map(p_rows, lay.probe_rows);
   }
