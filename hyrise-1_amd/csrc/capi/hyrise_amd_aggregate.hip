@@ -991,9 +991,7 @@ hy_status hy_projection(const hy_agg_input* input, const hy_expr_node* program, 
                      out_values, out_nulls, rows, items);
   t.done();
   HY_HIP(hipGetLastError());
-  // host staging above must outlive the async copies
-  HY_HIP(hipStreamSynchronize(s));
-  return HY_OK;
+  return HY_OK;  // asynchronous: the descriptors went through the pinned staging ring
 }
 
 hy_status hy_agg_float_sum(const uint64_t* limbs, uint32_t n_limbs, int32_t emin, uint64_t special, double* out) {
