@@ -280,6 +280,7 @@ hy_status table_scan_impl(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_
   for (uint32_t i = 0; i < n_chunks; ++i) {
     const int cls = scan_class(chunks[i]);
     if (cls < 0) return fail(HY_ERR_INVALID_ARGUMENT, "bad vid width");
+    if (chunks[i].op < HY_OP_EQ || chunks[i].op > HY_OP_IS_NOT_NULL) return fail(HY_ERR_INVALID_ARGUMENT, "scan op");
     if (chunks[i].column.size && !aligned16(chunks[i].column.data))
       return fail(HY_ERR_ALIGNMENT, "column data not 16-byte aligned");
     if (chunks[i].column.nulls && !aligned16(chunks[i].column.nulls))
@@ -427,6 +428,9 @@ hy_status hy_reference_scan(const hy_row_id* pos_list, uint64_t pos_list_size, c
   HY_HIP(hipMemsetAsync(count, 0, 8, s));
   if (pos_list_size == 0) return HY_OK;
   if (n_referenced_chunks > (1u << 20)) return fail(HY_ERR_UNSUPPORTED, "too many referenced chunks");
+  for (uint32_t i = 0; i < n_referenced_chunks; ++i)
+    if (referenced_chunks[i].op < HY_OP_EQ || referenced_chunks[i].op > HY_OP_IS_NOT_NULL)
+      return fail(HY_ERR_INVALID_ARGUMENT, "scan op");
   const uint64_t tiles = (pos_list_size + hyk::SCAN_TILE - 1) / hyk::SCAN_TILE;
   Carver cv{static_cast<char*>(workspace), workspace_bytes};
   auto* dst = cv.take<uint64_t>(tiles + 1);
@@ -463,7 +467,8 @@ hy_status hy_reference_scan(const hy_row_id* pos_list, uint64_t pos_list_size, c
     default: {
       // non-numeric columns (strings) are only scanned through their dictionaries: the comparison is on value ids
       for (uint32_t i = 0; i < n_referenced_chunks; ++i)
-        if (referenced_chunks[i].column.kind != HY_COL_DICT && referenced_chunks[i].op != HY_OP_NONE)
+        if (referenced_chunks[i].column.kind != HY_COL_DICT && referenced_chunks[i].op != HY_OP_NONE &&
+            referenced_chunks[i].op != HY_OP_IS_NULL)  // IS NULL reads only the null flags
           return fail(HY_ERR_UNSUPPORTED, "reference scan of an unencoded non-numeric column");
       st = go(int32_t{});
       break;
@@ -474,6 +479,31 @@ hy_status hy_reference_scan(const hy_row_id* pos_list, uint64_t pos_list_size, c
   HY_HIP(hipMemcpyAsync(&herr, dmisc + 1, 4, hipMemcpyDeviceToHost, s));
   HY_HIP(hipStreamSynchronize(s));
   if (herr) return fail(HY_ERR_KERNEL, "reference scan look-back did not complete");
+  return HY_OK;
+}
+
+hy_status hy_pos_list_null_positions(const hy_row_id* pos_list, uint64_t pos_list_size, uint32_t* out_positions,
+                                     uint64_t* count, void* workspace, size_t workspace_bytes, hy_stream_t stream) {
+  if (!count) return fail(HY_ERR_INVALID_ARGUMENT, "null count");
+  hipStream_t s = S(stream);
+  HY_HIP(hipMemsetAsync(count, 0, 8, s));
+  if (pos_list_size == 0) return HY_OK;
+  if (!pos_list || !out_positions) return fail(HY_ERR_INVALID_ARGUMENT, "null argument");
+  const uint64_t tiles = (pos_list_size + hyk::SCAN_TILE - 1) / hyk::SCAN_TILE;
+  Carver cv{static_cast<char*>(workspace), workspace_bytes};
+  auto* dst = cv.take<uint64_t>(tiles + 1);
+  auto* dmisc = cv.take<uint32_t>(64);
+  if (!cv.ok) return fail(HY_ERR_WORKSPACE, "null-position workspace too small");
+  HY_HIP(hipMemsetAsync(dst, 0, sizeof(uint64_t) * (tiles + 1), s));
+  HY_HIP(hipMemsetAsync(dmisc, 0, 256, s));
+  hyk::RefScanDesc d{pos_list, pos_list_size, nullptr, 0, tiles, dst, dmisc, dmisc + 1};
+  hipLaunchKernelGGL((hyk::ref_scan_kernel<int32_t, true>), dim3(static_cast<uint32_t>(tiles)),
+                     dim3(hyk::SCAN_THREADS), 0, s, d, hyk::ScanConst<int32_t>{}, out_positions, count);
+  HY_HIP(hipGetLastError());
+  uint32_t herr = 0;
+  HY_HIP(hipMemcpyAsync(&herr, dmisc + 1, 4, hipMemcpyDeviceToHost, s));
+  HY_HIP(hipStreamSynchronize(s));
+  if (herr) return fail(HY_ERR_KERNEL, "null-position look-back did not complete");
   return HY_OK;
 }
 

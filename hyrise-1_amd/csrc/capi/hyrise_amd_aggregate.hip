@@ -629,6 +629,8 @@ hy_status check_filter(const hy_agg_input* in, const AggPlan& plan) {
   for (uint32_t c = 0; c < in->n_chunks; ++c) {
     const hy_scan_chunk& f = in->filter[c];
     if (f.column.size != in->chunk_sizes[c]) return fail(HY_ERR_INVALID_ARGUMENT, "filter chunk size != input chunk");
+    if (f.op < HY_OP_EQ || f.op > HY_OP_IS_NOT_NULL || f.op == HY_OP_IS_NULL)
+      return fail(HY_ERR_UNSUPPORTED, "fused scan filter op");
     if (f.op == HY_OP_NONE || f.column.size == 0) continue;
     if (!f.column.data) return fail(HY_ERR_INVALID_ARGUMENT, "filter chunk without data");
     if (f.column.kind == HY_COL_DICT) {

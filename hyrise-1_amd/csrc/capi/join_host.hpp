@@ -190,6 +190,8 @@ inline hy_status plan_filter(const hy_join_filter* f, SidePlan& p, int32_t colum
   for (size_t i = 0; i < p.chunks.size(); ++i) {
     if (p.chunks[i].pos_list) return fail(HY_ERR_UNSUPPORTED, "a filtered join side must be a data table");
     const hy_scan_chunk& sc = p.filter[i];
+    if (sc.op < HY_OP_EQ || sc.op > HY_OP_IS_NOT_NULL || sc.op == HY_OP_IS_NULL)
+      return fail(HY_ERR_UNSUPPORTED, "fused scan filter op");
     if (sc.column.size != p.chunks[i].size) return fail(HY_ERR_INVALID_ARGUMENT, "filter chunk size != join chunk size");
     if (sc.column.size && !aligned16(sc.column.data)) return fail(HY_ERR_ALIGNMENT, "filter data not 16-byte aligned");
     if (sc.column.kind == HY_COL_DICT) {

@@ -132,7 +132,12 @@ void dictionary_predicate(const BaseDictionaryColumn& col, PredicateCondition co
 hy_scan_chunk scan_descriptor(const BaseColumn& column, DataType type, PredicateCondition cond,
                               const AllTypeVariant& value) {
   hy_scan_chunk sc{};
-  if (const auto* dict = dynamic_cast<const BaseDictionaryColumn*>(&column)) {
+  if (cond == PredicateCondition::IsNull || cond == PredicateCondition::IsNotNull) {
+    // IsNullTableScanImpl (is_null_table_scan_impl.cpp:35-117): no dictionary rewrite, the null test is per row
+    Assert(type != DataType::String || dynamic_cast<const BaseDictionaryColumn*>(&column) != nullptr,
+           "hyrise-amd: TableScan on an unencoded string column is not supported by the device path");
+    sc.op = cond == PredicateCondition::IsNull ? HY_OP_IS_NULL : HY_OP_IS_NOT_NULL;
+  } else if (const auto* dict = dynamic_cast<const BaseDictionaryColumn*>(&column)) {
     dictionary_predicate(*dict, cond, value, &sc.op, &sc.search_vid);
   } else {
     Assert(type != DataType::String,
@@ -199,8 +204,6 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
   switch (_predicate_condition) {
     case PredicateCondition::Like:
     case PredicateCondition::NotLike:
-    case PredicateCondition::IsNull:
-    case PredicateCondition::IsNotNull:
     case PredicateCondition::In:
       Fail("hyrise-amd: predicate " + predicate_condition_to_string(_predicate_condition) +
            " is not supported by the device TableScan");
@@ -210,8 +213,11 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
       break;
   }
   auto output = std::make_shared<Table>(in_table->column_definitions(), TableType::References);
-  // reference single_column_table_scan_impl.cpp:23-36: comparing with NULL matches nothing
-  if (variant_is_null(_right_value)) return output;
+  const bool null_test =
+      _predicate_condition == PredicateCondition::IsNull || _predicate_condition == PredicateCondition::IsNotNull;
+  // reference single_column_table_scan_impl.cpp:23-36: comparing with NULL matches nothing (IS [NOT] NULL ignores the
+  // right value, table_scan.cpp:186-189)
+  if (!null_test && variant_is_null(_right_value)) return output;
   require_device();
   hy_stream_t s = operator_stream();
   const auto col_type = in_table->column_data_type(_left_column_id);
@@ -237,7 +243,7 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
       sizes.push_back(static_cast<uint32_t>(column->size()));
     }
     if (descs.empty()) return output;
-    const auto constant = typed_constant(col_type, _right_value);
+    const auto constant = null_test ? ScanConstant{} : typed_constant(col_type, _right_value);
     size_t ws_bytes = 0;
     hy_check(hy_table_scan_workspace_size(sizes.data(), static_cast<uint32_t>(sizes.size()), &ws_bytes),
              "hy_table_scan_workspace_size");
@@ -283,7 +289,7 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
     std::vector<hy_scan_chunk> rdesc(rtable->chunk_count());
     for (ChunkID r = 0; r < rtable->chunk_count(); ++r)
       rdesc[r] = scan_descriptor(*rtable->get_chunk(r)->get_column(rcol), col_type, _predicate_condition, _right_value);
-    const auto constant = typed_constant(col_type, _right_value);
+    const auto constant = null_test ? ScanConstant{} : typed_constant(col_type, _right_value);
     const auto dpl = device_pos_list(pos_list);
     const uint64_t m = pos_list.size();
 
@@ -334,6 +340,17 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
                                        positions.as<uint32_t>(), ows.get(), ob, s),
                "hy_reference_scan_order");
       hy_check(hy_stream_synchronize(s), "sync");  // d_rank / asc / ows are released at scope end
+    }
+    if (_predicate_condition == PredicateCondition::IsNull) {
+      // IsNullTableScanImpl::handle_column(const ReferenceColumn&) (is_null_table_scan_impl.cpp:20-33): the NULL
+      // RowIDs of the referencing column match too, appended after the referenced columns' matches
+      uint64_t nulls = 0;
+      hy_check(hy_pos_list_null_positions(dpl->ptr(), m, positions.as<uint32_t>() + total, count.as<uint64_t>(),
+                                          ws.get(), ws_bytes, s),
+               "hy_pos_list_null_positions");
+      hy_check(hy_memcpy_dtoh(&nulls, count.get(), 8, s), "dtoh");
+      hy_check(hy_stream_synchronize(s), "sync");
+      total += nulls;
     }
     if (total == 0) continue;
     // filtered PosLists, shared per distinct input PosList (table_scan.cpp:115-145)

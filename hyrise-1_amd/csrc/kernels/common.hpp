@@ -80,6 +80,7 @@ __device__ __forceinline__ bool cmp_op(int op, T v, T c) {
     case HY_OP_GE:
       return v >= c;
     case HY_OP_ALL:
+    case HY_OP_IS_NOT_NULL:
       return true;
     default:
       return false;

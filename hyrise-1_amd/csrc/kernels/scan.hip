@@ -69,6 +69,11 @@ __device__ __forceinline__ uint32_t match_mask(const hy_scan_chunk& ch, uint32_t
   if constexpr (IS_DICT) {
     const E null_vid = static_cast<E>(ch.column.dictionary_size);
     const E s = static_cast<E>(ch.search_vid);
+    if (op == HY_OP_IS_NULL) {  // is_null_table_scan_impl.cpp:55-61: the iterator's is_null() is vid == null id
+#pragma unroll
+      for (int i = 0; i < 16; ++i) mask |= static_cast<uint32_t>(v[i] == null_vid) << i;
+      return mask & valid;
+    }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const bool m = (v[i] != null_vid) && cmp_op<E>(op, v[i], s);
@@ -77,6 +82,11 @@ __device__ __forceinline__ uint32_t match_mask(const hy_scan_chunk& ch, uint32_t
   } else {
     uint8_t nl[16];
     __builtin_memcpy(nl, &nulls, 16);
+    if (op == HY_OP_IS_NULL) {  // is_null_table_scan_impl.cpp:35-53 (a column without null flags matches none)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) mask |= static_cast<uint32_t>(nl[i] != 0) << i;
+      return mask & valid;
+    }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const bool m = (nl[i] == 0) && cmp_op<E>(op, v[i], constant.value);
@@ -213,15 +223,19 @@ __device__ __forceinline__ bool ref_match(const hy_scan_chunk& ch, uint32_t off,
       vid = reinterpret_cast<const uint16_t*>(ch.column.data)[off];
     else
       vid = reinterpret_cast<const uint32_t*>(ch.column.data)[off];
+    if (ch.op == HY_OP_IS_NULL) return vid == ch.column.dictionary_size;
     if (vid == ch.column.dictionary_size) return false;
     return cmp_op<uint32_t>(ch.op, vid, ch.search_vid);
   }
-  if (ch.column.nulls != nullptr && ch.column.nulls[off]) return false;
+  const bool is_null = ch.column.nulls != nullptr && ch.column.nulls[off];
+  if (ch.op == HY_OP_IS_NULL) return is_null;
+  if (is_null) return false;
   const T v = reinterpret_cast<const T*>(ch.column.data)[off];
   return cmp_op<T>(ch.op, v, constant);
 }
 
-template <typename T>
+// NULL_ROWS: select the NULL RowIDs of the PosList instead (hy_pos_list_null_positions).
+template <typename T, bool NULL_ROWS = false>
 __global__ __launch_bounds__(SCAN_THREADS) void ref_scan_kernel(RefScanDesc d, ScanConst<T> constant,
                                                                uint32_t* __restrict__ out_positions,
                                                                uint64_t* __restrict__ count) {
@@ -241,7 +255,9 @@ __global__ __launch_bounds__(SCAN_THREADS) void ref_scan_kernel(RefScanDesc d, S
     const uint64_t r = row0 + i;
     if (r < d.n) {
       const hy_row_id rid = d.pos_list[r];
-      if (rid.chunk_offset != 0xFFFFFFFFu && rid.chunk_id < d.n_chunks) {
+      if constexpr (NULL_ROWS) {
+        if (rid.chunk_offset == 0xFFFFFFFFu) mask |= 1u << i;  // RowID::is_null (types.hpp)
+      } else if (rid.chunk_offset != 0xFFFFFFFFu && rid.chunk_id < d.n_chunks) {
         const hy_scan_chunk& ch = d.chunks[rid.chunk_id];
         if (ref_match<T>(ch, rid.chunk_offset, constant.value)) mask |= 1u << i;
       }

@@ -138,7 +138,13 @@ enum {
   HY_OP_GT = 4, /* >   */
   HY_OP_GE = 5, /* >=  */
   HY_OP_ALL = 6, /* every non-NULL row (dictionary "matches all" early-out) */
-  HY_OP_NONE = 7 /* no row (dictionary "matches none" early-out) */
+  HY_OP_NONE = 7, /* no row (dictionary "matches none" early-out) */
+  /* IS NULL / IS NOT NULL (reference IsNullTableScanImpl, is_null_table_scan_impl.cpp:20-117): no constant, no
+   * dictionary rewrite; DICT rows are NULL iff vid == dictionary_size, VALUE rows iff their null flag is set.
+   * Supported by hy_table_scan / hy_table_scan_row_ids / hy_reference_scan; the fused scan filters of
+   * hy_scan_join_hash and hy_aggregate reject HY_OP_IS_NULL with HY_ERR_UNSUPPORTED. */
+  HY_OP_IS_NULL = 8,
+  HY_OP_IS_NOT_NULL = 9 /* every non-NULL row (same rows as HY_OP_ALL) */
 };
 
 typedef struct hy_scan_chunk {
@@ -181,6 +187,15 @@ hy_status hy_reference_scan(const hy_row_id* pos_list, uint64_t pos_list_size, c
                             uint32_t n_referenced_chunks, int32_t value_type, const void* constant,
                             uint32_t* out_positions, uint64_t* count, void* workspace, size_t workspace_bytes,
                             hy_stream_t stream);
+
+/*
+ * Positions i of pos_list whose RowID is NULL (chunk_offset == INVALID_CHUNK_OFFSET), ascending, to out_positions;
+ * *count (device) receives their number. An IS NULL scan over a ReferenceColumn appends these after the matches of
+ * the referenced columns (reference IsNullTableScanImpl::handle_column(const ReferenceColumn&),
+ * is_null_table_scan_impl.cpp:20-33). Workspace as hy_reference_scan_workspace_size(pos_list_size).
+ */
+hy_status hy_pos_list_null_positions(const hy_row_id* pos_list, uint64_t pos_list_size, uint32_t* out_positions,
+                                     uint64_t* count, void* workspace, size_t workspace_bytes, hy_stream_t stream);
 
 /*
  * out[i] = pos_list[positions[i]] for i < n (device gather; builds the filtered PosList of a reference-input

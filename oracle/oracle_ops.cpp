@@ -196,6 +196,30 @@ using Mapped = std::vector<std::pair<ChunkOffset, ChunkOffset>>;
 
 void scan_data_column(const BaseColumn& col, DataType type, PredicateCondition cond, const AllTypeVariant& value,
                       ChunkID chunk_id, const Mapped* mapped, PosList& out) {
+  if (cond == PredicateCondition::IsNull || cond == PredicateCondition::IsNotNull) {
+    // IsNullTableScanImpl (is_null_table_scan_impl.cpp:35-117 and is_null_table_scan_impl.hpp:45-75): a row matches
+    // iff its is_null() equals the predicate; the value-column all/none early-outs select the same rows
+    const bool want = cond == PredicateCondition::IsNull;
+    if (const auto* dict = dynamic_cast<const BaseDictionaryColumn*>(&col)) {
+      const auto& av = dict->attribute_vector();
+      const ValueID null_vid = dict->null_value_id();
+      auto one = [&](ChunkOffset into_referencing, ChunkOffset o) {
+        if ((av.get(o) == null_vid) == want) out.emplace_back(chunk_id, into_referencing);
+      };
+      if (mapped)
+        for (const auto& [a, b] : *mapped) one(a, b);
+      else
+        for (ChunkOffset o = 0; o < col.size(); ++o) one(o, o);
+      return;
+    }
+    resolve_data_type(type, [&](auto tag) {
+      using T = decltype(tag);
+      for_each_data<T>(col, mapped, [&](const Item<T>& it) {
+        if (it.is_null == want) out.emplace_back(chunk_id, it.chunk_offset);
+      });
+    });
+    return;
+  }
   if (const auto* dict = dynamic_cast<const BaseDictionaryColumn*>(&col)) {
     ValueID svid;
     switch (cond) {
@@ -291,7 +315,8 @@ std::shared_ptr<Table> table_scan(const std::shared_ptr<const Table>& in, Column
     auto matches = std::make_shared<PosList>();
     chunk_matches[ci] = matches;
     if (std::find(excluded.begin(), excluded.end(), chunk_id) != excluded.end()) return;
-    if (!variant_is_null(value)) {
+    const bool null_test = cond == PredicateCondition::IsNull || cond == PredicateCondition::IsNotNull;
+    if (null_test || !variant_is_null(value)) {
       const auto column = in->get_chunk(chunk_id)->get_column(col);
       if (const auto* rc = dynamic_cast<const ReferenceColumn*>(column.get())) {
         // split_pos_list_by_chunk_id: std::unordered_map<ChunkID, ChunkOffsetsList>
@@ -306,6 +331,10 @@ std::shared_ptr<Table> table_scan(const std::shared_ptr<const Table>& in, Column
           const auto rcol = rc->referenced_table()->get_chunk(ref_chunk)->get_column(rc->referenced_column_id());
           scan_data_column(*rcol, type, cond, value, chunk_id, &mapped, *matches);
         }
+        // is_null_table_scan_impl.cpp:20-33: NULL RowIDs of the referencing column match IS NULL, appended last
+        if (cond == PredicateCondition::IsNull)
+          for (ChunkOffset o = 0; o < pl.size(); ++o)
+            if (pl[o].is_null()) matches->emplace_back(chunk_id, o);
       } else {
         scan_data_column(*column, type, cond, value, chunk_id, nullptr, *matches);
       }

@@ -47,6 +47,8 @@ def compressed_column_cases():
         "LessThanEquals": [100, 102, 104, 106, 100, 102, 104, 106],
         "GreaterThan": [108, 110, 112, 108, 110, 112],
         "GreaterThanEquals": [106, 108, 110, 112, 106, 108, 110, 112],
+        "IsNull": [],
+        "IsNotNull": [100, 102, 104, 106, 108, 110, 112, 100, 102, 104, 106, 108, 110, 112],
     }
 
 
@@ -59,6 +61,8 @@ def referenced_compressed_cases():
         "LessThanEquals": [100, 102, 104, 100, 102, 104],
         "GreaterThan": [106, 106],
         "GreaterThanEquals": [104, 106, 104, 106],
+        "IsNull": [],
+        "IsNotNull": [100, 102, 104, 106, 100, 102, 104, 106],
     }
 
 
@@ -71,6 +75,8 @@ def weird_pos_list_cases():
         "LessThanEquals": [100, 102, 106, 108, 110, 110],
         "GreaterThan": [112],
         "GreaterThanEquals": [110, 110, 112],
+        "IsNull": [],
+        "IsNotNull": [100, 102, 106, 108, 110, 110, 112],
     }
 
 
@@ -96,6 +102,44 @@ def around_bounds_cases():  # ScanOnCompressedColumnAroundBounds, value 0
         "GreaterThanEquals": ALL_ROWS,
         "NotEquals": [102, 104, 106, 108, 110, 112, 102, 104, 106, 108, 110, 112],
     }
+
+
+# ScanForNullValues* (table_scan_test.cpp:503-601): scan_for_null_values scans column b with IS [NOT] NULL and
+# compares column a (multiset)
+NULL_VALUE_CASES = {"IsNull": [12, 123], "IsNotNull": [12345, None, 1234, 12345, 12, 1234]}
+NO_NULL_CASES = {"IsNull": [], "IsNotNull": [12345, 123, 1234]}
+NULL_ROW_ID_CASES = {"IsNull": [123, 1234], "IsNotNull": [12345, None]}
+NULL_ROW_ID = 0xFFFFFFFF
+
+
+def null_scan_tables(hy):
+    """(name, table, expected cases) for every ScanForNullValues* test of table_scan_test.cpp:503-601."""
+    out = []
+    for enc in (None, "Dictionary"):
+        t = hy.load_table(tbl("int_int_w_null_8_rows.tbl"), 4)
+        if enc:
+            hy.encode_all_chunks(t, getattr(hy.EncodingType, enc))
+        out.append((f"w_null_{enc}", t, NULL_VALUE_CASES))
+        out.append((f"ref_w_null_{enc}", to_referencing_table(hy, t), NULL_VALUE_CASES))
+        out.append((f"null_row_id_{enc}", referencing_table_w_null_row_id(hy, t), NULL_ROW_ID_CASES))
+    t = hy.load_table(tbl("int_float.tbl"), 4)
+    out.append(("without_nulls", t, NO_NULL_CASES))
+    out.append(("ref_without_nulls", to_referencing_table(hy, t), NO_NULL_CASES))
+    return out
+
+
+def referencing_table_w_null_row_id(hy, table):
+    """create_referencing_table_w_null_row_id (table_scan_test.cpp:130-155): two ReferenceColumns with different
+    PosLists, column b's starting with a NULL RowID."""
+    pa = [[0, 1], [1, 0], [0, 2], [0, 3]]
+    pb = [[NULL_ROW_ID, NULL_ROW_ID], [0, 0], [1, 2], [0, 1]]
+    out = hy.Table([("a", hy.DataType.Int, True), ("b", hy.DataType.Int, True)], hy.TableType.References)
+    out.append_chunk([hy.ReferenceColumn(table, 0, pa), hy.ReferenceColumn(table, 1, pb)])
+    return out
+
+
+def multiset(values):
+    return sorted(values, key=lambda v: (v is None, 0 if v is None else v))
 
 
 def column_values(table, column_id):

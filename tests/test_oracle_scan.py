@@ -90,3 +90,17 @@ def test_excluded_chunks(hy, oracle):
     t = hy.load_table(tbl("int_int_shuffled.tbl"), 7)
     out = oracle.table_scan(t, 0, hy.PredicateCondition.GreaterThanEquals, 0, [0])
     assert out.row_count() == t.get_chunk(1).size()
+
+
+def test_scan_for_null_values(hy, oracle):
+    for name, t, cases in sc.null_scan_tables(hy):
+        for cond, expected in cases.items():
+            out = oracle.table_scan(t, 1, getattr(hy.PredicateCondition, cond), None, [])
+            assert sc.multiset(sc.column_values(out, 0)) == sc.multiset(expected), (name, cond)
+
+
+def test_is_null_reference_order(hy, oracle):
+    """NULL RowIDs match IS NULL after the referenced columns' matches (is_null_table_scan_impl.cpp:20-33)."""
+    t = hy.load_table(tbl("int_int_w_null_8_rows.tbl"), 4)
+    out = oracle.table_scan(sc.referencing_table_w_null_row_id(hy, t), 1, hy.PredicateCondition.IsNull, None, [])
+    assert [list(r) for r in out.get_chunk(0).get_column(1).pos_list()] == [[0, 1], [sc.NULL_ROW_ID] * 2]

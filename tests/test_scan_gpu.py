@@ -126,6 +126,8 @@ def test_synthetic_scans(hy, oracle, dtype, encode):
         for cond in CONDS:
             v = distinct // 3 if dtype in ("int", "long") else (distinct // 3) * 0.25
             check(hy, oracle, w, 0, cond, v)
+        for cond in ("IsNull", "IsNotNull"):
+            check(hy, oracle, w, 0, cond, None)
         check(hy, oracle, w, 0, "LessThan", v, excluded=[1])
 
 
@@ -135,3 +137,29 @@ def test_scan_then_reference_scan_large(hy, oracle):
     w = wrap(hy, t)
     s1 = check(hy, oracle, w, 0, "LessThan", 24)
     check(hy, oracle, s1, 1, "GreaterThanEquals", 150_000)
+
+
+def test_scan_for_null_values(hy, oracle):
+    """ScanForNullValues* (table_scan_test.cpp:503-601): data, dictionary, referencing and NULL-RowID inputs."""
+    for name, t, cases in sc.null_scan_tables(hy):
+        w = wrap(hy, t)
+        for cond, expected in cases.items():
+            s = check(hy, oracle, w, 1, cond, None)
+            assert sc.multiset(sc.column_values(s.get_output(), 0)) == sc.multiset(expected), (name, cond)
+        check(hy, oracle, w, 0, "IsNull", None)  # column a: nullable in the null tables, non-nullable in int_float
+
+
+def test_is_null_reference_scan_large(hy, oracle):
+    """IS [NOT] NULL over a multi-chunk PosList (unordered_map group order) with NULL RowIDs mixed in."""
+    rng = np.random.default_rng(11)
+    for encode in (False, True):
+        t = synthetic(hy, rng, 120_000, 30_000, "int", 40, 0.1, encode)
+        pl = np.stack([rng.integers(0, 4, 50_000), rng.integers(0, 30_000, 50_000)], axis=1).astype(np.uint32)
+        pl[rng.random(50_000) < 0.05] = sc.NULL_ROW_ID
+        ref = hy.Table([("a", hy.DataType.Int, True), ("b", hy.DataType.Int, False)], hy.TableType.References)
+        ref.append_chunk([hy.ReferenceColumn(t, 0, pl), hy.ReferenceColumn(t, 1, pl)])
+        w = wrap(hy, ref)
+        for cond in ("IsNull", "IsNotNull"):
+            check(hy, oracle, w, 0, cond, None)
+        s1 = check(hy, oracle, wrap(hy, t), 0, "IsNotNull", None)
+        check(hy, oracle, s1, 0, "LessThan", 20)
