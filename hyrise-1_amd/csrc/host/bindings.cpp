@@ -290,8 +290,13 @@ PYBIND11_MODULE(_hyrise_host, m) {
   py::class_<TableWrapper, AbstractOperator, std::shared_ptr<TableWrapper>>(m, "TableWrapper")
       .def(py::init<std::shared_ptr<const Table>>());
 
+  py::class_<ColumnParameter>(m, "ColumnParameter")
+      .def(py::init([](ColumnID c) { return ColumnParameter{c}; }), py::arg("column_id"))
+      .def_readonly("column_id", &ColumnParameter::column_id);
   py::class_<TableScan, AbstractOperator, std::shared_ptr<TableScan>>(m, "TableScan")
       .def(py::init([](std::shared_ptr<AbstractOperator> in, ColumnID col, PredicateCondition cond, py::object value) {
+             if (py::isinstance<ColumnParameter>(value))
+               return std::make_shared<TableScan>(in, col, cond, value.cast<ColumnParameter>());
              return std::make_shared<TableScan>(in, col, cond, to_variant(value));
            }),
            py::arg("input"), py::arg("column_id"), py::arg("predicate_condition"), py::arg("value"))

@@ -192,6 +192,10 @@ std::vector<ChunkID> unordered_map_order(const std::vector<ChunkID>& first_appea
   return out;
 }
 
+std::shared_ptr<Table> column_comparison_scan(const std::shared_ptr<const Table>& in_table, ColumnID left_column_id,
+                                              PredicateCondition cond, ColumnID right_column_id,
+                                              const std::vector<bool>& excluded);
+
 }  // namespace
 
 const std::string TableScan::description() const {
@@ -211,6 +215,16 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
       Fail("Unsupported comparison type encountered");  // reference: BETWEEN is split before it reaches the scan
     default:
       break;
+  }
+  if (_right_column_id != INVALID_COLUMN_ID) {
+    // ColumnComparisonTableScanImpl (table_scan.cpp:191-199, column_comparison_table_scan_impl.cpp:23-84)
+    Assert(_predicate_condition != PredicateCondition::IsNull && _predicate_condition != PredicateCondition::IsNotNull,
+           "Unsupported comparison type encountered");
+    std::vector<bool> excluded(in_table->chunk_count(), false);
+    for (const auto c : _excluded_chunk_ids)
+      if (c < excluded.size()) excluded[c] = true;
+    _performance_data.rows_in = in_table->row_count();
+    return column_comparison_scan(in_table, _left_column_id, _predicate_condition, _right_column_id, excluded);
   }
   auto output = std::make_shared<Table>(in_table->column_definitions(), TableType::References);
   const bool null_test =
@@ -539,6 +553,83 @@ JoinSideInput describe_side(const std::shared_ptr<const Table>& table, ColumnID 
     in.fuse = fuse ? 1 : 0;
   }
   return in;
+}
+
+std::shared_ptr<Table> column_comparison_scan(const std::shared_ptr<const Table>& in_table, ColumnID left_column_id,
+                                              PredicateCondition cond, ColumnID right_column_id,
+                                              const std::vector<bool>& excluded) {
+  auto output = std::make_shared<Table>(in_table->column_definitions(), TableType::References);
+  const auto lt = in_table->column_data_type(left_column_id);
+  const auto rt = in_table->column_data_type(right_column_id);
+  Assert((lt == DataType::String) == (rt == DataType::String), "Invalid column combination detected!");
+  Assert(lt != DataType::String, "hyrise-amd: column comparison of string columns is not supported by the device path");
+  require_device();
+  hy_stream_t s = operator_stream();
+  JoinSideInput l = describe_side(in_table, left_column_id);
+  JoinSideInput r = describe_side(in_table, right_column_id);
+  std::vector<hy_join_chunk> lc, rc;
+  for (ChunkID c = 0; c < in_table->chunk_count(); ++c) {
+    if (excluded[c]) continue;
+    lc.push_back(l.chunks[c]);
+    rc.push_back(r.chunks[c]);
+  }
+  if (lc.empty()) return output;
+  hy_join_side ls{lc.data(), static_cast<uint32_t>(lc.size()), hy_type_of(lt), l.referenced.data(),
+                  static_cast<uint32_t>(l.referenced.size()), 0, 0};
+  hy_join_side rs{rc.data(), static_cast<uint32_t>(rc.size()), hy_type_of(rt), r.referenced.data(),
+                  static_cast<uint32_t>(r.referenced.size()), 0, 0};
+  const bool is_ref = in_table->type() == TableType::References;
+  size_t ws_bytes = 0;
+  hy_check(hy_column_compare_scan_workspace_size(&ls, &rs, is_ref ? 0 : 1, &ws_bytes),
+           "hy_column_compare_scan_workspace_size");
+  DeviceBuffer ws(ws_bytes, s);
+  uint64_t total_rows = 0;
+  for (const auto& c : lc) total_rows += c.size;
+  // data input: output RowIDs {chunk id, offset} (the PosLists); reference input: chunk offsets (positions to filter
+  // the input PosLists with, table_scan.cpp:104-145)
+  auto items = std::make_shared<DeviceBuffer>(std::max<uint64_t>(total_rows, 1) * (is_ref ? 4 : sizeof(RowID)));
+  DeviceBuffer counts(lc.size() * 4, s), n_out(8, s);
+  hy_check(hy_column_compare_scan(&ls, &rs, value_op(cond), is_ref ? nullptr : items->as<hy_row_id>(),
+                                  is_ref ? items->as<uint32_t>() : nullptr, counts.as<uint32_t>(), n_out.as<uint64_t>(),
+                                  ws.get(), ws_bytes, s),
+           "hy_column_compare_scan");
+  std::vector<uint32_t> h_counts(lc.size());
+  hy_check(hy_memcpy_dtoh(h_counts.data(), counts.get(), 4 * lc.size(), s), "dtoh");
+  hy_check(hy_stream_synchronize(s), "sync");
+  uint64_t begin = 0;
+  for (size_t k = 0; k < lc.size(); ++k) {
+    const uint32_t n = h_counts[k];
+    const ChunkID chunk_id = lc[k].chunk_id;
+    if (n == 0) continue;  // no empty output chunks (table_scan.cpp:99)
+    ChunkColumns cols;
+    if (!is_ref) {
+      auto pl = pos_list_from_device(items, begin, n);
+      pl->set_single_chunk_id(chunk_id);
+      for (ColumnID col = 0; col < in_table->column_count(); ++col)
+        cols.push_back(std::make_shared<ReferenceColumn>(in_table, col, pl));
+    } else {
+      const auto chunk = in_table->get_chunk(chunk_id);
+      std::map<const PosList*, std::shared_ptr<PosList>> filtered;
+      for (ColumnID col = 0; col < in_table->column_count(); ++col) {
+        const auto rcol = std::dynamic_pointer_cast<const ReferenceColumn>(chunk->get_column(col));
+        Assert(rcol != nullptr, "All columns should be of type ReferenceColumn.");
+        auto& f = filtered[rcol->pos_list().get()];
+        if (!f) {
+          const auto src = device_pos_list(*rcol->pos_list());
+          auto rows = std::make_shared<DeviceBuffer>(static_cast<uint64_t>(n) * sizeof(RowID));
+          hy_check(hy_gather_row_ids(src->ptr(), items->as<uint32_t>() + begin, n, rows->as<hy_row_id>(), s),
+                   "hy_gather_row_ids");
+          hy_check(hy_stream_synchronize(s), "sync");
+          f = pos_list_from_device(rows, 0, n);
+          f->set_single_chunk_id(rcol->pos_list()->single_chunk_id());
+        }
+        cols.push_back(std::make_shared<ReferenceColumn>(rcol->referenced_table(), rcol->referenced_column_id(), f));
+      }
+    }
+    output->append_chunk(cols);
+    begin += n;
+  }
+  return output;
 }
 
 int32_t join_mode(JoinMode m) {

@@ -74,6 +74,12 @@ class TableWrapper final : public AbstractOperator {
   std::shared_ptr<const Table> _table;
 };
 
+// The ColumnID alternative of the reference's right parameter (AllParameterVariant, all_parameter_variant.hpp):
+// TableScan compares two columns of its input (ColumnComparisonTableScanImpl, table_scan.cpp:191-199).
+struct ColumnParameter {
+  ColumnID column_id;
+};
+
 class TableScan final : public AbstractOperator {
  public:
   TableScan(std::shared_ptr<const AbstractOperator> in, ColumnID left_column_id, PredicateCondition predicate_condition,
@@ -82,12 +88,19 @@ class TableScan final : public AbstractOperator {
         _left_column_id(left_column_id),
         _predicate_condition(predicate_condition),
         _right_value(std::move(right_value)) {}
+  TableScan(std::shared_ptr<const AbstractOperator> in, ColumnID left_column_id, PredicateCondition predicate_condition,
+            ColumnParameter right_column)
+      : AbstractOperator(OperatorType::TableScan, std::move(in)),
+        _left_column_id(left_column_id),
+        _predicate_condition(predicate_condition),
+        _right_column_id(right_column.column_id) {}
 
   const std::string name() const override { return "TableScan"; }
   const std::string description() const override;
   ColumnID left_column_id() const { return _left_column_id; }
   PredicateCondition predicate_condition() const { return _predicate_condition; }
   const AllTypeVariant& right_value() const { return _right_value; }
+  ColumnID right_column_id() const { return _right_column_id; }  // INVALID_COLUMN_ID for a value comparison
   void set_excluded_chunk_ids(const std::vector<ChunkID>& ids) { _excluded_chunk_ids = ids; }
 
  protected:
@@ -97,6 +110,7 @@ class TableScan final : public AbstractOperator {
   ColumnID _left_column_id;
   PredicateCondition _predicate_condition;
   AllTypeVariant _right_value;
+  ColumnID _right_column_id = INVALID_COLUMN_ID;
   std::vector<ChunkID> _excluded_chunk_ids;
 };
 

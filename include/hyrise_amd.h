@@ -288,6 +288,25 @@ typedef struct hy_join_side {
   uint32_t referenced_chunk_base;
 } hy_join_side;
 
+/*
+ * Column-vs-column TableScan (reference ColumnComparisonTableScanImpl::scan_chunk,
+ * column_comparison_table_scan_impl.cpp:23-84 + BaseTableScanImpl::_binary_scan, base_table_scan_impl.hpp:64-76):
+ * for every chunk c of the two sides (same chunk count and sizes; both data chunks or both PosLists, the reference's
+ * "Invalid column combination" otherwise), row i matches iff neither value is NULL (a NULL RowID reads as NULL) and
+ * `left OP right` holds with op in HY_OP_EQ..HY_OP_GE under C++'s usual arithmetic conversions of the two
+ * HY_TYPE_* value types. Matches are written chunk-major, offsets ascending: either as RowIDs
+ * {left.chunks[c].chunk_id, i} (out_rows) or as chunk offsets (out_offsets) - exactly one of the two. counts[c]
+ * (device, n_chunks) receives the matches of chunk c, *n_out (device) their total; chunk c's matches start at the sum
+ * of counts of the chunks before it. Sides are hy_join_side descriptors (value_type, chunks, referenced chunks);
+ * fuse_dereference is ignored. Non-numeric (string) columns: HY_ERR_UNSUPPORTED.
+ */
+hy_status hy_column_compare_scan_workspace_size(const hy_join_side* left, const hy_join_side* right, int32_t out_rows,
+                                                size_t* bytes);
+hy_status hy_column_compare_scan(const hy_join_side* left, const hy_join_side* right, int32_t op,
+                                 hy_row_id* out_rows, uint32_t* out_offsets, uint32_t* counts, uint64_t* n_out,
+                                 void* workspace, size_t workspace_bytes, hy_stream_t stream);
+
+
 typedef struct hy_join_params {
   int32_t mode;           /* HY_JOIN_* */
   int32_t hashed_type;    /* HY_TYPE_* of JoinHashTraits<L,R>::HashType (hash_traits.hpp:9-42) */

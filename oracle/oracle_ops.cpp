@@ -303,8 +303,38 @@ void scan_data_column(const BaseColumn& col, DataType type, PredicateCondition c
   });
 }
 
+// ColumnComparisonTableScanImpl::scan_chunk (column_comparison_table_scan_impl.cpp:23-84) with _binary_scan
+// (base_table_scan_impl.hpp:64-76): row-wise, NULL on either side never matches, C++ arithmetic conversions compare.
+void compare_columns(const BaseColumn& left, DataType lt, const BaseColumn& right, DataType rt, PredicateCondition cond,
+                     ChunkID chunk_id, PosList& out) {
+  resolve_data_type(lt, [&](auto ltag) {
+    resolve_data_type(rt, [&](auto rtag) {
+      using L = std::decay_t<decltype(ltag)>;
+      using R = std::decay_t<decltype(rtag)>;
+      if constexpr (std::is_same_v<L, std::string> != std::is_same_v<R, std::string>) {
+        Fail("Invalid column combination detected!");
+      } else {
+        const bool l_ref = dynamic_cast<const ReferenceColumn*>(&left) != nullptr;
+        const bool r_ref = dynamic_cast<const ReferenceColumn*>(&right) != nullptr;
+        if (l_ref != r_ref) Fail("Invalid column combination detected!");
+        std::vector<std::pair<L, bool>> lv;
+        std::vector<std::pair<R, bool>> rv;
+        for_each_any<L>(left, [&](const Item<L>& it) { lv.emplace_back(it.value, it.is_null); });
+        for_each_any<R>(right, [&](const Item<R>& it) { rv.emplace_back(it.value, it.is_null); });
+        with_comparator(cond, [&](auto cmp) {
+          for (ChunkOffset o = 0; o < lv.size(); ++o) {
+            if (lv[o].second || rv[o].second) continue;
+            if (cmp(lv[o].first, rv[o].first)) out.emplace_back(chunk_id, o);
+          }
+        });
+      }
+    });
+  });
+}
+
 std::shared_ptr<Table> table_scan(const std::shared_ptr<const Table>& in, ColumnID col, PredicateCondition cond,
-                                  const AllTypeVariant& value, const std::vector<ChunkID>& excluded) {
+                                  const AllTypeVariant& value, const std::vector<ChunkID>& excluded,
+                                  ColumnID right_col = INVALID_COLUMN_ID) {
   if (cond == PredicateCondition::Between) Fail("Unsupported comparison type encountered");
   auto out = std::make_shared<Table>(in->column_definitions(), TableType::References);
   const DataType type = in->column_data_type(col);
@@ -315,6 +345,12 @@ std::shared_ptr<Table> table_scan(const std::shared_ptr<const Table>& in, Column
     auto matches = std::make_shared<PosList>();
     chunk_matches[ci] = matches;
     if (std::find(excluded.begin(), excluded.end(), chunk_id) != excluded.end()) return;
+    if (right_col != INVALID_COLUMN_ID) {  // table_scan.cpp:191-199
+      const auto chunk = in->get_chunk(chunk_id);
+      compare_columns(*chunk->get_column(col), type, *chunk->get_column(right_col), in->column_data_type(right_col), cond,
+                      chunk_id, *matches);
+      return;
+    }
     const bool null_test = cond == PredicateCondition::IsNull || cond == PredicateCondition::IsNotNull;
     if (null_test || !variant_is_null(value)) {
       const auto column = in->get_chunk(chunk_id)->get_column(col);
@@ -1136,12 +1172,13 @@ PYBIND11_MODULE(_hyrise_oracle, m) {
   m.def("threads", []() { return oracle::g_threads; });
   m.def("table_scan",
         [](std::shared_ptr<Table> in, ColumnID col, PredicateCondition cond, py::object value,
-           std::vector<ChunkID> excluded) {
+           std::vector<ChunkID> excluded, std::optional<ColumnID> right_column_id) {
+          const auto v = to_variant(value);
           py::gil_scoped_release rel;
-          return oracle::table_scan(in, col, cond, to_variant(value), excluded);
+          return oracle::table_scan(in, col, cond, v, excluded, right_column_id.value_or(INVALID_COLUMN_ID));
         },
         py::arg("table"), py::arg("column_id"), py::arg("predicate_condition"), py::arg("value"),
-        py::arg("excluded_chunk_ids") = std::vector<ChunkID>{});
+        py::arg("excluded_chunk_ids") = std::vector<ChunkID>{}, py::arg("right_column_id") = py::none());
   m.def("join_hash",
         [](std::shared_ptr<Table> l, std::shared_ptr<Table> r, JoinMode mode, std::pair<ColumnID, ColumnID> cols,
            uint32_t radix_bits) {

@@ -138,6 +138,22 @@ def referencing_table_w_null_row_id(hy, table):
     return out
 
 
+# Scan*ColumnWithFloatColumnWithNullValues (table_scan_test.cpp:383-439): a > b over int_int_w_null_8_rows (chunk 4),
+# as data / dictionary / referencing table; column a of the output
+COLUMN_COMPARE_EXPECTED = [12345, 1234, 12345, 1234]
+
+
+def column_compare_tables(hy):
+    out = []
+    for enc in (None, "Dictionary"):
+        t = hy.load_table(tbl("int_int_w_null_8_rows.tbl"), 4)
+        if enc:
+            hy.encode_all_chunks(t, getattr(hy.EncodingType, enc))
+        out.append((f"data_{enc}", t))
+        out.append((f"ref_{enc}", to_referencing_table(hy, t)))
+    return out
+
+
 def multiset(values):
     return sorted(values, key=lambda v: (v is None, 0 if v is None else v))
 

@@ -104,3 +104,20 @@ def test_is_null_reference_order(hy, oracle):
     t = hy.load_table(tbl("int_int_w_null_8_rows.tbl"), 4)
     out = oracle.table_scan(sc.referencing_table_w_null_row_id(hy, t), 1, hy.PredicateCondition.IsNull, None, [])
     assert [list(r) for r in out.get_chunk(0).get_column(1).pos_list()] == [[0, 1], [sc.NULL_ROW_ID] * 2]
+
+
+def test_column_comparison(hy, oracle):
+    for name, t in sc.column_compare_tables(hy):
+        out = oracle.table_scan(t, 0, hy.PredicateCondition.GreaterThan, None, [], right_column_id=1)
+        assert sc.multiset(sc.column_values(out, 0)) == sc.multiset(sc.COLUMN_COMPARE_EXPECTED), name
+
+
+def test_column_comparison_mixed_types(hy, oracle):
+    """int vs float compares as float (C++ usual arithmetic conversions, the reference's with_comparator)."""
+    t = hy.Table([("a", hy.DataType.Int, False), ("b", hy.DataType.Float, False)], hy.TableType.Data)
+    for a, b in ((1, 0.5), (2, 2.0), (3, 3.5), (16777217, 16777216.0)):
+        t.append([a, b])
+    gt = oracle.table_scan(t, 0, hy.PredicateCondition.GreaterThan, None, [], right_column_id=1)
+    eq = oracle.table_scan(t, 0, hy.PredicateCondition.Equals, None, [], right_column_id=1)
+    assert sc.column_values(gt, 0) == [1]
+    assert sc.column_values(eq, 0) == [2, 16777217]  # 16777217 -> 16777216.0f

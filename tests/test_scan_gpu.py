@@ -163,3 +163,59 @@ def test_is_null_reference_scan_large(hy, oracle):
             check(hy, oracle, w, 0, cond, None)
         s1 = check(hy, oracle, wrap(hy, t), 0, "IsNotNull", None)
         check(hy, oracle, s1, 0, "LessThan", 20)
+
+
+def check_cmp(hy, oracle, op, left, cond, right, excluded=None):
+    s = hy.TableScan(op, left, getattr(hy.PredicateCondition, cond), hy.ColumnParameter(right))
+    if excluded:
+        s.set_excluded_chunk_ids(excluded)
+    s.execute()
+    exp = oracle.table_scan(op.get_output(), left, getattr(hy.PredicateCondition, cond), None, excluded or [],
+                            right_column_id=right)
+    assert_identical(s.get_output(), exp)
+    return s
+
+
+def test_column_comparison_reference_cases(hy, oracle):
+    """Scan*ColumnWithFloatColumnWithNullValues (table_scan_test.cpp:383-439) plus every predicate."""
+    for name, t in sc.column_compare_tables(hy):
+        w = wrap(hy, t)
+        s = check_cmp(hy, oracle, w, 0, "GreaterThan", 1)
+        assert sc.multiset(sc.column_values(s.get_output(), 0)) == sc.multiset(sc.COLUMN_COMPARE_EXPECTED), name
+        for cond in CONDS:
+            check_cmp(hy, oracle, w, 1, cond, 0)
+    w = wrap(hy, hy.load_table(tbl("int_float.tbl"), 2))
+    for cond in CONDS:
+        check_cmp(hy, oracle, w, 0, cond, 1)
+        check_cmp(hy, oracle, w, 1, cond, 0)
+
+
+@pytest.mark.parametrize("types", [("int", "int"), ("int", "float"), ("long", "double"), ("long", "float"),
+                                   ("double", "int"), ("float", "long")])
+def test_column_comparison_synthetic(hy, oracle, types):
+    rng = np.random.default_rng(0x434D50)
+    dts = {"int": hy.DataType.Int, "long": hy.DataType.Long, "float": hy.DataType.Float, "double": hy.DataType.Double}
+    npt = {"int": np.int32, "long": np.int64, "float": np.float32, "double": np.float64}
+    n, chunk = 90_000, 20_011
+    cols = []
+    for ty in types:
+        v = rng.integers(0, 60, n).astype(npt[ty])
+        if ty in ("float", "double"):
+            v = (v * 0.5).astype(npt[ty])
+        cols.append(v)
+    nulls = [(rng.random(n) < 0.05).astype(np.uint8), (rng.random(n) < 0.05).astype(np.uint8)]
+    t = hy.Table.from_arrays([("a", dts[types[0]], True), ("b", dts[types[1]], True)], cols, nulls, chunk)
+    hy.encode_chunks(t, [1, 3], hy.EncodingType.Dictionary)  # mixed value / dictionary chunks
+    w = wrap(hy, t)
+    for cond in CONDS:
+        check_cmp(hy, oracle, w, 0, cond, 1)
+    check_cmp(hy, oracle, w, 0, "LessThan", 1, excluded=[0, 2])
+    # reference input (a scan's output, then a weird PosList with NULL RowIDs across chunks)
+    s1 = check(hy, oracle, w, 0, "IsNotNull", None)
+    check_cmp(hy, oracle, s1, 1, "GreaterThanEquals", 0)
+    pl = np.stack([rng.integers(0, 5, 30_000), rng.integers(0, 10_000, 30_000)], axis=1).astype(np.uint32)
+    pl[rng.random(30_000) < 0.05] = sc.NULL_ROW_ID
+    ref = hy.Table([("a", dts[types[0]], True), ("b", dts[types[1]], True)], hy.TableType.References)
+    ref.append_chunk([hy.ReferenceColumn(t, 0, pl), hy.ReferenceColumn(t, 1, pl)])
+    for cond in ("Equals", "LessThan", "GreaterThan"):
+        check_cmp(hy, oracle, wrap(hy, ref), 0, cond, 1)
