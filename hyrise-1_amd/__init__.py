@@ -49,6 +49,7 @@ ReferenceColumn = _host.ReferenceColumn
 AbstractOperator = _host.AbstractOperator
 TableWrapper = _host.TableWrapper
 TableScan = _host.TableScan
+ColumnParameter = _host.ColumnParameter
 JoinHash = _host.JoinHash
 Aggregate = _host.Aggregate
 AggregateColumnDefinition = _host.AggregateColumnDefinition

@@ -213,7 +213,7 @@ def test_column_comparison_synthetic(hy, oracle, types):
     # reference input (a scan's output, then a weird PosList with NULL RowIDs across chunks)
     s1 = check(hy, oracle, w, 0, "IsNotNull", None)
     check_cmp(hy, oracle, s1, 1, "GreaterThanEquals", 0)
-    pl = np.stack([rng.integers(0, 5, 30_000), rng.integers(0, 10_000, 30_000)], axis=1).astype(np.uint32)
+    pl = np.stack([rng.integers(0, 5, 30_000), rng.integers(0, 9_956, 30_000)], axis=1).astype(np.uint32)
     pl[rng.random(30_000) < 0.05] = sc.NULL_ROW_ID
     ref = hy.Table([("a", dts[types[0]], True), ("b", dts[types[1]], True)], hy.TableType.References)
     ref.append_chunk([hy.ReferenceColumn(t, 0, pl), hy.ReferenceColumn(t, 1, pl)])
