@@ -18,7 +18,7 @@ lib = ctypes.CDLL(LIB_PATH)
 HY_OK, HY_ERR_CAPACITY, HY_ERR_GROUP_BOUND = 0, 6, 8
 HY_TYPE_INT32, HY_TYPE_INT64, HY_TYPE_FLOAT, HY_TYPE_DOUBLE = 1, 2, 3, 4
 HY_COL_VALUE, HY_COL_DICT = 0, 1
-HY_OP_EQ, HY_OP_NE, HY_OP_LT, HY_OP_LE, HY_OP_GT, HY_OP_GE, HY_OP_ALL, HY_OP_NONE, HY_OP_IS_NULL, HY_OP_IS_NOT_NULL = range(10)
+HY_OP_EQ, HY_OP_NE, HY_OP_LT, HY_OP_LE, HY_OP_GT, HY_OP_GE, HY_OP_ALL, HY_OP_NONE, HY_OP_IS_NULL, HY_OP_IS_NOT_NULL, HY_OP_VID_SET = range(11)
 HY_JOIN_INNER, HY_JOIN_LEFT, HY_JOIN_RIGHT, HY_JOIN_SEMI, HY_JOIN_ANTI = 0, 1, 2, 5, 6
 HY_AGG_MIN, HY_AGG_MAX, HY_AGG_SUM, HY_AGG_AVG, HY_AGG_COUNT, HY_AGG_COUNT_DISTINCT = range(6)
 HY_AGG_MAX_AGGREGATES = 16
@@ -38,7 +38,7 @@ class ColumnChunk(ctypes.Structure):
 
 class ScanChunk(ctypes.Structure):
     _fields_ = [("column", ColumnChunk), ("op", ctypes.c_int32), ("search_vid", ctypes.c_uint32),
-                ("out_begin", ctypes.c_uint64)]
+                ("out_begin", ctypes.c_uint64), ("vid_set", ctypes.c_void_p)]
 
 
 HY_MIXED_CHUNKS = 0xFFFFFFFF

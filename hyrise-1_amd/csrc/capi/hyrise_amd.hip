@@ -280,7 +280,9 @@ hy_status table_scan_impl(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_
   for (uint32_t i = 0; i < n_chunks; ++i) {
     const int cls = scan_class(chunks[i]);
     if (cls < 0) return fail(HY_ERR_INVALID_ARGUMENT, "bad vid width");
-    if (chunks[i].op < HY_OP_EQ || chunks[i].op > HY_OP_IS_NOT_NULL) return fail(HY_ERR_INVALID_ARGUMENT, "scan op");
+    if (chunks[i].op < HY_OP_EQ || chunks[i].op > HY_OP_VID_SET) return fail(HY_ERR_INVALID_ARGUMENT, "scan op");
+    if (chunks[i].op == HY_OP_VID_SET && (chunks[i].column.kind != HY_COL_DICT || !chunks[i].vid_set))
+      return fail(HY_ERR_INVALID_ARGUMENT, "HY_OP_VID_SET needs a dictionary chunk and a vid_set");
     if (chunks[i].column.size && !aligned16(chunks[i].column.data))
       return fail(HY_ERR_ALIGNMENT, "column data not 16-byte aligned");
     if (chunks[i].column.nulls && !aligned16(chunks[i].column.nulls))
@@ -429,7 +431,9 @@ hy_status hy_reference_scan(const hy_row_id* pos_list, uint64_t pos_list_size, c
   if (pos_list_size == 0) return HY_OK;
   if (n_referenced_chunks > (1u << 20)) return fail(HY_ERR_UNSUPPORTED, "too many referenced chunks");
   for (uint32_t i = 0; i < n_referenced_chunks; ++i)
-    if (referenced_chunks[i].op < HY_OP_EQ || referenced_chunks[i].op > HY_OP_IS_NOT_NULL)
+    if (referenced_chunks[i].op < HY_OP_EQ || referenced_chunks[i].op > HY_OP_VID_SET ||
+        (referenced_chunks[i].op == HY_OP_VID_SET &&
+         (referenced_chunks[i].column.kind != HY_COL_DICT || !referenced_chunks[i].vid_set)))
       return fail(HY_ERR_INVALID_ARGUMENT, "scan op");
   const uint64_t tiles = (pos_list_size + hyk::SCAN_TILE - 1) / hyk::SCAN_TILE;
   Carver cv{static_cast<char*>(workspace), workspace_bytes};

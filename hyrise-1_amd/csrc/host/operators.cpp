@@ -4,7 +4,9 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <numeric>
+#include <regex>
 #include <unordered_map>
 
 namespace hyrise {
@@ -128,11 +130,143 @@ void dictionary_predicate(const BaseDictionaryColumn& col, PredicateCondition co
   }
 }
 
+// SQL LIKE semantics of the reference's LikeMatcher (src/lib/expression/evaluation/like_matcher.cpp:9-118): the
+// pattern is split into literal runs and the wildcards '%' / '_'; 'abc%', '%abc', '%abc%' and '%a%b%...%' are matched
+// with plain string searches, anything else through the ECMAScript regex '^...$' the reference builds (its escaping
+// leaves '[' and ']' as regex syntax, so those patterns behave as the reference's do).
+class LikePattern {
+ public:
+  explicit LikePattern(const std::string& pattern) {
+    std::vector<std::string> tokens;  // "%" / "_" wildcards, other tokens are literal runs
+    std::vector<bool> is_wild;
+    for (size_t i = 0; i < pattern.size();) {
+      if (pattern[i] == '%' || pattern[i] == '_') {
+        tokens.emplace_back(1, pattern[i]);
+        is_wild.push_back(true);
+        ++i;
+        continue;
+      }
+      const size_t next = pattern.find_first_of("_%", i);
+      tokens.push_back(pattern.substr(i, next == std::string::npos ? std::string::npos : next - i));
+      is_wild.push_back(false);
+      i = next == std::string::npos ? pattern.size() : next;
+    }
+    auto any = [&](size_t k) { return is_wild[k] && tokens[k] == "%"; };
+    auto lit = [&](size_t k) { return !is_wild[k]; };
+    const size_t n = tokens.size();
+    if (n == 2 && lit(0) && any(1)) {
+      _kind = Kind::StartsWith;
+      _parts = {tokens[0]};
+    } else if (n == 2 && any(0) && lit(1)) {
+      _kind = Kind::EndsWith;
+      _parts = {tokens[1]};
+    } else if (n == 3 && any(0) && lit(1) && any(2)) {
+      _kind = Kind::Contains;
+      _parts = {tokens[1]};
+    } else {
+      bool multi = true, expect_any = true;
+      for (size_t k = 0; k < n && multi; ++k) {
+        if (expect_any ? !any(k) : !lit(k)) multi = false;
+        if (multi && !expect_any) _parts.push_back(tokens[k]);
+        expect_any = !expect_any;
+      }
+      if (multi) {
+        _kind = Kind::MultipleContains;
+      } else {
+        _kind = Kind::Regex;
+        _parts.clear();
+        std::string re = "^";
+        for (const char ch : pattern) {
+          if (ch == '%') {
+            re += ".*";
+          } else if (ch == '_') {
+            re += '.';
+          } else {
+            if (std::strchr("\\.^$+?(){}|*", ch) != nullptr) re += '\\';
+            re += ch;
+          }
+        }
+        _regex = std::regex(re + "$");
+      }
+    }
+  }
+
+  bool operator()(const std::string& v) const {
+    switch (_kind) {
+      case Kind::StartsWith:
+        return v.compare(0, _parts[0].size(), _parts[0]) == 0 && v.size() >= _parts[0].size();
+      case Kind::EndsWith:
+        return v.size() >= _parts[0].size() && v.compare(v.size() - _parts[0].size(), _parts[0].size(), _parts[0]) == 0;
+      case Kind::Contains:
+        return v.find(_parts[0]) != std::string::npos;
+      case Kind::MultipleContains: {
+        size_t at = 0;
+        for (const auto& p : _parts) {
+          const size_t f = v.find(p, at);
+          if (f == std::string::npos) return false;
+          at = f + p.size();
+        }
+        return true;
+      }
+      default:
+        return std::regex_match(v, _regex);
+    }
+  }
+
+ private:
+  enum class Kind { StartsWith, EndsWith, Contains, MultipleContains, Regex };
+  Kind _kind = Kind::Regex;
+  std::vector<std::string> _parts;
+  std::regex _regex;
+};
+
+// LIKE / NOT LIKE over a dictionary chunk (like_table_scan_impl.cpp:48-83, 102-120): the pattern is evaluated once per
+// dictionary entry on the host; all / none early-outs, otherwise the device scans against the set of matching ids.
+void like_predicate(const BaseDictionaryColumn& column, PredicateCondition cond, const AllTypeVariant& value,
+                    hy_scan_chunk* sc, std::vector<std::shared_ptr<DeviceBuffer>>* keep) {
+  const auto* dict = dynamic_cast<const DictionaryColumn<std::string>*>(&column);
+  Assert(dict != nullptr, "LIKE operator only applicable on string columns.");
+  Assert(!variant_is_null(value), "Right value must not be NULL.");
+  const LikePattern matcher(type_cast<std::string>(value));
+  const bool invert = cond == PredicateCondition::NotLike;
+  const auto& d = dict->dictionary();
+  std::vector<uint32_t> bits((d.size() + 31) / 32 + 1, 0u);
+  size_t count = 0;
+  for (size_t v = 0; v < d.size(); ++v) {
+    if (matcher(d[v]) != invert) {
+      bits[v >> 5] |= 1u << (v & 31);
+      ++count;
+    }
+  }
+  if (count == d.size()) {
+    sc->op = HY_OP_ALL;
+    return;
+  }
+  if (count == 0) {
+    sc->op = HY_OP_NONE;
+    return;
+  }
+  sc->op = HY_OP_VID_SET;
+  auto buf = std::make_shared<DeviceBuffer>(bits.size() * 4);
+  hy_stream_t s = operator_stream();
+  hy_check(hy_memcpy_htod(buf->get(), bits.data(), bits.size() * 4, s), "htod");
+  hy_check(hy_stream_synchronize(s), "sync");  // `bits` is pageable host memory
+  sc->vid_set = buf->as<uint32_t>();
+  keep->push_back(std::move(buf));
+}
+
 // Builds the scan descriptor of one data column chunk. constant_out receives type_cast<T>(value) for value columns.
+// keep: device buffers the descriptor points to (LIKE id sets), alive until the scan has run.
 hy_scan_chunk scan_descriptor(const BaseColumn& column, DataType type, PredicateCondition cond,
-                              const AllTypeVariant& value) {
+                              const AllTypeVariant& value, std::vector<std::shared_ptr<DeviceBuffer>>* keep) {
   hy_scan_chunk sc{};
-  if (cond == PredicateCondition::IsNull || cond == PredicateCondition::IsNotNull) {
+  if (cond == PredicateCondition::Like || cond == PredicateCondition::NotLike) {
+    const auto* dict = dynamic_cast<const BaseDictionaryColumn*>(&column);
+    Assert(type == DataType::String, "LIKE operator only applicable on string columns.");
+    Assert(dict != nullptr,
+           "hyrise-amd: LIKE on an unencoded string column is not supported by the device path (encode the column)");
+    like_predicate(*dict, cond, value, &sc, keep);
+  } else if (cond == PredicateCondition::IsNull || cond == PredicateCondition::IsNotNull) {
     // IsNullTableScanImpl (is_null_table_scan_impl.cpp:35-117): no dictionary rewrite, the null test is per row
     Assert(type != DataType::String || dynamic_cast<const BaseDictionaryColumn*>(&column) != nullptr,
            "hyrise-amd: TableScan on an unencoded string column is not supported by the device path");
@@ -206,8 +340,6 @@ const std::string TableScan::description() const {
 std::shared_ptr<const Table> TableScan::_on_execute() {
   const auto in_table = input_table_left();
   switch (_predicate_condition) {
-    case PredicateCondition::Like:
-    case PredicateCondition::NotLike:
     case PredicateCondition::In:
       Fail("hyrise-amd: predicate " + predicate_condition_to_string(_predicate_condition) +
            " is not supported by the device TableScan");
@@ -226,7 +358,13 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
     _performance_data.rows_in = in_table->row_count();
     return column_comparison_scan(in_table, _left_column_id, _predicate_condition, _right_column_id, excluded);
   }
+  if (_predicate_condition == PredicateCondition::Like || _predicate_condition == PredicateCondition::NotLike)
+    Assert(in_table->column_data_type(_left_column_id) == DataType::String,
+           "LIKE operator only applicable on string columns.");  // table_scan.cpp:170-171
   auto output = std::make_shared<Table>(in_table->column_definitions(), TableType::References);
+  std::vector<std::shared_ptr<DeviceBuffer>> keep;  // LIKE id sets of the descriptors
+  const bool like = _predicate_condition == PredicateCondition::Like ||
+                    _predicate_condition == PredicateCondition::NotLike;
   const bool null_test =
       _predicate_condition == PredicateCondition::IsNull || _predicate_condition == PredicateCondition::IsNotNull;
   // reference single_column_table_scan_impl.cpp:23-36: comparing with NULL matches nothing (IS [NOT] NULL ignores the
@@ -249,7 +387,7 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
     for (ChunkID c = 0; c < in_table->chunk_count(); ++c) {
       if (excluded[c]) continue;
       const auto column = in_table->get_chunk(c)->get_column(_left_column_id);
-      auto d = scan_descriptor(*column, col_type, _predicate_condition, _right_value);
+      auto d = scan_descriptor(*column, col_type, _predicate_condition, _right_value, &keep);
       d.out_begin = total;
       total += column->size();
       descs.push_back(d);
@@ -257,7 +395,7 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
       sizes.push_back(static_cast<uint32_t>(column->size()));
     }
     if (descs.empty()) return output;
-    const auto constant = null_test ? ScanConstant{} : typed_constant(col_type, _right_value);
+    const auto constant = null_test || like ? ScanConstant{} : typed_constant(col_type, _right_value);
     size_t ws_bytes = 0;
     hy_check(hy_table_scan_workspace_size(sizes.data(), static_cast<uint32_t>(sizes.size()), &ws_bytes),
              "hy_table_scan_workspace_size");
@@ -302,8 +440,9 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
     const ColumnID rcol = ref->referenced_column_id();
     std::vector<hy_scan_chunk> rdesc(rtable->chunk_count());
     for (ChunkID r = 0; r < rtable->chunk_count(); ++r)
-      rdesc[r] = scan_descriptor(*rtable->get_chunk(r)->get_column(rcol), col_type, _predicate_condition, _right_value);
-    const auto constant = null_test ? ScanConstant{} : typed_constant(col_type, _right_value);
+      rdesc[r] = scan_descriptor(*rtable->get_chunk(r)->get_column(rcol), col_type, _predicate_condition, _right_value,
+                                 &keep);
+    const auto constant = null_test || like ? ScanConstant{} : typed_constant(col_type, _right_value);
     const auto dpl = device_pos_list(pos_list);
     const uint64_t m = pos_list.size();
 

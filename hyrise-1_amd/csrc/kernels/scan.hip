@@ -74,6 +74,16 @@ __device__ __forceinline__ uint32_t match_mask(const hy_scan_chunk& ch, uint32_t
       for (int i = 0; i < 16; ++i) mask |= static_cast<uint32_t>(v[i] == null_vid) << i;
       return mask & valid;
     }
+    if (op == HY_OP_VID_SET) {  // like_table_scan_impl.cpp:62-83: dictionary_matches[vid], NULL rows skipped
+      const uint32_t* __restrict__ set = ch.vid_set;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const uint32_t vid = static_cast<uint32_t>(v[i]);
+        const bool m = v[i] != null_vid && ((set[vid >> 5] >> (vid & 31)) & 1u);
+        mask |= static_cast<uint32_t>(m) << i;
+      }
+      return mask & valid;
+    }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const bool m = (v[i] != null_vid) && cmp_op<E>(op, v[i], s);
@@ -225,6 +235,7 @@ __device__ __forceinline__ bool ref_match(const hy_scan_chunk& ch, uint32_t off,
       vid = reinterpret_cast<const uint32_t*>(ch.column.data)[off];
     if (ch.op == HY_OP_IS_NULL) return vid == ch.column.dictionary_size;
     if (vid == ch.column.dictionary_size) return false;
+    if (ch.op == HY_OP_VID_SET) return (ch.vid_set[vid >> 5] >> (vid & 31)) & 1u;
     return cmp_op<uint32_t>(ch.op, vid, ch.search_vid);
   }
   const bool is_null = ch.column.nulls != nullptr && ch.column.nulls[off];

@@ -144,7 +144,12 @@ enum {
    * Supported by hy_table_scan / hy_table_scan_row_ids / hy_reference_scan; the fused scan filters of
    * hy_scan_join_hash and hy_aggregate reject HY_OP_IS_NULL with HY_ERR_UNSUPPORTED. */
   HY_OP_IS_NULL = 8,
-  HY_OP_IS_NOT_NULL = 9 /* every non-NULL row (same rows as HY_OP_ALL) */
+  HY_OP_IS_NOT_NULL = 9, /* every non-NULL row (same rows as HY_OP_ALL) */
+  /* DICT chunks only: rows whose value id v is set in vid_set (bit v % 32 of word v / 32). LIKE / NOT LIKE: the host
+   * evaluates the pattern once per dictionary entry (LikeTableScanImpl::_find_matches_in_dictionary,
+   * like_table_scan_impl.cpp:48-83, 102-120) and the device scans the attribute vector against that set. Scans only
+   * (the fused filters of hy_scan_join_hash / hy_aggregate reject it). */
+  HY_OP_VID_SET = 10
 };
 
 typedef struct hy_scan_chunk {
@@ -152,6 +157,7 @@ typedef struct hy_scan_chunk {
   int32_t op;            /* HY_OP_*; for DICT chunks compared against search_vid */
   uint32_t search_vid;   /* DICT: search value id (host-computed, reference _get_search_value_id) */
   uint64_t out_begin;    /* first output slot of this chunk (capacity = column.size) */
+  const uint32_t* vid_set; /* HY_OP_VID_SET: device bitmap over the chunk's value ids, else unused (NULL) */
 } hy_scan_chunk;
 
 /* Workspace bytes for a scan over chunks with the given sizes. */

@@ -20,6 +20,7 @@
 #include <functional>
 #include <map>
 #include <optional>
+#include <regex>
 #include <set>
 #include <thread>
 #include <unordered_map>
@@ -194,8 +195,136 @@ void with_comparator(PredicateCondition c, F&& f) {  // reference type_compariso
 // ---------------------------------------------------------------------------------------------------------------
 using Mapped = std::vector<std::pair<ChunkOffset, ChunkOffset>>;
 
+// LikeMatcher (src/lib/expression/evaluation/like_matcher.cpp:9-118): tokens of literal runs and the wildcards
+// '%' (AnyChars) / '_' (SingleChar); StartsWith / EndsWith / Contains / MultipleContains patterns are string searches,
+// everything else the regex sql_like_to_regex builds (its fixed replacement list, applied in order).
+struct OracleLike {
+  int kind = 4;  // 0 starts, 1 ends, 2 contains, 3 multiple contains, 4 regex
+  std::vector<std::string> strings;
+  std::regex re;
+
+  explicit OracleLike(const std::string& pattern) {
+    std::vector<std::string> tok;  // "\x01" = AnyChars, "\x02" = SingleChar, else literal
+    for (size_t p = 0; p < pattern.size();) {
+      if (pattern[p] == '%' || pattern[p] == '_') {
+        tok.push_back(pattern[p] == '%' ? "\x01" : "\x02");
+        ++p;
+      } else {
+        const auto q = std::min(pattern.find_first_of("_%", p), pattern.size());
+        tok.push_back(pattern.substr(p, q - p));
+        p = q;
+      }
+    }
+    auto is_any = [](const std::string& t) { return t == "\x01"; };
+    auto is_str = [](const std::string& t) { return t != "\x01" && t != "\x02"; };
+    if (tok.size() == 2 && is_str(tok[0]) && is_any(tok[1])) {
+      kind = 0;
+      strings = {tok[0]};
+      return;
+    }
+    if (tok.size() == 2 && is_any(tok[0]) && is_str(tok[1])) {
+      kind = 1;
+      strings = {tok[1]};
+      return;
+    }
+    if (tok.size() == 3 && is_any(tok[0]) && is_str(tok[1]) && is_any(tok[2])) {
+      kind = 2;
+      strings = {tok[1]};
+      return;
+    }
+    bool ok = true, want_any = true;
+    std::vector<std::string> parts;
+    for (const auto& t : tok) {
+      if (want_any ? !is_any(t) : !is_str(t)) {
+        ok = false;
+        break;
+      }
+      if (!want_any) parts.push_back(t);
+      want_any = !want_any;
+    }
+    if (ok) {
+      kind = 3;
+      strings = parts;
+      return;
+    }
+    std::string r = pattern;
+    const std::pair<std::string, std::string> repl[] = {{"\\", "\\\\"}, {".", "\\."}, {"^", "\\^"}, {"$", "\\$"},
+                                                        {"+", "\\+"},   {"?", "\\?"}, {"(", "\\("}, {")", "\\)"},
+                                                        {"{", "\\{"},   {"}", "\\}"}, {"|", "\\|"}, {"*", "\\*"},
+                                                        {"%", ".*"},    {"_", "."}};
+    for (const auto& [from, to] : repl) {
+      for (size_t at = r.find(from); at != std::string::npos; at = r.find(from, at + to.size())) r.replace(at, from.size(), to);
+    }
+    re = std::regex("^" + r + "$");
+  }
+
+  bool operator()(const std::string& v) const {
+    switch (kind) {
+      case 0:
+        return v.rfind(strings[0], 0) == 0;
+      case 1:
+        return v.size() >= strings[0].size() && v.substr(v.size() - strings[0].size()) == strings[0];
+      case 2:
+        return v.find(strings[0]) != std::string::npos;
+      case 3: {
+        size_t pos = 0;
+        for (const auto& p : strings) {
+          pos = v.find(p, pos);
+          if (pos == std::string::npos) return false;
+          pos += p.size();
+        }
+        return true;
+      }
+      default:
+        return std::regex_match(v, re);
+    }
+  }
+};
+
+// LikeTableScanImpl (like_table_scan_impl.cpp:20-120): value columns row by row; dictionary columns through the
+// per-entry match vector with the all / none early-outs. NULL rows never match (_unary_scan), NOT LIKE inverts.
+void like_scan_column(const BaseColumn& col, PredicateCondition cond, const AllTypeVariant& value, ChunkID chunk_id,
+                      const Mapped* mapped, PosList& out) {
+  const OracleLike matcher(type_cast<std::string>(value));
+  const bool invert = cond == PredicateCondition::NotLike;
+  auto each = [&](auto&& one) {
+    if (mapped)
+      for (const auto& [a, b] : *mapped) one(a, b);
+    else
+      for (ChunkOffset o = 0; o < col.size(); ++o) one(o, o);
+  };
+  if (const auto* dc = dynamic_cast<const DictionaryColumn<std::string>*>(&col)) {
+    std::vector<bool> dm;
+    size_t count = 0;
+    for (const auto& entry : dc->dictionary()) {
+      dm.push_back(matcher(entry) != invert);
+      count += dm.back();
+    }
+    if (count == 0) return;
+    const bool all = count == dm.size();
+    const auto& av = dc->attribute_vector();
+    each([&](ChunkOffset into, ChunkOffset o) {
+      const ValueID vid = av.get(o);
+      if (vid == dc->null_value_id()) return;
+      if (all || dm[vid]) out.emplace_back(chunk_id, into);
+    });
+    return;
+  }
+  const auto* vc = dynamic_cast<const ValueColumn<std::string>*>(&col);
+  Assert(vc != nullptr, "LIKE operator only applicable on string columns.");
+  each([&](ChunkOffset into, ChunkOffset o) {
+    if (vc->is_null(o)) return;
+    if (matcher(vc->values()[o]) != invert) out.emplace_back(chunk_id, into);
+  });
+}
+
 void scan_data_column(const BaseColumn& col, DataType type, PredicateCondition cond, const AllTypeVariant& value,
                       ChunkID chunk_id, const Mapped* mapped, PosList& out) {
+  if (cond == PredicateCondition::Like || cond == PredicateCondition::NotLike) {
+    Assert(type == DataType::String, "LIKE operator only applicable on string columns.");
+    like_scan_column(col, cond, value, chunk_id, mapped, out);
+    return;
+  }
   if (cond == PredicateCondition::IsNull || cond == PredicateCondition::IsNotNull) {
     // IsNullTableScanImpl (is_null_table_scan_impl.cpp:35-117 and is_null_table_scan_impl.hpp:45-75): a row matches
     // iff its is_null() equals the predicate; the value-column all/none early-outs select the same rows

@@ -154,6 +154,39 @@ def column_compare_tables(hy):
     return out
 
 
+# table_scan_string_test.cpp:100-330: (predicate, pattern, expected .tbl or a row count) on int_string_like.tbl
+LIKE_CASES = [
+    ("Like", "%", "int_string_like.tbl"),
+    ("Like", "%D%_m_f%", "int_string_like_starting.tbl"),
+    ("Like", "Dampf%", "int_string_like_starting.tbl"),
+    ("Like", "%gesellschaft", "int_string_like_ending.tbl"),
+    ("Like", "Schiff%schaft", "int_string_like_containing_wildcard.tbl"),
+    ("Like", "%schifffahrtsgesellschaft%", "int_string_like_containing.tbl"),
+    ("Like", "%not_there%", 0),
+    ("NotLike", "%", 0),
+    ("NotLike", "%foo%", "int_string_like.tbl"),
+    ("NotLike", "D_m_f%", "int_string_like_not_starting.tbl"),
+]
+# ScanLikeOnSpecialChars (:189-213) on int_string_like_special_chars.tbl
+LIKE_SPECIAL_CASES = [
+    ("%2^2%", "int_string_like_special_chars_1.tbl"),
+    ("%$%$%", "int_string_like_special_chars_1.tbl"),
+    ("%(%)%", "int_string_like_special_chars_2.tbl"),
+    ("%la\\.^$+?)({}.*__bl%", "int_string_like_special_chars_3.tbl"),
+]
+
+
+def like_tables(hy, encodings=(None, "Dictionary")):
+    """_gt_string (chunk 2, unencoded) and _gt_string_compressed (chunk 5, encoded), as tables."""
+    out = []
+    for enc in encodings:
+        t = hy.load_table(tbl("int_string_like.tbl"), 5 if enc else 2)
+        if enc:
+            hy.encode_all_chunks(t, getattr(hy.EncodingType, enc))
+        out.append((enc, t))
+    return out
+
+
 def multiset(values):
     return sorted(values, key=lambda v: (v is None, 0 if v is None else v))
 

@@ -121,3 +121,27 @@ def test_column_comparison_mixed_types(hy, oracle):
     eq = oracle.table_scan(t, 0, hy.PredicateCondition.Equals, None, [], right_column_id=1)
     assert sc.column_values(gt, 0) == [1]
     assert sc.column_values(eq, 0) == [2, 16777217]  # 16777217 -> 16777216.0f
+
+
+def _like_expect(hy, out, expected):
+    if isinstance(expected, int):
+        assert out.row_count() == expected
+    else:
+        assert_table_eq_unordered(out, hy.load_table(tbl(expected), 1))
+
+
+def test_like(hy, oracle):
+    """LIKE / NOT LIKE pinned to table_scan_string_test.cpp (unencoded, dictionary, referenced dictionary)."""
+    for enc, t in sc.like_tables(hy):
+        for cond, pattern, expected in sc.LIKE_CASES:
+            out = oracle.table_scan(t, 1, getattr(hy.PredicateCondition, cond), pattern, [])
+            _like_expect(hy, out, expected)
+            s1 = oracle.table_scan(t, 0, hy.PredicateCondition.GreaterThan, 0, [])
+            _like_expect(hy, oracle.table_scan(s1, 1, getattr(hy.PredicateCondition, cond), pattern, []), expected)
+    special = hy.load_table(tbl("int_string_like_special_chars.tbl"), 2)
+    for pattern, expected in sc.LIKE_SPECIAL_CASES:
+        _like_expect(hy, oracle.table_scan(special, 1, hy.PredicateCondition.Like, pattern, []), expected)
+    t = hy.load_table(tbl("int_string_like.tbl"), 2)
+    assert oracle.table_scan(t, 1, hy.PredicateCondition.Like, 1234, []).row_count() == 1  # ScanLikeNonStringValue
+    with pytest.raises(RuntimeError):  # ScanLikeNonStringColumn
+        oracle.table_scan(hy.load_table(tbl("int_float.tbl"), 2), 0, hy.PredicateCondition.Like, "%test", [])

@@ -219,3 +219,38 @@ def test_column_comparison_synthetic(hy, oracle, types):
     ref.append_chunk([hy.ReferenceColumn(t, 0, pl), hy.ReferenceColumn(t, 1, pl)])
     for cond in ("Equals", "LessThan", "GreaterThan"):
         check_cmp(hy, oracle, wrap(hy, ref), 0, cond, 1)
+
+
+def test_like_dictionary(hy, oracle):
+    """LIKE / NOT LIKE over dictionary-encoded string columns (table_scan_string_test.cpp *OnDict* and
+    *OnReferencedDict* cases + the special-character patterns), bit-exact against the oracle."""
+    for enc, t in sc.like_tables(hy, encodings=("Dictionary",)):
+        w = wrap(hy, t)
+        for cond, pattern, _ in sc.LIKE_CASES:
+            check(hy, oracle, w, 1, cond, pattern)
+            s1 = check(hy, oracle, w, 0, "GreaterThan", 0)
+            check(hy, oracle, s1, 1, cond, pattern)
+    special = hy.load_table(tbl("int_string_like_special_chars.tbl"), 2)
+    hy.encode_all_chunks(special, hy.EncodingType.Dictionary)
+    for pattern, expected in sc.LIKE_SPECIAL_CASES:
+        s = check(hy, oracle, wrap(hy, special), 1, "Like", pattern)
+        assert_table_eq_unordered(s.get_output(), hy.load_table(tbl(expected), 1))
+    with pytest.raises(RuntimeError):  # LIKE on a non-string column
+        device_scan(hy, wrap(hy, hy.load_table(tbl("int_float.tbl"), 2)), 0, "Like", "%test")
+
+
+def test_like_synthetic(hy, oracle):
+    """Many dictionaries (u8 / u16 id widths), NULLs, every pattern shape incl. the regex fallback."""
+    rng = np.random.default_rng(0x4C494B45)
+    words = ["".join(rng.choice(list("abcXYZ_%.("), rng.integers(0, 9))) for _ in range(700)]
+    n = 40_000
+    t = hy.Table([("a", hy.DataType.Int, False), ("s", hy.DataType.String, True)], hy.TableType.Data, 7_001)
+    for i in range(n):
+        t.append([i, None if rng.random() < 0.03 else words[rng.integers(0, 700 if i < 20_000 else 60)]])
+    hy.encode_all_chunks(t, hy.EncodingType.Dictionary)
+    w = wrap(hy, t)
+    for pattern in ("a%", "%Z", "%bc%", "%a%X%", "a_c%", "_", "%(%", "%.%", "X%a%c", "%", "abcabcabcabc%"):
+        for cond in ("Like", "NotLike"):
+            check(hy, oracle, w, 1, cond, pattern)
+    s1 = check(hy, oracle, w, 0, "GreaterThanEquals", 15_000)
+    check(hy, oracle, s1, 1, "Like", "%b%")
