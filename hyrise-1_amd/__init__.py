@@ -50,6 +50,8 @@ AbstractOperator = _host.AbstractOperator
 TableWrapper = _host.TableWrapper
 TableScan = _host.TableScan
 ColumnParameter = _host.ColumnParameter
+Validate = _host.Validate
+MAX_COMMIT_ID = _host.MAX_COMMIT_ID
 JoinHash = _host.JoinHash
 Aggregate = _host.Aggregate
 AggregateColumnDefinition = _host.AggregateColumnDefinition

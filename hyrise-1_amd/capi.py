@@ -217,6 +217,13 @@ _sigs = {
     "hy_column_compare_scan": (ctypes.c_int, [ctypes.POINTER(JoinSide), ctypes.POINTER(JoinSide), ctypes.c_int32,
                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                               ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "hy_validate_workspace_size": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, ctypes.POINTER(ctypes.c_size_t)]),
+    "hy_validate": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                   ctypes.c_void_p]),
+    "hy_validate_pos_list": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32,
+                                            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
     "hy_pos_list_null_positions": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
                                                   ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
 }

@@ -217,6 +217,21 @@ PYBIND11_MODULE(_hyrise_host, m) {
            [](const ReferenceColumn& c) { return reinterpret_cast<uintptr_t>(c.referenced_table().get()); });
 
   py::class_<Chunk, std::shared_ptr<Chunk>>(m, "Chunk")
+      .def("set_mvcc_columns",
+           [](Chunk& c, py::array_t<uint32_t> tids, py::array_t<uint32_t> begin, py::array_t<uint32_t> end) {
+             auto m = std::make_shared<MvccColumns>();
+             auto copy = [](py::array_t<uint32_t>& a, std::vector<uint32_t>& v) {
+               auto r = a.unchecked<1>();
+               v.resize(r.shape(0));
+               for (py::ssize_t i = 0; i < r.shape(0); ++i) v[i] = r(i);
+             };
+             copy(tids, m->tids);
+             copy(begin, m->begin_cids);
+             copy(end, m->end_cids);
+             c.set_mvcc_columns(m);
+           },
+           py::arg("tids"), py::arg("begin_cids"), py::arg("end_cids"))
+      .def("has_mvcc_columns", &Chunk::has_mvcc_columns)
       .def("size", &Chunk::size)
       .def("column_count", &Chunk::column_count)
       .def("get_column", &Chunk::get_column);
@@ -302,6 +317,10 @@ PYBIND11_MODULE(_hyrise_host, m) {
            py::arg("input"), py::arg("column_id"), py::arg("predicate_condition"), py::arg("value"))
       .def("set_excluded_chunk_ids", &TableScan::set_excluded_chunk_ids);
 
+  py::class_<Validate, AbstractOperator, std::shared_ptr<Validate>>(m, "Validate")
+      .def(py::init<std::shared_ptr<AbstractOperator>, uint32_t, uint32_t>(), py::arg("input"),
+           py::arg("transaction_id"), py::arg("snapshot_commit_id"));
+  m.attr("MAX_COMMIT_ID") = MvccColumns::MAX_COMMIT_ID;
   py::class_<JoinHash, AbstractOperator, std::shared_ptr<JoinHash>>(m, "JoinHash")
       .def(py::init([](std::shared_ptr<AbstractOperator> l, std::shared_ptr<AbstractOperator> r, JoinMode mode,
                        std::pair<ColumnID, ColumnID> cols, PredicateCondition cond, size_t radix_bits) {

@@ -5,6 +5,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <numeric>
 #include <regex>
 #include <unordered_map>
@@ -523,6 +524,120 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
         f->set_single_chunk_id(rc->pos_list()->single_chunk_id());  // a filtered PosList stays within its chunk
       }
       cols.push_back(std::make_shared<ReferenceColumn>(rc->referenced_table(), rc->referenced_column_id(), f));
+    }
+    output->append_chunk(cols);
+  }
+  return output;
+}
+
+// ================================================================================================================
+// Validate
+// ================================================================================================================
+namespace {
+
+// The MVCC vectors of a table's chunks, concatenated into three device arrays; descriptors point into them.
+struct DeviceMvcc {
+  std::vector<hy_mvcc_chunk> chunks;
+  std::vector<std::shared_ptr<DeviceBuffer>> keep;
+};
+
+DeviceMvcc upload_mvcc(const Table& table, hy_stream_t s) {
+  DeviceMvcc out;
+  uint64_t rows = 0;
+  for (ChunkID c = 0; c < table.chunk_count(); ++c) {
+    const auto m = table.get_chunk(c)->mvcc_columns();
+    Assert(m != nullptr, "Trying to use Validate on a table that has no MVCC columns");
+    rows += m->tids.size();
+  }
+  std::vector<uint32_t> all(3 * std::max<uint64_t>(rows, 1));
+  auto buf = std::make_shared<DeviceBuffer>(all.size() * 4);
+  uint64_t at = 0;
+  for (ChunkID c = 0; c < table.chunk_count(); ++c) {
+    const auto m = table.get_chunk(c)->mvcc_columns();
+    const uint64_t n = m->tids.size();
+    Assert(m->begin_cids.size() == n && m->end_cids.size() == n, "MVCC columns of different lengths");
+    std::copy(m->tids.begin(), m->tids.end(), all.begin() + at);
+    std::copy(m->begin_cids.begin(), m->begin_cids.end(), all.begin() + rows + at);
+    std::copy(m->end_cids.begin(), m->end_cids.end(), all.begin() + 2 * rows + at);
+    const uint32_t* base = buf->as<uint32_t>();
+    out.chunks.push_back(hy_mvcc_chunk{base + at, base + rows + at, base + 2 * rows + at, static_cast<uint32_t>(n), 0});
+    at += n;
+  }
+  hy_check(hy_memcpy_htod(buf->get(), all.data(), all.size() * 4, s), "htod");
+  hy_check(hy_stream_synchronize(s), "sync");  // `all` is pageable
+  out.keep.push_back(std::move(buf));
+  return out;
+}
+
+}  // namespace
+
+std::shared_ptr<const Table> Validate::_on_execute() {
+  const auto in_table = input_table_left();
+  auto output = std::make_shared<Table>(in_table->column_definitions(), TableType::References);
+  if (in_table->chunk_count() == 0) return output;
+  require_device();
+  hy_stream_t s = operator_stream();
+  _performance_data.rows_in = in_table->row_count();
+  if (in_table->type() == TableType::Data) {
+    const auto mvcc = upload_mvcc(*in_table, s);
+    std::vector<uint32_t> ids(in_table->chunk_count());
+    std::iota(ids.begin(), ids.end(), 0u);
+    const uint64_t rows = in_table->row_count();
+    size_t ws_bytes = 0;
+    hy_check(hy_validate_workspace_size(rows, in_table->chunk_count(), &ws_bytes), "hy_validate_workspace_size");
+    DeviceBuffer ws(ws_bytes, s), counts(in_table->chunk_count() * 4, s), n_out(8, s);
+    auto out_rows = std::make_shared<DeviceBuffer>(std::max<uint64_t>(rows, 1) * sizeof(RowID));
+    hy_check(hy_validate(mvcc.chunks.data(), in_table->chunk_count(), ids.data(), _transaction_id, _snapshot_commit_id,
+                         out_rows->as<hy_row_id>(), counts.as<uint32_t>(), n_out.as<uint64_t>(), ws.get(), ws_bytes, s),
+             "hy_validate");
+    std::vector<uint32_t> h_counts(in_table->chunk_count());
+    hy_check(hy_memcpy_dtoh(h_counts.data(), counts.get(), 4 * h_counts.size(), s), "dtoh");
+    hy_check(hy_stream_synchronize(s), "sync");
+    uint64_t begin = 0;
+    for (ChunkID c = 0; c < in_table->chunk_count(); ++c) {
+      if (h_counts[c] == 0) continue;  // validate.cpp:89-91: no empty output chunks
+      auto pl = pos_list_from_device(out_rows, begin, h_counts[c]);
+      pl->set_single_chunk_id(c);
+      ChunkColumns cols;
+      for (ColumnID col = 0; col < in_table->column_count(); ++col)
+        cols.push_back(std::make_shared<ReferenceColumn>(in_table, col, pl));
+      output->append_chunk(cols);
+      begin += h_counts[c];
+    }
+    return output;
+  }
+  // reference input (validate.cpp:47-70): column 0's PosList, checked against the referenced table's MVCC columns,
+  // becomes the PosList of every output column of the chunk
+  std::map<const Table*, DeviceMvcc> uploaded;
+  for (ChunkID c = 0; c < in_table->chunk_count(); ++c) {
+    const auto chunk = in_table->get_chunk(c);
+    const auto ref0 = std::dynamic_pointer_cast<const ReferenceColumn>(chunk->get_column(0));
+    Assert(ref0 != nullptr, "All columns should be of type ReferenceColumn.");
+    const auto& referenced = ref0->referenced_table();
+    auto it = uploaded.find(referenced.get());
+    if (it == uploaded.end()) it = uploaded.emplace(referenced.get(), upload_mvcc(*referenced, s)).first;
+    const auto& pos_list = *ref0->pos_list();
+    const uint64_t n = pos_list.size();
+    if (n == 0) continue;
+    const auto dpl = device_pos_list(pos_list);
+    size_t ws_bytes = 0;
+    hy_check(hy_validate_workspace_size(n, referenced->chunk_count(), &ws_bytes), "hy_validate_workspace_size");
+    DeviceBuffer ws(ws_bytes, s), n_out(8, s);
+    auto out_rows = std::make_shared<DeviceBuffer>(n * sizeof(RowID));
+    hy_check(hy_validate_pos_list(dpl->ptr(), n, it->second.chunks.data(), referenced->chunk_count(), _transaction_id,
+                                  _snapshot_commit_id, out_rows->as<hy_row_id>(), n_out.as<uint64_t>(), ws.get(),
+                                  ws_bytes, s),
+             "hy_validate_pos_list");
+    uint64_t visible = 0;
+    hy_check(hy_memcpy_dtoh(&visible, n_out.get(), 8, s), "dtoh");
+    hy_check(hy_stream_synchronize(s), "sync");
+    if (visible == 0) continue;
+    auto pl = pos_list_from_device(out_rows, 0, visible);
+    pl->set_single_chunk_id(ref0->pos_list()->single_chunk_id());
+    ChunkColumns cols;
+    for (ColumnID col = 0; col < in_table->column_count(); ++col) {
+      const auto rc = std::static_pointer_cast<const ReferenceColumn>(chunk->get_column(col));
+      cols.push_back(std::make_shared<ReferenceColumn>(referenced, rc->referenced_column_id(), pl));
     }
     output->append_chunk(cols);
   }

@@ -25,7 +25,7 @@
 
 namespace hyrise {
 
-enum class OperatorType { TableWrapper, TableScan, JoinHash, Aggregate, Projection, Mock };
+enum class OperatorType { TableWrapper, TableScan, JoinHash, Aggregate, Projection, Validate, Mock };
 
 struct OperatorPerformanceData {
   uint64_t walltime_ns = 0;  // reference operator_performance_data.hpp:15
@@ -112,6 +112,24 @@ class TableScan final : public AbstractOperator {
   AllTypeVariant _right_value;
   ColumnID _right_column_id = INVALID_COLUMN_ID;
   std::vector<ChunkID> _excluded_chunk_ids;
+};
+
+// Validate (reference operators/validate.cpp:36-95): the input rows visible to one transaction. The reference's
+// TransactionContext enters as its two fields, the transaction id and the snapshot commit id.
+class Validate final : public AbstractOperator {
+ public:
+  Validate(std::shared_ptr<const AbstractOperator> in, uint32_t transaction_id, uint32_t snapshot_commit_id)
+      : AbstractOperator(OperatorType::Validate, std::move(in)),
+        _transaction_id(transaction_id),
+        _snapshot_commit_id(snapshot_commit_id) {}
+  const std::string name() const override { return "Validate"; }
+
+ protected:
+  std::shared_ptr<const Table> _on_execute() override;
+
+ private:
+  uint32_t _transaction_id;
+  uint32_t _snapshot_commit_id;
 };
 
 class JoinHash final : public AbstractOperator {

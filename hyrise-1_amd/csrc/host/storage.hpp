@@ -12,6 +12,7 @@
 // Every column can carry a device-resident mirror (device.hpp) that GPU operators create on first use.
 #pragma once
 
+#include <limits>
 #include <algorithm>
 #include <memory>
 #include <mutex>
@@ -236,9 +237,19 @@ class ReferenceColumn final : public BaseColumn {
 
 using ChunkColumns = std::vector<std::shared_ptr<BaseColumn>>;
 
+// MVCC columns of a data chunk (reference storage/mvcc_columns.hpp:15-45): per row the id of the transaction holding
+// its lock (0 if none), the commit id of its insert and of its delete.
+struct MvccColumns {
+  static constexpr uint32_t MAX_COMMIT_ID = std::numeric_limits<uint32_t>::max() - 1;
+  std::vector<uint32_t> tids, begin_cids, end_cids;
+};
+
 class Chunk {
  public:
   explicit Chunk(ChunkColumns columns) : _columns(std::move(columns)) {}
+  bool has_mvcc_columns() const { return _mvcc != nullptr; }
+  std::shared_ptr<const MvccColumns> mvcc_columns() const { return _mvcc; }
+  void set_mvcc_columns(std::shared_ptr<const MvccColumns> m) { _mvcc = std::move(m); }
   size_t size() const { return _columns.empty() ? 0 : _columns[0]->size(); }
   uint16_t column_count() const { return static_cast<uint16_t>(_columns.size()); }
   std::shared_ptr<BaseColumn> get_column(ColumnID id) const { return _columns.at(id); }
@@ -249,6 +260,7 @@ class Chunk {
 
  private:
   ChunkColumns _columns;
+  std::shared_ptr<const MvccColumns> _mvcc;
 };
 
 struct TableColumnDefinition {

@@ -238,6 +238,36 @@ hy_status hy_expand_row_ids(uint32_t chunk_id, const uint32_t* offsets, uint64_t
                             hy_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------------------------
+ * Validate (MVCC visibility, reference src/lib/operators/validate.cpp:14-95)
+ *
+ * Row r of a chunk with MVCC columns is visible to transaction our_tid under snapshot_commit_id iff
+ *   snapshot_commit_id < end_cids[r] && ((snapshot_commit_id >= begin_cids[r]) != (tids[r] == our_tid)).
+ * ------------------------------------------------------------------------------------------------------------- */
+typedef struct hy_mvcc_chunk {
+  const uint32_t* tids;        /* device: TransactionID per row (0 unless locked), reference mvcc_columns.hpp:22 */
+  const uint32_t* begin_cids;  /* device: CommitID of the insert */
+  const uint32_t* end_cids;    /* device: CommitID of the delete (MAX_COMMIT_ID = 2^32-2 if none) */
+  uint32_t size;               /* rows */
+  uint32_t reserved;
+} hy_mvcc_chunk;
+
+/* n_rows: total rows of the chunks (hy_validate) or the PosList length (hy_validate_pos_list); n_chunks: chunks /
+ * referenced chunks. */
+hy_status hy_validate_workspace_size(uint64_t n_rows, uint32_t n_chunks, size_t* bytes);
+/* Data-table input: visible rows as RowIDs {chunk_ids[c], offset}, chunk-major, offsets ascending, at out_rows;
+ * counts[c] (device) per chunk, *n_out (device) in total. chunks / chunk_ids: HOST arrays. */
+hy_status hy_validate(const hy_mvcc_chunk* chunks, uint32_t n_chunks, const uint32_t* chunk_ids, uint32_t our_tid,
+                      uint32_t snapshot_commit_id, hy_row_id* out_rows, uint32_t* counts, uint64_t* n_out,
+                      void* workspace, size_t workspace_bytes, hy_stream_t stream);
+/* Reference input: the RowIDs of pos_list (into the referenced table, whose chunks' MVCC columns are
+ * referenced_chunks, HOST array indexed by chunk id) that are visible, in PosList order, at out_rows. NULL RowIDs are
+ * dropped. */
+hy_status hy_validate_pos_list(const hy_row_id* pos_list, uint64_t pos_list_size,
+                               const hy_mvcc_chunk* referenced_chunks, uint32_t n_referenced, uint32_t our_tid,
+                               uint32_t snapshot_commit_id, hy_row_id* out_rows, uint64_t* n_out, void* workspace,
+                               size_t workspace_bytes, hy_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------------------------
  * Hashing (reference src/lib/utils/murmur_hash.cpp:21-75, seed 17 from join_hash.cpp:680)
  * ------------------------------------------------------------------------------------------------------------- */
 /* out[i] = murmur_hash2(&keys[i], key_bytes, seed); key_bytes 4 or 8. */

@@ -531,6 +531,45 @@ std::shared_ptr<Table> table_scan(const std::shared_ptr<const Table>& in, Column
 }
 
 // ---------------------------------------------------------------------------------------------------------------
+// Validate: reference validate.cpp:14-95 (is_row_visible and the data / reference input branches)
+// ---------------------------------------------------------------------------------------------------------------
+bool is_row_visible(uint32_t our_tid, uint32_t snapshot, ChunkOffset o, const MvccColumns& m) {
+  const bool own_insert = m.tids[o] == our_tid && !(snapshot >= m.begin_cids[o]) && !(snapshot >= m.end_cids[o]);
+  const bool past_insert = m.tids[o] != our_tid && snapshot >= m.begin_cids[o] && !(snapshot >= m.end_cids[o]);
+  return own_insert || past_insert;
+}
+
+std::shared_ptr<Table> validate(const std::shared_ptr<const Table>& in, uint32_t our_tid, uint32_t snapshot) {
+  auto out = std::make_shared<Table>(in->column_definitions(), TableType::References);
+  for (ChunkID chunk_id = 0; chunk_id < in->chunk_count(); ++chunk_id) {
+    const auto chunk = in->get_chunk(chunk_id);
+    auto pl = std::make_shared<PosList>();
+    ChunkColumns cols;
+    if (const auto ref = std::dynamic_pointer_cast<const ReferenceColumn>(chunk->get_column(0))) {
+      const auto referenced = ref->referenced_table();
+      for (const auto& r : *ref->pos_list()) {
+        if (r.is_null()) continue;  // the reference dereferences it (undefined); the device drops NULL RowIDs
+        const auto m = referenced->get_chunk(r.chunk_id)->mvcc_columns();
+        Assert(m != nullptr, "Trying to use Validate on a table that has no MVCC columns");
+        if (is_row_visible(our_tid, snapshot, r.chunk_offset, *m)) pl->push_back(r);
+      }
+      for (ColumnID c = 0; c < chunk->column_count(); ++c)
+        cols.push_back(std::make_shared<ReferenceColumn>(
+            referenced, std::static_pointer_cast<const ReferenceColumn>(chunk->get_column(c))->referenced_column_id(),
+            pl));
+    } else {
+      const auto m = chunk->mvcc_columns();
+      Assert(m != nullptr, "Trying to use Validate on a table that has no MVCC columns");
+      for (ChunkOffset o = 0; o < chunk->size(); ++o)
+        if (is_row_visible(our_tid, snapshot, o, *m)) pl->emplace_back(chunk_id, o);
+      for (ColumnID c = 0; c < chunk->column_count(); ++c) cols.push_back(std::make_shared<ReferenceColumn>(in, c, pl));
+    }
+    if (!pl->empty()) out->append_chunk(cols);
+  }
+  return out;
+}
+
+// ---------------------------------------------------------------------------------------------------------------
 // JoinHash: reference join_hash.cpp:49-858
 // ---------------------------------------------------------------------------------------------------------------
 template <typename T>
@@ -1308,6 +1347,12 @@ PYBIND11_MODULE(_hyrise_oracle, m) {
         },
         py::arg("table"), py::arg("column_id"), py::arg("predicate_condition"), py::arg("value"),
         py::arg("excluded_chunk_ids") = std::vector<ChunkID>{}, py::arg("right_column_id") = py::none());
+  m.def("validate",
+        [](std::shared_ptr<Table> in, uint32_t tid, uint32_t snapshot) {
+          py::gil_scoped_release rel;
+          return oracle::validate(in, tid, snapshot);
+        },
+        py::arg("table"), py::arg("transaction_id"), py::arg("snapshot_commit_id"));
   m.def("join_hash",
         [](std::shared_ptr<Table> l, std::shared_ptr<Table> r, JoinMode mode, std::pair<ColumnID, ColumnID> cols,
            uint32_t radix_bits) {
