@@ -118,6 +118,53 @@ std::shared_ptr<DeviceColumn> device_column(const BaseColumn& column) {
           }
         });
       }
+    } else if (column.encoding_type() == EncodingType::RunLength ||
+               column.encoding_type() == EncodingType::FrameOfReference) {
+      // encoded chunk: upload the compressed arrays, expand them into a value mirror on the device
+      Assert(column.data_type() != DataType::String,
+             "hyrise-amd: encoded string columns other than Dictionary are not resident on the device");
+      resolve_data_type(column.data_type(), [&](auto tag) {
+        using T = decltype(tag);
+        if constexpr (!std::is_same_v<T, std::string>) {
+          const uint32_t n = static_cast<uint32_t>(column.size());
+          d->data = std::make_shared<DeviceBuffer>(std::max<size_t>(n, 1) * sizeof(T) + 16);
+          if (const auto* rl = dynamic_cast<const RunLengthColumn<T>*>(&column)) {
+            const auto dv = upload(rl->values().data(), rl->values().size() * sizeof(T), s);
+            const auto de = upload(rl->end_positions().data(), rl->end_positions().size() * 4, s);
+            const bool any_null =
+                std::find(rl->null_values().begin(), rl->null_values().end(), uint8_t{1}) != rl->null_values().end();
+            std::shared_ptr<DeviceBuffer> dn;
+            if (any_null) {
+              dn = upload(rl->null_values().data(), rl->null_values().size(), s);
+              d->nulls = std::make_shared<DeviceBuffer>(std::max<size_t>(n, 1) + 16);
+            }
+            hy_check(hy_decode_run_length(dv->get(), dn ? static_cast<const uint8_t*>(dn->get()) : nullptr,
+                                          static_cast<const uint32_t*>(de->get()),
+                                          static_cast<uint32_t>(rl->end_positions().size()), sizeof(T), n,
+                                          d->data->get(), any_null ? static_cast<uint8_t*>(d->nulls->get()) : nullptr,
+                                          s),
+                     "hy_decode_run_length");
+            hy_check(hy_stream_synchronize(s), "sync");  // the run arrays are released at scope end
+          } else if constexpr (std::is_same_v<T, int32_t> || std::is_same_v<T, int64_t>) {
+            const auto* fr = dynamic_cast<const FrameOfReferenceColumn<T>*>(&column);
+            Assert(fr != nullptr, "device_column: unknown encoded column");
+            const auto dm = upload(fr->block_minima().data(), fr->block_minima().size() * sizeof(T), s);
+            const auto& ov = fr->offset_values();
+            const auto doff = upload(ov.bytes().data(), ov.bytes().size(), s);
+            hy_check(hy_decode_frame_of_reference(dm->get(), hy_type_of(column.data_type()), doff->get(), ov.width(),
+                                                  n, d->data->get(), s),
+                     "hy_decode_frame_of_reference");
+            if (std::find(fr->null_values().begin(), fr->null_values().end(), uint8_t{1}) != fr->null_values().end())
+              d->nulls = upload(fr->null_values().data(), fr->null_values().size(), s);
+            hy_check(hy_stream_synchronize(s), "sync");
+          } else {
+            Fail("device_column: unknown encoded column");
+          }
+          d->desc.data = d->data->get();
+          if (d->nulls) d->desc.nulls = static_cast<const uint8_t*>(d->nulls->get());
+        }
+      });
+      d->desc.kind = HY_COL_VALUE;
     } else {
       Assert(!column.is_reference(), "device_column of a ReferenceColumn");
       Assert(column.data_type() != DataType::String,

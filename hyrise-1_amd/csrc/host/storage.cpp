@@ -134,18 +134,105 @@ std::shared_ptr<BaseColumn> encode_dictionary(const BaseColumn& base) {
   return out;
 }
 
+// reference run_length_column/run_length_encoder.hpp:22-66: a new run starts when NULL-ness or the value changes
+std::shared_ptr<BaseColumn> encode_run_length(const BaseColumn& base) {
+  std::shared_ptr<BaseColumn> out;
+  resolve_data_type(base.data_type(), [&](auto tag) {
+    using T = decltype(tag);
+    const auto* vc = dynamic_cast<const ValueColumn<T>*>(&base);
+    Assert(vc != nullptr, "encode_run_length needs a ValueColumn");
+    std::vector<T> values;
+    std::vector<uint8_t> nulls;
+    std::vector<ChunkOffset> ends;
+    for (ChunkOffset i = 0; i < vc->size(); ++i) {
+      const bool n = vc->is_null(i);
+      const T v = n ? T{} : vc->values()[i];
+      if (!ends.empty() && static_cast<bool>(nulls.back()) == n && (n || values.back() == v)) {
+        ends.back() = i;
+      } else {
+        values.push_back(v);
+        nulls.push_back(n ? 1 : 0);
+        ends.push_back(i);
+      }
+    }
+    out = std::make_shared<RunLengthColumn<T>>(std::move(values), std::move(nulls), std::move(ends));
+  });
+  return out;
+}
+
+// reference frame_of_reference/frame_of_reference_encoder.hpp:27-86 (NULL rows count as 0 for the block minimum)
+std::shared_ptr<BaseColumn> encode_frame_of_reference(const BaseColumn& base) {
+  std::shared_ptr<BaseColumn> out;
+  resolve_data_type(base.data_type(), [&](auto tag) {
+    using T = decltype(tag);
+    if constexpr (std::is_same_v<T, int32_t> || std::is_same_v<T, int64_t>) {
+      const auto* vc = dynamic_cast<const ValueColumn<T>*>(&base);
+      Assert(vc != nullptr, "encode_frame_of_reference needs a ValueColumn");
+      constexpr uint32_t B = FrameOfReferenceColumn<T>::block_size;
+      const size_t n = vc->size();
+      std::vector<T> minima;
+      std::vector<uint8_t> nulls(n);
+      std::vector<uint32_t> offsets(n);
+      uint32_t max_offset = 0;
+      for (size_t b = 0; b < n; b += B) {
+        const size_t e = std::min(n, b + B);
+        T mn = std::numeric_limits<T>::max(), mx = std::numeric_limits<T>::lowest();
+        for (size_t i = b; i < e; ++i) {
+          const T v = vc->is_null(static_cast<ChunkOffset>(i)) ? T{0} : vc->values()[i];
+          mn = std::min(mn, v);
+          mx = std::max(mx, v);
+        }
+        Assert(static_cast<std::make_unsigned_t<T>>(mx - mn) <= std::numeric_limits<uint32_t>::max(),
+               "Value range in block must fit into uint32_t.");
+        minima.push_back(mn);
+        for (size_t i = b; i < e; ++i) {
+          const bool isn = vc->is_null(static_cast<ChunkOffset>(i));
+          nulls[i] = isn ? 1 : 0;
+          offsets[i] = static_cast<uint32_t>((isn ? T{0} : vc->values()[i]) - mn);
+          max_offset = std::max(max_offset, offsets[i]);
+        }
+      }
+      auto av = std::make_shared<const AttributeVector>(offsets, max_offset);
+      out = std::make_shared<FrameOfReferenceColumn<T>>(std::move(minima), std::move(nulls), std::move(av));
+    } else {
+      Fail("FrameOfReference encoding supports int and long columns only");
+    }
+  });
+  return out;
+}
+
+namespace {
+std::shared_ptr<BaseColumn> encode_column(const BaseColumn& col, EncodingType encoding) {
+  switch (encoding) {
+    case EncodingType::Dictionary:
+      return encode_dictionary(col);
+    case EncodingType::RunLength:
+      return encode_run_length(col);
+    case EncodingType::FrameOfReference:
+      return encode_frame_of_reference(col);
+    default:
+      Fail("Encoding type not supported by the device path");
+  }
+}
+}  // namespace
+
 void ChunkEncoder::encode_chunks(const std::shared_ptr<Table>& table, const std::vector<ChunkID>& chunk_ids,
                                  EncodingType encoding) {
   Assert(table->type() == TableType::Data, "Only data tables can be encoded");
   if (encoding == EncodingType::Unencoded) return;
-  if (encoding != EncodingType::Dictionary)
-    Fail("Encoding type not supported by the device path (only Unencoded and Dictionary)");
+  if (encoding == EncodingType::FixedStringDictionary)
+    Fail("Encoding type not supported by the device path (FixedStringDictionary)");
   for (const auto chunk_id : chunk_ids) {
     const auto chunk = table->get_chunk(chunk_id);
     for (ColumnID c = 0; c < chunk->column_count(); ++c) {
       const auto col = chunk->get_column(c);
-      if (col->encoding_type() == EncodingType::Dictionary) continue;
-      chunk->replace_column(c, encode_dictionary(*col));
+      if (col->encoding_type() != EncodingType::Unencoded) continue;  // already encoded
+      // the reference's ChunkEncoder leaves string columns FrameOfReference cannot encode to the caller's spec;
+      // here FrameOfReference on a non-integer column keeps it unencoded
+      if (encoding == EncodingType::FrameOfReference && col->data_type() != DataType::Int &&
+          col->data_type() != DataType::Long)
+        continue;
+      chunk->replace_column(c, encode_column(*col, encoding));
     }
   }
 }

@@ -160,6 +160,63 @@ class AttributeVector {
   size_t _size = 0;
 };
 
+// RunLengthColumn (reference storage/run_length_column.hpp): one value + NULL flag per run, end_positions[r] = last
+// offset of run r. On the device it is decoded once into a value mirror (hy_decode_run_length).
+template <typename T>
+class RunLengthColumn final : public BaseColumn {
+ public:
+  RunLengthColumn(std::vector<T> values, std::vector<uint8_t> null_values, std::vector<ChunkOffset> end_positions)
+      : BaseColumn(data_type_from_type<T>()),
+        _values(std::move(values)),
+        _null_values(std::move(null_values)),
+        _end_positions(std::move(end_positions)) {}
+  size_t size() const override { return _end_positions.empty() ? 0 : _end_positions.back() + 1u; }
+  EncodingType encoding_type() const override { return EncodingType::RunLength; }
+  AllTypeVariant operator[](ChunkOffset o) const override {  // run_length_column.cpp:24-36
+    const auto run = static_cast<size_t>(
+        std::distance(_end_positions.cbegin(), std::lower_bound(_end_positions.cbegin(), _end_positions.cend(), o)));
+    if (_null_values.at(run)) return NullValue{};
+    return _values.at(run);
+  }
+  const std::vector<T>& values() const { return _values; }
+  const std::vector<uint8_t>& null_values() const { return _null_values; }
+  const std::vector<ChunkOffset>& end_positions() const { return _end_positions; }
+
+ private:
+  std::vector<T> _values;
+  std::vector<uint8_t> _null_values;
+  std::vector<ChunkOffset> _end_positions;
+};
+
+// FrameOfReferenceColumn (reference storage/frame_of_reference_column.hpp): per block of 2048 rows a minimum, per row
+// an unsigned offset (FixedSizeByteAligned u8/u16/u32) and a NULL flag; int32 / int64 only. Decoded on the device
+// once into a value mirror (hy_decode_frame_of_reference).
+template <typename T>
+class FrameOfReferenceColumn final : public BaseColumn {
+ public:
+  static constexpr uint32_t block_size = 2048u;
+  FrameOfReferenceColumn(std::vector<T> block_minima, std::vector<uint8_t> null_values,
+                         std::shared_ptr<const AttributeVector> offset_values)
+      : BaseColumn(data_type_from_type<T>()),
+        _block_minima(std::move(block_minima)),
+        _null_values(std::move(null_values)),
+        _offset_values(std::move(offset_values)) {}
+  size_t size() const override { return _null_values.size(); }
+  EncodingType encoding_type() const override { return EncodingType::FrameOfReference; }
+  AllTypeVariant operator[](ChunkOffset o) const override {  // frame_of_reference_column.cpp:25-37
+    if (_null_values.at(o)) return NullValue{};
+    return static_cast<T>(_block_minima.at(o / block_size) + static_cast<T>(_offset_values->get(o)));
+  }
+  const std::vector<T>& block_minima() const { return _block_minima; }
+  const std::vector<uint8_t>& null_values() const { return _null_values; }
+  const AttributeVector& offset_values() const { return *_offset_values; }
+
+ private:
+  std::vector<T> _block_minima;
+  std::vector<uint8_t> _null_values;
+  std::shared_ptr<const AttributeVector> _offset_values;
+};
+
 class BaseDictionaryColumn : public BaseColumn {
  public:
   using BaseColumn::BaseColumn;

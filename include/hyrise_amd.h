@@ -268,6 +268,20 @@ hy_status hy_validate_pos_list(const hy_row_id* pos_list, uint64_t pos_list_size
                                size_t workspace_bytes, hy_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------------------------
+ * Encoded chunks -> value mirrors in HBM (all pointers device)
+ * ------------------------------------------------------------------------------------------------------------- */
+/* RunLengthColumn (reference storage/run_length_column.hpp, run_length_column.cpp:24-36): row i takes the value and
+ * NULL flag of the first run r with end_positions[r] >= i. value_bytes 4 or 8; out_nulls may be NULL. */
+hy_status hy_decode_run_length(const void* values, const uint8_t* run_nulls, const uint32_t* end_positions,
+                               uint32_t n_runs, uint32_t value_bytes, uint32_t n_rows, void* out_values,
+                               uint8_t* out_nulls, hy_stream_t stream);
+/* FrameOfReferenceColumn (reference frame_of_reference_column.cpp:25-37): value = block_minima[i / 2048] + offset[i],
+ * offsets FixedSizeByteAligned of offset_width 1/2/4 bytes; value_type HY_TYPE_INT32 / HY_TYPE_INT64. (NULL flags
+ * are uploaded as they are.) */
+hy_status hy_decode_frame_of_reference(const void* block_minima, int32_t value_type, const void* offsets,
+                                       int32_t offset_width, uint32_t n_rows, void* out_values, hy_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------------------------
  * Hashing (reference src/lib/utils/murmur_hash.cpp:21-75, seed 17 from join_hash.cpp:680)
  * ------------------------------------------------------------------------------------------------------------- */
 /* out[i] = murmur_hash2(&keys[i], key_bytes, seed); key_bytes 4 or 8. */

@@ -128,7 +128,13 @@ void for_each_data(const BaseColumn& col, const std::vector<std::pair<ChunkOffse
       return {vc->values()[o], n};
     }
     const auto* dc = dynamic_cast<const DictionaryColumn<T>*>(&col);
-    Assert(dc != nullptr, "oracle: unsupported column type");
+    if (dc == nullptr) {  // RunLength / FrameOfReference: the column's own decoding (operator[])
+      Assert(col.encoding_type() == EncodingType::RunLength || col.encoding_type() == EncodingType::FrameOfReference,
+             "oracle: unsupported column type");
+      const auto v = col[o];
+      if (variant_is_null(v)) return {T{}, true};
+      return {std::get<T>(v), false};
+    }
     const ValueID vid = dc->attribute_vector().get(o);
     if (vid == dc->null_value_id()) return {T{}, true};
     return {dc->dictionary()[vid], false};

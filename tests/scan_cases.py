@@ -2,7 +2,7 @@
 from the test's inline vectors), shared by the oracle tests (CPU) and the device parity tests (GPU)."""
 from helpers import tbl, wrap
 
-ENCODINGS = ["Unencoded", "Dictionary"]
+ENCODINGS = ["Unencoded", "Dictionary", "RunLength", "FrameOfReference"]  # table_scan_test.cpp:206-209
 
 
 def int_int_tables(hy, encoding):
@@ -115,7 +115,7 @@ NULL_ROW_ID = 0xFFFFFFFF
 def null_scan_tables(hy):
     """(name, table, expected cases) for every ScanForNullValues* test of table_scan_test.cpp:503-601."""
     out = []
-    for enc in (None, "Dictionary"):
+    for enc in (None, "Dictionary", "RunLength", "FrameOfReference"):
         t = hy.load_table(tbl("int_int_w_null_8_rows.tbl"), 4)
         if enc:
             hy.encode_all_chunks(t, getattr(hy.EncodingType, enc))
@@ -145,7 +145,7 @@ COLUMN_COMPARE_EXPECTED = [12345, 1234, 12345, 1234]
 
 def column_compare_tables(hy):
     out = []
-    for enc in (None, "Dictionary"):
+    for enc in (None, "Dictionary", "RunLength", "FrameOfReference"):
         t = hy.load_table(tbl("int_int_w_null_8_rows.tbl"), 4)
         if enc:
             hy.encode_all_chunks(t, getattr(hy.EncodingType, enc))

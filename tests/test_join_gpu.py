@@ -128,3 +128,26 @@ def test_scan_over_join_output(hy, oracle, cond, value):
     exp_s = oracle.table_scan(exp_j, 2, pc, value, [])
     assert exp_s.row_count() > 0
     assert_identical(s.get_output(), exp_s)
+
+
+@pytest.mark.parametrize("encoding", ["RunLength", "FrameOfReference"])
+@pytest.mark.parametrize("mode", ["Inner", "Left", "Anti"])
+def test_encoded_join_columns(hy, oracle, encoding, mode):
+    """RunLength / FrameOfReference chunks (decoded into HBM value mirrors) on both join sides, NULLs included."""
+    rng = np.random.default_rng(23)
+    n1, n2 = 20_000, 35_000
+    k1 = np.sort(rng.integers(0, 3_000, n1)).astype(np.int64)  # sorted: long runs
+    k2 = rng.integers(0, 4_000, n2).astype(np.int32)
+    nl1 = (rng.random(n1) < 0.02).astype(np.uint8)
+    nl2 = (rng.random(n2) < 0.02).astype(np.uint8)
+    a = hy.Table.from_arrays([("k", hy.DataType.Long, True)], [k1], [nl1], 6_000)
+    b = hy.Table.from_arrays([("k", hy.DataType.Int, True), ("v", hy.DataType.Int, False)],
+                             [k2, np.arange(n2, dtype=np.int32)], [nl2, None], 8_191)
+    hy.encode_chunks(a, [0, 2], getattr(hy.EncodingType, encoding))
+    hy.encode_all_chunks(b, getattr(hy.EncodingType, encoding))
+    for left, right in ((a, b), (b, a)):
+        j = hy.JoinHash(wrap(hy, left), wrap(hy, right), getattr(hy.JoinMode, mode), (0, 0),
+                        hy.PredicateCondition.Equals)
+        j.execute()
+        exp, _ = oracle.join_hash(left, right, getattr(hy.JoinMode, mode), (0, 0))
+        assert_identical(j.get_output(), exp)
