@@ -197,3 +197,23 @@ def test_hash_aggregate_grows_past_its_group_bound(hy, oracle, monkeypatch):
     op.execute()
     assert not op.used_dense_path()
     assert_identical(op.get_output(), oracle.aggregate(t, ac.agg_defs(hy, aggs), [0]))
+
+
+@pytest.mark.parametrize("encoding", ["RunLength", "FrameOfReference"])
+def test_encoded_inputs(hy, oracle, encoding):
+    """Aggregates over RunLength / FrameOfReference chunks (decoded into HBM value mirrors), dense and hash paths,
+    mixed with unencoded chunks (FrameOfReference leaves the float columns unencoded, as it supports ints only)."""
+    rng = np.random.default_rng(41)
+    t = q1_like(hy, 200_000, 50_000, rng, nulls=True)
+    hy.encode_chunks(t, [0, 2, 3], getattr(hy.EncodingType, encoding))
+    w = wrap(hy, t)
+    scan = hy.TableScan(w, 6, hy.PredicateCondition.LessThanEquals, 10_471)
+    scan.execute()
+    agg = hy.Aggregate(scan, ac.agg_defs(hy, Q1_AGGS), [0, 1])
+    agg.execute()
+    ref_in = oracle.table_scan(t, 6, hy.PredicateCondition.LessThanEquals, 10_471, [])
+    assert_identical(agg.get_output(), oracle.aggregate(ref_in, ac.agg_defs(hy, Q1_AGGS), [0, 1]))
+    aggs = [(2, "Sum"), (3, "Min"), (6, "Max"), (None, "Count")]
+    op = hy.Aggregate(w, ac.agg_defs(hy, aggs), [6])
+    op.execute()
+    assert_identical(op.get_output(), oracle.aggregate(t, ac.agg_defs(hy, aggs), [6]))
