@@ -535,7 +535,7 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
 // ================================================================================================================
 namespace {
 
-// The MVCC vectors of a table's chunks, concatenated into three device arrays; descriptors point into them.
+// Device descriptors of a table's MVCC columns; each chunk's HBM copy is made once and cached on its MvccColumns.
 struct DeviceMvcc {
   std::vector<hy_mvcc_chunk> chunks;
   std::vector<std::shared_ptr<DeviceBuffer>> keep;
@@ -543,29 +543,30 @@ struct DeviceMvcc {
 
 DeviceMvcc upload_mvcc(const Table& table, hy_stream_t s) {
   DeviceMvcc out;
-  uint64_t rows = 0;
   for (ChunkID c = 0; c < table.chunk_count(); ++c) {
     const auto m = table.get_chunk(c)->mvcc_columns();
     Assert(m != nullptr, "Trying to use Validate on a table that has no MVCC columns");
-    rows += m->tids.size();
-  }
-  std::vector<uint32_t> all(3 * std::max<uint64_t>(rows, 1));
-  auto buf = std::make_shared<DeviceBuffer>(all.size() * 4);
-  uint64_t at = 0;
-  for (ChunkID c = 0; c < table.chunk_count(); ++c) {
-    const auto m = table.get_chunk(c)->mvcc_columns();
     const uint64_t n = m->tids.size();
     Assert(m->begin_cids.size() == n && m->end_cids.size() == n, "MVCC columns of different lengths");
-    std::copy(m->tids.begin(), m->tids.end(), all.begin() + at);
-    std::copy(m->begin_cids.begin(), m->begin_cids.end(), all.begin() + rows + at);
-    std::copy(m->end_cids.begin(), m->end_cids.end(), all.begin() + 2 * rows + at);
+    std::shared_ptr<DeviceBuffer> buf;
+    {
+      std::lock_guard<std::mutex> lock(m->device_mutex);
+      buf = std::static_pointer_cast<DeviceBuffer>(m->device);
+      if (!buf) {  // first use: one upload of the chunk's three vectors, kept with the MvccColumns
+        buf = std::make_shared<DeviceBuffer>(std::max<uint64_t>(3 * n, 4) * 4);
+        if (n) {
+          hy_check(hy_memcpy_htod(buf->get(), m->tids.data(), 4 * n, s), "htod");
+          hy_check(hy_memcpy_htod(buf->as<uint32_t>() + n, m->begin_cids.data(), 4 * n, s), "htod");
+          hy_check(hy_memcpy_htod(buf->as<uint32_t>() + 2 * n, m->end_cids.data(), 4 * n, s), "htod");
+        }
+        m->device = buf;
+      }
+    }
     const uint32_t* base = buf->as<uint32_t>();
-    out.chunks.push_back(hy_mvcc_chunk{base + at, base + rows + at, base + 2 * rows + at, static_cast<uint32_t>(n), 0});
-    at += n;
+    out.chunks.push_back(hy_mvcc_chunk{base, base + n, base + 2 * n, static_cast<uint32_t>(n), 0});
+    out.keep.push_back(std::move(buf));
   }
-  hy_check(hy_memcpy_htod(buf->get(), all.data(), all.size() * 4, s), "htod");
-  hy_check(hy_stream_synchronize(s), "sync");  // `all` is pageable
-  out.keep.push_back(std::move(buf));
+  hy_check(hy_stream_synchronize(s), "sync");
   return out;
 }
 

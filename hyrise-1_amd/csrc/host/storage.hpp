@@ -299,6 +299,10 @@ using ChunkColumns = std::vector<std::shared_ptr<BaseColumn>>;
 struct MvccColumns {
   static constexpr uint32_t MAX_COMMIT_ID = std::numeric_limits<uint32_t>::max() - 1;
   std::vector<uint32_t> tids, begin_cids, end_cids;
+  // HBM copy (tids | begin_cids | end_cids), made on first Validate; the vectors are not mutated after
+  // Chunk::set_mvcc_columns (a new MVCC state is a new MvccColumns object), so the copy stays valid
+  mutable std::mutex device_mutex;
+  mutable std::shared_ptr<void> device;
 };
 
 class Chunk {
