@@ -313,6 +313,20 @@ def main():
         t = trace.view(-1, 5).cpu().numpy().astype(np.float64) / 100.0  # 100 MHz device clock -> us
         np.savez(args.join_trace, stamps_us=t, out_pairs=part_count.cpu().numpy())
     g_li, g_ord, g_probe, g_pairs = n_li, n_ord, n_probe, int(pairs)
+    check = None
+    if mode == "join":  # pin the timed output at its full size (every pair, partition and scan offset)
+        thr = []
+        for c in range(n_lchunks):
+            op_ = scan_chunks[c].op
+            thr.append(256 if op_ == capi.HY_OP_ALL else (0 if op_ == capi.HY_OP_NONE else scan_chunks[c].search_vid))
+        if fused:
+            outs = (state["fout_b"], state["fout_p"], scan_off, scan_begin)
+        else:
+            outs = (state["out_b"], state["out_p"], None, None)
+        check = verify_headline(torch, L, stream, chunk, okey, lkey, vids, n_li, thr, outs, part_begin, part_count,
+                                radix_bits, g_pairs)
+        if check["status"] != "ok":
+            raise SystemExit(f"headline output check failed: {check}")
 
     # ---------------- per-kernel device time (HIP events on the launch stream) ----------------
     nk = ctypes.c_uint32(0)
@@ -422,6 +436,7 @@ def main():
             "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                         for k, v in kernels.items()},
             "cpu_baseline": cpu,
+            "check": check,
         }
         if mode == "scan":  # BASELINE.json configs[1]
             line["metric"] = "rows/sec TableScan lineitem.l_quantity<24, dictionary-encoded, one MI355X"
@@ -439,6 +454,59 @@ def main():
                               "parallelism": "single GPU"}
             line["roofline"]["scope"] = "JoinHash step (SURVEY 8(d): 4 B/build row + 4 B/probe row + 16 B/pair)"
         print(json.dumps(line))
+
+
+def verify_headline(torch, L, stream, chunk, okey, lkey, vids, n_li, thr, outs, part_begin, part_count, bits, pairs):
+    """Checks the timed step's output at its full size on the device (after the timed region). For an INNER join with
+    unique build keys these properties determine the reference's output exactly (join_hash.cpp:362-455, 829-855):
+      * every pair's o_orderkey[build RowID] == l_orderkey[probe RowID];
+      * the probe rows of all pairs are exactly the scan matches (every lineitem row's order exists);
+      * partition p's range holds only probe keys with murmur2(key, 17) & (2^bits - 1) == p;
+      * probe RowIDs ascend within each partition (the reference's probe order);
+      * the partitions' ranges tile the output buffer without gaps or overlap;
+      * fused path: the scan output offsets are the rows with vid < search_vid of their chunk (table_scan.cpp:78-164,
+        single_column_table_scan_impl.cpp:145-205), chunk by chunk."""
+    dev = okey.device
+    ob_t, op_t, scan_off, scan_begin = outs
+    ob = ob_t[: 2 * pairs].view(-1, 2).to(torch.int64)
+    op = op_t[: 2 * pairs].view(-1, 2).to(torch.int64)
+    bidx = ob[:, 0] * chunk + ob[:, 1]
+    pidx = op[:, 0] * chunk + op[:, 1]
+    del ob, op
+    res = {}
+    res["keys_equal"] = bool(torch.equal(okey[bidx], lkey[pidx]))
+    del bidx
+    sizes = torch.tensor([min(chunk, n_li - c * chunk) for c in range(len(thr))], dtype=torch.int64, device=dev)
+    t = torch.repeat_interleave(torch.tensor(thr, dtype=torch.int32, device=dev), sizes)
+    match = torch.nonzero(vids[:n_li].to(torch.int32) < t).flatten()
+    del t
+    res["probe_rows_are_scan_matches"] = bool(match.numel() == pairs and torch.equal(torch.sort(pidx).values, match))
+    if scan_off is not None:
+        n_m = int(scan_begin[-1].item())
+        res["scan_offsets"] = bool(n_m == match.numel() and
+                                   torch.equal(scan_off[:n_m].to(torch.int64), match % chunk))
+        starts = torch.searchsorted(match, torch.arange(0, n_li, chunk, device=dev))
+        res["scan_chunk_begins"] = bool(torch.equal(scan_begin[:-1], starts))
+    del match
+    n_parts = 1 << bits
+    cnt = part_count[:n_parts].to(torch.int64)
+    beg = part_begin[:n_parts].to(torch.int64)
+    order = torch.argsort(beg[cnt > 0])
+    pids = torch.nonzero(cnt > 0).flatten()[order]
+    cs = cnt[pids]
+    res["ranges_tile_output"] = bool(int(cs.sum()) == pairs and
+                                     torch.equal(beg[pids], torch.cumsum(cs, 0) - cs))
+    pid = torch.repeat_interleave(pids, cs)  # partition of each output slot
+    h = torch.empty(pairs, dtype=torch.int32, device=dev)
+    keys = lkey[pidx].contiguous()
+    st = L.hy_murmur2(keys.data_ptr(), pairs, 4, 17, h.data_ptr(), stream)
+    res["partition_ids"] = bool(st == 0 and torch.equal(h.to(torch.int64) & (n_parts - 1), pid))
+    same = pid[1:] == pid[:-1]
+    res["probe_order_within_partitions"] = bool(torch.all((pidx[1:] > pidx[:-1]) | ~same))
+    torch.cuda.synchronize()
+    res["status"] = "ok" if all(v for k, v in res.items()) else "MISMATCH"
+    res["pairs_checked"] = pairs
+    return res
 
 
 def kernel_stats(L):

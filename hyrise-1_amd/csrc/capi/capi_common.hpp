@@ -34,13 +34,46 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 // Host -> device copies of the descriptors a call builds on the host (chunk / side / column tables, offsets): staged
 // through a per-thread pinned ring so that hipMemcpyAsync is a real asynchronous DMA (a pageable source makes the
 // runtime stage it synchronously, at a fraction of the bandwidth - measurable with tens of thousands of chunks), and
-// so that the source may go out of scope right after the call. The ring wraps after a device synchronisation, which
-// every earlier copy out of it has then completed.
+// so that the source may go out of scope right after the call. Every copy re-records its stream's event (one event
+// per (stream, device) the thread has staged on: stream order makes the latest record cover the earlier copies); when
+// the ring wraps it waits on those events only - the ring's own DMAs - instead of the whole device, so other threads'
+// operator streams are not stalled, and copies staged for another GPU are covered too.
 struct PinnedRing {
+  struct Fence {
+    hipStream_t stream;
+    int device;
+    hipEvent_t event;
+  };
   char* buf = nullptr;
   size_t cap = 0, used = 0;
+  std::vector<Fence> fences;
   ~PinnedRing() {
+    for (auto& f : fences) (void)hipEventDestroy(f.event);
     if (buf) (void)hipHostFree(buf);
+  }
+  hy_status wait_all() {
+    for (auto& f : fences) HY_HIP(hipEventSynchronize(f.event));
+    return HY_OK;
+  }
+  hy_status fence(hipStream_t s) {
+    int dev = 0;
+    HY_HIP(hipGetDevice(&dev));
+    for (auto& f : fences)
+      if (f.stream == s && f.device == dev) {
+        HY_HIP(hipEventRecord(f.event, s));
+        return HY_OK;
+      }
+    if (fences.size() >= 32) {  // many short-lived streams: retire the fences (their copies are waited for first)
+      const hy_status w = wait_all();
+      if (w != HY_OK) return w;
+      for (auto& f : fences) (void)hipEventDestroy(f.event);
+      fences.clear();
+    }
+    Fence f{s, dev, nullptr};
+    HY_HIP(hipEventCreateWithFlags(&f.event, hipEventDisableTiming));
+    HY_HIP(hipEventRecord(f.event, s));
+    fences.push_back(f);
+    return HY_OK;
   }
 };
 inline hy_status staged_htod(void* dst, const void* src, size_t bytes, hipStream_t s) {
@@ -48,7 +81,8 @@ inline hy_status staged_htod(void* dst, const void* src, size_t bytes, hipStream
   thread_local PinnedRing ring;
   const size_t need = (bytes + 255) & ~size_t(255);
   if (ring.used + need > ring.cap) {
-    HY_HIP(hipDeviceSynchronize());  // every copy out of the ring has completed
+    const hy_status w = ring.wait_all();  // every copy out of the ring has completed
+    if (w != HY_OK) return w;
     if (need > ring.cap) {
       if (ring.buf) HY_HIP(hipHostFree(ring.buf));
       ring.buf = nullptr;
@@ -61,7 +95,7 @@ inline hy_status staged_htod(void* dst, const void* src, size_t bytes, hipStream
   std::memcpy(stage, src, bytes);
   ring.used += need;
   HY_HIP(hipMemcpyAsync(dst, stage, bytes, hipMemcpyHostToDevice, s));
-  return HY_OK;
+  return ring.fence(s);
 }
 #define HY_STAGE(dst, src, bytes, stream)                                              \
   do {                                                                                 \

@@ -27,6 +27,7 @@ struct hy_comm_s {
   int32_t n_ranks = 0;
   int32_t rank = 0;
   uint64_t* counts = nullptr;  // device scratch: n_ranks * 256 gathered bucket counts
+  uint32_t* flag = nullptr;    // device scratch: the exchange's all-reduced abort flag
 };
 
 namespace {
@@ -39,6 +40,17 @@ hy_status nccl_fail(ncclResult_t r, const char* what) {
   do {                                                 \
     const ncclResult_t r_ = (call);                    \
     if (r_ != ncclSuccess) return nccl_fail(r_, #call); \
+  } while (0)
+
+// An RCCL call inside ncclGroupStart/End: on failure the group is closed before returning, so the communicator is
+// left usable (its peers' matching calls then fail or complete instead of waiting on an open group).
+#define HY_NCCL_IN_GROUP(call)                       \
+  do {                                               \
+    const ncclResult_t r_ = (call);                  \
+    if (r_ != ncclSuccess) {                         \
+      (void)ncclGroupEnd();                          \
+      return nccl_fail(r_, #call);                   \
+    }                                                \
   } while (0)
 
 uint32_t owner_begin(uint32_t n_buckets, int32_t d, int32_t n) {
@@ -70,7 +82,9 @@ hy_status hy_comm_init(hy_comm_t* comm, int32_t n_ranks, const hy_comm_id* id, i
   }
   c->n_ranks = n_ranks;
   c->rank = rank;
-  if (hipMalloc(&c->counts, sizeof(uint64_t) * 256 * n_ranks) != hipSuccess) {
+  if (hipMalloc(&c->counts, sizeof(uint64_t) * 256 * n_ranks) != hipSuccess ||
+      hipMalloc(&c->flag, sizeof(uint32_t)) != hipSuccess) {
+    if (c->counts) (void)hipFree(c->counts);
     ncclCommDestroy(c->nccl);
     delete c;
     return fail(HY_ERR_DEVICE, "hipMalloc");
@@ -82,6 +96,7 @@ hy_status hy_comm_init(hy_comm_t* comm, int32_t n_ranks, const hy_comm_id* id, i
 hy_status hy_comm_destroy(hy_comm_t comm) {
   if (!comm) return HY_OK;
   if (comm->counts) (void)hipFree(comm->counts);
+  if (comm->flag) (void)hipFree(comm->flag);
   const ncclResult_t r = comm->nccl ? ncclCommDestroy(comm->nccl) : ncclSuccess;
   delete comm;
   return r == ncclSuccess ? HY_OK : nccl_fail(r, "ncclCommDestroy");
@@ -125,10 +140,20 @@ hy_status hy_join_exchange_records(hy_comm_t comm, const void* records, uint32_t
     recv_off[src + 1] = recv_off[src] + recv[src];
   }
   *recv_rows = recv_off[n];
-  if (recv_off[n] > recv_capacity) return fail(HY_ERR_CAPACITY, "exchange receive buffer too small");
-  if (recv_off[n] && !recv_records) return fail(HY_ERR_INVALID_ARGUMENT, "null receive buffer");
-  if (send_off[n] && !records) return fail(HY_ERR_INVALID_ARGUMENT, "null records");
+  // The abort decision is collective: a rank that returned early here would leave its peers blocked in their sends to
+  // it. Every rank contributes its own verdict (1: receive buffer too small, 2: null buffer) and all take the max.
+  uint32_t mine = recv_off[n] > recv_capacity ? 1u : 0u;
+  if ((recv_off[n] && !recv_records) || (send_off[n] && !records)) mine = 2u;
   hipStream_t s = S(stream);
+  uint32_t verdict = 0;
+  HY_HIP(hipMemcpyAsync(comm->flag, &mine, 4, hipMemcpyHostToDevice, s));
+  HY_NCCL(ncclAllReduce(comm->flag, comm->flag, 1, ncclUint32, ncclMax, comm->nccl, s));
+  HY_HIP(hipMemcpyAsync(&verdict, comm->flag, 4, hipMemcpyDeviceToHost, s));
+  HY_HIP(hipStreamSynchronize(s));
+  if (verdict == 1)
+    return fail(HY_ERR_CAPACITY, mine ? "exchange receive buffer too small"
+                                      : "exchange receive buffer of another rank too small");
+  if (verdict != 0) return fail(HY_ERR_INVALID_ARGUMENT, mine ? "null exchange buffer" : "null exchange buffer on another rank");
   const auto* src = static_cast<const char*>(records);
   auto* dst = static_cast<char*>(recv_records);
   const uint64_t rb = record_bytes;
@@ -137,8 +162,9 @@ hy_status hy_join_exchange_records(hy_comm_t comm, const void* records, uint32_t
   HY_NCCL(ncclGroupStart());
   for (int32_t k = 1; k < n; ++k) {  // peers in a rotating order, so that every link carries one message per round
     const int32_t to = (me + k) % n, from = (me - k + n) % n;
-    if (send[to]) HY_NCCL(ncclSend(src + send_off[to] * rb, send[to] * rb, ncclUint8, to, comm->nccl, s));
-    if (recv[from]) HY_NCCL(ncclRecv(dst + recv_off[from] * rb, recv[from] * rb, ncclUint8, from, comm->nccl, s));
+    if (send[to]) HY_NCCL_IN_GROUP(ncclSend(src + send_off[to] * rb, send[to] * rb, ncclUint8, to, comm->nccl, s));
+    if (recv[from])
+      HY_NCCL_IN_GROUP(ncclRecv(dst + recv_off[from] * rb, recv[from] * rb, ncclUint8, from, comm->nccl, s));
   }
   HY_NCCL(ncclGroupEnd());
   return HY_OK;

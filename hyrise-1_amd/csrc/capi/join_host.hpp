@@ -1124,6 +1124,13 @@ inline uint32_t ceil_log2(uint32_t n) {
   return b;
 }
 
+// Longest exclusive scan of the exchange partition's pass 0: one histogram row per first digit over the side's spans,
+// plus the fused TableScan's match row when the side is filtered (part1_compact writes it, join.hip).
+inline uint64_t exchange_scan_words(const SidePlan& p, const std::vector<uint32_t>& w) {
+  const uint64_t rows = (1ull << w[0]) + (p.filtered ? 1 : 0);
+  return std::max<uint64_t>(rows * std::max<uint64_t>(1, p.n_tiles1), 2);
+}
+
 template <typename H, typename P = hy_row_id>
 size_t exchange_partition_bytes(const SidePlan& p, uint32_t bits, const std::vector<uint32_t>& w) {
   Carver cv{nullptr, 0};
@@ -1131,7 +1138,7 @@ size_t exchange_partition_bytes(const SidePlan& p, uint32_t bits, const std::vec
   SideSizes z = sizes_of(p, false);
   carve_side<H, P>(cv, z, bits, std::vector<uint32_t>(w.begin(), w.begin() + 1), 1, false, b);
   Common c;
-  carve_common(cv, std::max<uint64_t>((1ull << w[0]) * std::max<uint64_t>(1, p.n_tiles1), 2), bits, &c);
+  carve_common(cv, exchange_scan_words(p, w), bits, &c);
   return cv.used + 256;
 }
 
@@ -1299,7 +1306,7 @@ hy_status exchange_partition_for_hashed(const SidePlan& p, int32_t value_type, c
       SideBufs<H, P> b;
       carve_side<H, P>(cv, sizes_of(p, false), bits, std::vector<uint32_t>(w.begin(), w.begin() + 1), 1, false, b);
       Common c{};
-      carve_common(cv, std::max<uint64_t>(uint64_t(T) * std::max<uint64_t>(1, p.n_tiles1), 2), bits, &c);
+      carve_common(cv, exchange_scan_words(p, w), bits, &c);
       if (!cv.ok) return fail(HY_ERR_WORKSPACE, "workspace");
       if (upload_side(p, b, s)) return HY_ERR_DEVICE;
       hy_status st2 = pass0_side<T_, H, P>("exchange", p, b, bits, w[0], params->seed, keep_nulls != 0, p.ref_base,

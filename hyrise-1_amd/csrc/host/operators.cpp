@@ -544,22 +544,31 @@ struct DeviceMvcc {
 DeviceMvcc upload_mvcc(const Table& table, hy_stream_t s) {
   DeviceMvcc out;
   for (ChunkID c = 0; c < table.chunk_count(); ++c) {
-    const auto m = table.get_chunk(c)->mvcc_columns();
+    const auto chunk = table.get_chunk(c);
+    const auto m = chunk->mvcc_columns();
     Assert(m != nullptr, "Trying to use Validate on a table that has no MVCC columns");
-    const uint64_t n = m->tids.size();
-    Assert(m->begin_cids.size() == n && m->end_cids.size() == n, "MVCC columns of different lengths");
+    // validate.cpp:101 iterates the chunk's rows: the MVCC vectors must cover them (they may be longer, as the
+    // reference's are while a chunk is being filled)
+    const uint64_t n = chunk->size();
+    Assert(m->tids.size() >= n && m->begin_cids.size() >= n && m->end_cids.size() >= n,
+           "MVCC columns shorter than the chunk");
     std::shared_ptr<DeviceBuffer> buf;
     {
       std::lock_guard<std::mutex> lock(m->device_mutex);
       buf = std::static_pointer_cast<DeviceBuffer>(m->device);
+      if (buf && m->device_rows != n) buf.reset();  // the chunk grew since the copy was made
       if (!buf) {  // first use: one upload of the chunk's three vectors, kept with the MvccColumns
         buf = std::make_shared<DeviceBuffer>(std::max<uint64_t>(3 * n, 4) * 4);
         if (n) {
           hy_check(hy_memcpy_htod(buf->get(), m->tids.data(), 4 * n, s), "htod");
           hy_check(hy_memcpy_htod(buf->as<uint32_t>() + n, m->begin_cids.data(), 4 * n, s), "htod");
           hy_check(hy_memcpy_htod(buf->as<uint32_t>() + 2 * n, m->end_cids.data(), 4 * n, s), "htod");
+          // published only once the copies have landed: another thread's Validate may use the cached buffer on its
+          // own stream right after the lock is released
+          hy_check(hy_stream_synchronize(s), "sync");
         }
         m->device = buf;
+        m->device_rows = n;
       }
     }
     const uint32_t* base = buf->as<uint32_t>();

@@ -17,6 +17,7 @@
 #include <memory>
 #include <mutex>
 #include <optional>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -303,6 +304,7 @@ struct MvccColumns {
   // Chunk::set_mvcc_columns (a new MVCC state is a new MvccColumns object), so the copy stays valid
   mutable std::mutex device_mutex;
   mutable std::shared_ptr<void> device;
+  mutable uint64_t device_rows = 0;  // rows the copy holds (the chunk's size when it was made)
 };
 
 class Chunk {
@@ -310,7 +312,12 @@ class Chunk {
   explicit Chunk(ChunkColumns columns) : _columns(std::move(columns)) {}
   bool has_mvcc_columns() const { return _mvcc != nullptr; }
   std::shared_ptr<const MvccColumns> mvcc_columns() const { return _mvcc; }
-  void set_mvcc_columns(std::shared_ptr<const MvccColumns> m) { _mvcc = std::move(m); }
+  void set_mvcc_columns(std::shared_ptr<const MvccColumns> m) {
+    // every row of the chunk needs its MVCC entries (validate.cpp:101 iterates chunk_in->size() rows)
+    if (m && (m->tids.size() < size() || m->begin_cids.size() < size() || m->end_cids.size() < size()))
+      throw std::logic_error("MVCC columns shorter than the chunk");
+    _mvcc = std::move(m);
+  }
   size_t size() const { return _columns.empty() ? 0 : _columns[0]->size(); }
   uint16_t column_count() const { return static_cast<uint16_t>(_columns.size()); }
   std::shared_ptr<BaseColumn> get_column(ColumnID id) const { return _columns.at(id); }

@@ -498,7 +498,9 @@ hy_status hy_join_exchange_join_rows(const void* build_records, const uint64_t* 
  *                             owners and receives, sender after sender, the records of its own buckets into
  *                             recv_records (device, recv_capacity records of record_bytes each); recv_counts (host,
  *                             N * n_local_buckets) is exactly the counts matrix step 2 takes; *recv_rows = rows
- *                             received. HY_ERR_CAPACITY (with *recv_rows set, nothing sent) if the buffer is too small.
+ *                             received. The abort decision is collective (one all-reduce of every rank's verdict
+ *                             before any send): if ANY rank's buffer is too small every rank returns HY_ERR_CAPACITY
+ *                             (each with its own *recv_rows set) and nothing is sent, so no rank is left blocked.
  * Asynchronous on `stream` like the other entry points; RCCL's send/recv round is stream-ordered.
  */
 #define HY_COMM_ID_BYTES 128

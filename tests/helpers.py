@@ -112,3 +112,23 @@ def wrap(hy, table):
     w = hy.TableWrapper(table)
     w.execute()
     return w
+
+
+def murmur2_int32_np(keys, seed=17):
+    """MurmurHash2 of 4-byte keys, vectorised (murmur_hash.cpp:21-75 for len = 4; pinned against the golden vectors in
+    test_murmur_golden.py)."""
+    import numpy as np
+
+    m = np.uint32(0x5BD1E995)
+    k = np.ascontiguousarray(keys, dtype=np.int32).view(np.uint32).copy()
+    with np.errstate(over="ignore"):
+        k *= m
+        k ^= k >> np.uint32(24)
+        k *= m
+        h = np.full(k.shape, np.uint32(seed ^ 4), dtype=np.uint32)
+        h *= m
+        h ^= k
+        h ^= h >> np.uint32(13)
+        h *= m
+        h ^= h >> np.uint32(15)
+    return h

@@ -80,3 +80,14 @@ def test_string_murmur_matches_reference_file(hy):
     fn.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32]
     for s in [b"", b"a", b"ab", b"abc", b"abcd", b"This", b"is a test", b"CCCCCCCCCCCCCCC", bytes(range(1, 200))]:
         assert hy.capi.lib.hy_murmur2_bytes(s, len(s), 17) == fn(s, len(s), 17), s
+
+
+def test_numpy_murmur_matches_golden_and_oracle(oracle):
+    """The vectorised numpy restatement the size tests use as their checker (helpers.murmur2_int32_np)."""
+    from helpers import murmur2_int32_np
+
+    keys = [int(k) for k in GOLD["int32"]]
+    assert murmur2_int32_np(np.array(keys)).tolist() == [int(v, 16) for v in GOLD["int32"].values()]
+    rng = np.random.default_rng(5)
+    sweep = rng.integers(-(2**31), 2**31, 500).astype(np.int32)
+    assert murmur2_int32_np(sweep).tolist() == [oracle.murmur2_int32(int(k), 17) for k in sweep]
