@@ -134,6 +134,11 @@ def main_q3(args):
     import numpy as np
     import torch
 
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 or os.environ.get("HY_BENCH_DIST"):
+        # N ranks: the distributed plan through the JoinHash radix shuffle (bench_q3_dist.py)
+        import bench_q3_dist
+
+        return bench_q3_dist.main_q3_dist(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -229,6 +229,13 @@ _sigs = {
                                             ctypes.c_void_p]),
     "hy_decode_frame_of_reference": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,
                                                     ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
+    "hy_exchange_record_row_ids": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                                                  ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
+    "hy_exchange_records_localize": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p,
+                                                    ctypes.c_void_p, ctypes.c_void_p]),
+    "hy_table_scan_row_ids": (ctypes.c_int, [ctypes.POINTER(ScanChunk), ctypes.c_uint32, ctypes.c_int32, ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_size_t, ctypes.c_void_p]),
     "hy_pos_list_null_positions": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
                                                   ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
 }

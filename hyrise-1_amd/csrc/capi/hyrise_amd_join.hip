@@ -246,13 +246,23 @@ hy_status plan_row_side(const hy_join_side* side, const hy_join_filter* filter, 
   if (params->radix_bits > 24) return fail(HY_ERR_UNSUPPORTED, "radix_bits > 24");
   hy_status st = plan_side(side, p);
   if (st != HY_OK) return st;
-  for (const auto& c : p.chunks)
-    if (c.pos_list) return fail(HY_ERR_UNSUPPORTED, "row-index exchange records need a data-table side");
+  // A reference side (a PosList per chunk, e.g. an earlier join's output) takes part with its rows dereferenced
+  // (write_output_columns, join_hash.cpp:584-592): the payload is then the row of the referenced data table.
+  const bool ref = !p.referenced.empty();
+  if (ref && !side->fuse_dereference)
+    return fail(HY_ERR_UNSUPPORTED, "row-index exchange records of a reference side need fuse_dereference");
+  if (ref && filter) return fail(HY_ERR_UNSUPPORTED, "a fused scan needs a data-table side");
+  p.fuse = ref ? 1 : 0;
   st = plan_filter(filter, p, side->value_type, params->hashed_type);
   if (st != HY_OK) return st;
-  if (p.n_rows + row_base >= (p.filtered ? 0x7FFFFFFFull : 0xFFFFFFFFull))
+  const uint64_t rows = ref ? p.ref_row_begin.back() : p.n_rows;
+  if (rows + row_base >= (p.filtered ? 0x7FFFFFFFull : 0xFFFFFFFFull))
     return fail(HY_ERR_UNSUPPORTED, "global row indexes exceed the 32-bit record payload");
-  for (auto& c : p.chunks) c.row_begin += row_base;  // payload = global row index
+  if (ref) {
+    for (auto& r : p.ref_row_begin) r += row_base;  // payload = global row of the referenced table
+  } else {
+    for (auto& c : p.chunks) c.row_begin += row_base;  // payload = global row index
+  }
   w = digit_plan(params->radix_bits, ceil_log2(n_ranks));
   if (w.empty() || (1u << w[0]) < n_ranks) return fail(HY_ERR_UNSUPPORTED, "radix bits too few for the ranks");
   return HY_OK;
@@ -411,6 +421,78 @@ hy_status hy_join_exchange_join_rows(const void* build_records, const uint64_t* 
 uint32_t hy_join_exchange_bucket_bits(uint32_t radix_bits, uint32_t n_ranks) {
   const auto w = digit_plan(radix_bits, ceil_log2(std::max<uint32_t>(1, n_ranks)));
   return w.empty() ? 0u : w[0];
+}
+
+}  // extern "C"
+
+// ---- columns carried with the exchange (include/hyrise_amd.h) ----
+namespace {
+
+__global__ void record_row_ids_kernel(const uint32_t* __restrict__ payloads, uint32_t stride_words, uint64_t n,
+                                      uint64_t row_base, hyk::RowMap m, hy_row_id* __restrict__ out) {
+  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const uint32_t p = payloads[i * stride_words];
+    out[i] = p == hyk::NULL_PAYLOAD ? hy_row_id{0xFFFFFFFFu, 0xFFFFFFFFu}
+                                    : hyk::map_row(m, static_cast<uint32_t>(p - row_base));
+  }
+}
+
+template <typename K>
+__global__ void localize_kernel(char* __restrict__ records, uint32_t record_bytes, uint64_t n, K* __restrict__ keys,
+                                uint32_t* __restrict__ old_payloads) {
+  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    char* r = records + i * record_bytes;
+    uint32_t* pay = reinterpret_cast<uint32_t*>(r + record_bytes / 2);
+    if (keys) keys[i] = *reinterpret_cast<const K*>(r);
+    if (old_payloads) old_payloads[i] = *pay;
+    *pay = static_cast<uint32_t>(i);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+hy_status hy_exchange_record_row_ids(const void* records, uint64_t n, uint32_t record_bytes, uint64_t row_base,
+                                     const uint32_t* chunk_sizes, uint32_t n_chunks, hy_row_id* out_row_ids,
+                                     hy_stream_t stream) {
+  if (record_bytes != 8 && record_bytes != 16) return fail(HY_ERR_INVALID_ARGUMENT, "record_bytes");
+  if (n == 0) return HY_OK;
+  if (!records || !out_row_ids || !chunk_sizes || n_chunks == 0) return fail(HY_ERR_INVALID_ARGUMENT, "null argument");
+  hipStream_t s = S(stream);
+  const std::vector<uint64_t> rb = layout_rows(chunk_sizes, n_chunks);
+  if (rb.back() >= 0xFFFFFFFFull) return fail(HY_ERR_UNSUPPORTED, "table exceeds 2^32-1 rows");
+  // the chunk prefix lives on the device for the non-uniform case; a small allocation per call
+  void* d_rb = nullptr;
+  HY_HIP(hipMallocAsync(&d_rb, 8 * rb.size(), s));
+  HY_STAGE(d_rb, rb.data(), 8 * rb.size(), s);
+  const hyk::RowMap m = make_map(static_cast<const uint64_t*>(d_rb), rb);
+  const auto* pay = reinterpret_cast<const uint32_t*>(static_cast<const char*>(records) + record_bytes / 2);
+  hipLaunchKernelGGL(record_row_ids_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, pay, record_bytes / 4, n, row_base,
+                     m, out_row_ids);
+  HY_HIP(hipGetLastError());
+  HY_HIP(hipFreeAsync(d_rb, s));
+  return HY_OK;
+}
+
+hy_status hy_exchange_records_localize(void* records, uint64_t n, uint32_t record_bytes, void* keys,
+                                       uint32_t* old_payloads, hy_stream_t stream) {
+  if (record_bytes != 8 && record_bytes != 16) return fail(HY_ERR_INVALID_ARGUMENT, "record_bytes");
+  if (n == 0) return HY_OK;
+  if (!records) return fail(HY_ERR_INVALID_ARGUMENT, "records");
+  if (n >= 0xFFFFFFFFull) return fail(HY_ERR_UNSUPPORTED, "more than 2^32-1 records");
+  hipStream_t s = S(stream);
+  auto* r = static_cast<char*>(records);
+  if (record_bytes == 8)
+    hipLaunchKernelGGL(localize_kernel<uint32_t>, dim3(grid_for(n, 256)), dim3(256), 0, s, r, 8u, n,
+                       static_cast<uint32_t*>(keys), old_payloads);
+  else
+    hipLaunchKernelGGL(localize_kernel<uint64_t>, dim3(grid_for(n, 256)), dim3(256), 0, s, r, 16u, n,
+                       static_cast<uint64_t*>(keys), old_payloads);
+  HY_HIP(hipGetLastError());
+  return HY_OK;
 }
 
 }  // extern "C"

@@ -64,6 +64,54 @@ def exchange_records(dist, records, bucket_counts, rank, world, device=None, rec
     return out, recv_matrix
 
 
+def exchange_columns(dist, columns, bucket_counts, rank, world, per_row=None):
+    """Routes this rank's exchange records AND the columns carried with them (include/hyrise_amd.h, "Columns carried
+    with the exchange"): every tensor in `columns` has one row per record, in record order (rows grouped by bucket as
+    step 1 wrote them; per_row[j] elements per row, default 1, e.g. 2 int64 words of 16-byte records). One all_gather
+    of the counts, one all_to_all_single per column with the same row splits. Returns (received columns,
+    recv_matrix)."""
+    import torch
+
+    dev = columns[0].device
+    counts = torch.as_tensor(np.asarray(bucket_counts, dtype=np.int64), device=dev)
+    gathered = [torch.empty_like(counts) for _ in range(world)]
+    dist.all_gather(gathered, counts)
+    send, recv, recv_matrix = exchange_plan(np.stack([g.cpu().numpy() for g in gathered]), rank, world)
+    n_send = sum(send)
+    out = []
+    for j, t in enumerate(columns):
+        per = per_row[j] if per_row else 1
+        r = torch.empty(sum(recv) * per, dtype=t.dtype, device=dev)
+        dist.all_to_all_single(r, t[: n_send * per].contiguous(), [x * per for x in recv], [x * per for x in send])
+        out.append(r)
+    return out, recv_matrix
+
+
+def exchange_columns_in_process(all_columns, all_counts, per_row=None):
+    """The same routing for N ranks simulated in one process (tests on one GPU): all_columns[r] = rank r's columns,
+    all_counts[r] = its bucket counts. Returns per rank (received columns, recv_matrix)."""
+    import torch
+
+    world = len(all_columns)
+    all_counts = np.stack([np.asarray(c, dtype=np.int64) for c in all_counts])
+    n_buckets = all_counts.shape[1]
+    out = []
+    for d in range(world):
+        lo, hi = owned_buckets(n_buckets, d, world)
+        _, _, recv_matrix = exchange_plan(all_counts, d, world)
+        cols = []
+        for j in range(len(all_columns[0])):
+            parts = []
+            for s in range(world):
+                t = all_columns[s][j]
+                per = per_row[j] if per_row else 1
+                b0, b1 = int(all_counts[s, :lo].sum()), int(all_counts[s, :hi].sum())
+                parts.append(t[b0 * per:b1 * per])
+            cols.append(torch.cat(parts) if parts else all_columns[0][j][:0])
+        out.append((cols, recv_matrix))
+    return out
+
+
 class RcclExchange:
     """The exchange step through the C-ABI's own RCCL communicator (hy_comm_init, hy_join_exchange_counts,
     hy_join_exchange_records): what a C++ Hyrise process linking libhyrise_amd.so calls. torch.distributed only hands

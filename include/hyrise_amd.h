@@ -464,6 +464,9 @@ uint32_t hy_join_exchange_bucket_bits(uint32_t radix_bits, uint32_t n_ranks);
  * hy_scan_join_hash; its out_offsets / out_chunk_begin receive the scan output of this shard).
  * hy_join_exchange_join_rows is step 2; the global tables' chunk layouts (chunk sizes in global chunk-id order) turn
  * the received row indexes into the output RowIDs {global chunk id, offset}.
+ * A reference side (an earlier operator's output: one PosList per chunk) takes part with fuse_dereference set: its
+ * records carry the REFERENCED table's row (row_base + the row's index in side->referenced, chunks in order), as
+ * write_output_columns dereferences a reference input (join_hash.cpp:584-592); no fused scan on such a side.
  */
 uint32_t hy_join_exchange_row_record_bytes(int32_t hashed_type);
 hy_status hy_scan_join_exchange_partition_workspace_size(const hy_join_side* side, const hy_join_filter* filter,
@@ -486,6 +489,28 @@ hy_status hy_join_exchange_join_rows(const void* build_records, const uint64_t* 
                                      hy_row_id* out_build, hy_row_id* out_probe, uint64_t out_capacity,
                                      uint64_t* partition_begin, uint32_t* partition_counts, hy_join_result* result,
                                      void* workspace, size_t workspace_bytes, hy_stream_t stream);
+
+/*
+ * Columns carried with the exchange (late materialisation across ranks). A distributed plan above a JoinHash needs
+ * column values of rows that live on other ranks (TPC-H 3's projection reads o_orderdate / o_shippriority of the
+ * build rows and l_extendedprice / l_discount of the probe rows, tpch_queries.cpp:101-106). The sender evaluates
+ * them for its own records and ships them beside the records, in record order, with the same split sizes; the
+ * receiver addresses them by the record's position in its receive buffer:
+ *   hy_exchange_record_row_ids   sender: RowIDs {chunk, offset} of the records' payload rows (payload - row_base in
+ *                                a table whose chunks have chunk_sizes) in record order - a PosList for hy_projection,
+ *                                which then evaluates any column / expression of the shard in record order.
+ *   hy_exchange_records_localize receiver: payload[i] := i (the record's position), after saving the old payloads to
+ *                                old_payloads and the keys (hashed type, 4 or 8 bytes) to keys (each may be NULL).
+ *                                hy_join_exchange_join_rows over the localized records with a layout of uniform chunks
+ *                                over the receive buffer then emits RowIDs {position / chunk, position % chunk} into
+ *                                the "received table", whose columns are the received attribute arrays.
+ * record_bytes: hy_join_exchange_row_record_bytes(hashed type) (payload at byte offset record_bytes / 2).
+ */
+hy_status hy_exchange_record_row_ids(const void* records, uint64_t n, uint32_t record_bytes, uint64_t row_base,
+                                     const uint32_t* chunk_sizes, uint32_t n_chunks, hy_row_id* out_row_ids,
+                                     hy_stream_t stream);
+hy_status hy_exchange_records_localize(void* records, uint64_t n, uint32_t record_bytes, void* keys,
+                                       uint32_t* old_payloads, hy_stream_t stream);
 
 /*
  * The exchange step between step 1 and step 2 over RCCL (xGMI), so that a C++ process runs the distributed join

@@ -174,7 +174,7 @@ def test_fused_equals_unfused_at_sf10(hy):
         referenced[c].data = ldev.ptr.value + 4 * c * chunk
         referenced[c].size = descs[c].size
         referenced[c].kind = capi.HY_COL_VALUE
-    for k, c in enumerate(nz):
+    for k, c in enumerate(nz.tolist()):
         pchunks[k].pos_list = rows.ptr.value + 8 * c * chunk
         pchunks[k].size = int(cnt[c])
         pchunks[k].chunk_id = k
