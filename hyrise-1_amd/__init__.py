@@ -51,6 +51,7 @@ TableWrapper = _host.TableWrapper
 TableScan = _host.TableScan
 ColumnParameter = _host.ColumnParameter
 Validate = _host.Validate
+TransactionContext = _host.TransactionContext
 MAX_COMMIT_ID = _host.MAX_COMMIT_ID
 JoinHash = _host.JoinHash
 Aggregate = _host.Aggregate

@@ -243,6 +243,7 @@ struct SideBufs {
   hyk::Rec<H, P>* recA;
   hyk::Rec<H, P>* recB;      // filtered sides: first the gapped per-span records of part1_compact
   uint32_t* span_count;      // filtered sides: matches per pass-0 span
+  uint64_t* mbits;           // filtered sides: the fused scan's match ballots (part1_mask), one per (tile, wave, item)
   uint8_t* digA;             // next-pass digit bytes beside recA / recB (sides with more than one pass)
   uint8_t* digB;
   uint32_t* segA;            // segment / partition bounds, ping-pong (2^bits + 1 entries)
@@ -301,6 +302,7 @@ void carve_side(Carver& cv, const SideSizes& z, uint32_t bits, const std::vector
   b.recA = own_recA ? cv.take<hyk::Rec<H, P>>(std::max<uint64_t>(1, z.rows)) : nullptr;
   b.recB = cv.take<hyk::Rec<H, P>>(std::max<uint64_t>(1, z.filtered ? std::max(z.rows, z.tiles1 * z.sub * hyk::PART_TILE) : z.rows));
   b.span_count = z.filtered ? cv.take<uint32_t>(std::max<uint64_t>(1, z.tiles1)) : nullptr;
+  b.mbits = z.filtered ? cv.take<uint64_t>(std::max<uint64_t>(1, z.tiles1 * z.sub * hyk::MASK_WORDS)) : nullptr;
   b.digA = z.digit_bytes ? cv.take<uint8_t>(std::max<uint64_t>(16, z.rows)) : nullptr;
   b.digB = z.digit_bytes ? cv.take<uint8_t>(std::max<uint64_t>(16, z.rows)) : nullptr;
   const uint64_t parts = (uint64_t(1) << bits) + 1;
@@ -388,13 +390,51 @@ inline int filter_kind(const SidePlan& p) {
   return width == 2 ? hyk::FK_DICT16 : width == 4 ? hyk::FK_DICT32 : width == 1 ? hyk::FK_DICT8 : hyk::FK_ANY;
 }
 
-// Pass 0 of a side with a fused TableScan: part1_compact (predicate + join column -> gapped row-order records in
-// recB, histograms, span counts), the histogram scan, then part1_spread (scan output + stable scatter into `out`).
+// The fused scan's pass 0 through gapped records (part1_compact / part1_spread) instead of match bits: opt-in A/B.
+inline bool filter_compact_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("HY_FILTER_COMPACT");
+    return e && std::strtol(e, nullptr, 10) != 0;
+  }();
+  return v;
+}
+
+// Pass 0 of a side with a fused TableScan: part1_mask (predicate + join column -> histograms with the scan-match row,
+// match bits), the histogram scan, then part1_spread_mask (scan output + compaction in LDS + stable scatter into
+// `out`). HY_FILTER_COMPACT=1: part1_compact (gapped row-order records in recB) + part1_spread instead.
 template <typename T, typename H, int LP, int FK>
 hy_status launch_filtered_pass0(const char* side_tag, const SidePlan& p, const hyk::Side& sd, const hyk::Digit& d0,
                                 const hyk::NextDigit& nd, uint32_t w0, uint32_t n_digits, SideBufs<H, uint32_t>& b,
                                 const Common& c, hipStream_t s, hyk::Rec<H, uint32_t>* out) {
   const dim3 grid(static_cast<uint32_t>(p.n_tiles1));
+  if (!filter_compact_enabled() && (p.sub == 1 || p.sub == 2)) {
+    {
+      KTimer kt_((std::string("part1_mask.") + side_tag).c_str(), s, p.n_rows);
+      hipLaunchKernelGGL((hyk::part1_mask<T, H, LP, FK>), grid, dim3(hyk::PART_THREADS), 0, s, sd, d0, n_digits,
+                         b.hist, b.mbits);
+      kt_.done();
+    }
+    HY_HIP(hipGetLastError());
+    hy_status st = run_scan(b.hist, b.off, uint64_t(n_digits + 1) * p.n_tiles1, c, s, b.grand_total);
+    if (st != HY_OK) return st;
+    hipLaunchKernelGGL(hyk::fused_scan_totals, dim3(grid_for(p.chunks.size() + 1, 256)), dim3(256), 0, s, b.off,
+                       p.n_tiles1, n_digits, b.grand_total, b.tile_begin, static_cast<uint32_t>(p.chunks.size()),
+                       b.total, p.scan_chunk_begin);
+    HY_HIP(hipGetLastError());
+    const hyk::Side& sd2 = sd;
+    {
+      KTimer kt_((std::string("part1_spread.") + side_tag).c_str(), s, p.n_rows);
+      if (p.sub == 2)
+        hipLaunchKernelGGL((hyk::part1_spread_mask<T, H, LP, 2>), grid, dim3(hyk::PART_THREADS), 0, s, sd2, d0, nd,
+                           n_digits, b.off, b.mbits, out);
+      else
+        hipLaunchKernelGGL((hyk::part1_spread_mask<T, H, LP, 1>), grid, dim3(hyk::PART_THREADS), 0, s, sd2, d0, nd,
+                           n_digits, b.off, b.mbits, out);
+      kt_.done();
+    }
+    HY_HIP(hipGetLastError());
+    return HY_OK;
+  }
   {
     KTimer kt_((std::string("part1_compact.") + side_tag).c_str(), s, p.n_rows);
     hipLaunchKernelGGL((hyk::part1_compact<T, H, LP, FK>), grid, dim3(hyk::PART_THREADS), 0, s, sd, d0, n_digits,
@@ -800,6 +840,7 @@ void carve_onepass(Carver& cv, const SidePlan& p, uint32_t bits, const std::vect
   b.recA = cv.take<hyk::Rec<H>>(std::max<uint64_t>(1, g.gapped));
   b.recB = cv.take<hyk::Rec<H>>(std::max<uint64_t>(1, p.n_rows));
   b.span_count = nullptr;
+  b.mbits = nullptr;
   b.digA = cv.take<uint8_t>(std::max<uint64_t>(16, g.gapped));
   b.digB = cv.take<uint8_t>(std::max<uint64_t>(16, p.n_rows));
   const uint64_t parts = (uint64_t(1) << bits) + 1;

@@ -300,7 +300,13 @@ PYBIND11_MODULE(_hyrise_host, m) {
       .def("get_output", [](const AbstractOperator& o) { return std::const_pointer_cast<Table>(o.get_output()); })
       .def("name", &AbstractOperator::name)
       .def("description", &AbstractOperator::description)
-      .def("performance_data", &AbstractOperator::performance_data);
+      .def("performance_data", &AbstractOperator::performance_data)
+      // the operator holds its context weakly (abstract_operator.cpp:95-98); Python keeps it alive with the operator
+      .def(
+          "set_transaction_context",
+          [](AbstractOperator& o, std::shared_ptr<TransactionContext> c) { o.set_transaction_context(c); },
+          py::keep_alive<1, 2>())
+      .def("transaction_context", &AbstractOperator::transaction_context);
 
   py::class_<TableWrapper, AbstractOperator, std::shared_ptr<TableWrapper>>(m, "TableWrapper")
       .def(py::init<std::shared_ptr<const Table>>());
@@ -317,9 +323,14 @@ PYBIND11_MODULE(_hyrise_host, m) {
            py::arg("input"), py::arg("column_id"), py::arg("predicate_condition"), py::arg("value"))
       .def("set_excluded_chunk_ids", &TableScan::set_excluded_chunk_ids);
 
+  py::class_<TransactionContext, std::shared_ptr<TransactionContext>>(m, "TransactionContext")
+      .def(py::init<uint32_t, uint32_t>(), py::arg("transaction_id"), py::arg("snapshot_commit_id"))
+      .def("transaction_id", &TransactionContext::transaction_id)
+      .def("snapshot_commit_id", &TransactionContext::snapshot_commit_id)
+      .def("aborted", &TransactionContext::aborted)
+      .def("set_aborted", &TransactionContext::set_aborted);
   py::class_<Validate, AbstractOperator, std::shared_ptr<Validate>>(m, "Validate")
-      .def(py::init<std::shared_ptr<AbstractOperator>, uint32_t, uint32_t>(), py::arg("input"),
-           py::arg("transaction_id"), py::arg("snapshot_commit_id"));
+      .def(py::init<std::shared_ptr<AbstractOperator>>(), py::arg("input"));
   m.attr("MAX_COMMIT_ID") = MvccColumns::MAX_COMMIT_ID;
   py::class_<JoinHash, AbstractOperator, std::shared_ptr<JoinHash>>(m, "JoinHash")
       .def(py::init([](std::shared_ptr<AbstractOperator> l, std::shared_ptr<AbstractOperator> r, JoinMode mode,

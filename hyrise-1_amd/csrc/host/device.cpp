@@ -221,4 +221,18 @@ std::shared_ptr<PosList> pos_list_from_device(std::shared_ptr<DeviceBuffer> rows
   return pl;
 }
 
+std::shared_ptr<PosList> pos_list_from_device(OutputArena& arena, std::shared_ptr<DeviceBuffer> rows, uint64_t offset,
+                                              uint64_t n) {
+  arena.lists->emplace_back();
+  PosList& pl = arena.lists->back();
+  pl.make_lazy(n, &fetch_pos_list);
+  arena.mirrors->emplace_back();
+  DevicePosList& d = arena.mirrors->back();
+  d.size = n;
+  d.rows = std::move(rows);
+  d.view_offset = offset;
+  pl.set_device_mirror(std::shared_ptr<DevicePosList>(arena.mirrors, &d));
+  return std::shared_ptr<PosList>(arena.lists, &pl);
+}
+
 }  // namespace hyrise

@@ -6,6 +6,7 @@
 // like the reference's Fail (src/lib/utils/assert.hpp:49-70).
 #pragma once
 
+#include <deque>
 #include <memory>
 #include <string>
 #include <vector>
@@ -83,6 +84,30 @@ struct DevicePosList {
 // Returns (creating on first use) the device mirror of a data column chunk. String columns are only resident as
 // dictionary attribute vectors (dictionary stays on the host).
 std::shared_ptr<DeviceColumn> device_column(const BaseColumn& column);
+
+// Output objects of an operator that emits many chunks (JoinHash: one per radix partition, 65,536 at SF100): the
+// chunks, their columns, PosLists and the PosLists' device mirrors live in four arenas (deques: elements never move);
+// the shared_ptrs handed out alias an arena's control block (no allocation, no control block per object). The arenas
+// own each other in one direction only - chunks -> columns -> PosLists -> mirrors - so the last chunk released frees
+// them all.
+struct OutputArena {
+  std::shared_ptr<std::deque<DevicePosList>> mirrors = std::make_shared<std::deque<DevicePosList>>();
+  std::shared_ptr<std::deque<PosList>> lists = std::make_shared<std::deque<PosList>>();
+  std::shared_ptr<std::deque<ReferenceColumn>> columns = std::make_shared<std::deque<ReferenceColumn>>();
+  std::shared_ptr<std::deque<Chunk>> chunks = std::make_shared<std::deque<Chunk>>();
+};
+// A lazy PosList in the arena over rows [offset, offset + n) of a device RowID array.
+std::shared_ptr<PosList> pos_list_from_device(OutputArena& arena, std::shared_ptr<DeviceBuffer> rows, uint64_t offset,
+                                              uint64_t n);
+inline std::shared_ptr<ReferenceColumn> arena_reference_column(OutputArena& arena, std::shared_ptr<const Table> table,
+                                                               ColumnID column, std::shared_ptr<const PosList> pos_list) {
+  arena.columns->emplace_back(std::move(table), column, std::move(pos_list));
+  return std::shared_ptr<ReferenceColumn>(arena.columns, &arena.columns->back());
+}
+inline std::shared_ptr<Chunk> arena_chunk(OutputArena& arena, ChunkColumns columns) {
+  arena.chunks->emplace_back(std::move(columns));
+  return std::shared_ptr<Chunk>(arena.chunks, &arena.chunks->back());
+}
 
 // Returns (uploading on first use) the device mirror of a PosList.
 std::shared_ptr<DevicePosList> device_pos_list(const PosList& pos_list);

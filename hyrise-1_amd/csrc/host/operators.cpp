@@ -33,7 +33,15 @@ void AbstractOperator::execute() {
   Assert(!_input_right || _input_right->get_output(), "Right input has not been executed");
   Assert(!_output, "Operator has already been executed");
   const auto t0 = std::chrono::steady_clock::now();
-  _output = _on_execute();
+  // abstract_operator.cpp:32-48: an aborted transaction skips the operator (empty output of the input's shape)
+  const auto context = transaction_context();
+  if (context && context->aborted()) {
+    _output = std::make_shared<Table>(_input_left ? _input_left->get_output()->column_definitions()
+                                                  : std::vector<TableColumnDefinition>{},
+                                      TableType::Data);
+    return;
+  }
+  _output = _on_execute(context);
   _on_cleanup();
   _performance_data.walltime_ns = static_cast<uint64_t>(
       std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count());
@@ -430,6 +438,9 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
   }
 
   // ---- reference-table input (base_single_column_table_scan_impl.cpp:36-60, table_scan.cpp:104-145) ----
+  // the referenced chunks' descriptors (dictionary rewrite, LIKE id sets uploaded) once per referenced table and column,
+  // not once per input chunk
+  std::map<std::pair<const Table*, ColumnID>, std::vector<hy_scan_chunk>> rdescs;
   for (ChunkID c = 0; c < in_table->chunk_count(); ++c) {
     if (excluded[c]) continue;
     const auto chunk = in_table->get_chunk(c);
@@ -439,25 +450,33 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
     if (pos_list.empty()) continue;
     const auto& rtable = ref->referenced_table();
     const ColumnID rcol = ref->referenced_column_id();
-    std::vector<hy_scan_chunk> rdesc(rtable->chunk_count());
-    for (ChunkID r = 0; r < rtable->chunk_count(); ++r)
-      rdesc[r] = scan_descriptor(*rtable->get_chunk(r)->get_column(rcol), col_type, _predicate_condition, _right_value,
-                                 &keep);
+    auto& rdesc = rdescs[{rtable.get(), rcol}];
+    if (rdesc.empty()) {
+      rdesc.resize(rtable->chunk_count());
+      for (ChunkID r = 0; r < rtable->chunk_count(); ++r)
+        rdesc[r] = scan_descriptor(*rtable->get_chunk(r)->get_column(rcol), col_type, _predicate_condition,
+                                   _right_value, &keep);
+    }
     const auto constant = null_test || like ? ScanConstant{} : typed_constant(col_type, _right_value);
     const auto dpl = device_pos_list(pos_list);
     const uint64_t m = pos_list.size();
 
-    // distinct referenced chunks in order of first appearance -> the reference's unordered_map iteration order
-    DeviceBuffer first(std::max<size_t>(rtable->chunk_count(), 1) * 8, s);
-    hy_check(hy_pos_list_chunk_first_seen(dpl->ptr(), m, rtable->chunk_count(), first.as<uint64_t>(), s),
-             "hy_pos_list_chunk_first_seen");
-    std::vector<uint64_t> h_first(rtable->chunk_count());
-    hy_check(hy_memcpy_dtoh(h_first.data(), first.get(), 8 * h_first.size(), s), "dtoh");
-    hy_check(hy_stream_synchronize(s), "sync");
+    // distinct referenced chunks in order of first appearance -> the reference's unordered_map iteration order; a
+    // PosList whose producer knows its only chunk (a TableScan's output) is one group without a device pass
     std::vector<ChunkID> seen;
-    for (ChunkID r = 0; r < h_first.size(); ++r)
-      if (h_first[r] != ~0ull) seen.push_back(r);
-    std::sort(seen.begin(), seen.end(), [&](ChunkID a, ChunkID b) { return h_first[a] < h_first[b]; });
+    if (pos_list.single_chunk_id() != INVALID_CHUNK_ID) {
+      seen.push_back(pos_list.single_chunk_id());
+    } else {
+      DeviceBuffer first(std::max<size_t>(rtable->chunk_count(), 1) * 8, s);
+      hy_check(hy_pos_list_chunk_first_seen(dpl->ptr(), m, rtable->chunk_count(), first.as<uint64_t>(), s),
+               "hy_pos_list_chunk_first_seen");
+      std::vector<uint64_t> h_first(rtable->chunk_count());
+      hy_check(hy_memcpy_dtoh(h_first.data(), first.get(), 8 * h_first.size(), s), "dtoh");
+      hy_check(hy_stream_synchronize(s), "sync");
+      for (ChunkID r = 0; r < h_first.size(); ++r)
+        if (h_first[r] != ~0ull) seen.push_back(r);
+      std::sort(seen.begin(), seen.end(), [&](ChunkID a, ChunkID b) { return h_first[a] < h_first[b]; });
+    }
     const auto groups = unordered_map_order(seen);
 
     size_t ws_bytes = 0;
@@ -582,6 +601,13 @@ DeviceMvcc upload_mvcc(const Table& table, hy_stream_t s) {
 }  // namespace
 
 std::shared_ptr<const Table> Validate::_on_execute() {
+  Fail("Validate can't be called without a transaction context.");
+}
+
+std::shared_ptr<const Table> Validate::_on_execute(std::shared_ptr<TransactionContext> transaction_context) {
+  if (!transaction_context) return _on_execute();
+  const uint32_t _transaction_id = transaction_context->transaction_id();
+  const uint32_t _snapshot_commit_id = transaction_context->snapshot_commit_id();
   const auto in_table = input_table_left();
   auto output = std::make_shared<Table>(in_table->column_definitions(), TableType::References);
   if (in_table->chunk_count() == 0) return output;
@@ -917,23 +943,23 @@ int32_t join_mode(JoinMode m) {
 // write_output_columns (join_hash.cpp:564-613) for one side of one partition. PosLists are lazy views: of the
 // join's output RowIDs, or - for a reference input - of that side's RowIDs dereferenced through one PosList group,
 // computed once for all partitions (rows [0, rows_used) of the output buffer) by a single launch.
-void write_output_columns(ChunkColumns& out, const std::shared_ptr<const Table>& input_table, const JoinSideInput& side,
-                          const std::shared_ptr<DeviceBuffer>& rows, uint64_t offset, uint64_t n, uint64_t rows_used,
-                          std::map<std::pair<int, uint64_t>, std::shared_ptr<PosList>>& cache,
+void write_output_columns(ChunkColumns& out, OutputArena& arena, const std::shared_ptr<const Table>& input_table,
+                          const JoinSideInput& side, const std::shared_ptr<DeviceBuffer>& rows, uint64_t offset,
+                          uint64_t n, uint64_t rows_used, std::map<std::pair<int, uint64_t>, std::shared_ptr<PosList>>& cache,
                           std::vector<std::shared_ptr<DeviceBuffer>>& group_ptr_arrays,
                           std::vector<std::shared_ptr<DeviceBuffer>>& group_deref,
                           std::shared_ptr<Table>& dummy_table) {
   if (input_table->type() == TableType::Data) {
-    auto pl = pos_list_from_device(rows, offset, n);
+    auto pl = pos_list_from_device(arena, rows, offset, n);
     for (ColumnID col = 0; col < input_table->column_count(); ++col)
-      out.push_back(std::make_shared<ReferenceColumn>(input_table, col, pl));
+      out.push_back(arena_reference_column(arena, input_table, col, pl));
     return;
   }
   if (input_table->chunk_count() == 0) {
     if (!dummy_table) dummy_table = Table::create_dummy_table(input_table->column_definitions());
-    auto pl = pos_list_from_device(rows, offset, n);
+    auto pl = pos_list_from_device(arena, rows, offset, n);
     for (ColumnID col = 0; col < input_table->column_count(); ++col)
-      out.push_back(std::make_shared<ReferenceColumn>(dummy_table, col, pl));
+      out.push_back(arena_reference_column(arena, dummy_table, col, pl));
     return;
   }
   std::shared_ptr<PosList> fused;
@@ -941,7 +967,7 @@ void write_output_columns(ChunkColumns& out, const std::shared_ptr<const Table>&
     const int g = side.column_group[col];
     std::shared_ptr<PosList> pl;
     if (side.fuse) {
-      if (!fused) fused = pos_list_from_device(rows, offset, n);
+      if (!fused) fused = pos_list_from_device(arena, rows, offset, n);
       pl = fused;
     } else {
       auto& cached = cache[{g, offset}];
@@ -959,12 +985,12 @@ void write_output_columns(ChunkColumns& out, const std::shared_ptr<const Table>&
                                           group_deref[g]->as<hy_row_id>(), s),
                    "hy_dereference_row_ids");
         }
-        cached = pos_list_from_device(group_deref[g], offset, n);
+        cached = pos_list_from_device(arena, group_deref[g], offset, n);
       }
       pl = cached;
     }
     const auto rc = std::static_pointer_cast<const ReferenceColumn>(input_table->get_chunk(0)->get_column(col));
-    out.push_back(std::make_shared<ReferenceColumn>(rc->referenced_table(), rc->referenced_column_id(), pl));
+    out.push_back(arena_reference_column(arena, rc->referenced_table(), rc->referenced_column_id(), pl));
   }
 }
 
@@ -1059,22 +1085,25 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
     used = std::max<uint64_t>(used, h_begin[part] + h_count[part]);
     nonempty.push_back(part);
   }
-  // One output chunk per non-empty partition (join_hash.cpp:829-855), in partition order. (Built serially: on
-  // several host threads the chunks' shared_ptr copies of the same tables and buffers contend on their reference
-  // counts - measured 87 ms against 28 ms serial for 65,536 chunks at SF100.)
+  // One output chunk per non-empty partition (join_hash.cpp:829-855), in partition order. The chunks, columns,
+  // PosLists and mirrors come from one output arena (device.hpp): no allocation or control block per object. (Built
+  // serially: on several host threads the shared_ptr copies of the same tables and buffers contend on their reference
+  // counts - measured 87 ms against 28 ms serial for 65,536 chunks at SF100, before the arena.)
+  OutputArena arena;
   auto build_chunk = [&](uint32_t part) {
     std::map<std::pair<int, uint64_t>, std::shared_ptr<PosList>> bcache, pcache;  // PosLists shared in the chunk
     ChunkColumns cols;
     cols.reserve(output->column_count());
     const uint64_t n = h_count[part], b0 = h_begin[part];
     if (inputs_swapped) {
-      write_output_columns(cols, probe_table, pside, out_p, b0, n, used, pcache, pptrs, pderef, pdummy);
-      if (!semi_anti) write_output_columns(cols, build_table, bside, out_b, b0, n, used, bcache, bptrs, bderef, bdummy);
+      write_output_columns(cols, arena, probe_table, pside, out_p, b0, n, used, pcache, pptrs, pderef, pdummy);
+      if (!semi_anti)
+        write_output_columns(cols, arena, build_table, bside, out_b, b0, n, used, bcache, bptrs, bderef, bdummy);
     } else {
-      write_output_columns(cols, build_table, bside, out_b, b0, n, used, bcache, bptrs, bderef, bdummy);
-      write_output_columns(cols, probe_table, pside, out_p, b0, n, used, pcache, pptrs, pderef, pdummy);
+      write_output_columns(cols, arena, build_table, bside, out_b, b0, n, used, bcache, bptrs, bderef, bdummy);
+      write_output_columns(cols, arena, probe_table, pside, out_p, b0, n, used, pcache, pptrs, pderef, pdummy);
     }
-    return std::make_shared<Chunk>(std::move(cols));
+    return arena_chunk(arena, std::move(cols));
   };
   std::vector<std::shared_ptr<Chunk>> chunks;
   chunks.reserve(nonempty.size());

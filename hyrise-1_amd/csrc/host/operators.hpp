@@ -32,6 +32,23 @@ struct OperatorPerformanceData {
   uint64_t rows_in = 0;
 };
 
+// The part of the reference's TransactionContext (concurrency/transaction_context.hpp) the hot path reads: the
+// transaction's id, its snapshot commit id and whether it aborted (AbstractOperator::execute skips the operator then,
+// abstract_operator.cpp:32-48). Commit / rollback live in the out-of-scope transaction manager.
+class TransactionContext {
+ public:
+  TransactionContext(uint32_t transaction_id, uint32_t snapshot_commit_id)
+      : _transaction_id(transaction_id), _snapshot_commit_id(snapshot_commit_id) {}
+  uint32_t transaction_id() const { return _transaction_id; }
+  uint32_t snapshot_commit_id() const { return _snapshot_commit_id; }
+  bool aborted() const { return _aborted; }
+  void set_aborted() { _aborted = true; }
+
+ private:
+  uint32_t _transaction_id, _snapshot_commit_id;
+  bool _aborted = false;
+};
+
 class AbstractOperator : public std::enable_shared_from_this<AbstractOperator> {
  public:
   AbstractOperator(OperatorType type, std::shared_ptr<const AbstractOperator> left = nullptr,
@@ -53,9 +70,16 @@ class AbstractOperator : public std::enable_shared_from_this<AbstractOperator> {
   std::shared_ptr<const Table> input_table_right() const { return _input_right->get_output(); }
   const OperatorPerformanceData& performance_data() const { return _performance_data; }
 
+  // abstract_operator.cpp:87-97: the operator's transaction (held weakly, as the reference does)
+  void set_transaction_context(const std::weak_ptr<TransactionContext>& context) { _transaction_context = context; }
+  std::shared_ptr<TransactionContext> transaction_context() const { return _transaction_context.lock(); }
+
  protected:
+  // execute() calls the context overload; operators that need no transaction implement the plain one
+  virtual std::shared_ptr<const Table> _on_execute(std::shared_ptr<TransactionContext>) { return _on_execute(); }
   virtual std::shared_ptr<const Table> _on_execute() = 0;
   virtual void _on_cleanup() {}
+  std::weak_ptr<TransactionContext> _transaction_context;
 
   const OperatorType _type;
   std::shared_ptr<const AbstractOperator> _input_left, _input_right;
@@ -116,20 +140,16 @@ class TableScan final : public AbstractOperator {
 
 // Validate (reference operators/validate.cpp:36-95): the input rows visible to one transaction. The reference's
 // TransactionContext enters as its two fields, the transaction id and the snapshot commit id.
+// validate.hpp:18-36: Validate(in), visibility from the operator's TransactionContext (set_transaction_context, as the
+// SQL pipeline does for every operator); without one, _on_execute() fails like the reference's (validate.cpp:45-47).
 class Validate final : public AbstractOperator {
  public:
-  Validate(std::shared_ptr<const AbstractOperator> in, uint32_t transaction_id, uint32_t snapshot_commit_id)
-      : AbstractOperator(OperatorType::Validate, std::move(in)),
-        _transaction_id(transaction_id),
-        _snapshot_commit_id(snapshot_commit_id) {}
+  explicit Validate(std::shared_ptr<const AbstractOperator> in) : AbstractOperator(OperatorType::Validate, std::move(in)) {}
   const std::string name() const override { return "Validate"; }
 
  protected:
+  std::shared_ptr<const Table> _on_execute(std::shared_ptr<TransactionContext> transaction_context) override;
   std::shared_ptr<const Table> _on_execute() override;
-
- private:
-  uint32_t _transaction_id;
-  uint32_t _snapshot_commit_id;
 };
 
 class JoinHash final : public AbstractOperator {

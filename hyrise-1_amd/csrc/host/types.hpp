@@ -20,6 +20,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <initializer_list>
+#include <iterator>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -68,18 +70,47 @@ class PosList;
 // PosList, so code in another shared object (the oracle module) reading it calls the producer's copy routine.
 using PosListFetch = void (*)(const PosList& pos_list, RowID* dst);
 
-// PosList: host vector of RowIDs (the reference's pmr_vector<RowID>) plus an optional device-resident mirror
-// in the same 8-byte layout, so that a downstream GPU operator does not re-upload what an upstream GPU
-// operator produced. A PosList a GPU operator produces is lazy: it knows its size and holds only the device mirror;
-// the host RowIDs are copied down on the first host access (element, iterator or data()), so an operator chain that
-// stays on the device never waits for a device-to-host copy per output chunk.
-class PosList : public std::vector<RowID> {
-  using Base = std::vector<RowID>;
+// PosList: the reference's `using PosList = pmr_vector<RowID>` (types.hpp:138) as a class with the same vector
+// interface (every member the reference's operators call on a PosList: size / empty / operator[] / at / data /
+// begin / end / cbegin / cend / front / back / push_back / emplace_back / reserve / resize / shrink_to_fit / clear /
+// insert / capacity / ==) plus an optional device-resident mirror in the same 8-byte layout, so that a downstream GPU
+// operator does not re-upload what an upstream GPU operator produced. A PosList a GPU operator produces is lazy: it
+// knows its size and holds only the device mirror; the host RowIDs are copied down on the first host access through
+// ANY member. The vector is a private member, not a base class: no access path can see the unfilled storage of a
+// lazy list. Code that needs the std::vector itself takes vector() (host copy made first). INTEGRATION.md 2 lists
+// this as the one type change of the drop-in.
+class PosList {
+  using Vec = std::vector<RowID>;
 
  public:
-  using Base::vector;
+  using value_type = RowID;
+  using size_type = Vec::size_type;
+  using difference_type = Vec::difference_type;
+  using reference = RowID&;
+  using const_reference = const RowID&;
+  using pointer = RowID*;
+  using const_pointer = const RowID*;
+  using iterator = Vec::iterator;
+  using const_iterator = Vec::const_iterator;
+
   PosList() = default;
-  explicit PosList(std::vector<RowID>&& v) : Base(std::move(v)) {}
+  explicit PosList(size_t n) : _v(n) {}
+  PosList(size_t n, const RowID& value) : _v(n, value) {}
+  PosList(std::initializer_list<RowID> l) : _v(l) {}
+  template <typename It, typename = typename std::iterator_traits<It>::iterator_category>
+  PosList(It first, It last) : _v(first, last) {}
+  explicit PosList(Vec&& v) : _v(std::move(v)) {}
+  PosList(const PosList& o) : _v(o.host()), _single_chunk_id(o._single_chunk_id) {}
+  PosList& operator=(const PosList& o) {
+    if (this != &o) {
+      Vec copy = o.host();
+      _v = std::move(copy);
+      _lazy = false;
+      _device.reset();
+      _single_chunk_id = o._single_chunk_id;
+    }
+    return *this;
+  }
 
   // A PosList of n RowIDs that live on the device (its mirror is set by the producer; fetch copies them down).
   static std::shared_ptr<PosList> lazy(size_t n, PosListFetch fetch) {
@@ -90,20 +121,55 @@ class PosList : public std::vector<RowID> {
     return p;
   }
   bool is_lazy() const { return _lazy; }
+  // makes an empty list lazy in place (lists allocated in an operator's output arena)
+  void make_lazy(size_t n, PosListFetch fetch) {
+    _v.clear();
+    _lazy_size = n;
+    _lazy = n > 0;
+    _fetch = fetch;
+  }
 
-  size_t size() const { return _lazy ? _lazy_size : Base::size(); }
+  // sizes need no host copy
+  size_t size() const { return _lazy ? _lazy_size : _v.size(); }
   bool empty() const { return size() == 0; }
+  size_t capacity() const { return _lazy ? _lazy_size : _v.capacity(); }
+  // element and iterator access: the host RowIDs (copied down first when lazy)
   const RowID& operator[](size_t i) const { return host()[i]; }
   RowID& operator[](size_t i) { return host()[i]; }
   const RowID& at(size_t i) const { return host().at(i); }
+  RowID& at(size_t i) { return host().at(i); }
   const RowID* data() const { return host().data(); }
   RowID* data() { return host().data(); }
-  Base::const_iterator begin() const { return host().begin(); }
-  Base::const_iterator end() const { return host().end(); }
-  Base::iterator begin() { return host().begin(); }
-  Base::iterator end() { return host().end(); }
+  const_iterator begin() const { return host().begin(); }
+  const_iterator end() const { return host().end(); }
+  const_iterator cbegin() const { return host().cbegin(); }
+  const_iterator cend() const { return host().cend(); }
+  iterator begin() { return host().begin(); }
+  iterator end() { return host().end(); }
   const RowID& front() const { return host().front(); }
   const RowID& back() const { return host().back(); }
+  RowID& front() { return host().front(); }
+  RowID& back() { return host().back(); }
+  const Vec& vector() const { return host(); }
+  // modifiers: the list becomes a plain host list; a device mirror no longer matches it and is dropped
+  void push_back(const RowID& r) { mutate().push_back(r); }
+  template <typename... A>
+  RowID& emplace_back(A&&... a) {
+    return mutate().emplace_back(std::forward<A>(a)...);
+  }
+  void reserve(size_t n) { host_mut().reserve(n); }
+  void shrink_to_fit() { host_mut().shrink_to_fit(); }
+  void resize(size_t n) { mutate().resize(n); }
+  void resize(size_t n, const RowID& v) { mutate().resize(n, v); }
+  void clear() { mutate().clear(); }
+  template <typename It>
+  iterator insert(const_iterator pos, It first, It last) {
+    const auto off = pos - host().cbegin();
+    auto& v = mutate();
+    return v.insert(v.cbegin() + off, first, last);
+  }
+  bool operator==(const PosList& o) const { return host() == o.host(); }
+  bool operator!=(const PosList& o) const { return !(*this == o); }
 
   std::shared_ptr<DevicePosList> device_mirror() const { return std::atomic_load(&_device); }
   void set_device_mirror(std::shared_ptr<DevicePosList> d) const { std::atomic_store(&_device, std::move(d)); }
@@ -115,20 +181,28 @@ class PosList : public std::vector<RowID> {
   void set_single_chunk_id(ChunkID c) { _single_chunk_id = c; }
 
  private:
-  Base& host() const {
+  Vec& host() const {
     auto& self = const_cast<PosList&>(*this);
     if (_lazy) {
       static std::mutex m;
       std::lock_guard<std::mutex> lock(m);
       if (_lazy) {
-        self.Base::resize(_lazy_size);
-        _fetch(*this, self.Base::data());
+        self._v.resize(_lazy_size);
+        _fetch(*this, self._v.data());
         _lazy = false;
       }
     }
-    return self;
+    return self._v;
+  }
+  Vec& host_mut() { return host(); }
+  Vec& mutate() {
+    Vec& v = host();
+    if (_device) set_device_mirror(nullptr);
+    _single_chunk_id = INVALID_CHUNK_ID;
+    return v;
   }
 
+  Vec _v;
   mutable std::shared_ptr<DevicePosList> _device;
   ChunkID _single_chunk_id = INVALID_CHUNK_ID;
   size_t _lazy_size = 0;

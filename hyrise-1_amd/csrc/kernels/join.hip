@@ -615,7 +615,8 @@ __global__ __launch_bounds__(PART_THREADS) __attribute__((amdgpu_waves_per_eu(4)
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// Pass 1 of a side with a fused TableScan, in two streaming kernels:
+// Pass 1 of a side with a fused TableScan, in two streaming kernels (opt-in, HY_FILTER_COMPACT=1; the default is
+// part1_mask / part1_spread_mask below):
 //   part1_compact: evaluates the predicate and reads the join column of every row of a span once, writes the span's
 //     matching rows as records in row order into the span's own slot of a gapped buffer (slot = span * SPAN
 //     records; no prefix across spans is needed), counts them per digit (histogram rows as part1_hist, plus the scan
@@ -734,6 +735,168 @@ __global__ __launch_bounds__(PART_THREADS) void part1_spread(Side s, Digit dg, N
       dr[k] = (dig << 24) | wave_rank_lds(dig, a, s_mask, s_cnt[w]);
     }
     staged_scatter<H, uint32_t>(recs, act, dr, s_cnt, s_delta, s_stage, s_scratch, n_digits, dg, nd, run, out);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Pass 1 of a side with a fused TableScan, without the gapped record round trip (the default; HY_FILTER_COMPACT=1
+// selects part1_compact / part1_spread above):
+//   part1_mask: the predicate and the join column of every row of a span: digit histogram of the rows that take part
+//     (+ the span's scan-match count as an extra histogram row) and the scan's match bits - one 64-bit ballot per
+//     (tile, wave, item), 1 bit per row. Writes 1/8 B per row instead of an 8-byte record per match.
+//   part1_spread_mask: re-reads the span's join column (the predicate column is not read again: its result is the
+//     bits), writes the scan output (chunk offsets of the matches, row order) and compacts the rows that take part into
+//     LDS in row order; the compacted records are then ranked and scattered by digit in rounds of one tile (stable
+//     LDS-staged scatter, as part1_scatter). Per matched row it moves 4 B of key again instead of the 8-byte record
+//     written and read back.
+// ------------------------------------------------------------------------------------------------------------
+constexpr int MASK_WORDS = PART_WAVES * PART_ITEMS;  // ballots per tile
+
+template <typename T, typename H, int LP, int FK>
+__global__ __launch_bounds__(PART_THREADS) void part1_mask(Side s, Digit dg, uint32_t n_digits,
+                                                          uint32_t* __restrict__ hist,
+                                                          uint64_t* __restrict__ match_bits) {
+  __shared__ uint32_t s_hist[256];
+  __shared__ uint32_t s_wc[PART_WAVES];
+  const uint64_t tile = xcd_tile(blockIdx.x, gridDim.x);  // span
+  for (int i = threadIdx.x; i < 256; i += PART_THREADS) s_hist[i] = 0;
+  const uint32_t c = s.tile_chunk[tile];
+  const SrcChunk ch = s.chunks[c];
+  const uint32_t base = static_cast<uint32_t>(tile - s.chunk_tile_begin[c]) * (s.sub * PART_TILE);
+  const uint32_t n_sub = min(s.sub, (ch.size - base + PART_TILE - 1) / PART_TILE);
+  const int w = threadIdx.x / WAVE, lane = __lane_id();
+  uint32_t matches = 0;  // this wave's scan matches in the span (wave-uniform)
+  __syncthreads();
+#pragma unroll 1
+  for (uint32_t j = 0; j < n_sub; ++j) {
+    const uint32_t rb = base + j * PART_TILE + w * WAVE_SPAN;
+    const uint32_t m = filter_items<FK>(s, c, rb);
+    H keys[PART_ITEMS];
+    uint32_t pays[PART_ITEMS];
+    const uint32_t act = bloom_filter_act<H>(s, keys, load_items<T, H, uint32_t, LP>(s, ch, rb, keys, pays) & m);
+#pragma unroll
+    for (int k = 0; k < PART_ITEMS; ++k)
+      if ((act >> k) & 1u) atomicAdd(&s_hist[digit_of<H>(dg, keys[k])], 1u);
+    uint64_t mine = 0;  // lane k < PART_ITEMS keeps item k's ballot: one coalesced 128-B store per wave
+#pragma unroll
+    for (int k = 0; k < PART_ITEMS; ++k) {
+      const uint64_t b = __ballot((m >> k) & 1u);
+      if (lane == k) mine = b;
+      matches += static_cast<uint32_t>(__popcll(b));
+    }
+    if (lane < PART_ITEMS) match_bits[(tile * s.sub + j) * MASK_WORDS + w * PART_ITEMS + lane] = mine;
+  }
+  if (lane == 0) s_wc[w] = matches;
+  __syncthreads();
+  for (uint32_t d = threadIdx.x; d < n_digits; d += PART_THREADS) hist[d * s.n_tiles + tile] = s_hist[d];
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int ww = 0; ww < PART_WAVES; ++ww) t += s_wc[ww];
+    hist[n_digits * s.n_tiles + tile] = t;
+  }
+}
+
+// SUB: tiles per span (the host's sub_filtered); the LDS holds the span's compacted records (at most SUB tiles).
+template <typename T, typename H, int LP, int SUB>
+__global__ __launch_bounds__(PART_THREADS) void part1_spread_mask(Side s, Digit dg, NextDigit nd, uint32_t n_digits,
+                                                                 const uint32_t* __restrict__ offsets,
+                                                                 const uint64_t* __restrict__ match_bits,
+                                                                 Rec<H, uint32_t>* __restrict__ out) {
+  static_assert(SUB >= 1 && SUB * PART_TILE * sizeof(Rec<H, uint32_t>) >= PART_WAVES * 256 * 8, "mask area");
+  __shared__ uint32_t s_cnt[PART_WAVES][256];
+  __shared__ uint32_t s_delta[256];
+  __shared__ uint32_t s_scratch[PART_WAVES + 1];
+  __shared__ uint32_t s_wm[PART_WAVES], s_wa[PART_WAVES];
+  __shared__ Rec<H, uint32_t> s_comp[SUB * PART_TILE];  // the span's compacted records; rounds stage in its front
+  const uint64_t tile = xcd_tile(blockIdx.x, gridDim.x);  // span
+  const uint32_t c = s.tile_chunk[tile];
+  const SrcChunk ch = s.chunks[c];
+  const uint32_t base = static_cast<uint32_t>(tile - s.chunk_tile_begin[c]) * (SUB * PART_TILE);
+  const uint32_t n_sub = min(static_cast<uint32_t>(SUB), (ch.size - base + PART_TILE - 1) / PART_TILE);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE), lane = __lane_id();
+  uint32_t run = threadIdx.x < n_digits ? offsets[threadIdx.x * s.n_tiles + tile] : 0u;
+  uint32_t scan_pos = offsets[n_digits * s.n_tiles + tile] - offsets[n_digits * s.n_tiles];  // span's first match
+  uint32_t comp_n = 0;
+#pragma unroll 1
+  for (uint32_t j = 0; j < n_sub; ++j) {
+    const uint32_t rb = base + j * PART_TILE + w * WAVE_SPAN;
+    const uint64_t* mb = match_bits + (tile * SUB + j) * MASK_WORDS + w * PART_ITEMS;
+    uint64_t b[PART_ITEMS];
+#pragma unroll
+    for (int k = 0; k < PART_ITEMS; ++k) b[k] = mb[k];  // wave-uniform words
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < PART_ITEMS; ++k) m |= static_cast<uint32_t>((b[k] >> lane) & 1u) << k;
+    H keys[PART_ITEMS];
+    uint32_t pays[PART_ITEMS];
+    const uint32_t act = bloom_filter_act<H>(s, keys, load_items<T, H, uint32_t, LP>(s, ch, rb, keys, pays) & m);
+    uint64_t a[PART_ITEMS];
+    uint32_t mc = 0, ac = 0;
+#pragma unroll
+    for (int k = 0; k < PART_ITEMS; ++k) {
+      a[k] = __ballot((act >> k) & 1u);
+      mc += static_cast<uint32_t>(__popcll(b[k]));
+      ac += static_cast<uint32_t>(__popcll(a[k]));
+    }
+    if (lane == 0) {
+      s_wm[w] = mc;
+      s_wa[w] = ac;
+    }
+    __syncthreads();
+    uint32_t mp = scan_pos, ap = comp_n, mt = 0, at = 0;
+#pragma unroll
+    for (int ww = 0; ww < PART_WAVES; ++ww) {
+      if (ww < w) {
+        mp += s_wm[ww];
+        ap += s_wa[ww];
+      }
+      mt += s_wm[ww];
+      at += s_wa[ww];
+    }
+    const uint64_t lt = lanemask_lt();
+#pragma unroll
+    for (int k = 0; k < PART_ITEMS; ++k) {
+      if (((m >> k) & 1u) && s.scan_out != nullptr)
+        s.scan_out[mp + static_cast<uint32_t>(__popcll(b[k] & lt))] = rb + k * WAVE + lane;
+      if ((act >> k) & 1u) {
+        Rec<H, uint32_t> r;
+        r.key = keys[k];
+        r.payload = pays[k];
+        s_comp[ap + static_cast<uint32_t>(__popcll(a[k] & lt))] = r;
+      }
+      mp += static_cast<uint32_t>(__popcll(b[k]));
+      ap += static_cast<uint32_t>(__popcll(a[k]));
+    }
+    scan_pos += mt;
+    comp_n += at;
+    __syncthreads();  // s_wm / s_wa are rewritten by the next tile; s_comp complete after the last
+  }
+  // stable scatter of the compacted records by digit, one tile-sized round at a time
+  uint64_t* s_mask = reinterpret_cast<uint64_t*>(s_comp) + w * 256;  // ranking masks alias the front of s_comp
+#pragma unroll 1
+  for (uint32_t r0 = 0; r0 < comp_n; r0 += PART_TILE) {
+    if (r0) __syncthreads();  // the previous round's write-out has read the staging area
+    Rec<H, uint32_t> recs[PART_ITEMS];
+    uint32_t act = 0;
+    const uint32_t i0 = r0 + w * WAVE_SPAN + lane;
+#pragma unroll
+    for (int k = 0; k < PART_ITEMS; ++k) {
+      const uint32_t i = i0 + k * WAVE;
+      recs[k] = s_comp[min(i, comp_n - 1)];
+      if (i < comp_n) act |= 1u << k;
+    }
+    __syncthreads();  // every record of the round is in registers before the masks / staging overwrite the front
+    clear_wave_counts(s_cnt[w]);
+    clear_wave_masks(s_mask);
+    uint32_t dr[PART_ITEMS];
+#pragma unroll
+    for (int k = 0; k < PART_ITEMS; ++k) {
+      const bool aa = (act >> k) & 1u;
+      const uint32_t dig = aa ? digit_of<H>(dg, recs[k].key) : 0u;
+      dr[k] = (dig << 24) | wave_rank_lds(dig, aa, s_mask, s_cnt[w]);
+    }
+    staged_scatter<H, uint32_t>(recs, act, dr, s_cnt, s_delta, s_comp, s_scratch, n_digits, dg, nd, run, out);
   }
 }
 

@@ -53,17 +53,42 @@ def test_oracle_validate_visibility_rule(hy, oracle):
     assert rows == [0, 1]  # own insert, past insert; deleted at 4, inserted at 9, own row already committed: invisible
 
 
+def validate_op(hy, inp, tid, snap):
+    """The reference's shape (validate.hpp:18-36): Validate(in) with the transaction's context set on the operator."""
+    v = hy.Validate(inp)
+    v.set_transaction_context(hy.TransactionContext(tid, snap))
+    return v
+
+
+def test_validate_needs_a_transaction_context(hy):
+    """validate.cpp:45-47: without a TransactionContext the operator fails (before any device work)."""
+    t = validate_input(hy)
+    with pytest.raises(RuntimeError, match="transaction context"):
+        hy.Validate(wrap(hy, t)).execute()
+
+
+def test_aborted_transaction_skips_the_operator(hy):
+    """abstract_operator.cpp:32-48: an aborted transaction's operators do not run (no device work)."""
+    t = validate_input(hy)
+    v = hy.Validate(wrap(hy, t))
+    ctx = hy.TransactionContext(1, 3)
+    ctx.set_aborted()
+    v.set_transaction_context(ctx)
+    v.execute()
+    assert v.get_output().row_count() == 0
+
+
 @pytest.mark.gpu
 def test_validate_reference_cases(hy, oracle):
     t = validate_input(hy)
     w = wrap(hy, t)
-    v = hy.Validate(w, 1, 3)
+    v = validate_op(hy, w, 1, 3)
     v.execute()
     assert_identical(v.get_output(), oracle.validate(t, 1, 3))
     assert_table_eq_unordered(v.get_output(), hy.load_table(tbl("validate_output_validated.tbl"), 2))
     s = hy.TableScan(w, 0, hy.PredicateCondition.GreaterThanEquals, 2)
     s.execute()
-    v2 = hy.Validate(s, 1, 3)
+    v2 = validate_op(hy, s, 1, 3)
     v2.execute()
     assert_identical(v2.get_output(), oracle.validate(s.get_output(), 1, 3))
     assert_table_eq_unordered(v2.get_output(), hy.load_table(tbl("validate_output_validated_scanned.tbl"), 2))
@@ -75,14 +100,14 @@ def test_validate_synthetic(hy, oracle):
     t = mvcc_table(hy, rng, 200_000, 30_011)
     w = wrap(hy, t)
     for tid, snap in ((1, 0), (2, 5), (3, 11), (9, 20)):
-        v = hy.Validate(w, tid, snap)
+        v = validate_op(hy, w, tid, snap)
         v.execute()
         assert_identical(v.get_output(), oracle.validate(t, tid, snap))
         s = hy.TableScan(w, 1, hy.PredicateCondition.LessThan, 40)
         s.execute()
-        v2 = hy.Validate(s, tid, snap)
+        v2 = validate_op(hy, s, tid, snap)
         v2.execute()
         assert_identical(v2.get_output(), oracle.validate(s.get_output(), tid, snap))
     no_mvcc = wrap(hy, hy.load_table(tbl("int_float.tbl"), 2))
     with pytest.raises(RuntimeError):
-        hy.Validate(no_mvcc, 1, 1).execute()
+        validate_op(hy, no_mvcc, 1, 1).execute()
