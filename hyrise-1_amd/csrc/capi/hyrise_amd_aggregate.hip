@@ -368,13 +368,21 @@ inline uint32_t p_groupby(const hy_agg_params* p) { return p->n_groupby; }
 
 // agg_dense_lanes<n_sums> on a persistent grid: as many workgroups as are resident at once (more would leave a
 // partly filled last round of workgroups - each works through many tiles in turn).
-template <int N>
-void launch_lanes_n(uint64_t n_tiles, size_t lds, hipStream_t s, const hyk::AggDesc& d, const hyk::LanePlan& lp,
-                    unsigned long long* records) {
+inline bool agg_prefetch() {
+  static const bool v = [] {
+    const char* e = std::getenv("HY_AGG_PREFETCH");
+    return e && std::strtol(e, nullptr, 10) != 0;
+  }();
+  return v;
+}
+
+template <int N, bool PF>
+void launch_lanes_pf(uint64_t n_tiles, size_t lds, hipStream_t s, const hyk::AggDesc& d, const hyk::LanePlan& lp,
+                     unsigned long long* records) {
   static int resident = 0;  // per instantiation; LDS per workgroup is small next to the VGPR limit
   if (resident == 0) {
     int per_cu = 0, dev = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hyk::agg_dense_lanes<N>, hyk::AGG_THREADS, lds) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hyk::agg_dense_lanes<N, PF>, hyk::AGG_THREADS, lds) !=
             hipSuccess ||
         hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -382,7 +390,16 @@ void launch_lanes_n(uint64_t n_tiles, size_t lds, hipStream_t s, const hyk::AggD
     resident = std::max(1, per_cu) * std::max(1, cus);
   }
   const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(n_tiles, static_cast<uint64_t>(resident)));
-  hipLaunchKernelGGL(hyk::agg_dense_lanes<N>, dim3(grid), dim3(hyk::AGG_THREADS), lds, s, d, lp, records);
+  hipLaunchKernelGGL((hyk::agg_dense_lanes<N, PF>), dim3(grid), dim3(hyk::AGG_THREADS), lds, s, d, lp, records);
+}
+
+template <int N>
+void launch_lanes_n(uint64_t n_tiles, size_t lds, hipStream_t s, const hyk::AggDesc& d, const hyk::LanePlan& lp,
+                    unsigned long long* records) {
+  if (agg_prefetch())
+    launch_lanes_pf<N, true>(n_tiles, lds, s, d, lp, records);
+  else
+    launch_lanes_pf<N, false>(n_tiles, lds, s, d, lp, records);
 }
 
 void launch_lanes(int n_sums, uint64_t n_tiles, size_t lds, hipStream_t s, const hyk::AggDesc& d,

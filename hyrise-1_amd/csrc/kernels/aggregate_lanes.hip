@@ -35,6 +35,7 @@ constexpr int LN_WINDOW = 18;        // 0 <= e - base <= LN_WINDOW: a value is <
 constexpr int LN_HEAD = 4;           // a new base leaves room for exponents up to 4 above the step's largest
 constexpr int LN_BASE_MAX = 200;     // fold pieces (base - 1 + 31 + 59 bits) stay inside the 9 float limbs
 constexpr int LN_FLUSH_STEPS = 512;  // 4 rows per lane per step: <= 2048 rows, partial sums < 2^(42 + 11) units
+constexpr int LN_DICT_CACHE = 64;    // dictionary entries of a loaded column kept in the wave's LDS (TPC-H 1: <= 50)
 
 enum : int32_t { LN_TERM_COL = 0, LN_TERM_LIT = 1, LN_TERM_LIT_COL = 2, LN_TERM_COL_LIT = 3 };
 enum : int32_t { LN_SUM_INT = 0, LN_SUM_FLOAT = 1, LN_SUM_CHECK = 2 };
@@ -88,7 +89,8 @@ struct LnHeader {
   unsigned long long rows, first, last, pad;  // rows: unused (the lanes count them)
 };
 __host__ __device__ inline size_t ln_wave_lds(int n_store, int n_sums) {
-  return size_t(n_store) * WAVE * 16 + size_t(n_sums) * WAVE * 8 + LN_GROUPS * sizeof(LnHeader) + LN_SUMS * 4;
+  return size_t(n_store) * WAVE * 16 + size_t(n_sums) * WAVE * 8 + LN_GROUPS * sizeof(LnHeader) + LN_SUMS * 4 +
+         size_t(LN_COLS) * LN_DICT_CACHE * 4;
 }
 
 // Chain operations. The term kind / op are wave-uniform: each case is a branch over the step's FQ_R rows (as selects
@@ -250,10 +252,13 @@ __device__ __forceinline__ bool ln_window_ok(const LanePlan& lp, const uint32_t 
   return ok;
 }
 
-template <int NS>
-// 3 waves per SIMD (<= 168 VGPRs): measured best on MI355X - 4 spills, 2 leaves too little latency hiding.
-__global__ __launch_bounds__(AGG_THREADS) __attribute__((amdgpu_waves_per_eu(3))) void agg_dense_lanes(AggDesc d, LanePlan lp,
-                                                              unsigned long long* __restrict__ records) {
+// PF: the next step's RowIDs are prefetched (8 more VGPRs). Round 2 measured 3 waves per SIMD (<= 168 VGPRs) best
+// without it (4 spills, 2 left too little latency hiding); with the prefetch and the LDS dictionaries a step has one
+// dependent global round trip instead of three, so the prefetching instance runs at 2 waves per SIMD (HY_AGG_PREFETCH
+// picks it; tools measure both).
+template <int NS, bool PF>
+__global__ __launch_bounds__(AGG_THREADS) __attribute__((amdgpu_waves_per_eu(PF ? 2 : 3))) void agg_dense_lanes(
+    AggDesc d, LanePlan lp, unsigned long long* __restrict__ records) {
   constexpr int NA = NS > 0 ? NS : 1;
   extern __shared__ __align__(16) unsigned char s_lanes[];
   const int lane = __lane_id();
@@ -265,6 +270,7 @@ __global__ __launch_bounds__(AGG_THREADS) __attribute__((amdgpu_waves_per_eu(3))
   double* stage = reinterpret_cast<double*>(vals + n_store * WAVE);  // [sum][lane]
   LnHeader* hdr = reinterpret_cast<LnHeader*>(stage + NS * WAVE);    // [table entry]
   int32_t* sbase = reinterpret_cast<int32_t*>(hdr + LN_GROUPS);       // [sum]
+  uint32_t* dcache = reinterpret_cast<uint32_t*>(sbase + LN_SUMS);     // [loaded column][dictionary entry]
   const ln_cptr<LaneTables> T = ln_const(lp.t);
   const ln_cptr<LnTerm> terms = ln_const(lp.terms);
   if (lane < LN_GROUPS) hdr[lane] = LnHeader{0, ~0ull, 0, 0};
@@ -284,12 +290,20 @@ __global__ __launch_bounds__(AGG_THREADS) __attribute__((amdgpu_waves_per_eu(3))
 #pragma unroll
   for (int s = 0; s < NA; ++s) fbase[s] = -1;
   uint32_t since = 0;
+  // The (referenced) chunk whose small dictionaries sit in dcache, and which loaded columns they are (bit li): a
+  // dictionary decode is then an LDS read instead of a dependent global load per row.
+  uint32_t cached_cc = 0xFFFFFFFFu, cached = 0;
 
   for (uint64_t tile = blockIdx.x; tile < d.n_tiles; tile += gridDim.x) {
     const uint32_t c = agg_tile_chunk(d, tile);
     const uint32_t size = d.chunk_size[c];
     const uint32_t span = static_cast<uint32_t>(tile - d.chunk_tile_begin[c]) * AGG_TILE + w * AGG_WAVE_SPAN;
     const uint64_t row0 = d.chunk_row_begin[c];
+    const uintptr_t pl = d.n_pos_groups ? reinterpret_cast<uintptr_t>(ln_const(d.pos_lists)[c]) : 0;
+    // RowIDs of the next step, loaded during the current one (after its column loads, so waiting for those does not
+    // wait for these)
+    unsigned long long next_rid[FQ_R];
+    bool have_next = false;  // a deferred step (continue below) leaves no prefetch for its successor
     for (int h = 0; h < AGG_ITEMS / FQ_R; ++h) {
       const uint32_t base = span + h * FQ_R * WAVE;
       if (base >= size) break;  // wave-uniform
@@ -301,16 +315,21 @@ __global__ __launch_bounds__(AGG_THREADS) __attribute__((amdgpu_waves_per_eu(3))
       // row offsets inside the (single) chunk the step's rows live in
       uint32_t off[FQ_R];
       uint32_t cc = c;
+      const bool prefetch = PF && d.n_pos_groups && h + 1 < AGG_ITEMS / FQ_R && base + FQ_R * WAVE < size;
       if (d.n_pos_groups) {
-        const uintptr_t pl = reinterpret_cast<uintptr_t>(ln_const(d.pos_lists)[c]);
         hy_row_id rid[FQ_R];
 #pragma unroll
         for (int k = 0; k < FQ_R; ++k) {
-          const uint32_t i = min(base + k * WAVE + lane, size - 1);
-          const unsigned long long q = *reinterpret_cast<const __attribute__((address_space(1))) unsigned long long*>(
-              pl + 8ull * i);
+          unsigned long long q;
+          if (!have_next) {
+            const uint32_t i = min(base + k * WAVE + lane, size - 1);
+            q = *reinterpret_cast<const __attribute__((address_space(1))) unsigned long long*>(pl + 8ull * i);
+          } else {
+            q = next_rid[k];
+          }
           rid[k] = hy_row_id{static_cast<uint32_t>(q), static_cast<uint32_t>(q >> 32)};
         }
+        have_next = false;
         cc = __builtin_amdgcn_readfirstlane(rid[0].chunk_id);
         bool same = true;
 #pragma unroll
@@ -327,6 +346,22 @@ __global__ __launch_bounds__(AGG_THREADS) __attribute__((amdgpu_waves_per_eu(3))
 #pragma unroll
         for (int k = 0; k < FQ_R; ++k) off[k] = ((act >> k) & 1u) ? base + k * WAVE + lane : 0u;
       }
+      // the chunk's small dictionaries into the wave's LDS (once per chunk change)
+      if (cc != cached_cc) {
+        cached = 0;
+#pragma unroll 1
+        for (int li = 0; li < LN_COLS; ++li) {
+          if (li >= lp.n_load) break;
+          const auto& ch = ln_const(T->load_chunks[li])[cc];
+          if (ch.kind == HY_COL_DICT && ch.dictionary_size <= LN_DICT_CACHE) {
+            if (static_cast<uint32_t>(lane) < ch.dictionary_size)
+              dcache[li * LN_DICT_CACHE + lane] =
+                  ln_load_word(reinterpret_cast<uintptr_t>(ch.dictionary), static_cast<uint32_t>(lane) * 4u);
+            cached |= 1u << li;
+          }
+        }
+        cached_cc = cc;
+      }
       // loads: every column's value / vid first (one batch in flight), then vids -> dictionary values
       uint32_t raw[LN_COLS][FQ_R];
 #pragma unroll
@@ -337,6 +372,15 @@ __global__ __launch_bounds__(AGG_THREADS) __attribute__((amdgpu_waves_per_eu(3))
         const uintptr_t p0 = reinterpret_cast<uintptr_t>(ch.data);
 #pragma unroll
         for (int k = 0; k < FQ_R; ++k) raw[li][k] = ln_load_elem(p0, off[k], wb);
+      }
+      if (prefetch) {  // the next step's RowIDs, behind this step's column loads
+        have_next = true;
+        const uint32_t nb = base + FQ_R * WAVE;
+#pragma unroll
+        for (int k = 0; k < FQ_R; ++k) {
+          const uint32_t i = min(nb + k * WAVE + lane, size - 1);
+          next_rid[k] = *reinterpret_cast<const __attribute__((address_space(1))) unsigned long long*>(pl + 8ull * i);
+        }
       }
       uint32_t g[FQ_R] = {0, 0, 0, 0};
       uint32_t nulls = 0;  // rows with a NULL in a non-group-by column
@@ -350,7 +394,14 @@ __global__ __launch_bounds__(AGG_THREADS) __attribute__((amdgpu_waves_per_eu(3))
         uint32_t nl = 0;
 #pragma unroll
         for (int k = 0; k < FQ_R; ++k) v[k] = raw[li][k];
-        if (dict) {
+        if (dict && ((cached >> li) & 1u)) {
+#pragma unroll
+          for (int k = 0; k < FQ_R; ++k) {
+            const bool isnull = v[k] >= ch.dictionary_size;
+            if (isnull) nl |= 1u << k;
+            v[k] = dcache[li * LN_DICT_CACHE + (isnull ? 0u : v[k])];
+          }
+        } else if (dict) {
           const uintptr_t dv = reinterpret_cast<uintptr_t>(ch.dictionary);
 #pragma unroll
           for (int k = 0; k < FQ_R; ++k) {
