@@ -62,9 +62,14 @@ $(LIB)/hyrise_amd_decode.o: $(CSRC)/capi/hyrise_amd_decode.hip $(CAPI_HDR)
 	@mkdir -p $(LIB)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
+$(LIB)/hyrise_amd_string.o: $(CSRC)/capi/hyrise_amd_string.hip $(CAPI_HDR)
+	@mkdir -p $(LIB)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
 $(LIB)/libhyrise_amd.so: $(LIB)/hyrise_amd.o $(LIB)/hyrise_amd_aggregate.o $(LIB)/hyrise_amd_order.o \
                          $(LIB)/hyrise_amd_comm.o $(LIB)/hyrise_amd_compare.o \
-                         $(LIB)/hyrise_amd_validate.o $(LIB)/hyrise_amd_decode.o $(JOIN_OBJS)
+                         $(LIB)/hyrise_amd_validate.o $(LIB)/hyrise_amd_decode.o $(LIB)/hyrise_amd_string.o \
+                         $(JOIN_OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 $(LIB)/libhyrise_host.so: $(HOST_SRC) $(HOST_HDR) $(LIB)/libhyrise_amd.so

@@ -105,6 +105,11 @@ class AggLayout(ctypes.Structure):
                 ("agg_limbs", ctypes.c_uint32 * HY_AGG_MAX_AGGREGATES)]
 
 
+class StringPredicate(ctypes.Structure):
+    _fields_ = [("value", ctypes.c_char_p), ("value_len", ctypes.c_uint32), ("pattern_regex", ctypes.c_int32),
+                ("pattern", ctypes.c_char_p), ("pattern_len", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
 _sigs = {
     "hy_get_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "hy_set_device": (ctypes.c_int, [ctypes.c_int]),
@@ -238,6 +243,18 @@ _sigs = {
                                              ctypes.c_size_t, ctypes.c_void_p]),
     "hy_pos_list_null_positions": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
                                                   ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "hy_string_table_scan_workspace_size": (ctypes.c_int, [ctypes.POINTER(ScanChunk), ctypes.c_uint32,
+                                                           ctypes.POINTER(StringPredicate),
+                                                           ctypes.POINTER(ctypes.c_size_t)]),
+    "hy_string_table_scan": (ctypes.c_int, [ctypes.POINTER(ScanChunk), ctypes.c_uint32, ctypes.POINTER(StringPredicate),
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "hy_string_reference_scan_workspace_size": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32,
+                                                               ctypes.POINTER(StringPredicate),
+                                                               ctypes.POINTER(ctypes.c_size_t)]),
+    "hy_string_reference_scan": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ScanChunk),
+                                                ctypes.c_uint32, ctypes.POINTER(StringPredicate), ctypes.c_void_p,
+                                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
 }
 HY_COMM_ID_BYTES = 128
 for _name, (_res, _args) in _sigs.items():

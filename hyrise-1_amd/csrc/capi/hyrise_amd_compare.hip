@@ -8,11 +8,14 @@
 // compaction (hipcub DeviceSelect::Flagged) then yields the matches chunk-major, offsets ascending - the PosLists
 // the reference's per-chunk jobs build. Per-chunk counts come from one atomic add per tile. Both inputs read 1x;
 // this is not a headline kernel, the extra flag/item pass (9-12 B per row) keeps it to two launches.
+// String columns (both sides HY_TYPE_STRING; STRING chunks or DICT chunks with packed dictionaries) compare as the
+// reference's std::string operators do (kernels/common.hpp string_compare).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "hyrise_amd.h"
@@ -42,6 +45,7 @@ struct CmpDesc {
 };
 
 // Value of row `off` of a data column chunk; returns true for NULL (value chunk null flag / dictionary null id).
+// Strings (T = hyk::DevString): the dictionary / value chunk's packed string array.
 template <typename T>
 __device__ __forceinline__ bool column_value(const hy_column_chunk& col, uint32_t off, T* v) {
   if (col.kind == HY_COL_DICT) {
@@ -49,11 +53,17 @@ __device__ __forceinline__ bool column_value(const hy_column_chunk& col, uint32_
                          : col.vid_width == 2 ? static_cast<const uint16_t*>(col.data)[off]
                                               : static_cast<const uint32_t*>(col.data)[off];
     if (vid >= col.dictionary_size) return true;
-    *v = static_cast<const T*>(col.dictionary)[vid];
+    if constexpr (std::is_same_v<T, hyk::DevString>)
+      *v = hyk::packed_string(col.dictionary, col.dictionary_size, vid);
+    else
+      *v = static_cast<const T*>(col.dictionary)[vid];
     return false;
   }
   if (col.nulls != nullptr && col.nulls[off]) return true;
-  *v = static_cast<const T*>(col.data)[off];
+  if constexpr (std::is_same_v<T, hyk::DevString>)
+    *v = hyk::packed_string(col.data, col.size, off);
+  else
+    *v = static_cast<const T*>(col.data)[off];
   return false;
 }
 
@@ -82,12 +92,17 @@ __global__ __launch_bounds__(CMP_THREADS) void compare_flags_kernel(CmpDesc d, v
   if (threadIdx.x == 0) s_count = 0;
   __syncthreads();
   if (off < lc.size) {
-    using C = decltype(L{} + R{});  // the comparator's operand type (usual arithmetic conversions)
     L lv{};
     R rv{};
     const bool ln = side_value<L>(d.left, lc, off, &lv);
     const bool rn = side_value<R>(d.right, rc, off, &rv);
-    const bool m = !ln && !rn && hyk::cmp_op<C>(d.op, static_cast<C>(lv), static_cast<C>(rv));
+    bool m = !ln && !rn;
+    if constexpr (std::is_same_v<L, hyk::DevString>) {
+      m = m && hyk::cmp_result(d.op, hyk::string_compare(lv, rv));  // std::string operators
+    } else {
+      using C = decltype(L{} + R{});  // the comparator's operand type (usual arithmetic conversions)
+      m = m && hyk::cmp_op<C>(d.op, static_cast<C>(lv), static_cast<C>(rv));
+    }
     const uint64_t g = d.chunk_row_begin[c] + off;
     flags[g] = m;
     if constexpr (ROWS)
@@ -112,8 +127,10 @@ hy_status check_sides(const hy_join_side* l, const hy_join_side* r, Geometry* g)
   if (!l || !r) return fail(HY_ERR_INVALID_ARGUMENT, "null side");
   if (l->n_chunks != r->n_chunks) return fail(HY_ERR_INVALID_ARGUMENT, "sides have different chunk counts");
   if ((l->n_chunks && (!l->chunks || !r->chunks))) return fail(HY_ERR_INVALID_ARGUMENT, "null chunks");
-  if (!type_size(l->value_type) || !type_size(r->value_type))
-    return fail(HY_ERR_UNSUPPORTED, "column comparison of non-numeric columns");
+  const bool ls = l->value_type == HY_TYPE_STRING, rs = r->value_type == HY_TYPE_STRING;
+  if (ls != rs) return fail(HY_ERR_INVALID_ARGUMENT, "string column compared with a numeric column");
+  if (!ls && (!type_size(l->value_type) || !type_size(r->value_type)))
+    return fail(HY_ERR_UNSUPPORTED, "column comparison value type");
   for (uint32_t c = 0; c < l->n_chunks; ++c) {
     const hy_join_chunk& a = l->chunks[c];
     const hy_join_chunk& b = r->chunks[c];
@@ -267,6 +284,9 @@ hy_status hy_column_compare_scan(const hy_join_side* left, const hy_join_side* r
     }
   };
   switch (left->value_type) {
+    case HY_TYPE_STRING:
+      st = launch(hyk::DevString{}, hyk::DevString{});
+      break;
     case HY_TYPE_INT32:
       st = with_right(int32_t{});
       break;

@@ -1,0 +1,430 @@
+// TableScans over std::string columns held on the device (include/hyrise_amd.h, "String scans"): unencoded
+// ValueColumn<std::string> chunks as packed string arrays (offsets + bytes), next to dictionary chunks.
+//
+// Reference: SingleColumnTableScanImpl::handle_column on a ValueColumn<std::string> (single_column_table_scan_impl.cpp:
+// 38-85: the comparator of type_comparison.hpp:100-123 between the row's std::string and type_cast<std::string>(value),
+// i.e. std::string::compare, bytes as unsigned char), LikeTableScanImpl on a value column (like_table_scan_impl.cpp:
+// 22-31, 86-97) with the LikeMatcher (like_matcher.cpp:9-118), and IsNullTableScanImpl for string value columns.
+// Dictionary chunks keep the host's dictionary rewrite (op + search_vid, or the LIKE id set) exactly as hy_table_scan.
+//
+// LIKE on the device: the pattern compiles (on the host, per call) to a bit-parallel NFA over at most 63 positions -
+// per position a byte set (a literal byte, '_' = any byte, a [...] class of the regex path) or a '%' star; per input
+// byte c: S = ((S & lit[c]) << 1) | (S & star & star_ok[c]), then the star closure S |= (S & star) << 1. The
+// reference's simple patterns ('abc%', '%abc', '%abc%', '%a%b%...%') are plain string searches: their '%' and '_'
+// match any byte. Other patterns take the reference's regex path (pattern -> ECMAScript '^...$', every regex special
+// escaped except '[' ']'): '_' and '%' become '.', which does not match '\n' or '\r', and [...] is a class.
+//
+// One flag launch evaluates every row (one thread per row, 256-row tiles never straddle chunks) and writes a flag and
+// the row's output item; one order-preserving compaction (hipcub DeviceSelect::Flagged) yields the matches in row
+// order. Not a headline path: string rows are read once, the flag/item pass adds 9-13 B per row.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "hyrise_amd.h"
+#include "capi_common.hpp"
+#include "../kernels/common.hpp"
+
+using namespace hyc;
+
+namespace {
+
+constexpr int STR_THREADS = 256;
+constexpr int LIKE_MAX_POSITIONS = 63;
+
+// The compiled LIKE pattern (device copy in the workspace).
+struct LikeNfa {
+  uint64_t lit[256];      // bit j: position j accepts byte c
+  uint64_t star_ok[256];  // bit j: star position j may consume byte c
+  uint64_t star;          // star positions
+  uint64_t accept;        // bit m
+  uint64_t start;         // closure of position 0
+};
+
+struct StrPred {
+  const char* value;  // device copy of the constant
+  uint32_t value_len;
+  const LikeNfa* nfa;  // null: no LIKE pattern
+};
+
+__host__ __device__ inline uint64_t star_closure(uint64_t s, uint64_t star) {
+  for (;;) {
+    const uint64_t n = s | ((s & star) << 1);
+    if (n == s) return s;
+    s = n;
+  }
+}
+
+__device__ inline bool like_match(const LikeNfa& a, const unsigned char* p, uint32_t n) {
+  uint64_t s = a.start;
+  for (uint32_t i = 0; i < n && s; ++i) {
+    const unsigned c = p[i];
+    s = star_closure(((s & a.lit[c]) << 1) | (s & a.star & a.star_ok[c]), a.star);
+  }
+  return (s & a.accept) != 0;
+}
+
+// Row `off` of a scan chunk: the reference's predicate for a dictionary chunk (value id vs search_vid / id set, as
+// hy_table_scan) or for a string value chunk (compare with the constant, LIKE, IS [NOT] NULL).
+__device__ inline bool string_row_match(const hy_scan_chunk& ch, uint32_t off, const StrPred& p) {
+  const int op = ch.op;
+  if (op == HY_OP_NONE) return false;
+  const hy_column_chunk& col = ch.column;
+  if (col.kind == HY_COL_DICT) {
+    const uint32_t vid = col.vid_width == 1   ? static_cast<const uint8_t*>(col.data)[off]
+                         : col.vid_width == 2 ? static_cast<const uint16_t*>(col.data)[off]
+                                              : static_cast<const uint32_t*>(col.data)[off];
+    const bool is_null = vid == col.dictionary_size;
+    if (op == HY_OP_IS_NULL) return is_null;
+    if (is_null) return false;
+    if (op == HY_OP_ALL || op == HY_OP_IS_NOT_NULL) return true;
+    if (op == HY_OP_VID_SET) return (ch.vid_set[vid >> 5] >> (vid & 31)) & 1u;
+    return hyk::cmp_op<uint32_t>(op, vid, ch.search_vid);
+  }
+  const bool is_null = col.nulls != nullptr && col.nulls[off];
+  if (op == HY_OP_IS_NULL) return is_null;
+  if (is_null) return false;
+  if (op == HY_OP_ALL || op == HY_OP_IS_NOT_NULL) return true;
+  const hyk::DevString v = hyk::packed_string(col.data, col.size, off);
+  if (op == HY_OP_LIKE || op == HY_OP_NOT_LIKE) return like_match(*p.nfa, v.p, v.n) == (op == HY_OP_LIKE);
+  return hyk::cmp_result(op, hyk::string_compare(v, hyk::DevString{reinterpret_cast<const unsigned char*>(p.value),
+                                                                   p.value_len}));
+}
+
+struct TableDesc {
+  const hy_scan_chunk* chunks;
+  const uint32_t* chunk_ids;
+  const uint32_t* tile_chunk;
+  const uint64_t* chunk_tile_begin;
+  const uint64_t* chunk_row_begin;
+  uint64_t n_tiles;
+};
+
+__global__ __launch_bounds__(STR_THREADS) void string_table_flags(TableDesc d, StrPred p, hy_row_id* __restrict__ items,
+                                                                 uint8_t* __restrict__ flags,
+                                                                 uint32_t* __restrict__ counts) {
+  __shared__ uint32_t s_count;
+  const uint64_t tile = blockIdx.x;
+  if (tile >= d.n_tiles) return;
+  const uint32_t c = d.tile_chunk[tile];
+  const hy_scan_chunk& ch = d.chunks[c];
+  const uint32_t off = static_cast<uint32_t>(tile - d.chunk_tile_begin[c]) * STR_THREADS + threadIdx.x;
+  if (threadIdx.x == 0) s_count = 0;
+  __syncthreads();
+  if (off < ch.column.size) {
+    const bool m = string_row_match(ch, off, p);
+    const uint64_t g = d.chunk_row_begin[c] + off;
+    flags[g] = m;
+    items[g] = hy_row_id{d.chunk_ids[c], off};
+    if (m) atomicAdd(&s_count, 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && s_count) atomicAdd(&counts[c], s_count);
+}
+
+__global__ __launch_bounds__(STR_THREADS) void string_reference_flags(const hy_row_id* __restrict__ pos_list, uint64_t n,
+                                                                     const hy_scan_chunk* __restrict__ referenced,
+                                                                     uint32_t n_referenced, StrPred p,
+                                                                     uint32_t* __restrict__ items,
+                                                                     uint8_t* __restrict__ flags) {
+  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const hy_row_id rid = pos_list[i];
+    bool m = false;
+    if (rid.chunk_offset != 0xFFFFFFFFu && rid.chunk_id < n_referenced)
+      m = string_row_match(referenced[rid.chunk_id], rid.chunk_offset, p);
+    flags[i] = m;
+    items[i] = static_cast<uint32_t>(i);
+  }
+}
+
+// ---- host: the LIKE pattern's NFA ----
+hy_status compile_like(const char* pattern, uint32_t len, int32_t regex, LikeNfa* a) {
+  std::memset(a, 0, sizeof(*a));
+  int m = 0;
+  auto position = [&](bool star) -> int {
+    if (m >= LIKE_MAX_POSITIONS) return -1;
+    if (star) a->star |= 1ull << m;
+    return m++;
+  };
+  const auto newline = [](unsigned c) { return c == '\n' || c == '\r'; };
+  for (uint32_t i = 0; i < len; ++i) {
+    const unsigned char ch = static_cast<unsigned char>(pattern[i]);
+    if (ch == '%') {
+      const int j = position(true);
+      if (j < 0) return fail(HY_ERR_UNSUPPORTED, "LIKE pattern longer than 63 positions");
+      for (unsigned c = 0; c < 256; ++c)
+        if (!(regex && newline(c))) a->star_ok[c] |= 1ull << j;
+    } else if (ch == '_') {
+      const int j = position(false);
+      if (j < 0) return fail(HY_ERR_UNSUPPORTED, "LIKE pattern longer than 63 positions");
+      for (unsigned c = 0; c < 256; ++c)
+        if (!(regex && newline(c))) a->lit[c] |= 1ull << j;
+    } else if (regex && ch == '[') {
+      // a character class of the regex the reference builds: members until ']'; '%' became ".*" and '_' "." there
+      // (both literal inside a class), every other byte is literal; "x-y" is a range of plain bytes
+      uint32_t k = i + 1;
+      std::vector<unsigned char> mem;
+      bool closed = false;
+      const int j = position(false);
+      if (j < 0) return fail(HY_ERR_UNSUPPORTED, "LIKE pattern longer than 63 positions");
+      while (k < len) {
+        const unsigned char x = static_cast<unsigned char>(pattern[k]);
+        if (x == ']' && k > i + 1) {
+          closed = true;
+          break;
+        }
+        if (x == ']') {  // "[]": the empty class matches nothing
+          closed = true;
+          break;
+        }
+        if (k + 2 < len && pattern[k + 1] == '-' && pattern[k + 2] != ']') {
+          const unsigned char y = static_cast<unsigned char>(pattern[k + 2]);
+          if (x == '%' || x == '_' || y == '%' || y == '_' || y < x)
+            return fail(HY_ERR_UNSUPPORTED, "LIKE character class range");
+          for (unsigned c = x; c <= y; ++c) mem.push_back(static_cast<unsigned char>(c));
+          k += 3;
+          continue;
+        }
+        if (x == '%') {
+          mem.push_back('.');
+          mem.push_back('*');
+        } else if (x == '_') {
+          mem.push_back('.');
+        } else {
+          mem.push_back(x);
+        }
+        ++k;
+      }
+      if (!closed) return fail(HY_ERR_UNSUPPORTED, "unterminated [ in a LIKE pattern (the reference's regex fails)");
+      for (const unsigned char c : mem) a->lit[c] |= 1ull << j;
+      i = k;
+    } else if (regex && ch == ']') {
+      return fail(HY_ERR_UNSUPPORTED, "] outside a class in a LIKE pattern");
+    } else {
+      const int j = position(false);
+      if (j < 0) return fail(HY_ERR_UNSUPPORTED, "LIKE pattern longer than 63 positions");
+      a->lit[ch] |= 1ull << j;
+    }
+  }
+  a->accept = 1ull << m;
+  a->start = star_closure(1ull, a->star);
+  return HY_OK;
+}
+
+struct Staged {
+  char* value;
+  LikeNfa* nfa;
+};
+
+void carve_pred(Carver& cv, const hy_string_predicate* pred, Staged* st) {
+  st->value = cv.take<char>(pred && pred->value_len ? pred->value_len + 16 : 16);
+  st->nfa = cv.take<LikeNfa>(1);
+}
+
+hy_status stage_pred(const hy_string_predicate* pred, const Staged& st, hipStream_t s, StrPred* p, bool need_like) {
+  p->value = st.value;
+  p->value_len = 0;
+  p->nfa = nullptr;
+  if (pred && pred->value_len) {
+    if (!pred->value) return fail(HY_ERR_INVALID_ARGUMENT, "string constant");
+    HY_STAGE(st.value, pred->value, pred->value_len, s);
+    p->value_len = pred->value_len;
+  }
+  if (need_like) {
+    if (!pred || (pred->pattern_len && !pred->pattern)) return fail(HY_ERR_INVALID_ARGUMENT, "LIKE pattern");
+    LikeNfa a;
+    const hy_status r = compile_like(pred->pattern, pred->pattern_len, pred->pattern_regex, &a);
+    if (r != HY_OK) return r;
+    HY_STAGE(st.nfa, &a, sizeof(a), s);
+    p->nfa = st.nfa;
+  }
+  return HY_OK;
+}
+
+hy_status check_ops(const hy_scan_chunk* chunks, uint32_t n, bool* need_like) {
+  *need_like = false;
+  for (uint32_t c = 0; c < n; ++c) {
+    const auto& ch = chunks[c];
+    if (ch.column.kind == HY_COL_DICT) {
+      if (ch.op < HY_OP_EQ || ch.op > HY_OP_VID_SET || (ch.op == HY_OP_VID_SET && !ch.vid_set))
+        return fail(HY_ERR_INVALID_ARGUMENT, "dictionary chunk op");
+    } else if (ch.column.kind == HY_COL_STRING) {
+      if (ch.op == HY_OP_VID_SET || ch.op < HY_OP_EQ || ch.op > HY_OP_NOT_LIKE)
+        return fail(HY_ERR_INVALID_ARGUMENT, "string chunk op");
+      if (ch.op == HY_OP_LIKE || ch.op == HY_OP_NOT_LIKE) *need_like = true;
+    } else if (ch.column.size) {
+      return fail(HY_ERR_INVALID_ARGUMENT, "string scans take STRING or DICT chunks");
+    }
+  }
+  return HY_OK;
+}
+
+template <typename Item>
+size_t select_temp(uint64_t rows) {
+  size_t t = 0;
+  (void)hipcub::DeviceSelect::Flagged(nullptr, t, static_cast<const Item*>(nullptr), static_cast<const uint8_t*>(nullptr),
+                                      static_cast<Item*>(nullptr), static_cast<uint64_t*>(nullptr),
+                                      static_cast<int>(rows));
+  return t + 16;
+}
+
+struct TableWs {
+  hy_scan_chunk* chunks;
+  uint32_t* ids;
+  uint32_t* tile_chunk;
+  uint64_t *tile_begin, *row_begin;
+  hy_row_id* items;
+  uint8_t* flags;
+  char* temp;
+  size_t temp_bytes;
+  Staged st;
+};
+
+void carve_table(Carver& cv, uint64_t rows, uint64_t tiles, uint32_t n, const hy_string_predicate* pred, TableWs* w) {
+  w->chunks = cv.take<hy_scan_chunk>(std::max<uint32_t>(1, n));
+  w->ids = cv.take<uint32_t>(std::max<uint32_t>(1, n));
+  w->tile_chunk = cv.take<uint32_t>(tiles + 1);
+  w->tile_begin = cv.take<uint64_t>(n + 1);
+  w->row_begin = cv.take<uint64_t>(n + 1);
+  w->items = cv.take<hy_row_id>(rows + 1);
+  w->flags = cv.take<uint8_t>(rows + 16);
+  w->temp_bytes = select_temp<hy_row_id>(rows);
+  w->temp = cv.take<char>(w->temp_bytes);
+  carve_pred(cv, pred, &w->st);
+}
+
+void table_geometry(const hy_scan_chunk* chunks, uint32_t n, uint64_t* rows, uint64_t* tiles) {
+  *rows = 0;
+  *tiles = 0;
+  for (uint32_t c = 0; c < n; ++c) {
+    *rows += chunks[c].column.size;
+    *tiles += (chunks[c].column.size + STR_THREADS - 1) / STR_THREADS;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+hy_status hy_string_table_scan_workspace_size(const hy_scan_chunk* chunks, uint32_t n_chunks,
+                                              const hy_string_predicate* pred, size_t* bytes) {
+  if (!bytes || (n_chunks && !chunks)) return fail(HY_ERR_INVALID_ARGUMENT, "null argument");
+  uint64_t rows, tiles;
+  table_geometry(chunks, n_chunks, &rows, &tiles);
+  Carver cv{nullptr, 0};
+  TableWs w;
+  carve_table(cv, rows, tiles, n_chunks, pred, &w);
+  *bytes = cv.used + 256;
+  return HY_OK;
+}
+
+hy_status hy_string_table_scan(const hy_scan_chunk* chunks, uint32_t n_chunks, const hy_string_predicate* pred,
+                               const uint32_t* chunk_ids, hy_row_id* out_rows, uint32_t* counts, uint64_t* n_out,
+                               void* workspace, size_t workspace_bytes, hy_stream_t stream) {
+  if ((n_chunks && (!chunks || !chunk_ids || !counts)) || !n_out) return fail(HY_ERR_INVALID_ARGUMENT, "null argument");
+  bool need_like = false;
+  hy_status st = check_ops(chunks, n_chunks, &need_like);
+  if (st != HY_OK) return st;
+  uint64_t rows, tiles;
+  table_geometry(chunks, n_chunks, &rows, &tiles);
+  if (rows >= 0x7FFFFFFFull) return fail(HY_ERR_UNSUPPORTED, "more than 2^31-1 rows");
+  hipStream_t s = S(stream);
+  HY_HIP(hipMemsetAsync(n_out, 0, 8, s));
+  if (n_chunks) HY_HIP(hipMemsetAsync(counts, 0, 4ull * n_chunks, s));
+  if (rows == 0) return HY_OK;
+  if (!out_rows) return fail(HY_ERR_INVALID_ARGUMENT, "out_rows");
+  Carver cv{static_cast<char*>(workspace), workspace_bytes};
+  TableWs w;
+  carve_table(cv, rows, tiles, n_chunks, pred, &w);
+  if (!cv.ok) return fail(HY_ERR_WORKSPACE, "string scan workspace too small");
+  StrPred p{};
+  st = stage_pred(pred, w.st, s, &p, need_like);
+  if (st != HY_OK) return st;
+  std::vector<uint32_t> tc(tiles);
+  std::vector<uint64_t> tb(n_chunks + 1), rb(n_chunks + 1);
+  uint64_t t = 0, r = 0;
+  for (uint32_t c = 0; c < n_chunks; ++c) {
+    tb[c] = t;
+    rb[c] = r;
+    const uint64_t k = (chunks[c].column.size + STR_THREADS - 1) / STR_THREADS;
+    for (uint64_t i = 0; i < k; ++i) tc[t + i] = c;
+    t += k;
+    r += chunks[c].column.size;
+  }
+  tb[n_chunks] = t;
+  rb[n_chunks] = r;
+  HY_STAGE(w.chunks, chunks, sizeof(hy_scan_chunk) * n_chunks, s);
+  HY_STAGE(w.ids, chunk_ids, 4ull * n_chunks, s);
+  HY_STAGE(w.tile_chunk, tc.data(), 4 * tiles, s);
+  HY_STAGE(w.tile_begin, tb.data(), 8ull * (n_chunks + 1), s);
+  HY_STAGE(w.row_begin, rb.data(), 8ull * (n_chunks + 1), s);
+  const TableDesc d{w.chunks, w.ids, w.tile_chunk, w.tile_begin, w.row_begin, tiles};
+  {
+    KTimer kt_("string_table_flags", s, rows);
+    hipLaunchKernelGGL(string_table_flags, dim3(static_cast<uint32_t>(tiles)), dim3(STR_THREADS), 0, s, d, p, w.items,
+                       w.flags, counts);
+    kt_.done();
+  }
+  HY_HIP(hipGetLastError());
+  HY_HIP(hipcub::DeviceSelect::Flagged(w.temp, w.temp_bytes, static_cast<const hy_row_id*>(w.items), w.flags, out_rows,
+                                       n_out, static_cast<int>(rows), s));
+  return HY_OK;
+}
+
+hy_status hy_string_reference_scan_workspace_size(uint64_t pos_list_size, uint32_t n_referenced,
+                                                  const hy_string_predicate* pred, size_t* bytes) {
+  if (!bytes) return fail(HY_ERR_INVALID_ARGUMENT, "null bytes");
+  Carver cv{nullptr, 0};
+  cv.take<hy_scan_chunk>(std::max<uint32_t>(1, n_referenced));
+  cv.take<uint32_t>(pos_list_size + 1);
+  cv.take<uint8_t>(pos_list_size + 16);
+  cv.take<char>(select_temp<uint32_t>(pos_list_size));
+  Staged stg;
+  carve_pred(cv, pred, &stg);
+  *bytes = cv.used + 256;
+  return HY_OK;
+}
+
+hy_status hy_string_reference_scan(const hy_row_id* pos_list, uint64_t pos_list_size,
+                                   const hy_scan_chunk* referenced_chunks, uint32_t n_referenced_chunks,
+                                   const hy_string_predicate* pred, uint32_t* out_positions, uint64_t* count,
+                                   void* workspace, size_t workspace_bytes, hy_stream_t stream) {
+  if (!count || (n_referenced_chunks && !referenced_chunks)) return fail(HY_ERR_INVALID_ARGUMENT, "null argument");
+  bool need_like = false;
+  hy_status st = check_ops(referenced_chunks, n_referenced_chunks, &need_like);
+  if (st != HY_OK) return st;
+  if (pos_list_size >= 0x7FFFFFFFull) return fail(HY_ERR_UNSUPPORTED, "more than 2^31-1 positions");
+  hipStream_t s = S(stream);
+  HY_HIP(hipMemsetAsync(count, 0, 8, s));
+  if (pos_list_size == 0) return HY_OK;
+  if (!pos_list || !out_positions) return fail(HY_ERR_INVALID_ARGUMENT, "null argument");
+  Carver cv{static_cast<char*>(workspace), workspace_bytes};
+  auto* dch = cv.take<hy_scan_chunk>(std::max<uint32_t>(1, n_referenced_chunks));
+  auto* items = cv.take<uint32_t>(pos_list_size + 1);
+  auto* flags = cv.take<uint8_t>(pos_list_size + 16);
+  size_t tb = select_temp<uint32_t>(pos_list_size);
+  char* temp = cv.take<char>(tb);
+  Staged stg;
+  carve_pred(cv, pred, &stg);
+  if (!cv.ok) return fail(HY_ERR_WORKSPACE, "string reference scan workspace too small");
+  StrPred p{};
+  st = stage_pred(pred, stg, s, &p, need_like);
+  if (st != HY_OK) return st;
+  HY_STAGE(dch, referenced_chunks, sizeof(hy_scan_chunk) * n_referenced_chunks, s);
+  {
+    KTimer kt_("string_reference_flags", s, pos_list_size);
+    hipLaunchKernelGGL(string_reference_flags, dim3(grid_for(pos_list_size, STR_THREADS)), dim3(STR_THREADS), 0, s,
+                       pos_list, pos_list_size, dch, n_referenced_chunks, p, items, flags);
+    kt_.done();
+  }
+  HY_HIP(hipGetLastError());
+  HY_HIP(hipcub::DeviceSelect::Flagged(temp, tb, static_cast<const uint32_t*>(items), flags, out_positions, count,
+                                       static_cast<int>(pos_list_size), s));
+  return HY_OK;
+}
+
+}  // extern "C"

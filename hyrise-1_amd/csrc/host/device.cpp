@@ -96,6 +96,28 @@ int32_t hy_type_of(DataType t) {
   }
 }
 
+// A packed string array (include/hyrise_amd.h, "Column chunk descriptors"): uint32 offsets[n + 1], then the bytes
+// at the next 16-byte boundary.
+std::shared_ptr<DeviceBuffer> upload_strings(const std::vector<std::string>& v, hy_stream_t s) {
+  const size_t n = v.size();
+  const size_t head = ((4 * (n + 1)) + 15) & ~size_t(15);
+  size_t bytes = 0;
+  for (const auto& x : v) bytes += x.size();
+  Assert(bytes < 0xFFFFFFFFull, "hyrise-amd: a string chunk exceeds 4 GiB");
+  std::vector<char> packed(head + bytes + 16, 0);
+  auto* off = reinterpret_cast<uint32_t*>(packed.data());
+  size_t at = 0;
+  for (size_t i = 0; i < n; ++i) {
+    off[i] = static_cast<uint32_t>(at);
+    std::memcpy(packed.data() + head + at, v[i].data(), v[i].size());
+    at += v[i].size();
+  }
+  off[n] = static_cast<uint32_t>(at);
+  auto buf = upload(packed.data(), packed.size(), s);
+  hy_check(hy_stream_synchronize(s), "hy_stream_synchronize");  // `packed` is pageable and local
+  return buf;
+}
+
 std::shared_ptr<DeviceColumn> device_column(const BaseColumn& column) {
   return column.device_mirror_or_create([&]() {
     hy_stream_t s = operator_stream();
@@ -108,16 +130,15 @@ std::shared_ptr<DeviceColumn> device_column(const BaseColumn& column) {
       d->desc.vid_width = av.width();
       d->desc.dictionary_size = static_cast<uint32_t>(dict->unique_values_count());
       d->desc.data = d->data->get();
-      if (column.data_type() != DataType::String) {
-        resolve_data_type(column.data_type(), [&](auto tag) {
-          using T = decltype(tag);
-          if constexpr (!std::is_same_v<T, std::string>) {
-            const auto& dv = static_cast<const DictionaryColumn<T>&>(column).dictionary();
-            d->dictionary = upload(dv.data(), dv.size() * sizeof(T), s);
-            d->desc.dictionary = d->dictionary->get();
-          }
-        });
-      }
+      resolve_data_type(column.data_type(), [&](auto tag) {
+        using T = decltype(tag);
+        const auto& dv = static_cast<const DictionaryColumn<T>&>(column).dictionary();
+        if constexpr (!std::is_same_v<T, std::string>)
+          d->dictionary = upload(dv.data(), dv.size() * sizeof(T), s);
+        else  // the dictionary's strings, packed (column comparisons and reference scans read them)
+          d->dictionary = upload_strings(dv, s);
+        d->desc.dictionary = d->dictionary->get();
+      });
     } else if (column.encoding_type() == EncodingType::RunLength ||
                column.encoding_type() == EncodingType::FrameOfReference) {
       // encoded chunk: upload the compressed arrays, expand them into a value mirror on the device
@@ -167,21 +188,20 @@ std::shared_ptr<DeviceColumn> device_column(const BaseColumn& column) {
       d->desc.kind = HY_COL_VALUE;
     } else {
       Assert(!column.is_reference(), "device_column of a ReferenceColumn");
-      Assert(column.data_type() != DataType::String,
-             "hyrise-amd: unencoded string columns are not resident on the device (dictionary-encode them)");
       resolve_data_type(column.data_type(), [&](auto tag) {
         using T = decltype(tag);
-        if constexpr (!std::is_same_v<T, std::string>) {
-          const auto& vc = static_cast<const ValueColumn<T>&>(column);
+        const auto& vc = static_cast<const ValueColumn<T>&>(column);
+        if constexpr (!std::is_same_v<T, std::string>)
           d->data = upload(vc.values().data(), vc.values().size() * sizeof(T), s);
-          d->desc.data = d->data->get();
-          if (vc.is_nullable()) {
-            d->nulls = upload(vc.null_values().data(), vc.null_values().size(), s);
-            d->desc.nulls = d->nulls->as<uint8_t>();
-          }
+        else  // ValueColumn<std::string>: the chunk's strings as one packed array
+          d->data = upload_strings(vc.values(), s);
+        d->desc.data = d->data->get();
+        if (vc.is_nullable()) {
+          d->nulls = upload(vc.null_values().data(), vc.null_values().size(), s);
+          d->desc.nulls = d->nulls->as<uint8_t>();
         }
       });
-      d->desc.kind = HY_COL_VALUE;
+      d->desc.kind = column.data_type() == DataType::String ? HY_COL_STRING : HY_COL_VALUE;
     }
     hy_check(hy_stream_synchronize(s), "hy_stream_synchronize");
     return d;

@@ -145,7 +145,7 @@ void dictionary_predicate(const BaseDictionaryColumn& col, PredicateCondition co
 // leaves '[' and ']' as regex syntax, so those patterns behave as the reference's do).
 class LikePattern {
  public:
-  explicit LikePattern(const std::string& pattern) {
+  explicit LikePattern(const std::string& pattern) : _source(pattern) {
     std::vector<std::string> tokens;  // "%" / "_" wildcards, other tokens are literal runs
     std::vector<bool> is_wild;
     for (size_t i = 0; i < pattern.size();) {
@@ -200,6 +200,28 @@ class LikePattern {
     }
   }
 
+  // The pattern the device matcher takes (hy_string_predicate): the simple kinds as the '%'-only pattern they match
+  // (a MultipleContains pattern matches anywhere, so it becomes '%a%b%'; '' matches every string, like '%'), the regex
+  // kind as written.
+  std::string device_pattern(int32_t* regex) const {
+    *regex = _kind == Kind::Regex ? 1 : 0;
+    switch (_kind) {
+      case Kind::StartsWith:
+        return _parts[0] + "%";
+      case Kind::EndsWith:
+        return "%" + _parts[0];
+      case Kind::Contains:
+        return "%" + _parts[0] + "%";
+      case Kind::MultipleContains: {
+        std::string p = "%";
+        for (const auto& x : _parts) p += x + "%";
+        return p;
+      }
+      default:
+        return _source;
+    }
+  }
+
   bool operator()(const std::string& v) const {
     switch (_kind) {
       case Kind::StartsWith:
@@ -227,6 +249,7 @@ class LikePattern {
   Kind _kind = Kind::Regex;
   std::vector<std::string> _parts;
   std::regex _regex;
+  std::string _source;
 };
 
 // LIKE / NOT LIKE over a dictionary chunk (like_table_scan_impl.cpp:48-83, 102-120): the pattern is evaluated once per
@@ -269,27 +292,43 @@ void like_predicate(const BaseDictionaryColumn& column, PredicateCondition cond,
 hy_scan_chunk scan_descriptor(const BaseColumn& column, DataType type, PredicateCondition cond,
                               const AllTypeVariant& value, std::vector<std::shared_ptr<DeviceBuffer>>* keep) {
   hy_scan_chunk sc{};
+  const auto* dict = dynamic_cast<const BaseDictionaryColumn*>(&column);
   if (cond == PredicateCondition::Like || cond == PredicateCondition::NotLike) {
-    const auto* dict = dynamic_cast<const BaseDictionaryColumn*>(&column);
     Assert(type == DataType::String, "LIKE operator only applicable on string columns.");
-    Assert(dict != nullptr,
-           "hyrise-amd: LIKE on an unencoded string column is not supported by the device path (encode the column)");
-    like_predicate(*dict, cond, value, &sc, keep);
+    if (dict)
+      like_predicate(*dict, cond, value, &sc, keep);
+    else  // LikeTableScanImpl on a value column (like_table_scan_impl.cpp:86-97): the device matches every row
+      sc.op = cond == PredicateCondition::Like ? HY_OP_LIKE : HY_OP_NOT_LIKE;
   } else if (cond == PredicateCondition::IsNull || cond == PredicateCondition::IsNotNull) {
     // IsNullTableScanImpl (is_null_table_scan_impl.cpp:35-117): no dictionary rewrite, the null test is per row
-    Assert(type != DataType::String || dynamic_cast<const BaseDictionaryColumn*>(&column) != nullptr,
-           "hyrise-amd: TableScan on an unencoded string column is not supported by the device path");
     sc.op = cond == PredicateCondition::IsNull ? HY_OP_IS_NULL : HY_OP_IS_NOT_NULL;
-  } else if (const auto* dict = dynamic_cast<const BaseDictionaryColumn*>(&column)) {
+  } else if (dict) {
     dictionary_predicate(*dict, cond, value, &sc.op, &sc.search_vid);
   } else {
-    Assert(type != DataType::String,
-           "hyrise-amd: TableScan on an unencoded string column is not supported by the device path");
     sc.op = value_op(cond);
   }
   sc.column = device_column(column)->desc;
   return sc;
 }
+
+// The constant / LIKE pattern of a scan over a string column (hy_string_table_scan / hy_string_reference_scan); the
+// strings are owned here and must outlive the call.
+struct StringScanPredicate {
+  std::string value, pattern;
+  hy_string_predicate pred{};
+  StringScanPredicate(PredicateCondition cond, const AllTypeVariant& v) {
+    if (cond == PredicateCondition::Like || cond == PredicateCondition::NotLike) {
+      Assert(!variant_is_null(v), "Right value must not be NULL.");
+      pattern = LikePattern(type_cast<std::string>(v)).device_pattern(&pred.pattern_regex);
+    } else if (cond != PredicateCondition::IsNull && cond != PredicateCondition::IsNotNull && !variant_is_null(v)) {
+      value = type_cast<std::string>(v);  // type_comparison.hpp:100-123 compares with type_cast<std::string>(value)
+    }
+    pred.value = value.data();
+    pred.value_len = static_cast<uint32_t>(value.size());
+    pred.pattern = pattern.data();
+    pred.pattern_len = static_cast<uint32_t>(pattern.size());
+  }
+};
 
 struct ScanConstant {
   alignas(8) unsigned char bytes[8] = {0};
@@ -404,25 +443,46 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
       sizes.push_back(static_cast<uint32_t>(column->size()));
     }
     if (descs.empty()) return output;
-    const auto constant = null_test || like ? ScanConstant{} : typed_constant(col_type, _right_value);
-    size_t ws_bytes = 0;
-    hy_check(hy_table_scan_workspace_size(sizes.data(), static_cast<uint32_t>(sizes.size()), &ws_bytes),
-             "hy_table_scan_workspace_size");
-    DeviceBuffer ws(ws_bytes, s);
-    // one launch writes every chunk's output RowIDs {chunk id, offset} at its input row range of `rows` (the PosLists
-    // the output chunks share), so no per-chunk expansion launch follows
     auto rows = std::make_shared<DeviceBuffer>(std::max<uint64_t>(total, 1) * sizeof(RowID));
     DeviceBuffer counts(descs.size() * 4, s);
-    hy_check(hy_table_scan_row_ids(descs.data(), static_cast<uint32_t>(descs.size()), hy_type_of(col_type),
-                                   constant.bytes, chunk_ids.data(), rows->as<hy_row_id>(), counts.as<uint32_t>(),
-                                   ws.get(), ws_bytes, s),
-             "hy_table_scan_row_ids");
     std::vector<uint32_t> h_counts(descs.size());
-    hy_check(hy_memcpy_dtoh(h_counts.data(), counts.get(), 4 * descs.size(), s), "hy_memcpy_dtoh");
-    hy_check(hy_stream_synchronize(s), "sync");
-    tr.mark("descriptors + scan + sync");
     std::vector<std::pair<uint64_t, uint32_t>> views;  // (offset, count) per chunk
-    for (size_t k = 0; k < descs.size(); ++k) views.emplace_back(descs[k].out_begin, h_counts[k]);
+    if (col_type == DataType::String) {
+      // string column (unencoded and / or dictionary chunks): the matches arrive compacted, chunk-major
+      const StringScanPredicate sp(_predicate_condition, _right_value);
+      size_t ws_bytes = 0;
+      hy_check(hy_string_table_scan_workspace_size(descs.data(), static_cast<uint32_t>(descs.size()), &sp.pred,
+                                                   &ws_bytes),
+               "hy_string_table_scan_workspace_size");
+      DeviceBuffer ws(ws_bytes, s), n_out(8, s);
+      hy_check(hy_string_table_scan(descs.data(), static_cast<uint32_t>(descs.size()), &sp.pred, chunk_ids.data(),
+                                    rows->as<hy_row_id>(), counts.as<uint32_t>(), n_out.as<uint64_t>(), ws.get(),
+                                    ws_bytes, s),
+               "hy_string_table_scan");
+      hy_check(hy_memcpy_dtoh(h_counts.data(), counts.get(), 4 * descs.size(), s), "hy_memcpy_dtoh");
+      hy_check(hy_stream_synchronize(s), "sync");
+      uint64_t at = 0;
+      for (size_t k = 0; k < descs.size(); ++k) {
+        views.emplace_back(at, h_counts[k]);
+        at += h_counts[k];
+      }
+    } else {
+      const auto constant = null_test || like ? ScanConstant{} : typed_constant(col_type, _right_value);
+      size_t ws_bytes = 0;
+      hy_check(hy_table_scan_workspace_size(sizes.data(), static_cast<uint32_t>(sizes.size()), &ws_bytes),
+               "hy_table_scan_workspace_size");
+      DeviceBuffer ws(ws_bytes, s);
+      // one launch writes every chunk's output RowIDs {chunk id, offset} at its input row range of `rows` (the
+      // PosLists the output chunks share), so no per-chunk expansion launch follows
+      hy_check(hy_table_scan_row_ids(descs.data(), static_cast<uint32_t>(descs.size()), hy_type_of(col_type),
+                                     constant.bytes, chunk_ids.data(), rows->as<hy_row_id>(), counts.as<uint32_t>(),
+                                     ws.get(), ws_bytes, s),
+               "hy_table_scan_row_ids");
+      hy_check(hy_memcpy_dtoh(h_counts.data(), counts.get(), 4 * descs.size(), s), "hy_memcpy_dtoh");
+      hy_check(hy_stream_synchronize(s), "sync");
+      for (size_t k = 0; k < descs.size(); ++k) views.emplace_back(descs[k].out_begin, h_counts[k]);
+    }
+    tr.mark("descriptors + scan + sync");
     // output PosLists are lazy views of `rows` (no copy to the host, no wait: later work is ordered on the stream)
     for (size_t k = 0; k < descs.size(); ++k) {
       if (views[k].second == 0) continue;  // reference table_scan.cpp:99: no empty output chunks
@@ -479,25 +539,41 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
     }
     const auto groups = unordered_map_order(seen);
 
-    size_t ws_bytes = 0;
+    const bool strings = col_type == DataType::String;
+    const StringScanPredicate sp(_predicate_condition, _right_value);
+    size_t ws_bytes = 0;  // also the workspace of hy_pos_list_null_positions
     hy_check(hy_reference_scan_workspace_size(m, &ws_bytes), "hy_reference_scan_workspace_size");
+    if (strings) {
+      size_t sb = 0;
+      hy_check(hy_string_reference_scan_workspace_size(m, static_cast<uint32_t>(rdesc.size()), &sp.pred, &sb),
+               "hy_string_reference_scan_workspace_size");
+      ws_bytes = std::max(ws_bytes, sb);
+    }
     DeviceBuffer ws(ws_bytes, s);
     DeviceBuffer positions(std::max<uint64_t>(m, 1) * 4, s);
     DeviceBuffer count(8, s);
+    // one scan over all referenced chunks: matching positions ascending
+    auto scan_into = [&](uint32_t* out) {
+      if (strings)
+        hy_check(hy_string_reference_scan(dpl->ptr(), m, rdesc.data(), static_cast<uint32_t>(rdesc.size()), &sp.pred,
+                                          out, count.as<uint64_t>(), ws.get(), ws_bytes, s),
+                 "hy_string_reference_scan");
+      else
+        hy_check(hy_reference_scan(dpl->ptr(), m, rdesc.data(), static_cast<uint32_t>(rdesc.size()),
+                                   hy_type_of(col_type), constant.bytes, out, count.as<uint64_t>(), ws.get(), ws_bytes,
+                                   s),
+                 "hy_reference_scan");
+    };
     uint64_t total = 0;
     if (groups.size() <= 1) {
-      hy_check(hy_reference_scan(dpl->ptr(), m, rdesc.data(), static_cast<uint32_t>(rdesc.size()), hy_type_of(col_type),
-                                 constant.bytes, positions.as<uint32_t>(), count.as<uint64_t>(), ws.get(), ws_bytes, s),
-               "hy_reference_scan");
+      scan_into(positions.as<uint32_t>());
       hy_check(hy_memcpy_dtoh(&total, count.get(), 8, s), "dtoh");
       hy_check(hy_stream_synchronize(s), "sync");
     } else {
       // all referenced chunks in one scan (ascending positions), then the matches reordered into the unordered_map's
       // group order (positions ascending inside each group) by one stable sort on the device
       DeviceBuffer asc(std::max<uint64_t>(m, 1) * 4, s);
-      hy_check(hy_reference_scan(dpl->ptr(), m, rdesc.data(), static_cast<uint32_t>(rdesc.size()), hy_type_of(col_type),
-                                 constant.bytes, asc.as<uint32_t>(), count.as<uint64_t>(), ws.get(), ws_bytes, s),
-               "hy_reference_scan");
+      scan_into(asc.as<uint32_t>());
       hy_check(hy_memcpy_dtoh(&total, count.get(), 8, s), "dtoh");
       hy_check(hy_stream_synchronize(s), "sync");
       std::vector<uint32_t> rank(rtable->chunk_count(), 0);
@@ -852,7 +928,6 @@ std::shared_ptr<Table> column_comparison_scan(const std::shared_ptr<const Table>
   const auto lt = in_table->column_data_type(left_column_id);
   const auto rt = in_table->column_data_type(right_column_id);
   Assert((lt == DataType::String) == (rt == DataType::String), "Invalid column combination detected!");
-  Assert(lt != DataType::String, "hyrise-amd: column comparison of string columns is not supported by the device path");
   require_device();
   hy_stream_t s = operator_stream();
   JoinSideInput l = describe_side(in_table, left_column_id);
@@ -864,9 +939,11 @@ std::shared_ptr<Table> column_comparison_scan(const std::shared_ptr<const Table>
     rc.push_back(r.chunks[c]);
   }
   if (lc.empty()) return output;
-  hy_join_side ls{lc.data(), static_cast<uint32_t>(lc.size()), hy_type_of(lt), l.referenced.data(),
+  // string columns: packed strings on the device (value chunks and dictionaries), compared as std::string's operators
+  const auto dtype = [](DataType t) { return t == DataType::String ? int32_t{HY_TYPE_STRING} : hy_type_of(t); };
+  hy_join_side ls{lc.data(), static_cast<uint32_t>(lc.size()), dtype(lt), l.referenced.data(),
                   static_cast<uint32_t>(l.referenced.size()), 0, 0};
-  hy_join_side rs{rc.data(), static_cast<uint32_t>(rc.size()), hy_type_of(rt), r.referenced.data(),
+  hy_join_side rs{rc.data(), static_cast<uint32_t>(rc.size()), dtype(rt), r.referenced.data(),
                   static_cast<uint32_t>(r.referenced.size()), 0, 0};
   const bool is_ref = in_table->type() == TableType::References;
   size_t ws_bytes = 0;

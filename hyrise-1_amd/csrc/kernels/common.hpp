@@ -88,6 +88,48 @@ __device__ __forceinline__ bool cmp_op(int op, T v, T c) {
 }
 
 // ------------------------------------------------------------------------------------------------------------
+// std::string values on the device: packed string arrays (include/hyrise_amd.h, "Column chunk descriptors").
+// ------------------------------------------------------------------------------------------------------------
+struct DevString {
+  const unsigned char* p;
+  uint32_t n;
+};
+
+// String i of a packed string array of `count` strings
+__device__ inline DevString packed_string(const void* packed, uint32_t count, uint32_t i) {
+  const uint32_t* off = static_cast<const uint32_t*>(packed);
+  const uint32_t b = off[i], e = off[i + 1];
+  const uintptr_t bytes = (reinterpret_cast<uintptr_t>(packed) + 4ull * (count + 1) + 15) & ~uintptr_t(15);
+  return DevString{reinterpret_cast<const unsigned char*>(bytes) + b, e - b};
+}
+
+// std::string::compare (char_traits<char>::compare: bytes as unsigned char, then the length): <0, 0, >0
+__device__ inline int string_compare(DevString a, DevString b) {
+  const uint32_t n = a.n < b.n ? a.n : b.n;
+  for (uint32_t i = 0; i < n; ++i)
+    if (a.p[i] != b.p[i]) return a.p[i] < b.p[i] ? -1 : 1;
+  return a.n < b.n ? -1 : (a.n > b.n ? 1 : 0);
+}
+
+// HY_OP_EQ..HY_OP_GE applied to a three-way comparison result
+__device__ inline bool cmp_result(int op, int c) {
+  switch (op) {
+    case HY_OP_EQ:
+      return c == 0;
+    case HY_OP_NE:
+      return c != 0;
+    case HY_OP_LT:
+      return c < 0;
+    case HY_OP_LE:
+      return c <= 0;
+    case HY_OP_GT:
+      return c > 0;
+    default:
+      return c >= 0;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
 // Wave64 helpers.
 // ------------------------------------------------------------------------------------------------------------
 __device__ inline int lane_id() { return __lane_id(); }

@@ -43,7 +43,7 @@ typedef struct hy_row_id {
 } hy_row_id;
 
 /* Column data types (reference src/lib/all_type_variant.hpp data_types). */
-enum { HY_TYPE_INT32 = 1, HY_TYPE_INT64 = 2, HY_TYPE_FLOAT = 3, HY_TYPE_DOUBLE = 4 };
+enum { HY_TYPE_INT32 = 1, HY_TYPE_INT64 = 2, HY_TYPE_FLOAT = 3, HY_TYPE_DOUBLE = 4, HY_TYPE_STRING = 5 };
 
 /* ---------------------------------------------------------------------------------------------------------------
  * Runtime
@@ -103,9 +103,18 @@ const char* hy_build_info(void);
  *                     dictionary = T[dictionary_size] sorted unique, null_value_id = dictionary_size
  *                     (reference dictionary_column/dictionary_encoder.hpp:87)
  *
+ *   HY_COL_STRING     ValueColumn<std::string> (same reference file): data = a packed string array (below) of
+ *                     the chunk's size values, nulls as HY_COL_VALUE. A DICT chunk of strings keeps its attribute
+ *                     vector in data and, when its strings are device-resident, a packed string array of its
+ *                     dictionary_size entries in dictionary.
+ *   packed string array of n strings: uint32 offsets[n + 1] (offsets[i] = byte start of string i, offsets[n] = total
+ *                     bytes), then the bytes at (const char*)offsets + 4 * (n + 1) rounded up to 16. String i is
+ *                     bytes[offsets[i], offsets[i + 1]) - std::string's value, compared byte-wise as unsigned char
+ *                     (std::char_traits<char>::compare).
+ *
  * All device pointers must be 16-byte aligned; buffers must be readable up to the next multiple of 16 bytes.
  * ------------------------------------------------------------------------------------------------------------- */
-enum { HY_COL_VALUE = 0, HY_COL_DICT = 1 };
+enum { HY_COL_VALUE = 0, HY_COL_DICT = 1, HY_COL_STRING = 2 };
 
 typedef struct hy_column_chunk {
   const void* data;          /* values (VALUE) or attribute vector (DICT) */
@@ -149,7 +158,12 @@ enum {
    * evaluates the pattern once per dictionary entry (LikeTableScanImpl::_find_matches_in_dictionary,
    * like_table_scan_impl.cpp:48-83, 102-120) and the device scans the attribute vector against that set. Scans only
    * (the fused filters of hy_scan_join_hash / hy_aggregate reject it). */
-  HY_OP_VID_SET = 10
+  HY_OP_VID_SET = 10,
+  /* STRING chunks only (hy_string_table_scan / hy_string_reference_scan): the row's value matches / does not match
+   * the LIKE pattern of the call's hy_string_predicate (LikeTableScanImpl on a value column,
+   * like_table_scan_impl.cpp:22-31, 86-97, with the reference's LikeMatcher, like_matcher.cpp:9-118). */
+  HY_OP_LIKE = 11,
+  HY_OP_NOT_LIKE = 12
 };
 
 typedef struct hy_scan_chunk {
@@ -236,6 +250,46 @@ hy_status hy_pos_list_chunk_first_seen(const hy_row_id* pos_list, uint64_t n, ui
 /* out[i] = {chunk_id, offsets[i]} — expands a single-chunk offset list into reference RowIDs. */
 hy_status hy_expand_row_ids(uint32_t chunk_id, const uint32_t* offsets, uint64_t n, hy_row_id* out,
                             hy_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------------------------
+ * String scans (std::string columns; reference SingleColumnTableScanImpl / LikeTableScanImpl / IsNullTableScanImpl
+ * on a ValueColumn<std::string>, single_column_table_scan_impl.cpp:38-85, like_table_scan_impl.cpp:22-31, 86-97,
+ * is_null_table_scan_impl.cpp:35-117)
+ *
+ * Chunks are HY_COL_STRING (compared with pred->value: HY_OP_EQ..HY_OP_GE as std::string::compare, unsigned bytes then
+ * length; HY_OP_LIKE / HY_OP_NOT_LIKE against pred->pattern; IS [NOT] NULL, ALL, NONE) or HY_COL_DICT (op + search_vid
+ * or HY_OP_VID_SET exactly as hy_table_scan: the host's dictionary rewrite). A table may mix both (an unencoded chunk
+ * beside dictionary chunks). NULL rows never match a comparison or LIKE.
+ * pattern_regex: 0 for the reference's simple patterns (LikeMatcher::pattern_string_to_pattern_tokens gives
+ * StartsWith / EndsWith / Contains / MultipleContains: '%' and '_' match any byte), 1 for every other pattern (the
+ * reference's std::regex path, like_matcher.cpp:27-52: '%' and '_' match any byte but '\n' / '\r'; '[...]' is a
+ * character class of the bytes inside, '%' inside one meaning '.' and '*', '_' meaning '.'). At most 63 pattern
+ * positions; "x-y" ranges of plain bytes; anything else the regex would reject -> HY_ERR_UNSUPPORTED.
+ * ------------------------------------------------------------------------------------------------------------- */
+typedef struct hy_string_predicate {
+  const char* value;      /* HOST: the constant (comparison ops), value_len bytes */
+  uint32_t value_len;
+  int32_t pattern_regex;  /* see above */
+  const char* pattern;    /* HOST: the LIKE pattern (HY_OP_LIKE / HY_OP_NOT_LIKE), pattern_len bytes */
+  uint32_t pattern_len;
+  uint32_t reserved;
+} hy_string_predicate;
+
+/* Data input: the matches of all chunks as RowIDs {chunk_ids[c], offset}, chunk-major, offsets ascending, at out_rows
+ * (device, capacity = rows); counts[c] (device) per chunk, *n_out (device) in total. chunks / chunk_ids: HOST arrays
+ * (out_begin unused). */
+hy_status hy_string_table_scan_workspace_size(const hy_scan_chunk* chunks, uint32_t n_chunks,
+                                              const hy_string_predicate* pred, size_t* bytes);
+hy_status hy_string_table_scan(const hy_scan_chunk* chunks, uint32_t n_chunks, const hy_string_predicate* pred,
+                               const uint32_t* chunk_ids, hy_row_id* out_rows, uint32_t* counts, uint64_t* n_out,
+                               void* workspace, size_t workspace_bytes, hy_stream_t stream);
+/* Reference input: as hy_reference_scan (positions of matching pos_list entries, ascending; NULL RowIDs never match). */
+hy_status hy_string_reference_scan_workspace_size(uint64_t pos_list_size, uint32_t n_referenced,
+                                                  const hy_string_predicate* pred, size_t* bytes);
+hy_status hy_string_reference_scan(const hy_row_id* pos_list, uint64_t pos_list_size,
+                                   const hy_scan_chunk* referenced_chunks, uint32_t n_referenced_chunks,
+                                   const hy_string_predicate* pred, uint32_t* out_positions, uint64_t* count,
+                                   void* workspace, size_t workspace_bytes, hy_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------------------------
  * Validate (MVCC visibility, reference src/lib/operators/validate.cpp:14-95)
@@ -348,7 +402,9 @@ typedef struct hy_join_side {
  * {left.chunks[c].chunk_id, i} (out_rows) or as chunk offsets (out_offsets) - exactly one of the two. counts[c]
  * (device, n_chunks) receives the matches of chunk c, *n_out (device) their total; chunk c's matches start at the sum
  * of counts of the chunks before it. Sides are hy_join_side descriptors (value_type, chunks, referenced chunks);
- * fuse_dereference is ignored. Non-numeric (string) columns: HY_ERR_UNSUPPORTED.
+ * fuse_dereference is ignored. String columns: both value types HY_TYPE_STRING (a string and a numeric column:
+ * HY_ERR_INVALID_ARGUMENT), chunks HY_COL_STRING or HY_COL_DICT with a packed string dictionary, compared as
+ * std::string's operators (unsigned bytes, then length).
  */
 hy_status hy_column_compare_scan_workspace_size(const hy_join_side* left, const hy_join_side* right, int32_t out_rows,
                                                 size_t* bytes);
