@@ -68,6 +68,8 @@ load_table = _host.load_table
 import_binary = _host.import_binary
 export_binary = _host.export_binary
 load_to_device = _host.load_to_device
+VectorCompressionType = _host.VectorCompressionType
+compress_vector = _host.compress_vector
 encode_chunks = _host.encode_chunks
 encode_all_chunks = _host.encode_all_chunks
 encode_columns = _host.encode_columns

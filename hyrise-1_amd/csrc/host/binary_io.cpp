@@ -110,6 +110,8 @@ void export_column(std::ofstream& f, const BaseColumn& column) {
   if (const auto* dc = dynamic_cast<const DictionaryColumn<T>*>(&column)) {  // export_binary.cpp:186-219
     write_value(f, BinaryColumnType::dictionary_column);
     const auto& av = dc->attribute_vector();
+    Assert(av.compression() == VectorCompressionType::FixedSizeByteAligned,  // export_binary.cpp:243-254
+           "Does only support fixed-size byte-aligned compressed attribute vectors.");
     write_value(f, static_cast<uint8_t>(av.width()));
     write_value(f, static_cast<uint32_t>(dc->dictionary().size()));
     write_values(f, dc->dictionary());

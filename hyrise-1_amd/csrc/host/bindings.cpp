@@ -160,6 +160,9 @@ PYBIND11_MODULE(_hyrise_host, m) {
       .value("RunLength", EncodingType::RunLength)
       .value("FixedStringDictionary", EncodingType::FixedStringDictionary)
       .value("FrameOfReference", EncodingType::FrameOfReference);
+  py::enum_<VectorCompressionType>(m, "VectorCompressionType")
+      .value("FixedSizeByteAligned", VectorCompressionType::FixedSizeByteAligned)
+      .value("SimdBp128", VectorCompressionType::SimdBp128);
   py::enum_<AggregateFunction>(m, "AggregateFunction")
       .value("Min", AggregateFunction::Min)
       .value("Max", AggregateFunction::Max)
@@ -187,6 +190,25 @@ PYBIND11_MODULE(_hyrise_host, m) {
         const auto* d = dynamic_cast<const BaseDictionaryColumn*>(&c);
         Assert(d != nullptr, "not a dictionary column");
         return d->attribute_vector().width();
+      })
+      .def("attribute_vector_compression", [](const BaseColumn& c) {
+        const auto* d = dynamic_cast<const BaseDictionaryColumn*>(&c);
+        Assert(d != nullptr, "not a dictionary column");
+        return d->attribute_vector().compression();
+      })
+      .def("attribute_vector_bytes", [](const BaseColumn& c) {  // FSBA ids or the SIMD-BP128 words
+        const auto* d = dynamic_cast<const BaseDictionaryColumn*>(&c);
+        Assert(d != nullptr, "not a dictionary column");
+        const auto& b = d->attribute_vector().bytes();
+        return py::bytes(reinterpret_cast<const char*>(b.data()), b.size());
+      })
+      .def("attribute_vector_ids", [](const BaseColumn& c) {  // every id through the vector's own decoder
+        const auto* d = dynamic_cast<const BaseDictionaryColumn*>(&c);
+        Assert(d != nullptr, "not a dictionary column");
+        const auto& av = d->attribute_vector();
+        std::vector<uint32_t> out(av.size());
+        for (size_t i = 0; i < out.size(); ++i) out[i] = av.get(i);
+        return out;
       })
       .def("lower_bound", [](const BaseColumn& c, py::object v) {
         const auto* d = dynamic_cast<const BaseDictionaryColumn*>(&c);
@@ -277,9 +299,22 @@ PYBIND11_MODULE(_hyrise_host, m) {
   m.def("export_binary", [](std::shared_ptr<Table> t, const std::string& f) { export_binary(t, f); },
         py::arg("table"), py::arg("filename"));
   m.def("load_to_device", [](std::shared_ptr<Table> t) { load_to_device(t); }, py::arg("table"));
-  m.def("encode_chunks", &ChunkEncoder::encode_chunks);
-  m.def("encode_all_chunks", &ChunkEncoder::encode_all_chunks);
-  m.def("encode_columns", &ChunkEncoder::encode_columns);
+  // the attribute-vector compressor on its own (SIMD-BP128 / FixedSizeByteAligned): (bytes, meta offsets, ids read
+  // back through the vector's decoder) - for the parity tests of the packing
+  m.def("compress_vector", [](const std::vector<uint32_t>& ids, uint32_t max_value, VectorCompressionType c) {
+    const AttributeVector av(ids, max_value, c);
+    std::vector<uint32_t> back(av.size());
+    for (size_t i = 0; i < back.size(); ++i) back[i] = av.get(i);
+    const auto& b = av.bytes();
+    return py::make_tuple(py::bytes(reinterpret_cast<const char*>(b.data()), b.size()), av.meta_offsets(), back,
+                          av.width());
+  });
+  m.def("encode_chunks", &ChunkEncoder::encode_chunks, py::arg("table"), py::arg("chunk_ids"), py::arg("encoding"),
+        py::arg("vector_compression") = VectorCompressionType::FixedSizeByteAligned);
+  m.def("encode_all_chunks", &ChunkEncoder::encode_all_chunks, py::arg("table"), py::arg("encoding"),
+        py::arg("vector_compression") = VectorCompressionType::FixedSizeByteAligned);
+  m.def("encode_columns", &ChunkEncoder::encode_columns, py::arg("table"), py::arg("column_ids"), py::arg("encoding"),
+        py::arg("vector_compression") = VectorCompressionType::FixedSizeByteAligned);
   m.def("synchronize", []() { hy_check(hy_stream_synchronize(operator_stream()), "hy_stream_synchronize"); },
         "Waits for the calling thread's operator stream (operator outputs are produced asynchronously).");
   m.def("join_hashed_type", &join_hashed_type);

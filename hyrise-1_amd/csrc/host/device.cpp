@@ -125,7 +125,18 @@ std::shared_ptr<DeviceColumn> device_column(const BaseColumn& column) {
     d->desc.size = static_cast<uint32_t>(column.size());
     if (const auto* dict = dynamic_cast<const BaseDictionaryColumn*>(&column)) {
       const auto& av = dict->attribute_vector();
-      d->data = upload(av.bytes().data(), av.bytes().size(), s);
+      if (av.compression() == VectorCompressionType::SimdBp128) {
+        // the packed words cross PCIe; the kernels read the FixedSizeByteAligned ids decoded from them in HBM
+        const auto words = upload(av.bytes().data(), av.bytes().size(), s);
+        const auto meta = upload(av.meta_offsets().data(), av.meta_offsets().size() * 4, s);
+        d->data = std::make_shared<DeviceBuffer>(std::max<size_t>(av.size(), 1) * av.width() + 16);
+        hy_check(hy_decode_simd_bp128(words->get(), meta->as<uint32_t>(), static_cast<uint32_t>(av.size()), av.width(),
+                                      d->data->get(), s),
+                 "hy_decode_simd_bp128");
+        hy_check(hy_stream_synchronize(s), "sync");  // words / meta are released at scope end
+      } else {
+        d->data = upload(av.bytes().data(), av.bytes().size(), s);
+      }
       d->desc.kind = HY_COL_DICT;
       d->desc.vid_width = av.width();
       d->desc.dictionary_size = static_cast<uint32_t>(dict->unique_values_count());

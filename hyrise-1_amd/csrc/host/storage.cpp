@@ -102,8 +102,83 @@ AllTypeVariant Table::get_value(ColumnID column_id, uint64_t row) const {
   Fail("Row does not exist.");
 }
 
+AttributeVector::AttributeVector(const std::vector<uint32_t>& vids, uint32_t max_value,
+                                 VectorCompressionType compression)
+    : _compression(compression) {
+  // reference fixed_size_byte_aligned_compressor.cpp:21-30: narrowest width that holds max_value
+  _width = max_value <= 0xFFu ? 1 : (max_value <= 0xFFFFu ? 2 : 4);
+  _size = vids.size();
+  if (compression == VectorCompressionType::FixedSizeByteAligned) {
+    _bytes.resize(_size * _width);
+    for (size_t i = 0; i < _size; ++i) {
+      const uint32_t v = vids[i];
+      std::memcpy(_bytes.data() + i * _width, &v, _width);  // little endian
+    }
+    return;
+  }
+  // SIMD-BP128 (simd_bp128_compressor.cpp:13-120): meta blocks of 16 x 128 ids, the last one zero-padded; a meta
+  // block's header word holds the 16 blocks' bit widths (the bits of the OR of the block's ids); then each of the
+  // first ceil(ids left / 128) blocks packed into `width` words.
+  std::vector<uint32_t> words;  // 4 per 16-byte word
+  for (size_t m0 = 0; m0 < _size; m0 += BP128_META) {
+    _meta.push_back(static_cast<uint32_t>(words.size() / 4));
+    const size_t in_meta = std::min<size_t>(BP128_META, _size - m0);
+    uint32_t widths[BP128_BLOCKS] = {0};
+    for (uint32_t b = 0; b < BP128_BLOCKS; ++b) {
+      uint32_t acc = 0;
+      for (uint32_t i = 0; i < BP128_BLOCK; ++i) {
+        const size_t k = m0 + b * BP128_BLOCK + i;
+        if (k < _size) acc |= vids[k];
+      }
+      while (acc) {
+        ++widths[b];
+        acc >>= 1;
+      }
+    }
+    uint32_t header[4] = {0, 0, 0, 0};
+    uint8_t wb[16];
+    for (uint32_t b = 0; b < BP128_BLOCKS; ++b) wb[b] = static_cast<uint8_t>(widths[b]);
+    std::memcpy(header, wb, 16);
+    words.insert(words.end(), header, header + 4);
+    const uint32_t blocks = static_cast<uint32_t>((in_meta + BP128_BLOCK - 1) / BP128_BLOCK);
+    for (uint32_t b = 0; b < blocks; ++b) {
+      const uint32_t w = widths[b];
+      const size_t base = words.size();
+      words.resize(base + 4 * w, 0u);
+      for (uint32_t i = 0; i < BP128_BLOCK && w; ++i) {
+        const size_t k = m0 + b * BP128_BLOCK + i;
+        const uint64_t v = k < _size ? vids[k] : 0u;
+        const uint32_t lane = i & 3u, bit = (i >> 2) * w, word = bit >> 5, shift = bit & 31u;
+        words[base + 4 * word + lane] |= static_cast<uint32_t>(v << shift);
+        if (shift + w > 32) words[base + 4 * (word + 1) + lane] |= static_cast<uint32_t>(v >> (32 - shift));
+      }
+    }
+  }
+  _bytes.resize(words.size() * 4);
+  if (!words.empty()) std::memcpy(_bytes.data(), words.data(), _bytes.size());
+}
+
+uint32_t AttributeVector::bp128_get(size_t i) const {
+  const size_t m = i / BP128_META;
+  const uint32_t b = static_cast<uint32_t>((i % BP128_META) / BP128_BLOCK), j = static_cast<uint32_t>(i % BP128_BLOCK);
+  const uint8_t* header = _bytes.data() + 16ull * _meta[m];
+  size_t word = _meta[m] + 1;
+  for (uint32_t k = 0; k < b; ++k) word += header[k];
+  const uint32_t w = header[b];
+  if (w == 0) return 0;
+  const uint32_t lane = j & 3u, bit = (j >> 2) * w, wi = bit >> 5, shift = bit & 31u;
+  auto lane_word = [&](size_t k) {
+    uint32_t v;
+    std::memcpy(&v, _bytes.data() + 16 * k + 4 * lane, 4);
+    return v;
+  };
+  uint64_t v = lane_word(word + wi) >> shift;
+  if (shift + w > 32) v |= static_cast<uint64_t>(lane_word(word + wi + 1)) << (32 - shift);
+  return w == 32 ? static_cast<uint32_t>(v) : static_cast<uint32_t>(v & ((1u << w) - 1u));
+}
+
 // reference dictionary_column/dictionary_encoder.hpp:57-130
-std::shared_ptr<BaseColumn> encode_dictionary(const BaseColumn& base) {
+std::shared_ptr<BaseColumn> encode_dictionary(const BaseColumn& base, VectorCompressionType compression) {
   std::shared_ptr<BaseColumn> out;
   resolve_data_type(base.data_type(), [&](auto tag) {
     using T = decltype(tag);
@@ -127,7 +202,7 @@ std::shared_ptr<BaseColumn> encode_dictionary(const BaseColumn& base) {
       }
     }
     const uint32_t max_value = static_cast<uint32_t>(dict.size() + 1u);
-    auto av = std::make_shared<const AttributeVector>(vids, max_value);
+    auto av = std::make_shared<const AttributeVector>(vids, max_value, compression);
     out = std::make_shared<DictionaryColumn<T>>(std::make_shared<const std::vector<T>>(std::move(dict)), std::move(av),
                                                 null_value_id);
   });
@@ -202,10 +277,11 @@ std::shared_ptr<BaseColumn> encode_frame_of_reference(const BaseColumn& base) {
 }
 
 namespace {
-std::shared_ptr<BaseColumn> encode_column(const BaseColumn& col, EncodingType encoding) {
+std::shared_ptr<BaseColumn> encode_column(const BaseColumn& col, EncodingType encoding,
+                                          VectorCompressionType compression) {
   switch (encoding) {
     case EncodingType::Dictionary:
-      return encode_dictionary(col);
+      return encode_dictionary(col, compression);
     case EncodingType::RunLength:
       return encode_run_length(col);
     case EncodingType::FrameOfReference:
@@ -217,7 +293,7 @@ std::shared_ptr<BaseColumn> encode_column(const BaseColumn& col, EncodingType en
 }  // namespace
 
 void ChunkEncoder::encode_chunks(const std::shared_ptr<Table>& table, const std::vector<ChunkID>& chunk_ids,
-                                 EncodingType encoding) {
+                                 EncodingType encoding, VectorCompressionType compression) {
   Assert(table->type() == TableType::Data, "Only data tables can be encoded");
   if (encoding == EncodingType::Unencoded) return;
   if (encoding == EncodingType::FixedStringDictionary)
@@ -232,13 +308,13 @@ void ChunkEncoder::encode_chunks(const std::shared_ptr<Table>& table, const std:
       if (encoding == EncodingType::FrameOfReference && col->data_type() != DataType::Int &&
           col->data_type() != DataType::Long)
         continue;
-      chunk->replace_column(c, encode_column(*col, encoding));
+      chunk->replace_column(c, encode_column(*col, encoding, compression));
     }
   }
 }
 
 void ChunkEncoder::encode_columns(const std::shared_ptr<Table>& table, const std::vector<ColumnID>& column_ids,
-                                  EncodingType encoding) {
+                                  EncodingType encoding, VectorCompressionType compression) {
   Assert(table->type() == TableType::Data, "Only data tables can be encoded");
   if (encoding == EncodingType::Unencoded) return;
   if (encoding != EncodingType::Dictionary)
@@ -252,7 +328,8 @@ void ChunkEncoder::encode_columns(const std::shared_ptr<Table>& table, const std
       const auto chunk = table->get_chunk(c);
       for (const auto col_id : column_ids) {
         const auto col = chunk->get_column(col_id);
-        if (col->encoding_type() != EncodingType::Dictionary) chunk->replace_column(col_id, encode_dictionary(*col));
+        if (col->encoding_type() != EncodingType::Dictionary)
+          chunk->replace_column(col_id, encode_dictionary(*col, compression));
       }
     }
   };
@@ -262,10 +339,11 @@ void ChunkEncoder::encode_columns(const std::shared_ptr<Table>& table, const std
   for (auto& t : pool) t.join();
 }
 
-void ChunkEncoder::encode_all_chunks(const std::shared_ptr<Table>& table, EncodingType encoding) {
+void ChunkEncoder::encode_all_chunks(const std::shared_ptr<Table>& table, EncodingType encoding,
+                                     VectorCompressionType compression) {
   std::vector<ChunkID> ids(table->chunk_count());
   for (ChunkID i = 0; i < ids.size(); ++i) ids[i] = i;
-  encode_chunks(table, ids, encoding);
+  encode_chunks(table, ids, encoding, compression);
 }
 
 namespace {

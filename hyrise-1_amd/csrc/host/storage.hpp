@@ -12,6 +12,7 @@
 // Every column can carry a device-resident mirror (device.hpp) that GPU operators create on first use.
 #pragma once
 
+#include <cstring>
 #include <limits>
 #include <algorithm>
 #include <memory>
@@ -118,24 +119,25 @@ class ValueColumn final : public BaseColumn {
   std::optional<std::vector<uint8_t>> _nulls;
 };
 
-// FixedSizeByteAligned attribute vector: uint8 / uint16 / uint32 value ids.
+// Attribute vector of value ids, in one of the reference's two compressions:
+//   FixedSizeByteAligned  uint8 / uint16 / uint32 per id, the narrowest that holds max_value
+//                         (reference fixed_size_byte_aligned_compressor.cpp:21-30)
+//   SimdBp128             the reference's SIMD-BP128 bit packing (vector_compression/simd_bp128/): 16-byte words;
+//                         per meta block of 16 x 128 ids one word of 16 bit widths, then per block `width` words in
+//                         which id i of the block sits in 32-bit lane i % 4, at bit (i / 4) * width of that lane's
+//                         little-endian bit stream (simd_bp128_packing.cpp:22-157, simd_bp128_compressor.cpp:13-120).
+//                         meta_offsets()[m] = index of meta block m's header word (host-side index, from the sizes).
+//                         width() is the byte width of the id's FixedSizeByteAligned form (the device mirror's).
 class AttributeVector {
  public:
   AttributeVector() = default;
-  AttributeVector(const std::vector<uint32_t>& vids, uint32_t max_value) {
-    // reference fixed_size_byte_aligned_compressor.cpp:21-30: narrowest width that holds max_value
-    _width = max_value <= 0xFFu ? 1 : (max_value <= 0xFFFFu ? 2 : 4);
-    _size = vids.size();
-    _bytes.resize(_size * _width);
-    for (size_t i = 0; i < _size; ++i) {
-      const uint32_t v = vids[i];
-      std::memcpy(_bytes.data() + i * _width, &v, _width);  // little endian
-    }
-  }
+  AttributeVector(const std::vector<uint32_t>& vids, uint32_t max_value,
+                  VectorCompressionType compression = VectorCompressionType::FixedSizeByteAligned);
   AttributeVector(std::vector<uint8_t>&& bytes, int width, size_t size)
       : _bytes(std::move(bytes)), _width(width), _size(size) {}
 
   uint32_t get(size_t i) const {
+    if (_compression == VectorCompressionType::SimdBp128) return bp128_get(i);
     switch (_width) {
       case 1:
         return _bytes[i];
@@ -153,12 +155,21 @@ class AttributeVector {
   }
   int width() const { return _width; }
   size_t size() const { return _size; }
+  VectorCompressionType compression() const { return _compression; }
+  // FixedSizeByteAligned: the ids; SimdBp128: the packed 16-byte words
   const std::vector<uint8_t>& bytes() const { return _bytes; }
+  const std::vector<uint32_t>& meta_offsets() const { return _meta; }
+
+  static constexpr uint32_t BP128_BLOCK = 128, BP128_BLOCKS = 16, BP128_META = BP128_BLOCK * BP128_BLOCKS;
 
  private:
+  uint32_t bp128_get(size_t i) const;
+
   std::vector<uint8_t> _bytes;
   int _width = 1;
   size_t _size = 0;
+  VectorCompressionType _compression = VectorCompressionType::FixedSizeByteAligned;
+  std::vector<uint32_t> _meta;
 };
 
 // RunLengthColumn (reference storage/run_length_column.hpp): one value + NULL flag per run, end_positions[r] = last
@@ -384,17 +395,23 @@ class Table {
 std::shared_ptr<BaseColumn> make_value_column(DataType t, bool nullable);
 
 // Dictionary encoding of one value column (reference dictionary_encoder.hpp:57-130).
-std::shared_ptr<BaseColumn> encode_dictionary(const BaseColumn& value_column);
+std::shared_ptr<BaseColumn> encode_dictionary(
+    const BaseColumn& value_column, VectorCompressionType compression = VectorCompressionType::FixedSizeByteAligned);
 
 // ChunkEncoder (reference src/lib/storage/chunk_encoder.cpp): encode chunks of a data table. Only Unencoded and
 // Dictionary exist on the device path; other encodings are rejected.
+// The vector compression applies to Dictionary's attribute vectors (reference ChunkEncodingSpec's
+// vector_compression_type); the other encodings keep FixedSizeByteAligned.
 struct ChunkEncoder {
   static void encode_chunks(const std::shared_ptr<Table>& table, const std::vector<ChunkID>& chunk_ids,
-                            EncodingType encoding);
-  static void encode_all_chunks(const std::shared_ptr<Table>& table, EncodingType encoding);
+                            EncodingType encoding,
+                            VectorCompressionType compression = VectorCompressionType::FixedSizeByteAligned);
+  static void encode_all_chunks(const std::shared_ptr<Table>& table, EncodingType encoding,
+                                VectorCompressionType compression = VectorCompressionType::FixedSizeByteAligned);
   // every chunk's columns column_ids (the others stay as they are); chunks in parallel
   static void encode_columns(const std::shared_ptr<Table>& table, const std::vector<ColumnID>& column_ids,
-                             EncodingType encoding);
+                             EncodingType encoding,
+                             VectorCompressionType compression = VectorCompressionType::FixedSizeByteAligned);
 };
 
 std::shared_ptr<Table> load_table(const std::string& file_name, uint32_t chunk_size = CHUNK_MAX_SIZE);

@@ -230,6 +230,8 @@ enum class PredicateCondition {
 enum class JoinMode { Inner, Left, Right, Outer, Cross, Semi, Anti };
 enum class TableType { References, Data };
 enum class EncodingType : uint8_t { Unencoded, Dictionary, RunLength, FixedStringDictionary, FrameOfReference };
+// reference storage/vector_compression/vector_compression.hpp: how a DictionaryColumn's attribute vector is stored
+enum class VectorCompressionType : uint8_t { FixedSizeByteAligned, SimdBp128 };
 enum class AggregateFunction { Min, Max, Sum, Avg, Count, CountDistinct };
 
 struct NullValue {

@@ -324,6 +324,13 @@ hy_status hy_validate_pos_list(const hy_row_id* pos_list, uint64_t pos_list_size
 /* ---------------------------------------------------------------------------------------------------------------
  * Encoded chunks -> value mirrors in HBM (all pointers device)
  * ------------------------------------------------------------------------------------------------------------- */
+/* SIMD-BP128 attribute vector (reference vector_compression/simd_bp128/, simd_bp128_decompressor.cpp) -> the
+ * FixedSizeByteAligned ids (out_width 1 / 2 / 4 bytes per id). words: the 16-byte words of the packing (per meta block
+ * of 2048 ids a header word of 16 bit widths, then each 128-id block's `width` words, id j of a block in 32-bit lane
+ * j % 4 at bit (j / 4) * width of that lane's stream); meta_offsets[m]: index (in 16-byte words) of meta block m's
+ * header, ceil(n_rows / 2048) entries. */
+hy_status hy_decode_simd_bp128(const void* words, const uint32_t* meta_offsets, uint32_t n_rows, int32_t out_width,
+                               void* out, hy_stream_t stream);
 /* RunLengthColumn (reference storage/run_length_column.hpp, run_length_column.cpp:24-36): row i takes the value and
  * NULL flag of the first run r with end_positions[r] >= i. value_bytes 4 or 8; out_nulls may be NULL. */
 hy_status hy_decode_run_length(const void* values, const uint8_t* run_nulls, const uint32_t* end_positions,
