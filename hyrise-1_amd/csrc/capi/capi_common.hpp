@@ -31,6 +31,13 @@ inline hipStream_t S(hy_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+// Chunk kinds every row-wise reader (join, aggregate, projection, column compare) takes: values and dictionaries.
+// Compressed RunLength / FrameOfReference chunks are scanned only (hy_table_scan family); the others read their
+// decoded value mirrors.
+inline bool row_readable(const hy_column_chunk& c) {
+  return c.size == 0 || c.kind == HY_COL_VALUE || c.kind == HY_COL_DICT;
+}
+
 // Host -> device copies of the descriptors a call builds on the host (chunk / side / column tables, offsets): staged
 // through a per-thread pinned ring so that hipMemcpyAsync is a real asynchronous DMA (a pageable source makes the
 // runtime stage it synchronously, at a fraction of the bandwidth - measurable with tens of thousands of chunks), and

@@ -2,6 +2,7 @@
 // the gfx950 TableScan / JoinHash kernels. Nothing here throws across the boundary; every failure becomes an
 // hy_status plus a thread-local message.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -195,17 +196,20 @@ const char* hy_build_info(void) { return "hyrise-amd gfx950 (CDNA4) HIP kernels:
 // ================================================================================================================
 namespace {
 
-enum ScanClass { SC_DICT8, SC_DICT16, SC_DICT32, SC_VALUE, SC_COUNT };
+enum ScanClass { SC_DICT8, SC_DICT16, SC_DICT32, SC_VALUE, SC_FOR8, SC_FOR16, SC_FOR32, SC_RLE, SC_COUNT };
+
+int width_class(int32_t w, int base) { return w == 1 ? base : w == 2 ? base + 1 : w == 4 ? base + 2 : -1; }
 
 int scan_class(const hy_scan_chunk& c) {
-  if (c.column.kind == HY_COL_VALUE) return SC_VALUE;
-  switch (c.column.vid_width) {
-    case 1:
-      return SC_DICT8;
-    case 2:
-      return SC_DICT16;
-    case 4:
-      return SC_DICT32;
+  switch (c.column.kind) {
+    case HY_COL_VALUE:
+      return SC_VALUE;
+    case HY_COL_DICT:
+      return width_class(c.column.vid_width, SC_DICT8);
+    case HY_COL_FOR:
+      return width_class(c.column.vid_width, SC_FOR8);
+    case HY_COL_RLE:
+      return SC_RLE;
   }
   return -1;
 }
@@ -216,10 +220,13 @@ uint64_t scan_tiles(uint32_t size) { return (uint64_t(size) + hyk::SCAN_TILE - 1
 int class_seg(int cls, int32_t value_type) {
   switch (cls) {
     case SC_DICT8:
+    case SC_FOR8:
       return hyk::seg_tiles<uint8_t>();
     case SC_DICT16:
+    case SC_FOR16:
       return hyk::seg_tiles<uint16_t>();
     case SC_DICT32:
+    case SC_FOR32:
       return hyk::seg_tiles<uint32_t>();
     default:
       return (value_type == HY_TYPE_INT64 || value_type == HY_TYPE_DOUBLE) ? hyk::seg_tiles<int64_t>()
@@ -227,16 +234,86 @@ int class_seg(int cls, int32_t value_type) {
   }
 }
 
-template <typename E, bool DICT, bool OUT_ROWID>
+template <typename E, int MODE, bool OUT_ROWID, typename V = E>
 hy_status launch_scan(const hyk::ScanLaunchDesc& d, const void* constant, void* out, uint32_t* counts,
                       hipStream_t s) {
-  hyk::ScanConst<E> c{};
-  if (!DICT && constant) std::memcpy(&c.value, constant, sizeof(E));
-  KTimer t(DICT ? "scan_dict" : "scan_value", s, d.n_rows);
-  hipLaunchKernelGGL((hyk::scan_kernel<E, DICT, OUT_ROWID>), dim3(static_cast<uint32_t>(d.n_tiles)),
+  hyk::ScanConst<V> c{};
+  if (MODE != hyk::MODE_DICT && constant) std::memcpy(&c.value, constant, sizeof(V));
+  KTimer t(MODE == hyk::MODE_DICT ? "scan_dict" : MODE == hyk::MODE_FOR ? "scan_frame_of_reference" : "scan_value", s,
+           d.n_rows);
+  hipLaunchKernelGGL((hyk::scan_kernel<E, MODE, OUT_ROWID, V>), dim3(static_cast<uint32_t>(d.n_tiles)),
                      dim3(hyk::SCAN_THREADS), 0, s, d, c, out, counts);
   t.done();
   HY_HIP(hipGetLastError());
+  return HY_OK;
+}
+
+template <typename E, bool OUT_ROWID>
+hy_status launch_for(const hyk::ScanLaunchDesc& d, int32_t value_type, const void* constant, void* out,
+                     uint32_t* counts, hipStream_t s) {
+  if (value_type == HY_TYPE_INT32)
+    return launch_scan<E, hyk::MODE_FOR, OUT_ROWID, int32_t>(d, constant, out, counts, s);
+  return launch_scan<E, hyk::MODE_FOR, OUT_ROWID, int64_t>(d, constant, out, counts, s);
+}
+
+// RunLength chunks of one call (hyk::rle_* kernels): per-run predicate, prefix over the matching runs' lengths, then
+// the row ranges expanded into each chunk's output. Run-level temporaries come from the stream-ordered pool (their
+// size follows the run count, which the workspace query does not see).
+template <bool OUT_ROWID>
+hy_status rle_scan(const hyk::RleDesc& d, const uint32_t* chunk_index, const uint32_t* chunk_ids,
+                   int32_t value_type, const void* constant, void* out, uint32_t* counts, uint64_t rows,
+                   hipStream_t s) {
+  const uint64_t n = d.n_runs;
+  uint32_t* match_len = nullptr;
+  uint64_t* prefix = nullptr;
+  void* temp = nullptr;
+  size_t temp_bytes = 0;
+  HY_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, temp_bytes, static_cast<const uint32_t*>(nullptr),
+                                          static_cast<uint64_t*>(nullptr), static_cast<int>(n + 1), s));
+  HY_HIP(hipMallocAsync(reinterpret_cast<void**>(&match_len), 4 * (n + 1), s));
+  HY_HIP(hipMallocAsync(reinterpret_cast<void**>(&prefix), 8 * (n + 1), s));
+  HY_HIP(hipMallocAsync(&temp, temp_bytes + 16, s));
+  hyk::RleDesc dd = d;
+  auto match = [&](auto tag) {
+    using T = decltype(tag);
+    hyk::ScanConst<T> c{};
+    if (constant) std::memcpy(&c.value, constant, sizeof(T));
+    hipLaunchKernelGGL((hyk::rle_match_kernel<T>), dim3(grid_for(n + 1, hyk::SCAN_THREADS)), dim3(hyk::SCAN_THREADS),
+                       0, s, dd, c, match_len);
+  };
+  {
+    KTimer kt("scan_run_length", s, rows);
+    switch (value_type) {
+      case HY_TYPE_INT32:
+        match(int32_t{});
+        break;
+      case HY_TYPE_INT64:
+        match(int64_t{});
+        break;
+      case HY_TYPE_FLOAT:
+        match(float{});
+        break;
+      default:
+        match(double{});
+        break;
+    }
+    HY_HIP(hipGetLastError());
+    HY_HIP(hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, match_len, prefix, static_cast<int>(n + 1), s));
+    hipLaunchKernelGGL(hyk::rle_counts_kernel, dim3((d.n_chunks + 255) / 256), dim3(256), 0, s, dd, prefix, chunk_index,
+                       counts);
+    HY_HIP(hipGetLastError());
+    uint64_t total = 0;
+    HY_HIP(hipMemcpyAsync(&total, prefix + n, 8, hipMemcpyDeviceToHost, s));
+    HY_HIP(hipStreamSynchronize(s));
+    if (total)
+      hipLaunchKernelGGL((hyk::rle_expand_kernel<OUT_ROWID>), dim3(grid_for(total, hyk::SCAN_THREADS)),
+                         dim3(hyk::SCAN_THREADS), 0, s, dd, prefix, total, chunk_ids, out);
+    kt.done();
+  }
+  HY_HIP(hipGetLastError());
+  HY_HIP(hipFreeAsync(match_len, s));
+  HY_HIP(hipFreeAsync(prefix, s));
+  HY_HIP(hipFreeAsync(temp, s));
   return HY_OK;
 }
 
@@ -279,7 +356,14 @@ hy_status table_scan_impl(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_
   std::vector<std::vector<uint32_t>> by_class(SC_COUNT);
   for (uint32_t i = 0; i < n_chunks; ++i) {
     const int cls = scan_class(chunks[i]);
-    if (cls < 0) return fail(HY_ERR_INVALID_ARGUMENT, "bad vid width");
+    if (cls < 0) return fail(HY_ERR_INVALID_ARGUMENT, "bad chunk kind / vid width");
+    if ((cls == SC_RLE || cls >= SC_FOR8) && chunks[i].column.size && !chunks[i].column.dictionary)
+      return fail(HY_ERR_INVALID_ARGUMENT, "compressed chunk without its minima / end positions");
+    if (cls == SC_RLE && chunks[i].column.size &&
+        (chunks[i].column.dictionary_size == 0 || chunks[i].column.dictionary_size > chunks[i].column.size))
+      return fail(HY_ERR_INVALID_ARGUMENT, "run count");
+    if (cls >= SC_FOR8 && cls <= SC_FOR32 && value_type != HY_TYPE_INT32 && value_type != HY_TYPE_INT64)
+      return fail(HY_ERR_UNSUPPORTED, "FrameOfReference chunks hold int32 / int64");
     if (chunks[i].op < HY_OP_EQ || chunks[i].op > HY_OP_VID_SET) return fail(HY_ERR_INVALID_ARGUMENT, "scan op");
     if (chunks[i].op == HY_OP_VID_SET && (chunks[i].column.kind != HY_COL_DICT || !chunks[i].vid_set))
       return fail(HY_ERR_INVALID_ARGUMENT, "HY_OP_VID_SET needs a dictionary chunk and a vid_set");
@@ -289,7 +373,7 @@ hy_status table_scan_impl(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_
       return fail(HY_ERR_ALIGNMENT, "null vector not 16-byte aligned");
     by_class[cls].push_back(i);
   }
-  if (!by_class[SC_VALUE].empty() &&
+  if ((!by_class[SC_VALUE].empty() || !by_class[SC_RLE].empty()) &&
       !(value_type == HY_TYPE_INT32 || value_type == HY_TYPE_INT64 || value_type == HY_TYPE_FLOAT ||
         value_type == HY_TYPE_DOUBLE))
     return fail(HY_ERR_UNSUPPORTED, "value scan type");
@@ -315,7 +399,10 @@ hy_status table_scan_impl(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_
       rows += hc[k].column.size;
       ht[k] = run;
       const uint64_t seg = static_cast<uint64_t>(class_seg(cls, value_type));
-      run += hc[k].op == HY_OP_NONE ? 0 : (scan_tiles(hc[k].column.size) + seg - 1) / seg;  // segments
+      if (cls == SC_RLE)  // runs, not tiles
+        run += hc[k].column.size ? hc[k].column.dictionary_size : 0;
+      else
+        run += hc[k].op == HY_OP_NONE ? 0 : (scan_tiles(hc[k].column.size) + seg - 1) / seg;  // segments
     }
     ht[nc] = run;
     hyk::ScanLaunchDesc d{};
@@ -323,8 +410,9 @@ hy_status table_scan_impl(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_
     auto* dti = cv.take<uint64_t>(nc + 1);
     auto* dix = cv.take<uint32_t>(nc);
     auto* dcid = cv.take<uint32_t>(nc);
-    auto* dst = cv.take<uint64_t>(run + 1);
-    auto* downer = cv.take<uint32_t>(run + 1);
+    const uint64_t words = cls == SC_RLE ? 0 : run;  // RLE: run-level arrays come from rle_scan's own pool
+    auto* dst = cv.take<uint64_t>(words + 1);
+    auto* downer = cv.take<uint32_t>(words + 1);
     auto* dmisc = cv.take<uint32_t>(64);
     if (!cv.ok) return fail(HY_ERR_WORKSPACE, "scan workspace too small");
     if (!error) {
@@ -338,9 +426,20 @@ hy_status table_scan_impl(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_
     hcid.resize(nc);
     for (uint32_t k = 0; k < nc; ++k) hcid[k] = chunk_ids ? chunk_ids[idx[k]] : idx[k];
     HY_STAGE(dcid, hcid.data(), sizeof(uint32_t) * nc, s);
-    HY_HIP(hipMemsetAsync(dst, 0, sizeof(uint64_t) * (run + 1), s));
+    HY_HIP(hipMemsetAsync(dst, 0, sizeof(uint64_t) * (words + 1), s));
     HY_HIP(hipMemsetAsync(dmisc, 0, 4, s));
     if (run == 0) continue;
+    if (cls == SC_RLE) {
+      uint32_t* run_chunk = nullptr;
+      HY_HIP(hipMallocAsync(reinterpret_cast<void**>(&run_chunk), 4 * (run + 1), s));
+      hipLaunchKernelGGL(hyk::fill_tile_owner, dim3((nc + 255) / 256), dim3(256), 0, s, dti, nc, run_chunk);
+      HY_HIP(hipGetLastError());
+      const hyk::RleDesc rd{dch, dti, run_chunk, run, nc};
+      const hy_status st = rle_scan<OUT_ROWID>(rd, dix, dcid, value_type, constant, out_offsets, counts, rows, s);
+      HY_HIP(hipFreeAsync(run_chunk, s));
+      if (st != HY_OK) return st;
+      continue;
+    }
     hipLaunchKernelGGL(hyk::fill_tile_owner, dim3((nc + 255) / 256), dim3(256), 0, s, dti, nc, downer);
     HY_HIP(hipGetLastError());
     d.tile_chunk = downer;
@@ -355,29 +454,39 @@ hy_status table_scan_impl(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_
     d.ticket = dmisc;
     d.error = error;
     hy_status st = HY_OK;
+    constexpr int DICT = hyk::MODE_DICT, VALUE = hyk::MODE_VALUE;
     switch (cls) {
       case SC_DICT8:
-        st = launch_scan<uint8_t, true, OUT_ROWID>(d, nullptr, out_offsets, counts, s);
+        st = launch_scan<uint8_t, DICT, OUT_ROWID>(d, nullptr, out_offsets, counts, s);
         break;
       case SC_DICT16:
-        st = launch_scan<uint16_t, true, OUT_ROWID>(d, nullptr, out_offsets, counts, s);
+        st = launch_scan<uint16_t, DICT, OUT_ROWID>(d, nullptr, out_offsets, counts, s);
         break;
       case SC_DICT32:
-        st = launch_scan<uint32_t, true, OUT_ROWID>(d, nullptr, out_offsets, counts, s);
+        st = launch_scan<uint32_t, DICT, OUT_ROWID>(d, nullptr, out_offsets, counts, s);
+        break;
+      case SC_FOR8:
+        st = launch_for<uint8_t, OUT_ROWID>(d, value_type, constant, out_offsets, counts, s);
+        break;
+      case SC_FOR16:
+        st = launch_for<uint16_t, OUT_ROWID>(d, value_type, constant, out_offsets, counts, s);
+        break;
+      case SC_FOR32:
+        st = launch_for<uint32_t, OUT_ROWID>(d, value_type, constant, out_offsets, counts, s);
         break;
       case SC_VALUE:
         switch (value_type) {
           case HY_TYPE_INT32:
-            st = launch_scan<int32_t, false, OUT_ROWID>(d, constant, out_offsets, counts, s);
+            st = launch_scan<int32_t, VALUE, OUT_ROWID>(d, constant, out_offsets, counts, s);
             break;
           case HY_TYPE_INT64:
-            st = launch_scan<int64_t, false, OUT_ROWID>(d, constant, out_offsets, counts, s);
+            st = launch_scan<int64_t, VALUE, OUT_ROWID>(d, constant, out_offsets, counts, s);
             break;
           case HY_TYPE_FLOAT:
-            st = launch_scan<float, false, OUT_ROWID>(d, constant, out_offsets, counts, s);
+            st = launch_scan<float, VALUE, OUT_ROWID>(d, constant, out_offsets, counts, s);
             break;
           case HY_TYPE_DOUBLE:
-            st = launch_scan<double, false, OUT_ROWID>(d, constant, out_offsets, counts, s);
+            st = launch_scan<double, VALUE, OUT_ROWID>(d, constant, out_offsets, counts, s);
             break;
         }
         break;
@@ -430,11 +539,16 @@ hy_status hy_reference_scan(const hy_row_id* pos_list, uint64_t pos_list_size, c
   HY_HIP(hipMemsetAsync(count, 0, 8, s));
   if (pos_list_size == 0) return HY_OK;
   if (n_referenced_chunks > (1u << 20)) return fail(HY_ERR_UNSUPPORTED, "too many referenced chunks");
-  for (uint32_t i = 0; i < n_referenced_chunks; ++i)
-    if (referenced_chunks[i].op < HY_OP_EQ || referenced_chunks[i].op > HY_OP_VID_SET ||
-        (referenced_chunks[i].op == HY_OP_VID_SET &&
-         (referenced_chunks[i].column.kind != HY_COL_DICT || !referenced_chunks[i].vid_set)))
+  for (uint32_t i = 0; i < n_referenced_chunks; ++i) {
+    const hy_scan_chunk& rc = referenced_chunks[i];
+    if (rc.op < HY_OP_EQ || rc.op > HY_OP_VID_SET ||
+        (rc.op == HY_OP_VID_SET && (rc.column.kind != HY_COL_DICT || !rc.vid_set)))
       return fail(HY_ERR_INVALID_ARGUMENT, "scan op");
+    if (rc.column.kind == HY_COL_STRING) return fail(HY_ERR_UNSUPPORTED, "string chunks: hy_string_reference_scan");
+    if ((rc.column.kind == HY_COL_RLE || rc.column.kind == HY_COL_FOR) && rc.column.size &&
+        (!rc.column.dictionary || (rc.column.kind == HY_COL_RLE && rc.column.dictionary_size == 0)))
+      return fail(HY_ERR_INVALID_ARGUMENT, "compressed chunk without its minima / end positions");
+  }
   const uint64_t tiles = (pos_list_size + hyk::SCAN_TILE - 1) / hyk::SCAN_TILE;
   Carver cv{static_cast<char*>(workspace), workspace_bytes};
   auto* dst = cv.take<uint64_t>(tiles + 1);

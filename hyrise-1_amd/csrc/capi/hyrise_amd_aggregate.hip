@@ -441,6 +441,8 @@ hy_status make_plan(const hy_agg_input* in, const hy_agg_params* p, AggPlan* pla
   for (uint32_t j = 0; j < in->n_columns; ++j) {
     const auto& c = in->columns[j];
     if (c.value_type < HY_TYPE_INT32 || c.value_type > HY_TYPE_DOUBLE) return fail(HY_ERR_UNSUPPORTED, "column type");
+    for (uint32_t k = 0; !c.n_nodes && c.chunks && k < c.n_chunks; ++k)
+      if (!row_readable(c.chunks[k])) return fail(HY_ERR_UNSUPPORTED, "aggregate input chunk kind");
     if (c.n_nodes) {  // expression column: evaluated in the kernel (fused) or materialised first
       hyk::ExprProgram prog;
       const hy_status st = validate_program(in, c.program, c.n_nodes, &prog);
@@ -649,6 +651,7 @@ hy_status check_filter(const hy_agg_input* in, const AggPlan& plan) {
     if (f.op < HY_OP_EQ || f.op > HY_OP_IS_NOT_NULL || f.op == HY_OP_IS_NULL)
       return fail(HY_ERR_UNSUPPORTED, "fused scan filter op");
     if (f.op == HY_OP_NONE || f.column.size == 0) continue;
+    if (!row_readable(f.column)) return fail(HY_ERR_UNSUPPORTED, "fused scan filter chunk kind");
     if (!f.column.data) return fail(HY_ERR_INVALID_ARGUMENT, "filter chunk without data");
     if (f.column.kind == HY_COL_DICT) {
       if (f.column.vid_width != 1 && f.column.vid_width != 2 && f.column.vid_width != 4)
@@ -914,6 +917,8 @@ hy_status check_proj_input(const hy_agg_input* in) {
     if (c.pos_group >= static_cast<int32_t>(in->n_pos_groups)) return fail(HY_ERR_INVALID_ARGUMENT, "pos_group");
     if (c.pos_group < 0 && c.n_chunks != in->n_chunks)
       return fail(HY_ERR_INVALID_ARGUMENT, "data column must have one chunk per input chunk");
+    for (uint32_t k = 0; c.chunks && k < c.n_chunks; ++k)
+      if (!row_readable(c.chunks[k])) return fail(HY_ERR_UNSUPPORTED, "projection input chunk kind");
   }
   return HY_OK;
 }

@@ -131,9 +131,18 @@ hy_status check_sides(const hy_join_side* l, const hy_join_side* r, Geometry* g)
   if (ls != rs) return fail(HY_ERR_INVALID_ARGUMENT, "string column compared with a numeric column");
   if (!ls && (!type_size(l->value_type) || !type_size(r->value_type)))
     return fail(HY_ERR_UNSUPPORTED, "column comparison value type");
+  auto kind_ok = [&](const hy_column_chunk& x) {
+    return x.size == 0 || x.kind == HY_COL_DICT || x.kind == (ls ? HY_COL_STRING : HY_COL_VALUE);
+  };
+  for (uint32_t i = 0; i < l->n_referenced; ++i)
+    if (!kind_ok(l->referenced[i])) return fail(HY_ERR_UNSUPPORTED, "column comparison chunk kind");
+  for (uint32_t i = 0; i < r->n_referenced; ++i)
+    if (!kind_ok(r->referenced[i])) return fail(HY_ERR_UNSUPPORTED, "column comparison chunk kind");
   for (uint32_t c = 0; c < l->n_chunks; ++c) {
     const hy_join_chunk& a = l->chunks[c];
     const hy_join_chunk& b = r->chunks[c];
+    if ((!a.pos_list && !kind_ok(a.column)) || (!b.pos_list && !kind_ok(b.column)))
+      return fail(HY_ERR_UNSUPPORTED, "column comparison chunk kind");
     if (a.size != b.size) return fail(HY_ERR_INVALID_ARGUMENT, "chunk sizes differ between the columns");
     if ((a.pos_list == nullptr) != (b.pos_list == nullptr))
       return fail(HY_ERR_INVALID_ARGUMENT, "Invalid column combination detected!");  // data vs reference column

@@ -147,6 +147,8 @@ inline hy_status plan_side(const hy_join_side* side, SidePlan& p) {
   for (uint32_t i = 0; i < side->n_chunks; ++i) {
     const hy_join_chunk& c = side->chunks[i];
     if (c.pos_list) is_ref = true;
+    if (!c.pos_list && !row_readable(c.column))
+      return fail(HY_ERR_UNSUPPORTED, "join chunk kind (RunLength / FrameOfReference: join the value mirror)");
     p.chunks[i] = src_from(c.column, c.pos_list, c.size, rows, c.single_chunk);
     p.chunks[i].chunk_id = c.chunk_id;
     p.row_begin[i] = rows;
@@ -161,6 +163,8 @@ inline hy_status plan_side(const hy_join_side* side, SidePlan& p) {
     p.ref_row_begin.resize(side->n_referenced + 1);
     uint64_t rr = 0;
     for (uint32_t i = 0; i < side->n_referenced; ++i) {
+      if (!row_readable(side->referenced[i]))
+        return fail(HY_ERR_UNSUPPORTED, "referenced chunk kind (RunLength / FrameOfReference: join the value mirror)");
       p.referenced[i] = src_from(side->referenced[i], nullptr, side->referenced[i].size, rr);
       p.ref_row_begin[i] = rr;
       rr += side->referenced[i].size;
@@ -192,6 +196,7 @@ inline hy_status plan_filter(const hy_join_filter* f, SidePlan& p, int32_t colum
     const hy_scan_chunk& sc = p.filter[i];
     if (sc.op < HY_OP_EQ || sc.op > HY_OP_IS_NOT_NULL || sc.op == HY_OP_IS_NULL)
       return fail(HY_ERR_UNSUPPORTED, "fused scan filter op");
+    if (!row_readable(sc.column)) return fail(HY_ERR_UNSUPPORTED, "fused scan filter chunk kind");
     if (sc.column.size != p.chunks[i].size) return fail(HY_ERR_INVALID_ARGUMENT, "filter chunk size != join chunk size");
     if (sc.column.size && !aligned16(sc.column.data)) return fail(HY_ERR_ALIGNMENT, "filter data not 16-byte aligned");
     if (sc.column.kind == HY_COL_DICT) {

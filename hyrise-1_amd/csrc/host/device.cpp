@@ -118,7 +118,10 @@ std::shared_ptr<DeviceBuffer> upload_strings(const std::vector<std::string>& v, 
   return buf;
 }
 
-std::shared_ptr<DeviceColumn> device_column(const BaseColumn& column) {
+namespace {
+// The column's device residency (created on first use); RunLength / FrameOfReference chunks hold only their compressed
+// arrays until device_column() decodes their value mirror.
+std::shared_ptr<DeviceColumn> resident(const BaseColumn& column) {
   return column.device_mirror_or_create([&]() {
     hy_stream_t s = operator_stream();
     auto d = std::make_shared<DeviceColumn>();
@@ -152,50 +155,43 @@ std::shared_ptr<DeviceColumn> device_column(const BaseColumn& column) {
       });
     } else if (column.encoding_type() == EncodingType::RunLength ||
                column.encoding_type() == EncodingType::FrameOfReference) {
-      // encoded chunk: upload the compressed arrays, expand them into a value mirror on the device
+      // encoded chunk: its compressed arrays go to HBM as they are (the TableScans' HY_COL_RLE / HY_COL_FOR form);
+      // the value mirror is decoded from them on the first row-wise use (decode_mirror)
       Assert(column.data_type() != DataType::String,
              "hyrise-amd: encoded string columns other than Dictionary are not resident on the device");
       resolve_data_type(column.data_type(), [&](auto tag) {
         using T = decltype(tag);
         if constexpr (!std::is_same_v<T, std::string>) {
-          const uint32_t n = static_cast<uint32_t>(column.size());
-          d->data = std::make_shared<DeviceBuffer>(std::max<size_t>(n, 1) * sizeof(T) + 16);
+          hy_column_chunk& c = d->compressed;
+          c.size = static_cast<uint32_t>(column.size());
           if (const auto* rl = dynamic_cast<const RunLengthColumn<T>*>(&column)) {
-            const auto dv = upload(rl->values().data(), rl->values().size() * sizeof(T), s);
-            const auto de = upload(rl->end_positions().data(), rl->end_positions().size() * 4, s);
-            const bool any_null =
-                std::find(rl->null_values().begin(), rl->null_values().end(), uint8_t{1}) != rl->null_values().end();
-            std::shared_ptr<DeviceBuffer> dn;
-            if (any_null) {
-              dn = upload(rl->null_values().data(), rl->null_values().size(), s);
-              d->nulls = std::make_shared<DeviceBuffer>(std::max<size_t>(n, 1) + 16);
-            }
-            hy_check(hy_decode_run_length(dv->get(), dn ? static_cast<const uint8_t*>(dn->get()) : nullptr,
-                                          static_cast<const uint32_t*>(de->get()),
-                                          static_cast<uint32_t>(rl->end_positions().size()), sizeof(T), n,
-                                          d->data->get(), any_null ? static_cast<uint8_t*>(d->nulls->get()) : nullptr,
-                                          s),
-                     "hy_decode_run_length");
-            hy_check(hy_stream_synchronize(s), "sync");  // the run arrays are released at scope end
+            d->c_data = upload(rl->values().data(), rl->values().size() * sizeof(T), s);
+            d->c_aux = upload(rl->end_positions().data(), rl->end_positions().size() * 4, s);
+            if (std::find(rl->null_values().begin(), rl->null_values().end(), uint8_t{1}) != rl->null_values().end())
+              d->c_nulls = upload(rl->null_values().data(), rl->null_values().size(), s);
+            c.kind = HY_COL_RLE;
+            c.dictionary_size = static_cast<uint32_t>(rl->end_positions().size());
           } else if constexpr (std::is_same_v<T, int32_t> || std::is_same_v<T, int64_t>) {
             const auto* fr = dynamic_cast<const FrameOfReferenceColumn<T>*>(&column);
             Assert(fr != nullptr, "device_column: unknown encoded column");
-            const auto dm = upload(fr->block_minima().data(), fr->block_minima().size() * sizeof(T), s);
             const auto& ov = fr->offset_values();
-            const auto doff = upload(ov.bytes().data(), ov.bytes().size(), s);
-            hy_check(hy_decode_frame_of_reference(dm->get(), hy_type_of(column.data_type()), doff->get(), ov.width(),
-                                                  n, d->data->get(), s),
-                     "hy_decode_frame_of_reference");
+            d->c_data = upload(ov.bytes().data(), ov.bytes().size(), s);
+            d->c_aux = upload(fr->block_minima().data(), fr->block_minima().size() * sizeof(T), s);
             if (std::find(fr->null_values().begin(), fr->null_values().end(), uint8_t{1}) != fr->null_values().end())
-              d->nulls = upload(fr->null_values().data(), fr->null_values().size(), s);
-            hy_check(hy_stream_synchronize(s), "sync");
+              d->c_nulls = upload(fr->null_values().data(), fr->null_values().size(), s);
+            c.kind = HY_COL_FOR;
+            c.vid_width = ov.width();
+            c.dictionary_size = static_cast<uint32_t>(fr->block_minima().size());
           } else {
             Fail("device_column: unknown encoded column");
           }
-          d->desc.data = d->data->get();
-          if (d->nulls) d->desc.nulls = static_cast<const uint8_t*>(d->nulls->get());
+          c.data = d->c_data->get();
+          c.dictionary = d->c_aux->get();
+          c.nulls = d->c_nulls ? d->c_nulls->as<uint8_t>() : nullptr;
         }
       });
+      d->has_compressed = true;
+      d->decoded = false;
       d->desc.kind = HY_COL_VALUE;
     } else {
       Assert(!column.is_reference(), "device_column of a ReferenceColumn");
@@ -217,6 +213,53 @@ std::shared_ptr<DeviceColumn> device_column(const BaseColumn& column) {
     hy_check(hy_stream_synchronize(s), "hy_stream_synchronize");
     return d;
   });
+}
+
+// The value mirror of a RunLength / FrameOfReference chunk, decoded in HBM from its compressed arrays.
+void decode_mirror(DeviceColumn& d, const BaseColumn& column) {
+  hy_stream_t s = operator_stream();
+  const hy_column_chunk& c = d.compressed;
+  const uint32_t n = c.size;
+  resolve_data_type(column.data_type(), [&](auto tag) {
+    using T = decltype(tag);
+    if constexpr (!std::is_same_v<T, std::string>) {
+      d.data = std::make_shared<DeviceBuffer>(std::max<size_t>(n, 1) * sizeof(T) + 16);
+      if (c.kind == HY_COL_RLE) {
+        if (c.nulls) d.nulls = std::make_shared<DeviceBuffer>(std::max<size_t>(n, 1) + 16);
+        if (n)
+          hy_check(hy_decode_run_length(c.data, c.nulls, static_cast<const uint32_t*>(c.dictionary), c.dictionary_size,
+                                        sizeof(T), n, d.data->get(), d.nulls ? d.nulls->as<uint8_t>() : nullptr, s),
+                   "hy_decode_run_length");
+      } else {
+        if (n)
+          hy_check(hy_decode_frame_of_reference(c.dictionary, hy_type_of(column.data_type()), c.data, c.vid_width, n,
+                                                d.data->get(), s),
+                   "hy_decode_frame_of_reference");
+        d.nulls = d.c_nulls;  // the row NULL flags are the same array
+      }
+    }
+  });
+  hy_check(hy_stream_synchronize(s), "hy_stream_synchronize");
+  d.desc.data = d.data->get();
+  d.desc.nulls = d.nulls ? d.nulls->as<uint8_t>() : nullptr;
+}
+}  // namespace
+
+std::shared_ptr<DeviceColumn> device_column(const BaseColumn& column) {
+  auto d = resident(column);
+  if (!d->decoded.load(std::memory_order_acquire)) {
+    std::lock_guard<std::mutex> lock(d->decode_mutex);
+    if (!d->decoded.load(std::memory_order_relaxed)) {
+      decode_mirror(*d, column);
+      d->decoded.store(true, std::memory_order_release);
+    }
+  }
+  return d;
+}
+
+hy_column_chunk device_scan_chunk(const BaseColumn& column) {
+  const auto d = resident(column);
+  return d->has_compressed ? d->compressed : d->desc;
 }
 
 std::shared_ptr<DevicePosList> device_pos_list(const PosList& pos_list) {

@@ -6,7 +6,9 @@
 // like the reference's Fail (src/lib/utils/assert.hpp:49-70).
 #pragma once
 
+#include <atomic>
 #include <deque>
+#include <mutex>
 #include <memory>
 #include <string>
 #include <vector>
@@ -67,10 +69,17 @@ hy_stream_t operator_stream();
 // Is a usable device present? Throws with a clear message if the HIP library reports none.
 void require_device();
 
-// Device mirror of one Value/Dictionary column chunk.
+// Device mirror of one column chunk. desc: what the row-wise kernels read (values / dictionary ids). RunLength and
+// FrameOfReference chunks also keep their compressed arrays in HBM (`compressed`, HY_COL_RLE / HY_COL_FOR), which
+// TableScans read directly; their value mirror (desc) is decoded from those on the first row-wise use only.
 struct DeviceColumn {
   std::shared_ptr<DeviceBuffer> data, nulls, dictionary;
   hy_column_chunk desc{};
+  std::shared_ptr<DeviceBuffer> c_data, c_nulls, c_aux;
+  hy_column_chunk compressed{};
+  bool has_compressed = false;
+  std::atomic<bool> decoded{true};
+  std::mutex decode_mutex;
 };
 
 // Device mirror of a PosList (same 8-byte RowID layout).
@@ -84,6 +93,9 @@ struct DevicePosList {
 // Returns (creating on first use) the device mirror of a data column chunk. String columns are only resident as
 // dictionary attribute vectors (dictionary stays on the host).
 std::shared_ptr<DeviceColumn> device_column(const BaseColumn& column);
+// The descriptor a TableScan reads: the compressed form of RunLength / FrameOfReference chunks (no value mirror is
+// decoded for them), device_column(column)->desc otherwise.
+hy_column_chunk device_scan_chunk(const BaseColumn& column);
 
 // Output objects of an operator that emits many chunks (JoinHash: one per radix partition, 65,536 at SF100): the
 // chunks, their columns, PosLists and the PosLists' device mirrors live in four arenas (deques: elements never move);

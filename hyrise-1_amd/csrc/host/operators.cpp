@@ -307,7 +307,7 @@ hy_scan_chunk scan_descriptor(const BaseColumn& column, DataType type, Predicate
   } else {
     sc.op = value_op(cond);
   }
-  sc.column = device_column(column)->desc;
+  sc.column = device_scan_chunk(column);  // RunLength / FrameOfReference: scanned in compressed form
   return sc;
 }
 

@@ -10,7 +10,16 @@
 // Matches are compacted order-preservingly: per-thread popcount -> workgroup exclusive sum -> decoupled look-back
 // across the tiles of the same chunk -> offsets staged in LDS -> coalesced stores.
 // The roofline is HBM: vid_width bytes read per row + 4 bytes written per match.
+//
+// Compressed chunks are scanned in their compressed form:
+//   FrameOfReference (MODE_FOR): the 1/2/4-byte offsets stream through the same tiles; a thread's 16 rows share one
+//     2048-row block, whose minimum is added back before the compare (frame_of_reference_column.cpp:25-37) -
+//     offset bytes per row instead of the value's 4 / 8.
+//   RunLength: one predicate evaluation per run, then the matching runs' row ranges are expanded straight into the
+//     output (rle_* kernels below) - the rows themselves are never read.
 #include <hip/hip_runtime.h>
+
+#include <type_traits>
 
 #include "common.hpp"
 
@@ -57,10 +66,14 @@ __host__ __device__ constexpr int seg_tiles() {
   return sizeof(E) >= 8 ? 1 : static_cast<int>(8 / sizeof(E));
 }
 
-// Match mask of the 16 rows [row0, row0 + 16) of chunk ch (bit i = row row0 + i matches).
-template <typename E, bool IS_DICT>
+enum { MODE_VALUE = 0, MODE_DICT = 1, MODE_FOR = 2 };
+
+// Match mask of the 16 rows [row0, row0 + 16) of chunk ch (bit i = row row0 + i matches). E: the element read from
+// memory (value / value id / frame-of-reference offset); V: the value type compared (E except for MODE_FOR).
+template <typename E, int MODE, typename V>
 __device__ __forceinline__ uint32_t match_mask(const hy_scan_chunk& ch, uint32_t row0, const E (&v)[16],
-                                               const u32x4& nulls, const ScanConst<E>& constant) {
+                                               const u32x4& nulls, const ScanConst<V>& constant) {
+  constexpr bool IS_DICT = MODE == MODE_DICT;
   const uint32_t n = ch.column.size;
   if (row0 >= n || ch.op == HY_OP_NONE) return 0u;
   uint32_t mask = 0;
@@ -97,19 +110,30 @@ __device__ __forceinline__ uint32_t match_mask(const hy_scan_chunk& ch, uint32_t
       for (int i = 0; i < 16; ++i) mask |= static_cast<uint32_t>(nl[i] != 0) << i;
       return mask & valid;
     }
+    if constexpr (MODE == MODE_FOR) {
+      const V base = static_cast<const V*>(ch.column.dictionary)[row0 >> 11];  // the 16 rows share one block
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const bool m = (nl[i] == 0) && cmp_op<E>(op, v[i], constant.value);
-      mask |= static_cast<uint32_t>(m) << i;
+      for (int i = 0; i < 16; ++i) {
+        const V x = static_cast<V>(base + static_cast<V>(v[i]));
+        const bool m = (nl[i] == 0) && cmp_op<V>(op, x, constant.value);
+        mask |= static_cast<uint32_t>(m) << i;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const bool m = (nl[i] == 0) && cmp_op<E>(op, v[i], constant.value);
+        mask |= static_cast<uint32_t>(m) << i;
+      }
     }
   }
   return mask & valid;
 }
 
-// E = element type read from memory (vid type for DICT, value type for VALUE); IS_DICT selects the semantics.
-// OUT_ROWID: write reference RowIDs {chunk_id, offset} (8 B) instead of chunk offsets (4 B).
-template <typename E, bool IS_DICT, bool OUT_ROWID>
-__global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanLaunchDesc d, ScanConst<E> constant,
+// E = element type read from memory (vid type for DICT, value type for VALUE, offset type for FOR); MODE selects the
+// semantics, V the compared value type. OUT_ROWID: write reference RowIDs {chunk_id, offset} (8 B) instead of chunk
+// offsets (4 B).
+template <typename E, int MODE, bool OUT_ROWID, typename V = E>
+__global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanLaunchDesc d, ScanConst<V> constant,
                                                            void* __restrict__ out_any,
                                                            uint32_t* __restrict__ counts) {
   __shared__ uint32_t s_stage[SCAN_TILE];
@@ -148,12 +172,13 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanLaunchDesc d, Sc
       nl[t] = u32x4{0u, 0u, 0u, 0u};
       if (r0 < n && ch.op != HY_OP_NONE) {
         load16(reinterpret_cast<const E*>(ch.column.data), r0, v[t]);
-        if (!IS_DICT && ch.column.nulls != nullptr) nl[t] = *reinterpret_cast<const u32x4*>(ch.column.nulls + r0);
+        if (MODE != MODE_DICT && ch.column.nulls != nullptr)
+          nl[t] = *reinterpret_cast<const u32x4*>(ch.column.nulls + r0);
       }
     }
 #pragma unroll
     for (int t = 0; t < SEG; ++t)
-      masks[t] = match_mask<E, IS_DICT>(ch, tile_row0 + t * SCAN_TILE + threadIdx.x * SCAN_ROWS_PER_THREAD, v[t],
+      masks[t] = match_mask<E, MODE, V>(ch, tile_row0 + t * SCAN_TILE + threadIdx.x * SCAN_ROWS_PER_THREAD, v[t],
                                         nl[t], constant);
   }
   uint32_t mine = 0;
@@ -238,9 +263,34 @@ __device__ __forceinline__ bool ref_match(const hy_scan_chunk& ch, uint32_t off,
     if (ch.op == HY_OP_VID_SET) return (ch.vid_set[vid >> 5] >> (vid & 31)) & 1u;
     return cmp_op<uint32_t>(ch.op, vid, ch.search_vid);
   }
+  if (ch.column.kind == HY_COL_RLE) {  // the row's run: the first with end_position >= off (run_length_column.cpp:24-36)
+    const uint32_t* ends = static_cast<const uint32_t*>(ch.column.dictionary);
+    uint32_t lo = 0, hi = ch.column.dictionary_size - 1;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (ends[mid] < off)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    const bool run_null = ch.column.nulls != nullptr && ch.column.nulls[lo];
+    if (ch.op == HY_OP_IS_NULL) return run_null;
+    if (run_null) return false;
+    return cmp_op<T>(ch.op, reinterpret_cast<const T*>(ch.column.data)[lo], constant);
+  }
   const bool is_null = ch.column.nulls != nullptr && ch.column.nulls[off];
   if (ch.op == HY_OP_IS_NULL) return is_null;
   if (is_null) return false;
+  if (ch.column.kind == HY_COL_FOR) {
+    const uint32_t o = ch.column.vid_width == 1   ? reinterpret_cast<const uint8_t*>(ch.column.data)[off]
+                       : ch.column.vid_width == 2 ? reinterpret_cast<const uint16_t*>(ch.column.data)[off]
+                                                  : reinterpret_cast<const uint32_t*>(ch.column.data)[off];
+    if constexpr (std::is_integral_v<T>)
+      return cmp_op<T>(ch.op, static_cast<T>(static_cast<const T*>(ch.column.dictionary)[off >> 11] + static_cast<T>(o)),
+                       constant);
+    else
+      return false;  // FrameOfReference holds int32 / int64 only
+  }
   const T v = reinterpret_cast<const T*>(ch.column.data)[off];
   return cmp_op<T>(ch.op, v, constant);
 }
@@ -301,6 +351,86 @@ __global__ __launch_bounds__(SCAN_THREADS) void ref_scan_kernel(RefScanDesc d, S
   __syncthreads();
   uint32_t* out = out_positions + s_prefix;
   for (uint32_t i = threadIdx.x; i < tile_total; i += SCAN_THREADS) out[i] = s_stage[i];
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// RunLength chunks scanned per run. Runs of all RLE chunks of one call are numbered globally (run g of chunk k =
+// run g - run_begin[k] of that chunk); a run matches as a whole (one value, one NULL flag), so the scan's output is
+// the concatenation of the matching runs' row ranges, in order.
+// ------------------------------------------------------------------------------------------------------------
+struct RleDesc {
+  const hy_scan_chunk* chunks;
+  const uint64_t* run_begin;  // n_chunks + 1
+  const uint32_t* run_chunk;  // n_runs
+  uint64_t n_runs;
+  uint32_t n_chunks;
+};
+
+__device__ __forceinline__ uint32_t rle_run_start(const hy_scan_chunk& ch, uint32_t r) {
+  return r == 0 ? 0u : static_cast<const uint32_t*>(ch.column.dictionary)[r - 1] + 1u;
+}
+
+// match_len[g] = rows of run g if it matches, else 0 (match_len[n_runs] = 0 so that an exclusive scan of n_runs + 1
+// entries also yields the total)
+template <typename T>
+__global__ __launch_bounds__(SCAN_THREADS) void rle_match_kernel(RleDesc d, ScanConst<T> constant,
+                                                                uint32_t* __restrict__ match_len) {
+  for (uint64_t g = blockIdx.x * (uint64_t)SCAN_THREADS + threadIdx.x; g <= d.n_runs;
+       g += (uint64_t)gridDim.x * SCAN_THREADS) {
+    if (g == d.n_runs) {
+      match_len[g] = 0;
+      continue;
+    }
+    const uint32_t k = d.run_chunk[g];
+    const hy_scan_chunk& ch = d.chunks[k];
+    const uint32_t r = static_cast<uint32_t>(g - d.run_begin[k]);
+    const uint32_t end = static_cast<const uint32_t*>(ch.column.dictionary)[r];
+    const uint32_t len = end - rle_run_start(ch, r) + 1u;
+    const bool null_run = ch.column.nulls != nullptr && ch.column.nulls[r];
+    bool m;
+    if (ch.op == HY_OP_NONE)
+      m = false;
+    else if (ch.op == HY_OP_IS_NULL)
+      m = null_run;
+    else
+      m = !null_run && cmp_op<T>(ch.op, static_cast<const T*>(ch.column.data)[r], constant.value);
+    match_len[g] = m ? len : 0u;
+  }
+}
+
+__global__ void rle_counts_kernel(RleDesc d, const uint64_t* __restrict__ prefix,
+                                  const uint32_t* __restrict__ chunk_index, uint32_t* __restrict__ counts) {
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < d.n_chunks; k += gridDim.x * blockDim.x)
+    counts[chunk_index[k]] = static_cast<uint32_t>(prefix[d.run_begin[k + 1]] - prefix[d.run_begin[k]]);
+}
+
+// Output j (of `total` matching rows): its run is the last g with prefix[g] <= j (a run with rows left, since empty
+// runs repeat the prefix); coalesced stores, one binary search per output over the L2-resident prefix.
+template <bool OUT_ROWID>
+__global__ __launch_bounds__(SCAN_THREADS) void rle_expand_kernel(RleDesc d, const uint64_t* __restrict__ prefix,
+                                                                 uint64_t total, const uint32_t* __restrict__ chunk_ids,
+                                                                 void* __restrict__ out_any) {
+  for (uint64_t j = blockIdx.x * (uint64_t)SCAN_THREADS + threadIdx.x; j < total;
+       j += (uint64_t)gridDim.x * SCAN_THREADS) {
+    uint64_t lo = 0, hi = d.n_runs;  // prefix[lo] <= j < prefix[hi]
+    while (hi - lo > 1) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (prefix[mid] <= j)
+        lo = mid;
+      else
+        hi = mid;
+    }
+    const uint64_t g = lo;
+    const uint32_t k = d.run_chunk[g];
+    const hy_scan_chunk& ch = d.chunks[k];
+    const uint32_t r = static_cast<uint32_t>(g - d.run_begin[k]);
+    const uint32_t offset = rle_run_start(ch, r) + static_cast<uint32_t>(j - prefix[g]);
+    const uint64_t slot = ch.out_begin + (j - prefix[d.run_begin[k]]);
+    if constexpr (OUT_ROWID)
+      static_cast<hy_row_id*>(out_any)[slot] = hy_row_id{chunk_ids[k], offset};
+    else
+      static_cast<uint32_t*>(out_any)[slot] = offset;
+  }
 }
 
 __global__ void gather_row_ids_kernel(const hy_row_id* __restrict__ pos_list, const uint32_t* __restrict__ positions,

@@ -114,7 +114,18 @@ const char* hy_build_info(void);
  *
  * All device pointers must be 16-byte aligned; buffers must be readable up to the next multiple of 16 bytes.
  * ------------------------------------------------------------------------------------------------------------- */
-enum { HY_COL_VALUE = 0, HY_COL_DICT = 1, HY_COL_STRING = 2 };
+/*
+ *   HY_COL_FOR        FrameOfReferenceColumn<int32/int64> (reference frame_of_reference_column.hpp, compressed form -
+ *                     TableScans only: hy_table_scan / hy_table_scan_row_ids / hy_reference_scan): data = offsets
+ *                     (vid_width 1 / 2 / 4 bytes, FixedSizeByteAligned), nulls = uint8 per row or NULL, dictionary =
+ *                     block minima (value_type, one per 2048 rows); row value = minima[row / 2048] + offset[row]
+ *   HY_COL_RLE        RunLengthColumn<T> (reference run_length_column.hpp, compressed form - TableScans only): data =
+ *                     run values (T[dictionary_size]), nulls = uint8 per run or NULL, dictionary = end_positions
+ *                     (uint32[dictionary_size], the last row of each run, ascending), dictionary_size = runs
+ * The other entry points (joins, aggregates, projections, column compares) read these chunks as HY_COL_VALUE mirrors
+ * (hy_decode_run_length / hy_decode_frame_of_reference) and reject HY_COL_FOR / HY_COL_RLE with HY_ERR_UNSUPPORTED.
+ */
+enum { HY_COL_VALUE = 0, HY_COL_DICT = 1, HY_COL_STRING = 2, HY_COL_FOR = 3, HY_COL_RLE = 4 };
 
 typedef struct hy_column_chunk {
   const void* data;          /* values (VALUE) or attribute vector (DICT) */

@@ -254,3 +254,43 @@ def test_like_synthetic(hy, oracle):
             check(hy, oracle, w, 1, cond, pattern)
     s1 = check(hy, oracle, w, 0, "GreaterThanEquals", 15_000)
     check(hy, oracle, s1, 1, "Like", "%b%")
+
+
+@pytest.mark.parametrize("dtype", ["int", "long", "float"])
+def test_compressed_scans_mixed_chunks(hy, oracle, dtype):
+    """RunLength and FrameOfReference chunks scanned in compressed form (hy_table_scan's HY_COL_RLE / HY_COL_FOR
+    classes) next to dictionary and unencoded chunks of the same column, in one call: clustered values (long runs)
+    and short runs, NULL runs, ragged chunk sizes, every predicate, data and reference inputs."""
+    rng = np.random.default_rng(0x524C45)
+    dt = {"int": hy.DataType.Int, "long": hy.DataType.Long, "float": hy.DataType.Float}[dtype]
+    npt = {"int": np.int32, "long": np.int64, "float": np.float32}[dtype]
+    n, chunk = 120_000, 23_011
+    runs = np.repeat(rng.integers(-50, 50, n // 7 + 1), rng.integers(1, 14, n // 7 + 1))[:n]
+    runs = np.concatenate([runs, rng.integers(-50, 50, n - len(runs))]) if len(runs) < n else runs
+    vals = runs.astype(npt)
+    if dtype == "long":
+        vals = vals * np.int64(1 << 33)
+    nulls = np.repeat((rng.random(n // 20 + 1) < 0.1).astype(np.uint8), 20)[:n]
+    t = hy.Table.from_arrays([("a", dt, True), ("b", hy.DataType.Int, False)], [vals, np.arange(n, dtype=np.int32)],
+                             [nulls, None], chunk)
+    hy.encode_chunks(t, [0, 3], hy.EncodingType.RunLength)
+    if dtype != "float":
+        hy.encode_chunks(t, [1, 4], hy.EncodingType.FrameOfReference)
+    hy.encode_chunks(t, [2], hy.EncodingType.Dictionary)
+    w = wrap(hy, t)
+    for cond in CONDS:
+        for v in (0, -17, 49, 60):
+            c = v * (1 << 33) if dtype == "long" else v
+            check(hy, oracle, w, 0, cond, c)
+    for cond in ("IsNull", "IsNotNull"):
+        check(hy, oracle, w, 0, cond, None)
+    check(hy, oracle, w, 0, "GreaterThan", 3, excluded=[1])
+    s1 = check(hy, oracle, w, 1, "GreaterThanEquals", 30_000)
+    check(hy, oracle, s1, 0, "LessThan", 5)
+    pl = np.stack([rng.integers(0, 6, 40_000), rng.integers(0, 5_000, 40_000)], axis=1).astype(np.uint32)
+    pl[rng.random(40_000) < 0.05] = sc.NULL_ROW_ID
+    ref = hy.Table([("a", dt, True), ("b", hy.DataType.Int, False)], hy.TableType.References)
+    ref.append_chunk([hy.ReferenceColumn(t, 0, pl), hy.ReferenceColumn(t, 1, pl)])
+    for cond, v in (("Equals", 7), ("LessThanEquals", -3), ("IsNull", None), ("NotEquals", 0)):
+        c = v * (1 << 33) if (dtype == "long" and v is not None) else v
+        check(hy, oracle, wrap(hy, ref), 0, cond, c)
