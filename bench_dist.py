@@ -142,14 +142,18 @@ def main_distributed(args):
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
-    L.hy_kernel_stats_reset()
-    L.hy_kernel_stats_enable(1)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         n_probe, pairs = step()
     torch.cuda.synchronize()
     dist.barrier()
     elapsed = time.perf_counter() - t0
+    # per-kernel device times: K more steps with HIP events around every launch (kept out of the timed region)
+    L.hy_kernel_stats_reset()
+    L.hy_kernel_stats_enable(1)
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
     L.hy_kernel_stats_enable(0)
     t = torch.tensor([elapsed], dtype=torch.float64, device=xdev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)

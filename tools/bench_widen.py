@@ -1,6 +1,7 @@
-"""Timing of the round-2 widening rows (IS NULL, column-vs-column, LIKE, Validate, RunLength / FrameOfReference
-decode) through the drop-in operators on SF10-sized synthetic tables (60M rows in 65,536-row chunks; LIKE on 6M
-string rows). Wall time per operator call after warm-up, inputs HBM-resident (device mirrors built in the warm-up);
+"""Timing of the widening rows (IS NULL, column-vs-column, LIKE, Validate, RunLength / FrameOfReference scanned
+compressed, SIMD-BP128 dictionaries, unencoded string columns: comparisons, LIKE on value columns, string column
+compares) through the drop-in operators on SF10-sized synthetic tables (60M rows in 65,536-row chunks; strings on 6M
+rows). Wall time per operator call after warm-up, inputs HBM-resident (device mirrors built in the warm-up);
 per-kernel device time comes from running this under `rocprofv3 --kernel-trace --stats`.
 
     python tools/bench_widen.py [--rows 60000000] [--steps 5]
@@ -70,7 +71,12 @@ def main():
     report("IS NOT NULL (value, int32)", ms, n, m, 5 + 8 * m / n)
     ms, m = timed(lambda: hy.TableScan(w, 0, C.LessThan, hy.ColumnParameter(1)), args.steps)
     report("a < b (column compare, int32 x int32)", ms, n, m, 9 + 8 * m / n)
-    ms, m = timed(lambda: hy.Validate(w, 1, 5), args.steps)
+    def validate():
+        v = hy.Validate(w)
+        v.set_transaction_context(hy.TransactionContext(1, 5))
+        return v
+
+    ms, m = timed(validate, args.steps)
     report("Validate (data input)", ms, n, m, 12 + 8 * m / n)
 
     for enc in ("RunLength", "FrameOfReference"):
@@ -80,13 +86,28 @@ def main():
         we.execute()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        s = hy.TableScan(we, 0, C.LessThan, 24)  # first use: upload + device decode of every chunk
+        s = hy.TableScan(we, 0, C.LessThan, 24)  # first use: upload of the compressed arrays, no decode
         s.execute()
         torch.cuda.synchronize()
-        report(f"{enc}: first scan incl. upload + decode", (time.perf_counter() - t0) * 1e3, n,
+        report(f"{enc}: first scan incl. upload of the compressed arrays", (time.perf_counter() - t0) * 1e3, n,
                s.get_output().row_count(), 4)
+        per_row = 12 / 60 if enc == "RunLength" else 2  # 50 runs per chunk x 12 B; u16 offsets
         ms, m = timed(lambda: hy.TableScan(we, 0, C.LessThan, 24), args.steps)
-        report(f"{enc}: scan a < 24 on the decoded mirror", ms, n, m, 4 + 8 * m / n)
+        report(f"{enc}: scan a < 24 in compressed form", ms, n, m, per_row + 8 * m / n)
+
+    tb = hy.Table.from_arrays([("a", hy.DataType.Int, False)], [a], [None], chunk)
+    hy.encode_all_chunks(tb, hy.EncodingType.Dictionary, hy.VectorCompressionType.SimdBp128)
+    wb = hy.TableWrapper(tb)
+    wb.execute()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    s = hy.TableScan(wb, 0, C.LessThan, 24)  # first use: upload of the packed words + device decode to u8 ids
+    s.execute()
+    torch.cuda.synchronize()
+    report("SIMD-BP128 dictionary: first scan incl. upload + hy_decode_simd_bp128", (time.perf_counter() - t0) * 1e3, n,
+           s.get_output().row_count(), 6 / 8 + 1)
+    ms, m = timed(lambda: hy.TableScan(wb, 0, C.LessThan, 24), args.steps)
+    report("SIMD-BP128 dictionary: scan a < 24 on the id mirror", ms, n, m, 1 + 8 * m / n)
 
     nl_ = args.like_rows
     words = np.array([f"{p} {q}" for p in ("special", "regular", "pending", "express", "final")
@@ -102,6 +123,22 @@ def main():
     report("LIKE '%special%requests%' (dictionary, u8 ids)", ms, nl_, m, 1 + 8 * m / nl_)
     ms, m = timed(lambda: hy.TableScan(ws, 0, C.NotLike, "%final%"), args.steps)
     report("NOT LIKE '%final%' (dictionary, u8 ids)", ms, nl_, m, 1 + 8 * m / nl_)
+
+    # unencoded string columns (packed string arrays in HBM): a row's bytes + its 4-byte offset
+    tu = hy.Table([("s", hy.DataType.String, False), ("t", hy.DataType.String, False)], hy.TableType.Data, chunk)
+    strs2 = words[rng.integers(0, len(words), nl_)]
+    for x, y in zip(strs, strs2):
+        tu.append([x, y])
+    wu = hy.TableWrapper(tu)
+    wu.execute()
+    avg = float(np.mean([len(x) for x in strs])) + 4
+    for name, cond, v in (("= 'pending ideas'", C.Equals, "pending ideas"), ("< 'final'", C.LessThan, "final"),
+                          ("LIKE '%special%requests%'", C.Like, "%special%requests%"),
+                          ("LIKE 'reg_lar%'", C.Like, "reg_lar%"), ("NOT LIKE '%final%'", C.NotLike, "%final%")):
+        ms, m = timed(lambda: hy.TableScan(wu, 0, cond, v), args.steps)
+        report(f"unencoded string {name}", ms, nl_, m, avg + 8 * m / nl_)
+    ms, m = timed(lambda: hy.TableScan(wu, 0, C.LessThan, hy.ColumnParameter(1)), args.steps)
+    report("s < t (string column compare, unencoded)", ms, nl_, m, 2 * avg + 8 * m / nl_)
 
 
 if __name__ == "__main__":
