@@ -64,6 +64,10 @@ def parse():
     p.add_argument("--unfused", action="store_true",
                    help="run TableScan and JoinHash as two C-ABI calls (hy_table_scan_row_ids, hy_join_hash) instead "
                         "of the fused hy_scan_join_hash (A/B of the fusion; single GPU)")
+    p.add_argument("--no-plan", action="store_true",
+                   help="call hy_scan_join_hash every step instead of executing a prepared plan (hy_scan_join_plan_*, "
+                        "which stages the 11,444 chunk / predicate descriptors to HBM once); same kernels, A/B of the "
+                        "per-call host staging")
     p.add_argument("--probe-gb", type=float, default=4.0, help="buffer size of the measured HBM roofline probe")
     p.add_argument("--join-trace", default=None,
                    help="debug: after the timed region run one traced step and write per-partition join phase "
@@ -230,7 +234,32 @@ def main():
     scan_begin = torch.zeros(n_lchunks + 1, dtype=torch.int64, device=dev)
     pfilter = capi.JoinFilter(scan_chunks, capi.HY_TYPE_FLOAT, None, scan_off.data_ptr(), scan_begin.data_ptr())
 
+    def run_fused_plan():
+        # the prepared plan (hy_scan_join_plan_*): the same kernels as hy_scan_join_hash, descriptors staged once
+        if "plan" not in state:
+            plan = ctypes.c_void_p()
+            capi.check(L.hy_scan_join_plan_create(ctypes.byref(build_side), None, ctypes.byref(probe_data_side),
+                                                  ctypes.byref(pfilter), ctypes.byref(params), ctypes.byref(plan)),
+                       "hy_scan_join_plan_create")
+            state["plan"] = plan
+            state["fcap"] = n_li + 64
+            state["fout_b"] = torch.empty(2 * state["fcap"], dtype=torch.int32, device=dev)
+            state["fout_p"] = torch.empty(2 * state["fcap"], dtype=torch.int32, device=dev)
+        res = capi.JoinResult()
+        st = L.hy_scan_join_plan_execute(state["plan"], state["fout_b"].data_ptr(), state["fout_p"].data_ptr(),
+                                         state["fcap"], part_begin.data_ptr(), part_count.data_ptr(), ctypes.byref(res),
+                                         stream)
+        if st == capi.HY_ERR_CAPACITY:
+            state["fcap"] = res.capacity_required + 64
+            state["fout_b"] = torch.empty(2 * state["fcap"], dtype=torch.int32, device=dev)
+            state["fout_p"] = torch.empty(2 * state["fcap"], dtype=torch.int32, device=dev)
+            return run_fused_plan()
+        capi.check(st, "hy_scan_join_plan_execute")
+        return res.total_pairs
+
     def run_fused():
+        if not args.no_plan:
+            return run_fused_plan()
         if "fws" not in state:
             wsb = ctypes.c_size_t(0)
             capi.check(L.hy_scan_join_hash_workspace_size(ctypes.byref(build_side), None, ctypes.byref(probe_data_side),
@@ -444,7 +473,8 @@ def main():
             "data": "synthetic (seeded counter-based TPC-H-shaped columns, resident in HBM)",
             "config": {"workload": f"TableScan(l_quantity<24, dictionary u8) -> JoinHash(orders ⋈ scan, "
                                    f"o_orderkey=l_orderkey, radix_bits={radix_bits})",
-                       "path": "fused hy_scan_join_hash" if fused else "hy_table_scan_row_ids + hy_join_hash",
+                       "path": ("fused hy_scan_join_hash" + ("" if args.no_plan else " (prepared plan)")) if fused
+                       else "hy_table_scan_row_ids + hy_join_hash",
                        "sf_total": args.sf, "lineitem_rows": g_li, "orders_rows": g_ord, "chunk_size": chunk,
                        "scan_matches": g_probe, "join_pairs": g_pairs,
                        "parallelism": "single GPU"},

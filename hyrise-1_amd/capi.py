@@ -245,6 +245,13 @@ _sigs = {
                                                   ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
     "hy_decode_simd_bp128": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int32,
                                              ctypes.c_void_p, ctypes.c_void_p]),
+    "hy_scan_join_plan_create": (ctypes.c_int, [ctypes.POINTER(JoinSide), ctypes.POINTER(JoinFilter),
+                                                 ctypes.POINTER(JoinSide), ctypes.POINTER(JoinFilter),
+                                                 ctypes.POINTER(JoinParams), ctypes.POINTER(ctypes.c_void_p)]),
+    "hy_scan_join_plan_execute": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(JoinResult),
+                                                  ctypes.c_void_p]),
+    "hy_scan_join_plan_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "hy_string_table_scan_workspace_size": (ctypes.c_int, [ctypes.POINTER(ScanChunk), ctypes.c_uint32,
                                                            ctypes.POINTER(StringPredicate),
                                                            ctypes.POINTER(ctypes.c_size_t)]),

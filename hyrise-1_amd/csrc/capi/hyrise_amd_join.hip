@@ -2,6 +2,8 @@
 // per-type translation units (hyrise_amd_join_*.hip, join_host.hpp).
 #include "join_host.hpp"
 
+#include <memory>
+
 using namespace hyc;
 using namespace hyj;
 
@@ -88,6 +90,82 @@ hy_status hy_scan_join_hash(const hy_join_side* build, const hy_join_filter* bui
       return join_f64(bp, pp, build->value_type, probe->value_type, params, out_build, out_probe, out_capacity,
                       partition_begin, partition_counts, result, workspace, workspace_bytes, s);
   }
+}
+
+}  // extern "C"
+
+// A prepared fused TableScan -> JoinHash (include/hyrise_amd.h, "Prepared plans"): the validated side plans, the
+// params and a workspace of its own, so that the descriptors are staged to HBM once.
+struct hy_join_plan_s {
+  SidePlan bp, pp;
+  hy_join_params params{};
+  int32_t build_type = 0, probe_type = 0;
+  void* workspace = nullptr;
+  size_t workspace_bytes = 0;
+};
+
+extern "C" {
+
+hy_status hy_scan_join_plan_create(const hy_join_side* build, const hy_join_filter* build_filter,
+                                   const hy_join_side* probe, const hy_join_filter* probe_filter,
+                                   const hy_join_params* params, hy_join_plan_t* plan) {
+  if (!plan) return fail(HY_ERR_INVALID_ARGUMENT, "plan");
+  *plan = nullptr;
+  auto p = std::make_unique<hy_join_plan_s>();
+  hy_status st = prepare(build, build_filter, probe, probe_filter, params, p->bp, p->pp);
+  if (st != HY_OK) return st;
+  if (params->key_hash && params->hashed_type != HY_TYPE_INT32)
+    return fail(HY_ERR_INVALID_ARGUMENT, "key_hash needs int32 key ids");
+  p->params = *params;
+  p->build_type = build->value_type;
+  p->probe_type = probe->value_type;
+  p->workspace_bytes = join_bytes_any(params->hashed_type, p->bp, p->pp, params->radix_bits);
+  HY_HIP(hipMalloc(&p->workspace, std::max<size_t>(p->workspace_bytes, 256)));
+  *plan = p.release();
+  return HY_OK;
+}
+
+hy_status hy_scan_join_plan_execute(hy_join_plan_t plan, hy_row_id* out_build, hy_row_id* out_probe,
+                                    uint64_t out_capacity, uint64_t* partition_begin, uint32_t* partition_counts,
+                                    hy_join_result* result, hy_stream_t stream) {
+  if (!plan) return fail(HY_ERR_INVALID_ARGUMENT, "plan");
+  if (!partition_begin || !partition_counts) return fail(HY_ERR_INVALID_ARGUMENT, "partition arrays");
+  hipStream_t s = S(stream);
+  struct KeyHashScope {
+    explicit KeyHashScope(const uint32_t* k) { g_key_hash = k; }
+    ~KeyHashScope() { g_key_hash = nullptr; }
+  } key_hash_scope(plan->params.key_hash);
+  const hy_join_params* prm = &plan->params;
+  hy_status st;
+  switch (prm->hashed_type) {
+    case HY_TYPE_INT32:
+      st = join_i32(plan->bp, plan->pp, plan->build_type, plan->probe_type, prm, out_build, out_probe, out_capacity,
+                    partition_begin, partition_counts, result, plan->workspace, plan->workspace_bytes, s);
+      break;
+    case HY_TYPE_INT64:
+      st = join_i64(plan->bp, plan->pp, plan->build_type, plan->probe_type, prm, out_build, out_probe, out_capacity,
+                    partition_begin, partition_counts, result, plan->workspace, plan->workspace_bytes, s);
+      break;
+    case HY_TYPE_FLOAT:
+      st = join_f32(plan->bp, plan->pp, plan->build_type, plan->probe_type, prm, out_build, out_probe, out_capacity,
+                    partition_begin, partition_counts, result, plan->workspace, plan->workspace_bytes, s);
+      break;
+    default:
+      st = join_f64(plan->bp, plan->pp, plan->build_type, plan->probe_type, prm, out_build, out_probe, out_capacity,
+                    partition_begin, partition_counts, result, plan->workspace, plan->workspace_bytes, s);
+      break;
+  }
+  // from now on the plan's workspace holds both sides' descriptors (the single-pass variant carves the workspace
+  // differently and may fall back within a call: it keeps staging every time)
+  if ((st == HY_OK || st == HY_ERR_CAPACITY) && !onepass_enabled()) plan->bp.device_ready = plan->pp.device_ready = true;
+  return st;
+}
+
+hy_status hy_scan_join_plan_destroy(hy_join_plan_t plan) {
+  if (!plan) return HY_OK;
+  if (plan->workspace) HY_HIP(hipFree(plan->workspace));
+  delete plan;
+  return HY_OK;
 }
 
 hy_status hy_join_hash_workspace_size(const hy_join_side* build, const hy_join_side* probe,

@@ -89,6 +89,9 @@ struct SidePlan {
   uint64_t filter_const = 0;
   uint32_t* scan_out = nullptr;
   uint64_t* scan_chunk_begin = nullptr;
+  // a prepared plan (hy_scan_join_plan_*) whose own workspace already holds this side's descriptors from an earlier
+  // execution: the upload is skipped (the carve of the workspace is deterministic for a plan)
+  bool device_ready = false;
 };
 
 inline uint32_t uniform_of(const std::vector<uint64_t>& row_begin) {
@@ -753,6 +756,7 @@ size_t classic_join_bytes(const SidePlan& bp, const SidePlan& pp, uint32_t bits)
 
 template <typename H, typename P>
 hy_status upload_side(const SidePlan& p, const SideBufs<H, P>& b, hipStream_t s) {
+  if (p.device_ready) return HY_OK;
   auto upload = [&](auto* dst, const auto& v) -> hy_status {
     if (!v.empty()) HY_STAGE(dst, v.data(), sizeof(v[0]) * v.size(), s);
     return HY_OK;

@@ -221,3 +221,43 @@ def test_selective_join_bloom_prefilter(hy, oracle, monkeypatch, mode, bloom):
     else:
         parts = run_fused(hy, dt.join_side(capi, ok), None, dt.join_side(capi, lk), None, params, cap)
     check_join(expected, parts, 1, swapped, mode in ("Semi", "Anti"))
+
+
+@pytest.mark.parametrize("mode", ["Inner", "Left"])
+def test_prepared_plan_equals_call(hy, mode):
+    """hy_scan_join_plan_execute (descriptors staged on the first execution only) equals hy_scan_join_hash, on its
+    first and on later executions, with the scan outputs cleared and the output buffers changed in between."""
+    capi, L = hy.capi, hy.capi.lib
+    rng = np.random.default_rng(0x504C4E)
+    okey, ostatus, lkey, lkey_nulls, qty, qty_nulls = orders_lineitem(rng, 30_000, True)
+    lk = dt.DeviceColumn(capi, lkey, lkey_nulls, 8_000, "Unencoded")
+    lq = dt.DeviceColumn(capi, qty, qty_nulls, 8_000, "Dictionary")
+    ok = dt.DeviceColumn(capi, okey, None, 6_000, "Unencoded")
+    lf = Filter(capi, lq, "LessThan", 24.0)
+    params = capi.JoinParams({"Inner": 0, "Left": 1}[mode], capi.HY_TYPE_INT32, L.hy_join_radix_bits(okey.size, 4), 17)
+    o_side, l_side = dt.join_side(capi, ok), dt.join_side(capi, lk)
+    cap = okey.size * 3 + lkey.size + 16
+    want = run_fused(hy, o_side, None, l_side, lf.f, params, cap)
+    want_scan = lf.scan_output()
+    plan = ctypes.c_void_p()
+    capi.check(L.hy_scan_join_plan_create(ctypes.byref(o_side), None, ctypes.byref(l_side), ctypes.byref(lf.f),
+                                          ctypes.byref(params), ctypes.byref(plan)), "hy_scan_join_plan_create")
+    n_parts = 1 << params.radix_bits
+    try:
+        for run in range(3):
+            zeros = np.zeros_like(lf.out.host)  # clear the scan output in place (the plan holds its pointer)
+            capi.check(L.hy_memcpy_htod(lf.out.ptr, zeros.ctypes.data, zeros.nbytes, None), "clear")
+            ob = capi.DeviceArray(np.full(cap * 2, run + 7, np.uint32))
+            op = capi.DeviceArray(np.full(cap * 2, run + 9, np.uint32))
+            pbeg, pcnt = capi.DeviceArray(np.zeros(n_parts, np.uint64)), capi.DeviceArray(np.zeros(n_parts, np.uint32))
+            res = capi.JoinResult()
+            capi.check(L.hy_scan_join_plan_execute(plan, ob.ptr, op.ptr, cap, pbeg.ptr, pcnt.ptr, ctypes.byref(res),
+                                                   None), "hy_scan_join_plan_execute")
+            b, p = ob.fetch().reshape(-1, 2), op.fetch().reshape(-1, 2)
+            got = [(b[x:x + c], p[x:x + c]) for x, c in zip(pbeg.fetch().astype(np.int64), pcnt.fetch().astype(np.int64))]
+            assert len(got) == len(want)
+            for (gb, gp), (wb, wp) in zip(got, want):
+                assert np.array_equal(gb, wb) and np.array_equal(gp, wp), f"execution {run}"
+            assert all(np.array_equal(a, c) for a, c in zip(lf.scan_output(), want_scan)), f"execution {run}: scan"
+    finally:
+        L.hy_scan_join_plan_destroy(plan)
