@@ -7,6 +7,7 @@ rc=$?
 echo "pytest rc=$rc"
 case $rc in 124|134|137|139) exit 1;; esac
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/r3d_bench.json 2> gpurun_out/r3d_bench.err || exit 2
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-plan > gpurun_out/r3d_bench_noplan.json 2> gpurun_out/r3d_bench_noplan.err || exit 9
 HY_PART_SUB_FILTERED=1 timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/r3d_bench_sub1.json 2> gpurun_out/r3d_bench_sub1.err || exit 3
 HY_FILTER_COMPACT=1 timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/r3d_bench_compact.json 2> gpurun_out/r3d_bench_compact.err || exit 4
 timeout -k 10 300 python -u bench.py --workload q1 --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/r3d_q1.json 2> gpurun_out/r3d_q1.err || exit 5
