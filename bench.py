@@ -103,6 +103,9 @@ def main():
     torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
     capi.check(L.hy_set_device(dev.index), "hy_set_device")
+    # a stream of our own as torch's current stream (torch's work, the events and every C-ABI launch share it): the
+    # prepared plan captures its launches into a hipGraph, which the legacy null stream does not allow
+    torch.cuda.set_stream(torch.cuda.Stream())
     stream = torch.cuda.current_stream().cuda_stream
     chunk = args.chunk
 

@@ -116,6 +116,8 @@ _sigs = {
     "hy_last_error_message": (ctypes.c_char_p, []),
     "hy_build_info": (ctypes.c_char_p, []),
     "hy_stream_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
+    "hy_stream_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p)]),
+    "hy_stream_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "hy_malloc": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]),
     "hy_free": (ctypes.c_int, [ctypes.c_void_p]),
     "hy_memcpy_htod": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),

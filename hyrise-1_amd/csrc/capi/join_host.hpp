@@ -23,6 +23,19 @@ namespace hyj {
 
 using namespace hyc;
 
+// Stream capture of a prepared plan's execution (hy_scan_join_plan_execute): while `capturing`, the final join launch
+// leaves its flags / total on the device (no D2H, no synchronisation inside the captured region) and reports where
+// they are; the plan reads them after each replay of the graph.
+struct CaptureState {
+  bool capturing = false;
+  const uint32_t* misc = nullptr;
+  const uint64_t* totals = nullptr;
+};
+inline CaptureState& capture_state() {
+  static thread_local CaptureState c;
+  return c;
+}
+
 // Tiles per span of the pass from column chunks (sub1) and of the record passes (sub2); HY_PART_SUB1 / HY_PART_SUB2
 // override them (tuning). Read once: workspace sizes and launches must agree.
 inline uint32_t sub_from_env(const char* name, uint32_t dflt) {
@@ -710,6 +723,11 @@ hy_status run_join_partitions(const uint32_t* build_begin, const uint32_t* probe
     kt_.done();
   }
   HY_HIP(hipGetLastError());
+  if (capture_state().capturing) {
+    capture_state().misc = c.misc;
+    capture_state().totals = c.totals;
+    return HY_OK;
+  }
   uint32_t flags[4] = {0, 0, 0, 0};
   uint64_t total = 0;
   HY_HIP(hipMemcpyAsync(flags, c.misc, 16, hipMemcpyDeviceToHost, s));

@@ -261,3 +261,43 @@ def test_prepared_plan_equals_call(hy, mode):
             assert all(np.array_equal(a, c) for a, c in zip(lf.scan_output(), want_scan)), f"execution {run}: scan"
     finally:
         L.hy_scan_join_plan_destroy(plan)
+
+
+def test_prepared_plan_graph_replay(hy):
+    """On a stream of its own the plan's third and later executions replay a captured hipGraph: same output as the
+    call; changed output buffers are recaptured; HY_PLAN_GRAPH=0 paths are covered by the test above."""
+    capi, L = hy.capi, hy.capi.lib
+    rng = np.random.default_rng(0x475250)
+    okey, ostatus, lkey, lkey_nulls, qty, qty_nulls = orders_lineitem(rng, 20_000, False)
+    lk = dt.DeviceColumn(capi, lkey, None, 5_000, "Unencoded")
+    lq = dt.DeviceColumn(capi, qty, qty_nulls, 5_000, "Dictionary")
+    ok = dt.DeviceColumn(capi, okey, None, 4_000, "Unencoded")
+    lf = Filter(capi, lq, "LessThan", 30.0)
+    params = capi.JoinParams(0, capi.HY_TYPE_INT32, L.hy_join_radix_bits(okey.size, 4), 17)
+    o_side, l_side = dt.join_side(capi, ok), dt.join_side(capi, lk)
+    cap = okey.size * 3 + lkey.size + 16
+    want = run_fused(hy, o_side, None, l_side, lf.f, params, cap)
+    stream = ctypes.c_void_p()
+    capi.check(L.hy_stream_create(ctypes.byref(stream)), "hy_stream_create")
+    plan = ctypes.c_void_p()
+    capi.check(L.hy_scan_join_plan_create(ctypes.byref(o_side), None, ctypes.byref(l_side), ctypes.byref(lf.f),
+                                          ctypes.byref(params), ctypes.byref(plan)), "plan")
+    n_parts = 1 << params.radix_bits
+    bufs = [tuple(capi.DeviceArray(np.zeros(n, t)) for n, t in ((cap * 2, np.uint32), (cap * 2, np.uint32),
+                                                                 (n_parts, np.uint64), (n_parts, np.uint32)))
+            for _ in range(2)]
+    try:
+        for run in range(6):
+            ob, op, pbeg, pcnt = bufs[0 if run < 4 else 1]
+            res = capi.JoinResult()
+            capi.check(L.hy_scan_join_plan_execute(plan, ob.ptr, op.ptr, cap, pbeg.ptr, pcnt.ptr, ctypes.byref(res),
+                                                   stream), "execute")
+            capi.check(L.hy_stream_synchronize(stream), "sync")
+            b, p = ob.fetch().reshape(-1, 2), op.fetch().reshape(-1, 2)
+            got = [(b[x:x + c], p[x:x + c]) for x, c in zip(pbeg.fetch().astype(np.int64), pcnt.fetch().astype(np.int64))]
+            assert res.total_pairs == sum(len(x) for _, x in want)
+            for (gb, gp), (wb, wp) in zip(got, want):
+                assert np.array_equal(gb, wb) and np.array_equal(gp, wp), f"execution {run}"
+    finally:
+        L.hy_scan_join_plan_destroy(plan)
+        L.hy_stream_destroy(stream)
