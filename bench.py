@@ -663,7 +663,9 @@ def cpu_baseline(hy, synth, sf, chunk, runs=5):
 
     oracle = helpers.load_oracle()
     threads, model = host_cpu()
-    out = {"unit": "rows/s", "kind": "port", "cpu_model": model, "nproc": os.cpu_count()}
+    out = {"unit": "rows/s", "kind": "port", "cpu_model": model, "nproc": os.cpu_count(),
+           "cores_note": "all cores this process may use: the GPU box grants one GPU's share of a larger machine "
+                         "(OMP_NUM_THREADS, 16 per GPU); nproc counts the whole machine"}
     for label, n_threads, sample_sf in (("all_cores", threads, sf), ("one_core", 1, sf / 5)):
         okey, lines = synth.orders_numpy(sample_sf)
         lkey, qty = synth.lineitem_numpy(okey, lines)
