@@ -29,7 +29,9 @@ namespace hyrise {
 class Table;
 struct DeviceColumn;  // device.hpp
 
-class BaseColumn : public std::enable_shared_from_this<BaseColumn> {
+// No enable_shared_from_this: operator outputs hold columns in arenas behind aliasing shared_ptrs (device.hpp), and
+// pybind11 would wrap such an object in a fresh owning pointer (then delete an arena element) for that base.
+class BaseColumn {
  public:
   explicit BaseColumn(DataType data_type) : _data_type(data_type) {}
   virtual ~BaseColumn();
