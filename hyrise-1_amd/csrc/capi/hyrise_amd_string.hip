@@ -202,9 +202,7 @@ hy_status compile_like(const char* pattern, uint32_t len, int32_t regex, LikeNfa
       if (!closed) return fail(HY_ERR_UNSUPPORTED, "unterminated [ in a LIKE pattern (the reference's regex fails)");
       for (const unsigned char c : mem) a->lit[c] |= 1ull << j;
       i = k;
-    } else if (regex && ch == ']') {
-      return fail(HY_ERR_UNSUPPORTED, "] outside a class in a LIKE pattern");
-    } else {
+    } else {  // (a ']' outside a class is a literal byte, as libstdc++'s ECMAScript grammar reads it)
       const int j = position(false);
       if (j < 0) return fail(HY_ERR_UNSUPPORTED, "LIKE pattern longer than 63 positions");
       a->lit[ch] |= 1ull << j;

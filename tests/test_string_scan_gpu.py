@@ -112,7 +112,8 @@ def test_string_synthetic(hy, oracle):
     s1 = check(hy, oracle, w, 0, "GreaterThanEquals", 9_000)
     check(hy, oracle, s1, 1, "Like", "%b%")
     check(hy, oracle, s1, 1, "GreaterThan", "X")
-    pl = np.stack([rng.integers(0, 5, 20_000), rng.integers(0, 2_000, 20_000)], axis=1).astype(np.uint32)
+    # valid RowIDs only: chunk 4 holds 30,000 - 4 * 7,001 = 1,996 rows
+    pl = np.stack([rng.integers(0, 5, 20_000), rng.integers(0, 1_996, 20_000)], axis=1).astype(np.uint32)
     pl[rng.random(20_000) < 0.05] = sc.NULL_ROW_ID
     ref = hy.Table([("a", hy.DataType.Int, False), ("s", hy.DataType.String, True)], hy.TableType.References)
     ref.append_chunk([hy.ReferenceColumn(t, 0, pl), hy.ReferenceColumn(t, 1, pl)])
