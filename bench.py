@@ -386,14 +386,14 @@ def main():
         e2e_bytes = n_li * 1 + n_probe * 8  # u8 value ids read, 8-byte RowIDs written
     elif mode == "join-only":
         e2e_bytes = n_ord * 4 + n_li * 4 + int(pairs) * 16
-    if fused and "part1_mask.probe" in kernels:  # match-bit pass (default)
+    if fused and "part1_mask.probe" in kernels:  # match-bit pass (HY_FILTER_COMPACT=0)
         moved = {
             "part1_mask.probe": n_li * 5 + n_li // 8,  # predicate ids + keys read, one match bit per row written
             "part1_spread.probe": n_li * 4 + n_li // 8 + n_probe * (8 + 4 + 1),  # keys + bits; records, offsets, digit
             "part2_hist.probe": n_probe * 1,
             "part2_scatter.probe": n_probe * 16,
         }
-    elif fused:  # compact -> spread (HY_FILTER_COMPACT=1)
+    elif fused:  # compact -> spread (default)
         moved = {
             "part1_compact.probe": n_li * 5 + n_probe * 8,
             "part1_spread.probe": n_probe * 8 + n_probe * (8 + 4 + 1),

@@ -93,6 +93,7 @@ struct AggPlan {
   hyk::LaneTables lt{};                    // agg_dense_lanes' tables (copied to the workspace)
   std::vector<hyk::LnTerm> lane_terms;     // lp.terms on the host
   std::vector<int32_t> lane_cols;          // input column of each loaded column
+  bool lanes_vec = false;                  // agg_dense_lanes<.., VEC>: data input, 16-byte aligned column chunks
 };
 
 // agg_dense_fused applies: the dense path; at most one PosList group; int32 group-by columns; every aggregate over a
@@ -335,6 +336,19 @@ void plan_lanes(const hy_agg_input* in, const hy_agg_params* p, AggPlan* plan) {
     }
   }
   plan->lanes = true;
+  // the contiguous-rows instance: a data input whose loaded columns' chunks (and a dictionary filter's id arrays) start
+  // 16-byte aligned, so one lane's 4 rows are one aligned vector load; HY_AGG_VEC=0 keeps the strided instance (A/B)
+  const char* ev = std::getenv("HY_AGG_VEC");
+  bool vec = in->n_pos_groups == 0 && !(ev && std::atoi(ev) == 0);
+  auto aligned = [](const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15u) == 0; };
+  for (const int32_t col : plan->lane_cols)
+    for (uint32_t k = 0; k < in->columns[col].n_chunks && vec; ++k)
+      vec = in->columns[col].chunks[k].size == 0 || aligned(in->columns[col].chunks[k].data);
+  if (in->filter)
+    for (uint32_t k = 0; k < in->n_chunks && vec; ++k)
+      vec = in->filter[k].column.kind != HY_COL_DICT || in->filter[k].column.size == 0 ||
+            aligned(in->filter[k].column.data);
+  plan->lanes_vec = vec;
 }
 
 // Record bytes a hash table may take without a caller-given bound (at load 1/2: 2 slots per expected group).
@@ -376,13 +390,13 @@ inline bool agg_prefetch() {
   return v;
 }
 
-template <int N, bool PF>
+template <int N, bool PF, bool VEC>
 void launch_lanes_pf(uint64_t n_tiles, size_t lds, hipStream_t s, const hyk::AggDesc& d, const hyk::LanePlan& lp,
                      unsigned long long* records) {
   static int resident = 0;  // per instantiation; LDS per workgroup is small next to the VGPR limit
   if (resident == 0) {
     int per_cu = 0, dev = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hyk::agg_dense_lanes<N, PF>, hyk::AGG_THREADS, lds) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hyk::agg_dense_lanes<N, PF, VEC>, hyk::AGG_THREADS, lds) !=
             hipSuccess ||
         hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -390,24 +404,26 @@ void launch_lanes_pf(uint64_t n_tiles, size_t lds, hipStream_t s, const hyk::Agg
     resident = std::max(1, per_cu) * std::max(1, cus);
   }
   const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(n_tiles, static_cast<uint64_t>(resident)));
-  hipLaunchKernelGGL((hyk::agg_dense_lanes<N, PF>), dim3(grid), dim3(hyk::AGG_THREADS), lds, s, d, lp, records);
+  hipLaunchKernelGGL((hyk::agg_dense_lanes<N, PF, VEC>), dim3(grid), dim3(hyk::AGG_THREADS), lds, s, d, lp, records);
 }
 
 template <int N>
-void launch_lanes_n(uint64_t n_tiles, size_t lds, hipStream_t s, const hyk::AggDesc& d, const hyk::LanePlan& lp,
-                    unsigned long long* records) {
-  if (agg_prefetch())
-    launch_lanes_pf<N, true>(n_tiles, lds, s, d, lp, records);
+void launch_lanes_n(bool vec, uint64_t n_tiles, size_t lds, hipStream_t s, const hyk::AggDesc& d,
+                    const hyk::LanePlan& lp, unsigned long long* records) {
+  if (vec)
+    launch_lanes_pf<N, false, true>(n_tiles, lds, s, d, lp, records);
+  else if (agg_prefetch())
+    launch_lanes_pf<N, true, false>(n_tiles, lds, s, d, lp, records);
   else
-    launch_lanes_pf<N, false>(n_tiles, lds, s, d, lp, records);
+    launch_lanes_pf<N, false, false>(n_tiles, lds, s, d, lp, records);
 }
 
-void launch_lanes(int n_sums, uint64_t n_tiles, size_t lds, hipStream_t s, const hyk::AggDesc& d,
+void launch_lanes(int n_sums, bool vec, uint64_t n_tiles, size_t lds, hipStream_t s, const hyk::AggDesc& d,
                   const hyk::LanePlan& lp, unsigned long long* records) {
   switch (n_sums) {
-#define HY_LANES_CASE(N)                                    \
-  case N:                                                   \
-    launch_lanes_n<N>(n_tiles, lds, s, d, lp, records);     \
+#define HY_LANES_CASE(N)                                         \
+  case N:                                                        \
+    launch_lanes_n<N>(vec, n_tiles, lds, s, d, lp, records);     \
     break;
     HY_LANES_CASE(0)
     HY_LANES_CASE(1)
@@ -802,7 +818,7 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
                           hyk::ln_wave_lds(lt.n_load - static_cast<int>(params->n_groupby), lt.n_sums);
       {
         KTimer t("agg_dense_lanes", s, plan.rows);
-        launch_lanes(lp.n_sums, plan.n_tiles, vlds, s, d, lp, w.records);
+        launch_lanes(lp.n_sums, plan.lanes_vec, plan.n_tiles, vlds, s, d, lp, w.records);
         t.done();
       }
       HY_HIP(hipGetLastError());

@@ -411,18 +411,21 @@ inline int filter_kind(const SidePlan& p) {
   return width == 2 ? hyk::FK_DICT16 : width == 4 ? hyk::FK_DICT32 : width == 1 ? hyk::FK_DICT8 : hyk::FK_ANY;
 }
 
-// The fused scan's pass 0 through gapped records (part1_compact / part1_spread) instead of match bits: opt-in A/B.
+// The fused scan's pass 0 through gapped records (part1_compact / part1_spread; the default) or through match bits
+// (part1_mask / part1_spread_mask; HY_FILTER_COMPACT=0). Measured on MI355X at SF100 (round 3): compact 1.43 + 1.52 ms,
+// match bits 0.94 + 3.16 ms with two-tile spans (2.08 ms with one-tile spans) - the match-bit spread pass compacts a
+// span into LDS before its scatter, which halves the resident workgroups and serialises load, compaction and scatter.
 inline bool filter_compact_enabled() {
   static const bool v = [] {
     const char* e = std::getenv("HY_FILTER_COMPACT");
-    return e && std::strtol(e, nullptr, 10) != 0;
+    return !(e && std::strtol(e, nullptr, 10) == 0);
   }();
   return v;
 }
 
-// Pass 0 of a side with a fused TableScan: part1_mask (predicate + join column -> histograms with the scan-match row,
-// match bits), the histogram scan, then part1_spread_mask (scan output + compaction in LDS + stable scatter into
-// `out`). HY_FILTER_COMPACT=1: part1_compact (gapped row-order records in recB) + part1_spread instead.
+// Pass 0 of a side with a fused TableScan: part1_compact (gapped row-order records in recB, histograms with the
+// scan-match row), the histogram scan, then part1_spread (scan output + stable scatter into `out`). HY_FILTER_COMPACT=0:
+// part1_mask (match bits) + part1_spread_mask (compaction in LDS) instead.
 template <typename T, typename H, int LP, int FK>
 hy_status launch_filtered_pass0(const char* side_tag, const SidePlan& p, const hyk::Side& sd, const hyk::Digit& d0,
                                 const hyk::NextDigit& nd, uint32_t w0, uint32_t n_digits, SideBufs<H, uint32_t>& b,

@@ -99,29 +99,68 @@ struct AggDesc {
   int32_t filter_type;
 };
 
-// Match mask of the FQ-style rows base + k * WAVE + lane (k < R) of input chunk c under the fused scan predicate
-// (reference SingleColumnTableScanImpl, single_column_table_scan_impl.cpp:38-205); rows past the chunk are 0.
+// Item k < R of a lane in one aggregation step is row first + k * STRIDE of its chunk: STRIDE = WAVE for the FQ-style
+// mapping (first = base + lane), STRIDE = 1 for a lane's R consecutive rows (first = base + lane * R; agg_dense_lanes
+// over a data input reads them with one vector load per column).
 template <int R>
-__device__ __forceinline__ uint32_t agg_filter_mask(const AggDesc& d, uint32_t c, uint32_t base) {
+__device__ __forceinline__ void vec_load_ids(const void* data, uint32_t width, uint32_t first, uint32_t (&v)[R]) {
+  static_assert(R == 4, "one dword / dwordx2 / dwordx4 per lane");
+  if (width == 1) {
+    const uint32_t w = *reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(
+        reinterpret_cast<uintptr_t>(data) + first);
+#pragma unroll
+    for (int k = 0; k < R; ++k) v[k] = (w >> (8 * k)) & 0xFFu;
+  } else if (width == 2) {
+    const uint2 w = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(data) + first);
+    v[0] = w.x & 0xFFFFu;
+    v[1] = w.x >> 16;
+    v[2] = w.y & 0xFFFFu;
+    v[3] = w.y >> 16;
+  } else {
+    const uint4 w = *reinterpret_cast<const uint4*>(static_cast<const uint32_t*>(data) + first);
+    v[0] = w.x;
+    v[1] = w.y;
+    v[2] = w.z;
+    v[3] = w.w;
+  }
+}
+
+// Match mask of a lane's items (see above) of input chunk c under the fused scan predicate (reference
+// SingleColumnTableScanImpl, single_column_table_scan_impl.cpp:38-205); rows past the chunk are 0. With STRIDE 1 a
+// dictionary predicate over the lane's whole run reads its ids with one vector load (the host checked alignment).
+template <int R, int STRIDE = WAVE>
+__device__ __forceinline__ uint32_t agg_filter_mask(const AggDesc& d, uint32_t c, uint32_t first) {
   const hy_scan_chunk f = d.filter[c];
   const uint32_t n = f.column.size;
   if (f.op == HY_OP_NONE || n == 0) return 0u;
-  const uint32_t lane = __lane_id();
   uint32_t m = 0;
   if (f.column.kind == HY_COL_DICT) {
     const uint32_t w = static_cast<uint32_t>(f.column.vid_width);
-#pragma unroll
-    for (int k = 0; k < R; ++k) {
-      const uint32_t i = min(base + k * WAVE + lane, n - 1);
-      const uint32_t vid = w == 1 ? static_cast<const uint8_t*>(f.column.data)[i]
-                           : w == 2 ? static_cast<const uint16_t*>(f.column.data)[i]
-                                    : static_cast<const uint32_t*>(f.column.data)[i];
-      m |= static_cast<uint32_t>(vid != f.column.dictionary_size && cmp_op<uint32_t>(f.op, vid, f.search_vid)) << k;
+    uint32_t vids[R];
+    bool loaded = false;
+    if constexpr (STRIDE == 1 && R == 4) {
+      if (first + R <= n) {
+        vec_load_ids<R>(f.column.data, w, first, vids);
+        loaded = true;
+      }
     }
+    if (!loaded) {
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        const uint32_t i = min(first + k * STRIDE, n - 1);
+        vids[k] = w == 1 ? static_cast<const uint8_t*>(f.column.data)[i]
+                  : w == 2 ? static_cast<const uint16_t*>(f.column.data)[i]
+                           : static_cast<const uint32_t*>(f.column.data)[i];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < R; ++k)
+      m |= static_cast<uint32_t>(vids[k] != f.column.dictionary_size && cmp_op<uint32_t>(f.op, vids[k], f.search_vid))
+           << k;
   } else {
 #pragma unroll
     for (int k = 0; k < R; ++k) {
-      const uint32_t i = min(base + k * WAVE + lane, n - 1);
+      const uint32_t i = min(first + k * STRIDE, n - 1);
       const bool nul = f.column.nulls != nullptr && f.column.nulls[i];
       bool hit = false;
       switch (d.filter_type) {
@@ -154,7 +193,7 @@ __device__ __forceinline__ uint32_t agg_filter_mask(const AggDesc& d, uint32_t c
   }
 #pragma unroll
   for (int k = 0; k < R; ++k)
-    if (base + k * WAVE + lane >= n) m &= ~(1u << k);
+    if (first + k * STRIDE >= n) m &= ~(1u << k);
   return m;
 }
 

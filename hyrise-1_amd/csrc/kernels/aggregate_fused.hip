@@ -193,7 +193,7 @@ __device__ __forceinline__ void fused_step(const AggDesc& d, const FusedPlan& fp
 #pragma unroll
       for (int k = 0; k < FQ_R; ++k)
         if (base + k * WAVE + lane < size) act |= 1u << k;
-      if (d.filter != nullptr && d.n_pos_groups == 0) act &= agg_filter_mask<FQ_R>(d, c, base);  // fused TableScan
+      if (d.filter != nullptr && d.n_pos_groups == 0) act &= agg_filter_mask<FQ_R>(d, c, base + __lane_id());  // fused TableScan
       hy_row_id rid[FQ_R];
       bool uniform = true;
       uint32_t cc = 0;

@@ -256,7 +256,11 @@ __device__ __forceinline__ bool ln_window_ok(const LanePlan& lp, const uint32_t 
 // without it (4 spills, 2 left too little latency hiding); with the prefetch and the LDS dictionaries a step has one
 // dependent global round trip instead of three, so the prefetching instance runs at 2 waves per SIMD (HY_AGG_PREFETCH
 // picks it; tools measure both).
-template <int NS, bool PF>
+// VEC (data input, no PosList): a lane's FQ_R rows of a step are consecutive (base + lane * FQ_R + k) instead of
+// strided by the wave (base + k * WAVE + lane), so every column is read with ONE vector load per lane and step (a
+// dword of four u8 ids, a dwordx2 of u16 ids, a dwordx4 of 4-byte values; the host checked 16-byte alignment) instead
+// of FQ_R single-element loads. A step still covers the same 256 rows, so deferred steps are unchanged.
+template <int NS, bool PF, bool VEC>
 __global__ __launch_bounds__(AGG_THREADS) __attribute__((amdgpu_waves_per_eu(PF ? 2 : 3))) void agg_dense_lanes(
     AggDesc d, LanePlan lp, unsigned long long* __restrict__ records) {
   constexpr int NA = NS > 0 ? NS : 1;
@@ -308,15 +312,18 @@ __global__ __launch_bounds__(AGG_THREADS) __attribute__((amdgpu_waves_per_eu(PF 
       const uint32_t base = span + h * FQ_R * WAVE;
       if (base >= size) break;  // wave-uniform
       const uint32_t step_id = static_cast<uint32_t>(tile) * FQ_STEPS_PER_TILE + w * (AGG_ITEMS / FQ_R) + h;
+      constexpr uint32_t STR = VEC ? 1u : static_cast<uint32_t>(WAVE);  // row step between a lane's items
+      const uint32_t first = VEC ? base + lane * FQ_R : base + lane;
+      const bool full = VEC && first + FQ_R <= size;                      // the lane's items all in the chunk
       uint32_t act = 0;
 #pragma unroll
       for (int k = 0; k < FQ_R; ++k)
-        if (base + k * WAVE + lane < size) act |= 1u << k;
+        if (first + k * STR < size) act |= 1u << k;
       // row offsets inside the (single) chunk the step's rows live in
       uint32_t off[FQ_R];
       uint32_t cc = c;
       const bool prefetch = PF && d.n_pos_groups && h + 1 < AGG_ITEMS / FQ_R && base + FQ_R * WAVE < size;
-      if (d.n_pos_groups) {
+      if (!VEC && d.n_pos_groups) {
         hy_row_id rid[FQ_R];
 #pragma unroll
         for (int k = 0; k < FQ_R; ++k) {
@@ -342,9 +349,9 @@ __global__ __launch_bounds__(AGG_THREADS) __attribute__((amdgpu_waves_per_eu(PF 
           continue;
         }
       } else {
-        if (d.filter != nullptr) act &= agg_filter_mask<FQ_R>(d, c, base);  // fused TableScan
+        if (d.filter != nullptr) act &= agg_filter_mask<FQ_R, STR>(d, c, first);  // fused TableScan
 #pragma unroll
-        for (int k = 0; k < FQ_R; ++k) off[k] = ((act >> k) & 1u) ? base + k * WAVE + lane : 0u;
+        for (int k = 0; k < FQ_R; ++k) off[k] = ((act >> k) & 1u) ? first + k * STR : 0u;
       }
       // the chunk's small dictionaries into the wave's LDS (once per chunk change)
       if (cc != cached_cc) {
@@ -370,8 +377,12 @@ __global__ __launch_bounds__(AGG_THREADS) __attribute__((amdgpu_waves_per_eu(PF 
         const auto& ch = ln_const(T->load_chunks[li])[cc];
         const uint32_t wb = ch.kind == HY_COL_DICT ? static_cast<uint32_t>(ch.vid_width) : 4u;
         const uintptr_t p0 = reinterpret_cast<uintptr_t>(ch.data);
+        if (full) {
+          vec_load_ids<FQ_R>(ch.data, wb, first, raw[li]);
+        } else {
 #pragma unroll
-        for (int k = 0; k < FQ_R; ++k) raw[li][k] = ln_load_elem(p0, off[k], wb);
+          for (int k = 0; k < FQ_R; ++k) raw[li][k] = ln_load_elem(p0, off[k], wb);
+        }
       }
       if (prefetch) {  // the next step's RowIDs, behind this step's column loads
         have_next = true;
@@ -566,6 +577,25 @@ __global__ __launch_bounds__(AGG_THREADS) __attribute__((amdgpu_waves_per_eu(PF 
 #pragma unroll
       for (int j = 0; j < LN_GROUPS; ++j) {
         if (tab[j] < 0) continue;
+        if constexpr (VEC) {  // row of (lane, k) = base + lane * FQ_R + k
+          uint32_t mine = 0;
+#pragma unroll
+          for (int k = 0; k < FQ_R; ++k) mine |= static_cast<uint32_t>(g[k] == static_cast<uint32_t>(tab[j])) << k;
+          const uint64_t anyb = __ballot(mine != 0);
+          if (anyb == 0) continue;
+          const uint64_t rb = row0 + base;
+          const int ll = 63 - __builtin_clzll(anyb);
+          const uint32_t ml = static_cast<uint32_t>(__shfl(static_cast<int>(mine), ll));
+          if (lane == 0)
+            atomicMax(&hdr[j].last, static_cast<unsigned long long>(rb + ll * FQ_R + 31 - __builtin_clz(ml)));
+          if (!((first_set >> j) & 1u)) {
+            const int lf = __builtin_ctzll(anyb);
+            const uint32_t mf = static_cast<uint32_t>(__shfl(static_cast<int>(mine), lf));
+            if (lane == 0) atomicMin(&hdr[j].first, static_cast<unsigned long long>(rb + lf * FQ_R + __builtin_ctz(mf)));
+            first_set |= 1u << j;
+          }
+          continue;
+        }
         uint64_t mk[FQ_R];
 #pragma unroll
         for (int k = 0; k < FQ_R; ++k) mk[k] = __ballot(g[k] == static_cast<uint32_t>(tab[j]));

@@ -268,7 +268,7 @@ def test_compressed_scans_mixed_chunks(hy, oracle, dtype):
     runs = np.repeat(rng.integers(-50, 50, n // 7 + 1), rng.integers(1, 14, n // 7 + 1))[:n]
     runs = np.concatenate([runs, rng.integers(-50, 50, n - len(runs))]) if len(runs) < n else runs
     vals = runs.astype(npt)
-    big = 1 << 40  # long: values past 32 bits (FrameOfReference blocks still span < 2^32, as its encoder requires)
+    big = 3_000_000_000  # long: past int32, yet a FoR block (NULLs count as 0) spans < 2^32, as its encoder asserts
     if dtype == "long":
         vals = vals + np.int64(big)
     nulls = np.repeat((rng.random(n // 20 + 1) < 0.1).astype(np.uint8), 20)[:n]

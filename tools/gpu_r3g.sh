@@ -10,3 +10,5 @@ HY_PART_SUB_FILTERED=1 timeout -k 10 240 python -u bench.py --steps 20 --warmup 
 timeout -k 10 240 python -u bench.py --workload q1 --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/r3g_q1.json 2> gpurun_out/r3g_q1.err || exit 3
 HY_AGG_PREFETCH=1 timeout -k 10 240 python -u bench.py --workload q1 --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/r3g_q1_pf.json 2> gpurun_out/r3g_q1_pf.err || exit 4
 timeout -k 10 240 python -u bench.py --workload q1 --q1-fused --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/r3g_q1_fused.json 2> gpurun_out/r3g_q1_fused.err || exit 5
+bash tools/pmc_lanes.sh q1 > gpurun_out/r3g_pmc_lanes.txt 2>&1 || exit 6
+bash tools/pmc_lanes.sh q1fused --q1-fused > gpurun_out/r3g_pmc_lanes_fused.txt 2>&1 || exit 7
