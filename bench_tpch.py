@@ -139,32 +139,15 @@ def main_q3(args):
         import bench_q3_dist
 
         return bench_q3_dist.main_q3_dist(args)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one GPU (N > 1 returned above: the plan through the JoinHash radix shuffle)
+    world = 1
     sys.path.insert(0, ROOT)
     hy = importlib.import_module("hyrise-1_amd")
     synth = importlib.import_module("hyrise-1_amd.synth")
     capi = hy.capi
     L = capi.lib
-    dist = None
-    if world > 1:
-        # BASELINE.json configs[4] on N GPUs, co-partitioned: orders sharded by contiguous chunk ranges, each order's
-        # lineitem rows on the same rank (lineitem is clustered by l_orderkey, dbgen build.c), the small customer
-        # table scanned by every rank. Both joins and the GROUP BY l_orderkey aggregate are then rank-local: no
-        # exchange, and the ranks' groups are disjoint (their union is the single-GPU result).
-        import torch.distributed as dist
-
-        if args.dist_backend == "nccl":
-            torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            torch.cuda.set_device(local % torch.cuda.device_count())
-            dist.init_process_group("gloo")
-    else:
-        torch.cuda.set_device(0)
+    torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
-    xdev = dev if (dist is None or args.dist_backend == "nccl") else torch.device("cpu")
     capi.check(L.hy_set_device(dev.index), "hy_set_device")
     stream = torch.cuda.current_stream().cuda_stream
     chunk = args.chunk
@@ -190,21 +173,6 @@ def main_q3(args):
     exp["groups"] = int(order_hit.sum())
     del seg_ok, o_date_ok, o_ok, l_date_ok, l_ok, rev
     n_ord_g, n_li_g = n_ord, n_li
-    if world > 1:  # this rank's orders chunks and their lineitem rows
-        n_oc_g = (n_ord + chunk - 1) // chunk
-        o_lo = min(n_ord, (rank * n_oc_g // world) * chunk)
-        o_hi = min(n_ord, ((rank + 1) * n_oc_g // world) * chunk)
-        oi = cols["l_order_index"]
-        l_lo = int(torch.searchsorted(oi, torch.tensor([o_lo], device=dev)).item())
-        l_hi = int(torch.searchsorted(oi, torch.tensor([o_hi], device=dev)).item())
-        for k in ("o_orderkey", "o_custkey", "o_orderdate", "o_shippriority"):
-            cols[k] = cols[k][o_lo:o_hi].contiguous()
-        for k in ("l_orderkey", "l_shipdate", "l_extendedprice", "l_discount"):
-            cols[k] = cols[k][l_lo:l_hi].contiguous()
-        del oi
-        cols.pop("l_order_index")
-        n_ord, n_li = o_hi - o_lo, l_hi - l_lo
-        torch.cuda.empty_cache()
 
     def padded(t):
         return torch.cat([t.contiguous(), torch.zeros(64, dtype=t.dtype, device=t.device)])
@@ -391,15 +359,9 @@ def main_q3(args):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         got = step()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     # per-kernel device times: K more steps with HIP events around every launch (kept out of the timed region)
@@ -412,14 +374,6 @@ def main_q3(args):
     got["orders_matches"] = int(o_begin[-1].item())
     got["lineitem_matches"] = int(l_begin[-1].item())
     local_groups = got["groups"]
-    if dist is not None:  # max time over ranks; counts summed (customer scanned by every rank: once)
-        t = torch.tensor([elapsed], dtype=torch.float64, device=xdev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        keys = ["join1_pairs", "join2_pairs", "groups", "orders_matches", "lineitem_matches"]
-        v = torch.tensor([got[k] for k in keys], dtype=torch.int64, device=xdev)
-        dist.all_reduce(v, op=dist.ReduceOp.SUM)
-        got.update({k: int(x) for k, x in zip(keys, v.tolist())})
 
     # ---------------- check ----------------
     lay = state["layout"]
@@ -439,15 +393,8 @@ def main_q3(args):
         s = ctypes.c_double(0)
         capi.check(L.hy_agg_float_sum(limbs, lay.agg_limbs[0], lay.agg_emin[0], int(r[w + 1]), ctypes.byref(s)))
         ok &= s.value == order_rev_h[oi]
-    if dist is not None:
-        okt = torch.tensor([1 if ok else 0], dtype=torch.int64, device=xdev)
-        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-        ok = bool(okt.item())
     if not ok:
         raise SystemExit(f"q3 result mismatch: {got} vs {exp}")
-    if rank != 0:
-        dist.destroy_process_group()
-        return
 
     from bench import kernel_stats, measured_roofline, host_cpu  # noqa: E402  (shared helpers)
 
@@ -473,19 +420,17 @@ def main_q3(args):
                 "frac": round(e2e / step_s / 1e9 / peak, 4), "alg_bytes_per_step": e2e, "alg_bytes": alg,
                 "traffic": None, "peak_source": "measured in this run (hy_stream_bandwidth_probe, best of read / copy)",
                 "dominant_kernel": dom, "dominant_ms_per_step": round(kernels[dom]["ms_total"] / K, 4)}
-    cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline_q3(hy, synth, args.cpu_sf, chunk, host_cpu)
+    cpu = None if args.no_cpu_baseline else cpu_baseline_q3(hy, synth, args.cpu_sf, chunk, host_cpu)
     line = {
         "metric": "rows/sec TPC-H 3 (Scan -> JoinHash -> JoinHash -> Projection -> Aggregate), 1/2/4/8 MI355X",
         "value": round((n_cust + n_ord + n_li) / step_s, 1), "unit": "rows/s", "n_gpus": world, "steps": K,
         "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 3), "higher_is_better": True,
-        "scaling": "strong" if world > 1 else "weak",
+        "scaling": "weak",
         "vs_baseline": None, "dtype": "int32/f32", "data": "synthetic (seeded counter-based TPC-H-shaped columns, "
                                                            "resident in HBM)",
         "config": {"workload": "TPC-H 3 (tpch_queries.cpp:101-106) without ORDER BY/LIMIT", "sf": args.sf,
                    "customer_rows": n_cust, "orders_rows": n_ord, "lineitem_rows": n_li, "chunk_size": chunk,
-                   **got, "parallelism": "single GPU" if world == 1 else
-                   f"co-partitioned x{world}: orders chunk ranges + their lineitem rows per rank, customer on every "
-                   f"rank; joins and GROUP BY l_orderkey rank-local, no exchange"},
+                   **got, "parallelism": "single GPU"},
         "check": {"ok": bool(ok), "expected": exp, "sampled_groups": len(sample)},
         "roofline": roofline,
         "hbm_probe": probe,
@@ -494,8 +439,6 @@ def main_q3(args):
         "cpu_baseline": cpu,
     }
     print(json.dumps(line))
-    if dist is not None:
-        dist.destroy_process_group()
 
 
 def cpu_baseline_q3(hy, synth, sf, chunk, host_cpu, runs=5):

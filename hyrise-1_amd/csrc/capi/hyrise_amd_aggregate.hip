@@ -14,6 +14,7 @@
 #include "../kernels/projection.hip"
 #include "../kernels/aggregate_fused.hip"
 #include "../kernels/aggregate_lanes.hip"
+#include "../kernels/aggregate_vec.hip"
 
 using namespace hyc;
 
@@ -94,6 +95,7 @@ struct AggPlan {
   std::vector<hyk::LnTerm> lane_terms;     // lp.terms on the host
   std::vector<int32_t> lane_cols;          // input column of each loaded column
   bool lanes_vec = false;                  // agg_dense_lanes<.., VEC>: data input, 16-byte aligned column chunks
+  bool dense_vec = false;                  // agg_dense_vec instead (its preconditions hold; the default then)
 };
 
 // agg_dense_fused applies: the dense path; at most one PosList group; int32 group-by columns; every aggregate over a
@@ -336,10 +338,13 @@ void plan_lanes(const hy_agg_input* in, const hy_agg_params* p, AggPlan* plan) {
     }
   }
   plan->lanes = true;
-  // the contiguous-rows instance: a data input whose loaded columns' chunks (and a dictionary filter's id arrays) start
-  // 16-byte aligned, so one lane's 4 rows are one aligned vector load; HY_AGG_VEC=0 keeps the strided instance (A/B)
+  // the contiguous-rows kernels: a data input whose loaded columns' chunks (and a dictionary filter's id arrays) start
+  // 16-byte aligned, so one lane's 4 rows are one aligned vector load. agg_dense_vec (default) additionally needs
+  // DICT or NULL-free VALUE chunks and < 2^32 rows; HY_AGG_VEC=1 runs agg_dense_lanes' contiguous instance instead,
+  // HY_AGG_VEC=0 its strided one (A/B).
   const char* ev = std::getenv("HY_AGG_VEC");
-  bool vec = in->n_pos_groups == 0 && !(ev && std::atoi(ev) == 0);
+  const int vec_mode = ev ? std::atoi(ev) : 2;
+  bool vec = in->n_pos_groups == 0 && vec_mode != 0;
   auto aligned = [](const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15u) == 0; };
   for (const int32_t col : plan->lane_cols)
     for (uint32_t k = 0; k < in->columns[col].n_chunks && vec; ++k)
@@ -349,6 +354,14 @@ void plan_lanes(const hy_agg_input* in, const hy_agg_params* p, AggPlan* plan) {
       vec = in->filter[k].column.kind != HY_COL_DICT || in->filter[k].column.size == 0 ||
             aligned(in->filter[k].column.data);
   plan->lanes_vec = vec;
+  bool dv = vec && vec_mode != 1 && plan->rows < (1ull << 32) - 1;
+  for (const int32_t col : plan->lane_cols)
+    for (uint32_t k = 0; k < in->columns[col].n_chunks && dv; ++k) {
+      const auto& ch = in->columns[col].chunks[k];
+      dv = ch.size == 0 || ch.kind == HY_COL_DICT || (ch.kind == HY_COL_VALUE && ch.nulls == nullptr);
+    }
+  for (int32_t q = 0; q < lp.n_sums && dv; ++q) dv = lp.sum_len[q] <= hyk::VEC_TERMS;
+  plan->dense_vec = dv;
 }
 
 // Record bytes a hash table may take without a caller-given bound (at load 1/2: 2 slots per expected group).
@@ -418,8 +431,55 @@ void launch_lanes_n(bool vec, uint64_t n_tiles, size_t lds, hipStream_t s, const
     launch_lanes_pf<N, false, false>(n_tiles, lds, s, d, lp, records);
 }
 
-void launch_lanes(int n_sums, bool vec, uint64_t n_tiles, size_t lds, hipStream_t s, const hyk::AggDesc& d,
-                  const hyk::LanePlan& lp, unsigned long long* records) {
+// agg_dense_vec<n_sums, all float sums>, persistent like agg_dense_lanes.
+template <int N, bool ALLF>
+void launch_dense_vec_t(uint64_t n_tiles, size_t lds, hipStream_t s, const hyk::AggDesc& d, const hyk::LanePlan& lp,
+                        unsigned long long* records) {
+  static int resident = 0;
+  if (resident == 0) {
+    int per_cu = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hyk::agg_dense_vec<N, ALLF>, hyk::AGG_THREADS, lds) !=
+            hipSuccess ||
+        hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      per_cu = 4, cus = 256;
+    resident = std::max(1, per_cu) * std::max(1, cus);
+  }
+  const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(n_tiles, static_cast<uint64_t>(resident)));
+  hipLaunchKernelGGL((hyk::agg_dense_vec<N, ALLF>), dim3(grid), dim3(hyk::AGG_THREADS), lds, s, d, lp, records);
+}
+
+template <int N>
+void launch_dense_vec(bool all_float, uint64_t n_tiles, size_t lds, hipStream_t s, const hyk::AggDesc& d,
+                      const hyk::LanePlan& lp, unsigned long long* records) {
+  if (all_float)
+    launch_dense_vec_t<N, true>(n_tiles, lds, s, d, lp, records);
+  else
+    launch_dense_vec_t<N, false>(n_tiles, lds, s, d, lp, records);
+}
+
+void launch_lanes(int n_sums, bool vec, bool dense_vec, bool all_float, uint64_t n_tiles, size_t lds, hipStream_t s,
+                  const hyk::AggDesc& d, const hyk::LanePlan& lp, unsigned long long* records) {
+  if (dense_vec) {
+    switch (n_sums) {
+#define HY_VEC_CASE(N)                                       \
+  case N:                                                    \
+    launch_dense_vec<N>(all_float, n_tiles, lds, s, d, lp, records);    \
+    return;
+      HY_VEC_CASE(0)
+      HY_VEC_CASE(1)
+      HY_VEC_CASE(2)
+      HY_VEC_CASE(3)
+      HY_VEC_CASE(4)
+      HY_VEC_CASE(5)
+      HY_VEC_CASE(6)
+      HY_VEC_CASE(7)
+      HY_VEC_CASE(8)
+#undef HY_VEC_CASE
+      default:
+        break;
+    }
+  }
   switch (n_sums) {
 #define HY_LANES_CASE(N)                                         \
   case N:                                                        \
@@ -631,7 +691,7 @@ void carve(Carver& cv, const hy_agg_input* in, const AggPlan& plan, AggWs* w) {
         std::max<uint32_t>(1, in->columns[j].n_nodes ? in->n_chunks : in->columns[j].n_chunks));
   w->word_op = cv.take<int32_t>(plan.word_op.size());
   w->fused_nodes = cv.take<hyk::FqOp>(std::max<size_t>(1, plan.fused_nodes.size()));
-  w->lane_terms = cv.take<hyk::LnTerm>(std::max<size_t>(1, plan.lane_terms.size()));
+  w->lane_terms = cv.take<hyk::LnTerm>(plan.lane_terms.size() + hyk::VEC_TERMS);  // padding: agg_dense_vec
   w->lane_tables = cv.take<hyk::LaneTables>(1);
   w->filter = cv.take<hy_scan_chunk>(in->filter ? std::max<uint32_t>(1, in->n_chunks) : 1);
   w->deferred = cv.take<uint32_t>(plan.lanes ? std::max<uint64_t>(1, plan.n_tiles * hyk::FQ_STEPS_PER_TILE) : 1);
@@ -813,12 +873,16 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
       for (int32_t li = 0; li < lt.n_load; ++li) lt.load_chunks[li] = d.cols[plan.lane_cols[li]].chunks;
       HY_STAGE(w.lane_tables, &lt, sizeof(lt), s);
       HY_STAGE(w.lane_terms, plan.lane_terms.data(), sizeof(hyk::LnTerm) * plan.lane_terms.size(), s);
+      // (agg_dense_vec reads VEC_TERMS terms per sum: the table is padded to LN_TERMS + VEC_TERMS entries)
       const hyk::LanePlan lp{lt.n_load, lt.n_sums, w.lane_tables, w.lane_terms, w.deferred, w.misc + 8};
-      const size_t vlds = size_t(hyk::AGG_THREADS / hyk::WAVE) *
-                          hyk::ln_wave_lds(lt.n_load - static_cast<int>(params->n_groupby), lt.n_sums);
+      const int n_store = lt.n_load - static_cast<int>(params->n_groupby);
+      const size_t vlds = size_t(hyk::AGG_THREADS / hyk::WAVE) * (plan.dense_vec ? hyk::vec_wave_lds(n_store, lt.n_sums)
+                                                                                 : hyk::ln_wave_lds(n_store, lt.n_sums));
+      bool all_float = true;
+      for (int32_t q = 0; q < lt.n_sums; ++q) all_float = all_float && lt.sum_kind[q] != hyk::LN_SUM_INT;
       {
-        KTimer t("agg_dense_lanes", s, plan.rows);
-        launch_lanes(lp.n_sums, plan.lanes_vec, plan.n_tiles, vlds, s, d, lp, w.records);
+        KTimer t(plan.dense_vec ? "agg_dense_vec" : "agg_dense_lanes", s, plan.rows);
+        launch_lanes(lp.n_sums, plan.lanes_vec, plan.dense_vec, all_float, plan.n_tiles, vlds, s, d, lp, w.records);
         t.done();
       }
       HY_HIP(hipGetLastError());

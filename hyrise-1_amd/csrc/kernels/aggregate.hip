@@ -102,27 +102,75 @@ struct AggDesc {
 // Item k < R of a lane in one aggregation step is row first + k * STRIDE of its chunk: STRIDE = WAVE for the FQ-style
 // mapping (first = base + lane), STRIDE = 1 for a lane's R consecutive rows (first = base + lane * R; agg_dense_lanes
 // over a data input reads them with one vector load per column).
+typedef uint32_t hy_u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t hy_u32x4 __attribute__((ext_vector_type(4)));
 template <int R>
 __device__ __forceinline__ void vec_load_ids(const void* data, uint32_t width, uint32_t first, uint32_t (&v)[R]) {
   static_assert(R == 4, "one dword / dwordx2 / dwordx4 per lane");
+  const uintptr_t p = reinterpret_cast<uintptr_t>(data);
   if (width == 1) {
-    const uint32_t w = *reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(
-        reinterpret_cast<uintptr_t>(data) + first);
+    const uint32_t w = *reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(p + first);
 #pragma unroll
     for (int k = 0; k < R; ++k) v[k] = (w >> (8 * k)) & 0xFFu;
   } else if (width == 2) {
-    const uint2 w = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(data) + first);
+    const hy_u32x2 w = *reinterpret_cast<const __attribute__((address_space(1))) hy_u32x2*>(p + 2ull * first);
     v[0] = w.x & 0xFFFFu;
     v[1] = w.x >> 16;
     v[2] = w.y & 0xFFFFu;
     v[3] = w.y >> 16;
   } else {
-    const uint4 w = *reinterpret_cast<const uint4*>(static_cast<const uint32_t*>(data) + first);
+    const hy_u32x4 w = *reinterpret_cast<const __attribute__((address_space(1))) hy_u32x4*>(p + 4ull * first);
     v[0] = w.x;
     v[1] = w.y;
     v[2] = w.z;
     v[3] = w.w;
   }
+}
+// The same rows one element at a time (a chunk's last, partial step), indexes clamped to the chunk.
+template <int R>
+__device__ __forceinline__ void elem_load_ids(const void* data, uint32_t width, uint32_t first, uint32_t size,
+                                              uint32_t (&v)[R]) {
+  const uintptr_t p = reinterpret_cast<uintptr_t>(data);
+  if (width == 1) {
+#pragma unroll
+    for (int k = 0; k < R; ++k)
+      v[k] = *reinterpret_cast<const __attribute__((address_space(1))) uint8_t*>(p + min(first + k, size - 1));
+  } else if (width == 2) {
+#pragma unroll
+    for (int k = 0; k < R; ++k)
+      v[k] = *reinterpret_cast<const __attribute__((address_space(1))) uint16_t*>(p + 2ull * min(first + k, size - 1));
+  } else {
+#pragma unroll
+    for (int k = 0; k < R; ++k)
+      v[k] = *reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(p + 4ull * min(first + k, size - 1));
+  }
+}
+
+// A dictionary predicate (op, search_vid) of the host's rewrite as an id range: a non-NULL id matches iff
+// ((id - lo) < span) != neg - EQ [s, s+1), LT [0, s), LE [0, s+1), NE / GE / GT their complements, ALL / IS NOT NULL
+// everything, NONE nothing. One subtract, compare and xor per row instead of a switch on the op.
+struct IdRange {
+  uint32_t lo, span, neg, dsize;
+  bool range;  // false: an op without a range form (VID_SET, ...)
+};
+__device__ __forceinline__ IdRange id_range(int32_t op, uint32_t svid, uint32_t dsize) {
+  IdRange r{0u, 0u, 0u, dsize, true};
+  switch (op) {
+    case HY_OP_EQ: r.lo = svid; r.span = 1; break;
+    case HY_OP_NE: r.lo = svid; r.span = 1; r.neg = 1; break;
+    case HY_OP_LT: r.span = svid; break;
+    case HY_OP_LE: r.span = svid + 1; break;
+    case HY_OP_GT: r.span = svid + 1; r.neg = 1; break;
+    case HY_OP_GE: r.span = svid; r.neg = 1; break;
+    case HY_OP_ALL:
+    case HY_OP_IS_NOT_NULL: r.neg = 1; break;
+    case HY_OP_NONE: break;
+    default: r.range = false; break;
+  }
+  return r;
+}
+__device__ __forceinline__ bool id_in_range(const IdRange& r, uint32_t id) {
+  return ((id - r.lo < r.span) != (r.neg != 0)) && id < r.dsize;
 }
 
 // Match mask of a lane's items (see above) of input chunk c under the fused scan predicate (reference
@@ -153,10 +201,16 @@ __device__ __forceinline__ uint32_t agg_filter_mask(const AggDesc& d, uint32_t c
                            : static_cast<const uint32_t*>(f.column.data)[i];
       }
     }
+    const IdRange ir = id_range(f.op, f.search_vid, f.column.dictionary_size);
+    if (ir.range) {
 #pragma unroll
-    for (int k = 0; k < R; ++k)
-      m |= static_cast<uint32_t>(vids[k] != f.column.dictionary_size && cmp_op<uint32_t>(f.op, vids[k], f.search_vid))
-           << k;
+      for (int k = 0; k < R; ++k) m |= static_cast<uint32_t>(id_in_range(ir, vids[k])) << k;
+    } else {
+#pragma unroll
+      for (int k = 0; k < R; ++k)
+        m |= static_cast<uint32_t>(vids[k] != f.column.dictionary_size && cmp_op<uint32_t>(f.op, vids[k], f.search_vid))
+             << k;
+    }
   } else {
 #pragma unroll
     for (int k = 0; k < R; ++k) {
@@ -398,7 +452,7 @@ __global__ __launch_bounds__(AGG_THREADS) void agg_dense_rows(AggDesc d, uint32_
   for (uint32_t i = threadIdx.x; i < n_words; i += AGG_THREADS) s_rec[i] = word_init(d.word_op[i % words]);
   __syncthreads();
   const int lane = __lane_id();
-  const int w = threadIdx.x / WAVE;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   const uint32_t H = d.n_gb;  // header starts after the key words
 
   for (uint64_t tile = blockIdx.x; tile < d.n_tiles; tile += gridDim.x) {
@@ -644,7 +698,7 @@ __global__ __launch_bounds__(AGG_THREADS) void agg_dense_span(AggDesc d, uint32_
   for (uint32_t i = threadIdx.x; i < n_words; i += AGG_THREADS) s_recd[i] = word_init(d.word_op[i % words]);
   __syncthreads();
   const int lane = __lane_id();
-  const int w = threadIdx.x / WAVE;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   const uint32_t H = d.n_gb;
 
   for (uint64_t tile = blockIdx.x; tile < d.n_tiles; tile += gridDim.x) {

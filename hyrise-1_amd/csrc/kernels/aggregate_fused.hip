@@ -520,7 +520,7 @@ __global__ __launch_bounds__(AGG_THREADS) void agg_dense_fused(AggDesc d, FusedP
   const uint32_t n_words = n_groups * words;
   for (uint32_t i = threadIdx.x; i < n_words; i += AGG_THREADS) s_recf[i] = word_init(d.word_op[i % words]);
   __syncthreads();
-  const int w = threadIdx.x / WAVE;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   if (steps == nullptr) {
     for (uint64_t tile = blockIdx.x; tile < d.n_tiles; tile += gridDim.x) {
       const uint32_t c = agg_tile_chunk(d, tile);

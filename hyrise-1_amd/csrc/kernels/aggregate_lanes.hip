@@ -266,7 +266,7 @@ __global__ __launch_bounds__(AGG_THREADS) __attribute__((amdgpu_waves_per_eu(PF 
   constexpr int NA = NS > 0 ? NS : 1;
   extern __shared__ __align__(16) unsigned char s_lanes[];
   const int lane = __lane_id();
-  const int w = threadIdx.x / WAVE;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);  // wave-uniform: steps branch on scalars
   const uint32_t H = d.n_gb;
   const int n_store = lp.n_load - static_cast<int>(H);
   unsigned char* wl = s_lanes + static_cast<size_t>(w) * ln_wave_lds(n_store, NS);

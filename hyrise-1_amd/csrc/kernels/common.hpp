@@ -179,7 +179,7 @@ __device__ inline uint32_t wave_sum(uint32_t v) {
 template <int NT>
 __device__ inline uint32_t block_exclusive_sum(uint32_t v, uint32_t* scratch, uint32_t* total) {
   constexpr int NW = NT / WAVE;
-  const int w = threadIdx.x / WAVE;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   const uint32_t incl = wave_inclusive_sum(v);
   if (__lane_id() == WAVE - 1) scratch[w] = incl;
   __syncthreads();

@@ -501,7 +501,7 @@ __device__ __forceinline__ void staged_scatter(const Rec<H, P> (&recs)[PART_ITEM
                                                uint32_t* s_delta, Rec<H, P>* s_stage, uint32_t* s_scratch,
                                                uint32_t n_digits, const Digit& dg, const NextDigit& nd,
                                                uint32_t& run, Rec<H, P>* __restrict__ out) {
-  const int w = threadIdx.x / WAVE;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   __syncthreads();  // every wave's counts are in s_cnt
   const uint32_t d = threadIdx.x;
   uint32_t tot = 0;
@@ -556,7 +556,7 @@ __global__ __launch_bounds__(PART_THREADS) void part1_hist(Side s, Digit dg, uin
   const SrcChunk ch = s.chunks[c];
   const uint32_t base = static_cast<uint32_t>(tile - s.chunk_tile_begin[c]) * (s.sub * PART_TILE);
   const uint32_t n_sub = min(s.sub, (ch.size - base + PART_TILE - 1) / PART_TILE);
-  const int w = threadIdx.x / WAVE;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
 #pragma unroll 1
   for (uint32_t j = 0; j < n_sub; ++j) {
     H keys[PART_ITEMS];
@@ -587,7 +587,7 @@ __global__ __launch_bounds__(PART_THREADS) __attribute__((amdgpu_waves_per_eu(4)
   const SrcChunk ch = s.chunks[c];
   const uint32_t base = static_cast<uint32_t>(tile - s.chunk_tile_begin[c]) * (s.sub * PART_TILE);
   const uint32_t n_sub = min(s.sub, (ch.size - base + PART_TILE - 1) / PART_TILE);
-  const int w = threadIdx.x / WAVE;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   uint32_t run = threadIdx.x < n_digits ? offsets[threadIdx.x * s.n_tiles + tile] : 0u;
 
   uint64_t* s_mask = reinterpret_cast<uint64_t*>(s_stage) + w * 256;  // ranking masks alias the staging area
@@ -641,7 +641,7 @@ __global__ __launch_bounds__(PART_THREADS) void part1_compact(Side s, Digit dg, 
   const SrcChunk ch = s.chunks[c];
   const uint32_t base = static_cast<uint32_t>(tile - s.chunk_tile_begin[c]) * (s.sub * PART_TILE);
   const uint32_t n_sub = min(s.sub, (ch.size - base + PART_TILE - 1) / PART_TILE);
-  const int w = threadIdx.x / WAVE, lane = __lane_id();
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE), lane = __lane_id();
   Rec<H, uint32_t>* out = gap_out + tile * (static_cast<uint64_t>(s.sub) * PART_TILE);
   uint32_t run = 0;
   __syncthreads();
@@ -704,7 +704,7 @@ __global__ __launch_bounds__(PART_THREADS) void part1_spread(Side s, Digit dg, N
   const uint32_t c = s.tile_chunk[tile];
   const uint32_t row0 = static_cast<uint32_t>(s.chunks[c].row_begin);  // payload -> chunk offset
   const Rec<H, uint32_t>* in = gap_in + tile * (static_cast<uint64_t>(s.sub) * PART_TILE);
-  const int w = threadIdx.x / WAVE;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   uint32_t run = threadIdx.x < n_digits ? offsets[threadIdx.x * s.n_tiles + tile] : 0u;
   const uint32_t srun = offsets[n_digits * s.n_tiles + tile] - offsets[n_digits * s.n_tiles];
   uint64_t* s_mask = reinterpret_cast<uint64_t*>(s_stage) + w * 256;  // ranking masks alias the staging area
@@ -764,7 +764,7 @@ __global__ __launch_bounds__(PART_THREADS) void part1_mask(Side s, Digit dg, uin
   const SrcChunk ch = s.chunks[c];
   const uint32_t base = static_cast<uint32_t>(tile - s.chunk_tile_begin[c]) * (s.sub * PART_TILE);
   const uint32_t n_sub = min(s.sub, (ch.size - base + PART_TILE - 1) / PART_TILE);
-  const int w = threadIdx.x / WAVE, lane = __lane_id();
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE), lane = __lane_id();
   uint32_t matches = 0;  // this wave's scan matches in the span (wave-uniform)
   __syncthreads();
 #pragma unroll 1
@@ -960,7 +960,7 @@ __global__ __launch_bounds__(PART_THREADS) void part1_onepass(Side s, Digit dg, 
   const uint32_t c = s.tile_chunk[tile];
   const SrcChunk ch = s.chunks[c];
   const uint32_t base = static_cast<uint32_t>(tile - s.chunk_tile_begin[c]) * PART_TILE;
-  const int w = threadIdx.x / WAVE, lane = __lane_id();
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE), lane = __lane_id();
   uint64_t* s_mask = reinterpret_cast<uint64_t*>(s_stage) + w * 256;  // ranking masks alias the staging area
   clear_wave_counts(s_cnt[w]);
   clear_wave_masks(s_mask);
@@ -1071,7 +1071,7 @@ static __global__ __launch_bounds__(PART_THREADS) void part1_scan_expand(Side s,
   __shared__ uint32_t s_w[PART_WAVES + 1];
   __shared__ uint32_t s_out[PART_TILE];
   const uint64_t tile = xcd_tile(blockIdx.x, gridDim.x);
-  const int w = threadIdx.x / WAVE, lane = __lane_id();
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE), lane = __lane_id();
   const uint32_t c = s.tile_chunk[tile];
   const uint32_t base = static_cast<uint32_t>(tile - s.chunk_tile_begin[c]) * PART_TILE + w * WAVE_SPAN;
   uint64_t b[PART_ITEMS];
@@ -1199,7 +1199,7 @@ __global__ __launch_bounds__(PART_THREADS) void part2_hist(Segs sg, Digit dg, ui
   uint32_t b0, b1, stride, toff;
   uint64_t hbase;
   seg_geometry(sg, sgi, n_digits, &b0, &b1, &hbase, &stride, &toff);
-  const int w = threadIdx.x / WAVE;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   const uint32_t sb = b0 + t_in * (sg.sub * PART_TILE);
   const uint32_t n_sub = min(sg.sub, (b1 - sb + PART_TILE - 1) / PART_TILE);
 #pragma unroll 1
@@ -1234,7 +1234,7 @@ __global__ __launch_bounds__(PART_THREADS) void part2_scatter(Segs sg, Digit dg,
   uint32_t b0, b1, stride, toff;
   uint64_t hbase;
   seg_geometry(sg, sgi, n_digits, &b0, &b1, &hbase, &stride, &toff);
-  const int w = threadIdx.x / WAVE;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   const uint32_t sb = b0 + t_in * (sg.sub * PART_TILE);
   const uint32_t n_sub = min(sg.sub, (b1 - sb + PART_TILE - 1) / PART_TILE);
   uint32_t run = threadIdx.x < n_digits ? offsets[hbase + threadIdx.x * stride + toff + t_in] : 0u;
@@ -1279,7 +1279,7 @@ static __global__ __launch_bounds__(PART_THREADS) void part2_hist_bytes(Segs sg,
   uint32_t b0, b1, stride, toff;
   uint64_t hbase;
   seg_geometry(sg, sgi, n_digits, &b0, &b1, &hbase, &stride, &toff);
-  const int w = threadIdx.x / WAVE;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   const uint32_t sb = b0 + t_in * (sg.sub * PART_TILE);
   const uint32_t n_sub = min(sg.sub, (b1 - sb + PART_TILE - 1) / PART_TILE);
 #pragma unroll 1
@@ -1654,7 +1654,7 @@ __device__ __forceinline__ uint64_t allocate_output(const JoinDesc& d, uint32_t 
 template <int JP, int NT, typename EF>
 __device__ __forceinline__ uint32_t pass_offsets(EF e_of, uint32_t* s_tot) {
   const int lane = __lane_id();
-  const int w = threadIdx.x / WAVE;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
 #pragma unroll
   for (int k = 0; k < JP; ++k) {
     const uint32_t e = e_of(k);

@@ -213,7 +213,8 @@ def test_lanes_path(hy, monkeypatch, case, input_kind):
     rf, ls, qty, price, disc, tax, iq, price_n, disc_n, doms = cols
     dcols = [dt.DeviceColumn(capi, rf, None, CHUNK, "Dictionary"), dt.DeviceColumn(capi, ls, None, CHUNK, "Dictionary"),
              dt.DeviceColumn(capi, qty, None, CHUNK, "Dictionary"),
-             dt.DeviceColumn(capi, price, price_n, CHUNK, "Dictionary" if case == "nulls" else "Unencoded"),
+             dt.DeviceColumn(capi, price, price_n if price_n.any() else None, CHUNK,
+                             "Dictionary" if case == "nulls" else "Unencoded"),
              dt.DeviceColumn(capi, disc, disc_n, CHUNK, "Dictionary"), dt.DeviceColumn(capi, tax, None, CHUNK,
                                                                                        "Dictionary"),
              dt.DeviceColumn(capi, iq, None, CHUNK, "Unencoded")]
@@ -239,14 +240,26 @@ def test_lanes_path(hy, monkeypatch, case, input_kind):
             sizes.append(pl.shape[0])
             rows += [int(i) * CHUNK + int(o) for i, o in zip(ids, offs)]
     exp = expected(cols, rows)
-    L.hy_kernel_stats_enable(1)
-    L.hy_kernel_stats_reset()
-    res_lanes = run(hy, dcols, pos, sizes, doms)
-    ran = kernels_ran(L)
-    L.hy_kernel_stats_enable(0)
-    assert "agg_dense_lanes" in ran, ran
-    check(res_lanes, exp)
+    # data input: agg_dense_vec (default), agg_dense_lanes' contiguous instance (HY_AGG_VEC=1) and its strided one (0)
+    headers = {}
+    for vec_mode in (("2", "1", "0") if input_kind == "data" else ("2",)):
+        monkeypatch.setenv("HY_AGG_VEC", vec_mode)
+        L.hy_kernel_stats_enable(1)
+        L.hy_kernel_stats_reset()
+        res_lanes = run(hy, dcols, pos, sizes, doms)
+        ran = kernels_ran(L)
+        L.hy_kernel_stats_enable(0)
+        want = "agg_dense_vec" if (input_kind == "data" and vec_mode == "2") else "agg_dense_lanes"
+        assert want in ran, (vec_mode, ran)
+        check(res_lanes, exp)
+        headers[vec_mode] = {(int(r[0]), int(r[1])): tuple(int(x) for x in r[2:6])
+                             for r in run(hy, dcols, pos, sizes, doms, raw=True)[0]}
     monkeypatch.setenv("HY_AGG_LANES", "0")
+    # NULL mask, first row, last row, rows of every group (the Aggregate's output order follows the first rows)
+    fused_headers = {(int(r[0]), int(r[1])): tuple(int(x) for x in r[2:6])
+                     for r in run(hy, dcols, pos, sizes, doms, raw=True)[0]}
+    for mode, hd in headers.items():
+        assert hd == fused_headers, mode
     res_fused = run(hy, dcols, pos, sizes, doms)
     check(res_fused, exp)
     assert res_lanes == res_fused or all(
@@ -308,7 +321,7 @@ def test_merge_of_partial_aggregates(hy, case, n_parts):
 @pytest.mark.parametrize("pred_enc,cond,value", [("Dictionary", "LessThanEquals", 300), ("Unencoded", "LessThan", 250),
                                                  ("Dictionary", "GreaterThan", 1000), ("Dictionary", "LessThan", 0)])
 @pytest.mark.parametrize("case", ["clean", "nulls", "odd_values"])
-def test_fused_scan_filter(hy, case, pred_enc, cond, value):
+def test_fused_scan_filter(hy, monkeypatch, case, pred_enc, cond, value):
     """hy_aggregate with a fused TableScan (hy_agg_input.filter) over a data input: every aggregate equals the
     aggregate of exactly the matching rows (numpy over the predicate's rows) - TPC-H 1's Scan -> Aggregate in one
     pass, the lanes path and the steps it defers to agg_dense_fused (NULLs, odd values) alike; predicates with all,
@@ -320,13 +333,16 @@ def test_fused_scan_filter(hy, case, pred_enc, cond, value):
     ship = rng.integers(0, 1000, N).astype(np.int32)  # > 256 distinct values: 2-byte value ids
     dcols = [dt.DeviceColumn(capi, rf, None, CHUNK, "Dictionary"), dt.DeviceColumn(capi, ls, None, CHUNK, "Dictionary"),
              dt.DeviceColumn(capi, qty, None, CHUNK, "Dictionary"),
-             dt.DeviceColumn(capi, price, price_n, CHUNK, "Dictionary" if case == "nulls" else "Unencoded"),
+             dt.DeviceColumn(capi, price, price_n if price_n.any() else None, CHUNK,
+                             "Dictionary" if case == "nulls" else "Unencoded"),
              dt.DeviceColumn(capi, disc, disc_n, CHUNK, "Dictionary"),
              dt.DeviceColumn(capi, tax, None, CHUNK, "Dictionary"), dt.DeviceColumn(capi, iq, None, CHUNK, "Unencoded")]
     pred = dt.DeviceColumn(capi, ship, None, CHUNK, pred_enc)
     chunks = pred.scan_chunks(cond, value)
     sizes = [d.size for d in dcols[0].descs]
-    res = run(hy, dcols, None, sizes, doms, filt=(chunks, capi.HY_TYPE_INT32, pred.constant(value)))
     op = {"LessThanEquals": np.less_equal, "LessThan": np.less, "GreaterThan": np.greater}[cond]
     rows = list(np.nonzero(op(ship, value))[0])
-    check(res, expected(cols, rows))
+    for vec_mode in ("2", "0"):  # agg_dense_vec, agg_dense_lanes (strided)
+        monkeypatch.setenv("HY_AGG_VEC", vec_mode)
+        res = run(hy, dcols, None, sizes, doms, filt=(chunks, capi.HY_TYPE_INT32, pred.constant(value)))
+        check(res, expected(cols, rows))
