@@ -52,9 +52,10 @@ def parse():
                         "TableScan l_quantity<24 alone (SF10 default); join-only: config 3, JoinHash lineitem x orders "
                         "over all lineitem rows (SF10 default)")
     p.add_argument("--q1-fused", action="store_true",
-                   help="q1: the TableScan fused into the aggregate (hy_agg_input.filter) instead of the reference plan "
-                        "(scan to PosLists, aggregate over them); measured no faster at SF100 (11.2 vs 11.0 ms): the "
-                        "aggregation kernel is latency-bound, not bound by the RowID bytes the fusion saves")
+                   help="q1: the TableScan fused into the aggregate (hy_agg_input.filter; agg_dense_vec) - the default")
+    p.add_argument("--q1-poslist", action="store_true",
+                   help="q1: the reference plan shape instead - TableScan to PosLists, the aggregate over them "
+                        "(agg_dense_lanes through the RowIDs); A/B")
     p.add_argument("--q1-materialize", action="store_true",
                    help="q1: materialise the two arithmetic expressions with hy_projection before the aggregate "
                         "(the reference's plan shape) instead of evaluating them inside it (A/B)")

@@ -640,7 +640,7 @@ def main_q1(args):
     state = {}
 
     # fused plan (default): the TableScan's predicate evaluated inside the aggregate over the data chunks
-    fused_scan = args.q1_fused and not args.q1_materialize
+    fused_scan = not (args.q1_poslist or args.q1_materialize)
     if fused_scan:
         data_cols = (capi.AggColumn * 8)()
         for j, (vt, chs, dom) in ref_cols.items():

@@ -361,6 +361,7 @@ void plan_lanes(const hy_agg_input* in, const hy_agg_params* p, AggPlan* plan) {
       dv = ch.size == 0 || ch.kind == HY_COL_DICT || (ch.kind == HY_COL_VALUE && ch.nulls == nullptr);
     }
   for (int32_t q = 0; q < lp.n_sums && dv; ++q) dv = lp.sum_len[q] <= hyk::VEC_TERMS;
+  dv = dv && lp.n_load <= hyk::VEC_COLS;
   plan->dense_vec = dv;
 }
 
@@ -878,7 +879,9 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
       const int n_store = lt.n_load - static_cast<int>(params->n_groupby);
       const size_t vlds = size_t(hyk::AGG_THREADS / hyk::WAVE) * (plan.dense_vec ? hyk::vec_wave_lds(n_store, lt.n_sums)
                                                                                  : hyk::ln_wave_lds(n_store, lt.n_sums));
-      bool all_float = true;
+      // the all-float instance (no per-value choice of conversion) unless HY_VEC_ALLF=0 (A/B)
+      const char* eaf = std::getenv("HY_VEC_ALLF");
+      bool all_float = !(eaf && std::atoi(eaf) == 0);
       for (int32_t q = 0; q < lt.n_sums; ++q) all_float = all_float && lt.sum_kind[q] != hyk::LN_SUM_INT;
       {
         KTimer t(plan.dense_vec ? "agg_dense_vec" : "agg_dense_lanes", s, plan.rows);

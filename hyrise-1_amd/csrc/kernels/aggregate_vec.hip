@@ -26,39 +26,13 @@
 namespace hyk {
 
 constexpr int VEC_TERMS = 4;  // terms per sum's chain (longer chains: agg_dense_lanes)
+constexpr int VEC_COLS = 7;   // loaded columns (more: agg_dense_lanes)
+constexpr uint32_t VEC_NO_DICT = 0xFFFFFFFFu;
 
 // Per-wave LDS of agg_dense_vec: the stored columns of a step (agg_dense_lanes' layout), the flush staging, the
 // small dictionaries, then the ids of the period's accumulated steps.
 __host__ __device__ inline size_t vec_wave_lds(int n_store, int n_sums) {
   return ln_wave_lds(n_store, n_sums) + LN_FLUSH_STEPS * 4;
-}
-
-// One column's 4 rows at `first` (vector loads when the wave's whole step is in the chunk: `full` is wave-uniform, so
-// the choice is a scalar branch), dictionary-decoded (LDS cache of small dictionaries, else a gather); nl: the rows
-// whose id is the NULL id.
-__device__ __forceinline__ void vec_column(const hy_column_chunk* __restrict__ chunks_c, int li, uint32_t c, uint32_t first,
-                                           uint32_t size, bool full, const uint32_t* dcache, uint32_t (&v)[FQ_R],
-                                           uint32_t* nl) {
-  const auto& ch = ln_const(chunks_c)[c];
-  const uint32_t dsize = ch.dictionary_size;
-  const bool dict = ch.kind == HY_COL_DICT;
-  const uint32_t width = dict ? static_cast<uint32_t>(ch.vid_width) : 4u;
-  if (full)
-    vec_load_ids<FQ_R>(ch.data, width, first, v);
-  else
-    elem_load_ids<FQ_R>(ch.data, width, first, size, v);
-  *nl = 0;
-  if (dict) {
-    const bool cached = dsize <= LN_DICT_CACHE;
-    const uintptr_t dv = reinterpret_cast<uintptr_t>(ch.dictionary);
-#pragma unroll
-    for (int k = 0; k < FQ_R; ++k) {
-      const bool isnull = v[k] >= dsize;
-      *nl |= static_cast<uint32_t>(isnull) << k;
-      const uint32_t id = isnull ? 0u : v[k];
-      v[k] = cached ? dcache[li * LN_DICT_CACHE + id] : ln_load_word(dv, id * 4u);
-    }
-  }
 }
 
 __device__ __forceinline__ uint32_t wave_max_u(uint32_t v) {
@@ -149,7 +123,7 @@ __device__ __forceinline__ void vec_flush(const AggDesc& d, const LanePlan& lp, 
 
 // ALLF: every sum is a float sum (TPC-H 1): no per-value choice between the float and the int32 conversion.
 template <int NS, bool ALLF>
-__global__ __launch_bounds__(AGG_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void agg_dense_vec(
+__global__ __launch_bounds__(AGG_THREADS) __attribute__((amdgpu_waves_per_eu(3))) void agg_dense_vec(
     AggDesc d, LanePlan lp, unsigned long long* __restrict__ records) {
   constexpr int NA = NS > 0 ? NS : 1;
   constexpr int R = FQ_R;
@@ -232,6 +206,22 @@ __global__ __launch_bounds__(AGG_THREADS) __attribute__((amdgpu_waves_per_eu(4))
       uint32_t act = 0;
 #pragma unroll
       for (int k = 0; k < R; ++k) act |= static_cast<uint32_t>(first + k < size) << k;
+      // (0) every column's ids / values of the step in flight at once (the descriptors are scalar loads of one
+      // batch), before anything waits on them
+      uint32_t raw[VEC_COLS][R];
+      uint32_t cdsize[VEC_COLS];  // dictionary size (ids >= it: NULL), VEC_NO_DICT for a value chunk
+#pragma unroll
+      for (int li = 0; li < VEC_COLS; ++li) {
+        if (li >= nl) break;
+        const auto& ch = ln_const(T->load_chunks[li])[c];
+        const bool dict = ch.kind == HY_COL_DICT;
+        const uint32_t width = dict ? static_cast<uint32_t>(ch.vid_width) : 4u;
+        cdsize[li] = dict ? ch.dictionary_size : VEC_NO_DICT;
+        if (full)
+          vec_load_ids<R>(ch.data, width, first, raw[li]);
+        else
+          elem_load_ids<R>(ch.data, width, first, size, raw[li]);
+      }
       if (f_mode == 1) {  // fused TableScan, dictionary predicate: one vector load of the ids, a range test per row
         uint32_t ids[R];
         if (full)
@@ -244,20 +234,36 @@ __global__ __launch_bounds__(AGG_THREADS) __attribute__((amdgpu_waves_per_eu(4))
         act &= agg_filter_mask<R, 1>(d, c, first);
       }
       if (__ballot(act != 0) == 0ull) continue;
+      // decode: dictionary ids -> values (LDS cache of small dictionaries, else a gather); nl: NULL ids
+      auto decode = [&](int li, uint32_t (&v)[R]) -> uint32_t {
+        uint32_t nl_ = 0;
+        if (cdsize[li] != VEC_NO_DICT) {
+          const bool cached = cdsize[li] <= LN_DICT_CACHE;
+          const uintptr_t dv = cached ? 0 : reinterpret_cast<uintptr_t>(ln_const(T->load_chunks[li])[c].dictionary);
+#pragma unroll
+          for (int k = 0; k < R; ++k) {
+            const bool isnull = v[k] >= cdsize[li];
+            nl_ |= static_cast<uint32_t>(isnull) << k;
+            const uint32_t id = isnull ? 0u : v[k];
+            v[k] = cached ? dcache[li * LN_DICT_CACHE + id] : ln_load_word(dv, id * 4u);
+          }
+        }
+        return nl_;
+      };
       // (1) group codes -> table entries (a refill may end the period)
       uint32_t g[R] = {0, 0, 0, 0};
       bool bad_code = false;
-#pragma unroll 1
-      for (uint32_t li = 0; li < H; ++li) {
-        uint32_t v[R], gn;
-        vec_column(T->load_chunks[li], static_cast<int>(li), c, first, size, full, dcache, v, &gn);
+#pragma unroll
+      for (int li = 0; li < FQ_MAX_GB; ++li) {
+        if (static_cast<uint32_t>(li) >= H) break;
+        const uint32_t gn = decode(li, raw[li]);
         const uint32_t domain = T->gb_domain[li], stride = T->gb_stride[li];
 #pragma unroll
         for (int k = 0; k < R; ++k) {
           const bool isnull = (gn >> k) & 1u;
-          const bool out = !isnull && v[k] >= domain;
+          const bool out = !isnull && raw[li][k] >= domain;
           bad_code = bad_code || (out && ((act >> k) & 1u));
-          g[k] += ((isnull || out) ? domain : v[k]) * stride;
+          g[k] += ((isnull || out) ? domain : raw[li][k]) * stride;
         }
       }
       if (bad_code) atomicOr(d.error, 2u);
@@ -310,14 +316,14 @@ __global__ __launch_bounds__(AGG_THREADS) __attribute__((amdgpu_waves_per_eu(4))
             e[k] = g[k] == static_cast<uint32_t>(tab[j]) ? static_cast<uint32_t>(j) : e[k];
         }
       }
-      // (2) the other loaded columns, decoded, into the wave's LDS
+      // (2) the other loaded columns, decoded, into the wave's LDS (the chains read them by column index)
       uint32_t vnull = 0;  // rows with a NULL in a non-group-by column
-#pragma unroll 1
-      for (int li = static_cast<int>(H); li < nl; ++li) {
-        uint32_t v[R], vn;
-        vec_column(T->load_chunks[li], li, c, first, size, full, dcache, v, &vn);
-        vnull |= vn;
-        vals[(li - static_cast<int>(H)) * WAVE + lane] = make_uint4(v[0], v[1], v[2], v[3]);
+#pragma unroll
+      for (int li = 0; li < VEC_COLS; ++li) {
+        if (li >= nl) break;
+        if (static_cast<uint32_t>(li) < H) continue;
+        vnull |= decode(li, raw[li]);
+        vals[(li - static_cast<int>(H)) * WAVE + lane] = make_uint4(raw[li][0], raw[li][1], raw[li][2], raw[li][3]);
       }
       if (__ballot((vnull & act) != 0) != 0ull) {
         ln_defer(lp, step_id);

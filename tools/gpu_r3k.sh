@@ -6,4 +6,4 @@ rc=$?
 echo "pytest rc=$rc"
 case $rc in 124|134|137|139) exit 1;; esac
 timeout -k 10 240 python -u bench.py --workload q1 --q1-fused --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/r3k_q1_fused.json 2> gpurun_out/r3k_q1_fused.err || exit 3
-bash tools/pmc_lanes.sh q1vec4 --q1-fused > gpurun_out/r3k_pmc_vec.txt 2>&1 || exit 7
+bash tools/pmc_lanes.sh q1vec5 --q1-fused > gpurun_out/r3k_pmc_vec.txt 2>&1 || exit 7
