@@ -769,8 +769,9 @@ size_t classic_join_bytes(const SidePlan& bp, const SidePlan& pp, uint32_t bits)
   uint64_t ha, hb, t;
   pass_sizes(sizes_of(bp, db), w, 1, &ha, &t);
   pass_sizes(sizes_of(pp, db), w, 1, &hb, &t);
-  Common c;
+  Common c, cb;  // (join_typed: the probe side's and the build side's)
   carve_common(cv, std::max({ha, hb, (uint64_t(1) << bits) + 1}), bits, &c);
+  carve_common(cv, std::max({ha, hb, (uint64_t(1) << bits) + 1}), bits, &cb);
   cv.take<uint32_t>(std::max<uint64_t>(1, bloom_words(bp.n_rows, pp.n_rows)));
   return cv.used + 256;
 }
@@ -1082,6 +1083,38 @@ inline SidePlan one_tile_spans(const SidePlan& p) {
 }
 
 // Workspace of a single-GPU join: enough for the single-pass path (when it applies) and for its fallback.
+// The build side's passes on a second stream, concurrent with the probe side's (they share nothing until the
+// partition join): the small build-side kernels and the probe side's scans leave HBM bandwidth idle that the other
+// side's streaming passes then use. One side stream and a fork / join event pair per thread and device, created on
+// first use (a stream being captured into a hipGraph forks into it by the event, as HIP capture allows).
+// HY_JOIN_OVERLAP=0 runs both sides on the caller's stream (A/B).
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+  int device = -1;
+};
+inline bool overlap_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("HY_JOIN_OVERLAP");
+    return !(e && std::strtol(e, nullptr, 10) == 0);
+  }();
+  return v;
+}
+inline SideStream* side_stream() {
+  static thread_local SideStream ss[16];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
+  SideStream& x = ss[dev];
+  if (!x.s) {
+    if (hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&x.join, hipEventDisableTiming) != hipSuccess)
+      return nullptr;
+    x.device = dev;
+  }
+  return &x;
+}
+
 template <typename H>
 size_t join_bytes(const SidePlan& bp, const SidePlan& pp, uint32_t bits) {
   size_t n = classic_join_bytes<H>(bp, pp, bits);
@@ -1121,14 +1154,22 @@ hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join
   uint64_t ha, hb2, t;
   pass_sizes(sizes_of(bp, db), w, 1, &ha, &t);
   pass_sizes(sizes_of(pp, db), w, 1, &hb2, &t);
-  Common c{};
+  Common c{}, cb{};  // c: the probe side and the partition join; cb: the build side (it may run concurrently)
   carve_common(cv, std::max({ha, hb2, (uint64_t(1) << bits) + 1}), bits, &c);
+  carve_common(cv, std::max({ha, hb2, (uint64_t(1) << bits) + 1}), bits, &cb);
   const uint64_t bloom_n = bloom_words(bp.n_rows, pp.n_rows);
   uint32_t* bloom = cv.take<uint32_t>(std::max<uint64_t>(1, bloom_n));
   if (!cv.ok) return fail(HY_ERR_WORKSPACE, "join workspace too small");
   if (upload_side(bp, bb, s) || upload_side(pp, pb, s)) return HY_ERR_DEVICE;
   const bool keep_nulls = prm->mode == HY_JOIN_LEFT || prm->mode == HY_JOIN_RIGHT;
   const bool use_bloom = bloom_n && (prm->mode == HY_JOIN_INNER || prm->mode == HY_JOIN_SEMI);
+  // the build side on the side stream unless the probe side needs its Bloom filter first
+  SideStream* ss = (!use_bloom && overlap_enabled()) ? side_stream() : nullptr;
+  const hipStream_t sb = ss ? ss->s : s;
+  if (ss) {
+    HY_HIP(hipEventRecord(ss->fork, s));
+    HY_HIP(hipStreamWaitEvent(sb, ss->fork, 0));
+  }
 
   hyk::Rec<H>* recs[2] = {nullptr, nullptr};
   uint32_t* bounds[2] = {nullptr, nullptr};
@@ -1136,16 +1177,19 @@ hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join
     const SidePlan& p = side == 0 ? bp : pp;
     SideBufs<H>& b = side == 0 ? bb : pb;
     const char* tag = side == 0 ? "build" : "probe";
+    const Common& cs = side == 0 ? cb : c;
+    const hipStream_t st_s = side == 0 ? sb : s;
     const hyk::NextDigit nd = next_digit(w, 0, bits, b.digA);
     hy_status st = side == 0
                        ? pass0_side<TB, H, uint32_t>(tag, p, b, bits, w.empty() ? 0 : w[0], prm->seed, false,
-                                                     p.ref_base, nd, c, s, b.recA)
+                                                     p.ref_base, nd, cs, st_s, b.recA)
                        : pass0_side<TP, H, uint32_t>(tag, p, b, bits, w.empty() ? 0 : w[0], prm->seed, keep_nulls,
-                                                     p.ref_base, nd, c, s, b.recA, use_bloom ? bloom : nullptr,
+                                                     p.ref_base, nd, cs, st_s, b.recA, use_bloom ? bloom : nullptr,
                                                      bloom_n);
     if (st != HY_OK) return st;
     st = local_passes<H, uint32_t>(tag, b, w, 1, bits, prm->seed, b.recA, b.recB, nd.bytes, b.digB, b.segA, b.segB,
-                                   w.empty() ? 1 : (1ull << w[0]), b.total, p.n_rows, c, s, &recs[side], &bounds[side]);
+                                   w.empty() ? 1 : (1ull << w[0]), b.total, p.n_rows, cs, st_s, &recs[side],
+                                   &bounds[side]);
     if (st != HY_OK) return st;
     if (side == 0 && use_bloom) {  // the probe side's prefilter over the build side's keys (its records)
       HY_HIP(hipMemsetAsync(bloom, 0, 4 * bloom_n, s));
@@ -1155,6 +1199,10 @@ hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join
       kt_.done();
       HY_HIP(hipGetLastError());
     }
+  }
+  if (ss) {  // the partition join waits for the build side
+    HY_HIP(hipEventRecord(ss->join, sb));
+    HY_HIP(hipStreamWaitEvent(s, ss->join, 0));
   }
   // filtered sides emit RowIDs of their data table (the scan's PosLists dereferenced, write_output_columns)
   const hyk::RowMap bmap = bp.fuse ? make_map(bb.ref_row_begin, bp.ref_row_begin) : make_map(bb.row_begin, bp.row_begin);
