@@ -453,9 +453,21 @@ def main():
     if traffic is not None:
         roofline["traffic"] = round(traffic)
         roofline["traffic_source"] = traffic_src
-    kernel_roofline = {"kernel": dom, "achieved": round(dk["achieved_GBps"], 1), "peak": round(peak, 1),
-                       "unit": "GB/s", "frac": round(dk["achieved_GBps"] / peak, 4),
-                       "ms_per_launch": round(dk["ms_per_launch"], 4), "bytes_per_launch": dk["bytes_per_launch"]}
+    # the contract's `roofline`: the dominant kernel among those whose bytes SURVEY 8(d) defines (join_partition =
+    # JoinHash: 4 B/build row + 4 B/probe row + 16 B/pair; scan_dict = TableScan), algorithmic bytes per launch over
+    # its average launch duration (HIP events on its stream, a timing pass outside the timed region), against the
+    # MI355X spec peak (MI355X_MICROARCH.md); traffic = its PMC bytes per launch from the committed rocprofv3 summary
+    alg_kernels = [k for k in ("join_partition", "scan_dict") if k in kernels and "achieved_GBps" in kernels[k]]
+    adom = max(alg_kernels, key=lambda k: kernels[k]["ms_total"]) if alg_kernels else dom
+    ak = kernels[adom]
+    k_traffic, k_src = committed_traffic(adom, args.sf, chunk, world) if mode == "join" else (None, None)
+    kernel_roofline = {"bound": "hbm", "kernel": adom, "achieved": round(ak["achieved_GBps"], 1),
+                       "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(ak["achieved_GBps"] / HBM_PEAK_GBPS, 4),
+                       "traffic": round(k_traffic) if k_traffic is not None else None,
+                       "traffic_source": k_src, "ms_per_launch": round(ak["ms_per_launch"], 4),
+                       "bytes_per_launch": ak["bytes_per_launch"], "peak_measured": round(peak, 1),
+                       "frac_of_measured_peak": round(ak["achieved_GBps"] / peak, 4),
+                       "peak_source": "MI355X_MICROARCH.md HBM3E spec; peak_measured: this run's stream probe"}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and mode == "join":
@@ -482,8 +494,8 @@ def main():
                        "sf_total": args.sf, "lineitem_rows": g_li, "orders_rows": g_ord, "chunk_size": chunk,
                        "scan_matches": g_probe, "join_pairs": g_pairs,
                        "parallelism": "single GPU"},
-            "roofline": roofline,
-            "kernel_roofline": kernel_roofline,
+            "roofline": kernel_roofline,
+            "roofline_e2e": roofline,
             "hbm_probe": probe,
             "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                         for k, v in kernels.items()},
@@ -496,7 +508,7 @@ def main():
                               "path": "hy_table_scan_row_ids + per-chunk counts to the host", "sf": args.sf,
                               "lineitem_rows": g_li, "chunk_size": chunk, "scan_matches": g_probe,
                               "parallelism": "single GPU"}
-            line["roofline"]["scope"] = "TableScan step (1 B/row value ids read + 8 B/match RowIDs written)"
+            line["roofline_e2e"]["scope"] = "TableScan step (1 B/row value ids read + 8 B/match RowIDs written)"
         elif mode == "join-only":  # BASELINE.json configs[2]
             line["metric"] = "rows/sec JoinHash lineitem⋈orders on l_orderkey, one MI355X"
             line["config"] = {"workload": f"JoinHash(orders ⋈ lineitem, o_orderkey=l_orderkey, radix_bits={radix_bits}) "
@@ -504,7 +516,7 @@ def main():
                               "path": "hy_join_hash (data tables on both sides)", "sf": args.sf,
                               "lineitem_rows": g_li, "orders_rows": g_ord, "chunk_size": chunk, "join_pairs": g_pairs,
                               "parallelism": "single GPU"}
-            line["roofline"]["scope"] = "JoinHash step (SURVEY 8(d): 4 B/build row + 4 B/probe row + 16 B/pair)"
+            line["roofline_e2e"]["scope"] = "JoinHash step (SURVEY 8(d): 4 B/build row + 4 B/probe row + 16 B/pair)"
         print(json.dumps(line))
 
 

@@ -25,6 +25,7 @@ columns: match and pair counts, group count and every sampled group's SUM exactl
 <= 7 float products, exact in double).
 """
 import ctypes
+import glob
 import importlib
 import json
 import os
@@ -832,6 +833,7 @@ def main_q1(args):
            "agg_dense_fused": n_match * 17}
     # agg_dense_lanes reads per matching row the 9 B of columns, plus its 8-B RowID on the PosList plan
     alg["agg_dense_lanes"] = n * 2 + n_match * 9 if fused_scan else n_match * 17
+    alg["agg_dense_vec"] = n * 2 + n_match * 9  # (data input: the fused plan only)
     e2e = sum(e2e_parts.values())
     for k, v in kernels.items():
         v["ms_per_launch"] = v["ms_total"] / max(v["launches"], 1)
@@ -847,6 +849,26 @@ def main_q1(args):
                 "dominant_kernel": dom, "dominant_ms_per_step": round(kernels[dom]["ms_total"] / K, 4),
                 "overhead_bytes_per_step": overhead,
                 "frac_incl_overhead": round((e2e + sum(overhead.values())) / step_s / 1e9 / peak, 4)}
+    # the contract's `roofline`: the dominant kernel, its SURVEY 8(d) bytes per launch over its average launch time,
+    # against the MI355X spec peak; traffic = its PMC bytes per launch from the committed rocprofv3 summary
+    kroof = None
+    if "alg_bytes_per_step" in kernels.get(dom, {}):
+        kd = kernels[dom]
+        per_launch = kd["alg_bytes_per_step"] * K / max(kd["launches"], 1)
+        ach = per_launch / (kd["ms_per_launch"] * 1e-3) / 1e9
+        traffic, src = None, None
+        here = os.path.dirname(os.path.abspath(__file__))
+        for f in reversed(sorted(glob.glob(os.path.join(here, "profiles", f"r*_rocprof_q1_sf{args.sf:g}_summary.json")))):
+            with open(f) as fh:
+                kk = json.load(fh).get("kernels", {}).get(dom, {})
+            if "hbm_bytes_per_launch" in kk and args.chunk == 100_000 and world == 1:
+                traffic, src = kk["hbm_bytes_per_launch"], os.path.relpath(f, here)
+                break
+        kroof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": 8000.0, "unit": "GB/s",
+                 "frac": round(ach / 8000.0, 4), "traffic": round(traffic) if traffic is not None else None,
+                 "traffic_source": src, "ms_per_launch": round(kd["ms_per_launch"], 4),
+                 "bytes_per_launch": per_launch, "peak_measured": round(peak, 1),
+                 "frac_of_measured_peak": round(ach / peak, 4)}
     # the reference Aggregate runs ~1e6 rows/s per core: a tenth of --cpu-sf keeps the sample near 10-30 s
     cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline_q1(hy, synth, args.cpu_sf / 10, chunk,
                                                                             host_cpu)
@@ -866,7 +888,8 @@ def main_q1(args):
                    f"chunk-sharded x{world}: per-rank scan + aggregate, all-gather of partial records, exact merge "
                    f"(hy_aggregate_merge)"},
         "check": {"ok": bool(ok), "groups": groups},
-        "roofline": roofline,
+        "roofline": kroof or roofline,
+        "roofline_e2e": roofline,
         "hbm_probe": probe,
         "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                     for k, v in kernels.items()},

@@ -1164,7 +1164,13 @@ hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join
   const bool keep_nulls = prm->mode == HY_JOIN_LEFT || prm->mode == HY_JOIN_RIGHT;
   const bool use_bloom = bloom_n && (prm->mode == HY_JOIN_INNER || prm->mode == HY_JOIN_SEMI);
   // the build side on the side stream unless the probe side needs its Bloom filter first
-  SideStream* ss = (!use_bloom && overlap_enabled()) ? side_stream() : nullptr;
+  // (not while per-kernel timing is on: concurrent kernels' event intervals would overlap and each read slower)
+  bool timing = false;
+  {
+    std::lock_guard<std::mutex> lock(g_kt_mutex);
+    timing = g_kt_enabled;
+  }
+  SideStream* ss = (!use_bloom && !timing && overlap_enabled()) ? side_stream() : nullptr;
   const hipStream_t sb = ss ? ss->s : s;
   if (ss) {
     HY_HIP(hipEventRecord(ss->fork, s));

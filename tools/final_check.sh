@@ -1,6 +1,6 @@
 set -e
-R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out; mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/fin_pytest.txt 2>&1
 timeout -k 10 200 python bench.py > $O/fin_bench.json 2> $O/fin_bench.err
 timeout -k 10 200 python bench.py --workload scan --no-cpu-baseline > $O/fin_scan.json 2>> $O/fin_bench.err
