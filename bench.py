@@ -599,7 +599,9 @@ def committed_traffic(kernel, sf, chunk, world):
     if world != 1 or chunk != 100_000:
         return None, None
     here = os.path.dirname(os.path.abspath(__file__))
-    files = sorted(glob.glob(os.path.join(here, "profiles", f"r*_rocprof_sf{sf:g}_summary.json")))
+    files = sorted(glob.glob(os.path.join(here, "profiles", f"r*_rocprof_sf{sf:g}_summary.json")) +
+                   glob.glob(os.path.join(here, "profiles", f"r*_rocprof_sf{sf:g}_fused_summary.json")),
+                   key=os.path.basename)  # newest round last
     for f in reversed(files):
         with open(f) as fh:
             k = json.load(fh).get("kernels", {}).get(ROCPROF_NAME.get(kernel, kernel), {})  # part*.build/.probe split
