@@ -254,17 +254,41 @@ class LikePattern {
   std::string _source;
 };
 
+// The id sets of one scan's LIKE / NOT LIKE dictionary chunks, uploaded together: the pattern is compiled once, every
+// chunk's bitmap is appended to one host array, and one copy (one stream sync) moves them all (instead of an
+// allocation, a copy and a sync per chunk).
+struct LikeBatch {
+  std::unique_ptr<LikePattern> matcher;
+  std::vector<uint32_t> words;
+  std::vector<std::pair<hy_scan_chunk*, size_t>> fix;  // descriptor, word offset of its id set
+  // Uploads the id sets and points the descriptors at them (the descriptors must not have moved since).
+  void finish(std::vector<std::shared_ptr<DeviceBuffer>>* keep) {
+    if (fix.empty()) return;
+    auto buf = std::make_shared<DeviceBuffer>(words.size() * 4);
+    hy_stream_t s = operator_stream();
+    hy_check(hy_memcpy_htod(buf->get(), words.data(), words.size() * 4, s), "htod");
+    hy_check(hy_stream_synchronize(s), "sync");  // `words` is pageable host memory
+    for (auto& [sc, off] : fix) sc->vid_set = buf->as<uint32_t>() + off;
+    keep->push_back(std::move(buf));
+    fix.clear();
+  }
+};
+
 // LIKE / NOT LIKE over a dictionary chunk (like_table_scan_impl.cpp:48-83, 102-120): the pattern is evaluated once per
-// dictionary entry on the host; all / none early-outs, otherwise the device scans against the set of matching ids.
-void like_predicate(const BaseDictionaryColumn& column, PredicateCondition cond, const AllTypeVariant& value,
-                    hy_scan_chunk* sc, std::vector<std::shared_ptr<DeviceBuffer>>* keep) {
+// dictionary entry on the host; all / none early-outs, otherwise the device scans against the set of matching ids
+// (appended to the scan's LikeBatch; the caller registers the descriptor's final address with it).
+size_t like_predicate(const BaseDictionaryColumn& column, PredicateCondition cond, const AllTypeVariant& value,
+                      hy_scan_chunk* sc, LikeBatch* batch) {
   const auto* dict = dynamic_cast<const DictionaryColumn<std::string>*>(&column);
   Assert(dict != nullptr, "LIKE operator only applicable on string columns.");
   Assert(!variant_is_null(value), "Right value must not be NULL.");
-  const LikePattern matcher(type_cast<std::string>(value));
+  if (!batch->matcher) batch->matcher = std::make_unique<LikePattern>(type_cast<std::string>(value));
+  const LikePattern& matcher = *batch->matcher;
   const bool invert = cond == PredicateCondition::NotLike;
   const auto& d = dict->dictionary();
-  std::vector<uint32_t> bits((d.size() + 31) / 32 + 1, 0u);
+  const size_t off = (batch->words.size() + 3) & ~size_t(3);  // 16-byte aligned id sets
+  batch->words.resize(off + (d.size() + 31) / 32 + 1, 0u);
+  uint32_t* bits = batch->words.data() + off;
   size_t count = 0;
   for (size_t v = 0; v < d.size(); ++v) {
     if (matcher(d[v]) != invert) {
@@ -272,33 +296,27 @@ void like_predicate(const BaseDictionaryColumn& column, PredicateCondition cond,
       ++count;
     }
   }
-  if (count == d.size()) {
-    sc->op = HY_OP_ALL;
-    return;
-  }
-  if (count == 0) {
-    sc->op = HY_OP_NONE;
-    return;
+  if (count == d.size() || count == 0) {
+    sc->op = count ? HY_OP_ALL : HY_OP_NONE;
+    batch->words.resize(off);
+    return SIZE_MAX;
   }
   sc->op = HY_OP_VID_SET;
-  auto buf = std::make_shared<DeviceBuffer>(bits.size() * 4);
-  hy_stream_t s = operator_stream();
-  hy_check(hy_memcpy_htod(buf->get(), bits.data(), bits.size() * 4, s), "htod");
-  hy_check(hy_stream_synchronize(s), "sync");  // `bits` is pageable host memory
-  sc->vid_set = buf->as<uint32_t>();
-  keep->push_back(std::move(buf));
+  return off;
 }
 
 // Builds the scan descriptor of one data column chunk. constant_out receives type_cast<T>(value) for value columns.
-// keep: device buffers the descriptor points to (LIKE id sets), alive until the scan has run.
+// LIKE id sets go to `batch` (*like_off: their word offset, SIZE_MAX if none): the caller registers the stored
+// descriptor with batch->fix and calls batch->finish (which keeps the device buffer alive in `keep`).
 hy_scan_chunk scan_descriptor(const BaseColumn& column, DataType type, PredicateCondition cond,
-                              const AllTypeVariant& value, std::vector<std::shared_ptr<DeviceBuffer>>* keep) {
+                              const AllTypeVariant& value, LikeBatch* batch, size_t* like_off) {
   hy_scan_chunk sc{};
+  *like_off = SIZE_MAX;
   const auto* dict = dynamic_cast<const BaseDictionaryColumn*>(&column);
   if (cond == PredicateCondition::Like || cond == PredicateCondition::NotLike) {
     Assert(type == DataType::String, "LIKE operator only applicable on string columns.");
     if (dict)
-      like_predicate(*dict, cond, value, &sc, keep);
+      *like_off = like_predicate(*dict, cond, value, &sc, batch);
     else  // LikeTableScanImpl on a value column (like_table_scan_impl.cpp:86-97): the device matches every row
       sc.op = cond == PredicateCondition::Like ? HY_OP_LIKE : HY_OP_NOT_LIKE;
   } else if (cond == PredicateCondition::IsNull || cond == PredicateCondition::IsNotNull) {
@@ -433,18 +451,25 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
     std::vector<hy_scan_chunk> descs;
     std::vector<ChunkID> chunk_ids;
     std::vector<uint32_t> sizes;
+    std::vector<size_t> like_offs;
+    LikeBatch like_sets;
     uint64_t total = 0;
     for (ChunkID c = 0; c < in_table->chunk_count(); ++c) {
       if (excluded[c]) continue;
       const auto column = in_table->get_chunk(c)->get_column(_left_column_id);
-      auto d = scan_descriptor(*column, col_type, _predicate_condition, _right_value, &keep);
+      size_t off;
+      auto d = scan_descriptor(*column, col_type, _predicate_condition, _right_value, &like_sets, &off);
       d.out_begin = total;
       total += column->size();
       descs.push_back(d);
+      like_offs.push_back(off);
       chunk_ids.push_back(c);
       sizes.push_back(static_cast<uint32_t>(column->size()));
     }
     if (descs.empty()) return output;
+    for (size_t k = 0; k < descs.size(); ++k)
+      if (like_offs[k] != SIZE_MAX) like_sets.fix.emplace_back(&descs[k], like_offs[k]);
+    like_sets.finish(&keep);
     auto rows = std::make_shared<DeviceBuffer>(std::max<uint64_t>(total, 1) * sizeof(RowID));
     DeviceBuffer counts(descs.size() * 4, s);
     std::vector<uint32_t> h_counts(descs.size());
@@ -515,9 +540,14 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
     auto& rdesc = rdescs[{rtable.get(), rcol}];
     if (rdesc.empty()) {
       rdesc.resize(rtable->chunk_count());
-      for (ChunkID r = 0; r < rtable->chunk_count(); ++r)
+      LikeBatch like_sets;
+      for (ChunkID r = 0; r < rtable->chunk_count(); ++r) {
+        size_t off;
         rdesc[r] = scan_descriptor(*rtable->get_chunk(r)->get_column(rcol), col_type, _predicate_condition,
-                                   _right_value, &keep);
+                                   _right_value, &like_sets, &off);
+        if (off != SIZE_MAX) like_sets.fix.emplace_back(&rdesc[r], off);  // (rdesc is sized: no reallocation)
+      }
+      like_sets.finish(&keep);
     }
     const auto constant = null_test || like ? ScanConstant{} : typed_constant(col_type, _right_value);
     const auto dpl = device_pos_list(pos_list);
