@@ -36,6 +36,44 @@ TempCache& temp_cache() {
 }
 }  // namespace
 
+namespace {
+constexpr size_t SLAB_POOL_BYTES = size_t(1) << 30;
+struct SlabPool {
+  std::mutex m;
+  std::vector<void*> free_blocks;
+};
+SlabPool& slab_pool() {
+  static SlabPool* p = new SlabPool;  // (never destroyed: arenas may be released during static destruction)
+  return *p;
+}
+}  // namespace
+
+void* slab_block_acquire() {
+  auto& p = slab_pool();
+  {
+    std::lock_guard<std::mutex> lock(p.m);
+    if (!p.free_blocks.empty()) {
+      void* b = p.free_blocks.back();
+      p.free_blocks.pop_back();
+      return b;
+    }
+  }
+  void* b = ::operator new(SLAB_BLOCK_BYTES, std::align_val_t(64));
+  return b;
+}
+
+void slab_block_release(void* block) {
+  auto& p = slab_pool();
+  {
+    std::lock_guard<std::mutex> lock(p.m);
+    if (p.free_blocks.size() * SLAB_BLOCK_BYTES < SLAB_POOL_BYTES) {
+      p.free_blocks.push_back(block);
+      return;
+    }
+  }
+  ::operator delete(block, std::align_val_t(64));
+}
+
 void* temp_block_acquire(size_t bytes, size_t* block_bytes) {
   size_t b = 4096;
   while (b < bytes) b <<= 1;
@@ -296,16 +334,16 @@ std::shared_ptr<PosList> pos_list_from_device(std::shared_ptr<DeviceBuffer> rows
 }
 
 std::shared_ptr<PosList> pos_list_from_device(OutputArena& arena, std::shared_ptr<DeviceBuffer> rows, uint64_t offset,
-                                              uint64_t n) {
-  arena.lists->emplace_back();
-  PosList& pl = arena.lists->back();
-  pl.make_lazy(n, &fetch_pos_list);
-  arena.mirrors->emplace_back();
-  DevicePosList& d = arena.mirrors->back();
+                                              uint64_t n, DevicePosList** mirror) {
+  DevicePosList& d = arena.mirrors->emplace_back();
   d.size = n;
   d.rows = std::move(rows);
   d.view_offset = offset;
-  pl.set_device_mirror(std::shared_ptr<DevicePosList>(arena.mirrors, &d));
+  if (mirror) *mirror = &d;
+  PosList& pl = arena.lists->emplace_back();
+  // (not through set_device_mirror: libstdc++'s atomic shared_ptr store takes a mutex from a global pool, which
+  // serialised the output builder threads)
+  pl.make_lazy(n, &fetch_pos_list, std::shared_ptr<DevicePosList>(arena.mirrors, &d));
   return std::shared_ptr<PosList>(arena.lists, &pl);
 }
 

@@ -8,6 +8,7 @@
 
 #include <atomic>
 #include <deque>
+#include <new>
 #include <mutex>
 #include <memory>
 #include <string>
@@ -55,6 +56,14 @@ class DeviceBuffer {
     return static_cast<T*>(_ptr);
   }
   size_t bytes() const { return _bytes; }
+  // exchanges the allocations (views that hold this object see the new one: an output's RowIDs sized after the
+  // PosLists over them were created)
+  void swap(DeviceBuffer& o) {
+    std::swap(_ptr, o._ptr);
+    std::swap(_bytes, o._bytes);
+    std::swap(_block, o._block);
+    std::swap(_temp, o._temp);
+  }
 
  private:
   void* _ptr = nullptr;
@@ -102,23 +111,58 @@ hy_column_chunk device_scan_chunk(const BaseColumn& column);
 // the shared_ptrs handed out alias an arena's control block (no allocation, no control block per object). The arenas
 // own each other in one direction only - chunks -> columns -> PosLists -> mirrors - so the last chunk released frees
 // them all.
-struct OutputArena {
-  std::shared_ptr<std::deque<DevicePosList>> mirrors = std::make_shared<std::deque<DevicePosList>>();
-  std::shared_ptr<std::deque<PosList>> lists = std::make_shared<std::deque<PosList>>();
-  std::shared_ptr<std::deque<ReferenceColumn>> columns = std::make_shared<std::deque<ReferenceColumn>>();
-  std::shared_ptr<std::deque<Chunk>> chunks = std::make_shared<std::deque<Chunk>>();
+//
+// The arenas' memory comes in 1 MiB host blocks that are recycled process-wide (up to SLAB_POOL_BYTES): an operator
+// that emits 65,536 chunks per execution would otherwise free its pages to the OS and fault them in again on the next
+// execution, and page faults from several builder threads serialise in the kernel.
+void* slab_block_acquire();
+void slab_block_release(void* block);
+constexpr size_t SLAB_BLOCK_BYTES = size_t(1) << 20;
+
+// Append-only sequence of T in recycled blocks (elements never move; destroyed in order with the slab).
+template <typename T>
+class Slab {
+ public:
+  static constexpr size_t PER_BLOCK = SLAB_BLOCK_BYTES / sizeof(T);
+  static_assert(PER_BLOCK >= 64 && alignof(T) <= 16, "slab element too large");
+  Slab() = default;
+  Slab(const Slab&) = delete;
+  Slab& operator=(const Slab&) = delete;
+  ~Slab() {
+    for (size_t i = 0; i < _n; ++i) at(i).~T();
+    for (void* b : _blocks) slab_block_release(b);
+  }
+  template <typename... A>
+  T& emplace_back(A&&... a) {
+    if (_n == _blocks.size() * PER_BLOCK) _blocks.push_back(slab_block_acquire());
+    T* p = new (static_cast<T*>(_blocks.back()) + _n % PER_BLOCK) T(std::forward<A>(a)...);
+    ++_n;
+    return *p;
+  }
+
+ private:
+  T& at(size_t i) { return static_cast<T*>(_blocks[i / PER_BLOCK])[i % PER_BLOCK]; }
+  std::vector<void*> _blocks;
+  size_t _n = 0;
 };
-// A lazy PosList in the arena over rows [offset, offset + n) of a device RowID array.
+
+struct OutputArena {
+  std::shared_ptr<Slab<DevicePosList>> mirrors = std::make_shared<Slab<DevicePosList>>();
+  std::shared_ptr<Slab<PosList>> lists = std::make_shared<Slab<PosList>>();
+  std::shared_ptr<Slab<ReferenceColumn>> columns = std::make_shared<Slab<ReferenceColumn>>();
+  std::shared_ptr<Slab<Chunk>> chunks = std::make_shared<Slab<Chunk>>();
+};
+// A lazy PosList in the arena over rows [offset, offset + n) of a device RowID array; *mirror (if given) receives its
+// device mirror, whose view the producer may still move (with PosList::set_lazy_size) before publishing the list.
 std::shared_ptr<PosList> pos_list_from_device(OutputArena& arena, std::shared_ptr<DeviceBuffer> rows, uint64_t offset,
-                                              uint64_t n);
+                                              uint64_t n, DevicePosList** mirror = nullptr);
 inline std::shared_ptr<ReferenceColumn> arena_reference_column(OutputArena& arena, std::shared_ptr<const Table> table,
                                                                ColumnID column, std::shared_ptr<const PosList> pos_list) {
-  arena.columns->emplace_back(std::move(table), column, std::move(pos_list));
-  return std::shared_ptr<ReferenceColumn>(arena.columns, &arena.columns->back());
+  return std::shared_ptr<ReferenceColumn>(arena.columns,
+                                         &arena.columns->emplace_back(std::move(table), column, std::move(pos_list)));
 }
 inline std::shared_ptr<Chunk> arena_chunk(OutputArena& arena, ChunkColumns columns) {
-  arena.chunks->emplace_back(std::move(columns));
-  return std::shared_ptr<Chunk>(arena.chunks, &arena.chunks->back());
+  return std::shared_ptr<Chunk>(arena.chunks, &arena.chunks->emplace_back(std::move(columns)));
 }
 
 // Returns (uploading on first use) the device mirror of a PosList.

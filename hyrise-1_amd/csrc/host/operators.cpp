@@ -1049,10 +1049,11 @@ int32_t join_mode(JoinMode m) {
   return HY_JOIN_INNER;
 }
 
-// write_output_columns (join_hash.cpp:564-613), prepared once per side: which table / column every output column
-// references, and which device RowID array its PosList views - the join's output RowIDs (data tables, the fused
-// dereference, an input without chunks), or that side's RowIDs dereferenced through one PosList group (reference
-// inputs; computed once for all partitions by a single launch). Columns of one group share one PosList per chunk.
+// write_output_columns (join_hash.cpp:564-613), prepared once per side before the join runs: which table / column
+// every output column references, and which device RowID array its PosList views - the join's output RowIDs (data
+// tables, the fused dereference, an input without chunks), or that side's RowIDs dereferenced through one PosList
+// group (reference inputs; computed for all partitions by a single launch once the join has run). Columns of one
+// group share one PosList per chunk.
 struct OutCol {
   const Table* table;
   ColumnID column;
@@ -1060,8 +1061,10 @@ struct OutCol {
 };
 struct SideOut {
   std::vector<OutCol> cols;
-  const DeviceBuffer* rows = nullptr;       // data-like side
-  std::vector<const DeviceBuffer*> deref;   // per group: dereferenced rows
+  const DeviceBuffer* rows = nullptr;                  // data-like side
+  std::vector<std::shared_ptr<DeviceBuffer>> deref;   // per group: dereferenced rows (allocated after the join)
+  std::vector<std::shared_ptr<DeviceBuffer>> ptr_arrays;  // per group: the group's device PosList pointers
+  int n_lists = 0;                                     // distinct PosLists per output chunk
 };
 
 // What one builder thread's output objects hold: aliasing pointers into this object's control block instead of
@@ -1072,8 +1075,7 @@ struct OutRefs {
 };
 
 SideOut describe_output(const std::shared_ptr<const Table>& input_table, const JoinSideInput& side,
-                        const std::shared_ptr<DeviceBuffer>& rows, uint64_t rows_used, OutRefs& refs,
-                        std::shared_ptr<Table>& dummy_table) {
+                        const std::shared_ptr<DeviceBuffer>& rows, OutRefs& refs, std::shared_ptr<Table>& dummy_table) {
   SideOut o;
   refs.buffers.push_back(rows);
   if (input_table->type() == TableType::Data || input_table->chunk_count() == 0) {
@@ -1085,10 +1087,16 @@ SideOut describe_output(const std::shared_ptr<const Table>& input_table, const J
     refs.tables.push_back(t);
     o.rows = rows.get();
     for (ColumnID col = 0; col < input_table->column_count(); ++col) o.cols.push_back(OutCol{t.get(), col, -1});
+    o.n_lists = 1;
     return o;
   }
-  if (side.fuse) o.rows = rows.get();
-  else o.deref.assign(side.groups.size(), nullptr);
+  if (side.fuse) {
+    o.rows = rows.get();
+    o.n_lists = 1;
+  } else {
+    o.deref.assign(side.groups.size(), nullptr);
+    o.ptr_arrays.assign(side.groups.size(), nullptr);
+  }
   hy_stream_t s = operator_stream();
   for (ColumnID col = 0; col < input_table->column_count(); ++col) {
     const auto rc = std::static_pointer_cast<const ReferenceColumn>(input_table->get_chunk(0)->get_column(col));
@@ -1101,26 +1109,36 @@ SideOut describe_output(const std::shared_ptr<const Table>& input_table, const J
     auto ptr_array = std::make_shared<DeviceBuffer>(ptrs.size() * sizeof(void*));
     hy_check(hy_memcpy_htod(ptr_array->get(), ptrs.data(), ptrs.size() * sizeof(void*), s), "htod");
     hy_check(hy_stream_synchronize(s), "sync");  // `ptrs` is pageable host memory
-    auto d = std::make_shared<DeviceBuffer>(std::max<uint64_t>(rows_used, 1) * sizeof(RowID));
-    hy_check(hy_dereference_row_ids(rows->as<hy_row_id>(), rows_used, ptr_array->as<const hy_row_id* const>(),
-                                    d->as<hy_row_id>(), s),
-             "hy_dereference_row_ids");
-    refs.buffers.push_back(ptr_array);  // (freed with the outputs: the launch above may still read it)
-    refs.buffers.push_back(d);
-    o.deref[g] = d.get();
+    o.ptr_arrays[g] = ptr_array;
+    o.deref[g] = std::make_shared<DeviceBuffer>();  // (sized once the join's output range is known)
+    refs.buffers.push_back(ptr_array);  // (freed with the outputs: the dereference launch may still read it)
+    refs.buffers.push_back(o.deref[g]);
+    ++o.n_lists;
   }
   return o;
 }
 
-// The columns of one output chunk (rows [offset, offset + n) of every side's RowIDs) from a builder's arena.
+// The dereferenced rows of a side's PosList groups, once the join has written `used` RowIDs.
+void dereference_groups(SideOut& o, const DeviceBuffer& rows, uint64_t used) {
+  hy_stream_t s = operator_stream();
+  for (size_t g = 0; g < o.deref.size(); ++g) {
+    if (!o.deref[g]) continue;
+    DeviceBuffer d(std::max<uint64_t>(used, 1) * sizeof(RowID));
+    o.deref[g]->swap(d);
+    hy_check(hy_dereference_row_ids(rows.as<hy_row_id>(), used, o.ptr_arrays[g]->as<const hy_row_id* const>(),
+                                    o.deref[g]->as<hy_row_id>(), s),
+             "hy_dereference_row_ids");
+  }
+}
+
+// The columns of one output chunk from a builder's arena, with empty PosLists whose views are set once the join's
+// partition ranges are known; the chunk's distinct PosLists and mirrors go to lists / mirrors (side.n_lists each).
 void write_chunk_columns(ChunkColumns& out, OutputArena& arena, const std::shared_ptr<OutRefs>& refs,
-                         const SideOut& side, uint64_t offset, uint64_t n) {
-  auto view = [&](const DeviceBuffer* b) {
-    return pos_list_from_device(arena, std::shared_ptr<DeviceBuffer>(refs, const_cast<DeviceBuffer*>(b)), offset, n);
-  };
+                         const SideOut& side, PosList** lists, DevicePosList** mirrors) {
   std::shared_ptr<PosList> own;
   std::shared_ptr<PosList> grp[8];
   std::vector<std::shared_ptr<PosList>> more;  // (more than 8 PosList groups: rare)
+  int k = 0;
   for (const auto& c : side.cols) {
     std::shared_ptr<PosList>* slot;
     if (c.group < 0) {
@@ -1131,7 +1149,12 @@ void write_chunk_columns(ChunkColumns& out, OutputArena& arena, const std::share
       if (more.size() <= static_cast<size_t>(c.group)) more.resize(c.group + 1);
       slot = &more[c.group];
     }
-    if (!*slot) *slot = view(c.group < 0 ? side.rows : side.deref[c.group]);
+    if (!*slot) {
+      const DeviceBuffer* b = c.group < 0 ? side.rows : side.deref[c.group].get();
+      *slot = pos_list_from_device(arena, std::shared_ptr<DeviceBuffer>(refs, const_cast<DeviceBuffer*>(b)), 0, 0,
+                                   &mirrors[k]);
+      lists[k++] = slot->get();
+    }
     out.push_back(arena_reference_column(arena, std::shared_ptr<const Table>(refs, c.table), c.column, *slot));
   }
 }
@@ -1196,15 +1219,71 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
   const uint32_t n_parts = 1u << prm.radix_bits;
   DeviceBuffer part_begin(8 * n_parts, s), part_count(4 * n_parts, s);
   uint64_t capacity = std::max<uint64_t>(probe_table->row_count() + build_table->row_count(), 16);
-  std::shared_ptr<DeviceBuffer> out_b, out_p;
+  auto out_b = std::make_shared<DeviceBuffer>(capacity * sizeof(RowID));
+  auto out_p = std::make_shared<DeviceBuffer>(capacity * sizeof(RowID));
+
+  // One output chunk per non-empty partition (join_hash.cpp:829-855), in partition order. The chunks of all
+  // partitions are built while the device runs the join - their columns and PosLists depend only on the inputs -
+  // and their PosLists' views are set from the partition ranges afterwards; empty partitions' chunks are dropped.
+  // Chunks, columns, PosLists and mirrors come from output arenas (device.hpp), and every pointer a builder hands
+  // out aliases its own OutRefs: several threads build without contending on shared reference counts (65,536
+  // chunks at SF100).
+  OutRefs base_refs;
+  std::shared_ptr<Table> dummy, pdummy;
+  const bool with_build = !(semi_anti && inputs_swapped);
+  SideOut bo = with_build ? describe_output(build_table, bside, out_b, base_refs, dummy) : SideOut{};
+  SideOut po = describe_output(probe_table, pside, out_p, base_refs, pdummy);
+  const int n_lists = bo.n_lists + po.n_lists;
+  std::vector<std::shared_ptr<Chunk>> chunks(n_parts);
+  std::vector<PosList*> lists(static_cast<size_t>(n_parts) * n_lists);
+  std::vector<DevicePosList*> mirrors(lists.size());
+  static const size_t max_workers = [] {  // HY_OP_THREADS caps the builder threads (A/B)
+    const char* e = std::getenv("HY_OP_THREADS");
+    return e ? std::max(1L, std::strtol(e, nullptr, 10)) : 16L;
+  }();
+  const unsigned workers = static_cast<unsigned>(
+      std::max<size_t>(1, std::min<size_t>({max_workers, std::thread::hardware_concurrency(), n_parts / 2048})));
+  std::atomic<size_t> next{0};
+  auto build = [&]() {
+    OutputArena arena;
+    auto refs = std::make_shared<OutRefs>(base_refs);
+    constexpr size_t BATCH = 256;
+    for (size_t i0; (i0 = next.fetch_add(BATCH)) < n_parts;) {
+      for (size_t i = i0; i < std::min<size_t>(n_parts, i0 + BATCH); ++i) {
+        ChunkColumns cols;
+        cols.reserve(output->column_count());
+        PosList** l = &lists[i * n_lists];
+        DevicePosList** m = &mirrors[i * n_lists];
+        if (inputs_swapped) {
+          write_chunk_columns(cols, arena, refs, po, l, m);
+          if (with_build) write_chunk_columns(cols, arena, refs, bo, l + po.n_lists, m + po.n_lists);
+        } else {
+          write_chunk_columns(cols, arena, refs, bo, l, m);
+          write_chunk_columns(cols, arena, refs, po, l + bo.n_lists, m + bo.n_lists);
+        }
+        chunks[i] = arena_chunk(arena, std::move(cols));
+      }
+    }
+  };
+  std::vector<std::thread> pool;  // (the builders touch no device state)
+  for (unsigned t = 1; t < workers; ++t) pool.emplace_back(build);
+  struct Joiner {  // the builders finish before anything they read goes away, also when the join throws
+    std::vector<std::thread>& pool;
+    ~Joiner() {
+      for (auto& t : pool)
+        if (t.joinable()) t.join();
+    }
+  } joiner{pool};
+
   hy_join_result res{};
   for (int attempt = 0; attempt < 2; ++attempt) {
-    out_b = std::make_shared<DeviceBuffer>(capacity * sizeof(RowID));
-    out_p = std::make_shared<DeviceBuffer>(capacity * sizeof(RowID));
     const hy_status st = hy_join_hash(&b, &p, &prm, out_b->as<hy_row_id>(), out_p->as<hy_row_id>(), capacity,
                                       part_begin.as<uint64_t>(), part_count.as<uint32_t>(), &res, ws.get(), ws_bytes, s);
     if (st == HY_ERR_CAPACITY && attempt == 0) {
       capacity = std::max<uint64_t>(res.capacity_required, 16);
+      DeviceBuffer nb(capacity * sizeof(RowID)), np(capacity * sizeof(RowID));
+      out_b->swap(nb);  // (the PosLists built so far view these objects, not their allocations)
+      out_p->swap(np);
       continue;
     }
     hy_check(st, "hy_join_hash");
@@ -1218,55 +1297,26 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
   tr.mark("join kernels + partition counts");
 
   uint64_t used = 0;  // the output range the partitions occupy
-  std::vector<uint32_t> nonempty;  // join_hash.cpp:835-837: no chunk for an empty partition
-  for (uint32_t part = 0; part < n_parts; ++part) {
-    if (!h_count[part]) continue;
-    used = std::max<uint64_t>(used, h_begin[part] + h_count[part]);
-    nonempty.push_back(part);
-  }
-  // One output chunk per non-empty partition (join_hash.cpp:829-855), in partition order. Chunks, columns, PosLists
-  // and mirrors come from output arenas (device.hpp), and every pointer a builder hands out aliases its own OutRefs:
-  // the chunks are built by several threads without contending on shared reference counts (65,536 chunks at SF100).
-  OutRefs base_refs;
-  std::shared_ptr<Table> dummy;
-  const SideOut bo = semi_anti && inputs_swapped ? SideOut{} : describe_output(build_table, bside, out_b, used, base_refs, dummy);
-  std::shared_ptr<Table> pdummy;
-  const SideOut po = describe_output(probe_table, pside, out_p, used, base_refs, pdummy);
-  std::vector<std::shared_ptr<Chunk>> chunks(nonempty.size());
-  const size_t n_chunks = nonempty.size();
-  static const size_t max_workers = [] {  // HY_OP_THREADS caps the builder threads (A/B)
-    const char* e = std::getenv("HY_OP_THREADS");
-    return e ? std::max(1L, std::strtol(e, nullptr, 10)) : 16L;
-  }();
-  const unsigned workers = static_cast<unsigned>(
-      std::max<size_t>(1, std::min<size_t>({max_workers, std::thread::hardware_concurrency(), n_chunks / 2048})));
-  std::atomic<size_t> next{0};
-  auto build = [&]() {
-    OutputArena arena;
-    auto refs = std::make_shared<OutRefs>(base_refs);
-    constexpr size_t BATCH = 256;
-    for (size_t i0; (i0 = next.fetch_add(BATCH)) < n_chunks;) {
-      for (size_t i = i0; i < std::min(n_chunks, i0 + BATCH); ++i) {
-        const uint32_t part = nonempty[i];
-        ChunkColumns cols;
-        cols.reserve(output->column_count());
-        const uint64_t n = h_count[part], b0 = h_begin[part];
-        if (inputs_swapped) {
-          write_chunk_columns(cols, arena, refs, po, b0, n);
-          if (!semi_anti) write_chunk_columns(cols, arena, refs, bo, b0, n);
-        } else {
-          write_chunk_columns(cols, arena, refs, bo, b0, n);
-          write_chunk_columns(cols, arena, refs, po, b0, n);
-        }
-        chunks[i] = arena_chunk(arena, std::move(cols));
-      }
-    }
-  };
-  std::vector<std::thread> pool;
-  for (unsigned t = 1; t < workers; ++t) pool.emplace_back(build);
-  build();
+  for (uint32_t part = 0; part < n_parts; ++part)
+    if (h_count[part]) used = std::max<uint64_t>(used, h_begin[part] + h_count[part]);
+  if (with_build) dereference_groups(bo, *out_b, used);
+  dereference_groups(po, *out_p, used);
+  build();  // (this thread joins the builders)
   for (auto& t : pool) t.join();
-  output->append_chunks(std::move(chunks));
+  std::vector<std::shared_ptr<Chunk>> nonempty;  // join_hash.cpp:835-837: no chunk for an empty partition
+  nonempty.reserve(n_parts);
+  for (uint32_t part = 0; part < n_parts; ++part) {
+    const uint32_t n = h_count[part];
+    if (!n) continue;
+    for (int k = 0; k < n_lists; ++k) {
+      const size_t i = static_cast<size_t>(part) * n_lists + k;
+      lists[i]->set_lazy_size(n);
+      mirrors[i]->size = n;
+      mirrors[i]->view_offset = h_begin[part];
+    }
+    nonempty.push_back(std::move(chunks[part]));
+  }
+  output->append_chunks(std::move(nonempty));
   tr.mark("output chunks");
   return output;
 }

@@ -122,11 +122,18 @@ class PosList {
   }
   bool is_lazy() const { return _lazy; }
   // makes an empty list lazy in place (lists allocated in an operator's output arena)
-  void make_lazy(size_t n, PosListFetch fetch) {
+  // with its device mirror (a plain store: the list is not shared with any other thread yet)
+  void make_lazy(size_t n, PosListFetch fetch, std::shared_ptr<DevicePosList> mirror) {
     _v.clear();
     _lazy_size = n;
     _lazy = n > 0;
     _fetch = fetch;
+    _device = std::move(mirror);
+  }
+  // the size of a lazy list that is not shared yet (its producer learns the sizes after creating the lists)
+  void set_lazy_size(size_t n) {
+    _lazy_size = n;
+    _lazy = n > 0;
   }
 
   // sizes need no host copy
