@@ -107,7 +107,7 @@ std::shared_ptr<DeviceColumn> device_column(const BaseColumn& column);
 hy_column_chunk device_scan_chunk(const BaseColumn& column);
 
 // Output objects of an operator that emits many chunks (JoinHash: one per radix partition, 65,536 at SF100): the
-// chunks, their columns, PosLists and the PosLists' device mirrors live in four arenas (deques: elements never move);
+// chunks, their columns, PosLists and the PosLists' device mirrors live in four arenas (slabs: elements never move);
 // the shared_ptrs handed out alias an arena's control block (no allocation, no control block per object). The arenas
 // own each other in one direction only - chunks -> columns -> PosLists -> mirrors - so the last chunk released frees
 // them all.

@@ -6,7 +6,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
 #include <map>
+#include <mutex>
 #include <numeric>
 #include <regex>
 #include <thread>
@@ -510,16 +512,21 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
       for (size_t k = 0; k < descs.size(); ++k) views.emplace_back(descs[k].out_begin, h_counts[k]);
     }
     tr.mark("descriptors + scan + sync");
-    // output PosLists are lazy views of `rows` (no copy to the host, no wait: later work is ordered on the stream)
+    // output PosLists are lazy views of `rows` (no copy to the host, no wait: later work is ordered on the stream);
+    // chunks, columns and PosLists from an output arena (device.hpp)
+    OutputArena arena;
+    std::vector<std::shared_ptr<Chunk>> out_chunks;
     for (size_t k = 0; k < descs.size(); ++k) {
       if (views[k].second == 0) continue;  // reference table_scan.cpp:99: no empty output chunks
-      auto pl = pos_list_from_device(rows, views[k].first, views[k].second);
+      auto pl = pos_list_from_device(arena, rows, views[k].first, views[k].second);
       pl->set_single_chunk_id(chunk_ids[k]);
       ChunkColumns cols;
+      cols.reserve(in_table->column_count());
       for (ColumnID col = 0; col < in_table->column_count(); ++col)
-        cols.push_back(std::make_shared<ReferenceColumn>(in_table, col, pl));
-      output->append_chunk(cols);
+        cols.push_back(arena_reference_column(arena, in_table, col, pl));
+      out_chunks.push_back(arena_chunk(arena, std::move(cols)));
     }
+    output->append_chunks(std::move(out_chunks));
     tr.mark("output chunks");
     return output;
   }
@@ -1244,7 +1251,19 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
   const unsigned workers = static_cast<unsigned>(
       std::max<size_t>(1, std::min<size_t>({max_workers, std::thread::hardware_concurrency(), n_parts / 2048})));
   std::atomic<size_t> next{0};
+  const auto spawn = std::chrono::steady_clock::now();
+  std::atomic<int64_t> last_done_us{0};  // (HY_OP_TRACE: when the builders finished)
   auto build = [&]() {
+    struct Done {
+      std::atomic<int64_t>& last;
+      std::chrono::steady_clock::time_point t0;
+      ~Done() {
+        const int64_t us = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0)
+                               .count();
+        for (int64_t cur = last.load(); cur < us && !last.compare_exchange_weak(cur, us);) {
+        }
+      }
+    } done{last_done_us, spawn};
     OutputArena arena;
     auto refs = std::make_shared<OutRefs>(base_refs);
     constexpr size_t BATCH = 256;
@@ -1265,15 +1284,56 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
       }
     }
   };
+  // once the partition ranges are known and every chunk is built, the same threads set the PosLists' views
+  std::vector<uint64_t> h_begin(n_parts);
+  std::vector<uint32_t> h_count(n_parts);
+  std::mutex phase_m;
+  std::condition_variable phase_cv;
+  int ranges = 0;      // 1: h_begin / h_count hold the ranges; -1: the join failed
+  unsigned built = 0;  // threads done building
+  std::atomic<size_t> next_view{0};
+  auto set_views = [&]() {
+    constexpr size_t BATCH = 2048;
+    for (size_t i0; (i0 = next_view.fetch_add(BATCH)) < n_parts;) {
+      for (size_t part = i0; part < std::min<size_t>(n_parts, i0 + BATCH); ++part) {
+        const uint32_t n = h_count[part];
+        if (!n) continue;
+        for (int k = 0; k < n_lists; ++k) {
+          const size_t i = part * n_lists + k;
+          lists[i]->set_lazy_size(n);
+          mirrors[i]->size = n;
+          mirrors[i]->view_offset = h_begin[part];
+        }
+      }
+    }
+  };
+  auto build_then_set_views = [&]() {
+    build();
+    std::unique_lock<std::mutex> lock(phase_m);
+    ++built;
+    phase_cv.notify_all();
+    phase_cv.wait(lock, [&] { return ranges < 0 || (ranges > 0 && built == workers); });
+    if (ranges < 0) return;
+    lock.unlock();
+    set_views();
+  };
   std::vector<std::thread> pool;  // (the builders touch no device state)
-  for (unsigned t = 1; t < workers; ++t) pool.emplace_back(build);
+  for (unsigned t = 1; t < workers; ++t) pool.emplace_back(build_then_set_views);
   struct Joiner {  // the builders finish before anything they read goes away, also when the join throws
     std::vector<std::thread>& pool;
+    std::mutex& m;
+    std::condition_variable& cv;
+    int& ranges;
     ~Joiner() {
+      {
+        std::lock_guard<std::mutex> lock(m);
+        ranges = -1;  // (also after the ranges: this thread may have thrown before it built its share)
+        cv.notify_all();
+      }
       for (auto& t : pool)
         if (t.joinable()) t.join();
     }
-  } joiner{pool};
+  } joiner{pool, phase_m, phase_cv, ranges};
 
   hy_join_result res{};
   for (int attempt = 0; attempt < 2; ++attempt) {
@@ -1289,8 +1349,6 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
     hy_check(st, "hy_join_hash");
     break;
   }
-  std::vector<uint64_t> h_begin(n_parts);
-  std::vector<uint32_t> h_count(n_parts);
   hy_check(hy_memcpy_dtoh(h_begin.data(), part_begin.get(), 8 * n_parts, s), "dtoh");
   hy_check(hy_memcpy_dtoh(h_count.data(), part_count.get(), 4 * n_parts, s), "dtoh");
   hy_check(hy_stream_synchronize(s), "sync");
@@ -1299,23 +1357,23 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
   uint64_t used = 0;  // the output range the partitions occupy
   for (uint32_t part = 0; part < n_parts; ++part)
     if (h_count[part]) used = std::max<uint64_t>(used, h_begin[part] + h_count[part]);
+  {
+    std::lock_guard<std::mutex> lock(phase_m);
+    ranges = 1;
+    phase_cv.notify_all();
+  }
   if (with_build) dereference_groups(bo, *out_b, used);
   dereference_groups(po, *out_p, used);
-  build();  // (this thread joins the builders)
+  build_then_set_views();  // (this thread joins the builders)
   for (auto& t : pool) t.join();
+  if (tr.on)
+    std::fprintf(stderr, "[op] JoinHash %u builders finished %.3f ms after they started\n", workers,
+                 last_done_us.load() / 1000.0);
+  tr.mark("output chunks built, views set");
   std::vector<std::shared_ptr<Chunk>> nonempty;  // join_hash.cpp:835-837: no chunk for an empty partition
   nonempty.reserve(n_parts);
-  for (uint32_t part = 0; part < n_parts; ++part) {
-    const uint32_t n = h_count[part];
-    if (!n) continue;
-    for (int k = 0; k < n_lists; ++k) {
-      const size_t i = static_cast<size_t>(part) * n_lists + k;
-      lists[i]->set_lazy_size(n);
-      mirrors[i]->size = n;
-      mirrors[i]->view_offset = h_begin[part];
-    }
-    nonempty.push_back(std::move(chunks[part]));
-  }
+  for (uint32_t part = 0; part < n_parts; ++part)
+    if (h_count[part]) nonempty.push_back(std::move(chunks[part]));
   output->append_chunks(std::move(nonempty));
   tr.mark("output chunks");
   return output;

@@ -78,7 +78,11 @@ void Table::append_chunk(const ChunkColumns& columns) {
   _chunks.push_back(std::make_shared<Chunk>(columns));
 }
 
+// The bulk form operators use for outputs they built consistent by construction (a JoinHash's 65,536 chunks at
+// SF100): the per-column checks are debug-only here, as the reference's DebugAssert, because walking every chunk's
+// columns and PosLists right after other threads built them costs several milliseconds of cache misses.
 void Table::append_chunks(std::vector<std::shared_ptr<Chunk>>&& chunks) {
+#ifdef HYRISE_DEBUG  // (reference: DebugAssert, active in HYRISE_DEBUG builds)
   for (const auto& ch : chunks) {
     Assert(ch->column_count() == _defs.size(), "append_chunk: wrong number of columns");
     for (const auto& c : ch->columns()) {
@@ -86,6 +90,7 @@ void Table::append_chunks(std::vector<std::shared_ptr<Chunk>>&& chunks) {
       Assert(c->is_reference() == (_type == TableType::References), "Invalid column type");
     }
   }
+#endif
   if (_chunks.empty()) {
     _chunks = std::move(chunks);
   } else {
