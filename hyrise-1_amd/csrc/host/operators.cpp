@@ -905,12 +905,16 @@ JoinSideInput describe_side(const std::shared_ptr<const Table>& table, ColumnID 
   };
   JoinSideInput in;
   const bool is_ref = table->type() == TableType::References;
+  const auto& chunks = table->chunks();
+  const auto ref_column = [&](ChunkID c, ColumnID col) -> const ReferenceColumn& {
+    return static_cast<const ReferenceColumn&>(*chunks[c]->columns()[col]);
+  };
   if (is_ref) {
     std::map<PosListsVec, int> ids;
     for (ColumnID col = 0; col < table->column_count(); ++col) {
       PosListsVec v;
-      for (ChunkID c = 0; c < table->chunk_count(); ++c)
-        v.push_back(std::static_pointer_cast<const ReferenceColumn>(table->get_chunk(c)->get_column(col))->pos_list());
+      v.reserve(chunks.size());
+      for (ChunkID c = 0; c < chunks.size(); ++c) v.push_back(ref_column(c, col).pos_list());
       auto it = ids.find(v);
       if (it == ids.end()) {
         it = ids.emplace(v, static_cast<int>(in.groups.size())).first;
@@ -920,40 +924,41 @@ JoinSideInput describe_side(const std::shared_ptr<const Table>& table, ColumnID 
     }
     in.join_group = in.column_group.at(column_id);
   }
-  std::shared_ptr<const Table> referenced;
+  const Table* referenced = nullptr;
   ColumnID rcol = 0;
-  for (ChunkID c = 0; c < table->chunk_count(); ++c) {
-    const auto column = table->get_chunk(c)->get_column(column_id);
+  in.chunks.reserve(chunks.size());
+  for (ChunkID c = 0; c < chunks.size(); ++c) {
+    const BaseColumn& column = *chunks[c]->columns().at(column_id);
     hy_join_chunk jc{};
     jc.chunk_id = c;
     jc.single_chunk = HY_MIXED_CHUNKS;
-    jc.size = static_cast<uint32_t>(column->size());
+    jc.size = static_cast<uint32_t>(column.size());
     if (is_ref) {
-      const auto rc = std::static_pointer_cast<const ReferenceColumn>(column);
+      const auto& rc = static_cast<const ReferenceColumn&>(column);
       if (!referenced) {
-        referenced = rc->referenced_table();
-        rcol = rc->referenced_column_id();
+        referenced = rc.referenced_table().get();
+        rcol = rc.referenced_column_id();
       }
-      Assert(rc->referenced_table() == referenced && rc->referenced_column_id() == rcol,
+      Assert(rc.referenced_table().get() == referenced && rc.referenced_column_id() == rcol,
              "hyrise-amd: a join column referencing several tables is not supported");
-      jc.pos_list = device_pos_list(*rc->pos_list())->ptr();
-      if (rc->pos_list()->single_chunk_id() != INVALID_CHUNK_ID) jc.single_chunk = rc->pos_list()->single_chunk_id();
+      const PosList& pl = *rc.pos_list();
+      jc.pos_list = device_pos_list(pl)->ptr();
+      if (pl.single_chunk_id() != INVALID_CHUNK_ID) jc.single_chunk = pl.single_chunk_id();
     } else {
-      jc.column = chunk_desc(*column);
+      jc.column = chunk_desc(column);
     }
     in.chunks.push_back(jc);
   }
   if (referenced) {
-    for (ChunkID r = 0; r < referenced->chunk_count(); ++r)
-      in.referenced.push_back(chunk_desc(*referenced->get_chunk(r)->get_column(rcol)));
+    const auto& rchunks = referenced->chunks();
+    in.referenced.reserve(rchunks.size());
+    for (const auto& rch : rchunks) in.referenced.push_back(chunk_desc(*rch->columns().at(rcol)));
     // fuse the dereference when every column shares the join column's PosLists and referenced table
     bool fuse = true;
     for (ColumnID col = 0; col < table->column_count() && fuse; ++col) {
       if (in.column_group[col] != in.join_group) fuse = false;
-      for (ChunkID c = 0; c < table->chunk_count() && fuse; ++c)
-        if (std::static_pointer_cast<const ReferenceColumn>(table->get_chunk(c)->get_column(col))->referenced_table() !=
-            referenced)
-          fuse = false;
+      for (ChunkID c = 0; c < chunks.size() && fuse; ++c)
+        if (ref_column(c, col).referenced_table().get() != referenced) fuse = false;
     }
     in.fuse = fuse ? 1 : 0;
   }
