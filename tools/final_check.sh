@@ -8,3 +8,4 @@ timeout -k 10 200 python bench.py --workload join-only --no-cpu-baseline > $O/fi
 timeout -k 10 300 python bench.py --workload q1 > $O/fin_q1.json 2>> $O/fin_bench.err
 timeout -k 10 300 python bench.py --workload q3 > $O/fin_q3.json 2>> $O/fin_bench.err
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/fin_smoke.txt 2>&1
+timeout -k 10 300 python -u bench.py --through-operators --steps 5 --warmup 2 --no-cpu-baseline > $O/fin_ops.json 2>> $O/fin_bench.err
