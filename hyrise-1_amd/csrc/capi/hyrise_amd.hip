@@ -216,12 +216,22 @@ int scan_class(const hy_scan_chunk& c) {
 
 uint64_t scan_tiles(uint32_t size) { return (uint64_t(size) + hyk::SCAN_TILE - 1) / hyk::SCAN_TILE; }
 
+// tiles per workgroup of 1-byte columns (HY_SCAN_SEG8: 2 / 4 / 8, A/B)
+int seg8() {
+  static const int v = [] {
+    const char* e = std::getenv("HY_SCAN_SEG8");
+    const int x = e ? std::atoi(e) : hyk::seg_tiles<uint8_t>();
+    return (x == 2 || x == 4) ? x : hyk::seg_tiles<uint8_t>();
+  }();
+  return v;
+}
+
 // tiles per scan workgroup for a column class (hyk::seg_tiles<E> of the class's element type)
 int class_seg(int cls, int32_t value_type) {
   switch (cls) {
     case SC_DICT8:
     case SC_FOR8:
-      return hyk::seg_tiles<uint8_t>();
+      return seg8();
     case SC_DICT16:
     case SC_FOR16:
       return hyk::seg_tiles<uint16_t>();
@@ -241,8 +251,21 @@ hy_status launch_scan(const hyk::ScanLaunchDesc& d, const void* constant, void* 
   if (MODE != hyk::MODE_DICT && constant) std::memcpy(&c.value, constant, sizeof(V));
   KTimer t(MODE == hyk::MODE_DICT ? "scan_dict" : MODE == hyk::MODE_FOR ? "scan_frame_of_reference" : "scan_value", s,
            d.n_rows);
-  hipLaunchKernelGGL((hyk::scan_kernel<E, MODE, OUT_ROWID, V>), dim3(static_cast<uint32_t>(d.n_tiles)),
-                     dim3(hyk::SCAN_THREADS), 0, s, d, c, out, counts);
+  const dim3 grid(static_cast<uint32_t>(d.n_tiles));
+  if constexpr (sizeof(E) == 1) {
+    if (seg8() == 2)
+      hipLaunchKernelGGL((hyk::scan_kernel<E, MODE, OUT_ROWID, V, 2>), grid, dim3(hyk::SCAN_THREADS), 0, s, d, c, out,
+                         counts);
+    else if (seg8() == 4)
+      hipLaunchKernelGGL((hyk::scan_kernel<E, MODE, OUT_ROWID, V, 4>), grid, dim3(hyk::SCAN_THREADS), 0, s, d, c, out,
+                         counts);
+    else
+      hipLaunchKernelGGL((hyk::scan_kernel<E, MODE, OUT_ROWID, V>), grid, dim3(hyk::SCAN_THREADS), 0, s, d, c, out,
+                         counts);
+  } else {
+    hipLaunchKernelGGL((hyk::scan_kernel<E, MODE, OUT_ROWID, V>), grid, dim3(hyk::SCAN_THREADS), 0, s, d, c, out,
+                       counts);
+  }
   t.done();
   HY_HIP(hipGetLastError());
   return HY_OK;

@@ -132,7 +132,8 @@ __device__ __forceinline__ uint32_t match_mask(const hy_scan_chunk& ch, uint32_t
 // E = element type read from memory (vid type for DICT, value type for VALUE, offset type for FOR); MODE selects the
 // semantics, V the compared value type. OUT_ROWID: write reference RowIDs {chunk_id, offset} (8 B) instead of chunk
 // offsets (4 B).
-template <typename E, int MODE, bool OUT_ROWID, typename V = E>
+// SEG: tiles per workgroup (seg_tiles<E>; the host may pick fewer for 1-byte elements: more, shorter workgroups).
+template <typename E, int MODE, bool OUT_ROWID, typename V = E, int SEG = seg_tiles<E>()>
 __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanLaunchDesc d, ScanConst<V> constant,
                                                            void* __restrict__ out_any,
                                                            uint32_t* __restrict__ counts) {
@@ -154,7 +155,6 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanLaunchDesc d, Sc
   const hy_scan_chunk ch = d.chunks[c];
   const uint64_t first_tile = d.chunk_tile_begin[c];
   // (for this kernel d.chunk_tile_begin / d.tile_chunk / d.n_tiles / d.status count segments of SEG tiles)
-  constexpr int SEG = seg_tiles<E>();
   const uint32_t tile_in_chunk = static_cast<uint32_t>(tile - first_tile);
   const uint32_t tile_row0 = tile_in_chunk * (SEG * SCAN_TILE);
   const uint32_t n = ch.column.size;
