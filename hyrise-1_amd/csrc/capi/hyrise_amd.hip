@@ -216,12 +216,14 @@ int scan_class(const hy_scan_chunk& c) {
 
 uint64_t scan_tiles(uint32_t size) { return (uint64_t(size) + hyk::SCAN_TILE - 1) / hyk::SCAN_TILE; }
 
-// tiles per workgroup of 1-byte columns (HY_SCAN_SEG8: 2 / 4 / 8, A/B)
+// tiles per workgroup of 1-byte columns: 4 (64 B of loads in flight per lane) - twice the workgroups of
+// seg_tiles<uint8_t> (8), whose single round of long workgroups left the chip idle in its tail (TableScan SF10
+// `scan_dict` 0.117 vs 0.153 ms; 2: 0.129 ms; profiles/r03d_scan_seg8_*). HY_SCAN_SEG8 = 2 / 8: A/B.
 int seg8() {
   static const int v = [] {
     const char* e = std::getenv("HY_SCAN_SEG8");
-    const int x = e ? std::atoi(e) : hyk::seg_tiles<uint8_t>();
-    return (x == 2 || x == 4) ? x : hyk::seg_tiles<uint8_t>();
+    const int x = e ? std::atoi(e) : 4;
+    return (x == 2 || x == 8) ? x : 4;
   }();
   return v;
 }
@@ -256,11 +258,11 @@ hy_status launch_scan(const hyk::ScanLaunchDesc& d, const void* constant, void* 
     if (seg8() == 2)
       hipLaunchKernelGGL((hyk::scan_kernel<E, MODE, OUT_ROWID, V, 2>), grid, dim3(hyk::SCAN_THREADS), 0, s, d, c, out,
                          counts);
-    else if (seg8() == 4)
-      hipLaunchKernelGGL((hyk::scan_kernel<E, MODE, OUT_ROWID, V, 4>), grid, dim3(hyk::SCAN_THREADS), 0, s, d, c, out,
+    else if (seg8() == 8)
+      hipLaunchKernelGGL((hyk::scan_kernel<E, MODE, OUT_ROWID, V, 8>), grid, dim3(hyk::SCAN_THREADS), 0, s, d, c, out,
                          counts);
     else
-      hipLaunchKernelGGL((hyk::scan_kernel<E, MODE, OUT_ROWID, V>), grid, dim3(hyk::SCAN_THREADS), 0, s, d, c, out,
+      hipLaunchKernelGGL((hyk::scan_kernel<E, MODE, OUT_ROWID, V, 4>), grid, dim3(hyk::SCAN_THREADS), 0, s, d, c, out,
                          counts);
   } else {
     hipLaunchKernelGGL((hyk::scan_kernel<E, MODE, OUT_ROWID, V>), grid, dim3(hyk::SCAN_THREADS), 0, s, d, c, out,
