@@ -59,6 +59,8 @@ def parse():
     p.add_argument("--q1-materialize", action="store_true",
                    help="q1: materialise the two arithmetic expressions with hy_projection before the aggregate "
                         "(the reference's plan shape) instead of evaluating them inside it (A/B)")
+    p.add_argument("--op-kernel-stats", action="store_true",
+                   help="--through-operators: record every step's per-kernel device time (HIP events)")
     p.add_argument("--through-operators", action="store_true",
                    help="time the headline step through TableScan / JoinHash::_on_execute (the drop-in operators, "
                         "bench_ops.py) instead of the C-ABI")

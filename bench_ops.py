@@ -54,17 +54,34 @@ def main_operators(args):
 
     for _ in range(args.warmup):
         step()
-    times, releases = [], []
+    times, releases, phases, pool = [], [], [], []
     scan = join = None
+    hy.op_trace_enable(True)  # every step's operator phase split (host wall time), to attribute any outlier step
+    hy.op_trace_take()
+    kstats = []
+    if getattr(args, "op_kernel_stats", False):  # per-step device time of every kernel (HIP events; no overlap)
+        from bench import kernel_stats
+        L = hy.capi.lib
     for _ in range(args.steps):
         # the previous step's output tables (65,536 chunks at SF100) are released before the timer starts; the
         # release is reported separately (release_ms)
         r0 = time.perf_counter()
         scan = join = None
         releases.append(time.perf_counter() - r0)
+        if getattr(args, "op_kernel_stats", False):
+            L.hy_kernel_stats_reset()
+            L.hy_kernel_stats_enable(1)
         t0 = time.perf_counter()
         scan, join = step()
         times.append(time.perf_counter() - t0)
+        if getattr(args, "op_kernel_stats", False):
+            L.hy_kernel_stats_enable(0)
+            ks = kernel_stats(L)
+            kstats.append({"device_ms": round(sum(k["ms_total"] for k in ks.values()), 3),
+                           "top": sorted(((round(k["ms_total"], 3), n) for n, k in ks.items()), reverse=True)[:3]})
+        phases.append({f"{op}: {phase}": round(ms, 3) for op, phase, ms in hy.op_trace_take()})
+        pool.append([round(b / 2**30, 2) for b in hy.pool_stats()])
+    hy.op_trace_enable(False)
     step_s = sum(times) / len(times)
     out = join.get_output()
     matches = scan.get_output().row_count()
@@ -74,7 +91,9 @@ def main_operators(args):
         "value": round((n_li + n_ord) / step_s, 1), "unit": "rows/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 3),
         "ms_per_step_runs": [round(t * 1e3, 3) for t in times],
-        "release_ms_runs": [round(t * 1e3, 3) for t in releases], "higher_is_better": True, "scaling": "strong",
+        "release_ms_runs": [round(t * 1e3, 3) for t in releases],
+        "phases_ms_runs": phases, "kernel_stats_runs": kstats or None, "pool_reserved_used_gib_runs": pool, "host_cpu_share": hy.host_cpu_share(),
+        "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "int32", "data": "synthetic (seeded counter-based TPC-H-shaped columns)",
         "config": {"workload": "TableScan(l_quantity<24) -> JoinHash(orders, scan) via _on_execute", "sf": args.sf,
                    "lineitem_rows": n_li, "orders_rows": n_ord, "chunk_size": chunk, "scan_matches": matches,

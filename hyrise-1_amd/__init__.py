@@ -50,6 +50,7 @@ AbstractOperator = _host.AbstractOperator
 TableWrapper = _host.TableWrapper
 TableScan = _host.TableScan
 ColumnParameter = _host.ColumnParameter
+ParameterID = _host.ParameterID
 Validate = _host.Validate
 TransactionContext = _host.TransactionContext
 MAX_COMMIT_ID = _host.MAX_COMMIT_ID
@@ -61,6 +62,7 @@ ArithmeticOperator = _host.ArithmeticOperator
 AbstractExpression = _host.AbstractExpression
 PQPColumnExpression = _host.PQPColumnExpression
 ValueExpression = _host.ValueExpression
+ParameterExpression = _host.ParameterExpression
 ArithmeticExpression = _host.ArithmeticExpression
 expression_common_type = _host.expression_common_type
 LogicError = _host.LogicError
@@ -78,5 +80,9 @@ join_hashed_type = _host.join_hashed_type
 join_radix_bits = _host.join_radix_bits
 device_count = _host.device_count
 build_info = _host.build_info
+op_trace_enable = _host.op_trace_enable
+op_trace_take = _host.op_trace_take
+pool_stats = _host.pool_stats
+host_cpu_share = _host.host_cpu_share
 
 from . import capi  # noqa: E402  (ctypes view of the C-ABI)

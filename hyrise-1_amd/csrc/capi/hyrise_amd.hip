@@ -91,6 +91,33 @@ hy_status hy_free_async(void* ptr, hy_stream_t stream) {
   return HY_OK;
 }
 
+hy_status hy_free_async_after(void* ptr, hy_stream_t free_stream, const hy_stream_t* wait_streams, uint32_t n_wait) {
+  if (!ptr) return HY_OK;
+  if (n_wait && !wait_streams) return fail(HY_ERR_INVALID_ARGUMENT, "wait_streams is NULL");
+  for (uint32_t i = 0; i < n_wait; ++i) {
+    if (wait_streams[i] == free_stream) continue;
+    hipEvent_t ev;
+    HY_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    hipError_t e = hipEventRecord(ev, S(wait_streams[i]));
+    if (e == hipSuccess) e = hipStreamWaitEvent(S(free_stream), ev, 0);
+    (void)hipEventDestroy(ev);  // (the wait holds what it needs)
+    HY_HIP(e);
+  }
+  HY_HIP(hipFreeAsync(ptr, S(free_stream)));
+  return HY_OK;
+}
+
+hy_status hy_pool_stats(uint64_t* reserved_bytes, uint64_t* used_bytes) {
+  if (!reserved_bytes || !used_bytes) return fail(HY_ERR_INVALID_ARGUMENT, "NULL output");
+  int dev = 0;
+  hipMemPool_t pool;
+  HY_HIP(hipGetDevice(&dev));
+  HY_HIP(hipDeviceGetDefaultMemPool(&pool, dev));
+  HY_HIP(hipMemPoolGetAttribute(pool, hipMemPoolAttrReservedMemCurrent, reserved_bytes));
+  HY_HIP(hipMemPoolGetAttribute(pool, hipMemPoolAttrUsedMemCurrent, used_bytes));
+  return HY_OK;
+}
+
 hy_status hy_memcpy_htod(void* dst, const void* src, size_t bytes, hy_stream_t stream) {
   if (bytes) HY_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, S(stream)));
   return HY_OK;

@@ -53,6 +53,14 @@ py::object to_py(const AllTypeVariant& v) {
   }
 }
 
+py::object parameter_to_py(const AllParameterVariant& p);
+
+ParameterMap to_parameter_map(const py::dict& d) {
+  ParameterMap m;
+  for (const auto& kv : d) m.emplace(ParameterID{kv.first.cast<size_t>()}, to_variant(kv.second));
+  return m;
+}
+
 py::array_t<uint32_t> pos_list_array(const PosList& pl) {
   py::array_t<uint32_t> a({static_cast<py::ssize_t>(pl.size()), static_cast<py::ssize_t>(2)});
   if (!pl.empty()) std::memcpy(a.mutable_data(), pl.data(), pl.size() * sizeof(RowID));
@@ -116,6 +124,17 @@ py::list table_rows(const Table& t) {
     }
   }
   return rows;
+}
+
+py::object parameter_to_py(const AllParameterVariant& p) {
+  switch (p.index()) {
+    case 0:
+      return to_py(std::get<AllTypeVariant>(p));
+    case 1:
+      return py::cast(std::get<ColumnParameter>(p));
+    default:
+      return py::cast(std::get<ParameterID>(p));
+  }
 }
 
 }  // namespace
@@ -231,7 +250,15 @@ PYBIND11_MODULE(_hyrise_host, m) {
              return std::make_shared<ReferenceColumn>(t, c, pos_list_from_array(pl));
            }),
            py::arg("referenced_table"), py::arg("referenced_column_id"), py::arg("pos_list"))
-      .def("pos_list", [](const ReferenceColumn& c) { return pos_list_array(*c.pos_list()); })
+      .def("pos_list",
+           [](const ReferenceColumn& c) {
+             const auto& pl = *c.pos_list();
+             {
+               py::gil_scoped_release release;  // (a lazy list's first host access copies it down)
+               static_cast<void>(pl.data());
+             }
+             return pos_list_array(pl);
+           })
       .def("pos_list_id", [](const ReferenceColumn& c) { return reinterpret_cast<uintptr_t>(c.pos_list().get()); })
       .def("referenced_table", [](const ReferenceColumn& c) { return std::const_pointer_cast<Table>(c.referenced_table()); })
       .def("referenced_column_id", &ReferenceColumn::referenced_column_id)
@@ -325,6 +352,18 @@ PYBIND11_MODULE(_hyrise_host, m) {
     return n;
   });
   m.def("build_info", []() { return std::string(hy_build_info()); });
+  m.def("op_trace_enable", &op_trace_enable, py::arg("on"));
+  m.def("op_trace_take", []() {
+    py::list l;
+    for (const auto& r : op_trace_take()) l.append(py::make_tuple(r.op, r.phase, r.ms));
+    return l;
+  });
+  m.def("pool_stats", []() {
+    uint64_t reserved = 0, used = 0;
+    hy_check(hy_pool_stats(&reserved, &used), "hy_pool_stats");
+    return py::make_tuple(reserved, used);
+  });
+  m.def("host_cpu_share", &host_cpu_share);
 
   py::class_<OperatorPerformanceData>(m, "OperatorPerformanceData")
       .def_readonly("walltime_ns", &OperatorPerformanceData::walltime_ns)
@@ -336,6 +375,16 @@ PYBIND11_MODULE(_hyrise_host, m) {
       .def("name", &AbstractOperator::name)
       .def("description", &AbstractOperator::description)
       .def("performance_data", &AbstractOperator::performance_data)
+      .def("deep_copy", &AbstractOperator::deep_copy)
+      .def("set_parameters",
+           [](AbstractOperator& o, const py::dict& parameters) { o.set_parameters(to_parameter_map(parameters)); },
+           py::arg("parameters"))
+      .def("input_left", [](const AbstractOperator& o) { return o.mutable_input_left(); })
+      .def("input_right", [](const AbstractOperator& o) { return o.mutable_input_right(); })
+      .def(
+          "set_transaction_context_recursively",
+          [](AbstractOperator& o, std::shared_ptr<TransactionContext> c) { o.set_transaction_context_recursively(c); },
+          py::keep_alive<1, 2>())
       // the operator holds its context weakly (abstract_operator.cpp:95-98); Python keeps it alive with the operator
       .def(
           "set_transaction_context",
@@ -348,14 +397,27 @@ PYBIND11_MODULE(_hyrise_host, m) {
 
   py::class_<ColumnParameter>(m, "ColumnParameter")
       .def(py::init([](ColumnID c) { return ColumnParameter{c}; }), py::arg("column_id"))
-      .def_readonly("column_id", &ColumnParameter::column_id);
+      .def_readonly("column_id", &ColumnParameter::column_id)
+      .def("__eq__", [](const ColumnParameter& a, const ColumnParameter& b) { return a == b; })
+      .def("__repr__", [](const ColumnParameter& c) { return "ColumnParameter(" + std::to_string(c.column_id) + ")"; });
+  py::class_<ParameterID>(m, "ParameterID")
+      .def(py::init([](size_t id) { return ParameterID{id}; }), py::arg("id"))
+      .def_readonly("id", &ParameterID::t)
+      .def("__eq__", [](const ParameterID& a, const ParameterID& b) { return a == b; })
+      .def("__hash__", [](const ParameterID& p) { return ParameterIDHash{}(p); })
+      .def("__repr__", [](const ParameterID& p) { return "ParameterID(" + std::to_string(p.t) + ")"; });
   py::class_<TableScan, AbstractOperator, std::shared_ptr<TableScan>>(m, "TableScan")
       .def(py::init([](std::shared_ptr<AbstractOperator> in, ColumnID col, PredicateCondition cond, py::object value) {
              if (py::isinstance<ColumnParameter>(value))
                return std::make_shared<TableScan>(in, col, cond, value.cast<ColumnParameter>());
+             if (py::isinstance<ParameterID>(value))
+               return std::make_shared<TableScan>(in, col, cond, value.cast<ParameterID>());
              return std::make_shared<TableScan>(in, col, cond, to_variant(value));
            }),
            py::arg("input"), py::arg("column_id"), py::arg("predicate_condition"), py::arg("value"))
+      .def("left_column_id", &TableScan::left_column_id)
+      .def("predicate_condition", &TableScan::predicate_condition)
+      .def("right_parameter", [](const TableScan& t) { return parameter_to_py(t.right_parameter()); })
       .def("set_excluded_chunk_ids", &TableScan::set_excluded_chunk_ids);
 
   py::class_<TransactionContext, std::shared_ptr<TransactionContext>>(m, "TransactionContext")
@@ -374,7 +436,10 @@ PYBIND11_MODULE(_hyrise_host, m) {
            }),
            py::arg("left"), py::arg("right"), py::arg("mode"), py::arg("column_ids"), py::arg("predicate_condition"),
            py::arg("radix_bits") = 9)
-      .def("used_radix_bits", &JoinHash::used_radix_bits);
+      .def("used_radix_bits", &JoinHash::used_radix_bits)
+      .def("mode", &JoinHash::mode)
+      .def("column_ids", &JoinHash::column_ids)
+      .def("predicate_condition", &JoinHash::predicate_condition);
 
   py::class_<AggregateColumnDefinition>(m, "AggregateColumnDefinition")
       .def(py::init<std::optional<ColumnID>, AggregateFunction>(), py::arg("column"), py::arg("function"))
@@ -385,7 +450,9 @@ PYBIND11_MODULE(_hyrise_host, m) {
       .def(py::init<std::shared_ptr<const AbstractOperator>, std::vector<AggregateColumnDefinition>,
                     std::vector<ColumnID>>(),
            py::arg("input"), py::arg("aggregates"), py::arg("groupby_column_ids"))
-      .def("used_dense_path", &Aggregate::used_dense_path);
+      .def("used_dense_path", &Aggregate::used_dense_path)
+      .def("aggregates", &Aggregate::aggregates)
+      .def("groupby_column_ids", &Aggregate::groupby_column_ids);
 
   // ---- Projection and its expressions (reference expression/*.hpp, operators/projection.hpp)
   py::enum_<ArithmeticOperator>(m, "ArithmeticOperator")
@@ -397,7 +464,8 @@ PYBIND11_MODULE(_hyrise_host, m) {
   py::class_<AbstractExpression, std::shared_ptr<AbstractExpression>>(m, "AbstractExpression")
       .def("data_type", &AbstractExpression::data_type)
       .def("is_nullable", &AbstractExpression::is_nullable)
-      .def("as_column_name", &AbstractExpression::as_column_name);
+      .def("as_column_name", &AbstractExpression::as_column_name)
+      .def("deep_copy", &AbstractExpression::deep_copy);
   py::class_<PQPColumnExpression, AbstractExpression, std::shared_ptr<PQPColumnExpression>>(m, "PQPColumnExpression")
       .def(py::init<ColumnID, DataType, bool, std::string>(), py::arg("column_id"), py::arg("data_type"),
            py::arg("nullable"), py::arg("column_name"))
@@ -413,6 +481,14 @@ PYBIND11_MODULE(_hyrise_host, m) {
            }),
            py::arg("value"), py::arg("data_type"))
       .def_property_readonly("value", [](const ValueExpression& e) { return to_py(e.value); });
+  py::class_<ParameterExpression, AbstractExpression, std::shared_ptr<ParameterExpression>>(m, "ParameterExpression")
+      .def(py::init([](size_t id) { return std::make_shared<ParameterExpression>(ParameterID{id}); }),
+           py::arg("parameter_id"))
+      .def_property_readonly("parameter_id", [](const ParameterExpression& e) { return e.parameter_id.t; })
+      .def_property_readonly("value", [](const ParameterExpression& e) -> py::object {
+        return e.value() ? to_py(*e.value()) : py::object(py::none());
+      })
+      .def_property_readonly("has_value", [](const ParameterExpression& e) { return e.value().has_value(); });
   py::class_<ArithmeticExpression, AbstractExpression, std::shared_ptr<ArithmeticExpression>>(m, "ArithmeticExpression")
       .def(py::init<ArithmeticOperator, std::shared_ptr<AbstractExpression>, std::shared_ptr<AbstractExpression>>(),
            py::arg("arithmetic_operator"), py::arg("left_operand"), py::arg("right_operand"))

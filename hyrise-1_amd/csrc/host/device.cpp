@@ -1,17 +1,39 @@
 #include "device.hpp"
 
+#include <sched.h>
+
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 
 namespace hyrise {
 
 namespace {
+// Every live operator stream of the process (one per thread that ran an operator), for device_buffer_free.
+struct StreamRegistry {
+  std::mutex m;
+  std::vector<hy_stream_t> streams;
+};
+StreamRegistry& stream_registry() {
+  static StreamRegistry* r = new StreamRegistry;  // (never destroyed: buffers may be released during exit)
+  return *r;
+}
+
 struct StreamHolder {
   hy_stream_t stream = nullptr;
   ~StreamHolder() {
-    if (stream) hy_stream_destroy(stream);
+    if (!stream) return;
+    auto& r = stream_registry();
+    {
+      std::lock_guard<std::mutex> lock(r.m);
+      r.streams.erase(std::remove(r.streams.begin(), r.streams.end(), stream), r.streams.end());
+    }
+    hy_stream_destroy(stream);  // (its pending work still completes)
   }
 };
+thread_local StreamHolder t_stream;
 
 std::shared_ptr<DeviceBuffer> upload(const void* host, size_t bytes, hy_stream_t s) {
   auto buf = std::make_shared<DeviceBuffer>(std::max<size_t>(bytes, 16));
@@ -111,12 +133,56 @@ void require_device() {
 }
 
 hy_stream_t operator_stream() {
-  thread_local StreamHolder holder;
-  if (!holder.stream) {
+  if (!t_stream.stream) {
     require_device();
-    hy_check(hy_stream_create(&holder.stream), "hy_stream_create");
+    hy_check(hy_stream_create(&t_stream.stream), "hy_stream_create");
+    auto& r = stream_registry();
+    std::lock_guard<std::mutex> lock(r.m);
+    r.streams.push_back(t_stream.stream);
   }
-  return holder.stream;
+  return t_stream.stream;
+}
+
+void operator_stream_synchronize_if_used() {
+  if (t_stream.stream) hy_check(hy_stream_synchronize(t_stream.stream), "hy_stream_synchronize");
+}
+
+void device_buffer_free(void* ptr) {
+  auto& r = stream_registry();
+  std::lock_guard<std::mutex> lock(r.m);
+  hy_stream_t s = t_stream.stream ? t_stream.stream : (r.streams.empty() ? nullptr : r.streams.front());
+  // (a destructor: a failure cannot be reported; the pool keeps the block then)
+  static_cast<void>(hy_free_async_after(ptr, s, r.streams.data(), static_cast<uint32_t>(r.streams.size())));
+}
+
+unsigned host_cpu_share() {
+  static const unsigned share = [] {
+    long n = 0;
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) n = CPU_COUNT(&set);
+    if (n <= 0) n = static_cast<long>(std::max(1u, std::thread::hardware_concurrency()));
+    auto cap = [&](long c) {
+      if (c > 0) n = std::min(n, c);
+    };
+    if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {  // cgroup v2: "<quota> <period>" or "max <period>"
+      char q[32] = {0};
+      long period = 0;
+      if (std::fscanf(f, "%31s %ld", q, &period) == 2 && std::strcmp(q, "max") != 0 && period > 0)
+        cap((std::strtol(q, nullptr, 10) + period - 1) / period);
+      std::fclose(f);
+    } else if (FILE* fq = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {  // cgroup v1
+      long quota = -1, period = 0;
+      if (std::fscanf(fq, "%ld", &quota) != 1) quota = -1;
+      std::fclose(fq);
+      if (FILE* fp = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+        if (std::fscanf(fp, "%ld", &period) == 1 && quota > 0 && period > 0) cap((quota + period - 1) / period);
+        std::fclose(fp);
+      }
+    }
+    if (const char* e = std::getenv("OMP_NUM_THREADS")) cap(std::strtol(e, nullptr, 10));
+    return static_cast<unsigned>(std::max(1L, n));
+  }();
+  return share;
 }
 
 int32_t hy_type_of(DataType t) {
@@ -312,7 +378,8 @@ std::shared_ptr<DevicePosList> device_pos_list(const PosList& pos_list) {
 }
 
 namespace {
-// the lazy PosLists' host copy (PosList::host): stream-ordered after the kernels that wrote the RowIDs
+// the lazy PosLists' host copy (PosList::host): after the kernels that wrote the RowIDs (their operator synchronised its
+// stream before execute() returned; on the producer's own thread the copy is stream-ordered after them as well)
 void fetch_pos_list(const PosList& pos_list, RowID* dst) {
   const auto d = pos_list.device_mirror();
   if (!d) throw std::logic_error("lazy PosList without a device mirror");

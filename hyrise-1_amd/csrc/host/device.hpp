@@ -30,6 +30,11 @@ inline void hy_check(hy_status st, const char* what) {
 void* temp_block_acquire(size_t bytes, size_t* block_bytes);
 hy_stream_t operator_stream();
 void temp_block_release(void* ptr, size_t block_bytes);
+// Returns a long-lived buffer to the device pool once every operator stream of the process has finished the work
+// enqueued so far (the operator streams are non-blocking: a free on the null stream would not be ordered after them).
+// The free is enqueued on the releasing thread's operator stream, so that thread's next output allocation reuses the
+// block (same-stream reuse needs no cross-stream dependency in the pool).
+void device_buffer_free(void* ptr);
 
 // Owning device allocation. Temporary (the `stream` constructor): a block of the calling thread's cache, for buffers
 // used only by that thread's operator stream while the operator runs; otherwise a plain allocation for buffers that
@@ -45,8 +50,8 @@ class DeviceBuffer {
     if (bytes) _ptr = temp_block_acquire(bytes, &_block);
   }
   ~DeviceBuffer() {
-    // freed on the null stream: ordered after the work of every (blocking) operator stream that may still read it
-    if (_ptr) _temp ? temp_block_release(_ptr, _block) : static_cast<void>(hy_free_async(_ptr, nullptr));
+    // ordered after the work of every operator stream that may still read it
+    if (_ptr) _temp ? temp_block_release(_ptr, _block) : device_buffer_free(_ptr);
   }
   DeviceBuffer(const DeviceBuffer&) = delete;
   DeviceBuffer& operator=(const DeviceBuffer&) = delete;
@@ -74,6 +79,8 @@ class DeviceBuffer {
 
 // Per-thread stream for operator execution (operators may run concurrently on scheduler workers).
 hy_stream_t operator_stream();
+// Waits for the calling thread's operator stream, if the thread has one (no stream is created).
+void operator_stream_synchronize_if_used();
 
 // Is a usable device present? Throws with a clear message if the HIP library reports none.
 void require_device();

@@ -7,6 +7,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <condition_variable>
+#include <exception>
 #include <map>
 #include <mutex>
 #include <numeric>
@@ -17,19 +18,43 @@
 namespace hyrise {
 
 namespace {
-// HY_OP_TRACE=1: host wall time of operator phases on stderr (where an operator step's time goes)
+// Host wall time of operator phases (where an operator step's time goes): HY_OP_TRACE=1 prints them on stderr;
+// op_trace_enable(true) records them for op_trace_take() (bench_ops.py keeps every step's split).
+std::atomic<bool> g_trace_record{false};
+std::mutex g_trace_m;
+std::vector<OpTraceRecord> g_trace;
+
 struct PhaseTrace {
   const char* op;
   std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
-  bool on = std::getenv("HY_OP_TRACE") != nullptr;
-  void mark(const char* phase) {
-    if (!on) return;
+  bool print = std::getenv("HY_OP_TRACE") != nullptr;
+  bool record = g_trace_record.load(std::memory_order_relaxed);
+  bool on = print || record;
+  void mark(const char* phase) { note(phase, since()); }
+  double since() {
     const auto now = std::chrono::steady_clock::now();
-    std::fprintf(stderr, "[op] %s %s %.3f ms\n", op, phase, std::chrono::duration<double, std::milli>(now - t).count());
+    const double ms = std::chrono::duration<double, std::milli>(now - t).count();
     t = now;
+    return ms;
+  }
+  void note(const std::string& phase, double ms) const {
+    if (print) std::fprintf(stderr, "[op] %s %s %.3f ms\n", op, phase.c_str(), ms);
+    if (record) {
+      std::lock_guard<std::mutex> lock(g_trace_m);
+      g_trace.push_back({op, phase, ms});
+    }
   }
 };
 }  // namespace
+
+void op_trace_enable(bool on) { g_trace_record.store(on); }
+
+std::vector<OpTraceRecord> op_trace_take() {
+  std::lock_guard<std::mutex> lock(g_trace_m);
+  std::vector<OpTraceRecord> out;
+  out.swap(g_trace);
+  return out;
+}
 
 // reference abstract_operator.cpp:25-54
 void AbstractOperator::execute() {
@@ -37,18 +62,49 @@ void AbstractOperator::execute() {
   Assert(!_input_right || _input_right->get_output(), "Right input has not been executed");
   Assert(!_output, "Operator has already been executed");
   const auto t0 = std::chrono::steady_clock::now();
-  // abstract_operator.cpp:32-48: an aborted transaction skips the operator (empty output of the input's shape)
+  // abstract_operator.cpp:32-41: an aborted transaction skips the operator; its output stays unset
   const auto context = transaction_context();
-  if (context && context->aborted()) {
-    _output = std::make_shared<Table>(_input_left ? _input_left->get_output()->column_definitions()
-                                                  : std::vector<TableColumnDefinition>{},
-                                      TableType::Data);
-    return;
-  }
+  if (context && context->aborted()) return;
   _output = _on_execute(context);
+  // The output is complete when execute() returns (the reference's contract): consumers may run on other threads,
+  // whose non-blocking operator streams are not ordered after this thread's kernels.
+  operator_stream_synchronize_if_used();
   _on_cleanup();
   _performance_data.walltime_ns = static_cast<uint64_t>(
       std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count());
+}
+
+// abstract_operator.cpp:100-106
+void AbstractOperator::set_transaction_context_recursively(const std::weak_ptr<TransactionContext>& context) {
+  set_transaction_context(context);
+  if (_input_left) mutable_input_left()->set_transaction_context_recursively(context);
+  if (_input_right) mutable_input_right()->set_transaction_context_recursively(context);
+}
+
+// abstract_operator.cpp:77-81
+std::shared_ptr<AbstractOperator> AbstractOperator::deep_copy() const {
+  std::unordered_map<const AbstractOperator*, std::shared_ptr<AbstractOperator>> copied_ops;
+  return _deep_copy_impl(copied_ops);
+}
+
+// abstract_operator.cpp:157-173
+std::shared_ptr<AbstractOperator> AbstractOperator::_deep_copy_impl(
+    std::unordered_map<const AbstractOperator*, std::shared_ptr<AbstractOperator>>& copied_ops) const {
+  const auto it = copied_ops.find(this);
+  if (it != copied_ops.end()) return it->second;
+  const auto left = _input_left ? _input_left->_deep_copy_impl(copied_ops) : std::shared_ptr<AbstractOperator>{};
+  const auto right = _input_right ? _input_right->_deep_copy_impl(copied_ops) : std::shared_ptr<AbstractOperator>{};
+  auto copy = _on_deep_copy(left, right);
+  if (_transaction_context) copy->set_transaction_context(*_transaction_context);
+  copied_ops.emplace(this, copy);
+  return copy;
+}
+
+// abstract_operator.cpp:147-151
+void AbstractOperator::set_parameters(const ParameterMap& parameters) {
+  _on_set_parameters(parameters);
+  if (_input_left) mutable_input_left()->set_parameters(parameters);
+  if (_input_right) mutable_input_right()->set_parameters(parameters);
 }
 
 // ================================================================================================================
@@ -407,8 +463,31 @@ const std::string TableScan::description() const {
          ")";
 }
 
+// table_scan.cpp:63-70: a ParameterID placeholder is replaced by its value when the map holds one
+void TableScan::_on_set_parameters(const ParameterMap& parameters) {
+  if (!is_parameter_id(_right_parameter)) return;
+  const auto it = parameters.find(std::get<ParameterID>(_right_parameter));
+  if (it == parameters.end()) return;
+  _right_parameter = it->second;
+}
+
+// table_scan.cpp:72-76 (excluded chunk ids are not part of the configuration, as in the reference)
+std::shared_ptr<AbstractOperator> TableScan::_on_deep_copy(const std::shared_ptr<AbstractOperator>& copied_input_left,
+                                                           const std::shared_ptr<AbstractOperator>&) const {
+  return std::make_shared<TableScan>(copied_input_left, _left_column_id, _predicate_condition, _right_parameter);
+}
+
 std::shared_ptr<const Table> TableScan::_on_execute() {
   const auto in_table = input_table_left();
+  // the reference's scan impls boost::get the value / column id: an unset placeholder cannot execute
+  if (is_parameter_id(_right_parameter))
+    Fail("TableScan: parameter " + std::to_string(std::get<ParameterID>(_right_parameter).t) +
+         " has no value (set_parameters first)");
+  static const AllTypeVariant no_value{};
+  const AllTypeVariant& right_value = is_variant(_right_parameter) ? std::get<AllTypeVariant>(_right_parameter)
+                                                                      : no_value;
+  const ColumnID right_column_id =
+      is_column_id(_right_parameter) ? std::get<ColumnParameter>(_right_parameter).column_id : INVALID_COLUMN_ID;
   switch (_predicate_condition) {
     case PredicateCondition::In:
       Fail("hyrise-amd: predicate " + predicate_condition_to_string(_predicate_condition) +
@@ -418,7 +497,7 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
     default:
       break;
   }
-  if (_right_column_id != INVALID_COLUMN_ID) {
+  if (right_column_id != INVALID_COLUMN_ID) {
     // ColumnComparisonTableScanImpl (table_scan.cpp:191-199, column_comparison_table_scan_impl.cpp:23-84)
     Assert(_predicate_condition != PredicateCondition::IsNull && _predicate_condition != PredicateCondition::IsNotNull,
            "Unsupported comparison type encountered");
@@ -426,7 +505,7 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
     for (const auto c : _excluded_chunk_ids)
       if (c < excluded.size()) excluded[c] = true;
     _performance_data.rows_in = in_table->row_count();
-    return column_comparison_scan(in_table, _left_column_id, _predicate_condition, _right_column_id, excluded);
+    return column_comparison_scan(in_table, _left_column_id, _predicate_condition, right_column_id, excluded);
   }
   if (_predicate_condition == PredicateCondition::Like || _predicate_condition == PredicateCondition::NotLike)
     Assert(in_table->column_data_type(_left_column_id) == DataType::String,
@@ -439,7 +518,7 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
       _predicate_condition == PredicateCondition::IsNull || _predicate_condition == PredicateCondition::IsNotNull;
   // reference single_column_table_scan_impl.cpp:23-36: comparing with NULL matches nothing (IS [NOT] NULL ignores the
   // right value, table_scan.cpp:186-189)
-  if (!null_test && variant_is_null(_right_value)) return output;
+  if (!null_test && variant_is_null(right_value)) return output;
   require_device();
   hy_stream_t s = operator_stream();
   const auto col_type = in_table->column_data_type(_left_column_id);
@@ -460,7 +539,7 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
       if (excluded[c]) continue;
       const auto column = in_table->get_chunk(c)->get_column(_left_column_id);
       size_t off;
-      auto d = scan_descriptor(*column, col_type, _predicate_condition, _right_value, &like_sets, &off);
+      auto d = scan_descriptor(*column, col_type, _predicate_condition, right_value, &like_sets, &off);
       d.out_begin = total;
       total += column->size();
       descs.push_back(d);
@@ -478,7 +557,7 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
     std::vector<std::pair<uint64_t, uint32_t>> views;  // (offset, count) per chunk
     if (col_type == DataType::String) {
       // string column (unencoded and / or dictionary chunks): the matches arrive compacted, chunk-major
-      const StringScanPredicate sp(_predicate_condition, _right_value);
+      const StringScanPredicate sp(_predicate_condition, right_value);
       size_t ws_bytes = 0;
       hy_check(hy_string_table_scan_workspace_size(descs.data(), static_cast<uint32_t>(descs.size()), &sp.pred,
                                                    &ws_bytes),
@@ -496,7 +575,7 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
         at += h_counts[k];
       }
     } else {
-      const auto constant = null_test || like ? ScanConstant{} : typed_constant(col_type, _right_value);
+      const auto constant = null_test || like ? ScanConstant{} : typed_constant(col_type, right_value);
       size_t ws_bytes = 0;
       hy_check(hy_table_scan_workspace_size(sizes.data(), static_cast<uint32_t>(sizes.size()), &ws_bytes),
                "hy_table_scan_workspace_size");
@@ -551,12 +630,12 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
       for (ChunkID r = 0; r < rtable->chunk_count(); ++r) {
         size_t off;
         rdesc[r] = scan_descriptor(*rtable->get_chunk(r)->get_column(rcol), col_type, _predicate_condition,
-                                   _right_value, &like_sets, &off);
+                                   right_value, &like_sets, &off);
         if (off != SIZE_MAX) like_sets.fix.emplace_back(&rdesc[r], off);  // (rdesc is sized: no reallocation)
       }
       like_sets.finish(&keep);
     }
-    const auto constant = null_test || like ? ScanConstant{} : typed_constant(col_type, _right_value);
+    const auto constant = null_test || like ? ScanConstant{} : typed_constant(col_type, right_value);
     const auto dpl = device_pos_list(pos_list);
     const uint64_t m = pos_list.size();
 
@@ -579,7 +658,7 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
     const auto groups = unordered_map_order(seen);
 
     const bool strings = col_type == DataType::String;
-    const StringScanPredicate sp(_predicate_condition, _right_value);
+    const StringScanPredicate sp(_predicate_condition, right_value);
     size_t ws_bytes = 0;  // also the workspace of hy_pos_list_null_positions
     hy_check(hy_reference_scan_workspace_size(m, &ws_bytes), "hy_reference_scan_workspace_size");
     if (strings) {
@@ -1254,7 +1333,7 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
     return e ? std::max(1L, std::strtol(e, nullptr, 10)) : 16L;
   }();
   const unsigned workers = static_cast<unsigned>(
-      std::max<size_t>(1, std::min<size_t>({max_workers, std::thread::hardware_concurrency(), n_parts / 2048})));
+      std::max<size_t>(1, std::min<size_t>({max_workers, host_cpu_share(), n_parts / 2048})));
   std::atomic<size_t> next{0};
   const auto spawn = std::chrono::steady_clock::now();
   std::atomic<int64_t> last_done_us{0};  // (HY_OP_TRACE: when the builders finished)
@@ -1312,13 +1391,20 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
       }
     }
   };
+  std::exception_ptr builder_error;  // a builder's exception, rethrown on this thread after the join
   auto build_then_set_views = [&]() {
-    build();
+    std::exception_ptr err;
+    try {
+      build();
+    } catch (...) {
+      err = std::current_exception();
+    }
     std::unique_lock<std::mutex> lock(phase_m);
+    if (err && !builder_error) builder_error = err;
     ++built;
     phase_cv.notify_all();
     phase_cv.wait(lock, [&] { return ranges < 0 || (ranges > 0 && built == workers); });
-    if (ranges < 0) return;
+    if (ranges < 0 || builder_error) return;  // (a failed builder left some partitions without PosLists)
     lock.unlock();
     set_views();
   };
@@ -1371,9 +1457,8 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
   dereference_groups(po, *out_p, used);
   build_then_set_views();  // (this thread joins the builders)
   for (auto& t : pool) t.join();
-  if (tr.on)
-    std::fprintf(stderr, "[op] JoinHash %u builders finished %.3f ms after they started\n", workers,
-                 last_done_us.load() / 1000.0);
+  if (builder_error) std::rethrow_exception(builder_error);
+  if (tr.on) tr.note("builders done after start (" + std::to_string(workers) + " threads)", last_done_us.load() / 1000.0);
   tr.mark("output chunks built, views set");
   std::vector<std::shared_ptr<Chunk>> nonempty;  // join_hash.cpp:835-837: no chunk for an empty partition
   nonempty.reserve(n_parts);

@@ -2,7 +2,10 @@
 //
 //   AbstractOperator::execute / get_output / _on_execute   reference src/lib/operators/abstract_operator.cpp:25-67
 //   TableWrapper                                           reference src/lib/operators/table_wrapper.cpp
-//   TableScan(in, ColumnID, PredicateCondition, value)     reference src/lib/operators/table_scan.hpp:22-23
+//   deep_copy / set_parameters / _on_deep_copy / _on_set_parameters
+//                                                          reference src/lib/operators/abstract_operator.hpp:107-155
+//   TableScan(in, ColumnID, PredicateCondition, AllParameterVariant)
+//                                                          reference src/lib/operators/table_scan.hpp:22-23
 //   JoinHash(l, r, JoinMode, ColumnIDPair, PredicateCondition, radix_bits = 9)
 //                                                          reference src/lib/operators/join_hash.hpp:26-28
 //   Aggregate(in, aggregates, groupby_column_ids)          reference src/lib/operators/aggregate.hpp:87-88
@@ -49,11 +52,18 @@ class TransactionContext {
   bool _aborted = false;
 };
 
+// A parameter's values by id: what set_parameters hands down a plan (reference abstract_operator.hpp:129).
+using ParameterMap = std::unordered_map<ParameterID, AllTypeVariant, ParameterIDHash>;
+
+// abstract_operator.hpp:70-172. Operators are not copyable (Noncopyable in the reference); deep_copy() makes a fresh,
+// unexecuted plan of the same configuration.
 class AbstractOperator : public std::enable_shared_from_this<AbstractOperator> {
  public:
   AbstractOperator(OperatorType type, std::shared_ptr<const AbstractOperator> left = nullptr,
                    std::shared_ptr<const AbstractOperator> right = nullptr)
       : _type(type), _input_left(std::move(left)), _input_right(std::move(right)) {}
+  AbstractOperator(const AbstractOperator&) = delete;
+  AbstractOperator& operator=(const AbstractOperator&) = delete;
   virtual ~AbstractOperator() = default;
 
   void execute();
@@ -66,20 +76,45 @@ class AbstractOperator : public std::enable_shared_from_this<AbstractOperator> {
 
   std::shared_ptr<const AbstractOperator> input_left() const { return _input_left; }
   std::shared_ptr<const AbstractOperator> input_right() const { return _input_right; }
+  // abstract_operator.cpp:121-127: the inputs with const cast away
+  std::shared_ptr<AbstractOperator> mutable_input_left() const {
+    return std::const_pointer_cast<AbstractOperator>(_input_left);
+  }
+  std::shared_ptr<AbstractOperator> mutable_input_right() const {
+    return std::const_pointer_cast<AbstractOperator>(_input_right);
+  }
   std::shared_ptr<const Table> input_table_left() const { return _input_left->get_output(); }
   std::shared_ptr<const Table> input_table_right() const { return _input_right->get_output(); }
   const OperatorPerformanceData& performance_data() const { return _performance_data; }
 
-  // abstract_operator.cpp:87-97: the operator's transaction (held weakly, as the reference does)
+  // abstract_operator.cpp:87-119: the operator's transaction (held weakly, as the reference does)
+  bool transaction_context_is_set() const { return _transaction_context.has_value(); }
   void set_transaction_context(const std::weak_ptr<TransactionContext>& context) { _transaction_context = context; }
-  std::shared_ptr<TransactionContext> transaction_context() const { return _transaction_context.lock(); }
+  std::shared_ptr<TransactionContext> transaction_context() const {
+    return _transaction_context ? _transaction_context->lock() : nullptr;
+  }
+  void set_transaction_context_recursively(const std::weak_ptr<TransactionContext>& context);
+
+  // abstract_operator.cpp:77-81, 157-173: a new instance of the same operator with the same configuration, inputs
+  // copied recursively; an input shared by two consumers (a diamond) is copied once.
+  std::shared_ptr<AbstractOperator> deep_copy() const;
+
+  // abstract_operator.cpp:147-151: parameters set in this operator, then in both inputs
+  void set_parameters(const ParameterMap& parameters);
 
  protected:
   // execute() calls the context overload; operators that need no transaction implement the plain one
   virtual std::shared_ptr<const Table> _on_execute(std::shared_ptr<TransactionContext>) { return _on_execute(); }
   virtual std::shared_ptr<const Table> _on_execute() = 0;
   virtual void _on_cleanup() {}
-  std::weak_ptr<TransactionContext> _transaction_context;
+  virtual void _on_set_parameters(const ParameterMap& parameters) = 0;
+  virtual std::shared_ptr<AbstractOperator> _on_deep_copy(
+      const std::shared_ptr<AbstractOperator>& copied_input_left,
+      const std::shared_ptr<AbstractOperator>& copied_input_right) const = 0;
+  std::shared_ptr<AbstractOperator> _deep_copy_impl(
+      std::unordered_map<const AbstractOperator*, std::shared_ptr<AbstractOperator>>& copied_ops) const;
+
+  std::optional<std::weak_ptr<TransactionContext>> _transaction_context;
 
   const OperatorType _type;
   std::shared_ptr<const AbstractOperator> _input_left, _input_right;
@@ -95,46 +130,42 @@ class TableWrapper final : public AbstractOperator {
 
  protected:
   std::shared_ptr<const Table> _on_execute() override { return _table; }
+  void _on_set_parameters(const ParameterMap&) override {}
+  std::shared_ptr<AbstractOperator> _on_deep_copy(const std::shared_ptr<AbstractOperator>&,
+                                                  const std::shared_ptr<AbstractOperator>&) const override {
+    return std::make_shared<TableWrapper>(_table);  // table_wrapper.cpp:14-18
+  }
   std::shared_ptr<const Table> _table;
-};
-
-// The ColumnID alternative of the reference's right parameter (AllParameterVariant, all_parameter_variant.hpp):
-// TableScan compares two columns of its input (ColumnComparisonTableScanImpl, table_scan.cpp:191-199).
-struct ColumnParameter {
-  ColumnID column_id;
 };
 
 class TableScan final : public AbstractOperator {
  public:
+  // table_scan.cpp:32-37: the right side is a value, a column of the input (ColumnParameter) or a ParameterID
+  // placeholder that set_parameters replaces by its value before execution.
   TableScan(std::shared_ptr<const AbstractOperator> in, ColumnID left_column_id, PredicateCondition predicate_condition,
-            AllTypeVariant right_value)
+            AllParameterVariant right_parameter)
       : AbstractOperator(OperatorType::TableScan, std::move(in)),
         _left_column_id(left_column_id),
         _predicate_condition(predicate_condition),
-        _right_value(std::move(right_value)) {}
-  TableScan(std::shared_ptr<const AbstractOperator> in, ColumnID left_column_id, PredicateCondition predicate_condition,
-            ColumnParameter right_column)
-      : AbstractOperator(OperatorType::TableScan, std::move(in)),
-        _left_column_id(left_column_id),
-        _predicate_condition(predicate_condition),
-        _right_column_id(right_column.column_id) {}
+        _right_parameter(std::move(right_parameter)) {}
 
   const std::string name() const override { return "TableScan"; }
   const std::string description() const override;
   ColumnID left_column_id() const { return _left_column_id; }
   PredicateCondition predicate_condition() const { return _predicate_condition; }
-  const AllTypeVariant& right_value() const { return _right_value; }
-  ColumnID right_column_id() const { return _right_column_id; }  // INVALID_COLUMN_ID for a value comparison
+  const AllParameterVariant& right_parameter() const { return _right_parameter; }
   void set_excluded_chunk_ids(const std::vector<ChunkID>& ids) { _excluded_chunk_ids = ids; }
 
  protected:
   std::shared_ptr<const Table> _on_execute() override;
+  void _on_set_parameters(const ParameterMap& parameters) override;
+  std::shared_ptr<AbstractOperator> _on_deep_copy(const std::shared_ptr<AbstractOperator>& copied_input_left,
+                                                  const std::shared_ptr<AbstractOperator>&) const override;
 
  private:
   ColumnID _left_column_id;
   PredicateCondition _predicate_condition;
-  AllTypeVariant _right_value;
-  ColumnID _right_column_id = INVALID_COLUMN_ID;
+  AllParameterVariant _right_parameter;
   std::vector<ChunkID> _excluded_chunk_ids;
 };
 
@@ -150,6 +181,11 @@ class Validate final : public AbstractOperator {
  protected:
   std::shared_ptr<const Table> _on_execute(std::shared_ptr<TransactionContext> transaction_context) override;
   std::shared_ptr<const Table> _on_execute() override;
+  void _on_set_parameters(const ParameterMap&) override {}  // validate.cpp:44
+  std::shared_ptr<AbstractOperator> _on_deep_copy(const std::shared_ptr<AbstractOperator>& copied_input_left,
+                                                  const std::shared_ptr<AbstractOperator>&) const override {
+    return std::make_shared<Validate>(copied_input_left);  // validate.cpp:38-42
+  }
 };
 
 class JoinHash final : public AbstractOperator {
@@ -167,9 +203,17 @@ class JoinHash final : public AbstractOperator {
   JoinMode mode() const { return _mode; }
   // radix bits actually used by the last execution (the constructor argument is ignored, as in the reference)
   uint32_t used_radix_bits() const { return _used_radix_bits; }
+  const std::pair<ColumnID, ColumnID>& column_ids() const { return _column_ids; }
+  PredicateCondition predicate_condition() const { return _predicate_condition; }
 
  protected:
   std::shared_ptr<const Table> _on_execute() override;
+  void _on_set_parameters(const ParameterMap&) override {}  // join_hash.cpp:47
+  // join_hash.cpp:41-45: the copy gets the default radix_bits (the argument is ignored by execution anyway)
+  std::shared_ptr<AbstractOperator> _on_deep_copy(const std::shared_ptr<AbstractOperator>& copied_input_left,
+                                                  const std::shared_ptr<AbstractOperator>& copied_input_right) const override {
+    return std::make_shared<JoinHash>(copied_input_left, copied_input_right, _mode, _column_ids, _predicate_condition);
+  }
 
  private:
   JoinMode _mode;
@@ -203,6 +247,11 @@ class Aggregate final : public AbstractOperator {
 
  protected:
   std::shared_ptr<const Table> _on_execute() override;
+  void _on_set_parameters(const ParameterMap&) override {}  // aggregate.cpp:78
+  std::shared_ptr<AbstractOperator> _on_deep_copy(const std::shared_ptr<AbstractOperator>& copied_input_left,
+                                                  const std::shared_ptr<AbstractOperator>&) const override {
+    return std::make_shared<Aggregate>(copied_input_left, _aggregates, _groupby_column_ids);  // aggregate.cpp:70-74
+  }
 
  private:
   std::vector<AggregateColumnDefinition> _aggregates;
@@ -224,7 +273,19 @@ class Projection final : public AbstractOperator {
 
  protected:
   std::shared_ptr<const Table> _on_execute() override;
+  // projection.cpp:25-33: placeholders in the expressions get their values; a copy deep-copies the expressions
+  void _on_set_parameters(const ParameterMap& parameters) override;
+  std::shared_ptr<AbstractOperator> _on_deep_copy(const std::shared_ptr<AbstractOperator>& copied_input_left,
+                                                  const std::shared_ptr<AbstractOperator>&) const override;
 };
+
+// Operator phase timings (host wall time): recorded while enabled, taken (and cleared) by op_trace_take.
+struct OpTraceRecord {
+  std::string op, phase;
+  double ms;
+};
+void op_trace_enable(bool on);
+std::vector<OpTraceRecord> op_trace_take();
 
 // JoinHashTraits (reference src/lib/operators/join_hash/hash_traits.hpp:9-42) over data types.
 DataType join_hashed_type(DataType left, DataType right);

@@ -101,6 +101,54 @@ std::string ValueExpression::as_column_name() const {  // value_expression.cpp:1
   return stream.str();
 }
 
+DataType ParameterExpression::data_type() const {
+  Assert(_value.has_value(), "Can't obtain type of unset ValuePlaceholder");
+  return data_type_of_variant(*_value);
+}
+
+bool ParameterExpression::is_nullable() const {
+  Assert(_value.has_value(), "Can't obtain nullability of unset ValuePlaceholder");
+  return variant_is_null(*_value);
+}
+
+std::string ParameterExpression::as_column_name() const {
+  std::ostringstream stream;
+  stream << "Parameter[id=" << parameter_id.t << "]";
+  if (_value) {
+    stream << "=";
+    std::visit(
+        [&](const auto& v) {
+          if constexpr (std::is_same_v<std::decay_t<decltype(v)>, NullValue>)
+            stream << "NULL";
+          else
+            stream << v;
+        },
+        *_value);
+  }
+  return stream.str();
+}
+
+void expressions_set_parameters(const std::vector<std::shared_ptr<AbstractExpression>>& expressions,
+                                const std::unordered_map<ParameterID, AllTypeVariant, ParameterIDHash>& parameters) {
+  for (const auto& e : expressions) {
+    if (e->type == ExpressionType::Parameter) {
+      auto& p = static_cast<ParameterExpression&>(*e);
+      const auto it = parameters.find(p.parameter_id);
+      if (it != parameters.end()) p.set_value(it->second);
+    } else {
+      expressions_set_parameters(e->arguments, parameters);
+    }
+  }
+}
+
+std::vector<std::shared_ptr<AbstractExpression>> expressions_deep_copy(
+    const std::vector<std::shared_ptr<AbstractExpression>>& expressions) {
+  std::vector<std::shared_ptr<AbstractExpression>> out;
+  out.reserve(expressions.size());
+  for (const auto& e : expressions) out.push_back(e->deep_copy());
+  return out;
+}
+
 DataType ArithmeticExpression::data_type() const {
   return expression_common_type(left_operand()->data_type(), right_operand()->data_type());
 }
@@ -195,17 +243,25 @@ void compile(const AbstractExpression& e, const Table& in, ExprInput& ei, std::v
       n.type = hy_type_of(in.column_data_type(c.column_id));
       break;
     }
-    case ExpressionType::Value: {
-      const auto& v = static_cast<const ValueExpression&>(e);
+    case ExpressionType::Value:
+    case ExpressionType::Parameter: {
+      // a set placeholder evaluates as a literal of its value (the reference's evaluator reads value())
+      const AllTypeVariant& value = e.type == ExpressionType::Value
+                                        ? static_cast<const ValueExpression&>(e).value
+                                        : [&]() -> const AllTypeVariant& {
+        const auto& p = static_cast<const ParameterExpression&>(e);
+        Assert(p.value().has_value(), "ParameterExpression: Parameter not set, cannot evaluate");
+        return *p.value();
+      }();
       n.kind = HY_EXPR_VALUE;
-      n.type = hy_type_of(v.data_type());  // 0 for NULL
-      Assert(v.data_type() != DataType::String, "hyrise-amd: arithmetic on a string literal");
+      n.type = hy_type_of(data_type_of_variant(value));  // 0 for NULL
+      Assert(data_type_of_variant(value) != DataType::String, "hyrise-amd: arithmetic on a string literal");
       std::visit(
           [&](const auto& x) {
             using V = std::decay_t<decltype(x)>;
             if constexpr (std::is_arithmetic_v<V>) std::memcpy(&n.value, &x, sizeof(V));
           },
-          v.value);
+          value);
       break;
     }
     case ExpressionType::Arithmetic: {
@@ -317,6 +373,13 @@ std::vector<std::shared_ptr<BaseColumn>> materialize_on_host(const Table& in, Co
 }
 
 }  // namespace
+
+void Projection::_on_set_parameters(const ParameterMap& parameters) { expressions_set_parameters(expressions, parameters); }
+
+std::shared_ptr<AbstractOperator> Projection::_on_deep_copy(const std::shared_ptr<AbstractOperator>& copied_input_left,
+                                                            const std::shared_ptr<AbstractOperator>&) const {
+  return std::make_shared<Projection>(copied_input_left, expressions_deep_copy(expressions));
+}
 
 std::shared_ptr<const Table> Projection::_on_execute() {
   const auto in = input_table_left();

@@ -326,7 +326,7 @@ void ChunkEncoder::encode_columns(const std::shared_ptr<Table>& table, const std
     Fail("Encoding type not supported by the device path (only Unencoded and Dictionary)");
   // chunks are independent: encoded in parallel (the reference encodes chunk by chunk in jobs as well)
   const ChunkID n = table->chunk_count();
-  const unsigned workers = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const unsigned workers = std::max(1u, std::min(16u, host_cpu_share()));
   std::atomic<ChunkID> next{0};
   auto work = [&]() {
     for (ChunkID c; (c = next.fetch_add(1)) < n;) {

@@ -26,6 +26,10 @@
 
 namespace hyrise {
 
+// CPUs this process may use: the affinity mask, capped by a cgroup CPU quota (cpu.max) and OMP_NUM_THREADS - a GPU
+// box grants one GPU's share of a larger machine, which std::thread::hardware_concurrency() does not see.
+unsigned host_cpu_share();
+
 class Table;
 struct DeviceColumn;  // device.hpp
 

@@ -25,6 +25,7 @@
 #include <memory>
 #include <mutex>
 #include <stdexcept>
+#include <thread>
 #include <string>
 #include <variant>
 #include <vector>
@@ -105,7 +106,7 @@ class PosList {
     if (this != &o) {
       Vec copy = o.host();
       _v = std::move(copy);
-      _lazy = false;
+      _state.store(HOST, std::memory_order_relaxed);
       _device.reset();
       _single_chunk_id = o._single_chunk_id;
     }
@@ -116,30 +117,30 @@ class PosList {
   static std::shared_ptr<PosList> lazy(size_t n, PosListFetch fetch) {
     auto p = std::make_shared<PosList>();
     p->_lazy_size = n;
-    p->_lazy = n > 0;
+    p->_state.store(n > 0 ? LAZY : HOST, std::memory_order_relaxed);
     p->_fetch = fetch;
     return p;
   }
-  bool is_lazy() const { return _lazy; }
+  bool is_lazy() const { return _state.load(std::memory_order_acquire) != HOST; }
   // makes an empty list lazy in place (lists allocated in an operator's output arena)
   // with its device mirror (a plain store: the list is not shared with any other thread yet)
   void make_lazy(size_t n, PosListFetch fetch, std::shared_ptr<DevicePosList> mirror) {
     _v.clear();
     _lazy_size = n;
-    _lazy = n > 0;
+    _state.store(n > 0 ? LAZY : HOST, std::memory_order_relaxed);
     _fetch = fetch;
     _device = std::move(mirror);
   }
   // the size of a lazy list that is not shared yet (its producer learns the sizes after creating the lists)
   void set_lazy_size(size_t n) {
     _lazy_size = n;
-    _lazy = n > 0;
+    _state.store(n > 0 ? LAZY : HOST, std::memory_order_relaxed);
   }
 
   // sizes need no host copy
-  size_t size() const { return _lazy ? _lazy_size : _v.size(); }
+  size_t size() const { return is_lazy() ? _lazy_size : _v.size(); }
   bool empty() const { return size() == 0; }
-  size_t capacity() const { return _lazy ? _lazy_size : _v.capacity(); }
+  size_t capacity() const { return is_lazy() ? _lazy_size : _v.capacity(); }
   // element and iterator access: the host RowIDs (copied down first when lazy)
   const RowID& operator[](size_t i) const { return host()[i]; }
   RowID& operator[](size_t i) { return host()[i]; }
@@ -188,18 +189,28 @@ class PosList {
   void set_single_chunk_id(ChunkID c) { _single_chunk_id = c; }
 
  private:
+  // The first host access of a lazy list copies it down; concurrent readers of the same list wait for that copy, readers
+  // of other lists are not involved (the state is per list: LAZY -> FETCHING -> HOST).
   Vec& host() const {
     auto& self = const_cast<PosList&>(*this);
-    if (_lazy) {
-      static std::mutex m;
-      std::lock_guard<std::mutex> lock(m);
-      if (_lazy) {
-        self._v.resize(_lazy_size);
-        _fetch(*this, self._v.data());
-        _lazy = false;
-      }
-    }
+    if (_state.load(std::memory_order_acquire) != HOST) self.fetch_once();
     return self._v;
+  }
+  void fetch_once() {
+    uint8_t expected = LAZY;
+    if (_state.compare_exchange_strong(expected, FETCHING, std::memory_order_acq_rel)) {
+      try {
+        _v.resize(_lazy_size);
+        _fetch(*this, _v.data());
+      } catch (...) {
+        _state.store(LAZY, std::memory_order_release);
+        throw;
+      }
+      _state.store(HOST, std::memory_order_release);
+      return;
+    }
+    while (_state.load(std::memory_order_acquire) == FETCHING) std::this_thread::yield();
+    if (_state.load(std::memory_order_acquire) == LAZY) fetch_once();  // (the fetching reader failed: try again)
   }
   Vec& host_mut() { return host(); }
   Vec& mutate() {
@@ -213,7 +224,8 @@ class PosList {
   mutable std::shared_ptr<DevicePosList> _device;
   ChunkID _single_chunk_id = INVALID_CHUNK_ID;
   size_t _lazy_size = 0;
-  mutable bool _lazy = false;
+  static constexpr uint8_t HOST = 0, LAZY = 1, FETCHING = 2;
+  mutable std::atomic<uint8_t> _state{HOST};
   PosListFetch _fetch = nullptr;
 };
 

@@ -56,6 +56,13 @@ hy_status hy_free(void* ptr);
  * long as their table. Freed memory is reused by later allocations ordered after the free on `stream`. */
 hy_status hy_malloc_async(void** ptr, size_t bytes, hy_stream_t stream);
 hy_status hy_free_async(void* ptr, hy_stream_t stream);
+/* Frees `ptr` into the pool on `free_stream` after the work already enqueued on each of `wait_streams` (an event
+ * recorded on each, waited for by `free_stream`): a buffer read by kernels of several non-blocking operator streams
+ * returns to the pool only when all of them are done with it, and a later allocation on `free_stream` reuses it
+ * without any cross-stream dependency. */
+hy_status hy_free_async_after(void* ptr, hy_stream_t free_stream, const hy_stream_t* wait_streams, uint32_t n_wait);
+/* The device pool's bytes held from the driver (reserved) and handed out (used). */
+hy_status hy_pool_stats(uint64_t* reserved_bytes, uint64_t* used_bytes);
 hy_status hy_memcpy_htod(void* dst, const void* src, size_t bytes, hy_stream_t stream);
 hy_status hy_memcpy_dtoh(void* dst, const void* src, size_t bytes, hy_stream_t stream);
 hy_status hy_memcpy_dtod(void* dst, const void* src, size_t bytes, hy_stream_t stream);

@@ -1197,8 +1197,12 @@ ExprAny evaluate(const AbstractExpression& e, const Table& in, ChunkID chunk_id)
     });
     return out;
   }
-  if (e.type == ExpressionType::Value) {
-    const auto& value = static_cast<const ValueExpression&>(e).value;
+  if (e.type == ExpressionType::Value || e.type == ExpressionType::Parameter) {
+    // a placeholder evaluates to its value (expression_evaluator.cpp:536-546)
+    if (e.type == ExpressionType::Parameter && !static_cast<const ParameterExpression&>(e).value())
+      Fail("ParameterExpression: Parameter not set, cannot evaluate");
+    const auto& value = e.type == ExpressionType::Value ? static_cast<const ValueExpression&>(e).value
+                                                        : *static_cast<const ParameterExpression&>(e).value();
     if (variant_is_null(value)) return AllNull{n};
     ExprAny out;
     with_data_type(e.data_type(), [&](auto tag) {
