@@ -80,7 +80,7 @@ def main_operators(args):
             kstats.append({"device_ms": round(sum(k["ms_total"] for k in ks.values()), 3),
                            "top": sorted(((round(k["ms_total"], 3), n) for n, k in ks.items()), reverse=True)[:3]})
         phases.append({f"{op}: {phase}": round(ms, 3) for op, phase, ms in hy.op_trace_take()})
-        pool.append([round(b / 2**30, 2) for b in hy.pool_stats()])
+        pool.append([round(b / 2**30, 2) for b in hy.pool_stats()] + [round(hy.device_memory()[0] / 2**30, 2)])
     hy.op_trace_enable(False)
     step_s = sum(times) / len(times)
     out = join.get_output()
@@ -92,7 +92,7 @@ def main_operators(args):
         "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 3),
         "ms_per_step_runs": [round(t * 1e3, 3) for t in times],
         "release_ms_runs": [round(t * 1e3, 3) for t in releases],
-        "phases_ms_runs": phases, "kernel_stats_runs": kstats or None, "pool_reserved_used_gib_runs": pool, "host_cpu_share": hy.host_cpu_share(),
+        "phases_ms_runs": phases, "kernel_stats_runs": kstats or None, "pool_reserved_used_device_free_gib_runs": pool, "host_cpu_share": hy.host_cpu_share(),
         "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "int32", "data": "synthetic (seeded counter-based TPC-H-shaped columns)",
         "config": {"workload": "TableScan(l_quantity<24) -> JoinHash(orders, scan) via _on_execute", "sf": args.sf,

@@ -83,6 +83,7 @@ build_info = _host.build_info
 op_trace_enable = _host.op_trace_enable
 op_trace_take = _host.op_trace_take
 pool_stats = _host.pool_stats
+device_memory = _host.device_memory
 host_cpu_share = _host.host_cpu_share
 
 from . import capi  # noqa: E402  (ctypes view of the C-ABI)

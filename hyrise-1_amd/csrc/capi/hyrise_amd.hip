@@ -107,6 +107,15 @@ hy_status hy_free_async_after(void* ptr, hy_stream_t free_stream, const hy_strea
   return HY_OK;
 }
 
+hy_status hy_device_memory(uint64_t* free_bytes, uint64_t* total_bytes) {
+  if (!free_bytes || !total_bytes) return fail(HY_ERR_INVALID_ARGUMENT, "NULL output");
+  size_t f = 0, t = 0;
+  HY_HIP(hipMemGetInfo(&f, &t));
+  *free_bytes = f;
+  *total_bytes = t;
+  return HY_OK;
+}
+
 hy_status hy_pool_stats(uint64_t* reserved_bytes, uint64_t* used_bytes) {
   if (!reserved_bytes || !used_bytes) return fail(HY_ERR_INVALID_ARGUMENT, "NULL output");
   int dev = 0;

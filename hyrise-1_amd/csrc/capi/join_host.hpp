@@ -415,6 +415,12 @@ inline int filter_kind(const SidePlan& p) {
 // (part1_mask / part1_spread_mask; HY_FILTER_COMPACT=0). Measured on MI355X at SF100 (round 3): compact 1.43 + 1.52 ms,
 // match bits 0.94 + 3.16 ms with two-tile spans (2.08 ms with one-tile spans) - the match-bit spread pass compacts a
 // span into LDS before its scatter, which halves the resident workgroups and serialises load, compaction and scatter.
+// HY_HASH_RECORDS=0: keep {key, payload} records up to the partition join also where HashSrc applies (A/B).
+inline bool hash_records_enabled() {
+  const char* e = std::getenv("HY_HASH_RECORDS");  // (read per call: a test switches it)
+  return !(e && std::strtol(e, nullptr, 10) == 0);
+}
+
 inline bool filter_compact_enabled() {
   static const bool v = [] {
     const char* e = std::getenv("HY_FILTER_COMPACT");
@@ -526,7 +532,8 @@ hy_status launch_pass0(const char* side_tag, const SidePlan& p, const hyk::Side&
 template <typename T, typename H, typename P>
 hy_status pass0_side(const char* side_tag, const SidePlan& p, SideBufs<H, P>& b, uint32_t bits, uint32_t w0,
                      uint32_t seed, bool keep_nulls, uint32_t ref_base, const hyk::NextDigit& nd, const Common& c,
-                     hipStream_t s, hyk::Rec<H, P>* out, const uint32_t* bloom = nullptr, uint64_t bloom_n = 0) {
+                     hipStream_t s, hyk::Rec<H, P>* out, const uint32_t* bloom = nullptr, uint64_t bloom_n = 0,
+                     bool bloom_by_hash = false) {
   hyk::Side sd{};
   sd.chunks = b.chunks;
   sd.n_chunks = static_cast<uint32_t>(p.chunks.size());
@@ -546,6 +553,8 @@ hy_status pass0_side(const char* side_tag, const SidePlan& p, SideBufs<H, P>& b,
   sd.scan_out = p.scan_out;
   sd.bloom = bloom;
   sd.bloom_mask = bloom ? static_cast<uint32_t>(bloom_n - 1) : 0u;
+  sd.bloom_by_hash = bloom_by_hash ? 1 : 0;
+  sd.seed = seed;
   const uint32_t n_digits = 1u << w0;
   hyk::Digit d0{full_mask(bits), bits - w0, n_digits - 1u, seed, g_key_hash};
   HY_HIP(hipMemsetAsync(b.total, 0, 8, s));
@@ -570,14 +579,32 @@ hy_status pass0_side(const char* side_tag, const SidePlan& p, SideBufs<H, P>& b,
   return HY_OK;
 }
 
+template <typename H, typename P>
+hyk::RecOut<H, P> aos_out(hyk::Rec<H, P>* recs) {
+  return hyk::RecOut<H, P>{recs, nullptr, nullptr, 0u, nullptr, 0u};
+}
+
+// The SoA form of a last record pass (hyk::RecOut / hyk::HashSrc) inside `area`, a record buffer of at least `rows`
+// 8-byte records: 16-bit hash remainders, then (16-byte aligned) the payloads - 6 B per record, so that with rows >= 16
+// both arrays stay readable 3 records past their end (HashSrc's group loads). A build side of a prefiltered join also
+// sets its Bloom words by hash (bloom_n words).
+template <typename H, typename P>
+hyk::RecOut<H, P> soa_out(void* area, uint64_t rows, uint32_t bits, uint32_t* bloom = nullptr, uint64_t bloom_n = 0) {
+  static_assert(sizeof(P) == 4, "SoA records carry 32-bit payloads");
+  auto* hk = static_cast<uint16_t*>(area);
+  auto* pay = reinterpret_cast<P*>(static_cast<char*>(area) + hyk::align16(2 * rows));
+  return hyk::RecOut<H, P>{nullptr, hk, pay, bits, bloom, bloom ? static_cast<uint32_t>(bloom_n - 1) : 0u};
+}
+
 // One record pass over segments sg (tile prefix and owners filled, grid = an upper bound of its tiles): histogram
 // (from the digit bytes dig_in when the previous pass wrote them, else from the records), scan, stable scatter by digit
 // (bits [shift, shift + w)) writing the next pass's digit bytes (nd), then the bounds of the n_groups * 2^w parts.
 template <typename H, typename P>
 hy_status record_pass(const char* side_tag, const SideBufs<H, P>& b, const hyk::Segs& sg, const hyk::Groups& gr,
                       uint32_t n_groups, uint64_t grid, uint32_t bits, uint32_t shift, uint32_t w, uint32_t seed,
-                      const hyk::Rec<H, P>* in, const uint8_t* dig_in, const hyk::NextDigit& nd, hyk::Rec<H, P>* out,
-                      const uint64_t* total, uint32_t* bounds, const Common& c, hipStream_t s, uint64_t rows) {
+                      const hyk::Rec<H, P>* in, const uint8_t* dig_in, const hyk::NextDigit& nd,
+                      const hyk::RecOut<H, P>& out, const uint64_t* total, uint32_t* bounds, const Common& c,
+                      hipStream_t s, uint64_t rows) {
   const uint32_t n_digits = 1u << w;
   hyk::Digit dg{full_mask(bits), shift, n_digits - 1u, seed, g_key_hash};
   if (grid) {
@@ -617,7 +644,7 @@ hy_status local_passes(const char* side_tag, SideBufs<H, P>& b, const std::vecto
                        uint32_t bits, uint32_t seed, hyk::Rec<H, P>* in, hyk::Rec<H, P>* spare, const uint8_t* dig_in,
                        uint8_t* dig_spare, uint32_t* seg, uint32_t* seg_spare, uint64_t n_segs,
                        const uint64_t* total, uint64_t rows, const Common& c, hipStream_t s, hyk::Rec<H, P>** recs,
-                       uint32_t** bounds) {
+                       uint32_t** bounds, const hyk::RecOut<H, P>* last_out = nullptr) {
   uint32_t below = 0;
   for (size_t i = first; i < w.size(); ++i) below += w[i];
   for (size_t i = first; i < w.size(); ++i) {
@@ -637,8 +664,9 @@ hy_status local_passes(const char* side_tag, SideBufs<H, P>& b, const std::vecto
     hyk::Segs sg{seg,     b.seg_tile_begin, b.tile_owner, static_cast<uint32_t>(n_segs), nullptr, nullptr, nullptr,
                  nullptr, sub2()};
     const hyk::NextDigit nd = next_digit(w, i, bits, dig_in ? dig_spare : nullptr);
+    const hyk::RecOut<H, P> out = (last_out && i + 1 == w.size()) ? *last_out : aos_out<H, P>(spare);
     st = record_pass<H, P>(side_tag, b, sg, hyk::Groups{nullptr, nullptr, nullptr}, static_cast<uint32_t>(n_segs), grid,
-                           bits, below, w[i], seed, in, dig_in, nd, spare, total, seg_spare, c, s, rows);
+                           bits, below, w[i], seed, in, dig_in, nd, out, total, seg_spare, c, s, rows);
     if (st != HY_OK) return st;
     std::swap(in, spare);
     std::swap(seg, seg_spare);
@@ -682,15 +710,18 @@ uint32_t lds_table_rows() {
   return rows;
 }
 
-// Per-partition LDS build/probe over partitioned records (partition bounds on the device). probe_rows_hint: an
-// upper bound of the probe rows; it picks the probe records per thread (JP) from the average partition.
-template <typename H, typename P>
+// Per-partition LDS build/probe over partitioned records (partition bounds on the device; the records as the last pass
+// wrote them: hyk::RecSrc or hyk::HashSrc). probe_rows_hint: an upper bound of the probe rows; it picks the probe
+// records per thread (JP) from the average partition. Partitions with more build rows than one LDS table (skewed keys)
+// are listed by join_partition and joined by join_partition_skewed, launched only when the build side is large
+// enough to have one.
+template <typename Src, typename P>
 hy_status run_join_partitions(const uint32_t* build_begin, const uint32_t* probe_begin, uint32_t n_parts,
-                              const hyk::Rec<H, P>* brec, const hyk::Rec<H, P>* precs, const hyk::RowMap& bmap,
-                              const hyk::RowMap& pmap, int32_t mode, hy_row_id* out_build, hy_row_id* out_probe,
-                              uint64_t out_capacity, uint64_t* partition_begin, uint32_t* partition_counts,
-                              hy_join_result* result, const Common& c, hipStream_t s, uint64_t units,
-                              uint64_t probe_rows_hint) {
+                              const Src& bsrc, const Src& psrc, const hyk::RowMap& bmap, const hyk::RowMap& pmap,
+                              int32_t mode, hy_row_id* out_build, hy_row_id* out_probe, uint64_t out_capacity,
+                              uint64_t* partition_begin, uint32_t* partition_counts, hy_join_result* result,
+                              const Common& c, hipStream_t s, uint64_t units, uint64_t probe_rows_hint) {
+  using H = typename Src::Key;
   constexpr int NT = hyk::JOIN_THREADS;
   // probe records per thread per pass: the wide variant (6) when the average partition needs more than 3/4 of JP_PER
   const uint64_t avg_probe = n_parts ? probe_rows_hint / n_parts : 0;
@@ -709,23 +740,38 @@ hy_status run_join_partitions(const uint32_t* build_begin, const uint32_t* probe
   jd.capacity = out_capacity;
   jd.error = c.misc + 1;
   jd.overflow = c.misc + 2;
+  jd.n_skewed = c.misc + 3;
+  jd.skewed = reinterpret_cast<uint32_t*>(c.join_status);  // (2^bits + 1) words of 8 B >= n_parts entries
   jd.total = c.totals + 1;
   jd.trace = g_join_trace;
   HY_HIP(hipMemsetAsync(c.misc, 0, 64 * 4, s));
   HY_HIP(hipMemsetAsync(c.totals, 0, 8 * 2, s));
   if (n_parts) {
-    KTimer kt_("join_partition", s, units);
-    auto launch = [&](auto kernel) {
-      hipLaunchKernelGGL(kernel, dim3(n_parts), dim3(NT), lds, s, jd, brec, precs, out_build, out_probe,
-                         partition_begin, partition_counts);
-    };
-    if (jd.trace)  // debug phase-trace instance (hy_debug_set_join_trace)
-      wide ? launch(hyk::join_partition<H, P, true, 6, NT>) : launch(hyk::join_partition<H, P, true, 4, NT>);
-    else
-      wide ? launch(hyk::join_partition<H, P, false, 6, NT>) : launch(hyk::join_partition<H, P, false, 4, NT>);
-    kt_.done();
+    {
+      KTimer kt_("join_partition", s, units);
+      auto launch = [&](auto kernel) {
+        hipLaunchKernelGGL(kernel, dim3(n_parts), dim3(NT), lds, s, jd, bsrc, psrc, out_build, out_probe,
+                           partition_begin, partition_counts);
+      };
+      constexpr int JW = Src::V == 1 ? 6 : 8;  // the wide variant's probe records per thread (a multiple of V)
+      if (jd.trace)  // debug phase-trace instance (hy_debug_set_join_trace)
+        wide ? launch(hyk::join_partition<Src, P, true, JW, NT>) : launch(hyk::join_partition<Src, P, true, 4, NT>);
+      else
+        wide ? launch(hyk::join_partition<Src, P, false, JW, NT>) : launch(hyk::join_partition<Src, P, false, 4, NT>);
+      kt_.done();
+    }
+    HY_HIP(hipGetLastError());
+    // a partition is skewed only with more than lds_max build rows: at most build_rows / (lds_max + 1) of them
+    const uint64_t build_rows = units > probe_rows_hint ? units - probe_rows_hint : 0;
+    const uint64_t max_skewed = std::min<uint64_t>(n_parts, build_rows / (uint64_t(lds_max) + 1));
+    if (max_skewed) {
+      KTimer kt_("join_partition_skewed", s, units);
+      hipLaunchKernelGGL((hyk::join_partition_skewed<Src, P, NT>), dim3(static_cast<uint32_t>(std::min<uint64_t>(max_skewed, 512))),
+                         dim3(NT), lds, s, jd, bsrc, psrc, out_build, out_probe, partition_begin, partition_counts);
+      kt_.done();
+      HY_HIP(hipGetLastError());
+    }
   }
-  HY_HIP(hipGetLastError());
   if (capture_state().capturing) {
     capture_state().misc = c.misc;
     capture_state().totals = c.totals;
@@ -1026,7 +1072,8 @@ hy_status onepass_side(const char* tag, const SidePlan& p, OneBufs<H>& o, uint32
   const hyk::Groups gr{o.group_hbase, o.group_tiles, o.group_out};
   const uint64_t grid = p.n_rows / span2() + 1 + nseg;
   const hyk::NextDigit nd1 = next_digit(w, 1, bits, b.digB);
-  st = record_pass<H, uint32_t>(tag, b, sg, gr, nd0, grid, bits, bits - w[0] - w1, w1, seed, b.recA, b.digA, nd1, b.recB,
+  st = record_pass<H, uint32_t>(tag, b, sg, gr, nd0, grid, bits, bits - w[0] - w1, w1, seed, b.recA, b.digA, nd1,
+                                aos_out<H, uint32_t>(b.recB),
                                 b.total, b.segA, c, s, p.n_rows);
   if (st != HY_OK) return st;
   if (w.size() == 2) {
@@ -1067,7 +1114,9 @@ hy_status join_typed_onepass(const SidePlan& bp, const SidePlan& pp, const hy_jo
   if (st != HY_OK) return st;
   const hyk::RowMap bmap = bp.fuse ? make_map(ob.b.ref_row_begin, bp.ref_row_begin) : make_map(ob.b.row_begin, bp.row_begin);
   const hyk::RowMap pmap = pp.fuse ? make_map(op.b.ref_row_begin, pp.ref_row_begin) : make_map(op.b.row_begin, pp.row_begin);
-  st = run_join_partitions<H, uint32_t>(bounds[0], bounds[1], 1u << bits, recs[0], recs[1], bmap, pmap, prm->mode,
+  st = run_join_partitions<hyk::RecSrc<H, uint32_t>, uint32_t>(bounds[0], bounds[1], 1u << bits,
+                                                               hyk::RecSrc<H, uint32_t>{recs[0]},
+                                                               hyk::RecSrc<H, uint32_t>{recs[1]}, bmap, pmap, prm->mode,
                                         out_build, out_probe, out_capacity, partition_begin, partition_counts, result,
                                         c, s, bp.n_rows + pp.n_rows, pp.n_rows);
   HY_HIP(hipStreamSynchronize(s));  // the flags' copies (run_join_partitions has synchronised on success)
@@ -1177,6 +1226,20 @@ hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join
     HY_HIP(hipStreamWaitEvent(sb, ss->fork, 0));
   }
 
+  // int32 keys (no string ids) with b >= 16 radix bits: the last record pass keeps 16 hash bits instead of the key
+  // (hyk::HashSrc), 6-byte records for the partition join; a prefilter is then keyed by hash and set by that pass
+  const bool soa = hash_records_enabled() && std::is_same_v<H, int32_t> && g_key_hash == nullptr && w.size() >= 2 &&
+                   bits >= 16 && bp.n_rows >= 16 && pp.n_rows >= 16;  // (>= 16: room for HashSrc's group reads)
+  hyk::RecOut<H, uint32_t> soa_outs[2];
+  if (soa) {
+    if (use_bloom) HY_HIP(hipMemsetAsync(bloom, 0, 4 * bloom_n, s));
+    // the record passes after pass 0 ping-pong recA -> recB -> recA ...: the last one writes recB after an odd count
+    const bool last_in_b = (w.size() - 1) % 2 == 1;
+    soa_outs[0] = soa_out<H, uint32_t>(last_in_b ? bb.recB : bb.recA, bp.n_rows, bits, use_bloom ? bloom : nullptr,
+                                       bloom_n);
+    soa_outs[1] = soa_out<H, uint32_t>(last_in_b ? pb.recB : pb.recA, pp.n_rows, bits);
+  }
+
   hyk::Rec<H>* recs[2] = {nullptr, nullptr};
   uint32_t* bounds[2] = {nullptr, nullptr};
   for (int side = 0; side < 2; ++side) {
@@ -1191,13 +1254,13 @@ hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join
                                                      p.ref_base, nd, cs, st_s, b.recA)
                        : pass0_side<TP, H, uint32_t>(tag, p, b, bits, w.empty() ? 0 : w[0], prm->seed, keep_nulls,
                                                      p.ref_base, nd, cs, st_s, b.recA, use_bloom ? bloom : nullptr,
-                                                     bloom_n);
+                                                     bloom_n, soa);
     if (st != HY_OK) return st;
     st = local_passes<H, uint32_t>(tag, b, w, 1, bits, prm->seed, b.recA, b.recB, nd.bytes, b.digB, b.segA, b.segB,
                                    w.empty() ? 1 : (1ull << w[0]), b.total, p.n_rows, cs, st_s, &recs[side],
-                                   &bounds[side]);
+                                   &bounds[side], soa ? &soa_outs[side] : nullptr);
     if (st != HY_OK) return st;
-    if (side == 0 && use_bloom) {  // the probe side's prefilter over the build side's keys (its records)
+    if (side == 0 && use_bloom && !soa) {  // the probe side's prefilter over the build side's keys (its records)
       HY_HIP(hipMemsetAsync(bloom, 0, 4 * bloom_n, s));
       KTimer kt_("bloom_build", s, p.n_rows);
       hipLaunchKernelGGL(hyk::bloom_build<H>, dim3(static_cast<uint32_t>(std::min<uint64_t>(grid_for(p.n_rows, 256), 4096))),
@@ -1213,9 +1276,22 @@ hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join
   // filtered sides emit RowIDs of their data table (the scan's PosLists dereferenced, write_output_columns)
   const hyk::RowMap bmap = bp.fuse ? make_map(bb.ref_row_begin, bp.ref_row_begin) : make_map(bb.row_begin, bp.row_begin);
   const hyk::RowMap pmap = pp.fuse ? make_map(pb.ref_row_begin, pp.ref_row_begin) : make_map(pb.row_begin, pp.row_begin);
-  return run_join_partitions<H, uint32_t>(bounds[0], bounds[1], 1u << bits, recs[0], recs[1], bmap, pmap, prm->mode,
-                                          out_build, out_probe, out_capacity, partition_begin, partition_counts,
-                                          result, c, s, bp.n_rows + pp.n_rows, pp.n_rows);
+  if (soa) {
+    auto run_hash = [&](auto tag) {
+      using HS = decltype(tag);
+      return run_join_partitions<HS, uint32_t>(bounds[0], bounds[1], 1u << bits, HS{soa_outs[0].hk, soa_outs[0].pay},
+                                               HS{soa_outs[1].hk, soa_outs[1].pay}, bmap, pmap, prm->mode, out_build,
+                                               out_probe, out_capacity, partition_begin, partition_counts, result, c,
+                                               s, bp.n_rows + pp.n_rows, pp.n_rows);
+    };
+    const char* g = std::getenv("HY_HASH_GROUP");  // records per lane and load (A/B): 1 (default) or 4
+    return (g && std::strtol(g, nullptr, 10) == 4) ? run_hash(hyk::HashSrc<uint32_t, 4>{})
+                                                  : run_hash(hyk::HashSrc<uint32_t, 1>{});
+  }
+  return run_join_partitions<hyk::RecSrc<H, uint32_t>, uint32_t>(
+      bounds[0], bounds[1], 1u << bits, hyk::RecSrc<H, uint32_t>{recs[0]}, hyk::RecSrc<H, uint32_t>{recs[1]}, bmap,
+      pmap, prm->mode, out_build, out_probe, out_capacity, partition_begin, partition_counts, result, c, s,
+      bp.n_rows + pp.n_rows, pp.n_rows);
 }
 
 template <typename F>
@@ -1383,7 +1459,8 @@ hy_status recv_side(const char* tag, const RecvPlan& r, RecvBufs<H, P>& rb, cons
   hyk::Groups gr{rb.group_hbase, rb.group_tiles, rb.group_out};
   // the merge pass must not write through a stale histogram entry: hist words are exactly the groups' tiles x digits
   hy_status st = record_pass<H, P>(tag, rb.b, sg, gr, nb, r.tiles, bits, shift, w1, seed, in, nullptr,
-                                   hyk::NextDigit{nullptr, 0, 0}, rb.b.recA, rb.b.total, rb.b.segA, c, s, r.rows);
+                                   hyk::NextDigit{nullptr, 0, 0}, aos_out<H, P>(rb.b.recA), rb.b.total, rb.b.segA, c, s,
+                                   r.rows);
   if (st != HY_OK) return st;
   return local_passes<H, P>(tag, rb.b, w, 2, bits, seed, rb.b.recA, rb.b.recB, nullptr, nullptr, rb.b.segA, rb.b.segB,
                             uint64_t(nb) << w1, rb.b.total, r.rows, c, s, recs, bounds);
@@ -1487,7 +1564,8 @@ hy_status exchange_join_for_hashed(const void* build_records, const void* probe_
     bmap = make_map(b_rows, lay.build_rows);
     pmap = make_map(p_rows, lay.probe_rows);
   }
-  return run_join_partitions<H, P>(bounds[0], bounds[1], n_parts, recs[0], recs[1], bmap, pmap, params->mode,
+  return run_join_partitions<hyk::RecSrc<H, P>, P>(bounds[0], bounds[1], n_parts, hyk::RecSrc<H, P>{recs[0]},
+                                                   hyk::RecSrc<H, P>{recs[1]}, bmap, pmap, params->mode,
                                    out_build, out_probe, out_capacity, partition_begin, partition_counts, result, c, s,
                                    rbp.rows + rpp.rows, rpp.rows);
 }

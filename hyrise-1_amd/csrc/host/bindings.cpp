@@ -364,6 +364,11 @@ PYBIND11_MODULE(_hyrise_host, m) {
     return py::make_tuple(reserved, used);
   });
   m.def("host_cpu_share", &host_cpu_share);
+  m.def("device_memory", []() {
+    uint64_t free_b = 0, total_b = 0;
+    hy_check(hy_device_memory(&free_b, &total_b), "hy_device_memory");
+    return py::make_tuple(free_b, total_b);
+  });
 
   py::class_<OperatorPerformanceData>(m, "OperatorPerformanceData")
       .def_readonly("walltime_ns", &OperatorPerformanceData::walltime_ns)

@@ -43,8 +43,17 @@ std::shared_ptr<DeviceBuffer> upload(const void* host, size_t bytes, hy_stream_t
 }  // namespace
 
 namespace {
-// size classes: powers of two from 4 KiB; at most TEMP_CACHE_BYTES kept per thread
-constexpr size_t TEMP_CACHE_BYTES = size_t(8) << 30;
+// size classes: powers of two from 4 KiB; at most temp_cache_bytes() kept per thread: an eighth of the device's memory
+// (36 GiB on MI355X), at least 8 GiB - enough to keep a JoinHash workspace of an SF100 join (a 16 GiB block):
+// freeing it after every execution costs a hipFree (a device-wide synchronisation and an unmap) per operator call
+size_t temp_cache_bytes() {
+  static const size_t bytes = [] {
+    uint64_t free_b = 0, total_b = 0;
+    if (hy_device_memory(&free_b, &total_b) != HY_OK || total_b == 0) return size_t(8) << 30;
+    return std::max<size_t>(size_t(8) << 30, static_cast<size_t>(total_b / 8));
+  }();
+  return bytes;
+}
 struct TempCache {
   std::vector<std::pair<size_t, void*>> free_blocks;  // (block bytes, ptr)
   size_t cached = 0;
@@ -118,7 +127,7 @@ void* temp_block_acquire(size_t bytes, size_t* block_bytes) {
 
 void temp_block_release(void* ptr, size_t block_bytes) {
   auto& c = temp_cache();
-  if (c.cached + block_bytes > TEMP_CACHE_BYTES) {
+  if (c.cached + block_bytes > temp_cache_bytes()) {
     hy_free(ptr);
     return;
   }

@@ -15,11 +15,12 @@
 //   pass 2  part2_hist / part2_scatter : inside every high-digit bucket, stable scatter by the LOW 8 bits. After
 //           pass 2 every radix partition is contiguous and in row order (MSD, so partition bounds fall out of the
 //           pass-2 histogram).
-//   join    join_partition : one workgroup per partition, taken in partition order by an atomic ticket. The build
-//           partition (~1-2k rows with the reference's radix-bit formula) is hashed into LDS; probe rows stream
-//           through it twice (count, then write) with a decoupled look-back across partitions in between, so the
-//           output of partition p starts right after partition p-1 — one contiguous pair of PosLists.
-// Roofline: HBM. Partition passes move 8 B/row per read or write; the join reads 8 B/row and writes 16 B/pair.
+//   join    join_partition : one workgroup per partition. The build partition (~1-2k rows with the reference's
+//           radix-bit formula) is hashed into LDS; probe records are matched from registers, counted, and written
+//           once one atomic add on the running total has reserved the partition's output range (partitions are
+//           located by their begin / count, so no workgroup waits on another).
+// Roofline: HBM. Partition passes move 8 B/row per read or write; the join reads 8 B/row (6 B for int32 keys with
+// b >= 16 radix bits, whose last pass keeps 16 hash bits instead of the key: HashSrc) and writes 16 B/pair.
 #include <hip/hip_runtime.h>
 
 #include "common.hpp"
@@ -131,6 +132,8 @@ struct Side {
   // stable order of the others (the reference's output is unchanged). The fused scan's output still lists it.
   const uint32_t* bloom;
   uint32_t bloom_mask;  // words - 1 (power of two)
+  int32_t bloom_by_hash;  // the filter is keyed by murmur2(key, seed) (bloom_slot_hash; SoA joins) instead of the key
+  uint32_t seed;
 };
 
 // Bloom filter words: one 32-bit word per key selected by a hash independent of the partition and bucket hashes,
@@ -148,6 +151,13 @@ __device__ __forceinline__ uint2 bloom_slot(H key, uint32_t mask) {
   return make_uint2(static_cast<uint32_t>(h) & mask, (1u << (hi & 31u)) | (1u << ((hi >> 5) & 31u)));
 }
 
+// The same words and bits from the key's murmur2 hash (a join whose build records keep hashes instead of keys).
+__device__ __forceinline__ uint2 bloom_slot_hash(uint32_t h, uint32_t mask) {
+  const uint64_t x = (static_cast<uint64_t>(h) ^ 0x9E3779B97F4A7C15ull) * 0xD6E8FEB86659FD93ull;
+  const uint32_t hi = static_cast<uint32_t>(x >> 32);
+  return make_uint2(static_cast<uint32_t>(x) & mask, (1u << (hi & 31u)) | (1u << ((hi >> 5) & 31u)));
+}
+
 template <typename H>
 __device__ __forceinline__ uint32_t bloom_filter_act(const Side& s, const H (&keys)[PART_ITEMS], uint32_t act) {
   if (s.bloom == nullptr) return act;
@@ -155,7 +165,8 @@ __device__ __forceinline__ uint32_t bloom_filter_act(const Side& s, const H (&ke
   uint32_t bits[PART_ITEMS];
 #pragma unroll
   for (int k = 0; k < PART_ITEMS; ++k) {  // all loads in flight before any test
-    const uint2 sl = bloom_slot<H>(keys[k], s.bloom_mask);
+    const uint2 sl = s.bloom_by_hash ? bloom_slot_hash(murmur2<H>(keys[k], s.seed), s.bloom_mask)
+                                     : bloom_slot<H>(keys[k], s.bloom_mask);
     bits[k] = sl.y;
     words[k] = ((act >> k) & 1u) ? s.bloom[sl.x] : sl.y;
   }
@@ -495,12 +506,51 @@ __device__ __forceinline__ void clear_wave_masks(uint64_t* wave_mask) {
 // tile's digit-d count.
 static_assert(PART_THREADS >= 256, "one thread per digit");
 static_assert(PART_TILE * 8 >= PART_WAVES * 256 * 8, "ranking masks fit the staging area");
+
+// Where a partition pass writes its records: {key, payload} records, or - the last pass of a side whose 4-byte keys
+// murmur2 maps one-to-one onto hashes (int32; see HashSrc) - two arrays: the hash bits above the radix bits (16 of
+// them when radix_bits >= 16; they identify the key inside its partition) and the payloads, 6 B per record instead of
+// 8. A SoA build side of a prefiltered join also sets its Bloom words (by hash, bloom_slot_hash) here.
+template <typename H, typename P>
+struct RecOut {
+  Rec<H, P>* recs;
+  uint16_t* hk;         // non-null: SoA output
+  P* pay;
+  uint32_t hk_shift;    // radix bits
+  uint32_t* bloom;      // or null
+  uint32_t bloom_mask;  // words - 1
+};
+
+template <typename H, typename P>
+__device__ __forceinline__ void store_record(const RecOut<H, P>& out, uint32_t o, const Rec<H, P>& r, uint32_t hash) {
+  if (out.hk != nullptr) {
+    out.hk[o] = static_cast<uint16_t>(hash >> out.hk_shift);
+    out.pay[o] = r.payload;
+    if (out.bloom != nullptr) {
+      const uint2 sl = bloom_slot_hash(hash, out.bloom_mask);
+      atomicOr(out.bloom + sl.x, sl.y);
+    }
+  } else {
+    out.recs[o] = r;
+  }
+}
+
 template <typename H, typename P>
 __device__ __forceinline__ void staged_scatter(const Rec<H, P> (&recs)[PART_ITEMS], uint32_t act,
                                                const uint32_t (&dr)[PART_ITEMS], uint32_t (*s_cnt)[256],
                                                uint32_t* s_delta, Rec<H, P>* s_stage, uint32_t* s_scratch,
                                                uint32_t n_digits, const Digit& dg, const NextDigit& nd,
                                                uint32_t& run, Rec<H, P>* __restrict__ out) {
+  staged_scatter<H, P>(recs, act, dr, s_cnt, s_delta, s_stage, s_scratch, n_digits, dg, nd, run,
+                       RecOut<H, P>{out, nullptr, nullptr, 0u, nullptr, 0u});
+}
+
+template <typename H, typename P>
+__device__ __forceinline__ void staged_scatter(const Rec<H, P> (&recs)[PART_ITEMS], uint32_t act,
+                                               const uint32_t (&dr)[PART_ITEMS], uint32_t (*s_cnt)[256],
+                                               uint32_t* s_delta, Rec<H, P>* s_stage, uint32_t* s_scratch,
+                                               uint32_t n_digits, const Digit& dg, const NextDigit& nd,
+                                               uint32_t& run, const RecOut<H, P>& out) {
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   __syncthreads();  // every wave's counts are in s_cnt
   const uint32_t d = threadIdx.x;
@@ -528,9 +578,10 @@ __device__ __forceinline__ void staged_scatter(const Rec<H, P> (&recs)[PART_ITEM
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < total; i += PART_THREADS) {
     const Rec<H, P> r = s_stage[i];
-    const uint32_t h = key_hash_of<H>(dg, r.key) & dg.mask;
+    const uint32_t hash = key_hash_of<H>(dg, r.key);
+    const uint32_t h = hash & dg.mask;
     const uint32_t o = i + s_delta[(h >> dg.shift) & dg.dmask];
-    out[o] = r;
+    store_record<H, P>(out, o, r, hash);
     if (nd.bytes != nullptr) nd.bytes[o] = static_cast<uint8_t>((h >> nd.shift) & nd.dmask);
   }
 }
@@ -615,8 +666,9 @@ __global__ __launch_bounds__(PART_THREADS) __attribute__((amdgpu_waves_per_eu(4)
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// Pass 1 of a side with a fused TableScan, in two streaming kernels (opt-in, HY_FILTER_COMPACT=1; the default is
-// part1_mask / part1_spread_mask below):
+// Pass 1 of a side with a fused TableScan, in two streaming kernels (the default; HY_FILTER_COMPACT=0 selects
+// part1_mask / part1_spread_mask below, which move 1.9 GB less at SF100 but measured slower: join_host.hpp
+// filter_compact_enabled):
 //   part1_compact: evaluates the predicate and reads the join column of every row of a span once, writes the span's
 //     matching rows as records in row order into the span's own slot of a gapped buffer (slot = span * SPAN
 //     records; no prefix across spans is needed), counts them per digit (histogram rows as part1_hist, plus the scan
@@ -739,8 +791,8 @@ __global__ __launch_bounds__(PART_THREADS) void part1_spread(Side s, Digit dg, N
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// Pass 1 of a side with a fused TableScan, without the gapped record round trip (the default; HY_FILTER_COMPACT=1
-// selects part1_compact / part1_spread above):
+// Pass 1 of a side with a fused TableScan, without the gapped record round trip (HY_FILTER_COMPACT=0; the default is
+// part1_compact / part1_spread above):
 //   part1_mask: the predicate and the join column of every row of a span: digit histogram of the rows that take part
 //     (+ the span's scan-match count as an extra histogram row) and the scan's match bits - one 64-bit ballot per
 //     (tile, wave, item), 1 bit per row. Writes 1/8 B per row instead of an 8-byte record per match.
@@ -1220,8 +1272,7 @@ __global__ __launch_bounds__(PART_THREADS) void part2_hist(Segs sg, Digit dg, ui
 template <typename H, typename P>
 __global__ __launch_bounds__(PART_THREADS) void part2_scatter(Segs sg, Digit dg, NextDigit nd, int dbits,
                                                              uint32_t n_digits, const Rec<H, P>* __restrict__ in,
-                                                             const uint32_t* __restrict__ offsets,
-                                                             Rec<H, P>* __restrict__ out) {
+                                                             const uint32_t* __restrict__ offsets, RecOut<H, P> out) {
   __shared__ uint32_t s_cnt[PART_WAVES][256];
   __shared__ uint32_t s_delta[256];
   __shared__ uint32_t s_scratch[PART_WAVES + 1];
@@ -1484,6 +1535,57 @@ struct JoinDesc {
   uint32_t* overflow;
   uint64_t* total;              // total pairs (written by the last partition)
   uint64_t* trace;              // debug phase stamps (hy_debug_set_join_trace) or null
+  uint32_t* skewed;             // partitions with more build rows than one LDS table (n_parts entries)
+  uint32_t* n_skewed;           // their count (zeroed before join_partition)
+};
+
+// Record sources of the partition join: what the last partition pass wrote.
+// load_group(i, keys, pays) reads the V records i .. i + V - 1 (i a multiple of V; up to V - 1 records past a side's
+// last one may be read and are ignored), so that a lane's consecutive records come in one vector load per array.
+template <typename H, typename P>
+struct RecSrc {  // {key, payload} records
+  using Key = H;
+  static constexpr int V = 1;
+  const Rec<H, P>* __restrict__ r;
+  __device__ __forceinline__ Rec<H, P> operator[](uint32_t i) const { return r[i]; }
+  __device__ __forceinline__ void load_group(uint32_t i, H (&k)[V], P (&p)[V]) const {
+    const Rec<H, P> x = r[i];
+    k[0] = x.key;
+    p[0] = x.payload;
+  }
+};
+// Hash records (RecOut's SoA form). murmur2 of a 4-byte key is a bijection: every step of murmur_hash.cpp:36-49, 68-70
+// on a 4-byte input - multiplications by the odd constant m, xor-shifts, the xor with (seed ^ 4) * m - is invertible.
+// So inside one radix partition (hash & (2^b - 1) fixed) two int32 keys are equal exactly when their hash bits above
+// the partition bits are; with b >= 16 those 32 - b <= 16 bits stand in for the key (6 B per record instead of 8).
+// GV records per lane and group: GV = 4 loads them with one 8-byte load of their remainders and one 16-byte load of
+// their payloads; GV = 1 takes one record per lane (2- and 4-byte loads, the stores of consecutive lanes adjacent).
+template <typename P, int GV = 1>
+struct HashSrc {
+  static_assert(sizeof(P) == 4, "hash records carry 32-bit payloads");
+  static_assert(GV == 1 || GV == 4, "groups of 1 or 4 records");
+  using Key = uint16_t;
+  static constexpr int V = GV;
+  const uint16_t* __restrict__ hk;  // 16-byte aligned; readable 3 records past the last
+  const P* __restrict__ pay;        // 16-byte aligned; readable 3 records past the last
+  __device__ __forceinline__ Rec<uint16_t, P> operator[](uint32_t i) const { return Rec<uint16_t, P>{hk[i], pay[i]}; }
+  __device__ __forceinline__ void load_group(uint32_t i, uint16_t (&k)[V], P (&p)[V]) const {
+    if constexpr (V == 1) {
+      k[0] = hk[i];
+      p[0] = pay[i];
+    } else {
+      const uint2 kk = *reinterpret_cast<const uint2*>(hk + i);
+      const uint4 pp = *reinterpret_cast<const uint4*>(pay + i);
+      k[0] = static_cast<uint16_t>(kk.x);
+      k[1] = static_cast<uint16_t>(kk.x >> 16);
+      k[2] = static_cast<uint16_t>(kk.y);
+      k[3] = static_cast<uint16_t>(kk.y >> 16);
+      p[0] = pp.x;
+      p[1] = pp.y;
+      p[2] = pp.z;
+      p[3] = pp.w;
+    }
+  }
 };
 
 template <typename H, typename P>
@@ -1558,27 +1660,39 @@ template <int NT>
 constexpr int build_per() {  // >= the largest 4-byte-key table in the default LDS budget / NT
   return NT >= 1024 ? 3 : 14;
 }
-template <typename H, typename P, int NT>
-__device__ __forceinline__ void build_table(const BTable<H, P>& t, const Rec<H, P>* __restrict__ build, uint32_t b0,
+template <typename Src, typename P, int NT>
+__device__ __forceinline__ void build_table(const BTable<typename Src::Key, P>& t, const Src& build, uint32_t b0,
                                             uint32_t n, uint32_t* s_scratch) {
-  Rec<H, P> r[build_per<NT>()];
+  using H = typename Src::Key;
+  constexpr int V = Src::V;                           // consecutive records per lane and group
+  constexpr int G = (build_per<NT>() + V - 1) / V;    // groups per lane and batch
+  constexpr uint32_t BATCH = G * V * NT;
+  // groups start at multiples of V: records [a0, a0 + lead) before the partition are loaded and ignored
+  const uint32_t a0 = b0 & ~uint32_t(V - 1), lead = b0 - a0, nr = n + lead;
+  H key[G][V];
+  P pay[G][V];
   auto load_batch = [&](uint32_t base) {
 #pragma unroll
-    for (int q = 0; q < build_per<NT>(); ++q) {
-      const uint32_t i = base + q * NT + threadIdx.x;
-      if (i < n) r[q] = build[b0 + i];
+    for (int q = 0; q < G; ++q) {
+      const uint32_t r = base + (q * NT + threadIdx.x) * V;
+      if (r < nr) build.load_group(a0 + r, key[q], pay[q]);
     }
   };
-  constexpr uint32_t BATCH = build_per<NT>() * NT;
+  auto in = [&](uint32_t base, int q, int v) {
+    const uint32_t r = base + (q * NT + threadIdx.x) * V + v;
+    return r >= lead && r < nr;
+  };
   load_batch(0);
   for (uint32_t i = threadIdx.x; i < t.NB; i += NT) t.end[i] = 0;
   __syncthreads();
   // pass 1: bucket sizes
-  for (uint32_t base = 0; base < n; base += BATCH) {
+  for (uint32_t base = 0; base < nr; base += BATCH) {
     if (base) load_batch(base);
 #pragma unroll
-    for (int q = 0; q < build_per<NT>(); ++q)
-      if (base + q * NT + threadIdx.x < n) atomicAdd(&t.end[bucket_of<H>(r[q].key, t.NB)], 1u);
+    for (int q = 0; q < G; ++q)
+#pragma unroll
+      for (int v = 0; v < V; ++v)
+        if (in(base, q, v)) atomicAdd(&t.end[bucket_of<H>(key[q][v], t.NB)], 1u);
   }
   __syncthreads();
   // bucket sizes -> bucket starts (each thread owns a contiguous run of buckets)
@@ -1595,13 +1709,16 @@ __device__ __forceinline__ void build_table(const BTable<H, P>& t, const Rec<H, 
   }
   __syncthreads();
   // pass 2: claim slots; afterwards end[b] is the end of bucket b
-  for (uint32_t base = 0; base < n; base += BATCH) {
-    if (base || n > BATCH) load_batch(base);
+  for (uint32_t base = 0; base < nr; base += BATCH) {
+    if (base || nr > BATCH) load_batch(base);
 #pragma unroll
-    for (int q = 0; q < build_per<NT>(); ++q) {
-      if (base + q * NT + threadIdx.x < n) {
-        const uint32_t pos = atomicAdd(&t.end[bucket_of<H>(r[q].key, t.NB)], 1u);
-        t.ents[pos] = r[q];
+    for (int q = 0; q < G; ++q) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        if (in(base, q, v)) {
+          const uint32_t pos = atomicAdd(&t.end[bucket_of<H>(key[q][v], t.NB)], 1u);
+          t.ents[pos] = Rec<H, P>{key[q][v], pay[q][v]};
+        }
       }
     }
   }
@@ -1695,12 +1812,12 @@ __device__ __forceinline__ uint32_t record_pos(uint32_t e, int k, const uint32_t
 }
 
 // Writes the build rows with `key` among build records [b0, b0 + n) in order, each paired with prow.
-template <typename H, typename P>
-__device__ __forceinline__ void write_duplicates(const JoinDesc& d, const Rec<H, P>* __restrict__ build, uint32_t b0,
-                                                 uint32_t n, H key, uint32_t count, hy_row_id prow, uint64_t o,
+template <typename Src>
+__device__ __forceinline__ void write_duplicates(const JoinDesc& d, const Src& build, uint32_t b0, uint32_t n,
+                                                 typename Src::Key key, uint32_t count, hy_row_id prow, uint64_t o,
                                                  hy_row_id* __restrict__ out_build, hy_row_id* __restrict__ out_probe) {
   for (uint32_t i = 0, m = 0; i < n && m < count; ++i) {
-    const Rec<H, P> br = build[b0 + i];
+    const auto br = build[b0 + i];
     if (br.key == key) {
       out_build[o] = map_row(d.build_map, br.payload);
       out_probe[o] = prow;
@@ -1711,50 +1828,65 @@ __device__ __forceinline__ void write_duplicates(const JoinDesc& d, const Rec<H,
 }
 
 // A partition whose build side fits one LDS table (the common case): the table is built once and every probe
-// record's (count, first entry) stays in registers from counting to writing.
-template <typename H, typename P, bool TRACE, int JP, int NT>
+// record's (count, first entry) stays in registers from counting to writing. A lane takes its records in groups of
+// Src::V consecutive ones (JP / V groups per pass), so the records' order is (pass, group, thread, record in group):
+// pass_offsets places the groups, a lane its group's records one after the other.
+template <typename Src, typename P, bool TRACE, int JP, int NT>
 __device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t p, unsigned char* smem,
-                                                    const Rec<H, P>* __restrict__ build,
-                                                    const Rec<H, P>* __restrict__ probe, hy_row_id* __restrict__ out_build,
-                                                    hy_row_id* __restrict__ out_probe,
+                                                    const Src& build, const Src& probe,
+                                                    hy_row_id* __restrict__ out_build, hy_row_id* __restrict__ out_probe,
                                                     uint64_t* __restrict__ part_out_begin,
                                                     uint32_t* __restrict__ part_out_count, uint32_t* s_tot,
                                                     uint64_t* s_base) {
+  using H = typename Src::Key;
+  constexpr int V = Src::V;
+  constexpr int K = JP / V;  // groups per thread per pass
+  static_assert(K * V == JP, "JP is a multiple of the group size");
   const uint32_t bb = d.build_begin[p], nb = d.build_begin[p + 1] - bb;
   const uint32_t pb = d.probe_begin[p], np = d.probe_begin[p + 1] - pb;
   const int mode = d.mode;
   const BTable<H, P> t = table_at<H, P>(smem, nb);
-  build_table<H, P, NT>(t, build, bb, nb, s_tot);
-  trace_stamp<TRACE>(d, p, 1);
-
-  // Per probe record only its payload and match info (count << 16 | first entry) stay in registers.
+  // groups start at multiples of V: probe records [a0, a0 + lead) before the partition are loaded and ignored
+  const uint32_t a0 = pb & ~uint32_t(V - 1), lead = pb - a0, nr = np + lead;
   constexpr uint32_t JP_PASS_ = JP * NT;
-  const uint32_t n_pass = (np + JP_PASS_ - 1) / JP_PASS_;
-  P ppay[JP];
-  uint32_t pinfo[JP];
-  auto load_and_match = [&](uint32_t pass) {
-    Rec<H, P> pr[JP];
-#pragma unroll
-    for (int k = 0; k < JP; ++k) {
-      const uint32_t j = pass * JP_PASS_ + k * NT + threadIdx.x;
-      if (j < np) pr[k] = probe[pb + j];
-    }
-#pragma unroll
-    for (int k = 0; k < JP; ++k) {
-      const uint32_t j = pass * JP_PASS_ + k * NT + threadIdx.x;
-      ppay[k] = pr[k].payload;
-      pinfo[k] = j < np ? table_lookup<H, P>(t, pr[k].key) : 0u;
-    }
+  const uint32_t n_pass = (nr + JP_PASS_ - 1) / JP_PASS_;
+  auto rel = [&](uint32_t pass, int k, int v) { return pass * JP_PASS_ + (k * NT + threadIdx.x) * V + v; };
+  auto in = [&](uint32_t pass, int k, int v) {
+    const uint32_t r = rel(pass, k, v);
+    return r >= lead && r < nr;
   };
+  // Per probe record only its payload and match info (count << 16 | first entry) stay in registers.
+  H key[K][V];
+  P ppay[K][V];
+  uint32_t pinfo[K][V];
+  auto load = [&](uint32_t pass) {
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      if (rel(pass, k, 0) < nr) probe.load_group(a0 + rel(pass, k, 0), key[k], ppay[k]);
+  };
+  auto match = [&](uint32_t pass) {
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+      for (int v = 0; v < V; ++v) pinfo[k][v] = in(pass, k, v) ? table_lookup<H, P>(t, key[k][v]) : 0u;
+  };
+  auto emit = [&](uint32_t pass, int k, int v) { return in(pass, k, v) ? emitted_for(mode, info_count(pinfo[k][v])) : 0u; };
+
+  // records of <= 8 bytes: the first pass's probe records are in flight while the table is built (wider ones would
+  // spill at this kernel's register budget)
+  constexpr bool PREFETCH = sizeof(Rec<H, P>) <= 8;
+  if (PREFETCH) load(0);
+  build_table<Src, P, NT>(t, build, bb, nb, s_tot);
+  trace_stamp<TRACE>(d, p, 1);
 
   uint32_t my = 0;
   for (uint32_t pass = 0; pass < n_pass; ++pass) {
-    load_and_match(pass);
+    if (pass || !PREFETCH) load(pass);
+    match(pass);
 #pragma unroll
-    for (int k = 0; k < JP; ++k) {
-      const uint32_t j = pass * JP_PASS_ + k * NT + threadIdx.x;
-      if (j < np) my += emitted_for(mode, info_count(pinfo[k]));
-    }
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+      for (int v = 0; v < V; ++v) my += emit(pass, k, v);
   }
   trace_stamp<TRACE>(d, p, 2);
   uint32_t part_total;
@@ -1765,30 +1897,39 @@ __device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t 
 
   uint64_t run = obase;
   for (uint32_t pass = 0; pass < n_pass; ++pass) {
-    if (n_pass > 1) load_and_match(pass);  // a single pass still holds its records and matches in registers
+    if (n_pass > 1) {  // a single pass still holds its records and matches in registers
+      load(pass);
+      match(pass);
+    }
     auto e_of = [&](int k) {
-      const uint32_t j = pass * JP_PASS_ + k * NT + threadIdx.x;
-      return j < np ? emitted_for(mode, info_count(pinfo[k])) : 0u;
-    };
-    const uint32_t pass_total = pass_offsets<JP, NT>(e_of, s_tot);
+      uint32_t e = 0;
 #pragma unroll
-    for (int k = 0; k < JP; ++k) {
-      const uint32_t c = info_count(pinfo[k]);
-      const uint32_t j = pass * JP_PASS_ + k * NT + threadIdx.x;
-      const uint32_t e = j < np ? emitted_for(mode, c) : 0u;
-      const uint64_t o = run + record_pos<JP, NT>(e, k, s_tot);
-      if (e == 0) continue;
-      const hy_row_id prow = map_row(d.probe_map, ppay[k]);
-      if (mode == HY_JOIN_SEMI || mode == HY_JOIN_ANTI) {
-        out_probe[o] = prow;
-      } else if (c == 0) {  // outer: probe row without a match
-        out_build[o] = hy_row_id{0xFFFFFFFFu, 0xFFFFFFFFu};
-        out_probe[o] = prow;
-      } else if (c == 1) {
-        out_build[o] = map_row(d.build_map, t.ents[info_index(pinfo[k])].payload);
-        out_probe[o] = prow;
-      } else {
-        write_duplicates<H, P>(d, build, bb, nb, t.ents[info_index(pinfo[k])].key, c, prow, o, out_build, out_probe);
+      for (int v = 0; v < V; ++v) e += emit(pass, k, v);
+      return e;
+    };
+    const uint32_t pass_total = pass_offsets<K, NT>(e_of, s_tot);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      uint64_t o = run + record_pos<K, NT>(e_of(k), k, s_tot);
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const uint32_t c = info_count(pinfo[k][v]);
+        const uint32_t e = emit(pass, k, v);
+        if (e == 0) continue;
+        const hy_row_id prow = map_row(d.probe_map, ppay[k][v]);
+        if (mode == HY_JOIN_SEMI || mode == HY_JOIN_ANTI) {
+          out_probe[o] = prow;
+        } else if (c == 0) {  // outer: probe row without a match
+          out_build[o] = hy_row_id{0xFFFFFFFFu, 0xFFFFFFFFu};
+          out_probe[o] = prow;
+        } else if (c == 1) {
+          out_build[o] = map_row(d.build_map, t.ents[info_index(pinfo[k][v])].payload);
+          out_probe[o] = prow;
+        } else {
+          write_duplicates<Src>(d, build, bb, nb, t.ents[info_index(pinfo[k][v])].key, c, prow, o, out_build,
+                                out_probe);
+        }
+        o += e;
       }
     }
     run += pass_total;
@@ -1799,20 +1940,21 @@ __device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t 
 // A partition with more build rows than one LDS table holds (skewed keys): consecutive sub-tables of L build rows.
 // Counts are summed over the sub-tables; matches are written sub-table by sub-table, i.e. in build order. Each
 // probe pass rebuilds the sub-tables twice (count, write), a cost only skewed partitions pay.
-template <typename H, typename P, bool TRACE, int NT>
+constexpr int JS_PER = 2;  // probe records per thread per pass of a skewed partition (1024-thread workgroups)
+template <typename Src, typename P, int NT>
 __device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t p, unsigned char* smem,
-                                                  const Rec<H, P>* __restrict__ build, const Rec<H, P>* __restrict__ probe,
-                                                  hy_row_id* __restrict__ out_build, hy_row_id* __restrict__ out_probe,
-                                                  uint64_t* __restrict__ part_out_begin,
-                                                  uint32_t* __restrict__ part_out_count, uint32_t* s_tot,
-                                                  uint64_t* s_base) {
+                                                     const Src& build, const Src& probe,
+                                                     hy_row_id* __restrict__ out_build, hy_row_id* __restrict__ out_probe,
+                                                     uint64_t* __restrict__ part_out_begin,
+                                                     uint32_t* __restrict__ part_out_count, uint32_t* s_tot,
+                                                     uint64_t* s_base) {
+  using H = typename Src::Key;
   const uint32_t bb = d.build_begin[p], nb = d.build_begin[p + 1] - bb;
   const uint32_t pb = d.probe_begin[p], np = d.probe_begin[p + 1] - pb;
   const uint32_t L = d.lds_max_build;
   const uint32_t n_sub = (nb + L - 1) / L;
   const int mode = d.mode;
-  constexpr int JS = NT >= 1024 ? 2 : 8;  // probe records per thread per pass (few: keeps this rare path's
-                                         // registers within the fast path's budget)
+  constexpr int JS = JS_PER;
   constexpr uint32_t JS_PASS = JS * NT;
   const uint32_t n_pass = (np + JS_PASS - 1) / JS_PASS;
 
@@ -1828,7 +1970,7 @@ __device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t
     for (uint32_t sub = 0; sub < n_sub; ++sub) {
       const uint32_t b0 = bb + sub * L, n = (sub + 1 == n_sub) ? nb - sub * L : L;
       const BTable<H, P> t = table_at<H, P>(smem, n);
-      build_table<H, P, NT>(t, build, b0, n, s_tot);
+      build_table<Src, P, NT>(t, build, b0, n, s_tot);
 #pragma unroll
       for (int k = 0; k < JS; ++k) {
         const uint32_t j = pass * JS_PASS + k * NT + threadIdx.x;
@@ -1847,11 +1989,9 @@ __device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t
       if (j < np) my += emitted_for(mode, pcn[k]);
     }
   }
-  trace_stamp<TRACE>(d, p, 2);
   uint32_t part_total;
   block_exclusive_sum<NT>(my, s_tot, &part_total);
   const uint64_t obase = allocate_output(d, p, part_total, part_out_begin, part_out_count, s_base);
-  trace_stamp<TRACE>(d, p, 3);
   if (obase + part_total > d.capacity) return;
 
   uint64_t run = obase;
@@ -1880,7 +2020,7 @@ __device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t
       for (uint32_t sub = 0; sub < n_sub; ++sub) {
         const uint32_t b0 = bb + sub * L, n = (sub + 1 == n_sub) ? nb - sub * L : L;
         const BTable<H, P> t = table_at<H, P>(smem, n);
-        build_table<H, P, NT>(t, build, b0, n, s_tot);
+        build_table<Src, P, NT>(t, build, b0, n, s_tot);
 #pragma unroll
         for (int k = 0; k < JS; ++k) {
           const uint32_t j = pass * JS_PASS + k * NT + threadIdx.x;
@@ -1894,7 +2034,7 @@ __device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t
             out_build[o] = map_row(d.build_map, t.ents[info_index(info)].payload);
             out_probe[o] = prow;
           } else {
-            write_duplicates<H, P>(d, build, b0, n, pr[k].key, cnt, prow, o, out_build, out_probe);
+            write_duplicates<Src>(d, build, b0, n, pr[k].key, cnt, prow, o, out_build, out_probe);
           }
           pos[k] += cnt;
         }
@@ -1905,25 +2045,45 @@ __device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t
   }
 }
 
-template <typename H, typename P, bool TRACE, int JP, int NT>
+// One 1024-thread workgroup per partition whose build side fits one LDS table - every partition unless keys are
+// skewed. A skewed partition is appended to d.skewed and left to join_partition_skewed, so that this kernel carries
+// only the fast path's registers (the sub-table path would spill at this kernel's 8-waves-per-SIMD budget).
+template <typename Src, typename P, bool TRACE, int JP, int NT>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT >= 1024 ? 8 : 4, 8))) void join_partition(
-    JoinDesc d, const Rec<H, P>* __restrict__ build, const Rec<H, P>* __restrict__ probe,
-    hy_row_id* __restrict__ out_build, hy_row_id* __restrict__ out_probe, uint64_t* __restrict__ part_out_begin,
-    uint32_t* __restrict__ part_out_count) {
+    JoinDesc d, Src build, Src probe, hy_row_id* __restrict__ out_build, hy_row_id* __restrict__ out_probe,
+    uint64_t* __restrict__ part_out_begin, uint32_t* __restrict__ part_out_count) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr int JS = NT >= 1024 ? 2 : 8;
-  __shared__ uint32_t s_tot[(JP > JS ? JP : JS) * (NT / WAVE) + 1];
+  __shared__ uint32_t s_tot[JP * (NT / WAVE) + 1];
   __shared__ uint64_t s_base;
   const uint32_t p = blockIdx.x;
   if (p >= d.n_parts) return;
+  if (d.build_begin[p + 1] - d.build_begin[p] > d.lds_max_build) {
+    if (threadIdx.x == 0) d.skewed[atomicAdd(d.n_skewed, 1u)] = p;
+    return;
+  }
   trace_stamp<TRACE>(d, p, 0);
-  if (d.build_begin[p + 1] - d.build_begin[p] <= d.lds_max_build)
-    partition_one_table<H, P, TRACE, JP, NT>(d, p, smem, build, probe, out_build, out_probe, part_out_begin,
+  partition_one_table<Src, P, TRACE, JP, NT>(d, p, smem, build, probe, out_build, out_probe, part_out_begin,
                                              part_out_count, s_tot, &s_base);
-  else
-    partition_sub_tables<H, P, TRACE, NT>(d, p, smem, build, probe, out_build, out_probe, part_out_begin,
-                                          part_out_count, s_tot, &s_base);
   trace_stamp<TRACE>(d, p, 4);
+}
+
+// The skewed partitions join_partition listed (launched after it on the same stream): a small grid loops over them.
+// Partition ranges are located by part_out_begin / count, so their order in the buffer does not matter.
+template <typename Src, typename P, int NT>
+__global__ __launch_bounds__(NT) void join_partition_skewed(JoinDesc d, Src build, Src probe,
+                                                            hy_row_id* __restrict__ out_build,
+                                                            hy_row_id* __restrict__ out_probe,
+                                                            uint64_t* __restrict__ part_out_begin,
+                                                            uint32_t* __restrict__ part_out_count) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ uint32_t s_tot[JS_PER * (NT / WAVE) + 1];
+  __shared__ uint64_t s_base;
+  const uint32_t n = *d.n_skewed;
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    partition_sub_tables<Src, P, NT>(d, d.skewed[i], smem, build, probe, out_build, out_probe, part_out_begin,
+                                     part_out_count, s_tot, &s_base);
+    __syncthreads();  // s_tot / s_base / LDS reused by the next partition
+  }
 }
 
 static __global__ void murmur_kernel_u32(const uint32_t* keys, uint64_t n, uint32_t seed, uint32_t* out) {

@@ -63,6 +63,8 @@ hy_status hy_free_async(void* ptr, hy_stream_t stream);
 hy_status hy_free_async_after(void* ptr, hy_stream_t free_stream, const hy_stream_t* wait_streams, uint32_t n_wait);
 /* The device pool's bytes held from the driver (reserved) and handed out (used). */
 hy_status hy_pool_stats(uint64_t* reserved_bytes, uint64_t* used_bytes);
+/* Free and total memory of the current device (hipMemGetInfo). */
+hy_status hy_device_memory(uint64_t* free_bytes, uint64_t* total_bytes);
 hy_status hy_memcpy_htod(void* dst, const void* src, size_t bytes, hy_stream_t stream);
 hy_status hy_memcpy_dtoh(void* dst, const void* src, size_t bytes, hy_stream_t stream);
 hy_status hy_memcpy_dtod(void* dst, const void* src, size_t bytes, hy_stream_t stream);

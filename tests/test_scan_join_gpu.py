@@ -301,3 +301,47 @@ def test_prepared_plan_graph_replay(hy):
     finally:
         L.hy_scan_join_plan_destroy(plan)
         L.hy_stream_destroy(stream)
+
+
+@pytest.mark.parametrize("bits", [16, 18])
+@pytest.mark.parametrize("mode", ["Inner", "Left", "Semi", "Anti"])
+@pytest.mark.parametrize("variant", ["hash_records", "skewed", "bloom", "key_records"])
+def test_hash_records(hy, oracle, monkeypatch, bits, mode, variant):
+    """int32 keys with b >= 16 radix bits: the last partition pass keeps the 16 murmur2 bits above the partition
+    instead of the key (6-byte SoA records; murmur2 is a bijection on 4-byte keys, so equal remainders inside a
+    partition are equal keys). Duplicate build keys, NULL probe keys, unmatched rows; `skewed` caps the LDS tables at
+    a few dozen rows so every partition goes through join_partition_skewed, `bloom` forces the probe-side prefilter
+    (then keyed by hash and set by the build side's last pass), `key_records` is HY_HASH_RECORDS=0. Output equals the
+    oracle's at the same radix bits, partition by partition."""
+    if variant == "skewed":
+        monkeypatch.setenv("HY_JOIN_LDS_BUDGET", "1024")
+    if variant == "bloom":
+        monkeypatch.setenv("HY_JOIN_BLOOM", "1")
+    if variant == "key_records":
+        monkeypatch.setenv("HY_HASH_RECORDS", "0")
+    capi = hy.capi
+    rng = np.random.default_rng(zlib.crc32(repr(("hash_records", bits, mode, variant)).encode()))
+    okey, ostatus, lkey, lkey_nulls, qty, qty_nulls = orders_lineitem(rng, 25_000, True)
+    lchunk, ochunk = 7_000, 4_000
+    lineitem = hy.Table.from_arrays([("l_orderkey", hy.DataType.Int, True), ("l_quantity", hy.DataType.Float, True)],
+                                    [lkey, qty], [lkey_nulls, qty_nulls], lchunk)
+    orders = hy.Table.from_arrays([("o_orderkey", hy.DataType.Int, False), ("o_status", hy.DataType.Int, False)],
+                                  [okey, ostatus], [], ochunk)
+    probe_t = oracle.table_scan(lineitem, 1, hy.PredicateCondition.LessThan, 30.0, [])
+    jm = getattr(hy.JoinMode, mode)
+    expected, used = oracle.join_hash(orders, probe_t, jm, (0, 0), radix_bits=bits)
+    assert used == bits
+    lk = dt.DeviceColumn(capi, lkey, lkey_nulls, lchunk, "Unencoded")
+    lq = dt.DeviceColumn(capi, qty, qty_nulls, lchunk, "Dictionary")
+    ok = dt.DeviceColumn(capi, okey, None, ochunk, "Unencoded")
+    lf = Filter(capi, lq, "LessThan", 30.0)
+    swapped = mode in ("Left", "Semi", "Anti") or orders.row_count() > probe_t.row_count()
+    params = capi.JoinParams({"Inner": 0, "Left": 1, "Semi": 5, "Anti": 6}[mode], capi.HY_TYPE_INT32, bits, 17)
+    cap_pairs = okey.size * 3 + lkey.size + 16
+    o_side, l_side = dt.join_side(capi, ok), dt.join_side(capi, lk)
+    if swapped:
+        parts = run_fused(hy, l_side, lf.f, o_side, None, params, cap_pairs)
+    else:
+        parts = run_fused(hy, o_side, None, l_side, lf.f, params, cap_pairs)
+    check_scan(probe_t, lf)
+    check_join(expected, parts, 2, swapped, mode in ("Semi", "Anti"))
