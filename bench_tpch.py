@@ -518,8 +518,8 @@ def main_q1(args):
     that the Aggregate then reads; here the two arithmetic expressions are expression columns of hy_aggregate,
     evaluated (in float, as the reference computes them) in the aggregation kernel, and every column is read through
     the scan's PosLists once - nothing is materialised. --q1-materialize runs the two hy_projection launches first
-    instead (A/B). Float SUM/AVG are exact (rounded once); they are checked against float64 torch sums of the same
-    float32 values (relative 1e-9), counts and SUM(l_quantity) exactly."""
+    instead (A/B). Float SUM/AVG are exact (rounded once); every sum is checked for equality with the correctly
+    rounded exact sum of the same float32 values (gsum), counts exactly."""
     import numpy as np
     import torch
 
@@ -564,7 +564,19 @@ def main_q1(args):
     sel = [gkey == g for g in range(6)]
 
     def gsum(v):
-        return [float(torch.sum(torch.where(m, v.to(torch.float64), 0.0))) for m in sel]
+        """Per group the correctly rounded double of the EXACT sum of the float32 values v: every value is an integer
+        mantissa times a power of two, so the int64 sums of the mantissas per (group, exponent) are exact (at most 2^30
+        rows x 2^24 per bucket), and one Python integer per group combines them; int / int rounds correctly."""
+        bits = v.contiguous().view(torch.int32)
+        e = (bits >> 23) & 0xFF
+        assert not bool((e == 0xFF).any()), "non-finite value"
+        m = ((bits & 0x7FFFFF) | torch.where(e > 0, 1 << 23, 0)).to(torch.int64)
+        m = torch.where(bits < 0, -m, m)
+        key = gkey.to(torch.int64) * 256 + torch.clamp(e, min=1).to(torch.int64)  # subnormals: exponent of e = 1
+        keep = gkey >= 0
+        buckets = torch.zeros(6 * 256, dtype=torch.int64, device=v.device).index_add_(0, key[keep], m[keep])
+        b = buckets.view(6, 256).cpu().tolist()
+        return [sum(int(x) << (ex - 1) for ex, x in enumerate(row) if x) / (1 << 149) for row in b]
 
     exp = {"count": [int(m.sum()) for m in sel], "qty": gsum(cols["l_quantity"]), "price": gsum(price),
            "disc_price": gsum(dp), "charge": gsum(ch), "disc": gsum(disc)}
@@ -796,7 +808,6 @@ def main_q1(args):
         capi.check(L.hy_agg_float_sum(limbs, lay.agg_limbs[a], lay.agg_emin[a], int(r[w + 1]), ctypes.byref(out)))
         return out.value
 
-    close = lambda a, b: abs(a - b) <= 1e-9 * max(1.0, abs(b))
     ok = n_match == n_match_exp and n_groups == sum(1 for c in exp["count"] if c)
     groups = {}
     for r in rec:
@@ -806,9 +817,11 @@ def main_q1(args):
                 "sum_charge": fsum(r, 3), "count_order": rows}
         vals["avg_qty"], vals["avg_price"] = vals["sum_qty"] / rows, vals["sum_base_price"] / rows
         vals["avg_disc"] = fsum(r, 6) / rows
+        # every float sum is the correctly rounded exact sum (aggregate.cpp:168-179 adds sequentially in double; the
+        # device accumulates exactly and rounds once): compared for equality
         ok &= rows == exp["count"][g] and vals["sum_qty"] == exp["qty"][g]
-        ok &= close(vals["sum_base_price"], exp["price"][g]) and close(vals["sum_disc_price"], exp["disc_price"][g])
-        ok &= close(vals["sum_charge"], exp["charge"][g]) and close(fsum(r, 6), exp["disc"][g])
+        ok &= vals["sum_base_price"] == exp["price"][g] and vals["sum_disc_price"] == exp["disc_price"][g]
+        ok &= vals["sum_charge"] == exp["charge"][g] and fsum(r, 6) == exp["disc"][g]
         groups["ANR"[int(r[0])] + "FO"[int(r[1])]] = vals
     if not ok:
         raise SystemExit(f"q1 result mismatch: {groups} vs {exp}")

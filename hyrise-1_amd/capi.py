@@ -46,7 +46,7 @@ HY_MIXED_CHUNKS = 0xFFFFFFFF
 
 class JoinChunk(ctypes.Structure):
     _fields_ = [("column", ColumnChunk), ("pos_list", ctypes.c_void_p), ("size", ctypes.c_uint32),
-                ("chunk_id", ctypes.c_uint32), ("single_chunk", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+                ("chunk_id", ctypes.c_uint32), ("single_chunk", ctypes.c_uint32), ("referenced_offset", ctypes.c_uint32)]
 
 
 class JoinSide(ctypes.Structure):

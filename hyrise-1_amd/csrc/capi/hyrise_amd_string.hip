@@ -7,9 +7,10 @@
 // 22-31, 86-97) with the LikeMatcher (like_matcher.cpp:9-118), and IsNullTableScanImpl for string value columns.
 // Dictionary chunks keep the host's dictionary rewrite (op + search_vid, or the LIKE id set) exactly as hy_table_scan.
 //
-// LIKE on the device: the pattern compiles (on the host, per call) to a bit-parallel NFA over at most 63 positions -
-// per position a byte set (a literal byte, '_' = any byte, a [...] class of the regex path) or a '%' star; per input
-// byte c: S = ((S & lit[c]) << 1) | (S & star & star_ok[c]), then the star closure S |= (S & star) << 1. The
+// LIKE on the device: the pattern compiles (on the host, per call) to a bit-parallel NFA over up to 1023 positions
+// (one 64-bit word per 64 of them; patterns of up to 63 positions take a one-word fast path) - per position a byte
+// set (a literal byte, '_' = any byte, a [...] class of the regex path) or a '%' star; per input byte c:
+// S = ((S & lit[c]) << 1) | (S & star & star_ok[c]), then the star closure S |= (S & star) << 1. The
 // reference's simple patterns ('abc%', '%abc', '%abc%', '%a%b%...%') are plain string searches: their '%' and '_'
 // match any byte. Other patterns take the reference's regex path (pattern -> ECMAScript '^...$', every regex special
 // escaped except '[' ']'): '_' and '%' become '.', which does not match '\n' or '\r', and [...] is a class.
@@ -33,15 +34,18 @@ using namespace hyc;
 namespace {
 
 constexpr int STR_THREADS = 256;
-constexpr int LIKE_MAX_POSITIONS = 63;
+constexpr int LIKE_MAX_WORDS = 16;                           // 64-bit state words of the NFA
+constexpr int LIKE_MAX_POSITIONS = 64 * LIKE_MAX_WORDS - 1;  // 1023 positions (+ the accept bit)
 
-// The compiled LIKE pattern (device copy in the workspace).
+// The compiled LIKE pattern (device copy in the workspace): a bitset NFA of `words` 64-bit words, position j in bit
+// j % 64 of word j / 64.
 struct LikeNfa {
-  uint64_t lit[256];      // bit j: position j accepts byte c
-  uint64_t star_ok[256];  // bit j: star position j may consume byte c
-  uint64_t star;          // star positions
-  uint64_t accept;        // bit m
-  uint64_t start;         // closure of position 0
+  uint64_t lit[256][LIKE_MAX_WORDS];      // bit j: position j accepts byte c
+  uint64_t star_ok[256][LIKE_MAX_WORDS];  // bit j: star position j may consume byte c
+  uint64_t star[LIKE_MAX_WORDS];          // star positions
+  uint64_t accept[LIKE_MAX_WORDS];        // bit m
+  uint64_t start[LIKE_MAX_WORDS];         // closure of position 0
+  uint32_t words;
 };
 
 struct StrPred {
@@ -58,13 +62,54 @@ __host__ __device__ inline uint64_t star_closure(uint64_t s, uint64_t star) {
   }
 }
 
-__device__ inline bool like_match(const LikeNfa& a, const unsigned char* p, uint32_t n) {
-  uint64_t s = a.start;
-  for (uint32_t i = 0; i < n && s; ++i) {
-    const unsigned c = p[i];
-    s = star_closure(((s & a.lit[c]) << 1) | (s & a.star & a.star_ok[c]), a.star);
+// The closure over a state of several words: a star position's successor is active too (carries cross words).
+__host__ __device__ inline void star_closure_words(uint64_t (&s)[LIKE_MAX_WORDS], const uint64_t* star, uint32_t words) {
+  for (bool changed = true; changed;) {
+    changed = false;
+    uint64_t carry = 0;
+#pragma unroll
+    for (int w = 0; w < LIKE_MAX_WORDS; ++w) {
+      if (w >= static_cast<int>(words)) break;
+      const uint64_t t = s[w] & star[w];
+      const uint64_t n = s[w] | (t << 1) | carry;
+      carry = t >> 63;
+      changed |= n != s[w];
+      s[w] = n;
+    }
   }
-  return (s & a.accept) != 0;
+}
+
+__device__ inline bool like_match(const LikeNfa& a, const unsigned char* p, uint32_t n) {
+  if (a.words == 1) {  // patterns of up to 63 positions: one word
+    uint64_t s = a.start[0];
+    for (uint32_t i = 0; i < n && s; ++i) {
+      const unsigned c = p[i];
+      s = star_closure(((s & a.lit[c][0]) << 1) | (s & a.star[0] & a.star_ok[c][0]), a.star[0]);
+    }
+    return (s & a.accept[0]) != 0;
+  }
+  uint64_t s[LIKE_MAX_WORDS];
+#pragma unroll
+  for (int w = 0; w < LIKE_MAX_WORDS; ++w) s[w] = w < static_cast<int>(a.words) ? a.start[w] : 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const unsigned c = p[i];
+    uint64_t carry = 0, any = 0;
+#pragma unroll
+    for (int w = 0; w < LIKE_MAX_WORDS; ++w) {
+      if (w >= static_cast<int>(a.words)) break;
+      const uint64_t adv = s[w] & a.lit[c][w];
+      s[w] = (adv << 1) | carry | (s[w] & a.star[w] & a.star_ok[c][w]);
+      carry = adv >> 63;
+      any |= s[w];
+    }
+    if (!any) return false;
+    star_closure_words(s, a.star, a.words);
+  }
+  uint64_t hit = 0;
+#pragma unroll
+  for (int w = 0; w < LIKE_MAX_WORDS; ++w)
+    if (w < static_cast<int>(a.words)) hit |= s[w] & a.accept[w];
+  return hit != 0;
 }
 
 // Row `off` of a scan chunk: the reference's predicate for a dictionary chunk (value id vs search_vid / id set, as
@@ -142,74 +187,119 @@ __global__ __launch_bounds__(STR_THREADS) void string_reference_flags(const hy_r
 }
 
 // ---- host: the LIKE pattern's NFA ----
+// The reference's regex text of a LIKE pattern (like_matcher.cpp:104-125, sql_like_to_regex without the anchors):
+// backslash doubled first, then the regex specials escaped, '%' -> ".*", '_' -> "." - inside [...] too.
+std::string like_to_regex(const char* pattern, uint32_t len) {
+  std::string r;
+  for (uint32_t i = 0; i < len; ++i) {
+    const char ch = pattern[i];
+    switch (ch) {
+      case '\\':
+        r += "\\\\";
+        break;
+      case '.': case '^': case '$': case '+': case '?': case '(': case ')': case '{': case '}': case '|': case '*':
+        r += '\\';
+        r += ch;
+        break;
+      case '%':
+        r += ".*";
+        break;
+      case '_':
+        r += '.';
+        break;
+      default:
+        r += ch;
+    }
+  }
+  return r;
+}
+
 hy_status compile_like(const char* pattern, uint32_t len, int32_t regex, LikeNfa* a) {
   std::memset(a, 0, sizeof(*a));
   int m = 0;
+  auto bit = [](uint64_t* words, int j) { words[j >> 6] |= 1ull << (j & 63); };
   auto position = [&](bool star) -> int {
     if (m >= LIKE_MAX_POSITIONS) return -1;
-    if (star) a->star |= 1ull << m;
+    if (star) bit(a->star, m);
     return m++;
   };
+  const char* too_long = "LIKE pattern longer than 1023 positions";
   const auto newline = [](unsigned c) { return c == '\n' || c == '\r'; };
-  for (uint32_t i = 0; i < len; ++i) {
-    const unsigned char ch = static_cast<unsigned char>(pattern[i]);
-    if (ch == '%') {
-      const int j = position(true);
-      if (j < 0) return fail(HY_ERR_UNSUPPORTED, "LIKE pattern longer than 63 positions");
-      for (unsigned c = 0; c < 256; ++c)
-        if (!(regex && newline(c))) a->star_ok[c] |= 1ull << j;
-    } else if (ch == '_') {
-      const int j = position(false);
-      if (j < 0) return fail(HY_ERR_UNSUPPORTED, "LIKE pattern longer than 63 positions");
-      for (unsigned c = 0; c < 256; ++c)
-        if (!(regex && newline(c))) a->lit[c] |= 1ull << j;
-    } else if (regex && ch == '[') {
-      // a character class of the regex the reference builds: members until ']'; '%' became ".*" and '_' "." there
-      // (both literal inside a class), every other byte is literal; "x-y" is a range of plain bytes
-      uint32_t k = i + 1;
-      std::vector<unsigned char> mem;
-      bool closed = false;
-      const int j = position(false);
-      if (j < 0) return fail(HY_ERR_UNSUPPORTED, "LIKE pattern longer than 63 positions");
-      while (k < len) {
-        const unsigned char x = static_cast<unsigned char>(pattern[k]);
-        if (x == ']' && k > i + 1) {
-          closed = true;
-          break;
-        }
-        if (x == ']') {  // "[]": the empty class matches nothing
-          closed = true;
-          break;
-        }
-        if (k + 2 < len && pattern[k + 1] == '-' && pattern[k + 2] != ']') {
-          const unsigned char y = static_cast<unsigned char>(pattern[k + 2]);
-          if (x == '%' || x == '_' || y == '%' || y == '_' || y < x)
-            return fail(HY_ERR_UNSUPPORTED, "LIKE character class range");
-          for (unsigned c = x; c <= y; ++c) mem.push_back(static_cast<unsigned char>(c));
-          k += 3;
-          continue;
-        }
-        if (x == '%') {
-          mem.push_back('.');
-          mem.push_back('*');
-        } else if (x == '_') {
-          mem.push_back('.');
-        } else {
-          mem.push_back(x);
-        }
-        ++k;
+  if (!regex) {  // the reference's string-search patterns: '%' any bytes, '_' any byte, everything else literal
+    for (uint32_t i = 0; i < len; ++i) {
+      const unsigned char ch = static_cast<unsigned char>(pattern[i]);
+      const int j = position(ch == '%');
+      if (j < 0) return fail(HY_ERR_UNSUPPORTED, too_long);
+      for (unsigned c = 0; c < 256; ++c) {
+        if (ch == '%') bit(a->star_ok[c], j);
+        else if (ch == '_' || c == ch) bit(a->lit[c], j);
       }
-      if (!closed) return fail(HY_ERR_UNSUPPORTED, "unterminated [ in a LIKE pattern (the reference's regex fails)");
-      for (const unsigned char c : mem) a->lit[c] |= 1ull << j;
-      i = k;
-    } else {  // (a ']' outside a class is a literal byte, as libstdc++'s ECMAScript grammar reads it)
-      const int j = position(false);
-      if (j < 0) return fail(HY_ERR_UNSUPPORTED, "LIKE pattern longer than 63 positions");
-      a->lit[ch] |= 1ull << j;
+    }
+  } else {
+    // the reference's std::regex (ECMAScript) over the regex text: '.' any byte but '\n' / '\r', ".*" a star of it,
+    // "\x" the literal x, [...] a class (members: "\x" escapes and plain bytes, "x-y" ranges; "[]" matches nothing),
+    // every other byte literal (a ']' outside a class too, as libstdc++ reads it)
+    const std::string re = like_to_regex(pattern, len);
+    const uint32_t n = static_cast<uint32_t>(re.size());
+    for (uint32_t i = 0; i < n; ++i) {
+      const unsigned char ch = static_cast<unsigned char>(re[i]);
+      if (ch == '.' && i + 1 < n && re[i + 1] == '*') {
+        const int j = position(true);
+        if (j < 0) return fail(HY_ERR_UNSUPPORTED, too_long);
+        for (unsigned c = 0; c < 256; ++c)
+          if (!newline(c)) bit(a->star_ok[c], j);
+        ++i;
+      } else if (ch == '.') {
+        const int j = position(false);
+        if (j < 0) return fail(HY_ERR_UNSUPPORTED, too_long);
+        for (unsigned c = 0; c < 256; ++c)
+          if (!newline(c)) bit(a->lit[c], j);
+      } else if (ch == '\\' && i + 1 < n) {
+        const int j = position(false);
+        if (j < 0) return fail(HY_ERR_UNSUPPORTED, too_long);
+        bit(a->lit[static_cast<unsigned char>(re[++i])], j);
+      } else if (ch == '[') {
+        const int j = position(false);
+        if (j < 0) return fail(HY_ERR_UNSUPPORTED, too_long);
+        uint32_t k = i + 1;
+        // one class atom at k: an escaped or plain byte; returns the byte and advances k
+        auto atom = [&](uint32_t& at) -> unsigned char {
+          if (re[at] == '\\' && at + 1 < n) {
+            at += 2;
+            return static_cast<unsigned char>(re[at - 1]);
+          }
+          return static_cast<unsigned char>(re[at++]);
+        };
+        bool closed = false;
+        while (k < n) {
+          if (re[k] == ']') {  // (the first ']' closes: "[]" is the empty class)
+            closed = true;
+            break;
+          }
+          const unsigned char x = atom(k);
+          if (k + 1 < n && re[k] == '-' && re[k + 1] != ']') {
+            uint32_t k2 = k + 1;
+            const unsigned char y = atom(k2);
+            if (y < x) return fail(HY_ERR_INVALID_ARGUMENT, "LIKE character class range out of order (the reference's regex fails)");
+            for (unsigned c = x; c <= y; ++c) bit(a->lit[c], j);
+            k = k2;
+          } else {
+            bit(a->lit[x], j);
+          }
+        }
+        if (!closed) return fail(HY_ERR_INVALID_ARGUMENT, "unterminated [ in a LIKE pattern (the reference's regex fails)");
+        i = k;
+      } else {
+        const int j = position(false);
+        if (j < 0) return fail(HY_ERR_UNSUPPORTED, too_long);
+        bit(a->lit[ch], j);
+      }
     }
   }
-  a->accept = 1ull << m;
-  a->start = star_closure(1ull, a->star);
+  bit(a->accept, m);
+  a->words = static_cast<uint32_t>(m / 64 + 1);
+  a->start[0] = 1;
+  star_closure_words(a->start, a->star, a->words);
   return HY_OK;
 }
 

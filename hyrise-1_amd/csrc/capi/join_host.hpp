@@ -167,6 +167,7 @@ inline hy_status plan_side(const hy_join_side* side, SidePlan& p) {
       return fail(HY_ERR_UNSUPPORTED, "join chunk kind (RunLength / FrameOfReference: join the value mirror)");
     p.chunks[i] = src_from(c.column, c.pos_list, c.size, rows, c.single_chunk);
     p.chunks[i].chunk_id = c.chunk_id;
+    p.chunks[i].ref_offset = c.pos_list ? c.referenced_offset : 0u;
     p.row_begin[i] = rows;
     rows += c.size;
   }
@@ -186,9 +187,14 @@ inline hy_status plan_side(const hy_join_side* side, SidePlan& p) {
       rr += side->referenced[i].size;
     }
     p.ref_row_begin[side->n_referenced] = rr;
-    for (const auto& c : p.chunks)
+    for (const auto& c : p.chunks) {
       if (c.pos_list && c.single_chunk != HY_MIXED_CHUNKS && c.single_chunk >= side->n_referenced)
         return fail(HY_ERR_INVALID_ARGUMENT, "single_chunk outside the referenced chunks");
+      if (c.pos_list && c.ref_offset > side->n_referenced)
+        return fail(HY_ERR_INVALID_ARGUMENT, "referenced_offset outside the referenced chunks");
+      if (c.ref_offset && side->fuse_dereference)
+        return fail(HY_ERR_INVALID_ARGUMENT, "fuse_dereference needs one referenced table");
+    }
     if (rr >= 0xFFFFFFFFull) return fail(HY_ERR_UNSUPPORTED, "referenced table exceeds 2^32-1 rows");
   }
   return HY_OK;

@@ -61,6 +61,8 @@ struct SrcChunk {
   int32_t kind;
   int32_t vid_width;
   uint64_t row_begin;         // first row of this chunk in the side's row space
+  uint32_t ref_offset;        // reference chunk: index in Side::referenced of its table's first chunk (several
+                              // referenced tables are concatenated there)
 };
 
 // Maps a 32-bit global row index of some table to its RowID.
@@ -228,7 +230,7 @@ __device__ __forceinline__ bool load_row(const Side& s, const SrcChunk& c, uint3
       valid = false;
       *payload = s.fuse_deref ? ref_payload<P>(false, rid, 0) : own_payload<P>(c.row_begin, c.chunk_id, off);
     } else {
-      const uint32_t rc = rid.chunk_id - s.ref_base;
+      const uint32_t rc = rid.chunk_id - s.ref_base + c.ref_offset;
       valid = read_column_value<T>(s.referenced[rc], rid.chunk_offset, &v, false);
       *payload = s.fuse_deref ? ref_payload<P>(true, rid, s.referenced_row_begin[rc])
                               : own_payload<P>(c.row_begin, c.chunk_id, off);

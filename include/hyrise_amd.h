@@ -398,10 +398,13 @@ typedef struct hy_join_chunk {
   const hy_row_id* pos_list;   /* reference-table chunk: device PosList of this chunk, or NULL */
   uint32_t size;               /* rows of this chunk (== column.size or PosList length) */
   uint32_t chunk_id;           /* chunk id of this chunk in its table */
-  uint32_t single_chunk;       /* reference chunk: id of the only referenced chunk when every non-NULL RowID of
-                                  pos_list points into it (e.g. a TableScan output over a data table), else
-                                  HY_MIXED_CHUNKS. Zero-initialised descriptors must set it. */
-  uint32_t reserved;
+  uint32_t single_chunk;       /* reference chunk: index in the side's `referenced` array of the only referenced
+                                  chunk when every non-NULL RowID of pos_list points into it (e.g. a TableScan output
+                                  over a data table), else HY_MIXED_CHUNKS. Zero-initialised descriptors must set it. */
+  uint32_t referenced_offset;  /* reference chunk: index in `referenced` of the first chunk of the table its PosList
+                                  references - a column whose chunks reference several tables lists those tables'
+                                  chunks one table after the other (RowID chunk_id c then reads referenced[
+                                  referenced_offset + c - referenced_chunk_base]); 0 with one referenced table */
 } hy_join_chunk;
 
 typedef struct hy_join_side {

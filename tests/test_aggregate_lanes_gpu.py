@@ -346,3 +346,75 @@ def test_fused_scan_filter(hy, monkeypatch, case, pred_enc, cond, value):
         monkeypatch.setenv("HY_AGG_VEC", vec_mode)
         res = run(hy, dcols, None, sizes, doms, filt=(chunks, capi.HY_TYPE_INT32, pred.constant(value)))
         check(res, expected(cols, rows))
+
+
+@pytest.mark.parametrize("case", ["clean", "nulls", "drift"])
+@pytest.mark.parametrize("cond,value", [("LessThanEquals", 300), ("GreaterThan", 700)])
+def test_fused_scan_filter_against_oracle(hy, oracle, monkeypatch, case, cond, value):
+    """agg_dense_vec with the TableScan fused (TPC-H 1's default plan) against the ORACLE's plan on the same table:
+    oracle TableScan (single_column_table_scan_impl.cpp) -> Projection of the two float expressions
+    (projection.cpp:39-87) -> Aggregate (aggregate.cpp:203-249, sequential double sums). Group keys, counts and int
+    sums equal; every float SUM / AVG is the exactly rounded sum (== math.fsum of the projected values) and within
+    1 ULP of the oracle's sequential sum, the north star's bar."""
+    capi, L = hy.capi, hy.capi.lib
+    rng = np.random.default_rng(zlib.crc32(f"vec-oracle/{case}/{cond}/{value}".encode()))
+    cols = columns(rng, case)
+    rf, ls, qty, price, disc, tax, iq, price_n, disc_n, doms = cols
+    ship = rng.integers(0, 1000, N).astype(np.int32)
+    dcols = [dt.DeviceColumn(capi, rf, None, CHUNK, "Dictionary"), dt.DeviceColumn(capi, ls, None, CHUNK, "Dictionary"),
+             dt.DeviceColumn(capi, qty, None, CHUNK, "Dictionary"),
+             dt.DeviceColumn(capi, price, price_n if price_n.any() else None, CHUNK,
+                             "Dictionary" if case == "nulls" else "Unencoded"),
+             dt.DeviceColumn(capi, disc, disc_n if disc_n.any() else None, CHUNK, "Dictionary"),
+             dt.DeviceColumn(capi, tax, None, CHUNK, "Dictionary"), dt.DeviceColumn(capi, iq, None, CHUNK, "Unencoded")]
+    pred = dt.DeviceColumn(capi, ship, None, CHUNK, "Dictionary")
+    sizes = [d.size for d in dcols[0].descs]
+    monkeypatch.setenv("HY_AGG_VEC", "2")
+    L.hy_kernel_stats_enable(1)
+    L.hy_kernel_stats_reset()
+    res = run(hy, dcols, None, sizes, doms,
+              filt=(pred.scan_chunks(cond, value), capi.HY_TYPE_INT32, pred.constant(value)))
+    ran = kernels_ran(L)
+    L.hy_kernel_stats_enable(0)
+    assert "agg_dense_vec" in ran, ran
+
+    # the oracle's plan over a table of the same columns
+    T = hy.DataType
+    table = hy.Table.from_arrays(
+        [("rf", T.Int, False), ("ls", T.Int, False), ("qty", T.Float, False), ("price", T.Float, True),
+         ("disc", T.Float, True), ("tax", T.Float, False), ("iq", T.Int, False), ("ship", T.Int, False)],
+        [rf, ls, qty, price, disc, tax, iq, ship], [None, None, None, price_n, disc_n, None, None, None], CHUNK)
+    hy.encode_columns(table, [7], hy.EncodingType.Dictionary)
+    scan = oracle.table_scan(table, 7, getattr(hy.PredicateCondition, cond), value, [])
+    c = lambda i: hy.PQPColumnExpression.from_table(scan, i)
+    A = hy.ArithmeticOperator
+    one = hy.ValueExpression(1)
+    dp = hy.ArithmeticExpression(A.Multiplication, c(3), hy.ArithmeticExpression(A.Subtraction, one, c(4)))
+    ch = hy.ArithmeticExpression(A.Multiplication, dp, hy.ArithmeticExpression(A.Addition, one, c(5)))
+    ie = hy.ArithmeticExpression(A.Subtraction, hy.ArithmeticExpression(A.Multiplication, c(6), hy.ValueExpression(3)),
+                                 hy.ValueExpression(7))
+    # projected columns in the C-ABI test's numbering: 0 rf, 1 ls, 2 qty, 3 price, 4 dp, 5 ch, 6 disc, 7 tax, 8 iq, 9 ie
+    proj = oracle.projection(scan, [c(0), c(1), c(2), c(3), dp, ch, c(4), c(5), c(6), ie])
+    F = {"SUM": "Sum", "AVG": "Avg", "COUNT": "Count"}
+    defs = [hy.AggregateColumnDefinition(None if col < 0 else col, getattr(hy.AggregateFunction, F[f]))
+            for f, col in AGGS]
+    agg = oracle.aggregate(proj, defs, [0, 1])
+    want = {(r[0], r[1]): r[2:] for r in agg.rows()}
+    proj_rows = proj.rows()
+    assert set(res) == set(want)
+    for g, vals in res.items():
+        members = [r for r in proj_rows if (r[0], r[1]) == g]
+        for a, (f, col) in enumerate(AGGS):
+            w = want[g][a]
+            if f == "COUNT":
+                got = vals["rows"] if col < 0 else vals[a]
+                assert got == w, (g, f, col)
+                continue
+            n, s = vals[a]
+            if col in (8, 9):  # int32 inputs: int64 sums, exact
+                assert (s if f == "SUM" else s / n) == w, (g, f, col)
+                continue
+            exact = math.fsum(r[col] for r in members if r[col] is not None)
+            got = s if f == "SUM" else s / n
+            assert s == exact, (g, f, col)  # the exactly rounded sum
+            assert abs(int(np.float64(got).view(np.int64)) - int(np.float64(w).view(np.int64))) <= 1, (g, f, col, got, w)

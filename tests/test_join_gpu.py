@@ -151,3 +151,36 @@ def test_encoded_join_columns(hy, oracle, encoding, mode):
         j.execute()
         exp, _ = oracle.join_hash(left, right, getattr(hy.JoinMode, mode), (0, 0))
         assert_identical(j.get_output(), exp)
+
+
+@pytest.mark.parametrize("mode", ["Inner", "Left", "Semi", "Anti"])
+def test_join_column_referencing_several_tables(hy, oracle, mode):
+    """A reference input whose chunks reference different tables (e.g. two scans' outputs appended into one table):
+    every row's key is read from its own chunk's table, as the reference's ReferenceColumn iterable does
+    (join_hash.cpp:248-276); the output columns name chunk 0's table, as write_output_columns does (:595-598).
+    RowID-exact against the oracle, with and without a single referenced chunk per PosList."""
+    rng = np.random.default_rng(77)
+    T = hy.DataType
+    tabs = []
+    for seed in range(3):
+        k = rng.integers(0, 2_000, 9_000).astype(np.int32)
+        v = np.arange(9_000, dtype=np.int32) + seed * 100_000
+        tabs.append(hy.Table.from_arrays([("k", T.Int, False), ("v", T.Int, False)], [k, v], [], 3_000))
+    hy.encode_chunks(tabs[1], [0, 2], hy.EncodingType.Dictionary)
+    ref = hy.Table([("k", T.Int, False), ("v", T.Int, False)], hy.TableType.References)
+    for i in range(7):
+        t = tabs[i % 3]
+        if i % 2:  # a PosList into one chunk of the table
+            c = int(rng.integers(0, 3))
+            pl = np.stack([np.full(1_500, c), rng.integers(0, 3_000, 1_500)], axis=1).astype(np.uint32)
+        else:  # a PosList across the table's chunks, NULL RowIDs included
+            pl = np.stack([rng.integers(0, 3, 2_000), rng.integers(0, 3_000, 2_000)], axis=1).astype(np.uint32)
+            pl[rng.random(2_000) < 0.02] = 0xFFFFFFFF
+        ref.append_chunk([hy.ReferenceColumn(t, 0, pl), hy.ReferenceColumn(t, 1, pl)])
+    other = hy.Table.from_arrays([("k", T.Int, False)], [rng.integers(0, 2_500, 12_000).astype(np.int32)], [], 4_000)
+    for left, right in ((ref, other), (other, ref)):
+        j = hy.JoinHash(wrap(hy, left), wrap(hy, right), getattr(hy.JoinMode, mode), (0, 0),
+                        hy.PredicateCondition.Equals)
+        j.execute()
+        exp, _ = oracle.join_hash(left, right, getattr(hy.JoinMode, mode), (0, 0))
+        assert_identical(j.get_output(), exp)

@@ -59,7 +59,7 @@ EDGE_VALUES = ["a]b", "a]bc", "ab", "a\nb", "a\rb", "a.b", "a*b", "ac", "", "[x"
                "Dampf", "dampf", "Dampfschiff", "schifffahrt", "a%b", "%", "_"]
 EDGE_PATTERNS = ["a]_%", "a]b", "a_b", "%%", "a[.]b", "a[%]b", "a[b-d]", "a[]b", "[[]x", "a[^b]", "_%_", "",
                  "a[-]b", "%\x80%", "a[\\]b", "a\nb", "%a%b", "%a%b%", "a%", "%b", "%_%", "D_mpf%", "__", "%[xz]",
-                 "a[.-z]b"]
+                 "a[.-z]b", "a[_-z]b", "a[%-z]b", "[*-.]%", "a[^-b]"]
 
 
 def edge_table(hy, rng, n, chunk, encode_chunks):
@@ -82,6 +82,36 @@ def test_like_edge_patterns(hy, oracle):
             check(hy, oracle, w, 1, cond, pattern)
     with pytest.raises(RuntimeError):  # the reference's std::regex rejects an unterminated class
         device_scan(hy, w, 1, "Like", "[a")
+    with pytest.raises(RuntimeError):  # "[a-%]" is the regex class "[a-.*]": a range out of order
+        device_scan(hy, w, 1, "Like", "a[a-%]b")
+
+
+def test_like_long_patterns(hy, oracle):
+    """Patterns of 64 to ~700 NFA positions (more than one 64-bit state word; the reference's std::regex takes any
+    length): '_' runs, '%' between them, [...] classes, literal runs, on long strings - against the oracle's
+    std::regex, on value chunks mixed with dictionary chunks."""
+    rng = np.random.default_rng(0x4C4F4E)
+    base = ["".join(rng.choice(list("ab"), rng.integers(40, 220))) for _ in range(300)]
+    t = hy.Table([("a", hy.DataType.Int, False), ("s", hy.DataType.String, True)], hy.TableType.Data, 1_499)
+    for i in range(6_000):
+        t.append([i, None if rng.random() < 0.03 else base[rng.integers(0, len(base))]])
+    hy.encode_chunks(t, [1], hy.EncodingType.Dictionary)
+    w = wrap(hy, t)
+    v = base[0]
+    patterns = [
+        "_" * 130 + "%",                                   # strings of >= 130 bytes
+        "%" + "a_" * 40 + "%",                             # 80 positions + stars
+        v[:100].replace("b", "_", 7) + "%",                # a 101-position prefix pattern
+        "[ab]" * 70 + "%",                                 # 70 classes
+        "%" + "%".join(v[i:i + 9] for i in range(0, 90, 9)) + "%",  # ten literal runs with stars (multi-contains)
+        v[:60] + "_%" + v[-5:] + "%_",                     # > 63 positions ending in stars
+        v,                                                 # one exact long string as a regex-free pattern
+        "%" + "_" * 700,                                   # 701 positions
+        v[:64] + "%" + "[a]" * 64,
+    ]
+    for pattern in patterns:
+        for cond in ("Like", "NotLike"):
+            check(hy, oracle, w, 1, cond, pattern)
 
 
 def random_strings(rng, k, alphabet="abcXYZ_%.(\n", max_len=12):

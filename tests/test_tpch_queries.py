@@ -167,7 +167,7 @@ def test_device_q1_full(hy, oracle):
     report = []
     worst = check_float_aggregates(a.get_output().rows(), exp.rows(), exp_proj.rows(), [0, 1], Q1_AGGS, 2, report)
     print(f"Q1 SF0.01: worst ULP distance device vs sequential oracle sum = {worst}")
-    assert worst <= 64
+    assert worst <= 1  # the north star's bar (BASELINE.json); measured: 0
 
 
 @pytest.mark.gpu
@@ -194,7 +194,7 @@ def test_device_q3(hy, oracle):
     worst = check_float_aggregates(a.get_output().rows(), exp.rows(), stages[-1].rows(), [0, 1, 2], [(3, "Sum")], 3,
                                    report)
     print(f"Q3 SF0.01: worst ULP distance device vs sequential oracle sum = {worst}")
-    assert worst <= 4
+    assert worst <= 1  # the north star's bar (BASELINE.json); measured: 0
     want = {(w[0], w[2], w[3]): w[1] for w in tf.answers()["q3"]}
     got = a.get_output().rows()
     assert sorted((r[0], r[1], r[2]) for r in got) == sorted(want)
