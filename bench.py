@@ -424,6 +424,14 @@ def main():
         # the join kernel's algorithmic bytes exactly as 8(d) counts JoinHash
         "join_partition": recv_build * 4 + recv_probe * 4 + int(pairs) * 16,
     })
+    # the partition join is join_partition plus the list kernels it defers partitions to (more probe records than one
+    # pass, more build rows than one LDS table): one logical kernel for the roofline, launched once per step
+    deferred = [k for k in ("join_partition_multi", "join_partition_skewed") if k in kernels]
+    if "join_partition" in kernels and deferred:
+        jp = kernels["join_partition"]
+        jp["includes"] = {k: round(kernels[k]["ms_total"] / max(kernels[k]["launches"], 1), 4) for k in deferred}
+        for k in deferred:
+            jp["ms_total"] += kernels.pop(k)["ms_total"]
     for k, v in kernels.items():
         per_launch_ms = v["ms_total"] / max(v["launches"], 1)
         v["ms_per_launch"] = per_launch_ms
@@ -451,7 +459,7 @@ def main():
                 "frac_read_only": round(e2e_read / step_s / 1e9 / peak, 4), "alg_read_bytes_per_step": e2e_read,
                 "peak_source": "measured in this run (hy_stream_bandwidth_probe, best of read / copy)",
                 "frac_of_spec_8000": round(e2e_gbps / HBM_PEAK_GBPS, 4)}
-    traffic, traffic_src = committed_traffic_step(args.sf, chunk, world, fused) if mode == "join" else (None, None)
+    traffic, traffic_src = committed_traffic_step(args.sf, chunk, world, fused, mode)
     if traffic is not None:
         roofline["traffic"] = round(traffic)
         roofline["traffic_source"] = traffic_src
@@ -462,7 +470,7 @@ def main():
     alg_kernels = [k for k in ("join_partition", "scan_dict") if k in kernels and "achieved_GBps" in kernels[k]]
     adom = max(alg_kernels, key=lambda k: kernels[k]["ms_total"]) if alg_kernels else dom
     ak = kernels[adom]
-    k_traffic, k_src = committed_traffic(adom, args.sf, chunk, world) if mode == "join" else (None, None)
+    k_traffic, k_src = committed_traffic(adom, args.sf, chunk, world, mode, fused)
     kernel_roofline = {"bound": "hbm", "kernel": adom, "achieved": round(ak["achieved_GBps"], 1),
                        "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(ak["achieved_GBps"] / HBM_PEAK_GBPS, 4),
                        "traffic": round(k_traffic) if k_traffic is not None else None,
@@ -593,20 +601,28 @@ def kernel_stats(L):
 ROCPROF_NAME = {"scan_dict": "scan_kernel", "scan_value": "scan_kernel"}
 
 
-def committed_traffic(kernel, sf, chunk, world):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary of this configuration
-    (profiles/rNN_rocprof_sf<SF>_summary.json, written by tools/profile_bench.sh: FETCH_SIZE x2 + WRITE_SIZE as the
-    MI355X guide prescribes). The counters need their own rocprofv3 passes, so they are not re-collected here; the
-    summary named in traffic_source is the evidence. None if no summary matches (other scale factor or N>1)."""
+def summary_files(mode, sf, fused):
+    """The committed PMC summaries of one bench configuration, newest round last (tools/profile_round.sh names them
+    rNN_rocprof_<workload>_summary.json; FETCH_SIZE x2 + WRITE_SIZE as the MI355X guide prescribes)."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    if mode == "join":
+        pats = [f"r*_rocprof_sf{sf:g}_fused_summary.json"] if fused else [f"r*_rocprof_sf{sf:g}_summary.json"]
+    else:
+        pats = [f"r*_rocprof_{mode.replace('-', '')}_sf{sf:g}_summary.json"]
+    files = [f for pat in pats for f in glob.glob(os.path.join(here, "profiles", pat))]
+    return here, sorted(files, key=os.path.basename)
+
+
+def committed_traffic(kernel, sf, chunk, world, mode="join", fused=True):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary of this configuration. The counters need
+    their own rocprofv3 passes, so they are not re-collected here; the summary named in traffic_source is the
+    evidence. None if no summary matches (other scale factor or N>1)."""
     if world != 1 or chunk != 100_000:
         return None, None
-    here = os.path.dirname(os.path.abspath(__file__))
-    files = sorted(glob.glob(os.path.join(here, "profiles", f"r*_rocprof_sf{sf:g}_summary.json")) +
-                   glob.glob(os.path.join(here, "profiles", f"r*_rocprof_sf{sf:g}_fused_summary.json")),
-                   key=os.path.basename)  # newest round last
+    here, files = summary_files(mode, sf, fused)
     for f in reversed(files):
         with open(f) as fh:
-            k = json.load(fh).get("kernels", {}).get(ROCPROF_NAME.get(kernel, kernel), {})  # part*.build/.probe split
+            k = json.load(fh).get("kernels", {}).get(ROCPROF_NAME.get(kernel, kernel), {})
         if "hbm_bytes_per_launch" in k:
             return k["hbm_bytes_per_launch"], os.path.relpath(f, here)
     return None, None
@@ -634,15 +650,13 @@ def measured_roofline(L, capi, torch, dev, stream, gb):
     return max(out["read_GBps"], out["copy_GBps"]), out
 
 
-def committed_traffic_step(sf, chunk, world, fused):
-    """HBM bytes per step (all kernels) from the newest committed PMC summary of this configuration
-    (profiles/rNN_rocprof_sf<SF>[_fused]_summary.json, tools/profile_bench.sh: FETCH_SIZE x2 + WRITE_SIZE per the
-    MI355X guide). None if no summary matches."""
+def committed_traffic_step(sf, chunk, world, fused, mode="join"):
+    """HBM bytes per step (all kernels) from the newest committed PMC summary of this configuration. None if no
+    summary matches."""
     if world != 1 or chunk != 100_000:
         return None, None
-    here = os.path.dirname(os.path.abspath(__file__))
-    pat = f"r*_rocprof_sf{sf:g}_fused_summary.json" if fused else f"r*_rocprof_sf{sf:g}_summary.json"
-    for f in reversed(sorted(glob.glob(os.path.join(here, "profiles", pat)))):
+    here, files = summary_files(mode, sf, fused)
+    for f in reversed(files):
         with open(f) as fh:
             d = json.load(fh)
         if "hbm_bytes_per_step" in d:

@@ -42,16 +42,23 @@ hy_status nccl_fail(ncclResult_t r, const char* what) {
     if (r_ != ncclSuccess) return nccl_fail(r_, #call); \
   } while (0)
 
-// An RCCL call inside ncclGroupStart/End: on failure the group is closed before returning, so the communicator is
-// left usable (its peers' matching calls then fail or complete instead of waiting on an open group).
-#define HY_NCCL_IN_GROUP(call)                       \
+// An RCCL call inside ncclGroupStart/End. Every argument of the point-to-point calls is validated (collectively, by the
+// abort verdict) before the group opens, so a failure here is RCCL's own. Closing the group would launch the part
+// already queued while peers wait on the sends and receives never queued, so the communicator is aborted instead: the
+// peers' calls then fail rather than wait, and this handle answers every later call with an error.
+#define HY_NCCL_IN_GROUP(comm, call)                 \
   do {                                               \
     const ncclResult_t r_ = (call);                  \
     if (r_ != ncclSuccess) {                         \
-      (void)ncclGroupEnd();                          \
+      (void)ncclCommAbort((comm)->nccl);             \
+      (comm)->nccl = nullptr;                        \
       return nccl_fail(r_, #call);                   \
     }                                                \
   } while (0)
+
+hy_status comm_usable(hy_comm_t comm) {
+  return comm->nccl ? HY_OK : fail(HY_ERR_DEVICE, "communicator was aborted by an earlier failed exchange");
+}
 
 uint32_t owner_begin(uint32_t n_buckets, int32_t d, int32_t n) {
   return static_cast<uint32_t>(uint64_t(d) * n_buckets / uint32_t(n));
@@ -106,6 +113,7 @@ hy_status hy_join_exchange_counts(hy_comm_t comm, const uint64_t* bucket_counts,
                                   uint64_t* all_counts, hy_stream_t stream) {
   if (!comm || !bucket_counts || !all_counts || n_buckets == 0 || n_buckets > 256)
     return fail(HY_ERR_INVALID_ARGUMENT, "exchange counts");
+  if (const hy_status st = comm_usable(comm); st != HY_OK) return st;
   hipStream_t s = S(stream);
   uint64_t* mine = comm->counts + uint64_t(comm->rank) * n_buckets;
   HY_HIP(hipMemcpyAsync(mine, bucket_counts, 8ull * n_buckets, hipMemcpyHostToDevice, s));
@@ -121,6 +129,7 @@ hy_status hy_join_exchange_records(hy_comm_t comm, const void* records, uint32_t
                                    hy_stream_t stream) {
   if (!comm || !all_counts || !recv_counts || !recv_rows || n_buckets == 0 || record_bytes == 0)
     return fail(HY_ERR_INVALID_ARGUMENT, "exchange records");
+  if (const hy_status st = comm_usable(comm); st != HY_OK) return st;
   const int32_t n = comm->n_ranks, me = comm->rank;
   if (n_buckets < static_cast<uint32_t>(n)) return fail(HY_ERR_INVALID_ARGUMENT, "fewer buckets than ranks");
   // this rank's runs per destination (its records are grouped by bucket, buckets ascending), and what it receives
@@ -162,11 +171,16 @@ hy_status hy_join_exchange_records(hy_comm_t comm, const void* records, uint32_t
   HY_NCCL(ncclGroupStart());
   for (int32_t k = 1; k < n; ++k) {  // peers in a rotating order, so that every link carries one message per round
     const int32_t to = (me + k) % n, from = (me - k + n) % n;
-    if (send[to]) HY_NCCL_IN_GROUP(ncclSend(src + send_off[to] * rb, send[to] * rb, ncclUint8, to, comm->nccl, s));
+    if (send[to]) HY_NCCL_IN_GROUP(comm, ncclSend(src + send_off[to] * rb, send[to] * rb, ncclUint8, to, comm->nccl, s));
     if (recv[from])
-      HY_NCCL_IN_GROUP(ncclRecv(dst + recv_off[from] * rb, recv[from] * rb, ncclUint8, from, comm->nccl, s));
+      HY_NCCL_IN_GROUP(comm, ncclRecv(dst + recv_off[from] * rb, recv[from] * rb, ncclUint8, from, comm->nccl, s));
   }
-  HY_NCCL(ncclGroupEnd());
+  const ncclResult_t end = ncclGroupEnd();
+  if (end != ncclSuccess) {
+    (void)ncclCommAbort(comm->nccl);
+    comm->nccl = nullptr;
+    return nccl_fail(end, "ncclGroupEnd");
+  }
   return HY_OK;
 }
 

@@ -435,18 +435,25 @@ inline bool filter_compact_enabled() {
   return v;
 }
 
+// Calls f with the kernel side tag (hyk::OnBuild / hyk::OnProbe) named by a runtime side tag ("build" / "probe").
+template <typename F>
+hy_status by_side(const char* tag, F&& f) {
+  return tag[0] == 'b' ? f(hyk::OnBuild{}) : f(hyk::OnProbe{});
+}
+
 // Pass 0 of a side with a fused TableScan: part1_compact (gapped row-order records in recB, histograms with the
 // scan-match row), the histogram scan, then part1_spread (scan output + stable scatter into `out`). HY_FILTER_COMPACT=0:
-// part1_mask (match bits) + part1_spread_mask (compaction in LDS) instead.
-template <typename T, typename H, int LP, int FK>
-hy_status launch_filtered_pass0(const char* side_tag, const SidePlan& p, const hyk::Side& sd, const hyk::Digit& d0,
+// part1_mask (match bits) + part1_spread_mask (compaction in LDS) instead, on a probe side.
+template <typename SD, typename T, typename H, int LP, int FK>
+hy_status launch_filtered_pass0(const SidePlan& p, const hyk::Side& sd, const hyk::Digit& d0,
                                 const hyk::NextDigit& nd, uint32_t w0, uint32_t n_digits, SideBufs<H, uint32_t>& b,
                                 const Common& c, hipStream_t s, hyk::Rec<H, uint32_t>* out) {
   const dim3 grid(static_cast<uint32_t>(p.n_tiles1));
-  if (!filter_compact_enabled() && (p.sub == 1 || p.sub == 2)) {
+  // the match-bit variant is an experiment on the headline's filtered (probe) side: built for that side only
+  if constexpr (std::is_same_v<SD, hyk::OnProbe>) if (!filter_compact_enabled() && (p.sub == 1 || p.sub == 2)) {
     {
-      KTimer kt_((std::string("part1_mask.") + side_tag).c_str(), s, p.n_rows);
-      hipLaunchKernelGGL((hyk::part1_mask<T, H, LP, FK>), grid, dim3(hyk::PART_THREADS), 0, s, sd, d0, n_digits,
+      KTimer kt_((std::string("part1_mask.") + SD::name).c_str(), s, p.n_rows);
+      hipLaunchKernelGGL((hyk::part1_mask<SD, T, H, LP, FK>), grid, dim3(hyk::PART_THREADS), 0, s, sd, d0, n_digits,
                          b.hist, b.mbits);
       kt_.done();
     }
@@ -459,12 +466,12 @@ hy_status launch_filtered_pass0(const char* side_tag, const SidePlan& p, const h
     HY_HIP(hipGetLastError());
     const hyk::Side& sd2 = sd;
     {
-      KTimer kt_((std::string("part1_spread.") + side_tag).c_str(), s, p.n_rows);
+      KTimer kt_((std::string("part1_spread.") + SD::name).c_str(), s, p.n_rows);
       if (p.sub == 2)
-        hipLaunchKernelGGL((hyk::part1_spread_mask<T, H, LP, 2>), grid, dim3(hyk::PART_THREADS), 0, s, sd2, d0, nd,
+        hipLaunchKernelGGL((hyk::part1_spread_mask<SD, T, H, LP, 2>), grid, dim3(hyk::PART_THREADS), 0, s, sd2, d0, nd,
                            n_digits, b.off, b.mbits, out);
       else
-        hipLaunchKernelGGL((hyk::part1_spread_mask<T, H, LP, 1>), grid, dim3(hyk::PART_THREADS), 0, s, sd2, d0, nd,
+        hipLaunchKernelGGL((hyk::part1_spread_mask<SD, T, H, LP, 1>), grid, dim3(hyk::PART_THREADS), 0, s, sd2, d0, nd,
                            n_digits, b.off, b.mbits, out);
       kt_.done();
     }
@@ -472,8 +479,8 @@ hy_status launch_filtered_pass0(const char* side_tag, const SidePlan& p, const h
     return HY_OK;
   }
   {
-    KTimer kt_((std::string("part1_compact.") + side_tag).c_str(), s, p.n_rows);
-    hipLaunchKernelGGL((hyk::part1_compact<T, H, LP, FK>), grid, dim3(hyk::PART_THREADS), 0, s, sd, d0, n_digits,
+    KTimer kt_((std::string("part1_compact.") + SD::name).c_str(), s, p.n_rows);
+    hipLaunchKernelGGL((hyk::part1_compact<SD, T, H, LP, FK>), grid, dim3(hyk::PART_THREADS), 0, s, sd, d0, n_digits,
                        b.hist, b.span_count, b.recB);
     kt_.done();
   }
@@ -485,8 +492,8 @@ hy_status launch_filtered_pass0(const char* side_tag, const SidePlan& p, const h
                      p.scan_chunk_begin);
   HY_HIP(hipGetLastError());
   {
-    KTimer kt_((std::string("part1_spread.") + side_tag).c_str(), s, p.n_rows);
-    hipLaunchKernelGGL((hyk::part1_spread<H>), grid, dim3(hyk::PART_THREADS), 0, s, sd, d0, nd, static_cast<int>(w0),
+    KTimer kt_((std::string("part1_spread.") + SD::name).c_str(), s, p.n_rows);
+    hipLaunchKernelGGL((hyk::part1_spread<SD, H>), grid, dim3(hyk::PART_THREADS), 0, s, sd, d0, nd, static_cast<int>(w0),
                        n_digits, b.off, b.span_count, b.recB, out);
     kt_.done();
   }
@@ -494,8 +501,8 @@ hy_status launch_filtered_pass0(const char* side_tag, const SidePlan& p, const h
   return HY_OK;
 }
 
-template <typename T, typename H, typename P, int LP>
-hy_status launch_pass0(const char* side_tag, const SidePlan& p, const hyk::Side& sd, const hyk::Digit& d0,
+template <typename SD, typename T, typename H, typename P, int LP>
+hy_status launch_pass0(const SidePlan& p, const hyk::Side& sd, const hyk::Digit& d0,
                        const hyk::NextDigit& nd, uint32_t w0, uint32_t n_digits, SideBufs<H, P>& b, const Common& c,
                        hipStream_t s, hyk::Rec<H, P>* out) {
   const bool filt = p.filtered;
@@ -503,13 +510,13 @@ hy_status launch_pass0(const char* side_tag, const SidePlan& p, const hyk::Side&
   if constexpr (LP != hyk::LP_REF1 && std::is_same_v<T, H> && std::is_same_v<P, uint32_t>) {
     switch (fk) {
       case hyk::FK_DICT8:
-        return launch_filtered_pass0<T, H, LP, hyk::FK_DICT8>(side_tag, p, sd, d0, nd, w0, n_digits, b, c, s, out);
+        return launch_filtered_pass0<SD, T, H, LP, hyk::FK_DICT8>(p, sd, d0, nd, w0, n_digits, b, c, s, out);
       case hyk::FK_DICT16:
-        return launch_filtered_pass0<T, H, LP, hyk::FK_DICT16>(side_tag, p, sd, d0, nd, w0, n_digits, b, c, s, out);
+        return launch_filtered_pass0<SD, T, H, LP, hyk::FK_DICT16>(p, sd, d0, nd, w0, n_digits, b, c, s, out);
       case hyk::FK_DICT32:
-        return launch_filtered_pass0<T, H, LP, hyk::FK_DICT32>(side_tag, p, sd, d0, nd, w0, n_digits, b, c, s, out);
+        return launch_filtered_pass0<SD, T, H, LP, hyk::FK_DICT32>(p, sd, d0, nd, w0, n_digits, b, c, s, out);
       case hyk::FK_ANY:
-        return launch_filtered_pass0<T, H, LP, hyk::FK_ANY>(side_tag, p, sd, d0, nd, w0, n_digits, b, c, s, out);
+        return launch_filtered_pass0<SD, T, H, LP, hyk::FK_ANY>(p, sd, d0, nd, w0, n_digits, b, c, s, out);
       default:
         break;
     }
@@ -517,16 +524,16 @@ hy_status launch_pass0(const char* side_tag, const SidePlan& p, const hyk::Side&
   if (filt) return fail(HY_ERR_UNSUPPORTED, "fused scan on a side whose join column type is not the hashed type");
   const dim3 grid(static_cast<uint32_t>(p.n_tiles1));
   {
-    KTimer kt_((std::string("part1_hist.") + side_tag).c_str(), s, p.n_rows);
-    hipLaunchKernelGGL((hyk::part1_hist<T, H, LP>), grid, dim3(hyk::PART_THREADS), 0, s, sd, d0, n_digits, b.hist);
+    KTimer kt_((std::string("part1_hist.") + SD::name).c_str(), s, p.n_rows);
+    hipLaunchKernelGGL((hyk::part1_hist<SD, T, H, LP>), grid, dim3(hyk::PART_THREADS), 0, s, sd, d0, n_digits, b.hist);
     kt_.done();
   }
   HY_HIP(hipGetLastError());
   hy_status st = run_scan(b.hist, b.off, uint64_t(n_digits) * p.n_tiles1, c, s, b.total);
   if (st != HY_OK) return st;
   {
-    KTimer kt_((std::string("part1_scatter.") + side_tag).c_str(), s, p.n_rows);
-    hipLaunchKernelGGL((hyk::part1_scatter<T, H, P, LP>), grid, dim3(hyk::PART_THREADS), 0, s, sd, d0, nd,
+    KTimer kt_((std::string("part1_scatter.") + SD::name).c_str(), s, p.n_rows);
+    hipLaunchKernelGGL((hyk::part1_scatter<SD, T, H, P, LP>), grid, dim3(hyk::PART_THREADS), 0, s, sd, d0, nd,
                        static_cast<int>(w0), n_digits, b.off, out);
     kt_.done();
   }
@@ -535,8 +542,8 @@ hy_status launch_pass0(const char* side_tag, const SidePlan& p, const hyk::Side&
 }
 
 // Pass 0: from column chunks into `out`, bucket bounds into b.segA (2^w0 buckets); next-digit bytes into nd.
-template <typename T, typename H, typename P>
-hy_status pass0_side(const char* side_tag, const SidePlan& p, SideBufs<H, P>& b, uint32_t bits, uint32_t w0,
+template <typename SD, typename T, typename H, typename P>
+hy_status pass0_side(const SidePlan& p, SideBufs<H, P>& b, uint32_t bits, uint32_t w0,
                      uint32_t seed, bool keep_nulls, uint32_t ref_base, const hyk::NextDigit& nd, const Common& c,
                      hipStream_t s, hyk::Rec<H, P>* out, const uint32_t* bloom = nullptr, uint64_t bloom_n = 0,
                      bool bloom_by_hash = false) {
@@ -572,11 +579,11 @@ hy_status pass0_side(const char* side_tag, const SidePlan& p, SideBufs<H, P>& b,
     const int lp = load_path(p);
     hy_status st;
     if (lp == hyk::LP_VALUE)
-      st = launch_pass0<T, H, P, hyk::LP_VALUE>(side_tag, p, sd, d0, nd, w0, n_digits, b, c, s, out);
+      st = launch_pass0<SD, T, H, P, hyk::LP_VALUE>(p, sd, d0, nd, w0, n_digits, b, c, s, out);
     else if (lp == hyk::LP_REF1)
-      st = launch_pass0<T, H, P, hyk::LP_REF1>(side_tag, p, sd, d0, nd, w0, n_digits, b, c, s, out);
+      st = launch_pass0<SD, T, H, P, hyk::LP_REF1>(p, sd, d0, nd, w0, n_digits, b, c, s, out);
     else
-      st = launch_pass0<T, H, P, hyk::LP_ANY>(side_tag, p, sd, d0, nd, w0, n_digits, b, c, s, out);
+      st = launch_pass0<SD, T, H, P, hyk::LP_ANY>(p, sd, d0, nd, w0, n_digits, b, c, s, out);
     if (st != HY_OK) return st;
   }
   hipLaunchKernelGGL(hyk::seg_bounds, dim3((n_digits + 1 + 255) / 256), dim3(256), 0, s, b.off, p.n_tiles1, n_digits,
@@ -605,8 +612,8 @@ hyk::RecOut<H, P> soa_out(void* area, uint64_t rows, uint32_t bits, uint32_t* bl
 // One record pass over segments sg (tile prefix and owners filled, grid = an upper bound of its tiles): histogram
 // (from the digit bytes dig_in when the previous pass wrote them, else from the records), scan, stable scatter by digit
 // (bits [shift, shift + w)) writing the next pass's digit bytes (nd), then the bounds of the n_groups * 2^w parts.
-template <typename H, typename P>
-hy_status record_pass(const char* side_tag, const SideBufs<H, P>& b, const hyk::Segs& sg, const hyk::Groups& gr,
+template <typename SD, typename H, typename P>
+hy_status record_pass(const SideBufs<H, P>& b, const hyk::Segs& sg, const hyk::Groups& gr,
                       uint32_t n_groups, uint64_t grid, uint32_t bits, uint32_t shift, uint32_t w, uint32_t seed,
                       const hyk::Rec<H, P>* in, const uint8_t* dig_in, const hyk::NextDigit& nd,
                       const hyk::RecOut<H, P>& out, const uint64_t* total, uint32_t* bounds, const Common& c,
@@ -615,12 +622,12 @@ hy_status record_pass(const char* side_tag, const SideBufs<H, P>& b, const hyk::
   hyk::Digit dg{full_mask(bits), shift, n_digits - 1u, seed, g_key_hash};
   if (grid) {
     {
-      KTimer kt_((std::string("part2_hist.") + side_tag).c_str(), s, rows);
+      KTimer kt_((std::string("part2_hist.") + SD::name).c_str(), s, rows);
       if (dig_in)
-        hipLaunchKernelGGL(hyk::part2_hist_bytes, dim3(static_cast<uint32_t>(grid)), dim3(hyk::PART_THREADS), 0, s,
+        hipLaunchKernelGGL(hyk::part2_hist_bytes<SD>, dim3(static_cast<uint32_t>(grid)), dim3(hyk::PART_THREADS), 0, s,
                            sg, n_digits, dig_in, b.hist);
       else
-        hipLaunchKernelGGL((hyk::part2_hist<H, P>), dim3(static_cast<uint32_t>(grid)), dim3(hyk::PART_THREADS), 0, s,
+        hipLaunchKernelGGL((hyk::part2_hist<SD, H, P>), dim3(static_cast<uint32_t>(grid)), dim3(hyk::PART_THREADS), 0, s,
                            sg, dg, n_digits, in, b.hist);
       kt_.done();
     }
@@ -628,8 +635,8 @@ hy_status record_pass(const char* side_tag, const SideBufs<H, P>& b, const hyk::
     hy_status st = run_scan(b.hist, b.off, grid * n_digits, c, s);
     if (st != HY_OK) return st;
     {
-      KTimer kt_((std::string("part2_scatter.") + side_tag).c_str(), s, rows);
-      hipLaunchKernelGGL((hyk::part2_scatter<H, P>), dim3(static_cast<uint32_t>(grid)), dim3(hyk::PART_THREADS), 0, s,
+      KTimer kt_((std::string("part2_scatter.") + SD::name).c_str(), s, rows);
+      hipLaunchKernelGGL((hyk::part2_scatter<SD, H, P>), dim3(static_cast<uint32_t>(grid)), dim3(hyk::PART_THREADS), 0, s,
                          sg, dg, nd, static_cast<int>(w), n_digits, in, b.off, out);
       kt_.done();
     }
@@ -645,8 +652,8 @@ hy_status record_pass(const char* side_tag, const SideBufs<H, P>& b, const hyk::
 // Record passes over contiguous segments (bounds in `seg`, n_segs of them) for digits w[first..]: ping-pong between
 // the two record buffers (and, when dig_in is given, the two digit-byte buffers). On return *recs / *bounds hold the
 // final records and partition bounds.
-template <typename H, typename P>
-hy_status local_passes(const char* side_tag, SideBufs<H, P>& b, const std::vector<uint32_t>& w, size_t first,
+template <typename SD, typename H, typename P>
+hy_status local_passes(SideBufs<H, P>& b, const std::vector<uint32_t>& w, size_t first,
                        uint32_t bits, uint32_t seed, hyk::Rec<H, P>* in, hyk::Rec<H, P>* spare, const uint8_t* dig_in,
                        uint8_t* dig_spare, uint32_t* seg, uint32_t* seg_spare, uint64_t n_segs,
                        const uint64_t* total, uint64_t rows, const Common& c, hipStream_t s, hyk::Rec<H, P>** recs,
@@ -671,7 +678,7 @@ hy_status local_passes(const char* side_tag, SideBufs<H, P>& b, const std::vecto
                  nullptr, sub2()};
     const hyk::NextDigit nd = next_digit(w, i, bits, dig_in ? dig_spare : nullptr);
     const hyk::RecOut<H, P> out = (last_out && i + 1 == w.size()) ? *last_out : aos_out<H, P>(spare);
-    st = record_pass<H, P>(side_tag, b, sg, hyk::Groups{nullptr, nullptr, nullptr}, static_cast<uint32_t>(n_segs), grid,
+    st = record_pass<SD, H, P>(b, sg, hyk::Groups{nullptr, nullptr, nullptr}, static_cast<uint32_t>(n_segs), grid,
                            bits, below, w[i], seed, in, dig_in, nd, out, total, seg_spare, c, s, rows);
     if (st != HY_OK) return st;
     std::swap(in, spare);
@@ -718,9 +725,11 @@ uint32_t lds_table_rows() {
 
 // Per-partition LDS build/probe over partitioned records (partition bounds on the device; the records as the last pass
 // wrote them: hyk::RecSrc or hyk::HashSrc). probe_rows_hint: an upper bound of the probe rows; it picks the probe
-// records per thread (JP) from the average partition. Partitions with more build rows than one LDS table (skewed keys)
-// are listed by join_partition and joined by join_partition_skewed, launched only when the build side is large
-// enough to have one.
+// records per thread (JP) from the average partition, and the kernel: join_partition (one pass of probe records per
+// partition; a partition needing more passes is listed for join_partition_multi) or, when the average partition needs
+// several passes, join_partition_multi over every partition. Partitions with more build rows than one LDS table
+// (skewed keys) are listed and joined by join_partition_skewed. The list kernels launch only when their list can be
+// non-empty.
 template <typename Src, typename P>
 hy_status run_join_partitions(const uint32_t* build_begin, const uint32_t* probe_begin, uint32_t n_parts,
                               const Src& bsrc, const Src& psrc, const hyk::RowMap& bmap, const hyk::RowMap& pmap,
@@ -747,19 +756,32 @@ hy_status run_join_partitions(const uint32_t* build_begin, const uint32_t* probe
   jd.error = c.misc + 1;
   jd.overflow = c.misc + 2;
   jd.n_skewed = c.misc + 3;
-  jd.skewed = reinterpret_cast<uint32_t*>(c.join_status);  // (2^bits + 1) words of 8 B >= n_parts entries
+  jd.n_multi = c.misc + 4;
+  jd.skewed = reinterpret_cast<uint32_t*>(c.join_status);  // (2^bits + 1) words of 8 B: 2 x n_parts entries
+  jd.multi = jd.skewed + n_parts;
   jd.total = c.totals + 1;
   jd.trace = g_join_trace;
   HY_HIP(hipMemsetAsync(c.misc, 0, 64 * 4, s));
   HY_HIP(hipMemsetAsync(c.totals, 0, 8 * 2, s));
-  if (n_parts) {
+  constexpr int JW = Src::V == 1 ? 6 : 8;  // the wide variant's probe records per thread (a multiple of V)
+  // most partitions need several probe passes (the average exceeds 3/4 of the wide pass): the multi-pass kernel takes
+  // every partition directly instead of the one-pass kernel deferring nearly all of them
+  const bool all_multi = avg_probe > static_cast<uint64_t>(3 * JW * NT / 4) && !jd.trace;
+  if (n_parts && all_multi) {
+    jd.multi = nullptr;
+    KTimer kt_("join_partition", s, units);
+    hipLaunchKernelGGL((hyk::join_partition_multi<Src, P, JW, NT>), dim3(n_parts), dim3(NT), lds, s, jd, bsrc, psrc,
+                       out_build, out_probe, partition_begin, partition_counts);
+    kt_.done();
+    HY_HIP(hipGetLastError());
+  }
+  if (n_parts && !all_multi) {
     {
       KTimer kt_("join_partition", s, units);
       auto launch = [&](auto kernel) {
         hipLaunchKernelGGL(kernel, dim3(n_parts), dim3(NT), lds, s, jd, bsrc, psrc, out_build, out_probe,
                            partition_begin, partition_counts);
       };
-      constexpr int JW = Src::V == 1 ? 6 : 8;  // the wide variant's probe records per thread (a multiple of V)
       if (jd.trace)  // debug phase-trace instance (hy_debug_set_join_trace)
         wide ? launch(hyk::join_partition<Src, P, true, JW, NT>) : launch(hyk::join_partition<Src, P, true, 4, NT>);
       else
@@ -767,7 +789,24 @@ hy_status run_join_partitions(const uint32_t* build_begin, const uint32_t* probe
       kt_.done();
     }
     HY_HIP(hipGetLastError());
-    // a partition is skewed only with more than lds_max build rows: at most build_rows / (lds_max + 1) of them
+    // deferred partitions: more probe records than one pass (at most probe_rows / (pass - V + 2) of them), more
+    // build rows than one table (at most build_rows / (lds_max + 1)); each list's kernel only when it can be non-empty
+    const uint32_t per_pass = static_cast<uint32_t>((wide ? JW : 4) * NT - (Src::V - 1));
+    const uint64_t max_multi = std::min<uint64_t>(n_parts, probe_rows_hint / (uint64_t(per_pass) + 1));
+    if (max_multi) {
+      KTimer kt_("join_partition_multi", s, units);
+      const dim3 g(static_cast<uint32_t>(std::min<uint64_t>(max_multi, 512)));
+      if (wide)
+        hipLaunchKernelGGL((hyk::join_partition_multi<Src, P, JW, NT>), g, dim3(NT), lds, s, jd, bsrc, psrc, out_build,
+                           out_probe, partition_begin, partition_counts);
+      else
+        hipLaunchKernelGGL((hyk::join_partition_multi<Src, P, 4, NT>), g, dim3(NT), lds, s, jd, bsrc, psrc, out_build,
+                           out_probe, partition_begin, partition_counts);
+      kt_.done();
+      HY_HIP(hipGetLastError());
+    }
+  }
+  if (n_parts) {
     const uint64_t build_rows = units > probe_rows_hint ? units - probe_rows_hint : 0;
     const uint64_t max_skewed = std::min<uint64_t>(n_parts, build_rows / (uint64_t(lds_max) + 1));
     if (max_skewed) {
@@ -1078,17 +1117,21 @@ hy_status onepass_side(const char* tag, const SidePlan& p, OneBufs<H>& o, uint32
   const hyk::Groups gr{o.group_hbase, o.group_tiles, o.group_out};
   const uint64_t grid = p.n_rows / span2() + 1 + nseg;
   const hyk::NextDigit nd1 = next_digit(w, 1, bits, b.digB);
-  st = record_pass<H, uint32_t>(tag, b, sg, gr, nd0, grid, bits, bits - w[0] - w1, w1, seed, b.recA, b.digA, nd1,
-                                aos_out<H, uint32_t>(b.recB),
-                                b.total, b.segA, c, s, p.n_rows);
+  st = by_side(tag, [&](auto sdt) {
+    return record_pass<decltype(sdt), H, uint32_t>(b, sg, gr, nd0, grid, bits, bits - w[0] - w1, w1, seed, b.recA,
+                                                   b.digA, nd1, aos_out<H, uint32_t>(b.recB), b.total, b.segA, c, s,
+                                                   p.n_rows);
+  });
   if (st != HY_OK) return st;
   if (w.size() == 2) {
     *recs = b.recB;
     *bounds = b.segA;
     return HY_OK;
   }
-  return local_passes<H, uint32_t>(tag, b, w, 2, bits, seed, b.recB, b.recA, b.digB, b.digA, b.segA, b.segB,
-                                   uint64_t(nd0) << w1, b.total, p.n_rows, c, s, recs, bounds);
+  return by_side(tag, [&](auto sdt) {
+    return local_passes<decltype(sdt), H, uint32_t>(b, w, 2, bits, seed, b.recB, b.recA, b.digB, b.digA, b.segA,
+                                                    b.segB, uint64_t(nd0) << w1, b.total, p.n_rows, c, s, recs, bounds);
+  });
 }
 
 // Both sides through onepass_side, then the partition joins. *overflow = the sides' flags (nonzero: results invalid,
@@ -1256,15 +1299,18 @@ hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join
     const hipStream_t st_s = side == 0 ? sb : s;
     const hyk::NextDigit nd = next_digit(w, 0, bits, b.digA);
     hy_status st = side == 0
-                       ? pass0_side<TB, H, uint32_t>(tag, p, b, bits, w.empty() ? 0 : w[0], prm->seed, false,
+                       ? pass0_side<hyk::OnBuild, TB, H, uint32_t>(p, b, bits, w.empty() ? 0 : w[0], prm->seed, false,
                                                      p.ref_base, nd, cs, st_s, b.recA)
-                       : pass0_side<TP, H, uint32_t>(tag, p, b, bits, w.empty() ? 0 : w[0], prm->seed, keep_nulls,
+                       : pass0_side<hyk::OnProbe, TP, H, uint32_t>(p, b, bits, w.empty() ? 0 : w[0], prm->seed, keep_nulls,
                                                      p.ref_base, nd, cs, st_s, b.recA, use_bloom ? bloom : nullptr,
                                                      bloom_n, soa);
     if (st != HY_OK) return st;
-    st = local_passes<H, uint32_t>(tag, b, w, 1, bits, prm->seed, b.recA, b.recB, nd.bytes, b.digB, b.segA, b.segB,
-                                   w.empty() ? 1 : (1ull << w[0]), b.total, p.n_rows, cs, st_s, &recs[side],
-                                   &bounds[side], soa ? &soa_outs[side] : nullptr);
+    st = by_side(tag, [&](auto sdt) {
+      return local_passes<decltype(sdt), H, uint32_t>(b, w, 1, bits, prm->seed, b.recA, b.recB, nd.bytes, b.digB,
+                                                      b.segA, b.segB, w.empty() ? 1 : (1ull << w[0]), b.total,
+                                                      p.n_rows, cs, st_s, &recs[side], &bounds[side],
+                                                      soa ? &soa_outs[side] : nullptr);
+    });
     if (st != HY_OK) return st;
     if (side == 0 && use_bloom && !soa) {  // the probe side's prefilter over the build side's keys (its records)
       HY_HIP(hipMemsetAsync(bloom, 0, 4 * bloom_n, s));
@@ -1464,12 +1510,15 @@ hy_status recv_side(const char* tag, const RecvPlan& r, RecvBufs<H, P>& rb, cons
                rb.seg_hbase, rb.seg_stride,     rb.seg_toff, sub2()};
   hyk::Groups gr{rb.group_hbase, rb.group_tiles, rb.group_out};
   // the merge pass must not write through a stale histogram entry: hist words are exactly the groups' tiles x digits
-  hy_status st = record_pass<H, P>(tag, rb.b, sg, gr, nb, r.tiles, bits, shift, w1, seed, in, nullptr,
-                                   hyk::NextDigit{nullptr, 0, 0}, aos_out<H, P>(rb.b.recA), rb.b.total, rb.b.segA, c, s,
-                                   r.rows);
-  if (st != HY_OK) return st;
-  return local_passes<H, P>(tag, rb.b, w, 2, bits, seed, rb.b.recA, rb.b.recB, nullptr, nullptr, rb.b.segA, rb.b.segB,
-                            uint64_t(nb) << w1, rb.b.total, r.rows, c, s, recs, bounds);
+  return by_side(tag, [&](auto sdt) {
+    using SD = decltype(sdt);
+    hy_status st = record_pass<SD, H, P>(rb.b, sg, gr, nb, r.tiles, bits, shift, w1, seed, in, nullptr,
+                                         hyk::NextDigit{nullptr, 0, 0}, aos_out<H, P>(rb.b.recA), rb.b.total,
+                                         rb.b.segA, c, s, r.rows);
+    if (st != HY_OK) return st;
+    return local_passes<SD, H, P>(rb.b, w, 2, bits, seed, rb.b.recA, rb.b.recB, nullptr, nullptr, rb.b.segA,
+                                  rb.b.segB, uint64_t(nb) << w1, rb.b.total, r.rows, c, s, recs, bounds);
+  });
 }
 
 // Global chunk layouts of the two tables (row-index exchange records): device row_begin arrays of the RowMaps.
@@ -1517,7 +1566,7 @@ hy_status exchange_partition_for_hashed(const SidePlan& p, int32_t value_type, c
       carve_common(cv, exchange_scan_words(p, w), bits, &c);
       if (!cv.ok) return fail(HY_ERR_WORKSPACE, "workspace");
       if (upload_side(p, b, s)) return HY_ERR_DEVICE;
-      hy_status st2 = pass0_side<T_, H, P>("exchange", p, b, bits, w[0], params->seed, keep_nulls != 0, p.ref_base,
+      hy_status st2 = pass0_side<hyk::OnExchange, T_, H, P>(p, b, bits, w[0], params->seed, keep_nulls != 0, p.ref_base,
                                            hyk::NextDigit{nullptr, 0, 0}, c, s,
                                            static_cast<hyk::Rec<H, P>*>(out_records));
       if (st2 != HY_OK) return st2;

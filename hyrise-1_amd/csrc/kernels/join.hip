@@ -110,6 +110,13 @@ __device__ __forceinline__ P ref_payload(bool has, const hy_row_id& rid, uint64_
     return has ? static_cast<uint32_t>(ref_row_begin + rid.chunk_offset) : NULL_PAYLOAD;
 }
 
+// Which join side a partition kernel works for. Only the kernel's name carries it (its code is the same), so that a
+// rocprofv3 kernel trace or counter pass attributes every partition launch to its side from the launch itself:
+// hyk::part2_scatter<hyk::OnProbe, ...> is the probe side's.
+struct OnBuild { static constexpr const char* name = "build"; };
+struct OnProbe { static constexpr const char* name = "probe"; };
+struct OnExchange { static constexpr const char* name = "exchange"; };  // a distributed join's pre-exchange pass
+
 struct Side {
   const SrcChunk* chunks;
   uint32_t n_chunks;
@@ -598,7 +605,7 @@ __device__ __forceinline__ void clear_wave_counts(uint32_t* wave_cnt) {
 // Pass 1: from column chunks.
 // ------------------------------------------------------------------------------------------------------------
 // Histogram rows: hist[d * n_tiles + tile] = rows of span `tile` with digit d.
-template <typename T, typename H, int LP>
+template <typename SD, typename T, typename H, int LP>
 __global__ __launch_bounds__(PART_THREADS) void part1_hist(Side s, Digit dg, uint32_t n_digits,
                                                           uint32_t* __restrict__ hist) {
   __shared__ uint32_t s_hist[256];
@@ -627,7 +634,7 @@ __global__ __launch_bounds__(PART_THREADS) void part1_hist(Side s, Digit dg, uin
   for (uint32_t d = threadIdx.x; d < n_digits; d += PART_THREADS) hist[d * s.n_tiles + tile] = s_hist[d];
 }
 
-template <typename T, typename H, typename P, int LP>
+template <typename SD, typename T, typename H, typename P, int LP>
 __global__ __launch_bounds__(PART_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void part1_scatter(
     Side s, Digit dg, NextDigit nd, int dbits, uint32_t n_digits, const uint32_t* __restrict__ offsets,
     Rec<H, P>* __restrict__ out) {
@@ -683,7 +690,7 @@ __global__ __launch_bounds__(PART_THREADS) __attribute__((amdgpu_waves_per_eu(4)
 // ------------------------------------------------------------------------------------------------------------
 constexpr uint32_t NULL_FLAG = 0x80000000u;  // payloads of filtered sides are row indexes < 2^31
 
-template <typename T, typename H, int LP, int FK>
+template <typename SD, typename T, typename H, int LP, int FK>
 __global__ __launch_bounds__(PART_THREADS) void part1_compact(Side s, Digit dg, uint32_t n_digits,
                                                              uint32_t* __restrict__ hist, uint32_t* __restrict__ span_count,
                                                              Rec<H, uint32_t>* __restrict__ gap_out) {
@@ -743,7 +750,7 @@ __global__ __launch_bounds__(PART_THREADS) void part1_compact(Side s, Digit dg, 
   }
 }
 
-template <typename H>
+template <typename SD, typename H>
 __global__ __launch_bounds__(PART_THREADS) void part1_spread(Side s, Digit dg, NextDigit nd, int dbits,
                                                             uint32_t n_digits, const uint32_t* __restrict__ offsets,
                                                             const uint32_t* __restrict__ span_count,
@@ -806,7 +813,7 @@ __global__ __launch_bounds__(PART_THREADS) void part1_spread(Side s, Digit dg, N
 // ------------------------------------------------------------------------------------------------------------
 constexpr int MASK_WORDS = PART_WAVES * PART_ITEMS;  // ballots per tile
 
-template <typename T, typename H, int LP, int FK>
+template <typename SD, typename T, typename H, int LP, int FK>
 __global__ __launch_bounds__(PART_THREADS) void part1_mask(Side s, Digit dg, uint32_t n_digits,
                                                           uint32_t* __restrict__ hist,
                                                           uint64_t* __restrict__ match_bits) {
@@ -852,7 +859,7 @@ __global__ __launch_bounds__(PART_THREADS) void part1_mask(Side s, Digit dg, uin
 }
 
 // SUB: tiles per span (the host's sub_filtered); the LDS holds the span's compacted records (at most SUB tiles).
-template <typename T, typename H, int LP, int SUB>
+template <typename SD, typename T, typename H, int LP, int SUB>
 __global__ __launch_bounds__(PART_THREADS) void part1_spread_mask(Side s, Digit dg, NextDigit nd, uint32_t n_digits,
                                                                  const uint32_t* __restrict__ offsets,
                                                                  const uint64_t* __restrict__ match_bits,
@@ -1239,7 +1246,7 @@ __device__ __forceinline__ void seg_geometry(const Segs& sg, uint32_t sgi, uint3
   *toff = sg.seg_toff ? sg.seg_toff[sgi] : 0u;
 }
 
-template <typename H, typename P>
+template <typename SD, typename H, typename P>
 __global__ __launch_bounds__(PART_THREADS) void part2_hist(Segs sg, Digit dg, uint32_t n_digits,
                                                           const Rec<H, P>* __restrict__ in, uint32_t* __restrict__ hist) {
   __shared__ uint32_t s_hist[256];
@@ -1271,7 +1278,7 @@ __global__ __launch_bounds__(PART_THREADS) void part2_hist(Segs sg, Digit dg, ui
   for (uint32_t d = threadIdx.x; d < n_digits; d += PART_THREADS) hist[hbase + d * stride + toff + t_in] = s_hist[d];
 }
 
-template <typename H, typename P>
+template <typename SD, typename H, typename P>
 __global__ __launch_bounds__(PART_THREADS) void part2_scatter(Segs sg, Digit dg, NextDigit nd, int dbits,
                                                              uint32_t n_digits, const Rec<H, P>* __restrict__ in,
                                                              const uint32_t* __restrict__ offsets, RecOut<H, P> out) {
@@ -1318,7 +1325,8 @@ __global__ __launch_bounds__(PART_THREADS) void part2_scatter(Segs sg, Digit dg,
 
 // part2_hist from the digit bytes the previous pass wrote beside the records (1 B per record instead of the record
 // and its hash); same tiles and histogram layout as part2_hist.
-static __global__ __launch_bounds__(PART_THREADS) void part2_hist_bytes(Segs sg, uint32_t n_digits,
+template <typename SD>
+__global__ __launch_bounds__(PART_THREADS) void part2_hist_bytes(Segs sg, uint32_t n_digits,
                                                                 const uint8_t* __restrict__ dig,
                                                                 uint32_t* __restrict__ hist) {
   __shared__ uint32_t s_hist[256];
@@ -1539,6 +1547,8 @@ struct JoinDesc {
   uint64_t* trace;              // debug phase stamps (hy_debug_set_join_trace) or null
   uint32_t* skewed;             // partitions with more build rows than one LDS table (n_parts entries)
   uint32_t* n_skewed;           // their count (zeroed before join_partition)
+  uint32_t* multi;              // partitions with more probe records than one pass (n_parts entries)
+  uint32_t* n_multi;            // their count (zeroed before join_partition)
 };
 
 // Record sources of the partition join: what the last partition pass wrote.
@@ -1829,11 +1839,12 @@ __device__ __forceinline__ void write_duplicates(const JoinDesc& d, const Src& b
   }
 }
 
-// A partition whose build side fits one LDS table (the common case): the table is built once and every probe
+// A partition whose build side fits one LDS table. Its probe records fit one pass of JP per thread in the common case
+// (!MULTI; join_partition defers the others to join_partition_multi): the table is built once and every probe
 // record's (count, first entry) stays in registers from counting to writing. A lane takes its records in groups of
 // Src::V consecutive ones (JP / V groups per pass), so the records' order is (pass, group, thread, record in group):
 // pass_offsets places the groups, a lane its group's records one after the other.
-template <typename Src, typename P, bool TRACE, int JP, int NT>
+template <typename Src, typename P, bool TRACE, int JP, int NT, bool MULTI = false>
 __device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t p, unsigned char* smem,
                                                     const Src& build, const Src& probe,
                                                     hy_row_id* __restrict__ out_build, hy_row_id* __restrict__ out_probe,
@@ -1850,8 +1861,7 @@ __device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t 
   const BTable<H, P> t = table_at<H, P>(smem, nb);
   // groups start at multiples of V: probe records [a0, a0 + lead) before the partition are loaded and ignored
   const uint32_t a0 = pb & ~uint32_t(V - 1), lead = pb - a0, nr = np + lead;
-  constexpr uint32_t JP_PASS_ = JP * NT;
-  const uint32_t n_pass = (nr + JP_PASS_ - 1) / JP_PASS_;
+  constexpr uint32_t JP_PASS_ = JP * NT;  // (!MULTI: nr <= JP_PASS_, one pass)
   auto rel = [&](uint32_t pass, int k, int v) { return pass * JP_PASS_ + (k * NT + threadIdx.x) * V + v; };
   auto in = [&](uint32_t pass, int k, int v) {
     const uint32_t r = rel(pass, k, v);
@@ -1876,43 +1886,22 @@ __device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t 
 
   // records of <= 8 bytes: the first pass's probe records are in flight while the table is built (wider ones would
   // spill at this kernel's register budget)
-  constexpr bool PREFETCH = sizeof(Rec<H, P>) <= 8;
+  constexpr bool PREFETCH = !MULTI && sizeof(Rec<H, P>) <= 8;
   if (PREFETCH) load(0);
   build_table<Src, P, NT>(t, build, bb, nb, s_tot);
   trace_stamp<TRACE>(d, p, 1);
 
-  uint32_t my = 0;
-  for (uint32_t pass = 0; pass < n_pass; ++pass) {
-    if (pass || !PREFETCH) load(pass);
-    match(pass);
+  auto e_of = [&](uint32_t pass, int k) {
+    uint32_t e = 0;
 #pragma unroll
-    for (int k = 0; k < K; ++k)
-#pragma unroll
-      for (int v = 0; v < V; ++v) my += emit(pass, k, v);
-  }
-  trace_stamp<TRACE>(d, p, 2);
-  uint32_t part_total;
-  block_exclusive_sum<NT>(my, s_tot, &part_total);
-  const uint64_t obase = allocate_output(d, p, part_total, part_out_begin, part_out_count, s_base);
-  trace_stamp<TRACE>(d, p, 3);
-  if (obase + part_total > d.capacity) return;
-
-  uint64_t run = obase;
-  for (uint32_t pass = 0; pass < n_pass; ++pass) {
-    if (n_pass > 1) {  // a single pass still holds its records and matches in registers
-      load(pass);
-      match(pass);
-    }
-    auto e_of = [&](int k) {
-      uint32_t e = 0;
-#pragma unroll
-      for (int v = 0; v < V; ++v) e += emit(pass, k, v);
-      return e;
-    };
-    const uint32_t pass_total = pass_offsets<K, NT>(e_of, s_tot);
+    for (int v = 0; v < V; ++v) e += emit(pass, k, v);
+    return e;
+  };
+  // writes the pairs of one pass from `run` on (pass_offsets has left the pass's per-(group, wave) offsets in s_tot)
+  auto write_pass = [&](uint32_t pass, uint64_t run) {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      uint64_t o = run + record_pos<K, NT>(e_of(k), k, s_tot);
+      uint64_t o = run + record_pos<K, NT>(e_of(pass, k), k, s_tot);
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         const uint32_t c = info_count(pinfo[k][v]);
@@ -1934,8 +1923,42 @@ __device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t 
         o += e;
       }
     }
-    run += pass_total;
-    __syncthreads();  // s_tot is reused by the next pass
+  };
+
+  if constexpr (!MULTI) {
+    // one pass (join_partition defers larger partitions): one scan over the records' emit counts gives the
+    // partition's total and every record's position
+    if (!PREFETCH) load(0);
+    match(0);
+    trace_stamp<TRACE>(d, p, 2);
+    const uint32_t part_total = pass_offsets<K, NT>([&](int k) { return e_of(0, k); }, s_tot);
+    const uint64_t obase = allocate_output(d, p, part_total, part_out_begin, part_out_count, s_base);
+    trace_stamp<TRACE>(d, p, 3);
+    if (obase + part_total > d.capacity) return;
+    write_pass(0, obase);
+  } else {
+    // several passes: count them all, reserve the partition's range, then reload, match and write pass by pass
+    const uint32_t n_pass = (nr + JP_PASS_ - 1) / JP_PASS_;
+    uint32_t my = 0;
+    for (uint32_t pass = 0; pass < n_pass; ++pass) {
+      if (pass || !PREFETCH) load(pass);
+      match(pass);
+#pragma unroll
+      for (int k = 0; k < K; ++k) my += e_of(pass, k);
+    }
+    uint32_t part_total;
+    block_exclusive_sum<NT>(my, s_tot, &part_total);
+    const uint64_t obase = allocate_output(d, p, part_total, part_out_begin, part_out_count, s_base);
+    if (obase + part_total > d.capacity) return;
+    uint64_t run = obase;
+    for (uint32_t pass = 0; pass < n_pass; ++pass) {
+      load(pass);
+      match(pass);
+      const uint32_t pass_total = pass_offsets<K, NT>([&](int k) { return e_of(pass, k); }, s_tot);
+      write_pass(pass, run);
+      run += pass_total;
+      __syncthreads();  // s_tot is reused by the next pass
+    }
   }
 }
 
@@ -2047,9 +2070,10 @@ __device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t
   }
 }
 
-// One 1024-thread workgroup per partition whose build side fits one LDS table - every partition unless keys are
-// skewed. A skewed partition is appended to d.skewed and left to join_partition_skewed, so that this kernel carries
-// only the fast path's registers (the sub-table path would spill at this kernel's 8-waves-per-SIMD budget).
+// One 1024-thread workgroup per partition whose build side fits one LDS table and whose probe records fit one pass -
+// every partition unless keys are skewed. Any other partition is appended to d.skewed and left to
+// join_partition_skewed, so that this kernel carries only the fast path's registers (the sub-table and multi-pass
+// paths would spill at this kernel's 8-waves-per-SIMD budget).
 template <typename Src, typename P, bool TRACE, int JP, int NT>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT >= 1024 ? 8 : 4, 8))) void join_partition(
     JoinDesc d, Src build, Src probe, hy_row_id* __restrict__ out_build, hy_row_id* __restrict__ out_probe,
@@ -2063,13 +2087,49 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT >= 1024 ?
     if (threadIdx.x == 0) d.skewed[atomicAdd(d.n_skewed, 1u)] = p;
     return;
   }
+  // (the probe records of one pass start at a multiple of the group size: up to V - 1 leading ones are skipped)
+  if (d.probe_begin[p + 1] - d.probe_begin[p] + (Src::V - 1) > static_cast<uint32_t>(JP * NT)) {
+    if (threadIdx.x == 0) d.multi[atomicAdd(d.n_multi, 1u)] = p;
+    return;
+  }
   trace_stamp<TRACE>(d, p, 0);
   partition_one_table<Src, P, TRACE, JP, NT>(d, p, smem, build, probe, out_build, out_probe, part_out_begin,
                                              part_out_count, s_tot, &s_base);
   trace_stamp<TRACE>(d, p, 4);
 }
 
-// The skewed partitions join_partition listed (launched after it on the same stream): a small grid loops over them.
+// Partitions with more probe records than one pass of join_partition (their build side fits one table): a grid of at
+// most two workgroups per CU loops over the list join_partition wrote (launched after it on the same stream) - or,
+// with d.multi null (the host expects most partitions to need several passes), one workgroup per partition instead of
+// join_partition.
+template <typename Src, typename P, int JP, int NT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT >= 1024 ? 8 : 4, 8))) void join_partition_multi(
+    JoinDesc d, Src build, Src probe, hy_row_id* __restrict__ out_build, hy_row_id* __restrict__ out_probe,
+    uint64_t* __restrict__ part_out_begin, uint32_t* __restrict__ part_out_count) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ uint32_t s_tot[JP * (NT / WAVE) + 1];
+  __shared__ uint64_t s_base;
+  if (d.multi == nullptr) {  // every partition (most need several passes): one workgroup each, skewed ones deferred
+    const uint32_t p = blockIdx.x;
+    if (p >= d.n_parts) return;
+    if (d.build_begin[p + 1] - d.build_begin[p] > d.lds_max_build) {
+      if (threadIdx.x == 0) d.skewed[atomicAdd(d.n_skewed, 1u)] = p;
+      return;
+    }
+    partition_one_table<Src, P, false, JP, NT, true>(d, p, smem, build, probe, out_build, out_probe, part_out_begin,
+                                                     part_out_count, s_tot, &s_base);
+    return;
+  }
+  const uint32_t n = *d.n_multi;
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    partition_one_table<Src, P, false, JP, NT, true>(d, d.multi[i], smem, build, probe, out_build, out_probe,
+                                                     part_out_begin, part_out_count, s_tot, &s_base);
+    __syncthreads();  // s_tot / s_base / LDS reused by the next partition
+  }
+}
+
+// The skewed partitions join_partition listed (launched after it on the same stream): a small grid loops over them,
+// each as consecutive LDS sub-tables and probe passes of JS_PER records per thread.
 // Partition ranges are located by part_out_begin / count, so their order in the buffer does not matter.
 template <typename Src, typename P, int NT>
 __global__ __launch_bounds__(NT) void join_partition_skewed(JoinDesc d, Src build, Src probe,

@@ -184,3 +184,19 @@ def test_join_column_referencing_several_tables(hy, oracle, mode):
         j.execute()
         exp, _ = oracle.join_hash(left, right, getattr(hy.JoinMode, mode), (0, 0))
         assert_identical(j.get_output(), exp)
+
+
+@pytest.mark.parametrize("mode", ["Inner", "Left", "Semi", "Anti"])
+def test_probe_skew_needs_several_passes(hy, oracle, mode):
+    """A few hot probe keys put tens of thousands of probe rows into single radix partitions while the average
+    partition takes one pass: those partitions are listed by join_partition and joined by join_partition_multi
+    (several probe passes), the rest in one pass; every partition's PosLists equal the oracle's."""
+    rng = np.random.default_rng(31)
+    build = rng.permutation(np.arange(200_000, dtype=np.int32))
+    probe = np.where(rng.random(300_000) < 0.3, rng.integers(0, 3, 300_000), rng.integers(0, 260_000, 300_000))
+    a = hy.Table.from_arrays([("k", hy.DataType.Int, False)], [build], [], 50_000)
+    b = hy.Table.from_arrays([("k", hy.DataType.Int, False)], [probe.astype(np.int32)], [], 65_536)
+    j = hy.JoinHash(wrap(hy, a), wrap(hy, b), getattr(hy.JoinMode, mode), (0, 0), hy.PredicateCondition.Equals)
+    j.execute()
+    exp, _ = oracle.join_hash(a, b, getattr(hy.JoinMode, mode), (0, 0))
+    assert_identical(j.get_output(), exp)

@@ -7,7 +7,8 @@
   the read bytes are doubled; WRITE_SIZE is taken as is.
 
 Kernel names are shortened to the framework's kernel function name (hyk::<name>) so they line up with bench.py's
-per-kernel table.
+per-kernel table; a partition kernel's side comes from its template tag (hyk::OnBuild / hyk::OnProbe), so each launch
+is attributed from its own name.
 """
 import csv
 import glob
@@ -19,20 +20,18 @@ from collections import defaultdict
 
 
 def short(name):
+    """hyk::<kernel>, plus .build / .probe / .exchange for the partition kernels, whose first template argument
+    (hyk::OnBuild / hyk::OnProbe / hyk::OnExchange) names the join side of the launch."""
     m = re.search(r"hyk::(\w+)", name)
-    return m.group(1) if m else name[:60]
+    if not m:
+        return name[:60]
+    side = re.search(r"hyk::On(Build|Probe|Exchange)", name)
+    return m.group(1) + ("." + side.group(1).lower() if side else "")
 
 
 def one(pattern):
     files = sorted(glob.glob(pattern, recursive=True))
     return files[-1] if files else None
-
-
-def split_sides(launches, steps):
-    """True when the launches alternate build / probe sides (an even count per step)."""
-    if steps:
-        return launches % (2 * steps) == 0
-    return launches % 2 == 0
 
 
 def main(out, steps=None):
@@ -47,21 +46,6 @@ def main(out, steps=None):
                 acc[k][1] += float(row["TotalDurationNs"])
         for k, (calls, tot) in acc.items():
             res["kernels"].setdefault(k, {}).update(calls=calls, avg_ns=tot / calls, total_ns=tot)
-    trace = one(os.path.join(out, "trace", "**", "*kernel_trace.csv"))
-    if trace:  # per-side average durations of the partition kernels (launch order: build, probe)
-        durs = defaultdict(list)
-        with open(trace) as f:
-            for row in csv.DictReader(f):
-                k = short(row["Kernel_Name"])
-                if k.startswith(("part1_", "part2_")):
-                    durs[k].append((int(row["Dispatch_Id"]), int(row["End_Timestamp"]) - int(row["Start_Timestamp"])))
-        for k, v in durs.items():
-            if not split_sides(len(v), None):
-                continue
-            v.sort()
-            for tag, sel in ((".build", v[0::2]), (".probe", v[1::2])):
-                if sel:
-                    res["kernels"].setdefault(k + tag, {}).update(calls=len(sel), avg_ns=sum(x for _, x in sel) / len(sel))
     for counter, scale in (("FETCH_SIZE", 2.0), ("WRITE_SIZE", 1.0)):
         f = one(os.path.join(out, counter, "**", "*counter_collection.csv"))
         if not f:
@@ -78,12 +62,6 @@ def main(out, steps=None):
         by_kernel = defaultdict(list)
         for d, v in per_dispatch.items():
             by_kernel[names[d]].append(v * 1024.0 * scale)
-        # partition kernels run once per join side, build first: split their launches into .build / .probe (only when
-        # a step launches them a multiple of twice - the fused path partitions both sides in one launch)
-        for k in [k for k in by_kernel if k.startswith(("part1_", "part2_")) and split_sides(len(by_kernel[k]), steps)]:
-            ordered = [v for d, v in sorted(((int(d), v) for d, v in per_dispatch.items() if names[d] == k))]
-            by_kernel[k + ".build"] = [v * 1024.0 * scale for v in ordered[0::2]]
-            by_kernel[k + ".probe"] = [v * 1024.0 * scale for v in ordered[1::2]]
         key = "hbm_read_bytes_per_launch" if counter == "FETCH_SIZE" else "hbm_write_bytes_per_launch"
         for k, vals in by_kernel.items():
             res["kernels"].setdefault(k, {})[key] = sum(vals) / len(vals)
@@ -94,8 +72,8 @@ def main(out, steps=None):
     if steps:  # the PMC runs' steps (warmup + timed): HBM bytes of one step over every kernel of the path
         total = 0.0
         for k, v in res["kernels"].items():
-            if k.startswith("stream_") or k.endswith((".build", ".probe")) or "hbm_bytes_per_launch" not in v:
-                continue  # the roofline probe is not part of a step; .build/.probe split the same launches
+            if k.startswith("stream_") or "hbm_bytes_per_launch" not in v:
+                continue  # the roofline probe is not part of a step
             total += v["hbm_bytes_per_launch"] * v.get("hbm_read_bytes_launches", 0)
         res["hbm_bytes_per_step"] = total / steps
         res["pmc_steps"] = steps
