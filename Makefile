@@ -32,7 +32,7 @@ $(LIB)/hyrise_amd.o: $(CSRC)/capi/hyrise_amd.hip $(CSRC)/kernels/scan.hip $(CSRC
 
 $(LIB)/hyrise_amd_aggregate.o: $(CSRC)/capi/hyrise_amd_aggregate.hip $(CSRC)/kernels/aggregate.hip $(CSRC)/kernels/projection.hip \
                                 $(CSRC)/kernels/aggregate_fused.hip $(CSRC)/kernels/aggregate_lanes.hip \
-                                $(CSRC)/kernels/aggregate_vec.hip $(CAPI_HDR)
+                                $(CSRC)/kernels/aggregate_vec.hip $(CSRC)/kernels/aggregate_stream.hip $(CAPI_HDR)
 	@mkdir -p $(LIB)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 

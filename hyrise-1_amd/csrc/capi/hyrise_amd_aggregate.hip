@@ -15,6 +15,7 @@
 #include "../kernels/aggregate_fused.hip"
 #include "../kernels/aggregate_lanes.hip"
 #include "../kernels/aggregate_vec.hip"
+#include "../kernels/aggregate_stream.hip"
 
 using namespace hyc;
 
@@ -96,6 +97,8 @@ struct AggPlan {
   std::vector<int32_t> lane_cols;          // input column of each loaded column
   bool lanes_vec = false;                  // agg_dense_lanes<.., VEC>: data input, 16-byte aligned column chunks
   bool dense_vec = false;                  // agg_dense_vec instead (its preconditions hold; the default then)
+  bool dense_stream = false;               // agg_dense_stream instead (its preconditions hold; the default then)
+  hyk::StreamLayout stream_layout{};       // its stage layout
 };
 
 // agg_dense_fused applies: the dense path; at most one PosList group; int32 group-by columns; every aggregate over a
@@ -179,6 +182,67 @@ void plan_fused(const hy_agg_input* in, const hy_agg_params* p, AggPlan* plan) {
     if (plan->d.fns[a].limbs && plan->d.fns[a].limbs != hyk::FLOAT_LIMBS) return;
   plan->fused = true;
 }
+
+// agg_dense_stream (aggregate_stream.hip) takes what agg_dense_vec takes when, in addition, every DICT chunk of a
+// loaded column has <= ST_DICT_MAX entries (decoded through the wave's LDS tables), at most ST_DCOLS loaded columns have
+// DICT chunks, at most ST_VALS loaded columns besides the group-by columns, the filter (if any) is a dictionary id range
+// on every chunk, the tile ids fit the step numbering and one step's column bytes (256 rows x each column's widest
+// chunk width) fit the stage. HY_AGG_STREAM=0: agg_dense_vec.
+void plan_stream(const hy_agg_input* in, AggPlan* plan) {
+  plan->dense_stream = false;
+  if (!plan->dense_vec) return;
+  if (const char* e = std::getenv("HY_AGG_STREAM"))
+    if (std::atoi(e) == 0) return;
+  if (plan->n_tiles >= (1ull << 28)) return;
+  if (plan->lt.n_load - static_cast<int32_t>(plan->d.n_gb) > hyk::ST_VALS) return;
+  hyk::StreamLayout L{};
+  uint32_t off = 0, slots = 0;
+  for (size_t li = 0; li < plan->lane_cols.size(); ++li) {
+    const auto& col = in->columns[plan->lane_cols[li]];
+    uint32_t width = 1;
+    bool dict = false;
+    for (uint32_t k = 0; k < col.n_chunks; ++k) {
+      const auto& ch = col.chunks[k];
+      if (ch.size == 0) continue;
+      if (ch.kind == HY_COL_DICT) {
+        if (ch.dictionary_size > hyk::ST_DICT_MAX) return;
+        dict = true;
+        width = std::max<uint32_t>(width, static_cast<uint32_t>(ch.vid_width));
+      } else {
+        width = 4;
+      }
+    }
+    L.col_off[li] = off;
+    off += 256u * width;
+    L.dict_slot[li] = hyk::ST_NO_SLOT;
+    if (dict) {
+      if (slots >= static_cast<uint32_t>(hyk::ST_DCOLS)) return;
+      L.dict_slot[li] = slots++;
+    }
+  }
+  if (in->filter) {
+    uint32_t width = 1;
+    for (uint32_t k = 0; k < in->n_chunks; ++k) {
+      const auto& f = in->filter[k];
+      if (f.column.size == 0) continue;
+      if (f.column.kind != HY_COL_DICT) return;
+      switch (f.op) {
+        case HY_OP_EQ: case HY_OP_NE: case HY_OP_LT: case HY_OP_LE: case HY_OP_GT: case HY_OP_GE:
+        case HY_OP_ALL: case HY_OP_IS_NOT_NULL: case HY_OP_NONE:
+          break;
+        default:
+          return;  // no id-range form (VID_SET, ...)
+      }
+      width = std::max<uint32_t>(width, static_cast<uint32_t>(f.column.vid_width));
+    }
+    L.filt_off = off;
+    off += 256u * width;
+  }
+  if (off > static_cast<uint32_t>(hyk::ST_STAGE)) return;
+  plan->stream_layout = L;
+  plan->dense_stream = true;
+}
+
 
 // agg_dense_lanes applies on top of agg_dense_fused: no MIN / MAX; every loaded column (group-by columns, columns
 // of SUM / AVG / COUNT inputs and of their expressions) 4 bytes wide, read through the single PosList group (or
@@ -363,6 +427,7 @@ void plan_lanes(const hy_agg_input* in, const hy_agg_params* p, AggPlan* plan) {
   for (int32_t q = 0; q < lp.n_sums && dv; ++q) dv = lp.sum_len[q] <= hyk::VEC_TERMS;
   dv = dv && lp.n_load <= hyk::VEC_COLS;
   plan->dense_vec = dv;
+  plan_stream(in, plan);
 }
 
 // Record bytes a hash table may take without a caller-given bound (at load 1/2: 2 slots per expected group).
@@ -457,6 +522,52 @@ void launch_dense_vec(bool all_float, uint64_t n_tiles, size_t lds, hipStream_t 
     launch_dense_vec_t<N, true>(n_tiles, lds, s, d, lp, records);
   else
     launch_dense_vec_t<N, false>(n_tiles, lds, s, d, lp, records);
+}
+
+// agg_dense_stream<n_sums, all float sums>, persistent: as many workgroups as are resident at once.
+template <int N, bool ALLF>
+void launch_dense_stream_t(uint64_t n_tiles, hipStream_t s, const hyk::AggDesc& d, const hyk::LanePlan& lp,
+                           const hyk::StreamLayout* layout, unsigned long long* records) {
+  static int resident = 0;
+  if (resident == 0) {
+    int per_cu = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hyk::agg_dense_stream<N, ALLF>, hyk::AGG_THREADS, 0) !=
+            hipSuccess ||
+        hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      per_cu = 4, cus = 256;
+    resident = std::max(1, per_cu) * std::max(1, cus);
+  }
+  // a wave takes whole tiles: enough workgroups for every tile a wave of its own, at most the resident ones
+  const uint64_t want = (n_tiles + hyk::ST_WAVES - 1) / hyk::ST_WAVES;
+  const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want, resident)));
+  hipLaunchKernelGGL((hyk::agg_dense_stream<N, ALLF>), dim3(grid), dim3(hyk::AGG_THREADS), 0, s, d, lp, layout,
+                     records);
+}
+
+void launch_dense_stream(int n_sums, bool all_float, uint64_t n_tiles, hipStream_t s, const hyk::AggDesc& d,
+                         const hyk::LanePlan& lp, const hyk::StreamLayout* layout, unsigned long long* records) {
+  switch (n_sums) {
+#define HY_STREAM_CASE(N)                                                                  \
+  case N:                                                                                  \
+    if (all_float)                                                                         \
+      launch_dense_stream_t<N, true>(n_tiles, s, d, lp, layout, records);                  \
+    else                                                                                   \
+      launch_dense_stream_t<N, false>(n_tiles, s, d, lp, layout, records);                 \
+    return;
+    HY_STREAM_CASE(0)
+    HY_STREAM_CASE(1)
+    HY_STREAM_CASE(2)
+    HY_STREAM_CASE(3)
+    HY_STREAM_CASE(4)
+    HY_STREAM_CASE(5)
+    HY_STREAM_CASE(6)
+    HY_STREAM_CASE(7)
+    HY_STREAM_CASE(8)
+#undef HY_STREAM_CASE
+    default:
+      break;
+  }
 }
 
 void launch_lanes(int n_sums, bool vec, bool dense_vec, bool all_float, uint64_t n_tiles, size_t lds, hipStream_t s,
@@ -672,6 +783,7 @@ struct AggWs {
   hyk::LnTerm* lane_terms;       // agg_dense_lanes: its chains
   uint32_t* deferred;            // agg_dense_lanes: steps left to agg_dense_fused
   hyk::LaneTables* lane_tables;
+  hyk::StreamLayout* stream_layout;
   hy_scan_chunk* filter;         // fused TableScan predicate chunks
   void* mat_values[hyk::AGG_MAX_COLUMNS];    // materialised expression columns
   uint8_t* mat_nulls[hyk::AGG_MAX_COLUMNS];
@@ -694,6 +806,7 @@ void carve(Carver& cv, const hy_agg_input* in, const AggPlan& plan, AggWs* w) {
   w->fused_nodes = cv.take<hyk::FqOp>(std::max<size_t>(1, plan.fused_nodes.size()));
   w->lane_terms = cv.take<hyk::LnTerm>(plan.lane_terms.size() + hyk::VEC_TERMS);  // padding: agg_dense_vec
   w->lane_tables = cv.take<hyk::LaneTables>(1);
+  w->stream_layout = cv.take<hyk::StreamLayout>(1);
   w->filter = cv.take<hy_scan_chunk>(in->filter ? std::max<uint32_t>(1, in->n_chunks) : 1);
   w->deferred = cv.take<uint32_t>(plan.lanes ? std::max<uint64_t>(1, plan.n_tiles * hyk::FQ_STEPS_PER_TILE) : 1);
   for (uint32_t e = 0; e < plan.expr_cols.size(); ++e) {
@@ -883,7 +996,12 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
       const char* eaf = std::getenv("HY_VEC_ALLF");
       bool all_float = !(eaf && std::atoi(eaf) == 0);
       for (int32_t q = 0; q < lt.n_sums; ++q) all_float = all_float && lt.sum_kind[q] != hyk::LN_SUM_INT;
-      {
+      if (plan.dense_stream) {
+        HY_STAGE(w.stream_layout, &plan.stream_layout, sizeof(plan.stream_layout), s);
+        KTimer t("agg_dense_stream", s, plan.rows);
+        launch_dense_stream(lp.n_sums, all_float, plan.n_tiles, s, d, lp, w.stream_layout, w.records);
+        t.done();
+      } else {
         KTimer t(plan.dense_vec ? "agg_dense_vec" : "agg_dense_lanes", s, plan.rows);
         launch_lanes(lp.n_sums, plan.lanes_vec, plan.dense_vec, all_float, plan.n_tiles, vlds, s, d, lp, w.records);
         t.done();

@@ -724,7 +724,8 @@ uint32_t lds_table_rows() {
 }
 
 // Per-partition LDS build/probe over partitioned records (partition bounds on the device; the records as the last pass
-// wrote them: hyk::RecSrc or hyk::HashSrc). probe_rows_hint: an upper bound of the probe rows; it picks the probe
+// wrote them: hyk::RecSrc or hyk::HashSrc). probe_rows_hint: an upper bound of the probe rows (probe_exact: their
+// number); it picks the probe
 // records per thread (JP) from the average partition, and the kernel: join_partition (one pass of probe records per
 // partition; a partition needing more passes is listed for join_partition_multi) or, when the average partition needs
 // several passes, join_partition_multi over every partition. Partitions with more build rows than one LDS table
@@ -735,7 +736,8 @@ hy_status run_join_partitions(const uint32_t* build_begin, const uint32_t* probe
                               const Src& bsrc, const Src& psrc, const hyk::RowMap& bmap, const hyk::RowMap& pmap,
                               int32_t mode, hy_row_id* out_build, hy_row_id* out_probe, uint64_t out_capacity,
                               uint64_t* partition_begin, uint32_t* partition_counts, hy_join_result* result,
-                              const Common& c, hipStream_t s, uint64_t units, uint64_t probe_rows_hint) {
+                              const Common& c, hipStream_t s, uint64_t units, uint64_t probe_rows_hint,
+                              bool probe_exact) {
   using H = typename Src::Key;
   constexpr int NT = hyk::JOIN_THREADS;
   // probe records per thread per pass: the wide variant (6) when the average partition needs more than 3/4 of JP_PER
@@ -766,7 +768,8 @@ hy_status run_join_partitions(const uint32_t* build_begin, const uint32_t* probe
   constexpr int JW = Src::V == 1 ? 6 : 8;  // the wide variant's probe records per thread (a multiple of V)
   // most partitions need several probe passes (the average exceeds 3/4 of the wide pass): the multi-pass kernel takes
   // every partition directly instead of the one-pass kernel deferring nearly all of them
-  const bool all_multi = avg_probe > static_cast<uint64_t>(3 * JW * NT / 4) && !jd.trace;
+  // (only when the probe rows are known: a filtered probe side's hint is its rows before the filter)
+  const bool all_multi = probe_exact && avg_probe > static_cast<uint64_t>(3 * JW * NT / 4) && !jd.trace;
   if (n_parts && all_multi) {
     jd.multi = nullptr;
     KTimer kt_("join_partition", s, units);
@@ -1167,7 +1170,7 @@ hy_status join_typed_onepass(const SidePlan& bp, const SidePlan& pp, const hy_jo
                                                                hyk::RecSrc<H, uint32_t>{recs[0]},
                                                                hyk::RecSrc<H, uint32_t>{recs[1]}, bmap, pmap, prm->mode,
                                         out_build, out_probe, out_capacity, partition_begin, partition_counts, result,
-                                        c, s, bp.n_rows + pp.n_rows, pp.n_rows);
+                                        c, s, bp.n_rows + pp.n_rows, pp.n_rows, !pp.filtered);
   HY_HIP(hipStreamSynchronize(s));  // the flags' copies (run_join_partitions has synchronised on success)
   *overflow = flags[0] | flags[1];
   return st;
@@ -1328,13 +1331,14 @@ hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join
   // filtered sides emit RowIDs of their data table (the scan's PosLists dereferenced, write_output_columns)
   const hyk::RowMap bmap = bp.fuse ? make_map(bb.ref_row_begin, bp.ref_row_begin) : make_map(bb.row_begin, bp.row_begin);
   const hyk::RowMap pmap = pp.fuse ? make_map(pb.ref_row_begin, pp.ref_row_begin) : make_map(pb.row_begin, pp.row_begin);
+  const bool probe_exact = !pp.filtered && !use_bloom;  // (a Bloom prefilter drops probe rows too)
   if (soa) {
     auto run_hash = [&](auto tag) {
       using HS = decltype(tag);
       return run_join_partitions<HS, uint32_t>(bounds[0], bounds[1], 1u << bits, HS{soa_outs[0].hk, soa_outs[0].pay},
                                                HS{soa_outs[1].hk, soa_outs[1].pay}, bmap, pmap, prm->mode, out_build,
                                                out_probe, out_capacity, partition_begin, partition_counts, result, c,
-                                               s, bp.n_rows + pp.n_rows, pp.n_rows);
+                                               s, bp.n_rows + pp.n_rows, pp.n_rows, probe_exact);
     };
     const char* g = std::getenv("HY_HASH_GROUP");  // records per lane and load (A/B): 1 (default) or 4
     return (g && std::strtol(g, nullptr, 10) == 4) ? run_hash(hyk::HashSrc<uint32_t, 4>{})
@@ -1343,7 +1347,7 @@ hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join
   return run_join_partitions<hyk::RecSrc<H, uint32_t>, uint32_t>(
       bounds[0], bounds[1], 1u << bits, hyk::RecSrc<H, uint32_t>{recs[0]}, hyk::RecSrc<H, uint32_t>{recs[1]}, bmap,
       pmap, prm->mode, out_build, out_probe, out_capacity, partition_begin, partition_counts, result, c, s,
-      bp.n_rows + pp.n_rows, pp.n_rows);
+      bp.n_rows + pp.n_rows, pp.n_rows, probe_exact);
 }
 
 template <typename F>
@@ -1622,7 +1626,7 @@ hy_status exchange_join_for_hashed(const void* build_records, const void* probe_
   return run_join_partitions<hyk::RecSrc<H, P>, P>(bounds[0], bounds[1], n_parts, hyk::RecSrc<H, P>{recs[0]},
                                                    hyk::RecSrc<H, P>{recs[1]}, bmap, pmap, params->mode,
                                    out_build, out_probe, out_capacity, partition_begin, partition_counts, result, c, s,
-                                   rbp.rows + rpp.rows, rpp.rows);
+                                   rbp.rows + rpp.rows, rpp.rows, true);
 }
 
 template <typename H>

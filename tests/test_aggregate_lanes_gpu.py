@@ -41,6 +41,8 @@ def columns(rng, case):
     if case == "nulls":
         price_n = (rng.random(N) < 0.002).astype(np.uint8)
         disc_n = (rng.random(N) < 0.001).astype(np.uint8)
+    elif case == "null_ids":  # NULL value ids in a small-dictionary column only (agg_dense_stream defers their steps)
+        disc_n = (rng.random(N) < 0.001).astype(np.uint8)
     elif case == "odd_values":  # steps leave the window / hold non-finite, denormal, negative, zero values
         price[rng.random(N) < 0.0005] = np.float32(-3.5e-30)
         price[rng.random(N) < 0.0005] = np.float32(7.0e25)
@@ -203,7 +205,19 @@ def kernels_ran(L):
     return names
 
 
-@pytest.mark.parametrize("case", ["clean", "nulls", "odd_values", "wide_range", "drift", "many_groups", "clustered"])
+# data-input kernels under test: (HY_AGG_VEC, HY_AGG_STREAM) -> the kernel that must run (agg_dense_stream where its
+# preconditions hold - every dictionary <= 63 entries, so not with the "nulls" case's dictionary-encoded prices)
+DATA_MODES = [("2", "1"), ("2", "0"), ("1", "0"), ("0", "0")]
+
+
+def data_kernel(vec_mode, stream_mode, stream_ok):
+    if vec_mode != "2":
+        return "agg_dense_lanes"
+    return "agg_dense_stream" if stream_mode == "1" and stream_ok else "agg_dense_vec"
+
+
+@pytest.mark.parametrize("case", ["clean", "nulls", "null_ids", "odd_values", "wide_range", "drift", "many_groups",
+                                  "clustered"])
 @pytest.mark.parametrize("input_kind", ["data", "reference", "reference_mixed"])
 def test_lanes_path(hy, monkeypatch, case, input_kind):
     capi = hy.capi
@@ -240,20 +254,22 @@ def test_lanes_path(hy, monkeypatch, case, input_kind):
             sizes.append(pl.shape[0])
             rows += [int(i) * CHUNK + int(o) for i, o in zip(ids, offs)]
     exp = expected(cols, rows)
-    # data input: agg_dense_vec (default), agg_dense_lanes' contiguous instance (HY_AGG_VEC=1) and its strided one (0)
+    # data input: agg_dense_stream (default), agg_dense_vec (HY_AGG_STREAM=0), agg_dense_lanes' contiguous instance
+    # (HY_AGG_VEC=1) and its strided one (0)
     headers = {}
-    for vec_mode in (("2", "1", "0") if input_kind == "data" else ("2",)):
+    for vec_mode, stream_mode in (DATA_MODES if input_kind == "data" else [("2", "1")]):
         monkeypatch.setenv("HY_AGG_VEC", vec_mode)
+        monkeypatch.setenv("HY_AGG_STREAM", stream_mode)
         L.hy_kernel_stats_enable(1)
         L.hy_kernel_stats_reset()
         res_lanes = run(hy, dcols, pos, sizes, doms)
         ran = kernels_ran(L)
         L.hy_kernel_stats_enable(0)
-        want = "agg_dense_vec" if (input_kind == "data" and vec_mode == "2") else "agg_dense_lanes"
-        assert want in ran, (vec_mode, ran)
+        want = data_kernel(vec_mode, stream_mode, case != "nulls") if input_kind == "data" else "agg_dense_lanes"
+        assert want in ran, (vec_mode, stream_mode, ran)
         check(res_lanes, exp)
-        headers[vec_mode] = {(int(r[0]), int(r[1])): tuple(int(x) for x in r[2:6])
-                             for r in run(hy, dcols, pos, sizes, doms, raw=True)[0]}
+        headers[vec_mode + stream_mode] = {(int(r[0]), int(r[1])): tuple(int(x) for x in r[2:6])
+                                           for r in run(hy, dcols, pos, sizes, doms, raw=True)[0]}
     monkeypatch.setenv("HY_AGG_LANES", "0")
     # NULL mask, first row, last row, rows of every group (the Aggregate's output order follows the first rows)
     fused_headers = {(int(r[0]), int(r[1])): tuple(int(x) for x in r[2:6])
@@ -342,16 +358,25 @@ def test_fused_scan_filter(hy, monkeypatch, case, pred_enc, cond, value):
     sizes = [d.size for d in dcols[0].descs]
     op = {"LessThanEquals": np.less_equal, "LessThan": np.less, "GreaterThan": np.greater}[cond]
     rows = list(np.nonzero(op(ship, value))[0])
-    for vec_mode in ("2", "0"):  # agg_dense_vec, agg_dense_lanes (strided)
+    for vec_mode, stream_mode in (("2", "1"), ("2", "0"), ("0", "0")):  # stream, vec, lanes (strided)
         monkeypatch.setenv("HY_AGG_VEC", vec_mode)
+        monkeypatch.setenv("HY_AGG_STREAM", stream_mode)
+        capi.lib.hy_kernel_stats_enable(1)
+        capi.lib.hy_kernel_stats_reset()
         res = run(hy, dcols, None, sizes, doms, filt=(chunks, capi.HY_TYPE_INT32, pred.constant(value)))
+        ran = kernels_ran(capi.lib)
+        capi.lib.hy_kernel_stats_enable(0)
+        # agg_dense_stream takes dictionary id-range filters only
+        assert data_kernel(vec_mode, stream_mode, case != "nulls" and pred_enc == "Dictionary") in ran, ran
         check(res, expected(cols, rows))
 
 
-@pytest.mark.parametrize("case", ["clean", "nulls", "drift"])
+@pytest.mark.parametrize("case", ["clean", "nulls", "null_ids", "drift"])
 @pytest.mark.parametrize("cond,value", [("LessThanEquals", 300), ("GreaterThan", 700)])
-def test_fused_scan_filter_against_oracle(hy, oracle, monkeypatch, case, cond, value):
-    """agg_dense_vec with the TableScan fused (TPC-H 1's default plan) against the ORACLE's plan on the same table:
+@pytest.mark.parametrize("stream_mode", ["1", "0"])
+def test_fused_scan_filter_against_oracle(hy, oracle, monkeypatch, case, cond, value, stream_mode):
+    """agg_dense_stream / agg_dense_vec with the TableScan fused (TPC-H 1's default plan) against the ORACLE's plan on
+    the same table:
     oracle TableScan (single_column_table_scan_impl.cpp) -> Projection of the two float expressions
     (projection.cpp:39-87) -> Aggregate (aggregate.cpp:203-249, sequential double sums). Group keys, counts and int
     sums equal; every float SUM / AVG is the exactly rounded sum (== math.fsum of the projected values) and within
@@ -370,13 +395,14 @@ def test_fused_scan_filter_against_oracle(hy, oracle, monkeypatch, case, cond, v
     pred = dt.DeviceColumn(capi, ship, None, CHUNK, "Dictionary")
     sizes = [d.size for d in dcols[0].descs]
     monkeypatch.setenv("HY_AGG_VEC", "2")
+    monkeypatch.setenv("HY_AGG_STREAM", stream_mode)
     L.hy_kernel_stats_enable(1)
     L.hy_kernel_stats_reset()
     res = run(hy, dcols, None, sizes, doms,
               filt=(pred.scan_chunks(cond, value), capi.HY_TYPE_INT32, pred.constant(value)))
     ran = kernels_ran(L)
     L.hy_kernel_stats_enable(0)
-    assert "agg_dense_vec" in ran, ran
+    assert data_kernel("2", stream_mode, case != "nulls") in ran, ran
 
     # the oracle's plan over a table of the same columns
     T = hy.DataType
