@@ -98,7 +98,7 @@ struct AggPlan {
   bool lanes_vec = false;                  // agg_dense_lanes<.., VEC>: data input, 16-byte aligned column chunks
   bool dense_vec = false;                  // agg_dense_vec instead (its preconditions hold; the default then)
   bool dense_stream = false;               // agg_dense_stream instead (its preconditions hold; the default then)
-  hyk::StreamLayout stream_layout{};       // its stage layout
+  hyk::StreamPlan stream_plan{};           // its stage layout and FMA-form chains
 };
 
 // agg_dense_fused applies: the dense path; at most one PosList group; int32 group-by columns; every aggregate over a
@@ -187,7 +187,8 @@ void plan_fused(const hy_agg_input* in, const hy_agg_params* p, AggPlan* plan) {
 // loaded column has <= ST_DICT_MAX entries (decoded through the wave's LDS tables), at most ST_DCOLS loaded columns have
 // DICT chunks, at most ST_VALS loaded columns besides the group-by columns, the filter (if any) is a dictionary id range
 // on every chunk, the tile ids fit the step numbering and one step's column bytes (256 rows x each column's widest
-// chunk width) fit the stage. HY_AGG_STREAM=0: agg_dense_vec.
+// chunk width) fit the stage, float sums are + - * chains (compiled to FMA-form terms), int32 sums plain columns and
+// the group codes < ST_CODES. HY_AGG_STREAM=0: agg_dense_vec.
 void plan_stream(const hy_agg_input* in, AggPlan* plan) {
   plan->dense_stream = false;
   if (!plan->dense_vec) return;
@@ -195,7 +196,7 @@ void plan_stream(const hy_agg_input* in, AggPlan* plan) {
     if (std::atoi(e) == 0) return;
   if (plan->n_tiles >= (1ull << 28)) return;
   if (plan->lt.n_load - static_cast<int32_t>(plan->d.n_gb) > hyk::ST_VALS) return;
-  hyk::StreamLayout L{};
+  hyk::StreamPlan L{};
   uint32_t off = 0, slots = 0;
   for (size_t li = 0; li < plan->lane_cols.size(); ++li) {
     const auto& col = in->columns[plan->lane_cols[li]];
@@ -239,7 +240,62 @@ void plan_stream(const hy_agg_input* in, AggPlan* plan) {
     off += 256u * width;
   }
   if (off > static_cast<uint32_t>(hyk::ST_STAGE)) return;
-  plan->stream_layout = L;
+  // the sums: float chains as FMA-form terms (hyk::StreamTerm), int32 sums of plain columns, COUNT-only inputs
+  const auto& lt = plan->lt;
+  for (int32_t q = 0; q < lt.n_sums; ++q) {
+    L.sum_first[q] = lt.sum_first[q];
+    L.sum_len[q] = lt.sum_len[q];
+    if (lt.sum_kind[q] == hyk::LN_SUM_CHECK) {
+      L.sum_kind[q] = hyk::ST_SUM_NONE;
+      continue;
+    }
+    if (lt.sum_kind[q] == hyk::LN_SUM_INT) {
+      const auto& t = plan->lane_terms[lt.sum_first[q]];
+      if (lt.sum_len[q] != 1 || t.kind != hyk::LN_TERM_COL || t.cvt) return;  // int32 chains: agg_dense_vec
+      L.sum_kind[q] = hyk::ST_SUM_INT;
+      L.terms[lt.sum_first[q]] = hyk::StreamTerm{1.f, -0.f, t.col, hyk::ST_SET};
+      continue;
+    }
+    L.sum_kind[q] = hyk::ST_SUM_FLOAT;
+    for (int32_t i = 0; i < lt.sum_len[q]; ++i) {
+      const hyk::LnTerm& t = plan->lane_terms[lt.sum_first[q] + i];
+      float lit;
+      std::memcpy(&lit, &t.lit, 4);
+      hyk::StreamTerm o{1.f, -0.f, t.col, t.cvt ? hyk::ST_CVT : 0};
+      // term = fma(x, a, b): one rounding, as x, lit + x, lit - x, lit * x, x - lit, x * lit compute
+      switch (t.kind) {
+        case hyk::LN_TERM_COL:
+          break;
+        case hyk::LN_TERM_LIT:
+          o = hyk::StreamTerm{0.f, lit, 0, hyk::ST_LIT};
+          break;
+        case hyk::LN_TERM_LIT_COL:
+        case hyk::LN_TERM_COL_LIT:
+          if (t.op == HY_EXPR_ADD) {
+            o.a = 1.f, o.b = lit;
+          } else if (t.op == HY_EXPR_SUB) {
+            if (t.kind == hyk::LN_TERM_LIT_COL) o.a = -1.f, o.b = lit;
+            else o.a = 1.f, o.b = -lit;
+          } else if (t.op == HY_EXPR_MUL) {
+            o.a = lit, o.b = -0.f;
+          } else {
+            return;
+          }
+          break;
+        default:
+          return;
+      }
+      if (i > 0) {
+        if (t.comb == HY_EXPR_ADD) o.flags |= hyk::ST_ADD;
+        else if (t.comb == HY_EXPR_SUB) o.flags |= t.rev ? hyk::ST_RSUB : hyk::ST_SUB;
+        else if (t.comb == HY_EXPR_MUL) o.flags |= hyk::ST_MUL;
+        else return;
+      }
+      L.terms[lt.sum_first[q] + i] = o;
+    }
+  }
+  if (plan->dense_groups > static_cast<uint32_t>(hyk::ST_CODES)) return;
+  plan->stream_plan = L;
   plan->dense_stream = true;
 }
 
@@ -524,14 +580,14 @@ void launch_dense_vec(bool all_float, uint64_t n_tiles, size_t lds, hipStream_t 
     launch_dense_vec_t<N, false>(n_tiles, lds, s, d, lp, records);
 }
 
-// agg_dense_stream<n_sums, all float sums>, persistent: as many workgroups as are resident at once.
-template <int N, bool ALLF>
+// agg_dense_stream<n_sums>, persistent: as many workgroups as are resident at once.
+template <int N>
 void launch_dense_stream_t(uint64_t n_tiles, hipStream_t s, const hyk::AggDesc& d, const hyk::LanePlan& lp,
-                           const hyk::StreamLayout* layout, unsigned long long* records) {
+                           const hyk::StreamPlan* plan, unsigned long long* records) {
   static int resident = 0;
   if (resident == 0) {
     int per_cu = 0, dev = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hyk::agg_dense_stream<N, ALLF>, hyk::AGG_THREADS, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hyk::agg_dense_stream<N>, hyk::AGG_THREADS, 0) !=
             hipSuccess ||
         hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -541,19 +597,15 @@ void launch_dense_stream_t(uint64_t n_tiles, hipStream_t s, const hyk::AggDesc& 
   // a wave takes whole tiles: enough workgroups for every tile a wave of its own, at most the resident ones
   const uint64_t want = (n_tiles + hyk::ST_WAVES - 1) / hyk::ST_WAVES;
   const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want, resident)));
-  hipLaunchKernelGGL((hyk::agg_dense_stream<N, ALLF>), dim3(grid), dim3(hyk::AGG_THREADS), 0, s, d, lp, layout,
-                     records);
+  hipLaunchKernelGGL((hyk::agg_dense_stream<N>), dim3(grid), dim3(hyk::AGG_THREADS), 0, s, d, lp, plan, records);
 }
 
-void launch_dense_stream(int n_sums, bool all_float, uint64_t n_tiles, hipStream_t s, const hyk::AggDesc& d,
-                         const hyk::LanePlan& lp, const hyk::StreamLayout* layout, unsigned long long* records) {
+void launch_dense_stream(int n_sums, uint64_t n_tiles, hipStream_t s, const hyk::AggDesc& d, const hyk::LanePlan& lp,
+                         const hyk::StreamPlan* plan, unsigned long long* records) {
   switch (n_sums) {
-#define HY_STREAM_CASE(N)                                                                  \
-  case N:                                                                                  \
-    if (all_float)                                                                         \
-      launch_dense_stream_t<N, true>(n_tiles, s, d, lp, layout, records);                  \
-    else                                                                                   \
-      launch_dense_stream_t<N, false>(n_tiles, s, d, lp, layout, records);                 \
+#define HY_STREAM_CASE(N)                                            \
+  case N:                                                            \
+    launch_dense_stream_t<N>(n_tiles, s, d, lp, plan, records);      \
     return;
     HY_STREAM_CASE(0)
     HY_STREAM_CASE(1)
@@ -783,7 +835,7 @@ struct AggWs {
   hyk::LnTerm* lane_terms;       // agg_dense_lanes: its chains
   uint32_t* deferred;            // agg_dense_lanes: steps left to agg_dense_fused
   hyk::LaneTables* lane_tables;
-  hyk::StreamLayout* stream_layout;
+  hyk::StreamPlan* stream_plan;
   hy_scan_chunk* filter;         // fused TableScan predicate chunks
   void* mat_values[hyk::AGG_MAX_COLUMNS];    // materialised expression columns
   uint8_t* mat_nulls[hyk::AGG_MAX_COLUMNS];
@@ -806,7 +858,7 @@ void carve(Carver& cv, const hy_agg_input* in, const AggPlan& plan, AggWs* w) {
   w->fused_nodes = cv.take<hyk::FqOp>(std::max<size_t>(1, plan.fused_nodes.size()));
   w->lane_terms = cv.take<hyk::LnTerm>(plan.lane_terms.size() + hyk::VEC_TERMS);  // padding: agg_dense_vec
   w->lane_tables = cv.take<hyk::LaneTables>(1);
-  w->stream_layout = cv.take<hyk::StreamLayout>(1);
+  w->stream_plan = cv.take<hyk::StreamPlan>(1);
   w->filter = cv.take<hy_scan_chunk>(in->filter ? std::max<uint32_t>(1, in->n_chunks) : 1);
   w->deferred = cv.take<uint32_t>(plan.lanes ? std::max<uint64_t>(1, plan.n_tiles * hyk::FQ_STEPS_PER_TILE) : 1);
   for (uint32_t e = 0; e < plan.expr_cols.size(); ++e) {
@@ -997,9 +1049,15 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
       bool all_float = !(eaf && std::atoi(eaf) == 0);
       for (int32_t q = 0; q < lt.n_sums; ++q) all_float = all_float && lt.sum_kind[q] != hyk::LN_SUM_INT;
       if (plan.dense_stream) {
-        HY_STAGE(w.stream_layout, &plan.stream_layout, sizeof(plan.stream_layout), s);
+        hyk::StreamPlan sp = plan.stream_plan;
+        sp.tile_chunk = d.tile_chunk;
+        sp.chunk_tile_begin = d.chunk_tile_begin;
+        sp.chunk_size = d.chunk_size;
+        sp.chunk_row_begin = d.chunk_row_begin;
+        sp.filter = d.filter;
+        HY_STAGE(w.stream_plan, &sp, sizeof(sp), s);
         KTimer t("agg_dense_stream", s, plan.rows);
-        launch_dense_stream(lp.n_sums, all_float, plan.n_tiles, s, d, lp, w.stream_layout, w.records);
+        launch_dense_stream(lp.n_sums, plan.n_tiles, s, d, lp, w.stream_plan, w.records);
         t.done();
       } else {
         KTimer t(plan.dense_vec ? "agg_dense_vec" : "agg_dense_lanes", s, plan.rows);

@@ -22,6 +22,8 @@ N, CHUNK = 60_000, 9_000
 # [rf, ls, qty, price, dp = price * (1 - disc), ch = dp * (1 + tax), disc, tax, iq (int32), iexpr = iq * 3 - 7 (int32)]
 AGGS = [("SUM", 2), ("SUM", 3), ("SUM", 4), ("SUM", 5), ("AVG", 2), ("AVG", 3), ("AVG", 6), ("COUNT", -1),
         ("SUM", 8), ("AVG", 9), ("COUNT", 7)]
+# TPC-H 1's aggregates alone (float sums of columns and chains, COUNT(*)): the shape agg_dense_stream takes
+Q1_AGGS = AGGS[:8]
 
 
 def columns(rng, case):
@@ -92,7 +94,7 @@ def fsum_inf(vals):
     return math.fsum(vals)
 
 
-def run(hy, dcols, pos_lists, sizes, doms, part=None, raw=False, filt=None):
+def run(hy, dcols, pos_lists, sizes, doms, part=None, raw=False, filt=None, aggs=AGGS):
     """hy_aggregate over the input (or over input chunks [lo, hi) with part=(lo, hi)); raw: (records, layout,
     params) instead of the decoded results."""
     capi, L = hy.capi, hy.capi.lib
@@ -128,8 +130,8 @@ def run(hy, dcols, pos_lists, sizes, doms, part=None, raw=False, filt=None):
     if filt is not None:  # fused TableScan: (ScanChunk array, value type, constant array)
         inp.filter, inp.filter_value_type, inp.filter_constant = filt[0], filt[1], filt[2].ctypes.data
     gb = (ctypes.c_int32 * 2)(0, 1)
-    defs = (capi.AggDef * len(AGGS))(*[capi.AggDef(getattr(capi, "HY_AGG_" + f), c) for f, c in AGGS])
-    prm = capi.AggParams(gb, 2, defs, len(AGGS), 0)
+    defs = (capi.AggDef * len(aggs))(*[capi.AggDef(getattr(capi, "HY_AGG_" + f), c) for f, c in aggs])
+    prm = capi.AggParams(gb, 2, defs, len(aggs), 0)
     lay = capi.AggLayout()
     capi.check(L.hy_aggregate_layout(ctypes.byref(inp), ctypes.byref(prm), ctypes.byref(lay)), "layout")
     assert lay.dense == 1
@@ -143,16 +145,16 @@ def run(hy, dcols, pos_lists, sizes, doms, part=None, raw=False, filt=None):
     rec = out.fetch().reshape(-1, lay.words)[:ng.value]
     if raw:
         return rec, lay, prm, (defs, gb)
-    return decode(hy, rec, lay)
+    return decode(hy, rec, lay, aggs)
 
 
-def decode(hy, rec, lay):
+def decode(hy, rec, lay, aggs=AGGS):
     capi, L = hy.capi, hy.capi.lib
     res = {}
     for r in rec:
         g = (int(r[0]), int(r[1]))
         vals = {"rows": int(r[2 + 3])}
-        for a, (f, c) in enumerate(AGGS):
+        for a, (f, c) in enumerate(aggs):
             wd = lay.agg_word[a]
             if c < 0:
                 continue
@@ -174,12 +176,12 @@ def same_float(a, b):
     return (math.isnan(a) and math.isnan(b)) or a == b
 
 
-def check(res, exp):
+def check(res, exp, aggs=AGGS):
     assert set(res) == set(exp)
     for g, e in exp.items():
         r = res[g]
         assert r["rows"] == e["rows"], g
-        for a, (f, c) in enumerate(AGGS):
+        for a, (f, c) in enumerate(aggs):
             if c < 0:
                 continue
             if f == "COUNT":
@@ -265,11 +267,26 @@ def test_lanes_path(hy, monkeypatch, case, input_kind):
         res_lanes = run(hy, dcols, pos, sizes, doms)
         ran = kernels_ran(L)
         L.hy_kernel_stats_enable(0)
-        want = data_kernel(vec_mode, stream_mode, case != "nulls") if input_kind == "data" else "agg_dense_lanes"
+        # (the int32 expression chain of AGGS is not agg_dense_stream's: that set never streams)
+        want = data_kernel(vec_mode, stream_mode, False) if input_kind == "data" else "agg_dense_lanes"
         assert want in ran, (vec_mode, stream_mode, ran)
         check(res_lanes, exp)
         headers[vec_mode + stream_mode] = {(int(r[0]), int(r[1])): tuple(int(x) for x in r[2:6])
                                            for r in run(hy, dcols, pos, sizes, doms, raw=True)[0]}
+    if input_kind == "data":  # TPC-H 1's aggregate set: agg_dense_stream where it applies, against agg_dense_vec
+        for vec_mode, stream_mode in DATA_MODES[:2]:
+            monkeypatch.setenv("HY_AGG_VEC", vec_mode)
+            monkeypatch.setenv("HY_AGG_STREAM", stream_mode)
+            L.hy_kernel_stats_enable(1)
+            L.hy_kernel_stats_reset()
+            res_q1 = run(hy, dcols, pos, sizes, doms, aggs=Q1_AGGS)
+            ran = kernels_ran(L)
+            L.hy_kernel_stats_enable(0)
+            assert data_kernel(vec_mode, stream_mode, case != "nulls") in ran, (stream_mode, ran)
+            check(res_q1, exp, Q1_AGGS)
+            headers["q1/" + vec_mode + stream_mode] = {(int(r[0]), int(r[1])): tuple(int(x) for x in r[2:6])
+                                                       for r in run(hy, dcols, pos, sizes, doms, raw=True,
+                                                                    aggs=Q1_AGGS)[0]}
     monkeypatch.setenv("HY_AGG_LANES", "0")
     # NULL mask, first row, last row, rows of every group (the Aggregate's output order follows the first rows)
     fused_headers = {(int(r[0]), int(r[1])): tuple(int(x) for x in r[2:6])
@@ -358,17 +375,18 @@ def test_fused_scan_filter(hy, monkeypatch, case, pred_enc, cond, value):
     sizes = [d.size for d in dcols[0].descs]
     op = {"LessThanEquals": np.less_equal, "LessThan": np.less, "GreaterThan": np.greater}[cond]
     rows = list(np.nonzero(op(ship, value))[0])
-    for vec_mode, stream_mode in (("2", "1"), ("2", "0"), ("0", "0")):  # stream, vec, lanes (strided)
+    # stream (TPC-H 1's aggregate set), vec, lanes (strided)
+    for vec_mode, stream_mode, aggs in (("2", "1", Q1_AGGS), ("2", "0", AGGS), ("0", "0", AGGS)):
         monkeypatch.setenv("HY_AGG_VEC", vec_mode)
         monkeypatch.setenv("HY_AGG_STREAM", stream_mode)
         capi.lib.hy_kernel_stats_enable(1)
         capi.lib.hy_kernel_stats_reset()
-        res = run(hy, dcols, None, sizes, doms, filt=(chunks, capi.HY_TYPE_INT32, pred.constant(value)))
+        res = run(hy, dcols, None, sizes, doms, filt=(chunks, capi.HY_TYPE_INT32, pred.constant(value)), aggs=aggs)
         ran = kernels_ran(capi.lib)
         capi.lib.hy_kernel_stats_enable(0)
         # agg_dense_stream takes dictionary id-range filters only
         assert data_kernel(vec_mode, stream_mode, case != "nulls" and pred_enc == "Dictionary") in ran, ran
-        check(res, expected(cols, rows))
+        check(res, expected(cols, rows), aggs)
 
 
 @pytest.mark.parametrize("case", ["clean", "nulls", "null_ids", "drift"])
@@ -398,8 +416,9 @@ def test_fused_scan_filter_against_oracle(hy, oracle, monkeypatch, case, cond, v
     monkeypatch.setenv("HY_AGG_STREAM", stream_mode)
     L.hy_kernel_stats_enable(1)
     L.hy_kernel_stats_reset()
+    aggs = Q1_AGGS if stream_mode == "1" else AGGS  # (agg_dense_stream: TPC-H 1's set, no int32 chain)
     res = run(hy, dcols, None, sizes, doms,
-              filt=(pred.scan_chunks(cond, value), capi.HY_TYPE_INT32, pred.constant(value)))
+              filt=(pred.scan_chunks(cond, value), capi.HY_TYPE_INT32, pred.constant(value)), aggs=aggs)
     ran = kernels_ran(L)
     L.hy_kernel_stats_enable(0)
     assert data_kernel("2", stream_mode, case != "nulls") in ran, ran
@@ -423,14 +442,14 @@ def test_fused_scan_filter_against_oracle(hy, oracle, monkeypatch, case, cond, v
     proj = oracle.projection(scan, [c(0), c(1), c(2), c(3), dp, ch, c(4), c(5), c(6), ie])
     F = {"SUM": "Sum", "AVG": "Avg", "COUNT": "Count"}
     defs = [hy.AggregateColumnDefinition(None if col < 0 else col, getattr(hy.AggregateFunction, F[f]))
-            for f, col in AGGS]
+            for f, col in aggs]
     agg = oracle.aggregate(proj, defs, [0, 1])
     want = {(r[0], r[1]): r[2:] for r in agg.rows()}
     proj_rows = proj.rows()
     assert set(res) == set(want)
     for g, vals in res.items():
         members = [r for r in proj_rows if (r[0], r[1]) == g]
-        for a, (f, col) in enumerate(AGGS):
+        for a, (f, col) in enumerate(aggs):
             w = want[g][a]
             if f == "COUNT":
                 got = vals["rows"] if col < 0 else vals[a]
