@@ -133,8 +133,10 @@ __device__ __forceinline__ uint32_t match_mask(const hy_scan_chunk& ch, uint32_t
 // semantics, V the compared value type. OUT_ROWID: write reference RowIDs {chunk_id, offset} (8 B) instead of chunk
 // offsets (4 B).
 // SEG: tiles per workgroup (seg_tiles<E>; the host may pick fewer for 1-byte elements: more, shorter workgroups).
+// 1-byte ids with at most 4 tiles per workgroup run at 8 waves per SIMD (<= 64 VGPRs: 76 otherwise, 6 waves).
 template <typename E, int MODE, bool OUT_ROWID, typename V = E, int SEG = seg_tiles<E>()>
-__global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanLaunchDesc d, ScanConst<V> constant,
+__global__ __launch_bounds__(SCAN_THREADS) __attribute__((amdgpu_waves_per_eu(sizeof(E) == 1 && SEG <= 4 ? 8 : 1)))
+void scan_kernel(ScanLaunchDesc d, ScanConst<V> constant,
                                                            void* __restrict__ out_any,
                                                            uint32_t* __restrict__ counts) {
   __shared__ uint32_t s_stage[SCAN_TILE];
@@ -222,7 +224,10 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScanLaunchDesc d, Sc
     __syncthreads();
     if constexpr (OUT_ROWID) {
       hy_row_id* out = static_cast<hy_row_id*>(out_any) + run;
-      for (uint32_t i = threadIdx.x; i < tile_total; i += SCAN_THREADS) out[i] = hy_row_id{cid, s_stage[i]};
+      // streaming stores: the RowIDs are read by a later operator, not by this kernel (8 B {chunk_id, offset} each)
+      uint64_t* out64 = reinterpret_cast<uint64_t*>(out);
+      for (uint32_t i = threadIdx.x; i < tile_total; i += SCAN_THREADS)
+        __builtin_nontemporal_store(static_cast<uint64_t>(cid) | (static_cast<uint64_t>(s_stage[i]) << 32), out64 + i);
     } else {
       uint32_t* out = static_cast<uint32_t*>(out_any) + run;
       for (uint32_t i = threadIdx.x; i < tile_total; i += SCAN_THREADS) out[i] = s_stage[i];
