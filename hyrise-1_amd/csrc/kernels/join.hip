@@ -73,6 +73,12 @@ struct RowMap {
   uint64_t magic;             // floor(2^64 / uniform) + 1 (uniform >= 2)
 };
 
+// A join output RowID: a streaming store (the pairs are read by later operators, not by the join).
+__device__ __forceinline__ void put_row(hy_row_id* p, hy_row_id v) {
+  __builtin_nontemporal_store(static_cast<uint64_t>(v.chunk_id) | (static_cast<uint64_t>(v.chunk_offset) << 32),
+                              reinterpret_cast<uint64_t*>(p));
+}
+
 __device__ __forceinline__ hy_row_id map_row(const RowMap& m, uint32_t idx) {
   if (idx == NULL_PAYLOAD) return hy_row_id{0xFFFFFFFFu, 0xFFFFFFFFu};
   if (m.uniform == 1) return hy_row_id{idx, 0u};
@@ -1831,8 +1837,8 @@ __device__ __forceinline__ void write_duplicates(const JoinDesc& d, const Src& b
   for (uint32_t i = 0, m = 0; i < n && m < count; ++i) {
     const auto br = build[b0 + i];
     if (br.key == key) {
-      out_build[o] = map_row(d.build_map, br.payload);
-      out_probe[o] = prow;
+      put_row(out_build + (o), map_row(d.build_map, br.payload));
+      put_row(out_probe + (o), prow);
       ++o;
       ++m;
     }
@@ -1909,13 +1915,13 @@ __device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t 
         if (e == 0) continue;
         const hy_row_id prow = map_row(d.probe_map, ppay[k][v]);
         if (mode == HY_JOIN_SEMI || mode == HY_JOIN_ANTI) {
-          out_probe[o] = prow;
+          put_row(out_probe + (o), prow);
         } else if (c == 0) {  // outer: probe row without a match
-          out_build[o] = hy_row_id{0xFFFFFFFFu, 0xFFFFFFFFu};
-          out_probe[o] = prow;
+          put_row(out_build + (o), hy_row_id{0xFFFFFFFFu, 0xFFFFFFFFu});
+          put_row(out_probe + (o), prow);
         } else if (c == 1) {
-          out_build[o] = map_row(d.build_map, t.ents[info_index(pinfo[k][v])].payload);
-          out_probe[o] = prow;
+          put_row(out_build + (o), map_row(d.build_map, t.ents[info_index(pinfo[k][v])].payload));
+          put_row(out_probe + (o), prow);
         } else {
           write_duplicates<Src>(d, build, bb, nb, t.ents[info_index(pinfo[k][v])].key, c, prow, o, out_build,
                                 out_probe);
@@ -2034,10 +2040,10 @@ __device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t
       pos[k] = record_pos<JS, NT>(e, k, s_tot);
       if (e == 0) continue;
       if (mode == HY_JOIN_SEMI || mode == HY_JOIN_ANTI) {
-        out_probe[run + pos[k]] = map_row(d.probe_map, pr[k].payload);
+        put_row(out_probe + (run + pos[k]), map_row(d.probe_map, pr[k].payload));
       } else if (pcn[k] == 0) {
-        out_build[run + pos[k]] = hy_row_id{0xFFFFFFFFu, 0xFFFFFFFFu};
-        out_probe[run + pos[k]] = map_row(d.probe_map, pr[k].payload);
+        put_row(out_build + (run + pos[k]), hy_row_id{0xFFFFFFFFu, 0xFFFFFFFFu});
+        put_row(out_probe + (run + pos[k]), map_row(d.probe_map, pr[k].payload));
       }
     }
     __syncthreads();  // s_tot consumed; LDS table region free
@@ -2056,8 +2062,8 @@ __device__ __forceinline__ void partition_sub_tables(const JoinDesc& d, uint32_t
           const hy_row_id prow = map_row(d.probe_map, pr[k].payload);
           const uint64_t o = run + pos[k];
           if (cnt == 1) {
-            out_build[o] = map_row(d.build_map, t.ents[info_index(info)].payload);
-            out_probe[o] = prow;
+            put_row(out_build + (o), map_row(d.build_map, t.ents[info_index(info)].payload));
+            put_row(out_probe + (o), prow);
           } else {
             write_duplicates<Src>(d, build, b0, n, pr[k].key, cnt, prow, o, out_build, out_probe);
           }
