@@ -1126,8 +1126,9 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
       kt.done();
       HY_HIP(hipGetLastError());
     }
-    hipLaunchKernelGGL(hyk::agg_hash_compact, dim3(grid_for(plan.cap, 256)), dim3(256), 0, s, d, t, out, out_capacity,
-                       n_out);
+    const uint64_t rows_of_slots = (plan.cap + 256ull * hyk::HC_ITEMS - 1) / (256ull * hyk::HC_ITEMS);
+    hipLaunchKernelGGL(hyk::agg_hash_compact, dim3(static_cast<uint32_t>(std::min<uint64_t>(rows_of_slots, 4096))),
+                       dim3(256), 0, s, d, t, out, out_capacity, n_out);
     HY_HIP(hipGetLastError());
   }
   uint32_t misc[4] = {0, 0, 0, 0};

@@ -77,6 +77,17 @@ inline uint64_t bloom_words(uint64_t build_rows, uint64_t probe_rows) {
   return w;
 }
 
+// Words reserved for a key-range bitmap prefilter (hyk::range_bitmap_words) next to the Bloom filter's: 64 bits per
+// build row, enough for key ranges up to 64x the build rows (TPC-H 3's join 2: 14.6 M orders over the 600 M
+// orderkey range at SF100, 41 bits per row); a wider range keeps the Bloom filter.
+inline uint64_t range_bitmap_words(uint64_t build_rows) {
+  return std::min<uint64_t>(2 * build_rows + 1024, uint64_t(1) << 28);
+}
+// The prefilter area: a 64-byte header (hyk::FilterHdr), then the larger of the two filters' words.
+inline uint64_t prefilter_words(uint64_t bloom_n, uint64_t build_rows) {
+  return bloom_n ? 16 + std::max(bloom_n, range_bitmap_words(build_rows)) : 1;
+}
+
 inline uint32_t sub2() {
   static const uint32_t v = sub_from_env("HY_PART_SUB2", 1);
   return v;
@@ -546,7 +557,8 @@ template <typename SD, typename T, typename H, typename P>
 hy_status pass0_side(const SidePlan& p, SideBufs<H, P>& b, uint32_t bits, uint32_t w0,
                      uint32_t seed, bool keep_nulls, uint32_t ref_base, const hyk::NextDigit& nd, const Common& c,
                      hipStream_t s, hyk::Rec<H, P>* out, const uint32_t* bloom = nullptr, uint64_t bloom_n = 0,
-                     bool bloom_by_hash = false) {
+                     bool bloom_by_hash = false, const hyk::FilterHdr* bloom_hdr = nullptr,
+                     uint64_t range_words = 0) {
   hyk::Side sd{};
   sd.chunks = b.chunks;
   sd.n_chunks = static_cast<uint32_t>(p.chunks.size());
@@ -567,6 +579,8 @@ hy_status pass0_side(const SidePlan& p, SideBufs<H, P>& b, uint32_t bits, uint32
   sd.bloom = bloom;
   sd.bloom_mask = bloom ? static_cast<uint32_t>(bloom_n - 1) : 0u;
   sd.bloom_by_hash = bloom_by_hash ? 1 : 0;
+  sd.bloom_hdr = bloom ? bloom_hdr : nullptr;
+  sd.range_words = range_words;
   sd.seed = seed;
   const uint32_t n_digits = 1u << w0;
   hyk::Digit d0{full_mask(bits), bits - w0, n_digits - 1u, seed, g_key_hash};
@@ -866,7 +880,7 @@ size_t classic_join_bytes(const SidePlan& bp, const SidePlan& pp, uint32_t bits)
   Common c, cb;  // (join_typed: the probe side's and the build side's)
   carve_common(cv, std::max({ha, hb, (uint64_t(1) << bits) + 1}), bits, &c);
   carve_common(cv, std::max({ha, hb, (uint64_t(1) << bits) + 1}), bits, &cb);
-  cv.take<uint32_t>(std::max<uint64_t>(1, bloom_words(bp.n_rows, pp.n_rows)));
+  cv.take<uint32_t>(prefilter_words(bloom_words(bp.n_rows, pp.n_rows), bp.n_rows));
   return cv.used + 256;
 }
 
@@ -1259,7 +1273,9 @@ hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join
   carve_common(cv, std::max({ha, hb2, (uint64_t(1) << bits) + 1}), bits, &c);
   carve_common(cv, std::max({ha, hb2, (uint64_t(1) << bits) + 1}), bits, &cb);
   const uint64_t bloom_n = bloom_words(bp.n_rows, pp.n_rows);
-  uint32_t* bloom = cv.take<uint32_t>(std::max<uint64_t>(1, bloom_n));
+  uint32_t* filter_area = cv.take<uint32_t>(prefilter_words(bloom_n, bp.n_rows));
+  auto* filter_hdr = reinterpret_cast<hyk::FilterHdr*>(filter_area);
+  uint32_t* bloom = filter_area + 16;
   if (!cv.ok) return fail(HY_ERR_WORKSPACE, "join workspace too small");
   if (upload_side(bp, bb, s) || upload_side(pp, pb, s)) return HY_ERR_DEVICE;
   const bool keep_nulls = prm->mode == HY_JOIN_LEFT || prm->mode == HY_JOIN_RIGHT;
@@ -1282,6 +1298,8 @@ hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join
   // (hyk::HashSrc), 6-byte records for the partition join; a prefilter is then keyed by hash and set by that pass
   const bool soa = hash_records_enabled() && std::is_same_v<H, int32_t> && g_key_hash == nullptr && w.size() >= 2 &&
                    bits >= 16 && bp.n_rows >= 16 && pp.n_rows >= 16;  // (>= 16: room for HashSrc's group reads)
+  // a record join with integer keys: the prefilter is a key-range bitmap when the build keys' range fits
+  const bool range_filter = use_bloom && !soa && std::is_integral_v<H>;
   hyk::RecOut<H, uint32_t> soa_outs[2];
   if (soa) {
     if (use_bloom) HY_HIP(hipMemsetAsync(bloom, 0, 4 * bloom_n, s));
@@ -1306,7 +1324,8 @@ hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join
                                                      p.ref_base, nd, cs, st_s, b.recA)
                        : pass0_side<hyk::OnProbe, TP, H, uint32_t>(p, b, bits, w.empty() ? 0 : w[0], prm->seed, keep_nulls,
                                                      p.ref_base, nd, cs, st_s, b.recA, use_bloom ? bloom : nullptr,
-                                                     bloom_n, soa);
+                                                     bloom_n, soa, range_filter ? filter_hdr : nullptr,
+                                                     range_filter ? range_bitmap_words(bp.n_rows) : 0);
     if (st != HY_OK) return st;
     st = by_side(tag, [&](auto sdt) {
       return local_passes<decltype(sdt), H, uint32_t>(b, w, 1, bits, prm->seed, b.recA, b.recB, nd.bytes, b.digB,
@@ -1316,10 +1335,16 @@ hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join
     });
     if (st != HY_OK) return st;
     if (side == 0 && use_bloom && !soa) {  // the probe side's prefilter over the build side's keys (its records)
-      HY_HIP(hipMemsetAsync(bloom, 0, 4 * bloom_n, s));
-      KTimer kt_("bloom_build", s, p.n_rows);
-      hipLaunchKernelGGL(hyk::bloom_build<H>, dim3(static_cast<uint32_t>(std::min<uint64_t>(grid_for(p.n_rows, 256), 4096))),
-                         dim3(256), 0, s, recs[0], b.total, bloom, static_cast<uint32_t>(bloom_n - 1));
+      const uint64_t rw = range_filter ? range_bitmap_words(bp.n_rows) : 0;
+      HY_HIP(hipMemsetAsync(filter_hdr, 0, sizeof(hyk::FilterHdr), s));
+      KTimer kt_("prefilter_build", s, p.n_rows);
+      if (range_filter)
+        hipLaunchKernelGGL(hyk::filter_range<H>, dim3(static_cast<uint32_t>(std::min<uint64_t>(grid_for(p.n_rows, 256), 1024))),
+                           dim3(256), 0, s, recs[0], b.total, filter_hdr);
+      hipLaunchKernelGGL(hyk::filter_clear<H>, dim3(static_cast<uint32_t>(std::min<uint64_t>(grid_for(std::max(bloom_n, rw) / 4, 256), 4096))),
+                         dim3(256), 0, s, filter_hdr, bloom, rw, bloom_n);
+      hipLaunchKernelGGL(hyk::filter_set<H>, dim3(static_cast<uint32_t>(std::min<uint64_t>(grid_for(p.n_rows, 256), 4096))),
+                         dim3(256), 0, s, recs[0], b.total, filter_hdr, bloom, rw, static_cast<uint32_t>(bloom_n - 1));
       kt_.done();
       HY_HIP(hipGetLastError());
     }

@@ -142,14 +142,42 @@ struct Side {
   uint64_t filter_const;             // type_cast<T>(constant) bits for VALUE predicate chunks
   int32_t filter_type;               // HY_TYPE_* of VALUE predicate chunks
   uint32_t* scan_out;
-  // Probe-side prefilter of a selective INNER / SEMI join (null: none): a blocked Bloom filter over the build keys;
-  // a probe row whose key is certainly absent takes no part - it could produce no output, and dropping it keeps the
-  // stable order of the others (the reference's output is unchanged). The fused scan's output still lists it.
+  // Probe-side prefilter of a selective INNER / SEMI join (null: none) over the build keys: a probe row whose key is
+  // certainly absent takes no part - it could produce no output, and dropping it keeps the stable order of the others
+  // (the reference's output is unchanged). The fused scan's output still lists it. The filter words are either
+  //  - a key-range bitmap (bloom_hdr set and the build keys' range fits range_words words): one bit per key value in
+  //    [lo, hi], exact, and read almost in order when the probe keys are clustered (lineitem by l_orderkey), or
+  //  - a blocked Bloom filter of bloom_mask + 1 words (one 32-bit word per key, two bits).
   const uint32_t* bloom;
-  uint32_t bloom_mask;  // words - 1 (power of two)
+  uint32_t bloom_mask;  // Bloom words - 1 (power of two)
   int32_t bloom_by_hash;  // the filter is keyed by murmur2(key, seed) (bloom_slot_hash; SoA joins) instead of the key
   uint32_t seed;
+  const struct FilterHdr* bloom_hdr;  // integer keys of record joins: the build keys' range (filter_range), or null
+  uint64_t range_words;               // words reserved for a key-range bitmap
 };
+
+// The build keys' range, set by filter_range: lo_c = max of ~ord_key (so that a zeroed header is an empty range),
+// hi = max of ord_key.
+struct FilterHdr {
+  unsigned long long lo_c;
+  unsigned long long hi;
+};
+
+// Keys as unsigned 64-bit values in the keys' order.
+template <typename H>
+__device__ __forceinline__ uint64_t ord_key(H k) {
+  if constexpr (std::is_signed_v<H>) return static_cast<uint64_t>(static_cast<int64_t>(k)) ^ (1ull << 63);
+  else return static_cast<uint64_t>(k);
+}
+
+// Words of the key-range bitmap for the header's range, or 0 when it does not fit range_words (or the build side
+// is empty): then the filter is the Bloom filter.
+__device__ __forceinline__ uint64_t range_bitmap_words(const FilterHdr* h, uint64_t range_words, uint64_t* lo) {
+  const uint64_t l = ~h->lo_c, hi = h->hi;
+  *lo = l;
+  if (hi < l || ((hi - l) >> 5) >= range_words) return 0;
+  return ((hi - l) >> 5) + 1;
+}
 
 // Bloom filter words: one 32-bit word per key selected by a hash independent of the partition and bucket hashes,
 // two bits set in it.
@@ -176,6 +204,24 @@ __device__ __forceinline__ uint2 bloom_slot_hash(uint32_t h, uint32_t mask) {
 template <typename H>
 __device__ __forceinline__ uint32_t bloom_filter_act(const Side& s, const H (&keys)[PART_ITEMS], uint32_t act) {
   if (s.bloom == nullptr) return act;
+  if constexpr (std::is_integral_v<H>) {
+    uint64_t lo;
+    if (s.bloom_hdr != nullptr && range_bitmap_words(s.bloom_hdr, s.range_words, &lo) != 0) {  // (uniform)
+      const uint64_t span = s.bloom_hdr->hi - lo;
+      uint32_t words[PART_ITEMS];
+      uint32_t bits[PART_ITEMS];
+#pragma unroll
+      for (int k = 0; k < PART_ITEMS; ++k) {  // all loads in flight before any test
+        const uint64_t d = ord_key(keys[k]) - lo;
+        bits[k] = 1u << (d & 31u);
+        words[k] = (((act >> k) & 1u) && d <= span) ? s.bloom[d >> 5] : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < PART_ITEMS; ++k)
+        if ((words[k] & bits[k]) == 0u) act &= ~(1u << k);
+      return act;
+    }
+  }
   uint32_t words[PART_ITEMS];
   uint32_t bits[PART_ITEMS];
 #pragma unroll
@@ -191,14 +237,73 @@ __device__ __forceinline__ uint32_t bloom_filter_act(const Side& s, const H (&ke
   return act;
 }
 
+// The prefilter of a record join, from the build side's records, in three launches: the keys' range (one atomic
+// pair per workgroup into a zeroed header), the filter words zeroed (the bitmap's or the Bloom filter's), the keys'
+// bits set.
 template <typename H>
-static __global__ void bloom_build(const Rec<H, uint32_t>* __restrict__ recs, const uint64_t* __restrict__ n,
-                                   uint32_t* __restrict__ bloom, uint32_t mask) {
+static __global__ __launch_bounds__(256) void filter_range(const Rec<H, uint32_t>* __restrict__ recs,
+                                                           const uint64_t* __restrict__ n, FilterHdr* __restrict__ hdr) {
+  __shared__ unsigned long long s_red[2][256 / WAVE];
   const uint64_t total = *n;
+  unsigned long long lo_c = 0, hi = 0;
   for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < total;
        i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
-    const uint2 sl = bloom_slot<H>(recs[i].key, mask);
-    atomicOr(bloom + sl.x, sl.y);
+    const uint64_t u = ord_key(recs[i].key);
+    lo_c = max(lo_c, static_cast<unsigned long long>(~u));
+    hi = max(hi, static_cast<unsigned long long>(u));
+  }
+#pragma unroll
+  for (int dd = 32; dd >= 1; dd >>= 1) {
+    lo_c = max(lo_c, static_cast<unsigned long long>(__shfl_xor(lo_c, dd, WAVE)));
+    hi = max(hi, static_cast<unsigned long long>(__shfl_xor(hi, dd, WAVE)));
+  }
+  if (__lane_id() == 0) {
+    s_red[0][threadIdx.x / WAVE] = lo_c;
+    s_red[1][threadIdx.x / WAVE] = hi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 256 / WAVE; ++w) {
+      lo_c = max(lo_c, s_red[0][w]);
+      hi = max(hi, s_red[1][w]);
+    }
+    if (lo_c != 0) atomicMax(&hdr->lo_c, lo_c);  // (no keys: lo_c = hi = 0)
+    if (hi != 0) atomicMax(&hdr->hi, hi);
+  }
+}
+
+template <typename H>
+static __global__ void filter_clear(const FilterHdr* __restrict__ hdr, uint32_t* __restrict__ words,
+                                    uint64_t range_words, uint64_t bloom_words) {
+  uint64_t lo;
+  const uint64_t rw = std::is_integral_v<H> ? range_bitmap_words(hdr, range_words, &lo) : 0;
+  const uint64_t nw = rw ? rw : bloom_words;
+  uint4* w4 = reinterpret_cast<uint4*>(words);  // (16-byte aligned: the words follow a 64-byte header)
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < (nw + 3) / 4; i += stride)
+    w4[i] = make_uint4(0u, 0u, 0u, 0u);
+}
+
+template <typename H>
+static __global__ void filter_set(const Rec<H, uint32_t>* __restrict__ recs, const uint64_t* __restrict__ n,
+                                  const FilterHdr* __restrict__ hdr, uint32_t* __restrict__ words,
+                                  uint64_t range_words, uint32_t mask) {
+  const uint64_t total = *n;
+  uint64_t lo = 0;
+  bool range = false;
+  if constexpr (std::is_integral_v<H>) range = range_bitmap_words(hdr, range_words, &lo) != 0;
+  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const H key = recs[i].key;
+    if (range) {
+      if constexpr (std::is_integral_v<H>) {
+        const uint64_t d = ord_key(key) - lo;
+        atomicOr(words + (d >> 5), 1u << (d & 31u));
+      }
+    } else {
+      const uint2 sl = bloom_slot<H>(key, mask);
+      atomicOr(words + sl.x, sl.y);
+    }
   }
 }
 

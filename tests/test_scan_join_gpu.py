@@ -193,20 +193,30 @@ def test_multi_digit_plans(hy, oracle, monkeypatch, bits, mode, key_enc, filtere
 
 @pytest.mark.parametrize("mode", ["Inner", "Semi", "Left", "Anti"])
 @pytest.mark.parametrize("bloom", ["0", "1", None])
-def test_selective_join_bloom_prefilter(hy, oracle, monkeypatch, mode, bloom):
+@pytest.mark.parametrize("span", ["narrow", "wide"])
+def test_selective_join_bloom_prefilter(hy, oracle, monkeypatch, mode, bloom, span):
     """A small build side against a large probe side where ~90% of the probe keys have no partner (TPC-H 3's shape):
-    the default heuristic (probe >= 16x build) enables the probe-side Bloom prefilter for INNER / SEMI, which drops
-    probe rows before partitioning; the output PosLists equal the oracle's, with the prefilter forced on, off and by
-    the heuristic."""
+    the default heuristic (probe >= 16x build) enables the probe-side prefilter for INNER / SEMI, which drops probe
+    rows before partitioning; the output PosLists equal the oracle's, with the prefilter forced on, off and by the
+    heuristic. `narrow` build keys (negative ones included) span a range the key-range bitmap covers (64 bits per build
+    row reserved); `wide` ones span the int32 range, so the prefilter falls back to the Bloom filter."""
     if bloom is not None:
         monkeypatch.setenv("HY_JOIN_BLOOM", bloom)
     else:
         monkeypatch.delenv("HY_JOIN_BLOOM", raising=False)
     capi = hy.capi
-    rng = np.random.default_rng(zlib.crc32(f"bloom/{mode}/{bloom}".encode()))
-    okey = rng.choice(np.arange(1, 200_000, dtype=np.int32), 4_000, replace=False)
+    rng = np.random.default_rng(zlib.crc32(f"bloom/{mode}/{bloom}/{span}".encode()))
+    if span == "narrow":
+        okey = rng.choice(np.arange(-100_000, 100_000, dtype=np.int32), 4_000, replace=False)
+        lkey = rng.integers(-100_000, -60_000, 150_000).astype(np.int32)  # ~2% of them find a partner
+        lkey[:50] = [-100_001, 100_000, np.iinfo(np.int32).min, np.iinfo(np.int32).max, 0] * 10  # the range's edges and beyond
+    else:
+        okey = np.unique(rng.integers(np.iinfo(np.int32).min, np.iinfo(np.int32).max, 4_000, dtype=np.int64))
+        okey = rng.permutation(okey).astype(np.int32)
+        lkey = rng.integers(np.iinfo(np.int32).min, np.iinfo(np.int32).max, 150_000, dtype=np.int64).astype(np.int32)
+        hit = rng.random(150_000) < 0.1
+        lkey[hit] = rng.choice(okey, int(hit.sum()))
     okey = np.concatenate([okey, okey[:300]])  # duplicate build keys
-    lkey = rng.integers(1, 40_000, 150_000).astype(np.int32)  # ~10% of them find a partner
     lineitem = hy.Table.from_arrays([("l_orderkey", hy.DataType.Int, False)], [lkey], [], 20_000)
     orders = hy.Table.from_arrays([("o_orderkey", hy.DataType.Int, False)], [okey], [], 3_000)
     jm = getattr(hy.JoinMode, mode)
