@@ -830,7 +830,6 @@ struct AggWs {
   hy_column_chunk* chunks[hyk::AGG_MAX_COLUMNS];
   int32_t* word_op;
   uint32_t* misc;  // [0] error, [2..3] n_out (u64)
-  unsigned long long* inserted;  // hash path: hyk::INSERT_SHARDS insert counters
   hyk::FqOp* fused_nodes;        // agg_dense_fused: its expression ops
   hyk::LnTerm* lane_terms;       // agg_dense_lanes: its chains
   uint32_t* deferred;            // agg_dense_lanes: steps left to agg_dense_fused
@@ -867,7 +866,6 @@ void carve(Carver& cv, const hy_agg_input* in, const AggPlan& plan, AggWs* w) {
     w->mat_nulls[j] = plan.materialize ? cv.take<uint8_t>(std::max<uint64_t>(16, plan.rows)) : nullptr;
   }
   w->misc = cv.take<uint32_t>(64);
-  w->inserted = cv.take<unsigned long long>(hyk::INSERT_SHARDS);
   if (plan.dense_groups) {
     w->state = nullptr;
     w->records = cv.take<unsigned long long>(uint64_t(plan.dense_groups) * plan.d.words);
@@ -1111,11 +1109,8 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
                        plan.dense_groups, w.records, out, out_capacity, n_out);
     HY_HIP(hipGetLastError());
   } else {
-    hyk::AggTable t{w.state, w.records, plan.cap, w.dstate, w.dkeys, plan.dcap, w.inserted,
-                    // per counter: its share of the load limit, with slack for the uneven split of slots
-                    (plan.max_groups + hyk::INSERT_SHARDS - 1) / hyk::INSERT_SHARDS * 5 / 4 + 4};
+    hyk::AggTable t{w.state, w.records, plan.cap, w.dstate, w.dkeys, plan.dcap};
     HY_HIP(hipMemsetAsync(w.state, 0, 4 * plan.cap, s));
-    HY_HIP(hipMemsetAsync(w.inserted, 0, 8 * hyk::INSERT_SHARDS, s));
     if (plan.dcap) HY_HIP(hipMemsetAsync(w.dstate, 0, 4 * plan.dcap, s));
     if (plan.rows) {
       KTimer kt("agg_hash_runs", s, plan.rows);
@@ -1138,7 +1133,9 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
   std::memcpy(&n, misc + 2, 8);
   *n_groups = n;
   if (misc[0] & 2u) return fail(HY_ERR_INVALID_ARGUMENT, "dense group-by code outside its domain");
-  if (misc[0] & 4u) {  // more groups than the table was sized for: suggest a bound 4x larger
+  const bool hashed = !plan.dense_groups;  // (the hash table branch above)
+  if ((misc[0] & 4u) || (hashed && n > plan.max_groups)) {  // more groups than the table was sized for: suggest a
+                                                            // bound 4x larger
     *n_groups = std::min<uint64_t>(std::max<uint64_t>(plan.rows, 1), std::max<uint64_t>(64, plan.cap / 2) * 4);
     return fail(HY_ERR_GROUP_BOUND, "more groups than group_bound; retry with *n_groups");
   }
