@@ -209,13 +209,18 @@ def main_q3(args):
 
     orders_side = data_side(capi, ocust_c, I32)
     li_side = data_side(capi, lkey_c, I32)
-    o_off = torch.empty(n_ord + 64, dtype=torch.int32, device=dev)
+    # The orders / lineitem scans feed only their join: the fused operator returns their per-chunk match counts and
+    # not their PosLists (hy_join_filter.out_offsets NULL), so a join side's first pass writes records for the rows
+    # that pass the prefilter only. HY_Q3_SCAN_POSLISTS=1 materialises the scans' PosLists as well (A/B).
+    scan_poslists = os.environ.get("HY_Q3_SCAN_POSLISTS") == "1"
+    o_off = torch.empty(n_ord + 64, dtype=torch.int32, device=dev) if scan_poslists else None
     o_begin = torch.zeros(n_oc + 1, dtype=torch.int64, device=dev)
-    ofilter = capi.JoinFilter(odate.scan_chunks(capi, "LessThan", D), I32, None, o_off.data_ptr(), o_begin.data_ptr())
-    l_off = torch.empty(n_li + 64, dtype=torch.int32, device=dev)
+    ofilter = capi.JoinFilter(odate.scan_chunks(capi, "LessThan", D), I32, None,
+                              o_off.data_ptr() if scan_poslists else None, o_begin.data_ptr())
+    l_off = torch.empty(n_li + 64, dtype=torch.int32, device=dev) if scan_poslists else None
     l_begin = torch.zeros(n_lc + 1, dtype=torch.int64, device=dev)
-    lfilter = capi.JoinFilter(ship.scan_chunks(capi, "GreaterThan", D), I32, None, l_off.data_ptr(),
-                              l_begin.data_ptr())
+    lfilter = capi.JoinFilter(ship.scan_chunks(capi, "GreaterThan", D), I32, None,
+                              l_off.data_ptr() if scan_poslists else None, l_begin.data_ptr())
     jc_dtype = np.dtype(capi.JoinChunk)
     cc_dtype = np.dtype(capi.ColumnChunk)
     state = {"ws": {}, "cap": {}}
@@ -430,7 +435,7 @@ def main_q3(args):
         "vs_baseline": None, "dtype": "int32/f32", "data": "synthetic (seeded counter-based TPC-H-shaped columns, "
                                                            "resident in HBM)",
         "config": {"workload": "TPC-H 3 (tpch_queries.cpp:101-106) without ORDER BY/LIMIT", "sf": args.sf,
-                   "customer_rows": n_cust, "orders_rows": n_ord, "lineitem_rows": n_li, "chunk_size": chunk,
+                   "customer_rows": n_cust, "orders_rows": n_ord, "lineitem_rows": n_li, "chunk_size": chunk, "scan_poslists": scan_poslists,
                    **got, "parallelism": "single GPU"},
         "check": {"ok": bool(ok), "expected": exp, "sampled_groups": len(sample)},
         "roofline": roofline,

@@ -796,6 +796,9 @@ __global__ __launch_bounds__(PART_THREADS) __attribute__((amdgpu_waves_per_eu(4)
 //     is still a scan match; its record carries NULL_FLAG in the payload and no digit.
 //   part1_spread: reads each span's records back (coalesced), writes the scan's output (chunk offsets, in row order)
 //     and scatters the taking-part records by digit exactly as part1_scatter would (stable LDS-staged scatter).
+// Without a scan output (scan_out null: the caller wants the join output and the scan's counts only), part1_compact
+// writes the records of the rows taking part alone - after a selective prefilter a few percent of the scan's matches
+// (TPC-H 3's lineitem side: 6 of 323 M) - and the scan row of the histogram still counts every match.
 // Traffic per matched row is one 8-byte record more than the single fused scatter, but both kernels are plain
 // streams, while the single kernel's load -> rank -> stage -> store chain per tile left it latency-bound.
 // ------------------------------------------------------------------------------------------------------------
@@ -806,7 +809,7 @@ __global__ __launch_bounds__(PART_THREADS) void part1_compact(Side s, Digit dg, 
                                                              uint32_t* __restrict__ hist, uint32_t* __restrict__ span_count,
                                                              Rec<H, uint32_t>* __restrict__ gap_out) {
   __shared__ uint32_t s_hist[257];
-  __shared__ uint32_t s_sc[WAVE + 1];
+  __shared__ uint32_t s_sc[WAVE + 2];
   const uint64_t tile = xcd_tile(blockIdx.x, gridDim.x);  // span
   for (int i = threadIdx.x; i < 257; i += PART_THREADS) s_hist[i] = 0;
   const uint32_t c = s.tile_chunk[tile];
@@ -815,19 +818,28 @@ __global__ __launch_bounds__(PART_THREADS) void part1_compact(Side s, Digit dg, 
   const uint32_t n_sub = min(s.sub, (ch.size - base + PART_TILE - 1) / PART_TILE);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE), lane = __lane_id();
   Rec<H, uint32_t>* out = gap_out + tile * (static_cast<uint64_t>(s.sub) * PART_TILE);
+  const bool scan_records = s.scan_out != nullptr;  // records of every scan match, or of the rows taking part only
   uint32_t run = 0;
+  if (threadIdx.x == 0) s_sc[WAVE + 1] = 0;  // scan matches of the span (without scan records)
   __syncthreads();
 #pragma unroll 1
   for (uint32_t j = 0; j < n_sub; ++j) {
     const uint32_t rb = base + j * PART_TILE + w * WAVE_SPAN;
-    const uint32_t m = filter_items<FK>(s, c, rb);
+    const uint32_t m_scan = filter_items<FK>(s, c, rb);
     H keys[PART_ITEMS];
     uint32_t pays[PART_ITEMS];
-    const uint32_t act = bloom_filter_act<H>(s, keys, load_items<T, H, uint32_t, LP>(s, ch, rb, keys, pays) & m);
+    const uint32_t act = bloom_filter_act<H>(s, keys, load_items<T, H, uint32_t, LP>(s, ch, rb, keys, pays) & m_scan);
+    const uint32_t m = scan_records ? m_scan : act;  // the rows written as records
 #pragma unroll
     for (int k = 0; k < PART_ITEMS; ++k)
       if ((act >> k) & 1u) atomicAdd(&s_hist[digit_of<H>(dg, keys[k])], 1u);
-    // row-order compaction of the matches: (wave, item) ballot counts -> prefix -> lane rank
+    if (!scan_records) {
+      uint32_t nm = 0;
+#pragma unroll
+      for (int k = 0; k < PART_ITEMS; ++k) nm += static_cast<uint32_t>(__popcll(__ballot((m_scan >> k) & 1u)));
+      if (lane == 0 && nm) atomicAdd(&s_sc[WAVE + 1], nm);
+    }
+    // row-order compaction of the records: (wave, item) ballot counts -> prefix -> lane rank
 #pragma unroll
     for (int k = 0; k < PART_ITEMS; ++k) {
       const uint64_t b = __ballot((m >> k) & 1u);
@@ -856,7 +868,7 @@ __global__ __launch_bounds__(PART_THREADS) void part1_compact(Side s, Digit dg, 
   }
   for (uint32_t d = threadIdx.x; d < n_digits; d += PART_THREADS) hist[d * s.n_tiles + tile] = s_hist[d];
   if (threadIdx.x == 0) {
-    hist[n_digits * s.n_tiles + tile] = run;
+    hist[n_digits * s.n_tiles + tile] = scan_records ? run : s_sc[WAVE + 1];
     span_count[tile] = run;
   }
 }

@@ -50,14 +50,14 @@ def run_fused(hy, build, bfilt, probe, pfilt, params, cap):
 class Filter:
     """hy_join_filter for `column cond value` on a DeviceColumn, with its output buffers."""
 
-    def __init__(self, capi, col, cond, value):
+    def __init__(self, capi, col, cond, value, offsets=True):
         self.chunks = col.scan_chunks(cond, value)
         self.const = col.constant(value)
         n = max(16, col.values.size)
         self.out = capi.DeviceArray(np.zeros(n, np.uint32))
         self.begin = capi.DeviceArray(np.zeros(col.n_chunks + 1, np.uint64))
-        self.f = capi.JoinFilter(self.chunks, dt.HY_TYPES[col.values.dtype], self.const.ctypes.data, self.out.ptr.value,
-                                 self.begin.ptr.value)
+        self.f = capi.JoinFilter(self.chunks, dt.HY_TYPES[col.values.dtype], self.const.ctypes.data,
+                                 self.out.ptr.value if offsets else None, self.begin.ptr.value)
 
     def scan_output(self):
         off, beg = self.out.fetch(), self.begin.fetch().astype(np.int64)
@@ -129,6 +129,50 @@ def test_scan_join_matches_operators(hy, oracle, monkeypatch, mode, qty_enc, key
     if of is not None:
         check_scan(left, of)
     check_join(expected, parts, 2, swapped, mode in ("Semi", "Anti"))
+
+
+@pytest.mark.parametrize("mode", ["Inner", "Left", "Semi"])
+@pytest.mark.parametrize("bloom", ["0", "1"])
+@pytest.mark.parametrize("build_filter", [False, True])
+def test_scan_join_counts_only(hy, oracle, monkeypatch, mode, bloom, build_filter):
+    """out_offsets NULL with out_chunk_begin set: the join output and the scans' per-chunk match counts only (no scan
+    PosLists). part1_compact then writes records for the rows taking part alone (after the prefilter), while the
+    scan's counts still include the matches the prefilter drops."""
+    monkeypatch.setenv("HY_JOIN_BLOOM", bloom)
+    capi = hy.capi
+    rng = np.random.default_rng(zlib.crc32(repr(("counts_only", mode, bloom, build_filter)).encode()))
+    okey, ostatus, lkey, lkey_nulls, qty, qty_nulls = orders_lineitem(rng, 40_000, True)
+    lchunk, ochunk = 9_000, 7_000
+    lineitem = hy.Table.from_arrays([("l_orderkey", hy.DataType.Int, True), ("l_quantity", hy.DataType.Float, True)],
+                                    [lkey, qty], [lkey_nulls, qty_nulls], lchunk)
+    orders = hy.Table.from_arrays([("o_orderkey", hy.DataType.Int, False), ("o_status", hy.DataType.Int, False)],
+                                  [okey, ostatus], [], ochunk)
+    scan_l = oracle.table_scan(lineitem, 1, hy.PredicateCondition.LessThan, 24.0, [])
+    left = oracle.table_scan(orders, 1, hy.PredicateCondition.GreaterThanEquals, 3, []) if build_filter else orders
+    expected, bits = oracle.join_hash(left, scan_l, getattr(hy.JoinMode, mode), (0, 0))
+    lk = dt.DeviceColumn(capi, lkey, lkey_nulls, lchunk, "Unencoded")
+    lq = dt.DeviceColumn(capi, qty, qty_nulls, lchunk, "Dictionary")
+    ok = dt.DeviceColumn(capi, okey, None, ochunk, "Unencoded")
+    os_ = dt.DeviceColumn(capi, ostatus, None, ochunk, "Dictionary")
+    lf = Filter(capi, lq, "LessThan", 24.0, offsets=False)
+    of = Filter(capi, os_, "GreaterThanEquals", 3, offsets=False) if build_filter else None
+    swapped = mode in ("Left", "Semi") or left.row_count() > scan_l.row_count()
+    o_side, l_side = dt.join_side(capi, ok), dt.join_side(capi, lk)
+    params = capi.JoinParams({"Inner": 0, "Left": 1, "Semi": 5}[mode], capi.HY_TYPE_INT32, bits, 17)
+    cap = okey.size * 3 + lkey.size + 16
+    o_f = of.f if of else None
+    if swapped:
+        parts = run_fused(hy, l_side, lf.f, o_side, o_f, params, cap)
+    else:
+        parts = run_fused(hy, o_side, o_f, l_side, lf.f, params, cap)
+    check_join(expected, parts, 2, swapped, mode == "Semi")
+    for table, filt, chunk in [(scan_l, lf, lchunk)] + ([(left, of, ochunk)] if of else []):
+        counts = np.diff(filt.begin.fetch().astype(np.int64))
+        want = np.zeros(counts.size, np.int64)
+        for k in range(table.chunk_count()):
+            pl = table.get_chunk(k).get_column(0).pos_list()
+            want[pl[0, 0]] = pl.shape[0]
+        assert np.array_equal(counts, want)
 
 
 def test_scan_join_empty_and_all_none(hy, oracle):
