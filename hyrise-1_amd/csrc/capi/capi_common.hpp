@@ -59,10 +59,22 @@ struct PinnedRing {
     if (buf) (void)hipHostFree(buf);
   }
   hy_status wait_all() {
-    for (auto& f : fences) HY_HIP(hipEventSynchronize(f.event));
+    for (auto& f : fences) {
+      if (hipEventSynchronize(f.event) == hipSuccess) continue;
+      // an event last recorded while its stream was being captured into a graph cannot be waited for (HIP refuses
+      // it): wait for the device instead - every copy out of the ring is then complete - and start new fences
+      (void)hipGetLastError();
+      HY_HIP(hipDeviceSynchronize());
+      for (auto& g : fences) (void)hipEventDestroy(g.event);
+      fences.clear();
+      return HY_OK;
+    }
     return HY_OK;
   }
   hy_status fence(hipStream_t s) {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    HY_HIP(hipStreamIsCapturing(s, &cap));
+    if (cap != hipStreamCaptureStatusNone) return HY_OK;  // (a copy captured into a graph: no event to wait for)
     int dev = 0;
     HY_HIP(hipGetDevice(&dev));
     for (auto& f : fences)
