@@ -73,7 +73,10 @@ struct PinnedRing {
   }
   hy_status fence(hipStream_t s) {
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    HY_HIP(hipStreamIsCapturing(s, &cap));
+    if (hipStreamIsCapturing(s, &cap) != hipSuccess) {  // (a query HIP refuses: treated as not capturing)
+      (void)hipGetLastError();
+      cap = hipStreamCaptureStatusNone;
+    }
     if (cap != hipStreamCaptureStatusNone) return HY_OK;  // (a copy captured into a graph: no event to wait for)
     int dev = 0;
     HY_HIP(hipGetDevice(&dev));
