@@ -491,8 +491,16 @@ hy_status launch_filtered_pass0(const SidePlan& p, const hyk::Side& sd, const hy
   }
   {
     KTimer kt_((std::string("part1_compact.") + SD::name).c_str(), s, p.n_rows);
-    hipLaunchKernelGGL((hyk::part1_compact<SD, T, H, LP, FK>), grid, dim3(hyk::PART_THREADS), 0, s, sd, d0, n_digits,
-                       b.hist, b.span_count, b.recB);
+    bool prefiltered = false;
+    if constexpr (std::is_same_v<SD, hyk::OnProbe>) prefiltered = sd.bloom != nullptr;  // (build sides have none)
+    if (prefiltered) {
+      if constexpr (std::is_same_v<SD, hyk::OnProbe>)
+        hipLaunchKernelGGL((hyk::part1_compact<SD, T, H, LP, FK, true>), grid, dim3(hyk::PART_THREADS), 0, s, sd, d0,
+                           n_digits, b.hist, b.span_count, b.recB);
+    } else {
+      hipLaunchKernelGGL((hyk::part1_compact<SD, T, H, LP, FK, false>), grid, dim3(hyk::PART_THREADS), 0, s, sd, d0,
+                         n_digits, b.hist, b.span_count, b.recB);
+    }
     kt_.done();
   }
   HY_HIP(hipGetLastError());

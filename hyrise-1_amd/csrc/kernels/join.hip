@@ -804,7 +804,9 @@ __global__ __launch_bounds__(PART_THREADS) __attribute__((amdgpu_waves_per_eu(4)
 // ------------------------------------------------------------------------------------------------------------
 constexpr uint32_t NULL_FLAG = 0x80000000u;  // payloads of filtered sides are row indexes < 2^31
 
-template <typename SD, typename T, typename H, int LP, int FK>
+// PF: the side has a probe-side prefilter (s.bloom). A separate instance: the prefilter's lookups hold registers
+// (151 VGPRs, 3 waves per SIMD, against 96 without them) that the headline's unprefiltered probe side does not need.
+template <typename SD, typename T, typename H, int LP, int FK, bool PF>
 __global__ __launch_bounds__(PART_THREADS) void part1_compact(Side s, Digit dg, uint32_t n_digits,
                                                              uint32_t* __restrict__ hist, uint32_t* __restrict__ span_count,
                                                              Rec<H, uint32_t>* __restrict__ gap_out) {
@@ -828,7 +830,8 @@ __global__ __launch_bounds__(PART_THREADS) void part1_compact(Side s, Digit dg, 
     const uint32_t m_scan = filter_items<FK>(s, c, rb);
     H keys[PART_ITEMS];
     uint32_t pays[PART_ITEMS];
-    const uint32_t act = bloom_filter_act<H>(s, keys, load_items<T, H, uint32_t, LP>(s, ch, rb, keys, pays) & m_scan);
+    uint32_t act = load_items<T, H, uint32_t, LP>(s, ch, rb, keys, pays) & m_scan;
+    if constexpr (PF) act = bloom_filter_act<H>(s, keys, act);
     const uint32_t m = scan_records ? m_scan : act;  // the rows written as records
 #pragma unroll
     for (int k = 0; k < PART_ITEMS; ++k)
