@@ -1192,6 +1192,7 @@ __global__ __launch_bounds__(256) void agg_hash_compact(AggDesc d, AggTable t, u
                                                         uint64_t capacity, unsigned long long* __restrict__ n_out) {
   __shared__ uint32_t s_scan[256 / WAVE + 1];
   __shared__ unsigned long long s_base;
+  __shared__ uint16_t s_src[256 * HC_ITEMS];  // the row's occupied slots (offsets in the row), in output order
   constexpr uint64_t PER = 256ull * HC_ITEMS;
   for (uint64_t b0 = blockIdx.x * PER; b0 < t.cap; b0 += static_cast<uint64_t>(gridDim.x) * PER) {
     uint32_t occ = 0;  // bit i: slot b0 + i * 256 + threadIdx.x holds a group
@@ -1204,18 +1205,23 @@ __global__ __launch_bounds__(256) void agg_hash_compact(AggDesc d, AggTable t, u
     const uint32_t pos = block_exclusive_sum<256>(static_cast<uint32_t>(__popc(occ)), s_scan, &total);
     if (threadIdx.x == 0) s_base = total ? atomicAdd(n_out, static_cast<unsigned long long>(total)) : 0ull;
     __syncthreads();
-    uint64_t idx = s_base + pos;
+    // the row's records copied word by word by the whole workgroup: consecutive lanes read and write consecutive
+    // words (one lane copying a whole record wrote 8-byte pieces 19 words apart: ~5x the output bytes in partial
+    // line writes at TPC-H 3)
+    uint32_t r = pos;
     while (occ) {
       const int i = __builtin_ctz(occ);
       occ &= occ - 1;
-      if (idx < capacity) {
-        const unsigned long long* rec = t.records + (b0 + static_cast<uint64_t>(i) * 256 + threadIdx.x) * d.words;
-        unsigned long long* o = out + idx * d.words;
-        for (uint32_t w = 0; w < d.words; ++w) o[w] = rec[w];
-      }
-      ++idx;
+      s_src[r++] = static_cast<uint16_t>(i * 256 + threadIdx.x);
     }
-    __syncthreads();  // s_base read by every thread before the next row's
+    __syncthreads();
+    const uint64_t base = s_base;
+    const uint32_t W = d.words;
+    for (uint32_t e = threadIdx.x; e < total * W; e += 256) {
+      const uint32_t rr = e / W, w = e - rr * W;
+      if (base + rr < capacity) out[(base + rr) * W + w] = t.records[(b0 + s_src[rr]) * W + w];
+    }
+    __syncthreads();  // s_base and s_src read by every thread before the next row's
   }
 }
 
