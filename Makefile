@@ -14,7 +14,7 @@ CXXFLAGS  := -std=c++17 -O2 -fPIC -Wall -Wno-unused-function -Iinclude -I$(CSRC)
 HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Iinclude
 
 HOST_SRC  := $(CSRC)/host/storage.cpp $(CSRC)/host/device.cpp $(CSRC)/host/operators.cpp $(CSRC)/host/aggregate.cpp \
-             $(CSRC)/host/projection.cpp $(CSRC)/host/binary_io.cpp
+             $(CSRC)/host/projection.cpp $(CSRC)/host/binary_io.cpp $(CSRC)/host/scheduler.cpp
 HOST_HDR  := $(wildcard $(CSRC)/host/*.hpp) include/hyrise_amd.h
 
 all: $(LIB)/libhyrise_amd.so $(LIB)/libhyrise_host.so $(LIB)/_hyrise_host$(EXTSUF) $(LIB)/exchange_check

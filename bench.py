@@ -42,9 +42,10 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (RCCL; one GPU per rank) or gloo (host-staged exchange: rehearsal of N ranks on one GPU)")
-    p.add_argument("--transport", choices=["capi", "torch"], default="torch",
-                   help="N>1 over RCCL: torch's all_to_all (default: torch bundles its own RCCL / HIP runtime) or the "
-                        "library's own communicator (hy_join_exchange_counts/records, the C++ integration's path)")
+    p.add_argument("--transport", choices=["capi", "torch"], default="capi",
+                   help="N>1 over RCCL: the library's own communicator (default: hy_join_exchange_counts/records, the "
+                        "C++ integration's path; in a torch process it binds torch's RCCL under the same soname) or "
+                        "torch's all_to_all_single")
     p.add_argument("--workload", choices=["join", "q1", "q3", "scan", "join-only"], default="join",
                    help="join: the headline TableScan+JoinHash (BASELINE.json metric); q1: BASELINE config 4, "
                         "TPC-H 1 TableScan -> Projection -> Aggregate (8 aggregates) on one GPU; q3: BASELINE config 5 at N=1, "
@@ -353,6 +354,18 @@ def main():
         np.savez(args.join_trace, stamps_us=t, out_pairs=part_count.cpu().numpy())
     g_li, g_ord, g_probe, g_pairs = n_li, n_ord, n_probe, int(pairs)
     check = None
+    if mode == "scan":  # config 2: every chunk's count and every RowID of the timed step's output
+        thr = [256 if scan_chunks[c].op == capi.HY_OP_ALL else (0 if scan_chunks[c].op == capi.HY_OP_NONE
+               else scan_chunks[c].search_vid) for c in range(n_lchunks)]
+        check = verify_scan(torch, chunk, vids, n_li, thr, scan_rows, scan_counts)
+        if check["status"] != "ok":
+            raise SystemExit(f"scan output check failed: {check}")
+    if mode == "join-only":  # config 3: the headline's join properties with every lineitem row as a probe row
+        check = verify_headline(torch, L, stream, chunk, okey, lkey, vids, n_li, [256] * n_lchunks,
+                                (state["jout_b"], state["jout_p"], None, None), part_begin, part_count, radix_bits,
+                                g_pairs)
+        if check["status"] != "ok":
+            raise SystemExit(f"join-only output check failed: {check}")
     if mode == "join":  # pin the timed output at its full size (every pair, partition and scan offset)
         thr = []
         for c in range(n_lchunks):
@@ -480,8 +493,9 @@ def main():
                        "peak_source": "MI355X_MICROARCH.md HBM3E spec; peak_measured: this run's stream probe"}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and mode == "join":
-        cpu = cpu_baseline(hy, synth, args.cpu_sf, chunk)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # (config 3's sample is half the scale factor: its join takes every lineitem row, ~2x the headline's)
+        cpu = cpu_baseline(hy, synth, args.cpu_sf / (2 if mode == "join-only" else 1), chunk, mode=mode)
 
     if rank == 0:
         line = {
@@ -528,6 +542,28 @@ def main():
                               "parallelism": "single GPU"}
             line["roofline_e2e"]["scope"] = "JoinHash step (SURVEY 8(d): 4 B/build row + 4 B/probe row + 16 B/pair)"
         print(json.dumps(line))
+
+
+def verify_scan(torch, chunk, vids, n_li, thr, scan_rows, scan_counts):
+    """Config 2's TableScan output at its full size: per chunk the match count, and every RowID {chunk, offset} of the
+    matches (vid < search value id of their chunk, single_column_table_scan_impl.cpp:145-205) in row order, chunk c's
+    written from c * chunk on (its out_begin)."""
+    dev = vids.device
+    n_chunks = len(thr)
+    sizes = torch.tensor([min(chunk, n_li - c * chunk) for c in range(n_chunks)], dtype=torch.int64, device=dev)
+    t = torch.repeat_interleave(torch.tensor(thr, dtype=torch.int32, device=dev), sizes)
+    match = torch.nonzero(vids[:n_li].to(torch.int32) < t).flatten()
+    del t
+    c = match // chunk
+    first = torch.searchsorted(match, torch.arange(0, n_li, chunk, device=dev))
+    counts = torch.diff(torch.cat([first, torch.tensor([match.numel()], device=dev)]))
+    res = {"chunk_counts": bool(torch.equal(scan_counts[:n_chunks].to(torch.int64), counts))}
+    pos = c * chunk + (torch.arange(match.numel(), device=dev) - first[c])
+    rows = scan_rows.view(-1, 2)[pos].to(torch.int64)
+    res["row_ids"] = bool(torch.equal(rows[:, 0], c) and torch.equal(rows[:, 1], match % chunk))
+    res["status"] = "ok" if all(res.values()) else "MISMATCH"
+    res["matches_checked"] = int(match.numel())
+    return res
 
 
 def verify_headline(torch, L, stream, chunk, okey, lkey, vids, n_li, thr, outs, part_begin, part_count, bits, pairs):
@@ -682,11 +718,12 @@ def host_cpu():
     return max(1, n), model
 
 
-def cpu_baseline(hy, synth, sf, chunk, runs=5):
+def cpu_baseline(hy, synth, sf, chunk, runs=5, mode="join"):
     """The oracle (CPU restatement of the reference operators with the reference's per-chunk / per-partition jobs)
     on a bounded sample of the same workload: TableScan(l_quantity < 24) on dictionary-encoded lineitem, then
-    JoinHash(orders, scan output). Median of `runs` warm runs on all host cores of this process, and on 1 core at a
-    fifth of the sample."""
+    JoinHash(orders, scan output) - or, for config 2 (mode "scan"), the TableScan alone, and for config 3 ("join-only")
+    JoinHash(orders, lineitem) over every lineitem row. Median of `runs` warm runs on all host cores of this process,
+    and on 1 core at a fifth of the sample."""
     import numpy as np
 
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -707,18 +744,25 @@ def cpu_baseline(hy, synth, sf, chunk, runs=5):
         hy.encode_all_chunks(lineitem, hy.EncodingType.Dictionary)
         oracle.set_threads(n_threads)
         times = []
+        scan = join = None
         for _ in range(runs + 1):  # the first run warms caches and allocators
             t0 = time.perf_counter()
-            scan = oracle.table_scan(lineitem, 1, hy.PredicateCondition.LessThan, 24, [])
-            join, _bits = oracle.join_hash(orders, scan, hy.JoinMode.Inner, (0, 0))
+            if mode != "join-only":
+                scan = oracle.table_scan(lineitem, 1, hy.PredicateCondition.LessThan, 24, [])
+            if mode != "scan":
+                join, _bits = oracle.join_hash(orders, lineitem if mode == "join-only" else scan, hy.JoinMode.Inner,
+                                               (0, 0))
             times.append(time.perf_counter() - t0)
         oracle.set_threads(1)
         med = sorted(times[1:])[len(times[1:]) // 2]
-        rows = lineitem.row_count() + orders.row_count()
+        rows = lineitem.row_count() + (0 if mode == "scan" else orders.row_count())
+        what = {"join": f"scan {scan.row_count() if scan else 0} matches, join {join.row_count() if join else 0} pairs",
+                "scan": f"scan {scan.row_count() if scan else 0} matches",
+                "join-only": f"join {join.row_count() if join else 0} pairs"}[mode]
         out[label] = {"value": round(rows / med, 1), "cores": n_threads, "median_s": round(med, 3),
                       "runs_s": [round(t, 3) for t in times[1:]],
                       "sample": f"SF{sample_sf:g}: {lineitem.row_count()} lineitem + {orders.row_count()} orders "
-                                f"rows, scan {scan.row_count()} matches, join {join.row_count()} pairs"}
+                                f"rows, {what}"}
         del orders, lineitem, scan, join
     out["value"], out["cores"] = out["all_cores"]["value"], out["all_cores"]["cores"]
     out["sample"] = out["all_cores"]["sample"] + f"; median of {runs}"

@@ -8,13 +8,17 @@ and lineitem (hyrise-1_amd/synth.shard_torch: the union of the shards is exactly
     build   hy_scan_join_exchange_partition(orders shard)                    8-byte records {o_orderkey, global row}
     probe   hy_scan_join_exchange_partition(lineitem shard, l_quantity < 24)  the scan runs in the same pass and writes
                                                                              the shard's scan output (chunk offsets)
-    exchange  per side: all_gather of the first-digit bucket counts, one all_to_all_single of the records (RCCL over
-              xGMI with --dist-backend nccl; host-staged gloo rehearsal otherwise)
+    exchange  per side: the first-digit bucket counts to every rank, then one all-to-all of the records - by default
+              through the library's own RCCL communicator (hy_join_exchange_counts / hy_join_exchange_records, the
+              C++ integration's path; --transport torch: torch's all_to_all_single), over xGMI with --dist-backend
+              nccl; host-staged gloo rehearsal otherwise
     join    hy_join_exchange_join_rows: remaining radix passes + LDS build/probe of this rank's partitions; output
             RowIDs name global chunks (the ranks' outputs in rank order = the single-GPU output)
 
 The radix bits come from the GLOBAL build size (join_hash.cpp:640-668), so partitions are the single-GPU ones. Timing:
 barrier + synchronize around K steps, the max over ranks; value = all ranks' base rows (orders + lineitem) / time.
+Check: every rank's output partitions against the single-GPU layout computed from the shards (pairs, probe and build
+row sums per partition, probe rows ascending inside each; dist.headline_expected / check_partition_output).
 """
 import ctypes
 import importlib
@@ -60,6 +64,9 @@ def main_distributed(args):
     n_ord_g, n_li_g = sum(sh["o_layout"]), sum(sh["l_layout"])
     okey, lkey, qty = sh["o_orderkey"], sh["l_orderkey"], sh["l_quantity"]
     n_ord, n_li = okey.numel(), lkey.numel()
+    radix_bits = L.hy_join_radix_bits(n_ord_g, 4)  # global build size (join_hash.cpp:640-668)
+    # the single-GPU layout's per-partition pairs / row sums over the whole database (the output check below)
+    expected = hdist.headline_expected(dist, lkey, qty < 24, sh["l_row_base"], radix_bits)
     vids, present = synth.dictionary_encode_small_domain(qty, chunk, 50)
     del qty
     present_h = present.cpu().numpy()
@@ -106,7 +113,6 @@ def main_distributed(args):
     scan_begin = torch.zeros(n_lc + 1, dtype=torch.int64, device=dev)
     pfilter = capi.JoinFilter(scan_chunks, capi.HY_TYPE_FLOAT, None, scan_off.data_ptr(), scan_begin.data_ptr())
 
-    radix_bits = L.hy_join_radix_bits(n_ord_g, 4)  # global build size (join_hash.cpp:640-668)
     xj = hdist.ExchangeJoin(capi, radix_bits, world, capi.HY_TYPE_INT32, capi.HY_JOIN_INNER, 17, rows=True,
                             build_layout=sh["o_layout"], probe_layout=sh["l_layout"])
     rb = xj.record_bytes
@@ -135,6 +141,7 @@ def main_distributed(args):
         out = xj.join(brecv, bmat, precv, pmat, rank, stream, dev)
         state["recv_rows"] = (int(bmat.sum()), int(pmat.sum()))
         state["sent_bytes"] = (int(bcnt.sum()) + int(pcnt.sum())) * rb
+        state["out"] = out
         return int(pcnt.sum()), out[4]
 
     for _ in range(args.warmup):
@@ -155,6 +162,16 @@ def main_distributed(args):
         step()
     torch.cuda.synchronize()
     L.hy_kernel_stats_enable(0)
+    # per-rank output check of the last step against the single-GPU layout (dist.check_partition_output)
+    out_b, out_p, pbeg, pcnt = state["out"][:4]
+    first_bucket, _ = hdist.owned_buckets(xj.n_buckets, rank, world)
+    check = hdist.check_partition_output(expected, out_b, out_p, pbeg, pcnt,
+                                         first_bucket << (radix_bits - xj.first_bits), chunk)
+    bad = torch.tensor([0 if all(check.values()) else 1], dtype=torch.int64, device=xdev)
+    dist.all_reduce(bad)
+    check["ranks_failing"] = int(bad.item())
+    check["status"] = "ok" if check["ranks_failing"] == 0 else "mismatch"
+    check["pairs_checked"] = None  # set below from the whole job's pairs
     t = torch.tensor([elapsed], dtype=torch.float64, device=xdev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
@@ -162,6 +179,8 @@ def main_distributed(args):
     dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     g_probe, g_pairs, g_sent = (int(x) for x in tot.tolist())
     assert int(scan_begin[n_lc].item()) == n_probe  # the fused scan's output = the probe records
+    check["pairs_checked"] = g_pairs
+    check["expected_pairs"] = int(expected[0].sum())
 
     from bench import kernel_stats, HBM_PEAK_GBPS  # noqa: E402  (shared helpers)
 
@@ -204,6 +223,7 @@ def main_distributed(args):
             "kernels_rank0": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                               for k, v in kernels.items()},
             "cpu_baseline": None,
+            "check": check,
         }
         print(json.dumps(line))
     if rx is not None:

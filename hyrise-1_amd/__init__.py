@@ -85,5 +85,7 @@ op_trace_take = _host.op_trace_take
 pool_stats = _host.pool_stats
 device_memory = _host.device_memory
 host_cpu_share = _host.host_cpu_share
+set_job_scheduler = _host.set_job_scheduler
+DescriptionMode = _host.DescriptionMode
 
 from . import capi  # noqa: E402  (ctypes view of the C-ABI)

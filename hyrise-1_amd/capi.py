@@ -160,6 +160,8 @@ _sigs = {
                                      ctypes.c_void_p]),
     "hy_agg_float_sum": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32, ctypes.c_int32,
                                         ctypes.c_uint64, ctypes.POINTER(ctypes.c_double)]),
+    "hy_agg_float_sums": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                         ctypes.c_uint32, ctypes.c_int32, ctypes.c_void_p]),
     "hy_agg_decode_ordered": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_int32]),
     "hy_join_exchange_bucket_bits": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32]),
     "hy_join_exchange_partition_workspace_size": (ctypes.c_int, [ctypes.POINTER(JoinSide), ctypes.POINTER(JoinParams),

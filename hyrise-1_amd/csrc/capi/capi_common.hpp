@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cassert>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -59,25 +60,10 @@ struct PinnedRing {
     if (buf) (void)hipHostFree(buf);
   }
   hy_status wait_all() {
-    for (auto& f : fences) {
-      if (hipEventSynchronize(f.event) == hipSuccess) continue;
-      // an event last recorded while its stream was being captured into a graph cannot be waited for (HIP refuses
-      // it): wait for the device instead - every copy out of the ring is then complete - and start new fences
-      (void)hipGetLastError();
-      HY_HIP(hipDeviceSynchronize());
-      for (auto& g : fences) (void)hipEventDestroy(g.event);
-      fences.clear();
-      return HY_OK;
-    }
+    for (auto& f : fences) HY_HIP(hipEventSynchronize(f.event));
     return HY_OK;
   }
   hy_status fence(hipStream_t s) {
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &cap) != hipSuccess) {  // (a query HIP refuses: treated as not capturing)
-      (void)hipGetLastError();
-      cap = hipStreamCaptureStatusNone;
-    }
-    if (cap != hipStreamCaptureStatusNone) return HY_OK;  // (a copy captured into a graph: no event to wait for)
     int dev = 0;
     HY_HIP(hipGetDevice(&dev));
     for (auto& f : fences)
@@ -98,8 +84,26 @@ struct PinnedRing {
     return HY_OK;
   }
 };
+// A stream being captured into a graph is refused: the copy would become a graph node reading a ring slot that later
+// staging reuses (or frees), so every replay would upload whatever the slot then holds. Captured regions (a prepared
+// plan's execution, hyrise_amd_join.hip) stage nothing; their descriptors are in the plan's workspace beforehand.
+inline bool stream_capturing(hipStream_t s) {
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cap) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return cap != hipStreamCaptureStatusNone;
+}
+
 inline hy_status staged_htod(void* dst, const void* src, size_t bytes, hipStream_t s) {
   if (bytes == 0) return HY_OK;
+  if (stream_capturing(s)) {
+#ifdef HYRISE_DEBUG
+    assert(!"staged_htod on a capturing stream");  // debug builds stop at the offending call
+#endif
+    return fail(HY_ERR_INVALID_ARGUMENT, "host-staged copy on a stream being captured into a graph");
+  }
   thread_local PinnedRing ring;
   const size_t need = (bytes + 255) & ~size_t(255);
   if (ring.used + need > ring.cap) {

@@ -1332,6 +1332,18 @@ hy_status hy_agg_float_sum(const uint64_t* limbs, uint32_t n_limbs, int32_t emin
   return HY_OK;
 }
 
+hy_status hy_agg_float_sums(const uint64_t* records, uint64_t n_records, uint32_t words, uint32_t sum_word,
+                            uint32_t n_limbs, int32_t emin, double* out) {
+  if (n_records && (!records || !out)) return fail(HY_ERR_INVALID_ARGUMENT, "null argument");
+  if (sum_word + 2 + n_limbs > words) return fail(HY_ERR_INVALID_ARGUMENT, "sum words outside the record");
+  for (uint64_t g = 0; g < n_records; ++g) {
+    const uint64_t* r = records + g * words;
+    const hy_status st = hy_agg_float_sum(r + sum_word + 2, n_limbs, emin, r[sum_word + 1], out + g);
+    if (st != HY_OK) return st;
+  }
+  return HY_OK;
+}
+
 // Merge of partial aggregates (the multi-GPU Aggregate: each rank aggregates its chunk range, the ranks' records are
 // all-gathered and merged here). Exact: counts and integer sums add; float sums add limb by limb in 128-bit and are
 // carry-normalised back into the layout's limbs (the exact sum of the parts, so hy_agg_float_sum of the merged record

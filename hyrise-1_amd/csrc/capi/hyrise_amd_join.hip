@@ -53,6 +53,7 @@ extern "C" {
 hy_status hy_scan_join_hash_workspace_size(const hy_join_side* build, const hy_join_filter* build_filter,
                                            const hy_join_side* probe, const hy_join_filter* probe_filter,
                                            const hy_join_params* params, size_t* bytes) {
+  KnobScope knob_scope;
   if (!bytes) return fail(HY_ERR_INVALID_ARGUMENT, "bytes");
   SidePlan bp, pp;
   hy_status st = prepare(build, build_filter, probe, probe_filter, params, bp, pp);
@@ -66,6 +67,7 @@ hy_status hy_scan_join_hash(const hy_join_side* build, const hy_join_filter* bui
                             hy_row_id* out_probe, uint64_t out_capacity, uint64_t* partition_begin,
                             uint32_t* partition_counts, hy_join_result* result, void* workspace,
                             size_t workspace_bytes, hy_stream_t stream) {
+  KnobScope knob_scope;
   SidePlan bp, pp;
   hy_status st = prepare(build, build_filter, probe, probe_filter, params, bp, pp);
   if (st != HY_OK) return st;
@@ -113,6 +115,7 @@ struct hy_join_plan_s {
   const uint32_t* misc = nullptr;   // the captured join's flags / total (device)
   const uint64_t* totals = nullptr;
   bool no_graph = false;
+  JoinKnobs knobs;  // the environment's knobs when the plan was created; every execution runs under them
   ~hy_join_plan_s() {
     if (exec) (void)hipGraphExecDestroy(exec);
     if (graph) (void)hipGraphDestroy(graph);
@@ -171,6 +174,7 @@ extern "C" {
 hy_status hy_scan_join_plan_create(const hy_join_side* build, const hy_join_filter* build_filter,
                                    const hy_join_side* probe, const hy_join_filter* probe_filter,
                                    const hy_join_params* params, hy_join_plan_t* plan) {
+  KnobScope knob_scope;
   if (!plan) return fail(HY_ERR_INVALID_ARGUMENT, "plan");
   *plan = nullptr;
   auto p = std::make_unique<hy_join_plan_s>();
@@ -179,6 +183,7 @@ hy_status hy_scan_join_plan_create(const hy_join_side* build, const hy_join_filt
   if (params->key_hash && params->hashed_type != HY_TYPE_INT32)
     return fail(HY_ERR_INVALID_ARGUMENT, "key_hash needs int32 key ids");
   p->params = *params;
+  p->knobs = knobs();
   p->build_type = build->value_type;
   p->probe_type = probe->value_type;
   p->workspace_bytes = join_bytes_any(params->hashed_type, p->bp, p->pp, params->radix_bits);
@@ -193,6 +198,7 @@ hy_status hy_scan_join_plan_execute(hy_join_plan_t plan, hy_row_id* out_build, h
   if (!plan) return fail(HY_ERR_INVALID_ARGUMENT, "plan");
   if (!partition_begin || !partition_counts) return fail(HY_ERR_INVALID_ARGUMENT, "partition arrays");
   hipStream_t s = S(stream);
+  KnobScope knob_scope(plan->knobs);
   struct KeyHashScope {
     explicit KeyHashScope(const uint32_t* k) { g_key_hash = k; }
     ~KeyHashScope() { g_key_hash = nullptr; }
@@ -259,6 +265,7 @@ hy_status hy_scan_join_plan_destroy(hy_join_plan_t plan) {
 
 hy_status hy_join_hash_workspace_size(const hy_join_side* build, const hy_join_side* probe,
                                       const hy_join_params* params, size_t* bytes) {
+  KnobScope knob_scope;
   return hy_scan_join_hash_workspace_size(build, nullptr, probe, nullptr, params, bytes);
 }
 
@@ -266,12 +273,14 @@ hy_status hy_join_hash(const hy_join_side* build, const hy_join_side* probe, con
                        hy_row_id* out_build, hy_row_id* out_probe, uint64_t out_capacity, uint64_t* partition_begin,
                        uint32_t* partition_counts, hy_join_result* result, void* workspace, size_t workspace_bytes,
                        hy_stream_t stream) {
+  KnobScope knob_scope;
   return hy_scan_join_hash(build, nullptr, probe, nullptr, params, out_build, out_probe, out_capacity,
                            partition_begin, partition_counts, result, workspace, workspace_bytes, stream);
 }
 
 hy_status hy_join_exchange_partition_workspace_size(const hy_join_side* side, const hy_join_params* params,
                                                     uint32_t n_ranks, size_t* bytes) {
+  KnobScope knob_scope;
   if (!bytes || !params || n_ranks == 0) return fail(HY_ERR_INVALID_ARGUMENT, "null argument");
   SidePlan p;
   hy_status st = plan_side(side, p);
@@ -300,6 +309,7 @@ hy_status hy_join_exchange_partition_workspace_size(const hy_join_side* side, co
 hy_status hy_join_exchange_partition(const hy_join_side* side, const hy_join_params* params, int32_t keep_nulls,
                                      uint32_t n_ranks, void* out_records, uint64_t* bucket_counts, void* workspace,
                                      size_t workspace_bytes, hy_stream_t stream) {
+  KnobScope knob_scope;
   if (!params || !bucket_counts || n_ranks == 0) return fail(HY_ERR_INVALID_ARGUMENT, "null argument");
   if (params->radix_bits > 24) return fail(HY_ERR_UNSUPPORTED, "radix_bits > 24");
   if (params->key_hash) return fail(HY_ERR_UNSUPPORTED, "string join keys in the distributed join");
@@ -331,6 +341,7 @@ hy_status hy_join_exchange_partition(const hy_join_side* side, const hy_join_par
 hy_status hy_join_exchange_join_workspace_size(const uint64_t* build_counts, const uint64_t* probe_counts,
                                                uint32_t n_senders, uint32_t n_buckets, const hy_join_params* params,
                                                size_t* bytes) {
+  KnobScope knob_scope;
   if (!bytes || !params || !build_counts || !probe_counts || n_senders == 0)
     return fail(HY_ERR_INVALID_ARGUMENT, "null argument");
   const uint32_t bits = params->radix_bits;
@@ -364,6 +375,7 @@ hy_status hy_join_exchange_join(const void* build_records, const uint64_t* build
                                 hy_row_id* out_probe, uint64_t out_capacity, uint64_t* partition_begin,
                                 uint32_t* partition_counts, hy_join_result* result, void* workspace,
                                 size_t workspace_bytes, hy_stream_t stream) {
+  KnobScope knob_scope;
   if (!params || !build_counts || !probe_counts || n_senders == 0 || !partition_begin || !partition_counts)
     return fail(HY_ERR_INVALID_ARGUMENT, "null argument");
   if (params->radix_bits > 24) return fail(HY_ERR_UNSUPPORTED, "radix_bits > 24");
@@ -440,6 +452,7 @@ hy_status plan_row_side(const hy_join_side* side, const hy_join_filter* filter, 
 hy_status hy_scan_join_exchange_partition_workspace_size(const hy_join_side* side, const hy_join_filter* filter,
                                                          const hy_join_params* params, uint32_t n_ranks,
                                                          size_t* bytes) {
+  KnobScope knob_scope;
   if (!bytes) return fail(HY_ERR_INVALID_ARGUMENT, "bytes");
   SidePlan p;
   std::vector<uint32_t> w;
@@ -466,6 +479,7 @@ hy_status hy_scan_join_exchange_partition(const hy_join_side* side, const hy_joi
                                           const hy_join_params* params, int32_t keep_nulls, uint32_t n_ranks,
                                           uint64_t row_base, void* out_records, uint64_t* bucket_counts,
                                           void* workspace, size_t workspace_bytes, hy_stream_t stream) {
+  KnobScope knob_scope;
   if (!bucket_counts) return fail(HY_ERR_INVALID_ARGUMENT, "bucket_counts");
   if (params && params->key_hash) return fail(HY_ERR_UNSUPPORTED, "string join keys in the distributed join");
   SidePlan p;
@@ -523,6 +537,7 @@ hy_status hy_join_exchange_join_rows_workspace_size(const uint64_t* build_counts
                                                     const hy_join_params* params, const uint32_t* build_chunk_sizes,
                                                     uint32_t n_build_chunks, const uint32_t* probe_chunk_sizes,
                                                     uint32_t n_probe_chunks, size_t* bytes) {
+  KnobScope knob_scope;
   if (!bytes) return fail(HY_ERR_INVALID_ARGUMENT, "bytes");
   RecvPlan rb, rp;
   std::vector<uint32_t> w;
@@ -556,6 +571,7 @@ hy_status hy_join_exchange_join_rows(const void* build_records, const uint64_t* 
                                      hy_row_id* out_build, hy_row_id* out_probe, uint64_t out_capacity,
                                      uint64_t* partition_begin, uint32_t* partition_counts, hy_join_result* result,
                                      void* workspace, size_t workspace_bytes, hy_stream_t stream) {
+  KnobScope knob_scope;
   if (!partition_begin || !partition_counts) return fail(HY_ERR_INVALID_ARGUMENT, "partition arrays");
   RecvPlan rb, rp;
   std::vector<uint32_t> w;

@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -36,6 +37,63 @@ inline CaptureState& capture_state() {
   return c;
 }
 
+// Per-call tuning and test knobs of a join: environment variables, read once per C-ABI call (KnobScope at the entry
+// points) so that tests can switch them between calls. A prepared plan snapshots them when it is created and executes
+// under that snapshot, so its workspace carve, every eager execution and a captured graph's replays all use the layout
+// the plan was sized and captured with, whatever the environment says later (HY_HASH_RECORDS /
+// HY_HASH_GROUP / HY_ONEPASS were read per call and could differ between a capture and the plan's sizing).
+struct JoinKnobs {
+  int bloom = -1;                      // HY_JOIN_BLOOM: -1 heuristic, 0 never, 1 always
+  bool hash_records = true;            // HY_HASH_RECORDS
+  int hash_group = 1;                  // HY_HASH_GROUP: 1 or 4 records per lane and load
+  bool blocked = false;                // HY_BLOCKED: pass 0 in Infinity-Cache row blocks (opt-in, see block_count)
+  uint64_t block_bytes = 128ull << 20; // HY_BLOCK_MB
+  uint64_t block_rows = 0;             // HY_BLOCK_ROWS (test knob: rows per block instead of bytes)
+  uint64_t lds_budget = 0;             // HY_JOIN_LDS_BUDGET (test knob; 0: the default budget)
+  bool onepass = false;                // HY_ONEPASS
+  uint64_t onepass_cap_div = 8;        // HY_ONEPASS_CAP_DIV
+  uint64_t onepass_cap = 0;            // HY_ONEPASS_CAP (0: computed)
+};
+
+inline JoinKnobs knobs_from_env() {
+  JoinKnobs k;
+  auto num = [](const char* name, long long dflt) {
+    const char* e = std::getenv(name);
+    return e ? std::strtoll(e, nullptr, 10) : dflt;
+  };
+  if (const char* e = std::getenv("HY_JOIN_BLOOM")) k.bloom = std::strtol(e, nullptr, 10) == 0 ? 0 : std::strtol(e, nullptr, 10) == 1 ? 1 : -1;
+  k.hash_records = num("HY_HASH_RECORDS", 1) != 0;
+  k.hash_group = num("HY_HASH_GROUP", 1) == 4 ? 4 : 1;
+  k.blocked = num("HY_BLOCKED", 0) != 0;
+  const long long mb = num("HY_BLOCK_MB", 128);
+  k.block_bytes = uint64_t(mb > 0 ? mb : 128) << 20;
+  k.block_rows = static_cast<uint64_t>(std::max<long long>(0, num("HY_BLOCK_ROWS", 0)));
+  k.lds_budget = static_cast<uint64_t>(std::max<long long>(0, num("HY_JOIN_LDS_BUDGET", 0)));
+  k.onepass = num("HY_ONEPASS", 0) != 0;
+  k.onepass_cap_div = static_cast<uint64_t>(std::max<long long>(1, num("HY_ONEPASS_CAP_DIV", 8)));
+  k.onepass_cap = static_cast<uint64_t>(std::max<long long>(0, num("HY_ONEPASS_CAP", 0)));
+  return k;
+}
+
+inline const JoinKnobs*& knob_override() {
+  static thread_local const JoinKnobs* k = nullptr;
+  return k;
+}
+inline JoinKnobs knobs() {
+  const JoinKnobs* k = knob_override();
+  return k ? *k : knobs_from_env();
+}
+// The knobs of one C-ABI call: a snapshot of the environment, or a prepared plan's own.
+struct KnobScope {
+  JoinKnobs own;
+  const JoinKnobs* prev;
+  KnobScope() : own(knobs_from_env()), prev(knob_override()) { knob_override() = &own; }
+  explicit KnobScope(const JoinKnobs& k) : own(k), prev(knob_override()) { knob_override() = &own; }
+  ~KnobScope() { knob_override() = prev; }
+  KnobScope(const KnobScope&) = delete;
+  KnobScope& operator=(const KnobScope&) = delete;
+};
+
 // Tiles per span of the pass from column chunks (sub1) and of the record passes (sub2); HY_PART_SUB1 / HY_PART_SUB2
 // override them (tuning). Read once: workspace sizes and launches must agree.
 inline uint32_t sub_from_env(const char* name, uint32_t dflt) {
@@ -50,8 +108,8 @@ inline uint32_t sub1() {
 // Spans of a side with a fused TableScan: two tiles, so that part1_spread's spans hold about as many matches as
 // a record pass's tile (measured on MI355X at SF100: 1.70 ms for part1_spread vs 2.52 ms with one-tile spans);
 // HY_PART_SUB_FILTERED overrides it.
-inline uint32_t sub_filtered() {
-  static const uint32_t v = sub_from_env("HY_PART_SUB_FILTERED", 2);
+inline uint32_t sub_filtered() {  // (at most hyk::GAP_SPAN_MAX rows: part1_compact's 16-bit in-span offsets)
+  static const uint32_t v = std::min<uint32_t>(sub_from_env("HY_PART_SUB_FILTERED", 2), hyk::GAP_SPAN_MAX / hyk::PART_TILE);
   return v;
 }
 // Next-digit bytes beside the records of a pass that has a successor (HY_DIGIT_BYTES=0 turns them off: the next
@@ -68,9 +126,9 @@ inline bool digit_bytes_enabled() {
 // a foreign-key join like the headline's, probe / build ~ 4, keeps the plain path). 16 bits per build key.
 // HY_JOIN_BLOOM=0 / 1 turns it off / on regardless of the ratio. Returns the filter's words (0: none).
 inline uint64_t bloom_words(uint64_t build_rows, uint64_t probe_rows) {
-  const char* e = std::getenv("HY_JOIN_BLOOM");
-  const bool force = e && std::strtol(e, nullptr, 10) == 1;
-  if ((e && std::strtol(e, nullptr, 10) == 0) || build_rows == 0) return 0;
+  const int mode = knobs().bloom;
+  const bool force = mode == 1;
+  if (mode == 0 || build_rows == 0) return 0;
   if (!force && probe_rows < 16 * build_rows) return 0;
   uint64_t w = 1024;
   while (w < build_rows / 2 && w < (uint64_t(1) << 31)) w <<= 1;
@@ -163,8 +221,42 @@ inline void plan_spans(SidePlan& p, uint32_t sub) {
   p.n_tiles1 = tiles;
 }
 
+// The LDS ordering that the partition passes' ranking relies on (hyk::wave_rank_add), checked once per device before
+// its first join (hyk::rank_order_check against the mask ranking). Skipped while the device cannot run it (a stream
+// capture in progress elsewhere); a device that breaks it fails every join loudly.
+inline hy_status check_rank_order() {
+  static std::mutex m;
+  static int state[64] = {};  // 0: not checked yet, 1: holds, 2: broken
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return HY_OK;
+  std::lock_guard<std::mutex> lock(m);
+  if (state[dev] == 0) {
+    uint32_t* d = nullptr;
+    hipStream_t cs = nullptr;
+    if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) return HY_OK;
+    uint32_t bad = 0;
+    bool ran = false;
+    if (hipMalloc(&d, 4) == hipSuccess) {
+      ran = hipMemsetAsync(d, 0, 4, cs) == hipSuccess;
+      if (ran) {
+        hipLaunchKernelGGL(hyk::rank_order_check, dim3(1), dim3(256), 0, cs, 96u, d);
+        ran = hipGetLastError() == hipSuccess && hipMemcpyAsync(&bad, d, 4, hipMemcpyDeviceToHost, cs) == hipSuccess &&
+              hipStreamSynchronize(cs) == hipSuccess;
+      }
+      (void)hipFree(d);
+    }
+    (void)hipStreamDestroy(cs);
+    (void)hipGetLastError();
+    if (ran) state[dev] = bad == 0 ? 1 : 2;
+  }
+  if (state[dev] == 2)
+    return fail(HY_ERR_KERNEL, "this device's LDS atomics do not rank in lane order (hyk::wave_rank_add)");
+  return HY_OK;
+}
+
 inline hy_status plan_side(const hy_join_side* side, SidePlan& p) {
   if (!side || (side->n_chunks && !side->chunks)) return fail(HY_ERR_INVALID_ARGUMENT, "join side");
+  if (hy_status st = check_rank_order()) return st;
   p.ref_base = side->referenced_chunk_base;
   p.chunks.resize(side->n_chunks);
   p.tile_begin.resize(side->n_chunks + 1);
@@ -292,6 +384,19 @@ struct SideBufs {
   uint32_t* tile_owner;      // largest pass's tiles
   uint64_t* total;           // rows taking part (device)
   uint64_t* grand_total;     // total of a fused-scan histogram (records + scan matches)
+  // pass 0 in row blocks (block_plan; null when the side is not blocked): per (block, digit) run begin / count, the
+  // scan matches before each block, and the first record pass's segments (runs) and groups (buckets)
+  uint32_t* cls_begin;
+  uint32_t* cls_count;
+  uint64_t* scan_base;
+  uint32_t* bseg_begin;
+  uint32_t* bseg_end;
+  uint32_t* bseg_stride;
+  uint32_t* bseg_toff;
+  uint64_t* bseg_hbase;
+  uint64_t* group_hbase;
+  uint32_t* group_tiles;
+  uint32_t* group_out;
 };
 
 struct SideSizes {
@@ -300,6 +405,7 @@ struct SideSizes {
   size_t n_chunks = 0, n_referenced = 0;
   bool filtered = false;           // one more histogram row in pass 0 (the scan's matches)
   bool digit_bytes = false;        // next-digit byte arrays (single-GPU sides with more than one pass)
+  uint32_t blocks = 0;             // pass 0 in row blocks (block_plan): their number, else 0
 };
 
 // Largest histogram of any pass, and the largest tile count of any record pass.
@@ -320,7 +426,7 @@ inline void pass_sizes(const SideSizes& z, const std::vector<uint32_t>& w, uint6
       segs *= digits;
       continue;
     }
-    segs = digits;
+    segs = digits * std::max<uint64_t>(1, z.blocks);  // a blocked pass 0: one run per (digit, block)
   }
 }
 
@@ -352,6 +458,23 @@ void carve_side(Carver& cv, const SideSizes& z, uint32_t bits, const std::vector
   b.tile_owner = cv.take<uint32_t>(max_tiles);
   b.total = cv.take<uint64_t>(1);
   b.grand_total = cv.take<uint64_t>(1);
+  b.cls_begin = b.cls_count = b.bseg_begin = b.bseg_end = b.bseg_stride = b.bseg_toff = nullptr;
+  b.scan_base = b.bseg_hbase = b.group_hbase = nullptr;
+  b.group_tiles = b.group_out = nullptr;
+  if (z.blocks && !w.empty()) {
+    const uint64_t nd0 = uint64_t(1) << w[0], nseg = nd0 * z.blocks;
+    b.cls_begin = cv.take<uint32_t>(uint64_t(z.blocks) * 256);
+    b.cls_count = cv.take<uint32_t>(uint64_t(z.blocks) * 256);
+    b.scan_base = cv.take<uint64_t>(z.blocks + 1);
+    b.bseg_begin = cv.take<uint32_t>(nseg);
+    b.bseg_end = cv.take<uint32_t>(nseg);
+    b.bseg_stride = cv.take<uint32_t>(nseg);
+    b.bseg_toff = cv.take<uint32_t>(nseg);
+    b.bseg_hbase = cv.take<uint64_t>(nseg);
+    b.group_hbase = cv.take<uint64_t>(nd0);
+    b.group_tiles = cv.take<uint32_t>(nd0);
+    b.group_out = cv.take<uint32_t>(nd0);
+  }
 }
 
 struct Common {
@@ -363,34 +486,54 @@ struct Common {
 };
 
 inline void carve_common(Carver& cv, uint64_t max_scan, uint32_t bits, Common* c) {
-  c->scan_status_words = max_scan / hyk::SCAN_BLOCK + 2;
+  c->scan_status_words = max_scan / hyk::SCAN_BLOCK + 3;  // look-back words of every tile + the ticket
   c->scan_status = cv.take<uint64_t>(c->scan_status_words);
   c->misc = cv.take<uint32_t>(64);
   c->totals = cv.take<uint64_t>(8);
   c->join_status = cv.take<uint64_t>((uint64_t(1) << bits) + 1);
 }
 
+// n: the length, or with n_dev its upper bound (the device length is *n_dev * n_mul, exclusive_scan_u32).
 inline hy_status run_scan(const uint32_t* in, uint32_t* out, uint64_t n, const Common& c, hipStream_t s,
-                          uint64_t* total_out = nullptr) {
+                          uint64_t* total_out = nullptr, const uint64_t* n_dev = nullptr, uint32_t n_mul = 1) {
   if (n == 0) {
     if (total_out) HY_HIP(hipMemsetAsync(total_out, 0, 8, s));
     return HY_OK;
   }
   const uint64_t tiles = (n + hyk::SCAN_BLOCK - 1) / hyk::SCAN_BLOCK;
-  if (tiles + 1 > c.scan_status_words) return fail(HY_ERR_WORKSPACE, "scan status");
-  HY_HIP(hipMemsetAsync(c.scan_status, 0, sizeof(uint64_t) * (tiles + 1), s));
-  HY_HIP(hipMemsetAsync(c.misc, 0, 4, s));
+  if (tiles + 2 > c.scan_status_words) return fail(HY_ERR_WORKSPACE, "scan status");
+  // the look-back words and (in the word after them) the tile ticket, zeroed by one memset
+  HY_HIP(hipMemsetAsync(c.scan_status, 0, sizeof(uint64_t) * (tiles + 2), s));
+  uint32_t* ticket = reinterpret_cast<uint32_t*>(c.scan_status + tiles + 1);
   KTimer kt_("exclusive_scan", s, n);
   const bool vec = reinterpret_cast<uintptr_t>(in) % 16 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0;
   hipLaunchKernelGGL(vec ? hyk::exclusive_scan_u32<true> : hyk::exclusive_scan_u32<false>,
-                     dim3(static_cast<uint32_t>(tiles)), dim3(hyk::SCAN_T), 0, s, in, out, n, c.scan_status, c.misc,
-                     c.misc + 1, total_out);
+                     dim3(static_cast<uint32_t>(tiles)), dim3(hyk::SCAN_T), 0, s, in, out, n, c.scan_status, ticket,
+                     c.misc + 1, total_out, n_dev, n_mul);
   kt_.done();
   HY_HIP(hipGetLastError());
   return HY_OK;
 }
 
 inline uint32_t full_mask(uint32_t bits) { return bits >= 32 ? 0xFFFFFFFFu : ((1u << bits) - 1u); }
+
+template <typename H, typename P>
+hyk::RecOut<H, P> aos_out(hyk::Rec<H, P>* recs) {
+  return hyk::RecOut<H, P>{recs, nullptr, nullptr, 0u, nullptr, 0u};
+}
+
+// The SoA form of a last record pass (hyk::RecOut / hyk::HashSrc) inside `area`, a record buffer of at least `rows`
+// 8-byte records: 16-bit hash remainders, then (16-byte aligned) the payloads - 6 B per record, so that with rows >= 16
+// both arrays stay readable 3 records past their end (HashSrc's group loads). A build side of a prefiltered join also
+// sets its Bloom words by hash (bloom_n words).
+template <typename H, typename P>
+hyk::RecOut<H, P> soa_out(void* area, uint64_t rows, uint32_t bits, uint32_t* bloom = nullptr, uint64_t bloom_n = 0) {
+  static_assert(sizeof(P) == 4, "SoA records carry 32-bit payloads");
+  auto* hk = static_cast<uint16_t*>(area);
+  auto* pay = reinterpret_cast<P*>(static_cast<char*>(area) + hyk::align16(2 * rows));
+  return hyk::RecOut<H, P>{nullptr, hk, pay, bits, bloom, bloom ? static_cast<uint32_t>(bloom_n - 1) : 0u};
+}
+
 
 // The load path every chunk of the side allows (hyk::LP_*): lean kernels for the all-value and all-single-chunk
 // reference sides, the general one otherwise.
@@ -433,10 +576,7 @@ inline int filter_kind(const SidePlan& p) {
 // match bits 0.94 + 3.16 ms with two-tile spans (2.08 ms with one-tile spans) - the match-bit spread pass compacts a
 // span into LDS before its scatter, which halves the resident workgroups and serialises load, compaction and scatter.
 // HY_HASH_RECORDS=0: keep {key, payload} records up to the partition join also where HashSrc applies (A/B).
-inline bool hash_records_enabled() {
-  const char* e = std::getenv("HY_HASH_RECORDS");  // (read per call: a test switches it)
-  return !(e && std::strtol(e, nullptr, 10) == 0);
-}
+inline bool hash_records_enabled() { return knobs().hash_records; }
 
 inline bool filter_compact_enabled() {
   static const bool v = [] {
@@ -458,7 +598,7 @@ hy_status by_side(const char* tag, F&& f) {
 template <typename SD, typename T, typename H, int LP, int FK>
 hy_status launch_filtered_pass0(const SidePlan& p, const hyk::Side& sd, const hyk::Digit& d0,
                                 const hyk::NextDigit& nd, uint32_t w0, uint32_t n_digits, SideBufs<H, uint32_t>& b,
-                                const Common& c, hipStream_t s, hyk::Rec<H, uint32_t>* out) {
+                                const Common& c, hipStream_t s, const hyk::RecOut<H, uint32_t>& out) {
   const dim3 grid(static_cast<uint32_t>(p.n_tiles1));
   // the match-bit variant is an experiment on the headline's filtered (probe) side: built for that side only
   if constexpr (std::is_same_v<SD, hyk::OnProbe>) if (!filter_compact_enabled() && (p.sub == 1 || p.sub == 2)) {
@@ -478,17 +618,22 @@ hy_status launch_filtered_pass0(const SidePlan& p, const hyk::Side& sd, const hy
     const hyk::Side& sd2 = sd;
     {
       KTimer kt_((std::string("part1_spread.") + SD::name).c_str(), s, p.n_rows);
+      if (out.hk != nullptr) return fail(HY_ERR_UNSUPPORTED, "match-bit pass 0 writes {key, payload} records");
       if (p.sub == 2)
         hipLaunchKernelGGL((hyk::part1_spread_mask<SD, T, H, LP, 2>), grid, dim3(hyk::PART_THREADS), 0, s, sd2, d0, nd,
-                           n_digits, b.off, b.mbits, out);
+                           n_digits, b.off, b.mbits, out.recs);
       else
         hipLaunchKernelGGL((hyk::part1_spread_mask<SD, T, H, LP, 1>), grid, dim3(hyk::PART_THREADS), 0, s, sd2, d0, nd,
-                           n_digits, b.off, b.mbits, out);
+                           n_digits, b.off, b.mbits, out.recs);
       kt_.done();
     }
     HY_HIP(hipGetLastError());
     return HY_OK;
   }
+  // the gapped records in recB, SoA: keys, then (16-byte aligned) the 16-bit in-span offsets (hyk::GAP_NULL)
+  const uint64_t gap_n = p.n_tiles1 * p.sub * hyk::PART_TILE;
+  H* gap_keys = reinterpret_cast<H*>(b.recB);
+  uint16_t* gap_offs = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(b.recB) + hyk::align16(sizeof(H) * gap_n));
   {
     KTimer kt_((std::string("part1_compact.") + SD::name).c_str(), s, p.n_rows);
     bool prefiltered = false;
@@ -496,10 +641,10 @@ hy_status launch_filtered_pass0(const SidePlan& p, const hyk::Side& sd, const hy
     if (prefiltered) {
       if constexpr (std::is_same_v<SD, hyk::OnProbe>)
         hipLaunchKernelGGL((hyk::part1_compact<SD, T, H, LP, FK, true>), grid, dim3(hyk::PART_THREADS), 0, s, sd, d0,
-                           n_digits, b.hist, b.span_count, b.recB);
+                           n_digits, b.hist, b.span_count, gap_keys, gap_offs);
     } else {
       hipLaunchKernelGGL((hyk::part1_compact<SD, T, H, LP, FK, false>), grid, dim3(hyk::PART_THREADS), 0, s, sd, d0,
-                         n_digits, b.hist, b.span_count, b.recB);
+                         n_digits, b.hist, b.span_count, gap_keys, gap_offs);
     }
     kt_.done();
   }
@@ -513,7 +658,7 @@ hy_status launch_filtered_pass0(const SidePlan& p, const hyk::Side& sd, const hy
   {
     KTimer kt_((std::string("part1_spread.") + SD::name).c_str(), s, p.n_rows);
     hipLaunchKernelGGL((hyk::part1_spread<SD, H>), grid, dim3(hyk::PART_THREADS), 0, s, sd, d0, nd, static_cast<int>(w0),
-                       n_digits, b.off, b.span_count, b.recB, out);
+                       n_digits, b.off, b.span_count, gap_keys, gap_offs, out);
     kt_.done();
   }
   HY_HIP(hipGetLastError());
@@ -523,7 +668,7 @@ hy_status launch_filtered_pass0(const SidePlan& p, const hyk::Side& sd, const hy
 template <typename SD, typename T, typename H, typename P, int LP>
 hy_status launch_pass0(const SidePlan& p, const hyk::Side& sd, const hyk::Digit& d0,
                        const hyk::NextDigit& nd, uint32_t w0, uint32_t n_digits, SideBufs<H, P>& b, const Common& c,
-                       hipStream_t s, hyk::Rec<H, P>* out) {
+                       hipStream_t s, const hyk::RecOut<H, P>& out) {
   const bool filt = p.filtered;
   const int fk = filter_kind(p);
   if constexpr (LP != hyk::LP_REF1 && std::is_same_v<T, H> && std::is_same_v<P, uint32_t>) {
@@ -564,9 +709,15 @@ hy_status launch_pass0(const SidePlan& p, const hyk::Side& sd, const hyk::Digit&
 template <typename SD, typename T, typename H, typename P>
 hy_status pass0_side(const SidePlan& p, SideBufs<H, P>& b, uint32_t bits, uint32_t w0,
                      uint32_t seed, bool keep_nulls, uint32_t ref_base, const hyk::NextDigit& nd, const Common& c,
-                     hipStream_t s, hyk::Rec<H, P>* out, const uint32_t* bloom = nullptr, uint64_t bloom_n = 0,
+                     hipStream_t s, const hyk::RecOut<H, P>& out, const uint32_t* bloom = nullptr, uint64_t bloom_n = 0,
                      bool bloom_by_hash = false, const hyk::FilterHdr* bloom_hdr = nullptr,
-                     uint64_t range_words = 0) {
+                     uint64_t range_words = 0);
+
+// The kernels' view of a side inside the workspace (pass 0).
+template <typename H, typename P>
+hyk::Side make_side(const SidePlan& p, const SideBufs<H, P>& b, uint32_t seed, bool keep_nulls, uint32_t ref_base,
+                    const uint32_t* bloom, uint64_t bloom_n, bool bloom_by_hash, const hyk::FilterHdr* bloom_hdr,
+                    uint64_t range_words) {
   hyk::Side sd{};
   sd.chunks = b.chunks;
   sd.n_chunks = static_cast<uint32_t>(p.chunks.size());
@@ -590,6 +741,15 @@ hy_status pass0_side(const SidePlan& p, SideBufs<H, P>& b, uint32_t bits, uint32
   sd.bloom_hdr = bloom ? bloom_hdr : nullptr;
   sd.range_words = range_words;
   sd.seed = seed;
+  return sd;
+}
+
+template <typename SD, typename T, typename H, typename P>
+hy_status pass0_side(const SidePlan& p, SideBufs<H, P>& b, uint32_t bits, uint32_t w0,
+                     uint32_t seed, bool keep_nulls, uint32_t ref_base, const hyk::NextDigit& nd, const Common& c,
+                     hipStream_t s, const hyk::RecOut<H, P>& out, const uint32_t* bloom, uint64_t bloom_n,
+                     bool bloom_by_hash, const hyk::FilterHdr* bloom_hdr, uint64_t range_words) {
+  const hyk::Side sd = make_side(p, b, seed, keep_nulls, ref_base, bloom, bloom_n, bloom_by_hash, bloom_hdr, range_words);
   const uint32_t n_digits = 1u << w0;
   hyk::Digit d0{full_mask(bits), bits - w0, n_digits - 1u, seed, g_key_hash};
   HY_HIP(hipMemsetAsync(b.total, 0, 8, s));
@@ -612,23 +772,6 @@ hy_status pass0_side(const SidePlan& p, SideBufs<H, P>& b, uint32_t bits, uint32
                      b.total, b.segA);
   HY_HIP(hipGetLastError());
   return HY_OK;
-}
-
-template <typename H, typename P>
-hyk::RecOut<H, P> aos_out(hyk::Rec<H, P>* recs) {
-  return hyk::RecOut<H, P>{recs, nullptr, nullptr, 0u, nullptr, 0u};
-}
-
-// The SoA form of a last record pass (hyk::RecOut / hyk::HashSrc) inside `area`, a record buffer of at least `rows`
-// 8-byte records: 16-bit hash remainders, then (16-byte aligned) the payloads - 6 B per record, so that with rows >= 16
-// both arrays stay readable 3 records past their end (HashSrc's group loads). A build side of a prefiltered join also
-// sets its Bloom words by hash (bloom_n words).
-template <typename H, typename P>
-hyk::RecOut<H, P> soa_out(void* area, uint64_t rows, uint32_t bits, uint32_t* bloom = nullptr, uint64_t bloom_n = 0) {
-  static_assert(sizeof(P) == 4, "SoA records carry 32-bit payloads");
-  auto* hk = static_cast<uint16_t*>(area);
-  auto* pay = reinterpret_cast<P*>(static_cast<char*>(area) + hyk::align16(2 * rows));
-  return hyk::RecOut<H, P>{nullptr, hk, pay, bits, bloom, bloom ? static_cast<uint32_t>(bloom_n - 1) : 0u};
 }
 
 // One record pass over segments sg (tile prefix and owners filled, grid = an upper bound of its tiles): histogram
@@ -654,12 +797,13 @@ hy_status record_pass(const SideBufs<H, P>& b, const hyk::Segs& sg, const hyk::G
       kt_.done();
     }
     HY_HIP(hipGetLastError());
-    hy_status st = run_scan(b.hist, b.off, grid * n_digits, c, s);
+    // (scanned over the tiles that exist, not the grid's upper bound)
+    hy_status st = run_scan(b.hist, b.off, grid * n_digits, c, s, nullptr, sg.seg_tile_begin + sg.n_segs, n_digits);
     if (st != HY_OK) return st;
     {
       KTimer kt_((std::string("part2_scatter.") + SD::name).c_str(), s, rows);
-      hipLaunchKernelGGL((hyk::part2_scatter<SD, H, P>), dim3(static_cast<uint32_t>(grid)), dim3(hyk::PART_THREADS), 0, s,
-                         sg, dg, nd, static_cast<int>(w), n_digits, in, b.off, out);
+      hipLaunchKernelGGL((hyk::part2_scatter<SD, H, P>), dim3(static_cast<uint32_t>(grid)), dim3(hyk::PART_THREADS), 0,
+                         s, sg, dg, nd, static_cast<int>(w), n_digits, in, b.off, out);
       kt_.done();
     }
     HY_HIP(hipGetLastError());
@@ -719,6 +863,196 @@ hy_status local_passes(SideBufs<H, P>& b, const std::vector<uint32_t>& w, size_t
   return HY_OK;
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Pass 0 in Infinity-Cache-sized row blocks (hyk::part1_count / part1_fill, join.hip): per block a counting read, the
+// block's histogram scan and a second read - served on-die - that writes the scan output and the stable scatter into
+// the block's own region; the first record pass then reads every bucket as its runs in block order (block_geometry).
+// Opt-in (HY_BLOCKED=1) for single-GPU sides with two or more radix digits; HY_BLOCK_MB sets the input bytes per block
+// (default 128 MiB: the block plus what its fill writes stays within the 256 MiB Infinity Cache,
+// profiles/r05_mall_probe.jsonl). Measured on MI355X at SF100 (round 5, profiles/r05_blocked_ab.txt): SLOWER than the
+// classic passes - headline 8.47 ms against 7.03 ms. The re-read is nearly free, but the passes are not bandwidth-bound:
+// per 128 MB block part1_count takes 52-56 us (2.4 TB/s) and part1_fill 108 us, whose ranking and staging run over
+// every row of the block where part1_spread handles only the compacted matches (probe side 23 x (56 + 108) us + 23 x
+// ~25 us of scans, totals and launch gaps = 4.3 ms against 1.24 + 1.32 ms).
+// ---------------------------------------------------------------------------------------------------------------
+constexpr uint32_t MAX_BLOCKS = 64;
+
+inline bool blocked_enabled() { return knobs().blocked; }
+inline uint64_t block_target_bytes() { return knobs().block_bytes; }
+inline uint64_t block_target_rows_override() { return knobs().block_rows; }
+
+// Input bytes per row of a side's pass 0: the join column (through a PosList also the 8-byte RowID) and the fused
+// scan's predicate column.
+inline uint64_t pass0_row_bytes(const SidePlan& p, uint32_t key_bytes) {
+  bool ref = false;
+  for (const auto& c : p.chunks) ref = ref || c.pos_list != nullptr;
+  uint64_t b = key_bytes + (ref ? 8 : 0);
+  if (p.filtered) {
+    uint64_t fb = 1;
+    for (const auto& f : p.filter)
+      if (f.column.size) fb = std::max<uint64_t>(fb, f.column.kind == HY_COL_DICT ? f.column.vid_width : 8);
+    b += fb;
+  }
+  return b;
+}
+
+// Blocks of a side (0: not blocked): pass-0 spans split into contiguous ranges of about block_target_bytes() of input.
+inline uint32_t block_count(const SidePlan& p, uint32_t key_bytes, size_t plan_digits, bool int32_keys) {
+  // (instantiated for int32 hashed keys only: an opt-in experiment need not multiply the other types' kernels)
+  if (!int32_keys || !blocked_enabled() || plan_digits < 2 || p.n_tiles1 == 0) return 0;
+  uint64_t k;
+  if (const uint64_t rows = block_target_rows_override())
+    k = (p.n_rows + rows - 1) / std::max<uint64_t>(rows, 1);
+  else
+    k = (p.n_rows * pass0_row_bytes(p, key_bytes) + block_target_bytes() - 1) / block_target_bytes();
+  return static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>({k, MAX_BLOCKS, p.n_tiles1})));
+}
+
+struct BlockPlan {
+  uint32_t n = 0;
+  std::vector<uint64_t> t0;        // n + 1 span bounds
+  std::vector<uint32_t> rec_base;  // first row of each block's first span = start of its record region
+  std::vector<uint32_t> c_lo;      // n + 1: chunks whose first span lies in block k are [c_lo[k], c_lo[k + 1])
+};
+
+inline BlockPlan block_plan(const SidePlan& p, uint32_t n) {
+  BlockPlan b;
+  b.n = n;
+  b.t0.resize(n + 1);
+  b.rec_base.resize(n);
+  const uint64_t span = uint64_t(p.sub) * hyk::PART_TILE;
+  size_t c = 0;
+  for (uint32_t k = 0; k <= n; ++k) {
+    b.t0[k] = p.n_tiles1 * k / n;
+    if (k == n) break;
+    while (c + 1 < p.chunks.size() && p.tile_begin[c + 1] <= b.t0[k]) ++c;  // the chunk holding span t0 (non-empty)
+    b.rec_base[k] = static_cast<uint32_t>(p.row_begin[c] + (b.t0[k] - p.tile_begin[c]) * span);
+  }
+  // chunk_begin entries (n_chunks + 1, the last at tile_begin = n_tiles) by the block holding their first span
+  b.c_lo.resize(n + 1);
+  size_t cc = 0;
+  for (uint32_t k = 0; k < n; ++k) {
+    while (cc <= p.chunks.size() && p.tile_begin[cc] < b.t0[k]) ++cc;
+    b.c_lo[k] = static_cast<uint32_t>(cc);
+  }
+  b.c_lo[n] = static_cast<uint32_t>(p.chunks.size() + 1);
+  return b;
+}
+
+template <typename SD, typename T, typename H, int LP, int FK, bool PF>
+hy_status launch_blocks(const SidePlan& p, const BlockPlan& bl, const hyk::Side& sd, const hyk::Digit& d0,
+                        const hyk::NextDigit& nd, uint32_t n_digits, SideBufs<H, uint32_t>& b, const Common& c,
+                        hipStream_t s, hyk::Rec<H, uint32_t>* out) {
+  constexpr bool filt = FK != hyk::FK_NONE;
+  if (filt) HY_HIP(hipMemsetAsync(b.scan_base, 0, 8, s));
+  for (uint32_t k = 0; k < bl.n; ++k) {
+    const uint64_t t0 = bl.t0[k];
+    const uint32_t nt = static_cast<uint32_t>(bl.t0[k + 1] - t0);
+    {
+      KTimer kt_((std::string("part1_count.") + SD::name).c_str(), s, p.n_rows);
+      hipLaunchKernelGGL((hyk::part1_count<SD, T, H, LP, FK, PF>), dim3(nt), dim3(hyk::PART_THREADS), 0, s, sd, d0,
+                         n_digits, t0, b.hist);
+      kt_.done();
+    }
+    HY_HIP(hipGetLastError());
+    hy_status st = run_scan(b.hist, b.off, uint64_t(n_digits + (filt ? 1 : 0)) * nt, c, s, b.grand_total);
+    if (st != HY_OK) return st;
+    hipLaunchKernelGGL(hyk::block_totals, dim3(1), dim3(256), 0, s, b.off, nt, n_digits, filt ? 1 : 0, b.grand_total, k,
+                       bl.rec_base[k], t0, p.n_tiles1, k + 1 == bl.n ? 1 : 0, b.cls_begin, b.cls_count, b.scan_base,
+                       b.tile_begin, bl.c_lo[k], bl.c_lo[k + 1], filt ? p.scan_chunk_begin : nullptr);
+    HY_HIP(hipGetLastError());
+    {
+      KTimer kt_((std::string("part1_fill.") + SD::name).c_str(), s, p.n_rows);
+      hipLaunchKernelGGL((hyk::part1_fill<SD, T, H, LP, FK, PF>), dim3(nt), dim3(hyk::PART_THREADS), 0, s, sd, d0, nd,
+                         n_digits, t0, b.off, bl.rec_base[k], b.scan_base + k, out);
+      kt_.done();
+    }
+    HY_HIP(hipGetLastError());
+  }
+  return HY_OK;
+}
+
+// Filter kind / prefilter dispatch of one load path. A fused scan needs the join column in the hashed type and a
+// data-table side (as launch_pass0); the prefiltered instances exist for probe sides only.
+template <typename SD, typename T, typename H, int LP>
+hy_status launch_blocks_lp(const SidePlan& p, const BlockPlan& bl, const hyk::Side& sd, const hyk::Digit& d0,
+                           const hyk::NextDigit& nd, uint32_t n_digits, SideBufs<H, uint32_t>& b, const Common& c,
+                           hipStream_t s, hyk::Rec<H, uint32_t>* out) {
+  constexpr bool probe = std::is_same_v<SD, hyk::OnProbe>;
+  const bool pf = probe && sd.bloom != nullptr;
+  auto go = [&](auto fk_tag) -> hy_status {
+    constexpr int FK = decltype(fk_tag)::value;
+    if constexpr (probe) {
+      if (pf) return launch_blocks<SD, T, H, LP, FK, true>(p, bl, sd, d0, nd, n_digits, b, c, s, out);
+    }
+    return launch_blocks<SD, T, H, LP, FK, false>(p, bl, sd, d0, nd, n_digits, b, c, s, out);
+  };
+  if (!p.filtered) return go(std::integral_constant<int, hyk::FK_NONE>{});
+  if constexpr (LP != hyk::LP_REF1 && std::is_same_v<T, H>) {
+    switch (filter_kind(p)) {
+      case hyk::FK_DICT8:
+        return go(std::integral_constant<int, hyk::FK_DICT8>{});
+      case hyk::FK_DICT16:
+        return go(std::integral_constant<int, hyk::FK_DICT16>{});
+      case hyk::FK_DICT32:
+        return go(std::integral_constant<int, hyk::FK_DICT32>{});
+      default:
+        return go(std::integral_constant<int, hyk::FK_ANY>{});
+    }
+  }
+  return fail(HY_ERR_UNSUPPORTED, "fused scan on a side whose join column type is not the hashed type");
+}
+
+// The side's pass 0 in blocks, then the first record pass over the runs (grouped by bucket) and the remaining record
+// passes. On return *recs / *bounds hold the final records and partition bounds (as local_passes).
+template <typename SD, typename T, typename H>
+hy_status blocked_side(const SidePlan& p, SideBufs<H, uint32_t>& b, uint32_t bits, const std::vector<uint32_t>& w,
+                       uint32_t n_blocks, const hyk::Side& sd, const Common& c, hipStream_t s, hyk::Rec<H>** recs,
+                       uint32_t** bounds, const hyk::RecOut<H, uint32_t>* last_out) {
+  const uint32_t nd0 = 1u << w[0], w1 = w[1];
+  const BlockPlan bl = block_plan(p, n_blocks);
+  const hyk::Digit d0{full_mask(bits), bits - w[0], nd0 - 1u, sd.seed, g_key_hash};
+  const hyk::NextDigit nd = next_digit(w, 0, bits, b.digA);
+  HY_HIP(hipMemsetAsync(b.total, 0, 8, s));
+  if (p.filtered && p.scan_chunk_begin) HY_HIP(hipMemsetAsync(p.scan_chunk_begin, 0, 8 * (p.chunks.size() + 1), s));
+  hipLaunchKernelGGL(hyk::fill_tile_owner, dim3((sd.n_chunks + 255) / 256), dim3(256), 0, s, b.tile_begin, sd.n_chunks,
+                     b.tile_owner);
+  HY_HIP(hipGetLastError());
+  const int lp = load_path(p);
+  hy_status st;
+  if (lp == hyk::LP_VALUE)
+    st = launch_blocks_lp<SD, T, H, hyk::LP_VALUE>(p, bl, sd, d0, nd, nd0, b, c, s, b.recA);
+  else if (lp == hyk::LP_REF1)
+    st = launch_blocks_lp<SD, T, H, hyk::LP_REF1>(p, bl, sd, d0, nd, nd0, b, c, s, b.recA);
+  else
+    st = launch_blocks_lp<SD, T, H, hyk::LP_ANY>(p, bl, sd, d0, nd, nd0, b, c, s, b.recA);
+  if (st != HY_OK) return st;
+  const uint32_t nseg = nd0 * bl.n;
+  hipLaunchKernelGGL(hyk::block_geometry, dim3(1), dim3(256), 0, s, b.cls_begin, b.cls_count, bl.n, nd0,
+                     static_cast<uint32_t>(span2()), 1u << w1, b.bseg_begin, b.bseg_end, b.bseg_stride, b.bseg_toff,
+                     b.bseg_hbase, b.seg_tile_begin, b.group_hbase, b.group_tiles, b.group_out, b.total);
+  HY_HIP(hipGetLastError());
+  hipLaunchKernelGGL(hyk::fill_tile_owner, dim3(grid_for(nseg, 256)), dim3(256), 0, s, b.seg_tile_begin, nseg,
+                     b.tile_owner);
+  HY_HIP(hipGetLastError());
+  const hyk::Segs sg{b.bseg_begin, b.seg_tile_begin, b.tile_owner, nseg, b.bseg_end, b.bseg_hbase, b.bseg_stride,
+                     b.bseg_toff, sub2()};
+  const hyk::Groups gr{b.group_hbase, b.group_tiles, b.group_out};
+  const uint64_t grid = p.n_rows / span2() + 1 + nseg;
+  const hyk::NextDigit nd1 = next_digit(w, 1, bits, b.digB);
+  const hyk::RecOut<H, uint32_t> out1 = (last_out && w.size() == 2) ? *last_out : aos_out<H, uint32_t>(b.recB);
+  st = record_pass<SD, H, uint32_t>(b, sg, gr, nd0, grid, bits, bits - w[0] - w1, w1, sd.seed, b.recA, nd.bytes, nd1,
+                                    out1, b.total, b.segA, c, s, p.n_rows);
+  if (st != HY_OK) return st;
+  if (w.size() == 2) {
+    *recs = b.recB;
+    *bounds = b.segA;
+    return HY_OK;
+  }
+  return local_passes<SD, H, uint32_t>(b, w, 2, bits, sd.seed, b.recB, b.recA, nd1.bytes, b.digA, b.segA, b.segB,
+                                       uint64_t(nd0) << w1, b.total, p.n_rows, c, s, recs, bounds, last_out);
+}
+
 inline hyk::RowMap make_map(const uint64_t* dev_row_begin, const std::vector<uint64_t>& host_row_begin) {
   hyk::RowMap m{};
   m.row_begin = dev_row_begin;
@@ -739,7 +1073,7 @@ inline hyk::RowMap make_map(const uint64_t* dev_row_begin, const std::vector<uin
 template <typename H, typename P>
 uint32_t lds_table_rows() {
   size_t budget = sizeof(hyk::Rec<H, P>) > 8 ? 72 * 1024 : 40 * 1024;
-  if (const char* e = std::getenv("HY_JOIN_LDS_BUDGET")) budget = std::strtoull(e, nullptr, 10);  // test knob
+  if (const uint64_t b = knobs().lds_budget) budget = b;  // test knob
   uint32_t rows = hyk::LDS_MAX_ROWS;
   while (rows > 16 && hyk::table_bytes<H, P>(rows) > budget) rows = rows * 7 / 8;
   return rows;
@@ -862,8 +1196,9 @@ hy_status run_join_partitions(const uint32_t* build_begin, const uint32_t* probe
   return HY_OK;
 }
 
-inline SideSizes sizes_of(const SidePlan& p, bool digit_bytes) {
+inline SideSizes sizes_of(const SidePlan& p, bool digit_bytes, uint32_t blocks = 0) {
   SideSizes z;
+  z.blocks = blocks;
   z.rows = p.n_rows;
   z.tiles1 = p.n_tiles1;
   z.sub = p.sub;
@@ -878,13 +1213,15 @@ template <typename H>
 size_t classic_join_bytes(const SidePlan& bp, const SidePlan& pp, uint32_t bits) {
   const auto w = digit_plan(bits, 0);
   const bool db = w.size() > 1 && digit_bytes_enabled();
+  constexpr bool i32 = std::is_same_v<H, int32_t>;
+  const uint32_t kb = block_count(bp, sizeof(H), w.size(), i32), kp = block_count(pp, sizeof(H), w.size(), i32);
   Carver cv{nullptr, 0};
   SideBufs<H> a, b;
-  carve_side<H, uint32_t>(cv, sizes_of(bp, db), bits, w, 1, true, a);
-  carve_side<H, uint32_t>(cv, sizes_of(pp, db), bits, w, 1, true, b);
+  carve_side<H, uint32_t>(cv, sizes_of(bp, db, kb), bits, w, 1, true, a);
+  carve_side<H, uint32_t>(cv, sizes_of(pp, db, kp), bits, w, 1, true, b);
   uint64_t ha, hb, t;
-  pass_sizes(sizes_of(bp, db), w, 1, &ha, &t);
-  pass_sizes(sizes_of(pp, db), w, 1, &hb, &t);
+  pass_sizes(sizes_of(bp, db, kb), w, 1, &ha, &t);
+  pass_sizes(sizes_of(pp, db, kp), w, 1, &hb, &t);
   Common c, cb;  // (join_typed: the probe side's and the build side's)
   carve_common(cv, std::max({ha, hb, (uint64_t(1) << bits) + 1}), bits, &c);
   carve_common(cv, std::max({ha, hb, (uint64_t(1) << bits) + 1}), bits, &cb);
@@ -917,8 +1254,7 @@ hy_status upload_side(const SidePlan& p, const SideBufs<H, P>& b, hipStream_t s)
 // overflow (skewed keys) falls back to the two-read path.
 // ---------------------------------------------------------------------------------------------------------------
 inline bool onepass_enabled() {
-  const char* e = std::getenv("HY_ONEPASS");
-  return e && std::strtol(e, nullptr, 10) != 0;
+  return knobs().onepass;
 }
 
 struct OnepassGeo {
@@ -938,10 +1274,10 @@ inline OnepassGeo onepass_geo(const SidePlan& p, uint32_t n_digits0) {
   g.grid = static_cast<uint32_t>(max_tiles * hyk::NCLASS);
   const uint64_t class_rows = max_tiles * hyk::PART_TILE;
   uint64_t div = 8;
-  if (const char* e = std::getenv("HY_ONEPASS_CAP_DIV")) div = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
+  div = knobs().onepass_cap_div;
   const uint64_t expect = (class_rows + n_digits0 - 1) / n_digits0;
   g.cap = std::min<uint64_t>(class_rows, expect + expect / div + (div > 1000 ? 0 : hyk::PART_TILE));
-  if (const char* e = std::getenv("HY_ONEPASS_CAP")) g.cap = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
+  if (const uint64_t cap = knobs().onepass_cap) g.cap = cap;
   g.gapped = g.cap * n_digits0 * hyk::NCLASS;
   return g;
 }
@@ -1270,13 +1606,15 @@ hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join
   if (workspace_bytes < classic_join_bytes<H>(bp, pp, bits)) return fail(HY_ERR_WORKSPACE, "join workspace too small");
   const auto w = digit_plan(bits, 0);
   const bool db = w.size() > 1 && digit_bytes_enabled();
+  constexpr bool i32 = std::is_same_v<H, int32_t>;
+  const uint32_t blocks[2] = {block_count(bp, sizeof(H), w.size(), i32), block_count(pp, sizeof(H), w.size(), i32)};
   Carver cv{static_cast<char*>(workspace), workspace_bytes};
   SideBufs<H> bb, pb;
-  carve_side<H, uint32_t>(cv, sizes_of(bp, db), bits, w, 1, true, bb);
-  carve_side<H, uint32_t>(cv, sizes_of(pp, db), bits, w, 1, true, pb);
+  carve_side<H, uint32_t>(cv, sizes_of(bp, db, blocks[0]), bits, w, 1, true, bb);
+  carve_side<H, uint32_t>(cv, sizes_of(pp, db, blocks[1]), bits, w, 1, true, pb);
   uint64_t ha, hb2, t;
-  pass_sizes(sizes_of(bp, db), w, 1, &ha, &t);
-  pass_sizes(sizes_of(pp, db), w, 1, &hb2, &t);
+  pass_sizes(sizes_of(bp, db, blocks[0]), w, 1, &ha, &t);
+  pass_sizes(sizes_of(pp, db, blocks[1]), w, 1, &hb2, &t);
   Common c{}, cb{};  // c: the probe side and the partition join; cb: the build side (it may run concurrently)
   carve_common(cv, std::max({ha, hb2, (uint64_t(1) << bits) + 1}), bits, &c);
   carve_common(cv, std::max({ha, hb2, (uint64_t(1) << bits) + 1}), bits, &cb);
@@ -1309,6 +1647,7 @@ hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join
   // a record join with integer keys: the prefilter is a key-range bitmap when the build keys' range fits
   const bool range_filter = use_bloom && !soa && std::is_integral_v<H>;
   hyk::RecOut<H, uint32_t> soa_outs[2];
+  const hyk::RecOut<H, uint32_t> pass0_outs[2] = {aos_out<H, uint32_t>(bb.recA), aos_out<H, uint32_t>(pb.recA)};
   if (soa) {
     if (use_bloom) HY_HIP(hipMemsetAsync(bloom, 0, 4 * bloom_n, s));
     // the record passes after pass 0 ping-pong recA -> recB -> recA ...: the last one writes recB after an odd count
@@ -1327,11 +1666,25 @@ hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join
     const Common& cs = side == 0 ? cb : c;
     const hipStream_t st_s = side == 0 ? sb : s;
     const hyk::NextDigit nd = next_digit(w, 0, bits, b.digA);
+    if (blocks[side]) {  // pass 0 in row blocks and the record passes after it
+      const bool pf = side == 1 && use_bloom;
+      const hyk::Side sd = make_side(p, b, prm->seed, side == 1 && keep_nulls, p.ref_base, pf ? bloom : nullptr, bloom_n,
+                                     soa, pf && range_filter ? filter_hdr : nullptr,
+                                     pf && range_filter ? range_bitmap_words(bp.n_rows) : 0);
+      const hyk::RecOut<H, uint32_t>* lo = soa ? &soa_outs[side] : nullptr;
+      hy_status st = HY_ERR_UNSUPPORTED;
+      if constexpr (i32)
+        st = side == 0 ? blocked_side<hyk::OnBuild, TB, H>(p, b, bits, w, blocks[0], sd, cs, st_s, &recs[0], &bounds[0],
+                                                           lo)
+                       : blocked_side<hyk::OnProbe, TP, H>(p, b, bits, w, blocks[1], sd, cs, st_s, &recs[1], &bounds[1],
+                                                           lo);
+      if (st != HY_OK) return st;
+    } else {
     hy_status st = side == 0
                        ? pass0_side<hyk::OnBuild, TB, H, uint32_t>(p, b, bits, w.empty() ? 0 : w[0], prm->seed, false,
-                                                     p.ref_base, nd, cs, st_s, b.recA)
+                                                     p.ref_base, nd, cs, st_s, pass0_outs[0])
                        : pass0_side<hyk::OnProbe, TP, H, uint32_t>(p, b, bits, w.empty() ? 0 : w[0], prm->seed, keep_nulls,
-                                                     p.ref_base, nd, cs, st_s, b.recA, use_bloom ? bloom : nullptr,
+                                                     p.ref_base, nd, cs, st_s, pass0_outs[1], use_bloom ? bloom : nullptr,
                                                      bloom_n, soa, range_filter ? filter_hdr : nullptr,
                                                      range_filter ? range_bitmap_words(bp.n_rows) : 0);
     if (st != HY_OK) return st;
@@ -1342,6 +1695,7 @@ hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join
                                                       soa ? &soa_outs[side] : nullptr);
     });
     if (st != HY_OK) return st;
+    }
     if (side == 0 && use_bloom && !soa) {  // the probe side's prefilter over the build side's keys (its records)
       const uint64_t rw = range_filter ? range_bitmap_words(bp.n_rows) : 0;
       HY_HIP(hipMemsetAsync(filter_hdr, 0, sizeof(hyk::FilterHdr), s));
@@ -1373,9 +1727,8 @@ hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join
                                                out_probe, out_capacity, partition_begin, partition_counts, result, c,
                                                s, bp.n_rows + pp.n_rows, pp.n_rows, probe_exact);
     };
-    const char* g = std::getenv("HY_HASH_GROUP");  // records per lane and load (A/B): 1 (default) or 4
-    return (g && std::strtol(g, nullptr, 10) == 4) ? run_hash(hyk::HashSrc<uint32_t, 4>{})
-                                                  : run_hash(hyk::HashSrc<uint32_t, 1>{});
+    // records per lane and load (A/B, HY_HASH_GROUP): 1 (default) or 4
+    return knobs().hash_group == 4 ? run_hash(hyk::HashSrc<uint32_t, 4>{}) : run_hash(hyk::HashSrc<uint32_t, 1>{});
   }
   return run_join_partitions<hyk::RecSrc<H, uint32_t>, uint32_t>(
       bounds[0], bounds[1], 1u << bits, hyk::RecSrc<H, uint32_t>{recs[0]}, hyk::RecSrc<H, uint32_t>{recs[1]}, bmap,
@@ -1605,7 +1958,7 @@ hy_status exchange_partition_for_hashed(const SidePlan& p, int32_t value_type, c
       if (upload_side(p, b, s)) return HY_ERR_DEVICE;
       hy_status st2 = pass0_side<hyk::OnExchange, T_, H, P>(p, b, bits, w[0], params->seed, keep_nulls != 0, p.ref_base,
                                            hyk::NextDigit{nullptr, 0, 0}, c, s,
-                                           static_cast<hyk::Rec<H, P>*>(out_records));
+                                           aos_out<H, P>(static_cast<hyk::Rec<H, P>*>(out_records)));
       if (st2 != HY_OK) return st2;
       std::vector<uint32_t> bounds(T + 1);
       HY_HIP(hipMemcpyAsync(bounds.data(), b.segA, 4 * (T + 1), hipMemcpyDeviceToHost, s));

@@ -6,6 +6,7 @@
 
 #include "device.hpp"
 #include "operators.hpp"
+#include "scheduler.hpp"
 #include "storage.hpp"
 
 namespace py = pybind11;
@@ -374,11 +375,28 @@ PYBIND11_MODULE(_hyrise_host, m) {
       .def_readonly("walltime_ns", &OperatorPerformanceData::walltime_ns)
       .def_readonly("rows_in", &OperatorPerformanceData::rows_in);
 
+  // the host scheduler the operators submit their jobs to (scheduler.hpp): "pool" (n workers fed from one queue),
+  // "inline" (jobs run when scheduled) or None (a thread per job)
+  m.def(
+      "set_job_scheduler",
+      [](py::object kind, unsigned workers) {
+        if (kind.is_none()) return set_job_scheduler(nullptr);
+        const std::string k = kind.cast<std::string>();
+        if (k == "pool") return set_job_scheduler(make_pool_scheduler(workers));
+        if (k == "inline") return set_job_scheduler(make_inline_scheduler());
+        throw std::invalid_argument("job scheduler kind: pool, inline or None");
+      },
+      py::arg("kind"), py::arg("workers") = 4);
+
+  py::enum_<DescriptionMode>(m, "DescriptionMode")
+      .value("SingleLine", DescriptionMode::SingleLine)
+      .value("MultiLine", DescriptionMode::MultiLine);
+
   py::class_<AbstractOperator, std::shared_ptr<AbstractOperator>>(m, "AbstractOperator")
       .def("execute", &AbstractOperator::execute, py::call_guard<py::gil_scoped_release>())
       .def("get_output", [](const AbstractOperator& o) { return std::const_pointer_cast<Table>(o.get_output()); })
       .def("name", &AbstractOperator::name)
-      .def("description", &AbstractOperator::description)
+      .def("description", &AbstractOperator::description, py::arg("description_mode") = DescriptionMode::SingleLine)
       .def("performance_data", &AbstractOperator::performance_data)
       .def("deep_copy", &AbstractOperator::deep_copy)
       .def("set_parameters",

@@ -3,6 +3,7 @@
 #include <sched.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -26,11 +27,12 @@ struct StreamHolder {
   ~StreamHolder() {
     if (!stream) return;
     auto& r = stream_registry();
-    {
-      std::lock_guard<std::mutex> lock(r.m);
-      r.streams.erase(std::remove(r.streams.begin(), r.streams.end(), stream), r.streams.end());
-    }
+    std::lock_guard<std::mutex> lock(r.m);
+    r.streams.erase(std::remove(r.streams.begin(), r.streams.end(), stream), r.streams.end());
     hy_stream_destroy(stream);  // (its pending work still completes)
+    // a DeviceBuffer freed later on this thread (another thread_local's destructor) must not name the destroyed
+    // stream: device_buffer_free then falls back to a registered stream or the null stream
+    stream = nullptr;
   }
 };
 thread_local StreamHolder t_stream;
@@ -43,9 +45,11 @@ std::shared_ptr<DeviceBuffer> upload(const void* host, size_t bytes, hy_stream_t
 }  // namespace
 
 namespace {
-// size classes: powers of two from 4 KiB; at most temp_cache_bytes() kept per thread: an eighth of the device's memory
-// (36 GiB on MI355X), at least 8 GiB - enough to keep a JoinHash workspace of an SF100 join (a 16 GiB block):
-// freeing it after every execution costs a hipFree (a device-wide synchronisation and an unmap) per operator call
+// size classes: powers of two from 4 KiB, cached per thread; at most temp_cache_bytes() kept by ALL threads together
+// (g_temp_cached: an eighth of the device's memory, 36 GiB on MI355X, at least 8 GiB) - enough to keep a JoinHash
+// workspace of an SF100 join (a 16 GiB block): freeing it after every execution costs a hipFree (a device-wide
+// synchronisation and an unmap) per operator call. A failed allocation frees the thread's cached blocks and retries.
+std::atomic<size_t> g_temp_cached{0};
 size_t temp_cache_bytes() {
   static const size_t bytes = [] {
     uint64_t free_b = 0, total_b = 0;
@@ -57,9 +61,13 @@ size_t temp_cache_bytes() {
 struct TempCache {
   std::vector<std::pair<size_t, void*>> free_blocks;  // (block bytes, ptr)
   size_t cached = 0;
-  ~TempCache() {
+  void trim() {
     for (auto& b : free_blocks) hy_free(b.second);
+    free_blocks.clear();
+    g_temp_cached -= cached;
+    cached = 0;
   }
+  ~TempCache() { trim(); }
 };
 TempCache& temp_cache() {
   thread_local TempCache c;
@@ -115,22 +123,30 @@ void* temp_block_acquire(size_t bytes, size_t* block_bytes) {
       c.free_blocks[i] = c.free_blocks.back();
       c.free_blocks.pop_back();
       c.cached -= b;
+      g_temp_cached -= b;
       *block_bytes = b;
       return p;
     }
   }
   void* p = nullptr;
-  hy_check(hy_malloc(&p, b), "hy_malloc");
+  if (hy_malloc(&p, b) != HY_OK) {  // device memory short: give back this thread's cached blocks, then retry once
+    c.trim();
+    hy_check(hy_malloc(&p, b), "hy_malloc");
+  }
   *block_bytes = b;
   return p;
 }
 
 void temp_block_release(void* ptr, size_t block_bytes) {
   auto& c = temp_cache();
-  if (c.cached + block_bytes > temp_cache_bytes()) {
-    hy_free(ptr);
-    return;
-  }
+  // reserve the block's bytes in the process-wide budget; over it, the block goes back to the device
+  size_t cur = g_temp_cached.load();
+  do {
+    if (cur + block_bytes > temp_cache_bytes()) {
+      hy_free(ptr);
+      return;
+    }
+  } while (!g_temp_cached.compare_exchange_weak(cur, cur + block_bytes));
   c.free_blocks.emplace_back(block_bytes, ptr);
   c.cached += block_bytes;
 }

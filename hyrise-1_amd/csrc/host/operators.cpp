@@ -1,4 +1,5 @@
 #include "operators.hpp"
+#include "scheduler.hpp"
 
 #include <algorithm>
 #include <atomic>
@@ -458,9 +459,55 @@ std::shared_ptr<Table> column_comparison_scan(const std::shared_ptr<const Table>
 
 }  // namespace
 
-const std::string TableScan::description() const {
-  return "TableScan (Col #" + std::to_string(_left_column_id) + " " + predicate_condition_to_string(_predicate_condition) +
-         ")";
+namespace {
+
+// all_parameter_variant.cpp:11-23 (to_string): placeholder, column, or the value as boost::lexical_cast prints it
+std::string parameter_to_string(const AllParameterVariant& x) {
+  if (is_parameter_id(x)) return "Placeholder #" + std::to_string(std::get<ParameterID>(x).t);
+  if (is_column_id(x)) return "Col #" + std::to_string(std::get<ColumnParameter>(x).column_id);
+  const AllTypeVariant& v = std::get<AllTypeVariant>(x);
+  return variant_is_null(v) ? std::string("NULL") : detail::to_lexical_string(v, 6);
+}
+
+std::string join_mode_to_string(JoinMode m) {  // constant_mappings.cpp:54-57
+  switch (m) {
+    case JoinMode::Cross:
+      return "Cross";
+    case JoinMode::Inner:
+      return "Inner";
+    case JoinMode::Left:
+      return "Left";
+    case JoinMode::Outer:
+      return "Outer";
+    case JoinMode::Right:
+      return "Right";
+    case JoinMode::Semi:
+      return "Semi";
+    default:
+      return "Anti";
+  }
+}
+
+}  // namespace
+
+// table_scan.cpp:51-61
+const std::string TableScan::description(DescriptionMode description_mode) const {
+  std::string column_name = "Col #" + std::to_string(_left_column_id);
+  if (_input_left && input_table_left()) column_name = input_table_left()->column_name(_left_column_id);
+  const char* separator = description_mode == DescriptionMode::MultiLine ? "\n" : " ";
+  return name() + separator + "(" + column_name + " " + predicate_condition_to_string(_predicate_condition) + " " +
+         parameter_to_string(_right_parameter) + ")";
+}
+
+// abstract_join_operator.cpp:30-43
+const std::string AbstractJoinOperator::description(DescriptionMode description_mode) const {
+  std::string left = "Col #" + std::to_string(_column_ids.first);
+  std::string right = "Col #" + std::to_string(_column_ids.second);
+  if (_input_left && input_table_left()) left = input_table_left()->column_name(_column_ids.first);
+  if (_input_right && input_table_right()) right = input_table_right()->column_name(_column_ids.second);
+  const char* separator = description_mode == DescriptionMode::MultiLine ? "\n" : " ";
+  return name() + separator + "(" + join_mode_to_string(_mode) + " Join where " + left + " " +
+         predicate_condition_to_string(_predicate_condition) + " " + right + ")";
 }
 
 // table_scan.cpp:63-70: a ParameterID placeholder is replaced by its value when the map holds one
@@ -1344,12 +1391,10 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
   std::vector<std::shared_ptr<Chunk>> chunks(n_parts);
   std::vector<PosList*> lists(static_cast<size_t>(n_parts) * n_lists);
   std::vector<DevicePosList*> mirrors(lists.size());
-  static const size_t max_workers = [] {  // HY_OP_THREADS caps the builder threads (A/B)
+  static const size_t max_workers = [] {  // HY_OP_THREADS caps the builder jobs (A/B)
     const char* e = std::getenv("HY_OP_THREADS");
     return e ? std::max(1L, std::strtol(e, nullptr, 10)) : 16L;
   }();
-  const unsigned workers = static_cast<unsigned>(
-      std::max<size_t>(1, std::min<size_t>({max_workers, host_cpu_share(), n_parts / 2048})));
   std::atomic<size_t> next{0};
   const auto spawn = std::chrono::steady_clock::now();
   std::atomic<int64_t> last_done_us{0};  // (HY_OP_TRACE: when the builders finished)
@@ -1384,13 +1429,9 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
       }
     }
   };
-  // once the partition ranges are known and every chunk is built, the same threads set the PosLists' views
+  // once the partition ranges are known and every chunk is built, jobs set the PosLists' views
   std::vector<uint64_t> h_begin(n_parts);
   std::vector<uint32_t> h_count(n_parts);
-  std::mutex phase_m;
-  std::condition_variable phase_cv;
-  int ranges = 0;      // 1: h_begin / h_count hold the ranges; -1: the join failed
-  unsigned built = 0;  // threads done building
   std::atomic<size_t> next_view{0};
   auto set_views = [&]() {
     constexpr size_t BATCH = 2048;
@@ -1407,40 +1448,18 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
       }
     }
   };
-  std::exception_ptr builder_error;  // a builder's exception, rethrown on this thread after the join
-  auto build_then_set_views = [&]() {
-    std::exception_ptr err;
-    try {
-      build();
-    } catch (...) {
-      err = std::current_exception();
-    }
-    std::unique_lock<std::mutex> lock(phase_m);
-    if (err && !builder_error) builder_error = err;
-    ++built;
-    phase_cv.notify_all();
-    phase_cv.wait(lock, [&] { return ranges < 0 || (ranges > 0 && built == workers); });
-    if (ranges < 0 || builder_error) return;  // (a failed builder left some partitions without PosLists)
-    lock.unlock();
-    set_views();
-  };
-  std::vector<std::thread> pool;  // (the builders touch no device state)
-  for (unsigned t = 1; t < workers; ++t) pool.emplace_back(build_then_set_views);
-  struct Joiner {  // the builders finish before anything they read goes away, also when the join throws
-    std::vector<std::thread>& pool;
-    std::mutex& m;
-    std::condition_variable& cv;
-    int& ranges;
-    ~Joiner() {
-      {
-        std::lock_guard<std::mutex> lock(m);
-        ranges = -1;  // (also after the ranges: this thread may have thrown before it built its share)
-        cv.notify_all();
-      }
-      for (auto& t : pool)
-        if (t.joinable()) t.join();
-    }
-  } joiner{pool, phase_m, phase_cv, ranges};
+  // The builders are jobs of the host's scheduler (scheduler.hpp; join_hash.cpp:139-182 submits JobTasks and waits in
+  // CurrentScheduler::wait_for_tasks), scheduled before the join's kernels so that they run while the device joins;
+  // without a registered scheduler each job has a thread of its own. The group is declared after everything the jobs
+  // read, so its destructor waits for them also when the join throws.
+  JobGroup builders;
+  static const size_t parts_per_job = [] {  // at least this many partitions per job (HY_OP_PARTS_PER_JOB: tests)
+    const char* e = std::getenv("HY_OP_PARTS_PER_JOB");
+    return e ? std::max(1L, std::strtol(e, nullptr, 10)) : 2048L;
+  }();
+  const unsigned workers = static_cast<unsigned>(std::max<size_t>(
+      1, std::min<size_t>({max_workers, builders.concurrency(host_cpu_share()), n_parts / parts_per_job})));
+  for (unsigned t = 0; t < workers; ++t) builders.schedule(build);
 
   hy_join_result res{};
   for (int attempt = 0; attempt < 2; ++attempt) {
@@ -1464,17 +1483,15 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
   uint64_t used = 0;  // the output range the partitions occupy
   for (uint32_t part = 0; part < n_parts; ++part)
     if (h_count[part]) used = std::max<uint64_t>(used, h_begin[part] + h_count[part]);
-  {
-    std::lock_guard<std::mutex> lock(phase_m);
-    ranges = 1;
-    phase_cv.notify_all();
-  }
   if (with_build) dereference_groups(bo, *out_b, used);
   dereference_groups(po, *out_p, used);
-  build_then_set_views();  // (this thread joins the builders)
-  for (auto& t : pool) t.join();
-  if (builder_error) std::rethrow_exception(builder_error);
-  if (tr.on) tr.note("builders done after start (" + std::to_string(workers) + " threads)", last_done_us.load() / 1000.0);
+  builders.wait();  // (rethrows a builder's exception)
+  {
+    JobGroup viewers;
+    for (unsigned t = 0; t < workers; ++t) viewers.schedule(set_views);
+    viewers.wait();
+  }
+  if (tr.on) tr.note("builders done after start (" + std::to_string(workers) + " jobs)", last_done_us.load() / 1000.0);
   tr.mark("output chunks built, views set");
   std::vector<std::shared_ptr<Chunk>> nonempty;  // join_hash.cpp:835-837: no chunk for an empty partition
   nonempty.reserve(n_parts);

@@ -1,6 +1,9 @@
 // Operator layer: the reference's AbstractOperator surface with GPU-backed TableScan / JoinHash / Aggregate.
 //
 //   AbstractOperator::execute / get_output / _on_execute   reference src/lib/operators/abstract_operator.cpp:25-67
+//   AbstractReadOnlyOperator                               reference src/lib/operators/abstract_read_only_operator.hpp:12-33
+//   AbstractJoinOperator (mode, column ids, predicate, description)
+//                                                          reference src/lib/operators/abstract_join_operator.hpp:25-53
 //   TableWrapper                                           reference src/lib/operators/table_wrapper.cpp
 //   deep_copy / set_parameters / _on_deep_copy / _on_set_parameters
 //                                                          reference src/lib/operators/abstract_operator.hpp:107-155
@@ -29,6 +32,9 @@
 namespace hyrise {
 
 enum class OperatorType { TableWrapper, TableScan, JoinHash, Aggregate, Projection, Validate, Mock };
+
+// types.hpp:197 of the reference: how description() lays out an operator's parameters
+enum class DescriptionMode { SingleLine, MultiLine };
 
 struct OperatorPerformanceData {
   uint64_t walltime_ns = 0;  // reference operator_performance_data.hpp:15
@@ -72,7 +78,11 @@ class AbstractOperator : public std::enable_shared_from_this<AbstractOperator> {
 
   OperatorType type() const { return _type; }
   virtual const std::string name() const = 0;
-  virtual const std::string description() const { return name(); }
+  // abstract_operator.hpp:93, abstract_operator.cpp:76
+  virtual const std::string description(DescriptionMode description_mode = DescriptionMode::SingleLine) const {
+    (void)description_mode;
+    return name();
+  }
 
   std::shared_ptr<const AbstractOperator> input_left() const { return _input_left; }
   std::shared_ptr<const AbstractOperator> input_right() const { return _input_right; }
@@ -103,9 +113,8 @@ class AbstractOperator : public std::enable_shared_from_this<AbstractOperator> {
   void set_parameters(const ParameterMap& parameters);
 
  protected:
-  // execute() calls the context overload; operators that need no transaction implement the plain one
-  virtual std::shared_ptr<const Table> _on_execute(std::shared_ptr<TransactionContext>) { return _on_execute(); }
-  virtual std::shared_ptr<const Table> _on_execute() = 0;
+  // execute() calls the context overload (abstract_operator.cpp:47); AbstractReadOnlyOperator forwards it to the plain one
+  virtual std::shared_ptr<const Table> _on_execute(std::shared_ptr<TransactionContext> transaction_context) = 0;
   virtual void _on_cleanup() {}
   virtual void _on_set_parameters(const ParameterMap& parameters) = 0;
   virtual std::shared_ptr<AbstractOperator> _on_deep_copy(
@@ -122,10 +131,46 @@ class AbstractOperator : public std::enable_shared_from_this<AbstractOperator> {
   OperatorPerformanceData _performance_data;
 };
 
-class TableWrapper final : public AbstractOperator {
+// abstract_read_only_operator.hpp:12-33: the operators that do not write their inputs; only Validate reads the
+// transaction context, the others implement the plain _on_execute().
+class AbstractReadOnlyOperator : public AbstractOperator {
+ public:
+  using AbstractOperator::AbstractOperator;
+
+ protected:
+  std::shared_ptr<const Table> _on_execute(std::shared_ptr<TransactionContext>) override { return _on_execute(); }
+  virtual std::shared_ptr<const Table> _on_execute() = 0;
+};
+
+// abstract_join_operator.hpp:25-53 / abstract_join_operator.cpp:9-45: a join of two inputs on one column pair; owns the
+// mode, the column pair and the predicate, and the description every join shares.
+class AbstractJoinOperator : public AbstractReadOnlyOperator {
+ public:
+  AbstractJoinOperator(OperatorType type, std::shared_ptr<const AbstractOperator> left,
+                       std::shared_ptr<const AbstractOperator> right, JoinMode mode,
+                       std::pair<ColumnID, ColumnID> column_ids, PredicateCondition predicate_condition)
+      : AbstractReadOnlyOperator(type, std::move(left), std::move(right)),
+        _mode(mode),
+        _column_ids(column_ids),
+        _predicate_condition(predicate_condition) {
+    Assert(mode != JoinMode::Cross, "Specified JoinMode not supported by an AbstractJoin, use Product etc. instead.");
+  }
+  JoinMode mode() const { return _mode; }
+  const std::pair<ColumnID, ColumnID>& column_ids() const { return _column_ids; }
+  PredicateCondition predicate_condition() const { return _predicate_condition; }
+  const std::string description(DescriptionMode description_mode = DescriptionMode::SingleLine) const override;
+
+ protected:
+  const JoinMode _mode;
+  const std::pair<ColumnID, ColumnID> _column_ids;
+  const PredicateCondition _predicate_condition;
+  void _on_set_parameters(const ParameterMap&) override {}  // abstract_join_operator.cpp:45
+};
+
+class TableWrapper final : public AbstractReadOnlyOperator {
  public:
   explicit TableWrapper(std::shared_ptr<const Table> table)
-      : AbstractOperator(OperatorType::TableWrapper), _table(std::move(table)) {}
+      : AbstractReadOnlyOperator(OperatorType::TableWrapper), _table(std::move(table)) {}
   const std::string name() const override { return "TableWrapper"; }
 
  protected:
@@ -138,19 +183,19 @@ class TableWrapper final : public AbstractOperator {
   std::shared_ptr<const Table> _table;
 };
 
-class TableScan final : public AbstractOperator {
+class TableScan final : public AbstractReadOnlyOperator {
  public:
   // table_scan.cpp:32-37: the right side is a value, a column of the input (ColumnParameter) or a ParameterID
   // placeholder that set_parameters replaces by its value before execution.
   TableScan(std::shared_ptr<const AbstractOperator> in, ColumnID left_column_id, PredicateCondition predicate_condition,
             AllParameterVariant right_parameter)
-      : AbstractOperator(OperatorType::TableScan, std::move(in)),
+      : AbstractReadOnlyOperator(OperatorType::TableScan, std::move(in)),
         _left_column_id(left_column_id),
         _predicate_condition(predicate_condition),
         _right_parameter(std::move(right_parameter)) {}
 
   const std::string name() const override { return "TableScan"; }
-  const std::string description() const override;
+  const std::string description(DescriptionMode description_mode = DescriptionMode::SingleLine) const override;
   ColumnID left_column_id() const { return _left_column_id; }
   PredicateCondition predicate_condition() const { return _predicate_condition; }
   const AllParameterVariant& right_parameter() const { return _right_parameter; }
@@ -173,9 +218,10 @@ class TableScan final : public AbstractOperator {
 // TransactionContext enters as its two fields, the transaction id and the snapshot commit id.
 // validate.hpp:18-36: Validate(in), visibility from the operator's TransactionContext (set_transaction_context, as the
 // SQL pipeline does for every operator); without one, _on_execute() fails like the reference's (validate.cpp:45-47).
-class Validate final : public AbstractOperator {
+class Validate final : public AbstractReadOnlyOperator {
  public:
-  explicit Validate(std::shared_ptr<const AbstractOperator> in) : AbstractOperator(OperatorType::Validate, std::move(in)) {}
+  explicit Validate(std::shared_ptr<const AbstractOperator> in)
+      : AbstractReadOnlyOperator(OperatorType::Validate, std::move(in)) {}
   const std::string name() const override { return "Validate"; }
 
  protected:
@@ -188,27 +234,22 @@ class Validate final : public AbstractOperator {
   }
 };
 
-class JoinHash final : public AbstractOperator {
+// join_hash.hpp:24-30: JoinHash : AbstractJoinOperator
+class JoinHash final : public AbstractJoinOperator {
  public:
   JoinHash(std::shared_ptr<const AbstractOperator> left, std::shared_ptr<const AbstractOperator> right, JoinMode mode,
            std::pair<ColumnID, ColumnID> column_ids, PredicateCondition predicate_condition, size_t radix_bits = 9)
-      : AbstractOperator(OperatorType::JoinHash, std::move(left), std::move(right)),
-        _mode(mode),
-        _column_ids(column_ids),
-        _predicate_condition(predicate_condition),
+      : AbstractJoinOperator(OperatorType::JoinHash, std::move(left), std::move(right), mode, column_ids,
+                             predicate_condition),
         _radix_bits(radix_bits) {
     Assert(predicate_condition == PredicateCondition::Equals, "Operator not supported by Hash Join.");
   }
   const std::string name() const override { return "JoinHash"; }
-  JoinMode mode() const { return _mode; }
   // radix bits actually used by the last execution (the constructor argument is ignored, as in the reference)
   uint32_t used_radix_bits() const { return _used_radix_bits; }
-  const std::pair<ColumnID, ColumnID>& column_ids() const { return _column_ids; }
-  PredicateCondition predicate_condition() const { return _predicate_condition; }
 
  protected:
   std::shared_ptr<const Table> _on_execute() override;
-  void _on_set_parameters(const ParameterMap&) override {}  // join_hash.cpp:47
   // join_hash.cpp:41-45: the copy gets the default radix_bits (the argument is ignored by execution anyway)
   std::shared_ptr<AbstractOperator> _on_deep_copy(const std::shared_ptr<AbstractOperator>& copied_input_left,
                                                   const std::shared_ptr<AbstractOperator>& copied_input_right) const override {
@@ -216,9 +257,6 @@ class JoinHash final : public AbstractOperator {
   }
 
  private:
-  JoinMode _mode;
-  std::pair<ColumnID, ColumnID> _column_ids;
-  PredicateCondition _predicate_condition;
   size_t _radix_bits;
   uint32_t _used_radix_bits = 0;
 };
@@ -229,11 +267,11 @@ struct AggregateColumnDefinition {
   AggregateFunction function;
 };
 
-class Aggregate final : public AbstractOperator {
+class Aggregate final : public AbstractReadOnlyOperator {
  public:
   Aggregate(std::shared_ptr<const AbstractOperator> in, std::vector<AggregateColumnDefinition> aggregates,
             std::vector<ColumnID> groupby_column_ids)
-      : AbstractOperator(OperatorType::Aggregate, std::move(in)),
+      : AbstractReadOnlyOperator(OperatorType::Aggregate, std::move(in)),
         _aggregates(std::move(aggregates)),
         _groupby_column_ids(std::move(groupby_column_ids)) {
     Assert(!(_aggregates.empty() && _groupby_column_ids.empty()),
@@ -263,10 +301,10 @@ class Aggregate final : public AbstractOperator {
 // column per expression; PQPColumn expressions forward the input column when the output table type equals the
 // input's (a projection of columns only keeps the input's type; anything computed makes a Data table). Arithmetic
 // expressions are evaluated on the device (hy_projection), one launch per expression over all chunks.
-class Projection final : public AbstractOperator {
+class Projection final : public AbstractReadOnlyOperator {
  public:
   Projection(std::shared_ptr<const AbstractOperator> in, std::vector<std::shared_ptr<AbstractExpression>> expressions)
-      : AbstractOperator(OperatorType::Projection, std::move(in)), expressions(std::move(expressions)) {}
+      : AbstractReadOnlyOperator(OperatorType::Projection, std::move(in)), expressions(std::move(expressions)) {}
   const std::string name() const override { return "Projection"; }
 
   const std::vector<std::shared_ptr<AbstractExpression>> expressions;

@@ -948,49 +948,96 @@ __device__ __forceinline__ void table_store(unsigned long long* p, uint64_t v) {
 }
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// Returns the slot of the group with the given key words, inserting it (record initialised) if new; ~0 on failure.
-__device__ __forceinline__ uint64_t group_slot(const AggDesc& d, const AggTable& t, const uint64_t* key, uint32_t nk) {
+// The records one wave claims in one probe round, staged for the wave's cooperative initialisation.
+struct ClaimStage {
+  uint64_t slot[WAVE];
+  uint64_t key[WAVE][AGG_MAX_GROUPBY + 1];
+};
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Every lane of the wave calls this together; a lane with `want` gets the slot of the group with its key words,
+// inserted if new, ~0 on failure (other lanes: ~0). The probe loop runs in wave-uniform rounds: the slots the wave's
+// lanes claim in a round are initialised by the whole wave - consecutive lanes store consecutive words of the claimed
+// records, so a 19-word record leaves as ~3 line writes instead of 19 separate 8-byte write-throughs - drained, and
+// published before the next round. No claim outlives its round, so a lane that meets a slot locked by its own wave
+// only waits for that round's publish.
+__device__ __forceinline__ uint64_t group_slot_wave(const AggDesc& d, const AggTable& t, const uint64_t* key,
+                                                    uint32_t nk, bool want, ClaimStage& cs) {
   uint64_t h = 0x9E3779B97F4A7C15ull;
   for (uint32_t i = 0; i < nk; ++i) h = mix64(h ^ key[i]);
   uint64_t s = h & (t.cap - 1);
   // a READY slot's state word carries a tag of the key's hash (>= HSLOT_READY): other keys are skipped without
   // loading their key words
   const uint32_t tag = static_cast<uint32_t>(h >> 32) | HSLOT_READY;
-  uint64_t probes = 0, spins = 0;
-  while (probes < t.cap && spins < LOCK_SPIN_LIMIT) {
-    const uint32_t st = __hip_atomic_load(&t.state[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (st == HSLOT_EMPTY) {
-      uint32_t expected = HSLOT_EMPTY;
-      if (__hip_atomic_compare_exchange_strong(&t.state[s], &expected, HSLOT_LOCKED, __ATOMIC_RELAXED,
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-        // (no insert counter: the compaction counts the groups, and past the load limit the host reports
-        // HY_ERR_GROUP_BOUND. A counter per insert - even 64 sharded ones - serialises ~10^4 atomics per word at the
-        // L2: TPC-H 3 SF100, 1.1 M groups, 2 ms.)
-        unsigned long long* rec = t.records + s * d.words;
-        for (uint32_t i = 0; i < nk; ++i) table_store(rec + i, key[i]);
-        for (uint32_t i = nk; i < d.words; ++i) table_store(rec + i, word_init(d.word_op[i]));
-        drain_stores();
-        __hip_atomic_store(&t.state[s], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return s;
+  const uint32_t W = d.words;
+  const int lane = __lane_id();
+  uint64_t result = ~0ull, probes = 0, spins = 0;
+  bool active = want;
+  while (__ballot(active)) {
+    bool claimed = false;
+    if (active) {
+      if (probes >= t.cap || spins >= LOCK_SPIN_LIMIT) {
+        atomicOr(d.error, 1u);
+        active = false;
+      } else {
+        const uint32_t st = __hip_atomic_load(&t.state[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (st == HSLOT_EMPTY) {
+          // (no insert counter: the compaction counts the groups, and past the load limit the host reports
+          // HY_ERR_GROUP_BOUND. A counter per insert - even 64 sharded ones - serialises ~10^4 atomics per word at
+          // the L2: TPC-H 3 SF100, 1.1 M groups, 2 ms.) A lost race re-reads the same slot next round.
+          uint32_t expected = HSLOT_EMPTY;
+          claimed = __hip_atomic_compare_exchange_strong(&t.state[s], &expected, HSLOT_LOCKED, __ATOMIC_RELAXED,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (st == HSLOT_LOCKED) {
+          ++spins;
+        } else {
+          bool match = false;
+          if (st == tag) {
+            const unsigned long long* rec = t.records + s * W;
+            uint64_t diff = 0;  // every key word loaded at once (no short-circuit chain of dependent loads)
+            for (uint32_t i = 0; i < nk; ++i) diff |= table_load(rec + i) ^ key[i];
+            match = diff == 0;
+          }
+          if (match) {
+            result = s;
+            active = false;
+          } else {
+            s = (s + 1) & (t.cap - 1);
+            ++probes;
+          }
+        }
       }
-      continue;  // lost the race: re-read the same slot
     }
-    if (st == HSLOT_LOCKED) {
-      ++spins;
-      __builtin_amdgcn_s_sleep(1);
+    const uint64_t cm = __ballot(claimed);
+    if (cm == 0) {
+      if (__ballot(active)) __builtin_amdgcn_s_sleep(1);  // only locked slots left to wait for
       continue;
     }
-    if (st == tag) {
-      const unsigned long long* rec = t.records + s * d.words;
-      uint64_t diff = 0;  // every key word loaded at once (no short-circuit chain of dependent loads)
-      for (uint32_t i = 0; i < nk; ++i) diff |= table_load(rec + i) ^ key[i];
-      if (diff == 0) return s;
+    if (claimed) {
+      const uint32_t r = static_cast<uint32_t>(__popcll(cm & lanemask_lt()));
+      cs.slot[r] = s;
+      for (uint32_t i = 0; i < nk; ++i) cs.key[r][i] = key[i];
     }
-    s = (s + 1) & (t.cap - 1);
-    ++probes;
+    wave_lds_sync();
+    const uint32_t n = static_cast<uint32_t>(__popcll(cm));
+    for (uint32_t e = lane; e < n * W; e += WAVE) {
+      const uint32_t q = e / W, w = e - q * W;
+      table_store(t.records + cs.slot[q] * W + w, w < nk ? cs.key[q][w] : word_init(d.word_op[w]));
+    }
+    drain_stores();
+    wave_lds_sync();  // (the stage is rewritten next round)
+    if (claimed) {
+      __hip_atomic_store(&t.state[s], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      result = s;
+      active = false;
+    }
   }
-  atomicOr(d.error, 1u);
-  return ~0ull;
+  return result;
 }
 
 // true if (tag, value) was not in the distinct set yet
@@ -1069,6 +1116,7 @@ inline uint32_t flat_items(uint64_t rows) {
 
 __global__ __launch_bounds__(AGG_THREADS) void agg_hash_runs(AggDesc d, AggTable t, uint64_t total_rows,
                                                              uint32_t items) {
+  __shared__ ClaimStage s_claim[AGG_THREADS / WAVE];
   const int lane = __lane_id();
   const uint64_t tile_row0 = static_cast<uint64_t>(blockIdx.x) * AGG_THREADS * items;
   const uint32_t H = d.n_gb;
@@ -1111,8 +1159,7 @@ __global__ __launch_bounds__(AGG_THREADS) void agg_hash_runs(AggDesc d, AggTable
     const int end = after ? __builtin_ctzll(after) - 1 : WAVE - 1;
     const uint64_t run_mask = (end == WAVE - 1 ? ~0ull : ((2ull << end) - 1)) & ~((1ull << start) - 1);
     const bool tail = valid && end == lane;
-    uint64_t s = ~0ull;
-    if (tail) s = group_slot(d, t, key, H + 1);
+    uint64_t s = group_slot_wave(d, t, key, H + 1, tail, s_claim[threadIdx.x / WAVE]);
     s = __shfl(s, end, WAVE);  // the run's slot, in every lane of the run
     unsigned long long* rec = (valid && s != ~0ull) ? t.records + s * d.words : nullptr;
     if (tail && rec) {

@@ -612,6 +612,53 @@ __device__ __forceinline__ uint32_t wave_rank_lds(uint32_t digit, bool active, u
   return rank;
 }
 
+// The same stable ranking with ONE returning LDS add per item: gfx950's LDS applies the lanes of an atomic that hit the
+// same counter in ascending lane order, and a wave's LDS instructions in program order, so the old value an item's add
+// returns is its rank among the wave's same-digit items before it in (item, lane) order, and the counter ends at the
+// digit's count (what wave_rank_lds computes with an or / read / clear of the digit's lane mask and a read / advance of
+// its counter). Measured on MI355X (tools/rank_probe.hip, profiles/r05_rank_probe_*.jsonl): equal to the stable ranks
+// for all of 201 M items in uniform, 4-digit, single-digit and half-active waves; >= 1.8x wave_rank_lds's throughput.
+// The property is checked on each device before its first partition launch (rank_order_check, join_host.hpp), and a
+// device that breaks it fails the join with HY_ERR_KERNEL instead of producing an unstable order.
+__device__ __forceinline__ uint32_t wave_rank_add(uint32_t digit, bool active, uint32_t* wave_cnt) {
+  return active ? __hip_atomic_fetch_add(&wave_cnt[digit], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0u;
+}
+
+// Self-check of wave_rank_add against wave_rank_lds (one 256-thread workgroup; *bad counts mismatching items): waves
+// of uniform, 4-digit, single-digit and half-active items, the collision patterns of skewed keys included.
+static __global__ __launch_bounds__(256) void rank_order_check(uint32_t rounds, uint32_t* __restrict__ bad) {
+  __shared__ uint32_t s_cnt_a[4][256];
+  __shared__ uint32_t s_cnt_m[4][256];
+  __shared__ uint64_t s_mask[4][256];
+  const int w = threadIdx.x / WAVE, lane = __lane_id();
+  uint32_t nbad = 0;
+  for (uint32_t r = 0; r < rounds; ++r) {
+    for (int i = lane; i < 256; i += WAVE) {
+      s_cnt_a[w][i] = 0;
+      s_cnt_m[w][i] = 0;
+      s_mask[w][i] = 0;
+    }
+    const uint32_t kind = (r * 4 + w) % 6;
+    const uint32_t span = kind % 3 == 0 ? 256u : kind % 3 == 1 ? 4u : 1u;
+    uint32_t dig[16], ra[16];
+    bool act[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t h = murmur2<int32_t>(static_cast<int32_t>((r * 4 + w) * 1024 + k * WAVE + lane), 0x5EEDu);
+      dig[k] = (h % span) * (256u / span);
+      act[k] = kind < 3 || ((h >> 16) & 1u);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) ra[k] = wave_rank_add(dig[k], act[k], s_cnt_a[w]);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t rm = wave_rank_lds(dig[k], act[k], s_mask[w], s_cnt_m[w]);
+      if (act[k] && rm != ra[k]) ++nbad;
+    }
+  }
+  if (nbad) atomicAdd(bad, nbad);
+}
+
 // Zeroes this wave's 256 digit masks (the wave alone uses them until the next block barrier).
 __device__ __forceinline__ void clear_wave_masks(uint64_t* wave_mask) {
 #pragma unroll
@@ -748,7 +795,7 @@ __global__ __launch_bounds__(PART_THREADS) void part1_hist(Side s, Digit dg, uin
 template <typename SD, typename T, typename H, typename P, int LP>
 __global__ __launch_bounds__(PART_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void part1_scatter(
     Side s, Digit dg, NextDigit nd, int dbits, uint32_t n_digits, const uint32_t* __restrict__ offsets,
-    Rec<H, P>* __restrict__ out) {
+    RecOut<H, P> out) {
   __shared__ uint32_t s_cnt[PART_WAVES][256];
   __shared__ uint32_t s_delta[256];
   __shared__ uint32_t s_scratch[PART_WAVES + 1];
@@ -761,12 +808,10 @@ __global__ __launch_bounds__(PART_THREADS) __attribute__((amdgpu_waves_per_eu(4)
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   uint32_t run = threadIdx.x < n_digits ? offsets[threadIdx.x * s.n_tiles + tile] : 0u;
 
-  uint64_t* s_mask = reinterpret_cast<uint64_t*>(s_stage) + w * 256;  // ranking masks alias the staging area
 #pragma unroll 1
   for (uint32_t j = 0; j < n_sub; ++j) {
     if (j) __syncthreads();  // the previous tile's write-out has read s_stage
     clear_wave_counts(s_cnt[w]);
-    clear_wave_masks(s_mask);
     H keys[PART_ITEMS];
     P pays[PART_ITEMS];
     uint32_t dr[PART_ITEMS];  // digit << 24 | rank within the wave (rank < WAVE_SPAN)
@@ -777,7 +822,7 @@ __global__ __launch_bounds__(PART_THREADS) __attribute__((amdgpu_waves_per_eu(4)
     for (int k = 0; k < PART_ITEMS; ++k) {
       const bool a = (act >> k) & 1u;
       const uint32_t dig = a ? digit_of<H>(dg, keys[k]) : 0u;
-      dr[k] = (dig << 24) | wave_rank_lds(dig, a, s_mask, s_cnt[w]);
+      dr[k] = (dig << 24) | wave_rank_add(dig, a, s_cnt[w]);
       recs[k].key = keys[k];
       recs[k].payload = pays[k];
     }
@@ -799,17 +844,22 @@ __global__ __launch_bounds__(PART_THREADS) __attribute__((amdgpu_waves_per_eu(4)
 // Without a scan output (scan_out null: the caller wants the join output and the scan's counts only), part1_compact
 // writes the records of the rows taking part alone - after a selective prefilter a few percent of the scan's matches
 // (TPC-H 3's lineitem side: 6 of 323 M) - and the scan row of the histogram still counts every match.
-// Traffic per matched row is one 8-byte record more than the single fused scatter, but both kernels are plain
-// streams, while the single kernel's load -> rank -> stage -> store chain per tile left it latency-bound.
+// Traffic per matched row is one record more than the single fused scatter, but both kernels are plain streams,
+// while the single kernel's load -> rank -> stage -> store chain per tile left it latency-bound. The gapped records are
+// SoA and 6 bytes for 4-byte keys (round 5): the key, and the row as its 16-bit offset inside the span (spans hold at
+// most GAP_SPAN_MAX rows) with GAP_NULL marking a scan match that does not take part - against 8-byte {key, row}
+// records, 2 bytes less written and read back per match (0.55 + 0.55 GB per SF100 headline step).
 // ------------------------------------------------------------------------------------------------------------
 constexpr uint32_t NULL_FLAG = 0x80000000u;  // payloads of filtered sides are row indexes < 2^31
+constexpr uint32_t GAP_NULL = 0x8000u;       // gapped record of a scan match whose row does not take part
+constexpr uint32_t GAP_SPAN_MAX = 0x8000u;   // rows per span of a filtered side (offsets below GAP_NULL)
 
 // PF: the side has a probe-side prefilter (s.bloom). A separate instance: the prefilter's lookups hold registers
 // (151 VGPRs, 3 waves per SIMD, against 96 without them) that the headline's unprefiltered probe side does not need.
 template <typename SD, typename T, typename H, int LP, int FK, bool PF>
 __global__ __launch_bounds__(PART_THREADS) void part1_compact(Side s, Digit dg, uint32_t n_digits,
                                                              uint32_t* __restrict__ hist, uint32_t* __restrict__ span_count,
-                                                             Rec<H, uint32_t>* __restrict__ gap_out) {
+                                                             H* __restrict__ gap_keys, uint16_t* __restrict__ gap_offs) {
   __shared__ uint32_t s_hist[257];
   __shared__ uint32_t s_sc[WAVE + 2];
   const uint64_t tile = xcd_tile(blockIdx.x, gridDim.x);  // span
@@ -819,7 +869,8 @@ __global__ __launch_bounds__(PART_THREADS) void part1_compact(Side s, Digit dg, 
   const uint32_t base = static_cast<uint32_t>(tile - s.chunk_tile_begin[c]) * (s.sub * PART_TILE);
   const uint32_t n_sub = min(s.sub, (ch.size - base + PART_TILE - 1) / PART_TILE);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE), lane = __lane_id();
-  Rec<H, uint32_t>* out = gap_out + tile * (static_cast<uint64_t>(s.sub) * PART_TILE);
+  H* out_keys = gap_keys + tile * (static_cast<uint64_t>(s.sub) * PART_TILE);
+  uint16_t* out_offs = gap_offs + tile * (static_cast<uint64_t>(s.sub) * PART_TILE);
   const bool scan_records = s.scan_out != nullptr;  // records of every scan match, or of the rows taking part only
   uint32_t run = 0;
   if (threadIdx.x == 0) s_sc[WAVE + 1] = 0;  // scan matches of the span (without scan records)
@@ -860,10 +911,9 @@ __global__ __launch_bounds__(PART_THREADS) void part1_compact(Side s, Digit dg, 
     for (int k = 0; k < PART_ITEMS; ++k) {
       const uint64_t b = __ballot((m >> k) & 1u);
       if ((m >> k) & 1u) {
-        Rec<H, uint32_t> r;
-        r.key = keys[k];
-        r.payload = pays[k] | (((act >> k) & 1u) ? 0u : NULL_FLAG);
-        out[run + s_sc[w * PART_ITEMS + k] + static_cast<uint32_t>(__popcll(b & lanemask_lt()))] = r;
+        const uint32_t o = run + s_sc[w * PART_ITEMS + k] + static_cast<uint32_t>(__popcll(b & lanemask_lt()));
+        out_keys[o] = keys[k];
+        out_offs[o] = static_cast<uint16_t>((rb - base + k * WAVE + lane) | (((act >> k) & 1u) ? 0u : GAP_NULL));
       }
     }
     run += s_sc[WAVE];
@@ -880,8 +930,9 @@ template <typename SD, typename H>
 __global__ __launch_bounds__(PART_THREADS) void part1_spread(Side s, Digit dg, NextDigit nd, int dbits,
                                                             uint32_t n_digits, const uint32_t* __restrict__ offsets,
                                                             const uint32_t* __restrict__ span_count,
-                                                            const Rec<H, uint32_t>* __restrict__ gap_in,
-                                                            Rec<H, uint32_t>* __restrict__ out) {
+                                                            const H* __restrict__ gap_keys,
+                                                            const uint16_t* __restrict__ gap_offs,
+                                                            RecOut<H, uint32_t> out) {
   __shared__ uint32_t s_cnt[PART_WAVES][256];
   __shared__ uint32_t s_delta[256];
   __shared__ uint32_t s_scratch[PART_WAVES + 1];
@@ -889,37 +940,43 @@ __global__ __launch_bounds__(PART_THREADS) void part1_spread(Side s, Digit dg, N
   const uint64_t tile = xcd_tile(blockIdx.x, gridDim.x);  // span
   const uint32_t n = span_count[tile];
   const uint32_t c = s.tile_chunk[tile];
-  const uint32_t row0 = static_cast<uint32_t>(s.chunks[c].row_begin);  // payload -> chunk offset
-  const Rec<H, uint32_t>* in = gap_in + tile * (static_cast<uint64_t>(s.sub) * PART_TILE);
+  const uint32_t base = static_cast<uint32_t>(tile - s.chunk_tile_begin[c]) * (s.sub * PART_TILE);  // in the chunk
+  const uint32_t row0 = static_cast<uint32_t>(s.chunks[c].row_begin) + base;  // row of the span's first row
+  const H* in_keys = gap_keys + tile * (static_cast<uint64_t>(s.sub) * PART_TILE);
+  const uint16_t* in_offs = gap_offs + tile * (static_cast<uint64_t>(s.sub) * PART_TILE);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   uint32_t run = threadIdx.x < n_digits ? offsets[threadIdx.x * s.n_tiles + tile] : 0u;
   const uint32_t srun = offsets[n_digits * s.n_tiles + tile] - offsets[n_digits * s.n_tiles];
-  uint64_t* s_mask = reinterpret_cast<uint64_t*>(s_stage) + w * 256;  // ranking masks alias the staging area
   const uint32_t n_sub = (n + PART_TILE - 1) / PART_TILE;
 #pragma unroll 1
   for (uint32_t j = 0; j < n_sub; ++j) {
     if (j) __syncthreads();  // the previous tile's write-out has read s_stage
     clear_wave_counts(s_cnt[w]);
-    clear_wave_masks(s_mask);
     Rec<H, uint32_t> recs[PART_ITEMS];
     uint32_t dr[PART_ITEMS];
     uint32_t act = 0;
     const uint32_t r0 = j * PART_TILE + w * WAVE_SPAN + __lane_id();
+    uint32_t offs[PART_ITEMS];
 #pragma unroll
-    for (int k = 0; k < PART_ITEMS; ++k) recs[k] = in[min(r0 + k * WAVE, n - 1)];  // unconditional (see load_items)
+    for (int k = 0; k < PART_ITEMS; ++k) {  // unconditional (see load_items)
+      recs[k].key = in_keys[min(r0 + k * WAVE, n - 1)];
+      offs[k] = in_offs[min(r0 + k * WAVE, n - 1)];
+    }
 #pragma unroll
     for (int k = 0; k < PART_ITEMS; ++k) {
       const uint32_t i = r0 + k * WAVE;
+      const uint32_t off = offs[k] & (GAP_NULL - 1u);
+      recs[k].payload = row0 + off;
       if (i < n) {
-        if (s.scan_out != nullptr) s.scan_out[srun + i] = (recs[k].payload & ~NULL_FLAG) - row0;
-        if (!(recs[k].payload & NULL_FLAG)) act |= 1u << k;
+        if (s.scan_out != nullptr) s.scan_out[srun + i] = base + off;
+        if (!(offs[k] & GAP_NULL)) act |= 1u << k;
       }
     }
 #pragma unroll
     for (int k = 0; k < PART_ITEMS; ++k) {
       const bool a = (act >> k) & 1u;
       const uint32_t dig = a ? digit_of<H>(dg, recs[k].key) : 0u;
-      dr[k] = (dig << 24) | wave_rank_lds(dig, a, s_mask, s_cnt[w]);
+      dr[k] = (dig << 24) | wave_rank_add(dig, a, s_cnt[w]);
     }
     staged_scatter<H, uint32_t>(recs, act, dr, s_cnt, s_delta, s_stage, s_scratch, n_digits, dg, nd, run, out);
   }
@@ -1060,7 +1117,6 @@ __global__ __launch_bounds__(PART_THREADS) void part1_spread_mask(Side s, Digit 
     __syncthreads();  // s_wm / s_wa are rewritten by the next tile; s_comp complete after the last
   }
   // stable scatter of the compacted records by digit, one tile-sized round at a time
-  uint64_t* s_mask = reinterpret_cast<uint64_t*>(s_comp) + w * 256;  // ranking masks alias the front of s_comp
 #pragma unroll 1
   for (uint32_t r0 = 0; r0 < comp_n; r0 += PART_TILE) {
     if (r0) __syncthreads();  // the previous round's write-out has read the staging area
@@ -1075,15 +1131,313 @@ __global__ __launch_bounds__(PART_THREADS) void part1_spread_mask(Side s, Digit 
     }
     __syncthreads();  // every record of the round is in registers before the masks / staging overwrite the front
     clear_wave_counts(s_cnt[w]);
-    clear_wave_masks(s_mask);
     uint32_t dr[PART_ITEMS];
 #pragma unroll
     for (int k = 0; k < PART_ITEMS; ++k) {
       const bool aa = (act >> k) & 1u;
       const uint32_t dig = aa ? digit_of<H>(dg, recs[k].key) : 0u;
-      dr[k] = (dig << 24) | wave_rank_lds(dig, aa, s_mask, s_cnt[w]);
+      dr[k] = (dig << 24) | wave_rank_add(dig, aa, s_cnt[w]);
     }
     staged_scatter<H, uint32_t>(recs, act, dr, s_cnt, s_delta, s_comp, s_scratch, n_digits, dg, nd, run, out);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Pass 1 in row blocks sized for the Infinity Cache (the default for large sides; join_host.hpp block_plan): the
+// side's spans are cut into K contiguous blocks of ~100-200 MB of input each, and every block runs
+//   part1_count : the predicate (fused TableScan) and the join column of every row of the block's spans - digit
+//                 histogram of the rows taking part, plus the scan-match row - as part1_hist / part1_compact count;
+//   exclusive scan of the block's histogram (digit-major over its spans) and block_totals;
+//   part1_fill  : the same rows read AGAIN - served by the 256 MiB Infinity Cache, which still holds the block that
+//                 part1_count has just streamed (MI355X_MICROARCH.md "Infinity Cache": a table stays resident while it
+//                 plus the bytes moved in between fit; profiles/r05_mall_probe.jsonl: a re-read of 96-256 MB blocks
+//                 costs ~0.14 ms/GB less than from HBM, i.e. close to nothing) - writes the scan's output (chunk
+//                 offsets, row order) and the stable LDS-staged scatter of the records by the high digit.
+// Block k's records land in a region of its own, [row_base_k, row_base_k + records_k) (rows of the earlier blocks:
+// records <= rows), digit-major inside it, so no prefix across blocks is needed before a block's fill; the first
+// record pass then reads bucket d as the K runs (d, k) in block order - the interleaved-segment geometry of the
+// distributed receiver (block_geometry). Against part1_compact + part1_spread this drops the gapped record round trip
+// (write + re-read of 8 B per match) from HBM; against part1_hist + part1_scatter the second read of the column.
+// ------------------------------------------------------------------------------------------------------------
+// part1_count's loads for value chunks with 16-byte aligned data: lane l takes the 16 consecutive rows r0 .. r0 + 15
+// (r0 = wave span + 16 l) with 16-byte vector loads - a count does not care which lane holds which row - instead of 16
+// strided element loads per column. Rows past the chunk are masked out.
+template <typename T, typename H>
+__device__ __forceinline__ uint32_t load_keys_contig(const SrcChunk& ch, uint32_t r0, H (&keys)[PART_ITEMS]) {
+  static_assert(PART_ITEMS * sizeof(T) % 16 == 0, "whole vectors");
+  const T* data = static_cast<const T*>(ch.data);
+  if (r0 + PART_ITEMS <= ch.size) {
+    constexpr int NV = PART_ITEMS * sizeof(T) / 16;
+    uint4 u[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) u[j] = reinterpret_cast<const uint4*>(data + r0)[j];
+    T v[PART_ITEMS];
+    __builtin_memcpy(v, u, sizeof(v));
+#pragma unroll
+    for (int i = 0; i < PART_ITEMS; ++i) keys[i] = static_cast<H>(v[i]);
+    return 0xFFFFu;
+  }
+  uint32_t act = 0;
+#pragma unroll
+  for (int i = 0; i < PART_ITEMS; ++i) {
+    const uint32_t r = r0 + i;
+    keys[i] = static_cast<H>(data[min(r, ch.size - 1)]);
+    if (r < ch.size) act |= 1u << i;
+  }
+  return act;
+}
+
+template <typename E>
+__device__ __forceinline__ uint32_t filter_dict_contig(const hy_scan_chunk& f, uint32_t r0) {
+  static_assert(PART_ITEMS * sizeof(E) % 16 == 0, "whole vectors");
+  const E* data = static_cast<const E*>(f.column.data);
+  const uint32_t n = f.column.size;
+  E v[PART_ITEMS];
+  if (r0 + PART_ITEMS <= n) {
+    constexpr int NV = PART_ITEMS * sizeof(E) / 16;
+    uint4 u[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) u[j] = reinterpret_cast<const uint4*>(data + r0)[j];
+    __builtin_memcpy(v, u, sizeof(v));
+  } else {
+#pragma unroll
+    for (int i = 0; i < PART_ITEMS; ++i) v[i] = data[min(r0 + i, n - 1)];
+  }
+  const E null_vid = static_cast<E>(f.column.dictionary_size);
+  const E sv = static_cast<E>(f.search_vid);
+  const int op = f.op;
+  uint32_t m = 0;
+#pragma unroll
+  for (int i = 0; i < PART_ITEMS; ++i)
+    m |= static_cast<uint32_t>(r0 + i < n && v[i] != null_vid && cmp_op<E>(op, v[i], sv)) << i;
+  return m;
+}
+
+template <typename SD, typename T, typename H, int LP, int FK, bool PF>
+__global__ __launch_bounds__(PART_THREADS) void part1_count(Side s, Digit dg, uint32_t n_digits, uint64_t t0,
+                                                           uint32_t* __restrict__ hist) {
+  // value chunks with a dictionary (or no) predicate: the contiguous vector loads
+  constexpr bool CONTIG = LP == LP_VALUE && (FK == FK_NONE || FK == FK_DICT8 || FK == FK_DICT16 || FK == FK_DICT32);
+  __shared__ uint32_t s_hist[256];
+  __shared__ uint32_t s_sc;
+  const uint32_t nt = gridDim.x;
+  const uint32_t lt = xcd_tile(blockIdx.x, nt);
+  const uint64_t tile = t0 + lt;  // span
+  for (int i = threadIdx.x; i < 256; i += PART_THREADS) s_hist[i] = 0;
+  if (threadIdx.x == 0) s_sc = 0;
+  const uint32_t c = s.tile_chunk[tile];
+  const SrcChunk ch = s.chunks[c];
+  const uint32_t base = static_cast<uint32_t>(tile - s.chunk_tile_begin[c]) * (s.sub * PART_TILE);
+  const uint32_t n_sub = min(s.sub, (ch.size - base + PART_TILE - 1) / PART_TILE);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE), lane = __lane_id();
+  __syncthreads();
+  uint32_t nm = 0;  // this wave's scan matches (wave-uniform)
+#pragma unroll 1
+  for (uint32_t j = 0; j < n_sub; ++j) {
+    const uint32_t rb = base + j * PART_TILE + w * WAVE_SPAN;
+    uint32_t m_scan = 0xFFFFu;
+    H keys[PART_ITEMS];
+    uint32_t act;
+    bool contig = false;
+    if constexpr (CONTIG) {
+      const hy_scan_chunk* f = FK != FK_NONE ? &s.filter[c] : nullptr;
+      contig = (reinterpret_cast<uintptr_t>(ch.data) & 15u) == 0 &&
+               (FK == FK_NONE || f->op == HY_OP_NONE || f->column.size == 0 ||
+                (reinterpret_cast<uintptr_t>(f->column.data) & 15u) == 0);  // (uniform)
+      if (contig) {
+        const uint32_t r0 = rb + lane * PART_ITEMS;
+        if constexpr (FK != FK_NONE) {
+          if (f->op == HY_OP_NONE || f->column.size == 0)
+            m_scan = 0u;
+          else if constexpr (FK == FK_DICT8)
+            m_scan = filter_dict_contig<uint8_t>(*f, r0);
+          else if constexpr (FK == FK_DICT16)
+            m_scan = filter_dict_contig<uint16_t>(*f, r0);
+          else
+            m_scan = filter_dict_contig<uint32_t>(*f, r0);
+        }
+        act = load_keys_contig<T, H>(ch, r0, keys) & m_scan;
+      }
+    }
+    if (!contig) {
+      if constexpr (FK != FK_NONE) m_scan = filter_items<FK>(s, c, rb);
+      uint32_t pays[PART_ITEMS];
+      act = load_items<T, H, uint32_t, LP>(s, ch, rb, keys, pays) & m_scan;
+    }
+    if constexpr (PF) act = bloom_filter_act<H>(s, keys, act);
+#pragma unroll
+    for (int k = 0; k < PART_ITEMS; ++k)
+      if ((act >> k) & 1u) atomicAdd(&s_hist[digit_of<H>(dg, keys[k])], 1u);
+    if constexpr (FK != FK_NONE) {
+#pragma unroll
+      for (int k = 0; k < PART_ITEMS; ++k) nm += static_cast<uint32_t>(__popcll(__ballot((m_scan >> k) & 1u)));
+    }
+  }
+  if constexpr (FK != FK_NONE)
+    if (lane == 0 && nm) atomicAdd(&s_sc, nm);
+  __syncthreads();
+  for (uint32_t d = threadIdx.x; d < n_digits; d += PART_THREADS) hist[d * nt + lt] = s_hist[d];
+  if constexpr (FK != FK_NONE)
+    if (threadIdx.x == 0) hist[n_digits * nt + lt] = s_sc;
+}
+
+// rec_base: first record position of the block (its first row); scan_base: the scan matches of the earlier blocks
+// (device, set by block_totals). offsets: the block's exclusive histogram scan.
+template <typename SD, typename T, typename H, int LP, int FK, bool PF>
+__global__ __launch_bounds__(PART_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void part1_fill(
+    Side s, Digit dg, NextDigit nd, uint32_t n_digits, uint64_t t0, const uint32_t* __restrict__ offsets,
+    uint32_t rec_base, const uint64_t* __restrict__ scan_base, Rec<H, uint32_t>* __restrict__ out) {
+  __shared__ uint32_t s_cnt[PART_WAVES][256];
+  __shared__ uint32_t s_delta[256];
+  __shared__ uint32_t s_scratch[PART_WAVES + 1];
+  __shared__ uint32_t s_sc[WAVE + 1];
+  __shared__ Rec<H, uint32_t> s_stage[PART_TILE];
+  const uint32_t nt = gridDim.x;
+  const uint32_t lt = xcd_tile(blockIdx.x, nt);
+  const uint64_t tile = t0 + lt;  // span
+  const uint32_t c = s.tile_chunk[tile];
+  const SrcChunk ch = s.chunks[c];
+  const uint32_t base = static_cast<uint32_t>(tile - s.chunk_tile_begin[c]) * (s.sub * PART_TILE);
+  const uint32_t n_sub = min(s.sub, (ch.size - base + PART_TILE - 1) / PART_TILE);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE), lane = __lane_id();
+  uint32_t run = threadIdx.x < n_digits ? rec_base + offsets[threadIdx.x * nt + lt] : 0u;
+  uint32_t srun = 0;  // the span's first scan match (output position)
+  if constexpr (FK != FK_NONE)
+    srun = static_cast<uint32_t>(*scan_base) + offsets[n_digits * nt + lt] - offsets[n_digits * nt];
+#pragma unroll 1
+  for (uint32_t j = 0; j < n_sub; ++j) {
+    if (j) __syncthreads();  // the previous tile's write-out has read s_stage and s_sc
+    clear_wave_counts(s_cnt[w]);
+    const uint32_t rb = base + j * PART_TILE + w * WAVE_SPAN;
+    uint32_t m_scan = 0xFFFFu;
+    if constexpr (FK != FK_NONE) m_scan = filter_items<FK>(s, c, rb);
+    H keys[PART_ITEMS];
+    uint32_t pays[PART_ITEMS];
+    uint32_t act = load_items<T, H, uint32_t, LP>(s, ch, rb, keys, pays) & m_scan;
+    if constexpr (PF) act = bloom_filter_act<H>(s, keys, act);
+    const bool scan_out = FK != FK_NONE && s.scan_out != nullptr;
+    if (scan_out) {
+#pragma unroll
+      for (int k = 0; k < PART_ITEMS; ++k) {
+        const uint64_t b = __ballot((m_scan >> k) & 1u);
+        if (lane == 0) s_sc[w * PART_ITEMS + k] = static_cast<uint32_t>(__popcll(b));
+      }
+    }
+    Rec<H, uint32_t> recs[PART_ITEMS];
+    uint32_t dr[PART_ITEMS];  // digit << 24 | rank within the wave
+#pragma unroll
+    for (int k = 0; k < PART_ITEMS; ++k) {
+      const bool a = (act >> k) & 1u;
+      const uint32_t dig = a ? digit_of<H>(dg, keys[k]) : 0u;
+      dr[k] = (dig << 24) | wave_rank_add(dig, a, s_cnt[w]);
+      recs[k].key = keys[k];
+      recs[k].payload = pays[k];
+    }
+    if (scan_out) {  // the tile's scan matches in row order: (wave, item) ballot counts -> prefix -> lane rank
+      __syncthreads();
+      if (threadIdx.x < WAVE) {
+        const uint32_t v = s_sc[threadIdx.x];
+        const uint32_t incl = wave_inclusive_sum(v);
+        s_sc[threadIdx.x] = incl - v;
+        if (threadIdx.x == WAVE - 1) s_sc[WAVE] = incl;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < PART_ITEMS; ++k) {
+        const uint64_t b = __ballot((m_scan >> k) & 1u);
+        if ((m_scan >> k) & 1u)
+          s.scan_out[srun + s_sc[w * PART_ITEMS + k] + static_cast<uint32_t>(__popcll(b & lanemask_lt()))] =
+              rb + k * WAVE + lane;
+      }
+      srun += s_sc[WAVE];
+    }
+    staged_scatter<H, uint32_t>(recs, act, dr, s_cnt, s_delta, s_stage, s_scratch, n_digits, dg, nd, run, out);
+  }
+}
+
+// After block k's histogram scan (nt spans; records = the scan total, or for a fused scan the first entry of its
+// scan row): the block's per-digit runs for block_geometry, the scan matches of blocks <= k (scan_base[k + 1]) and
+// the scan's chunk begins of the chunks whose first span lies in this block, [c_lo, c_hi) (the last block also takes the
+// trailing span-less chunks and the end entry).
+static __global__ __launch_bounds__(256) void block_totals(const uint32_t* __restrict__ offsets, uint32_t nt,
+                                                           uint32_t n_digits, int filtered,
+                                                           const uint64_t* __restrict__ scan_total, uint32_t k,
+                                                           uint32_t rec_base, uint64_t t0, uint64_t n_tiles,
+                                                           int last_block, uint32_t* __restrict__ cls_begin,
+                                                           uint32_t* __restrict__ cls_count,
+                                                           uint64_t* __restrict__ scan_base,
+                                                           const uint64_t* __restrict__ chunk_tile_begin,
+                                                           uint32_t c_lo, uint32_t c_hi,
+                                                           uint64_t* __restrict__ chunk_begin) {
+  const uint64_t total = *scan_total;
+  const uint32_t records = filtered ? offsets[static_cast<uint64_t>(n_digits) * nt] : static_cast<uint32_t>(total);
+  for (uint32_t d = threadIdx.x; d < n_digits; d += blockDim.x) {
+    const uint32_t b = offsets[static_cast<uint64_t>(d) * nt];
+    const uint32_t e = d + 1 < n_digits ? offsets[static_cast<uint64_t>(d + 1) * nt] : records;
+    cls_begin[k * 256 + d] = rec_base + b;
+    cls_count[k * 256 + d] = e - b;
+  }
+  if (!filtered) return;
+  const uint64_t sb = scan_base[k];
+  if (threadIdx.x == 0) scan_base[k + 1] = sb + (total - records);
+  if (chunk_begin == nullptr) return;
+  const uint64_t row = static_cast<uint64_t>(n_digits) * nt;
+  for (uint32_t cc = c_lo + threadIdx.x; cc < c_hi; cc += blockDim.x) {  // (the host's range of such chunks)
+    const uint64_t t = chunk_tile_begin[cc];
+    if (t >= t0 && t < t0 + nt)
+      chunk_begin[cc] = sb + offsets[row + (t - t0)] - records;
+    else if (last_block && t >= n_tiles)
+      chunk_begin[cc] = sb + (total - records);
+  }
+}
+
+// Geometry of the record pass over the blocks' runs (one workgroup, thread g = pass-1 bucket g): bucket g's segments
+// are the runs (g, k), k = 0..K-1 in block order; their tiles of `span` records are interleaved in the histogram by
+// (bucket, digit, block, tile), as onepass_geometry lays out its classes, and the bucket's output starts at the records
+// of all earlier buckets. Writes the segment / group arrays, the tile prefix (n_groups * K + 1) and the record total.
+static __global__ __launch_bounds__(256) void block_geometry(const uint32_t* __restrict__ cls_begin,
+                                                             const uint32_t* __restrict__ cls_count, uint32_t n_blocks,
+                                                             uint32_t n_groups, uint32_t span, uint32_t next_digits,
+                                                             uint32_t* seg_begin, uint32_t* seg_end,
+                                                             uint32_t* seg_stride, uint32_t* seg_toff,
+                                                             uint64_t* seg_hbase, uint64_t* seg_tile_begin,
+                                                             uint64_t* group_hbase, uint32_t* group_tiles,
+                                                             uint32_t* group_out, uint64_t* total) {
+  __shared__ uint32_t s_scratch[256 / WAVE + 1];
+  const uint32_t g = threadIdx.x;
+  uint32_t gt = 0, gc = 0;
+  if (g < n_groups) {
+    for (uint32_t k = 0; k < n_blocks; ++k) {
+      const uint32_t n = cls_count[k * 256 + g];
+      gt += (n + span - 1) / span;
+      gc += n;
+    }
+  }
+  uint32_t tiles_total, rows_total;
+  const uint32_t tile_base = block_exclusive_sum<256>(gt, s_scratch, &tiles_total);
+  const uint32_t out_base = block_exclusive_sum<256>(gc, s_scratch, &rows_total);
+  if (g < n_groups) {
+    const uint64_t hb = static_cast<uint64_t>(tile_base) * next_digits;
+    uint32_t toff = 0;
+    for (uint32_t k = 0; k < n_blocks; ++k) {
+      const uint32_t q = g * n_blocks + k;
+      const uint32_t n = cls_count[k * 256 + g];
+      const uint32_t b0 = cls_begin[k * 256 + g];
+      seg_begin[q] = b0;
+      seg_end[q] = b0 + n;
+      seg_stride[q] = gt;
+      seg_toff[q] = toff;
+      seg_hbase[q] = hb;
+      seg_tile_begin[q] = tile_base + toff;
+      toff += (n + span - 1) / span;
+    }
+    group_hbase[g] = hb;
+    group_tiles[g] = gt;
+    group_out[g] = out_base;
+  }
+  if (g == 0) {
+    seg_tile_begin[n_groups * n_blocks] = tiles_total;
+    *total = rows_total;
   }
 }
 
@@ -1148,9 +1502,7 @@ __global__ __launch_bounds__(PART_THREADS) void part1_onepass(Side s, Digit dg, 
   const SrcChunk ch = s.chunks[c];
   const uint32_t base = static_cast<uint32_t>(tile - s.chunk_tile_begin[c]) * PART_TILE;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE), lane = __lane_id();
-  uint64_t* s_mask = reinterpret_cast<uint64_t*>(s_stage) + w * 256;  // ranking masks alias the staging area
   clear_wave_counts(s_cnt[w]);
-  clear_wave_masks(s_mask);
   const uint32_t rb = base + w * WAVE_SPAN;
   uint32_t m = 0xFFFFu;
   if constexpr (FK != FK_NONE) {
@@ -1175,7 +1527,7 @@ __global__ __launch_bounds__(PART_THREADS) void part1_onepass(Side s, Digit dg, 
   for (int k = 0; k < PART_ITEMS; ++k) {
     const bool a = (act >> k) & 1u;
     const uint32_t dig = a ? digit_of<H>(dg, keys[k]) : 0u;
-    dr[k] = (dig << 24) | wave_rank_lds(dig, a, s_mask, s_cnt[w]);
+    dr[k] = (dig << 24) | wave_rank_add(dig, a, s_cnt[w]);
     recs[k].key = keys[k];
     recs[k].payload = pays[k];
   }
@@ -1424,12 +1776,10 @@ __global__ __launch_bounds__(PART_THREADS) void part2_scatter(Segs sg, Digit dg,
   const uint32_t sb = b0 + t_in * (sg.sub * PART_TILE);
   const uint32_t n_sub = min(sg.sub, (b1 - sb + PART_TILE - 1) / PART_TILE);
   uint32_t run = threadIdx.x < n_digits ? offsets[hbase + threadIdx.x * stride + toff + t_in] : 0u;
-  uint64_t* s_mask = reinterpret_cast<uint64_t*>(s_stage) + w * 256;  // ranking masks alias the staging area
 #pragma unroll 1
   for (uint32_t j = 0; j < n_sub; ++j) {
     if (j) __syncthreads();  // the previous tile's write-out has read s_stage
     clear_wave_counts(s_cnt[w]);
-    clear_wave_masks(s_mask);
     Rec<H, P> recs[PART_ITEMS];
     uint32_t dr[PART_ITEMS];  // digit << 24 | rank within the wave
     uint32_t act = 0;
@@ -1443,7 +1793,7 @@ __global__ __launch_bounds__(PART_THREADS) void part2_scatter(Segs sg, Digit dg,
     for (int k = 0; k < PART_ITEMS; ++k) {
       const bool a = (act >> k) & 1u;
       const uint32_t dig = a ? digit_of<H>(dg, recs[k].key) : 0u;
-      dr[k] = (dig << 24) | wave_rank_lds(dig, a, s_mask, s_cnt[w]);
+      dr[k] = (dig << 24) | wave_rank_add(dig, a, s_cnt[w]);
     }
     staged_scatter<H, P>(recs, act, dr, s_cnt, s_delta, s_stage, s_scratch, n_digits, dg, nd, run, out);
   }
@@ -1466,18 +1816,24 @@ __global__ __launch_bounds__(PART_THREADS) void part2_hist_bytes(Segs sg, uint32
   uint32_t b0, b1, stride, toff;
   uint64_t hbase;
   seg_geometry(sg, sgi, n_digits, &b0, &b1, &hbase, &stride, &toff);
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   const uint32_t sb = b0 + t_in * (sg.sub * PART_TILE);
   const uint32_t n_sub = min(sg.sub, (b1 - sb + PART_TILE - 1) / PART_TILE);
+  // the tile's bytes [lo, hi) as 16-byte vectors from the aligned address below lo (the digit arrays are 256-byte
+  // aligned and padded): one load per thread instead of 16 byte loads per lane
 #pragma unroll 1
   for (uint32_t j = 0; j < n_sub; ++j) {
-    const uint32_t r0 = sb + j * PART_TILE + w * WAVE_SPAN + __lane_id();
-    uint32_t d[PART_ITEMS];
+    const uint32_t lo = sb + j * PART_TILE, hi = min(lo + PART_TILE, b1), a0 = lo & ~15u;
+    const uint32_t nv = (hi - a0 + 15) / 16;
+    for (uint32_t v = threadIdx.x; v < nv; v += PART_THREADS) {
+      const uint4 u = reinterpret_cast<const uint4*>(dig + a0)[v];
+      const uint32_t words[4] = {u.x, u.y, u.z, u.w};
+      const uint32_t p0 = a0 + v * 16;
 #pragma unroll
-    for (int k = 0; k < PART_ITEMS; ++k) d[k] = dig[min(r0 + k * WAVE, b1 - 1)];
-#pragma unroll
-    for (int k = 0; k < PART_ITEMS; ++k)
-      if (r0 + k * WAVE < b1) atomicAdd(&s_hist[d[k]], 1u);
+      for (int i = 0; i < 16; ++i) {
+        const uint32_t p = p0 + i;
+        if (p >= lo && p < hi) atomicAdd(&s_hist[(words[i >> 2] >> (8 * (i & 3))) & 0xFFu], 1u);
+      }
+    }
   }
   __syncthreads();
   for (uint32_t d = threadIdx.x; d < n_digits; d += PART_THREADS) hist[hbase + d * stride + toff + t_in] = s_hist[d];
@@ -1562,15 +1918,19 @@ constexpr int SCAN_BLOCK = SCAN_T * SCAN_PER;
 // Lane t of the workgroup holds the four 4-element groups at (k * SCAN_T + t) * 4, k = 0..3: every load and store
 // instruction of a wave then moves 1 KB of consecutive words (16 B per lane). The block's prefix runs over the
 // groups in (k, t) order - four workgroup scans - followed by the decoupled look-back across blocks.
+// n_dev (optional): the length is min(n, *n_dev * n_mul), read on the device - a record pass's histogram covers the
+// tiles that exist (seg_tile_begin's last entry), while the host sizes the grid for the upper bound.
 template <bool VEC>
 __global__ __launch_bounds__(SCAN_T) void exclusive_scan_u32(const uint32_t* __restrict__ in,
                                                              uint32_t* __restrict__ out, uint64_t n,
                                                              uint64_t* __restrict__ status, uint32_t* ticket,
-                                                             uint32_t* error, uint64_t* total_out) {
+                                                             uint32_t* error, uint64_t* total_out,
+                                                             const uint64_t* __restrict__ n_dev, uint32_t n_mul) {
   static_assert(SCAN_PER == 16, "four groups of four per lane");
   __shared__ uint32_t s_scratch[SCAN_T / WAVE + 1];
   __shared__ uint64_t s_tile;
   __shared__ uint64_t s_prefix;
+  if (n_dev != nullptr) n = min(n, *n_dev * n_mul);
   if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
   __syncthreads();
   const uint64_t tile = s_tile;

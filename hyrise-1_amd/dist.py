@@ -32,6 +32,81 @@ def owned_buckets(n_buckets, rank, world):
     return rank * n_buckets // world, (rank + 1) * n_buckets // world
 
 
+def murmur2_int32_torch(keys, seed=17):
+    """MurmurHash2 of 4-byte keys on torch tensors (murmur_hash.cpp:21-75 for len = 4; the numpy twin is pinned by
+    tests/test_murmur_golden.py). 32-bit arithmetic in int64 lanes."""
+    import torch
+
+    M, m = 0xFFFFFFFF, 0x5BD1E995
+    k = keys.to(torch.int64) & M
+    k = (k * m) & M
+    k = k ^ (k >> 24)
+    k = (k * m) & M
+    h = torch.full_like(k, ((seed ^ 4) * m) & M)
+    h = h ^ k
+    h = h ^ (h >> 13)
+    h = (h * m) & M
+    return h ^ (h >> 15)
+
+
+def partition_sums(partitions, probe_rows, build_rows, n_parts):
+    """Per partition: (pairs, sum of probe rows, sum of build rows) as int64 tensors of n_parts entries."""
+    import torch
+
+    dev = partitions.device
+    out = [torch.zeros(n_parts, dtype=torch.int64, device=dev) for _ in range(3)]
+    out[0].index_add_(0, partitions, torch.ones_like(partitions))
+    out[1].index_add_(0, partitions, probe_rows)
+    out[2].index_add_(0, partitions, build_rows)
+    return out
+
+
+def headline_expected(dist, lkey, match, l_row_base, radix_bits, seed=17):
+    """The single-GPU layout of the headline join over the whole (sharded) database: per global partition the pairs,
+    the sum of their probe rows and of their build rows, from this rank's shard (its scan matches: l_orderkey of
+    every matching lineitem row meets exactly one order, whose row follows from the dbgen sparse key
+    ((i >> 3) << 5) + (i & 7), i = row + 1) summed over the ranks. Only the join's definition enters: murmur2 seed 17
+    partitions (join_hash.cpp:253) and the reference's output order is checked separately (probe rows ascending)."""
+    import torch
+
+    idx = torch.nonzero(match, as_tuple=True)[0]
+    keys = lkey[idx].to(torch.int64)
+    parts = murmur2_int32_torch(keys, seed) & ((1 << radix_bits) - 1)
+    orow = (((keys >> 5) << 3) + (keys & 7)) - 1
+    sums = partition_sums(parts, idx.to(torch.int64) + l_row_base, orow, 1 << radix_bits)
+    for t in sums:
+        dist.all_reduce(t)
+    return sums
+
+
+def check_partition_output(expected, out_b, out_p, part_begin, part_count, first_part, chunk):
+    """This rank's join output (its owned partitions [first_part, first_part + n)) against headline_expected: pairs,
+    probe / build row sums per partition, and probe rows strictly ascending inside every partition (the reference's
+    probe order). RowIDs name global chunks of `chunk` rows. Returns a dict of the checks (all True = ok)."""
+    import torch
+
+    n = part_count.numel()
+    counts = part_count.to(torch.int64)
+    total = int(counts.sum())
+    dev = counts.device
+    pid = torch.repeat_interleave(torch.arange(n, device=dev), counts)
+    excl = torch.cumsum(counts, 0) - counts
+    pos = torch.repeat_interleave(part_begin.to(torch.int64), counts) + (
+        torch.arange(total, device=dev) - torch.repeat_interleave(excl, counts))
+    p = out_p.view(torch.int32).view(-1, 2)[pos].to(torch.int64)
+    b = out_b.view(torch.int32).view(-1, 2)[pos].to(torch.int64)
+    prow, brow = p[:, 0] * chunk + p[:, 1], b[:, 0] * chunk + b[:, 1]
+    got = partition_sums(pid, prow, brow, n)
+    want = [t[first_part:first_part + n] for t in expected]
+    same_part = pid[1:] == pid[:-1]
+    return {
+        "pair_counts": bool(torch.equal(got[0], want[0])),
+        "probe_row_sums": bool(torch.equal(got[1], want[1])),
+        "build_row_sums": bool(torch.equal(got[2], want[2])),
+        "probe_ascending_within_partitions": bool(((prow[1:] > prow[:-1]) | ~same_part).all()),
+    }
+
+
 def exchange_plan(all_counts, rank, world):
     """all_counts[s][b] = rows of bucket b on sender s (every rank's counts, from all_gather).
     Returns (send_rows[d], recv_rows[s], recv_matrix[s][j]) for this rank: rows sent to each destination rank, rows

@@ -799,6 +799,11 @@ hy_status hy_aggregate_merge(const hy_agg_params* params, const hy_agg_layout* l
                              const uint64_t* part_groups, const uint64_t* part_row_base, uint32_t n_parts,
                              uint64_t* out, uint64_t out_capacity, uint64_t* n_out);
 hy_status hy_agg_float_sum(const uint64_t* limbs, uint32_t n_limbs, int32_t emin, uint64_t special, double* out);
+/* hy_agg_float_sum over n_records HOST group records of `words` words each: out[g] = the float SUM of the aggregate
+ * whose words start at sum_word of record g (its non-finite flags at sum_word + 1, n_limbs limbs from sum_word + 2).
+ * The host side of reading a large GROUP BY result back (TPC-H 3's 1.1 M groups at SF100). */
+hy_status hy_agg_float_sums(const uint64_t* records, uint64_t n_records, uint32_t words, uint32_t sum_word,
+                            uint32_t n_limbs, int32_t emin, double* out);
 uint64_t hy_agg_decode_ordered(uint64_t ordered, int32_t value_type);
 
 #ifdef __cplusplus

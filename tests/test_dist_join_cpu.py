@@ -67,16 +67,50 @@ def _worker(rank, world, port, out_dir):
         bkeys, brows = sides["build"]
         pkeys, prows = sides["probe"]
         bpart, ppart = _partitions(oracle, bkeys, bits), _partitions(oracle, pkeys, bits)
-        out = []
+        out, per_part = [], []
         for p in range(lo << (bits - w0), hi << (bits - w0)):
             bsel = np.nonzero(bpart == p)[0]  # received order: sender (= global row) order
             table = {}
             for i in bsel:
                 table.setdefault(int(bkeys[i]), []).append(int(brows[i]))
             pairs = [(b, int(prows[i])) for i in np.nonzero(ppart == p)[0] for b in table.get(int(pkeys[i]), [])]
+            per_part.append(np.array(pairs, dtype=np.int64).reshape(-1, 2))
             if pairs:
-                out.append(np.array(pairs, dtype=np.int64))
+                out.append(per_part[-1])
         np.savez(os.path.join(out_dir, f"r{rank}.npz"), *out)
+        # the bench's per-rank output check (dist.headline_expected / check_partition_output) on this layout, laid out
+        # as the device writes it (RowID pairs, partitions placed in an arbitrary order: here reversed), then corrupted
+        expected = hd.headline_expected(dist, sh["l_orderkey"], sh["l_quantity"] < 24, sh["l_row_base"], bits)
+
+        def device_layout(parts):
+            counts = np.array([len(x) for x in parts], dtype=np.int64)
+            begin = np.zeros(len(parts), dtype=np.int64)
+            at = 0
+            for i in reversed(range(len(parts))):
+                begin[i] = at
+                at += counts[i]
+            rid = np.zeros((2, max(1, at), 2), dtype=np.int32)
+            for i, x in enumerate(parts):
+                for col in (0, 1):
+                    rid[col, begin[i]:begin[i] + counts[i], 0] = x[:, col] // CHUNK
+                    rid[col, begin[i]:begin[i] + counts[i], 1] = x[:, col] % CHUNK
+            return (torch.from_numpy(rid[0]), torch.from_numpy(rid[1]), torch.from_numpy(begin),
+                    torch.from_numpy(counts.astype(np.int32)))
+
+        first_part = lo << (bits - w0)
+        checks = {"ok": hd.check_partition_output(expected, *device_layout(per_part), first_part, CHUNK)}
+        big = [i for i, x in enumerate(per_part) if len(x) >= 2]
+        if len(big) >= 2:
+            moved = [x.copy() for x in per_part]
+            moved[big[0]][0, 0], moved[big[1]][0, 0] = per_part[big[1]][0, 0], per_part[big[0]][0, 0]
+            checks["build_swapped"] = hd.check_partition_output(expected, *device_layout(moved), first_part, CHUNK)
+            flipped = [x.copy() for x in per_part]
+            flipped[big[0]] = flipped[big[0]][::-1].copy()
+            checks["probe_reversed"] = hd.check_partition_output(expected, *device_layout(flipped), first_part, CHUNK)
+        import json
+
+        with open(os.path.join(out_dir, f"check{rank}.json"), "w") as f:
+            json.dump(checks, f)
     finally:
         dist.destroy_process_group()
 
@@ -106,3 +140,13 @@ def test_distributed_scan_join_equals_single_node(tmp_path, world):
         b, p = ch.get_column(0).pos_list().astype(np.int64), ch.get_column(1).pos_list().astype(np.int64)
         assert np.array_equal(b[:, 0] * CHUNK + b[:, 1], pairs[:, 0]), f"output chunk {k}: build RowIDs"
         assert np.array_equal(p[:, 0] * CHUNK + p[:, 1], pairs[:, 1]), f"output chunk {k}: probe RowIDs"
+    # the distributed bench's per-rank output check: passes on the right layout, catches moved and reordered pairs
+    import json
+
+    for r in range(world):
+        checks = json.load(open(tmp_path / f"check{r}.json"))
+        assert all(checks["ok"].values()), checks["ok"]
+        if "build_swapped" in checks:
+            assert not checks["build_swapped"]["build_row_sums"]
+            assert not checks["probe_reversed"]["probe_ascending_within_partitions"]
+            assert checks["probe_reversed"]["probe_row_sums"]  # (the same rows, in the wrong order)

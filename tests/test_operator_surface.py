@@ -156,3 +156,26 @@ def test_aborted_transaction_leaves_output_unset(hy):
     downstream = hy.TableScan(scan, 0, hy.PredicateCondition.Equals, 1)
     with pytest.raises(RuntimeError, match="Left input has not been executed"):
         downstream.execute()
+
+
+def test_descriptions_and_layering(hy):
+    """description(DescriptionMode) of TableScan (table_scan.cpp:51-61) and of every join (AbstractJoinOperator,
+    abstract_join_operator.cpp:30-43): executed inputs lend their column names (else "Col #i"), the predicate and the
+    parameter follow; MultiLine breaks after the name. JoinHash keeps AbstractJoinOperator's mode / column ids /
+    predicate accessors (join_hash.hpp:24, abstract_join_operator.hpp:34-37)."""
+    w = int_int(hy)
+    a, b = w.get_output().column_names()
+    lt, ge, eq = hy.PredicateCondition.LessThan, hy.PredicateCondition.GreaterThanEquals, hy.PredicateCondition.Equals
+    scan = hy.TableScan(w, 1, lt, 24)
+    assert scan.description() == f"TableScan ({b} < 24)"
+    assert scan.description(hy.DescriptionMode.MultiLine) == f"TableScan\n({b} < 24)"
+    assert hy.TableScan(w, 0, ge, hy.ParameterID(3)).description() == f"TableScan ({a} >= Placeholder #3)"
+    assert hy.TableScan(w, 0, lt, hy.ColumnParameter(1)).description() == f"TableScan ({a} < Col #1)"
+    assert hy.TableScan(w, 0, lt, ("float", 2.5)).description() == f"TableScan ({a} < 2.5)"
+    join = hy.JoinHash(w, scan, hy.JoinMode.Inner, (0, 1), eq)  # the scan has not run: its column by index
+    assert join.description() == f"JoinHash (Inner Join where {a} = Col #1)"
+    assert join.description(hy.DescriptionMode.MultiLine) == f"JoinHash\n(Inner Join where {a} = Col #1)"
+    assert hy.JoinHash(w, w, hy.JoinMode.Semi, (1, 0), eq).description() == f"JoinHash (Semi Join where {b} = {a})"
+    assert join.mode() == hy.JoinMode.Inner and join.column_ids() == (0, 1) and join.predicate_condition() == eq
+    with pytest.raises(Exception):
+        hy.JoinHash(w, w, hy.JoinMode.Cross, (0, 0), eq)  # abstract_join_operator.cpp:16-17

@@ -128,6 +128,42 @@ def test_concurrent_operators(hy, oracle):
         check_plan(hy, oracle, fact, dim, threshold, scan, join, agg)
 
 
+@pytest.mark.parametrize("scheduler", ["pool", "inline"])
+def test_operators_under_a_job_scheduler(hy, oracle, scheduler):
+    """JoinHash's output chunk builders as jobs of a registered host scheduler (scheduler.hpp; join_hash.cpp:139-182
+    waits for its JobTasks in CurrentScheduler::wait_for_tasks): a 3-worker pool shared by 4 threads that run
+    TableScan -> JoinHash -> Aggregate concurrently (more jobs than workers: every thread's builders queue behind the
+    others'), and the inline scheduler (jobs run as they are scheduled). HY_OP_PARTS_PER_JOB=64 (set for the whole
+    session by conftest) splits even these small joins into several jobs. Every output equals the oracle's."""
+    hy.set_job_scheduler(scheduler, 3)
+    try:
+        private = []
+        for t in range(4):
+            fact, dim = fact_dim(hy, 40 + t)
+            private.append((fact, dim, wrap(hy, fact), wrap(hy, dim)))
+        start = threading.Barrier(4)
+
+        def worker(t):
+            start.wait()
+            done = []
+            for it in range(3):
+                fact, dim, f, d = private[t]
+                threshold = 9 + 5 * t + it
+                ops = plan(hy, f, d, threshold)
+                for op in ops:
+                    op.execute()
+                done.append((fact, dim, threshold, ops))
+            return done
+
+        with ThreadPoolExecutor(4) as pool:
+            results = [r for fut in [pool.submit(worker, t) for t in range(4)] for r in fut.result()]
+        hy.synchronize()
+        for fact, dim, threshold, (scan, join, agg) in results:
+            check_plan(hy, oracle, fact, dim, threshold, scan, join, agg)
+    finally:
+        hy.set_job_scheduler(None)
+
+
 def test_concurrent_pos_list_reads(hy, oracle):
     """Host reads of one lazy output PosList from several threads at once copy it down once and all see the same
     RowIDs (PosList::host per-list fetch, types.hpp)."""

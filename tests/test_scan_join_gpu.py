@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 import device_tables as dt
+from helpers import wrap
 
 pytestmark = pytest.mark.gpu
 
@@ -193,13 +194,17 @@ def test_scan_join_empty_and_all_none(hy, oracle):
 @pytest.mark.parametrize("bits", [12, 16, 20])
 @pytest.mark.parametrize("mode", ["Inner", "Left", "Semi"])
 @pytest.mark.parametrize("key_enc,filtered", [("Unencoded", True), ("Dictionary", True), ("Unencoded", False)])
-@pytest.mark.parametrize("onepass,cap", [(False, None), (True, None), (True, "64")])
+@pytest.mark.parametrize("onepass,cap", [(False, None), (True, None), (True, "64"), ("blocked", None)])
 def test_multi_digit_plans(hy, oracle, monkeypatch, bits, mode, key_enc, filtered, onepass, cap):
     """Radix plans of two and three digits through the default two-read first pass, the opt-in single-pass first
     radix pass (HY_ONEPASS=1, part1_onepass: gapped per-class bucket regions, look-back per digit) and, with
-    HY_ONEPASS_CAP=64, its overflow fallback: scan output and every partition's PosLists equal the oracle's at the
-    same radix bits (the reference constructor's radix_bits, join_hash.hpp:28)."""
-    if onepass:
+    HY_ONEPASS_CAP=64, its overflow fallback, and the opt-in pass 0 in Infinity-Cache row blocks (HY_BLOCKED=1,
+    part1_count / part1_fill; 7,000-row blocks, so every side has several): scan output and every partition's
+    PosLists equal the oracle's at the same radix bits (the reference constructor's radix_bits, join_hash.hpp:28)."""
+    if onepass == "blocked":
+        monkeypatch.setenv("HY_BLOCKED", "1")
+        monkeypatch.setenv("HY_BLOCK_ROWS", "7000")
+    elif onepass:
         monkeypatch.setenv("HY_ONEPASS", "1")
     if cap is not None:
         monkeypatch.setenv("HY_ONEPASS_CAP", cap)
@@ -343,6 +348,56 @@ def test_prepared_plan_graph_replay(hy):
     try:
         for run in range(6):
             ob, op, pbeg, pcnt = bufs[0 if run < 4 else 1]
+            res = capi.JoinResult()
+            capi.check(L.hy_scan_join_plan_execute(plan, ob.ptr, op.ptr, cap, pbeg.ptr, pcnt.ptr, ctypes.byref(res),
+                                                   stream), "execute")
+            capi.check(L.hy_stream_synchronize(stream), "sync")
+            b, p = ob.fetch().reshape(-1, 2), op.fetch().reshape(-1, 2)
+            got = [(b[x:x + c], p[x:x + c]) for x, c in zip(pbeg.fetch().astype(np.int64), pcnt.fetch().astype(np.int64))]
+            assert res.total_pairs == sum(len(x) for _, x in want)
+            for (gb, gp), (wb, wp) in zip(got, want):
+                assert np.array_equal(gb, wb) and np.array_equal(gp, wp), f"execution {run}"
+    finally:
+        L.hy_scan_join_plan_destroy(plan)
+        L.hy_stream_destroy(stream)
+
+
+def test_prepared_plan_replay_after_ring_wrap(hy, monkeypatch):
+    """A captured plan replays from its own workspace, never from the per-thread pinned staging ring (ADVICE r04,
+    VERDICT r04 item 2): after the graph is captured, a string TableScan on the same thread stages a 17 MiB constant -
+    the ring wraps and is reallocated - and the replays still equal the call. The plan also keeps the knobs it was
+    created with: HY_HASH_RECORDS flipped after creation changes neither its layout nor its output."""
+    capi, L = hy.capi, hy.capi.lib
+    rng = np.random.default_rng(0x57524150)
+    okey, ostatus, lkey, lkey_nulls, qty, qty_nulls = orders_lineitem(rng, 20_000, False)
+    lk = dt.DeviceColumn(capi, lkey, None, 5_000, "Unencoded")
+    lq = dt.DeviceColumn(capi, qty, qty_nulls, 5_000, "Dictionary")
+    ok = dt.DeviceColumn(capi, okey, None, 4_000, "Unencoded")
+    lf = Filter(capi, lq, "LessThan", 30.0)
+    params = capi.JoinParams(0, capi.HY_TYPE_INT32, 16, 17)  # >= 16 bits: 6-byte hash records in the last pass
+    o_side, l_side = dt.join_side(capi, ok), dt.join_side(capi, lk)
+    cap = okey.size * 3 + lkey.size + 16
+    want = run_fused(hy, o_side, None, l_side, lf.f, params, cap)
+    stream = ctypes.c_void_p()
+    capi.check(L.hy_stream_create(ctypes.byref(stream)), "hy_stream_create")
+    plan = ctypes.c_void_p()
+    capi.check(L.hy_scan_join_plan_create(ctypes.byref(o_side), None, ctypes.byref(l_side), ctypes.byref(lf.f),
+                                          ctypes.byref(params), ctypes.byref(plan)), "plan")
+    n_parts = 1 << params.radix_bits
+    ob, op = capi.DeviceArray(np.zeros(cap * 2, np.uint32)), capi.DeviceArray(np.zeros(cap * 2, np.uint32))
+    pbeg, pcnt = capi.DeviceArray(np.zeros(n_parts, np.uint64)), capi.DeviceArray(np.zeros(n_parts, np.uint32))
+    strings = hy.Table([("s", hy.DataType.String, False)], hy.TableType.Data, 64)
+    for i in range(100):
+        strings.append([f"s{i}"])
+    try:
+        for run in range(8):
+            if run == 4:  # graph captured at execution 2 and replayed since: wrap the ring on this thread
+                scan = hy.TableScan(wrap(hy, strings), 0, hy.PredicateCondition.Equals, "x" * (17 << 20))
+                scan.execute()
+                assert scan.get_output().row_count() == 0
+            if run == 6:
+                monkeypatch.setenv("HY_HASH_RECORDS", "0")
+            capi.check(L.hy_memcpy_htod(ob.ptr, np.zeros(cap * 2, np.uint32).ctypes.data, cap * 8, None), "clear")
             res = capi.JoinResult()
             capi.check(L.hy_scan_join_plan_execute(plan, ob.ptr, op.ptr, cap, pbeg.ptr, pcnt.ptr, ctypes.byref(res),
                                                    stream), "execute")
