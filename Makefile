@@ -32,7 +32,8 @@ $(LIB)/hyrise_amd.o: $(CSRC)/capi/hyrise_amd.hip $(CSRC)/kernels/scan.hip $(CSRC
 
 $(LIB)/hyrise_amd_aggregate.o: $(CSRC)/capi/hyrise_amd_aggregate.hip $(CSRC)/kernels/aggregate.hip $(CSRC)/kernels/projection.hip \
                                 $(CSRC)/kernels/aggregate_fused.hip $(CSRC)/kernels/aggregate_lanes.hip \
-                                $(CSRC)/kernels/aggregate_vec.hip $(CSRC)/kernels/aggregate_stream.hip $(CAPI_HDR)
+                                $(CSRC)/kernels/aggregate_vec.hip $(CSRC)/kernels/aggregate_stream.hip $(CAPI_HDR) \
+                                $(CSRC)/capi/agg_jit.hpp $(CSRC)/kernels/agg_jit_prelude.hpp
 	@mkdir -p $(LIB)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
@@ -42,6 +43,15 @@ JOIN_OBJS  := $(patsubst %,$(LIB)/hyrise_amd_%.o,$(JOIN_TUS))
 $(JOIN_OBJS): $(LIB)/hyrise_amd_%.o: $(CSRC)/capi/hyrise_amd_%.hip $(CSRC)/capi/join_host.hpp $(CSRC)/kernels/join.hip $(CAPI_HDR)
 	@mkdir -p $(LIB)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+# plan-compiled aggregation: host code (hiprtc) with the device prelude embedded as text
+$(LIB)/agg_jit_prelude.inc: $(CSRC)/kernels/agg_jit_prelude.hpp tools/embed_text.py
+	@mkdir -p $(LIB)
+	$(PY) tools/embed_text.py kJitPrelude $< > $@
+
+$(LIB)/hyrise_amd_agg_jit.o: $(CSRC)/capi/hyrise_amd_agg_jit.cpp $(CSRC)/capi/agg_jit.hpp $(CSRC)/kernels/agg_jit_prelude.hpp \
+                             $(LIB)/agg_jit_prelude.inc include/hyrise_amd.h
+	$(HIPCC) --offload-arch=$(ARCH) -std=c++17 -O2 -fPIC -Iinclude -I$(LIB) -c -o $@ $<
 
 $(LIB)/hyrise_amd_order.o: $(CSRC)/capi/hyrise_amd_order.hip $(CAPI_HDR)
 	@mkdir -p $(LIB)
@@ -70,8 +80,8 @@ $(LIB)/hyrise_amd_string.o: $(CSRC)/capi/hyrise_amd_string.hip $(CAPI_HDR)
 $(LIB)/libhyrise_amd.so: $(LIB)/hyrise_amd.o $(LIB)/hyrise_amd_aggregate.o $(LIB)/hyrise_amd_order.o \
                          $(LIB)/hyrise_amd_comm.o $(LIB)/hyrise_amd_compare.o \
                          $(LIB)/hyrise_amd_validate.o $(LIB)/hyrise_amd_decode.o $(LIB)/hyrise_amd_string.o \
-                         $(JOIN_OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+                         $(LIB)/hyrise_amd_agg_jit.o $(JOIN_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -L/opt/rocm/lib -lrccl -lhiprtc -Wl,-rpath,/opt/rocm/lib
 
 $(LIB)/libhyrise_host.so: $(HOST_SRC) $(HOST_HDR) $(LIB)/libhyrise_amd.so
 	$(CXX) $(CXXFLAGS) -shared -o $@ $(HOST_SRC) -L$(LIB) -lhyrise_amd -Wl,-rpath,'$$ORIGIN'

@@ -85,6 +85,7 @@ op_trace_take = _host.op_trace_take
 pool_stats = _host.pool_stats
 device_memory = _host.device_memory
 host_cpu_share = _host.host_cpu_share
+release_drain = _host.release_drain
 set_job_scheduler = _host.set_job_scheduler
 DescriptionMode = _host.DescriptionMode
 

@@ -5,8 +5,11 @@
 #include <unordered_map>
 
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <string>
 #include <vector>
 
 #include "capi_common.hpp"
@@ -16,6 +19,7 @@
 #include "../kernels/aggregate_lanes.hip"
 #include "../kernels/aggregate_vec.hip"
 #include "../kernels/aggregate_stream.hip"
+#include "agg_jit.hpp"
 
 using namespace hyc;
 
@@ -99,6 +103,8 @@ struct AggPlan {
   bool dense_vec = false;                  // agg_dense_vec instead (its preconditions hold; the default then)
   bool dense_stream = false;               // agg_dense_stream instead (its preconditions hold; the default then)
   hyk::StreamPlan stream_plan{};           // its stage layout and FMA-form chains
+  bool dense_jit = false;                  // the stream plan compiled into its own kernel (hyrise_amd_agg_jit.cpp)
+  hyjit::Shape jit_shape{};
 };
 
 // agg_dense_fused applies: the dense path; at most one PosList group; int32 group-by columns; every aggregate over a
@@ -240,6 +246,8 @@ void plan_stream(const hy_agg_input* in, AggPlan* plan) {
     off += 256u * width;
   }
   if (off > static_cast<uint32_t>(hyk::ST_STAGE)) return;
+  L.stage_bytes = off;
+  L.n_dslots = slots;
   // the sums: float chains as FMA-form terms (hyk::StreamTerm), int32 sums of plain columns, COUNT-only inputs
   const auto& lt = plan->lt;
   for (int32_t q = 0; q < lt.n_sums; ++q) {
@@ -297,6 +305,67 @@ void plan_stream(const hy_agg_input* in, AggPlan* plan) {
   if (plan->dense_groups > static_cast<uint32_t>(hyk::ST_CODES)) return;
   plan->stream_plan = L;
   plan->dense_stream = true;
+  // the plan-compiled kernel (default; HY_AGG_JIT=0: agg_dense_stream) when every loaded column has one encoding and
+  // width over all its chunks, and so has the filter
+  const char* ej = std::getenv("HY_AGG_JIT");
+  if (ej && std::atoi(ej) == 0) return;
+  hyjit::Shape& sh = plan->jit_shape;
+  sh = hyjit::Shape{};
+  sh.n_gb = static_cast<int32_t>(plan->d.n_gb);
+  sh.n_load = lt.n_load;
+  sh.n_sums = lt.n_sums;
+  sh.words = plan->d.words;
+  if (sh.n_load > hyj::MAX_COLS || sh.n_sums > hyjit::MAX_SUMS || lt.n_cnt > hyjit::MAX_CNT) return;
+  for (int32_t li = 0; li < sh.n_load; ++li) {
+    const auto& col = in->columns[plan->lane_cols[li]];
+    int kind = -1, width = 0;
+    for (uint32_t k = 0; k < col.n_chunks; ++k) {
+      const auto& ch = col.chunks[k];
+      if (ch.size == 0) continue;
+      const int kk = ch.kind == HY_COL_DICT ? 1 : 0;
+      const int ww = kk ? ch.vid_width : 4;
+      if ((kind >= 0 && kind != kk) || (width && width != ww)) return;
+      kind = kk;
+      width = ww;
+    }
+    sh.dict[li] = kind == 1;
+    sh.width[li] = width ? width : 4;
+    sh.col_off[li] = L.col_off[li];
+    sh.dict_slot[li] = L.dict_slot[li];
+    if (li < sh.n_gb) {
+      sh.gb_domain[li] = lt.gb_domain[li];
+      sh.gb_stride[li] = lt.gb_stride[li];
+    }
+  }
+  if (in->filter) {
+    sh.filtered = 1;
+    for (uint32_t k = 0; k < in->n_chunks; ++k) {
+      const auto& f = in->filter[k];
+      if (f.column.size == 0) continue;
+      if (sh.f_width && sh.f_width != f.column.vid_width) return;
+      sh.f_width = f.column.vid_width;
+    }
+    if (!sh.f_width) sh.f_width = 1;
+    sh.filt_off = L.filt_off;
+  }
+  sh.stage_bytes = L.stage_bytes;
+  sh.n_dslots = L.n_dslots;
+  for (int32_t q = 0; q < lt.n_sums; ++q) {
+    sh.sum_kind[q] = L.sum_kind[q];
+    sh.sum_first[q] = L.sum_first[q];
+    sh.sum_len[q] = L.sum_len[q];
+    sh.sum_nfn[q] = lt.sum_nfn[q];
+    for (int32_t f = 0; f < lt.sum_nfn[q] && f < hyjit::MAX_FNS; ++f) sh.sum_word[q][f] = lt.sum_word[q][f];
+    sh.sum_limbs[q] = lt.sum_limbs[q];
+    for (int32_t t = 0; t < L.sum_len[q]; ++t) {
+      const int32_t i = L.sum_first[q] + t;
+      if (i >= hyjit::MAX_TERMS) return;
+      sh.terms[i] = hyjit::Term{L.terms[i].a, L.terms[i].b, L.terms[i].col, L.terms[i].flags};
+    }
+  }
+  sh.n_cnt = lt.n_cnt;
+  for (int32_t f = 0; f < lt.n_cnt; ++f) sh.cnt_word[f] = lt.cnt_word[f];
+  plan->dense_jit = true;
 }
 
 
@@ -1054,9 +1123,36 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
         sp.chunk_row_begin = d.chunk_row_begin;
         sp.filter = d.filter;
         HY_STAGE(w.stream_plan, &sp, sizeof(sp), s);
-        KTimer t("agg_dense_stream", s, plan.rows);
-        launch_dense_stream(lp.n_sums, plan.n_tiles, s, d, lp, w.stream_plan, w.records);
-        t.done();
+        std::string jit_err;
+        bool ran_jit = false;
+        if (plan.dense_jit) {
+          hyj::JitArgs ja{};
+          for (int32_t li = 0; li < lt.n_load; ++li)
+            ja.cols[li] = reinterpret_cast<const hyj::ColumnChunk*>(lt.load_chunks[li]);
+          ja.filter = reinterpret_cast<const hyj::ScanChunk*>(d.filter);
+          ja.tile_chunk = d.tile_chunk;
+          ja.chunk_tile_begin = d.chunk_tile_begin;
+          ja.chunk_size = d.chunk_size;
+          ja.chunk_row_begin = d.chunk_row_begin;
+          ja.records = w.records;
+          ja.deferred = w.deferred;
+          ja.n_deferred = w.misc + 8;
+          ja.error = d.error;
+          ja.n_tiles = plan.n_tiles;
+          KTimer t("agg_dense_jit", s, plan.rows);
+          ran_jit = hyjit::launch(plan.jit_shape, ja, s, &jit_err);
+          t.done();
+          if (!ran_jit) {  // (reported once per process; agg_dense_stream runs instead)
+            static std::once_flag warned;
+            std::call_once(warned, [&] { std::fprintf(stderr, "hyrise-amd: plan-compiled aggregate unavailable (%s); "
+                                                              "using agg_dense_stream\n", jit_err.c_str()); });
+          }
+        }
+        if (!ran_jit) {
+          KTimer t("agg_dense_stream", s, plan.rows);
+          launch_dense_stream(lp.n_sums, plan.n_tiles, s, d, lp, w.stream_plan, w.records);
+          t.done();
+        }
       } else {
         KTimer t(plan.dense_vec ? "agg_dense_vec" : "agg_dense_lanes", s, plan.rows);
         launch_lanes(lp.n_sums, plan.lanes_vec, plan.dense_vec, all_float, plan.n_tiles, vlds, s, d, lp, w.records);

@@ -365,6 +365,8 @@ PYBIND11_MODULE(_hyrise_host, m) {
     return py::make_tuple(reserved, used);
   });
   m.def("host_cpu_share", &host_cpu_share);
+  m.def("release_drain", &release_drain, py::call_guard<py::gil_scoped_release>(),
+        "wait until the chunks of dropped large tables (destroyed on a background thread) are gone");
   m.def("device_memory", []() {
     uint64_t free_b = 0, total_b = 0;
     hy_check(hy_device_memory(&free_b, &total_b), "hy_device_memory");

@@ -1,6 +1,10 @@
 #include "storage.hpp"
 
 #include <atomic>
+#include <condition_variable>
+#include <cstdlib>
+#include <deque>
+#include <mutex>
 #include <thread>
 
 #include <fstream>
@@ -81,6 +85,65 @@ void Table::append_chunk(const ChunkColumns& columns) {
 // The bulk form operators use for outputs they built consistent by construction (a JoinHash's 65,536 chunks at
 // SF100): the per-column checks are debug-only here, as the reference's DebugAssert, because walking every chunk's
 // columns and PosLists right after other threads built them costs several milliseconds of cache misses.
+namespace {
+
+// Destroys handed-over chunk lists on one background thread (never joined: the process-exit hook drains it while the
+// HIP runtime is still up, since the hook is registered after the first device allocation it frees).
+class ChunkReaper {
+ public:
+  void push(std::vector<std::shared_ptr<Chunk>>&& chunks) {
+    std::lock_guard<std::mutex> lock(_m);
+    if (!_started) {
+      _started = true;
+      std::thread([this] { run(); }).detach();
+      std::atexit([] { chunk_reaper().drain(); });
+    }
+    _queue.push_back(std::move(chunks));
+    _cv.notify_all();
+  }
+  void drain() {
+    std::unique_lock<std::mutex> lock(_m);
+    _cv.wait(lock, [&] { return _queue.empty() && _busy == 0; });
+  }
+  static ChunkReaper& chunk_reaper() {
+    static ChunkReaper* r = new ChunkReaper;  // (leaked: outlives static destruction)
+    return *r;
+  }
+
+ private:
+  void run() {
+    for (;;) {
+      std::vector<std::shared_ptr<Chunk>> chunks;
+      {
+        std::unique_lock<std::mutex> lock(_m);
+        _cv.wait(lock, [&] { return !_queue.empty(); });
+        chunks = std::move(_queue.front());
+        _queue.pop_front();
+        ++_busy;
+      }
+      chunks.clear();
+      std::lock_guard<std::mutex> lock(_m);
+      --_busy;
+      _cv.notify_all();
+    }
+  }
+  std::mutex _m;
+  std::condition_variable _cv;
+  std::deque<std::vector<std::shared_ptr<Chunk>>> _queue;
+  size_t _busy = 0;
+  bool _started = false;
+};
+
+constexpr size_t BACKGROUND_RELEASE_CHUNKS = 1024;
+
+}  // namespace
+
+Table::~Table() {
+  if (_chunks.size() >= BACKGROUND_RELEASE_CHUNKS) ChunkReaper::chunk_reaper().push(std::move(_chunks));
+}
+
+void release_drain() { ChunkReaper::chunk_reaper().drain(); }
+
 void Table::append_chunks(std::vector<std::shared_ptr<Chunk>>&& chunks) {
 #ifdef HYRISE_DEBUG  // (reference: DebugAssert, active in HYRISE_DEBUG builds)
   for (const auto& ch : chunks) {

@@ -361,6 +361,12 @@ class Table {
  public:
   Table(TableColumnDefinitions defs, TableType type, uint32_t max_chunk_size = CHUNK_MAX_SIZE)
       : _defs(std::move(defs)), _type(type), _max_chunk_size(max_chunk_size) {}
+  // A table of many chunks (a JoinHash output has one per radix partition: 65,536 at SF100, ~8 allocations each) hands
+  // its chunks to a background thread to destroy: dropping an operator's output costs the dropping thread a move
+  // instead of ~7 ms of frees. release_drain() waits until every handed-over chunk is destroyed.
+  ~Table();
+  Table(const Table&) = delete;
+  Table& operator=(const Table&) = delete;
 
   const TableColumnDefinitions& column_definitions() const { return _defs; }
   TableType type() const { return _type; }
@@ -396,6 +402,8 @@ class Table {
   uint32_t _max_chunk_size;
   std::vector<std::shared_ptr<Chunk>> _chunks;
 };
+
+void release_drain();
 
 // Creates an empty ValueColumn<T> for a data type.
 std::shared_ptr<BaseColumn> make_value_column(DataType t, bool nullable);

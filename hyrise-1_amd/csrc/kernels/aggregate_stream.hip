@@ -58,6 +58,8 @@ struct StreamPlan {
   uint32_t col_off[LN_COLS];    // stage byte offset of loaded column li (256 rows x its widest chunk width)
   uint32_t dict_slot[LN_COLS];  // decode table of loaded column li (< ST_DCOLS), or ST_NO_SLOT
   uint32_t filt_off;            // stage byte offset of the filter ids
+  uint32_t stage_bytes;         // one step's column bytes + filter ids (<= ST_STAGE)
+  uint32_t n_dslots;            // decode tables in use
   int32_t sum_kind[LN_SUMS];    // ST_SUM_*
   int32_t sum_first[LN_SUMS], sum_len[LN_SUMS];
   StreamTerm terms[LN_TERMS + VEC_TERMS];

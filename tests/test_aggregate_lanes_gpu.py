@@ -207,15 +207,33 @@ def kernels_ran(L):
     return names
 
 
-# data-input kernels under test: (HY_AGG_VEC, HY_AGG_STREAM) -> the kernel that must run (agg_dense_stream where its
-# preconditions hold - every dictionary <= 63 entries, so not with the "nulls" case's dictionary-encoded prices)
-DATA_MODES = [("2", "1"), ("2", "0"), ("1", "0"), ("0", "0")]
+# data-input kernels under test: (HY_AGG_VEC, stream mode) -> the kernel that must run. Stream mode "j": the plan-compiled
+# kernel agg_dense_jit (the default), "1": agg_dense_stream (HY_AGG_JIT=0), "0": neither (HY_AGG_STREAM=0) - the stream
+# kernels where their preconditions hold (every dictionary <= 63 entries, so not with the "nulls" case's
+# dictionary-encoded prices)
+DATA_MODES = [("2", "j"), ("2", "1"), ("2", "0"), ("1", "0"), ("0", "0")]
+
+
+def set_modes(monkeypatch, vec_mode, stream_mode):
+    monkeypatch.setenv("HY_AGG_VEC", vec_mode)
+    monkeypatch.setenv("HY_AGG_STREAM", "0" if stream_mode == "0" else "1")
+    monkeypatch.setenv("HY_AGG_JIT", "1" if stream_mode == "j" else "0")
+
+
+STREAM_KERNELS = {"agg_dense_jit", "agg_dense_stream"}
+
+
+def only_kernel(want, ran):
+    """`want` ran, and no other stream kernel did (a plan-compiled kernel that fails falls back to agg_dense_stream)."""
+    return want in ran and not ((STREAM_KERNELS - {want}) & ran)
 
 
 def data_kernel(vec_mode, stream_mode, stream_ok):
     if vec_mode != "2":
         return "agg_dense_lanes"
-    return "agg_dense_stream" if stream_mode == "1" and stream_ok else "agg_dense_vec"
+    if stream_mode == "0" or not stream_ok:
+        return "agg_dense_vec"
+    return {"j": "agg_dense_jit", "1": "agg_dense_stream"}[stream_mode]
 
 
 @pytest.mark.parametrize("case", ["clean", "nulls", "null_ids", "odd_values", "wide_range", "drift", "many_groups",
@@ -259,9 +277,8 @@ def test_lanes_path(hy, monkeypatch, case, input_kind):
     # data input: agg_dense_stream (default), agg_dense_vec (HY_AGG_STREAM=0), agg_dense_lanes' contiguous instance
     # (HY_AGG_VEC=1) and its strided one (0)
     headers = {}
-    for vec_mode, stream_mode in (DATA_MODES if input_kind == "data" else [("2", "1")]):
-        monkeypatch.setenv("HY_AGG_VEC", vec_mode)
-        monkeypatch.setenv("HY_AGG_STREAM", stream_mode)
+    for vec_mode, stream_mode in (DATA_MODES if input_kind == "data" else [("2", "j")]):
+        set_modes(monkeypatch, vec_mode, stream_mode)
         L.hy_kernel_stats_enable(1)
         L.hy_kernel_stats_reset()
         res_lanes = run(hy, dcols, pos, sizes, doms)
@@ -269,20 +286,19 @@ def test_lanes_path(hy, monkeypatch, case, input_kind):
         L.hy_kernel_stats_enable(0)
         # (the int32 expression chain of AGGS is not agg_dense_stream's: that set never streams)
         want = data_kernel(vec_mode, stream_mode, False) if input_kind == "data" else "agg_dense_lanes"
-        assert want in ran, (vec_mode, stream_mode, ran)
+        assert only_kernel(want, ran), (vec_mode, stream_mode, ran)
         check(res_lanes, exp)
         headers[vec_mode + stream_mode] = {(int(r[0]), int(r[1])): tuple(int(x) for x in r[2:6])
                                            for r in run(hy, dcols, pos, sizes, doms, raw=True)[0]}
     if input_kind == "data":  # TPC-H 1's aggregate set: agg_dense_stream where it applies, against agg_dense_vec
-        for vec_mode, stream_mode in DATA_MODES[:2]:
-            monkeypatch.setenv("HY_AGG_VEC", vec_mode)
-            monkeypatch.setenv("HY_AGG_STREAM", stream_mode)
+        for vec_mode, stream_mode in DATA_MODES[:3]:
+            set_modes(monkeypatch, vec_mode, stream_mode)
             L.hy_kernel_stats_enable(1)
             L.hy_kernel_stats_reset()
             res_q1 = run(hy, dcols, pos, sizes, doms, aggs=Q1_AGGS)
             ran = kernels_ran(L)
             L.hy_kernel_stats_enable(0)
-            assert data_kernel(vec_mode, stream_mode, case != "nulls") in ran, (stream_mode, ran)
+            assert only_kernel(data_kernel(vec_mode, stream_mode, case != "nulls"), ran), (stream_mode, ran)
             check(res_q1, exp, Q1_AGGS)
             headers["q1/" + vec_mode + stream_mode] = {(int(r[0]), int(r[1])): tuple(int(x) for x in r[2:6])
                                                        for r in run(hy, dcols, pos, sizes, doms, raw=True,
@@ -376,24 +392,23 @@ def test_fused_scan_filter(hy, monkeypatch, case, pred_enc, cond, value):
     op = {"LessThanEquals": np.less_equal, "LessThan": np.less, "GreaterThan": np.greater}[cond]
     rows = list(np.nonzero(op(ship, value))[0])
     # stream (TPC-H 1's aggregate set), vec, lanes (strided)
-    for vec_mode, stream_mode, aggs in (("2", "1", Q1_AGGS), ("2", "0", AGGS), ("0", "0", AGGS)):
-        monkeypatch.setenv("HY_AGG_VEC", vec_mode)
-        monkeypatch.setenv("HY_AGG_STREAM", stream_mode)
+    for vec_mode, stream_mode, aggs in (("2", "j", Q1_AGGS), ("2", "1", Q1_AGGS), ("2", "0", AGGS), ("0", "0", AGGS)):
+        set_modes(monkeypatch, vec_mode, stream_mode)
         capi.lib.hy_kernel_stats_enable(1)
         capi.lib.hy_kernel_stats_reset()
         res = run(hy, dcols, None, sizes, doms, filt=(chunks, capi.HY_TYPE_INT32, pred.constant(value)), aggs=aggs)
         ran = kernels_ran(capi.lib)
         capi.lib.hy_kernel_stats_enable(0)
         # agg_dense_stream takes dictionary id-range filters only
-        assert data_kernel(vec_mode, stream_mode, case != "nulls" and pred_enc == "Dictionary") in ran, ran
+        assert only_kernel(data_kernel(vec_mode, stream_mode, case != "nulls" and pred_enc == "Dictionary"), ran), ran
         check(res, expected(cols, rows), aggs)
 
 
 @pytest.mark.parametrize("case", ["clean", "nulls", "null_ids", "drift"])
 @pytest.mark.parametrize("cond,value", [("LessThanEquals", 300), ("GreaterThan", 700)])
-@pytest.mark.parametrize("stream_mode", ["1", "0"])
+@pytest.mark.parametrize("stream_mode", ["j", "1", "0"])
 def test_fused_scan_filter_against_oracle(hy, oracle, monkeypatch, case, cond, value, stream_mode):
-    """agg_dense_stream / agg_dense_vec with the TableScan fused (TPC-H 1's default plan) against the ORACLE's plan on
+    """agg_dense_jit / agg_dense_stream / agg_dense_vec with the TableScan fused (TPC-H 1's default plan) against the ORACLE's plan on
     the same table:
     oracle TableScan (single_column_table_scan_impl.cpp) -> Projection of the two float expressions
     (projection.cpp:39-87) -> Aggregate (aggregate.cpp:203-249, sequential double sums). Group keys, counts and int
@@ -412,16 +427,15 @@ def test_fused_scan_filter_against_oracle(hy, oracle, monkeypatch, case, cond, v
              dt.DeviceColumn(capi, tax, None, CHUNK, "Dictionary"), dt.DeviceColumn(capi, iq, None, CHUNK, "Unencoded")]
     pred = dt.DeviceColumn(capi, ship, None, CHUNK, "Dictionary")
     sizes = [d.size for d in dcols[0].descs]
-    monkeypatch.setenv("HY_AGG_VEC", "2")
-    monkeypatch.setenv("HY_AGG_STREAM", stream_mode)
+    set_modes(monkeypatch, "2", stream_mode)
     L.hy_kernel_stats_enable(1)
     L.hy_kernel_stats_reset()
-    aggs = Q1_AGGS if stream_mode == "1" else AGGS  # (agg_dense_stream: TPC-H 1's set, no int32 chain)
+    aggs = Q1_AGGS if stream_mode != "0" else AGGS  # (agg_dense_stream: TPC-H 1's set, no int32 chain)
     res = run(hy, dcols, None, sizes, doms,
               filt=(pred.scan_chunks(cond, value), capi.HY_TYPE_INT32, pred.constant(value)), aggs=aggs)
     ran = kernels_ran(L)
     L.hy_kernel_stats_enable(0)
-    assert data_kernel("2", stream_mode, case != "nulls") in ran, ran
+    assert only_kernel(data_kernel("2", stream_mode, case != "nulls"), ran), ran
 
     # the oracle's plan over a table of the same columns
     T = hy.DataType
