@@ -147,6 +147,10 @@ _sigs = {
                                                  ctypes.c_void_p]),
     "hy_expand_row_ids": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                          ctypes.c_void_p]),
+    "hy_table_scan_count": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_size_t, ctypes.c_void_p]),
+    "hy_expand_chunk_row_ids": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                               ctypes.c_void_p, ctypes.c_void_p]),
     "hy_aggregate_layout": (ctypes.c_int, [ctypes.POINTER(AggInput), ctypes.POINTER(AggParams),
                                            ctypes.POINTER(AggLayout)]),
     "hy_aggregate_workspace_size": (ctypes.c_int, [ctypes.POINTER(AggInput), ctypes.POINTER(AggParams),

@@ -715,6 +715,54 @@ hy_status hy_expand_row_ids(uint32_t chunk_id, const uint32_t* offsets, uint64_t
   return HY_OK;
 }
 
+hy_status hy_table_scan_count(const hy_scan_chunk* chunks, uint32_t n_chunks, uint32_t* counts, void* workspace,
+                              size_t workspace_bytes, hy_stream_t stream) {
+  if (n_chunks == 0) return HY_OK;
+  if (!chunks || !counts) return fail(HY_ERR_INVALID_ARGUMENT, "null argument");
+  int width = 0;
+  for (uint32_t c = 0; c < n_chunks; ++c) {
+    const auto& ch = chunks[c];
+    if (ch.column.kind != HY_COL_DICT || ch.op == HY_OP_IS_NULL || (ch.op == HY_OP_VID_SET && !ch.vid_set))
+      return fail(HY_ERR_UNSUPPORTED, "hy_table_scan_count: dictionary predicates only");
+    if (ch.column.size && (reinterpret_cast<uintptr_t>(ch.column.data) & 15u))
+      return fail(HY_ERR_INVALID_ARGUMENT, "hy_table_scan_count: chunk data must be 16-byte aligned");
+    if (ch.column.size) {
+      if (width && width != ch.column.vid_width) return fail(HY_ERR_UNSUPPORTED, "hy_table_scan_count: mixed id widths");
+      width = ch.column.vid_width;
+    }
+  }
+  if (workspace_bytes < sizeof(hy_scan_chunk) * n_chunks) return fail(HY_ERR_INVALID_ARGUMENT, "workspace too small");
+  hipStream_t s = S(stream);
+  auto* d_chunks = static_cast<hy_scan_chunk*>(workspace);
+  HY_STAGE(d_chunks, chunks, sizeof(hy_scan_chunk) * n_chunks, s);
+  switch (width) {
+    case 0:
+      HY_HIP(hipMemsetAsync(counts, 0, 4ull * n_chunks, s));
+      return HY_OK;
+    case 1:
+      hipLaunchKernelGGL(hyk::scan_count_kernel<uint8_t>, dim3(n_chunks), dim3(256), 0, s, d_chunks, counts);
+      break;
+    case 2:
+      hipLaunchKernelGGL(hyk::scan_count_kernel<uint16_t>, dim3(n_chunks), dim3(256), 0, s, d_chunks, counts);
+      break;
+    default:
+      hipLaunchKernelGGL(hyk::scan_count_kernel<uint32_t>, dim3(n_chunks), dim3(256), 0, s, d_chunks, counts);
+      break;
+  }
+  HY_HIP(hipGetLastError());
+  return HY_OK;
+}
+
+hy_status hy_expand_chunk_row_ids(const uint32_t* offsets, const uint64_t* chunk_begin, const uint32_t* chunk_ids,
+                                  uint32_t n_chunks, hy_row_id* out, hy_stream_t stream) {
+  if (n_chunks == 0) return HY_OK;
+  if (!offsets || !chunk_begin || !out) return fail(HY_ERR_INVALID_ARGUMENT, "null argument");
+  hipLaunchKernelGGL(hyk::expand_chunk_row_ids_kernel, dim3(n_chunks), dim3(256), 0, S(stream), offsets, chunk_begin,
+                     chunk_ids, out);
+  HY_HIP(hipGetLastError());
+  return HY_OK;
+}
+
 // ================================================================================================================
 // Hashing
 // ================================================================================================================

@@ -108,8 +108,8 @@ inline uint32_t sub1() {
 // Spans of a side with a fused TableScan: two tiles, so that part1_spread's spans hold about as many matches as
 // a record pass's tile (measured on MI355X at SF100: 1.70 ms for part1_spread vs 2.52 ms with one-tile spans);
 // HY_PART_SUB_FILTERED overrides it.
-inline uint32_t sub_filtered() {  // (at most hyk::GAP_SPAN_MAX rows: part1_compact's 16-bit in-span offsets)
-  static const uint32_t v = std::min<uint32_t>(sub_from_env("HY_PART_SUB_FILTERED", 2), hyk::GAP_SPAN_MAX / hyk::PART_TILE);
+inline uint32_t sub_filtered() {
+  static const uint32_t v = sub_from_env("HY_PART_SUB_FILTERED", 2);
   return v;
 }
 // Next-digit bytes beside the records of a pass that has a successor (HY_DIGIT_BYTES=0 turns them off: the next
@@ -630,10 +630,6 @@ hy_status launch_filtered_pass0(const SidePlan& p, const hyk::Side& sd, const hy
     HY_HIP(hipGetLastError());
     return HY_OK;
   }
-  // the gapped records in recB, SoA: keys, then (16-byte aligned) the 16-bit in-span offsets (hyk::GAP_NULL)
-  const uint64_t gap_n = p.n_tiles1 * p.sub * hyk::PART_TILE;
-  H* gap_keys = reinterpret_cast<H*>(b.recB);
-  uint16_t* gap_offs = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(b.recB) + hyk::align16(sizeof(H) * gap_n));
   {
     KTimer kt_((std::string("part1_compact.") + SD::name).c_str(), s, p.n_rows);
     bool prefiltered = false;
@@ -641,10 +637,10 @@ hy_status launch_filtered_pass0(const SidePlan& p, const hyk::Side& sd, const hy
     if (prefiltered) {
       if constexpr (std::is_same_v<SD, hyk::OnProbe>)
         hipLaunchKernelGGL((hyk::part1_compact<SD, T, H, LP, FK, true>), grid, dim3(hyk::PART_THREADS), 0, s, sd, d0,
-                           n_digits, b.hist, b.span_count, gap_keys, gap_offs);
+                           n_digits, b.hist, b.span_count, b.recB);
     } else {
       hipLaunchKernelGGL((hyk::part1_compact<SD, T, H, LP, FK, false>), grid, dim3(hyk::PART_THREADS), 0, s, sd, d0,
-                         n_digits, b.hist, b.span_count, gap_keys, gap_offs);
+                         n_digits, b.hist, b.span_count, b.recB);
     }
     kt_.done();
   }
@@ -658,7 +654,7 @@ hy_status launch_filtered_pass0(const SidePlan& p, const hyk::Side& sd, const hy
   {
     KTimer kt_((std::string("part1_spread.") + SD::name).c_str(), s, p.n_rows);
     hipLaunchKernelGGL((hyk::part1_spread<SD, H>), grid, dim3(hyk::PART_THREADS), 0, s, sd, d0, nd, static_cast<int>(w0),
-                       n_digits, b.off, b.span_count, gap_keys, gap_offs, out);
+                       n_digits, b.off, b.span_count, b.recB, out);
     kt_.done();
   }
   HY_HIP(hipGetLastError());
@@ -1122,10 +1118,13 @@ hy_status run_join_partitions(const uint32_t* build_begin, const uint32_t* probe
   HY_HIP(hipMemsetAsync(c.misc, 0, 64 * 4, s));
   HY_HIP(hipMemsetAsync(c.totals, 0, 8 * 2, s));
   constexpr int JW = Src::V == 1 ? 6 : 8;  // the wide variant's probe records per thread (a multiple of V)
-  // most partitions need several probe passes (the average exceeds 3/4 of the wide pass): the multi-pass kernel takes
-  // every partition directly instead of the one-pass kernel deferring nearly all of them
-  // (only when the probe rows are known: a filtered probe side's hint is its rows before the filter)
-  const bool all_multi = probe_exact && avg_probe > static_cast<uint64_t>(3 * JW * NT / 4) && !jd.trace;
+  // most partitions need several probe passes (the average plus four standard deviations of a uniform spread exceeds
+  // the wide pass): the multi-pass kernel takes every partition directly instead of the one-pass kernel deferring
+  // nearly all of them (only when the probe rows are known: a filtered probe side's hint is its rows before the
+  // filter). (Round 4 switched at 3/4 of the pass: TPC-H SF10's 7,324 probe rows per partition went to the count +
+  // reload + write passes of join_partition_multi although nearly all fit one 8,192-record pass.)
+  const double wide_pass = double(JW * NT - (Src::V - 1));
+  const bool all_multi = probe_exact && double(avg_probe) + 4.0 * std::sqrt(double(avg_probe)) > wide_pass && !jd.trace;
   if (n_parts && all_multi) {
     jd.multi = nullptr;
     KTimer kt_("join_partition", s, units);

@@ -524,6 +524,118 @@ std::shared_ptr<AbstractOperator> TableScan::_on_deep_copy(const std::shared_ptr
   return std::make_shared<TableScan>(copied_input_left, _left_column_id, _predicate_condition, _right_parameter);
 }
 
+namespace {
+
+// A TableScan over a data table (not strings), as a deferred producer of its output (Table::Producer): it runs on the
+// first access of the output - or inside the JoinHash that consumes the output, which evaluates the predicate in its
+// first radix pass and hands the matches back (fulfil_from_offsets; JoinHash::_on_execute, "fused TableScan").
+struct DataScan final : Table::Producer {
+  std::shared_ptr<const Table> in_table;
+  ColumnID column_id = 0;
+  DataType col_type = DataType::Int;
+  std::vector<hy_scan_chunk> descs;  // one per scanned chunk, out_begin = its first row in `rows`
+  std::vector<ChunkID> chunk_ids;
+  std::vector<uint32_t> sizes;
+  ScanConstant constant;
+  uint64_t total = 0;
+  bool all_chunks = false;  // the scanned chunks are every chunk of in_table, in order
+
+  // the output chunks: one per scanned chunk with a match (table_scan.cpp:99), its PosList a view of `rows`
+  std::vector<std::shared_ptr<Chunk>> chunks_from(const std::shared_ptr<DeviceBuffer>& rows,
+                                                  const std::vector<std::pair<uint64_t, uint32_t>>& views) const {
+    OutputArena arena;
+    std::vector<std::shared_ptr<Chunk>> out;
+    for (size_t k = 0; k < descs.size(); ++k) {
+      if (views[k].second == 0) continue;
+      auto pl = pos_list_from_device(arena, rows, views[k].first, views[k].second);
+      pl->set_single_chunk_id(chunk_ids[k]);
+      ChunkColumns cols;
+      cols.reserve(in_table->column_count());
+      for (ColumnID col = 0; col < in_table->column_count(); ++col)
+        cols.push_back(arena_reference_column(arena, in_table, col, pl));
+      out.push_back(arena_chunk(arena, std::move(cols)));
+    }
+    return out;
+  }
+
+  // the scan on its own: one launch writes every chunk's RowIDs at its row range of `rows`
+  std::vector<std::shared_ptr<Chunk>> produce() override {
+    hy_stream_t s = operator_stream();
+    PhaseTrace tr{"TableScan (deferred)"};
+    size_t ws_bytes = 0;
+    hy_check(hy_table_scan_workspace_size(sizes.data(), static_cast<uint32_t>(sizes.size()), &ws_bytes),
+             "hy_table_scan_workspace_size");
+    DeviceBuffer ws(ws_bytes, s);
+    auto rows = std::make_shared<DeviceBuffer>(std::max<uint64_t>(total, 1) * sizeof(RowID));
+    DeviceBuffer counts(descs.size() * 4, s);
+    std::vector<uint32_t> h_counts(descs.size());
+    hy_check(hy_table_scan_row_ids(descs.data(), static_cast<uint32_t>(descs.size()), hy_type_of(col_type),
+                                   constant.bytes, chunk_ids.data(), rows->as<hy_row_id>(), counts.as<uint32_t>(),
+                                   ws.get(), ws_bytes, s),
+             "hy_table_scan_row_ids");
+    hy_check(hy_memcpy_dtoh(h_counts.data(), counts.get(), 4 * descs.size(), s), "hy_memcpy_dtoh");
+    hy_check(hy_stream_synchronize(s), "sync");
+    tr.mark("scan + counts");
+    std::vector<std::pair<uint64_t, uint32_t>> views;
+    for (size_t k = 0; k < descs.size(); ++k) views.emplace_back(descs[k].out_begin, h_counts[k]);
+    auto out = chunks_from(rows, views);
+    tr.mark("output chunks");
+    return out;
+  }
+
+  // matches of the scan per chunk, counted without output (the fused consumer's swap rule needs the output's row
+  // count; with the counts the output chunks are built while the consumer's join runs): kept in `counts`
+  std::vector<uint32_t> counts;
+  uint64_t count_matches() {
+    hy_stream_t s = operator_stream();
+    DeviceBuffer ws(std::max<size_t>(sizeof(hy_scan_chunk) * descs.size(), 16), s), d_counts(descs.size() * 4, s);
+    hy_check(hy_table_scan_count(descs.data(), static_cast<uint32_t>(descs.size()), d_counts.as<uint32_t>(), ws.get(),
+                                 ws.bytes(), s),
+             "hy_table_scan_count");
+    counts.assign(descs.size(), 0);
+    hy_check(hy_memcpy_dtoh(counts.data(), d_counts.get(), 4 * descs.size(), s), "hy_memcpy_dtoh");
+    hy_check(hy_stream_synchronize(s), "sync");
+    uint64_t n = 0;
+    for (const uint32_t c : counts) n += c;
+    return n;
+  }
+  // the output chunks over `rows` laid out by `counts` (chunk k's RowIDs at the sum of the counts before it)
+  std::vector<std::shared_ptr<Chunk>> chunks_for(const std::shared_ptr<DeviceBuffer>& rows) const {
+    std::vector<std::pair<uint64_t, uint32_t>> views;
+    uint64_t at = 0;
+    for (const uint32_t c : counts) {
+      views.emplace_back(at, c);
+      at += c;
+    }
+    return chunks_from(rows, views);
+  }
+
+  // the predicate as the fused join's filter can take it: every chunk a dictionary chunk of one id width (the
+  // hy_table_scan_count preconditions), no IS NULL, every chunk of the table scanned
+  bool fusable() const {
+    if (!all_chunks || descs.empty()) return false;
+    int width = 0;
+    for (const auto& d : descs) {
+      if (d.column.kind != HY_COL_DICT || d.op == HY_OP_IS_NULL || d.op == HY_OP_IS_NOT_NULL || d.op == HY_OP_VID_SET)
+        return false;
+      if ((reinterpret_cast<uintptr_t>(d.column.data) & 15u) != 0) return false;
+      if (d.column.size) {
+        if (width && width != d.column.vid_width) return false;
+        width = d.column.vid_width;
+      }
+    }
+    return true;
+  }
+};
+
+// HY_OP_FUSE_SCAN=0: TableScans run when they execute (no deferral, no fusion into JoinHash)
+bool scan_fusion_enabled() {
+  const char* e = std::getenv("HY_OP_FUSE_SCAN");
+  return !(e && std::atoi(e) == 0);
+}
+
+}  // namespace
+
 std::shared_ptr<const Table> TableScan::_on_execute() {
   const auto in_table = input_table_left();
   // the reference's scan impls boost::get the value / column id: an unset placeholder cannot execute
@@ -582,22 +694,60 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
     std::vector<size_t> like_offs;
     LikeBatch like_sets;
     uint64_t total = 0;
-    for (ChunkID c = 0; c < in_table->chunk_count(); ++c) {
-      if (excluded[c]) continue;
-      const auto column = in_table->get_chunk(c)->get_column(_left_column_id);
-      size_t off;
-      auto d = scan_descriptor(*column, col_type, _predicate_condition, right_value, &like_sets, &off);
-      d.out_begin = total;
-      total += column->size();
-      descs.push_back(d);
-      like_offs.push_back(off);
-      chunk_ids.push_back(c);
-      sizes.push_back(static_cast<uint32_t>(column->size()));
+    for (ChunkID c = 0; c < in_table->chunk_count(); ++c)
+      if (!excluded[c]) chunk_ids.push_back(c);
+    descs.resize(chunk_ids.size());
+    like_offs.assign(chunk_ids.size(), SIZE_MAX);
+    sizes.resize(chunk_ids.size());
+    // the descriptors (dictionary rewrite per chunk, ~0.25 us each: 1.5 ms for SF100's 6,000 chunks on one thread)
+    // by jobs of the host's scheduler; LIKE patterns share one batch of id sets and stay on this thread
+    auto describe = [&](size_t k0, size_t k1, LikeBatch* batch) {
+      for (size_t k = k0; k < k1; ++k) {
+        const auto column = in_table->get_chunk(chunk_ids[k])->get_column(_left_column_id);
+        descs[k] = scan_descriptor(*column, col_type, _predicate_condition, right_value, batch, &like_offs[k]);
+        sizes[k] = static_cast<uint32_t>(column->size());
+      }
+    };
+    constexpr size_t CHUNKS_PER_JOB = 512;
+    if (like || chunk_ids.size() < 2 * CHUNKS_PER_JOB) {
+      describe(0, chunk_ids.size(), &like_sets);
+    } else {
+      JobGroup jobs;
+      const size_t n_jobs = std::min<size_t>(jobs.concurrency(host_cpu_share()),
+                                             (chunk_ids.size() + CHUNKS_PER_JOB - 1) / CHUNKS_PER_JOB);
+      const size_t per = (chunk_ids.size() + n_jobs - 1) / n_jobs;
+      for (size_t j = 0; j < n_jobs; ++j)
+        jobs.schedule([&, j] {
+          LikeBatch unused;
+          describe(j * per, std::min(chunk_ids.size(), (j + 1) * per), &unused);
+        });
+      jobs.wait();
+    }
+    for (size_t k = 0; k < descs.size(); ++k) {
+      descs[k].out_begin = total;
+      total += sizes[k];
     }
     if (descs.empty()) return output;
     for (size_t k = 0; k < descs.size(); ++k)
       if (like_offs[k] != SIZE_MAX) like_sets.fix.emplace_back(&descs[k], like_offs[k]);
     like_sets.finish(&keep);
+    tr.mark("descriptors");
+    if (col_type != DataType::String && !like && scan_fusion_enabled()) {
+      // deferred: the scan runs when its output is first read, or inside the JoinHash that consumes it
+      auto scan = std::make_shared<DataScan>();
+      scan->in_table = in_table;
+      scan->column_id = _left_column_id;
+      scan->col_type = col_type;
+      scan->descs = std::move(descs);
+      scan->chunk_ids = std::move(chunk_ids);
+      scan->sizes = std::move(sizes);
+      scan->constant = null_test ? ScanConstant{} : typed_constant(col_type, right_value);
+      scan->total = total;
+      scan->all_chunks = scan->descs.size() == in_table->chunk_count();
+      output->set_pending(std::move(scan));
+      tr.mark("deferred");
+      return output;
+    }
     auto rows = std::make_shared<DeviceBuffer>(std::max<uint64_t>(total, 1) * sizeof(RowID));
     DeviceBuffer counts(descs.size() * 4, s);
     std::vector<uint32_t> h_counts(descs.size());
@@ -633,11 +783,12 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
                                      constant.bytes, chunk_ids.data(), rows->as<hy_row_id>(), counts.as<uint32_t>(),
                                      ws.get(), ws_bytes, s),
                "hy_table_scan_row_ids");
+      tr.mark("scan launched");
       hy_check(hy_memcpy_dtoh(h_counts.data(), counts.get(), 4 * descs.size(), s), "hy_memcpy_dtoh");
       hy_check(hy_stream_synchronize(s), "sync");
       for (size_t k = 0; k < descs.size(); ++k) views.emplace_back(descs[k].out_begin, h_counts[k]);
     }
-    tr.mark("descriptors + scan + sync");
+    tr.mark("counts synchronised");
     // output PosLists are lazy views of `rows` (no copy to the host, no wait: later work is ordered on the stream);
     // chunks, columns and PosLists from an output arena (device.hpp)
     OutputArena arena;
@@ -1318,17 +1469,44 @@ void write_chunk_columns(ChunkColumns& out, OutputArena& arena, const std::share
 std::shared_ptr<const Table> JoinHash::_on_execute() {
   const auto left_in = input_table_left();
   const auto right_in = input_table_right();
+  const bool string_keys =
+      join_hashed_type(left_in->column_data_type(_column_ids.first), right_in->column_data_type(_column_ids.second)) ==
+      DataType::String;
+  // A deferred TableScan input (DataScan) whose predicate the join's first radix pass can evaluate: its output's row
+  // count comes from a count-only scan (the swap rule below needs it), and if it becomes the probe side the scan runs
+  // fused into the join (hy_scan_join_hash) and its output is built from the join's by-product.
+  const bool fuse_modes = _mode == JoinMode::Inner || _mode == JoinMode::Outer;
+  auto fusable_scan = [&](const std::shared_ptr<const Table>& t) -> std::shared_ptr<DataScan> {
+    if (!scan_fusion_enabled() || string_keys || !fuse_modes) return nullptr;
+    auto scan = std::dynamic_pointer_cast<DataScan>(t->pending());
+    return scan && scan->fusable() ? scan : nullptr;
+  };
+  const auto left_scan = fusable_scan(left_in), right_scan = fusable_scan(right_in);
+  const uint64_t left_rows = left_scan ? left_scan->count_matches() : left_in->row_count();
+  const uint64_t right_rows = right_scan ? right_scan->count_matches() : right_in->row_count();
   // reference join_hash.cpp:55-76
   bool inputs_swapped = (_mode == JoinMode::Left || _mode == JoinMode::Anti || _mode == JoinMode::Semi);
-  if (!inputs_swapped && left_in->row_count() > right_in->row_count()) inputs_swapped = true;
+  if (!inputs_swapped && left_rows > right_rows) inputs_swapped = true;
   const auto build_table = inputs_swapped ? right_in : left_in;
   const auto probe_table = inputs_swapped ? left_in : right_in;
+  const uint64_t build_rows = inputs_swapped ? right_rows : left_rows;
+  const uint64_t probe_rows = inputs_swapped ? left_rows : right_rows;
   const ColumnID build_col = inputs_swapped ? _column_ids.second : _column_ids.first;
   const ColumnID probe_col = inputs_swapped ? _column_ids.first : _column_ids.second;
   const DataType build_type = build_table->column_data_type(build_col);
   const DataType probe_type = probe_table->column_data_type(probe_col);
   const DataType hashed = join_hashed_type(build_type, probe_type);
-  const bool string_keys = hashed == DataType::String;
+  // the probe side's scan runs fused when this join takes it over (a build-side scan is produced when it is read)
+  std::shared_ptr<DataScan> fused_scan = inputs_swapped ? left_scan : right_scan;
+  if (fused_scan && std::const_pointer_cast<Table>(probe_table)->take_pending() != fused_scan) fused_scan = nullptr;
+  // (if the join fails before the scan's output is built, the scan goes back to being produced on access)
+  struct Untake {
+    std::shared_ptr<Table> table;
+    std::shared_ptr<DataScan> scan;
+    ~Untake() {
+      if (scan) table->set_pending(scan);
+    }
+  } untake{fused_scan ? std::const_pointer_cast<Table>(probe_table) : nullptr, fused_scan};
 
   const bool semi_anti = _mode == JoinMode::Semi || _mode == JoinMode::Anti;
   TableColumnDefinitions defs;
@@ -1343,12 +1521,14 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
   auto output = std::make_shared<Table>(defs, TableType::References);
   require_device();
   hy_stream_t s = operator_stream();
-  _performance_data.rows_in = build_table->row_count() + probe_table->row_count();
+  _performance_data.rows_in = build_rows + probe_rows;
   PhaseTrace tr{"JoinHash"};
 
   StringKeys strings;
   JoinSideInput bside = describe_side(build_table, build_col, string_keys ? &strings : nullptr);
-  JoinSideInput pside = describe_side(probe_table, probe_col, string_keys ? &strings : nullptr);
+  // fused: the probe side is the scan's data table, filtered inside the join
+  const std::shared_ptr<const Table> probe_data = fused_scan ? fused_scan->in_table : probe_table;
+  JoinSideInput pside = describe_side(probe_data, probe_col, string_keys ? &strings : nullptr);
   const int32_t btype = string_keys ? HY_TYPE_INT32 : hy_type_of(build_type);
   const int32_t ptype = string_keys ? HY_TYPE_INT32 : hy_type_of(probe_type);
   hy_join_side b{bside.chunks.data(), static_cast<uint32_t>(bside.chunks.size()), btype,
@@ -1362,17 +1542,36 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
   // the constructor's radix_bits is ignored and recomputed from the build side (join_hash.cpp:640-668)
   // sizeof(LeftType) of the build column's type; a std::string is 32 bytes in libstdc++
   const uint32_t build_size = build_type == DataType::String ? 32u : static_cast<uint32_t>(data_type_size(build_type));
-  prm.radix_bits = hy_join_radix_bits(build_table->row_count(), build_size);
+  prm.radix_bits = hy_join_radix_bits(build_rows, build_size);
   prm.seed = 17;
   _used_radix_bits = prm.radix_bits;
 
   tr.mark("describe sides");
+  // the fused scan's filter and its by-product (the scan's matches, chunk by chunk); the scan's output chunks - their
+  // sizes known from the count - are built by a job while the join runs, over RowIDs expanded after it
+  std::unique_ptr<DeviceBuffer> scan_offsets, scan_begin;
+  std::shared_ptr<DeviceBuffer> scan_rows;
+  std::vector<std::shared_ptr<Chunk>> scan_chunks;
+  JobGroup scan_builder;
+  hy_join_filter pf{};
+  if (fused_scan) {
+    scan_rows = std::make_shared<DeviceBuffer>(std::max<uint64_t>(probe_rows, 1) * sizeof(RowID));
+    scan_builder.schedule([&] { scan_chunks = fused_scan->chunks_for(scan_rows); });
+    scan_offsets = std::make_unique<DeviceBuffer>(std::max<uint64_t>(fused_scan->total, 1) * 4, s);
+    scan_begin = std::make_unique<DeviceBuffer>((fused_scan->descs.size() + 1) * 8, s);
+    pf = hy_join_filter{fused_scan->descs.data(), hy_type_of(fused_scan->col_type), fused_scan->constant.bytes,
+                        scan_offsets->as<uint32_t>(), scan_begin->as<uint64_t>()};
+  }
   size_t ws_bytes = 0;
-  hy_check(hy_join_hash_workspace_size(&b, &p, &prm, &ws_bytes), "hy_join_hash_workspace_size");
+  if (fused_scan)
+    hy_check(hy_scan_join_hash_workspace_size(&b, nullptr, &p, &pf, &prm, &ws_bytes),
+             "hy_scan_join_hash_workspace_size");
+  else
+    hy_check(hy_join_hash_workspace_size(&b, &p, &prm, &ws_bytes), "hy_join_hash_workspace_size");
   DeviceBuffer ws(ws_bytes, s);
   const uint32_t n_parts = 1u << prm.radix_bits;
   DeviceBuffer part_begin(8 * n_parts, s), part_count(4 * n_parts, s);
-  uint64_t capacity = std::max<uint64_t>(probe_table->row_count() + build_table->row_count(), 16);
+  uint64_t capacity = std::max<uint64_t>(probe_rows + build_rows, 16);
   auto out_b = std::make_shared<DeviceBuffer>(capacity * sizeof(RowID));
   auto out_p = std::make_shared<DeviceBuffer>(capacity * sizeof(RowID));
 
@@ -1386,7 +1585,7 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
   std::shared_ptr<Table> dummy, pdummy;
   const bool with_build = !(semi_anti && inputs_swapped);
   SideOut bo = with_build ? describe_output(build_table, bside, out_b, base_refs, dummy) : SideOut{};
-  SideOut po = describe_output(probe_table, pside, out_p, base_refs, pdummy);
+  SideOut po = describe_output(probe_data, pside, out_p, base_refs, pdummy);
   const int n_lists = bo.n_lists + po.n_lists;
   std::vector<std::shared_ptr<Chunk>> chunks(n_parts);
   std::vector<PosList*> lists(static_cast<size_t>(n_parts) * n_lists);
@@ -1463,8 +1662,12 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
 
   hy_join_result res{};
   for (int attempt = 0; attempt < 2; ++attempt) {
-    const hy_status st = hy_join_hash(&b, &p, &prm, out_b->as<hy_row_id>(), out_p->as<hy_row_id>(), capacity,
-                                      part_begin.as<uint64_t>(), part_count.as<uint32_t>(), &res, ws.get(), ws_bytes, s);
+    const hy_status st =
+        fused_scan ? hy_scan_join_hash(&b, nullptr, &p, &pf, &prm, out_b->as<hy_row_id>(), out_p->as<hy_row_id>(),
+                                       capacity, part_begin.as<uint64_t>(), part_count.as<uint32_t>(), &res, ws.get(),
+                                       ws_bytes, s)
+                   : hy_join_hash(&b, &p, &prm, out_b->as<hy_row_id>(), out_p->as<hy_row_id>(), capacity,
+                                  part_begin.as<uint64_t>(), part_count.as<uint32_t>(), &res, ws.get(), ws_bytes, s);
     if (st == HY_ERR_CAPACITY && attempt == 0) {
       capacity = std::max<uint64_t>(res.capacity_required, 16);
       DeviceBuffer nb(capacity * sizeof(RowID)), np(capacity * sizeof(RowID));
@@ -1472,13 +1675,30 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
       out_p->swap(np);
       continue;
     }
-    hy_check(st, "hy_join_hash");
+    hy_check(st, fused_scan ? "hy_scan_join_hash" : "hy_join_hash");
     break;
   }
   hy_check(hy_memcpy_dtoh(h_begin.data(), part_begin.get(), 8 * n_parts, s), "dtoh");
   hy_check(hy_memcpy_dtoh(h_count.data(), part_count.get(), 4 * n_parts, s), "dtoh");
+  std::vector<uint64_t> h_scan_begin(fused_scan ? fused_scan->descs.size() + 1 : 0);
+  if (fused_scan)
+    hy_check(hy_memcpy_dtoh(h_scan_begin.data(), scan_begin->get(), 8 * h_scan_begin.size(), s), "dtoh");
   hy_check(hy_stream_synchronize(s), "sync");
   tr.mark("join kernels + partition counts");
+  if (fused_scan) {  // the scan's output from the join's by-product: one expansion launch into the chunks' RowIDs
+    uint64_t at = 0;
+    for (size_t k = 0; k < fused_scan->counts.size(); ++k) {
+      Assert(h_scan_begin[k] == at, "fused TableScan: the join's scan output disagrees with the scan's count");
+      at += fused_scan->counts[k];
+    }
+    hy_check(hy_expand_chunk_row_ids(scan_offsets->as<uint32_t>(), scan_begin->as<uint64_t>(), nullptr,
+                                     static_cast<uint32_t>(fused_scan->descs.size()), scan_rows->as<hy_row_id>(), s),
+             "hy_expand_chunk_row_ids");
+    scan_builder.wait();
+    std::const_pointer_cast<Table>(probe_table)->fulfil(std::move(scan_chunks));
+    untake.scan = nullptr;
+    tr.mark("fused TableScan output");
+  }
 
   uint64_t used = 0;  // the output range the partitions occupy
   for (uint32_t part = 0; part < n_parts; ++part)

@@ -47,6 +47,7 @@ std::vector<std::string> Table::column_names() const {
 }
 
 uint64_t Table::row_count() const {
+  resolve();
   uint64_t n = 0;
   for (const auto& c : _chunks) n += c->size();
   return n;
@@ -62,17 +63,20 @@ std::shared_ptr<BaseColumn> make_value_column(DataType t, bool nullable) {
 }
 
 void Table::append_mutable_chunk() {
+  resolve();
   ChunkColumns cols;
   for (const auto& d : _defs) cols.push_back(make_value_column(d.data_type, d.nullable));
   _chunks.push_back(std::make_shared<Chunk>(std::move(cols)));
 }
 
 void Table::append(const std::vector<AllTypeVariant>& values) {
+  resolve();
   if (_chunks.empty() || _chunks.back()->size() >= _max_chunk_size) append_mutable_chunk();
   _chunks.back()->append(values);
 }
 
 void Table::append_chunk(const ChunkColumns& columns) {
+  resolve();
   Assert(columns.size() == _defs.size(), "append_chunk: wrong number of columns");
   const size_t n = columns.empty() ? 0 : columns[0]->size();
   for (const auto& c : columns) {
@@ -138,6 +142,45 @@ constexpr size_t BACKGROUND_RELEASE_CHUNKS = 1024;
 
 }  // namespace
 
+void Table::set_pending(std::shared_ptr<Producer> producer) {
+  std::lock_guard<std::mutex> lock(_pending_m);
+  _pending = std::move(producer);
+  _taken = false;
+  _pending_flag.store(_pending != nullptr, std::memory_order_release);
+  _pending_cv.notify_all();
+}
+
+std::shared_ptr<Table::Producer> Table::pending() const {
+  std::lock_guard<std::mutex> lock(_pending_m);
+  return _taken ? nullptr : _pending;
+}
+
+std::shared_ptr<Table::Producer> Table::take_pending() {
+  std::lock_guard<std::mutex> lock(_pending_m);
+  if (!_pending || _taken) return nullptr;
+  _taken = true;
+  return _pending;
+}
+
+void Table::fulfil(std::vector<std::shared_ptr<Chunk>>&& chunks) {
+  std::lock_guard<std::mutex> lock(_pending_m);
+  _chunks = std::move(chunks);
+  _pending = nullptr;
+  _taken = false;
+  _pending_flag.store(false, std::memory_order_release);
+  _pending_cv.notify_all();
+}
+
+void Table::resolve_slow() const {
+  std::unique_lock<std::mutex> lock(_pending_m);
+  // a consumer that took the producer fulfils the table: other accessors wait for it
+  _pending_cv.wait(lock, [&] { return !_taken || !_pending; });
+  if (!_pending) return;
+  auto producer = std::move(_pending);
+  _chunks = producer->produce();
+  _pending_flag.store(false, std::memory_order_release);
+}
+
 Table::~Table() {
   if (_chunks.size() >= BACKGROUND_RELEASE_CHUNKS) ChunkReaper::chunk_reaper().push(std::move(_chunks));
 }
@@ -145,6 +188,7 @@ Table::~Table() {
 void release_drain() { ChunkReaper::chunk_reaper().drain(); }
 
 void Table::append_chunks(std::vector<std::shared_ptr<Chunk>>&& chunks) {
+  resolve();
 #ifdef HYRISE_DEBUG  // (reference: DebugAssert, active in HYRISE_DEBUG builds)
   for (const auto& ch : chunks) {
     Assert(ch->column_count() == _defs.size(), "append_chunk: wrong number of columns");
@@ -163,6 +207,7 @@ void Table::append_chunks(std::vector<std::shared_ptr<Chunk>>&& chunks) {
 }
 
 AllTypeVariant Table::get_value(ColumnID column_id, uint64_t row) const {
+  resolve();
   for (const auto& c : _chunks) {
     if (row < c->size()) return (*c->get_column(column_id))[static_cast<ChunkOffset>(row)];
     row -= c->size();

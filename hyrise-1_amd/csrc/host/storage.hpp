@@ -15,6 +15,8 @@
 #include <cstring>
 #include <limits>
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <memory>
 #include <mutex>
 #include <optional>
@@ -378,10 +380,34 @@ class Table {
   std::vector<std::string> column_names() const;
 
   uint32_t max_chunk_size() const { return _max_chunk_size; }
-  uint32_t chunk_count() const { return static_cast<uint32_t>(_chunks.size()); }
+  uint32_t chunk_count() const {
+    resolve();
+    return static_cast<uint32_t>(_chunks.size());
+  }
   uint64_t row_count() const;
-  std::shared_ptr<Chunk> get_chunk(ChunkID id) const { return _chunks.at(id); }
-  const std::vector<std::shared_ptr<Chunk>>& chunks() const { return _chunks; }
+  std::shared_ptr<Chunk> get_chunk(ChunkID id) const {
+    resolve();
+    return _chunks.at(id);
+  }
+  const std::vector<std::shared_ptr<Chunk>>& chunks() const {
+    resolve();
+    return _chunks;
+  }
+
+  // A table whose chunks are produced on first access: an operator's output computed lazily, so that the consumer
+  // that reads it next can produce it as a by-product of its own work (a TableScan whose JoinHash evaluates the scan
+  // predicate inside its first radix pass, operators.cpp). Every accessor of the chunks resolves the table first; the
+  // producer runs once, on the first accessing thread. A consumer that produces the chunks itself takes the producer
+  // (take_pending) and installs them with fulfil().
+  struct Producer {
+    virtual ~Producer() = default;
+    virtual std::vector<std::shared_ptr<Chunk>> produce() = 0;
+  };
+  void set_pending(std::shared_ptr<Producer> producer);
+  std::shared_ptr<Producer> pending() const;  // the unresolved producer, or null
+  // takes the producer if it is still pending (null otherwise): the caller must fulfil() the table
+  std::shared_ptr<Producer> take_pending();
+  void fulfil(std::vector<std::shared_ptr<Chunk>>&& chunks);
 
   // reference table.cpp: append a row, opening a new chunk when the last one is full
   void append(const std::vector<AllTypeVariant>& values);
@@ -397,10 +423,19 @@ class Table {
   }
 
  private:
+  void resolve() const {
+    if (_pending_flag.load(std::memory_order_acquire)) resolve_slow();
+  }
+  void resolve_slow() const;
   TableColumnDefinitions _defs;
   TableType _type;
   uint32_t _max_chunk_size;
-  std::vector<std::shared_ptr<Chunk>> _chunks;
+  mutable std::vector<std::shared_ptr<Chunk>> _chunks;
+  mutable std::mutex _pending_m;
+  mutable std::condition_variable _pending_cv;
+  mutable std::shared_ptr<Producer> _pending;
+  mutable bool _taken = false;  // a consumer took the producer and will fulfil() the table
+  mutable std::atomic<bool> _pending_flag{false};
 };
 
 void release_drain();

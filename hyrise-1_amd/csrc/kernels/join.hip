@@ -844,22 +844,19 @@ __global__ __launch_bounds__(PART_THREADS) __attribute__((amdgpu_waves_per_eu(4)
 // Without a scan output (scan_out null: the caller wants the join output and the scan's counts only), part1_compact
 // writes the records of the rows taking part alone - after a selective prefilter a few percent of the scan's matches
 // (TPC-H 3's lineitem side: 6 of 323 M) - and the scan row of the histogram still counts every match.
-// Traffic per matched row is one record more than the single fused scatter, but both kernels are plain streams,
-// while the single kernel's load -> rank -> stage -> store chain per tile left it latency-bound. The gapped records are
-// SoA and 6 bytes for 4-byte keys (round 5): the key, and the row as its 16-bit offset inside the span (spans hold at
-// most GAP_SPAN_MAX rows) with GAP_NULL marking a scan match that does not take part - against 8-byte {key, row}
-// records, 2 bytes less written and read back per match (0.55 + 0.55 GB per SF100 headline step).
+// Traffic per matched row is one 8-byte record more than the single fused scatter, but both kernels are plain
+// streams, while the single kernel's load -> rank -> stage -> store chain per tile left it latency-bound. (Round 5
+// measured 6-byte SoA gapped records - key + 16-bit in-span offset - and reverted them: part1_spread 1.27-1.32 ->
+// 1.50 ms for the 2 bytes less per match, part1_compact unchanged.)
 // ------------------------------------------------------------------------------------------------------------
 constexpr uint32_t NULL_FLAG = 0x80000000u;  // payloads of filtered sides are row indexes < 2^31
-constexpr uint32_t GAP_NULL = 0x8000u;       // gapped record of a scan match whose row does not take part
-constexpr uint32_t GAP_SPAN_MAX = 0x8000u;   // rows per span of a filtered side (offsets below GAP_NULL)
 
 // PF: the side has a probe-side prefilter (s.bloom). A separate instance: the prefilter's lookups hold registers
 // (151 VGPRs, 3 waves per SIMD, against 96 without them) that the headline's unprefiltered probe side does not need.
 template <typename SD, typename T, typename H, int LP, int FK, bool PF>
 __global__ __launch_bounds__(PART_THREADS) void part1_compact(Side s, Digit dg, uint32_t n_digits,
                                                              uint32_t* __restrict__ hist, uint32_t* __restrict__ span_count,
-                                                             H* __restrict__ gap_keys, uint16_t* __restrict__ gap_offs) {
+                                                             Rec<H, uint32_t>* __restrict__ gap_out) {
   __shared__ uint32_t s_hist[257];
   __shared__ uint32_t s_sc[WAVE + 2];
   const uint64_t tile = xcd_tile(blockIdx.x, gridDim.x);  // span
@@ -869,8 +866,7 @@ __global__ __launch_bounds__(PART_THREADS) void part1_compact(Side s, Digit dg, 
   const uint32_t base = static_cast<uint32_t>(tile - s.chunk_tile_begin[c]) * (s.sub * PART_TILE);
   const uint32_t n_sub = min(s.sub, (ch.size - base + PART_TILE - 1) / PART_TILE);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE), lane = __lane_id();
-  H* out_keys = gap_keys + tile * (static_cast<uint64_t>(s.sub) * PART_TILE);
-  uint16_t* out_offs = gap_offs + tile * (static_cast<uint64_t>(s.sub) * PART_TILE);
+  Rec<H, uint32_t>* out = gap_out + tile * (static_cast<uint64_t>(s.sub) * PART_TILE);
   const bool scan_records = s.scan_out != nullptr;  // records of every scan match, or of the rows taking part only
   uint32_t run = 0;
   if (threadIdx.x == 0) s_sc[WAVE + 1] = 0;  // scan matches of the span (without scan records)
@@ -911,9 +907,10 @@ __global__ __launch_bounds__(PART_THREADS) void part1_compact(Side s, Digit dg, 
     for (int k = 0; k < PART_ITEMS; ++k) {
       const uint64_t b = __ballot((m >> k) & 1u);
       if ((m >> k) & 1u) {
-        const uint32_t o = run + s_sc[w * PART_ITEMS + k] + static_cast<uint32_t>(__popcll(b & lanemask_lt()));
-        out_keys[o] = keys[k];
-        out_offs[o] = static_cast<uint16_t>((rb - base + k * WAVE + lane) | (((act >> k) & 1u) ? 0u : GAP_NULL));
+        Rec<H, uint32_t> r;
+        r.key = keys[k];
+        r.payload = pays[k] | (((act >> k) & 1u) ? 0u : NULL_FLAG);
+        out[run + s_sc[w * PART_ITEMS + k] + static_cast<uint32_t>(__popcll(b & lanemask_lt()))] = r;
       }
     }
     run += s_sc[WAVE];
@@ -930,8 +927,7 @@ template <typename SD, typename H>
 __global__ __launch_bounds__(PART_THREADS) void part1_spread(Side s, Digit dg, NextDigit nd, int dbits,
                                                             uint32_t n_digits, const uint32_t* __restrict__ offsets,
                                                             const uint32_t* __restrict__ span_count,
-                                                            const H* __restrict__ gap_keys,
-                                                            const uint16_t* __restrict__ gap_offs,
+                                                            const Rec<H, uint32_t>* __restrict__ gap_in,
                                                             RecOut<H, uint32_t> out) {
   __shared__ uint32_t s_cnt[PART_WAVES][256];
   __shared__ uint32_t s_delta[256];
@@ -940,10 +936,8 @@ __global__ __launch_bounds__(PART_THREADS) void part1_spread(Side s, Digit dg, N
   const uint64_t tile = xcd_tile(blockIdx.x, gridDim.x);  // span
   const uint32_t n = span_count[tile];
   const uint32_t c = s.tile_chunk[tile];
-  const uint32_t base = static_cast<uint32_t>(tile - s.chunk_tile_begin[c]) * (s.sub * PART_TILE);  // in the chunk
-  const uint32_t row0 = static_cast<uint32_t>(s.chunks[c].row_begin) + base;  // row of the span's first row
-  const H* in_keys = gap_keys + tile * (static_cast<uint64_t>(s.sub) * PART_TILE);
-  const uint16_t* in_offs = gap_offs + tile * (static_cast<uint64_t>(s.sub) * PART_TILE);
+  const uint32_t row0 = static_cast<uint32_t>(s.chunks[c].row_begin);  // payload -> chunk offset
+  const Rec<H, uint32_t>* in = gap_in + tile * (static_cast<uint64_t>(s.sub) * PART_TILE);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   uint32_t run = threadIdx.x < n_digits ? offsets[threadIdx.x * s.n_tiles + tile] : 0u;
   const uint32_t srun = offsets[n_digits * s.n_tiles + tile] - offsets[n_digits * s.n_tiles];
@@ -956,20 +950,14 @@ __global__ __launch_bounds__(PART_THREADS) void part1_spread(Side s, Digit dg, N
     uint32_t dr[PART_ITEMS];
     uint32_t act = 0;
     const uint32_t r0 = j * PART_TILE + w * WAVE_SPAN + __lane_id();
-    uint32_t offs[PART_ITEMS];
 #pragma unroll
-    for (int k = 0; k < PART_ITEMS; ++k) {  // unconditional (see load_items)
-      recs[k].key = in_keys[min(r0 + k * WAVE, n - 1)];
-      offs[k] = in_offs[min(r0 + k * WAVE, n - 1)];
-    }
+    for (int k = 0; k < PART_ITEMS; ++k) recs[k] = in[min(r0 + k * WAVE, n - 1)];  // unconditional (see load_items)
 #pragma unroll
     for (int k = 0; k < PART_ITEMS; ++k) {
       const uint32_t i = r0 + k * WAVE;
-      const uint32_t off = offs[k] & (GAP_NULL - 1u);
-      recs[k].payload = row0 + off;
       if (i < n) {
-        if (s.scan_out != nullptr) s.scan_out[srun + i] = base + off;
-        if (!(offs[k] & GAP_NULL)) act |= 1u << k;
+        if (s.scan_out != nullptr) s.scan_out[srun + i] = (recs[k].payload & ~NULL_FLAG) - row0;
+        if (!(recs[k].payload & NULL_FLAG)) act |= 1u << k;
       }
     }
 #pragma unroll

@@ -458,4 +458,40 @@ __global__ void expand_row_ids_kernel(uint32_t chunk_id, const uint32_t* __restr
     out[i] = hy_row_id{chunk_id, offsets[i]};
 }
 
+// Matches per chunk of a dictionary predicate, counted only (no output): workgroup c counts chunk c (its rows' value
+// ids in 16-element vector loads, as scan_kernel reads them). The row count a consumer needs before a deferred scan
+// runs inside its join (the reference's swap rule compares the inputs' row counts, join_hash.cpp:55-76).
+template <typename E>
+__global__ __launch_bounds__(256) void scan_count_kernel(const hy_scan_chunk* __restrict__ chunks,
+                                                         uint32_t* __restrict__ counts) {
+  __shared__ uint32_t s_n;
+  if (threadIdx.x == 0) s_n = 0;
+  __syncthreads();
+  const hy_scan_chunk ch = chunks[blockIdx.x];
+  const E* base = static_cast<const E*>(ch.column.data);
+  const u32x4 no_nulls{0u, 0u, 0u, 0u};
+  const ScanConst<E> unused{};
+  uint32_t n = 0;
+  for (uint32_t row0 = threadIdx.x * 16u; row0 < ch.column.size; row0 += 256u * 16u) {
+    E v[16];
+    load16(base, row0, v);
+    n += static_cast<uint32_t>(__popc(match_mask<E, MODE_DICT, E>(ch, row0, v, no_nulls, unused)));
+  }
+  if (n) atomicAdd(&s_n, n);
+  __syncthreads();
+  if (threadIdx.x == 0) counts[blockIdx.x] = s_n;
+}
+
+// Every chunk's offset list at once (a fused TableScan's output, hy_scan_join_hash's out_offsets / out_chunk_begin):
+// workgroup c expands chunk c's range [chunk_begin[c], chunk_begin[c + 1]) with chunk id chunk_ids[c] (c when null).
+__global__ __launch_bounds__(256) void expand_chunk_row_ids_kernel(const uint32_t* __restrict__ offsets,
+                                                                   const uint64_t* __restrict__ chunk_begin,
+                                                                   const uint32_t* __restrict__ chunk_ids,
+                                                                   hy_row_id* __restrict__ out) {
+  const uint32_t c = blockIdx.x;
+  const uint64_t b = chunk_begin[c], e = chunk_begin[c + 1];
+  const uint32_t id = chunk_ids ? chunk_ids[c] : c;
+  for (uint64_t i = b + threadIdx.x; i < e; i += 256) out[i] = hy_row_id{id, offsets[i]};
+}
+
 }  // namespace hyk

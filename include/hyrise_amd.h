@@ -214,6 +214,15 @@ hy_status hy_table_scan_row_ids(const hy_scan_chunk* chunks, uint32_t n_chunks, 
                                 void* workspace, size_t workspace_bytes, hy_stream_t stream);
 
 /*
+ * Matches per chunk of a scan over DICT chunks, counted only (no output): counts[c] (device) = the rows of chunk c
+ * that hy_table_scan would emit. chunks: HOST array (one id width over the non-empty chunks, no IS NULL); workspace:
+ * n_chunks * sizeof(hy_scan_chunk) bytes. The row count a TableScan's consumer needs before the scan itself runs
+ * fused into that consumer (a JoinHash's swap rule compares its inputs' row counts, join_hash.cpp:55-76).
+ */
+hy_status hy_table_scan_count(const hy_scan_chunk* chunks, uint32_t n_chunks, uint32_t* counts, void* workspace,
+                              size_t workspace_bytes, hy_stream_t stream);
+
+/*
  * Scan over a ReferenceColumn (reference BaseSingleColumnTableScanImpl::handle_column(const ReferenceColumn&),
  * base_single_column_table_scan_impl.cpp:36-60): for each position i of pos_list (device RowIDs) whose RowID is
  * not NULL, the referenced value is read from referenced_chunks[row.chunk_id] and compared. Positions of matches
@@ -270,6 +279,12 @@ hy_status hy_pos_list_chunk_first_seen(const hy_row_id* pos_list, uint64_t n, ui
 /* out[i] = {chunk_id, offsets[i]} — expands a single-chunk offset list into reference RowIDs. */
 hy_status hy_expand_row_ids(uint32_t chunk_id, const uint32_t* offsets, uint64_t n, hy_row_id* out,
                             hy_stream_t stream);
+/* The same for the offset lists of n_chunks chunks in one launch (a fused TableScan's output of hy_scan_join_hash):
+ * out[i] = {chunk_ids[c], offsets[i]} for i in [chunk_begin[c], chunk_begin[c + 1]). All device arrays; chunk_ids
+ * NULL means chunk id c. Replaces the per-chunk PosList materialisation of table_scan.cpp:87-99 for a scan whose
+ * matches its consumer's join computed. */
+hy_status hy_expand_chunk_row_ids(const uint32_t* offsets, const uint64_t* chunk_begin, const uint32_t* chunk_ids,
+                                  uint32_t n_chunks, hy_row_id* out, hy_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------------------------
  * String scans (std::string columns; reference SingleColumnTableScanImpl / LikeTableScanImpl / IsNullTableScanImpl

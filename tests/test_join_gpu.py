@@ -58,6 +58,33 @@ def test_orders_lineitem_join(hy, oracle, n_orders, chunk):
     assert_identical(j2.get_output(), exp2)
 
 
+@pytest.mark.parametrize("fuse", ["1", "0"])
+@pytest.mark.parametrize("order", ["join_first", "scan_first", "semi"])
+def test_deferred_scan_fused_into_join(hy, oracle, monkeypatch, fuse, order):
+    """TableScan -> JoinHash through the operators: a scan over a data table is deferred (its output produced on
+    first access), and the JoinHash that takes it as its probe side evaluates the predicate in its first radix pass
+    and builds the scan's output from the join's by-product (HY_OP_FUSE_SCAN=0: the scan runs when it executes).
+    Both outputs equal the oracle's whatever is read first; a Semi join (not fused) produces the scan on access."""
+    monkeypatch.setenv("HY_OP_FUSE_SCAN", fuse)
+    rng = np.random.default_rng(7)
+    orders, lineitem = orders_lineitem(hy, 30_000, 10_000, rng)
+    hy.encode_all_chunks(lineitem, hy.EncodingType.Dictionary)
+    o, l = wrap(hy, orders), wrap(hy, lineitem)
+    s = hy.TableScan(l, 1, hy.PredicateCondition.LessThan, 24)
+    s.execute()
+    exp_s = oracle.table_scan(lineitem, 1, hy.PredicateCondition.LessThan, 24, [])
+    if order == "scan_first":  # the scan's output produced before the join reads it
+        assert_identical(s.get_output(), exp_s)
+    mode = hy.JoinMode.Semi if order == "semi" else hy.JoinMode.Inner
+    j = hy.JoinHash(o, s, mode, (0, 0), hy.PredicateCondition.Equals)
+    j.execute()
+    exp_j, bits = oracle.join_hash(orders, exp_s, mode, (0, 0))
+    assert j.used_radix_bits() == bits
+    assert_identical(j.get_output(), exp_j)
+    assert_identical(s.get_output(), exp_s)
+    assert s.get_output().row_count() == exp_s.row_count()
+
+
 @pytest.mark.parametrize("lds_budget", [None, 1024])
 @pytest.mark.parametrize("mode", ["Inner", "Left", "Right", "Semi", "Anti"])
 def test_duplicates_and_nulls(hy, oracle, mode, lds_budget, monkeypatch):
