@@ -22,7 +22,7 @@ run() {  # name, bench args
   timeout -s KILL 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run -f csv -- \
     python3 "$R/bench.py" "$@" --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/bench_under_trace.json" 2> "$OUT/trace.err"
   for c in FETCH_SIZE WRITE_SIZE; do
-    timeout -s KILL 400 rocprofv3 --pmc $c --kernel-include-regex 'hyk::' -d "$OUT/$c" -o run -f csv -- \
+    timeout -s KILL 400 rocprofv3 --pmc $c --kernel-include-regex 'hyk::|agg_jit' -d "$OUT/$c" -o run -f csv -- \
       python3 "$R/bench.py" "$@" --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/bench_under_$c.json" 2> "$OUT/$c.err"
   done
   python3 "$R/tools/summarize_rocprof.py" "$OUT" 5 > "$R/gpurun_out/${TAG}_rocprof_${name}_summary.json"
