@@ -279,6 +279,8 @@ def main_q3(args):
                  expr_column(capi, 4, F32), capi.ExprNode(capi.HY_EXPR_SUB, F32, F32, 0, 0),
                  capi.ExprNode(capi.HY_EXPR_MUL, F32, F32, 0, 0)]]
     programs = [(capi.ExprNode * len(p))(*p) for p in programs]
+    prog_ptrs = (ctypes.c_void_p * len(programs))(*[ctypes.addressof(p) for p in programs])
+    prog_lens = (ctypes.c_uint32 * len(programs))(*[len(p) for p in programs])
     groupby = (ctypes.c_int32 * 3)(0, 1, 2)
     agg_defs = (capi.AggDef * 1)(capi.AggDef(capi.HY_AGG_SUM, 3))
     agg_params = capi.AggParams(groupby, 3, agg_defs, 1, 0)
@@ -321,9 +323,10 @@ def main_q3(args):
             state["proj_rows"] = pairs2
             state["proj"] = torch.empty(4, pairs2 + 64, dtype=torch.int32, device=dev)
         proj = state["proj"]
-        for j, prog in enumerate(programs):
-            capi.check(L.hy_projection(ctypes.byref(pin), prog, len(prog), proj[j].data_ptr(), None, pws.data_ptr(),
-                                       pws.numel(), stream), "hy_projection")
+        # the four SELECT-list expressions in one launch (the reference's Projection evaluates them per chunk)
+        outs = (ctypes.c_void_p * 4)(*[proj[j].data_ptr() for j in range(4)])
+        capi.check(L.hy_projection_multi(ctypes.byref(pin), prog_ptrs, prog_lens, 4, outs, None, pws.data_ptr(),
+                                         pws.numel(), stream), "hy_projection_multi")
         mark("projection")
         # Aggregate over the projection's output (a data table with the join output's chunking)
         rb = np.concatenate([[0], np.cumsum(n2.astype(np.int64))])[:-1].astype(np.uint64)

@@ -162,6 +162,9 @@ _sigs = {
     "hy_projection": (ctypes.c_int, [ctypes.POINTER(AggInput), ctypes.POINTER(ExprNode), ctypes.c_uint32,
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                      ctypes.c_void_p]),
+    "hy_projection_multi": (ctypes.c_int, [ctypes.POINTER(AggInput), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                           ctypes.c_void_p]),
     "hy_agg_float_sum": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32, ctypes.c_int32,
                                         ctypes.c_uint64, ctypes.POINTER(ctypes.c_double)]),
     "hy_agg_float_sums": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,

@@ -907,6 +907,8 @@ struct AggWs {
   hy_scan_chunk* filter;         // fused TableScan predicate chunks
   void* mat_values[hyk::AGG_MAX_COLUMNS];    // materialised expression columns
   uint8_t* mat_nulls[hyk::AGG_MAX_COLUMNS];
+  hyk::ExprProgram* mat_progs;   // their programs and outputs (one projection launch for all of them)
+  hyk::ProjOut* mat_outs;
   uint32_t* state;
   unsigned long long* records;
   uint32_t* dstate;
@@ -934,6 +936,8 @@ void carve(Carver& cv, const hy_agg_input* in, const AggPlan& plan, AggWs* w) {
     w->mat_values[j] = plan.materialize ? cv.take<uint64_t>(std::max<uint64_t>(2, plan.rows)) : nullptr;
     w->mat_nulls[j] = plan.materialize ? cv.take<uint8_t>(std::max<uint64_t>(16, plan.rows)) : nullptr;
   }
+  w->mat_progs = cv.take<hyk::ExprProgram>(std::max<size_t>(1, plan.expr_cols.size()));
+  w->mat_outs = cv.take<hyk::ProjOut>(std::max<size_t>(1, plan.expr_cols.size()));
   w->misc = cv.take<uint32_t>(64);
   if (plan.dense_groups) {
     w->state = nullptr;
@@ -1068,14 +1072,21 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
   // expression columns outside the fused kernel: materialised (projection kernel over the same input), then read as
   // data columns with NULL flags
   std::vector<std::vector<hy_column_chunk>> mat_chunks(plan.expr_cols.size());
-  for (uint32_t e = 0; e < plan.expr_cols.size() && plan.materialize && plan.rows; ++e) {
-    const uint32_t j = plan.expr_cols[e];
+  if (!plan.expr_cols.empty() && plan.materialize && plan.rows) {
+    std::vector<hyk::ProjOut> outs(plan.expr_cols.size());
+    for (uint32_t e = 0; e < plan.expr_cols.size(); ++e)
+      outs[e] = hyk::ProjOut{w.mat_progs + e, w.mat_values[plan.expr_cols[e]], w.mat_nulls[plan.expr_cols[e]]};
+    HY_STAGE(w.mat_progs, plan.exprs.data(), sizeof(hyk::ExprProgram) * plan.expr_cols.size(), s);
+    HY_STAGE(w.mat_outs, outs.data(), sizeof(hyk::ProjOut) * outs.size(), s);
     const uint32_t items = hyk::flat_items(plan.rows);
     const uint64_t tile_rows = uint64_t(hyk::AGG_THREADS) * items;
     hipLaunchKernelGGL(hyk::projection_kernel, dim3(static_cast<uint32_t>((plan.rows + tile_rows - 1) / tile_rows)),
-                       dim3(hyk::AGG_THREADS), 0, s, d, plan.exprs[e], w.mat_values[j], w.mat_nulls[j], plan.rows,
+                       dim3(hyk::AGG_THREADS), 0, s, d, w.mat_outs, static_cast<uint32_t>(outs.size()), plan.rows,
                        items);
     HY_HIP(hipGetLastError());
+  }
+  for (uint32_t e = 0; e < plan.expr_cols.size() && plan.materialize && plan.rows; ++e) {
+    const uint32_t j = plan.expr_cols[e];
     const int bytes = (plan.exprs[e].out_type == HY_TYPE_INT64 || plan.exprs[e].out_type == HY_TYPE_DOUBLE) ? 8 : 4;
     auto& chs = mat_chunks[e];
     chs.resize(input->n_chunks);
@@ -1249,6 +1260,8 @@ struct ProjWs {
   uint64_t* row_begin;
   const hy_row_id** pos_lists;
   hy_column_chunk* chunks[hyk::AGG_MAX_COLUMNS];
+  hyk::ExprProgram* progs;  // HY_PROJ_MAX_OUTPUTS
+  hyk::ProjOut* outs;
 };
 
 void carve_proj(Carver& cv, const hy_agg_input* in, ProjWs* w) {
@@ -1256,6 +1269,51 @@ void carve_proj(Carver& cv, const hy_agg_input* in, ProjWs* w) {
   w->pos_lists = cv.take<const hy_row_id*>(std::max<uint64_t>(1, uint64_t(in->n_pos_groups) * in->n_chunks));
   for (uint32_t j = 0; j < in->n_columns; ++j)
     w->chunks[j] = cv.take<hy_column_chunk>(std::max<uint32_t>(1, in->columns[j].n_chunks));
+  w->progs = cv.take<hyk::ExprProgram>(HY_PROJ_MAX_OUTPUTS);
+  w->outs = cv.take<hyk::ProjOut>(HY_PROJ_MAX_OUTPUTS);
+}
+
+// A postfix program checked against the input (stack depth, column indexes, types) into its kernel form.
+hy_status compile_program(const hy_agg_input* input, const hy_expr_node* program, uint32_t n_nodes,
+                          hyk::ExprProgram* prog) {
+  if (!program || n_nodes == 0 || n_nodes > HY_EXPR_MAX_NODES) return fail(HY_ERR_INVALID_ARGUMENT, "program size");
+  *prog = hyk::ExprProgram{};
+  int depth = 0;
+  for (uint32_t i = 0; i < n_nodes; ++i) {
+    const hy_expr_node& nd = program[i];
+    prog->nodes[i] = nd;
+    const bool typed = nd.type >= HY_TYPE_INT32 && nd.type <= HY_TYPE_DOUBLE;
+    switch (nd.kind) {
+      case HY_EXPR_COLUMN:
+        if (nd.column < 0 || nd.column >= static_cast<int32_t>(input->n_columns))
+          return fail(HY_ERR_INVALID_ARGUMENT, "expression column");
+        if (nd.type != input->columns[nd.column].value_type) return fail(HY_ERR_INVALID_ARGUMENT, "column node type");
+        ++depth;
+        break;
+      case HY_EXPR_VALUE:
+        if (!typed && nd.type != 0) return fail(HY_ERR_INVALID_ARGUMENT, "literal type");
+        ++depth;
+        break;
+      case HY_EXPR_ADD:
+      case HY_EXPR_SUB:
+      case HY_EXPR_MUL:
+      case HY_EXPR_DIV:
+      case HY_EXPR_MOD:
+        if (depth < 2) return fail(HY_ERR_INVALID_ARGUMENT, "expression stack underflow");
+        if (!typed || nd.calc_type < HY_TYPE_INT32 || nd.calc_type > HY_TYPE_DOUBLE)
+          return fail(HY_ERR_INVALID_ARGUMENT, "arithmetic node types");
+        --depth;
+        break;
+      default:
+        return fail(HY_ERR_INVALID_ARGUMENT, "expression node kind");
+    }
+    if (depth > HY_EXPR_MAX_DEPTH) return fail(HY_ERR_UNSUPPORTED, "expression deeper than HY_EXPR_MAX_DEPTH");
+  }
+  if (depth != 1) return fail(HY_ERR_INVALID_ARGUMENT, "program does not leave one value");
+  prog->n_nodes = n_nodes;
+  prog->out_type = program[n_nodes - 1].type;
+  if (prog->out_type == 0) return fail(HY_ERR_UNSUPPORTED, "an all-NULL expression has no column type");
+  return HY_OK;
 }
 
 hy_status check_proj_input(const hy_agg_input* in) {
@@ -1289,55 +1347,26 @@ hy_status hy_projection_workspace_size(const hy_agg_input* input, size_t* bytes)
   return HY_OK;
 }
 
-hy_status hy_projection(const hy_agg_input* input, const hy_expr_node* program, uint32_t n_nodes, void* out_values,
-                        uint8_t* out_nulls, void* workspace, size_t workspace_bytes, hy_stream_t stream) {
+hy_status hy_projection_multi(const hy_agg_input* input, const hy_expr_node* const* programs, const uint32_t* n_nodes,
+                              uint32_t n_programs, void* const* out_values, uint8_t* const* out_nulls, void* workspace,
+                              size_t workspace_bytes, hy_stream_t stream) {
   hy_status st = check_proj_input(input);
   if (st != HY_OK) return st;
-  if (!program || n_nodes == 0 || n_nodes > HY_EXPR_MAX_NODES) return fail(HY_ERR_INVALID_ARGUMENT, "program size");
-  // validate the postfix program: stack depth, column indexes, types
-  hyk::ExprProgram prog{};
-  int depth = 0;
-  for (uint32_t i = 0; i < n_nodes; ++i) {
-    const hy_expr_node& nd = program[i];
-    prog.nodes[i] = nd;
-    const bool typed = nd.type >= HY_TYPE_INT32 && nd.type <= HY_TYPE_DOUBLE;
-    switch (nd.kind) {
-      case HY_EXPR_COLUMN:
-        if (nd.column < 0 || nd.column >= static_cast<int32_t>(input->n_columns))
-          return fail(HY_ERR_INVALID_ARGUMENT, "expression column");
-        if (nd.type != input->columns[nd.column].value_type) return fail(HY_ERR_INVALID_ARGUMENT, "column node type");
-        ++depth;
-        break;
-      case HY_EXPR_VALUE:
-        if (!typed && nd.type != 0) return fail(HY_ERR_INVALID_ARGUMENT, "literal type");
-        ++depth;
-        break;
-      case HY_EXPR_ADD:
-      case HY_EXPR_SUB:
-      case HY_EXPR_MUL:
-      case HY_EXPR_DIV:
-      case HY_EXPR_MOD:
-        if (depth < 2) return fail(HY_ERR_INVALID_ARGUMENT, "expression stack underflow");
-        if (!typed || nd.calc_type < HY_TYPE_INT32 || nd.calc_type > HY_TYPE_DOUBLE)
-          return fail(HY_ERR_INVALID_ARGUMENT, "arithmetic node types");
-        --depth;
-        break;
-      default:
-        return fail(HY_ERR_INVALID_ARGUMENT, "expression node kind");
-    }
-    if (depth > HY_EXPR_MAX_DEPTH) return fail(HY_ERR_UNSUPPORTED, "expression deeper than HY_EXPR_MAX_DEPTH");
+  if (n_programs == 0 || n_programs > HY_PROJ_MAX_OUTPUTS || !programs || !n_nodes || !out_values)
+    return fail(HY_ERR_INVALID_ARGUMENT, "programs");
+  hyk::ExprProgram progs[HY_PROJ_MAX_OUTPUTS];
+  for (uint32_t i = 0; i < n_programs; ++i) {
+    st = compile_program(input, programs[i], n_nodes[i], &progs[i]);
+    if (st != HY_OK) return st;
   }
-  if (depth != 1) return fail(HY_ERR_INVALID_ARGUMENT, "program does not leave one value");
-  prog.n_nodes = n_nodes;
-  prog.out_type = program[n_nodes - 1].type;
-  if (prog.out_type == 0) return fail(HY_ERR_UNSUPPORTED, "an all-NULL expression has no column type");
   std::vector<uint64_t> row_begin(input->n_chunks + 1, 0);
   for (uint32_t c = 0; c < input->n_chunks; ++c) row_begin[c + 1] = row_begin[c] + input->chunk_sizes[c];
   const uint64_t rows = row_begin[input->n_chunks];
   if (rows == 0) return HY_OK;
+  for (uint32_t i = 0; i < n_programs; ++i)
+    if (!out_values[i]) return fail(HY_ERR_INVALID_ARGUMENT, "out_values");
   const uint32_t items = hyk::flat_items(rows);  // tiles over global rows
   const uint64_t tiles = (rows + uint64_t(hyk::AGG_THREADS) * items - 1) / (uint64_t(hyk::AGG_THREADS) * items);
-  if (!out_values) return fail(HY_ERR_INVALID_ARGUMENT, "out_values");
   hipStream_t s = S(stream);
   Carver cv{static_cast<char*>(workspace), workspace_bytes};
   ProjWs w;
@@ -1346,6 +1375,10 @@ hy_status hy_projection(const hy_agg_input* input, const hy_expr_node* program, 
   HY_STAGE(w.row_begin, row_begin.data(), 8 * row_begin.size(), s);
   const uint64_t n_pl = uint64_t(input->n_pos_groups) * input->n_chunks;
   if (n_pl) HY_STAGE(w.pos_lists, input->pos_lists, sizeof(void*) * n_pl, s);
+  hyk::ProjOut outs[HY_PROJ_MAX_OUTPUTS];
+  for (uint32_t i = 0; i < n_programs; ++i) outs[i] = hyk::ProjOut{w.progs + i, out_values[i], out_nulls ? out_nulls[i] : nullptr};
+  HY_STAGE(w.progs, progs, sizeof(hyk::ExprProgram) * n_programs, s);
+  HY_STAGE(w.outs, outs, sizeof(hyk::ProjOut) * n_programs, s);
   hyk::AggDesc d{};
   d.n_cols = input->n_columns;
   d.n_pos_groups = input->n_pos_groups;
@@ -1364,11 +1397,17 @@ hy_status hy_projection(const hy_agg_input* input, const hy_expr_node* program, 
   d.pos_lists = w.pos_lists;
   d.chunk_row_begin = w.row_begin;
   KTimer t("projection", s, rows);
-  hipLaunchKernelGGL(hyk::projection_kernel, dim3(static_cast<uint32_t>(tiles)), dim3(hyk::AGG_THREADS), 0, s, d, prog,
-                     out_values, out_nulls, rows, items);
+  hipLaunchKernelGGL(hyk::projection_kernel, dim3(static_cast<uint32_t>(tiles)), dim3(hyk::AGG_THREADS), 0, s, d, w.outs,
+                     n_programs, rows, items);
   t.done();
   HY_HIP(hipGetLastError());
   return HY_OK;  // asynchronous: the descriptors went through the pinned staging ring
+}
+
+hy_status hy_projection(const hy_agg_input* input, const hy_expr_node* program, uint32_t n_nodes, void* out_values,
+                        uint8_t* out_nulls, void* workspace, size_t workspace_bytes, hy_stream_t stream) {
+  // (a null out_values is rejected after the empty-input early return, as hy_projection_multi checks it)
+  return hy_projection_multi(input, &program, &n_nodes, 1, &out_values, &out_nulls, workspace, workspace_bytes, stream);
 }
 
 hy_status hy_agg_float_sum(const uint64_t* limbs, uint32_t n_limbs, int32_t emin, uint64_t special, double* out) {

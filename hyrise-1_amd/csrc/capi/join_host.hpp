@@ -53,6 +53,7 @@ struct JoinKnobs {
   bool onepass = false;                // HY_ONEPASS
   uint64_t onepass_cap_div = 8;        // HY_ONEPASS_CAP_DIV
   uint64_t onepass_cap = 0;            // HY_ONEPASS_CAP (0: computed)
+  bool filter_buckets = true;          // HY_FILTER_BUCKETS: prefilter words set per LDS region (0: global atomics)
 };
 
 inline JoinKnobs knobs_from_env() {
@@ -72,6 +73,7 @@ inline JoinKnobs knobs_from_env() {
   k.onepass = num("HY_ONEPASS", 0) != 0;
   k.onepass_cap_div = static_cast<uint64_t>(std::max<long long>(1, num("HY_ONEPASS_CAP_DIV", 8)));
   k.onepass_cap = static_cast<uint64_t>(std::max<long long>(0, num("HY_ONEPASS_CAP", 0)));
+  k.filter_buckets = num("HY_FILTER_BUCKETS", 1) != 0;
   return k;
 }
 
@@ -141,9 +143,35 @@ inline uint64_t bloom_words(uint64_t build_rows, uint64_t probe_rows) {
 inline uint64_t range_bitmap_words(uint64_t build_rows) {
   return std::min<uint64_t>(2 * build_rows + 1024, uint64_t(1) << 28);
 }
-// The prefilter area: a 64-byte header (hyk::FilterHdr), then the larger of the two filters' words.
+// The prefilter built per LDS region (hyk::filter_bucket_*) when its words allow it: the count / scatter grid, the
+// largest region shift the device can pick (it sizes the set kernel's LDS), an upper bound of the regions and the
+// region x workgroup matrix's length. blocks == 0: the global-atomic build (filter_clear + filter_set).
+struct FilterBuckets {
+  uint32_t blocks = 0, shift = 0, bins = 0;
+  uint64_t scan_len = 0;
+};
+inline FilterBuckets filter_buckets(uint64_t bloom_n, uint64_t build_rows) {
+  FilterBuckets f;
+  if (!bloom_n || !knobs().filter_buckets) return f;
+  const uint64_t maxw = std::max(bloom_n, range_bitmap_words(build_rows));
+  uint32_t shift = hyk::FB_SHIFT_MIN;
+  while (((maxw + (uint64_t(1) << shift) - 1) >> shift) > hyk::FB_BINS) ++shift;
+  if (shift > hyk::FB_SHIFT_MAX) return f;
+  f.shift = shift;
+  // (the device may pick a smaller shift for a narrower key range: up to FB_BINS regions of the smallest size)
+  f.bins = static_cast<uint32_t>(std::min<uint64_t>(hyk::FB_BINS, (maxw + (uint64_t(1) << hyk::FB_SHIFT_MIN) - 1) >>
+                                                                      hyk::FB_SHIFT_MIN));
+  f.blocks = static_cast<uint32_t>(std::clamp<uint64_t>(build_rows / 16384, 1, 256));
+  f.scan_len = uint64_t(f.bins) * f.blocks;
+  return f;
+}
+// The prefilter area: a 64-byte header (hyk::FilterHdr), then the larger of the two filters' words, then the bucketed
+// build's matrix (twice: counts and offsets), its items (one word per build row) and two 64-bit counters.
 inline uint64_t prefilter_words(uint64_t bloom_n, uint64_t build_rows) {
-  return bloom_n ? 16 + std::max(bloom_n, range_bitmap_words(build_rows)) : 1;
+  if (!bloom_n) return 1;
+  const FilterBuckets f = filter_buckets(bloom_n, build_rows);
+  const uint64_t fb = f.blocks ? 2 * f.scan_len + build_rows + 8 : 0;
+  return 16 + ((std::max(bloom_n, range_bitmap_words(build_rows)) + 3) & ~uint64_t(3)) + fb;
 }
 
 inline uint32_t sub2() {
@@ -1222,7 +1250,8 @@ size_t classic_join_bytes(const SidePlan& bp, const SidePlan& pp, uint32_t bits)
   pass_sizes(sizes_of(bp, db, kb), w, 1, &ha, &t);
   pass_sizes(sizes_of(pp, db, kp), w, 1, &hb, &t);
   Common c, cb;  // (join_typed: the probe side's and the build side's)
-  carve_common(cv, std::max({ha, hb, (uint64_t(1) << bits) + 1}), bits, &c);
+  const uint64_t fb_scan = filter_buckets(bloom_words(bp.n_rows, pp.n_rows), bp.n_rows).scan_len;
+  carve_common(cv, std::max({ha, hb, (uint64_t(1) << bits) + 1, fb_scan}), bits, &c);
   carve_common(cv, std::max({ha, hb, (uint64_t(1) << bits) + 1}), bits, &cb);
   cv.take<uint32_t>(prefilter_words(bloom_words(bp.n_rows, pp.n_rows), bp.n_rows));
   return cv.used + 256;
@@ -1615,12 +1644,18 @@ hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join
   pass_sizes(sizes_of(bp, db, blocks[0]), w, 1, &ha, &t);
   pass_sizes(sizes_of(pp, db, blocks[1]), w, 1, &hb2, &t);
   Common c{}, cb{};  // c: the probe side and the partition join; cb: the build side (it may run concurrently)
-  carve_common(cv, std::max({ha, hb2, (uint64_t(1) << bits) + 1}), bits, &c);
-  carve_common(cv, std::max({ha, hb2, (uint64_t(1) << bits) + 1}), bits, &cb);
   const uint64_t bloom_n = bloom_words(bp.n_rows, pp.n_rows);
+  const FilterBuckets fbk = filter_buckets(bloom_n, bp.n_rows);
+  carve_common(cv, std::max({ha, hb2, (uint64_t(1) << bits) + 1, fbk.scan_len}), bits, &c);
+  carve_common(cv, std::max({ha, hb2, (uint64_t(1) << bits) + 1}), bits, &cb);
   uint32_t* filter_area = cv.take<uint32_t>(prefilter_words(bloom_n, bp.n_rows));
   auto* filter_hdr = reinterpret_cast<hyk::FilterHdr*>(filter_area);
   uint32_t* bloom = filter_area + 16;
+  // the bucketed build's scratch after the filter words (prefilter_words)
+  uint32_t* fb_hist = bloom_n ? bloom + ((std::max(bloom_n, range_bitmap_words(bp.n_rows)) + 3) & ~uint64_t(3)) : nullptr;
+  uint32_t* fb_off = fb_hist ? fb_hist + fbk.scan_len : nullptr;
+  uint32_t* fb_items = fb_off ? fb_off + fbk.scan_len : nullptr;
+  uint64_t* fb_count = fb_items ? reinterpret_cast<uint64_t*>(fb_items + ((bp.n_rows + 1) & ~uint64_t(1))) : nullptr;
   if (!cv.ok) return fail(HY_ERR_WORKSPACE, "join workspace too small");
   if (upload_side(bp, bb, s) || upload_side(pp, pb, s)) return HY_ERR_DEVICE;
   const bool keep_nulls = prm->mode == HY_JOIN_LEFT || prm->mode == HY_JOIN_RIGHT;
@@ -1702,10 +1737,25 @@ hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join
       if (range_filter)
         hipLaunchKernelGGL(hyk::filter_range<H>, dim3(static_cast<uint32_t>(std::min<uint64_t>(grid_for(p.n_rows, 256), 1024))),
                            dim3(256), 0, s, recs[0], b.total, filter_hdr);
-      hipLaunchKernelGGL(hyk::filter_clear<H>, dim3(static_cast<uint32_t>(std::min<uint64_t>(grid_for(std::max(bloom_n, rw) / 4, 256), 4096))),
-                         dim3(256), 0, s, filter_hdr, bloom, rw, bloom_n);
-      hipLaunchKernelGGL(hyk::filter_set<H>, dim3(static_cast<uint32_t>(std::min<uint64_t>(grid_for(p.n_rows, 256), 4096))),
-                         dim3(256), 0, s, recs[0], b.total, filter_hdr, bloom, rw, static_cast<uint32_t>(bloom_n - 1));
+      const uint32_t bmask = static_cast<uint32_t>(bloom_n - 1);
+      if (fbk.blocks) {  // per LDS region: count, scan, scatter, set (the set also writes the words no key sets)
+        const dim3 fbt(hyk::FB_THREADS);
+        hipLaunchKernelGGL(hyk::filter_bucket_count<H>, dim3(fbk.blocks), fbt, 0, s, recs[0], b.total, filter_hdr, rw,
+                           bloom_n, bmask, fb_hist, fb_count);
+        HY_HIP(hipGetLastError());
+        if (hy_status st = run_scan(fb_hist, fb_off, fbk.scan_len, c, s, fb_count + 1, fb_count, fbk.blocks); st != HY_OK)
+          return st;
+        hipLaunchKernelGGL(hyk::filter_bucket_scatter<H>, dim3(fbk.blocks), fbt, 0, s, recs[0], b.total, filter_hdr, rw,
+                           bloom_n, bmask, fb_off, fb_items);
+        HY_HIP(hipGetLastError());
+        hipLaunchKernelGGL(hyk::filter_bucket_set<H>, dim3(fbk.bins), fbt, static_cast<size_t>(4u << fbk.shift), s,
+                           filter_hdr, rw, bloom_n, fb_off, fb_count + 1, fbk.blocks, fb_items, bloom);
+      } else {
+        hipLaunchKernelGGL(hyk::filter_clear<H>, dim3(static_cast<uint32_t>(std::min<uint64_t>(grid_for(std::max(bloom_n, rw) / 4, 256), 4096))),
+                           dim3(256), 0, s, filter_hdr, bloom, rw, bloom_n);
+        hipLaunchKernelGGL(hyk::filter_set<H>, dim3(static_cast<uint32_t>(std::min<uint64_t>(grid_for(p.n_rows, 256), 4096))),
+                           dim3(256), 0, s, recs[0], b.total, filter_hdr, bloom, rw, bmask);
+      }
       kt_.done();
       HY_HIP(hipGetLastError());
     }

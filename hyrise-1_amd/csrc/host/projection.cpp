@@ -278,14 +278,26 @@ void compile(const AbstractExpression& e, const Table& in, ExprInput& ei, std::v
   Assert(prog.size() <= HY_EXPR_MAX_NODES, "hyrise-amd: expression has too many nodes for the device projection");
 }
 
-// Evaluates one expression over all chunks of `in` into one ValueColumn per chunk.
-std::vector<std::shared_ptr<BaseColumn>> evaluate_on_device(const AbstractExpression& e, const Table& in) {
+// Distinct input columns an expression's leaves reference, beyond those already in `ei`.
+void new_columns(const AbstractExpression& e, const ExprInput& ei, std::vector<ColumnID>& seen) {
+  if (e.type == ExpressionType::PQPColumn) {
+    const ColumnID c = static_cast<const PQPColumnExpression&>(e).column_id;
+    if (std::find(ei.column_ids.begin(), ei.column_ids.end(), c) == ei.column_ids.end() &&
+        std::find(seen.begin(), seen.end(), c) == seen.end())
+      seen.push_back(c);
+  } else if (e.type == ExpressionType::Arithmetic) {
+    const auto& a = static_cast<const ArithmeticExpression&>(e);
+    new_columns(*a.left_operand(), ei, seen);
+    new_columns(*a.right_operand(), ei, seen);
+  }
+}
+
+// Evaluates expressions over all chunks of `in` into one ValueColumn per chunk each: one hy_projection_multi launch
+// per batch (the batch's expressions share the input columns, at most HY_AGG_MAX_COLUMNS, and RowID reads), one
+// stream synchronisation per batch.
+std::vector<std::vector<std::shared_ptr<BaseColumn>>> evaluate_on_device(
+    const std::vector<const AbstractExpression*>& exprs, const Table& in) {
   hy_stream_t s = operator_stream();
-  ExprInput ei;
-  std::vector<hy_expr_node> prog;
-  compile(e, in, ei, prog);
-  const DataType type = e.data_type();
-  const bool nullable = e.is_nullable();
   const uint32_t n_chunks = in.chunk_count();
   std::vector<uint32_t> sizes(n_chunks);
   std::vector<uint64_t> row_begin(n_chunks + 1, 0);
@@ -294,65 +306,97 @@ std::vector<std::shared_ptr<BaseColumn>> evaluate_on_device(const AbstractExpres
     row_begin[c + 1] = row_begin[c] + sizes[c];
   }
   const uint64_t rows = row_begin[n_chunks];
-  for (size_t j = 0; j < ei.columns.size(); ++j) {
-    ei.columns[j].chunks = ei.chunks[j].data();
-    ei.columns[j].n_chunks = static_cast<uint32_t>(ei.chunks[j].size());
-  }
-  std::vector<const hy_row_id*> pos_ptrs;
-  for (const auto& lists : ei.group_lists)
-    for (const auto& pl : lists) pos_ptrs.push_back(device_pos_list(*pl)->ptr());
-  hy_agg_input hin{};
-  hin.n_chunks = n_chunks;
-  hin.chunk_sizes = sizes.data();
-  hin.pos_lists = pos_ptrs.data();
-  hin.n_pos_groups = static_cast<uint32_t>(ei.group_lists.size());
-  hin.columns = ei.columns.data();
-  hin.n_columns = static_cast<uint32_t>(ei.columns.size());
-  Assert(hin.n_pos_groups <= HY_AGG_MAX_POS_GROUPS, "hyrise-amd: too many PosList groups for the device projection");
-
-  const size_t width = data_type_size(type);
-  auto values = std::make_shared<DeviceBuffer>(std::max<uint64_t>(rows, 1) * width + 16);
-  auto nulls = nullable ? std::make_shared<DeviceBuffer>(std::max<uint64_t>(rows, 1) + 16) : nullptr;
-  size_t ws_bytes = 0;
-  hy_check(hy_projection_workspace_size(&hin, &ws_bytes), "hy_projection_workspace_size");
-  DeviceBuffer ws(ws_bytes, s);
-  hy_check(hy_projection(&hin, prog.data(), static_cast<uint32_t>(prog.size()), values->get(),
-                         nulls ? nulls->as<uint8_t>() : nullptr, ws.get(), ws_bytes, s),
-           "hy_projection");
-
-  std::vector<std::shared_ptr<BaseColumn>> out;
-  resolve_data_type(type, [&](auto tag) {
-    using T = decltype(tag);
-    if constexpr (!std::is_same_v<T, std::string>) {
-      std::vector<T> all(rows);
-      std::vector<uint8_t> all_nulls(nullable ? rows : 0);
-      if (rows) hy_check(hy_memcpy_dtoh(all.data(), values->get(), rows * sizeof(T), s), "dtoh");
-      if (nullable && rows) hy_check(hy_memcpy_dtoh(all_nulls.data(), nulls->get(), rows, s), "dtoh");
-      hy_check(hy_stream_synchronize(s), "sync");
-      for (ChunkID c = 0; c < n_chunks; ++c) {
-        std::vector<T> v(all.begin() + row_begin[c], all.begin() + row_begin[c + 1]);
-        std::optional<std::vector<uint8_t>> nv;
-        if (nullable) {
-          nv.emplace(all_nulls.begin() + row_begin[c], all_nulls.begin() + row_begin[c + 1]);
-          for (size_t i = 0; i < v.size(); ++i)
-            if ((*nv)[i]) v[i] = T{};  // NULL rows hold T{} (the device leaves them unspecified)
-        }
-        auto col = std::make_shared<ValueColumn<T>>(std::move(v), std::move(nv));
-        // the result already is in HBM: its slice becomes the column's device mirror when 16-byte aligned
-        const uint64_t off = row_begin[c] * sizeof(T);
-        if (!nullable && off % 16 == 0) {
-          auto d = std::make_shared<DeviceColumn>();
-          d->data = values;
-          d->desc.data = static_cast<char*>(values->get()) + off;
-          d->desc.size = sizes[c];
-          d->desc.kind = HY_COL_VALUE;
-          col->set_device_mirror(d);
-        }
-        out.push_back(col);
-      }
+  std::vector<std::vector<std::shared_ptr<BaseColumn>>> result(exprs.size());
+  size_t next = 0;
+  while (next < exprs.size()) {
+    // the batch: expressions while their input columns fit one hy_agg_input
+    ExprInput ei;
+    std::vector<std::vector<hy_expr_node>> progs;
+    const size_t first = next;
+    while (next < exprs.size() && progs.size() < HY_PROJ_MAX_OUTPUTS) {
+      std::vector<ColumnID> extra;
+      new_columns(*exprs[next], ei, extra);
+      if (!progs.empty() && ei.columns.size() + extra.size() > HY_AGG_MAX_COLUMNS) break;
+      progs.emplace_back();
+      compile(*exprs[next], in, ei, progs.back());
+      ++next;
     }
-  });
-  return out;
+    for (size_t j = 0; j < ei.columns.size(); ++j) {
+      ei.columns[j].chunks = ei.chunks[j].data();
+      ei.columns[j].n_chunks = static_cast<uint32_t>(ei.chunks[j].size());
+    }
+    std::vector<const hy_row_id*> pos_ptrs;
+    for (const auto& lists : ei.group_lists)
+      for (const auto& pl : lists) pos_ptrs.push_back(device_pos_list(*pl)->ptr());
+    hy_agg_input hin{};
+    hin.n_chunks = n_chunks;
+    hin.chunk_sizes = sizes.data();
+    hin.pos_lists = pos_ptrs.data();
+    hin.n_pos_groups = static_cast<uint32_t>(ei.group_lists.size());
+    hin.columns = ei.columns.data();
+    hin.n_columns = static_cast<uint32_t>(ei.columns.size());
+    Assert(hin.n_pos_groups <= HY_AGG_MAX_POS_GROUPS, "hyrise-amd: too many PosList groups for the device projection");
+
+    const size_t n = progs.size();
+    std::vector<std::shared_ptr<DeviceBuffer>> values(n), nulls(n);
+    std::vector<const hy_expr_node*> prog_ptrs(n);
+    std::vector<uint32_t> prog_lens(n);
+    std::vector<void*> outs(n);
+    std::vector<uint8_t*> out_nulls(n);
+    for (size_t i = 0; i < n; ++i) {
+      const AbstractExpression& e = *exprs[first + i];
+      values[i] = std::make_shared<DeviceBuffer>(std::max<uint64_t>(rows, 1) * data_type_size(e.data_type()) + 16);
+      nulls[i] = e.is_nullable() ? std::make_shared<DeviceBuffer>(std::max<uint64_t>(rows, 1) + 16) : nullptr;
+      prog_ptrs[i] = progs[i].data();
+      prog_lens[i] = static_cast<uint32_t>(progs[i].size());
+      outs[i] = values[i]->get();
+      out_nulls[i] = nulls[i] ? nulls[i]->as<uint8_t>() : nullptr;
+    }
+    size_t ws_bytes = 0;
+    hy_check(hy_projection_workspace_size(&hin, &ws_bytes), "hy_projection_workspace_size");
+    DeviceBuffer ws(ws_bytes, s);
+    hy_check(hy_projection_multi(&hin, prog_ptrs.data(), prog_lens.data(), static_cast<uint32_t>(n), outs.data(),
+                                 out_nulls.data(), ws.get(), ws_bytes, s),
+             "hy_projection_multi");
+
+    for (size_t i = 0; i < n; ++i) {
+      const AbstractExpression& e = *exprs[first + i];
+      const bool nullable = e.is_nullable();
+      auto& out = result[first + i];
+      resolve_data_type(e.data_type(), [&](auto tag) {
+        using T = decltype(tag);
+        if constexpr (!std::is_same_v<T, std::string>) {
+          std::vector<T> all(rows);
+          std::vector<uint8_t> all_nulls(nullable ? rows : 0);
+          if (rows) hy_check(hy_memcpy_dtoh(all.data(), values[i]->get(), rows * sizeof(T), s), "dtoh");
+          if (nullable && rows) hy_check(hy_memcpy_dtoh(all_nulls.data(), nulls[i]->get(), rows, s), "dtoh");
+          hy_check(hy_stream_synchronize(s), "sync");
+          for (ChunkID c = 0; c < n_chunks; ++c) {
+            std::vector<T> v(all.begin() + row_begin[c], all.begin() + row_begin[c + 1]);
+            std::optional<std::vector<uint8_t>> nv;
+            if (nullable) {
+              nv.emplace(all_nulls.begin() + row_begin[c], all_nulls.begin() + row_begin[c + 1]);
+              for (size_t r = 0; r < v.size(); ++r)
+                if ((*nv)[r]) v[r] = T{};  // NULL rows hold T{} (the device leaves them unspecified)
+            }
+            auto col = std::make_shared<ValueColumn<T>>(std::move(v), std::move(nv));
+            // the result already is in HBM: its slice becomes the column's device mirror when 16-byte aligned
+            const uint64_t off = row_begin[c] * sizeof(T);
+            if (!nullable && off % 16 == 0) {
+              auto d = std::make_shared<DeviceColumn>();
+              d->data = values[i];
+              d->desc.data = static_cast<char*>(values[i]->get()) + off;
+              d->desc.size = sizes[c];
+              d->desc.kind = HY_COL_VALUE;
+              col->set_device_mirror(d);
+            }
+            out.push_back(col);
+          }
+        }
+      });
+    }
+  }
+  return result;
 }
 
 // A column of a reference table materialized on the host (string columns, which the device holds only as
@@ -393,6 +437,8 @@ std::shared_ptr<const Table> Projection::_on_execute() {
   _performance_data.rows_in = in->row_count();
 
   std::vector<std::vector<std::shared_ptr<BaseColumn>>> computed(expressions.size());
+  std::vector<const AbstractExpression*> on_device;
+  std::vector<size_t> device_index;
   for (size_t i = 0; i < expressions.size(); ++i) {
     const auto& e = *expressions[i];
     if (e.type == ExpressionType::PQPColumn && forward) continue;
@@ -402,8 +448,13 @@ std::shared_ptr<const Table> Projection::_on_execute() {
       continue;
     }
     Assert(e.data_type() != DataType::String, "hyrise-amd: string-valued expressions are not supported");
+    on_device.push_back(&e);
+    device_index.push_back(i);
+  }
+  if (!on_device.empty()) {
     require_device();
-    computed[i] = evaluate_on_device(e, *in);
+    auto cols = evaluate_on_device(on_device, *in);
+    for (size_t k = 0; k < cols.size(); ++k) computed[device_index[k]] = std::move(cols[k]);
   }
   for (ChunkID c = 0; c < in->chunk_count(); ++c) {
     ChunkColumns cols;

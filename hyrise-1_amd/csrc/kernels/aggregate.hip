@@ -1089,6 +1089,56 @@ __device__ __forceinline__ uint32_t advance_chunk(const AggDesc& d, uint32_t c, 
   return c;
 }
 
+// The chunks a tile's rows fall into, as first-row offsets from the tile's first row in LDS: a row's chunk is then a
+// binary search in LDS instead of a chain of dependent global loads (row_chunk's search, then advance_chunk's walk
+// over the ~46-row partitions of a join output: ~9 dependent loads per row, TPC-H 3's projection / aggregate inputs).
+// A tile spanning more than CW_MAX chunks (empty chunks) falls back to row_chunk per row.
+constexpr uint32_t CW_MAX = 2048;
+struct ChunkWin {
+  uint32_t c0, n;    // first chunk, chunks
+  uint64_t base0;    // first row of chunk c0
+};
+struct ChunkWinLds {
+  uint32_t begin[CW_MAX];  // begin[i] = first row of chunk c0 + i - tile_row0 (0 for i = 0)
+  uint32_t c[2];
+  uint64_t base0;
+};
+// Every thread of the workgroup calls it (two barriers); rows [tile_row0, tile_end) with tile_end <= total rows.
+__device__ __forceinline__ ChunkWin chunk_window(const AggDesc& d, uint64_t tile_row0, uint64_t tile_end,
+                                                 ChunkWinLds& s) {
+  if (threadIdx.x == 0) {
+    const uint32_t c0 = tile_end > tile_row0 ? row_chunk(d, tile_row0) : 0u;
+    s.c[0] = c0;
+    s.c[1] = tile_end > tile_row0 ? row_chunk(d, tile_end - 1) : c0;
+    s.base0 = d.chunk_row_begin[c0];
+  }
+  __syncthreads();
+  ChunkWin w{s.c[0], s.c[1] - s.c[0] + 1, s.base0};
+  if (w.n <= CW_MAX)
+    for (uint32_t i = threadIdx.x; i < w.n; i += blockDim.x)
+      s.begin[i] = i == 0 ? 0u : static_cast<uint32_t>(d.chunk_row_begin[w.c0 + i] - tile_row0);
+  __syncthreads();
+  return w;
+}
+// Chunk and chunk offset of `row` of the tile (the last chunk whose first row is <= row, as row_chunk).
+__device__ __forceinline__ uint32_t win_chunk(const AggDesc& d, const ChunkWin& w, const ChunkWinLds& s,
+                                              uint64_t tile_row0, uint64_t row, uint32_t* off) {
+  if (w.n > CW_MAX) {
+    const uint32_t c = row_chunk(d, row);
+    *off = static_cast<uint32_t>(row - d.chunk_row_begin[c]);
+    return c;
+  }
+  const uint32_t r = static_cast<uint32_t>(row - tile_row0);
+  uint32_t lo = 0, hi = w.n;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (s.begin[mid] <= r) lo = mid;
+    else hi = mid;
+  }
+  *off = lo ? r - s.begin[lo] : static_cast<uint32_t>(row - w.base0);
+  return w.c0 + lo;
+}
+
 // Inclusive scan inside runs of lanes: lane i combines lanes [start, i] of its run.
 template <typename T, typename Op>
 __device__ __forceinline__ T run_scan(T v, int start, Op op) {
@@ -1117,11 +1167,13 @@ inline uint32_t flat_items(uint64_t rows) {
 __global__ __launch_bounds__(AGG_THREADS) void agg_hash_runs(AggDesc d, AggTable t, uint64_t total_rows,
                                                              uint32_t items) {
   __shared__ ClaimStage s_claim[AGG_THREADS / WAVE];
+  __shared__ ChunkWinLds s_win;
   const int lane = __lane_id();
   const uint64_t tile_row0 = static_cast<uint64_t>(blockIdx.x) * AGG_THREADS * items;
   const uint32_t H = d.n_gb;
   uint32_t c = 0;
-  bool have_c = false;
+  const ChunkWin win =
+      chunk_window(d, tile_row0, min(total_rows, tile_row0 + static_cast<uint64_t>(AGG_THREADS) * items), s_win);
   for (uint32_t k = 0; k < items; ++k) {
     const uint64_t wave_row0 = tile_row0 + static_cast<uint64_t>(k) * AGG_THREADS + (threadIdx.x & ~(WAVE - 1u));
     if (wave_row0 >= total_rows) break;  // wave-uniform
@@ -1132,9 +1184,7 @@ __global__ __launch_bounds__(AGG_THREADS) void agg_hash_runs(AggDesc d, AggTable
     uint64_t key[AGG_MAX_GROUPBY + 1];
     for (uint32_t j = 0; j <= H; ++j) key[j] = 0;
     if (valid) {
-      c = have_c ? advance_chunk(d, c, row) : row_chunk(d, row);
-      have_c = true;
-      off = static_cast<uint32_t>(row - d.chunk_row_begin[c]);
+      c = win_chunk(d, win, s_win, tile_row0, row, &off);
       if (d.n_pos_groups) load_refs(d, c, off, &refs);
       uint64_t nulls = 0;
       for (uint32_t j = 0; j < H; ++j) {

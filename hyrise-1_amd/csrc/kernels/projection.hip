@@ -1,5 +1,5 @@
-// Projection kernel for gfx950: evaluates one arithmetic expression (postfix program of hy_expr_node) per input row
-// and writes the result column (values + NULL flags) for all chunks of the input in one launch.
+// Projection kernel for gfx950: evaluates arithmetic expressions (postfix programs of hy_expr_node) per input row and
+// writes their result columns (values + NULL flags) for all chunks of the input in one launch.
 //
 // Reference: Projection::_on_execute (src/lib/operators/projection.cpp:39-87) evaluates every expression per chunk
 // with ExpressionEvaluator; arithmetic is Functor<std::common_type_t<A, B>>(a, b) assigned to the expression's
@@ -145,77 +145,91 @@ __device__ __forceinline__ uint64_t expr_arith(int32_t op, int32_t calc, uint64_
 }
 
 
-__global__ __launch_bounds__(AGG_THREADS) void projection_kernel(AggDesc d, ExprProgram prog, void* __restrict__ out,
-                                                                uint8_t* __restrict__ out_nulls, uint64_t total_rows,
-                                                                uint32_t items) {
+// One output column of a projection launch: the program (device copy) and where its values / NULL flags go.
+struct ProjOut {
+  const ExprProgram* prog;
+  void* values;
+  uint8_t* nulls;  // may be null
+};
+
+// Every program of the launch over every row (hy_projection_multi: the reference's Projection evaluates all its
+// expressions per chunk, projection.cpp:52-85): the row's chunk (LDS window), its RowIDs and the programs' column
+// reads are shared by the programs instead of repeated per launch.
+__global__ __launch_bounds__(AGG_THREADS) void projection_kernel(AggDesc d, const ProjOut* __restrict__ outs,
+                                                                uint32_t n_outs, uint64_t total_rows, uint32_t items) {
+  __shared__ ChunkWinLds s_win;
   const uint64_t tile_row0 = static_cast<uint64_t>(blockIdx.x) * AGG_THREADS * items;
-  const bool wide_out = is_wide(prog.out_type);
-  uint32_t c = 0;
-  bool have_c = false;
+  const ChunkWin win =
+      chunk_window(d, tile_row0, min(total_rows, tile_row0 + static_cast<uint64_t>(AGG_THREADS) * items), s_win);
 #pragma unroll 1
   for (uint32_t k = 0; k < items; ++k) {
     const uint64_t row = tile_row0 + static_cast<uint64_t>(k) * AGG_THREADS + threadIdx.x;
     if (row >= total_rows) break;
-    c = have_c ? advance_chunk(d, c, row) : row_chunk(d, row);
-    have_c = true;
-    const uint32_t off = static_cast<uint32_t>(row - d.chunk_row_begin[c]);
+    uint32_t off;
+    const uint32_t c = win_chunk(d, win, s_win, tile_row0, row, &off);
     RowRefs refs;
     if (d.n_pos_groups) load_refs(d, c, off, &refs);
-    // value stack in registers: every slot access is an unrolled compare against the (uniform) stack pointer, so the
-    // arrays are never indexed dynamically (which would place them in scratch memory)
-    uint64_t val[HY_EXPR_MAX_DEPTH];
-    bool nul[HY_EXPR_MAX_DEPTH];
-    int32_t typ[HY_EXPR_MAX_DEPTH];
-    auto push = [&](int sp, uint64_t v, bool n, int32_t t) {
+#pragma unroll 1
+    for (uint32_t o = 0; o < n_outs; ++o) {
+      const ProjOut po = outs[o];
+      const ExprProgram& prog = *po.prog;
+      // value stack in registers: every slot access is an unrolled compare against the (uniform) stack pointer, so
+      // the arrays are never indexed dynamically (which would place them in scratch memory)
+      uint64_t val[HY_EXPR_MAX_DEPTH];
+      bool nul[HY_EXPR_MAX_DEPTH];
+      int32_t typ[HY_EXPR_MAX_DEPTH];
+      auto push = [&](int sp, uint64_t v, bool n, int32_t t) {
 #pragma unroll
-      for (int j = 0; j < HY_EXPR_MAX_DEPTH; ++j)
-        if (j == sp) {
-          val[j] = v;
-          nul[j] = n;
-          typ[j] = t;
-        }
-    };
-    auto peek = [&](int sp, uint64_t* v, bool* n, int32_t* t) {
+        for (int j = 0; j < HY_EXPR_MAX_DEPTH; ++j)
+          if (j == sp) {
+            val[j] = v;
+            nul[j] = n;
+            typ[j] = t;
+          }
+      };
+      auto peek = [&](int sp, uint64_t* v, bool* n, int32_t* t) {
 #pragma unroll
-      for (int j = 0; j < HY_EXPR_MAX_DEPTH; ++j)
-        if (j == sp) {
-          *v = val[j];
-          *n = nul[j];
-          *t = typ[j];
+        for (int j = 0; j < HY_EXPR_MAX_DEPTH; ++j)
+          if (j == sp) {
+            *v = val[j];
+            *n = nul[j];
+            *t = typ[j];
+          }
+      };
+      int sp = 0;
+      const uint32_t n_nodes = prog.n_nodes;
+      for (uint32_t i = 0; i < n_nodes; ++i) {
+        const hy_expr_node nd = prog.nodes[i];
+        if (nd.kind == HY_EXPR_COLUMN) {
+          uint64_t bits = 0;
+          const bool ok = read_col(d, d.cols[nd.column], c, off, refs, &bits);
+          push(sp++, bits, !ok, nd.type);
+        } else if (nd.kind == HY_EXPR_VALUE) {
+          push(sp++, nd.value, nd.type == 0, nd.type);
+        } else {
+          uint64_t a = 0, b = 0;
+          bool na = true, nb = true;
+          int32_t ta = 0, tb = 0;
+          peek(sp - 1, &b, &nb, &tb);
+          peek(sp - 2, &a, &na, &ta);
+          sp -= 2;
+          bool null = na || nb || ta == 0 || tb == 0;
+          uint64_t r = 0;
+          if (!null) {
+            r = expr_arith(nd.kind, nd.calc_type, expr_convert(a, ta, nd.calc_type), expr_convert(b, tb, nd.calc_type),
+                           &null);
+            r = expr_convert(r, nd.calc_type, nd.type);
+          }
+          push(sp++, null ? 0 : r, null, nd.type);
         }
-    };
-    int sp = 0;
-    for (uint32_t i = 0; i < prog.n_nodes; ++i) {
-      const hy_expr_node& nd = prog.nodes[i];
-      if (nd.kind == HY_EXPR_COLUMN) {
-        uint64_t bits = 0;
-        const bool ok = read_col(d, d.cols[nd.column], c, off, refs, &bits);
-        push(sp++, bits, !ok, nd.type);
-      } else if (nd.kind == HY_EXPR_VALUE) {
-        push(sp++, nd.value, nd.type == 0, nd.type);
-      } else {
-        uint64_t a = 0, b = 0;
-        bool na = true, nb = true;
-        int32_t ta = 0, tb = 0;
-        peek(sp - 1, &b, &nb, &tb);
-        peek(sp - 2, &a, &na, &ta);
-        sp -= 2;
-        bool null = na || nb || ta == 0 || tb == 0;
-        uint64_t r = 0;
-        if (!null) {
-          r = expr_arith(nd.kind, nd.calc_type, expr_convert(a, ta, nd.calc_type), expr_convert(b, tb, nd.calc_type),
-                         &null);
-          r = expr_convert(r, nd.calc_type, nd.type);
-        }
-        push(sp++, null ? 0 : r, null, nd.type);
       }
+      const uint64_t r = val[0];
+      if (is_wide(prog.out_type))
+        static_cast<uint64_t*>(po.values)[row] = r;
+      else
+        static_cast<uint32_t*>(po.values)[row] = static_cast<uint32_t>(r);
+      if (po.nulls != nullptr) po.nulls[row] = nul[0] ? 1 : 0;
     }
-    const uint64_t r = val[0];
-    if (wide_out)
-      static_cast<uint64_t*>(out)[row] = r;
-    else
-      static_cast<uint32_t*>(out)[row] = static_cast<uint32_t>(r);
-    if (out_nulls != nullptr) out_nulls[row] = nul[0] ? 1 : 0;
   }
 }
 

@@ -800,6 +800,15 @@ hy_status hy_aggregate(const hy_agg_input* input, const hy_agg_params* params, u
 hy_status hy_projection_workspace_size(const hy_agg_input* input, size_t* bytes);
 hy_status hy_projection(const hy_agg_input* input, const hy_expr_node* program, uint32_t n_nodes, void* out_values,
                         uint8_t* out_nulls, void* workspace, size_t workspace_bytes, hy_stream_t stream);
+/* Several expressions over the same input in one launch, as the reference's Projection evaluates every expression of
+ * its node per chunk (projection.cpp:52-85): program i (n_nodes[i] nodes) writes out_values[i] / out_nulls[i]
+ * (out_nulls may be NULL, or hold NULL entries). The rows' chunks, RowIDs and column reads are shared by the programs;
+ * each result equals hy_projection's for that program. n_programs <= HY_PROJ_MAX_OUTPUTS; the workspace is
+ * hy_projection_workspace_size's. */
+enum { HY_PROJ_MAX_OUTPUTS = 16 };
+hy_status hy_projection_multi(const hy_agg_input* input, const hy_expr_node* const* programs, const uint32_t* n_nodes,
+                              uint32_t n_programs, void* const* out_values, uint8_t* const* out_nulls, void* workspace,
+                              size_t workspace_bytes, hy_stream_t stream);
 
 /* Host helpers: the correctly rounded double of an exact limb sum, and the value bits behind an ordered word. */
 /*

@@ -282,6 +282,43 @@ def test_selective_join_bloom_prefilter(hy, oracle, monkeypatch, mode, bloom, sp
     check_join(expected, parts, 1, swapped, mode in ("Semi", "Anti"))
 
 
+@pytest.mark.parametrize("mode", ["Inner", "Semi"])
+@pytest.mark.parametrize("span", ["narrow", "wide"])
+@pytest.mark.parametrize("buckets", ["1", "0"])
+def test_prefilter_built_per_region(hy, oracle, monkeypatch, mode, span, buckets):
+    """The prefilter's words set per LDS region (filter_bucket_count / scan / scatter / set; HY_FILTER_BUCKETS=0: one
+    global atomic per key) with a build side large enough for several regions and several count workgroups: the
+    key-range bitmap (`narrow`: 60,000 keys over a 3 M range, 12 regions of 8,192 words) and the Bloom filter (`wide`:
+    keys over the int32 range). The output PosLists equal the oracle's."""
+    monkeypatch.setenv("HY_JOIN_BLOOM", "1")
+    monkeypatch.setenv("HY_FILTER_BUCKETS", buckets)
+    capi = hy.capi
+    rng = np.random.default_rng(zlib.crc32(f"regions/{mode}/{span}".encode()))
+    if span == "narrow":
+        okey = rng.choice(np.arange(-1_000_000, 2_000_000, dtype=np.int32), 60_000, replace=False)
+        lkey = rng.integers(-1_100_000, 2_100_000, 400_000).astype(np.int32)
+    else:
+        okey = np.unique(rng.integers(np.iinfo(np.int32).min, np.iinfo(np.int32).max, 60_000, dtype=np.int64))
+        okey = rng.permutation(okey).astype(np.int32)
+        lkey = rng.integers(np.iinfo(np.int32).min, np.iinfo(np.int32).max, 400_000, dtype=np.int64).astype(np.int32)
+        hit = rng.random(400_000) < 0.05
+        lkey[hit] = rng.choice(okey, int(hit.sum()))
+    lineitem = hy.Table.from_arrays([("l_orderkey", hy.DataType.Int, False)], [lkey], [], 50_000)
+    orders = hy.Table.from_arrays([("o_orderkey", hy.DataType.Int, False)], [okey], [], 20_000)
+    jm = getattr(hy.JoinMode, mode)
+    expected, bits = oracle.join_hash(orders, lineitem, jm, (0, 0))
+    lk = dt.DeviceColumn(capi, lkey, None, 50_000, "Unencoded")
+    ok = dt.DeviceColumn(capi, okey, None, 20_000, "Unencoded")
+    swapped = mode == "Semi"
+    params = capi.JoinParams({"Inner": 0, "Semi": 5}[mode], capi.HY_TYPE_INT32, bits, 17)
+    cap = okey.size * 4 + lkey.size + 16
+    if swapped:
+        parts = run_fused(hy, dt.join_side(capi, lk), None, dt.join_side(capi, ok), None, params, cap)
+    else:
+        parts = run_fused(hy, dt.join_side(capi, ok), None, dt.join_side(capi, lk), None, params, cap)
+    check_join(expected, parts, 1, swapped, mode == "Semi")
+
+
 @pytest.mark.parametrize("mode", ["Inner", "Left"])
 def test_prepared_plan_equals_call(hy, mode):
     """hy_scan_join_plan_execute (descriptors staged on the first execution only) equals hy_scan_join_hash, on its
