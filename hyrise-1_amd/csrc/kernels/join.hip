@@ -1948,7 +1948,10 @@ __global__ __launch_bounds__(PART_THREADS) void part2_scatter(Segs sg, Digit dg,
 }
 
 // part2_hist from the digit bytes the previous pass wrote beside the records (1 B per record instead of the record
-// and its hash); same tiles and histogram layout as part2_hist.
+// and its hash); same tiles and histogram layout as part2_hist. (Round 5 measured eight tiles per workgroup with every
+// load issued first: 0.166 against 0.171 ms at SF100, not adopted. tools/hist_probe.hip: the same counts cost 0.17 ms
+// without any LDS atomic when each workgroup writes its 256 entries into the digit-major matrix, 0.09 ms tile-major -
+// the histogram's scattered 4-byte writes, not the counting, bound the pass.)
 template <typename SD>
 __global__ __launch_bounds__(PART_THREADS) void part2_hist_bytes(Segs sg, uint32_t n_digits,
                                                                 const uint8_t* __restrict__ dig,

@@ -1,0 +1,289 @@
+// TableScan probe (config 2 shape: SF10 l_quantity, u8 value ids, 100,000-row chunks, RowID output): the product's
+// scan_kernel (csrc/kernels/scan.hip: 4-tile segments, workgroup-staged stores) against scan_dict8_kernel below
+// (dword loads, ballot-placed matches, wave-private LDS staging), on the same descriptors; outputs and per-chunk
+// counts compared. Measured (profiles/r05_scan_probe.jsonl): 0.108 vs 0.142 ms (0.165 ms storing from registers).
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -o tools/scan_probe tools/scan_probe.hip
+#include "../hyrise-1_amd/csrc/kernels/scan.hip"
+
+namespace hyk {
+// ------------------------------------------------------------------------------------------------------------
+// 1-byte value ids without LDS staging (an alternative to scan_kernel for u8 ids; measured slower, not in the product): lane l of wave w reads dword i * 64 + l of the wave's span, i.e. rows
+// span + 256 i + 4 l + j (j = 0..3, one 256-byte coalesced load per wave and group). A lane's <= 4 matches of group i
+// go to consecutive positions at the lane's prefix - three ballots over the bits of its count give it - of the wave's
+// own LDS slice, which the wave then stores coalesced (8-byte RowIDs, streaming). One barrier pair per workgroup (the
+// segment's look-back), no per-tile block scans or workgroup barriers around the staging (scan_kernel's LDS stores
+// conflicted about once per instruction, profiles/r04_pmc_scan_kernel_sq.txt). Storing each lane's matches straight
+// from registers measured 0.165 ms against 0.108 (tools/scan_probe.hip): the partial lines cost more than the LDS.
+// G groups of 256 rows per wave: a workgroup (segment) covers 4 * 256 * G rows, G = 16 -> 16384 = scan_kernel's
+// 4-tile segment, so the host's segment geometry is unchanged.
+// ------------------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t match4_dict(const hy_scan_chunk& ch, uint32_t v, uint32_t valid) {
+  const uint32_t null_vid = static_cast<uint32_t>(ch.column.dictionary_size);
+  const uint32_t s = static_cast<uint32_t>(ch.search_vid);
+  const int op = ch.op;
+  uint32_t m = 0;
+  if (op == HY_OP_IS_NULL) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) m |= static_cast<uint32_t>(((v >> (8 * j)) & 0xFFu) == null_vid) << j;
+  } else if (op == HY_OP_VID_SET) {
+    const uint32_t* __restrict__ set = ch.vid_set;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t vid = (v >> (8 * j)) & 0xFFu;
+      m |= static_cast<uint32_t>(vid != null_vid && ((set[vid >> 5] >> (vid & 31)) & 1u)) << j;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t vid = (v >> (8 * j)) & 0xFFu;
+      m |= static_cast<uint32_t>(vid != null_vid && cmp_op<uint32_t>(op, vid, s)) << j;
+    }
+  }
+  return m & valid;
+}
+
+// LDS written by some lanes of a wave and read by others: the wave's own ordering point (no workgroup barrier).
+__device__ __forceinline__ void scan_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <bool OUT_ROWID, int G>
+__global__ __launch_bounds__(SCAN_THREADS) void scan_dict8_kernel(ScanLaunchDesc d, void* __restrict__ out_any,
+                                                                  uint32_t* __restrict__ counts) {
+  constexpr uint32_t NW = SCAN_THREADS / WAVE;
+  __shared__ uint32_t s_w[NW + 1];
+  __shared__ uint32_t s_stage[NW][256];
+  __shared__ uint64_t s_tile;
+  __shared__ uint32_t s_chunk;
+  __shared__ uint64_t s_prefix;
+  if (threadIdx.x == 0) {
+    const uint64_t tile = atomicAdd(d.ticket, 1u);
+    s_tile = tile;
+    s_chunk = tile < d.n_tiles ? d.tile_chunk[tile] : 0u;
+  }
+  __syncthreads();
+  const uint64_t tile = s_tile;
+  if (tile >= d.n_tiles) return;
+  const uint32_t c = s_chunk;
+  const hy_scan_chunk ch = d.chunks[c];
+  const uint64_t first_tile = d.chunk_tile_begin[c];
+  const uint32_t n = ch.column.size;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE), lane = __lane_id();
+  const uint32_t wrow0 = static_cast<uint32_t>(tile - first_tile) * (NW * 256u * G) + w * (256u * G);
+  const uint8_t* __restrict__ data = static_cast<const uint8_t*>(ch.column.data);
+  uint32_t m[G];
+  {
+    uint32_t v[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {  // all loads in flight first; the chunk's last dword is read byte by byte
+      const uint32_t r = wrow0 + g * 256u + lane * 4u;
+      if (r + 4 <= n) {
+        v[g] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(data + r));
+      } else {
+        v[g] = 0;
+        for (uint32_t j = 0; j < 4 && r + j < n; ++j) v[g] |= static_cast<uint32_t>(data[r + j]) << (8 * j);
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const uint32_t r = wrow0 + g * 256u + lane * 4u;
+      const uint32_t valid = r >= n ? 0u : (n - r >= 4 ? 0xFu : (1u << (n - r)) - 1u);
+      m[g] = ch.op == HY_OP_NONE ? 0u : match4_dict(ch, v[g], valid);
+    }
+  }
+  uint32_t mine = 0;
+#pragma unroll
+  for (int g = 0; g < G; ++g) mine += __popc(m[g]);
+  const uint32_t wave_total = static_cast<uint32_t>(wave_sum64(mine));
+  if (lane == 0) s_w[w] = wave_total;
+  __syncthreads();
+  if (threadIdx.x < WAVE) {  // wave 0: the segment's total, its look-back, the waves' offsets
+    uint32_t seg_total = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < NW; ++i) seg_total += s_w[i];
+    uint64_t prefix = 0;
+    if (tile == first_tile) {
+      if (threadIdx.x == 0) lb_publish(&d.status[tile], LB_FLAG_PREFIX, seg_total);
+    } else {
+      if (threadIdx.x == 0) lb_publish(&d.status[tile], LB_FLAG_AGG, seg_total);
+      prefix = lb_lookback_wave(d.status, first_tile, tile, d.error);
+      if (threadIdx.x == 0) lb_publish(&d.status[tile], LB_FLAG_PREFIX, prefix + seg_total);
+    }
+    if (threadIdx.x == 0) {
+      s_prefix = prefix;
+      if (tile == d.chunk_tile_begin[c + 1] - 1) counts[d.chunk_index[c]] = static_cast<uint32_t>(prefix + seg_total);
+    }
+  }
+  __syncthreads();
+  uint64_t run = ch.out_begin + s_prefix;
+  for (uint32_t i = 0; i < w; ++i) run += s_w[i];
+  const uint64_t lt = lanemask_lt();
+  const uint32_t cid = OUT_ROWID ? d.chunk_ids[c] : 0u;
+  // per group: the lanes' matches staged in the wave's own LDS slice in row order, then stored coalesced (no
+  // workgroup barrier: the slice is the wave's)
+  uint32_t* stage = s_stage[w];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const uint32_t cnt = __popc(m[g]);  // 0..4: its prefix over the lanes from the ballots of its three bits
+    const uint64_t b0 = __ballot(cnt & 1u), b1 = __ballot(cnt & 2u), b2 = __ballot(cnt & 4u);
+    const uint32_t pre = __popcll(b0 & lt) + 2u * __popcll(b1 & lt) + 4u * __popcll(b2 & lt);
+    const uint32_t tot = __popcll(b0) + 2u * __popcll(b1) + 4u * __popcll(b2);
+    const uint32_t r = wrow0 + g * 256u + lane * 4u;
+    uint32_t k = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if ((m[g] >> j) & 1u) stage[pre + k++] = r + j;
+    scan_wave_sync();
+    for (uint32_t i = lane; i < tot; i += WAVE) {
+      if constexpr (OUT_ROWID)
+        __builtin_nontemporal_store(static_cast<uint64_t>(cid) | (static_cast<uint64_t>(stage[i]) << 32),
+                                    static_cast<uint64_t*>(out_any) + run + i);
+      else
+        static_cast<uint32_t*>(out_any)[run + i] = stage[i];
+    }
+    scan_wave_sync();  // the slice is rewritten by the next group
+    run += tot;
+  }
+}
+
+}  // namespace hyk
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                         \
+  do {                                                                                \
+    hipError_t e_ = (x);                                                              \
+    if (e_ != hipSuccess) {                                                           \
+      std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      std::exit(1);                                                                   \
+    }                                                                                 \
+  } while (0)
+
+int main(int argc, char** argv) {
+  const uint64_t n = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 60007078ull;
+  const uint32_t chunk = 100000;
+  const uint32_t nc = static_cast<uint32_t>((n + chunk - 1) / chunk);
+  std::vector<uint8_t> vids(n);
+  uint64_t x = 0x9E3779B97F4A7C15ull;
+  for (auto& b : vids) {
+    x ^= x << 13;
+    x ^= x >> 7;
+    x ^= x << 17;
+    b = static_cast<uint8_t>(x % 50);
+  }
+  uint8_t* d_v;
+  CK(hipMalloc(&d_v, n + 64));
+  CK(hipMemcpy(d_v, vids.data(), n, hipMemcpyHostToDevice));
+  std::vector<hy_scan_chunk> ch(nc);
+  std::vector<uint64_t> seg_begin(nc + 1);
+  std::vector<uint32_t> idx(nc), cid(nc);
+  uint64_t run = 0;
+  for (uint32_t c = 0; c < nc; ++c) {
+    const uint32_t size = static_cast<uint32_t>(std::min<uint64_t>(chunk, n - uint64_t(c) * chunk));
+    ch[c] = hy_scan_chunk{};
+    ch[c].column.data = d_v + uint64_t(c) * chunk;
+    ch[c].column.size = size;
+    ch[c].column.dictionary_size = 50;
+    ch[c].column.kind = HY_COL_DICT;
+    ch[c].column.vid_width = 1;
+    ch[c].search_vid = 23;
+    ch[c].op = HY_OP_LT;
+    ch[c].out_begin = uint64_t(c) * chunk;
+    seg_begin[c] = run;
+    run += ((size + hyk::SCAN_TILE - 1) / hyk::SCAN_TILE + 3) / 4;
+    idx[c] = c;
+    cid[c] = c + 7;
+  }
+  seg_begin[nc] = run;
+  std::vector<uint32_t> owner(run);
+  for (uint32_t c = 0; c < nc; ++c)
+    for (uint64_t t = seg_begin[c]; t < seg_begin[c + 1]; ++t) owner[t] = c;
+  hy_scan_chunk* d_ch;
+  uint64_t *d_sb, *d_status, *d_out;
+  uint32_t *d_owner, *d_idx, *d_cid, *d_ticket, *d_err, *d_counts;
+  CK(hipMalloc(&d_ch, sizeof(hy_scan_chunk) * nc));
+  CK(hipMalloc(&d_sb, 8 * (nc + 1)));
+  CK(hipMalloc(&d_status, 8 * (run + 1)));
+  CK(hipMalloc(&d_out, 8 * (n + 64)));
+  CK(hipMalloc(&d_owner, 4 * run));
+  CK(hipMalloc(&d_idx, 4 * nc));
+  CK(hipMalloc(&d_cid, 4 * nc));
+  CK(hipMalloc(&d_ticket, 4));
+  CK(hipMalloc(&d_err, 4));
+  CK(hipMalloc(&d_counts, 4 * nc));
+  CK(hipMemcpy(d_ch, ch.data(), sizeof(hy_scan_chunk) * nc, hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_sb, seg_begin.data(), 8 * (nc + 1), hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_owner, owner.data(), 4 * run, hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_idx, idx.data(), 4 * nc, hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_cid, cid.data(), 4 * nc, hipMemcpyHostToDevice));
+  CK(hipMemset(d_err, 0, 4));
+  hyk::ScanLaunchDesc d{};
+  d.chunks = d_ch;
+  d.chunk_tile_begin = d_sb;
+  d.tile_chunk = d_owner;
+  d.chunk_index = d_idx;
+  d.chunk_ids = d_cid;
+  d.n_rows = n;
+  d.n_chunks = nc;
+  d.n_tiles = run;
+  d.status = d_status;
+  d.ticket = d_ticket;
+  d.error = d_err;
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  std::vector<uint64_t> ref;
+  std::vector<uint32_t> ref_counts;
+  for (int v = 0; v < 2; ++v) {
+    auto launch = [&]() {
+      CK(hipMemsetAsync(d_status, 0, 8 * (run + 1)));
+      CK(hipMemsetAsync(d_ticket, 0, 4));
+      if (v == 0)
+        hyk::scan_kernel<uint8_t, hyk::MODE_DICT, true, uint8_t, 4><<<run, hyk::SCAN_THREADS>>>(d, {}, d_out, d_counts);
+      else
+        hyk::scan_dict8_kernel<true, 16><<<run, hyk::SCAN_THREADS>>>(d, d_out, d_counts);
+    };
+    CK(hipMemset(d_out, 0xFF, 8 * n));
+    launch();
+    CK(hipDeviceSynchronize());
+    std::vector<uint64_t> out(n);
+    std::vector<uint32_t> counts(nc);
+    CK(hipMemcpy(out.data(), d_out, 8 * n, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(counts.data(), d_counts, 4 * nc, hipMemcpyDeviceToHost));
+    if (v == 0) {
+      ref = out;
+      ref_counts = counts;
+    }
+    // events around each kernel: the memsets stay outside
+    float total = 0;
+    for (int r = 0; r < 20; ++r) {
+      CK(hipMemsetAsync(d_status, 0, 8 * (run + 1)));
+      CK(hipMemsetAsync(d_ticket, 0, 4));
+      CK(hipEventRecord(a));
+      if (v == 0)
+        hyk::scan_kernel<uint8_t, hyk::MODE_DICT, true, uint8_t, 4><<<run, hyk::SCAN_THREADS>>>(d, {}, d_out, d_counts);
+      else
+        hyk::scan_dict8_kernel<true, 16><<<run, hyk::SCAN_THREADS>>>(d, d_out, d_counts);
+      CK(hipEventRecord(b));
+      CK(hipEventSynchronize(b));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, a, b));
+      total += ms;
+    }
+    uint64_t matches = 0;
+    for (auto c : counts) matches += c;
+    uint32_t err = 0;
+    CK(hipMemcpy(&err, d_err, 4, hipMemcpyDeviceToHost));
+    const double bytes = double(n) + 8.0 * double(matches);
+    std::printf("{\"kernel\": \"%s\", \"ms\": %.4f, \"matches\": %llu, \"alg_GBps\": %.1f, \"frac_spec\": %.3f, "
+                "\"equal\": %d, \"error\": %u}\n",
+                v == 0 ? "scan_kernel_seg4" : "scan_dict8_kernel_g16", total / 20, (unsigned long long)matches,
+                bytes / (total / 20 * 1e-3) / 1e9, bytes / (total / 20 * 1e-3) / 8e12,
+                int(out == ref && counts == ref_counts), err);
+  }
+  return 0;
+}
