@@ -467,28 +467,37 @@ hy_status table_scan_impl(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_
     }
     ht[nc] = run;
     hyk::ScanLaunchDesc d{};
+    // descriptors, segment prefix, chunk indexes, chunk ids and segment owners carved back to back and uploaded as ONE
+    // staged copy; then the look-back words and the ticket / error words cleared by one memset
     auto* dch = cv.take<hy_scan_chunk>(nc);
     auto* dti = cv.take<uint64_t>(nc + 1);
     auto* dix = cv.take<uint32_t>(nc);
     auto* dcid = cv.take<uint32_t>(nc);
     const uint64_t words = cls == SC_RLE ? 0 : run;  // RLE: run-level arrays come from rle_scan's own pool
-    auto* dst = cv.take<uint64_t>(words + 1);
     auto* downer = cv.take<uint32_t>(words + 1);
+    auto* dst = cv.take<uint64_t>(words + 1);
     auto* dmisc = cv.take<uint32_t>(64);
     if (!cv.ok) return fail(HY_ERR_WORKSPACE, "scan workspace too small");
-    if (!error) {
-      error = dmisc + 1;
-      HY_HIP(hipMemsetAsync(error, 0, 4, s));
-    }
-    HY_STAGE(dch, hc.data(), sizeof(hy_scan_chunk) * nc, s);
-    HY_STAGE(dti, ht.data(), sizeof(uint64_t) * (nc + 1), s);
-    HY_STAGE(dix, idx.data(), sizeof(uint32_t) * nc, s);
+    if (!error) error = dmisc + 1;  // (cleared by this class's memset below)
     auto& hcid = h_cids[cls];
     hcid.resize(nc);
     for (uint32_t k = 0; k < nc; ++k) hcid[k] = chunk_ids ? chunk_ids[idx[k]] : idx[k];
-    HY_STAGE(dcid, hcid.data(), sizeof(uint32_t) * nc, s);
-    HY_HIP(hipMemsetAsync(dst, 0, sizeof(uint64_t) * (words + 1), s));
-    HY_HIP(hipMemsetAsync(dmisc, 0, 4, s));
+    {
+      char* const base = reinterpret_cast<char*>(dch);
+      std::vector<char> image(reinterpret_cast<char*>(downer + words + 1) - base, 0);
+      auto put = [&](void* dev, const void* src, size_t bytes) {
+        if (bytes) std::memcpy(image.data() + (static_cast<char*>(dev) - base), src, bytes);
+      };
+      put(dch, hc.data(), sizeof(hy_scan_chunk) * nc);
+      put(dti, ht.data(), sizeof(uint64_t) * (nc + 1));
+      put(dix, idx.data(), sizeof(uint32_t) * nc);
+      put(dcid, hcid.data(), sizeof(uint32_t) * nc);
+      uint32_t* owner = reinterpret_cast<uint32_t*>(image.data() + (reinterpret_cast<char*>(downer) - base));
+      for (uint32_t k = 0; k < nc; ++k)
+        for (uint64_t t = ht[k]; t < ht[k + 1] && cls != SC_RLE; ++t) owner[t] = k;  // (fill_tile_owner's result)
+      HY_STAGE(dch, image.data(), image.size(), s);
+    }
+    HY_HIP(hipMemsetAsync(dst, 0, reinterpret_cast<char*>(dmisc + 64) - reinterpret_cast<char*>(dst), s));
     if (run == 0) continue;
     if (cls == SC_RLE) {
       uint32_t* run_chunk = nullptr;
@@ -501,8 +510,6 @@ hy_status table_scan_impl(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_
       if (st != HY_OK) return st;
       continue;
     }
-    hipLaunchKernelGGL(hyk::fill_tile_owner, dim3((nc + 255) / 256), dim3(256), 0, s, dti, nc, downer);
-    HY_HIP(hipGetLastError());
     d.tile_chunk = downer;
     d.chunks = dch;
     d.chunk_tile_begin = dti;
