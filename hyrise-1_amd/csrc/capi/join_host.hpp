@@ -575,7 +575,13 @@ inline int load_path(const SidePlan& p) {
            p.referenced[c.single_chunk].size > 0;
   }
   if (value) return hyk::LP_VALUE;
-  return ref1 ? hyk::LP_REF1 : hyk::LP_ANY;
+  if (ref1) return hyk::LP_REF1;
+  // PosLists over several chunks: the batched path when every referenced chunk is a ValueColumn without NULLs and
+  // chunk 0 (the NULL RowIDs' stand-in) is not empty
+  bool refm = !p.referenced.empty() && p.referenced[0].size > 0;
+  for (const auto& c : p.chunks) refm = refm && (c.size == 0 || c.pos_list != nullptr);
+  for (const auto& r : p.referenced) refm = refm && (r.size == 0 || (r.kind == HY_COL_VALUE && r.nulls == nullptr));
+  return refm ? hyk::LP_REFM : hyk::LP_ANY;
 }
 
 // Next-pass digit of pass i of the plan w (bits [shift, shift + w[i + 1])), or none.
@@ -695,7 +701,7 @@ hy_status launch_pass0(const SidePlan& p, const hyk::Side& sd, const hyk::Digit&
                        hipStream_t s, const hyk::RecOut<H, P>& out) {
   const bool filt = p.filtered;
   const int fk = filter_kind(p);
-  if constexpr (LP != hyk::LP_REF1 && std::is_same_v<T, H> && std::is_same_v<P, uint32_t>) {
+  if constexpr (LP != hyk::LP_REF1 && LP != hyk::LP_REFM && std::is_same_v<T, H> && std::is_same_v<P, uint32_t>) {
     switch (fk) {
       case hyk::FK_DICT8:
         return launch_filtered_pass0<SD, T, H, LP, hyk::FK_DICT8>(p, sd, d0, nd, w0, n_digits, b, c, s, out);
@@ -788,6 +794,8 @@ hy_status pass0_side(const SidePlan& p, SideBufs<H, P>& b, uint32_t bits, uint32
       st = launch_pass0<SD, T, H, P, hyk::LP_VALUE>(p, sd, d0, nd, w0, n_digits, b, c, s, out);
     else if (lp == hyk::LP_REF1)
       st = launch_pass0<SD, T, H, P, hyk::LP_REF1>(p, sd, d0, nd, w0, n_digits, b, c, s, out);
+    else if (lp == hyk::LP_REFM)
+      st = launch_pass0<SD, T, H, P, hyk::LP_REFM>(p, sd, d0, nd, w0, n_digits, b, c, s, out);
     else
       st = launch_pass0<SD, T, H, P, hyk::LP_ANY>(p, sd, d0, nd, w0, n_digits, b, c, s, out);
     if (st != HY_OK) return st;

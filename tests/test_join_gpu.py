@@ -213,6 +213,34 @@ def test_join_column_referencing_several_tables(hy, oracle, mode):
         assert_identical(j.get_output(), exp)
 
 
+@pytest.mark.parametrize("mode", ["Inner", "Left", "Right", "Semi", "Anti"])
+@pytest.mark.parametrize("tables", [1, 3])
+def test_poslists_over_several_value_chunks(hy, oracle, mode, tables):
+    """Reference inputs whose PosLists span several ValueColumn chunks (a join output as the next join's input, TPC-H
+    3's second build side): the batched load path (RowIDs, chunk pointers, values as three load phases; join_host's
+    LP_REFM), with NULL RowIDs, one or several referenced tables, on either side. RowID-exact against the oracle."""
+    rng = np.random.default_rng(91 + tables)
+    T = hy.DataType
+    tabs = []
+    for seed in range(tables):
+        k = rng.integers(0, 3_000, 12_000).astype(np.int32)
+        v = np.arange(12_000, dtype=np.int32) + seed * 100_000
+        tabs.append(hy.Table.from_arrays([("k", T.Int, False), ("v", T.Int, False)], [k, v], [], 2_500))
+    ref = hy.Table([("k", T.Int, False), ("v", T.Int, False)], hy.TableType.References)
+    for i in range(6):
+        t = tabs[i % tables]
+        pl = np.stack([rng.integers(0, 5, 3_000), rng.integers(0, 2_000, 3_000)], axis=1).astype(np.uint32)
+        pl[rng.random(3_000) < 0.03] = 0xFFFFFFFF
+        ref.append_chunk([hy.ReferenceColumn(t, 0, pl), hy.ReferenceColumn(t, 1, pl)])
+    other = hy.Table.from_arrays([("k", T.Int, False)], [rng.integers(0, 3_500, 15_000).astype(np.int32)], [], 4_000)
+    for left, right in ((ref, other), (other, ref)):
+        j = hy.JoinHash(wrap(hy, left), wrap(hy, right), getattr(hy.JoinMode, mode), (0, 0),
+                        hy.PredicateCondition.Equals)
+        j.execute()
+        exp, _ = oracle.join_hash(left, right, getattr(hy.JoinMode, mode), (0, 0))
+        assert_identical(j.get_output(), exp)
+
+
 @pytest.mark.parametrize("mode", ["Inner", "Left", "Semi", "Anti"])
 def test_probe_skew_needs_several_passes(hy, oracle, mode):
     """A few hot probe keys put tens of thousands of probe rows into single radix partitions while the average
