@@ -148,6 +148,214 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_dict8_kernel(ScanLaunchDesc
   }
 }
 
+
+// Variant of scan_kernel<u8, DICT, RowID, SEG=4>: the four tiles' per-thread counts packed 16 bits each into one 64-bit
+// value, so one workgroup scan gives every tile's positions (one barrier set per segment instead of one per tile), and
+// the matches staged by 16 predicated LDS stores at popcount positions instead of a loop over the set bits.
+constexpr int P_SEG = 4;
+__global__ __launch_bounds__(SCAN_THREADS) __attribute__((amdgpu_waves_per_eu(8)))
+void scan_packed_kernel(ScanLaunchDesc d, void* __restrict__ out_any, uint32_t* __restrict__ counts) {
+  __shared__ uint32_t s_stage[SCAN_TILE];
+  __shared__ uint64_t s_w64[SCAN_THREADS / WAVE + 1];
+  __shared__ uint64_t s_tile;
+  __shared__ uint32_t s_chunk;
+  __shared__ uint64_t s_prefix;
+  if (threadIdx.x == 0) {
+    const uint64_t tile = atomicAdd(d.ticket, 1u);
+    s_tile = tile;
+    s_chunk = tile < d.n_tiles ? d.tile_chunk[tile] : 0u;
+  }
+  __syncthreads();
+  const uint64_t tile = s_tile;
+  if (tile >= d.n_tiles) return;
+  const uint32_t c = s_chunk;
+  const hy_scan_chunk ch = d.chunks[c];
+  const uint64_t first_tile = d.chunk_tile_begin[c];
+  const uint32_t tile_row0 = static_cast<uint32_t>(tile - first_tile) * (P_SEG * SCAN_TILE);
+  const uint32_t n = ch.column.size;
+  uint32_t masks[P_SEG];
+  {
+    uint8_t v[P_SEG][16];
+    u32x4 nl[P_SEG];
+#pragma unroll
+    for (int t = 0; t < P_SEG; ++t) {
+      const uint32_t r0 = tile_row0 + t * SCAN_TILE + threadIdx.x * SCAN_ROWS_PER_THREAD;
+      nl[t] = u32x4{0u, 0u, 0u, 0u};
+      if (r0 < n && ch.op != HY_OP_NONE) load16(reinterpret_cast<const uint8_t*>(ch.column.data), r0, v[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < P_SEG; ++t)
+      masks[t] = match_mask<uint8_t, MODE_DICT, uint8_t>(ch, tile_row0 + t * SCAN_TILE + threadIdx.x * SCAN_ROWS_PER_THREAD,
+                                                         v[t], nl[t], ScanConst<uint8_t>{});
+  }
+  uint64_t packed = 0;
+#pragma unroll
+  for (int t = 0; t < P_SEG; ++t) packed |= static_cast<uint64_t>(__popc(masks[t])) << (16 * t);
+  // workgroup exclusive scan of the packed counts (fields never carry: <= 4096 per tile)
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
+  const uint64_t incl = wave_inclusive_sum64(packed);
+  if (__lane_id() == WAVE - 1) s_w64[w] = incl;
+  __syncthreads();
+  uint64_t before = 0, total = 0;
+#pragma unroll
+  for (int i = 0; i < SCAN_THREADS / WAVE; ++i) {
+    const uint64_t x = s_w64[i];
+    if (i < w) before += x;
+    total += x;
+  }
+  const uint64_t excl = before + incl - packed;
+  uint32_t seg_total = 0;
+#pragma unroll
+  for (int t = 0; t < P_SEG; ++t) seg_total += static_cast<uint32_t>((total >> (16 * t)) & 0xFFFFu);
+  if (threadIdx.x < WAVE) {
+    uint64_t prefix = 0;
+    if (tile == first_tile) {
+      if (threadIdx.x == 0) lb_publish(&d.status[tile], LB_FLAG_PREFIX, seg_total);
+    } else {
+      if (threadIdx.x == 0) lb_publish(&d.status[tile], LB_FLAG_AGG, seg_total);
+      prefix = lb_lookback_wave(d.status, first_tile, tile, d.error);
+      if (threadIdx.x == 0) lb_publish(&d.status[tile], LB_FLAG_PREFIX, prefix + seg_total);
+    }
+    if (threadIdx.x == 0) {
+      s_prefix = prefix;
+      if (tile == d.chunk_tile_begin[c + 1] - 1) counts[d.chunk_index[c]] = static_cast<uint32_t>(prefix + seg_total);
+    }
+  }
+  __syncthreads();
+  uint64_t run = ch.out_begin + s_prefix;
+  const uint32_t cid = d.chunk_ids[c];
+#pragma unroll
+  for (int t = 0; t < P_SEG; ++t) {
+    if (tile_row0 + t * SCAN_TILE >= n) break;  // uniform
+    const uint32_t r0 = tile_row0 + t * SCAN_TILE + threadIdx.x * SCAN_ROWS_PER_THREAD;
+    const uint32_t tile_total = static_cast<uint32_t>((total >> (16 * t)) & 0xFFFFu);
+    const uint32_t pos = static_cast<uint32_t>((excl >> (16 * t)) & 0xFFFFu);
+    const uint32_t m = masks[t];
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if ((m >> i) & 1u) s_stage[pos + __popc(m & ((1u << i) - 1u))] = r0 + i;
+    __syncthreads();
+    uint64_t* out64 = static_cast<uint64_t*>(out_any) + run;
+    for (uint32_t i = threadIdx.x; i < tile_total; i += SCAN_THREADS)
+      __builtin_nontemporal_store(static_cast<uint64_t>(cid) | (static_cast<uint64_t>(s_stage[i]) << 32), out64 + i);
+    run += tile_total;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) __attribute__((amdgpu_waves_per_eu(8)))
+void scan_seg_stage_kernel(ScanLaunchDesc d, void* __restrict__ out_any, uint32_t* __restrict__ counts) {
+  __shared__ uint16_t s_stage[P_SEG * SCAN_TILE];  // the segment's match offsets (segment-relative, 16 bits)
+  __shared__ uint64_t s_w64[SCAN_THREADS / WAVE + 1];
+  __shared__ uint64_t s_tile;
+  __shared__ uint32_t s_chunk;
+  __shared__ uint64_t s_prefix;
+  if (threadIdx.x == 0) {
+    const uint64_t tile = atomicAdd(d.ticket, 1u);
+    s_tile = tile;
+    s_chunk = tile < d.n_tiles ? d.tile_chunk[tile] : 0u;
+  }
+  __syncthreads();
+  const uint64_t tile = s_tile;
+  if (tile >= d.n_tiles) return;
+  const uint32_t c = s_chunk;
+  const hy_scan_chunk ch = d.chunks[c];
+  const uint64_t first_tile = d.chunk_tile_begin[c];
+  const uint32_t tile_row0 = static_cast<uint32_t>(tile - first_tile) * (P_SEG * SCAN_TILE);
+  const uint32_t n = ch.column.size;
+  uint32_t masks[P_SEG];
+  {
+    uint8_t v[P_SEG][16];
+    u32x4 nl[P_SEG];
+#pragma unroll
+    for (int t = 0; t < P_SEG; ++t) {
+      const uint32_t r0 = tile_row0 + t * SCAN_TILE + threadIdx.x * SCAN_ROWS_PER_THREAD;
+      nl[t] = u32x4{0u, 0u, 0u, 0u};
+      if (r0 < n && ch.op != HY_OP_NONE) load16(reinterpret_cast<const uint8_t*>(ch.column.data), r0, v[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < P_SEG; ++t)
+      masks[t] = match_mask<uint8_t, MODE_DICT, uint8_t>(ch, tile_row0 + t * SCAN_TILE + threadIdx.x * SCAN_ROWS_PER_THREAD,
+                                                         v[t], nl[t], ScanConst<uint8_t>{});
+  }
+  uint64_t packed = 0;
+#pragma unroll
+  for (int t = 0; t < P_SEG; ++t) packed |= static_cast<uint64_t>(__popc(masks[t])) << (16 * t);
+  // workgroup exclusive scan of the packed counts (fields never carry: <= 4096 per tile)
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
+  const uint64_t incl = wave_inclusive_sum64(packed);
+  if (__lane_id() == WAVE - 1) s_w64[w] = incl;
+  __syncthreads();
+  uint64_t before = 0, total = 0;
+#pragma unroll
+  for (int i = 0; i < SCAN_THREADS / WAVE; ++i) {
+    const uint64_t x = s_w64[i];
+    if (i < w) before += x;
+    total += x;
+  }
+  const uint64_t excl = before + incl - packed;
+  uint32_t seg_total = 0;
+#pragma unroll
+  for (int t = 0; t < P_SEG; ++t) seg_total += static_cast<uint32_t>((total >> (16 * t)) & 0xFFFFu);
+  if (threadIdx.x < WAVE) {
+    uint64_t prefix = 0;
+    if (tile == first_tile) {
+      if (threadIdx.x == 0) lb_publish(&d.status[tile], LB_FLAG_PREFIX, seg_total);
+    } else {
+      if (threadIdx.x == 0) lb_publish(&d.status[tile], LB_FLAG_AGG, seg_total);
+      prefix = lb_lookback_wave(d.status, first_tile, tile, d.error);
+      if (threadIdx.x == 0) lb_publish(&d.status[tile], LB_FLAG_PREFIX, prefix + seg_total);
+    }
+    if (threadIdx.x == 0) {
+      s_prefix = prefix;
+      if (tile == d.chunk_tile_begin[c + 1] - 1) counts[d.chunk_index[c]] = static_cast<uint32_t>(prefix + seg_total);
+    }
+  }
+  __syncthreads();
+  const uint64_t run = ch.out_begin + s_prefix;
+  const uint32_t cid = d.chunk_ids[c];
+  // every tile's matches staged at once (positions from the packed scan), one barrier, then the segment's stores
+  uint32_t tbase = 0;
+#pragma unroll
+  for (int t = 0; t < P_SEG; ++t) {
+    const uint32_t pos = tbase + static_cast<uint32_t>((excl >> (16 * t)) & 0xFFFFu);
+    const uint32_t m = masks[t];
+    const uint32_t o0 = t * SCAN_TILE + threadIdx.x * SCAN_ROWS_PER_THREAD;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if ((m >> i) & 1u) s_stage[pos + __popc(m & ((1u << i) - 1u))] = static_cast<uint16_t>(o0 + i);
+    tbase += static_cast<uint32_t>((total >> (16 * t)) & 0xFFFFu);
+  }
+  __syncthreads();
+  uint64_t* out64 = static_cast<uint64_t*>(out_any) + run;
+  for (uint32_t i = threadIdx.x; i < seg_total; i += SCAN_THREADS)
+    __builtin_nontemporal_store(static_cast<uint64_t>(cid) | (static_cast<uint64_t>(tile_row0 + s_stage[i]) << 32),
+                                out64 + i);
+}
+
+// Ceilings for the same grid: every workgroup only streams its share of the output (27.6 M 8-byte RowIDs, coalesced,
+// streaming stores), or only loads its 16384 ids and counts the matches (no stores but the count).
+__global__ __launch_bounds__(SCAN_THREADS) void store_only_kernel(uint64_t n_out, uint32_t n_wg, uint64_t* __restrict__ out) {
+  const uint64_t per = (n_out + n_wg - 1) / n_wg;
+  const uint64_t b = per * blockIdx.x, e = min(n_out, b + per);
+  for (uint64_t i = b + threadIdx.x; i < e; i += SCAN_THREADS) __builtin_nontemporal_store(i, out + i);
+}
+__global__ __launch_bounds__(SCAN_THREADS) void load_count_kernel(const uint8_t* __restrict__ v, uint64_t n,
+                                                                  uint32_t* __restrict__ sink) {
+  const uint64_t r0 = static_cast<uint64_t>(blockIdx.x) * 16384 + threadIdx.x * 16;
+  uint32_t c = 0;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const uint64_t r = r0 + t * 4096;
+    if (r + 16 <= n) {
+      const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(v + r));
+      const uint32_t w[4] = {x[0], x[1], x[2], x[3]};
+#pragma unroll
+      for (int i = 0; i < 16; ++i) c += ((w[i >> 2] >> (8 * (i & 3))) & 0xFFu) < 23u;
+    }
+  }
+  if (c == 0xFFFFFFFFu) sink[0] = c;
+}
 }  // namespace hyk
 
 #include <cstdio>
@@ -238,14 +446,18 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&b));
   std::vector<uint64_t> ref;
   std::vector<uint32_t> ref_counts;
-  for (int v = 0; v < 2; ++v) {
+  for (int v = 0; v < 4; ++v) {
     auto launch = [&]() {
       CK(hipMemsetAsync(d_status, 0, 8 * (run + 1)));
       CK(hipMemsetAsync(d_ticket, 0, 4));
       if (v == 0)
         hyk::scan_kernel<uint8_t, hyk::MODE_DICT, true, uint8_t, 4><<<run, hyk::SCAN_THREADS>>>(d, {}, d_out, d_counts);
-      else
+      else if (v == 1)
         hyk::scan_dict8_kernel<true, 16><<<run, hyk::SCAN_THREADS>>>(d, d_out, d_counts);
+      else if (v == 2)
+        hyk::scan_packed_kernel<<<run, hyk::SCAN_THREADS>>>(d, d_out, d_counts);
+      else
+        hyk::scan_seg_stage_kernel<<<run, hyk::SCAN_THREADS>>>(d, d_out, d_counts);
     };
     CK(hipMemset(d_out, 0xFF, 8 * n));
     launch();
@@ -266,8 +478,12 @@ int main(int argc, char** argv) {
       CK(hipEventRecord(a));
       if (v == 0)
         hyk::scan_kernel<uint8_t, hyk::MODE_DICT, true, uint8_t, 4><<<run, hyk::SCAN_THREADS>>>(d, {}, d_out, d_counts);
-      else
+      else if (v == 1)
         hyk::scan_dict8_kernel<true, 16><<<run, hyk::SCAN_THREADS>>>(d, d_out, d_counts);
+      else if (v == 2)
+        hyk::scan_packed_kernel<<<run, hyk::SCAN_THREADS>>>(d, d_out, d_counts);
+      else
+        hyk::scan_seg_stage_kernel<<<run, hyk::SCAN_THREADS>>>(d, d_out, d_counts);
       CK(hipEventRecord(b));
       CK(hipEventSynchronize(b));
       float ms = 0;
@@ -281,9 +497,25 @@ int main(int argc, char** argv) {
     const double bytes = double(n) + 8.0 * double(matches);
     std::printf("{\"kernel\": \"%s\", \"ms\": %.4f, \"matches\": %llu, \"alg_GBps\": %.1f, \"frac_spec\": %.3f, "
                 "\"equal\": %d, \"error\": %u}\n",
-                v == 0 ? "scan_kernel_seg4" : "scan_dict8_kernel_g16", total / 20, (unsigned long long)matches,
+                v == 0 ? "scan_kernel_seg4" : v == 1 ? "scan_dict8_kernel_g16" : v == 2 ? "scan_packed_kernel" : "scan_seg_stage_kernel", total / 20, (unsigned long long)matches,
                 bytes / (total / 20 * 1e-3) / 1e9, bytes / (total / 20 * 1e-3) / 8e12,
                 int(out == ref && counts == ref_counts), err);
+  }
+  for (int v = 4; v < 6; ++v) {
+    float total = 0;
+    for (int r = 0; r < 20; ++r) {
+      CK(hipEventRecord(a));
+      if (v == 4)
+        hyk::store_only_kernel<<<run, hyk::SCAN_THREADS>>>(27602404ull, static_cast<uint32_t>(run), d_out);
+      else
+        hyk::load_count_kernel<<<run, hyk::SCAN_THREADS>>>(d_v, n, d_counts);
+      CK(hipEventRecord(b));
+      CK(hipEventSynchronize(b));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, a, b));
+      total += ms;
+    }
+    std::printf("{\"kernel\": \"%s\", \"ms\": %.4f}\n", v == 4 ? "store_only_221MB" : "load_count_60MB", total / 20);
   }
   return 0;
 }
