@@ -237,7 +237,7 @@ void scan_packed_kernel(ScanLaunchDesc d, void* __restrict__ out_any, uint32_t* 
     __syncthreads();
     uint64_t* out64 = static_cast<uint64_t*>(out_any) + run;
     for (uint32_t i = threadIdx.x; i < tile_total; i += SCAN_THREADS)
-      __builtin_nontemporal_store(static_cast<uint64_t>(cid) | (static_cast<uint64_t>(s_stage[i]) << 32), out64 + i);
+      out64[i] = static_cast<uint64_t>(cid) | (static_cast<uint64_t>(s_stage[i]) << 32);  // plain stores (L2 / MALL)
     run += tile_total;
     __syncthreads();
   }
@@ -339,6 +339,19 @@ __global__ __launch_bounds__(SCAN_THREADS) void store_only_kernel(uint64_t n_out
   const uint64_t per = (n_out + n_wg - 1) / n_wg;
   const uint64_t b = per * blockIdx.x, e = min(n_out, b + per);
   for (uint64_t i = b + threadIdx.x; i < e; i += SCAN_THREADS) __builtin_nontemporal_store(i, out + i);
+}
+__global__ __launch_bounds__(SCAN_THREADS) void store16_only_kernel(uint64_t n_out, uint32_t n_wg, uint64_t* __restrict__ out) {
+  const uint64_t per = ((n_out + n_wg - 1) / n_wg + 1) & ~uint64_t(1);  // even: 16-byte aligned pairs
+  const uint64_t b = per * blockIdx.x, e = min(n_out, b + per);
+  for (uint64_t i = b + 2 * threadIdx.x; i + 1 < e; i += 2 * SCAN_THREADS) {
+    u32x4 v = {static_cast<uint32_t>(i), 7u, static_cast<uint32_t>(i + 1), 7u};
+    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(out + i));
+  }
+}
+__global__ __launch_bounds__(SCAN_THREADS) void store_plain_kernel(uint64_t n_out, uint32_t n_wg, uint64_t* __restrict__ out) {
+  const uint64_t per = (n_out + n_wg - 1) / n_wg;
+  const uint64_t b = per * blockIdx.x, e = min(n_out, b + per);
+  for (uint64_t i = b + threadIdx.x; i < e; i += SCAN_THREADS) out[i] = i;
 }
 __global__ __launch_bounds__(SCAN_THREADS) void load_count_kernel(const uint8_t* __restrict__ v, uint64_t n,
                                                                   uint32_t* __restrict__ sink) {
@@ -497,16 +510,20 @@ int main(int argc, char** argv) {
     const double bytes = double(n) + 8.0 * double(matches);
     std::printf("{\"kernel\": \"%s\", \"ms\": %.4f, \"matches\": %llu, \"alg_GBps\": %.1f, \"frac_spec\": %.3f, "
                 "\"equal\": %d, \"error\": %u}\n",
-                v == 0 ? "scan_kernel_seg4" : v == 1 ? "scan_dict8_kernel_g16" : v == 2 ? "scan_packed_kernel" : "scan_seg_stage_kernel", total / 20, (unsigned long long)matches,
+                v == 0 ? "scan_kernel_seg4" : v == 1 ? "scan_dict8_kernel_g16" : v == 2 ? "scan_packed_kernel_plain_stores" : "scan_seg_stage_kernel", total / 20, (unsigned long long)matches,
                 bytes / (total / 20 * 1e-3) / 1e9, bytes / (total / 20 * 1e-3) / 8e12,
                 int(out == ref && counts == ref_counts), err);
   }
-  for (int v = 4; v < 6; ++v) {
+  for (int v = 4; v < 8; ++v) {
     float total = 0;
     for (int r = 0; r < 20; ++r) {
       CK(hipEventRecord(a));
       if (v == 4)
         hyk::store_only_kernel<<<run, hyk::SCAN_THREADS>>>(27602404ull, static_cast<uint32_t>(run), d_out);
+      else if (v == 6)
+        hyk::store16_only_kernel<<<run, hyk::SCAN_THREADS>>>(27602404ull, static_cast<uint32_t>(run), d_out);
+      else if (v == 7)
+        hyk::store_plain_kernel<<<run, hyk::SCAN_THREADS>>>(27602404ull, static_cast<uint32_t>(run), d_out);
       else
         hyk::load_count_kernel<<<run, hyk::SCAN_THREADS>>>(d_v, n, d_counts);
       CK(hipEventRecord(b));
@@ -515,7 +532,7 @@ int main(int argc, char** argv) {
       CK(hipEventElapsedTime(&ms, a, b));
       total += ms;
     }
-    std::printf("{\"kernel\": \"%s\", \"ms\": %.4f}\n", v == 4 ? "store_only_221MB" : "load_count_60MB", total / 20);
+    std::printf("{\"kernel\": \"%s\", \"ms\": %.4f}\n", v == 4 ? "store_only_221MB" : v == 5 ? "load_count_60MB" : v == 6 ? "store16_nt_221MB" : "store8_plain_221MB", total / 20);
   }
   return 0;
 }
