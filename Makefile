@@ -15,9 +15,15 @@ HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Iinc
 
 HOST_SRC  := $(CSRC)/host/storage.cpp $(CSRC)/host/device.cpp $(CSRC)/host/operators.cpp $(CSRC)/host/aggregate.cpp \
              $(CSRC)/host/projection.cpp $(CSRC)/host/binary_io.cpp $(CSRC)/host/scheduler.cpp
-HOST_HDR  := $(wildcard $(CSRC)/host/*.hpp) include/hyrise_amd.h
+HOST_HDR  := $(wildcard $(CSRC)/host/*.hpp) include/hyrise_amd.h include/hyrise_amd_trace.h
 
-all: $(LIB)/libhyrise_amd.so $(LIB)/libhyrise_host.so $(LIB)/_hyrise_host$(EXTSUF) $(LIB)/exchange_check
+all: $(LIB)/libhyrise_amd.so $(LIB)/libhyrise_host.so $(LIB)/_hyrise_host$(EXTSUF) $(LIB)/exchange_check $(LIB)/host_concurrency_check_tsan
+
+# host-side concurrency checks (deferred tables, job groups, chunk reaper) under ThreadSanitizer: no GPU, run by
+# tests/test_host_concurrency.py
+$(LIB)/host_concurrency_check_tsan: tests/native/host_concurrency_check.cpp $(CSRC)/host/storage.cpp $(CSRC)/host/scheduler.cpp $(HOST_HDR)
+	@mkdir -p $(LIB)
+	$(CXX) -std=c++17 -O1 -g -fsanitize=thread -I$(CSRC)/host -Iinclude -o $@ $< $(CSRC)/host/storage.cpp $(CSRC)/host/scheduler.cpp -lpthread
 
 # native (no Python, no torch) check of the C-ABI RCCL exchange, run by tests/test_dist_join_gpu.py on the GPU
 $(LIB)/exchange_check: tests/native/exchange_check.cpp include/hyrise_amd.h $(LIB)/libhyrise_amd.so
@@ -40,7 +46,7 @@ $(LIB)/hyrise_amd_aggregate.o: $(CSRC)/capi/hyrise_amd_aggregate.hip $(CSRC)/ker
 JOIN_TUS   := join join_i32 join_i64 join_f32 join_f64
 JOIN_OBJS  := $(patsubst %,$(LIB)/hyrise_amd_%.o,$(JOIN_TUS))
 
-$(JOIN_OBJS): $(LIB)/hyrise_amd_%.o: $(CSRC)/capi/hyrise_amd_%.hip $(CSRC)/capi/join_host.hpp $(CSRC)/kernels/join.hip $(CAPI_HDR)
+$(JOIN_OBJS): $(LIB)/hyrise_amd_%.o: $(CSRC)/capi/hyrise_amd_%.hip $(CSRC)/capi/join_host.hpp $(CSRC)/kernels/join.hip $(CSRC)/kernels/join_direct.hip $(CAPI_HDR)
 	@mkdir -p $(LIB)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
@@ -73,6 +79,10 @@ $(LIB)/hyrise_amd_decode.o: $(CSRC)/capi/hyrise_amd_decode.hip $(CAPI_HDR)
 	@mkdir -p $(LIB)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
+$(LIB)/hyrise_amd_trace.o: $(CSRC)/capi/hyrise_amd_trace.hip include/hyrise_amd_trace.h $(CSRC)/capi/capi_common.hpp
+	@mkdir -p $(LIB)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
 $(LIB)/hyrise_amd_string.o: $(CSRC)/capi/hyrise_amd_string.hip $(CAPI_HDR)
 	@mkdir -p $(LIB)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
@@ -80,11 +90,12 @@ $(LIB)/hyrise_amd_string.o: $(CSRC)/capi/hyrise_amd_string.hip $(CAPI_HDR)
 $(LIB)/libhyrise_amd.so: $(LIB)/hyrise_amd.o $(LIB)/hyrise_amd_aggregate.o $(LIB)/hyrise_amd_order.o \
                          $(LIB)/hyrise_amd_comm.o $(LIB)/hyrise_amd_compare.o \
                          $(LIB)/hyrise_amd_validate.o $(LIB)/hyrise_amd_decode.o $(LIB)/hyrise_amd_string.o \
-                         $(LIB)/hyrise_amd_agg_jit.o $(JOIN_OBJS)
+                         $(LIB)/hyrise_amd_agg_jit.o $(LIB)/hyrise_amd_trace.o $(JOIN_OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -L/opt/rocm/lib -lrccl -lhiprtc -Wl,-rpath,/opt/rocm/lib
 
 $(LIB)/libhyrise_host.so: $(HOST_SRC) $(HOST_HDR) $(LIB)/libhyrise_amd.so
-	$(CXX) $(CXXFLAGS) -shared -o $@ $(HOST_SRC) -L$(LIB) -lhyrise_amd -Wl,-rpath,'$$ORIGIN'
+	$(CXX) $(CXXFLAGS) -I/opt/rocm/include -shared -o $@ $(HOST_SRC) -L$(LIB) -lhyrise_amd -L/opt/rocm/lib \
+	  -lrocprofiler-sdk-roctx -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,/opt/rocm/lib
 
 $(LIB)/_hyrise_host$(EXTSUF): $(CSRC)/host/bindings.cpp $(HOST_HDR) $(LIB)/libhyrise_host.so
 	$(CXX) $(CXXFLAGS) -I$(PYINC) -I$(PYBIND) -shared -o $@ $(CSRC)/host/bindings.cpp -L$(LIB) -lhyrise_host \

@@ -57,7 +57,14 @@ class JoinSide(ctypes.Structure):
 
 class JoinFilter(ctypes.Structure):
     _fields_ = [("chunks", ctypes.POINTER(ScanChunk)), ("value_type", ctypes.c_int32), ("constant", ctypes.c_void_p),
-                ("out_offsets", ctypes.c_void_p), ("out_chunk_begin", ctypes.c_void_p)]
+                ("out_offsets", ctypes.c_void_p), ("out_chunk_begin", ctypes.c_void_p), ("n_chunks", ctypes.c_uint32)]
+
+    def __init__(self, chunks=None, value_type=0, constant=None, out_offsets=None, out_chunk_begin=None,
+                 n_chunks=None):
+        # n_chunks defaults to the length of a ctypes array of predicate chunks (the side's chunk count)
+        if n_chunks is None:
+            n_chunks = len(chunks) if chunks is not None and hasattr(chunks, "__len__") else 0
+        super().__init__(chunks, value_type, constant, out_offsets, out_chunk_begin, n_chunks)
 
 
 class JoinParams(ctypes.Structure):
@@ -293,8 +300,8 @@ def check(status, what=""):
 
 
 def declared_symbols():
-    """Entry points declared in include/hyrise_amd.h."""
-    text = open(HEADER_PATH).read()
+    """Entry points declared in include/hyrise_amd.h and include/hyrise_amd_trace.h."""
+    text = open(HEADER_PATH).read() + open(os.path.join(os.path.dirname(HEADER_PATH), "hyrise_amd_trace.h")).read()
     return sorted(set(re.findall(r"^\s*(?:hy_status|uint32_t|uint64_t|const char\*)\s+(hy_\w+)\s*\(", text, re.M)))
 
 

@@ -114,6 +114,7 @@ struct hy_join_plan_s {
   uint64_t graph_capacity = 0;
   const uint32_t* misc = nullptr;   // the captured join's flags / total (device)
   const uint64_t* totals = nullptr;
+  const uint32_t* direct_overflow = nullptr;  // the captured direct pass's region-overflow flag, or null
   bool no_graph = false;
   JoinKnobs knobs;  // the environment's knobs when the plan was created; every execution runs under them
   ~hy_join_plan_s() {
@@ -144,12 +145,18 @@ hy_status run_plan(hy_join_plan_s* plan, hy_row_id* out_build, hy_row_id* out_pr
 }
 
 // After a replay: the join's flags and total, exactly as run_join_partitions reads them after an eager execution.
-hy_status finish_replay(const hy_join_plan_s* plan, uint64_t out_capacity, hy_join_result* result, hipStream_t s) {
+// *direct_overflow: a direct pass's region overflowed (the output is invalid; the caller reruns on the classic passes).
+hy_status finish_replay(const hy_join_plan_s* plan, uint64_t out_capacity, hy_join_result* result, hipStream_t s,
+                        bool* direct_overflow) {
   uint32_t flags[4] = {0, 0, 0, 0};
+  uint32_t dflag = 0;
   uint64_t total = 0;
   HY_HIP(hipMemcpyAsync(flags, plan->misc, 16, hipMemcpyDeviceToHost, s));
   HY_HIP(hipMemcpyAsync(&total, plan->totals + 1, 8, hipMemcpyDeviceToHost, s));
+  if (plan->direct_overflow) HY_HIP(hipMemcpyAsync(&dflag, plan->direct_overflow, 4, hipMemcpyDeviceToHost, s));
   HY_HIP(hipStreamSynchronize(s));
+  *direct_overflow = dflag != 0;
+  if (dflag) return HY_OK;
   if (flags[1]) return fail(HY_ERR_KERNEL, "join look-back did not complete");
   if (result) {
     result->total_pairs = total;
@@ -211,9 +218,24 @@ hy_status hy_scan_join_plan_execute(hy_join_plan_t plan, hy_row_id* out_build, h
   }
   const bool same = plan->exec && plan->graph_stream == s && plan->graph_capacity == out_capacity &&
                     std::equal(args, args + 5, plan->graph_args);
+  // a direct pass that overflowed a region: the plan keeps the classic passes from now on (its graph is dropped and
+  // its descriptors staged again by the eager execution below, whose carve is the classic one)
+  auto drop_direct = [&]() {
+    plan->knobs.direct = false;
+    knob_scope.own.direct = false;
+    if (plan->exec) (void)hipGraphExecDestroy(plan->exec);
+    if (plan->graph) (void)hipGraphDestroy(plan->graph);
+    plan->exec = nullptr;
+    plan->graph = nullptr;
+    plan->direct_overflow = nullptr;
+    plan->bp.device_ready = plan->pp.device_ready = false;
+  };
   if (same && !timing) {  // replay the captured launches
     HY_HIP(hipGraphLaunch(plan->exec, s));
-    return finish_replay(plan, out_capacity, result, s);
+    bool ovf = false;
+    const hy_status st = finish_replay(plan, out_capacity, result, s, &ovf);
+    if (!ovf) return st;
+    drop_direct();
   }
   if (plan->bp.device_ready && plan->pp.device_ready && !timing && !plan->no_graph && graphs_enabled() &&
       s != nullptr) {
@@ -238,8 +260,13 @@ hy_status hy_scan_join_plan_execute(hy_join_plan_t plan, hy_row_id* out_build, h
         std::copy(args, args + 5, plan->graph_args);
         plan->misc = cs.misc;
         plan->totals = cs.totals;
+        plan->direct_overflow = cs.direct_overflow;
         HY_HIP(hipGraphLaunch(plan->exec, s));
-        return finish_replay(plan, out_capacity, result, s);
+        bool ovf = false;
+        const hy_status st2 = finish_replay(plan, out_capacity, result, s, &ovf);
+        if (!ovf) return st2;
+        drop_direct();
+        return run_plan(plan, out_build, out_probe, out_capacity, partition_begin, partition_counts, result, s);
       }
       if (g) (void)hipGraphDestroy(g);
       (void)hipGetLastError();
@@ -248,8 +275,10 @@ hy_status hy_scan_join_plan_execute(hy_join_plan_t plan, hy_row_id* out_build, h
     }
     plan->no_graph = true;  // capture is not available here: execute eagerly from now on
   }
+  direct_fell_back() = false;
   const hy_status st =
       run_plan(plan, out_build, out_probe, out_capacity, partition_begin, partition_counts, result, s);
+  if (direct_fell_back()) plan->knobs.direct = false;  // (the classic carve's descriptors are staged now)
   // from now on the plan's workspace holds both sides' descriptors (the single-pass variant carves the workspace
   // differently and may fall back within a call: it keeps staging every time)
   if ((st == HY_OK || st == HY_ERR_CAPACITY) && !onepass_enabled()) plan->bp.device_ready = plan->pp.device_ready = true;

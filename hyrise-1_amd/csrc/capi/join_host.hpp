@@ -18,6 +18,7 @@
 #include "hyrise_amd.h"
 #include "../kernels/common.hpp"
 #include "../kernels/join.hip"
+#include "../kernels/join_direct.hip"
 #include "capi_common.hpp"
 
 namespace hyj {
@@ -31,6 +32,7 @@ struct CaptureState {
   bool capturing = false;
   const uint32_t* misc = nullptr;
   const uint64_t* totals = nullptr;
+  const uint32_t* direct_overflow = nullptr;  // the direct pass's region-overflow flag (join_direct.hip), or null
 };
 inline CaptureState& capture_state() {
   static thread_local CaptureState c;
@@ -54,6 +56,9 @@ struct JoinKnobs {
   uint64_t onepass_cap_div = 8;        // HY_ONEPASS_CAP_DIV
   uint64_t onepass_cap = 0;            // HY_ONEPASS_CAP (0: computed)
   bool filter_buckets = true;          // HY_FILTER_BUCKETS: prefilter words set per LDS region (0: global atomics)
+  bool direct = true;                  // HY_JOIN_DIRECT: direct partitioning of a filtered side (join_direct.hip)
+  uint32_t direct_span = 16;           // HY_DIRECT_SPAN: tiles per span of the direct first pass
+  uint32_t direct_groups = 0;          // HY_DIRECT_GROUPS: span groups per bucket of the direct second pass (0: auto)
 };
 
 inline JoinKnobs knobs_from_env() {
@@ -74,6 +79,9 @@ inline JoinKnobs knobs_from_env() {
   k.onepass_cap_div = static_cast<uint64_t>(std::max<long long>(1, num("HY_ONEPASS_CAP_DIV", 8)));
   k.onepass_cap = static_cast<uint64_t>(std::max<long long>(0, num("HY_ONEPASS_CAP", 0)));
   k.filter_buckets = num("HY_FILTER_BUCKETS", 1) != 0;
+  k.direct = num("HY_JOIN_DIRECT", 1) != 0;
+  k.direct_span = static_cast<uint32_t>(std::min<long long>(std::max<long long>(1, num("HY_DIRECT_SPAN", 16)), 64));
+  k.direct_groups = static_cast<uint32_t>(std::min<long long>(std::max<long long>(0, num("HY_DIRECT_GROUPS", 0)), 4096));
   return k;
 }
 
@@ -337,6 +345,9 @@ inline hy_status plan_filter(const hy_join_filter* f, SidePlan& p, int32_t colum
   if (column_type != hashed_type)
     return fail(HY_ERR_UNSUPPORTED, "a fused scan needs the side's join column to have the hashed type");
   if (p.chunks.size() && !f->chunks) return fail(HY_ERR_INVALID_ARGUMENT, "filter chunks");
+  if (f->n_chunks < p.chunks.size())
+    return fail(HY_ERR_INVALID_ARGUMENT, "filter has " + std::to_string(f->n_chunks) + " predicate chunks for a side of " +
+                                             std::to_string(p.chunks.size()) + " chunks");
   if (p.n_rows >= 0x7FFFFFFFull) return fail(HY_ERR_UNSUPPORTED, "filtered join side exceeds 2^31-1 rows");
   p.filtered = true;
   p.filter.assign(f->chunks, f->chunks + p.chunks.size());
@@ -1570,6 +1581,221 @@ hy_status join_typed_onepass(const SidePlan& bp, const SidePlan& pp, const hy_jo
   return st;
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Direct partitioning of a side with a fused TableScan (kernels/join_direct.hip): span match counts, part1_direct
+// (one read of the predicate and the keys; records into (span, bucket) regions), part2g_hist / part2g_scatter over
+// (bucket, span group) run lists. Replaces part1_compact + part1_spread + the per-tile record pass of a two-digit plan:
+// at SF100 the 8-byte record round trip (2.3 GB written, read back) and the per-tile histograms are gone. A region
+// overflow (keys far more skewed than murmur2 spreads them) is detected on the device and the join reruns on the
+// classic passes (join_typed). HY_JOIN_DIRECT=0 keeps the classic passes (A/B).
+// ---------------------------------------------------------------------------------------------------------------
+struct DirectPlan {
+  bool ok = false;
+  SidePlan plan;           // the side with spans of knobs().direct_span tiles
+  uint64_t n_spans = 0;
+  uint64_t regions = 0;    // records of all regions at their largest (every row matching)
+  uint32_t groups = 0;     // span groups per bucket of the second pass (H)
+  uint32_t per = 0;        // spans per group
+  uint32_t nd0 = 0, nd1 = 0;
+};
+
+// Whether the direct passes take a side, and their geometry. keep_nulls / prefiltered sides stay on the classic
+// passes (their records carry NULL rows or skip rows the scan matched).
+template <typename H>
+DirectPlan direct_plan(const SidePlan& p, uint32_t bits, bool keep_nulls, bool prefiltered) {
+  DirectPlan d;
+  const auto w = digit_plan(bits, 0);
+  const JoinKnobs k = knobs();
+  if (!k.direct || k.blocked || !p.filtered || w.size() != 2 || keep_nulls || prefiltered || p.fuse ||
+      !p.referenced.empty())
+    return d;
+  if (filter_kind(p) == hyk::FK_NONE) return d;
+  const int lp = load_path(p);
+  if (lp != hyk::LP_VALUE && lp != hyk::LP_ANY) return d;
+  d.plan = p;
+  plan_spans(d.plan, k.direct_span);
+  d.n_spans = d.plan.n_tiles1;
+  if (d.n_spans == 0 || d.n_spans >= 0x7FFFFFFFull) return d;
+  d.nd0 = 1u << w[0];
+  d.nd1 = 1u << w[1];
+  const uint64_t span_rows = uint64_t(d.plan.sub) * hyk::PART_TILE;
+  uint64_t regions = 0;
+  for (size_t c = 0; c < d.plan.chunks.size(); ++c) {
+    const uint64_t rows = d.plan.chunks[c].size;
+    for (uint64_t r0 = 0; r0 < rows; r0 += span_rows)
+      regions += uint64_t(d.nd0) * hyk::direct_cap(static_cast<uint32_t>(std::min(span_rows, rows - r0)), d.nd0);
+  }
+  if (regions >= 0xFFFFFFFFull) return d;  // (record indexes of the regions are scanned in 32 bits)
+  d.regions = regions;
+  const uint64_t min_groups = (d.n_spans + hyk::GROUP_MAX_RUNS - 1) / hyk::GROUP_MAX_RUNS;
+  uint64_t h = k.direct_groups ? k.direct_groups : std::max<uint64_t>(1, (1024 + d.nd0 - 1) / d.nd0);
+  h = std::min<uint64_t>(std::max(h, min_groups), d.n_spans);
+  d.per = static_cast<uint32_t>((d.n_spans + h - 1) / h);
+  d.groups = static_cast<uint32_t>((d.n_spans + d.per - 1) / d.per);
+  d.ok = true;
+  return d;
+}
+
+template <typename H>
+struct DirectBufs {
+  SideBufs<H> b;  // the side's descriptors (chunks, spans, predicate chunks); nothing else of it is used
+  uint32_t *span_cnt, *span_scan, *span_cap, *cap_words, *rbase32, *counts, *hist, *off, *bounds, *overflow;
+  uint64_t* span_rbase;
+  uint64_t* totals;  // [0] scan matches, [1] region records, [2] records taking part
+  hyk::Rec<H>* regions;
+  uint8_t* dig;
+  hyk::Rec<H>* out;  // the last pass's records: {key, payload} or the hash-record (SoA) area
+};
+
+template <typename H>
+void carve_direct(Carver& cv, const DirectPlan& d, uint32_t bits, DirectBufs<H>& o) {
+  const SidePlan& p = d.plan;
+  const size_t nc = p.chunks.size();
+  o.b = SideBufs<H>{};
+  o.b.chunks = cv.take<hyk::SrcChunk>(std::max<size_t>(1, nc));
+  o.b.tile_begin = cv.take<uint64_t>(nc + 1);
+  o.b.row_begin = cv.take<uint64_t>(nc + 1);
+  o.b.referenced = cv.take<hyk::SrcChunk>(1);
+  o.b.ref_row_begin = cv.take<uint64_t>(1);
+  o.b.filter = cv.take<hy_scan_chunk>(std::max<size_t>(1, nc));
+  o.b.tile_owner = cv.take<uint32_t>(std::max<uint64_t>(1, d.n_spans));
+  const uint64_t ns = std::max<uint64_t>(1, d.n_spans);
+  o.span_cnt = cv.take<uint32_t>(ns);
+  o.span_scan = cv.take<uint32_t>(ns);
+  o.span_cap = cv.take<uint32_t>(ns);
+  o.cap_words = cv.take<uint32_t>(ns);
+  o.rbase32 = cv.take<uint32_t>(ns);
+  o.span_rbase = cv.take<uint64_t>(ns);
+  o.counts = cv.take<uint32_t>(uint64_t(d.nd0) * ns);
+  const uint64_t hw = uint64_t(d.nd0) * d.nd1 * std::max<uint32_t>(1, d.groups);
+  o.hist = cv.take<uint32_t>(hw);
+  o.off = cv.take<uint32_t>(hw);
+  o.bounds = cv.take<uint32_t>((uint64_t(1) << bits) + 1);
+  o.overflow = cv.take<uint32_t>(4);
+  o.totals = cv.take<uint64_t>(4);
+  o.regions = cv.take<hyk::Rec<H>>(std::max<uint64_t>(1, d.regions));
+  o.dig = cv.take<uint8_t>(std::max<uint64_t>(16, d.regions));
+  o.out = cv.take<hyk::Rec<H>>(std::max<uint64_t>(16, p.n_rows));
+}
+
+template <typename H>
+size_t direct_scan_words(const DirectPlan& d) {
+  return std::max<uint64_t>(d.n_spans, uint64_t(d.nd0) * d.nd1 * std::max<uint32_t>(1, d.groups));
+}
+
+template <typename SD, typename T, typename H, int LP, int FK>
+void launch_part1_direct(const DirectPlan& d, const hyk::Side& sd, const hyk::Digit& d0, const hyk::NextDigit& nd,
+                         const hyk::DirectGeo& g, hyk::Rec<H>* regions, hipStream_t s) {
+  hipLaunchKernelGGL((hyk::part1_direct<SD, T, H, LP, FK>), dim3(static_cast<uint32_t>(d.n_spans)),
+                     dim3(hyk::PART_THREADS), 0, s, sd, d0, nd, d.nd0, g, regions);
+}
+
+template <typename SD, typename T, typename H, int LP>
+hy_status part1_direct_lp(const DirectPlan& d, int fk, const hyk::Side& sd, const hyk::Digit& d0,
+                          const hyk::NextDigit& nd, const hyk::DirectGeo& g, hyk::Rec<H>* regions, hipStream_t s) {
+  switch (fk) {
+    case hyk::FK_DICT8:
+      launch_part1_direct<SD, T, H, LP, hyk::FK_DICT8>(d, sd, d0, nd, g, regions, s);
+      break;
+    case hyk::FK_DICT16:
+      launch_part1_direct<SD, T, H, LP, hyk::FK_DICT16>(d, sd, d0, nd, g, regions, s);
+      break;
+    case hyk::FK_DICT32:
+      launch_part1_direct<SD, T, H, LP, hyk::FK_DICT32>(d, sd, d0, nd, g, regions, s);
+      break;
+    default:
+      launch_part1_direct<SD, T, H, LP, hyk::FK_ANY>(d, sd, d0, nd, g, regions, s);
+      break;
+  }
+  HY_HIP(hipGetLastError());
+  return HY_OK;
+}
+
+// The direct passes of one side into last_out (the final partitions); *bounds receives the partition bounds.
+template <typename SD, typename T, typename H>
+hy_status direct_side(const DirectPlan& d, DirectBufs<H>& o, uint32_t bits, uint32_t seed, const Common& c,
+                      hipStream_t s, const hyk::RecOut<H, uint32_t>& last_out, uint32_t** bounds) {
+  const SidePlan& p = d.plan;
+  const uint32_t n_spans = static_cast<uint32_t>(d.n_spans);
+  const uint32_t nc = static_cast<uint32_t>(p.chunks.size());
+  const hyk::Side sd = make_side(p, o.b, seed, false, p.ref_base, nullptr, 0, false, nullptr, 0);
+  HY_HIP(hipMemsetAsync(o.overflow, 0, 16, s));
+  hipLaunchKernelGGL(hyk::fill_tile_owner, dim3(grid_for(nc, 256)), dim3(256), 0, s, o.b.tile_begin, nc, o.b.tile_owner);
+  HY_HIP(hipGetLastError());
+  const int fk = filter_kind(p);
+  {
+    KTimer kt_((std::string("span_match_count.") + SD::name).c_str(), s, p.n_rows);
+    auto count = [&](auto kernel) {
+      hipLaunchKernelGGL(kernel, dim3(n_spans), dim3(hyk::PART_THREADS), 0, s, sd, d.nd0, o.span_cnt, o.span_cap,
+                         o.cap_words);
+    };
+    if (fk == hyk::FK_DICT8)
+      count(hyk::span_match_count<hyk::FK_DICT8>);
+    else if (fk == hyk::FK_DICT16)
+      count(hyk::span_match_count<hyk::FK_DICT16>);
+    else if (fk == hyk::FK_DICT32)
+      count(hyk::span_match_count<hyk::FK_DICT32>);
+    else
+      count(hyk::span_match_count<hyk::FK_ANY>);
+    kt_.done();
+  }
+  HY_HIP(hipGetLastError());
+  hy_status st = run_scan(o.span_cnt, o.span_scan, n_spans, c, s, o.totals + 0);
+  if (st != HY_OK) return st;
+  st = run_scan(o.cap_words, o.rbase32, n_spans, c, s, o.totals + 1);
+  if (st != HY_OK) return st;
+  hipLaunchKernelGGL(hyk::widen_u32, dim3(grid_for(n_spans, 256)), dim3(256), 0, s, o.rbase32, n_spans, o.span_rbase);
+  HY_HIP(hipGetLastError());
+  if (p.scan_chunk_begin) {
+    hipLaunchKernelGGL(hyk::direct_chunk_begin, dim3(grid_for(nc + 1, 256)), dim3(256), 0, s, o.span_scan, n_spans,
+                       o.b.tile_begin, nc, o.totals + 0, p.scan_chunk_begin);
+    HY_HIP(hipGetLastError());
+  }
+  const hyk::DirectGeo g{o.span_rbase, o.span_cap, o.span_scan, o.counts, o.overflow, n_spans};
+  const hyk::Digit d0{full_mask(bits), bits - (31 - __builtin_clz(d.nd0)), d.nd0 - 1u, seed, g_key_hash};
+  // (HY_DIRECT_NOBYTES: an experiment that skips the digit bytes - the second pass's histogram is then wrong)
+  static const bool no_bytes = std::getenv("HY_DIRECT_NOBYTES") != nullptr;
+  const hyk::NextDigit nd{no_bytes ? nullptr : o.dig, 0u, d.nd1 - 1u};
+  {
+    KTimer kt_((std::string("part1_direct.") + SD::name).c_str(), s, p.n_rows);
+    st = load_path(p) == hyk::LP_VALUE ? part1_direct_lp<SD, T, H, hyk::LP_VALUE>(d, fk, sd, d0, nd, g, o.regions, s)
+                                       : part1_direct_lp<SD, T, H, hyk::LP_ANY>(d, fk, sd, d0, nd, g, o.regions, s);
+    kt_.done();
+    if (st != HY_OK) return st;
+  }
+  const hyk::GroupGeo gg{o.span_rbase, o.span_cap, o.counts, n_spans, d.groups, d.per};
+  const dim3 g2(d.nd0 * d.groups);
+  {
+    KTimer kt_((std::string("part2g_hist.") + SD::name).c_str(), s, p.n_rows);
+    hipLaunchKernelGGL(hyk::part2g_hist<SD>, g2, dim3(hyk::PART_THREADS), 0, s, gg, d.nd1, o.dig, o.hist);
+    kt_.done();
+  }
+  HY_HIP(hipGetLastError());
+  st = run_scan(o.hist, o.off, uint64_t(d.nd0) * d.nd1 * d.groups, c, s, o.totals + 2);
+  if (st != HY_OK) return st;
+  const hyk::Digit d1{full_mask(bits), 0u, d.nd1 - 1u, seed, g_key_hash};
+  {
+    KTimer kt_((std::string("part2g_scatter.") + SD::name).c_str(), s, p.n_rows);
+    hipLaunchKernelGGL((hyk::part2g_scatter<SD, H, uint32_t>), g2, dim3(hyk::PART_THREADS), 0, s, gg, d1, d.nd1,
+                       o.regions, o.off, last_out);
+    kt_.done();
+  }
+  HY_HIP(hipGetLastError());
+  const uint32_t n_parts = d.nd0 * d.nd1;
+  hipLaunchKernelGGL(hyk::group_bounds, dim3(grid_for(n_parts + 1, 256)), dim3(256), 0, s, o.off, n_parts, d.groups,
+                     o.totals + 2, o.bounds);
+  HY_HIP(hipGetLastError());
+  *bounds = o.bounds;
+  return HY_OK;
+}
+
+// A join whose direct pass overflowed a region reran on the classic passes (read by prepared plans, which then keep
+// the classic passes: their workspace holds the classic carve's descriptors from that execution on).
+inline bool& direct_fell_back() {
+  static thread_local bool v = false;
+  return v;
+}
+
 // Pass-0 spans of one tile each (part1_onepass handles one tile per workgroup).
 inline SidePlan one_tile_spans(const SidePlan& p) {
   SidePlan q = p;
@@ -1610,52 +1836,86 @@ inline SideStream* side_stream() {
   return &x;
 }
 
+// Workspace of a join whose probe side takes the direct passes (join_typed's carve with direct set).
+template <typename H>
+size_t direct_join_bytes(const SidePlan& bp, const DirectPlan& dpl, uint32_t bits) {
+  const auto w = digit_plan(bits, 0);
+  const bool db = w.size() > 1 && digit_bytes_enabled();
+  constexpr bool i32 = std::is_same_v<H, int32_t>;
+  const uint32_t kb = block_count(bp, sizeof(H), w.size(), i32);
+  Carver cv{nullptr, 0};
+  SideBufs<H> a;
+  DirectBufs<H> o;
+  carve_side<H, uint32_t>(cv, sizes_of(bp, db, kb), bits, w, 1, true, a);
+  carve_direct<H>(cv, dpl, bits, o);
+  uint64_t ha, t;
+  pass_sizes(sizes_of(bp, db, kb), w, 1, &ha, &t);
+  Common c, cb;
+  const uint64_t fb_scan = filter_buckets(bloom_words(bp.n_rows, dpl.plan.n_rows), bp.n_rows).scan_len;
+  carve_common(cv, std::max({ha, uint64_t(direct_scan_words<H>(dpl)), (uint64_t(1) << bits) + 1, fb_scan}), bits, &c);
+  carve_common(cv, std::max({ha, (uint64_t(1) << bits) + 1}), bits, &cb);
+  cv.take<uint32_t>(prefilter_words(bloom_words(bp.n_rows, dpl.plan.n_rows), bp.n_rows));
+  return cv.used + 256;
+}
+
 template <typename H>
 size_t join_bytes(const SidePlan& bp, const SidePlan& pp, uint32_t bits) {
   size_t n = classic_join_bytes<H>(bp, pp, bits);
+  if constexpr (std::is_integral_v<H>) {
+    const DirectPlan dpl = direct_plan<H>(pp, bits, false, false);
+    if (dpl.ok) n = std::max(n, direct_join_bytes<H>(bp, dpl, bits));
+  }
   const auto w = digit_plan(bits, 0);
   const SidePlan b1 = one_tile_spans(bp), p1 = one_tile_spans(pp);
   if (onepass_ok(b1, w) && onepass_ok(p1, w)) n = std::max(n, onepass_bytes<H>(b1, p1, bits));
   return n;
 }
 
+// The classic passes, or (allow_direct) the direct passes for the probe side where they apply; *direct_overflow
+// (eager executions) receives whether a direct region overflowed - the output is then invalid.
 template <typename TB, typename TP, typename H>
-hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join_params* prm, hy_row_id* out_build,
-                     hy_row_id* out_probe, uint64_t out_capacity, uint64_t* partition_begin,
-                     uint32_t* partition_counts, hy_join_result* result, void* workspace, size_t workspace_bytes,
-                     hipStream_t s) {
+hy_status join_typed_passes(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join_params* prm,
+                            hy_row_id* out_build, hy_row_id* out_probe, uint64_t out_capacity,
+                            uint64_t* partition_begin, uint32_t* partition_counts, hy_join_result* result,
+                            void* workspace, size_t workspace_bytes, hipStream_t s, bool allow_direct,
+                            bool* direct_overflow) {
   const uint32_t bits = prm->radix_bits;
-  {
-    const auto w = digit_plan(bits, 0);
-    const SidePlan b1 = one_tile_spans(bp_in), p1 = one_tile_spans(pp_in);
-    if (onepass_ok(b1, w) && onepass_ok(p1, w) && workspace_bytes >= onepass_bytes<H>(b1, p1, bits)) {
-      uint32_t overflow = 0;
-      const hy_status st = join_typed_onepass<TB, TP, H>(b1, p1, prm, out_build, out_probe, out_capacity,
-                                                         partition_begin, partition_counts, result, workspace,
-                                                         workspace_bytes, s, &overflow);
-      if (overflow == 0) return st;
-      // a gapped region overflowed (or a look-back timed out): the two-read path below recomputes everything
-    }
-  }
+  const bool keep_nulls = prm->mode == HY_JOIN_LEFT || prm->mode == HY_JOIN_RIGHT;
+  const uint64_t bloom_n = bloom_words(bp_in.n_rows, pp_in.n_rows);
+  const bool use_bloom = bloom_n && (prm->mode == HY_JOIN_INNER || prm->mode == HY_JOIN_SEMI);
+  DirectPlan dpl;
+  if constexpr (std::is_same_v<TP, H> && std::is_integral_v<H>)
+    if (allow_direct) dpl = direct_plan<H>(pp_in, bits, keep_nulls, use_bloom);
+  const bool direct = dpl.ok;
   const SidePlan& bp = bp_in;
-  const SidePlan& pp = pp_in;
-  if (workspace_bytes < classic_join_bytes<H>(bp, pp, bits)) return fail(HY_ERR_WORKSPACE, "join workspace too small");
+  const SidePlan& pp = direct ? dpl.plan : pp_in;
+  if (workspace_bytes < (direct ? direct_join_bytes<H>(bp, dpl, bits) : classic_join_bytes<H>(bp, pp, bits)))
+    return fail(HY_ERR_WORKSPACE, "join workspace too small");
   const auto w = digit_plan(bits, 0);
   const bool db = w.size() > 1 && digit_bytes_enabled();
   constexpr bool i32 = std::is_same_v<H, int32_t>;
-  const uint32_t blocks[2] = {block_count(bp, sizeof(H), w.size(), i32), block_count(pp, sizeof(H), w.size(), i32)};
+  const uint32_t blocks[2] = {block_count(bp, sizeof(H), w.size(), i32),
+                              direct ? 0u : block_count(pp, sizeof(H), w.size(), i32)};
   Carver cv{static_cast<char*>(workspace), workspace_bytes};
   SideBufs<H> bb, pb;
+  DirectBufs<H> dbuf{};
   carve_side<H, uint32_t>(cv, sizes_of(bp, db, blocks[0]), bits, w, 1, true, bb);
-  carve_side<H, uint32_t>(cv, sizes_of(pp, db, blocks[1]), bits, w, 1, true, pb);
+  if (direct) {
+    carve_direct<H>(cv, dpl, bits, dbuf);
+    pb = dbuf.b;
+  } else {
+    carve_side<H, uint32_t>(cv, sizes_of(pp, db, blocks[1]), bits, w, 1, true, pb);
+  }
   uint64_t ha, hb2, t;
   pass_sizes(sizes_of(bp, db, blocks[0]), w, 1, &ha, &t);
-  pass_sizes(sizes_of(pp, db, blocks[1]), w, 1, &hb2, &t);
+  if (direct)
+    hb2 = direct_scan_words<H>(dpl);
+  else
+    pass_sizes(sizes_of(pp, db, blocks[1]), w, 1, &hb2, &t);
   Common c{}, cb{};  // c: the probe side and the partition join; cb: the build side (it may run concurrently)
-  const uint64_t bloom_n = bloom_words(bp.n_rows, pp.n_rows);
   const FilterBuckets fbk = filter_buckets(bloom_n, bp.n_rows);
   carve_common(cv, std::max({ha, hb2, (uint64_t(1) << bits) + 1, fbk.scan_len}), bits, &c);
-  carve_common(cv, std::max({ha, hb2, (uint64_t(1) << bits) + 1}), bits, &cb);
+  carve_common(cv, std::max({ha, (uint64_t(1) << bits) + 1}), bits, &cb);
   uint32_t* filter_area = cv.take<uint32_t>(prefilter_words(bloom_n, bp.n_rows));
   auto* filter_hdr = reinterpret_cast<hyk::FilterHdr*>(filter_area);
   uint32_t* bloom = filter_area + 16;
@@ -1666,8 +1926,6 @@ hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join
   uint64_t* fb_count = fb_items ? reinterpret_cast<uint64_t*>(fb_items + ((bp.n_rows + 1) & ~uint64_t(1))) : nullptr;
   if (!cv.ok) return fail(HY_ERR_WORKSPACE, "join workspace too small");
   if (upload_side(bp, bb, s) || upload_side(pp, pb, s)) return HY_ERR_DEVICE;
-  const bool keep_nulls = prm->mode == HY_JOIN_LEFT || prm->mode == HY_JOIN_RIGHT;
-  const bool use_bloom = bloom_n && (prm->mode == HY_JOIN_INNER || prm->mode == HY_JOIN_SEMI);
   // the build side on the side stream unless the probe side needs its Bloom filter first
   // (not while per-kernel timing is on: concurrent kernels' event intervals would overlap and each read slower)
   bool timing = false;
@@ -1696,7 +1954,8 @@ hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join
     const bool last_in_b = (w.size() - 1) % 2 == 1;
     soa_outs[0] = soa_out<H, uint32_t>(last_in_b ? bb.recB : bb.recA, bp.n_rows, bits, use_bloom ? bloom : nullptr,
                                        bloom_n);
-    soa_outs[1] = soa_out<H, uint32_t>(last_in_b ? pb.recB : pb.recA, pp.n_rows, bits);
+    soa_outs[1] = soa_out<H, uint32_t>(direct ? static_cast<void*>(dbuf.out) : (last_in_b ? pb.recB : pb.recA),
+                                       pp.n_rows, bits);
   }
 
   hyk::Rec<H>* recs[2] = {nullptr, nullptr};
@@ -1708,7 +1967,14 @@ hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join
     const Common& cs = side == 0 ? cb : c;
     const hipStream_t st_s = side == 0 ? sb : s;
     const hyk::NextDigit nd = next_digit(w, 0, bits, b.digA);
-    if (blocks[side]) {  // pass 0 in row blocks and the record passes after it
+    if (side == 1 && direct) {  // the probe side's direct passes (join_direct.hip)
+      if constexpr (std::is_same_v<TP, H> && std::is_integral_v<H>) {
+        const hyk::RecOut<H, uint32_t> lo = soa ? soa_outs[1] : aos_out<H, uint32_t>(dbuf.out);
+        hy_status st = direct_side<hyk::OnProbe, TP, H>(dpl, dbuf, bits, prm->seed, c, s, lo, &bounds[1]);
+        if (st != HY_OK) return st;
+        recs[1] = dbuf.out;
+      }
+    } else if (blocks[side]) {  // pass 0 in row blocks and the record passes after it
       const bool pf = side == 1 && use_bloom;
       const hyk::Side sd = make_side(p, b, prm->seed, side == 1 && keep_nulls, p.ref_base, pf ? bloom : nullptr, bloom_n,
                                      soa, pf && range_filter ? filter_hdr : nullptr,
@@ -1776,6 +2042,7 @@ hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join
   const hyk::RowMap bmap = bp.fuse ? make_map(bb.ref_row_begin, bp.ref_row_begin) : make_map(bb.row_begin, bp.row_begin);
   const hyk::RowMap pmap = pp.fuse ? make_map(pb.ref_row_begin, pp.ref_row_begin) : make_map(pb.row_begin, pp.row_begin);
   const bool probe_exact = !pp.filtered && !use_bloom;  // (a Bloom prefilter drops probe rows too)
+  hy_status st = HY_OK;
   if (soa) {
     auto run_hash = [&](auto tag) {
       using HS = decltype(tag);
@@ -1785,12 +2052,56 @@ hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join
                                                s, bp.n_rows + pp.n_rows, pp.n_rows, probe_exact);
     };
     // records per lane and load (A/B, HY_HASH_GROUP): 1 (default) or 4
-    return knobs().hash_group == 4 ? run_hash(hyk::HashSrc<uint32_t, 4>{}) : run_hash(hyk::HashSrc<uint32_t, 1>{});
+    st = knobs().hash_group == 4 ? run_hash(hyk::HashSrc<uint32_t, 4>{}) : run_hash(hyk::HashSrc<uint32_t, 1>{});
+  } else {
+    st = run_join_partitions<hyk::RecSrc<H, uint32_t>, uint32_t>(
+        bounds[0], bounds[1], 1u << bits, hyk::RecSrc<H, uint32_t>{recs[0]}, hyk::RecSrc<H, uint32_t>{recs[1]}, bmap,
+        pmap, prm->mode, out_build, out_probe, out_capacity, partition_begin, partition_counts, result, c, s,
+        bp.n_rows + pp.n_rows, pp.n_rows, probe_exact);
   }
-  return run_join_partitions<hyk::RecSrc<H, uint32_t>, uint32_t>(
-      bounds[0], bounds[1], 1u << bits, hyk::RecSrc<H, uint32_t>{recs[0]}, hyk::RecSrc<H, uint32_t>{recs[1]}, bmap,
-      pmap, prm->mode, out_build, out_probe, out_capacity, partition_begin, partition_counts, result, c, s,
-      bp.n_rows + pp.n_rows, pp.n_rows, probe_exact);
+  if (direct) {
+    if (capture_state().capturing) {  // (a prepared plan's replay reads the flag after the graph: finish_replay)
+      capture_state().direct_overflow = dbuf.overflow;
+    } else if (direct_overflow) {
+      uint32_t f = 0;
+      HY_HIP(hipMemcpyAsync(&f, dbuf.overflow, 4, hipMemcpyDeviceToHost, s));
+      HY_HIP(hipStreamSynchronize(s));
+      *direct_overflow = f != 0;
+    }
+  }
+  return st;
+}
+
+template <typename TB, typename TP, typename H>
+hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join_params* prm, hy_row_id* out_build,
+                     hy_row_id* out_probe, uint64_t out_capacity, uint64_t* partition_begin,
+                     uint32_t* partition_counts, hy_join_result* result, void* workspace, size_t workspace_bytes,
+                     hipStream_t s) {
+  const uint32_t bits = prm->radix_bits;
+  {
+    const auto w = digit_plan(bits, 0);
+    const SidePlan b1 = one_tile_spans(bp_in), p1 = one_tile_spans(pp_in);
+    if (onepass_ok(b1, w) && onepass_ok(p1, w) && workspace_bytes >= onepass_bytes<H>(b1, p1, bits)) {
+      uint32_t overflow = 0;
+      const hy_status st = join_typed_onepass<TB, TP, H>(b1, p1, prm, out_build, out_probe, out_capacity,
+                                                         partition_begin, partition_counts, result, workspace,
+                                                         workspace_bytes, s, &overflow);
+      if (overflow == 0) return st;
+      // a gapped region overflowed (or a look-back timed out): the two-read path below recomputes everything
+    }
+  }
+  bool overflow = false;
+  const hy_status st = join_typed_passes<TB, TP, H>(bp_in, pp_in, prm, out_build, out_probe, out_capacity,
+                                                    partition_begin, partition_counts, result, workspace,
+                                                    workspace_bytes, s, true, &overflow);
+  if (!overflow || (st != HY_OK && st != HY_ERR_CAPACITY)) return st;
+  // a direct region overflowed: the classic passes recompute everything (the workspace is carved differently, so
+  // both sides' descriptors are staged again)
+  direct_fell_back() = true;
+  SidePlan b2 = bp_in, p2 = pp_in;
+  b2.device_ready = p2.device_ready = false;
+  return join_typed_passes<TB, TP, H>(b2, p2, prm, out_build, out_probe, out_capacity, partition_begin,
+                                      partition_counts, result, workspace, workspace_bytes, s, false, nullptr);
 }
 
 template <typename F>

@@ -375,7 +375,10 @@ PYBIND11_MODULE(_hyrise_host, m) {
 
   py::class_<OperatorPerformanceData>(m, "OperatorPerformanceData")
       .def_readonly("walltime_ns", &OperatorPerformanceData::walltime_ns)
-      .def_readonly("rows_in", &OperatorPerformanceData::rows_in);
+      .def_readonly("rows_in", &OperatorPerformanceData::rows_in)
+      .def_readonly("device_ns", &OperatorPerformanceData::device_ns)
+      .def_readonly("bytes_read", &OperatorPerformanceData::bytes_read)
+      .def_readonly("bytes_written", &OperatorPerformanceData::bytes_written);
 
   // the host scheduler the operators submit their jobs to (scheduler.hpp): "pool" (n workers fed from one queue),
   // "inline" (jobs run when scheduled) or None (a thread per job)

@@ -1,6 +1,10 @@
 #include "operators.hpp"
 #include "scheduler.hpp"
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
+#include "hyrise_amd_trace.h"
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -57,6 +61,42 @@ std::vector<OpTraceRecord> op_trace_take() {
   return out;
 }
 
+namespace {
+// A roctx range per operator execution (rocprofv3 --marker-trace shows each operator around its kernels).
+struct OperatorRange {
+  explicit OperatorRange(const std::string& name) { roctxRangePushA(name.c_str()); }
+  ~OperatorRange() { roctxRangePop(); }
+};
+
+// The device time of the operator's stream work: an event on this thread's operator stream before _on_execute and
+// one after it. finish() (after the stream's synchronisation) returns the nanoseconds between them, 0 when the
+// operator issued nothing on the stream (the events then complete back to back).
+struct DeviceSpan {
+  struct Events {
+    hy_event_t start = nullptr, stop = nullptr;
+    ~Events() {
+      hy_event_destroy(start);
+      hy_event_destroy(stop);
+    }
+  };
+  Events* ev = nullptr;
+  DeviceSpan() {
+    int n = 0;
+    if (hy_get_device_count(&n) != HY_OK || n <= 0) return;  // (no device: the operator fails on its own)
+    thread_local Events events;
+    if (!events.start && (hy_event_create(&events.start) != HY_OK || hy_event_create(&events.stop) != HY_OK)) return;
+    if (hy_event_record(events.start, operator_stream()) == HY_OK) ev = &events;
+  }
+  uint64_t finish() {
+    uint64_t ns = 0;
+    if (ev && hy_event_record(ev->stop, operator_stream()) == HY_OK &&
+        hy_event_elapsed_ns(ev->start, ev->stop, &ns) == HY_OK)
+      return ns;
+    return 0;
+  }
+};
+}  // namespace
+
 // reference abstract_operator.cpp:25-54
 void AbstractOperator::execute() {
   Assert(!_input_left || _input_left->get_output(), "Left input has not been executed");
@@ -66,10 +106,13 @@ void AbstractOperator::execute() {
   // abstract_operator.cpp:32-41: an aborted transaction skips the operator; its output stays unset
   const auto context = transaction_context();
   if (context && context->aborted()) return;
+  OperatorRange range(name());
+  DeviceSpan span;
   _output = _on_execute(context);
   // The output is complete when execute() returns (the reference's contract): consumers may run on other threads,
   // whose non-blocking operator streams are not ordered after this thread's kernels.
   operator_stream_synchronize_if_used();
+  _performance_data.device_ns = span.finish();
   _on_cleanup();
   _performance_data.walltime_ns = static_cast<uint64_t>(
       std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count());
@@ -614,6 +657,10 @@ struct DataScan final : Table::Producer {
   // hy_table_scan_count preconditions), no IS NULL, every chunk of the table scanned
   bool fusable() const {
     if (!all_chunks || descs.empty()) return false;
+    // the descriptors were built when the scan executed: the table may have grown since (Table::append_chunks)
+    if (descs.size() != in_table->chunk_count()) return false;
+    for (size_t k = 0; k < descs.size(); ++k)
+      if (in_table->get_chunk(chunk_ids[k])->size() != sizes[k]) return false;
     int width = 0;
     for (const auto& d : descs) {
       if (d.column.kind != HY_COL_DICT || d.op == HY_OP_IS_NULL || d.op == HY_OP_IS_NOT_NULL || d.op == HY_OP_VID_SET)
@@ -789,6 +836,16 @@ std::shared_ptr<const Table> TableScan::_on_execute() {
       for (size_t k = 0; k < descs.size(); ++k) views.emplace_back(descs[k].out_begin, h_counts[k]);
     }
     tr.mark("counts synchronised");
+    {  // algorithmic bytes: the predicate column's stored bytes (ids / values), 8 B per output RowID
+      uint64_t rd = 0, wr = 0;
+      for (size_t k = 0; k < descs.size(); ++k) {
+        const auto& c = descs[k].column;
+        rd += uint64_t(sizes[k]) * (c.kind == HY_COL_DICT ? c.vid_width : col_type == DataType::String ? 4 : data_type_size(col_type));
+        wr += uint64_t(views[k].second) * sizeof(RowID);
+      }
+      _performance_data.bytes_read = rd;
+      _performance_data.bytes_written = wr;
+    }
     // output PosLists are lazy views of `rows` (no copy to the host, no wait: later work is ordered on the stream);
     // chunks, columns and PosLists from an output arena (device.hpp)
     OutputArena arena;
@@ -1560,7 +1617,8 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
     scan_offsets = std::make_unique<DeviceBuffer>(std::max<uint64_t>(fused_scan->total, 1) * 4, s);
     scan_begin = std::make_unique<DeviceBuffer>((fused_scan->descs.size() + 1) * 8, s);
     pf = hy_join_filter{fused_scan->descs.data(), hy_type_of(fused_scan->col_type), fused_scan->constant.bytes,
-                        scan_offsets->as<uint32_t>(), scan_begin->as<uint64_t>()};
+                        scan_offsets->as<uint32_t>(), scan_begin->as<uint64_t>(),
+                        static_cast<uint32_t>(fused_scan->descs.size())};
   }
   size_t ws_bytes = 0;
   if (fused_scan)
@@ -1695,6 +1753,9 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
                                      static_cast<uint32_t>(fused_scan->descs.size()), scan_rows->as<hy_row_id>(), s),
              "hy_expand_chunk_row_ids");
     scan_builder.wait();
+    // consumers blocked in resolve() on other threads read scan_rows from their own streams as soon as the chunks are
+    // published: the expansion must have finished (execute()'s own sync comes later)
+    hy_check(hy_stream_synchronize(s), "sync");
     std::const_pointer_cast<Table>(probe_table)->fulfil(std::move(scan_chunks));
     untake.scan = nullptr;
     tr.mark("fused TableScan output");
@@ -1703,6 +1764,21 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
   uint64_t used = 0;  // the output range the partitions occupy
   for (uint32_t part = 0; part < n_parts; ++part)
     if (h_count[part]) used = std::max<uint64_t>(used, h_begin[part] + h_count[part]);
+  {  // algorithmic bytes: both join columns (+ 8 B per row read through a PosList, + the fused scan's predicate ids
+     // of every scanned row), 16 B per output pair (+ the fused scan's 8 B RowIDs)
+    const uint64_t kb = build_type == DataType::String ? 4 : data_type_size(build_type);
+    const uint64_t kp = probe_type == DataType::String ? 4 : data_type_size(probe_type);
+    uint64_t rd = build_rows * (kb + (build_table->type() == TableType::References ? 8 : 0));
+    if (fused_scan) {
+      uint64_t vid = 0;
+      for (const auto& d : fused_scan->descs) vid += uint64_t(d.column.size) * d.column.vid_width;
+      rd += fused_scan->total * kp + vid;
+    } else {
+      rd += probe_rows * (kp + (probe_table->type() == TableType::References ? 8 : 0));
+    }
+    _performance_data.bytes_read = rd;
+    _performance_data.bytes_written = res.total_pairs * 2 * sizeof(RowID) + (fused_scan ? probe_rows * sizeof(RowID) : 0);
+  }
   if (with_build) dereference_groups(bo, *out_b, used);
   dereference_groups(po, *out_p, used);
   builders.wait();  // (rethrows a builder's exception)

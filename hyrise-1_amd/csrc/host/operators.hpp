@@ -36,9 +36,17 @@ enum class OperatorType { TableWrapper, TableScan, JoinHash, Aggregate, Projecti
 // types.hpp:197 of the reference: how description() lays out an operator's parameters
 enum class DescriptionMode { SingleLine, MultiLine };
 
+// reference operator_performance_data.hpp:10-15 (walltime), extended at that documented extension point with what
+// ran on the device: the time between the first and the last command the operator issued on its stream (device_ns:
+// 0 when it issued none - a TableScan deferred into the JoinHash that consumes it is timed in that JoinHash), and the
+// algorithmic HBM bytes its kernels read and wrote (SURVEY.md 8(d) per-unit figures: inputs' column bytes, output
+// RowIDs / values), so that bytes / device_ns is the operator's achieved bandwidth.
 struct OperatorPerformanceData {
   uint64_t walltime_ns = 0;  // reference operator_performance_data.hpp:15
   uint64_t rows_in = 0;
+  uint64_t device_ns = 0;
+  uint64_t bytes_read = 0;
+  uint64_t bytes_written = 0;
 };
 
 // The part of the reference's TransactionContext (concurrency/transaction_context.hpp) the hot path reads: the

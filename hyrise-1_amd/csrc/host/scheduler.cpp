@@ -110,13 +110,27 @@ void JobGroup::schedule(std::function<void()> job) {
     }
     finish_one(e);
   };
-  if (_scheduler)
-    _scheduler->schedule(std::move(wrapped));
-  else
+  if (_scheduler) {
+    // The job runs once, on whichever takes it first: a worker of the scheduler, or wait() on the waiting thread
+    // (the worker's queue entry holds only the claim, never `this`).
+    auto claim = std::make_shared<Claimable>();
+    claim->run = std::move(wrapped);
+    _claims.push_back(claim);
+    _scheduler->schedule([claim] {
+      if (!claim->taken.exchange(true)) claim->run();
+    });
+  } else {
     _threads.emplace_back(std::move(wrapped));
+  }
 }
 
 void JobGroup::wait() {
+  // Jobs no worker has started yet run here, on the waiting thread (CurrentScheduler::wait_for_tasks lets the waiting
+  // worker make progress the same way, worker.cpp _wait_for_tasks): operators that wait for their jobs while running on
+  // the scheduler's own workers cannot deadlock when every worker is such a waiter.
+  for (auto& claim : _claims)
+    if (!claim->taken.exchange(true)) claim->run();
+  _claims.clear();
   for (auto& t : _threads)
     if (t.joinable()) t.join();
   _threads.clear();

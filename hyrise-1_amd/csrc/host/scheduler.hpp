@@ -8,6 +8,7 @@
 // on a thread of its own, joined by wait() (the behaviour before the hook existed).
 #pragma once
 
+#include <atomic>
 #include <condition_variable>
 #include <exception>
 #include <functional>
@@ -50,8 +51,13 @@ class JobGroup {
   unsigned concurrency(unsigned dflt) const;
 
  private:
+  struct Claimable {
+    std::atomic<bool> taken{false};
+    std::function<void()> run;
+  };
   void finish_one(std::exception_ptr e);
   std::shared_ptr<JobScheduler> _scheduler;
+  std::vector<std::shared_ptr<Claimable>> _claims;  // jobs handed to _scheduler (wait() runs those not yet taken)
   std::vector<std::thread> _threads;
   std::mutex _m;
   std::condition_variable _cv;

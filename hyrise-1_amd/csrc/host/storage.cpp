@@ -176,9 +176,14 @@ void Table::resolve_slow() const {
   // a consumer that took the producer fulfils the table: other accessors wait for it
   _pending_cv.wait(lock, [&] { return !_taken || !_pending; });
   if (!_pending) return;
-  auto producer = std::move(_pending);
-  _chunks = producer->produce();
+  // the producer stays pending until produce() succeeds: a failing scan (Fail in produce) leaves the table pending,
+  // so the error reaches every accessor instead of an empty table that looks valid
+  const auto producer = _pending;
+  auto chunks = producer->produce();
+  _chunks = std::move(chunks);
+  _pending = nullptr;
   _pending_flag.store(false, std::memory_order_release);
+  _pending_cv.notify_all();
 }
 
 Table::~Table() {

@@ -510,6 +510,8 @@ typedef struct hy_join_filter {
   const void* constant;         /* HOST pointer to the constant of VALUE predicate chunks (type_cast<T>(value)) */
   uint32_t* out_offsets;        /* device, capacity = side rows, or NULL */
   uint64_t* out_chunk_begin;    /* device, n_chunks + 1 entries, or NULL */
+  uint32_t n_chunks;            /* entries of chunks: at least the side's n_chunks (HY_ERR_INVALID_ARGUMENT
+                                   otherwise - a filter built for a table that has grown since) */
 } hy_join_filter;
 
 hy_status hy_scan_join_hash_workspace_size(const hy_join_side* build, const hy_join_filter* build_filter,
