@@ -6,6 +6,8 @@
 
 #include <algorithm>
 #include <cassert>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -39,6 +41,15 @@ inline bool row_readable(const hy_column_chunk& c) {
   return c.size == 0 || c.kind == HY_COL_VALUE || c.kind == HY_COL_DICT;
 }
 
+inline bool stream_capturing(hipStream_t s) {
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cap) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return cap != hipStreamCaptureStatusNone;
+}
+
 // Host -> device copies of the descriptors a call builds on the host (chunk / side / column tables, offsets): staged
 // through a per-thread pinned ring so that hipMemcpyAsync is a real asynchronous DMA (a pageable source makes the
 // runtime stage it synchronously, at a fraction of the bandwidth - measurable with tens of thousands of chunks), and
@@ -60,7 +71,30 @@ struct PinnedRing {
     if (buf) (void)hipHostFree(buf);
   }
   hy_status wait_all() {
-    for (auto& f : fences) HY_HIP(hipEventSynchronize(f.event));
+    for (auto& f : fences) {
+      const hipError_t e = hipEventSynchronize(f.event);
+      if (e == hipSuccess) continue;
+      (void)hipGetLastError();
+      // The runtime refuses the wait when it holds the event for one recorded in a stream capture
+      // (hipErrorCapturedEvent). The ring records its fences on non-capturing streams only, so this is the runtime's
+      // view, not a captured copy; the stream itself covers the ring's copies: wait for it, and re-create the event.
+      if (std::getenv("HY_DEBUG_RING"))
+        std::fprintf(stderr, "hyrise-amd ring: fence on stream %p device %d: %s (stream capturing now: %d)\n",
+                     static_cast<void*>(f.stream), f.device, hipGetErrorString(e), int(stream_capturing(f.stream)));
+      if (stream_capturing(f.stream))
+        return fail(HY_ERR_DEVICE, std::string("pinned staging ring: fence wait on a capturing stream: ") +
+                                       hipGetErrorString(e));
+      int cur = 0;
+      HY_HIP(hipGetDevice(&cur));
+      HY_HIP(hipSetDevice(f.device));
+      const hipError_t w = hipStreamSynchronize(f.stream);
+      (void)hipEventDestroy(f.event);
+      f.event = nullptr;
+      const hipError_t c = hipEventCreateWithFlags(&f.event, hipEventDisableTiming);
+      HY_HIP(hipSetDevice(cur));
+      HY_HIP(w);
+      HY_HIP(c);
+    }
     return HY_OK;
   }
   hy_status fence(hipStream_t s) {
@@ -69,6 +103,8 @@ struct PinnedRing {
     for (auto& f : fences)
       if (f.stream == s && f.device == dev) {
         HY_HIP(hipEventRecord(f.event, s));
+        if (std::getenv("HY_DEBUG_RING") && stream_capturing(s))
+          std::fprintf(stderr, "hyrise-amd ring: fence recorded on capturing stream %p\n", static_cast<void*>(s));
         return HY_OK;
       }
     if (fences.size() >= 32) {  // many short-lived streams: retire the fences (their copies are waited for first)
@@ -87,15 +123,6 @@ struct PinnedRing {
 // A stream being captured into a graph is refused: the copy would become a graph node reading a ring slot that later
 // staging reuses (or frees), so every replay would upload whatever the slot then holds. Captured regions (a prepared
 // plan's execution, hyrise_amd_join.hip) stage nothing; their descriptors are in the plan's workspace beforehand.
-inline bool stream_capturing(hipStream_t s) {
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(s, &cap) != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
-  }
-  return cap != hipStreamCaptureStatusNone;
-}
-
 inline hy_status staged_htod(void* dst, const void* src, size_t bytes, hipStream_t s) {
   if (bytes == 0) return HY_OK;
   if (stream_capturing(s)) {
@@ -157,6 +184,12 @@ struct KStat {
   uint64_t units = 0;
 };
 extern std::mutex g_kt_mutex;
+// Held while a stream is being captured into a hipGraph (hy_scan_join_plan_execute) and while hy_free_async_after
+// orders a free after other streams: that function records events on every operator stream - from any thread, e.g.
+// the background chunk reaper - and an event recorded on a stream under capture becomes a node of that capture, and
+// a stream that waits on it joins the capture (its own later work is then captured instead of executed, and the
+// capture ends unjoined). Recursive: a thread never blocks itself.
+extern std::recursive_mutex g_capture_m;
 extern uint64_t* g_join_trace;  // hy_debug_set_join_trace
 extern thread_local const uint32_t* g_key_hash;  // hy_join_params.key_hash of the join running on this thread
 extern bool g_kt_enabled;

@@ -23,6 +23,7 @@
 namespace hyc {
 thread_local std::string g_last_error;
 std::mutex g_kt_mutex;
+std::recursive_mutex g_capture_m;
 uint64_t* g_join_trace = nullptr;
 thread_local const uint32_t* g_key_hash = nullptr;
 bool g_kt_enabled = false;
@@ -94,6 +95,8 @@ hy_status hy_free_async(void* ptr, hy_stream_t stream) {
 hy_status hy_free_async_after(void* ptr, hy_stream_t free_stream, const hy_stream_t* wait_streams, uint32_t n_wait) {
   if (!ptr) return HY_OK;
   if (n_wait && !wait_streams) return fail(HY_ERR_INVALID_ARGUMENT, "wait_streams is NULL");
+  // (not while another thread captures one of these streams: see g_capture_m)
+  std::lock_guard<std::recursive_mutex> capture_lock(g_capture_m);
   for (uint32_t i = 0; i < n_wait; ++i) {
     if (wait_streams[i] == free_stream) continue;
     hipEvent_t ev;

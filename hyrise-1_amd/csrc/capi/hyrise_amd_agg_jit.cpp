@@ -12,12 +12,16 @@
 // (single_column_table_scan_impl.cpp:145-205). Results are bit-identical to agg_dense_stream's (same exact sums).
 #include "agg_jit.hpp"
 
+#include <dlfcn.h>
 #include <hip/hiprtc.h>
+#include <unistd.h>
 
 #include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
+#include <iterator>
 #include <memory>
 #include <mutex>
 #include <sstream>
@@ -372,6 +376,57 @@ std::vector<char> rtc(const std::string& src, const std::string& arch, std::stri
   return code;
 }
 
+// Code objects persist on disk, keyed by a hash of the target and the generated source: a plan shape pays hiprtc's
+// ~1.7 s once per machine and library build instead of once per process. The directory is jit_cache/ next to this
+// library (HY_JIT_CACHE_DIR overrides it, HY_JIT_CACHE=0 turns the cache off); entries are written to a temporary file
+// and renamed, so concurrent processes never read a partial one, and an entry that fails to load is recompiled.
+uint64_t fnv1a(const std::string& s, uint64_t h = 1469598103934665603ull) {
+  for (unsigned char c : s) h = (h ^ c) * 1099511628211ull;
+  return h;
+}
+
+std::string cache_dir() {
+  if (const char* e = std::getenv("HY_JIT_CACHE")) {
+    if (std::strtol(e, nullptr, 10) == 0) return {};
+  }
+  if (const char* d = std::getenv("HY_JIT_CACHE_DIR")) return d;
+  Dl_info info{};
+  if (dladdr(reinterpret_cast<void*>(&fnv1a), &info) == 0 || !info.dli_fname) return {};
+  std::string lib = info.dli_fname;
+  const size_t slash = lib.rfind('/');
+  return (slash == std::string::npos ? std::string(".") : lib.substr(0, slash)) + "/jit_cache";
+}
+
+std::string cache_path(const std::string& src, const std::string& arch) {
+  const std::string dir = cache_dir();
+  if (dir.empty()) return {};
+  char name[64];
+  std::snprintf(name, sizeof(name), "/agg_jit_%016llx.co",
+                static_cast<unsigned long long>(fnv1a(src, fnv1a(arch + "\n" + std::string(kJitPrelude)))));
+  return dir + name;
+}
+
+std::vector<char> cache_load(const std::string& path) {
+  if (path.empty()) return {};
+  std::ifstream f(path, std::ios::binary);
+  if (!f) return {};
+  return std::vector<char>(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
+}
+
+void cache_store(const std::string& path, const std::vector<char>& code) {
+  if (path.empty() || code.empty()) return;
+  const std::string dir = path.substr(0, path.rfind('/'));
+  (void)std::system(("mkdir -p '" + dir + "' 2>/dev/null").c_str());
+  const std::string tmp = path + ".tmp" + std::to_string(static_cast<long>(getpid()));
+  {
+    std::ofstream f(tmp, std::ios::binary);
+    if (!f) return;
+    f.write(code.data(), static_cast<std::streamsize>(code.size()));
+    if (!f) return;
+  }
+  if (std::rename(tmp.c_str(), path.c_str()) != 0) std::remove(tmp.c_str());
+}
+
 struct Compiled {
   hipModule_t module = nullptr;
   hipFunction_t fn = nullptr;
@@ -392,14 +447,27 @@ std::shared_ptr<Compiled> compile(const std::string& src) {
   std::string arch = "gfx950";
   if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.gcnArchName[0])
     arch = prop.gcnArchName;
-  const std::vector<char> code = rtc(src, arch, &out->error);
-  if (code.empty()) return out;
-  if (hipModuleLoadData(&out->module, code.data()) != hipSuccess ||
-      hipModuleGetFunction(&out->fn, out->module, "agg_jit") != hipSuccess) {
-    out->error = "hipModuleLoadData / hipModuleGetFunction failed";
+  const std::string path = cache_path(src, arch);
+  std::vector<char> code = cache_load(path);
+  bool cached = !code.empty();
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    if (code.empty()) {
+      code = rtc(src, arch, &out->error);
+      if (code.empty()) return out;
+      cached = false;
+    }
+    if (hipModuleLoadData(&out->module, code.data()) == hipSuccess &&
+        hipModuleGetFunction(&out->fn, out->module, "agg_jit") == hipSuccess)
+      break;
+    (void)hipGetLastError();
     out->fn = nullptr;
-    return out;
+    out->error = "hipModuleLoadData / hipModuleGetFunction failed";
+    if (!cached) return out;
+    code.clear();  // a stale or damaged cache entry: compile it again
   }
+  if (!out->fn) return out;
+  out->error.clear();
+  if (!cached) cache_store(path, code);
   int per_cu = 0, cus = 0;
   if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, out->fn, 256, 0) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)

@@ -1,5 +1,6 @@
 // C entry points of JoinHash (include/hyrise_amd.h): argument checks and the dispatch on the hashed type to the
 // per-type translation units (hyrise_amd_join_*.hip, join_host.hpp).
+#include <cstdio>
 #include "join_host.hpp"
 
 #include <memory>
@@ -245,6 +246,7 @@ hy_status hy_scan_join_plan_execute(hy_join_plan_t plan, hy_row_id* out_build, h
     plan->exec = nullptr;
     plan->graph = nullptr;
     hy_status st = HY_OK;
+    std::unique_lock<std::recursive_mutex> capture_lock(g_capture_m);  // (no free orders itself after s meanwhile)
     if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) == hipSuccess) {
       capture_state() = CaptureState{true, nullptr, nullptr};
       st = run_plan(plan, out_build, out_probe, out_capacity, partition_begin, partition_counts, result, s);
@@ -252,6 +254,14 @@ hy_status hy_scan_join_plan_execute(hy_join_plan_t plan, hy_row_id* out_build, h
       capture_state() = CaptureState{};
       hipGraph_t g = nullptr;
       const hipError_t e = hipStreamEndCapture(s, &g);
+      capture_lock.unlock();
+      if (std::getenv("HY_DEBUG_RING")) {
+        hipStreamCaptureStatus after = hipStreamCaptureStatusNone;
+        const hipError_t qe = hipStreamIsCapturing(s, &after);
+        std::fprintf(stderr, "hyrise-amd capture: stream %p run_plan %d (%s) end %s graph %p misc %p; after: %s %d\n",
+                     static_cast<void*>(s), int(st), st == HY_OK ? "" : g_last_error.c_str(), hipGetErrorString(e),
+                     static_cast<void*>(g), static_cast<const void*>(cs.misc), hipGetErrorString(qe), int(after));
+      }
       if (st == HY_OK && e == hipSuccess && g && cs.misc &&
           hipGraphInstantiate(&plan->exec, g, nullptr, nullptr, 0) == hipSuccess) {
         plan->graph = g;

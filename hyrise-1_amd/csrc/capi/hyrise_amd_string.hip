@@ -112,8 +112,41 @@ __device__ inline bool like_match(const LikeNfa& a, const unsigned char* p, uint
   return hit != 0;
 }
 
+// The predicate on one string value (NULL or not): compare with the constant, LIKE, IS [NOT] NULL.
+__device__ inline bool string_value_match(int op, bool is_null, const hyk::DevString& v, const StrPred& p) {
+  if (op == HY_OP_IS_NULL) return is_null;
+  if (is_null) return false;
+  if (op == HY_OP_ALL || op == HY_OP_IS_NOT_NULL) return true;
+  if (op == HY_OP_LIKE || op == HY_OP_NOT_LIKE) return like_match(*p.nfa, v.p, v.n) == (op == HY_OP_LIKE);
+  return hyk::cmp_result(op, hyk::string_compare(v, hyk::DevString{reinterpret_cast<const unsigned char*>(p.value),
+                                                                   p.value_len}));
+}
+
+// The run of row `off` of a RunLength chunk (run_length_column.cpp:24-36: the first run whose end position is >= off;
+// end positions in column.dictionary, dictionary_size runs).
+__device__ inline uint32_t rle_run_of(const hy_column_chunk& col, uint32_t off) {
+  const uint32_t* ends = static_cast<const uint32_t*>(col.dictionary);
+  uint32_t lo = 0, hi = col.dictionary_size - 1u;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (ends[mid] < off)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+// Run r of a RunLength string chunk: its packed value and NULL flag.
+__device__ inline bool rle_run_match(const hy_scan_chunk& ch, uint32_t r, const StrPred& p) {
+  const hy_column_chunk& col = ch.column;
+  return string_value_match(ch.op, col.nulls != nullptr && col.nulls[r], hyk::packed_string(col.data, col.dictionary_size, r),
+                            p);
+}
+
 // Row `off` of a scan chunk: the reference's predicate for a dictionary chunk (value id vs search_vid / id set, as
-// hy_table_scan) or for a string value chunk (compare with the constant, LIKE, IS [NOT] NULL).
+// hy_table_scan), for a string value chunk (compare with the constant, LIKE, IS [NOT] NULL) or for a RunLength chunk
+// (the predicate of the row's run).
 __device__ inline bool string_row_match(const hy_scan_chunk& ch, uint32_t off, const StrPred& p) {
   const int op = ch.op;
   if (op == HY_OP_NONE) return false;
@@ -129,14 +162,8 @@ __device__ inline bool string_row_match(const hy_scan_chunk& ch, uint32_t off, c
     if (op == HY_OP_VID_SET) return (ch.vid_set[vid >> 5] >> (vid & 31)) & 1u;
     return hyk::cmp_op<uint32_t>(op, vid, ch.search_vid);
   }
-  const bool is_null = col.nulls != nullptr && col.nulls[off];
-  if (op == HY_OP_IS_NULL) return is_null;
-  if (is_null) return false;
-  if (op == HY_OP_ALL || op == HY_OP_IS_NOT_NULL) return true;
-  const hyk::DevString v = hyk::packed_string(col.data, col.size, off);
-  if (op == HY_OP_LIKE || op == HY_OP_NOT_LIKE) return like_match(*p.nfa, v.p, v.n) == (op == HY_OP_LIKE);
-  return hyk::cmp_result(op, hyk::string_compare(v, hyk::DevString{reinterpret_cast<const unsigned char*>(p.value),
-                                                                   p.value_len}));
+  if (col.kind == HY_COL_RLE) return rle_run_match(ch, rle_run_of(col, off), p);
+  return string_value_match(op, col.nulls != nullptr && col.nulls[off], hyk::packed_string(col.data, col.size, off), p);
 }
 
 struct TableDesc {
@@ -146,7 +173,25 @@ struct TableDesc {
   const uint64_t* chunk_tile_begin;
   const uint64_t* chunk_row_begin;
   uint64_t n_tiles;
+  const uint64_t* run_base;  // RunLength chunks: index of the chunk's first run in run_flags
+  const uint8_t* run_flags;  // the predicate per run (string_rle_runs)
 };
+
+// RunLength chunks of a table scan: the predicate once per run (the reference's RunLength iterable yields a run's value
+// for each of its positions; the value and the predicate are the same for all of them). One thread per run, 256-run
+// tiles inside one chunk.
+__global__ __launch_bounds__(STR_THREADS) void string_rle_runs(const hy_scan_chunk* __restrict__ chunks,
+                                                              const uint32_t* __restrict__ tile_chunk,
+                                                              const uint64_t* __restrict__ chunk_tile_begin,
+                                                              const uint64_t* __restrict__ run_base, uint64_t n_tiles,
+                                                              StrPred p, uint8_t* __restrict__ run_flags) {
+  const uint64_t tile = blockIdx.x;
+  if (tile >= n_tiles) return;
+  const uint32_t c = tile_chunk[tile];
+  const hy_scan_chunk& ch = chunks[c];
+  const uint32_t r = static_cast<uint32_t>(tile - chunk_tile_begin[c]) * STR_THREADS + threadIdx.x;
+  if (r < ch.column.dictionary_size) run_flags[run_base[c] + r] = ch.op != HY_OP_NONE && rle_run_match(ch, r, p);
+}
 
 __global__ __launch_bounds__(STR_THREADS) void string_table_flags(TableDesc d, StrPred p, hy_row_id* __restrict__ items,
                                                                  uint8_t* __restrict__ flags,
@@ -160,7 +205,9 @@ __global__ __launch_bounds__(STR_THREADS) void string_table_flags(TableDesc d, S
   if (threadIdx.x == 0) s_count = 0;
   __syncthreads();
   if (off < ch.column.size) {
-    const bool m = string_row_match(ch, off, p);
+    const bool m = ch.column.kind == HY_COL_RLE
+                       ? ch.op != HY_OP_NONE && d.run_flags[d.run_base[c] + rle_run_of(ch.column, off)] != 0
+                       : string_row_match(ch, off, p);
     const uint64_t g = d.chunk_row_begin[c] + off;
     flags[g] = m;
     items[g] = hy_row_id{d.chunk_ids[c], off};
@@ -340,12 +387,14 @@ hy_status check_ops(const hy_scan_chunk* chunks, uint32_t n, bool* need_like) {
     if (ch.column.kind == HY_COL_DICT) {
       if (ch.op < HY_OP_EQ || ch.op > HY_OP_VID_SET || (ch.op == HY_OP_VID_SET && !ch.vid_set))
         return fail(HY_ERR_INVALID_ARGUMENT, "dictionary chunk op");
-    } else if (ch.column.kind == HY_COL_STRING) {
+    } else if (ch.column.kind == HY_COL_STRING || ch.column.kind == HY_COL_RLE) {
       if (ch.op == HY_OP_VID_SET || ch.op < HY_OP_EQ || ch.op > HY_OP_NOT_LIKE)
         return fail(HY_ERR_INVALID_ARGUMENT, "string chunk op");
+      if (ch.column.kind == HY_COL_RLE && ch.column.size && (ch.column.dictionary_size == 0 || !ch.column.dictionary))
+        return fail(HY_ERR_INVALID_ARGUMENT, "RunLength chunk without runs");
       if (ch.op == HY_OP_LIKE || ch.op == HY_OP_NOT_LIKE) *need_like = true;
     } else if (ch.column.size) {
-      return fail(HY_ERR_INVALID_ARGUMENT, "string scans take STRING or DICT chunks");
+      return fail(HY_ERR_INVALID_ARGUMENT, "string scans take STRING, RLE or DICT chunks");
     }
   }
   return HY_OK;
@@ -365,6 +414,9 @@ struct TableWs {
   uint32_t* ids;
   uint32_t* tile_chunk;
   uint64_t *tile_begin, *row_begin;
+  uint32_t* run_tile_chunk;
+  uint64_t *run_tile_begin, *run_base;
+  uint8_t* run_flags;
   hy_row_id* items;
   uint8_t* flags;
   char* temp;
@@ -372,12 +424,17 @@ struct TableWs {
   Staged st;
 };
 
-void carve_table(Carver& cv, uint64_t rows, uint64_t tiles, uint32_t n, const hy_string_predicate* pred, TableWs* w) {
+void carve_table(Carver& cv, uint64_t rows, uint64_t tiles, uint64_t runs, uint64_t run_tiles, uint32_t n,
+                 const hy_string_predicate* pred, TableWs* w) {
   w->chunks = cv.take<hy_scan_chunk>(std::max<uint32_t>(1, n));
   w->ids = cv.take<uint32_t>(std::max<uint32_t>(1, n));
   w->tile_chunk = cv.take<uint32_t>(tiles + 1);
   w->tile_begin = cv.take<uint64_t>(n + 1);
   w->row_begin = cv.take<uint64_t>(n + 1);
+  w->run_tile_chunk = cv.take<uint32_t>(run_tiles + 1);
+  w->run_tile_begin = cv.take<uint64_t>(n + 1);
+  w->run_base = cv.take<uint64_t>(n + 1);
+  w->run_flags = cv.take<uint8_t>(runs + 16);
   w->items = cv.take<hy_row_id>(rows + 1);
   w->flags = cv.take<uint8_t>(rows + 16);
   w->temp_bytes = select_temp<hy_row_id>(rows);
@@ -385,12 +442,16 @@ void carve_table(Carver& cv, uint64_t rows, uint64_t tiles, uint32_t n, const hy
   carve_pred(cv, pred, &w->st);
 }
 
-void table_geometry(const hy_scan_chunk* chunks, uint32_t n, uint64_t* rows, uint64_t* tiles) {
-  *rows = 0;
-  *tiles = 0;
+void table_geometry(const hy_scan_chunk* chunks, uint32_t n, uint64_t* rows, uint64_t* tiles, uint64_t* runs,
+                    uint64_t* run_tiles) {
+  *rows = *tiles = *runs = *run_tiles = 0;
   for (uint32_t c = 0; c < n; ++c) {
     *rows += chunks[c].column.size;
     *tiles += (chunks[c].column.size + STR_THREADS - 1) / STR_THREADS;
+    if (chunks[c].column.kind == HY_COL_RLE && chunks[c].column.size) {
+      *runs += chunks[c].column.dictionary_size;
+      *run_tiles += (chunks[c].column.dictionary_size + STR_THREADS - 1) / STR_THREADS;
+    }
   }
 }
 
@@ -401,11 +462,11 @@ extern "C" {
 hy_status hy_string_table_scan_workspace_size(const hy_scan_chunk* chunks, uint32_t n_chunks,
                                               const hy_string_predicate* pred, size_t* bytes) {
   if (!bytes || (n_chunks && !chunks)) return fail(HY_ERR_INVALID_ARGUMENT, "null argument");
-  uint64_t rows, tiles;
-  table_geometry(chunks, n_chunks, &rows, &tiles);
+  uint64_t rows, tiles, runs, run_tiles;
+  table_geometry(chunks, n_chunks, &rows, &tiles, &runs, &run_tiles);
   Carver cv{nullptr, 0};
   TableWs w;
-  carve_table(cv, rows, tiles, n_chunks, pred, &w);
+  carve_table(cv, rows, tiles, runs, run_tiles, n_chunks, pred, &w);
   *bytes = cv.used + 256;
   return HY_OK;
 }
@@ -417,8 +478,8 @@ hy_status hy_string_table_scan(const hy_scan_chunk* chunks, uint32_t n_chunks, c
   bool need_like = false;
   hy_status st = check_ops(chunks, n_chunks, &need_like);
   if (st != HY_OK) return st;
-  uint64_t rows, tiles;
-  table_geometry(chunks, n_chunks, &rows, &tiles);
+  uint64_t rows, tiles, runs, run_tiles;
+  table_geometry(chunks, n_chunks, &rows, &tiles, &runs, &run_tiles);
   if (rows >= 0x7FFFFFFFull) return fail(HY_ERR_UNSUPPORTED, "more than 2^31-1 rows");
   hipStream_t s = S(stream);
   HY_HIP(hipMemsetAsync(n_out, 0, 8, s));
@@ -427,7 +488,7 @@ hy_status hy_string_table_scan(const hy_scan_chunk* chunks, uint32_t n_chunks, c
   if (!out_rows) return fail(HY_ERR_INVALID_ARGUMENT, "out_rows");
   Carver cv{static_cast<char*>(workspace), workspace_bytes};
   TableWs w;
-  carve_table(cv, rows, tiles, n_chunks, pred, &w);
+  carve_table(cv, rows, tiles, runs, run_tiles, n_chunks, pred, &w);
   if (!cv.ok) return fail(HY_ERR_WORKSPACE, "string scan workspace too small");
   StrPred p{};
   st = stage_pred(pred, w.st, s, &p, need_like);
@@ -445,12 +506,37 @@ hy_status hy_string_table_scan(const hy_scan_chunk* chunks, uint32_t n_chunks, c
   }
   tb[n_chunks] = t;
   rb[n_chunks] = r;
+  // RunLength chunks: their runs' tiles and each chunk's first run in run_flags
+  std::vector<uint32_t> rtc(run_tiles);
+  std::vector<uint64_t> rtb(n_chunks + 1), rbase(n_chunks + 1);
+  uint64_t rt = 0, rr = 0;
+  for (uint32_t c = 0; c < n_chunks; ++c) {
+    rtb[c] = rt;
+    rbase[c] = rr;
+    if (chunks[c].column.kind != HY_COL_RLE || chunks[c].column.size == 0) continue;
+    const uint64_t k = (chunks[c].column.dictionary_size + STR_THREADS - 1) / STR_THREADS;
+    for (uint64_t i = 0; i < k; ++i) rtc[rt + i] = c;
+    rt += k;
+    rr += chunks[c].column.dictionary_size;
+  }
+  rtb[n_chunks] = rt;
+  rbase[n_chunks] = rr;
   HY_STAGE(w.chunks, chunks, sizeof(hy_scan_chunk) * n_chunks, s);
   HY_STAGE(w.ids, chunk_ids, 4ull * n_chunks, s);
   HY_STAGE(w.tile_chunk, tc.data(), 4 * tiles, s);
   HY_STAGE(w.tile_begin, tb.data(), 8ull * (n_chunks + 1), s);
   HY_STAGE(w.row_begin, rb.data(), 8ull * (n_chunks + 1), s);
-  const TableDesc d{w.chunks, w.ids, w.tile_chunk, w.tile_begin, w.row_begin, tiles};
+  if (run_tiles) {
+    HY_STAGE(w.run_tile_chunk, rtc.data(), 4 * run_tiles, s);
+    HY_STAGE(w.run_tile_begin, rtb.data(), 8ull * (n_chunks + 1), s);
+    HY_STAGE(w.run_base, rbase.data(), 8ull * (n_chunks + 1), s);
+    KTimer kt_("string_rle_runs", s, runs);
+    hipLaunchKernelGGL(string_rle_runs, dim3(static_cast<uint32_t>(run_tiles)), dim3(STR_THREADS), 0, s, w.chunks,
+                       w.run_tile_chunk, w.run_tile_begin, w.run_base, run_tiles, p, w.run_flags);
+    kt_.done();
+    HY_HIP(hipGetLastError());
+  }
+  const TableDesc d{w.chunks, w.ids, w.tile_chunk, w.tile_begin, w.row_begin, tiles, w.run_base, w.run_flags};
   {
     KTimer kt_("string_table_flags", s, rows);
     hipLaunchKernelGGL(string_table_flags, dim3(static_cast<uint32_t>(tiles)), dim3(STR_THREADS), 0, s, d, p, w.items,

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -56,7 +57,8 @@ struct JoinKnobs {
   uint64_t onepass_cap_div = 8;        // HY_ONEPASS_CAP_DIV
   uint64_t onepass_cap = 0;            // HY_ONEPASS_CAP (0: computed)
   bool filter_buckets = true;          // HY_FILTER_BUCKETS: prefilter words set per LDS region (0: global atomics)
-  bool direct = true;                  // HY_JOIN_DIRECT: direct partitioning of a filtered side (join_direct.hip)
+  bool rank_ballot = false;            // HY_RANK_BALLOT: rank by ballots (the fallback of a failed rank_order_check)
+  bool direct = false;                 // HY_JOIN_DIRECT: direct partitioning of a filtered side (join_direct.hip)
   uint32_t direct_span = 16;           // HY_DIRECT_SPAN: tiles per span of the direct first pass
   uint32_t direct_groups = 0;          // HY_DIRECT_GROUPS: span groups per bucket of the direct second pass (0: auto)
 };
@@ -79,7 +81,8 @@ inline JoinKnobs knobs_from_env() {
   k.onepass_cap_div = static_cast<uint64_t>(std::max<long long>(1, num("HY_ONEPASS_CAP_DIV", 8)));
   k.onepass_cap = static_cast<uint64_t>(std::max<long long>(0, num("HY_ONEPASS_CAP", 0)));
   k.filter_buckets = num("HY_FILTER_BUCKETS", 1) != 0;
-  k.direct = num("HY_JOIN_DIRECT", 1) != 0;
+  k.rank_ballot = num("HY_RANK_BALLOT", 0) != 0;
+  k.direct = num("HY_JOIN_DIRECT", 0) != 0;
   k.direct_span = static_cast<uint32_t>(std::min<long long>(std::max<long long>(1, num("HY_DIRECT_SPAN", 16)), 64));
   k.direct_groups = static_cast<uint32_t>(std::min<long long>(std::max<long long>(0, num("HY_DIRECT_GROUPS", 0)), 4096));
   return k;
@@ -259,7 +262,12 @@ inline void plan_spans(SidePlan& p, uint32_t sub) {
 
 // The LDS ordering that the partition passes' ranking relies on (hyk::wave_rank_add), checked once per device before
 // its first join (hyk::rank_order_check against the mask ranking). Skipped while the device cannot run it (a stream
-// capture in progress elsewhere); a device that breaks it fails every join loudly.
+// capture in progress elsewhere); on a device that breaks it the passes rank by ballots (rank_ballot), slower but
+// independent of the LDS atomics' lane order.
+inline std::atomic<bool>* rank_broken() {
+  static std::atomic<bool> broken[64] = {};
+  return broken;
+}
 inline hy_status check_rank_order() {
   static std::mutex m;
   static int state[64] = {};  // 0: not checked yet, 1: holds, 2: broken
@@ -285,9 +293,17 @@ inline hy_status check_rank_order() {
     (void)hipGetLastError();
     if (ran) state[dev] = bad == 0 ? 1 : 2;
   }
-  if (state[dev] == 2)
-    return fail(HY_ERR_KERNEL, "this device's LDS atomics do not rank in lane order (hyk::wave_rank_add)");
+  if (state[dev] == 2) rank_broken()[dev] = true;  // the partition passes rank by ballots on this device instead
   return HY_OK;
+}
+
+// 1 when the partition passes rank by ballots (hyk::rank_item): the device failed rank_order_check, or
+// HY_RANK_BALLOT=1 (tests force the fallback with it).
+inline uint32_t rank_ballot() {
+  int dev = 0;
+  if (knobs().rank_ballot) return 1u;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0u;
+  return rank_broken()[dev] ? 1u : 0u;
 }
 
 inline hy_status plan_side(const hy_join_side* side, SidePlan& p) {
@@ -792,7 +808,7 @@ hy_status pass0_side(const SidePlan& p, SideBufs<H, P>& b, uint32_t bits, uint32
                      bool bloom_by_hash, const hyk::FilterHdr* bloom_hdr, uint64_t range_words) {
   const hyk::Side sd = make_side(p, b, seed, keep_nulls, ref_base, bloom, bloom_n, bloom_by_hash, bloom_hdr, range_words);
   const uint32_t n_digits = 1u << w0;
-  hyk::Digit d0{full_mask(bits), bits - w0, n_digits - 1u, seed, g_key_hash};
+  hyk::Digit d0{full_mask(bits), bits - w0, n_digits - 1u, seed, g_key_hash, rank_ballot()};
   HY_HIP(hipMemsetAsync(b.total, 0, 8, s));
   if (p.filtered && p.scan_chunk_begin) HY_HIP(hipMemsetAsync(p.scan_chunk_begin, 0, 8 * (p.chunks.size() + 1), s));
   if (p.n_tiles1 > 0) {
@@ -827,7 +843,7 @@ hy_status record_pass(const SideBufs<H, P>& b, const hyk::Segs& sg, const hyk::G
                       const hyk::RecOut<H, P>& out, const uint64_t* total, uint32_t* bounds, const Common& c,
                       hipStream_t s, uint64_t rows) {
   const uint32_t n_digits = 1u << w;
-  hyk::Digit dg{full_mask(bits), shift, n_digits - 1u, seed, g_key_hash};
+  hyk::Digit dg{full_mask(bits), shift, n_digits - 1u, seed, g_key_hash, rank_ballot()};
   if (grid) {
     {
       KTimer kt_((std::string("part2_hist.") + SD::name).c_str(), s, rows);
@@ -1054,7 +1070,7 @@ hy_status blocked_side(const SidePlan& p, SideBufs<H, uint32_t>& b, uint32_t bit
                        uint32_t** bounds, const hyk::RecOut<H, uint32_t>* last_out) {
   const uint32_t nd0 = 1u << w[0], w1 = w[1];
   const BlockPlan bl = block_plan(p, n_blocks);
-  const hyk::Digit d0{full_mask(bits), bits - w[0], nd0 - 1u, sd.seed, g_key_hash};
+  const hyk::Digit d0{full_mask(bits), bits - w[0], nd0 - 1u, sd.seed, g_key_hash, rank_ballot()};
   const hyk::NextDigit nd = next_digit(w, 0, bits, b.digA);
   HY_HIP(hipMemsetAsync(b.total, 0, 8, s));
   if (p.filtered && p.scan_chunk_begin) HY_HIP(hipMemsetAsync(p.scan_chunk_begin, 0, 8 * (p.chunks.size() + 1), s));
@@ -1463,7 +1479,7 @@ hy_status onepass_side(const char* tag, const SidePlan& p, OneBufs<H>& o, uint32
   hipLaunchKernelGGL(hyk::fill_tile_owner, dim3((sd.n_chunks + 255) / 256), dim3(256), 0, s, b.tile_begin, sd.n_chunks,
                      b.tile_owner);
   HY_HIP(hipGetLastError());
-  const hyk::Digit d0{full_mask(bits), bits - w[0], nd0 - 1u, seed, g_key_hash};
+  const hyk::Digit d0{full_mask(bits), bits - w[0], nd0 - 1u, seed, g_key_hash, rank_ballot()};
   const hyk::NextDigit nd = next_digit(w, 0, bits, b.digA);
   static const uint32_t win = [] {
     const char* e = std::getenv("HY_ONEPASS_WIN");
@@ -1752,7 +1768,7 @@ hy_status direct_side(const DirectPlan& d, DirectBufs<H>& o, uint32_t bits, uint
     HY_HIP(hipGetLastError());
   }
   const hyk::DirectGeo g{o.span_rbase, o.span_cap, o.span_scan, o.counts, o.overflow, n_spans};
-  const hyk::Digit d0{full_mask(bits), bits - (31 - __builtin_clz(d.nd0)), d.nd0 - 1u, seed, g_key_hash};
+  const hyk::Digit d0{full_mask(bits), bits - (31 - __builtin_clz(d.nd0)), d.nd0 - 1u, seed, g_key_hash, rank_ballot()};
   // (HY_DIRECT_NOBYTES: an experiment that skips the digit bytes - the second pass's histogram is then wrong)
   static const bool no_bytes = std::getenv("HY_DIRECT_NOBYTES") != nullptr;
   const hyk::NextDigit nd{no_bytes ? nullptr : o.dig, 0u, d.nd1 - 1u};
@@ -1773,7 +1789,7 @@ hy_status direct_side(const DirectPlan& d, DirectBufs<H>& o, uint32_t bits, uint
   HY_HIP(hipGetLastError());
   st = run_scan(o.hist, o.off, uint64_t(d.nd0) * d.nd1 * d.groups, c, s, o.totals + 2);
   if (st != HY_OK) return st;
-  const hyk::Digit d1{full_mask(bits), 0u, d.nd1 - 1u, seed, g_key_hash};
+  const hyk::Digit d1{full_mask(bits), 0u, d.nd1 - 1u, seed, g_key_hash, rank_ballot()};
   {
     KTimer kt_((std::string("part2g_scatter.") + SD::name).c_str(), s, p.n_rows);
     hipLaunchKernelGGL((hyk::part2g_scatter<SD, H, uint32_t>), g2, dim3(hyk::PART_THREADS), 0, s, gg, d1, d.nd1,
@@ -1935,9 +1951,28 @@ hy_status join_typed_passes(const SidePlan& bp_in, const SidePlan& pp_in, const 
   }
   SideStream* ss = (!use_bloom && !timing && overlap_enabled()) ? side_stream() : nullptr;
   const hipStream_t sb = ss ? ss->s : s;
+  // Every return after the fork joins the side stream back into s: an error return that left it forked let the build
+  // side's kernels run on past the call, unordered with the caller's stream - which then reuses the workspace (the
+  // operators' per-thread block cache relies on stream order), and a capture ended unjoined.
+  struct JoinBack {
+    SideStream* ss;
+    hipStream_t sb, s;
+    bool armed = false;
+    hipError_t join() {
+      if (!armed) return hipSuccess;
+      armed = false;
+      hipError_t e = hipEventRecord(ss->join, sb);
+      if (e == hipSuccess) e = hipStreamWaitEvent(s, ss->join, 0);
+      return e;
+    }
+    ~JoinBack() {
+      if (armed && join() != hipSuccess) (void)hipGetLastError();
+    }
+  } join_back{ss, sb, s};
   if (ss) {
     HY_HIP(hipEventRecord(ss->fork, s));
     HY_HIP(hipStreamWaitEvent(sb, ss->fork, 0));
+    join_back.armed = true;
   }
 
   // int32 keys (no string ids) with b >= 16 radix bits: the last record pass keeps 16 hash bits instead of the key
@@ -2034,10 +2069,7 @@ hy_status join_typed_passes(const SidePlan& bp_in, const SidePlan& pp_in, const 
       HY_HIP(hipGetLastError());
     }
   }
-  if (ss) {  // the partition join waits for the build side
-    HY_HIP(hipEventRecord(ss->join, sb));
-    HY_HIP(hipStreamWaitEvent(s, ss->join, 0));
-  }
+  HY_HIP(join_back.join());  // the partition join waits for the build side
   // filtered sides emit RowIDs of their data table (the scan's PosLists dereferenced, write_output_columns)
   const hyk::RowMap bmap = bp.fuse ? make_map(bb.ref_row_begin, bp.ref_row_begin) : make_map(bb.row_begin, bp.row_begin);
   const hyk::RowMap pmap = pp.fuse ? make_map(pb.ref_row_begin, pp.ref_row_begin) : make_map(pb.row_begin, pp.row_begin);

@@ -175,7 +175,13 @@ void operator_stream_synchronize_if_used() {
 void device_buffer_free(void* ptr) {
   auto& r = stream_registry();
   std::lock_guard<std::mutex> lock(r.m);
-  hy_stream_t s = t_stream.stream ? t_stream.stream : (r.streams.empty() ? nullptr : r.streams.front());
+  // a thread without an operator stream (the chunk reaper, an embedding's own threads) frees on a stream of its own
+  // kind, not on another thread's operator stream (which would then wait for every other stream's work)
+  static hy_stream_t release_stream = [] {
+    hy_stream_t x = nullptr;
+    return hy_stream_create(&x) == HY_OK ? x : nullptr;
+  }();
+  hy_stream_t s = t_stream.stream ? t_stream.stream : release_stream;
   // (a destructor: a failure cannot be reported; the pool keeps the block then)
   static_cast<void>(hy_free_async_after(ptr, s, r.streams.data(), static_cast<uint32_t>(r.streams.size())));
 }
@@ -286,11 +292,25 @@ std::shared_ptr<DeviceColumn> resident(const BaseColumn& column) {
                column.encoding_type() == EncodingType::FrameOfReference) {
       // encoded chunk: its compressed arrays go to HBM as they are (the TableScans' HY_COL_RLE / HY_COL_FOR form);
       // the value mirror is decoded from them on the first row-wise use (decode_mirror)
-      Assert(column.data_type() != DataType::String,
-             "hyrise-amd: encoded string columns other than Dictionary are not resident on the device");
       resolve_data_type(column.data_type(), [&](auto tag) {
         using T = decltype(tag);
-        if constexpr (!std::is_same_v<T, std::string>) {
+        if constexpr (std::is_same_v<T, std::string>) {
+          // RunLength strings (FrameOfReference takes integers only): the runs' values as one packed string array,
+          // their end positions and NULL flags - the string TableScans evaluate the predicate once per run
+          const auto* rl = dynamic_cast<const RunLengthColumn<std::string>*>(&column);
+          Assert(rl != nullptr, "device_column: unknown encoded string column");
+          hy_column_chunk& c = d->compressed;
+          c.size = static_cast<uint32_t>(column.size());
+          d->c_data = upload_strings(rl->values(), s);
+          d->c_aux = upload(rl->end_positions().data(), rl->end_positions().size() * 4, s);
+          if (std::find(rl->null_values().begin(), rl->null_values().end(), uint8_t{1}) != rl->null_values().end())
+            d->c_nulls = upload(rl->null_values().data(), rl->null_values().size(), s);
+          c.kind = HY_COL_RLE;
+          c.dictionary_size = static_cast<uint32_t>(rl->end_positions().size());
+          c.data = d->c_data->get();
+          c.dictionary = d->c_aux->get();
+          c.nulls = d->c_nulls ? d->c_nulls->as<uint8_t>() : nullptr;
+        } else {
           hy_column_chunk& c = d->compressed;
           c.size = static_cast<uint32_t>(column.size());
           if (const auto* rl = dynamic_cast<const RunLengthColumn<T>*>(&column)) {
@@ -321,7 +341,7 @@ std::shared_ptr<DeviceColumn> resident(const BaseColumn& column) {
       });
       d->has_compressed = true;
       d->decoded = false;
-      d->desc.kind = HY_COL_VALUE;
+      d->desc.kind = column.data_type() == DataType::String ? HY_COL_STRING : HY_COL_VALUE;
     } else {
       Assert(!column.is_reference(), "device_column of a ReferenceColumn");
       resolve_data_type(column.data_type(), [&](auto tag) {
@@ -351,7 +371,29 @@ void decode_mirror(DeviceColumn& d, const BaseColumn& column) {
   const uint32_t n = c.size;
   resolve_data_type(column.data_type(), [&](auto tag) {
     using T = decltype(tag);
-    if constexpr (!std::is_same_v<T, std::string>) {
+    if constexpr (std::is_same_v<T, std::string>) {
+      // RunLength strings row-wise (column compares, projections): the runs expanded on the host into a packed string
+      // array per row (string rows are not a device-decoded format), NULL flags per row
+      const auto& rl = static_cast<const RunLengthColumn<std::string>&>(column);
+      std::vector<std::string> rows(n);
+      std::vector<uint8_t> nulls(std::max<size_t>(n, 1) + 16, 0);
+      bool any_null = false;
+      size_t r = 0;
+      for (uint32_t i = 0; i < n; ++i) {
+        while (rl.end_positions()[r] < i) ++r;
+        if (rl.null_values()[r]) {
+          nulls[i] = 1;
+          any_null = true;
+        } else {
+          rows[i] = rl.values()[r];
+        }
+      }
+      d.data = upload_strings(rows, s);
+      if (any_null) {
+        d.nulls = upload(nulls.data(), nulls.size(), s);
+        hy_check(hy_stream_synchronize(s), "hy_stream_synchronize");  // `nulls` is pageable and local
+      }
+    } else {
       d.data = std::make_shared<DeviceBuffer>(std::max<size_t>(n, 1) * sizeof(T) + 16);
       if (c.kind == HY_COL_RLE) {
         if (c.nulls) d.nulls = std::make_shared<DeviceBuffer>(std::max<size_t>(n, 1) + 16);

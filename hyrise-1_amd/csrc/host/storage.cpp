@@ -394,12 +394,42 @@ std::shared_ptr<BaseColumn> encode_frame_of_reference(const BaseColumn& base) {
   return out;
 }
 
+// reference dictionary_column/dictionary_encoder.hpp:36-48, 132-138 with EncodingType::FixedStringDictionary: the
+// values as FixedStrings of the longest value's length (a value reads back up to its first '\0'), sorted and unique;
+// std::string columns only.
+std::shared_ptr<BaseColumn> encode_fixed_string_dictionary(const BaseColumn& base, VectorCompressionType compression) {
+  const auto* vc = dynamic_cast<const ValueColumn<std::string>*>(&base);
+  if (!vc) Fail("FixedStringDictionary encoding supports string columns only");
+  const auto& values = vc->values();
+  size_t len = 0;
+  for (const auto& v : values) len = std::max(len, v.size());
+  auto fixed = [&](const std::string& v) { return std::string(v.data(), strnlen(v.data(), v.size())); };
+  std::vector<std::string> dict;
+  dict.reserve(values.size());
+  for (size_t i = 0; i < values.size(); ++i)
+    if (!vc->is_null(static_cast<ChunkOffset>(i))) dict.push_back(fixed(values[i]));
+  std::sort(dict.begin(), dict.end());
+  dict.erase(std::unique(dict.begin(), dict.end()), dict.end());
+  const auto null_value_id = static_cast<uint32_t>(dict.size());
+  std::vector<uint32_t> vids(values.size());
+  for (size_t i = 0; i < values.size(); ++i)
+    vids[i] = vc->is_null(static_cast<ChunkOffset>(i))
+                  ? null_value_id
+                  : static_cast<uint32_t>(std::lower_bound(dict.cbegin(), dict.cend(), fixed(values[i])) - dict.cbegin());
+  std::vector<char> chars(len ? len * dict.size() : 1, '\0');  // (fixed_string_vector.hpp:27-33: one byte if len 0)
+  for (size_t i = 0; i < dict.size() && len; ++i) std::memcpy(chars.data() + i * len, dict[i].data(), dict[i].size());
+  auto av = std::make_shared<const AttributeVector>(vids, static_cast<uint32_t>(dict.size() + 1u), compression);
+  return std::make_shared<FixedStringDictionaryColumn>(std::move(chars), len, dict.size(), std::move(av), null_value_id);
+}
+
 namespace {
 std::shared_ptr<BaseColumn> encode_column(const BaseColumn& col, EncodingType encoding,
                                           VectorCompressionType compression) {
   switch (encoding) {
     case EncodingType::Dictionary:
       return encode_dictionary(col, compression);
+    case EncodingType::FixedStringDictionary:
+      return encode_fixed_string_dictionary(col, compression);
     case EncodingType::RunLength:
       return encode_run_length(col);
     case EncodingType::FrameOfReference:
@@ -414,8 +444,6 @@ void ChunkEncoder::encode_chunks(const std::shared_ptr<Table>& table, const std:
                                  EncodingType encoding, VectorCompressionType compression) {
   Assert(table->type() == TableType::Data, "Only data tables can be encoded");
   if (encoding == EncodingType::Unencoded) return;
-  if (encoding == EncodingType::FixedStringDictionary)
-    Fail("Encoding type not supported by the device path (FixedStringDictionary)");
   for (const auto chunk_id : chunk_ids) {
     const auto chunk = table->get_chunk(chunk_id);
     for (ColumnID c = 0; c < chunk->column_count(); ++c) {
@@ -426,6 +454,8 @@ void ChunkEncoder::encode_chunks(const std::shared_ptr<Table>& table, const std:
       if (encoding == EncodingType::FrameOfReference && col->data_type() != DataType::Int &&
           col->data_type() != DataType::Long)
         continue;
+      // likewise FixedStringDictionary (a string-only encoding) keeps numeric columns unencoded
+      if (encoding == EncodingType::FixedStringDictionary && col->data_type() != DataType::String) continue;
       chunk->replace_column(c, encode_column(*col, encoding, compression));
     }
   }
@@ -435,8 +465,6 @@ void ChunkEncoder::encode_columns(const std::shared_ptr<Table>& table, const std
                                   EncodingType encoding, VectorCompressionType compression) {
   Assert(table->type() == TableType::Data, "Only data tables can be encoded");
   if (encoding == EncodingType::Unencoded) return;
-  if (encoding != EncodingType::Dictionary)
-    Fail("Encoding type not supported by the device path (only Unencoded and Dictionary)");
   // chunks are independent: encoded in parallel (the reference encodes chunk by chunk in jobs as well)
   const ChunkID n = table->chunk_count();
   const unsigned workers = std::max(1u, std::min(16u, host_cpu_share()));
@@ -446,8 +474,10 @@ void ChunkEncoder::encode_columns(const std::shared_ptr<Table>& table, const std
       const auto chunk = table->get_chunk(c);
       for (const auto col_id : column_ids) {
         const auto col = chunk->get_column(col_id);
-        if (col->encoding_type() != EncodingType::Dictionary)
-          chunk->replace_column(col_id, encode_dictionary(*col, compression));
+        // (the reference's per-column ChunkEncodingSpec, chunk_encoder.cpp: a column already in `encoding` stays)
+        if (col->encoding_type() == encoding) continue;
+        if (col->encoding_type() != EncodingType::Unencoded) Fail("encode_columns re-encodes unencoded columns only");
+        chunk->replace_column(col_id, encode_column(*col, encoding, compression));
       }
     }
   };

@@ -248,7 +248,7 @@ class BaseDictionaryColumn : public BaseColumn {
 };
 
 template <typename T>
-class DictionaryColumn final : public BaseDictionaryColumn {
+class DictionaryColumn : public BaseDictionaryColumn {
  public:
   DictionaryColumn(std::shared_ptr<const std::vector<T>> dictionary, std::shared_ptr<const AttributeVector> av,
                    ValueID null_value_id)
@@ -290,6 +290,38 @@ class DictionaryColumn final : public BaseDictionaryColumn {
   std::shared_ptr<const std::vector<T>> _dictionary;
   std::shared_ptr<const AttributeVector> _attribute_vector;
   ValueID _null_value_id;
+};
+
+// FixedStringDictionaryColumn (reference storage/fixed_string_dictionary_column.hpp, fixed_string_vector.hpp): a string
+// dictionary stored as one char array of fixed-width entries (every entry padded with '\0' to the longest value's
+// length, dictionary_encoder.hpp:132-138), plus the attribute vector. An entry reads as its chars up to the first
+// '\0' (FixedString::string, fixed_string.cpp), so values are compared, bounded and returned exactly as the
+// reference's. It is a DictionaryColumn<std::string> over those decoded entries: scans rewrite predicates to value ids
+// and the device reads the attribute vector as for Dictionary; encoding_type() tells the two apart.
+class FixedStringDictionaryColumn final : public DictionaryColumn<std::string> {
+ public:
+  FixedStringDictionaryColumn(std::vector<char> chars, size_t string_length, size_t n_entries,
+                              std::shared_ptr<const AttributeVector> av, ValueID null_value_id)
+      : DictionaryColumn<std::string>(decode(chars, string_length, n_entries), std::move(av), null_value_id),
+        _chars(std::move(chars)),
+        _string_length(string_length) {}
+  EncodingType encoding_type() const override { return EncodingType::FixedStringDictionary; }
+  // the fixed-width entries (string_length() bytes each; one '\0' byte when every value is empty)
+  const std::vector<char>& fixed_string_chars() const { return _chars; }
+  size_t string_length() const { return _string_length; }
+
+ private:
+  static std::shared_ptr<const std::vector<std::string>> decode(const std::vector<char>& chars, size_t len, size_t n) {
+    auto v = std::make_shared<std::vector<std::string>>();
+    v->reserve(n);
+    for (size_t i = 0; i < n; ++i) {
+      const char* p = chars.data() + i * len;
+      v->emplace_back(p, len ? strnlen(p, len) : 0);
+    }
+    return v;
+  }
+  std::vector<char> _chars;
+  size_t _string_length;
 };
 
 class ReferenceColumn final : public BaseColumn {

@@ -64,27 +64,62 @@ __host__ __device__ inline uint32_t murmur2(T key, uint32_t seed) {
 
 // Predicate of one row (HY_OP_*): value compare of the reference's with_comparator (type_comparison.hpp:100-123), or
 // the value-id compare of the dictionary rewrite (single_column_table_scan_impl.hpp:52-76).
+// Branch-free: the op selects which of (v < c, v == c, v > c) accept and whether the result is inverted (one nibble
+// per op of CMP_OP_CODES: bit 0 <, bit 1 ==, bit 2 >, bit 3 invert; != is "not ==", so NaN != c holds as in C++,
+// ALL / IS NOT NULL accept every row, NONE / IS NULL / anything else none). A switch here compiled to a scalar branch
+// tree per element of the scans' unrolled 16-row loops (~10,000 instructions for one 4-tile u8 scan; round-6
+// tools/scan_probe.hip: the count pass alone took 47 us against a 10 us read ceiling).
+constexpr uint64_t CMP_OP_CODES = 0x80086431A2ull;  // ops 0..9: EQ NE LT LE GT GE ALL NONE IS_NULL IS_NOT_NULL
+__device__ __forceinline__ uint32_t cmp_op_code(int op) {
+  return static_cast<uint32_t>(op) < 10u ? static_cast<uint32_t>(CMP_OP_CODES >> (4 * op)) & 15u : 0u;
+}
+template <typename T>
+__device__ __forceinline__ bool cmp_code(uint32_t code, T v, T c) {
+  const bool r = ((code & 1u) != 0 & (v < c)) | ((code & 2u) != 0 & (v == c)) | ((code & 4u) != 0 & (v > c));
+  return r != ((code & 8u) != 0);
+}
 template <typename T>
 __device__ __forceinline__ bool cmp_op(int op, T v, T c) {
+  return cmp_code<T>(cmp_op_code(op), v, c);
+}
+
+// A dictionary predicate (op, search value id s) of the host's rewrite over value ids whose NULL id is dsize (the
+// dictionary size, reference dictionary_encoder.hpp: null_value_id = dictionary.size()), as one id range and one
+// excluded id: a row matches iff (id - lo) < span and id != except. EQ [s, s+1), LT [0, s), LE [0, s+1), GT [s+1,
+// dsize), GE [s, dsize), ALL / IS NOT NULL [0, dsize), IS NULL [dsize, dsize+1), NE [0, dsize) except s, NONE and
+// the rest nothing; every range is clipped to [0, dsize] so the NULL id only ever matches IS NULL. Two compares per
+// row instead of a compare per op: the scans' unrolled 16-row loops measured 25 -> 12 us for the count of config 2's
+// 60 M u8 ids (round-6 tools/scan_probe.hip, seg_count_var3 vs _var1). Ids are compared as read (E-width, widened).
+struct DictPred {
+  uint32_t lo, span, except;
+};
+__device__ __forceinline__ DictPred dict_pred(int op, uint32_t s, uint32_t dsize) {
+  const uint32_t s1 = s < dsize ? s + 1 : dsize;  // min(s + 1, dsize)
+  const uint32_t s0 = s < dsize ? s : dsize;      // min(s, dsize)
   switch (op) {
     case HY_OP_EQ:
-      return v == c;
+      return {s0, s1 - s0, dsize};
     case HY_OP_NE:
-      return v != c;
+      return {0u, dsize, s};
     case HY_OP_LT:
-      return v < c;
+      return {0u, s0, dsize};
     case HY_OP_LE:
-      return v <= c;
+      return {0u, s1, dsize};
     case HY_OP_GT:
-      return v > c;
+      return {s1, dsize - s1, dsize};
     case HY_OP_GE:
-      return v >= c;
+      return {s0, dsize - s0, dsize};
     case HY_OP_ALL:
     case HY_OP_IS_NOT_NULL:
-      return true;
+      return {0u, dsize, dsize};
+    case HY_OP_IS_NULL:
+      return {dsize, 1u, dsize + 1u};
     default:
-      return false;
+      return {0u, 0u, 0u};
   }
+}
+__device__ __forceinline__ bool dict_match(const DictPred& p, uint32_t id) {
+  return (id - p.lo < p.span) & (id != p.except);
 }
 
 // ------------------------------------------------------------------------------------------------------------

@@ -657,10 +657,9 @@ __device__ __forceinline__ uint32_t filter_items_t(const hy_scan_chunk& f, uint3
   uint32_t m = 0;
   const int op = f.op;
   if constexpr (DICT) {
-    const E null_vid = static_cast<E>(f.column.dictionary_size);
-    const E s = static_cast<E>(f.search_vid);
+    const DictPred pr = dict_pred(op, static_cast<E>(f.search_vid), static_cast<E>(f.column.dictionary_size));
 #pragma unroll
-    for (int k = 0; k < PART_ITEMS; ++k) m |= static_cast<uint32_t>(v[k] != null_vid && cmp_op<E>(op, v[k], s)) << k;
+    for (int k = 0; k < PART_ITEMS; ++k) m |= static_cast<uint32_t>(dict_match(pr, v[k])) << k;
   } else {
     E c;
     __builtin_memcpy(&c, &cbits, sizeof(E));
@@ -722,6 +721,9 @@ struct Digit {
   // string join keys (hy_join_params.key_hash): int32 keys are ids of distinct strings and key_hash[id] is the
   // string's murmur2 (murmur_hash.hpp:16-20), so partitioning follows the reference's string hashes; else null
   const uint32_t* key_hash;
+  // 1: stable ranking by per-bit ballots (wave_rank) instead of one LDS fetch-add per item (wave_rank_add): the
+  // fallback for a device whose rank_order_check failed (join_host.hpp check_rank_order), or HY_RANK_BALLOT=1
+  uint32_t ballot_rank;
 };
 
 // The partitioning hash of a key: murmur2 over its bytes (join_hash.cpp:253), or the precomputed string hash.
@@ -816,6 +818,14 @@ __device__ __forceinline__ uint32_t wave_rank_lds(uint32_t digit, bool active, u
 // device that breaks it fails the join with HY_ERR_KERNEL instead of producing an unstable order.
 __device__ __forceinline__ uint32_t wave_rank_add(uint32_t digit, bool active, uint32_t* wave_cnt) {
   return active ? __hip_atomic_fetch_add(&wave_cnt[digit], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0u;
+}
+
+// The stable rank of a partition pass's item: wave_rank_add, or on a device that failed rank_order_check (and under
+// HY_RANK_BALLOT=1) the per-bit ballot ranking, which relies on nothing but ballots and one wave's in-order LDS access
+// (dg.ballot_rank is a kernel argument: the branch is uniform). Every lane of the wave calls it for every item.
+__device__ __forceinline__ uint32_t rank_item(const Digit& dg, uint32_t digit, bool active, uint32_t* wave_cnt) {
+  if (dg.ballot_rank) return wave_rank(digit, active, 8, wave_cnt);
+  return wave_rank_add(digit, active, wave_cnt);
 }
 
 // Self-check of wave_rank_add against wave_rank_lds (one 256-thread workgroup; *bad counts mismatching items): waves
@@ -1016,7 +1026,7 @@ __global__ __launch_bounds__(PART_THREADS) __attribute__((amdgpu_waves_per_eu(4)
     for (int k = 0; k < PART_ITEMS; ++k) {
       const bool a = (act >> k) & 1u;
       const uint32_t dig = a ? digit_of<H>(dg, keys[k]) : 0u;
-      dr[k] = (dig << 24) | wave_rank_add(dig, a, s_cnt[w]);
+      dr[k] = (dig << 24) | rank_item(dg, dig, a, s_cnt[w]);
       recs[k].key = keys[k];
       recs[k].payload = pays[k];
     }
@@ -1158,7 +1168,7 @@ __global__ __launch_bounds__(PART_THREADS) void part1_spread(Side s, Digit dg, N
     for (int k = 0; k < PART_ITEMS; ++k) {
       const bool a = (act >> k) & 1u;
       const uint32_t dig = a ? digit_of<H>(dg, recs[k].key) : 0u;
-      dr[k] = (dig << 24) | wave_rank_add(dig, a, s_cnt[w]);
+      dr[k] = (dig << 24) | rank_item(dg, dig, a, s_cnt[w]);
     }
     staged_scatter<H, uint32_t>(recs, act, dr, s_cnt, s_delta, s_stage, s_scratch, n_digits, dg, nd, run, out);
   }
@@ -1318,7 +1328,7 @@ __global__ __launch_bounds__(PART_THREADS) void part1_spread_mask(Side s, Digit 
     for (int k = 0; k < PART_ITEMS; ++k) {
       const bool aa = (act >> k) & 1u;
       const uint32_t dig = aa ? digit_of<H>(dg, recs[k].key) : 0u;
-      dr[k] = (dig << 24) | wave_rank_add(dig, aa, s_cnt[w]);
+      dr[k] = (dig << 24) | rank_item(dg, dig, aa, s_cnt[w]);
     }
     staged_scatter<H, uint32_t>(recs, act, dr, s_cnt, s_delta, s_comp, s_scratch, n_digits, dg, nd, run, out);
   }
@@ -1385,13 +1395,10 @@ __device__ __forceinline__ uint32_t filter_dict_contig(const hy_scan_chunk& f, u
 #pragma unroll
     for (int i = 0; i < PART_ITEMS; ++i) v[i] = data[min(r0 + i, n - 1)];
   }
-  const E null_vid = static_cast<E>(f.column.dictionary_size);
-  const E sv = static_cast<E>(f.search_vid);
-  const int op = f.op;
+  const DictPred pr = dict_pred(f.op, static_cast<E>(f.search_vid), static_cast<E>(f.column.dictionary_size));
   uint32_t m = 0;
 #pragma unroll
-  for (int i = 0; i < PART_ITEMS; ++i)
-    m |= static_cast<uint32_t>(r0 + i < n && v[i] != null_vid && cmp_op<E>(op, v[i], sv)) << i;
+  for (int i = 0; i < PART_ITEMS; ++i) m |= static_cast<uint32_t>((r0 + i < n) & dict_match(pr, v[i])) << i;
   return m;
 }
 
@@ -1511,7 +1518,7 @@ __global__ __launch_bounds__(PART_THREADS) __attribute__((amdgpu_waves_per_eu(4)
     for (int k = 0; k < PART_ITEMS; ++k) {
       const bool a = (act >> k) & 1u;
       const uint32_t dig = a ? digit_of<H>(dg, keys[k]) : 0u;
-      dr[k] = (dig << 24) | wave_rank_add(dig, a, s_cnt[w]);
+      dr[k] = (dig << 24) | rank_item(dg, dig, a, s_cnt[w]);
       recs[k].key = keys[k];
       recs[k].payload = pays[k];
     }
@@ -1709,7 +1716,7 @@ __global__ __launch_bounds__(PART_THREADS) void part1_onepass(Side s, Digit dg, 
   for (int k = 0; k < PART_ITEMS; ++k) {
     const bool a = (act >> k) & 1u;
     const uint32_t dig = a ? digit_of<H>(dg, keys[k]) : 0u;
-    dr[k] = (dig << 24) | wave_rank_add(dig, a, s_cnt[w]);
+    dr[k] = (dig << 24) | rank_item(dg, dig, a, s_cnt[w]);
     recs[k].key = keys[k];
     recs[k].payload = pays[k];
   }
@@ -1975,7 +1982,7 @@ __global__ __launch_bounds__(PART_THREADS) void part2_scatter(Segs sg, Digit dg,
     for (int k = 0; k < PART_ITEMS; ++k) {
       const bool a = (act >> k) & 1u;
       const uint32_t dig = a ? digit_of<H>(dg, recs[k].key) : 0u;
-      dr[k] = (dig << 24) | wave_rank_add(dig, a, s_cnt[w]);
+      dr[k] = (dig << 24) | rank_item(dg, dig, a, s_cnt[w]);
     }
     staged_scatter<H, P>(recs, act, dr, s_cnt, s_delta, s_stage, s_scratch, n_digits, dg, nd, run, out);
   }

@@ -214,7 +214,7 @@ __global__ __launch_bounds__(PART_THREADS) void part1_direct(Side s, Digit dg, N
     for (int k = 0; k < PART_ITEMS; ++k) {
       const bool a = (act >> k) & 1u;
       const uint32_t dig = a ? digit_of<H>(dg, keys[k]) : 0u;
-      dr[k] = (dig << 24) | wave_rank_add(dig, a, s_cnt[w]);
+      dr[k] = (dig << 24) | rank_item(dg, dig, a, s_cnt[w]);
       r[k].key = keys[k];
       r[k].payload = pays[k];
     }
@@ -365,7 +365,7 @@ __global__ __launch_bounds__(PART_THREADS) void part2g_scatter(GroupGeo gg, Digi
     for (int k = 0; k < PART_ITEMS; ++k) {
       const bool a = (act >> k) & 1u;
       const uint32_t dig = a ? digit_of<H>(dg, recs[k].key) : 0u;
-      dr[k] = (dig << 24) | wave_rank_add(dig, a, s_cnt[w]);
+      dr[k] = (dig << 24) | rank_item(dg, dig, a, s_cnt[w]);
     }
     staged_scatter<H, P>(recs, act, dr, s_cnt, s_delta, s_stage, s_scratch, n_digits, dg, none, run, out);
   }

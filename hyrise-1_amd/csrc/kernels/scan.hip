@@ -25,6 +25,8 @@
 
 namespace hyk {
 
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+
 constexpr int SCAN_THREADS = 256;
 constexpr int SCAN_ROWS_PER_THREAD = 16;
 constexpr int SCAN_TILE = SCAN_THREADS * SCAN_ROWS_PER_THREAD;  // 4096
@@ -81,12 +83,6 @@ __device__ __forceinline__ uint32_t match_mask(const hy_scan_chunk& ch, uint32_t
   const int op = ch.op;
   if constexpr (IS_DICT) {
     const E null_vid = static_cast<E>(ch.column.dictionary_size);
-    const E s = static_cast<E>(ch.search_vid);
-    if (op == HY_OP_IS_NULL) {  // is_null_table_scan_impl.cpp:55-61: the iterator's is_null() is vid == null id
-#pragma unroll
-      for (int i = 0; i < 16; ++i) mask |= static_cast<uint32_t>(v[i] == null_vid) << i;
-      return mask & valid;
-    }
     if (op == HY_OP_VID_SET) {  // like_table_scan_impl.cpp:62-83: dictionary_matches[vid], NULL rows skipped
       const uint32_t* __restrict__ set = ch.vid_set;
 #pragma unroll
@@ -97,11 +93,11 @@ __device__ __forceinline__ uint32_t match_mask(const hy_scan_chunk& ch, uint32_t
       }
       return mask & valid;
     }
+    // comparisons, ALL / NONE and IS [NOT] NULL (is_null_table_scan_impl.cpp:55-61: the iterator's is_null() is
+    // vid == null id) as one id range
+    const DictPred pr = dict_pred(op, static_cast<E>(ch.search_vid), null_vid);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const bool m = (v[i] != null_vid) && cmp_op<E>(op, v[i], s);
-      mask |= static_cast<uint32_t>(m) << i;
-    }
+    for (int i = 0; i < 16; ++i) mask |= static_cast<uint32_t>(dict_match(pr, v[i])) << i;
   } else {
     uint8_t nl[16];
     __builtin_memcpy(nl, &nulls, 16);
@@ -115,13 +111,13 @@ __device__ __forceinline__ uint32_t match_mask(const hy_scan_chunk& ch, uint32_t
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const V x = static_cast<V>(base + static_cast<V>(v[i]));
-        const bool m = (nl[i] == 0) && cmp_op<V>(op, x, constant.value);
+        const bool m = (nl[i] == 0) & cmp_op<V>(op, x, constant.value);
         mask |= static_cast<uint32_t>(m) << i;
       }
     } else {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const bool m = (nl[i] == 0) && cmp_op<E>(op, v[i], constant.value);
+        const bool m = (nl[i] == 0) & cmp_op<E>(op, v[i], constant.value);
         mask |= static_cast<uint32_t>(m) << i;
       }
     }
@@ -224,10 +220,25 @@ void scan_kernel(ScanLaunchDesc d, ScanConst<V> constant,
     __syncthreads();
     if constexpr (OUT_ROWID) {
       hy_row_id* out = static_cast<hy_row_id*>(out_any) + run;
-      // streaming stores: the RowIDs are read by a later operator, not by this kernel (8 B {chunk_id, offset} each)
+      // streaming stores: the RowIDs are read by a later operator, not by this kernel (8 B {chunk_id, offset} each),
+      // two per 16-byte store from a 16-byte boundary on (tools/scan_probe.hip, profiles/r05_scan_probe.jsonl: the
+      // 221 MB RowID write of config 2 takes 0.052 ms this way against 0.063 ms with one 8-byte store per RowID)
       uint64_t* out64 = reinterpret_cast<uint64_t*>(out);
-      for (uint32_t i = threadIdx.x; i < tile_total; i += SCAN_THREADS)
-        __builtin_nontemporal_store(static_cast<uint64_t>(cid) | (static_cast<uint64_t>(s_stage[i]) << 32), out64 + i);
+      const uint32_t lead = (reinterpret_cast<uintptr_t>(out64) & 15u) ? 1u : 0u;  // (RowIDs are 8-byte aligned)
+      if (lead && threadIdx.x == 0 && tile_total)
+        __builtin_nontemporal_store(static_cast<uint64_t>(cid) | (static_cast<uint64_t>(s_stage[0]) << 32), out64);
+      const uint32_t body = tile_total > lead ? tile_total - lead : 0u;
+      u64x2* out128 = reinterpret_cast<u64x2*>(out64 + lead);
+      for (uint32_t p = threadIdx.x; p < body / 2; p += SCAN_THREADS) {
+        const uint32_t i = lead + 2 * p;
+        u64x2 v;
+        v.x = static_cast<uint64_t>(cid) | (static_cast<uint64_t>(s_stage[i]) << 32);
+        v.y = static_cast<uint64_t>(cid) | (static_cast<uint64_t>(s_stage[i + 1]) << 32);
+        __builtin_nontemporal_store(v, out128 + p);
+      }
+      if ((body & 1u) && threadIdx.x == SCAN_THREADS - 1)
+        __builtin_nontemporal_store(static_cast<uint64_t>(cid) | (static_cast<uint64_t>(s_stage[tile_total - 1]) << 32),
+                                    out64 + tile_total - 1);
     } else {
       uint32_t* out = static_cast<uint32_t*>(out_any) + run;
       for (uint32_t i = threadIdx.x; i < tile_total; i += SCAN_THREADS) out[i] = s_stage[i];

@@ -130,7 +130,11 @@ const char* hy_build_info(void);
  *                     block minima (value_type, one per 2048 rows); row value = minima[row / 2048] + offset[row]
  *   HY_COL_RLE        RunLengthColumn<T> (reference run_length_column.hpp, compressed form - TableScans only): data =
  *                     run values (T[dictionary_size]), nulls = uint8 per run or NULL, dictionary = end_positions
- *                     (uint32[dictionary_size], the last row of each run, ascending), dictionary_size = runs
+ *                     (uint32[dictionary_size], the last row of each run, ascending), dictionary_size = runs.
+ *                     RunLengthColumn<std::string> (string scans only): data = a packed string array (below) of
+ *                     the runs' values, the rest as above; the predicate is evaluated once per run.
+ *   FixedStringDictionaryColumn (reference fixed_string_dictionary_column.hpp) is passed as HY_COL_DICT: its
+ *                     fixed-width entries decoded up to their first '\0', as a packed string array in dictionary.
  * The other entry points (joins, aggregates, projections, column compares) read these chunks as HY_COL_VALUE mirrors
  * (hy_decode_run_length / hy_decode_frame_of_reference) and reject HY_COL_FOR / HY_COL_RLE with HY_ERR_UNSUPPORTED.
  */
@@ -292,9 +296,10 @@ hy_status hy_expand_chunk_row_ids(const uint32_t* offsets, const uint64_t* chunk
  * is_null_table_scan_impl.cpp:35-117)
  *
  * Chunks are HY_COL_STRING (compared with pred->value: HY_OP_EQ..HY_OP_GE as std::string::compare, unsigned bytes then
- * length; HY_OP_LIKE / HY_OP_NOT_LIKE against pred->pattern; IS [NOT] NULL, ALL, NONE) or HY_COL_DICT (op + search_vid
- * or HY_OP_VID_SET exactly as hy_table_scan: the host's dictionary rewrite). A table may mix both (an unencoded chunk
- * beside dictionary chunks). NULL rows never match a comparison or LIKE.
+ * length; HY_OP_LIKE / HY_OP_NOT_LIKE against pred->pattern; IS [NOT] NULL, ALL, NONE), HY_COL_RLE of strings (the
+ * same predicate on each run's value, spread to the run's rows) or HY_COL_DICT (op + search_vid or HY_OP_VID_SET exactly
+ * as hy_table_scan: the host's dictionary rewrite). A table may mix them (an unencoded chunk beside dictionary and
+ * run-length chunks). NULL rows never match a comparison or LIKE.
  * pattern_regex: 0 for the reference's simple patterns (LikeMatcher::pattern_string_to_pattern_tokens gives
  * StartsWith / EndsWith / Contains / MultipleContains: '%' and '_' match any byte), 1 for every other pattern (the
  * reference's std::regex path, like_matcher.cpp:27-52: '%' and '_' match any byte but '\n' / '\r'; '[...]' is a

@@ -317,7 +317,16 @@ void like_scan_column(const BaseColumn& col, PredicateCondition cond, const AllT
     return;
   }
   const auto* vc = dynamic_cast<const ValueColumn<std::string>*>(&col);
-  Assert(vc != nullptr, "LIKE operator only applicable on string columns.");
+  if (vc == nullptr) {  // RunLength: position by position through the column's decoding (the generic iterable,
+                        // like_table_scan_impl.cpp:86-97)
+    Assert(col.encoding_type() == EncodingType::RunLength, "LIKE operator only applicable on string columns.");
+    each([&](ChunkOffset into, ChunkOffset o) {
+      const auto v = col[o];
+      if (variant_is_null(v)) return;
+      if (matcher(std::get<std::string>(v)) != invert) out.emplace_back(chunk_id, into);
+    });
+    return;
+  }
   each([&](ChunkOffset into, ChunkOffset o) {
     if (vc->is_null(o)) return;
     if (matcher(vc->values()[o]) != invert) out.emplace_back(chunk_id, into);

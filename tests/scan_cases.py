@@ -176,14 +176,23 @@ LIKE_SPECIAL_CASES = [
 ]
 
 
-def like_tables(hy, encodings=(None, "Dictionary")):
-    """_gt_string (chunk 2, unencoded) and _gt_string_compressed (chunk 5, encoded), as tables."""
+STRING_ENCODINGS = ("Unencoded", "Dictionary", "FixedStringDictionary", "RunLength")  # table_scan_string_test.cpp:69-72
+
+
+def string_compressed(hy, enc):
+    """_gt_string_compressed (table_scan_string_test.cpp:46-57): chunk size 5, the int column unencoded and the
+    string column in `enc` (the reference's ChunkEncodingSpec {Unencoded, GetParam()})."""
+    t = hy.load_table(tbl("int_string_like.tbl"), 5)
+    if enc and enc != "Unencoded":
+        hy.encode_columns(t, [1], getattr(hy.EncodingType, enc))
+    return t
+
+
+def like_tables(hy, encodings=(None,) + STRING_ENCODINGS):
+    """_gt_string (chunk 2, unencoded) and _gt_string_compressed in each encoding, as tables."""
     out = []
     for enc in encodings:
-        t = hy.load_table(tbl("int_string_like.tbl"), 5 if enc else 2)
-        if enc:
-            hy.encode_all_chunks(t, getattr(hy.EncodingType, enc))
-        out.append((enc, t))
+        out.append((enc, string_compressed(hy, enc) if enc else hy.load_table(tbl("int_string_like.tbl"), 2)))
     return out
 
 

@@ -16,6 +16,11 @@ from test_scan_join_gpu import Filter, check_join, check_scan, orders_lineitem, 
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def direct_on(monkeypatch):
+    monkeypatch.setenv("HY_JOIN_DIRECT", "1")  # (opt-in: the classic passes are the default)
+
+
 def lineitem_orders(hy, rng, n_orders, lchunk, ochunk, skew=0.0):
     okey, ostatus, lkey, lkey_nulls, qty, qty_nulls = orders_lineitem(rng, n_orders, True)
     if skew:  # a share of the probe rows on one build key: its bucket's regions overflow
@@ -32,7 +37,6 @@ def lineitem_orders(hy, rng, n_orders, lchunk, ochunk, skew=0.0):
 @pytest.mark.parametrize("span,groups", [("1", "0"), ("3", "7"), ("16", "1"), ("5", "0")])
 @pytest.mark.parametrize("key_enc", ["Unencoded", "Dictionary"])
 def test_direct_passes_match_oracle(hy, oracle, monkeypatch, bits, span, groups, key_enc):
-    monkeypatch.setenv("HY_JOIN_DIRECT", "1")
     monkeypatch.setenv("HY_DIRECT_SPAN", span)
     monkeypatch.setenv("HY_DIRECT_GROUPS", groups)
     monkeypatch.setenv("HY_JOIN_BLOOM", "0")
@@ -153,3 +157,33 @@ def test_direct_prepared_plan_replays(hy, oracle, monkeypatch, skew):
     finally:
         L.hy_scan_join_plan_destroy(plan)
         L.hy_stream_destroy(stream)
+
+
+@pytest.mark.parametrize("direct", ["0", "1"])
+@pytest.mark.parametrize("mode", ["Inner", "Left", "Semi"])
+def test_ballot_rank_fallback(hy, oracle, monkeypatch, direct, mode):
+    """HY_RANK_BALLOT=1 forces the ranking a device falls back to when rank_order_check fails (per-bit ballots,
+    hyk::rank_item) in every partition pass - classic and direct, both sides: the output still equals the oracle's."""
+    monkeypatch.setenv("HY_RANK_BALLOT", "1")
+    monkeypatch.setenv("HY_JOIN_DIRECT", direct)
+    monkeypatch.setenv("HY_JOIN_BLOOM", "0")
+    capi = hy.capi
+    rng = np.random.default_rng(zlib.crc32(repr(("ballot", direct, mode)).encode()))
+    okey, lkey, lkey_nulls, qty, qty_nulls, lineitem, orders = lineitem_orders(hy, rng, 20_000, 7_000, 3_000)
+    probe_t = oracle.table_scan(lineitem, 1, hy.PredicateCondition.LessThan, 24.0, [])
+    jm = getattr(hy.JoinMode, mode)
+    expected, bits = oracle.join_hash(orders, probe_t, jm, (0, 0), radix_bits=16)
+    lk = dt.DeviceColumn(capi, lkey, lkey_nulls, 7_000, "Unencoded")
+    lq = dt.DeviceColumn(capi, qty, qty_nulls, 7_000, "Dictionary")
+    ok = dt.DeviceColumn(capi, okey, None, 3_000, "Unencoded")
+    lf = Filter(capi, lq, "LessThan", 24.0)
+    swapped = mode in ("Left", "Semi")
+    params = capi.JoinParams({"Inner": 0, "Left": 1, "Semi": 5}[mode], capi.HY_TYPE_INT32, bits, 17)
+    o_side, l_side = dt.join_side(capi, ok), dt.join_side(capi, lk)
+    cap = okey.size * 3 + lkey.size + 16
+    if swapped:
+        parts = run_fused(hy, l_side, lf.f, o_side, None, params, cap)
+    else:
+        parts = run_fused(hy, o_side, None, l_side, lf.f, params, cap)
+    check_scan(probe_t, lf)
+    check_join(expected, parts, 2, swapped, mode == "Semi")

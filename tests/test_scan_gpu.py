@@ -224,7 +224,7 @@ def test_column_comparison_synthetic(hy, oracle, types):
 def test_like_dictionary(hy, oracle):
     """LIKE / NOT LIKE over dictionary-encoded string columns (table_scan_string_test.cpp *OnDict* and
     *OnReferencedDict* cases + the special-character patterns), bit-exact against the oracle."""
-    for enc, t in sc.like_tables(hy, encodings=("Dictionary",)):
+    for enc, t in sc.like_tables(hy, encodings=("Dictionary", "FixedStringDictionary")):
         w = wrap(hy, t)
         for cond, pattern, _ in sc.LIKE_CASES:
             check(hy, oracle, w, 1, cond, pattern)

@@ -1,6 +1,6 @@
 """Device TableScans over std::string columns held in HBM (packed string arrays): comparisons, LIKE / NOT LIKE and
-IS [NOT] NULL on unencoded chunks (alone and mixed with dictionary chunks), reference inputs, and string column-vs-
-column comparisons - bit-exact PosLists against the oracle, plus the reference's expected tables of
+IS [NOT] NULL on unencoded, Dictionary, FixedStringDictionary and RunLength chunks (alone and mixed), reference
+inputs, and string column-vs-column comparisons - bit-exact PosLists against the oracle, plus the reference's expected tables of
 table_scan_string_test.cpp."""
 import numpy as np
 import pytest
@@ -13,16 +13,14 @@ pytestmark = pytest.mark.gpu
 
 
 def string_table(hy, encoding):
-    """_gt_string_compressed of table_scan_string_test.cpp:47-57 (chunk 5, string column in `encoding`)."""
-    t = hy.load_table(tbl("int_string_like.tbl"), 5)
-    if encoding:
-        hy.encode_all_chunks(t, getattr(hy.EncodingType, encoding))
-    return wrap(hy, t)
+    """_gt_string_compressed of table_scan_string_test.cpp:46-57 (chunk 5, string column in `encoding`)."""
+    return wrap(hy, sc.string_compressed(hy, encoding))
 
 
-@pytest.mark.parametrize("encoding", [None, "Dictionary"])
+@pytest.mark.parametrize("encoding", sc.STRING_ENCODINGS)
 def test_string_compare_reference_cases(hy, oracle, encoding):
-    """ScanEquals / ScanNotEquals / ScanLessThan (table_scan_string_test.cpp:74-97)."""
+    """ScanEquals / ScanNotEquals / ScanLessThan (table_scan_string_test.cpp:74-97) in the reference's four
+    encodings (:69-72), then every comparison against the oracle."""
     w = string_table(hy, encoding)
     for cond, value, rows, expected in (("Equals", "Reeperbahn", 1, "int_string_like_equals.tbl"),
                                         ("NotEquals", "Reeperbahn", 5, "int_string_like_not_equals.tbl"),
@@ -33,6 +31,62 @@ def test_string_compare_reference_cases(hy, oracle, encoding):
     for cond in CONDS:
         for v in ("", "Dampf", "Reeperbahn", "zzz", "Schifffahrtsgesellschaft"):
             check(hy, oracle, w, 1, cond, v)
+
+
+@pytest.mark.parametrize("encoding", sc.STRING_ENCODINGS)
+def test_like_compressed_reference_cases(hy, oracle, encoding):
+    """The *OnDict* / *OnReferencedDict* LIKE and NOT LIKE TEST_Ps of table_scan_string_test.cpp (:99-187), which the
+    reference runs on _gt_string_compressed in all four encodings: the expected tables, and the oracle's PosLists."""
+    w = string_table(hy, encoding)
+    for cond, pattern, expected in sc.LIKE_CASES:
+        s = check(hy, oracle, w, 1, cond, pattern)
+        s1 = check(hy, oracle, w, 0, "GreaterThan", 0)
+        s2 = check(hy, oracle, s1, 1, cond, pattern)
+        for out in (s.get_output(), s2.get_output()):
+            if isinstance(expected, int):
+                assert out.row_count() == expected
+            else:
+                assert_table_eq_unordered(out, hy.load_table(tbl(expected), 1))
+
+
+@pytest.mark.parametrize("encoding", ["FixedStringDictionary", "RunLength"])
+def test_string_encoded_synthetic(hy, oracle, encoding):
+    """Seeded string columns in FixedStringDictionary / RunLength chunks mixed with unencoded and dictionary chunks:
+    runs of repeated values and NULL runs (RunLength), values of different lengths under one fixed width, ragged chunk
+    tails; every comparison, IS [NOT] NULL, LIKE shapes, then a referencing table across the encodings."""
+    rng = np.random.default_rng(0x46534452)
+    words = random_strings(rng, 300)
+    n, chunk = 40_000, 9_001
+    t = hy.Table([("a", hy.DataType.Int, False), ("s", hy.DataType.String, True)], hy.TableType.Data, chunk)
+    i = 0
+    while i < n:  # runs of 1..40 equal values (NULL runs included)
+        v = None if rng.random() < 0.06 else words[rng.integers(0, len(words))]
+        for _ in range(int(rng.integers(1, 41))):
+            if i < n:
+                t.append([i, v])
+                i += 1
+    hy.encode_chunks(t, [0, 2, 4], getattr(hy.EncodingType, encoding))
+    hy.encode_chunks(t, [1], hy.EncodingType.Dictionary)
+    w = wrap(hy, t)
+    for cond in CONDS:
+        for v in ("abc", "", words[5], "ZZZ", "a", words[11] + "\x00"):
+            check(hy, oracle, w, 1, cond, v)
+    for cond in ("IsNull", "IsNotNull"):
+        check(hy, oracle, w, 1, cond, None)
+    for pattern in ("a%", "%Z", "%bc%", "%a%X%", "a_c%", "_", "%(%", "%", "[ab]%", "%\n%"):
+        for cond in ("Like", "NotLike"):
+            check(hy, oracle, w, 1, cond, pattern)
+    s1 = check(hy, oracle, w, 0, "GreaterThanEquals", 7_000)
+    check(hy, oracle, s1, 1, "Like", "%b%")
+    check(hy, oracle, s1, 1, "LessThan", "X")
+    # valid RowIDs only: chunk 4 holds 40,000 - 4 * 9,001 = 3,996 rows
+    pl = np.stack([rng.integers(0, 5, 20_000), rng.integers(0, 3_996, 20_000)], axis=1).astype(np.uint32)
+    pl[rng.random(20_000) < 0.05] = sc.NULL_ROW_ID
+    ref = hy.Table([("a", hy.DataType.Int, False), ("s", hy.DataType.String, True)], hy.TableType.References)
+    ref.append_chunk([hy.ReferenceColumn(t, 0, pl), hy.ReferenceColumn(t, 1, pl)])
+    wr = wrap(hy, ref)
+    for cond, v in (("Equals", words[7]), ("GreaterThanEquals", "b"), ("Like", "%a%"), ("IsNull", None)):
+        check(hy, oracle, wr, 1, cond, v)
 
 
 def test_like_unencoded(hy, oracle):

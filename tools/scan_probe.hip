@@ -369,6 +369,239 @@ __global__ __launch_bounds__(SCAN_THREADS) void load_count_kernel(const uint8_t*
   }
   if (c == 0xFFFFFFFFu) sink[0] = c;
 }
+// Two-pass form (round 6): seg_count_kernel counts each 4-tile segment's matches (ids read once), scan_write_kernel
+// re-reads the ids and takes its segment's output position from the counts of the <= 6 segments before it in its
+// chunk (no look-back, no ticket: every workgroup stores as soon as its own loads are back).
+__global__ __launch_bounds__(SCAN_THREADS) __attribute__((amdgpu_waves_per_eu(8)))
+void seg_count_kernel(ScanLaunchDesc d, uint32_t* __restrict__ seg_cnt) {
+  __shared__ uint32_t s_scratch[SCAN_THREADS / WAVE + 1];
+  const uint64_t tile = blockIdx.x;
+  const uint32_t c = d.tile_chunk[tile];
+  const hy_scan_chunk ch = d.chunks[c];
+  const uint32_t row0 = static_cast<uint32_t>(tile - d.chunk_tile_begin[c]) * (4 * SCAN_TILE);
+  const uint32_t n = ch.column.size;
+  uint32_t mine = 0;
+  uint8_t v[4][16];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const uint32_t r0 = row0 + t * SCAN_TILE + threadIdx.x * SCAN_ROWS_PER_THREAD;
+    if (r0 < n) load16(reinterpret_cast<const uint8_t*>(ch.column.data), r0, v[t]);
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const uint32_t r0 = row0 + t * SCAN_TILE + threadIdx.x * SCAN_ROWS_PER_THREAD;
+    if (r0 < n) mine += __popc(match_mask<uint8_t, MODE_DICT, uint8_t>(ch, r0, v[t], u32x4{0u, 0u, 0u, 0u}, {}));
+  }
+  uint32_t total;
+  block_exclusive_sum<SCAN_THREADS>(mine, s_scratch, &total);
+  if (threadIdx.x == 0) seg_cnt[tile] = total;
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) __attribute__((amdgpu_waves_per_eu(8)))
+void scan_write_kernel(ScanLaunchDesc d, const uint32_t* __restrict__ seg_cnt, uint64_t* __restrict__ out_any,
+                       uint32_t* __restrict__ counts) {
+  __shared__ uint32_t s_stage[SCAN_TILE];
+  __shared__ uint32_t s_scratch[SCAN_THREADS / WAVE + 1];
+  __shared__ uint32_t s_prefix;
+  const uint64_t tile = blockIdx.x;
+  const uint32_t c = d.tile_chunk[tile];
+  const hy_scan_chunk ch = d.chunks[c];
+  const uint64_t first_tile = d.chunk_tile_begin[c];
+  const uint32_t tile_row0 = static_cast<uint32_t>(tile - first_tile) * (4 * SCAN_TILE);
+  const uint32_t n = ch.column.size;
+  uint32_t masks[4];
+  {
+    uint8_t v[4][16];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const uint32_t r0 = tile_row0 + t * SCAN_TILE + threadIdx.x * SCAN_ROWS_PER_THREAD;
+      if (r0 < n) load16(reinterpret_cast<const uint8_t*>(ch.column.data), r0, v[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const uint32_t r0 = tile_row0 + t * SCAN_TILE + threadIdx.x * SCAN_ROWS_PER_THREAD;
+      masks[t] = r0 < n ? match_mask<uint8_t, MODE_DICT, uint8_t>(ch, r0, v[t], u32x4{0u, 0u, 0u, 0u}, {}) : 0u;
+    }
+  }
+  if (threadIdx.x < WAVE) {
+    const uint64_t before = tile - first_tile;
+    uint32_t p = threadIdx.x < before ? seg_cnt[first_tile + threadIdx.x] : 0u;
+    for (int o = 32; o > 0; o >>= 1) p += __shfl_xor(p, o);
+    if (threadIdx.x == 0) {
+      s_prefix = p;
+      if (tile + 1 == d.chunk_tile_begin[c + 1]) counts[d.chunk_index[c]] = p + seg_cnt[tile];
+    }
+  }
+  __syncthreads();
+  uint64_t run = ch.out_begin + s_prefix;
+  const uint32_t cid = d.chunk_ids[c];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    if (tile_row0 + t * SCAN_TILE >= n) break;
+    const uint32_t r0 = tile_row0 + t * SCAN_TILE + threadIdx.x * SCAN_ROWS_PER_THREAD;
+    uint32_t tile_total;
+    uint32_t pos = block_exclusive_sum<SCAN_THREADS>(__popc(masks[t]), s_scratch, &tile_total);
+    uint32_t m = masks[t];
+    while (m) {
+      const int i = __builtin_ctz(m);
+      m &= m - 1;
+      s_stage[pos++] = r0 + i;
+    }
+    __syncthreads();
+    uint64_t* out64 = out_any + run;
+    const uint32_t lead = (reinterpret_cast<uintptr_t>(out64) & 15u) ? 1u : 0u;
+    if (lead && threadIdx.x == 0 && tile_total)
+      __builtin_nontemporal_store(static_cast<uint64_t>(cid) | (static_cast<uint64_t>(s_stage[0]) << 32), out64);
+    const uint32_t body = tile_total > lead ? tile_total - lead : 0u;
+    u64x2* out128 = reinterpret_cast<u64x2*>(out64 + lead);
+    for (uint32_t p = threadIdx.x; p < body / 2; p += SCAN_THREADS) {
+      const uint32_t i = lead + 2 * p;
+      u64x2 v;
+      v.x = static_cast<uint64_t>(cid) | (static_cast<uint64_t>(s_stage[i]) << 32);
+      v.y = static_cast<uint64_t>(cid) | (static_cast<uint64_t>(s_stage[i + 1]) << 32);
+      __builtin_nontemporal_store(v, out128 + p);
+    }
+    if ((body & 1u) && threadIdx.x == SCAN_THREADS - 1)
+      __builtin_nontemporal_store(static_cast<uint64_t>(cid) | (static_cast<uint64_t>(s_stage[tile_total - 1]) << 32),
+                                  out64 + tile_total - 1);
+    run += tile_total;
+    __syncthreads();
+  }
+}
+// Read ceilings (round 6): 4,201 workgroups read the 60 MB of ids in the product's tile layout (lane l of a tile
+// reads bytes [16 l, 16 l + 16) of each 4096-byte tile) or contiguously, with streaming or plain loads, and count
+// matches; the sink store depends on a runtime key so the loads stay.
+template <int VARIANT>
+__global__ __launch_bounds__(SCAN_THREADS) __attribute__((amdgpu_waves_per_eu(8)))
+void read_probe_kernel(ScanLaunchDesc d, const uint8_t* __restrict__ v, uint64_t n, uint32_t key,
+                       uint32_t* __restrict__ sink) {
+  const uint8_t* base = v;
+  uint64_t seg0 = static_cast<uint64_t>(blockIdx.x) * 16384;
+  if (VARIANT == 4) {  // through the product's descriptor chain
+    const uint32_t c = d.tile_chunk[blockIdx.x];
+    base = static_cast<const uint8_t*>(d.chunks[c].column.data);
+    seg0 = static_cast<uint64_t>(blockIdx.x - d.chunk_tile_begin[c]) * 16384;
+  }
+  uint32_t acc = 0;
+  u32x4 x[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const uint64_t r = VARIANT == 2 ? seg0 + threadIdx.x * 64 + t * 16 : seg0 + t * 4096 + threadIdx.x * 16;
+    const u32x4* p = reinterpret_cast<const u32x4*>(base + r);
+    if (VARIANT == 0) x[t] = __builtin_nontemporal_load(p);
+    else x[t] = *p;
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t w = x[t][i];
+      acc += ((w & 0xFFu) < 23u) + (((w >> 8) & 0xFFu) < 23u) + (((w >> 16) & 0xFFu) < 23u) + ((w >> 24) < 23u);
+      acc ^= w;
+    }
+  if (acc == key) sink[threadIdx.x] = acc;
+}
+// Count-pass variants: VARIANT 1 = product loads + a plain u8 "< search_vid" compare (no match_mask), block sum;
+// VARIANT 2 = as 1 with a wave reduction and one atomicAdd per wave (no barrier); VARIANT 3 = match_mask, wave reduce.
+template <int VARIANT>
+__global__ __launch_bounds__(SCAN_THREADS) __attribute__((amdgpu_waves_per_eu(8)))
+void seg_count_var_kernel(ScanLaunchDesc d, uint32_t* __restrict__ seg_cnt) {
+  __shared__ uint32_t s_scratch[SCAN_THREADS / WAVE + 1];
+  const uint64_t tile = blockIdx.x;
+  const uint32_t c = d.tile_chunk[tile];
+  const hy_scan_chunk ch = d.chunks[c];
+  const uint32_t row0 = static_cast<uint32_t>(tile - d.chunk_tile_begin[c]) * (4 * SCAN_TILE);
+  const uint32_t n = ch.column.size;
+  uint32_t mine = 0;
+  u32x4 x[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const uint32_t r0 = row0 + t * SCAN_TILE + threadIdx.x * SCAN_ROWS_PER_THREAD;
+    x[t] = r0 < n ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(
+                        static_cast<const uint8_t*>(ch.column.data) + r0))
+                  : u32x4{0u, 0u, 0u, 0u};
+  }
+  const uint32_t sv = static_cast<uint32_t>(ch.search_vid);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const uint32_t r0 = row0 + t * SCAN_TILE + threadIdx.x * SCAN_ROWS_PER_THREAD;
+    if (VARIANT == 3) {
+      uint8_t v[16];
+      __builtin_memcpy(v, &x[t], 16);
+      mine += __popc(match_mask<uint8_t, MODE_DICT, uint8_t>(ch, r0, v, u32x4{0u, 0u, 0u, 0u}, {}));
+    } else {
+      const uint32_t valid = r0 >= n ? 0u : (n - r0) >= 16 ? 0xFFFFu : ((1u << (n - r0)) - 1u);
+      uint32_t m = 0;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) m |= static_cast<uint32_t>(((x[t][i >> 2] >> (8 * (i & 3))) & 0xFFu) < sv) << i;
+      mine += __popc(m & valid);
+    }
+  }
+  if (VARIANT == 1) {
+    uint32_t total;
+    block_exclusive_sum<SCAN_THREADS>(mine, s_scratch, &total);
+    if (threadIdx.x == 0) seg_cnt[tile] = total;
+  } else {
+    for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&seg_cnt[tile], mine);
+  }
+}
+// One workgroup per chunk (round 6): 1024 threads walk the chunk in passes of 16384 rows (one 16-byte load per lane,
+// the next pass's load issued before this pass's stores), so a chunk's output position is just the running count -
+// no look-back, no ticket. Offsets are staged as u16 within the pass (32 KB LDS), then stored as 16-byte RowID pairs.
+constexpr int CS_THREADS = 1024;
+constexpr uint32_t CS_PASS = CS_THREADS * 16;
+__global__ __launch_bounds__(CS_THREADS) void chunk_scan_kernel(const hy_scan_chunk* __restrict__ chunks,
+                                                                const uint32_t* __restrict__ chunk_ids,
+                                                                uint64_t* __restrict__ out_any,
+                                                                uint32_t* __restrict__ counts) {
+  __shared__ uint16_t s_stage[CS_PASS];
+  __shared__ uint32_t s_scratch[CS_THREADS / WAVE + 1];
+  const uint32_t c = blockIdx.x;
+  const hy_scan_chunk ch = chunks[c];
+  const uint32_t n = ch.column.size;
+  const uint32_t cid = chunk_ids[c];
+  const uint8_t* data = static_cast<const uint8_t*>(ch.column.data);
+  uint64_t run = ch.out_begin;
+  u32x4 nxt = {0u, 0u, 0u, 0u};
+  if (threadIdx.x * 16 < n) nxt = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(data + threadIdx.x * 16));
+  for (uint32_t p0 = 0; p0 < n; p0 += CS_PASS) {
+    const u32x4 cur = nxt;
+    const uint32_t rn = p0 + CS_PASS + threadIdx.x * 16;
+    if (rn < n) nxt = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(data + rn));
+    const uint32_t r0 = p0 + threadIdx.x * 16;
+    uint8_t v[16];
+    __builtin_memcpy(v, &cur, 16);
+    uint32_t m = match_mask<uint8_t, MODE_DICT, uint8_t>(ch, r0, v, u32x4{0u, 0u, 0u, 0u}, {});
+    uint32_t total;
+    uint32_t pos = block_exclusive_sum<CS_THREADS>(__popc(m), s_scratch, &total);
+    while (m) {
+      const int i = __builtin_ctz(m);
+      m &= m - 1;
+      s_stage[pos++] = static_cast<uint16_t>(threadIdx.x * 16 + i);
+    }
+    __syncthreads();
+    uint64_t* out64 = out_any + run;
+    const uint32_t lead = (reinterpret_cast<uintptr_t>(out64) & 15u) ? 1u : 0u;
+    if (lead && threadIdx.x == 0 && total)
+      __builtin_nontemporal_store(static_cast<uint64_t>(cid) | (static_cast<uint64_t>(p0 + s_stage[0]) << 32), out64);
+    const uint32_t body = total > lead ? total - lead : 0u;
+    u64x2* out128 = reinterpret_cast<u64x2*>(out64 + lead);
+    for (uint32_t q = threadIdx.x; q < body / 2; q += CS_THREADS) {
+      const uint32_t i = lead + 2 * q;
+      u64x2 w;
+      w.x = static_cast<uint64_t>(cid) | (static_cast<uint64_t>(p0 + s_stage[i]) << 32);
+      w.y = static_cast<uint64_t>(cid) | (static_cast<uint64_t>(p0 + s_stage[i + 1]) << 32);
+      __builtin_nontemporal_store(w, out128 + q);
+    }
+    if ((body & 1u) && threadIdx.x == CS_THREADS - 1)
+      __builtin_nontemporal_store(static_cast<uint64_t>(cid) | (static_cast<uint64_t>(p0 + s_stage[total - 1]) << 32),
+                                  out64 + total - 1);
+    run += total;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) counts[c] = static_cast<uint32_t>(run - ch.out_begin);
+}
 }  // namespace hyk
 
 #include <cstdio>
@@ -513,6 +746,106 @@ int main(int argc, char** argv) {
                 v == 0 ? "scan_kernel_seg4" : v == 1 ? "scan_dict8_kernel_g16" : v == 2 ? "scan_packed_kernel_plain_stores" : "scan_seg_stage_kernel", total / 20, (unsigned long long)matches,
                 bytes / (total / 20 * 1e-3) / 1e9, bytes / (total / 20 * 1e-3) / 8e12,
                 int(out == ref && counts == ref_counts), err);
+  }
+  {
+    uint32_t* d_seg;
+    CK(hipMalloc(&d_seg, 4 * run));
+    CK(hipMemset(d_out, 0xFF, 8 * n));
+    hyk::seg_count_kernel<<<run, hyk::SCAN_THREADS>>>(d, d_seg);
+    hyk::scan_write_kernel<<<run, hyk::SCAN_THREADS>>>(d, d_seg, d_out, d_counts);
+    CK(hipDeviceSynchronize());
+    std::vector<uint64_t> out(n);
+    std::vector<uint32_t> counts(nc);
+    CK(hipMemcpy(out.data(), d_out, 8 * n, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(counts.data(), d_counts, 4 * nc, hipMemcpyDeviceToHost));
+    hipEvent_t m;
+    CK(hipEventCreate(&m));
+    float ta = 0, tb = 0;
+    for (int r = 0; r < 20; ++r) {
+      CK(hipEventRecord(a));
+      hyk::seg_count_kernel<<<run, hyk::SCAN_THREADS>>>(d, d_seg);
+      CK(hipEventRecord(m));
+      hyk::scan_write_kernel<<<run, hyk::SCAN_THREADS>>>(d, d_seg, d_out, d_counts);
+      CK(hipEventRecord(b));
+      CK(hipEventSynchronize(b));
+      float x = 0, y = 0;
+      CK(hipEventElapsedTime(&x, a, m));
+      CK(hipEventElapsedTime(&y, m, b));
+      ta += x;
+      tb += y;
+    }
+    std::printf("{\"kernel\": \"two_pass\", \"count_ms\": %.4f, \"write_ms\": %.4f, \"ms\": %.4f, \"equal\": %d}\n",
+                ta / 20, tb / 20, (ta + tb) / 20, int(out == ref && counts == ref_counts));
+  }
+  for (int v = 0; v < 5; ++v) {
+    float total = 0;
+    const uint64_t n_full = (n / 16384) * 16384;  // whole segments only (the probe reads 16384 bytes per workgroup)
+    const uint32_t wgs = static_cast<uint32_t>(n_full / 16384);
+    for (int r = 0; r < 20; ++r) {
+      CK(hipMemset(d_out, 0, 8 * n));  // evict the ids from the Infinity Cache as the pipeline's writes would
+      CK(hipEventRecord(a));
+      if (v == 0) hyk::read_probe_kernel<0><<<wgs, hyk::SCAN_THREADS>>>(d, d_v, n, 0xFFFFFFFFu, d_counts);
+      else if (v == 1) hyk::read_probe_kernel<1><<<wgs, hyk::SCAN_THREADS>>>(d, d_v, n, 0xFFFFFFFFu, d_counts);
+      else if (v == 2) hyk::read_probe_kernel<2><<<wgs, hyk::SCAN_THREADS>>>(d, d_v, n, 0xFFFFFFFFu, d_counts);
+      else if (v == 3) hyk::read_probe_kernel<1><<<wgs, hyk::SCAN_THREADS>>>(d, d_v, n, 0xFFFFFFFFu, d_counts);
+      else hyk::read_probe_kernel<4><<<wgs, hyk::SCAN_THREADS>>>(d, d_v, n, 0xFFFFFFFFu, d_counts);
+      CK(hipEventRecord(b));
+      CK(hipEventSynchronize(b));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, a, b));
+      total += ms;
+    }
+    static const char* names[] = {"read_tile_nt", "read_tile_plain", "read_contig_plain", "read_tile_plain_again",
+                                  "read_tile_plain_descchain"};
+    std::printf("{\"kernel\": \"%s\", \"ms\": %.4f, \"GBps\": %.1f}\n", names[v], total / 20,
+                double(n_full) / (total / 20 * 1e-3) / 1e9);
+  }
+  {
+    uint32_t* d_seg;
+    CK(hipMalloc(&d_seg, 4 * run));
+    for (int v = 1; v <= 3; ++v) {
+      float total = 0;
+      for (int r = 0; r < 20; ++r) {
+        CK(hipMemset(d_out, 0, 8 * n));
+        CK(hipMemset(d_seg, 0, 4 * run));
+        CK(hipEventRecord(a));
+        if (v == 1) hyk::seg_count_var_kernel<1><<<run, hyk::SCAN_THREADS>>>(d, d_seg);
+        else if (v == 2) hyk::seg_count_var_kernel<2><<<run, hyk::SCAN_THREADS>>>(d, d_seg);
+        else hyk::seg_count_var_kernel<3><<<run, hyk::SCAN_THREADS>>>(d, d_seg);
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, a, b));
+        total += ms;
+      }
+      std::vector<uint32_t> seg(run);
+      CK(hipMemcpy(seg.data(), d_seg, 4 * run, hipMemcpyDeviceToHost));
+      uint64_t sum = 0;
+      for (auto x : seg) sum += x;
+      std::printf("{\"kernel\": \"seg_count_var%d\", \"ms\": %.4f, \"matches\": %llu}\n", v, total / 20,
+                  (unsigned long long)sum);
+    }
+  }
+  {
+    CK(hipMemset(d_out, 0xFF, 8 * n));
+    hyk::chunk_scan_kernel<<<nc, hyk::CS_THREADS>>>(d_ch, d_cid, d_out, d_counts);
+    CK(hipDeviceSynchronize());
+    std::vector<uint64_t> out(n);
+    std::vector<uint32_t> counts(nc);
+    CK(hipMemcpy(out.data(), d_out, 8 * n, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(counts.data(), d_counts, 4 * nc, hipMemcpyDeviceToHost));
+    float total = 0;
+    for (int r = 0; r < 20; ++r) {
+      CK(hipEventRecord(a));
+      hyk::chunk_scan_kernel<<<nc, hyk::CS_THREADS>>>(d_ch, d_cid, d_out, d_counts);
+      CK(hipEventRecord(b));
+      CK(hipEventSynchronize(b));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, a, b));
+      total += ms;
+    }
+    std::printf("{\"kernel\": \"chunk_scan_1024\", \"ms\": %.4f, \"equal\": %d}\n", total / 20,
+                int(out == ref && counts == ref_counts));
   }
   for (int v = 4; v < 8; ++v) {
     float total = 0;
