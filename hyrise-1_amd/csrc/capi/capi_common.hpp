@@ -57,37 +57,63 @@ inline bool stream_capturing(hipStream_t s) {
 // per (stream, device) the thread has staged on: stream order makes the latest record cover the earlier copies); when
 // the ring wraps it waits on those events only - the ring's own DMAs - instead of the whole device, so other threads'
 // operator streams are not stalled, and copies staged for another GPU are covered too.
+struct PinnedRing;
+// Every thread's ring, so that hy_stream_destroy can drop the fences of a stream it destroys from all of them (a fence
+// event whose stream is gone is not safe to wait on: the runtime follows the event to its recording stream).
+struct RingRegistry {
+  std::mutex m;
+  std::vector<PinnedRing*> rings;
+};
+inline RingRegistry& ring_registry() {
+  static RingRegistry* r = new RingRegistry;  // (leaked: thread-local rings may outlive static destruction)
+  return *r;
+}
 struct PinnedRing {
   struct Fence {
     hipStream_t stream;
     int device;
     hipEvent_t event;
   };
+  std::mutex m;  // the owner's staging against another thread's forget_stream
   char* buf = nullptr;
   size_t cap = 0, used = 0;
   std::vector<Fence> fences;
+  PinnedRing() {
+    auto& r = ring_registry();
+    std::lock_guard<std::mutex> lock(r.m);
+    r.rings.push_back(this);
+  }
   ~PinnedRing() {
+    {
+      auto& r = ring_registry();
+      std::lock_guard<std::mutex> lock(r.m);
+      r.rings.erase(std::remove(r.rings.begin(), r.rings.end(), this), r.rings.end());
+    }
     for (auto& f : fences) (void)hipEventDestroy(f.event);
     if (buf) (void)hipHostFree(buf);
+  }
+  // (the stream has been synchronised: its fences are complete)
+  void forget_stream(hipStream_t s) {
+    std::lock_guard<std::mutex> lock(m);
+    for (auto& f : fences)
+      if (f.stream == s) (void)hipEventDestroy(f.event);
+    fences.erase(std::remove_if(fences.begin(), fences.end(), [&](const Fence& f) { return f.stream == s; }),
+                 fences.end());
   }
   hy_status wait_all() {
     for (auto& f : fences) {
       const hipError_t e = hipEventSynchronize(f.event);
       if (e == hipSuccess) continue;
       (void)hipGetLastError();
-      // The runtime refuses the wait when it holds the event for one recorded in a stream capture
-      // (hipErrorCapturedEvent). The ring records its fences on non-capturing streams only, so this is the runtime's
-      // view, not a captured copy; the stream itself covers the ring's copies: wait for it, and re-create the event.
+      // a fence the runtime will not wait on (its stream destroyed outside hy_stream_destroy, or in a state the
+      // runtime refuses): the whole device covers the ring's copies; the event is re-created
       if (std::getenv("HY_DEBUG_RING"))
-        std::fprintf(stderr, "hyrise-amd ring: fence on stream %p device %d: %s (stream capturing now: %d)\n",
-                     static_cast<void*>(f.stream), f.device, hipGetErrorString(e), int(stream_capturing(f.stream)));
-      if (stream_capturing(f.stream))
-        return fail(HY_ERR_DEVICE, std::string("pinned staging ring: fence wait on a capturing stream: ") +
-                                       hipGetErrorString(e));
+        std::fprintf(stderr, "hyrise-amd ring: fence on stream %p device %d: %s\n", static_cast<void*>(f.stream),
+                     f.device, hipGetErrorString(e));
       int cur = 0;
       HY_HIP(hipGetDevice(&cur));
       HY_HIP(hipSetDevice(f.device));
-      const hipError_t w = hipStreamSynchronize(f.stream);
+      const hipError_t w = hipDeviceSynchronize();
       (void)hipEventDestroy(f.event);
       f.event = nullptr;
       const hipError_t c = hipEventCreateWithFlags(&f.event, hipEventDisableTiming);
@@ -103,8 +129,6 @@ struct PinnedRing {
     for (auto& f : fences)
       if (f.stream == s && f.device == dev) {
         HY_HIP(hipEventRecord(f.event, s));
-        if (std::getenv("HY_DEBUG_RING") && stream_capturing(s))
-          std::fprintf(stderr, "hyrise-amd ring: fence recorded on capturing stream %p\n", static_cast<void*>(s));
         return HY_OK;
       }
     if (fences.size() >= 32) {  // many short-lived streams: retire the fences (their copies are waited for first)
@@ -120,6 +144,12 @@ struct PinnedRing {
     return HY_OK;
   }
 };
+// hy_stream_destroy: no ring keeps a fence on the stream afterwards
+inline void ring_forget_stream(hipStream_t s) {
+  auto& r = ring_registry();
+  std::lock_guard<std::mutex> lock(r.m);
+  for (PinnedRing* ring : r.rings) ring->forget_stream(s);
+}
 // A stream being captured into a graph is refused: the copy would become a graph node reading a ring slot that later
 // staging reuses (or frees), so every replay would upload whatever the slot then holds. Captured regions (a prepared
 // plan's execution, hyrise_amd_join.hip) stage nothing; their descriptors are in the plan's workspace beforehand.
@@ -132,6 +162,7 @@ inline hy_status staged_htod(void* dst, const void* src, size_t bytes, hipStream
     return fail(HY_ERR_INVALID_ARGUMENT, "host-staged copy on a stream being captured into a graph");
   }
   thread_local PinnedRing ring;
+  std::lock_guard<std::mutex> ring_lock(ring.m);
   const size_t need = (bytes + 255) & ~size_t(255);
   if (ring.used + need > ring.cap) {
     const hy_status w = ring.wait_all();  // every copy out of the ring has completed

@@ -158,6 +158,9 @@ hy_status hy_stream_create(hy_stream_t* stream) {
 }
 
 hy_status hy_stream_destroy(hy_stream_t stream) {
+  // the staging rings' fences on this stream are complete once it is; they are dropped before the handle dies
+  HY_HIP(hipStreamSynchronize(S(stream)));
+  ring_forget_stream(S(stream));
   HY_HIP(hipStreamDestroy(S(stream)));
   return HY_OK;
 }

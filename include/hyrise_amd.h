@@ -70,6 +70,9 @@ hy_status hy_memcpy_dtoh(void* dst, const void* src, size_t bytes, hy_stream_t s
 hy_status hy_memcpy_dtod(void* dst, const void* src, size_t bytes, hy_stream_t stream);
 hy_status hy_memset(void* dst, int value, size_t bytes, hy_stream_t stream);
 hy_status hy_stream_create(hy_stream_t* stream);
+/* Waits for the stream's work, then destroys it. Streams handed to the entry points (which stage their host
+ * descriptors through a per-thread pinned ring fenced by events on the caller's stream) are destroyed with this
+ * function, which also drops those fences; an embedding that destroys such a stream itself first synchronises it. */
 hy_status hy_stream_destroy(hy_stream_t stream);
 hy_status hy_stream_synchronize(hy_stream_t stream);
 /*
