@@ -208,6 +208,7 @@ struct KernelTiming {
   std::string name;
   hipEvent_t start, stop;
   uint64_t units;
+  hipStream_t stream;  // (hy_stream_destroy resolves the stream's pending timings before the handle dies)
 };
 struct KStat {
   uint64_t count = 0;
@@ -250,6 +251,7 @@ struct KTimer {
     on = true;
     kt.name = name;
     kt.units = units;
+    kt.stream = stream;
     kt.start = kt_event();
     kt.stop = kt_event();
     (void)hipEventRecord(kt.start, s);

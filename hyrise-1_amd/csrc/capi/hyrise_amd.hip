@@ -157,10 +157,43 @@ hy_status hy_stream_create(hy_stream_t* stream) {
   return HY_OK;
 }
 
+namespace {
+// one pending kernel timing into the stats (g_kt_mutex held; its stop event has completed or is waited for)
+hy_status kt_resolve_locked(const KernelTiming& k) {
+  HY_HIP(hipEventSynchronize(k.stop));
+  float ms = 0;
+  HY_HIP(hipEventElapsedTime(&ms, k.start, k.stop));
+  auto it = std::find_if(g_kt_stats.begin(), g_kt_stats.end(), [&](const auto& e) { return e.first == k.name; });
+  if (it == g_kt_stats.end()) {
+    g_kt_stats.emplace_back(k.name, KStat{});
+    it = g_kt_stats.end() - 1;
+  }
+  it->second.count += 1;
+  it->second.total_ms += ms;
+  it->second.units += k.units;
+  g_kt_pool.push_back(k.start);
+  g_kt_pool.push_back(k.stop);
+  return HY_OK;
+}
+}  // namespace
+
 hy_status hy_stream_destroy(hy_stream_t stream) {
-  // the staging rings' fences on this stream are complete once it is; they are dropped before the handle dies
+  // Every event this library recorded on the stream is finished with before the handle dies: the runtime follows an
+  // event to the stream it was last recorded on when the event is waited for, and a destroyed stream there is a read
+  // - and, when the freed memory happens to look like an active capture, a write - of freed runtime memory
+  // (the staging rings' fences and the pending kernel timings).
   HY_HIP(hipStreamSynchronize(S(stream)));
   ring_forget_stream(S(stream));
+  {
+    std::lock_guard<std::mutex> lock(g_kt_mutex);
+    hy_status st = HY_OK;
+    for (const auto& k : g_kt_pending)
+      if (k.stream == S(stream) && st == HY_OK) st = kt_resolve_locked(k);
+    g_kt_pending.erase(std::remove_if(g_kt_pending.begin(), g_kt_pending.end(),
+                                      [&](const KernelTiming& k) { return k.stream == S(stream); }),
+                       g_kt_pending.end());
+    if (st != HY_OK) return st;
+  }
   HY_HIP(hipStreamDestroy(S(stream)));
   return HY_OK;
 }
@@ -199,19 +232,8 @@ hy_status hy_kernel_stats_reset(void) {
 hy_status hy_kernel_stats_collect(uint32_t* n_kernels) {
   std::lock_guard<std::mutex> lock(g_kt_mutex);
   for (auto& k : g_kt_pending) {
-    HY_HIP(hipEventSynchronize(k.stop));
-    float ms = 0;
-    HY_HIP(hipEventElapsedTime(&ms, k.start, k.stop));
-    auto it = std::find_if(g_kt_stats.begin(), g_kt_stats.end(), [&](const auto& e) { return e.first == k.name; });
-    if (it == g_kt_stats.end()) {
-      g_kt_stats.emplace_back(k.name, KStat{});
-      it = g_kt_stats.end() - 1;
-    }
-    it->second.count += 1;
-    it->second.total_ms += ms;
-    it->second.units += k.units;
-    g_kt_pool.push_back(k.start);
-    g_kt_pool.push_back(k.stop);
+    const hy_status st = kt_resolve_locked(k);
+    if (st != HY_OK) return st;
   }
   g_kt_pending.clear();
   if (n_kernels) *n_kernels = static_cast<uint32_t>(g_kt_stats.size());
@@ -288,27 +310,43 @@ int class_seg(int cls, int32_t value_type) {
   }
 }
 
+// HY_SCAN_TWO_PASS=0: the one-pass look-back kernel for every chunk (A/B); otherwise chunks of at most
+// hyk::SCAN_TWO_PASS_SEGS segments (6.5 M rows at 1-byte ids) take the count + write kernels
+bool scan_two_pass_enabled() {
+  const char* e = std::getenv("HY_SCAN_TWO_PASS");  // (read per call: tests switch it)
+  return !(e && std::atoi(e) == 0);
+}
+
+template <typename E, int MODE, bool OUT_ROWID, typename V, int SEG>
+void launch_scan_seg(const hyk::ScanLaunchDesc& d, const hyk::ScanConst<V>& c, void* out, uint32_t* counts,
+                     bool two_pass, hipStream_t s) {
+  const dim3 grid(static_cast<uint32_t>(d.n_tiles)), block(hyk::SCAN_THREADS);
+  if (two_pass) {
+    hipLaunchKernelGGL((hyk::scan_count_kernel<E, MODE, V, SEG>), grid, block, 0, s, d, c);
+    hipLaunchKernelGGL((hyk::scan_write_kernel<OUT_ROWID, SEG>), grid, block, 0, s, d, out, counts);
+  } else {
+    hipLaunchKernelGGL((hyk::scan_kernel<E, MODE, OUT_ROWID, V, SEG>), grid, block, 0, s, d, c, out, counts);
+  }
+}
+
+// two_pass: every chunk of the class has at most hyk::SCAN_TWO_PASS_SEGS segments
 template <typename E, int MODE, bool OUT_ROWID, typename V = E>
-hy_status launch_scan(const hyk::ScanLaunchDesc& d, const void* constant, void* out, uint32_t* counts,
+hy_status launch_scan(const hyk::ScanLaunchDesc& d, const void* constant, void* out, uint32_t* counts, bool two_pass,
                       hipStream_t s) {
   hyk::ScanConst<V> c{};
   if (MODE != hyk::MODE_DICT && constant) std::memcpy(&c.value, constant, sizeof(V));
+  // (the two kernels of a two-pass scan are timed as one: the scan's time)
   KTimer t(MODE == hyk::MODE_DICT ? "scan_dict" : MODE == hyk::MODE_FOR ? "scan_frame_of_reference" : "scan_value", s,
            d.n_rows);
-  const dim3 grid(static_cast<uint32_t>(d.n_tiles));
   if constexpr (sizeof(E) == 1) {
     if (seg8() == 2)
-      hipLaunchKernelGGL((hyk::scan_kernel<E, MODE, OUT_ROWID, V, 2>), grid, dim3(hyk::SCAN_THREADS), 0, s, d, c, out,
-                         counts);
+      launch_scan_seg<E, MODE, OUT_ROWID, V, 2>(d, c, out, counts, two_pass, s);
     else if (seg8() == 8)
-      hipLaunchKernelGGL((hyk::scan_kernel<E, MODE, OUT_ROWID, V, 8>), grid, dim3(hyk::SCAN_THREADS), 0, s, d, c, out,
-                         counts);
+      launch_scan_seg<E, MODE, OUT_ROWID, V, 8>(d, c, out, counts, two_pass, s);
     else
-      hipLaunchKernelGGL((hyk::scan_kernel<E, MODE, OUT_ROWID, V, 4>), grid, dim3(hyk::SCAN_THREADS), 0, s, d, c, out,
-                         counts);
+      launch_scan_seg<E, MODE, OUT_ROWID, V, 4>(d, c, out, counts, two_pass, s);
   } else {
-    hipLaunchKernelGGL((hyk::scan_kernel<E, MODE, OUT_ROWID, V>), grid, dim3(hyk::SCAN_THREADS), 0, s, d, c, out,
-                       counts);
+    launch_scan_seg<E, MODE, OUT_ROWID, V, hyk::seg_tiles<E>()>(d, c, out, counts, two_pass, s);
   }
   t.done();
   HY_HIP(hipGetLastError());
@@ -317,10 +355,10 @@ hy_status launch_scan(const hyk::ScanLaunchDesc& d, const void* constant, void* 
 
 template <typename E, bool OUT_ROWID>
 hy_status launch_for(const hyk::ScanLaunchDesc& d, int32_t value_type, const void* constant, void* out,
-                     uint32_t* counts, hipStream_t s) {
+                     uint32_t* counts, bool two_pass, hipStream_t s) {
   if (value_type == HY_TYPE_INT32)
-    return launch_scan<E, hyk::MODE_FOR, OUT_ROWID, int32_t>(d, constant, out, counts, s);
-  return launch_scan<E, hyk::MODE_FOR, OUT_ROWID, int64_t>(d, constant, out, counts, s);
+    return launch_scan<E, hyk::MODE_FOR, OUT_ROWID, int32_t>(d, constant, out, counts, two_pass, s);
+  return launch_scan<E, hyk::MODE_FOR, OUT_ROWID, int64_t>(d, constant, out, counts, two_pass, s);
 }
 
 // RunLength chunks of one call (hyk::rle_* kernels): per-run predicate, prefix over the matching runs' lengths, then
@@ -394,6 +432,9 @@ size_t scan_class_bytes(uint32_t n_chunks, uint64_t n_tiles) {
   cv.take<uint64_t>(n_tiles + 1);
   cv.take<uint32_t>(n_tiles + 1);
   cv.take<uint32_t>(64);
+  // two-pass masks: per lane one 32-bit word per two tiles of a segment - at most one per tile, plus up to 4 for a
+  // chunk's last, partial segment
+  cv.take<uint32_t>((n_tiles + 4ull * n_chunks) * hyk::SCAN_THREADS);
   return cv.used + 256;
 }
 
@@ -460,7 +501,7 @@ hy_status table_scan_impl(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_
     auto& ht = h_tiles[cls];
     hc.resize(nc);
     ht.resize(nc + 1);
-    uint64_t run = 0, rows = 0;
+    uint64_t run = 0, rows = 0, max_segs = 0;
     for (uint32_t k = 0; k < nc; ++k) {
       hc[k] = chunks[idx[k]];
       rows += hc[k].column.size;
@@ -470,8 +511,10 @@ hy_status table_scan_impl(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_
         run += hc[k].column.size ? hc[k].column.dictionary_size : 0;
       else
         run += hc[k].op == HY_OP_NONE ? 0 : (scan_tiles(hc[k].column.size) + seg - 1) / seg;  // segments
+      max_segs = std::max(max_segs, run - ht[k]);
     }
     ht[nc] = run;
+    const bool two_pass = scan_two_pass_enabled() && max_segs <= hyk::SCAN_TWO_PASS_SEGS;
     hyk::ScanLaunchDesc d{};
     // descriptors, segment prefix, chunk indexes, chunk ids and segment owners carved back to back and uploaded as ONE
     // staged copy; then the look-back words and the ticket / error words cleared by one memset
@@ -483,6 +526,10 @@ hy_status table_scan_impl(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_
     auto* downer = cv.take<uint32_t>(words + 1);
     auto* dst = cv.take<uint64_t>(words + 1);
     auto* dmisc = cv.take<uint32_t>(64);
+    // the two-pass masks: mask_words(seg) 32-bit words per lane and segment (seg tiles of 4096 rows: <= one per tile)
+    const uint64_t seg_of_class = cls == SC_RLE ? 0 : static_cast<uint64_t>(class_seg(cls, value_type));
+    auto* dmasks = two_pass ? cv.take<uint32_t>(words * hyk::mask_words(static_cast<int>(seg_of_class)) * hyk::SCAN_THREADS)
+                            : nullptr;
     if (!cv.ok) return fail(HY_ERR_WORKSPACE, "scan workspace too small");
     if (!error) error = dmisc + 1;  // (cleared by this class's memset below)
     auto& hcid = h_cids[cls];
@@ -527,40 +574,41 @@ hy_status table_scan_impl(const hy_scan_chunk* chunks, uint32_t n_chunks, int32_
     d.status = dst;
     d.ticket = dmisc;
     d.error = error;
+    d.masks = dmasks;
     hy_status st = HY_OK;
     constexpr int DICT = hyk::MODE_DICT, VALUE = hyk::MODE_VALUE;
     switch (cls) {
       case SC_DICT8:
-        st = launch_scan<uint8_t, DICT, OUT_ROWID>(d, nullptr, out_offsets, counts, s);
+        st = launch_scan<uint8_t, DICT, OUT_ROWID>(d, nullptr, out_offsets, counts, two_pass, s);
         break;
       case SC_DICT16:
-        st = launch_scan<uint16_t, DICT, OUT_ROWID>(d, nullptr, out_offsets, counts, s);
+        st = launch_scan<uint16_t, DICT, OUT_ROWID>(d, nullptr, out_offsets, counts, two_pass, s);
         break;
       case SC_DICT32:
-        st = launch_scan<uint32_t, DICT, OUT_ROWID>(d, nullptr, out_offsets, counts, s);
+        st = launch_scan<uint32_t, DICT, OUT_ROWID>(d, nullptr, out_offsets, counts, two_pass, s);
         break;
       case SC_FOR8:
-        st = launch_for<uint8_t, OUT_ROWID>(d, value_type, constant, out_offsets, counts, s);
+        st = launch_for<uint8_t, OUT_ROWID>(d, value_type, constant, out_offsets, counts, two_pass, s);
         break;
       case SC_FOR16:
-        st = launch_for<uint16_t, OUT_ROWID>(d, value_type, constant, out_offsets, counts, s);
+        st = launch_for<uint16_t, OUT_ROWID>(d, value_type, constant, out_offsets, counts, two_pass, s);
         break;
       case SC_FOR32:
-        st = launch_for<uint32_t, OUT_ROWID>(d, value_type, constant, out_offsets, counts, s);
+        st = launch_for<uint32_t, OUT_ROWID>(d, value_type, constant, out_offsets, counts, two_pass, s);
         break;
       case SC_VALUE:
         switch (value_type) {
           case HY_TYPE_INT32:
-            st = launch_scan<int32_t, VALUE, OUT_ROWID>(d, constant, out_offsets, counts, s);
+            st = launch_scan<int32_t, VALUE, OUT_ROWID>(d, constant, out_offsets, counts, two_pass, s);
             break;
           case HY_TYPE_INT64:
-            st = launch_scan<int64_t, VALUE, OUT_ROWID>(d, constant, out_offsets, counts, s);
+            st = launch_scan<int64_t, VALUE, OUT_ROWID>(d, constant, out_offsets, counts, two_pass, s);
             break;
           case HY_TYPE_FLOAT:
-            st = launch_scan<float, VALUE, OUT_ROWID>(d, constant, out_offsets, counts, s);
+            st = launch_scan<float, VALUE, OUT_ROWID>(d, constant, out_offsets, counts, two_pass, s);
             break;
           case HY_TYPE_DOUBLE:
-            st = launch_scan<double, VALUE, OUT_ROWID>(d, constant, out_offsets, counts, s);
+            st = launch_scan<double, VALUE, OUT_ROWID>(d, constant, out_offsets, counts, two_pass, s);
             break;
         }
         break;

@@ -83,9 +83,12 @@ struct DeviceSpan {
   DeviceSpan() {
     int n = 0;
     if (hy_get_device_count(&n) != HY_OK || n <= 0) return;  // (no device: the operator fails on its own)
+    // the thread's operator stream first: thread-local objects are destroyed in the reverse order of their first use,
+    // so the events go before the stream they are recorded on (hy_stream_destroy)
+    hy_stream_t s = operator_stream();
     thread_local Events events;
     if (!events.start && (hy_event_create(&events.start) != HY_OK || hy_event_create(&events.stop) != HY_OK)) return;
-    if (hy_event_record(events.start, operator_stream()) == HY_OK) ev = &events;
+    if (hy_event_record(events.start, s) == HY_OK) ev = &events;
   }
   uint64_t finish() {
     uint64_t ns = 0;

@@ -43,7 +43,11 @@ struct ScanLaunchDesc {
   uint64_t* status;                  // n_tiles look-back words (zeroed)
   uint32_t* ticket;                  // zeroed
   uint32_t* error;                   // zeroed before the first launch of a call
+  uint32_t* masks;                   // two-pass scans: the count pass's match masks, mask_words(SEG) x 256 per segment
 };
+
+// 32-bit words a lane's SEG 16-bit tile masks take (two tiles per word)
+__host__ __device__ constexpr int mask_words(int seg) { return (seg + 1) / 2; }
 
 template <typename T>
 struct ScanConst {
@@ -130,80 +134,35 @@ __device__ __forceinline__ uint32_t match_mask(const hy_scan_chunk& ch, uint32_t
 // offsets (4 B).
 // SEG: tiles per workgroup (seg_tiles<E>; the host may pick fewer for 1-byte elements: more, shorter workgroups).
 // 1-byte ids with at most 4 tiles per workgroup run at 8 waves per SIMD (<= 64 VGPRs: 76 otherwise, 6 waves).
-template <typename E, int MODE, bool OUT_ROWID, typename V = E, int SEG = seg_tiles<E>()>
-__global__ __launch_bounds__(SCAN_THREADS) __attribute__((amdgpu_waves_per_eu(sizeof(E) == 1 && SEG <= 4 ? 8 : 1)))
-void scan_kernel(ScanLaunchDesc d, ScanConst<V> constant,
-                                                           void* __restrict__ out_any,
-                                                           uint32_t* __restrict__ counts) {
-  __shared__ uint32_t s_stage[SCAN_TILE];
-  __shared__ uint32_t s_scratch[SCAN_THREADS / WAVE + 1];
-  __shared__ uint64_t s_tile;
-  __shared__ uint32_t s_chunk;
-  __shared__ uint64_t s_prefix;
 
-  if (threadIdx.x == 0) {
-    const uint64_t tile = atomicAdd(d.ticket, 1u);
-    s_tile = tile;
-    s_chunk = tile < d.n_tiles ? d.tile_chunk[tile] : 0u;
-  }
-  __syncthreads();
-  const uint64_t tile = s_tile;
-  if (tile >= d.n_tiles) return;
-  const uint32_t c = s_chunk;
-  const hy_scan_chunk ch = d.chunks[c];
-  const uint64_t first_tile = d.chunk_tile_begin[c];
-  // (for this kernel d.chunk_tile_begin / d.tile_chunk / d.n_tiles / d.status count segments of SEG tiles)
-  const uint32_t tile_in_chunk = static_cast<uint32_t>(tile - first_tile);
-  const uint32_t tile_row0 = tile_in_chunk * (SEG * SCAN_TILE);
+// The per-lane 16-bit match masks of one segment (SEG consecutive tiles from tile_row0 of chunk ch): all SEG loads
+// per lane issued up front, then the compares.
+template <typename E, int MODE, typename V, int SEG>
+__device__ __forceinline__ void segment_masks(const hy_scan_chunk& ch, uint32_t tile_row0, const ScanConst<V>& constant,
+                                              uint32_t (&masks)[SEG]) {
   const uint32_t n = ch.column.size;
-
-  // One workgroup = one segment of SEG consecutive tiles of this chunk: all SEG loads per lane are issued up front,
-  // the per-lane 16-bit match masks stay in registers, the segment's count is chained to its predecessors by one
-  // decoupled look-back, and the tiles' offsets are then compacted tile by tile through LDS into coalesced stores.
-  uint32_t masks[SEG];
-  {
-    E v[SEG][16];
-    u32x4 nl[SEG];
+  E v[SEG][16];
+  u32x4 nl[SEG];
 #pragma unroll
-    for (int t = 0; t < SEG; ++t) {
-      const uint32_t r0 = tile_row0 + t * SCAN_TILE + threadIdx.x * SCAN_ROWS_PER_THREAD;
-      nl[t] = u32x4{0u, 0u, 0u, 0u};
-      if (r0 < n && ch.op != HY_OP_NONE) {
-        load16(reinterpret_cast<const E*>(ch.column.data), r0, v[t]);
-        if (MODE != MODE_DICT && ch.column.nulls != nullptr)
-          nl[t] = *reinterpret_cast<const u32x4*>(ch.column.nulls + r0);
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < SEG; ++t)
-      masks[t] = match_mask<E, MODE, V>(ch, tile_row0 + t * SCAN_TILE + threadIdx.x * SCAN_ROWS_PER_THREAD, v[t],
-                                        nl[t], constant);
-  }
-  uint32_t mine = 0;
-#pragma unroll
-  for (int t = 0; t < SEG; ++t) mine += __popc(masks[t]);
-  uint32_t seg_total;
-  block_exclusive_sum<SCAN_THREADS>(mine, s_scratch, &seg_total);
-
-  // Decoupled look-back across the segments of this chunk (wave 0, 64 predecessors per poll).
-  if (threadIdx.x < WAVE) {
-    uint64_t prefix = 0;
-    if (tile == first_tile) {
-      if (threadIdx.x == 0) lb_publish(&d.status[tile], LB_FLAG_PREFIX, seg_total);
-    } else {
-      if (threadIdx.x == 0) lb_publish(&d.status[tile], LB_FLAG_AGG, seg_total);
-      prefix = lb_lookback_wave(d.status, first_tile, tile, d.error);
-      if (threadIdx.x == 0) lb_publish(&d.status[tile], LB_FLAG_PREFIX, prefix + seg_total);
-    }
-    if (threadIdx.x == 0) {
-      s_prefix = prefix;
-      const uint64_t last_tile = d.chunk_tile_begin[c + 1] - 1;
-      if (tile == last_tile) counts[d.chunk_index[c]] = static_cast<uint32_t>(prefix + seg_total);
+  for (int t = 0; t < SEG; ++t) {
+    const uint32_t r0 = tile_row0 + t * SCAN_TILE + threadIdx.x * SCAN_ROWS_PER_THREAD;
+    nl[t] = u32x4{0u, 0u, 0u, 0u};
+    if (r0 < n && ch.op != HY_OP_NONE) {
+      load16(reinterpret_cast<const E*>(ch.column.data), r0, v[t]);
+      if (MODE != MODE_DICT && ch.column.nulls != nullptr) nl[t] = *reinterpret_cast<const u32x4*>(ch.column.nulls + r0);
     }
   }
-  __syncthreads();
-  uint64_t run = ch.out_begin + s_prefix;
-  const uint32_t cid = OUT_ROWID ? d.chunk_ids[c] : 0u;
+#pragma unroll
+  for (int t = 0; t < SEG; ++t)
+    masks[t] = match_mask<E, MODE, V>(ch, tile_row0 + t * SCAN_TILE + threadIdx.x * SCAN_ROWS_PER_THREAD, v[t], nl[t],
+                                      constant);
+}
+
+// A segment's matches, tile by tile, compacted through LDS into coalesced stores from output position `run` on.
+template <bool OUT_ROWID, int SEG>
+__device__ __forceinline__ void segment_store(const uint32_t (&masks)[SEG], uint32_t tile_row0, uint32_t n, uint64_t run,
+                                              uint32_t cid, void* __restrict__ out_any, uint32_t* s_stage,
+                                              uint32_t* s_scratch) {
 #pragma unroll
   for (int t = 0; t < SEG; ++t) {
     if (tile_row0 + t * SCAN_TILE >= n) break;  // uniform
@@ -246,6 +205,139 @@ void scan_kernel(ScanLaunchDesc d, ScanConst<V> constant,
     run += tile_total;
     __syncthreads();  // s_stage is refilled by the next tile
   }
+}
+
+// One pass: a segment's count is chained to its predecessors in the chunk by a decoupled look-back. For chunks of any
+// number of segments (the two-pass kernels below take chunks of at most SCAN_TWO_PASS_SEGS segments).
+template <typename E, int MODE, bool OUT_ROWID, typename V = E, int SEG = seg_tiles<E>()>
+__global__ __launch_bounds__(SCAN_THREADS) __attribute__((amdgpu_waves_per_eu(sizeof(E) == 1 && SEG <= 4 ? 8 : 1)))
+void scan_kernel(ScanLaunchDesc d, ScanConst<V> constant, void* __restrict__ out_any, uint32_t* __restrict__ counts) {
+  __shared__ uint32_t s_stage[SCAN_TILE];
+  __shared__ uint32_t s_scratch[SCAN_THREADS / WAVE + 1];
+  __shared__ uint64_t s_tile;
+  __shared__ uint32_t s_chunk;
+  __shared__ uint64_t s_prefix;
+
+  if (threadIdx.x == 0) {
+    const uint64_t tile = atomicAdd(d.ticket, 1u);
+    s_tile = tile;
+    s_chunk = tile < d.n_tiles ? d.tile_chunk[tile] : 0u;
+  }
+  __syncthreads();
+  const uint64_t tile = s_tile;
+  if (tile >= d.n_tiles) return;
+  const uint32_t c = s_chunk;
+  const hy_scan_chunk ch = d.chunks[c];
+  const uint64_t first_tile = d.chunk_tile_begin[c];
+  // (for this kernel d.chunk_tile_begin / d.tile_chunk / d.n_tiles / d.status count segments of SEG tiles)
+  const uint32_t tile_row0 = static_cast<uint32_t>(tile - first_tile) * (SEG * SCAN_TILE);
+
+  // One workgroup = one segment of SEG consecutive tiles of this chunk: the per-lane 16-bit match masks stay in
+  // registers, the segment's count is chained to its predecessors by one decoupled look-back, and the tiles' offsets
+  // are then compacted tile by tile through LDS into coalesced stores.
+  uint32_t masks[SEG];
+  segment_masks<E, MODE, V, SEG>(ch, tile_row0, constant, masks);
+  uint32_t mine = 0;
+#pragma unroll
+  for (int t = 0; t < SEG; ++t) mine += __popc(masks[t]);
+  uint32_t seg_total;
+  block_exclusive_sum<SCAN_THREADS>(mine, s_scratch, &seg_total);
+
+  // Decoupled look-back across the segments of this chunk (wave 0, 64 predecessors per poll).
+  if (threadIdx.x < WAVE) {
+    uint64_t prefix = 0;
+    if (tile == first_tile) {
+      if (threadIdx.x == 0) lb_publish(&d.status[tile], LB_FLAG_PREFIX, seg_total);
+    } else {
+      if (threadIdx.x == 0) lb_publish(&d.status[tile], LB_FLAG_AGG, seg_total);
+      prefix = lb_lookback_wave(d.status, first_tile, tile, d.error);
+      if (threadIdx.x == 0) lb_publish(&d.status[tile], LB_FLAG_PREFIX, prefix + seg_total);
+    }
+    if (threadIdx.x == 0) {
+      s_prefix = prefix;
+      const uint64_t last_tile = d.chunk_tile_begin[c + 1] - 1;
+      if (tile == last_tile) counts[d.chunk_index[c]] = static_cast<uint32_t>(prefix + seg_total);
+    }
+  }
+  __syncthreads();
+  segment_store<OUT_ROWID, SEG>(masks, tile_row0, ch.column.size, ch.out_begin + s_prefix,
+                                OUT_ROWID ? d.chunk_ids[c] : 0u, out_any, s_stage, s_scratch);
+}
+
+// Two passes (round 6): scan_count_kernel evaluates the predicate over every segment, writes the lanes' match masks
+// (2 bytes per 16 rows: 1/8 of the u8 ids) and the segment's count (d.status, one 32-bit count per segment);
+// scan_write_kernel then reads only the masks - not the column - takes its output position from the counts of the
+// segments before it in its chunk (at most SCAN_TWO_PASS_SEGS - 1, summed by one wave) and stores the RowIDs. No ticket,
+// no look-back: every workgroup stores as soon as its masks are back. The look-back's chain of cross-XCD flag
+// hand-offs cost more than the second pass (config 2: one pass 0.101 ms; count 0.016 + write 0.064 ms re-reading the
+// ids, tools/scan_probe.hip and profiles/r06_scan_*).
+constexpr uint32_t SCAN_TWO_PASS_SEGS = 64;
+
+template <typename E, int MODE, typename V = E, int SEG = seg_tiles<E>()>
+__global__ __launch_bounds__(SCAN_THREADS) __attribute__((amdgpu_waves_per_eu(sizeof(E) == 1 && SEG <= 4 ? 8 : 1)))
+void scan_count_kernel(ScanLaunchDesc d, ScanConst<V> constant) {
+  __shared__ uint32_t s_scratch[SCAN_THREADS / WAVE + 1];
+  const uint64_t tile = blockIdx.x;
+  const uint32_t c = d.tile_chunk[tile];
+  const hy_scan_chunk ch = d.chunks[c];
+  const uint32_t tile_row0 = static_cast<uint32_t>(tile - d.chunk_tile_begin[c]) * (SEG * SCAN_TILE);
+  uint32_t masks[SEG];
+  segment_masks<E, MODE, V, SEG>(ch, tile_row0, constant, masks);
+  uint32_t mine = 0;
+#pragma unroll
+  for (int t = 0; t < SEG; ++t) mine += __popc(masks[t]);
+  constexpr int MW = mask_words(SEG);
+  uint32_t* mw = d.masks + tile * (MW * SCAN_THREADS) + threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < MW; ++k)
+    __builtin_nontemporal_store(masks[2 * k] | (2 * k + 1 < SEG ? masks[2 * k + 1] << 16 : 0u), mw + k * SCAN_THREADS);
+  // one wave sum per wave, one LDS word each, one store
+  mine = wave_inclusive_sum(mine);
+  if (__lane_id() == WAVE - 1) s_scratch[threadIdx.x / WAVE] = mine;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t total = 0;
+#pragma unroll
+    for (int w = 0; w < SCAN_THREADS / WAVE; ++w) total += s_scratch[w];
+    reinterpret_cast<uint32_t*>(d.status)[tile] = total;
+  }
+}
+
+template <bool OUT_ROWID, int SEG>
+__global__ __launch_bounds__(SCAN_THREADS) __attribute__((amdgpu_waves_per_eu(SEG <= 4 ? 8 : 1)))
+void scan_write_kernel(ScanLaunchDesc d, void* __restrict__ out_any, uint32_t* __restrict__ counts) {
+  __shared__ uint32_t s_stage[SCAN_TILE];
+  __shared__ uint32_t s_scratch[SCAN_THREADS / WAVE + 1];
+  __shared__ uint32_t s_prefix;
+  const uint64_t tile = blockIdx.x;
+  const uint32_t c = d.tile_chunk[tile];
+  const uint64_t first_tile = d.chunk_tile_begin[c];
+  const uint32_t tile_row0 = static_cast<uint32_t>(tile - first_tile) * (SEG * SCAN_TILE);
+  constexpr int MW = mask_words(SEG);
+  uint32_t masks[SEG];
+  {
+    const uint32_t* mw = d.masks + tile * (MW * SCAN_THREADS) + threadIdx.x;
+    uint32_t w[MW];
+#pragma unroll
+    for (int k = 0; k < MW; ++k) w[k] = __builtin_nontemporal_load(mw + k * SCAN_THREADS);
+#pragma unroll
+    for (int t = 0; t < SEG; ++t) masks[t] = (w[t / 2] >> (16 * (t & 1))) & 0xFFFFu;
+  }
+  if (threadIdx.x < WAVE) {
+    const uint32_t* seg_count = reinterpret_cast<const uint32_t*>(d.status);
+    const uint64_t before = tile - first_tile;  // < SCAN_TWO_PASS_SEGS (the host's condition for this kernel)
+    uint32_t p = threadIdx.x < before ? seg_count[first_tile + threadIdx.x] : 0u;
+#pragma unroll
+    for (int o = WAVE / 2; o > 0; o >>= 1) p += __shfl_xor(p, o);
+    if (threadIdx.x == 0) {
+      s_prefix = p;
+      if (tile + 1 == d.chunk_tile_begin[c + 1]) counts[d.chunk_index[c]] = p + seg_count[tile];
+    }
+  }
+  __syncthreads();
+  const hy_scan_chunk& ch = d.chunks[c];
+  segment_store<OUT_ROWID, SEG>(masks, tile_row0, ch.column.size, ch.out_begin + s_prefix,
+                                OUT_ROWID ? d.chunk_ids[c] : 0u, out_any, s_stage, s_scratch);
 }
 
 // ------------------------------------------------------------------------------------------------------------

@@ -131,6 +131,23 @@ def test_synthetic_scans(hy, oracle, dtype, encode):
         check(hy, oracle, w, 0, "LessThan", v, excluded=[1])
 
 
+@pytest.mark.parametrize("two_pass", ["1", "0"])
+def test_scan_paths_one_and_two_pass(hy, oracle, monkeypatch, two_pass):
+    """The count + write kernels (chunks of at most 64 segments) and the one-pass look-back kernel (HY_SCAN_TWO_PASS=0,
+    or a class with a longer chunk) give the same PosLists: u8 / u16 ids and int values, a 1.2 M-row chunk (74 u8
+    segments: its class takes the look-back kernel) beside 100,000- and 7-row chunks, RowID and offset outputs."""
+    monkeypatch.setenv("HY_SCAN_TWO_PASS", two_pass)
+    rng = np.random.default_rng(0x3250)
+    for n, chunk, distinct, encode in ((400_000, 100_000, 50, True), (300_007, 100_000, 1_000, True),
+                                       (250_000, 65_536, 1 << 20, False), (1_300_007, 1_200_000, 40, True)):
+        t = synthetic(hy, rng, n, chunk, "int", distinct, 0.02, encode)
+        w = wrap(hy, t)
+        for cond, v in (("LessThan", distinct // 3), ("GreaterThanEquals", distinct // 2), ("Equals", 7),
+                        ("NotEquals", 7), ("IsNull", None), ("IsNotNull", None)):
+            check(hy, oracle, w, 0, cond, v)
+        check(hy, oracle, w, 0, "LessThan", distinct // 3, excluded=[0])
+
+
 def test_scan_then_reference_scan_large(hy, oracle):
     rng = np.random.default_rng(7)
     t = synthetic(hy, rng, 300_000, 100_000, "int", 50, 0.0, True)
