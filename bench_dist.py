@@ -118,13 +118,18 @@ def main_distributed(args):
     rb = xj.record_bytes
     state = {}
     # RCCL transport: the library's own communicator (default) or torch.distributed's all_to_all (--transport torch)
-    rx, transport_note = None, "torch all_to_all"
+    rx, transport_note, transport = None, "torch all_to_all", "torch"
+    transport_error = None
     if args.dist_backend == "nccl" and args.transport == "capi":
         try:
             rx = hdist.RcclExchange(capi, dist, rank, world, dev)
             transport_note = "hy_join_exchange_counts/records (C-ABI RCCL communicator)"
-        except Exception as e:  # noqa: BLE001 - recorded in the bench line, the run continues on torch's RCCL
+            transport = "capi-rccl"
+        except Exception as e:  # noqa: BLE001 - the line says so: "transport": "torch-fallback" + the error
             transport_note = f"torch all_to_all (C-ABI communicator failed: {e})"
+            transport, transport_error = "torch-fallback", str(e)
+            print(f"bench_dist: rank {rank}: the C-ABI RCCL communicator failed ({e}); this run measures torch's "
+                  f"all_to_all instead and its line says \"transport\": \"torch-fallback\"", file=sys.stderr)
 
     def step():
         brec, bcnt = xj.partition(build_side, n_ord, False, stream, dev, key="build", row_base=sh["o_row_base"])
@@ -211,6 +216,7 @@ def main_distributed(args):
                                    f"distributed JoinHash(orders ⋈ scan, o_orderkey=l_orderkey, "
                                    f"radix_bits={radix_bits})",
                        "path": "hy_scan_join_exchange_partition + " + transport_note + " + hy_join_exchange_join_rows",
+                       "transport": transport, "transport_error": transport_error,
                        "sf_total": global_sf, "lineitem_rows": n_li_g, "orders_rows": n_ord_g, "chunk_size": chunk,
                        "scan_matches": g_probe, "join_pairs": g_pairs, "record_bytes": rb,
                        "exchange_bytes_per_step": g_sent,
