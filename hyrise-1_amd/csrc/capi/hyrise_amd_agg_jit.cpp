@@ -91,11 +91,13 @@ void emit_issue(std::ostringstream& o, const Shape& p) {
 }  // namespace
 
 std::string source(const Shape& p) {
-  // waves per SIMD the kernel is compiled for (2: no spills at TPC-H 1; HY_AGG_JIT_WAVES=3 / 4: A/B)
+  // waves per SIMD the kernel is compiled for: 3 (TPC-H 1 SF100, one box, alternating runs, profiles/r06_q1_jit_ab.txt:
+  // 3 waves with per-group selects 3.84 ms; 2 waves 4.64, or 4.13 with the round-5 0/1 FMA form; 3 waves with the FMA
+  // form 4.87 - 168 VGPRs, a few spilled, beat 181 at 2 waves). HY_AGG_JIT_WAVES: A/B
   static const int wpe = [] {
     const char* e = std::getenv("HY_AGG_JIT_WAVES");
-    const int v = e ? std::atoi(e) : 2;
-    return v >= 1 && v <= 8 ? v : 2;
+    const int v = e ? std::atoi(e) : 3;
+    return v >= 1 && v <= 8 ? v : 3;
   }();
   std::ostringstream o;
   const int H = p.n_gb, NS = p.n_sums, NA = NS > 0 ? NS : 1;
@@ -288,10 +290,16 @@ std::string source(const Shape& p) {
     << "    if (__ballot((vnull & act) != 0) != 0ull) {  // NULLs in the other loaded columns\n"
     << "      defer_step(a, step_id);\n      continue;\n    }\n"
     << "    uint32_t onehot = 0;\n"
-    << "#pragma unroll\n    for (int k = 0; k < R; ++k) onehot |= 1u << (e[k] * 4u + static_cast<uint32_t>(k));\n"
-    << "    double m[R][GROUPS];\n"
-    << "#pragma unroll\n    for (int k = 0; k < R; ++k)\n#pragma unroll\n      for (int j = 0; j < GROUPS; ++j) "
-       "m[k][j] = (onehot >> (4 * j + k)) & 1u ? 1.0 : 0.0;\n";
+    << "#pragma unroll\n    for (int k = 0; k < R; ++k) onehot |= 1u << (e[k] * 4u + static_cast<uint32_t>(k));\n";
+  // HY_AGG_JIT_SELECT=0 (A/B): the round-5 form, one FMA per group with a 0/1 double per row and group
+  static const bool select = [] {
+    const char* e = std::getenv("HY_AGG_JIT_SELECT");
+    return !(e && std::strtol(e, nullptr, 10) == 0);
+  }();
+  if (!select)
+    o << "    double m[R][GROUPS];\n"
+      << "#pragma unroll\n    for (int k = 0; k < R; ++k)\n#pragma unroll\n      for (int j = 0; j < GROUPS; ++j) "
+         "m[k][j] = (onehot >> (4 * j + k)) & 1u ? 1.0 : 0.0;\n";
   // (C) the sums: chains straight-line, then (D) their accumulation
   for (int s = 0; s < NS; ++s) {
     const int kind = p.sum_kind[s];
@@ -327,8 +335,11 @@ std::string source(const Shape& p) {
         << "], (__float_as_uint(rf[k]) << 1) - 1u);\n";
     o << "#pragma unroll\n      for (int k = 0; k < R; ++k) {\n"
       << "        const double xv = " << (kind == 2 ? "static_cast<double>(static_cast<int32_t>(ri[k]))" : "static_cast<double>(rf[k])")
-      << ";\n#pragma unroll\n        for (int j = 0; j < GROUPS; ++j) acc[j][" << s << "] = __builtin_fma(m[k][j], xv, acc[j][" << s
-      << "]);\n      }\n    }\n";
+      << ";\n#pragma unroll\n        for (int j = 0; j < GROUPS; ++j) acc[j][" << s << "] = ";
+    if (select)  // the row's value added to its group's accumulator only (no 0/1 doubles in registers)
+      o << "(onehot >> (4 * j + k)) & 1u ? acc[j][" << s << "] + xv : acc[j][" << s << "];\n      }\n    }\n";
+    else
+      o << "__builtin_fma(m[k][j], xv, acc[j][" << s << "]);\n      }\n    }\n";
   }
   o << "#pragma unroll\n    for (int j = 0; j < GROUPS; ++j) {\n"
     << "      const uint32_t mb = (onehot >> (4 * j)) & 0xFu;\n"
