@@ -2785,7 +2785,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT >= 1024 ?
     JoinDesc d, Src build, Src probe, hy_row_id* __restrict__ out_build, hy_row_id* __restrict__ out_probe,
     uint64_t* __restrict__ part_out_begin, uint32_t* __restrict__ part_out_count) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ uint32_t s_tot[2 * JP * (NT / WAVE) + 1];
+  __shared__ uint32_t s_tot[JP * (NT / WAVE) + 1];
   __shared__ uint64_t s_base;
   if (d.multi == nullptr) {  // every partition (most need several passes): one workgroup each, skewed ones deferred
     const uint32_t p = blockIdx.x;
@@ -2794,14 +2794,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT >= 1024 ?
       if (threadIdx.x == 0) d.skewed[atomicAdd(d.n_skewed, 1u)] = p;
       return;
     }
-    // up to two passes' records: one pass of 2 * JP per thread, each record loaded and matched once (round 6; the
-    // count + reload + write passes below load and match every record twice); larger partitions take the passes
-    if (d.probe_begin[p + 1] - d.probe_begin[p] + (Src::V - 1) <= static_cast<uint32_t>(2 * JP * NT))
-      partition_one_table<Src, P, false, 2 * JP, NT>(d, p, smem, build, probe, out_build, out_probe, part_out_begin,
+    partition_one_table<Src, P, false, JP, NT, true>(d, p, smem, build, probe, out_build, out_probe, part_out_begin,
                                                      part_out_count, s_tot, &s_base);
-    else
-      partition_one_table<Src, P, false, JP, NT, true>(d, p, smem, build, probe, out_build, out_probe, part_out_begin,
-                                                       part_out_count, s_tot, &s_base);
     return;
   }
   const uint32_t n = *d.n_multi;
