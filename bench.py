@@ -633,8 +633,11 @@ def kernel_stats(L):
     return out
 
 
-# bench.py's kernel-table names -> the HIP kernel function names rocprofv3 reports
-ROCPROF_NAME = {"scan_dict": "scan_kernel", "scan_value": "scan_kernel"}
+# bench.py's kernel-table names -> the HIP kernel function names rocprofv3 reports (a list: the kernel-table entry
+# times several launches as one - the two-pass TableScan's count and write kernels - and its traffic is their sum;
+# older summaries name the one-pass scan_kernel)
+ROCPROF_NAME = {"scan_dict": [["scan_count_kernel", "scan_write_kernel"], ["scan_kernel"]],
+                "scan_value": [["scan_count_kernel", "scan_write_kernel"], ["scan_kernel"]]}
 
 
 def summary_files(mode, sf, fused):
@@ -658,9 +661,10 @@ def committed_traffic(kernel, sf, chunk, world, mode="join", fused=True):
     here, files = summary_files(mode, sf, fused)
     for f in reversed(files):
         with open(f) as fh:
-            k = json.load(fh).get("kernels", {}).get(ROCPROF_NAME.get(kernel, kernel), {})
-        if "hbm_bytes_per_launch" in k:
-            return k["hbm_bytes_per_launch"], os.path.relpath(f, here)
+            ks = json.load(fh).get("kernels", {})
+        for names in ROCPROF_NAME.get(kernel, [[kernel]]):
+            if all("hbm_bytes_per_launch" in ks.get(n, {}) for n in names):
+                return sum(ks[n]["hbm_bytes_per_launch"] for n in names), os.path.relpath(f, here)
     return None, None
 
 
