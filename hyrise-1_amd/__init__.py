@@ -82,6 +82,8 @@ device_count = _host.device_count
 build_info = _host.build_info
 op_trace_enable = _host.op_trace_enable
 op_trace_take = _host.op_trace_take
+join_plan_cache_stats = _host.join_plan_cache_stats
+join_plan_cache_clear = _host.join_plan_cache_clear
 pool_stats = _host.pool_stats
 device_memory = _host.device_memory
 host_cpu_share = _host.host_cpu_share

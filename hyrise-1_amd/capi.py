@@ -57,14 +57,15 @@ class JoinSide(ctypes.Structure):
 
 class JoinFilter(ctypes.Structure):
     _fields_ = [("chunks", ctypes.POINTER(ScanChunk)), ("value_type", ctypes.c_int32), ("constant", ctypes.c_void_p),
-                ("out_offsets", ctypes.c_void_p), ("out_chunk_begin", ctypes.c_void_p), ("n_chunks", ctypes.c_uint32)]
+                ("out_offsets", ctypes.c_void_p), ("out_chunk_begin", ctypes.c_void_p), ("n_chunks", ctypes.c_uint32),
+                ("out_row_ids", ctypes.c_void_p)]
 
     def __init__(self, chunks=None, value_type=0, constant=None, out_offsets=None, out_chunk_begin=None,
-                 n_chunks=None):
+                 n_chunks=None, out_row_ids=None):
         # n_chunks defaults to the length of a ctypes array of predicate chunks (the side's chunk count)
         if n_chunks is None:
             n_chunks = len(chunks) if chunks is not None and hasattr(chunks, "__len__") else 0
-        super().__init__(chunks, value_type, constant, out_offsets, out_chunk_begin, n_chunks)
+        super().__init__(chunks, value_type, constant, out_offsets, out_chunk_begin, n_chunks, out_row_ids)
 
 
 class JoinParams(ctypes.Structure):
@@ -269,6 +270,7 @@ _sigs = {
     "hy_scan_join_plan_execute": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(JoinResult),
                                                   ctypes.c_void_p]),
+    "hy_scan_join_plan_rebind": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(JoinFilter), ctypes.POINTER(JoinFilter)]),
     "hy_scan_join_plan_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "hy_string_table_scan_workspace_size": (ctypes.c_int, [ctypes.POINTER(ScanChunk), ctypes.c_uint32,
                                                            ctypes.POINTER(StringPredicate),

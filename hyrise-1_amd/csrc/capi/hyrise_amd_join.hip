@@ -1,6 +1,7 @@
 // C entry points of JoinHash (include/hyrise_amd.h): argument checks and the dispatch on the hashed type to the
 // per-type translation units (hyrise_amd_join_*.hip, join_host.hpp).
 #include <cstdio>
+#include <cstring>
 #include "join_host.hpp"
 
 #include <memory>
@@ -295,6 +296,57 @@ hy_status hy_scan_join_plan_execute(hy_join_plan_t plan, hy_row_id* out_build, h
   return st;
 }
 
+hy_status hy_scan_join_plan_rebind(hy_join_plan_t plan, const hy_join_filter* build_filter,
+                                   const hy_join_filter* probe_filter) {
+  if (!plan) return fail(HY_ERR_INVALID_ARGUMENT, "plan");
+  // validate both sides before changing either
+  struct Bind {
+    uint32_t* offsets;
+    uint64_t* begin;
+    hy_row_id* rows;
+  } bind[2] = {};
+  const SidePlan* sides[2] = {&plan->bp, &plan->pp};
+  const hy_join_filter* filters[2] = {build_filter, probe_filter};
+  for (int i = 0; i < 2; ++i) {
+    const SidePlan& p = *sides[i];
+    const hy_join_filter* f = filters[i];
+    if (!p.filtered) {
+      if (f) return fail(HY_ERR_INVALID_ARGUMENT, "rebind: a filter for a side the plan does not filter");
+      continue;
+    }
+    if (!f) return fail(HY_ERR_INVALID_ARGUMENT, "rebind: the plan filters this side");
+    if (f->n_chunks < p.chunks.size() || (p.chunks.size() && !f->chunks) || f->value_type != p.filter_type)
+      return fail(HY_ERR_INVALID_ARGUMENT, "rebind: the filter differs from the plan's");
+    if (p.chunks.size() && std::memcmp(f->chunks, p.filter.data(), sizeof(hy_scan_chunk) * p.chunks.size()) != 0)
+      return fail(HY_ERR_INVALID_ARGUMENT, "rebind: the predicate chunks differ from the plan's");
+    if (f->out_row_ids && (!f->out_offsets || !f->out_chunk_begin))
+      return fail(HY_ERR_INVALID_ARGUMENT, "out_row_ids needs out_offsets and out_chunk_begin");
+    // which outputs exist shapes the plan's workspace carve: only the pointers may change
+    if ((f->out_offsets != nullptr) != (p.scan_out != nullptr) ||
+        (f->out_chunk_begin != nullptr) != (p.scan_chunk_begin != nullptr))
+      return fail(HY_ERR_INVALID_ARGUMENT, "rebind: out_offsets / out_chunk_begin must stay set (or unset) as at create");
+    bind[i] = Bind{f->out_offsets, f->out_chunk_begin, f->out_row_ids};
+  }
+  SidePlan* mut[2] = {&plan->bp, &plan->pp};
+  bool changed = false;
+  for (int i = 0; i < 2; ++i) {
+    if (!mut[i]->filtered) continue;
+    changed |= mut[i]->scan_out != bind[i].offsets || mut[i]->scan_chunk_begin != bind[i].begin ||
+               mut[i]->scan_rows != bind[i].rows;
+    mut[i]->scan_out = bind[i].offsets;
+    mut[i]->scan_chunk_begin = bind[i].begin;
+    mut[i]->scan_rows = bind[i].rows;
+  }
+  if (changed) {  // a captured graph holds the old pointers; a plan rebound per execution runs its launches eagerly
+    if (plan->exec) (void)hipGraphExecDestroy(plan->exec);
+    if (plan->graph) (void)hipGraphDestroy(plan->graph);
+    plan->exec = nullptr;
+    plan->graph = nullptr;
+    plan->no_graph = true;
+  }
+  return HY_OK;
+}
+
 hy_status hy_scan_join_plan_destroy(hy_join_plan_t plan) {
   if (!plan) return HY_OK;
   if (plan->workspace) HY_HIP(hipFree(plan->workspace));
@@ -473,6 +525,8 @@ hy_status plan_row_side(const hy_join_side* side, const hy_join_filter* filter, 
   p.fuse = ref ? 1 : 0;
   st = plan_filter(filter, p, side->value_type, params->hashed_type);
   if (st != HY_OK) return st;
+  if (p.scan_rows)
+    return fail(HY_ERR_UNSUPPORTED, "out_row_ids on an exchange side (expand out_offsets: hy_expand_chunk_row_ids)");
   const uint64_t rows = ref ? p.ref_row_begin.back() : p.n_rows;
   if (rows + row_base >= (p.filtered ? 0x7FFFFFFFull : 0xFFFFFFFFull))
     return fail(HY_ERR_UNSUPPORTED, "global row indexes exceed the 32-bit record payload");

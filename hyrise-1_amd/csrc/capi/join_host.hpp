@@ -61,6 +61,7 @@ struct JoinKnobs {
   bool direct = false;                 // HY_JOIN_DIRECT: direct partitioning of a filtered side (join_direct.hip)
   uint32_t direct_span = 16;           // HY_DIRECT_SPAN: tiles per span of the direct first pass
   uint32_t direct_groups = 0;          // HY_DIRECT_GROUPS: span groups per bucket of the direct second pass (0: auto)
+  bool join_stash = true;              // HY_JOIN_STASH: two-pass partitions keep their first pass in LDS (0: reload it)
 };
 
 inline JoinKnobs knobs_from_env() {
@@ -85,6 +86,7 @@ inline JoinKnobs knobs_from_env() {
   k.direct = num("HY_JOIN_DIRECT", 0) != 0;
   k.direct_span = static_cast<uint32_t>(std::min<long long>(std::max<long long>(1, num("HY_DIRECT_SPAN", 16)), 64));
   k.direct_groups = static_cast<uint32_t>(std::min<long long>(std::max<long long>(0, num("HY_DIRECT_GROUPS", 0)), 4096));
+  k.join_stash = num("HY_JOIN_STASH", 1) != 0;
   return k;
 }
 
@@ -210,6 +212,7 @@ struct SidePlan {
   uint64_t filter_const = 0;
   uint32_t* scan_out = nullptr;
   uint64_t* scan_chunk_begin = nullptr;
+  hy_row_id* scan_rows = nullptr;        // hy_join_filter.out_row_ids
   // a prepared plan (hy_scan_join_plan_*) whose own workspace already holds this side's descriptors from an earlier
   // execution: the upload is skipped (the carve of the workspace is deterministic for a plan)
   bool device_ready = false;
@@ -370,6 +373,9 @@ inline hy_status plan_filter(const hy_join_filter* f, SidePlan& p, int32_t colum
   p.filter_type = f->value_type;
   p.scan_out = f->out_offsets;
   p.scan_chunk_begin = f->out_chunk_begin;
+  p.scan_rows = f->out_row_ids;
+  if (p.scan_rows && (!p.scan_out || !p.scan_chunk_begin))
+    return fail(HY_ERR_INVALID_ARGUMENT, "out_row_ids needs out_offsets and out_chunk_begin");
   bool value = false;
   for (size_t i = 0; i < p.chunks.size(); ++i) {
     if (p.chunks[i].pos_list) return fail(HY_ERR_UNSUPPORTED, "a filtered join side must be a data table");
@@ -647,6 +653,13 @@ inline bool filter_compact_enabled() {
   return v;
 }
 
+// The hy_join_filter.out_row_ids arrays that the current join's part1_spread wrote directly (this thread, reset by
+// join_typed); the other pass-0 variants write offsets, which join_typed expands into the RowIDs at the end.
+inline std::vector<const hy_row_id*>& scan_rows_written() {
+  thread_local std::vector<const hy_row_id*> v;
+  return v;
+}
+
 // Calls f with the kernel side tag (hyk::OnBuild / hyk::OnProbe) named by a runtime side tag ("build" / "probe").
 template <typename F>
 hy_status by_side(const char* tag, F&& f) {
@@ -712,10 +725,15 @@ hy_status launch_filtered_pass0(const SidePlan& p, const hyk::Side& sd, const hy
                      p.n_tiles1, n_digits, b.grand_total, b.tile_begin, static_cast<uint32_t>(p.chunks.size()), b.total,
                      p.scan_chunk_begin);
   HY_HIP(hipGetLastError());
+  hyk::Side sdr = sd;
+  if (p.scan_rows) {  // the scan's PosLists straight from the ranking pass (no expansion of the offsets afterwards)
+    sdr.scan_rows = p.scan_rows;
+    scan_rows_written().push_back(p.scan_rows);
+  }
   {
     KTimer kt_((std::string("part1_spread.") + SD::name).c_str(), s, p.n_rows);
-    hipLaunchKernelGGL((hyk::part1_spread<SD, H>), grid, dim3(hyk::PART_THREADS), 0, s, sd, d0, nd, static_cast<int>(w0),
-                       n_digits, b.off, b.span_count, b.recB, out);
+    hipLaunchKernelGGL((hyk::part1_spread<SD, H>), grid, dim3(hyk::PART_THREADS), 0, s, sdr, d0, nd,
+                       static_cast<int>(w0), n_digits, b.off, b.span_count, b.recB, out);
     kt_.done();
   }
   HY_HIP(hipGetLastError());
@@ -792,6 +810,7 @@ hyk::Side make_side(const SidePlan& p, const SideBufs<H, P>& b, uint32_t seed, b
   sd.filter_const = p.filter_const;
   sd.filter_type = p.filter_type;
   sd.scan_out = p.scan_out;
+  sd.scan_rows = nullptr;  // (set by launch_filtered_pass0 for part1_spread only)
   sd.bloom = bloom;
   sd.bloom_mask = bloom ? static_cast<uint32_t>(bloom_n - 1) : 0u;
   sd.bloom_by_hash = bloom_by_hash ? 1 : 0;
@@ -1138,6 +1157,24 @@ uint32_t lds_table_rows() {
   return rows;
 }
 
+// Whether join_partition_multi<Src, P, JP, NT> may take `bytes` of dynamic LDS (set once per instance above 64 KB).
+template <typename Src, typename P, int JP, int NT>
+bool stash_lds_ok(size_t bytes) {
+  if (bytes <= 64 * 1024) return true;
+  static std::mutex m;
+  static size_t granted = 0;
+  std::lock_guard<std::mutex> lock(m);
+  if (bytes <= granted) return true;
+  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&hyk::join_partition_multi<Src, P, JP, NT>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bytes));
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  granted = bytes;
+  return true;
+}
+
 // Per-partition LDS build/probe over partitioned records (partition bounds on the device; the records as the last pass
 // wrote them: hyk::RecSrc or hyk::HashSrc). probe_rows_hint: an upper bound of the probe rows (probe_exact: their
 // number); it picks the probe
@@ -1188,10 +1225,24 @@ hy_status run_join_partitions(const uint32_t* build_begin, const uint32_t* probe
   // reload + write passes of join_partition_multi although nearly all fit one 8,192-record pass.)
   const double wide_pass = double(JW * NT - (Src::V - 1));
   const bool all_multi = probe_exact && double(avg_probe) + 4.0 * std::sqrt(double(avg_probe)) > wide_pass && !jd.trace;
+  // join_partition_multi (JW records per thread): a two-pass partition keeps its first pass in LDS (jd.stash_rows)
+  // when its table and the stash fit half a CU's LDS (two 1024-thread workgroups per CU)
+  hyk::JoinDesc jdm = jd;
+  size_t lds_m = lds;
+  if (knobs().join_stash) {
+    const size_t stash = size_t(JW) * NT * (sizeof(P) + 4);
+    const size_t half = 80 * 1024 - 1024;  // (the kernel's static LDS: s_tot, s_base)
+    uint32_t rows = std::min<uint32_t>(lds_max, hyk::LDS_MAX_ROWS);
+    while (rows > 16 && hyk::table_bytes<H, P>(rows) + stash > half) rows = rows * 15 / 16;
+    if (rows > 16 && stash_lds_ok<Src, P, JW, NT>(std::max(lds, hyk::table_bytes<H, P>(rows) + stash))) {
+      jdm.stash_rows = rows;
+      lds_m = std::max(lds, hyk::table_bytes<H, P>(rows) + stash);
+    }
+  }
   if (n_parts && all_multi) {
-    jd.multi = nullptr;
+    jdm.multi = nullptr;
     KTimer kt_("join_partition", s, units);
-    hipLaunchKernelGGL((hyk::join_partition_multi<Src, P, JW, NT>), dim3(n_parts), dim3(NT), lds, s, jd, bsrc, psrc,
+    hipLaunchKernelGGL((hyk::join_partition_multi<Src, P, JW, NT>), dim3(n_parts), dim3(NT), lds_m, s, jdm, bsrc, psrc,
                        out_build, out_probe, partition_begin, partition_counts);
     kt_.done();
     HY_HIP(hipGetLastError());
@@ -1218,8 +1269,8 @@ hy_status run_join_partitions(const uint32_t* build_begin, const uint32_t* probe
       KTimer kt_("join_partition_multi", s, units);
       const dim3 g(static_cast<uint32_t>(std::min<uint64_t>(max_multi, 512)));
       if (wide)
-        hipLaunchKernelGGL((hyk::join_partition_multi<Src, P, JW, NT>), g, dim3(NT), lds, s, jd, bsrc, psrc, out_build,
-                           out_probe, partition_begin, partition_counts);
+        hipLaunchKernelGGL((hyk::join_partition_multi<Src, P, JW, NT>), g, dim3(NT), lds_m, s, jdm, bsrc, psrc,
+                           out_build, out_probe, partition_begin, partition_counts);
       else
         hipLaunchKernelGGL((hyk::join_partition_multi<Src, P, 4, NT>), g, dim3(NT), lds, s, jd, bsrc, psrc, out_build,
                            out_probe, partition_begin, partition_counts);
@@ -2105,10 +2156,10 @@ hy_status join_typed_passes(const SidePlan& bp_in, const SidePlan& pp_in, const 
 }
 
 template <typename TB, typename TP, typename H>
-hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join_params* prm, hy_row_id* out_build,
-                     hy_row_id* out_probe, uint64_t out_capacity, uint64_t* partition_begin,
-                     uint32_t* partition_counts, hy_join_result* result, void* workspace, size_t workspace_bytes,
-                     hipStream_t s) {
+hy_status join_typed_any(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join_params* prm, hy_row_id* out_build,
+                         hy_row_id* out_probe, uint64_t out_capacity, uint64_t* partition_begin,
+                         uint32_t* partition_counts, hy_join_result* result, void* workspace, size_t workspace_bytes,
+                         hipStream_t s) {
   const uint32_t bits = prm->radix_bits;
   {
     const auto w = digit_plan(bits, 0);
@@ -2134,6 +2185,27 @@ hy_status join_typed(const SidePlan& bp_in, const SidePlan& pp_in, const hy_join
   b2.device_ready = p2.device_ready = false;
   return join_typed_passes<TB, TP, H>(b2, p2, prm, out_build, out_probe, out_capacity, partition_begin,
                                       partition_counts, result, workspace, workspace_bytes, s, false, nullptr);
+}
+
+// The join, then the fused scans' RowIDs (hy_join_filter.out_row_ids) of every side whose pass 0 wrote offsets.
+template <typename TB, typename TP, typename H>
+hy_status join_typed(const SidePlan& bp, const SidePlan& pp, const hy_join_params* prm, hy_row_id* out_build,
+                     hy_row_id* out_probe, uint64_t out_capacity, uint64_t* partition_begin,
+                     uint32_t* partition_counts, hy_join_result* result, void* workspace, size_t workspace_bytes,
+                     hipStream_t s) {
+  scan_rows_written().clear();
+  const hy_status st = join_typed_any<TB, TP, H>(bp, pp, prm, out_build, out_probe, out_capacity, partition_begin,
+                                                 partition_counts, result, workspace, workspace_bytes, s);
+  if (st != HY_OK && st != HY_ERR_CAPACITY) return st;
+  for (const SidePlan* p : {&bp, &pp}) {
+    if (!p->filtered || !p->scan_rows) continue;
+    const auto& done = scan_rows_written();
+    if (std::find(done.begin(), done.end(), p->scan_rows) != done.end()) continue;
+    const hy_status e = hy_expand_chunk_row_ids(p->scan_out, p->scan_chunk_begin, nullptr,
+                                                static_cast<uint32_t>(p->chunks.size()), p->scan_rows, s);
+    if (e != HY_OK) return e;
+  }
+  return st;
 }
 
 template <typename F>

@@ -354,6 +354,8 @@ PYBIND11_MODULE(_hyrise_host, m) {
   });
   m.def("build_info", []() { return std::string(hy_build_info()); });
   m.def("op_trace_enable", &op_trace_enable, py::arg("on"));
+  m.def("join_plan_cache_stats", &join_plan_cache_stats);
+  m.def("join_plan_cache_clear", &join_plan_cache_clear);
   m.def("op_trace_take", []() {
     py::list l;
     for (const auto& r : op_trace_take()) l.append(py::make_tuple(r.op, r.phase, r.ms));

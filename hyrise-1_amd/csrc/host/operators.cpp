@@ -20,6 +20,8 @@
 #include <thread>
 #include <unordered_map>
 
+#include <unistd.h>  // environ
+
 namespace hyrise {
 
 namespace {
@@ -1524,7 +1526,139 @@ void write_chunk_columns(ChunkColumns& out, OutputArena& arena, const std::share
   }
 }
 
+// Prepared plans (hy_scan_join_plan_*) of JoinHash executions over data tables, kept for re-executions of the same
+// shape - a prepared statement executed again, or a plan re-run by the scheduler - so that the side and predicate
+// descriptors are validated and staged to HBM once per shape (SF100's fused TableScan -> JoinHash: 9,155 + 1,500 chunk
+// and 6,000 predicate descriptors) instead of once per execution. A plan matches an execution whose descriptors are
+// byte-identical (device pointers of every column chunk included: the staged copies are then exactly what the call
+// would stage) under the same HY_* knobs. A plan is used by one execution at a time (taken out of the cache, put back
+// after the execution's stream synchronised); each execution rebinds it to its own TableScan output buffers.
+// HY_OP_PLAN_CACHE = plans kept (default 2; 0 disables). Join inputs with PosLists change per execution and do not use
+// the cache.
+struct CachedJoinPlan {
+  std::vector<hy_join_chunk> bchunks, pchunks;
+  hy_join_side bside{}, pside{};
+  std::vector<hy_scan_chunk> filter;
+  hy_join_filter pf{};
+  ScanConstant constant;
+  bool filtered = false;
+  hy_join_params prm{};
+  std::string knobs;
+  hy_join_plan_t plan = nullptr;
+  ~CachedJoinPlan() {
+    if (plan) (void)hy_scan_join_plan_destroy(plan);
+  }
+};
+
+std::string join_knobs() {  // the HY_* environment a plan was created under (its knobs snapshot)
+  std::string k;
+  for (char** e = ::environ; e && *e; ++e)
+    if (std::strncmp(*e, "HY_", 3) == 0) k.append(*e).push_back('\n');
+  return k;
+}
+
+bool same_side(const hy_join_side& a, const std::vector<hy_join_chunk>& ac, const hy_join_side& b) {
+  return a.n_chunks == b.n_chunks && a.value_type == b.value_type && a.n_referenced == b.n_referenced &&
+         a.fuse_dereference == b.fuse_dereference && a.referenced_chunk_base == b.referenced_chunk_base &&
+         (b.n_chunks == 0 || std::memcmp(ac.data(), b.chunks, sizeof(hy_join_chunk) * b.n_chunks) == 0);
+}
+
+class JoinPlanCache {
+ public:
+  static JoinPlanCache& get() {
+    static JoinPlanCache* c = new JoinPlanCache();  // (never destroyed: no HIP call after the runtime's teardown)
+    return *c;
+  }
+  static size_t capacity() {
+    static const size_t v = [] {
+      const char* e = std::getenv("HY_OP_PLAN_CACHE");
+      return e ? static_cast<size_t>(std::max(0L, std::strtol(e, nullptr, 10))) : size_t{2};
+    }();
+    return v;
+  }
+  // the plan for this execution: a cached one of the same shape, or a new one (nullptr when the cache is off)
+  std::unique_ptr<CachedJoinPlan> take(const hy_join_side& b, const hy_join_side& p, const hy_join_filter* pf,
+                                       const ScanConstant* constant, const hy_join_params& prm) {
+    if (capacity() == 0) return nullptr;
+    const std::string knobs = join_knobs();
+    {
+      std::lock_guard<std::mutex> lock(_m);
+      for (auto it = _idle.begin(); it != _idle.end(); ++it) {
+        const CachedJoinPlan& e = **it;
+        if (e.knobs != knobs || std::memcmp(&e.prm, &prm, sizeof(prm)) != 0 || e.filtered != (pf != nullptr) ||
+            !same_side(e.bside, e.bchunks, b) || !same_side(e.pside, e.pchunks, p))
+          continue;
+        if (pf && (e.pf.value_type != pf->value_type || e.pf.n_chunks != pf->n_chunks ||
+                   std::memcmp(e.constant.bytes, constant->bytes, sizeof(e.constant.bytes)) != 0 ||
+                   (pf->n_chunks && std::memcmp(e.filter.data(), pf->chunks, sizeof(hy_scan_chunk) * pf->n_chunks))))
+          continue;
+        auto found = std::move(*it);
+        _idle.erase(it);
+        ++_hits;
+        return found;
+      }
+      ++_misses;
+    }
+    auto e = std::make_unique<CachedJoinPlan>();
+    e->bchunks.assign(b.chunks, b.chunks + b.n_chunks);
+    e->pchunks.assign(p.chunks, p.chunks + p.n_chunks);
+    e->bside = b;
+    e->bside.chunks = e->bchunks.data();
+    e->pside = p;
+    e->pside.chunks = e->pchunks.data();
+    e->prm = prm;
+    e->knobs = knobs;
+    e->filtered = pf != nullptr;
+    if (pf) {
+      e->filter.assign(pf->chunks, pf->chunks + pf->n_chunks);
+      e->constant = *constant;
+      e->pf = *pf;
+      e->pf.chunks = e->filter.data();
+      e->pf.constant = e->constant.bytes;
+    }
+    hy_check(hy_scan_join_plan_create(&e->bside, nullptr, &e->pside, pf ? &e->pf : nullptr, &e->prm, &e->plan),
+             "hy_scan_join_plan_create");
+    return e;
+  }
+  // back into the cache once the execution's stream has synchronised (the oldest plan beyond the capacity is freed)
+  void put(std::unique_ptr<CachedJoinPlan> e) {
+    std::unique_ptr<CachedJoinPlan> evicted;
+    {
+      std::lock_guard<std::mutex> lock(_m);
+      _idle.push_back(std::move(e));
+      if (_idle.size() > capacity()) {
+        evicted = std::move(_idle.front());
+        _idle.erase(_idle.begin());
+      }
+    }
+  }
+  std::pair<uint64_t, uint64_t> stats() {
+    std::lock_guard<std::mutex> lock(_m);
+    return {_hits, _misses};
+  }
+  void clear() {
+    std::vector<std::unique_ptr<CachedJoinPlan>> gone;
+    std::lock_guard<std::mutex> lock(_m);
+    gone.swap(_idle);
+  }
+
+ private:
+  std::mutex _m;
+  std::vector<std::unique_ptr<CachedJoinPlan>> _idle;
+  uint64_t _hits = 0, _misses = 0;
+};
+
+bool data_side(const hy_join_side& s) {
+  if (s.n_referenced) return false;
+  for (uint32_t i = 0; i < s.n_chunks; ++i)
+    if (s.chunks[i].pos_list) return false;
+  return true;
+}
+
 }  // namespace
+
+std::pair<uint64_t, uint64_t> join_plan_cache_stats() { return JoinPlanCache::get().stats(); }
+void join_plan_cache_clear() { JoinPlanCache::get().clear(); }
 
 std::shared_ptr<const Table> JoinHash::_on_execute() {
   const auto left_in = input_table_left();
@@ -1619,22 +1753,34 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
     scan_builder.schedule([&] { scan_chunks = fused_scan->chunks_for(scan_rows); });
     scan_offsets = std::make_unique<DeviceBuffer>(std::max<uint64_t>(fused_scan->total, 1) * 4, s);
     scan_begin = std::make_unique<DeviceBuffer>((fused_scan->descs.size() + 1) * 8, s);
+    // the scan's PosLists come straight from the join's ranking pass (out_row_ids)
     pf = hy_join_filter{fused_scan->descs.data(), hy_type_of(fused_scan->col_type), fused_scan->constant.bytes,
                         scan_offsets->as<uint32_t>(), scan_begin->as<uint64_t>(),
-                        static_cast<uint32_t>(fused_scan->descs.size())};
+                        static_cast<uint32_t>(fused_scan->descs.size()), scan_rows->as<hy_row_id>()};
+  }
+  // a prepared plan of this shape (data-table sides), rebound to this execution's scan output buffers; else one call
+  std::unique_ptr<CachedJoinPlan> cached;
+  if (!string_keys && data_side(b) && data_side(p)) {
+    cached = JoinPlanCache::get().take(b, p, fused_scan ? &pf : nullptr, fused_scan ? &fused_scan->constant : nullptr,
+                                       prm);
+    if (cached) hy_check(hy_scan_join_plan_rebind(cached->plan, nullptr, fused_scan ? &pf : nullptr), "rebind");
   }
   size_t ws_bytes = 0;
-  if (fused_scan)
+  if (cached)
+    ws_bytes = 0;  // (the plan's own workspace)
+  else if (fused_scan)
     hy_check(hy_scan_join_hash_workspace_size(&b, nullptr, &p, &pf, &prm, &ws_bytes),
              "hy_scan_join_hash_workspace_size");
   else
     hy_check(hy_join_hash_workspace_size(&b, &p, &prm, &ws_bytes), "hy_join_hash_workspace_size");
   DeviceBuffer ws(ws_bytes, s);
+  tr.mark("plan");
   const uint32_t n_parts = 1u << prm.radix_bits;
   DeviceBuffer part_begin(8 * n_parts, s), part_count(4 * n_parts, s);
   uint64_t capacity = std::max<uint64_t>(probe_rows + build_rows, 16);
   auto out_b = std::make_shared<DeviceBuffer>(capacity * sizeof(RowID));
   auto out_p = std::make_shared<DeviceBuffer>(capacity * sizeof(RowID));
+  tr.mark("buffers");
 
   // One output chunk per non-empty partition (join_hash.cpp:829-855), in partition order. The chunks of all
   // partitions are built while the device runs the join - their columns and PosLists depend only on the inputs -
@@ -1720,15 +1866,18 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
   const unsigned workers = static_cast<unsigned>(std::max<size_t>(
       1, std::min<size_t>({max_workers, builders.concurrency(host_cpu_share()), n_parts / parts_per_job})));
   for (unsigned t = 0; t < workers; ++t) builders.schedule(build);
+  tr.mark("output described, builders scheduled");
 
   hy_join_result res{};
   for (int attempt = 0; attempt < 2; ++attempt) {
     const hy_status st =
-        fused_scan ? hy_scan_join_hash(&b, nullptr, &p, &pf, &prm, out_b->as<hy_row_id>(), out_p->as<hy_row_id>(),
-                                       capacity, part_begin.as<uint64_t>(), part_count.as<uint32_t>(), &res, ws.get(),
-                                       ws_bytes, s)
-                   : hy_join_hash(&b, &p, &prm, out_b->as<hy_row_id>(), out_p->as<hy_row_id>(), capacity,
-                                  part_begin.as<uint64_t>(), part_count.as<uint32_t>(), &res, ws.get(), ws_bytes, s);
+        cached ? hy_scan_join_plan_execute(cached->plan, out_b->as<hy_row_id>(), out_p->as<hy_row_id>(), capacity,
+                                           part_begin.as<uint64_t>(), part_count.as<uint32_t>(), &res, s)
+        : fused_scan
+            ? hy_scan_join_hash(&b, nullptr, &p, &pf, &prm, out_b->as<hy_row_id>(), out_p->as<hy_row_id>(), capacity,
+                                part_begin.as<uint64_t>(), part_count.as<uint32_t>(), &res, ws.get(), ws_bytes, s)
+            : hy_join_hash(&b, &p, &prm, out_b->as<hy_row_id>(), out_p->as<hy_row_id>(), capacity,
+                           part_begin.as<uint64_t>(), part_count.as<uint32_t>(), &res, ws.get(), ws_bytes, s);
     if (st == HY_ERR_CAPACITY && attempt == 0) {
       capacity = std::max<uint64_t>(res.capacity_required, 16);
       DeviceBuffer nb(capacity * sizeof(RowID)), np(capacity * sizeof(RowID));
@@ -1739,26 +1888,24 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
     hy_check(st, fused_scan ? "hy_scan_join_hash" : "hy_join_hash");
     break;
   }
+  tr.mark("join launched");
   hy_check(hy_memcpy_dtoh(h_begin.data(), part_begin.get(), 8 * n_parts, s), "dtoh");
   hy_check(hy_memcpy_dtoh(h_count.data(), part_count.get(), 4 * n_parts, s), "dtoh");
   std::vector<uint64_t> h_scan_begin(fused_scan ? fused_scan->descs.size() + 1 : 0);
   if (fused_scan)
     hy_check(hy_memcpy_dtoh(h_scan_begin.data(), scan_begin->get(), 8 * h_scan_begin.size(), s), "dtoh");
   hy_check(hy_stream_synchronize(s), "sync");
-  tr.mark("join kernels + partition counts");
-  if (fused_scan) {  // the scan's output from the join's by-product: one expansion launch into the chunks' RowIDs
+  if (cached) JoinPlanCache::get().put(std::move(cached));  // (its workspace is idle: the stream synchronised)
+  tr.mark("join kernels + partition counts synchronised");
+  if (fused_scan) {  // the scan's output: the join wrote its RowIDs (out_row_ids) before the sync above
     uint64_t at = 0;
     for (size_t k = 0; k < fused_scan->counts.size(); ++k) {
       Assert(h_scan_begin[k] == at, "fused TableScan: the join's scan output disagrees with the scan's count");
       at += fused_scan->counts[k];
     }
-    hy_check(hy_expand_chunk_row_ids(scan_offsets->as<uint32_t>(), scan_begin->as<uint64_t>(), nullptr,
-                                     static_cast<uint32_t>(fused_scan->descs.size()), scan_rows->as<hy_row_id>(), s),
-             "hy_expand_chunk_row_ids");
     scan_builder.wait();
     // consumers blocked in resolve() on other threads read scan_rows from their own streams as soon as the chunks are
-    // published: the expansion must have finished (execute()'s own sync comes later)
-    hy_check(hy_stream_synchronize(s), "sync");
+    // published: every write of it was ordered before the stream synchronisation above
     std::const_pointer_cast<Table>(probe_table)->fulfil(std::move(scan_chunks));
     untake.scan = nullptr;
     tr.mark("fused TableScan output");

@@ -333,6 +333,11 @@ struct OpTraceRecord {
 void op_trace_enable(bool on);
 std::vector<OpTraceRecord> op_trace_take();
 
+// JoinHash's prepared-plan cache (operators.cpp, JoinPlanCache): {hits, misses} since the start, and freeing the
+// cached plans (their workspaces).
+std::pair<uint64_t, uint64_t> join_plan_cache_stats();
+void join_plan_cache_clear();
+
 // JoinHashTraits (reference src/lib/operators/join_hash/hash_traits.hpp:9-42) over data types.
 DataType join_hashed_type(DataType left, DataType right);
 

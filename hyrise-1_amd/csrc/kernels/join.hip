@@ -142,6 +142,8 @@ struct Side {
   uint64_t filter_const;             // type_cast<T>(constant) bits for VALUE predicate chunks
   int32_t filter_type;               // HY_TYPE_* of VALUE predicate chunks
   uint32_t* scan_out;
+  // or (part1_spread only; null elsewhere) the scan's output as RowIDs {c, chunk offset} at the same positions
+  hy_row_id* scan_rows;
   // Probe-side prefilter of a selective INNER / SEMI join (null: none) over the build keys: a probe row whose key is
   // certainly absent takes no part - it could produce no output, and dropping it keeps the stable order of the others
   // (the reference's output is unchanged). The fused scan's output still lists it. The filter words are either
@@ -1160,7 +1162,10 @@ __global__ __launch_bounds__(PART_THREADS) void part1_spread(Side s, Digit dg, N
     for (int k = 0; k < PART_ITEMS; ++k) {
       const uint32_t i = r0 + k * WAVE;
       if (i < n) {
-        if (s.scan_out != nullptr) s.scan_out[srun + i] = (recs[k].payload & ~NULL_FLAG) - row0;
+        if (s.scan_rows != nullptr)
+          s.scan_rows[srun + i] = hy_row_id{c, (recs[k].payload & ~NULL_FLAG) - row0};
+        else if (s.scan_out != nullptr)
+          s.scan_out[srun + i] = (recs[k].payload & ~NULL_FLAG) - row0;
         if (!(recs[k].payload & NULL_FLAG)) act |= 1u << k;
       }
     }
@@ -2227,6 +2232,10 @@ struct JoinDesc {
   uint32_t* n_skewed;           // their count (zeroed before join_partition)
   uint32_t* multi;              // partitions with more probe records than one pass (n_parts entries)
   uint32_t* n_multi;            // their count (zeroed before join_partition)
+  // join_partition_multi: a partition of <= 2 passes whose build side has <= stash_rows rows keeps its first pass's
+  // probe payloads and match infos in LDS after a table of stash_rows rows (0: no stash) instead of reloading and
+  // re-matching the pass after the count
+  uint32_t stash_rows;
 };
 
 // Record sources of the partition join: what the last partition pass wrote.
@@ -2615,8 +2624,57 @@ __device__ __forceinline__ void partition_one_table(const JoinDesc& d, uint32_t 
     if (obase + part_total > d.capacity) return;
     write_pass(0, obase);
   } else {
-    // several passes: count them all, reserve the partition's range, then reload, match and write pass by pass
     const uint32_t n_pass = (nr + JP_PASS_ - 1) / JP_PASS_;
+    if (n_pass <= 1 || (n_pass == 2 && nb <= d.stash_rows)) {
+      // one pass, or two with the first one's payloads and match infos stashed in LDS (thread-private slots after the
+      // table): every record is loaded and matched once; the second pass is written from registers behind the first
+      // one's total, then the first pass is restored and written at the range's start
+      load(0);
+      match(0);
+      uint32_t my0 = 0;
+#pragma unroll
+      for (int k = 0; k < K; ++k) my0 += e_of(0, k);
+      if (n_pass <= 1) {
+        const uint32_t part_total = pass_offsets<K, NT>([&](int k) { return e_of(0, k); }, s_tot);
+        const uint64_t obase = allocate_output(d, p, part_total, part_out_begin, part_out_count, s_base);
+        if (obase + part_total > d.capacity) return;
+        write_pass(0, obase);
+        return;
+      }
+      P* st_pay = reinterpret_cast<P*>(smem + table_bytes<H, P>(d.stash_rows));
+      uint32_t* st_info = reinterpret_cast<uint32_t*>(st_pay + JP_PASS_);
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          st_pay[(k * V + v) * NT + threadIdx.x] = ppay[k][v];
+          st_info[(k * V + v) * NT + threadIdx.x] = pinfo[k][v];
+        }
+      load(1);
+      match(1);
+      uint32_t my1 = 0;
+#pragma unroll
+      for (int k = 0; k < K; ++k) my1 += e_of(1, k);
+      uint32_t total0, total1;
+      block_exclusive_sum<NT>(my0, s_tot, &total0);
+      block_exclusive_sum<NT>(my1, s_tot, &total1);
+      const uint64_t obase = allocate_output(d, p, total0 + total1, part_out_begin, part_out_count, s_base);
+      if (obase + total0 + total1 > d.capacity) return;
+      pass_offsets<K, NT>([&](int k) { return e_of(1, k); }, s_tot);
+      write_pass(1, obase + total0);
+      __syncthreads();  // s_tot is reused by the first pass's offsets
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          ppay[k][v] = st_pay[(k * V + v) * NT + threadIdx.x];
+          pinfo[k][v] = st_info[(k * V + v) * NT + threadIdx.x];
+        }
+      pass_offsets<K, NT>([&](int k) { return e_of(0, k); }, s_tot);
+      write_pass(0, obase);
+      return;
+    }
+    // more passes: count them all, reserve the partition's range, then reload, match and write pass by pass
     uint32_t my = 0;
     for (uint32_t pass = 0; pass < n_pass; ++pass) {
       if (pass || !PREFETCH) load(pass);

@@ -520,6 +520,12 @@ typedef struct hy_join_filter {
   uint64_t* out_chunk_begin;    /* device, n_chunks + 1 entries, or NULL */
   uint32_t n_chunks;            /* entries of chunks: at least the side's n_chunks (HY_ERR_INVALID_ARGUMENT
                                    otherwise - a filter built for a table that has grown since) */
+  hy_row_id* out_row_ids;       /* device, capacity = side rows, or NULL: the TableScan's output as RowIDs
+                                   {c, offset} (c = the side's chunk index) at the positions out_offsets would take -
+                                   the PosLists of the scan's output chunks, written by the pass that ranks the matches
+                                   (no expansion afterwards). Needs out_offsets and out_chunk_begin (scratch for
+                                   passes that produce offsets first); out_offsets' contents are then unspecified.
+                                   hy_scan_join_hash / prepared plans only (the exchange entry points refuse it) */
 } hy_join_filter;
 
 hy_status hy_scan_join_hash_workspace_size(const hy_join_side* build, const hy_join_filter* build_filter,
@@ -546,6 +552,13 @@ hy_status hy_scan_join_plan_create(const hy_join_side* build, const hy_join_filt
 hy_status hy_scan_join_plan_execute(hy_join_plan_t plan, hy_row_id* out_build, hy_row_id* out_probe,
                                     uint64_t out_capacity, uint64_t* partition_begin, uint32_t* partition_counts,
                                     hy_join_result* result, hy_stream_t stream);
+/* Points the plan's fused scans at new output buffers (out_offsets / out_chunk_begin / out_row_ids of the filters) for
+ * the following executions - an operator re-executing a cached plan writes each execution's TableScan output into
+ * buffers of its own. The filters' predicate chunks must equal the plan's (HY_ERR_INVALID_ARGUMENT otherwise), and
+ * out_offsets / out_chunk_begin stay set or unset as at create; a plan whose pointers changed executes its launches
+ * eagerly from then on (a captured graph would hold the old ones). */
+hy_status hy_scan_join_plan_rebind(hy_join_plan_t plan, const hy_join_filter* build_filter,
+                                   const hy_join_filter* probe_filter);
 hy_status hy_scan_join_plan_destroy(hy_join_plan_t plan);
 
 /* ---------------------------------------------------------------------------------------------------------------

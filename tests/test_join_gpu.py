@@ -255,3 +255,32 @@ def test_probe_skew_needs_several_passes(hy, oracle, mode):
     j.execute()
     exp, _ = oracle.join_hash(a, b, getattr(hy.JoinMode, mode), (0, 0))
     assert_identical(j.get_output(), exp)
+
+
+def test_join_plan_cache_reexecution(hy, oracle):
+    """Re-executions of TableScan -> JoinHash of one shape run the cached prepared plan (JoinPlanCache, rebound to each
+    execution's TableScan output): every execution's join and scan outputs equal the oracle's - also after another
+    predicate (a new shape, a cache miss) ran in between - and earlier outputs stay valid while later ones are made."""
+    rng = np.random.default_rng(23)
+    orders, lineitem = orders_lineitem(hy, 30_000, 10_000, rng)
+    hy.encode_all_chunks(lineitem, hy.EncodingType.Dictionary)
+    o, l = wrap(hy, orders), wrap(hy, lineitem)
+    hy.join_plan_cache_clear()
+    hits0, misses0 = hy.join_plan_cache_stats()
+    kept = []
+    for i, value in enumerate([24, 24, 31, 24, 24]):
+        s = hy.TableScan(l, 1, hy.PredicateCondition.LessThan, value)
+        s.execute()
+        j = hy.JoinHash(o, s, hy.JoinMode.Inner, (0, 0), hy.PredicateCondition.Equals)
+        j.execute()
+        exp_s = oracle.table_scan(lineitem, 1, hy.PredicateCondition.LessThan, value, [])
+        exp_j, _ = oracle.join_hash(orders, exp_s, hy.JoinMode.Inner, (0, 0))
+        assert_identical(j.get_output(), exp_j)
+        assert_identical(s.get_output(), exp_s)
+        kept.append((j, s, exp_j, exp_s))
+    for j, s, exp_j, exp_s in kept:  # the cached plan wrote every execution's outputs into buffers of their own
+        assert_identical(j.get_output(), exp_j)
+        assert_identical(s.get_output(), exp_s)
+    hits, misses = hy.join_plan_cache_stats()
+    assert misses - misses0 == 2 and hits - hits0 == 3  # shapes <24 and <31
+    hy.join_plan_cache_clear()

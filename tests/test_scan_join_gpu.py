@@ -51,17 +51,26 @@ def run_fused(hy, build, bfilt, probe, pfilt, params, cap):
 class Filter:
     """hy_join_filter for `column cond value` on a DeviceColumn, with its output buffers."""
 
-    def __init__(self, capi, col, cond, value, offsets=True):
+    def __init__(self, capi, col, cond, value, offsets=True, rows=False):
         self.chunks = col.scan_chunks(cond, value)
         self.const = col.constant(value)
         n = max(16, col.values.size)
         self.out = capi.DeviceArray(np.zeros(n, np.uint32))
         self.begin = capi.DeviceArray(np.zeros(col.n_chunks + 1, np.uint64))
+        # out_row_ids: the scan's PosLists as RowIDs (pre-filled with a pattern no RowID of the scan takes)
+        self.rows = capi.DeviceArray(np.full(n * 2, 0xDEADBEEF, np.uint32)) if rows else None
         self.f = capi.JoinFilter(self.chunks, dt.HY_TYPES[col.values.dtype], self.const.ctypes.data,
-                                 self.out.ptr.value if offsets else None, self.begin.ptr.value)
+                                 self.out.ptr.value if offsets else None, self.begin.ptr.value,
+                                 out_row_ids=self.rows.ptr.value if rows else None)
 
     def scan_output(self):
-        off, beg = self.out.fetch(), self.begin.fetch().astype(np.int64)
+        beg = self.begin.fetch().astype(np.int64)
+        if self.rows is not None:  # the offsets of the RowIDs, whose chunk ids must name their chunk
+            rows = self.rows.fetch().reshape(-1, 2)
+            for c in range(beg.size - 1):
+                assert (rows[beg[c]:beg[c + 1], 0] == c).all(), f"out_row_ids chunk {c}: chunk ids"
+            return [rows[beg[c]:beg[c + 1], 1] for c in range(beg.size - 1)]
+        off = self.out.fetch()
         return [off[beg[c]:beg[c + 1]] for c in range(beg.size - 1)]
 
 
@@ -237,6 +246,66 @@ def test_multi_digit_plans(hy, oracle, monkeypatch, bits, mode, key_enc, filtere
     if lf is not None:
         check_scan(probe_t, lf)
     check_join(expected, parts, 2, swapped, mode == "Semi")
+
+
+@pytest.mark.parametrize("variant", ["classic", "onepass", "blocked", "direct", "bloom", "build_filter"])
+@pytest.mark.parametrize("mode", ["Inner", "Left"])
+def test_scan_row_ids_from_every_pass0(hy, oracle, monkeypatch, variant, mode):
+    """hy_join_filter.out_row_ids: the fused scan's PosLists written as RowIDs - by part1_spread itself on the classic
+    pass 0, expanded from the offsets after the join on the other pass-0 variants (single-pass, row blocks, direct
+    partitioning) - equal the oracle TableScan's output RowID for RowID, and the join output is unchanged."""
+    env = {"onepass": {"HY_ONEPASS": "1"}, "blocked": {"HY_BLOCKED": "1", "HY_BLOCK_ROWS": "7000"},
+           "direct": {"HY_JOIN_DIRECT": "1"}, "bloom": {"HY_JOIN_BLOOM": "1"}}.get(variant, {})
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    capi = hy.capi
+    rng = np.random.default_rng(zlib.crc32(repr(("row_ids", variant, mode)).encode()))
+    okey, ostatus, lkey, lkey_nulls, qty, qty_nulls = orders_lineitem(rng, 30_000, True)
+    lchunk, ochunk = 6_000, 5_000
+    lineitem = hy.Table.from_arrays([("l_orderkey", hy.DataType.Int, True), ("l_quantity", hy.DataType.Float, True)],
+                                    [lkey, qty], [lkey_nulls, qty_nulls], lchunk)
+    orders = hy.Table.from_arrays([("o_orderkey", hy.DataType.Int, False), ("o_status", hy.DataType.Int, False)],
+                                  [okey, ostatus], [], ochunk)
+    build_filter = variant == "build_filter"
+    scan_l = oracle.table_scan(lineitem, 1, hy.PredicateCondition.LessThan, 24.0, [])
+    left = oracle.table_scan(orders, 1, hy.PredicateCondition.GreaterThanEquals, 3, []) if build_filter else orders
+    expected, bits = oracle.join_hash(left, scan_l, getattr(hy.JoinMode, mode), (0, 0), radix_bits=16)
+    lk = dt.DeviceColumn(capi, lkey, lkey_nulls, lchunk, "Unencoded")
+    lq = dt.DeviceColumn(capi, qty, qty_nulls, lchunk, "Dictionary")
+    ok = dt.DeviceColumn(capi, okey, None, ochunk, "Unencoded")
+    os_ = dt.DeviceColumn(capi, ostatus, None, ochunk, "Dictionary")
+    lf = Filter(capi, lq, "LessThan", 24.0, rows=True)
+    of = Filter(capi, os_, "GreaterThanEquals", 3, rows=True) if build_filter else None
+    swapped = mode == "Left" or left.row_count() > scan_l.row_count()
+    params = capi.JoinParams({"Inner": 0, "Left": 1}[mode], capi.HY_TYPE_INT32, bits, 17)
+    cap = okey.size * 3 + lkey.size + 16
+    o_side, l_side = dt.join_side(capi, ok), dt.join_side(capi, lk)
+    o_f = of.f if of else None
+    if swapped:
+        parts = run_fused(hy, l_side, lf.f, o_side, o_f, params, cap)
+    else:
+        parts = run_fused(hy, o_side, o_f, l_side, lf.f, params, cap)
+    check_scan(scan_l, lf)
+    if of is not None:
+        check_scan(left, of)
+    check_join(expected, parts, 2, swapped, False)
+
+
+def test_scan_row_ids_need_offsets(hy):
+    """out_row_ids without out_offsets is refused (HY_ERR_INVALID_ARGUMENT): other pass-0 variants stage offsets."""
+    capi = hy.capi
+    rng = np.random.default_rng(3)
+    okey, _, lkey, _, qty, qty_nulls = orders_lineitem(rng, 2_000, False)
+    lk = dt.DeviceColumn(capi, lkey, None, 1_000, "Unencoded")
+    lq = dt.DeviceColumn(capi, qty, qty_nulls, 1_000, "Dictionary")
+    ok = dt.DeviceColumn(capi, okey, None, 1_000, "Unencoded")
+    lf = Filter(capi, lq, "LessThan", 24.0, offsets=False, rows=True)
+    params = capi.JoinParams(0, capi.HY_TYPE_INT32, capi.lib.hy_join_radix_bits(okey.size, 4), 17)
+    wsb = ctypes.c_size_t()
+    st = capi.lib.hy_scan_join_hash_workspace_size(ctypes.byref(dt.join_side(capi, ok)), None,
+                                                   ctypes.byref(dt.join_side(capi, lk)), ctypes.byref(lf.f),
+                                                   ctypes.byref(params), ctypes.byref(wsb))
+    assert st == 1  # HY_ERR_INVALID_ARGUMENT
 
 
 
@@ -491,3 +560,38 @@ def test_hash_records(hy, oracle, monkeypatch, bits, mode, variant):
         parts = run_fused(hy, o_side, None, l_side, lf.f, params, cap_pairs)
     check_scan(probe_t, lf)
     check_join(expected, parts, 2, swapped, mode in ("Semi", "Anti"))
+
+
+@pytest.mark.parametrize("stash", ["1", "0"])
+@pytest.mark.parametrize("avg", [6_100, 6_600])
+@pytest.mark.parametrize("mode", ["Inner", "Left", "Right", "Semi", "Anti"])
+def test_two_pass_partitions(hy, oracle, monkeypatch, stash, avg, mode):
+    """Partitions whose probe records need about two passes of join_partition_multi (the all-multi launch: every
+    partition there, as TPC-H SF10's 8,192 partitions of ~7,300 probe rows): with HY_JOIN_STASH=1 a two-pass partition
+    keeps its first pass's payloads and match infos in LDS (no reload, no second match), one-pass partitions are
+    written from registers, and a partition of a hot key takes the count + reload passes; HY_JOIN_STASH=0 reloads every
+    multi-pass partition. Duplicate build keys, unmatched probe keys; every partition's PosLists equal the oracle's."""
+    monkeypatch.setenv("HY_JOIN_STASH", stash)
+    capi = hy.capi
+    rng = np.random.default_rng(zlib.crc32(repr(("two_pass", avg, mode)).encode()))
+    bits, nb = 5, 60_000
+    bkeys = rng.permutation(nb).astype(np.int32)
+    bkeys = np.concatenate([bkeys, bkeys[rng.integers(0, nb, nb // 20)]])
+    n_probe = avg << bits
+    pkeys = rng.integers(-2_000, nb, n_probe)
+    pkeys[rng.random(n_probe) < 0.02] = 7  # one hot key: its partition needs three passes or more
+    pkeys = pkeys.astype(np.int32)
+    B = hy.Table.from_arrays([("k", hy.DataType.Int, False)], [bkeys], [], 20_000)
+    P = hy.Table.from_arrays([("k", hy.DataType.Int, False)], [pkeys], [], 50_000)
+    jm = getattr(hy.JoinMode, mode)
+    swapped = mode in ("Left", "Semi", "Anti")  # the reference's swap: the right input builds
+    expected, used = (oracle.join_hash(P, B, jm, (0, 0), radix_bits=bits) if swapped
+                      else oracle.join_hash(B, P, jm, (0, 0), radix_bits=bits))
+    assert used == bits
+    bcol = dt.DeviceColumn(capi, bkeys, None, 20_000, "Unencoded")
+    pcol = dt.DeviceColumn(capi, pkeys, None, 50_000, "Unencoded")
+    params = capi.JoinParams({"Inner": 0, "Left": 1, "Right": 2, "Semi": 5, "Anti": 6}[mode], capi.HY_TYPE_INT32,
+                             bits, 17)
+    parts = run_fused(hy, dt.join_side(capi, bcol), None, dt.join_side(capi, pcol), None, params,
+                      bkeys.size * 4 + n_probe + 16)
+    check_join(expected, parts, 1, swapped, mode in ("Semi", "Anti"))
