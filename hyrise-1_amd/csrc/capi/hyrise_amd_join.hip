@@ -337,13 +337,16 @@ hy_status hy_scan_join_plan_rebind(hy_join_plan_t plan, const hy_join_filter* bu
     mut[i]->scan_chunk_begin = bind[i].begin;
     mut[i]->scan_rows = bind[i].rows;
   }
-  if (changed) {  // a captured graph holds the old pointers; a plan rebound per execution runs its launches eagerly
+  // a rebound plan runs its launches eagerly from now on: a captured graph holds the old pointers, and an operator that
+  // rebinds per execution (its outputs are new buffers each time) would capture again on every call - and capture on a
+  // stream while other threads' operators launch, allocate and free
+  if (changed) {
     if (plan->exec) (void)hipGraphExecDestroy(plan->exec);
     if (plan->graph) (void)hipGraphDestroy(plan->graph);
     plan->exec = nullptr;
     plan->graph = nullptr;
-    plan->no_graph = true;
   }
+  plan->no_graph = true;
   return HY_OK;
 }
 

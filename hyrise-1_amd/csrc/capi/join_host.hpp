@@ -1157,24 +1157,6 @@ uint32_t lds_table_rows() {
   return rows;
 }
 
-// Whether join_partition_multi<Src, P, JP, NT> may take `bytes` of dynamic LDS (set once per instance above 64 KB).
-template <typename Src, typename P, int JP, int NT>
-bool stash_lds_ok(size_t bytes) {
-  if (bytes <= 64 * 1024) return true;
-  static std::mutex m;
-  static size_t granted = 0;
-  std::lock_guard<std::mutex> lock(m);
-  if (bytes <= granted) return true;
-  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&hyk::join_partition_multi<Src, P, JP, NT>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bytes));
-  if (e != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
-  }
-  granted = bytes;
-  return true;
-}
-
 // Per-partition LDS build/probe over partitioned records (partition bounds on the device; the records as the last pass
 // wrote them: hyk::RecSrc or hyk::HashSrc). probe_rows_hint: an upper bound of the probe rows (probe_exact: their
 // number); it picks the probe
@@ -1234,7 +1216,9 @@ hy_status run_join_partitions(const uint32_t* build_begin, const uint32_t* probe
     const size_t half = 80 * 1024 - 1024;  // (the kernel's static LDS: s_tot, s_base)
     uint32_t rows = std::min<uint32_t>(lds_max, hyk::LDS_MAX_ROWS);
     while (rows > 16 && hyk::table_bytes<H, P>(rows) + stash > half) rows = rows * 15 / 16;
-    if (rows > 16 && stash_lds_ok<Src, P, JW, NT>(std::max(lds, hyk::table_bytes<H, P>(rows) + stash))) {
+    // (no hipFuncSetAttribute for the > 64 KB launch: HIP ignores the dynamic-LDS attribute on AMD devices, and calling
+    // it from several threads at once while others launched aborted the process in test_concurrent_operators)
+    if (rows > 16) {
       jdm.stash_rows = rows;
       lds_m = std::max(lds, hyk::table_bytes<H, P>(rows) + stash);
     }

@@ -555,8 +555,8 @@ hy_status hy_scan_join_plan_execute(hy_join_plan_t plan, hy_row_id* out_build, h
 /* Points the plan's fused scans at new output buffers (out_offsets / out_chunk_begin / out_row_ids of the filters) for
  * the following executions - an operator re-executing a cached plan writes each execution's TableScan output into
  * buffers of its own. The filters' predicate chunks must equal the plan's (HY_ERR_INVALID_ARGUMENT otherwise), and
- * out_offsets / out_chunk_begin stay set or unset as at create; a plan whose pointers changed executes its launches
- * eagerly from then on (a captured graph would hold the old ones). */
+ * out_offsets / out_chunk_begin stay set or unset as at create; a rebound plan executes its launches eagerly from then
+ * on (no hipGraph capture: a captured graph would hold the old pointers). Either filter NULL where the plan has none. */
 hy_status hy_scan_join_plan_rebind(hy_join_plan_t plan, const hy_join_filter* build_filter,
                                    const hy_join_filter* probe_filter);
 hy_status hy_scan_join_plan_destroy(hy_join_plan_t plan);
