@@ -84,6 +84,7 @@ op_trace_enable = _host.op_trace_enable
 op_trace_take = _host.op_trace_take
 join_plan_cache_stats = _host.join_plan_cache_stats
 join_plan_cache_clear = _host.join_plan_cache_clear
+join_plan_cache_set_capacity = _host.join_plan_cache_set_capacity
 pool_stats = _host.pool_stats
 device_memory = _host.device_memory
 host_cpu_share = _host.host_cpu_share

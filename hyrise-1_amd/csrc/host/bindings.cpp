@@ -356,6 +356,7 @@ PYBIND11_MODULE(_hyrise_host, m) {
   m.def("op_trace_enable", &op_trace_enable, py::arg("on"));
   m.def("join_plan_cache_stats", &join_plan_cache_stats);
   m.def("join_plan_cache_clear", &join_plan_cache_clear);
+  m.def("join_plan_cache_set_capacity", &join_plan_cache_set_capacity, py::arg("plans"));
   m.def("op_trace_take", []() {
     py::list l;
     for (const auto& r : op_trace_take()) l.append(py::make_tuple(r.op, r.phase, r.ms));

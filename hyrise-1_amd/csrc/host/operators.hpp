@@ -337,6 +337,8 @@ std::vector<OpTraceRecord> op_trace_take();
 // cached plans (their workspaces).
 std::pair<uint64_t, uint64_t> join_plan_cache_stats();
 void join_plan_cache_clear();
+// plans kept (HY_OP_PLAN_CACHE at start, default 0 = off)
+void join_plan_cache_set_capacity(size_t plans);
 
 // JoinHashTraits (reference src/lib/operators/join_hash/hash_traits.hpp:9-42) over data types.
 DataType join_hashed_type(DataType left, DataType right);

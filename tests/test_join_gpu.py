@@ -265,7 +265,7 @@ def test_join_plan_cache_reexecution(hy, oracle):
     orders, lineitem = orders_lineitem(hy, 30_000, 10_000, rng)
     hy.encode_all_chunks(lineitem, hy.EncodingType.Dictionary)
     o, l = wrap(hy, orders), wrap(hy, lineitem)
-    hy.join_plan_cache_clear()
+    hy.join_plan_cache_set_capacity(2)  # (opt-in: HY_OP_PLAN_CACHE, default off)
     hits0, misses0 = hy.join_plan_cache_stats()
     kept = []
     for i, value in enumerate([24, 24, 31, 24, 24]):
@@ -283,4 +283,4 @@ def test_join_plan_cache_reexecution(hy, oracle):
         assert_identical(s.get_output(), exp_s)
     hits, misses = hy.join_plan_cache_stats()
     assert misses - misses0 == 2 and hits - hits0 == 3  # shapes <24 and <31
-    hy.join_plan_cache_clear()
+    hy.join_plan_cache_set_capacity(0)
