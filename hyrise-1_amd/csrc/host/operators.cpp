@@ -1652,6 +1652,14 @@ class JoinPlanCache {
   uint64_t _hits = 0, _misses = 0;
 };
 
+bool scan_rowids_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("HY_OP_SCAN_ROWIDS");
+    return e && std::strtol(e, nullptr, 10) != 0;
+  }();
+  return v;
+}
+
 bool data_side(const hy_join_side& s) {
   if (s.n_referenced) return false;
   for (uint32_t i = 0; i < s.n_chunks; ++i)
@@ -1761,10 +1769,12 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
     scan_builder.schedule([&] { scan_chunks = fused_scan->chunks_for(scan_rows); });
     scan_offsets = std::make_unique<DeviceBuffer>(std::max<uint64_t>(fused_scan->total, 1) * 4, s);
     scan_begin = std::make_unique<DeviceBuffer>((fused_scan->descs.size() + 1) * 8, s);
-    // the scan's PosLists come straight from the join's ranking pass (out_row_ids)
+    // HY_OP_SCAN_ROWIDS=1: the scan's PosLists come straight from the join's ranking pass (out_row_ids) instead of an
+    // expansion of its offsets after the join (opt-in: see DESIGN.md, round 6 second session)
     pf = hy_join_filter{fused_scan->descs.data(), hy_type_of(fused_scan->col_type), fused_scan->constant.bytes,
                         scan_offsets->as<uint32_t>(), scan_begin->as<uint64_t>(),
-                        static_cast<uint32_t>(fused_scan->descs.size()), scan_rows->as<hy_row_id>()};
+                        static_cast<uint32_t>(fused_scan->descs.size()),
+                        scan_rowids_enabled() ? scan_rows->as<hy_row_id>() : nullptr};
   }
   // a prepared plan of this shape (data-table sides), rebound to this execution's scan output buffers; else one call
   std::unique_ptr<CachedJoinPlan> cached;
@@ -1905,11 +1915,17 @@ std::shared_ptr<const Table> JoinHash::_on_execute() {
   hy_check(hy_stream_synchronize(s), "sync");
   if (cached) JoinPlanCache::get().put(std::move(cached));  // (its workspace is idle: the stream synchronised)
   tr.mark("join kernels + partition counts synchronised");
-  if (fused_scan) {  // the scan's output: the join wrote its RowIDs (out_row_ids) before the sync above
+  if (fused_scan) {  // the scan's output: RowIDs written by the join (out_row_ids), or expanded from its offsets here
     uint64_t at = 0;
     for (size_t k = 0; k < fused_scan->counts.size(); ++k) {
       Assert(h_scan_begin[k] == at, "fused TableScan: the join's scan output disagrees with the scan's count");
       at += fused_scan->counts[k];
+    }
+    if (!pf.out_row_ids) {
+      hy_check(hy_expand_chunk_row_ids(scan_offsets->as<uint32_t>(), scan_begin->as<uint64_t>(), nullptr,
+                                       static_cast<uint32_t>(fused_scan->descs.size()), scan_rows->as<hy_row_id>(), s),
+               "hy_expand_chunk_row_ids");
+      hy_check(hy_stream_synchronize(s), "sync");  // (consumers on other threads read scan_rows once published)
     }
     scan_builder.wait();
     // consumers blocked in resolve() on other threads read scan_rows from their own streams as soon as the chunks are
