@@ -61,7 +61,7 @@ struct JoinKnobs {
   bool direct = false;                 // HY_JOIN_DIRECT: direct partitioning of a filtered side (join_direct.hip)
   uint32_t direct_span = 16;           // HY_DIRECT_SPAN: tiles per span of the direct first pass
   uint32_t direct_groups = 0;          // HY_DIRECT_GROUPS: span groups per bucket of the direct second pass (0: auto)
-  bool join_stash = true;              // HY_JOIN_STASH: two-pass partitions keep their first pass in LDS (0: reload it)
+  bool join_stash = false;             // HY_JOIN_STASH=1: two-pass partitions keep their first pass in LDS (opt-in)
 };
 
 inline JoinKnobs knobs_from_env() {
@@ -86,7 +86,7 @@ inline JoinKnobs knobs_from_env() {
   k.direct = num("HY_JOIN_DIRECT", 0) != 0;
   k.direct_span = static_cast<uint32_t>(std::min<long long>(std::max<long long>(1, num("HY_DIRECT_SPAN", 16)), 64));
   k.direct_groups = static_cast<uint32_t>(std::min<long long>(std::max<long long>(0, num("HY_DIRECT_GROUPS", 0)), 4096));
-  k.join_stash = num("HY_JOIN_STASH", 1) != 0;
+  k.join_stash = num("HY_JOIN_STASH", 0) != 0;
   return k;
 }
 
